@@ -1,0 +1,67 @@
+// pybind11 bindings of the device plane (module `_device`).  Pointers and
+// streams cross the boundary as integers (tensor.data_ptr(), stream.cuda_stream)
+// so the module does not link libtorch.
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include "device_comm.hpp"
+#include "ops.hpp"
+
+namespace py = pybind11;
+using namespace ccmpi::dev;
+
+PYBIND11_MODULE(_device, m) {
+  m.doc() = "ccmpi device plane: hand-written CDNA4 collectives + kernels (HIP, gfx950)";
+  m.attr("ALGO_ONESHOT") = (int)ALGO_ONESHOT;
+  m.attr("ALGO_TWOSHOT") = (int)ALGO_TWOSHOT;
+  m.attr("ALGO_REDUCE_BCAST") = (int)ALGO_REDUCE_BCAST;
+  m.attr("MAX_RANKS") = kMaxRanks;
+  m.attr("MAX_BLOCKS") = kMaxBlocks;
+  m.def("reduce_supported", &device_reduce_supported);
+  m.def("rccl_unique_id", []() { return py::bytes(DeviceComm::rccl_unique_id()); });
+
+  py::class_<DeviceComm>(m, "DeviceComm")
+      .def(py::init<int, int, int, uint64_t>(), py::arg("rank"), py::arg("size"), py::arg("device"),
+           py::arg("scratch_bytes") = 0)
+      .def_property_readonly("rank", &DeviceComm::rank)
+      .def_property_readonly("size", &DeviceComm::size)
+      .def_property_readonly("device", &DeviceComm::device)
+      .def("signal_handle", [](const DeviceComm& d) { return py::bytes(d.signal_handle()); })
+      .def("connect", [](DeviceComm& d, const std::vector<std::string>& hs) { d.connect(hs); })
+      .def("export_range", [](const DeviceComm& d, uint64_t ptr) {
+        auto r = d.export_range(ptr);
+        return py::make_tuple(py::bytes(r.first), r.second);
+      })
+      .def("add_segment", &DeviceComm::add_segment)
+      .def("find", [](const DeviceComm& d, uint64_t ptr, uint64_t n) {
+        uint64_t off = 0;
+        int s = d.find(ptr, n, &off);
+        return py::make_tuple(s, off);
+      })
+      .def_property_readonly("scratch_bytes", &DeviceComm::scratch_bytes)
+      .def("allreduce", &DeviceComm::allreduce, py::call_guard<py::gil_scoped_release>())
+      .def("reduce_scatter", &DeviceComm::reduce_scatter, py::call_guard<py::gil_scoped_release>())
+      .def("allgather", &DeviceComm::allgather, py::call_guard<py::gil_scoped_release>())
+      .def("alltoall", &DeviceComm::alltoall, py::call_guard<py::gil_scoped_release>())
+      .def("bcast", &DeviceComm::bcast, py::call_guard<py::gil_scoped_release>())
+      .def("local_reduce", &DeviceComm::local_reduce, py::call_guard<py::gil_scoped_release>())
+      .def("rccl_init", [](DeviceComm& d, py::bytes uid) {
+        std::string u = uid;
+        py::gil_scoped_release g;
+        d.rccl_init(u);
+      })
+      .def_property_readonly("rccl_ready", &DeviceComm::rccl_ready)
+      .def("rccl_allreduce", &DeviceComm::rccl_allreduce, py::call_guard<py::gil_scoped_release>())
+      .def("rccl_reduce_scatter", &DeviceComm::rccl_reduce_scatter, py::call_guard<py::gil_scoped_release>())
+      .def("rccl_allgather", &DeviceComm::rccl_allgather, py::call_guard<py::gil_scoped_release>())
+      .def("rccl_alltoall", &DeviceComm::rccl_alltoall, py::call_guard<py::gil_scoped_release>())
+      .def("rccl_bcast", &DeviceComm::rccl_bcast, py::call_guard<py::gil_scoped_release>())
+      .def("p2p_ring_allreduce", &DeviceComm::p2p_ring_allreduce, py::call_guard<py::gil_scoped_release>())
+      .def("p2p_rhd_allreduce", &DeviceComm::p2p_rhd_allreduce, py::call_guard<py::gil_scoped_release>())
+      .def("p2p_pairwise_alltoall", &DeviceComm::p2p_pairwise_alltoall, py::call_guard<py::gil_scoped_release>())
+      .def("error_code", &DeviceComm::error_code, py::call_guard<py::gil_scoped_release>())
+      .def("clear_error", &DeviceComm::clear_error)
+      .def("set_timeout_seconds", &DeviceComm::set_timeout_seconds);
+
+  register_ops(m);
+}

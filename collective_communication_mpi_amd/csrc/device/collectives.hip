@@ -1,0 +1,493 @@
+// Hand-written collectives over IPC-mapped peer HBM (xGMI on an 8x MI355X node;
+// same-device peers when several ranks share one GPU).
+//
+// Reference semantics they implement (mpi_wrapper/comm.py):
+//   Allreduce      :18-22   -> allreduce_{oneshot,twoshot}; reduce_bcast = the
+//                              reference's own myAllreduce algorithm (:63-107)
+//   Allgather      :24-29   -> allgather (pull)
+//   Reduce_scatter :31-36   -> reduce_scatter (block), pull + in-register sum
+//   Alltoall       :41-61   -> alltoall (pull), also myAlltoall / myAlltoall2 (:110-199)
+//   (+ bcast, used by the façade and the harness)
+//
+// Structure shared by every kernel (one CTA = "block" b):
+//   1. publish: lane j (< nranks) writes this rank's buffer codes into rank j's
+//      signal buffer at [block b][my rank], release, then the phase-0 flag = epoch.
+//   2. wait until all ranks' phase-0 flags for block b reach epoch (bounded spin).
+//   3. body: CTA b works on its contiguous share of the vectors, reading peers
+//      with system-coherent 16-B buffer loads (every peer's bytes in flight at
+//      once: all 7 xGMI links busy), reducing in registers in rank order
+//      0..p-1 (deterministic, bitwise identical on every rank).
+//   4. phase flags between dependent stages (two-shot) and a final flag so no
+//      rank returns (and lets its buffers be overwritten) while a peer still
+//      reads them.
+// Block b only ever waits for block b of its peers, so there is no grid-wide
+// barrier; grids are sized identically on all ranks from (bytes, nranks).
+// Reductions through LDS would add a round trip without reuse (each byte is
+// read once), so partial sums stay in VGPRs.
+#include "common.hpp"
+#include "collectives.hpp"
+
+namespace ccmpi {
+namespace dev {
+
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kUnroll = 2;
+
+struct BlockRange {
+  uint64_t lo, hi;
+};
+
+__device__ __forceinline__ BlockRange split_range(uint64_t n, int parts, int idx) {
+  uint64_t per = (n + parts - 1) / parts;
+  uint64_t lo = per * idx;
+  uint64_t hi = lo + per;
+  if (lo > n) lo = n;
+  if (hi > n) hi = n;
+  return {lo, hi};
+}
+
+__device__ __forceinline__ char* uniform_ptr(char* p) {
+  uint64_t v = (uint64_t)p;
+  uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+  uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  return (char*)(((uint64_t)hi << 32) | lo);
+}
+
+// Per-CTA prologue: bump the epoch, publish up to two buffer codes, barrier.
+// Returns false on timeout.  `codes` (LDS) receives every rank's codes.
+__device__ bool start_phase(const CollArgs& a, uint64_t* s_epoch, uint64_t (*codes)[kMaxRanks]) {
+  const PeerTable* pt = a.pt;
+  const int b = blockIdx.x, t = threadIdx.x, me = pt->rank, nr = pt->size;
+  if (t == 0) *s_epoch = a.epochs[b] + 1;
+  __syncthreads();
+  const uint64_t e = *s_epoch;
+  Signals* mine = pt->sig[me];
+  if (t < nr) {
+    Signals* peer = pt->sig[t];
+    signal_store(&peer->addr[0][b][me], a.src_code);
+    signal_store(&peer->addr[1][b][me], a.res_code);
+    // make every prior write of this rank (earlier kernels' output in this
+    // XCD's L2, e.g. the tensor we are about to publish) visible system-wide
+    release_sys();
+    signal_store(&peer->flag[0][b][me], e);
+  }
+  bool ok = true;
+  if (t < nr) {
+    ok = wait_geq(&mine->flag[0][b][t], e, a.timeout_ticks, &mine->error, 0x100 + t);
+    if (ok) {
+      codes[0][t] = __hip_atomic_load(&mine->addr[0][b][t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      codes[1][t] = __hip_atomic_load(&mine->addr[1][b][t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+  ok = __syncthreads_and(ok);
+  return ok;
+}
+
+// Stage flag `phase` (1..3): every thread's stores are drained, then lane j
+// tells rank j, then we wait for all ranks.  Returns false on timeout.
+__device__ bool sync_phase(const CollArgs& a, int phase, uint64_t e) {
+  const PeerTable* pt = a.pt;
+  const int b = blockIdx.x, t = threadIdx.x, me = pt->rank, nr = pt->size;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  Signals* mine = pt->sig[me];
+  if (t < nr) {
+    release_sys();
+    signal_store(&pt->sig[t]->flag[phase][b][me], e);
+  }
+  bool ok = true;
+  if (t < nr) ok = wait_geq(&mine->flag[phase][b][t], e, a.timeout_ticks, &mine->error, 0x100 * (phase + 1) + t);
+  ok = __syncthreads_and(ok);
+  return ok;
+}
+
+__device__ __forceinline__ void finish(const CollArgs& a, uint64_t e) {
+  if (threadIdx.x == 0) a.epochs[blockIdx.x] = e;
+}
+
+// ---------------------------------------------------------------------------
+// scalar element helpers for the (< 16 B) tail of reductions
+// ---------------------------------------------------------------------------
+template <int DT> struct Elem;
+template <> struct Elem<DT_F32> { using A = float; static constexpr int B = 4;
+  __device__ static A ld(Rsrc r, uint32_t o) { return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r.r, o, 0, kCachePolicySys)); }
+  __device__ static void st(Rsrc r, uint32_t o, A v) { __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r.r, o, 0, kCachePolicySys); } };
+template <> struct Elem<DT_I32> { using A = int32_t; static constexpr int B = 4;
+  __device__ static A ld(Rsrc r, uint32_t o) { return (int32_t)__builtin_amdgcn_raw_buffer_load_b32(r.r, o, 0, kCachePolicySys); }
+  __device__ static void st(Rsrc r, uint32_t o, A v) { __builtin_amdgcn_raw_buffer_store_b32((uint32_t)v, r.r, o, 0, kCachePolicySys); } };
+template <> struct Elem<DT_BF16> { using A = float; static constexpr int B = 2;
+  __device__ static A ld(Rsrc r, uint32_t o) { return __uint_as_float((uint32_t)__builtin_amdgcn_raw_buffer_load_b16(r.r, o, 0, kCachePolicySys) << 16); }
+  __device__ static void st(Rsrc r, uint32_t o, A v) { __builtin_amdgcn_raw_buffer_store_b16((uint16_t)f32_to_bf16_bits(v), r.r, o, 0, kCachePolicySys); } };
+template <> struct Elem<DT_F16> { using A = float; static constexpr int B = 2;
+  __device__ static A ld(Rsrc r, uint32_t o) { return (float)__builtin_bit_cast(_Float16, (uint16_t)__builtin_amdgcn_raw_buffer_load_b16(r.r, o, 0, kCachePolicySys)); }
+  __device__ static void st(Rsrc r, uint32_t o, A v) { __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(uint16_t, (_Float16)v), r.r, o, 0, kCachePolicySys); } };
+template <> struct Elem<DT_F64> { using A = double; static constexpr int B = 8;
+  __device__ static A ld(Rsrc r, uint32_t o) { auto v = __builtin_amdgcn_raw_buffer_load_b64(r.r, o, 0, kCachePolicySys); return __hiloint2double((int)v[1], (int)v[0]); }
+  __device__ static void st(Rsrc r, uint32_t o, A v) { typedef unsigned u2 __attribute__((ext_vector_type(2))); u2 x; x[0] = (uint32_t)__double2loint(v); x[1] = (uint32_t)__double2hiint(v); __builtin_amdgcn_raw_buffer_store_b64(x, r.r, o, 0, kCachePolicySys); } };
+template <> struct Elem<DT_I64> { using A = int64_t; static constexpr int B = 8;
+  __device__ static A ld(Rsrc r, uint32_t o) { auto v = __builtin_amdgcn_raw_buffer_load_b64(r.r, o, 0, kCachePolicySys); return (int64_t)(((uint64_t)v[1] << 32) | v[0]); }
+  __device__ static void st(Rsrc r, uint32_t o, A v) { typedef unsigned u2 __attribute__((ext_vector_type(2))); u2 x; x[0] = (uint32_t)v; x[1] = (uint32_t)((uint64_t)v >> 32); __builtin_amdgcn_raw_buffer_store_b64(x, r.r, o, 0, kCachePolicySys); } };
+
+// Reduce bytes [off, off+len) of every rank's buffer (codes[j]) into dst (local).
+// Vector part by all threads; element tail by thread 0.
+template <int DT, int OP, int NRM>
+__device__ void reduce_span(const PeerTable* pt, const uint64_t* codes, uint64_t off, uint64_t len,
+                            uint64_t total_bytes, char* dst) {
+  const int nr = pt->size;
+  const uint64_t vbytes = len & ~15ull;
+  // process in windows of < 2 GiB so 32-bit voffsets suffice
+  const uint64_t kWin = 1ull << 30;
+  for (uint64_t w = 0; w < vbytes; w += kWin) {
+    const uint32_t wl = (uint32_t)min(kWin, vbytes - w);
+    Rsrc src[NRM];
+#pragma unroll
+    for (int j = 0; j < NRM; ++j)
+      if (j < nr) src[j] = make_rsrc(uniform_ptr(resolve(pt, j, codes[j]) + off + w), wl);
+    Rsrc out = make_rsrc(uniform_ptr(dst + w), wl);
+    const uint32_t nv = wl / 16;
+    for (uint32_t v = threadIdx.x; v < nv; v += kThreads * kUnroll) {
+      VecAcc<DT> acc[kUnroll];
+      u32x4 x[kUnroll][NRM];
+#pragma unroll
+      for (int j = 0; j < NRM; ++j) {
+        if (j < nr) {
+#pragma unroll
+          for (int u = 0; u < kUnroll; ++u) {
+            uint32_t vv = v + u * kThreads;
+            if (vv < nv) x[u][j] = ld16(src[j], vv * 16);
+          }
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u) {
+        uint32_t vv = v + u * kThreads;
+        if (vv < nv) {
+          acc[u].load(x[u][0]);
+#pragma unroll
+          for (int j = 1; j < NRM; ++j)
+            if (j < nr) acc[u].template acc<OP>(x[u][j]);
+          st16(out, vv * 16, acc[u].store());
+        }
+      }
+    }
+  }
+  const uint64_t tail = len - vbytes;
+  if (tail && threadIdx.x == 0) {
+    using E = Elem<DT>;
+    char* base0 = dst + vbytes;
+    Rsrc out = make_rsrc(base0, (uint32_t)tail);
+    for (uint32_t o = 0; o < tail; o += E::B) {
+      typename E::A acc = E::ld(make_rsrc(resolve(pt, 0, codes[0]) + off + vbytes, (uint32_t)tail), o);
+      for (int j = 1; j < nr; ++j)
+        acc = apply_op<OP>(acc, E::ld(make_rsrc(resolve(pt, j, codes[j]) + off + vbytes, (uint32_t)tail), o));
+      E::st(out, o, acc);
+    }
+  }
+  (void)total_bytes;
+}
+
+// Copy bytes [0,len) from `src` (any mapped address) to `dst` (local).
+__device__ void copy_span(const char* src, char* dst, uint64_t len) {
+  const uint64_t kWin = 1ull << 30;
+  const uint64_t vbytes = len & ~15ull;
+  for (uint64_t w = 0; w < vbytes; w += kWin) {
+    const uint32_t wl = (uint32_t)min(kWin, vbytes - w);
+    Rsrc s = make_rsrc(uniform_ptr(const_cast<char*>(src) + w), wl);
+    Rsrc d = make_rsrc(uniform_ptr(dst + w), wl);
+    const uint32_t nv = wl / 16;
+    for (uint32_t v = threadIdx.x; v < nv; v += kThreads * 4) {
+      u32x4 x[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (v + u * kThreads < nv) x[u] = ld16(s, (v + u * kThreads) * 16);
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (v + u * kThreads < nv) st16(d, (v + u * kThreads) * 16, x[u]);
+    }
+  }
+  const uint64_t tail = len - vbytes;
+  if (tail && threadIdx.x == 0) {
+    Rsrc s = make_rsrc(const_cast<char*>(src) + vbytes, (uint32_t)tail);
+    Rsrc d = make_rsrc(dst + vbytes, (uint32_t)tail);
+    for (uint32_t o = 0; o < tail; ++o)
+      __builtin_amdgcn_raw_buffer_store_b8(__builtin_amdgcn_raw_buffer_load_b8(s.r, o, 0, kCachePolicySys), d.r, o, 0, kCachePolicySys);
+  }
+}
+
+// Copy from several peers at once: dst_j <- src_j for j in [0,nr) except skip.
+// Keeps all peers' loads in flight together (all links busy).
+template <int NRM>
+__device__ void gather_spans(const char* const* srcs, char* const* dsts, int nr, int skip, uint64_t len) {
+  const uint64_t kWin = 1ull << 30;
+  const uint64_t vbytes = len & ~15ull;
+  for (uint64_t w = 0; w < vbytes; w += kWin) {
+    const uint32_t wl = (uint32_t)min(kWin, vbytes - w);
+    Rsrc s[NRM], d[NRM];
+#pragma unroll
+    for (int j = 0; j < NRM; ++j) {
+      if (j < nr && j != skip) {
+        s[j] = make_rsrc(uniform_ptr(const_cast<char*>(srcs[j]) + w), wl);
+        d[j] = make_rsrc(uniform_ptr(dsts[j] + w), wl);
+      }
+    }
+    const uint32_t nv = wl / 16;
+    for (uint32_t v = threadIdx.x; v < nv; v += kThreads * kUnroll) {
+      u32x4 x[kUnroll][NRM];
+#pragma unroll
+      for (int j = 0; j < NRM; ++j)
+        if (j < nr && j != skip)
+#pragma unroll
+          for (int u = 0; u < kUnroll; ++u)
+            if (v + u * kThreads < nv) x[u][j] = ld16(s[j], (v + u * kThreads) * 16);
+#pragma unroll
+      for (int j = 0; j < NRM; ++j)
+        if (j < nr && j != skip)
+#pragma unroll
+          for (int u = 0; u < kUnroll; ++u)
+            if (v + u * kThreads < nv) st16(d[j], (v + u * kThreads) * 16, x[u][j]);
+    }
+  }
+  const uint64_t tail = len - vbytes;
+  if (tail && threadIdx.x == 0) {
+    for (int j = 0; j < nr; ++j) {
+      if (j == skip) continue;
+      Rsrc s = make_rsrc(const_cast<char*>(srcs[j]) + vbytes, (uint32_t)tail);
+      Rsrc d = make_rsrc(dsts[j] + vbytes, (uint32_t)tail);
+      for (uint32_t o = 0; o < tail; ++o)
+        __builtin_amdgcn_raw_buffer_store_b8(__builtin_amdgcn_raw_buffer_load_b8(s.r, o, 0, kCachePolicySys), d.r, o, 0, kCachePolicySys);
+    }
+  }
+}
+
+// Element-aligned partition of `nbytes` into `parts` pieces whose boundaries
+// are multiples of 16 B (except the end).
+__device__ __forceinline__ BlockRange part16(uint64_t nbytes, int parts, int idx) {
+  uint64_t nv = (nbytes + 15) / 16;
+  BlockRange r = split_range(nv, parts, idx);
+  r.lo *= 16;
+  r.hi *= 16;
+  if (r.hi > nbytes) r.hi = nbytes;
+  if (r.lo > nbytes) r.lo = nbytes;
+  return r;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// kernels
+// ---------------------------------------------------------------------------
+
+// One-shot: each rank reads the whole buffer from every rank and reduces.
+template <int DT, int OP, int NRM>
+__global__ void __launch_bounds__(kThreads) k_allreduce_oneshot(CollArgs a) {
+  __shared__ uint64_t s_epoch;
+  __shared__ uint64_t codes[2][kMaxRanks];
+  if (!start_phase(a, &s_epoch, codes)) return;
+  const uint64_t e = s_epoch;
+  BlockRange r = part16(a.nbytes, gridDim.x, blockIdx.x);
+  if (r.hi > r.lo) reduce_span<DT, OP, NRM>(a.pt, codes[0], r.lo, r.hi - r.lo, a.nbytes, a.out + r.lo);
+  if (!sync_phase(a, 3, e)) return;
+  finish(a, e);
+}
+
+// Two-shot: reduce-scatter (rank r owns shard r) into the published result
+// buffer, phase barrier, then all-gather of the shards into `out`.
+template <int DT, int OP, int NRM>
+__global__ void __launch_bounds__(kThreads) k_allreduce_twoshot(CollArgs a) {
+  __shared__ uint64_t s_epoch;
+  __shared__ uint64_t codes[2][kMaxRanks];
+  if (!start_phase(a, &s_epoch, codes)) return;
+  const uint64_t e = s_epoch;
+  const PeerTable* pt = a.pt;
+  const int me = pt->rank, nr = pt->size;
+  // shard boundaries (16-B aligned), then this CTA's slice of each shard
+  BlockRange mys = part16(a.nbytes, nr, me);
+  BlockRange sub = part16(mys.hi - mys.lo, gridDim.x, blockIdx.x);
+  char* res_local = resolve(pt, me, codes[1][me]);
+  if (sub.hi > sub.lo)
+    reduce_span<DT, OP, NRM>(pt, codes[0], mys.lo + sub.lo, sub.hi - sub.lo, a.nbytes, res_local + mys.lo + sub.lo);
+  if (!sync_phase(a, 1, e)) return;
+  // all-gather: shard j's slice `blockIdx` lives in rank j's result buffer
+  __shared__ const char* srcs[kMaxRanks];
+  __shared__ char* dsts[kMaxRanks];
+  __shared__ uint64_t lens[kMaxRanks];
+  if (threadIdx.x < nr) {
+    int j = threadIdx.x;
+    BlockRange sj = part16(a.nbytes, nr, j);
+    BlockRange bj = part16(sj.hi - sj.lo, gridDim.x, blockIdx.x);
+    srcs[j] = resolve(pt, j, codes[1][j]) + sj.lo + bj.lo;
+    dsts[j] = a.out + sj.lo + bj.lo;
+    lens[j] = bj.hi - bj.lo;
+  }
+  __syncthreads();
+  // shard slices differ by at most 16 B between ranks: copy the common length
+  // for everybody at once, then the stragglers individually.
+  uint64_t common = lens[0];
+  for (int j = 1; j < nr; ++j) common = min(common, lens[j]);
+  const int skip = (a.out == res_local) ? me : -1;
+  if (common) gather_spans<NRM>(srcs, dsts, nr, skip, common);
+  for (int j = 0; j < nr; ++j)
+    if (j != skip && lens[j] > common) copy_span(srcs[j] + common, dsts[j] + common, lens[j] - common);
+  if (!sync_phase(a, 3, e)) return;
+  finish(a, e);
+}
+
+// Reference algorithm (mpi_wrapper/comm.py:63-107): the root reduces every
+// rank's buffer in rank order, then every other rank copies the root's result.
+template <int DT, int OP, int NRM>
+__global__ void __launch_bounds__(kThreads) k_allreduce_reduce_bcast(CollArgs a) {
+  __shared__ uint64_t s_epoch;
+  __shared__ uint64_t codes[2][kMaxRanks];
+  if (!start_phase(a, &s_epoch, codes)) return;
+  const uint64_t e = s_epoch;
+  const PeerTable* pt = a.pt;
+  const int me = pt->rank, root = a.root;
+  BlockRange r = part16(a.nbytes, gridDim.x, blockIdx.x);
+  if (me == root && r.hi > r.lo)
+    reduce_span<DT, OP, NRM>(pt, codes[0], r.lo, r.hi - r.lo, a.nbytes, resolve(pt, me, codes[1][me]) + r.lo);
+  if (!sync_phase(a, 1, e)) return;
+  if (r.hi > r.lo) {
+    char* src = resolve(pt, root, codes[1][root]) + r.lo;
+    if (src != a.out + r.lo) copy_span(src, a.out + r.lo, r.hi - r.lo);
+  }
+  if (!sync_phase(a, 3, e)) return;
+  finish(a, e);
+}
+
+// Reduce-scatter (block): out = sum_j in_j[me*nbytes : (me+1)*nbytes].
+template <int DT, int OP, int NRM>
+__global__ void __launch_bounds__(kThreads) k_reduce_scatter(CollArgs a) {
+  __shared__ uint64_t s_epoch;
+  __shared__ uint64_t codes[2][kMaxRanks];
+  if (!start_phase(a, &s_epoch, codes)) return;
+  const uint64_t e = s_epoch;
+  const PeerTable* pt = a.pt;
+  BlockRange r = part16(a.nbytes, gridDim.x, blockIdx.x);
+  if (r.hi > r.lo)
+    reduce_span<DT, OP, NRM>(pt, codes[0], (uint64_t)pt->rank * a.nbytes + r.lo, r.hi - r.lo, a.nbytes, a.out + r.lo);
+  if (!sync_phase(a, 3, e)) return;
+  finish(a, e);
+}
+
+// All-gather: out[j*nbytes ...] = in_j.  (mode 0)
+// All-to-all: out[j*nbytes ...] = in_j[me*nbytes ...].  (mode 1)
+// Broadcast : out = in_root.  (mode 2)
+template <int MODE, int NRM>
+__global__ void __launch_bounds__(kThreads) k_move(CollArgs a) {
+  __shared__ uint64_t s_epoch;
+  __shared__ uint64_t codes[2][kMaxRanks];
+  if (!start_phase(a, &s_epoch, codes)) return;
+  const uint64_t e = s_epoch;
+  const PeerTable* pt = a.pt;
+  const int me = pt->rank, nr = pt->size;
+  BlockRange r = part16(a.nbytes, gridDim.x, blockIdx.x);
+  if (r.hi > r.lo) {
+    if (MODE == 2) {
+      if (me != a.root) copy_span(resolve(pt, a.root, codes[0][a.root]) + r.lo, a.out + r.lo, r.hi - r.lo);
+    } else {
+      __shared__ const char* srcs[kMaxRanks];
+      __shared__ char* dsts[kMaxRanks];
+      if (threadIdx.x < nr) {
+        int j = threadIdx.x;
+        uint64_t soff = (MODE == 1 ? (uint64_t)me * a.nbytes : 0) + r.lo;
+        srcs[j] = resolve(pt, j, codes[0][j]) + soff;
+        dsts[j] = a.out + (uint64_t)j * a.nbytes + r.lo;
+      }
+      __syncthreads();
+      gather_spans<NRM>(srcs, dsts, nr, -1, r.hi - r.lo);
+    }
+  }
+  if (!sync_phase(a, 3, e)) return;
+  finish(a, e);
+}
+
+// Local element-wise reduction: out = op(in0, in1, ...) for the fused
+// last-axis reduce-scatter and the P2P ring/RHD schedules.
+template <int DT, int OP>
+__global__ void __launch_bounds__(kThreads) k_local_reduce(LocalReduceArgs a) {
+  // vectors grid-strided; each input pointer must be 16-B aligned
+  const uint64_t nv = a.nbytes / 16;
+  for (uint64_t v = (uint64_t)blockIdx.x * kThreads + threadIdx.x; v < nv; v += (uint64_t)gridDim.x * kThreads) {
+    VecAcc<DT> acc;
+    acc.load(*reinterpret_cast<const u32x4*>(a.in[0] + v * 16));
+    for (int j = 1; j < a.n_in; ++j) acc.template acc<OP>(*reinterpret_cast<const u32x4*>(a.in[j] + v * 16));
+    *reinterpret_cast<u32x4*>(a.out + v * 16) = acc.store();
+  }
+  const uint64_t tail = a.nbytes - nv * 16;
+  if (tail && blockIdx.x == 0 && threadIdx.x == 0) {
+    using E = Elem<DT>;
+    for (uint32_t o = 0; o < tail; o += E::B) {
+      typename E::A acc = E::ld(make_rsrc(a.in[0] + nv * 16, (uint32_t)tail), o);
+      for (int j = 1; j < a.n_in; ++j) acc = apply_op<OP>(acc, E::ld(make_rsrc(a.in[j] + nv * 16, (uint32_t)tail), o));
+      E::st(make_rsrc(a.out + nv * 16, (uint32_t)tail), o, acc);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// host-side launchers
+// ---------------------------------------------------------------------------
+int grid_for(uint64_t bytes_per_cta_work, int max_blocks) {
+  // ~64 KiB of output per CTA minimum; at most max_blocks CTAs
+  uint64_t g = (bytes_per_cta_work + (64u << 10) - 1) / (64u << 10);
+  if (g < 1) g = 1;
+  if (g > (uint64_t)max_blocks) g = max_blocks;
+  if (g > (uint64_t)kMaxBlocks) g = kMaxBlocks;
+  return (int)g;
+}
+
+template <typename F>
+static void with_nrm(int nranks, F&& f) {
+  if (nranks <= 8) f.template operator()<8>();
+  else if (nranks <= kMaxRanks) f.template operator()<kMaxRanks>();
+  else throw std::invalid_argument("ccmpi: too many ranks for the device communicator");
+}
+
+void launch_allreduce(int algo, const CollArgs& a, int nranks, int dtype, int op, int grid, hipStream_t s) {
+  with_nrm(nranks, [&]<int R>() {
+    dispatch_dt_op(dtype, op, [&]<int D, int O>() {
+      switch (algo) {
+        case ALGO_ONESHOT: hipLaunchKernelGGL((k_allreduce_oneshot<D, O, R>), dim3(grid), dim3(kThreads), 0, s, a); break;
+        case ALGO_TWOSHOT: hipLaunchKernelGGL((k_allreduce_twoshot<D, O, R>), dim3(grid), dim3(kThreads), 0, s, a); break;
+        case ALGO_REDUCE_BCAST: hipLaunchKernelGGL((k_allreduce_reduce_bcast<D, O, R>), dim3(grid), dim3(kThreads), 0, s, a); break;
+        default: throw std::invalid_argument("ccmpi: bad allreduce algo");
+      }
+    });
+  });
+  CCMPI_HIP_CHECK(hipGetLastError());
+}
+
+void launch_reduce_scatter(const CollArgs& a, int nranks, int dtype, int op, int grid, hipStream_t s) {
+  with_nrm(nranks, [&]<int R>() {
+    dispatch_dt_op(dtype, op, [&]<int D, int O>() {
+      hipLaunchKernelGGL((k_reduce_scatter<D, O, R>), dim3(grid), dim3(kThreads), 0, s, a);
+    });
+  });
+  CCMPI_HIP_CHECK(hipGetLastError());
+}
+
+void launch_move(int mode, const CollArgs& a, int nranks, int grid, hipStream_t s) {
+  with_nrm(nranks, [&]<int R>() {
+    switch (mode) {
+      case MOVE_ALLGATHER: hipLaunchKernelGGL((k_move<0, R>), dim3(grid), dim3(kThreads), 0, s, a); break;
+      case MOVE_ALLTOALL: hipLaunchKernelGGL((k_move<1, R>), dim3(grid), dim3(kThreads), 0, s, a); break;
+      case MOVE_BCAST: hipLaunchKernelGGL((k_move<2, R>), dim3(grid), dim3(kThreads), 0, s, a); break;
+      default: throw std::invalid_argument("ccmpi: bad move mode");
+    }
+  });
+  CCMPI_HIP_CHECK(hipGetLastError());
+}
+
+void launch_local_reduce(const LocalReduceArgs& a, int dtype, int op, hipStream_t s) {
+  uint64_t nv = a.nbytes / 16;
+  int grid = (int)std::min<uint64_t>(std::max<uint64_t>((nv + kThreads - 1) / kThreads, 1), 2048);
+  dispatch_dt_op(dtype, op, [&]<int D, int O>() {
+    hipLaunchKernelGGL((k_local_reduce<D, O>), dim3(grid), dim3(kThreads), 0, s, a);
+  });
+  CCMPI_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace dev
+}  // namespace ccmpi

@@ -1,0 +1,47 @@
+// Host-visible interface of the hand-written collective kernels.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "common.hpp"
+
+namespace ccmpi {
+namespace dev {
+
+enum AllreduceAlgo : int {
+  ALGO_ONESHOT = 0,       // every rank reads everything (small messages)
+  ALGO_TWOSHOT = 1,       // reduce-scatter + all-gather over all links (large)
+  ALGO_REDUCE_BCAST = 2,  // reference algorithm: reduce to root, broadcast
+};
+
+enum MoveMode : int { MOVE_ALLGATHER = 0, MOVE_ALLTOALL = 1, MOVE_BCAST = 2 };
+
+struct CollArgs {
+  const PeerTable* pt;     // device-resident peer table
+  uint64_t* epochs;        // per-CTA epoch counters (device, local)
+  uint64_t src_code;       // this rank's published input  (addr_code)
+  uint64_t res_code;       // this rank's published result buffer (two-shot / reduce_bcast)
+  char* out;               // local output pointer (16-B aligned)
+  uint64_t nbytes;         // see each kernel
+  uint64_t timeout_ticks;  // bounded spins, 100 MHz ticks
+  int root;
+  int pad;
+};
+
+struct LocalReduceArgs {
+  const char* in[kMaxRanks];
+  char* out;
+  uint64_t nbytes;
+  int n_in;
+  int pad;
+};
+
+int grid_for(uint64_t bytes_per_cta_work, int max_blocks);
+void launch_allreduce(int algo, const CollArgs& a, int nranks, int dtype, int op, int grid, hipStream_t s);
+void launch_reduce_scatter(const CollArgs& a, int nranks, int dtype, int op, int grid, hipStream_t s);
+void launch_move(int mode, const CollArgs& a, int nranks, int grid, hipStream_t s);
+void launch_local_reduce(const LocalReduceArgs& a, int dtype, int op, hipStream_t s);
+
+}  // namespace dev
+}  // namespace ccmpi

@@ -1,0 +1,601 @@
+// Device communicator implementation (host code; kernels in collectives.hip).
+#include "device_comm.hpp"
+
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+#include <stdexcept>
+
+namespace ccmpi {
+namespace dev {
+
+namespace {
+
+std::mutex g_ipc_mu;
+std::map<std::string, std::pair<void*, int>> g_ipc;  // handle bytes -> (base, refs)
+
+ncclDataType_t nccl_dt(int dt) {
+  switch (dt) {
+    case DT_I8: return ncclInt8;
+    case DT_U8: case DT_BOOL: case DT_BYTE: return ncclUint8;
+    case DT_I32: return ncclInt32;
+    case DT_U32: return ncclUint32;
+    case DT_I64: return ncclInt64;
+    case DT_U64: return ncclUint64;
+    case DT_F16: return ncclFloat16;
+    case DT_BF16: return ncclBfloat16;
+    case DT_F32: return ncclFloat32;
+    case DT_F64: return ncclFloat64;
+  }
+  throw std::invalid_argument("ccmpi: dtype unsupported by RCCL: " + std::to_string(dt));
+}
+
+ncclRedOp_t nccl_op(int op) {
+  switch (op) {
+    case OP_SUM: return ncclSum;
+    case OP_PROD: return ncclProd;
+    case OP_MIN: return ncclMin;
+    case OP_MAX: return ncclMax;
+  }
+  throw std::invalid_argument("ccmpi: op unsupported by RCCL: " + std::to_string(op));
+}
+
+#define CCMPI_NCCL_CHECK(expr)                                                                   \
+  do {                                                                                            \
+    ncclResult_t _r = (expr);                                                                     \
+    if (_r != ncclSuccess)                                                                        \
+      throw std::runtime_error(std::string("RCCL error: ") + ncclGetErrorString(_r) + " at " #expr); \
+  } while (0)
+
+inline hipStream_t S(uint64_t s) { return reinterpret_cast<hipStream_t>(s); }
+
+}  // namespace
+
+void* ipc_open(const std::string& handle) {
+  std::lock_guard<std::mutex> g(g_ipc_mu);
+  auto it = g_ipc.find(handle);
+  if (it != g_ipc.end()) {
+    it->second.second++;
+    return it->second.first;
+  }
+  if (handle.size() != sizeof(hipIpcMemHandle_t)) throw std::invalid_argument("ccmpi: bad IPC handle size");
+  hipIpcMemHandle_t h;
+  std::memcpy(&h, handle.data(), sizeof(h));
+  void* p = nullptr;
+  CCMPI_HIP_CHECK(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess));
+  g_ipc[handle] = {p, 1};
+  return p;
+}
+
+void ipc_close(const std::string& handle) {
+  std::lock_guard<std::mutex> g(g_ipc_mu);
+  auto it = g_ipc.find(handle);
+  if (it == g_ipc.end()) return;
+  if (--it->second.second == 0) {
+    (void)hipIpcCloseMemHandle(it->second.first);
+    g_ipc.erase(it);
+  }
+}
+
+DeviceComm::DeviceComm(int rank, int size, int device, uint64_t /*scratch_bytes*/)
+    : rank_(rank), size_(size), device_(device) {
+  if (size < 1 || size > kMaxRanks) throw std::invalid_argument("ccmpi: device communicator supports 1..16 ranks");
+  CCMPI_HIP_CHECK(hipSetDevice(device));
+  CCMPI_HIP_CHECK(hipExtMallocWithFlags(reinterpret_cast<void**>(&sig_), sizeof(Signals), hipDeviceMallocUncached));
+  CCMPI_HIP_CHECK(hipMemset(sig_, 0, sizeof(Signals)));
+  CCMPI_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&epochs_), sizeof(uint64_t) * kMaxBlocks));
+  CCMPI_HIP_CHECK(hipMemset(epochs_, 0, sizeof(uint64_t) * kMaxBlocks));
+  CCMPI_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&dev_pt_), sizeof(PeerTable)));
+  std::memset(&host_pt_, 0, sizeof(host_pt_));
+  host_pt_.rank = rank;
+  host_pt_.size = size;
+  peer_sig_.assign(size, nullptr);
+  peer_sig_[rank] = sig_;
+  host_pt_.sig[rank] = sig_;
+  if (const char* t = std::getenv("CCMPI_DEVICE_TIMEOUT_S")) set_timeout_seconds(std::atof(t));
+  CCMPI_HIP_CHECK(hipDeviceSynchronize());
+  sync_table_();
+}
+
+DeviceComm::~DeviceComm() {
+  (void)hipSetDevice(device_);
+  (void)hipDeviceSynchronize();
+  if (nccl_) ncclCommDestroy(nccl_);
+  for (auto& h : opened_) ipc_close(h);
+  if (sig_) (void)hipFree(sig_);
+  if (epochs_) (void)hipFree(epochs_);
+  if (dev_pt_) (void)hipFree(dev_pt_);
+}
+
+void DeviceComm::sync_table_() {
+  CCMPI_HIP_CHECK(hipMemcpy(dev_pt_, &host_pt_, sizeof(PeerTable), hipMemcpyHostToDevice));
+}
+
+std::string DeviceComm::signal_handle() const {
+  hipIpcMemHandle_t h;
+  CCMPI_HIP_CHECK(hipIpcGetMemHandle(&h, sig_));
+  return std::string(reinterpret_cast<const char*>(&h), sizeof(h));
+}
+
+void DeviceComm::connect(const std::vector<std::string>& sig_handles) {
+  if ((int)sig_handles.size() != size_) throw std::invalid_argument("ccmpi: need one signal handle per rank");
+  CCMPI_HIP_CHECK(hipSetDevice(device_));
+  for (int j = 0; j < size_; ++j) {
+    if (j == rank_) continue;
+    void* p = ipc_open(sig_handles[j]);
+    opened_.push_back(sig_handles[j]);
+    peer_sig_[j] = static_cast<Signals*>(p);
+    host_pt_.sig[j] = peer_sig_[j];
+  }
+  sync_table_();
+}
+
+std::pair<std::string, uint64_t> DeviceComm::export_range(uint64_t ptr) const {
+  hipDeviceptr_t base = nullptr;
+  size_t sz = 0;
+  CCMPI_HIP_CHECK(hipMemGetAddressRange(&base, &sz, reinterpret_cast<hipDeviceptr_t>(ptr)));
+  hipIpcMemHandle_t h;
+  CCMPI_HIP_CHECK(hipIpcGetMemHandle(&h, base));
+  return {std::string(reinterpret_cast<const char*>(&h), sizeof(h)), ptr - (uint64_t)base};
+}
+
+int DeviceComm::add_segment(uint64_t local_ptr, uint64_t bytes, const std::vector<std::string>& handles,
+                            const std::vector<uint64_t>& offsets) {
+  if ((int)segs_.size() >= kMaxSegs) throw std::runtime_error("ccmpi: too many symmetric segments");
+  if ((int)handles.size() != size_ || (int)offsets.size() != size_)
+    throw std::invalid_argument("ccmpi: add_segment needs one handle per rank");
+  CCMPI_HIP_CHECK(hipSetDevice(device_));
+  const int s = (int)segs_.size();
+  segs_.push_back(SegInfo{reinterpret_cast<char*>(local_ptr), bytes, false});
+  peer_seg_.emplace_back(size_, nullptr);
+  for (int j = 0; j < size_; ++j) {
+    char* p;
+    if (j == rank_) {
+      p = reinterpret_cast<char*>(local_ptr);
+    } else {
+      p = static_cast<char*>(ipc_open(handles[j])) + offsets[j];
+      opened_.push_back(handles[j]);
+    }
+    peer_seg_[s][j] = p;
+    host_pt_.seg[j][s] = p;
+  }
+  host_pt_.seg_bytes[s] = bytes;
+  host_pt_.nsegs = (int)segs_.size();
+  sync_table_();
+  return s;
+}
+
+int DeviceComm::find(uint64_t ptr, uint64_t nbytes, uint64_t* off) const {
+  for (size_t s = 0; s < segs_.size(); ++s) {
+    uint64_t b = (uint64_t)segs_[s].local;
+    if (ptr >= b && ptr + nbytes <= b + segs_[s].bytes) {
+      if (off) *off = ptr - b;
+      return (int)s;
+    }
+  }
+  return -1;
+}
+
+uint64_t DeviceComm::code_of_(uint64_t ptr, uint64_t nbytes) const {
+  if (ptr % 16) return 0;
+  uint64_t off = 0;
+  int s = find(ptr, nbytes, &off);
+  if (s < 0) return 0;
+  return addr_code(s, off);
+}
+
+CollArgs DeviceComm::args_(uint64_t src_code, uint64_t res_code, char* out, uint64_t nbytes, int root) const {
+  CollArgs a{};
+  a.pt = dev_pt_;
+  a.epochs = epochs_;
+  a.src_code = src_code;
+  a.res_code = res_code;
+  a.out = out;
+  a.nbytes = nbytes;
+  a.timeout_ticks = timeout_ticks_;
+  a.root = root;
+  return a;
+}
+
+int DeviceComm::grid_(uint64_t work_bytes, int max_blocks) const {
+  if (max_blocks <= 0) max_blocks = 256;
+  return grid_for(work_bytes, std::min(max_blocks, kMaxBlocks));
+}
+
+void DeviceComm::allreduce(uint64_t in, uint64_t out, uint64_t count, int dtype, int op, int algo,
+                           uint64_t stream, int max_blocks, bool symmetric) {
+  const uint64_t es = dtype_bytes(dtype), nbytes = count * es;
+  if (!device_reduce_supported(dtype, op)) throw std::invalid_argument("ccmpi: unsupported device reduction");
+  if (nbytes == 0) return;
+  CCMPI_HIP_CHECK(hipSetDevice(device_));
+  hipStream_t st = S(stream);
+  if (size_ == 1) {
+    if (in != out) CCMPI_HIP_CHECK(hipMemcpyAsync((void*)out, (void*)in, nbytes, hipMemcpyDeviceToDevice, st));
+    return;
+  }
+  const bool needs_res = algo != ALGO_ONESHOT;
+  if (symmetric && !(algo == ALGO_ONESHOT && in == out)) {
+    uint64_t sc = code_of_(in, nbytes), rc = needs_res ? code_of_(out, nbytes) : 0;
+    if (!sc || (needs_res && !rc) || out % 16)
+      throw std::invalid_argument("ccmpi: symmetric allreduce needs 16-B aligned registered buffers");
+    const uint64_t work = algo == ALGO_TWOSHOT ? nbytes / size_ : nbytes;
+    launch_allreduce(algo, args_(sc, rc, (char*)out, nbytes, 0), size_, dtype, op, grid_(work, max_blocks), st);
+    return;
+  }
+  if (scratch_bytes() < 64 * es) throw std::runtime_error("ccmpi: scratch segment missing or too small");
+  // chunk size identical on all ranks: half the scratch, 16-B and element aligned
+  uint64_t chunk = (scratch_bytes() / 2) / (16 * es) * (16 * es);
+  char* stage = reinterpret_cast<char*>(scratch_ptr());
+  for (uint64_t off = 0; off < nbytes; off += chunk) {
+    const uint64_t n = std::min(chunk, nbytes - off);
+    uint64_t sc = (algo == ALGO_ONESHOT && in == out) ? 0 : code_of_(in + off, n);
+    if (!sc) {
+      CCMPI_HIP_CHECK(hipMemcpyAsync(stage, (void*)(in + off), n, hipMemcpyDeviceToDevice, st));
+      sc = addr_code(0, 0);
+    }
+    const bool out_ok = (out + off) % 16 == 0;
+    uint64_t rc = 0;
+    char* outp = (char*)(out + off);
+    if (needs_res) {
+      rc = out_ok ? code_of_(out + off, n) : 0;
+      if (!rc) rc = addr_code(0, chunk);
+    }
+    if (!out_ok) outp = stage + chunk;
+    const uint64_t work = algo == ALGO_TWOSHOT ? n / size_ : n;
+    launch_allreduce(algo, args_(sc, rc, outp, n, 0), size_, dtype, op, grid_(work, max_blocks), st);
+    if (!out_ok) CCMPI_HIP_CHECK(hipMemcpyAsync((void*)(out + off), stage + chunk, n, hipMemcpyDeviceToDevice, st));
+  }
+}
+
+void DeviceComm::reduce_scatter(uint64_t in, uint64_t out, uint64_t count_per_rank, int dtype, int op,
+                                uint64_t stream, int max_blocks, bool symmetric) {
+  const uint64_t es = dtype_bytes(dtype), blk = count_per_rank * es;
+  if (!device_reduce_supported(dtype, op)) throw std::invalid_argument("ccmpi: unsupported device reduction");
+  if (blk == 0) return;
+  CCMPI_HIP_CHECK(hipSetDevice(device_));
+  hipStream_t st = S(stream);
+  if (size_ == 1) {
+    if (in != out) CCMPI_HIP_CHECK(hipMemcpyAsync((void*)out, (void*)in, blk, hipMemcpyDeviceToDevice, st));
+    return;
+  }
+  // the kernel reads block `me` of every rank at offset me*nbytes of the
+  // published base; with chunking the staged layout is [p][chunk].
+  if (symmetric) {
+    uint64_t sc = code_of_(in, blk * size_);
+    if (!sc || out % 16) throw std::invalid_argument("ccmpi: symmetric reduce_scatter needs aligned registered input");
+    launch_reduce_scatter(args_(sc, 0, (char*)out, blk, 0), size_, dtype, op, grid_(blk, max_blocks), st);
+    return;
+  }
+  uint64_t chunk = (scratch_bytes() / 2 / size_) / (16 * es) * (16 * es);
+  if (chunk == 0) throw std::runtime_error("ccmpi: scratch too small for reduce_scatter");
+  char* stage = reinterpret_cast<char*>(scratch_ptr());
+  for (uint64_t off = 0; off < blk; off += chunk) {
+    const uint64_t n = std::min(chunk, blk - off);
+    for (int j = 0; j < size_; ++j)
+      CCMPI_HIP_CHECK(hipMemcpyAsync(stage + j * n, (void*)(in + j * blk + off), n, hipMemcpyDeviceToDevice, st));
+    const bool out_ok = (out + off) % 16 == 0;
+    char* outp = out_ok ? (char*)(out + off) : stage + scratch_bytes() / 2;
+    launch_reduce_scatter(args_(addr_code(0, 0), 0, outp, n, 0), size_, dtype, op, grid_(n, max_blocks), st);
+    if (!out_ok) CCMPI_HIP_CHECK(hipMemcpyAsync((void*)(out + off), outp, n, hipMemcpyDeviceToDevice, st));
+  }
+}
+
+void DeviceComm::allgather(uint64_t in, uint64_t out, uint64_t bytes_per_rank, uint64_t stream, int max_blocks,
+                           bool symmetric) {
+  if (bytes_per_rank == 0) return;
+  CCMPI_HIP_CHECK(hipSetDevice(device_));
+  hipStream_t st = S(stream);
+  if (size_ == 1) {
+    if (in != out) CCMPI_HIP_CHECK(hipMemcpyAsync((void*)out, (void*)in, bytes_per_rank, hipMemcpyDeviceToDevice, st));
+    return;
+  }
+  if (symmetric) {
+    uint64_t sc = code_of_(in, bytes_per_rank);
+    if (!sc || out % 16 || bytes_per_rank % 16) {
+      if (!sc) throw std::invalid_argument("ccmpi: symmetric allgather needs an aligned registered input");
+    }
+    if (out % 16 == 0 && bytes_per_rank % 16 == 0) {
+      launch_move(MOVE_ALLGATHER, args_(sc, 0, (char*)out, bytes_per_rank, 0), size_, grid_(bytes_per_rank * size_, max_blocks), st);
+      return;
+    }
+  }
+  // chunk over the per-rank block; destination blocks are strided by
+  // bytes_per_rank so each chunk gathers into a [p][n] staging area first
+  // unless the output layout can take it directly (n == bytes_per_rank).
+  uint64_t chunk = (scratch_bytes() / 2 / (size_ + 1)) / 16 * 16;
+  if (chunk == 0) throw std::runtime_error("ccmpi: scratch too small for allgather");
+  char* stage = reinterpret_cast<char*>(scratch_ptr());
+  char* gath = stage + chunk;
+  for (uint64_t off = 0; off < bytes_per_rank; off += chunk) {
+    const uint64_t n = std::min(chunk, bytes_per_rank - off);
+    uint64_t sc = code_of_(in + off, n);
+    if (!sc) {
+      CCMPI_HIP_CHECK(hipMemcpyAsync(stage, (void*)(in + off), n, hipMemcpyDeviceToDevice, st));
+      sc = addr_code(0, 0);
+    }
+    const bool direct = (n == bytes_per_rank) && out % 16 == 0 && n % 16 == 0;
+    char* dst = direct ? (char*)out : gath;
+    launch_move(MOVE_ALLGATHER, args_(sc, 0, dst, n, 0), size_, grid_(n * size_, max_blocks), st);
+    if (!direct)
+      CCMPI_HIP_CHECK(hipMemcpy2DAsync((void*)(out + off), bytes_per_rank, gath, n, n, size_, hipMemcpyDeviceToDevice, st));
+  }
+}
+
+void DeviceComm::alltoall(uint64_t in, uint64_t out, uint64_t bytes_per_peer, uint64_t stream, int max_blocks,
+                          bool symmetric) {
+  if (bytes_per_peer == 0) return;
+  CCMPI_HIP_CHECK(hipSetDevice(device_));
+  hipStream_t st = S(stream);
+  if (size_ == 1) {
+    if (in != out) CCMPI_HIP_CHECK(hipMemcpyAsync((void*)out, (void*)in, bytes_per_peer, hipMemcpyDeviceToDevice, st));
+    return;
+  }
+  const uint64_t total = bytes_per_peer * size_;
+  if (symmetric && in != out && out % 16 == 0 && bytes_per_peer % 16 == 0) {
+    uint64_t sc = code_of_(in, total);
+    if (!sc) throw std::invalid_argument("ccmpi: symmetric alltoall needs an aligned registered input");
+    launch_move(MOVE_ALLTOALL, args_(sc, 0, (char*)out, bytes_per_peer, 0), size_, grid_(total, max_blocks), st);
+    return;
+  }
+  uint64_t chunk = (scratch_bytes() / 2 / size_) / 16 * 16;
+  if (chunk == 0) throw std::runtime_error("ccmpi: scratch too small for alltoall");
+  char* stage = reinterpret_cast<char*>(scratch_ptr());
+  char* gath = stage + scratch_bytes() / 2;
+  for (uint64_t off = 0; off < bytes_per_peer; off += chunk) {
+    const uint64_t n = std::min(chunk, bytes_per_peer - off);
+    // pack [p][n] (always staged: the reader indexes my block at me*n)
+    CCMPI_HIP_CHECK(hipMemcpy2DAsync(stage, n, (void*)(in + off), bytes_per_peer, n, size_, hipMemcpyDeviceToDevice, st));
+    launch_move(MOVE_ALLTOALL, args_(addr_code(0, 0), 0, gath, n, 0), size_, grid_(n * size_, max_blocks), st);
+    CCMPI_HIP_CHECK(hipMemcpy2DAsync((void*)(out + off), bytes_per_peer, gath, n, n, size_, hipMemcpyDeviceToDevice, st));
+  }
+}
+
+void DeviceComm::bcast(uint64_t buf, uint64_t nbytes, int root, uint64_t stream, int max_blocks, bool symmetric) {
+  if (nbytes == 0 || size_ == 1) return;
+  CCMPI_HIP_CHECK(hipSetDevice(device_));
+  hipStream_t st = S(stream);
+  if (symmetric && buf % 16 == 0) {
+    uint64_t sc = code_of_(buf, nbytes);
+    if (!sc) throw std::invalid_argument("ccmpi: symmetric bcast needs an aligned registered buffer");
+    launch_move(MOVE_BCAST, args_(sc, 0, (char*)buf, nbytes, root), size_, grid_(nbytes, max_blocks), st);
+    return;
+  }
+  uint64_t chunk = (scratch_bytes() / 2) / 16 * 16;
+  char* stage = reinterpret_cast<char*>(scratch_ptr());
+  for (uint64_t off = 0; off < nbytes; off += chunk) {
+    const uint64_t n = std::min(chunk, nbytes - off);
+    uint64_t sc = code_of_(buf + off, n);
+    if (!sc || rank_ == root) {
+      if (rank_ == root) CCMPI_HIP_CHECK(hipMemcpyAsync(stage, (void*)(buf + off), n, hipMemcpyDeviceToDevice, st));
+      sc = addr_code(0, 0);
+    }
+    const bool out_ok = (buf + off) % 16 == 0;
+    char* dst = out_ok ? (char*)(buf + off) : stage + chunk;
+    launch_move(MOVE_BCAST, args_(sc, 0, dst, n, root), size_, grid_(n, max_blocks), st);
+    if (!out_ok && rank_ != root)
+      CCMPI_HIP_CHECK(hipMemcpyAsync((void*)(buf + off), dst, n, hipMemcpyDeviceToDevice, st));
+  }
+}
+
+void DeviceComm::local_reduce(const std::vector<uint64_t>& ins, uint64_t out, uint64_t count, int dtype, int op,
+                              uint64_t stream) {
+  if (ins.empty() || ins.size() > (size_t)kMaxRanks) throw std::invalid_argument("ccmpi: local_reduce takes 1..16 inputs");
+  LocalReduceArgs a{};
+  for (size_t i = 0; i < ins.size(); ++i) {
+    if (ins[i] % 16) throw std::invalid_argument("ccmpi: local_reduce inputs must be 16-B aligned");
+    a.in[i] = reinterpret_cast<const char*>(ins[i]);
+  }
+  if (out % 16) throw std::invalid_argument("ccmpi: local_reduce output must be 16-B aligned");
+  a.n_in = (int)ins.size();
+  a.out = reinterpret_cast<char*>(out);
+  a.nbytes = count * dtype_bytes(dtype);
+  if (!a.nbytes) return;
+  CCMPI_HIP_CHECK(hipSetDevice(device_));
+  launch_local_reduce(a, dtype, op, S(stream));
+}
+
+// ---------------------------------------------------------------------------
+// RCCL
+// ---------------------------------------------------------------------------
+std::string DeviceComm::rccl_unique_id() {
+  ncclUniqueId id;
+  CCMPI_NCCL_CHECK(ncclGetUniqueId(&id));
+  return std::string(reinterpret_cast<const char*>(&id), sizeof(id));
+}
+
+void DeviceComm::rccl_init(const std::string& uid) {
+  if (nccl_) return;
+  if (uid.size() != sizeof(ncclUniqueId)) throw std::invalid_argument("ccmpi: bad RCCL unique id");
+  ncclUniqueId id;
+  std::memcpy(&id, uid.data(), sizeof(id));
+  CCMPI_HIP_CHECK(hipSetDevice(device_));
+  CCMPI_NCCL_CHECK(ncclCommInitRank(&nccl_, size_, id, rank_));
+}
+
+#define CCMPI_NEED_RCCL() \
+  if (!nccl_) throw std::runtime_error("ccmpi: RCCL communicator not initialised")
+
+void DeviceComm::rccl_allreduce(uint64_t in, uint64_t out, uint64_t count, int dtype, int op, uint64_t stream) {
+  CCMPI_NEED_RCCL();
+  CCMPI_NCCL_CHECK(ncclAllReduce((void*)in, (void*)out, count, nccl_dt(dtype), nccl_op(op), nccl_, S(stream)));
+}
+
+void DeviceComm::rccl_reduce_scatter(uint64_t in, uint64_t out, uint64_t count, int dtype, int op, uint64_t stream) {
+  CCMPI_NEED_RCCL();
+  CCMPI_NCCL_CHECK(ncclReduceScatter((void*)in, (void*)out, count, nccl_dt(dtype), nccl_op(op), nccl_, S(stream)));
+}
+
+void DeviceComm::rccl_allgather(uint64_t in, uint64_t out, uint64_t count, int dtype, uint64_t stream) {
+  CCMPI_NEED_RCCL();
+  CCMPI_NCCL_CHECK(ncclAllGather((void*)in, (void*)out, count, nccl_dt(dtype), nccl_, S(stream)));
+}
+
+void DeviceComm::rccl_alltoall(uint64_t in, uint64_t out, uint64_t count, int dtype, uint64_t stream) {
+  CCMPI_NEED_RCCL();
+  CCMPI_NCCL_CHECK(ncclAllToAll((void*)in, (void*)out, count, nccl_dt(dtype), nccl_, S(stream)));
+}
+
+void DeviceComm::rccl_bcast(uint64_t buf, uint64_t count, int dtype, int root, uint64_t stream) {
+  CCMPI_NEED_RCCL();
+  CCMPI_NCCL_CHECK(ncclBroadcast((void*)buf, (void*)buf, count, nccl_dt(dtype), root, nccl_, S(stream)));
+}
+
+namespace {
+int gcd(int a, int b) { return b ? gcd(b, a % b) : a; }
+int modinv(int a, int m) {
+  for (int x = 1; x < m; ++x)
+    if ((a * x) % m == 1) return x;
+  return 1;
+}
+}  // namespace
+
+void DeviceComm::p2p_ring_allreduce(uint64_t buf, uint64_t count, int dtype, int op, uint64_t stream, int rings,
+                                    uint64_t tmp) {
+  CCMPI_NEED_RCCL();
+  const int p = size_;
+  if (p == 1 || count == 0) return;
+  const uint64_t es = dtype_bytes(dtype);
+  const uint64_t q = std::max<uint64_t>(1, 16 / es);  // elements per 16 B
+  hipStream_t st = S(stream);
+  ncclDataType_t ndt = nccl_dt(dtype);
+  // strides coprime to p -> Hamiltonian rings i -> i+s (mod p)
+  std::vector<int> strides;
+  for (int s = 1; s < p && (int)strides.size() < std::max(1, rings); ++s)
+    if (gcd(s, p) == 1) strides.push_back(s);
+  const int R = (int)strides.size();
+  // element layout: ring k owns part k; each part has p chunks (16-B aligned)
+  std::vector<uint64_t> part_lo(R + 1);
+  for (int k = 0; k <= R; ++k) part_lo[k] = (count * k / R) / q * q;
+  part_lo[R] = count;
+  auto chunk_of = [&](int k, int c, uint64_t* lo, uint64_t* n) {
+    uint64_t plo = part_lo[k], pn = part_lo[k + 1] - plo;
+    uint64_t a = (pn * c / p) / q * q, b = c + 1 == p ? pn : (pn * (c + 1) / p) / q * q;
+    *lo = plo + a;
+    *n = b - a;
+  };
+  // temp area per ring: the largest chunk of that ring
+  std::vector<uint64_t> tmp_off(R + 1, 0);
+  for (int k = 0; k < R; ++k) {
+    uint64_t mx = 0;
+    for (int c = 0; c < p; ++c) { uint64_t lo, n; chunk_of(k, c, &lo, &n); mx = std::max(mx, n); }
+    tmp_off[k + 1] = tmp_off[k] + (mx * es + 15) / 16 * 16;
+  }
+  std::vector<int> idx(R), right(R), left(R);
+  for (int k = 0; k < R; ++k) {
+    int s = strides[k];
+    idx[k] = (rank_ * modinv(s, p)) % p;  // position in ring 0, s, 2s, ...
+    right[k] = (rank_ + s) % p;
+    left[k] = (rank_ - s + p) % p;
+  }
+  char* b = reinterpret_cast<char*>(buf);
+  char* t = reinterpret_cast<char*>(tmp);
+  // reduce-scatter
+  for (int step = 0; step < p - 1; ++step) {
+    CCMPI_NCCL_CHECK(ncclGroupStart());
+    for (int k = 0; k < R; ++k) {
+      uint64_t slo, sn, rlo, rn;
+      chunk_of(k, ((idx[k] - step) % p + p) % p, &slo, &sn);
+      chunk_of(k, ((idx[k] - step - 1) % p + p) % p, &rlo, &rn);
+      if (sn) CCMPI_NCCL_CHECK(ncclSend(b + slo * es, sn, ndt, right[k], nccl_, st));
+      if (rn) CCMPI_NCCL_CHECK(ncclRecv(t + tmp_off[k], rn, ndt, left[k], nccl_, st));
+    }
+    CCMPI_NCCL_CHECK(ncclGroupEnd());
+    for (int k = 0; k < R; ++k) {
+      uint64_t rlo, rn;
+      chunk_of(k, ((idx[k] - step - 1) % p + p) % p, &rlo, &rn);
+      if (rn) local_reduce({(uint64_t)(b + rlo * es), (uint64_t)(t + tmp_off[k])}, (uint64_t)(b + rlo * es), rn, dtype, op, stream);
+    }
+  }
+  // all-gather: rank holds reduced chunk idx+1
+  for (int step = 0; step < p - 1; ++step) {
+    CCMPI_NCCL_CHECK(ncclGroupStart());
+    for (int k = 0; k < R; ++k) {
+      uint64_t slo, sn, rlo, rn;
+      chunk_of(k, ((idx[k] + 1 - step) % p + p) % p, &slo, &sn);
+      chunk_of(k, ((idx[k] - step) % p + p) % p, &rlo, &rn);
+      if (sn) CCMPI_NCCL_CHECK(ncclSend(b + slo * es, sn, ndt, right[k], nccl_, st));
+      if (rn) CCMPI_NCCL_CHECK(ncclRecv(b + rlo * es, rn, ndt, left[k], nccl_, st));
+    }
+    CCMPI_NCCL_CHECK(ncclGroupEnd());
+  }
+}
+
+void DeviceComm::p2p_rhd_allreduce(uint64_t buf, uint64_t count, int dtype, int op, uint64_t stream, uint64_t tmp) {
+  CCMPI_NEED_RCCL();
+  const int p = size_;
+  if (p == 1 || count == 0) return;
+  if (p & (p - 1)) throw std::invalid_argument("ccmpi: recursive halving-doubling needs a power-of-two rank count");
+  const uint64_t es = dtype_bytes(dtype);
+  const uint64_t q = std::max<uint64_t>(1, 16 / es);
+  hipStream_t st = S(stream);
+  ncclDataType_t ndt = nccl_dt(dtype);
+  char* b = reinterpret_cast<char*>(buf);
+  char* t = reinterpret_cast<char*>(tmp);
+  auto cut = [&](uint64_t lo, uint64_t hi) { uint64_t m = lo + ((hi - lo) / 2) / q * q; return m; };
+  uint64_t lo = 0, hi = count;
+  std::vector<std::pair<uint64_t, uint64_t>> hist;
+  for (int mask = p / 2; mask >= 1; mask /= 2) {
+    const int partner = rank_ ^ mask;
+    const uint64_t mid = cut(lo, hi);
+    uint64_t keep_lo, keep_hi, send_lo, send_hi;
+    if (rank_ & mask) { keep_lo = mid; keep_hi = hi; send_lo = lo; send_hi = mid; }
+    else { keep_lo = lo; keep_hi = mid; send_lo = mid; send_hi = hi; }
+    CCMPI_NCCL_CHECK(ncclGroupStart());
+    if (send_hi > send_lo) CCMPI_NCCL_CHECK(ncclSend(b + send_lo * es, send_hi - send_lo, ndt, partner, nccl_, st));
+    if (keep_hi > keep_lo) CCMPI_NCCL_CHECK(ncclRecv(t, keep_hi - keep_lo, ndt, partner, nccl_, st));
+    CCMPI_NCCL_CHECK(ncclGroupEnd());
+    if (keep_hi > keep_lo)
+      local_reduce({(uint64_t)(b + keep_lo * es), (uint64_t)t}, (uint64_t)(b + keep_lo * es), keep_hi - keep_lo, dtype, op, stream);
+    hist.push_back({lo, hi});
+    lo = keep_lo;
+    hi = keep_hi;
+  }
+  for (int mask = 1; mask <= p / 2; mask *= 2) {
+    const int partner = rank_ ^ mask;
+    auto prev = hist.back();
+    hist.pop_back();
+    // partner owns the other half of `prev`
+    uint64_t olo = (lo == prev.first) ? hi : prev.first;
+    uint64_t ohi = (lo == prev.first) ? prev.second : lo;
+    CCMPI_NCCL_CHECK(ncclGroupStart());
+    if (hi > lo) CCMPI_NCCL_CHECK(ncclSend(b + lo * es, hi - lo, ndt, partner, nccl_, st));
+    if (ohi > olo) CCMPI_NCCL_CHECK(ncclRecv(b + olo * es, ohi - olo, ndt, partner, nccl_, st));
+    CCMPI_NCCL_CHECK(ncclGroupEnd());
+    lo = prev.first;
+    hi = prev.second;
+  }
+}
+
+void DeviceComm::p2p_pairwise_alltoall(uint64_t in, uint64_t out, uint64_t bytes_per_peer, uint64_t stream) {
+  CCMPI_NEED_RCCL();
+  hipStream_t st = S(stream);
+  char* i = reinterpret_cast<char*>(in);
+  char* o = reinterpret_cast<char*>(out);
+  CCMPI_HIP_CHECK(hipMemcpyAsync(o + rank_ * bytes_per_peer, i + rank_ * bytes_per_peer, bytes_per_peer,
+                                 hipMemcpyDeviceToDevice, st));
+  // reference myAlltoall2 (mpi_wrapper/comm.py:162-199): pairwise rounds; round k
+  // exchanges with rank+k / rank-k, each round one grouped send+recv.
+  for (int k = 1; k < size_; ++k) {
+    int to = (rank_ + k) % size_, from = (rank_ - k + size_) % size_;
+    CCMPI_NCCL_CHECK(ncclGroupStart());
+    CCMPI_NCCL_CHECK(ncclSend(i + to * bytes_per_peer, bytes_per_peer, ncclUint8, to, nccl_, st));
+    CCMPI_NCCL_CHECK(ncclRecv(o + from * bytes_per_peer, bytes_per_peer, ncclUint8, from, nccl_, st));
+    CCMPI_NCCL_CHECK(ncclGroupEnd());
+  }
+}
+
+uint32_t DeviceComm::error_code() {
+  CCMPI_HIP_CHECK(hipSetDevice(device_));
+  CCMPI_HIP_CHECK(hipDeviceSynchronize());
+  uint32_t e = 0;
+  CCMPI_HIP_CHECK(hipMemcpy(&e, &sig_->error, sizeof(e), hipMemcpyDeviceToHost));
+  return e;
+}
+
+void DeviceComm::clear_error() {
+  CCMPI_HIP_CHECK(hipSetDevice(device_));
+  CCMPI_HIP_CHECK(hipMemset(&sig_->error, 0, sizeof(uint32_t)));
+}
+
+}  // namespace dev
+}  // namespace ccmpi

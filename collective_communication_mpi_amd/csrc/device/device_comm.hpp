@@ -1,0 +1,117 @@
+// Device communicator: one per (host communicator, process).  Owns
+//  * the uncached signal buffer peers write flags into (IPC-exported),
+//  * per-CTA epoch counters,
+//  * the device-resident PeerTable (peer signal buffers + symmetric segments),
+//  * a symmetric scratch segment used to stage non-registered tensors,
+//  * optionally an RCCL communicator (library baseline + P2P schedules).
+// Bootstrap data (IPC handles, RCCL unique id) is exchanged by the Python
+// layer over the host plane; this class never talks to other processes itself.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <map>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "collectives.hpp"
+#include "common.hpp"
+
+namespace ccmpi {
+namespace dev {
+
+struct SegInfo {
+  char* local = nullptr;   // this rank's base
+  uint64_t bytes = 0;
+  bool owned = false;      // allocated by us (freed in dtor)
+};
+
+class DeviceComm {
+ public:
+  DeviceComm(int rank, int size, int device, uint64_t scratch_bytes);
+  ~DeviceComm();
+
+  int rank() const { return rank_; }
+  int size() const { return size_; }
+  int device() const { return device_; }
+
+  // ---- bootstrap ---------------------------------------------------------
+  std::string signal_handle() const;                       // IPC handle bytes of my Signals
+  void connect(const std::vector<std::string>& sig_handles);
+  // Register a local range as symmetric segment `seg` (collective, same index
+  // on every rank).  Returns (handle bytes, offset from allocation base).
+  std::pair<std::string, uint64_t> export_range(uint64_t ptr) const;
+  int add_segment(uint64_t local_ptr, uint64_t bytes,
+                  const std::vector<std::string>& handles, const std::vector<uint64_t>& offsets);
+  int scratch_segment() const { return 0; }
+  uint64_t scratch_bytes() const { return segs_.empty() ? 0 : segs_[0].bytes; }
+  uint64_t scratch_ptr() const { return segs_.empty() ? 0 : (uint64_t)segs_[0].local; }
+  // (segment, offset) of a local pointer, or -1 if not inside a segment
+  int find(uint64_t ptr, uint64_t nbytes, uint64_t* off) const;
+
+  // ---- hand-written collectives (stream-ordered, graph-capturable) ----------
+  // `symmetric`: caller guarantees every rank passes registered buffers, so
+  // no staging/chunking is needed.  Otherwise inputs are staged through the
+  // scratch segment in chunks whose size is identical on all ranks.
+  void allreduce(uint64_t in, uint64_t out, uint64_t count, int dtype, int op, int algo,
+                 uint64_t stream, int max_blocks, bool symmetric);
+  void reduce_scatter(uint64_t in, uint64_t out, uint64_t count_per_rank, int dtype, int op,
+                      uint64_t stream, int max_blocks, bool symmetric);
+  void allgather(uint64_t in, uint64_t out, uint64_t bytes_per_rank, uint64_t stream, int max_blocks,
+                 bool symmetric);
+  void alltoall(uint64_t in, uint64_t out, uint64_t bytes_per_peer, uint64_t stream, int max_blocks,
+                bool symmetric);
+  void bcast(uint64_t buf, uint64_t nbytes, int root, uint64_t stream, int max_blocks, bool symmetric);
+  void local_reduce(const std::vector<uint64_t>& ins, uint64_t out, uint64_t count, int dtype, int op,
+                    uint64_t stream);
+
+  // ---- RCCL (vendor library: baseline + P2P transport) ---------------------
+  static std::string rccl_unique_id();
+  void rccl_init(const std::string& uid);
+  bool rccl_ready() const { return nccl_ != nullptr; }
+  void rccl_allreduce(uint64_t in, uint64_t out, uint64_t count, int dtype, int op, uint64_t stream);
+  void rccl_reduce_scatter(uint64_t in, uint64_t out, uint64_t count, int dtype, int op, uint64_t stream);
+  void rccl_allgather(uint64_t in, uint64_t out, uint64_t count, int dtype, uint64_t stream);
+  void rccl_alltoall(uint64_t in, uint64_t out, uint64_t count, int dtype, uint64_t stream);
+  void rccl_bcast(uint64_t buf, uint64_t count, int dtype, int root, uint64_t stream);
+  // Ring / recursive-halving-doubling all-reduce built from RCCL send/recv plus
+  // our local reduction kernel (north-star "hand-written on RCCL P2P").
+  // `rings` concurrent rings with strides coprime to p use that many links.
+  void p2p_ring_allreduce(uint64_t buf, uint64_t count, int dtype, int op, uint64_t stream, int rings,
+                          uint64_t tmp);
+  void p2p_rhd_allreduce(uint64_t buf, uint64_t count, int dtype, int op, uint64_t stream, uint64_t tmp);
+  void p2p_pairwise_alltoall(uint64_t in, uint64_t out, uint64_t bytes_per_peer, uint64_t stream);
+
+  // ---- health ------------------------------------------------------------
+  uint32_t error_code();  // synchronises; 0 = ok
+  void clear_error();
+  uint64_t timeout_ticks() const { return timeout_ticks_; }
+  void set_timeout_seconds(double s) { timeout_ticks_ = (uint64_t)(s * 1e8); }
+
+ private:
+  void sync_table_();
+  CollArgs args_(uint64_t src_code, uint64_t res_code, char* out, uint64_t nbytes, int root) const;
+  int grid_(uint64_t work_bytes, int max_blocks) const;
+  uint64_t code_of_(uint64_t ptr, uint64_t nbytes) const;  // 0 if not registered / misaligned
+
+  int rank_, size_, device_;
+  Signals* sig_ = nullptr;               // mine (uncached)
+  std::vector<Signals*> peer_sig_;       // mapped (mine at [rank_])
+  std::vector<SegInfo> segs_;            // [0] = scratch
+  std::vector<std::vector<char*>> peer_seg_;  // [seg][rank]
+  PeerTable host_pt_{};
+  PeerTable* dev_pt_ = nullptr;
+  uint64_t* epochs_ = nullptr;
+  uint64_t timeout_ticks_ = 2000000000ull;  // 20 s
+  ncclComm_t nccl_ = nullptr;
+  std::vector<std::string> opened_;      // handles we opened (for release)
+};
+
+// Process-wide registry so a handle opened by two communicators maps once.
+void* ipc_open(const std::string& handle);
+void ipc_close(const std::string& handle);
+
+}  // namespace dev
+}  // namespace ccmpi

@@ -1,0 +1,14 @@
+// Collects every op family's pybind registration.
+#include "ops.hpp"
+
+namespace ccmpi {
+namespace dev {
+
+void register_layout_ops(pybind11::module_& m);
+
+void register_ops(pybind11::module_& m) {
+  register_layout_ops(m);
+}
+
+}  // namespace dev
+}  // namespace ccmpi

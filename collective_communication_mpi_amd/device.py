@@ -1,0 +1,296 @@
+"""Device plane: GPU collectives for one host communicator.
+
+``DeviceGroup`` owns a native ``DeviceComm`` (csrc/device/device_comm.cpp) and
+bootstraps it over the host plane: signal-buffer and symmetric-segment IPC
+handles are exchanged with the host all-gather, the RCCL unique id with the
+host broadcast.  Collectives run on the caller's current HIP stream, so they
+order with surrounding torch work and can be captured in a HIP graph.
+
+Algorithms (``algo=``):
+
+=================  ============================================================
+``oneshot``        every rank pulls all peers' buffers and reduces (latency)
+``twoshot``        reduce-scatter + all-gather, all peers in flight (bandwidth)
+``reduce_bcast``   the reference myAllreduce algorithm (mpi_wrapper/comm.py:63)
+``ring``           RCCL send/recv rings + our LDS-free reduction kernel;
+                   ``rings=k`` concurrent rings with coprime strides use k links
+``rhd``            recursive halving/doubling over RCCL send/recv
+``rccl``           vendor RCCL collective (the "library" baseline)
+``auto``           tuned choice (size thresholds; ``tune()`` measures them)
+=================  ============================================================
+
+Tensors obtained from :meth:`DeviceGroup.empty` live in symmetric segments
+(same offset on every rank, peer-mapped once), so collectives on them need no
+staging.  Any other CUDA tensor works too: it is staged through the scratch
+segment in identically sized chunks on every rank.
+"""
+from __future__ import annotations
+
+import os
+import threading
+from typing import Dict, List, Optional, Sequence, Tuple
+
+from . import _native
+
+_OPS = {"SUM": 0, "PROD": 1, "MIN": 2, "MAX": 3}
+
+
+def op_code(op) -> int:
+    """Map MPI.Op / string / int to the device op code."""
+    if isinstance(op, int):
+        return op
+    name = getattr(op, "name", op)
+    try:
+        return _OPS[str(name).upper()]
+    except KeyError:
+        raise NotImplementedError(f"device reduction op {op!r} not supported (SUM, PROD, MIN, MAX)") from None
+
+
+def dtype_code(torch_dtype) -> int:
+    import torch
+
+    table = {
+        torch.int8: 0, torch.uint8: 1, torch.int16: 2, torch.int32: 4, torch.int64: 6,
+        torch.float16: 8, torch.bfloat16: 9, torch.float32: 10, torch.float64: 11, torch.bool: 12,
+    }
+    try:
+        return table[torch_dtype]
+    except KeyError:
+        raise TypeError(f"unsupported device dtype {torch_dtype}") from None
+
+
+def _env_int(name: str, default: int) -> int:
+    v = os.environ.get(name)
+    return int(v) if v else default
+
+
+class DeviceGroup:
+    """GPU side of a communicator (one per host communicator per process)."""
+
+    def __init__(self, host_comm, device=None, scratch_bytes: Optional[int] = None) -> None:
+        import torch
+
+        self.torch = torch
+        self.host = host_comm
+        self.rank = host_comm.Get_rank()
+        self.size = host_comm.Get_size()
+        if device is None:
+            n = torch.cuda.device_count()
+            local = int(os.environ.get("CCMPI_LOCAL_RANK", os.environ.get("LOCAL_RANK", "0")))
+            device = torch.device("cuda", local % max(n, 1))
+        self.device = torch.device(device)
+        torch.cuda.set_device(self.device)
+        self.D = _native.device()
+        self.dc = self.D.DeviceComm(self.rank, self.size, self.device.index or 0)
+        self.dc.connect([bytes(h) for h in host_comm.allgather(bytes(self.dc.signal_handle()))])
+        # how many ranks share each physical GPU (multi-process-per-GPU testing):
+        # all their CTAs must be co-resident, so the grid is capped.
+        props = torch.cuda.get_device_properties(self.device)
+        key = f"{getattr(props, 'pci_bus_id', 0)}:{getattr(props, 'pci_device_id', 0)}:{props.name}:{self.device.index}"
+        keys = host_comm.allgather(key)
+        self.ranks_per_device = keys.count(key)
+        self.shared_device = self.ranks_per_device > 1
+        default_blocks = 256 if not self.shared_device else max(1, 96 // self.ranks_per_device)
+        self.max_blocks = _env_int("CCMPI_MAX_BLOCKS", default_blocks)
+        if scratch_bytes is None:
+            scratch_bytes = _env_int("CCMPI_SCRATCH_MB", 64 if self.shared_device else 512) << 20
+        self._keep: List = []
+        self._pool: List[Tuple[object, int, int]] = []  # (tensor, used, cap) sub-allocation pools
+        self.scratch = torch.empty(max(scratch_bytes, 1 << 16), dtype=torch.uint8, device=self.device)
+        seg = self._register(self.scratch)
+        assert seg == 0, "scratch must be segment 0"
+        self._rccl = False
+        self.oneshot_max = _env_int("CCMPI_ONESHOT_MAX_BYTES", 256 << 10)
+        self.tuned: Dict[Tuple[int, int], str] = {}
+        self._lock = threading.Lock()
+
+    # ------------------------------------------------------------------ memory
+    def _register(self, t) -> int:
+        """Collectively register tensor storage as a symmetric segment."""
+        h, off = self.dc.export_range(t.data_ptr())
+        allh = self.host.allgather((bytes(h), int(off)))
+        seg = self.dc.add_segment(t.data_ptr(), t.numel() * t.element_size(),
+                                  [x[0] for x in allh], [x[1] for x in allh])
+        self._keep.append(t)
+        return seg
+
+    def empty(self, shape, dtype=None, pool_bytes: int = 64 << 20):
+        """Collective symmetric allocation (same call sequence on every rank).
+
+        Large tensors get their own segment; small ones are carved (256-B
+        aligned) from a shared pooled segment.  Memory lives until the group dies.
+        """
+        torch = self.torch
+        dtype = dtype or torch.float32
+        if isinstance(shape, int):
+            shape = (shape,)
+        n = 1
+        for s in shape:
+            n *= int(s)
+        nbytes = n * torch.empty((), dtype=dtype).element_size()
+        need = (max(nbytes, 1) + 255) // 256 * 256
+        if need >= pool_bytes // 4:
+            raw = torch.empty(need, dtype=torch.uint8, device=self.device)
+            self._register(raw)
+            return raw[:nbytes].view(dtype).view(shape)
+        for i, (buf, used, cap) in enumerate(self._pool):
+            if used + need <= cap:
+                self._pool[i] = (buf, used + need, cap)
+                return buf[used:used + nbytes].view(dtype).view(shape)
+        buf = torch.empty(pool_bytes, dtype=torch.uint8, device=self.device)
+        self._register(buf)
+        self._pool.append((buf, need, pool_bytes))
+        return buf[:nbytes].view(dtype).view(shape)
+
+    def zeros(self, shape, dtype=None):
+        t = self.empty(shape, dtype)
+        t.zero_()
+        return t
+
+    def is_symmetric(self, t) -> bool:
+        seg, _ = self.dc.find(t.data_ptr(), t.numel() * t.element_size())
+        return seg > 0
+
+    # -------------------------------------------------------------------- rccl
+    def ensure_rccl(self) -> None:
+        """Collective: create the RCCL communicator on first use."""
+        if self._rccl:
+            return
+        uid = self.D.rccl_unique_id() if self.rank == 0 else None
+        uid = self.host.bcast(uid, root=0)
+        self.dc.rccl_init(uid)
+        self._rccl = True
+
+    # ----------------------------------------------------------------- helpers
+    def _stream(self) -> int:
+        return self.torch.cuda.current_stream(self.device).cuda_stream
+
+    def _check(self, t, name: str):
+        if not (hasattr(t, "is_cuda") and t.is_cuda):
+            raise TypeError(f"{name} must be a CUDA tensor")
+        if not t.is_contiguous():
+            raise ValueError(f"{name} must be contiguous")
+        return t
+
+    def _symm(self, *ts) -> bool:
+        return all(self.is_symmetric(t) and t.data_ptr() % 16 == 0 for t in ts)
+
+    def pick_allreduce(self, nbytes: int) -> str:
+        if self.size == 1:
+            return "twoshot"
+        key = (self.size, max(0, nbytes.bit_length() - 1))
+        if key in self.tuned:
+            return self.tuned[key]
+        forced = os.environ.get("CCMPI_ALLREDUCE_ALGO")
+        if forced:
+            return forced
+        return "oneshot" if nbytes <= self.oneshot_max else "twoshot"
+
+    # ------------------------------------------------------------- collectives
+    def allreduce(self, src, dst=None, op="SUM", algo: str = "auto", rings: int = 0) -> object:
+        dst = src if dst is None else dst
+        self._check(src, "src")
+        self._check(dst, "dst")
+        if src.numel() != dst.numel() or src.dtype != dst.dtype:
+            raise ValueError("allreduce: src/dst must match in size and dtype")
+        opc, dt = op_code(op), dtype_code(src.dtype)
+        nbytes = src.numel() * src.element_size()
+        if algo == "auto":
+            algo = self.pick_allreduce(nbytes)
+        s = self._stream()
+        if algo in ("oneshot", "twoshot", "reduce_bcast"):
+            a = {"oneshot": self.D.ALGO_ONESHOT, "twoshot": self.D.ALGO_TWOSHOT,
+                 "reduce_bcast": self.D.ALGO_REDUCE_BCAST}[algo]
+            self.dc.allreduce(src.data_ptr(), dst.data_ptr(), src.numel(), dt, opc, a, s, self.max_blocks,
+                              self._symm(src, dst))
+        elif algo == "rccl":
+            self.ensure_rccl()
+            self.dc.rccl_allreduce(src.data_ptr(), dst.data_ptr(), src.numel(), dt, opc, s)
+        elif algo in ("ring", "rhd"):
+            self.ensure_rccl()
+            if dst.data_ptr() != src.data_ptr():
+                dst.copy_(src)
+            need = (nbytes // max(1, self.size) + 4096) * 2
+            tmp = self.scratch if need <= self.scratch.numel() else self.torch.empty(need, dtype=self.torch.uint8, device=self.device)
+            if algo == "ring":
+                k = rings or _env_int("CCMPI_RINGS", 1)
+                self.dc.p2p_ring_allreduce(dst.data_ptr(), dst.numel(), dt, opc, s, k, tmp.data_ptr())
+            else:
+                self.dc.p2p_rhd_allreduce(dst.data_ptr(), dst.numel(), dt, opc, s, tmp.data_ptr())
+        else:
+            raise ValueError(f"unknown allreduce algorithm {algo!r}")
+        return dst
+
+    def reduce_scatter(self, src, dst, op="SUM", algo: str = "direct"):
+        self._check(src, "src")
+        self._check(dst, "dst")
+        if src.numel() != dst.numel() * self.size:
+            raise ValueError("reduce_scatter: src must hold size * dst elements")
+        opc, dt = op_code(op), dtype_code(src.dtype)
+        s = self._stream()
+        if algo == "rccl":
+            self.ensure_rccl()
+            self.dc.rccl_reduce_scatter(src.data_ptr(), dst.data_ptr(), dst.numel(), dt, opc, s)
+        else:
+            self.dc.reduce_scatter(src.data_ptr(), dst.data_ptr(), dst.numel(), dt, opc, s, self.max_blocks,
+                                   self._symm(src))
+        return dst
+
+    def allgather(self, src, dst, algo: str = "direct"):
+        self._check(src, "src")
+        self._check(dst, "dst")
+        if dst.numel() != src.numel() * self.size or src.dtype != dst.dtype:
+            raise ValueError("allgather: dst must hold size * src elements of the same dtype")
+        s = self._stream()
+        nb = src.numel() * src.element_size()
+        if algo == "rccl":
+            self.ensure_rccl()
+            self.dc.rccl_allgather(src.data_ptr(), dst.data_ptr(), nb, 1, s)
+        else:
+            self.dc.allgather(src.data_ptr(), dst.data_ptr(), nb, s, self.max_blocks, self._symm(src) and dst.data_ptr() % 16 == 0)
+        return dst
+
+    def alltoall(self, src, dst, algo: str = "direct"):
+        self._check(src, "src")
+        self._check(dst, "dst")
+        if src.numel() != dst.numel() or src.numel() % self.size:
+            raise ValueError("alltoall: src/dst must match and be divisible by the group size")
+        s = self._stream()
+        blk = src.numel() * src.element_size() // self.size
+        if algo == "rccl":
+            self.ensure_rccl()
+            self.dc.rccl_alltoall(src.data_ptr(), dst.data_ptr(), blk, 1, s)
+        elif algo == "pairwise":
+            self.ensure_rccl()
+            self.dc.p2p_pairwise_alltoall(src.data_ptr(), dst.data_ptr(), blk, s)
+        else:
+            self.dc.alltoall(src.data_ptr(), dst.data_ptr(), blk, s, self.max_blocks, self._symm(src))
+        return dst
+
+    def bcast(self, buf, root: int = 0, algo: str = "direct"):
+        self._check(buf, "buf")
+        s = self._stream()
+        if algo == "rccl":
+            self.ensure_rccl()
+            self.dc.rccl_bcast(buf.data_ptr(), buf.numel() * buf.element_size(), 1, root, s)
+        else:
+            self.dc.bcast(buf.data_ptr(), buf.numel() * buf.element_size(), root, s, self.max_blocks, self._symm(buf))
+        return buf
+
+    def local_reduce(self, inputs: Sequence, out, op="SUM"):
+        self.dc.local_reduce([t.data_ptr() for t in inputs], out.data_ptr(), out.numel(), dtype_code(out.dtype),
+                             op_code(op), self._stream())
+        return out
+
+    # ------------------------------------------------------------------ health
+    def check(self) -> None:
+        """Synchronise and raise if any device collective timed out."""
+        code = self.dc.error_code()
+        if code:
+            self.dc.clear_error()
+            raise RuntimeError(f"device collective timeout/fault code 0x{code:x} on rank {self.rank} "
+                               f"(phase {code >> 8}, peer {code & 0xff})")
+
+    def barrier(self) -> None:
+        self.torch.cuda.synchronize(self.device)
+        self.host.Barrier()

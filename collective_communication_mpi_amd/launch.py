@@ -1,0 +1,147 @@
+"""``mpirun``-compatible single-node launcher.
+
+    python -m collective_communication_mpi_amd.launch -n 8 python mpi-test.py --test_case myallreduce
+    scripts/mpirun -n 4 python3 -m pytest tests/test_transformer_forward.py --with-mpi
+
+The reference is launched with ``mpirun -n {4,8} python ...`` (reference
+README.md:52-136,189).  This launcher starts N ranks of the command on this
+host with ``CCMPI_RANK/CCMPI_SIZE/CCMPI_LOCAL_RANK/CCMPI_JOBID`` set (plus
+``LOCAL_RANK`` so GPU ranks pick a device), prefixes nothing, propagates the
+first failing exit code and tears down the remaining ranks (no orphaned
+spinners), and enforces an optional wall-clock ``--timeout``.
+
+Open MPI style flags that make no sense for a single-host shm runtime
+(``--oversubscribe``, ``--allow-run-as-root``, ``--bind-to X``, ``-H host``) are
+accepted and ignored; ``-x VAR[=VAL]`` exports a variable.
+"""
+from __future__ import annotations
+
+import os
+import signal
+import subprocess
+import sys
+import time
+import uuid
+from pathlib import Path
+from typing import List, Optional
+
+REPO = Path(__file__).resolve().parent.parent
+
+_FLAG_WITH_ARG_IGNORED = {"--bind-to", "--map-by", "-H", "--host", "--hostfile", "-hostfile", "--mca", "-ppn"}
+_FLAG_IGNORED = {"--oversubscribe", "--allow-run-as-root", "-l", "--tag-output", "-prepend-rank"}
+
+
+def parse(argv: List[str]):
+    n = 1
+    timeout: Optional[float] = None
+    exports = {}
+    i = 0
+    while i < len(argv):
+        a = argv[i]
+        if a in ("-n", "-np", "--np", "-c"):
+            n = int(argv[i + 1]); i += 2
+        elif a.startswith("-n") and a[2:].isdigit():
+            n = int(a[2:]); i += 1
+        elif a == "--timeout":
+            timeout = float(argv[i + 1]); i += 2
+        elif a == "-x":
+            kv = argv[i + 1]
+            if "=" in kv:
+                k, v = kv.split("=", 1)
+            else:
+                k, v = kv, os.environ.get(kv, "")
+            exports[k] = v
+            i += 2
+        elif a in _FLAG_WITH_ARG_IGNORED:
+            i += 2
+        elif a in _FLAG_IGNORED:
+            i += 1
+        elif a == "--mca":
+            i += 3
+        elif a == "--":
+            i += 1
+            break
+        else:
+            break
+    cmd = argv[i:]
+    if not cmd:
+        raise SystemExit("usage: launch -n N [--timeout S] [-x VAR=VAL] command [args...]")
+    return n, timeout, exports, cmd
+
+
+def launch(n: int, cmd: List[str], timeout: Optional[float] = None, env_extra=None,
+           job_id: Optional[str] = None) -> int:
+    job = job_id or uuid.uuid4().hex[:16]
+    procs = []
+    base = dict(os.environ)
+    base.update(env_extra or {})
+    pp = base.get("PYTHONPATH", "")
+    base["PYTHONPATH"] = str(REPO) + (os.pathsep + pp if pp else "")
+    for r in range(n):
+        env = dict(base)
+        env.update({
+            "CCMPI_RANK": str(r), "CCMPI_SIZE": str(n),
+            "CCMPI_LOCAL_RANK": str(r), "CCMPI_LOCAL_SIZE": str(n),
+            "CCMPI_JOBID": job, "LOCAL_RANK": str(r),
+        })
+        # Foreign launcher variables would make the runtime pick the wrong rank.
+        for k in ("PMI_RANK", "PMI_SIZE", "OMPI_COMM_WORLD_RANK", "OMPI_COMM_WORLD_SIZE", "RANK", "WORLD_SIZE"):
+            env.pop(k, None)
+        procs.append(subprocess.Popen(cmd, env=env, start_new_session=True))
+
+    def kill_all(sig=signal.SIGTERM):
+        for p in procs:
+            if p.poll() is None:
+                try:
+                    os.killpg(p.pid, sig)
+                except ProcessLookupError:
+                    pass
+
+    def on_signal(signum, _frame):
+        kill_all(signal.SIGTERM)
+
+    old = {s: signal.signal(s, on_signal) for s in (signal.SIGINT, signal.SIGTERM)}
+    t0 = time.monotonic()
+    rc = 0
+    try:
+        while True:
+            alive = False
+            for p in procs:
+                code = p.poll()
+                if code is None:
+                    alive = True
+                elif code != 0 and rc == 0:
+                    rc = code if code > 0 else 128 - code
+            if rc != 0:
+                break
+            if not alive:
+                break
+            if timeout is not None and time.monotonic() - t0 > timeout:
+                sys.stderr.write(f"[launch] timeout after {timeout:.0f}s; killing {n} ranks\n")
+                rc = 124
+                break
+            time.sleep(0.01)
+    finally:
+        if rc != 0:
+            kill_all(signal.SIGTERM)
+            deadline = time.monotonic() + 5
+            while time.monotonic() < deadline and any(p.poll() is None for p in procs):
+                time.sleep(0.05)
+            kill_all(signal.SIGKILL)
+        for p in procs:
+            try:
+                p.wait(timeout=10)
+            except subprocess.TimeoutExpired:
+                pass
+        for s, h in old.items():
+            signal.signal(s, h)
+    return rc
+
+
+def main(argv=None) -> int:
+    n, timeout, exports, cmd = parse(list(sys.argv[1:] if argv is None else argv))
+    return launch(n, cmd, timeout, exports)
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())
