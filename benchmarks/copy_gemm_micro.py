@@ -1,0 +1,48 @@
+"""Single-GPU micro-benchmarks: device copy (k_copy vs runtime blit) and the
+MFMA GEMM vs hipBLASLt (torch.matmul) on the harness shapes + 4096^3/8192^3."""
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+import torch  # noqa: E402
+
+from collective_communication_mpi_amd import _native  # noqa: E402
+from collective_communication_mpi_amd.ops import gemm_nt  # noqa: E402
+
+
+def tmin(fn, iters=20, warm=5):
+    for _ in range(warm):
+        fn()
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(iters):
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        fn()
+        e.record()
+        e.synchronize()
+        ts.append(s.elapsed_time(e))
+    ts.sort()
+    return ts[len(ts) // 2]
+
+
+D = _native.device()
+dc = D.DeviceComm(0, 1, 0)
+n = 1 << 30
+x = torch.empty(n, dtype=torch.uint8, device="cuda").random_()
+y = torch.empty_like(x)
+st = torch.cuda.current_stream().cuda_stream
+for eng in (False, True):
+    dc.set_copy_engine(eng)
+    ms = tmin(lambda: dc.allreduce(x.data_ptr(), y.data_ptr(), n // 4, 10, 0, 1, st, 256, False))
+    print(f"copy 1GiB {'blit' if eng else 'k_copy'}: {ms:.3f} ms = {n / ms / 1e6:.0f} GB/s algbw", flush=True)
+assert torch.equal(x, y)
+for (M, N, K) in [(32768, 768, 64), (32768, 384, 768), (32768, 16, 128), (4096, 4096, 4096), (8192, 8192, 8192)]:
+    a = torch.randn(M, K, device="cuda").bfloat16()
+    b = torch.randn(N, K, device="cuda").bfloat16()
+    ours = tmin(lambda: gemm_nt(a, b))
+    ref = tmin(lambda: a @ b.T)
+    fl = 2 * M * N * K
+    print(f"gemm {M}x{N}x{K}: ours {ours:.3f} ms ({fl / ours / 1e9:.0f} TF/s)  hipBLASLt {ref:.3f} ms "
+          f"({fl / ref / 1e9:.0f} TF/s)", flush=True)

@@ -1,0 +1,228 @@
+// Fused attention for short sequences (the MNIST harness: S = 16 patches,
+// head_dim 64), forward and backward, one workgroup per (batch, local head).
+//
+// Inputs come straight from the fused QKV GEMM output [B*S][3*Hl*D] (q | k | v
+// column blocks, head h at columns h*D..h*D+D-1 of each block) so no split /
+// transpose / contiguous copies are needed; the output [B*S][Hl*D] is exactly
+// the row-parallel fc_o's input layout.  The whole S x S score tile lives in
+// LDS, so the softmax is exact (no online rescaling) and the log-sum-exp is
+// stored for the backward recompute.  At S <= 64 the S x S x D products are a
+// few thousand FMAs per head: the kernel is load/latency bound, so it uses
+// fp32 VALU dot products from LDS rather than MFMA tiles (which need >= 16x16x32).
+#include <pybind11/pybind11.h>
+
+#include "common.hpp"
+#include "ops.hpp"
+
+namespace ccmpi {
+namespace dev {
+
+namespace {
+
+__device__ __forceinline__ float ld_bf16(const uint16_t* p) { return __uint_as_float((uint32_t)(*p) << 16); }
+__device__ __forceinline__ void st_bf16(uint16_t* p, float v) { *p = (uint16_t)f32_to_bf16_bits(v); }
+
+__device__ __forceinline__ float wave_max(float v) {
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+  return v;
+}
+__device__ __forceinline__ float wave_sum(float v) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+struct AttnArgs {
+  const uint16_t* qkv;  // [B*S][ld_qkv]
+  uint16_t* o;          // [B*S][ld_o]
+  float* lse;           // [B*Hl][S]
+  const uint16_t* dout; // [B*S][ld_o]   (bwd)
+  uint16_t* dqkv;       // [B*S][ld_qkv] (bwd)
+  int B, S, Hl, D, ld_qkv, ld_o;
+  float scale;
+};
+
+// stage an S x D head tile (bf16, row stride ld) into fp32 LDS [S][D+1]
+__device__ __forceinline__ void stage(float* dst, const uint16_t* src, int S, int D, int ld) {
+  for (int idx = threadIdx.x; idx < S * D; idx += blockDim.x) {
+    const int i = idx / D, d = idx % D;
+    dst[i * (D + 1) + d] = ld_bf16(src + (size_t)i * ld + d);
+  }
+}
+
+__global__ void __launch_bounds__(256) k_attn_fwd(AttnArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int S = a.S, D = a.D, Dp = D + 1, Sp = S + 1;
+  const int b = blockIdx.x / a.Hl, h = blockIdx.x % a.Hl;
+  float* q = sm;
+  float* k = q + S * Dp;
+  float* v = k + S * Dp;
+  float* P = v + S * Dp;
+  const uint16_t* base = a.qkv + (size_t)b * S * a.ld_qkv + h * D;
+  const int HD = a.Hl * D;
+  stage(q, base, S, D, a.ld_qkv);
+  stage(k, base + HD, S, D, a.ld_qkv);
+  stage(v, base + 2 * HD, S, D, a.ld_qkv);
+  __syncthreads();
+  for (int idx = threadIdx.x; idx < S * S; idx += blockDim.x) {
+    const int i = idx / S, j = idx % S;
+    float s = 0.f;
+    for (int d = 0; d < D; ++d) s += q[i * Dp + d] * k[j * Dp + d];
+    P[i * Sp + j] = s * a.scale;
+  }
+  __syncthreads();
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, nw = blockDim.x >> 6;
+  for (int i = wave; i < S; i += nw) {
+    const float x = lane < S ? P[i * Sp + lane] : -INFINITY;
+    const float m = wave_max(x);
+    const float e = lane < S ? __expf(x - m) : 0.f;
+    const float sum = wave_sum(e);
+    if (lane < S) P[i * Sp + lane] = e / sum;
+    if (lane == 0) a.lse[((size_t)b * a.Hl + h) * S + i] = m + __logf(sum);
+  }
+  __syncthreads();
+  uint16_t* obase = a.o + (size_t)b * S * a.ld_o + h * D;
+  for (int idx = threadIdx.x; idx < S * D; idx += blockDim.x) {
+    const int i = idx / D, d = idx % D;
+    float acc = 0.f;
+    for (int j = 0; j < S; ++j) acc += P[i * Sp + j] * v[j * Dp + d];
+    st_bf16(obase + (size_t)i * a.ld_o + d, acc);
+  }
+}
+
+__global__ void __launch_bounds__(256) k_attn_bwd(AttnArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int S = a.S, D = a.D, Dp = D + 1, Sp = S + 1;
+  const int b = blockIdx.x / a.Hl, h = blockIdx.x % a.Hl;
+  float* q = sm;
+  float* k = q + S * Dp;
+  float* v = k + S * Dp;
+  float* o = v + S * Dp;
+  float* dO = o + S * Dp;
+  float* P = dO + S * Dp;
+  float* dS = P + S * Sp;
+  float* delta = dS + S * Sp;
+  const int HD = a.Hl * D;
+  const uint16_t* base = a.qkv + (size_t)b * S * a.ld_qkv + h * D;
+  stage(q, base, S, D, a.ld_qkv);
+  stage(k, base + HD, S, D, a.ld_qkv);
+  stage(v, base + 2 * HD, S, D, a.ld_qkv);
+  stage(o, a.o + (size_t)b * S * a.ld_o + h * D, S, D, a.ld_o);
+  stage(dO, a.dout + (size_t)b * S * a.ld_o + h * D, S, D, a.ld_o);
+  __syncthreads();
+  const float* lse = a.lse + ((size_t)b * a.Hl + h) * S;
+  for (int idx = threadIdx.x; idx < S * S; idx += blockDim.x) {
+    const int i = idx / S, j = idx % S;
+    float s = 0.f, dp = 0.f;
+    for (int d = 0; d < D; ++d) {
+      s += q[i * Dp + d] * k[j * Dp + d];
+      dp += dO[i * Dp + d] * v[j * Dp + d];
+    }
+    P[i * Sp + j] = __expf(s * a.scale - lse[i]);
+    dS[i * Sp + j] = dp;
+  }
+  for (int i = threadIdx.x; i < S; i += blockDim.x) {
+    float t = 0.f;
+    for (int d = 0; d < D; ++d) t += dO[i * Dp + d] * o[i * Dp + d];
+    delta[i] = t;
+  }
+  __syncthreads();
+  for (int idx = threadIdx.x; idx < S * S; idx += blockDim.x) {
+    const int i = idx / S, j = idx % S;
+    dS[i * Sp + j] = P[i * Sp + j] * (dS[i * Sp + j] - delta[i]);
+  }
+  __syncthreads();
+  uint16_t* gq = a.dqkv + (size_t)b * S * a.ld_qkv + h * D;
+  uint16_t* gk = gq + HD;
+  uint16_t* gv = gq + 2 * HD;
+  for (int idx = threadIdx.x; idx < S * D; idx += blockDim.x) {
+    const int i = idx / D, d = idx % D;  // i: query row for dQ, key row for dK / dV
+    float dq = 0.f, dk = 0.f, dv = 0.f;
+    for (int j = 0; j < S; ++j) {
+      dq += dS[i * Sp + j] * k[j * Dp + d];
+      dk += dS[j * Sp + i] * q[j * Dp + d];
+      dv += P[j * Sp + i] * dO[j * Dp + d];
+    }
+    st_bf16(gq + (size_t)i * a.ld_qkv + d, dq * a.scale);
+    st_bf16(gk + (size_t)i * a.ld_qkv + d, dk * a.scale);
+    st_bf16(gv + (size_t)i * a.ld_qkv + d, dv);
+  }
+}
+
+size_t fwd_lds(int S, int D) { return sizeof(float) * (3 * S * (D + 1) + S * (S + 1)); }
+size_t bwd_lds(int S, int D) { return sizeof(float) * (5 * S * (D + 1) + 2 * S * (S + 1) + S); }
+
+void check_dims(int S, int D, bool bwd) {
+  if (S < 1 || S > 64 || D < 1 || D > 256) throw std::invalid_argument("attn_small: need 1 <= S <= 64, D <= 256");
+  if ((bwd ? bwd_lds(S, D) : fwd_lds(S, D)) > 160 * 1024) throw std::invalid_argument("attn_small: tile exceeds LDS");
+}
+
+void attn_fwd(uint64_t qkv, uint64_t o, uint64_t lse, int B, int S, int Hl, int D, int ld_qkv, int ld_o, float scale,
+              uint64_t stream) {
+  check_dims(S, D, false);
+  AttnArgs a{(const uint16_t*)qkv, (uint16_t*)o, (float*)lse, nullptr, nullptr, B, S, Hl, D, ld_qkv, ld_o, scale};
+  hipLaunchKernelGGL(k_attn_fwd, dim3(B * Hl), dim3(256), fwd_lds(S, D), (hipStream_t)stream, a);
+  CCMPI_HIP_CHECK(hipGetLastError());
+}
+
+void attn_bwd(uint64_t qkv, uint64_t o, uint64_t lse, uint64_t dout, uint64_t dqkv, int B, int S, int Hl, int D,
+              int ld_qkv, int ld_o, float scale, uint64_t stream) {
+  check_dims(S, D, true);
+  AttnArgs a{(const uint16_t*)qkv, (uint16_t*)o, (float*)lse, (const uint16_t*)dout, (uint16_t*)dqkv,
+             B, S, Hl, D, ld_qkv, ld_o, scale};
+  hipLaunchKernelGGL(k_attn_bwd, dim3(B * Hl), dim3(256), bwd_lds(S, D), (hipStream_t)stream, a);
+  CCMPI_HIP_CHECK(hipGetLastError());
+}
+
+// ---------------------------------------------------------------------------
+// Fused AdamW on a flat fp32 parameter buffer + bf16 compute copy (one pass).
+// g is the (DP-summed) gradient; grad_scale folds the 1/dp average in.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_adamw(float* __restrict__ p, const float* __restrict__ g,
+                                               float* __restrict__ m, float* __restrict__ v,
+                                               uint16_t* __restrict__ p16, uint64_t n, float lr, float b1, float b2,
+                                               float eps, float wd, float bc1, float bc2, float grad_scale) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const float gi = g[i] * grad_scale;
+    const float mi = b1 * m[i] + (1.f - b1) * gi;
+    const float vi = b2 * v[i] + (1.f - b2) * gi * gi;
+    m[i] = mi;
+    v[i] = vi;
+    float pi = p[i] * (1.f - lr * wd);
+    pi -= lr * (mi / bc1) / (sqrtf(vi / bc2) + eps);
+    p[i] = pi;
+    if (p16) p16[i] = (uint16_t)f32_to_bf16_bits(pi);
+  }
+}
+
+__global__ void __launch_bounds__(256) k_cast_bf16(const float* __restrict__ x, uint16_t* __restrict__ y, uint64_t n) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    y[i] = (uint16_t)f32_to_bf16_bits(x[i]);
+}
+
+void adamw(uint64_t p, uint64_t g, uint64_t m, uint64_t v, uint64_t p16, uint64_t n, float lr, float b1, float b2,
+           float eps, float wd, int step, float grad_scale, uint64_t stream) {
+  const float bc1 = 1.f - powf(b1, (float)step), bc2 = 1.f - powf(b2, (float)step);
+  const int grid = (int)std::min<uint64_t>((n + 255) / 256, 2048);
+  hipLaunchKernelGGL(k_adamw, dim3(grid), dim3(256), 0, (hipStream_t)stream, (float*)p, (const float*)g, (float*)m,
+                     (float*)v, (uint16_t*)p16, n, lr, b1, b2, eps, wd, bc1, bc2, grad_scale);
+  CCMPI_HIP_CHECK(hipGetLastError());
+}
+
+void cast_bf16(uint64_t x, uint64_t y, uint64_t n, uint64_t stream) {
+  const int grid = (int)std::min<uint64_t>((n + 255) / 256, 2048);
+  hipLaunchKernelGGL(k_cast_bf16, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const float*)x, (uint16_t*)y, n);
+  CCMPI_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace
+
+void register_attn_ops(pybind11::module_& m) {
+  namespace py = pybind11;
+  m.def("attn_small_fwd", &attn_fwd, py::call_guard<py::gil_scoped_release>());
+  m.def("attn_small_bwd", &attn_bwd, py::call_guard<py::gil_scoped_release>());
+  m.def("adamw_step", &adamw, py::call_guard<py::gil_scoped_release>());
+  m.def("cast_bf16", &cast_bf16, py::call_guard<py::gil_scoped_release>());
+}
+
+}  // namespace dev
+}  // namespace ccmpi

@@ -61,7 +61,8 @@ PYBIND11_MODULE(_device, m) {
       .def("p2p_pairwise_alltoall", &DeviceComm::p2p_pairwise_alltoall, py::call_guard<py::gil_scoped_release>())
       .def("error_code", &DeviceComm::error_code, py::call_guard<py::gil_scoped_release>())
       .def("clear_error", &DeviceComm::clear_error)
-      .def("set_timeout_seconds", &DeviceComm::set_timeout_seconds);
+      .def("set_timeout_seconds", &DeviceComm::set_timeout_seconds)
+      .def("set_copy_engine", &DeviceComm::set_copy_engine);
 
   register_ops(m);
 }

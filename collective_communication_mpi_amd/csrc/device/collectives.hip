@@ -426,9 +426,43 @@ __global__ void __launch_bounds__(kThreads) k_local_reduce(LocalReduceArgs a) {
   }
 }
 
+// Streaming device copy (single-rank "all-reduce" and staging): 16-B
+// non-temporal loads/stores, 4 vectors in flight per lane, grid-stride.
+__global__ void __launch_bounds__(kThreads) k_copy(const u32x4* __restrict__ src, u32x4* __restrict__ dst, uint64_t nv) {
+  const uint64_t stride = (uint64_t)gridDim.x * kThreads;
+  uint64_t v = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
+  for (; v + 3 * stride < nv; v += 4 * stride) {
+    u32x4 a = __builtin_nontemporal_load(src + v);
+    u32x4 b = __builtin_nontemporal_load(src + v + stride);
+    u32x4 c = __builtin_nontemporal_load(src + v + 2 * stride);
+    u32x4 d = __builtin_nontemporal_load(src + v + 3 * stride);
+    __builtin_nontemporal_store(a, dst + v);
+    __builtin_nontemporal_store(b, dst + v + stride);
+    __builtin_nontemporal_store(c, dst + v + 2 * stride);
+    __builtin_nontemporal_store(d, dst + v + 3 * stride);
+  }
+  for (; v < nv; v += stride) __builtin_nontemporal_store(__builtin_nontemporal_load(src + v), dst + v);
+}
+
 // ---------------------------------------------------------------------------
 // host-side launchers
 // ---------------------------------------------------------------------------
+void launch_copy(const void* src, void* dst, uint64_t nbytes, hipStream_t s) {
+  if (nbytes == 0 || src == dst) return;
+  const uint64_t a = (uint64_t)src | (uint64_t)dst;
+  if (a % 16 || nbytes < (1u << 20)) {
+    CCMPI_HIP_CHECK(hipMemcpyAsync(dst, src, nbytes, hipMemcpyDeviceToDevice, s));
+    return;
+  }
+  const uint64_t nv = nbytes / 16;
+  const int grid = (int)std::min<uint64_t>((nv + kThreads - 1) / kThreads, 4096);
+  hipLaunchKernelGGL(k_copy, dim3(grid), dim3(kThreads), 0, s, (const u32x4*)src, (u32x4*)dst, nv);
+  CCMPI_HIP_CHECK(hipGetLastError());
+  if (nbytes % 16)
+    CCMPI_HIP_CHECK(hipMemcpyAsync((char*)dst + nv * 16, (const char*)src + nv * 16, nbytes % 16,
+                                   hipMemcpyDeviceToDevice, s));
+}
+
 int grid_for(uint64_t bytes_per_cta_work, int max_blocks) {
   // ~64 KiB of output per CTA minimum; at most max_blocks CTAs
   uint64_t g = (bytes_per_cta_work + (64u << 10) - 1) / (64u << 10);

@@ -93,6 +93,7 @@ DeviceComm::DeviceComm(int rank, int size, int device, uint64_t /*scratch_bytes*
   peer_sig_[rank] = sig_;
   host_pt_.sig[rank] = sig_;
   if (const char* t = std::getenv("CCMPI_DEVICE_TIMEOUT_S")) set_timeout_seconds(std::atof(t));
+  if (const char* c = std::getenv("CCMPI_COPY_ENGINE")) copy_engine_ = std::atoi(c) != 0;
   CCMPI_HIP_CHECK(hipDeviceSynchronize());
   sync_table_();
 }
@@ -210,7 +211,10 @@ void DeviceComm::allreduce(uint64_t in, uint64_t out, uint64_t count, int dtype,
   CCMPI_HIP_CHECK(hipSetDevice(device_));
   hipStream_t st = S(stream);
   if (size_ == 1) {
-    if (in != out) CCMPI_HIP_CHECK(hipMemcpyAsync((void*)out, (void*)in, nbytes, hipMemcpyDeviceToDevice, st));
+    if (in != out) {
+      if (copy_engine_) CCMPI_HIP_CHECK(hipMemcpyAsync((void*)out, (void*)in, nbytes, hipMemcpyDeviceToDevice, st));
+      else launch_copy((const void*)in, (void*)out, nbytes, st);
+    }
     return;
   }
   const bool needs_res = algo != ALGO_ONESHOT;

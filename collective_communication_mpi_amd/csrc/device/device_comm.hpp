@@ -89,6 +89,7 @@ class DeviceComm {
   void clear_error();
   uint64_t timeout_ticks() const { return timeout_ticks_; }
   void set_timeout_seconds(double s) { timeout_ticks_ = (uint64_t)(s * 1e8); }
+  void set_copy_engine(bool on) { copy_engine_ = on; }
 
  private:
   void sync_table_();
@@ -106,6 +107,7 @@ class DeviceComm {
   uint64_t* epochs_ = nullptr;
   uint64_t timeout_ticks_ = 2000000000ull;  // 20 s
   ncclComm_t nccl_ = nullptr;
+  bool copy_engine_ = true;               // single-rank copies: runtime blit (measured faster than k_copy)
   std::vector<std::string> opened_;      // handles we opened (for release)
 };
 

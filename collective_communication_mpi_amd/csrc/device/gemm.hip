@@ -1,0 +1,212 @@
+// bf16 GEMM on CDNA4 matrix cores with fused epilogue, for the TP layers of
+// the DP x TP harness (fc_q/k/v column-parallel, fc_o row-parallel, patch
+// embedding).  The reference leaves this compute "taken care of" elsewhere
+// (README.md:173-175); here it is the hot op of the training step.
+//
+//   C[M,N] = act(alpha * A[M,K] . B[N,K]^T + bias[N]) (+ C if accumulate)
+//
+// A and B are both K-contiguous ("NT"; PyTorch Linear weights are [out, in]),
+// bf16, rows 16-B aligned (K % 8 == 0, lda/ldb % 8 == 0).  Backward passes
+// feed transposed copies made by k_transpose (below).
+//
+// Tiling: 128x128 output tile per 256-thread workgroup (4 waves as 2x2, each
+// wave 64x64 = 4x4 v_mfma_f32_16x16x32_bf16 tiles), BK = 64, two LDS buffers
+// (64 KiB).  Global -> register loads of tile k+1 are issued before the MFMAs
+// of tile k and written to the other LDS buffer after them (one barrier per
+// K-step).  LDS rows are 128 B; the 16-B chunk index is XOR-swizzled with
+// (row & 7) so a 16-lane ds_read_b128 group touches 8 different slots.
+// Workgroup ids are remapped so that consecutive N-tiles of one M-row of
+// tiles land on the same XCD (shared A panel in that XCD's L2).
+#include <pybind11/pybind11.h>
+
+#include "common.hpp"
+#include "ops.hpp"
+
+namespace ccmpi {
+namespace dev {
+
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+constexpr int BM = 128, BN = 128, BK = 64, NT = 256;
+constexpr int kRowBytes = BK * 2;  // 128 B per LDS row
+
+struct GemmArgs {
+  const uint16_t* A;
+  const uint16_t* B;
+  void* C;
+  const void* bias;
+  int M, N, K;
+  int lda, ldb, ldc;
+  float alpha;
+  int accumulate;  // C += result
+  int bias_kind;   // 0 none, 1 fp32, 2 bf16
+  int act;         // 0 none, 1 relu, 2 gelu(tanh)
+  int out_bf16;    // 0 fp32 out, 1 bf16 out
+};
+
+__device__ __forceinline__ float bf2f(uint16_t h) { return __uint_as_float((uint32_t)h << 16); }
+
+__device__ __forceinline__ float gelu_tanh(float x) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  return 0.5f * x * (1.f + tanhf(k0 * (x + k1 * x * x * x)));
+}
+
+__global__ void __launch_bounds__(NT) k_gemm_nt(GemmArgs g) {
+  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * (BM + BN) * kRowBytes];
+  const int tiles_n = (g.N + BN - 1) / BN, tiles_m = (g.M + BM - 1) / BM;
+  const int nwg = tiles_n * tiles_m;
+  // bijective XCD-aware remap: blocks b, b+8, b+16, ... (same XCD) get consecutive tile ids
+  int wg = blockIdx.x;
+  {
+    const int q = nwg / 8, r = nwg % 8, x = wg % 8;
+    wg = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + wg / 8;
+  }
+  const int bm = (wg / tiles_n) * BM, bn = (wg % tiles_n) * BN;
+  const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
+  const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
+
+  auto As = [&](int buf) { return smem + buf * ((BM + BN) * kRowBytes); };
+  auto Bs = [&](int buf) { return smem + buf * ((BM + BN) * kRowBytes) + BM * kRowBytes; };
+
+  floatx4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  uint4 ra[4], rb[4];
+  const int srow = t >> 3, schunk = t & 7;
+  auto gload = [&](int k0) {
+    const int gk = k0 + schunk * 8;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = srow + 32 * i;
+      const int gm = bm + r, gn = bn + r;
+      ra[i] = (gm < g.M && gk < g.K) ? *reinterpret_cast<const uint4*>(g.A + (size_t)gm * g.lda + gk) : uint4{0, 0, 0, 0};
+      rb[i] = (gn < g.N && gk < g.K) ? *reinterpret_cast<const uint4*>(g.B + (size_t)gn * g.ldb + gk) : uint4{0, 0, 0, 0};
+    }
+  };
+  auto swrite = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = srow + 32 * i;
+      const int off = r * kRowBytes + ((schunk ^ (r & 7)) << 4);
+      *reinterpret_cast<uint4*>(As(buf) + off) = ra[i];
+      *reinterpret_cast<uint4*>(Bs(buf) + off) = rb[i];
+    }
+  };
+
+  gload(0);
+  swrite(0);
+  __syncthreads();
+  const int nk = (g.K + BK - 1) / BK;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) gload((kt + 1) * BK);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 af[4], bf[4];
+      const int chunk = ks * 4 + (lane >> 4);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int ra_ = wm + i * 16 + (lane & 15);
+        af[i] = *reinterpret_cast<const bf16x8*>(As(cur) + ra_ * kRowBytes + ((chunk ^ (ra_ & 7)) << 4));
+        const int rb_ = wn + i * 16 + (lane & 15);
+        bf[i] = *reinterpret_cast<const bf16x8*>(Bs(cur) + rb_ * kRowBytes + ((chunk ^ (rb_ & 7)) << 4));
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf[j], acc[i][j], 0, 0, 0);
+    }
+    if (kt + 1 < nk) swrite(cur ^ 1);
+    __syncthreads();
+  }
+
+  // epilogue: lane holds D[4*(lane>>4) + r][lane & 15] of each 16x16 tile
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int col = bn + wn + j * 16 + (lane & 15);
+    if (col >= g.N) continue;
+    float b = 0.f;
+    if (g.bias_kind == 1) b = reinterpret_cast<const float*>(g.bias)[col];
+    else if (g.bias_kind == 2) b = bf2f(reinterpret_cast<const uint16_t*>(g.bias)[col]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = bm + wm + i * 16 + (lane >> 4) * 4 + r;
+        if (row >= g.M) continue;
+        float v = g.alpha * acc[i][j][r] + b;
+        if (g.act == 1) v = fmaxf(v, 0.f);
+        else if (g.act == 2) v = gelu_tanh(v);
+        const size_t o = (size_t)row * g.ldc + col;
+        if (g.out_bf16) {
+          uint16_t* C = reinterpret_cast<uint16_t*>(g.C);
+          if (g.accumulate) v += bf2f(C[o]);
+          C[o] = (uint16_t)f32_to_bf16_bits(v);
+        } else {
+          float* C = reinterpret_cast<float*>(g.C);
+          if (g.accumulate) v += C[o];
+          C[o] = v;
+        }
+      }
+    }
+  }
+}
+
+// 2-D transpose of 16-bit elements through a padded 64x65 LDS tile.
+__global__ void __launch_bounds__(256) k_transpose16(const uint16_t* __restrict__ src, uint16_t* __restrict__ dst,
+                                                     int R, int C, int lds, int ldd) {
+  __shared__ uint16_t tile[64][65];
+  const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  for (int y = ty; y < 64; y += 4) {
+    const int r = r0 + y, c = c0 + tx;
+    if (r < R && c < C) tile[y][tx] = src[(size_t)r * lds + c];
+  }
+  __syncthreads();
+  for (int y = ty; y < 64; y += 4) {
+    const int c = c0 + y, r = r0 + tx;  // dst row = c, col = r
+    if (c < C && r < R) dst[(size_t)c * ldd + r] = tile[tx][y];
+  }
+}
+
+void gemm_nt(uint64_t A, uint64_t B, uint64_t C, uint64_t bias, int M, int N, int K, int lda, int ldb, int ldc,
+             float alpha, bool accumulate, int bias_kind, int act, bool out_bf16, uint64_t stream) {
+  if (M <= 0 || N <= 0) return;
+  if (K % 8 || lda % 8 || ldb % 8 || (A % 16) || (B % 16))
+    throw std::invalid_argument("ccmpi gemm: K, lda, ldb must be multiples of 8 and A/B 16-B aligned");
+  GemmArgs g{reinterpret_cast<const uint16_t*>(A), reinterpret_cast<const uint16_t*>(B), reinterpret_cast<void*>(C),
+             reinterpret_cast<const void*>(bias), M, N, K, lda, ldb, ldc, alpha, accumulate ? 1 : 0, bias_kind,
+             act, out_bf16 ? 1 : 0};
+  const int nwg = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  hipLaunchKernelGGL(k_gemm_nt, dim3(nwg), dim3(NT), 0, reinterpret_cast<hipStream_t>(stream), g);
+  CCMPI_HIP_CHECK(hipGetLastError());
+}
+
+void transpose16(uint64_t src, uint64_t dst, int R, int C, int lds, int ldd, uint64_t stream) {
+  if (R <= 0 || C <= 0) return;
+  dim3 grid((C + 63) / 64, (R + 63) / 64);
+  hipLaunchKernelGGL(k_transpose16, grid, dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+                     reinterpret_cast<const uint16_t*>(src), reinterpret_cast<uint16_t*>(dst), R, C, lds, ldd);
+  CCMPI_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace
+
+void register_gemm_ops(pybind11::module_& m) {
+  m.def("gemm_nt", &gemm_nt, "C = act(alpha*A.B^T + bias) (+C); A[M,K], B[N,K] bf16",
+        pybind11::arg("A"), pybind11::arg("B"), pybind11::arg("C"), pybind11::arg("bias"), pybind11::arg("M"),
+        pybind11::arg("N"), pybind11::arg("K"), pybind11::arg("lda"), pybind11::arg("ldb"), pybind11::arg("ldc"),
+        pybind11::arg("alpha"), pybind11::arg("accumulate"), pybind11::arg("bias_kind"), pybind11::arg("act"),
+        pybind11::arg("out_bf16"), pybind11::arg("stream"), pybind11::call_guard<pybind11::gil_scoped_release>());
+  m.def("transpose16", &transpose16, "dst[C,R] = src[R,C]^T for 16-bit elements",
+        pybind11::call_guard<pybind11::gil_scoped_release>());
+}
+
+}  // namespace dev
+}  // namespace ccmpi

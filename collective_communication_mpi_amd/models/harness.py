@@ -1,0 +1,157 @@
+"""Training / benchmarking harness for the DP x TP MNIST transformer layer.
+
+    scripts/mpirun -n 2 python -m collective_communication_mpi_amd.models.harness --tp 2 --steps 20
+    torchrun --nproc-per-node 8 -m collective_communication_mpi_amd.models.harness --tp 2 --steps 100
+
+``bench_forward`` is what ``bench.py`` reports as the DP x TP forward step time:
+the forward pass (patchify, embedding GEMM, QKV GEMM, attention, fc_o GEMM,
+TP all-reduce, pooling) captured once into a HIP graph and replayed, timed over
+K replays between barriers (max over ranks).  The full training step
+(forward + backward + bucketed DP all-reduce + fused AdamW) is timed eagerly.
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+from ..data.preprocess import synthetic_mnist
+from .mnist_tp import LayerConfig, MnistTPLayer, local_batch, patchify
+
+
+def _hc(comm):
+    return comm.comm if hasattr(comm, "comm") else comm
+
+
+def _sync_barrier(comm):
+    torch.cuda.synchronize()
+    _hc(comm).Barrier()
+
+
+def build(comm, tp: int, batch: int, **kw):
+    world = comm.Get_size()
+    cfg = LayerConfig(batch=batch, tp=tp, dp=world // tp, **kw)
+    layer = MnistTPLayer(comm, cfg)
+    x_all, y_all = synthetic_mnist(cfg.batch * cfg.dp * 2, seed=cfg.seed)
+    return cfg, layer, x_all, y_all
+
+
+def train_step(layer: MnistTPLayer, cfg: LayerConfig, xb, yb):
+    xp = patchify(xb, cfg)
+    logits = layer.forward(xp, xb.shape[0])
+    loss, dlogits = layer.loss_and_grad(logits, yb, cfg.batch * cfg.dp)
+    layer.zero_grad()
+    layer.backward(dlogits)
+    layer.step()
+    return loss
+
+
+def bench_forward(comm, tp: int = 2, batch: int = 2048, steps: int = 20, warmup: int = 5, graph: bool = True):
+    from .. import mpi as MPI
+
+    hc = _hc(comm)
+    rank = comm.Get_rank()
+    cfg, layer, x_all, y_all = build(comm, tp, batch)
+    xb, yb = local_batch(cfg, x_all, y_all, 0, rank, layer.device)
+    xp_static = patchify(xb, cfg)
+
+    def fwd():
+        xp_static.copy_(patchify(xb, cfg))
+        return layer.forward(xp_static, cfg.batch)
+
+    for _ in range(3):
+        fwd()
+    torch.cuda.synchronize()
+    used_graph = False
+    g = None
+    if graph and os.environ.get("CCMPI_NO_GRAPH") != "1":
+        try:
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                fwd()
+            torch.cuda.current_stream().wait_stream(s)
+            torch.cuda.synchronize()
+            _sync_barrier(comm)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                fwd()
+            used_graph = True
+        except Exception as e:  # noqa: BLE001 - fall back to eager, reported in the result
+            if rank == 0:
+                print(f"[harness] graph capture failed, timing eager: {e}", file=sys.stderr)
+            g = None
+    run = g.replay if g is not None else fwd
+    for _ in range(warmup):
+        run()
+    _sync_barrier(comm)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        run()
+    torch.cuda.synchronize()
+    hc.Barrier()
+    fwd_s = hc.allreduce(time.perf_counter() - t0, op=MPI.MAX) / steps
+    # training step (eager)
+    for _ in range(2):
+        train_step(layer, cfg, xb, yb)
+    _sync_barrier(comm)
+    t0 = time.perf_counter()
+    n_train = max(3, steps // 2)
+    loss = None
+    for i in range(n_train):
+        loss = train_step(layer, cfg, xb, yb)
+    torch.cuda.synchronize()
+    hc.Barrier()
+    train_s = hc.allreduce(time.perf_counter() - t0, op=MPI.MAX) / n_train
+    loss_v = hc.allreduce(float(loss.item()), op=MPI.SUM) / cfg.tp  # sum over DP of per-replica shares
+    return {"tp": cfg.tp, "dp": cfg.dp, "fwd_ms": fwd_s * 1e3, "train_ms": train_s * 1e3,
+            "global_batch": cfg.batch * cfg.dp, "seq_len": cfg.seq, "tokens_per_step": cfg.batch * cfg.dp * cfg.seq,
+            "hip_graph": used_graph, "fc_o_mode": cfg.fc_o_mode, "loss": round(loss_v, 5)}
+
+
+def smoke_step(comm) -> None:
+    """One tiny forward + backward + optimizer step (driver smoke)."""
+    tp = 2 if comm.Get_size() % 2 == 0 and comm.Get_size() > 1 else 1
+    cfg, layer, x_all, y_all = build(comm, tp, batch=64)
+    xb, yb = local_batch(cfg, x_all, y_all, 0, comm.Get_rank(), layer.device)
+    loss = train_step(layer, cfg, xb, yb)
+    torch.cuda.synchronize()
+    assert torch.isfinite(loss).item(), "non-finite loss"
+    assert torch.isfinite(layer.flat.g).all().item(), "non-finite gradients"
+
+
+def main(argv=None) -> int:
+    from .. import MPI, Communicator
+
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--tp", type=int, default=1)
+    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--lr", type=float, default=2e-3)
+    ap.add_argument("--fc-o-mode", default="row")
+    ap.add_argument("--log", default="")
+    args = ap.parse_args(argv)
+    comm = Communicator(MPI.COMM_WORLD)
+    local = int(os.environ.get("LOCAL_RANK", os.environ.get("CCMPI_LOCAL_RANK", "0")))
+    torch.cuda.set_device(local % torch.cuda.device_count())
+    cfg, layer, x_all, y_all = build(comm, args.tp, args.batch, lr=args.lr, fc_o_mode=args.fc_o_mode)
+    hc = _hc(comm)
+    losses = []
+    for step in range(args.steps):
+        xb, yb = local_batch(cfg, x_all, y_all, step, comm.Get_rank(), layer.device)
+        loss = train_step(layer, cfg, xb, yb)
+        lv = hc.allreduce(float(loss.item()), op=MPI.SUM) / cfg.tp
+        losses.append(lv)
+        if comm.Get_rank() == 0:
+            print(f"step {step} loss {lv:.5f}", flush=True)
+    if args.log and comm.Get_rank() == 0:
+        np.save(args.log, np.array(losses))
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())

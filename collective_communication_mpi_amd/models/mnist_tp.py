@@ -1,0 +1,314 @@
+"""DP x TP transformer layer on MNIST-shaped data: the training harness the
+reference assumes but does not ship (README.md:173-181: "transformer compute,
+training loop and MNIST data were taken care of"; the layer dims come from its
+tests: fc_q/k/v 768 -> 256 column-parallel, fc_o 256 -> 10, test_get_info.py:68-69,152-153).
+
+Model (per image): 28x28 -> 16 patches of 7x7 (49 px, zero-padded to 64) ->
+patch embedding 64 -> 768 (+ bias + learned position) -> fused QKV projection
+768 -> 3x256 (4 heads x 64) -> softmax attention over the 16 patches ->
+fc_o 256 -> 10 -> mean over patches -> cross-entropy.
+
+Parallelism: mp-major 2-D grid from ``get_info`` (rank = dp_idx * tp + tp_idx).
+* fc_q/k/v are column-parallel: TP rank t owns heads [t*H/tp, (t+1)*H/tp), i.e.
+  rows of the fused QKV weight; attention is local to a rank's heads.
+* fc_o is row-parallel (``fc_o_mode="row"``, default): each rank multiplies its
+  local attention output by its input-dim shard of W_o, and ONE TP all-reduce
+  (hand-written device kernel, symmetric buffers, graph-capturable) sums the
+  partial outputs.  ``fc_o_mode="naive"`` runs the reference's collects instead
+  (model/func_impl.py:76-187): all-gather the input, out-sharded fc_o, all-gather
+  the output; backward slices the output gradient and reduce-scatters grad_x.
+* the embedding input gradient is TP-partial and is all-reduced (Megatron's
+  "f" operator) so replicated parameters get identical gradients on every TP rank.
+* DP: gradients in a flat fp32 buffer on the DP group's symmetric heap,
+  three buckets in backward order, all-reduced on a side stream while the
+  remaining backward GEMMs run (parallel/dp.py).
+
+All GEMMs are the hand-written MFMA kernel (ops.gemm_nt); attention is the
+fused short-sequence kernel; the optimizer is one fused AdamW pass.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+from typing import Optional
+
+import numpy as np
+import torch
+
+from .. import _native
+from ..ops import gemm_nt, transpose
+from ..parallel.dp import FlatParams, GradBuckets
+from ..parallel.layout import device_group_for, get_info, naive_collect_backward_output, naive_collect_backward_x, \
+    naive_collect_forward_input, naive_collect_forward_output
+
+
+@dataclass
+class LayerConfig:
+    d_model: int = 768
+    d_attn: int = 256
+    n_heads: int = 4
+    n_classes: int = 10
+    img: int = 28
+    patch: int = 7
+    patch_pad: int = 64
+    out_pad: int = 16        # fc_o output rows padded to 16 (MFMA-friendly K for dX = dZ . W_o)
+    batch: int = 2048        # images per DP replica
+    tp: int = 1
+    dp: int = 1
+    fc_o_mode: str = "row"   # "row" (Megatron, 1 all-reduce) | "naive" (reference collects)
+    lr: float = 1e-3
+    weight_decay: float = 0.0
+    seed: int = 1234
+    dp_algo: str = "auto"
+    overlap: bool = True
+
+    @property
+    def seq(self) -> int:
+        return (self.img // self.patch) ** 2
+
+    @property
+    def head_dim(self) -> int:
+        return self.d_attn // self.n_heads
+
+
+def patchify(x: torch.Tensor, cfg: LayerConfig) -> torch.Tensor:
+    """(B, 784) float -> (B*16, 64) bf16 patches (7x7 pixels, zero-padded)."""
+    B = x.shape[0]
+    g = cfg.img // cfg.patch
+    p = x.view(B, g, cfg.patch, g, cfg.patch).permute(0, 1, 3, 2, 4).reshape(B * g * g, cfg.patch * cfg.patch)
+    out = torch.zeros(B * g * g, cfg.patch_pad, dtype=torch.bfloat16, device=x.device)
+    out[:, : cfg.patch * cfg.patch] = p
+    return out
+
+
+def full_init(cfg: LayerConfig):
+    """Unsharded fp32 weights from a seeded CPU generator (identical on all ranks)."""
+    g = torch.Generator().manual_seed(cfg.seed)
+    d, a, pp = cfg.d_model, cfg.d_attn, cfg.patch * cfg.patch
+    w = {
+        "emb_w": torch.randn(d, cfg.patch_pad, generator=g) / math.sqrt(pp),
+        "emb_b": torch.zeros(d),
+        "pos": torch.randn(cfg.seq, d, generator=g) * 0.02,
+        "q_w": torch.randn(a, d, generator=g) / math.sqrt(d),
+        "k_w": torch.randn(a, d, generator=g) / math.sqrt(d),
+        "v_w": torch.randn(a, d, generator=g) / math.sqrt(d),
+        "q_b": torch.zeros(a), "k_b": torch.zeros(a), "v_b": torch.zeros(a),
+        "o_w": torch.randn(cfg.n_classes, a, generator=g) / math.sqrt(a),
+        "o_b": torch.zeros(cfg.n_classes),
+    }
+    w["emb_w"][:, pp:] = 0.0  # padding columns of each patch never carry signal
+    return w
+
+
+class MnistTPLayer:
+    def __init__(self, comm, cfg: LayerConfig, device=None):
+        self.cfg = cfg
+        self.comm = comm
+        world, rank = comm.Get_size(), comm.Get_rank()
+        if cfg.tp * cfg.dp != world:
+            raise ValueError(f"tp*dp = {cfg.tp * cfg.dp} != world size {world}")
+        if cfg.n_heads % cfg.tp:
+            raise ValueError("n_heads must be divisible by tp")
+        self.tp_idx, self.dp_idx, self.mp_comm, self.dp_comm, _, _ = get_info(
+            comm, rank, cfg.tp, cfg.dp, "fc_q", cfg.d_model, cfg.d_attn)
+        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self.tp_dev = device_group_for(self.mp_comm) if cfg.tp > 1 else None
+        self.dp_dev = device_group_for(self.dp_comm) if cfg.dp > 1 else None
+        self.hl = cfg.n_heads // cfg.tp
+        self.hd = self.hl * cfg.head_dim  # local attention width
+        d = cfg.d_model
+        specs = [  # backward order -> bucket layout
+            ("o_w", (cfg.out_pad, self.hd)), ("o_b", (cfg.out_pad,)),
+            ("qkv_w", (3 * self.hd, d)), ("qkv_b", (3 * self.hd,)),
+            ("emb_w", (d, cfg.patch_pad)), ("emb_b", (d,)), ("pos", (cfg.seq, d)),
+        ]
+        grad_alloc = (lambda n: self.dp_dev.zeros(n, torch.float32)) if self.dp_dev is not None else None
+        self.flat = FlatParams(specs, self.device, grad_alloc)
+        self.buckets = GradBuckets(self.flat, self.dp_dev, [["o_w", "o_b"], ["qkv_w", "qkv_b"],
+                                                            ["emb_w", "emb_b", "pos"]],
+                                   algo=cfg.dp_algo, overlap=cfg.overlap)
+        self._load(full_init(cfg))
+        self._bufs = {}
+
+    # ------------------------------------------------------------- params
+    def _load(self, w):
+        cfg, t = self.cfg, self.tp_idx
+        sl = slice(t * self.hd, (t + 1) * self.hd)
+        P = self.flat.param
+        P("emb_w").copy_(w["emb_w"])
+        P("emb_b").copy_(w["emb_b"])
+        P("pos").copy_(w["pos"])
+        P("qkv_w").copy_(torch.cat([w["q_w"][sl], w["k_w"][sl], w["v_w"][sl]]))
+        P("qkv_b").copy_(torch.cat([w["q_b"][sl], w["k_b"][sl], w["v_b"][sl]]))
+        ow = torch.zeros(cfg.out_pad, self.hd)
+        ow[: cfg.n_classes] = w["o_w"][:, sl]
+        P("o_w").copy_(ow)
+        ob = torch.zeros(cfg.out_pad)
+        ob[: cfg.n_classes] = w["o_b"]
+        P("o_b").copy_(ob)
+        self.flat.refresh_bf16()
+
+    def gathered_full(self):
+        """Reassemble the unsharded weights (CPU, fp32) for checks."""
+        cfg = self.cfg
+        hc = self.mp_comm.comm if hasattr(self.mp_comm, "comm") else self.mp_comm
+        parts = hc.allgather({k: self.flat.param(k).detach().cpu() for k in ("qkv_w", "qkv_b", "o_w")})
+        q = torch.cat([p["qkv_w"][: self.hd] for p in parts])
+        return {"q_w": q, "o_w": torch.cat([p["o_w"][: cfg.n_classes] for p in parts], dim=1),
+                "emb_w": self.flat.param("emb_w").detach().cpu()}
+
+    # ------------------------------------------------------------ buffers
+    def _buf(self, name, shape, dtype, symmetric_on=None):
+        key = (name, tuple(shape), dtype)
+        b = self._bufs.get(key)
+        if b is None:
+            b = symmetric_on.empty(shape, dtype) if symmetric_on is not None else torch.empty(
+                shape, dtype=dtype, device=self.device)
+            self._bufs[key] = b
+        return b
+
+    # ------------------------------------------------------------ forward
+    def forward(self, xp: torch.Tensor, B: int) -> torch.Tensor:
+        """xp: (B*S, 64) bf16 patches -> logits (B, n_classes) fp32.  Saves activations."""
+        cfg = self.cfg
+        S, d = cfg.seq, cfg.d_model
+        M = B * S
+        P16 = self.flat.param16
+        h = self._buf("h", (M, d), torch.bfloat16)
+        gemm_nt(xp, P16("emb_w"), out=h, bias=self.flat.param("emb_b"))
+        h.view(B, S, d).add_(P16("pos"))
+        qkv = self._buf("qkv", (M, 3 * self.hd), torch.bfloat16)
+        gemm_nt(h, P16("qkv_w"), out=qkv, bias=self.flat.param("qkv_b"))
+        att = self._buf("att", (M, self.hd), torch.bfloat16)
+        lse = self._buf("lse", (B * self.hl, S), torch.float32)
+        D = _native.device()
+        st = torch.cuda.current_stream(self.device).cuda_stream
+        D.attn_small_fwd(qkv.data_ptr(), att.data_ptr(), lse.data_ptr(), B, S, self.hl, cfg.head_dim,
+                         qkv.stride(0), att.stride(0), 1.0 / math.sqrt(cfg.head_dim), st)
+        if cfg.fc_o_mode == "naive" and cfg.tp > 1:
+            z = self._forward_naive_fc_o(att, B)
+        else:
+            z = self._buf("z", (M, cfg.out_pad), torch.float32, self.tp_dev)
+            gemm_nt(att, P16("o_w"), out=z, out_dtype=torch.float32)
+            if self.tp_dev is not None:
+                self.tp_dev.allreduce(z, z, "SUM")  # row-parallel: one TP all-reduce
+        logits = z.view(B, S, cfg.out_pad)[:, :, : cfg.n_classes].mean(dim=1) + self.flat.param("o_b")[: cfg.n_classes]
+        self._saved = (xp, h, qkv, att, lse, B)
+        return logits
+
+    def _forward_naive_fc_o(self, att, B):
+        """Reference collects: gather fc_o's input, out-sharded fc_o, gather its output."""
+        cfg = self.cfg
+        S = cfg.seq
+        att_full = naive_collect_forward_input(att.view(B, S, self.hd), self.mp_comm, cfg.tp)
+        att_full = att_full.reshape(B * S, cfg.d_attn)
+        w_full = self._naive_o_w_full()
+        k = cfg.out_pad // cfg.tp
+        w_sh = w_full[self.tp_idx * k:(self.tp_idx + 1) * k].contiguous()
+        out_local = gemm_nt(att_full, w_sh, out_dtype=torch.float32)
+        z = naive_collect_forward_output(out_local.view(B, S, k), self.mp_comm, cfg.tp).reshape(B * S, cfg.out_pad)
+        self._naive = (att_full, w_sh)
+        return z
+
+    def _naive_o_w_full(self):
+        """[out_pad][d_attn] bf16: all TP ranks' input-dim shards side by side."""
+        cfg = self.cfg
+        w = self.flat.param16("o_w")
+        parts = torch.empty(cfg.tp, cfg.out_pad, self.hd, dtype=torch.bfloat16, device=self.device)
+        self.tp_dev.allgather(w.contiguous().view(-1), parts.view(-1))
+        return torch.cat(list(parts), dim=1).contiguous()
+
+    # ------------------------------------------------------------ backward
+    def loss_and_grad(self, logits: torch.Tensor, y: torch.Tensor, global_batch: int):
+        """Cross-entropy (mean over the global batch); returns (local loss sum / global batch, dlogits)."""
+        lp = torch.log_softmax(logits, dim=1)
+        loss = -lp.gather(1, y.long().view(-1, 1)).sum() / global_batch
+        dlogits = lp.exp()
+        dlogits[torch.arange(y.numel(), device=y.device), y.long()] -= 1.0
+        return loss, dlogits / global_batch
+
+    def backward(self, dlogits: torch.Tensor) -> None:
+        cfg = self.cfg
+        xp, h, qkv, att, lse, B = self._saved
+        S, d = cfg.seq, cfg.d_model
+        M = B * S
+        G = self.flat.grad
+        P16 = self.flat.param16
+        D = _native.device()
+        st = torch.cuda.current_stream(self.device).cuda_stream
+        # ---- output head: z[b,s,c] -> logits[b,c] = mean_s z + o_b
+        G("o_b")[: cfg.n_classes].add_(dlogits.sum(0))
+        dz = self._buf("dz", (M, cfg.out_pad), torch.bfloat16)
+        dz.zero_()
+        dz.view(B, S, cfg.out_pad)[:, :, : cfg.n_classes] = (dlogits / S).unsqueeze(1).to(torch.bfloat16)
+        datt = self._buf("datt", (M, self.hd), torch.bfloat16)
+        if cfg.fc_o_mode == "naive" and cfg.tp > 1:
+            self._backward_naive_fc_o(dz, datt, B)
+        else:
+            # row-parallel fc_o: dz is replicated on every TP rank (identity backward of the reduce)
+            dzT = transpose(dz)                                   # [out_pad, M]
+            attT = transpose(att)                                 # [hd, M]
+            gemm_nt(dzT, attT, out=G("o_w"), accumulate=True, out_dtype=torch.float32)
+            oT = transpose(P16("o_w"))                            # [hd, out_pad]
+            gemm_nt(dz, oT, out=datt)
+        self.buckets.ready(0)
+        # ---- attention
+        dqkv = self._buf("dqkv", (M, 3 * self.hd), torch.bfloat16)
+        D.attn_small_bwd(qkv.data_ptr(), att.data_ptr(), lse.data_ptr(), datt.data_ptr(), dqkv.data_ptr(), B, S,
+                         self.hl, cfg.head_dim, qkv.stride(0), att.stride(0), 1.0 / math.sqrt(cfg.head_dim), st)
+        # ---- fused QKV projection (column-parallel)
+        gemm_nt(transpose(dqkv), transpose(h), out=G("qkv_w"), accumulate=True, out_dtype=torch.float32)
+        G("qkv_b").add_(dqkv.float().sum(0))
+        self.buckets.ready(1)
+        dh = self._buf("dh", (M, d), torch.bfloat16, self.tp_dev)
+        gemm_nt(dqkv, transpose(P16("qkv_w")), out=dh)
+        if self.tp_dev is not None:
+            self.tp_dev.allreduce(dh, dh, "SUM")  # column-parallel input grad is TP-partial (fp32 sum inside)
+        # ---- embedding (replicated across TP)
+        gemm_nt(transpose(dh), transpose(xp), out=G("emb_w"), accumulate=True, out_dtype=torch.float32)
+        dh32 = dh.float()
+        G("emb_b").add_(dh32.sum(0))
+        G("pos").add_(dh32.view(B, S, d).sum(0))
+        self.buckets.ready(2)
+
+    def _backward_naive_fc_o(self, dz, datt, B):
+        """Reference backward collects: slice the output grad, local dX, reduce-scatter dX."""
+        cfg = self.cfg
+        S = cfg.seq
+        att_full, w_sh = self._naive
+        k = cfg.out_pad // cfg.tp
+        dz_local = naive_collect_backward_output(dz.view(B, S, cfg.out_pad), self.tp_idx, cfg.tp)
+        dz_local = dz_local.reshape(B * S, k).contiguous()
+        # weight grad of this rank's OUT-sharded rows [k, d_attn]; the stored parameter is the
+        # row-parallel INPUT shard [out_pad, hd], so assemble all ranks' rows (tiny) and slice columns
+        gw_sh = gemm_nt(transpose(dz_local), transpose(att_full), out_dtype=torch.float32)  # [k, d_attn]
+        gw_full = torch.zeros(cfg.out_pad, cfg.d_attn, dtype=torch.float32, device=self.device)
+        gw_full[self.tp_idx * k:(self.tp_idx + 1) * k] = gw_sh
+        self.tp_dev.allreduce(gw_full, gw_full, "SUM")
+        self.flat.grad("o_w").add_(gw_full[:, self.tp_idx * self.hd:(self.tp_idx + 1) * self.hd])
+        dx_full = gemm_nt(dz_local, transpose(w_sh), out_dtype=torch.bfloat16)     # [M, d_attn] partial
+        dx = naive_collect_backward_x(dx_full.view(B, S, cfg.d_attn), self.mp_comm, cfg.tp)
+        datt.copy_(dx.reshape(B * S, self.hd))
+
+    def zero_grad(self) -> None:
+        self.flat.g.zero_()
+
+    def step(self) -> None:
+        self.buckets.wait()
+        self.flat.adamw(self.cfg.lr, weight_decay=self.cfg.weight_decay, grad_scale=1.0 / self.cfg.dp)
+
+
+def local_batch(cfg: LayerConfig, x_all: np.ndarray, y_all: np.ndarray, step: int, rank: int, device):
+    """This rank's share of global batch ``step``: the global batch is
+    ``batch * dp`` consecutive samples; ``split_data`` (reference
+    data_parallel_preprocess.py:45-59 semantics) gives DP group ``rank // tp`` its
+    contiguous block, identical on every TP rank of the group."""
+    from ..data.preprocess import split_data
+
+    G = cfg.batch * cfg.dp
+    nb = max(1, x_all.shape[0] // G)
+    i = step % nb
+    xs, ys = split_data(x_all[i * G:(i + 1) * G], y_all[i * G:(i + 1) * G], cfg.tp, cfg.dp, rank)
+    xb = torch.from_numpy(np.ascontiguousarray(xs)).to(device)
+    yb = torch.from_numpy(np.ascontiguousarray(ys)).to(device)
+    return xb, yb

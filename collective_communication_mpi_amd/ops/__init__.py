@@ -1,0 +1,11 @@
+"""Device ops backed by the hand-written HIP kernels of ``_device`` (gfx950).
+
+Every op fails loudly (raises) when the extension is missing or an input
+violates a kernel precondition; there is no silent eager fallback."""
+from .kernels import (  # noqa: F401
+    gemm_nt,
+    linear,
+    transpose,
+    interleave_lastaxis,
+    deinterleave_lastaxis,
+)

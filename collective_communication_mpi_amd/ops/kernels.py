@@ -1,0 +1,98 @@
+"""Python entry points of the device kernels (csrc/device/*.hip)."""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from .. import _native
+
+_ACT = {None: 0, "none": 0, "relu": 1, "gelu": 2}
+
+
+def _D():
+    return _native.device()
+
+
+def _stream(t: torch.Tensor) -> int:
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def gemm_nt(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None, bias: Optional[torch.Tensor] = None,
+            alpha: float = 1.0, accumulate: bool = False, act: Optional[str] = None,
+            out_dtype: torch.dtype = torch.bfloat16) -> torch.Tensor:
+    """``out = act(alpha * a @ b.T + bias) (+ out)`` on MFMA (v_mfma_f32_16x16x32_bf16).
+
+    a: [M, K] bf16 row-major (row stride may exceed K), b: [N, K] bf16; K % 8 == 0.
+    bias: [N] fp32 or bf16.  out: [M, N] bf16 or fp32 (fp32 accumulate inside).
+    """
+    if a.dtype != torch.bfloat16 or b.dtype != torch.bfloat16:
+        raise TypeError("gemm_nt expects bf16 operands")
+    if a.dim() != 2 or b.dim() != 2 or a.shape[1] != b.shape[1]:
+        raise ValueError(f"gemm_nt shape mismatch: {tuple(a.shape)} x {tuple(b.shape)}^T")
+    if a.stride(1) != 1 or b.stride(1) != 1:
+        raise ValueError("gemm_nt operands must be K-contiguous")
+    M, K = a.shape
+    N = b.shape[0]
+    if out is None:
+        if accumulate:
+            raise ValueError("accumulate needs an output tensor")
+        out = torch.empty((M, N), dtype=out_dtype, device=a.device)
+    if out.stride(1) != 1 or out.shape != (M, N):
+        raise ValueError("gemm_nt output must be [M, N] with unit column stride")
+    if out.dtype not in (torch.bfloat16, torch.float32):
+        raise TypeError("gemm_nt output must be bf16 or fp32")
+    bias_kind = 0
+    bias_ptr = 0
+    if bias is not None:
+        bias_kind = 1 if bias.dtype == torch.float32 else 2
+        if bias.dtype not in (torch.float32, torch.bfloat16) or not bias.is_contiguous() or bias.numel() != N:
+            raise ValueError("bias must be a contiguous [N] fp32/bf16 tensor")
+        bias_ptr = bias.data_ptr()
+    _D().gemm_nt(a.data_ptr(), b.data_ptr(), out.data_ptr(), bias_ptr, M, N, K, a.stride(0), b.stride(0),
+                 out.stride(0), float(alpha), bool(accumulate), bias_kind, _ACT[act], out.dtype == torch.bfloat16,
+                 _stream(a))
+    return out
+
+
+def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, act: Optional[str] = None,
+           out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``x[..., K] @ w[N, K].T + bias`` with the MFMA GEMM (bf16 out)."""
+    lead = x.shape[:-1]
+    y = gemm_nt(x.reshape(-1, x.shape[-1]), w, out=None if out is None else out.reshape(-1, w.shape[0]),
+                bias=bias, act=act)
+    return y.reshape(*lead, w.shape[0])
+
+
+def transpose(x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """2-D transpose of a 16-bit tensor (LDS-tiled kernel)."""
+    if x.dim() != 2 or x.element_size() != 2 or x.stride(1) != 1:
+        raise ValueError("transpose expects a 2-D row-contiguous 16-bit tensor")
+    R, C = x.shape
+    if out is None:
+        out = torch.empty((C, R), dtype=x.dtype, device=x.device)
+    _D().transpose16(x.data_ptr(), out.data_ptr(), R, C, x.stride(0), out.stride(0), _stream(x))
+    return out
+
+
+def interleave_lastaxis(stage: torch.Tensor, p: int) -> torch.Tensor:
+    """``[p, *lead, k] -> [*lead, p*k]`` (np.concatenate(parts, axis=-1))."""
+    stage = stage.contiguous()
+    lead, k = stage.shape[1:-1], stage.shape[-1]
+    M = stage[0].numel() // max(k, 1)
+    out = torch.empty(*lead, p * k, dtype=stage.dtype, device=stage.device)
+    _D().interleave_lastaxis(stage.data_ptr(), out.data_ptr(), M, p, k * stage.element_size(), _stream(stage))
+    return out
+
+
+def deinterleave_lastaxis(x: torch.Tensor, p: int) -> torch.Tensor:
+    """``[*lead, p*k] -> [p, *lead, k]`` (np.stack(np.split(x, p, axis=-1)))."""
+    x = x.contiguous()
+    n = x.shape[-1]
+    if n % p:
+        raise ValueError("last axis not divisible by p")
+    k = n // p
+    M = x.numel() // max(n, 1)
+    out = torch.empty(p, *x.shape[:-1], k, dtype=x.dtype, device=x.device)
+    _D().deinterleave_lastaxis(x.data_ptr(), out.data_ptr(), M, p, k * x.element_size(), _stream(x))
+    return out

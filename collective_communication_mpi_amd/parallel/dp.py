@@ -1,0 +1,114 @@
+"""Data parallelism: flat parameter/gradient storage and bucketed gradient
+all-reduce overlapped with the backward pass.
+
+The reference only shards data across DP groups (data_parallel_preprocess.py:45-59)
+and builds ``dp_comm`` (func_impl.py:61-62); "we simply just split the batch"
+(README.md:177).  Here the DP group also synchronises gradients:
+
+* every parameter lives in one flat fp32 master buffer (+ a bf16 compute copy
+  + AdamW moments); gradients live in one flat fp32 buffer allocated from the
+  DP device group's *symmetric heap*, so bucket all-reduces run zero-copy
+  (no staging) with the hand-written two-shot kernel over all xGMI links;
+* the layout is in backward order, so each bucket is a contiguous range that
+  becomes ready as soon as its layer's weight-gradient GEMMs are issued;
+* ``GradBuckets.ready(i)`` records an event on the compute stream and launches
+  bucket ``i``'s all-reduce on a dedicated communication stream: the collective
+  overlaps the remaining backward GEMMs; ``wait()`` joins before the optimizer.
+* the 1/dp average is folded into the fused AdamW kernel (one pass over the
+  flat buffers that also refreshes the bf16 compute copy).
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import torch
+
+from .. import _native
+
+_ALIGN = 64  # elements: keeps every parameter view 256-B aligned
+
+
+class FlatParams:
+    def __init__(self, specs: Sequence[Tuple[str, Tuple[int, ...]]], device, grad_alloc=None):
+        self.specs = list(specs)
+        self.offsets: Dict[str, Tuple[int, int, Tuple[int, ...]]] = {}
+        off = 0
+        for name, shape in self.specs:
+            n = 1
+            for s in shape:
+                n *= int(s)
+            self.offsets[name] = (off, n, tuple(shape))
+            off += (n + _ALIGN - 1) // _ALIGN * _ALIGN
+        self.numel = max(off, _ALIGN)
+        self.device = torch.device(device)
+        self.p32 = torch.zeros(self.numel, dtype=torch.float32, device=self.device)
+        self.p16 = torch.zeros(self.numel, dtype=torch.bfloat16, device=self.device)
+        self.g = grad_alloc(self.numel) if grad_alloc else torch.zeros(self.numel, dtype=torch.float32,
+                                                                          device=self.device)
+        self.g.zero_()
+        self.m = torch.zeros_like(self.p32)
+        self.v = torch.zeros_like(self.p32)
+        self.step_count = 0
+
+    def view(self, buf: torch.Tensor, name: str) -> torch.Tensor:
+        off, n, shape = self.offsets[name]
+        return buf[off:off + n].view(shape)
+
+    def param(self, name):
+        return self.view(self.p32, name)
+
+    def param16(self, name):
+        return self.view(self.p16, name)
+
+    def grad(self, name):
+        return self.view(self.g, name)
+
+    def range_of(self, names: Sequence[str]) -> Tuple[int, int]:
+        lo = min(self.offsets[n][0] for n in names)
+        hi = max(self.offsets[n][0] + (self.offsets[n][1] + _ALIGN - 1) // _ALIGN * _ALIGN for n in names)
+        return lo, hi
+
+    def refresh_bf16(self) -> None:
+        _native.device().cast_bf16(self.p32.data_ptr(), self.p16.data_ptr(), self.numel,
+                                   torch.cuda.current_stream(self.device).cuda_stream)
+
+    def adamw(self, lr: float, betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0,
+              grad_scale: float = 1.0) -> None:
+        self.step_count += 1
+        _native.device().adamw_step(self.p32.data_ptr(), self.g.data_ptr(), self.m.data_ptr(), self.v.data_ptr(),
+                                    self.p16.data_ptr(), self.numel, lr, betas[0], betas[1], eps, weight_decay,
+                                    self.step_count, grad_scale, torch.cuda.current_stream(self.device).cuda_stream)
+
+
+class GradBuckets:
+    """Bucketed DP gradient all-reduce on a side stream."""
+
+    def __init__(self, flat: FlatParams, dp_group, buckets: Sequence[Sequence[str]], algo: str = "auto",
+                 overlap: bool = True):
+        self.flat = flat
+        self.dp = dp_group  # DeviceGroup or None (dp == 1)
+        self.ranges = [flat.range_of(b) for b in buckets]
+        self.algo = algo
+        self.overlap = overlap
+        self.stream = torch.cuda.Stream(device=flat.device) if (dp_group is not None and overlap) else None
+        self.events: List[torch.cuda.Event] = [torch.cuda.Event() for _ in self.ranges]
+        self.launched = 0
+
+    def ready(self, i: int) -> None:
+        if self.dp is None or self.dp.size == 1:
+            return
+        lo, hi = self.ranges[i]
+        seg = self.flat.g[lo:hi]
+        if self.stream is None:
+            self.dp.allreduce(seg, seg, "SUM", self.algo)
+            return
+        ev = self.events[i]
+        ev.record(torch.cuda.current_stream(self.flat.device))
+        self.stream.wait_event(ev)
+        with torch.cuda.stream(self.stream):
+            self.dp.allreduce(seg, seg, "SUM", self.algo)
+        self.launched += 1
+
+    def wait(self) -> None:
+        if self.stream is not None:
+            torch.cuda.current_stream(self.flat.device).wait_stream(self.stream)

@@ -1,0 +1,56 @@
+"""Native host plane + Communicator façade across rank counts (CPU)."""
+import numpy as np
+import pytest
+from hypothesis import given, settings
+from hypothesis import strategies as st
+
+from _launch import py, run_ranks
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 4, 8])
+def test_host_plane_all_ops(n):
+    r = run_ranks(n, py("tests/workers/host_worker.py"), timeout=300,
+                  env={"CCMPI_SLOT_BYTES": str(64 << 10), "CCMPI_RING_BYTES": str(16 << 10)})
+    assert "host plane OK" in r.stdout
+
+
+def test_mpi_test_cli_cases():
+    for case in ["allreduce", "allgather", "reduce_scatter", "split", "alltoall"]:
+        r = run_ranks(8, py("mpi-test.py", "--test_case", case), timeout=120)
+        assert "Rank 7" in r.stdout
+    r = run_ranks(8, py("mpi-test.py", "--test_case", "myallreduce", "--runs", "20"), timeout=120)
+    assert "All runs produced correct results." in r.stdout and "Average myAllreduce time" in r.stdout
+    r = run_ranks(8, py("mpi-test.py", "--test_case", "myalltoall", "--runs", "20"), timeout=120)
+    assert "All runs produced correct results." in r.stdout
+    r = run_ranks(3, py("mpi-test.py"), timeout=60)
+    assert sorted(l for l in r.stdout.splitlines() if l.startswith("This is rank")) == [
+        "This is rank 0.", "This is rank 1.", "This is rank 2."]
+
+
+def test_launcher_propagates_failure():
+    r = run_ranks(3, py("-c", "import os,sys; sys.exit(3 if os.environ['CCMPI_RANK']=='1' else 0)"),
+                  timeout=60, check=False)
+    assert r.returncode == 3
+
+
+_DT = {"int8": 0, "uint8": 1, "int16": 2, "uint16": 3, "int32": 4, "uint32": 5, "int64": 6, "uint64": 7,
+       "float16": 8, "float32": 10, "float64": 11}
+
+
+@settings(max_examples=60, deadline=None)
+@given(dt=st.sampled_from(["int8", "int16", "int32", "int64", "uint16", "float16", "float32", "float64"]),
+       op=st.sampled_from(["SUM", "PROD", "MIN", "MAX"]), n=st.integers(0, 300), seed=st.integers(0, 2 ** 16))
+def test_native_reduce_matches_numpy(dt, op, n, seed):
+    from collective_communication_mpi_amd import _native
+
+    h = _native.host()
+    g = np.random.default_rng(seed)
+    a = (g.standard_normal(n) * 5).astype(dt) if dt.startswith("f") else g.integers(-9, 9, n).astype(dt)
+    b = (g.standard_normal(n) * 5).astype(dt) if dt.startswith("f") else g.integers(-9, 9, n).astype(dt)
+    ref = {"SUM": np.add, "PROD": np.multiply, "MIN": np.minimum, "MAX": np.maximum}[op](a, b)
+    out = a.copy()
+    h.reduce_local(b, out, _DT[dt], ["SUM", "PROD", "MIN", "MAX"].index(op))
+    if dt.startswith("f"):
+        np.testing.assert_allclose(out, ref, rtol=1e-3 if dt == "float16" else 1e-6)
+    else:
+        np.testing.assert_array_equal(out, ref)

@@ -1,0 +1,193 @@
+"""Multi-rank checks of the native host plane + Communicator (CPU only).
+
+Each rank regenerates every peer's input from (seed, rank), so results are
+checked against a NumPy oracle without extra communication."""
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", ".."))
+from collective_communication_mpi_amd import MPI, Communicator  # noqa: E402
+
+comm = MPI.COMM_WORLD
+rank, p = comm.Get_rank(), comm.Get_size()
+SLOT = comm._hc.slot_bytes
+fails = []
+
+
+def inp(r, n, dt, salt):
+    g = np.random.default_rng(10_000 * salt + r)
+    if np.dtype(dt).kind == "f":
+        return (g.standard_normal(n) * 4).astype(dt)
+    if np.dtype(dt).kind == "b":
+        return g.integers(0, 2, n).astype(dt)
+    info = np.iinfo(dt)
+    return g.integers(max(info.min, -50), min(info.max, 50), n).astype(dt)
+
+
+def expect(eq, name):
+    if not eq:
+        fails.append(name)
+
+
+NP_OPS = {"SUM": np.add, "PROD": np.multiply, "MIN": np.minimum, "MAX": np.maximum}
+salt = 0
+# ---- Allreduce: dtypes x ops x sizes (incl. multi-chunk) + IN_PLACE
+for dt in [np.int8, np.int32, np.int64, np.uint16, np.float16, np.float32, np.float64]:
+    for opname in ["SUM", "MIN", "MAX", "PROD"]:
+        for n in [1, 5, 1000, SLOT // np.dtype(dt).itemsize + 77]:
+            salt += 1
+            if opname == "PROD" and n > 1000:
+                continue
+            xs = [inp(r, n, dt, salt) for r in range(p)]
+            ref = xs[0].copy()
+            for x in xs[1:]:
+                ref = NP_OPS[opname](ref, x)
+            out = np.empty(n, dt)
+            comm.Allreduce(xs[rank], out, op=getattr(MPI, opname))
+            ok = np.allclose(out, ref, rtol=1e-2, atol=1e-2) if np.dtype(dt).kind == "f" else np.array_equal(out, ref)
+            expect(ok, f"Allreduce {dt.__name__} {opname} n={n}")
+            buf = xs[rank].copy()
+            comm.Allreduce(MPI.IN_PLACE, buf, op=getattr(MPI, opname))
+            expect(np.array_equal(buf, out), f"Allreduce IN_PLACE {dt.__name__} {opname}")
+# ---- rooted / vector collectives
+for n in [3, SLOT // 8 + 5]:
+    salt += 1
+    xs = [inp(r, n, np.float64, salt) for r in range(p)]
+    root = p - 1
+    out = np.empty(n) if rank == root else None
+    comm.Reduce(xs[rank], out, op=MPI.SUM, root=root)
+    if rank == root:
+        expect(np.allclose(out, sum(xs)), f"Reduce n={n}")
+    b = xs[rank].copy()
+    comm.Bcast(b, root=1 % p)
+    expect(np.array_equal(b, xs[1 % p]), f"Bcast n={n}")
+    ag = np.empty(p * n)
+    comm.Allgather(xs[rank], ag)
+    expect(np.array_equal(ag, np.concatenate(xs)), f"Allgather n={n}")
+    g = np.empty(p * n) if rank == 0 else None
+    comm.Gather(xs[rank], g, root=0)
+    if rank == 0:
+        expect(np.array_equal(g, np.concatenate(xs)), f"Gather n={n}")
+    sc = np.empty(n)
+    comm.Scatter(np.concatenate(xs) if rank == 0 else None, sc, root=0)
+    expect(np.array_equal(sc, xs[rank]), f"Scatter n={n}")
+    big = [inp(r, p * n, np.int64, salt) for r in range(p)]
+    rs = np.empty(n, np.int64)
+    comm.Reduce_scatter_block(big[rank], rs, op=MPI.SUM)
+    expect(np.array_equal(rs, sum(big)[rank * n:(rank + 1) * n]), f"Reduce_scatter_block n={n}")
+    a2a = np.empty(p * n, np.int64)
+    comm.Alltoall(big[rank], a2a)
+    expect(np.array_equal(a2a, np.concatenate([big[j][rank * n:(rank + 1) * n] for j in range(p)])), f"Alltoall n={n}")
+    sc_ = np.empty(n, np.int64)
+    comm.Scan(big[rank][:n], sc_, op=MPI.SUM)
+    expect(np.array_equal(sc_, sum(b_[:n] for b_ in big[: rank + 1])), f"Scan n={n}")
+# variable counts
+counts = [r + 1 for r in range(p)]
+displs = list(np.cumsum([0] + counts[:-1]))
+mine = np.full(counts[rank], rank, np.int32)
+agv = np.empty(sum(counts), np.int32)
+comm.Allgatherv(mine, [agv, counts, displs, MPI.INT])
+expect(np.array_equal(agv, np.concatenate([np.full(c, r, np.int32) for r, c in enumerate(counts)])), "Allgatherv")
+src = np.arange(sum(counts), dtype=np.float32) * (rank + 1)
+rsv = np.empty(counts[rank], np.float32)
+comm.Reduce_scatter(src, rsv, recvcounts=counts, op=MPI.SUM)
+tot = np.arange(sum(counts), dtype=np.float32) * sum(range(1, p + 1))
+expect(np.allclose(rsv, tot[displs[rank]:displs[rank] + counts[rank]]), "Reduce_scatter(v)")
+# ---- point to point: tags out of order, ANY_SOURCE, probe, big messages
+if p > 1:
+    nxt, prv = (rank + 1) % p, (rank - 1) % p
+    a = np.full(10, rank, np.int64)
+    b_ = np.full(10, rank + 100, np.int64)
+    r1 = comm.Isend(a, dest=nxt, tag=1)
+    r2 = comm.Isend(b_, dest=nxt, tag=2)
+    x2 = np.empty(10, np.int64)
+    x1 = np.empty(10, np.int64)
+    st = MPI.Status()
+    comm.Recv(x2, source=prv, tag=2, status=st)   # matches the second message first
+    comm.Recv(x1, source=MPI.ANY_SOURCE, tag=1)
+    MPI.Request.Waitall([r1, r2])
+    expect(np.all(x2 == prv + 100) and np.all(x1 == prv) and st.Get_source() == prv and st.Get_tag() == 2
+           and st.Get_count(MPI.LONG) == 10, "tag matching")
+    big = np.arange(3_000_001, dtype=np.float64) + rank
+    got = np.empty_like(big)
+    comm.Sendrecv(big, dest=nxt, sendtag=7, recvbuf=got, source=prv, recvtag=7)
+    expect(np.array_equal(got, np.arange(3_000_001, dtype=np.float64) + prv), "big Sendrecv")
+    comm.send({"from": rank, "list": list(range(rank))}, dest=nxt, tag=9)
+    obj = comm.recv(source=prv, tag=9)
+    expect(obj == {"from": prv, "list": list(range(prv))}, "object send/recv")
+    req = comm.isend([rank] * 3, dest=prv, tag=11)
+    o2 = comm.irecv(source=nxt, tag=11).wait()
+    req.Wait()
+    expect(o2 == [nxt] * 3, "isend/irecv objects")
+# ---- object collectives, split, dup
+expect(comm.allgather(rank * 2) == [r * 2 for r in range(p)], "allgather obj")
+expect(comm.alltoall([(rank, j) for j in range(p)]) == [(j, rank) for j in range(p)], "alltoall obj")
+expect(comm.bcast({"x": rank} if rank == 0 else None, root=0) == {"x": 0}, "bcast obj")
+expect(comm.allreduce(rank, op=MPI.MAX) == p - 1, "allreduce obj")
+sub = comm.Split(color=rank % 2, key=-rank)
+members = [r for r in range(p) if r % 2 == rank % 2]
+expect(sub.Get_size() == len(members) and sub.Get_rank() == sorted(members, reverse=True).index(rank), "Split key order")
+expect(sub.allreduce(rank) == sum(members), "Split allreduce")
+sub2 = sub.Split(color=0, key=0)
+expect(sub2.allreduce(1) == len(members), "nested Split")
+none = comm.Split(color=MPI.UNDEFINED if rank == 0 else 1, key=0)
+expect((none is MPI.COMM_NULL) if rank == 0 else none.Get_size() == p - 1, "Split UNDEFINED")
+dup = comm.Dup()
+expect(dup.allreduce(1) == p, "Dup")
+expect(MPI.COMM_SELF.Get_size() == 1, "COMM_SELF")
+# ---- Communicator façade: my* algorithms vs library + reference byte accounting
+C = Communicator(comm)
+for algo in ["reduce_bcast", "ring", "rhd"]:
+    for dt, op in [(np.int64, MPI.MIN), (np.float64, MPI.SUM), (np.int32, MPI.MAX)]:
+        for n in [1, p, 100, 1001]:
+            salt += 1
+            x = inp(rank, n, dt, salt)
+            lib, my = np.empty_like(x), np.empty_like(x)
+            C.Allreduce(x, lib, op=op)
+            C.myAllreduce(x, my, op=op, algo=algo)
+            ok = np.allclose(lib, my) if np.dtype(dt).kind == "f" else np.array_equal(lib, my)
+            expect(ok, f"myAllreduce {algo} {dt.__name__} {op} n={n}")
+for n in [p, 4 * p, 1000 * p]:
+    x = np.arange(n, dtype=np.int64) + 1000 * rank
+    lib, my, my2 = np.empty_like(x), np.empty_like(x), np.empty_like(x)
+    C.Alltoall(x, lib)
+    C.myAlltoall(x, my)
+    C.myAlltoall2(x, my2)
+    expect(np.array_equal(lib, my) and np.array_equal(lib, my2), f"myAlltoall n={n}")
+try:
+    C.myAllreduce(np.ones(3), np.ones(3), op=MPI.BAND)
+    expect(False, "myAllreduce must reject BAND on every rank")
+except NotImplementedError:
+    pass
+A = Communicator(comm)
+S = 800
+x = np.zeros(100, np.int64)
+A.Allreduce(x, np.empty_like(x))
+expect(A.total_bytes_transferred == S * 2 * (p - 1), "accounting Allreduce")
+A.total_bytes_transferred = 0
+A.myAllreduce(x, np.empty_like(x), op=MPI.MIN)
+expect(A.total_bytes_transferred == (2 * S * (p - 1) if rank == 0 else 2 * S), "accounting myAllreduce")
+A.total_bytes_transferred = 0
+A.Allgather(np.zeros(2, np.int64), np.empty(2 * p, np.int64))
+expect(A.total_bytes_transferred == 16 * (p - 1) + 16 * p * (p - 1), "accounting Allgather")
+A.total_bytes_transferred = 0
+A.Reduce_scatter(np.zeros(2 * p, np.int64), np.empty(2, np.int64))
+expect(A.total_bytes_transferred == 16 * p * (p - 1) + 16 * (p - 1), "accounting Reduce_scatter")
+A.total_bytes_transferred = 0
+A.Alltoall(np.zeros(4 * p, np.int32), np.empty(4 * p, np.int32))
+expect(A.total_bytes_transferred == 2 * 16 * (p - 1), "accounting Alltoall")
+A.total_bytes_transferred = 0
+A.myAlltoall(np.zeros(4 * p, np.int32), np.empty(4 * p, np.int32))
+A.myAlltoall2(np.zeros(4 * p, np.int32), np.empty(4 * p, np.int32))
+expect(A.total_bytes_transferred == 2 * (2 * 16 * (p - 1)), "accounting myAlltoall(2)")
+child = A.Split(key=rank, color=0)
+expect(child.total_bytes_transferred == 0 and child.Get_size() == p, "Split resets the counter")
+
+comm.Barrier()
+if fails:
+    print(f"[rank {rank}] {len(fails)} FAILURES: {fails[:10]}", flush=True)
+    sys.exit(1)
+if rank == 0:
+    print(f"host plane OK at {p} ranks", flush=True)
