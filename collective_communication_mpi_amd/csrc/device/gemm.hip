@@ -45,6 +45,7 @@ struct GemmArgs {
   int bias_kind;   // 0 none, 1 fp32, 2 bf16
   int act;         // 0 none, 1 relu, 2 gelu(tanh)
   int out_bf16;    // 0 fp32 out, 1 bf16 out
+  int splitk;      // >1: K split over workgroups, fp32 atomic-add epilogue into C
 };
 
 __device__ __forceinline__ float bf2f(uint16_t h) { return __uint_as_float((uint32_t)h << 16); }
@@ -57,13 +58,16 @@ __device__ __forceinline__ float gelu_tanh(float x) {
 __global__ void __launch_bounds__(NT) k_gemm_nt(GemmArgs g) {
   __shared__ __attribute__((aligned(16))) unsigned char smem[2 * (BM + BN) * kRowBytes];
   const int tiles_n = (g.N + BN - 1) / BN, tiles_m = (g.M + BM - 1) / BM;
-  const int nwg = tiles_n * tiles_m;
-  // bijective XCD-aware remap: blocks b, b+8, b+16, ... (same XCD) get consecutive tile ids
+  const int nwg = tiles_n * tiles_m * g.splitk;
+  // bijective XCD-aware remap: blocks b, b+8, b+16, ... (same XCD) get consecutive ids;
+  // the K slices of one tile are adjacent ids, so they share an XCD (and its L2)
   int wg = blockIdx.x;
   {
     const int q = nwg / 8, r = nwg % 8, x = wg % 8;
     wg = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + wg / 8;
   }
+  const int split = wg % g.splitk;
+  wg /= g.splitk;
   const int bm = (wg / tiles_n) * BM, bn = (wg % tiles_n) * BN;
   const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
   const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
@@ -99,13 +103,18 @@ __global__ void __launch_bounds__(NT) k_gemm_nt(GemmArgs g) {
     }
   };
 
-  gload(0);
-  swrite(0);
+  const int nk_all = (g.K + BK - 1) / BK;
+  const int per = (nk_all + g.splitk - 1) / g.splitk;
+  const int kt0 = split * per;
+  const int nk = max(0, min(nk_all, kt0 + per) - kt0);
+  if (nk > 0) {
+    gload(kt0 * BK);
+    swrite(0);
+  }
   __syncthreads();
-  const int nk = (g.K + BK - 1) / BK;
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
-    if (kt + 1 < nk) gload((kt + 1) * BK);
+    if (kt + 1 < nk) gload((kt0 + kt + 1) * BK);
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       bf16x8 af[4], bf[4];
@@ -132,8 +141,10 @@ __global__ void __launch_bounds__(NT) k_gemm_nt(GemmArgs g) {
     const int col = bn + wn + j * 16 + (lane & 15);
     if (col >= g.N) continue;
     float b = 0.f;
-    if (g.bias_kind == 1) b = reinterpret_cast<const float*>(g.bias)[col];
-    else if (g.bias_kind == 2) b = bf2f(reinterpret_cast<const uint16_t*>(g.bias)[col]);
+    if (split == 0) {
+      if (g.bias_kind == 1) b = reinterpret_cast<const float*>(g.bias)[col];
+      else if (g.bias_kind == 2) b = bf2f(reinterpret_cast<const uint16_t*>(g.bias)[col]);
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
 #pragma unroll
@@ -141,6 +152,10 @@ __global__ void __launch_bounds__(NT) k_gemm_nt(GemmArgs g) {
         const int row = bm + wm + i * 16 + (lane >> 4) * 4 + r;
         if (row >= g.M) continue;
         float v = g.alpha * acc[i][j][r] + b;
+        if (g.splitk > 1) {  // partial sums of K slices meet in C (fp32, pre-initialised)
+          atomicAdd(reinterpret_cast<float*>(g.C) + (size_t)row * g.ldc + col, v);
+          continue;
+        }
         if (g.act == 1) v = fmaxf(v, 0.f);
         else if (g.act == 2) v = gelu_tanh(v);
         const size_t o = (size_t)row * g.ldc + col;
@@ -153,6 +168,128 @@ __global__ void __launch_bounds__(NT) k_gemm_nt(GemmArgs g) {
           if (g.accumulate) v += C[o];
           C[o] = v;
         }
+      }
+    }
+  }
+}
+
+
+// ---------------------------------------------------------------------------
+// "TN" GEMM for weight gradients: C[N1,N2] (+)= alpha * sum_m A[m,n1] * B[m,n2]
+// with A [M][N1] and B [M][N2] row-major (n contiguous), i.e. dW = dY^T X
+// without materialising any transpose.  Tiles of 64 m-rows x 128 columns are
+// staged as-is into LDS; MFMA operands (8 consecutive m for one column per
+// lane) come out of gfx950's transposing LDS read ds_read_b64_tr_b16, two
+// reads per operand per 32-deep k-step.  LDS rows are 256 B + 32 B pad (row r
+// starts 8 banks after row r-1) and the two 128-B halves of rows with bit 3
+// set are swapped, so every tr read (a 32-lane half spans rows r..r+3 and
+// r+8..r+11) is bank-conflict free.  K (= batch*seq) is long and M, N small:
+// the split-K grid fills the chip and partial tiles meet through fp32
+// atomic adds.
+// ---------------------------------------------------------------------------
+typedef short v4s __attribute__((ext_vector_type(4)));
+constexpr int kTnRow = 288;             // bytes per LDS row (256 data + 32 pad)
+constexpr int kTnTile = BK * kTnRow;    // one operand tile
+
+__device__ __forceinline__ int tn_off(int row, int byte) { return row * kTnRow + (byte ^ (((row >> 3) & 1) << 7)); }
+
+__global__ void __launch_bounds__(NT) k_gemm_tn(GemmArgs g) {
+  __shared__ __attribute__((aligned(16))) unsigned char smem[4 * kTnTile];
+  // here: g.M = N1 (rows of C), g.N = N2 (cols of C), g.K = M (reduction)
+  const int tiles_n = (g.N + BN - 1) / BN, tiles_m = (g.M + BM - 1) / BM;
+  const int nwg = tiles_n * tiles_m * g.splitk;
+  int wg = blockIdx.x;
+  {
+    const int q = nwg / 8, r = nwg % 8, x = wg % 8;
+    wg = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + wg / 8;
+  }
+  const int split = wg % g.splitk;
+  wg /= g.splitk;
+  const int bm = (wg / tiles_n) * BM, bn = (wg % tiles_n) * BN;
+  const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
+  const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
+  auto As = [&](int buf) { return smem + buf * (2 * kTnTile); };
+  auto Bs = [&](int buf) { return smem + buf * (2 * kTnTile) + kTnTile; };
+
+  floatx4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  uint4 ra[4], rb[4];
+  const int schunk = t & 15, srow = t >> 4;  // 16 chunks of 16 B per 128-column row
+  auto gload = [&](int m0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = m0 + srow + 16 * i;
+      const int ca = bm + schunk * 8, cb = bn + schunk * 8;
+      ra[i] = (m < g.K && ca < g.M) ? *reinterpret_cast<const uint4*>(g.A + (size_t)m * g.lda + ca) : uint4{0, 0, 0, 0};
+      rb[i] = (m < g.K && cb < g.N) ? *reinterpret_cast<const uint4*>(g.B + (size_t)m * g.ldb + cb) : uint4{0, 0, 0, 0};
+    }
+  };
+  auto swrite = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = srow + 16 * i;
+      *reinterpret_cast<uint4*>(As(buf) + tn_off(r, schunk * 16)) = ra[i];
+      *reinterpret_cast<uint4*>(Bs(buf) + tn_off(r, schunk * 16)) = rb[i];
+    }
+  };
+  const int nk_all = (g.K + BK - 1) / BK;
+  const int per = (nk_all + g.splitk - 1) / g.splitk;
+  const int kt0 = split * per;
+  const int nk = max(0, min(nk_all, kt0 + per) - kt0);
+  if (nk > 0) {
+    gload(kt0 * BK);
+    swrite(0);
+  }
+  __syncthreads();
+  const int grp = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) gload((kt0 + kt + 1) * BK);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 af[4], bf[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        v4s a0, a1, b0, b1;
+        const int r0 = ks * 32 + grp * 8 + q;
+        const int ca = (wm + i * 16 + 4 * p) * 2, cb = (wn + i * 16 + 4 * p) * 2;
+        a0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(As(cur) + tn_off(r0, ca)));
+        a1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(As(cur) + tn_off(r0 + 4, ca)));
+        b0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(Bs(cur) + tn_off(r0, cb)));
+        b1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(Bs(cur) + tn_off(r0 + 4, cb)));
+        typedef short v8s __attribute__((ext_vector_type(8)));
+        v8s av = __builtin_shufflevector(a0, a1, 0, 1, 2, 3, 4, 5, 6, 7);
+        v8s bv = __builtin_shufflevector(b0, b1, 0, 1, 2, 3, 4, 5, 6, 7);
+        af[i] = __builtin_bit_cast(bf16x8, av);
+        bf[i] = __builtin_bit_cast(bf16x8, bv);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf[j], acc[i][j], 0, 0, 0);
+    }
+    if (kt + 1 < nk) swrite(cur ^ 1);
+    __syncthreads();
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int col = bn + wn + j * 16 + (lane & 15);
+    if (col >= g.N) continue;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = bm + wm + i * 16 + (lane >> 4) * 4 + r;
+        if (row >= g.M) continue;
+        const float v = g.alpha * acc[i][j][r];
+        const size_t o = (size_t)row * g.ldc + col;
+        float* C = reinterpret_cast<float*>(g.C);
+        if (g.splitk > 1) atomicAdd(C + o, v);
+        else C[o] = g.accumulate ? C[o] + v : v;
       }
     }
   }
@@ -176,15 +313,38 @@ __global__ void __launch_bounds__(256) k_transpose16(const uint16_t* __restrict_
 }
 
 void gemm_nt(uint64_t A, uint64_t B, uint64_t C, uint64_t bias, int M, int N, int K, int lda, int ldb, int ldc,
-             float alpha, bool accumulate, int bias_kind, int act, bool out_bf16, uint64_t stream) {
+             float alpha, bool accumulate, int bias_kind, int act, bool out_bf16, int splitk, uint64_t stream) {
   if (M <= 0 || N <= 0) return;
   if (K % 8 || lda % 8 || ldb % 8 || (A % 16) || (B % 16))
     throw std::invalid_argument("ccmpi gemm: K, lda, ldb must be multiples of 8 and A/B 16-B aligned");
+  if (splitk < 1) splitk = 1;
+  if (splitk > 1 && (out_bf16 || act != 0))
+    throw std::invalid_argument("ccmpi gemm: split-K needs an fp32 output and no activation");
+  if (splitk > 1 && !accumulate)
+    CCMPI_HIP_CHECK(hipMemset2DAsync(reinterpret_cast<void*>(C), (size_t)ldc * 4, 0, (size_t)N * 4, M,
+                                     reinterpret_cast<hipStream_t>(stream)));
   GemmArgs g{reinterpret_cast<const uint16_t*>(A), reinterpret_cast<const uint16_t*>(B), reinterpret_cast<void*>(C),
              reinterpret_cast<const void*>(bias), M, N, K, lda, ldb, ldc, alpha, accumulate ? 1 : 0, bias_kind,
-             act, out_bf16 ? 1 : 0};
-  const int nwg = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+             act, out_bf16 ? 1 : 0, splitk};
+  const int nwg = ((M + BM - 1) / BM) * ((N + BN - 1) / BN) * splitk;
   hipLaunchKernelGGL(k_gemm_nt, dim3(nwg), dim3(NT), 0, reinterpret_cast<hipStream_t>(stream), g);
+  CCMPI_HIP_CHECK(hipGetLastError());
+}
+
+// C[N1,N2] (+)= alpha * A[M,N1]^T . B[M,N2]; fp32 output.
+void gemm_tn(uint64_t A, uint64_t B, uint64_t C, int M, int N1, int N2, int lda, int ldb, int ldc, float alpha,
+             bool accumulate, int splitk, uint64_t stream) {
+  if (N1 <= 0 || N2 <= 0 || M <= 0) return;
+  if (N1 % 8 || N2 % 8 || lda % 8 || ldb % 8 || (A % 16) || (B % 16))
+    throw std::invalid_argument("ccmpi gemm_tn: N1, N2, lda, ldb must be multiples of 8 and A/B 16-B aligned");
+  if (splitk < 1) splitk = 1;
+  if (splitk > 1 && !accumulate)
+    CCMPI_HIP_CHECK(hipMemset2DAsync(reinterpret_cast<void*>(C), (size_t)ldc * 4, 0, (size_t)N2 * 4, N1,
+                                     reinterpret_cast<hipStream_t>(stream)));
+  GemmArgs g{reinterpret_cast<const uint16_t*>(A), reinterpret_cast<const uint16_t*>(B), reinterpret_cast<void*>(C),
+             nullptr, N1, N2, M, lda, ldb, ldc, alpha, accumulate ? 1 : 0, 0, 0, 0, splitk};
+  const int nwg = ((N1 + BM - 1) / BM) * ((N2 + BN - 1) / BN) * splitk;
+  hipLaunchKernelGGL(k_gemm_tn, dim3(nwg), dim3(NT), 0, reinterpret_cast<hipStream_t>(stream), g);
   CCMPI_HIP_CHECK(hipGetLastError());
 }
 
@@ -203,7 +363,10 @@ void register_gemm_ops(pybind11::module_& m) {
         pybind11::arg("A"), pybind11::arg("B"), pybind11::arg("C"), pybind11::arg("bias"), pybind11::arg("M"),
         pybind11::arg("N"), pybind11::arg("K"), pybind11::arg("lda"), pybind11::arg("ldb"), pybind11::arg("ldc"),
         pybind11::arg("alpha"), pybind11::arg("accumulate"), pybind11::arg("bias_kind"), pybind11::arg("act"),
-        pybind11::arg("out_bf16"), pybind11::arg("stream"), pybind11::call_guard<pybind11::gil_scoped_release>());
+        pybind11::arg("out_bf16"), pybind11::arg("splitk"), pybind11::arg("stream"),
+        pybind11::call_guard<pybind11::gil_scoped_release>());
+  m.def("gemm_tn", &gemm_tn, "C[N1,N2] (+)= alpha*A[M,N1]^T.B[M,N2] (fp32 out, split-K atomics)",
+        pybind11::call_guard<pybind11::gil_scoped_release>());
   m.def("transpose16", &transpose16, "dst[C,R] = src[R,C]^T for 16-bit elements",
         pybind11::call_guard<pybind11::gil_scoped_release>());
 }

@@ -36,7 +36,7 @@ import numpy as np
 import torch
 
 from .. import _native
-from ..ops import gemm_nt, transpose
+from ..ops import gemm_nt, gemm_tn, transpose
 from ..parallel.dp import FlatParams, GradBuckets
 from ..parallel.layout import device_group_for, get_info, naive_collect_backward_output, naive_collect_backward_x, \
     naive_collect_forward_input, naive_collect_forward_output
@@ -246,10 +246,8 @@ class MnistTPLayer:
             self._backward_naive_fc_o(dz, datt, B)
         else:
             # row-parallel fc_o: dz is replicated on every TP rank (identity backward of the reduce)
-            dzT = transpose(dz)                                   # [out_pad, M]
-            attT = transpose(att)                                 # [hd, M]
-            gemm_nt(dzT, attT, out=G("o_w"), accumulate=True, out_dtype=torch.float32)
-            oT = transpose(P16("o_w"))                            # [hd, out_pad]
+            gemm_tn(dz, att, out=G("o_w"), accumulate=True)      # dW_o = dZ^T . att
+            oT = transpose(P16("o_w"))                            # [hd, out_pad] (tiny)
             gemm_nt(dz, oT, out=datt)
         self.buckets.ready(0)
         # ---- attention
@@ -257,7 +255,7 @@ class MnistTPLayer:
         D.attn_small_bwd(qkv.data_ptr(), att.data_ptr(), lse.data_ptr(), datt.data_ptr(), dqkv.data_ptr(), B, S,
                          self.hl, cfg.head_dim, qkv.stride(0), att.stride(0), 1.0 / math.sqrt(cfg.head_dim), st)
         # ---- fused QKV projection (column-parallel)
-        gemm_nt(transpose(dqkv), transpose(h), out=G("qkv_w"), accumulate=True, out_dtype=torch.float32)
+        gemm_tn(dqkv, h, out=G("qkv_w"), accumulate=True)      # dW_qkv = dQKV^T . h
         G("qkv_b").add_(dqkv.float().sum(0))
         self.buckets.ready(1)
         dh = self._buf("dh", (M, d), torch.bfloat16, self.tp_dev)
@@ -265,7 +263,7 @@ class MnistTPLayer:
         if self.tp_dev is not None:
             self.tp_dev.allreduce(dh, dh, "SUM")  # column-parallel input grad is TP-partial (fp32 sum inside)
         # ---- embedding (replicated across TP)
-        gemm_nt(transpose(dh), transpose(xp), out=G("emb_w"), accumulate=True, out_dtype=torch.float32)
+        gemm_tn(dh, xp, out=G("emb_w"), accumulate=True)       # dW_emb = dH^T . patches
         dh32 = dh.float()
         G("emb_b").add_(dh32.sum(0))
         G("pos").add_(dh32.view(B, S, d).sum(0))
@@ -281,7 +279,7 @@ class MnistTPLayer:
         dz_local = dz_local.reshape(B * S, k).contiguous()
         # weight grad of this rank's OUT-sharded rows [k, d_attn]; the stored parameter is the
         # row-parallel INPUT shard [out_pad, hd], so assemble all ranks' rows (tiny) and slice columns
-        gw_sh = gemm_nt(transpose(dz_local), transpose(att_full), out_dtype=torch.float32)  # [k, d_attn]
+        gw_sh = gemm_tn(dz_local, att_full)                                                # [k, d_attn]
         gw_full = torch.zeros(cfg.out_pad, cfg.d_attn, dtype=torch.float32, device=self.device)
         gw_full[self.tp_idx * k:(self.tp_idx + 1) * k] = gw_sh
         self.tp_dev.allreduce(gw_full, gw_full, "SUM")

@@ -4,6 +4,7 @@ Every op fails loudly (raises) when the extension is missing or an input
 violates a kernel precondition; there is no silent eager fallback."""
 from .kernels import (  # noqa: F401
     gemm_nt,
+    gemm_tn,
     linear,
     transpose,
     interleave_lastaxis,

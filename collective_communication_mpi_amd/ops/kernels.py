@@ -18,9 +18,16 @@ def _stream(t: torch.Tensor) -> int:
     return torch.cuda.current_stream(t.device).cuda_stream
 
 
+def _auto_splitk(tiles: int, K: int) -> int:
+    """Split K until the grid has ~2 workgroups per CU, keeping >= 4 K-tiles per split."""
+    nk = (K + 63) // 64
+    want = max(1, 512 // max(tiles, 1))
+    return int(max(1, min(want, nk // 4, 32)))
+
+
 def gemm_nt(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None, bias: Optional[torch.Tensor] = None,
             alpha: float = 1.0, accumulate: bool = False, act: Optional[str] = None,
-            out_dtype: torch.dtype = torch.bfloat16) -> torch.Tensor:
+            out_dtype: torch.dtype = torch.bfloat16, splitk: Optional[int] = None) -> torch.Tensor:
     """``out = act(alpha * a @ b.T + bias) (+ out)`` on MFMA (v_mfma_f32_16x16x32_bf16).
 
     a: [M, K] bf16 row-major (row stride may exceed K), b: [N, K] bf16; K % 8 == 0.
@@ -49,9 +56,35 @@ def gemm_nt(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None
         if bias.dtype not in (torch.float32, torch.bfloat16) or not bias.is_contiguous() or bias.numel() != N:
             raise ValueError("bias must be a contiguous [N] fp32/bf16 tensor")
         bias_ptr = bias.data_ptr()
+    if splitk is None:
+        fp32_plain = out.dtype == torch.float32 and act is None
+        splitk = _auto_splitk(((M + 127) // 128) * ((N + 127) // 128), K) if fp32_plain else 1
     _D().gemm_nt(a.data_ptr(), b.data_ptr(), out.data_ptr(), bias_ptr, M, N, K, a.stride(0), b.stride(0),
                  out.stride(0), float(alpha), bool(accumulate), bias_kind, _ACT[act], out.dtype == torch.bfloat16,
-                 _stream(a))
+                 int(splitk), _stream(a))
+    return out
+
+
+def gemm_tn(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None, alpha: float = 1.0,
+            accumulate: bool = False, splitk: Optional[int] = None) -> torch.Tensor:
+    """``out[N1, N2] (+)= alpha * a[M, N1].T @ b[M, N2]`` (weight gradients dW = dY^T X) in fp32,
+    reading both operands M-major through ds_read_b64_tr_b16 (no transposes)."""
+    if a.dtype != torch.bfloat16 or b.dtype != torch.bfloat16:
+        raise TypeError("gemm_tn expects bf16 operands")
+    if a.dim() != 2 or b.dim() != 2 or a.shape[0] != b.shape[0] or a.stride(1) != 1 or b.stride(1) != 1:
+        raise ValueError(f"gemm_tn shape mismatch: {tuple(a.shape)}^T x {tuple(b.shape)}")
+    M, N1 = a.shape
+    N2 = b.shape[1]
+    if out is None:
+        if accumulate:
+            raise ValueError("accumulate needs an output tensor")
+        out = torch.empty((N1, N2), dtype=torch.float32, device=a.device)
+    if out.dtype != torch.float32 or out.shape != (N1, N2) or out.stride(1) != 1:
+        raise ValueError("gemm_tn output must be fp32 [N1, N2] with unit column stride")
+    if splitk is None:
+        splitk = _auto_splitk(((N1 + 127) // 128) * ((N2 + 127) // 128), M)
+    _D().gemm_tn(a.data_ptr(), b.data_ptr(), out.data_ptr(), M, N1, N2, a.stride(0), b.stride(0), out.stride(0),
+                 float(alpha), bool(accumulate), int(splitk), _stream(a))
     return out
 
 

@@ -97,3 +97,41 @@ def test_single_rank_communicator_paths():
     z = torch.empty(3, 1 << 18, device="cuda")
     comm.Allgather(x[: 3 << 18].reshape(3, -1)[0], z[0])
     assert comm.total_bytes_transferred == 0  # p = 1: no traffic in any formula
+
+
+@pytest.mark.parametrize("M,N1,N2", [(64, 16, 128), (32768, 384, 768), (32768, 768, 64), (1000, 136, 72), (7, 8, 8)])
+@pytest.mark.parametrize("splitk", [1, 4, None])
+def test_gemm_tn_weight_grad(M, N1, N2, splitk):
+    from collective_communication_mpi_amd.ops import gemm_tn
+
+    g = torch.Generator(device="cuda").manual_seed(M + N1 + N2)
+    a = torch.randn(M, N1, device="cuda", generator=g).bfloat16()
+    b = torch.randn(M, N2, device="cuda", generator=g).bfloat16()
+    ref = a.float().T @ b.float()
+    out = gemm_tn(a, b, splitk=splitk)
+    torch.testing.assert_close(out, ref, rtol=2e-3, atol=2e-3 * M ** 0.5)
+    acc = torch.ones(N1, N2, device="cuda")
+    gemm_tn(a, b, out=acc, accumulate=True, alpha=0.5, splitk=splitk)
+    torch.testing.assert_close(acc, 1 + 0.5 * ref, rtol=2e-3, atol=2e-3 * M ** 0.5)
+
+
+def test_gemm_tn_asymmetric():
+    """A^T with A = I and asymmetric B catches row/column swaps in the tr-read path."""
+    from collective_communication_mpi_amd.ops import gemm_tn
+
+    n = 128
+    a = torch.eye(n, device="cuda").bfloat16()
+    b = torch.arange(n * n, device="cuda", dtype=torch.float32).reshape(n, n).remainder(89).bfloat16()
+    torch.testing.assert_close(gemm_tn(a, b, splitk=1), b.float())
+    torch.testing.assert_close(gemm_tn(b, a, splitk=1), b.float().T)
+
+
+@pytest.mark.parametrize("splitk", [2, 8])
+def test_gemm_nt_splitk(splitk):
+    from collective_communication_mpi_amd.ops import gemm_nt
+
+    a = torch.randn(256, 4096, device="cuda").bfloat16()
+    b = torch.randn(192, 4096, device="cuda").bfloat16()
+    bias = torch.randn(192, device="cuda")
+    y = gemm_nt(a, b, bias=bias, out_dtype=torch.float32, splitk=splitk)
+    torch.testing.assert_close(y, _ref(a, b, bias), rtol=2e-3, atol=0.15)
