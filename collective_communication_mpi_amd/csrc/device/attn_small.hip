@@ -37,8 +37,13 @@ struct AttnArgs {
   float* lse;           // [B*Hl][S]
   const uint16_t* dout; // [B*S][ld_o]   (bwd)
   uint16_t* dqkv;       // [B*S][ld_qkv] (bwd)
+  float* dbias;         // [3*Hl*D] fp32, += column sums of dqkv (bwd, optional)
   int B, S, Hl, D, ld_qkv, ld_o;
   float scale;
+  uint16_t* pool;       // fwd, optional: [B][ld_pool] bf16 mean over the S rows of O
+  int ld_pool;
+  int dout_bstride;     // bwd: dO row (b, i) at dout + b*dout_bstride + i*dout_rstride + h*D
+  int dout_rstride;     //      (rstride 0 = the pooled-gradient broadcast over the S rows)
 };
 
 // stage an S x D head tile (bf16, row stride ld) into fp32 LDS [S][D+1]
@@ -81,11 +86,31 @@ __global__ void __launch_bounds__(256) k_attn_fwd(AttnArgs a) {
   }
   __syncthreads();
   uint16_t* obase = a.o + (size_t)b * S * a.ld_o + h * D;
+  // pooled output (mean over the S rows) for the pooled row-parallel fc_o; with
+  // blockDim % D == 0 each thread keeps one column, so it sums in registers
+  float* colsum = q;  // q is dead after the scores
+  const bool pool = a.pool != nullptr;
+  if (pool) {
+    for (int c = threadIdx.x; c < D; c += blockDim.x) colsum[c] = 0.f;
+    __syncthreads();
+  }
+  const bool fixed_col = (blockDim.x % D) == 0;
+  float ps = 0.f;
   for (int idx = threadIdx.x; idx < S * D; idx += blockDim.x) {
     const int i = idx / D, d = idx % D;
     float acc = 0.f;
     for (int j = 0; j < S; ++j) acc += P[i * Sp + j] * v[j * Dp + d];
     st_bf16(obase + (size_t)i * a.ld_o + d, acc);
+    if (pool) {
+      if (fixed_col) ps += acc;
+      else atomicAdd(&colsum[d], acc);
+    }
+  }
+  if (pool) {
+    if (fixed_col && threadIdx.x < S * D) atomicAdd(&colsum[threadIdx.x % D], ps);
+    __syncthreads();
+    for (int d = threadIdx.x; d < D; d += blockDim.x)
+      st_bf16(a.pool + (size_t)b * a.ld_pool + h * D + d, colsum[d] / (float)S);
   }
 }
 
@@ -107,7 +132,13 @@ __global__ void __launch_bounds__(256) k_attn_bwd(AttnArgs a) {
   stage(k, base + HD, S, D, a.ld_qkv);
   stage(v, base + 2 * HD, S, D, a.ld_qkv);
   stage(o, a.o + (size_t)b * S * a.ld_o + h * D, S, D, a.ld_o);
-  stage(dO, a.dout + (size_t)b * S * a.ld_o + h * D, S, D, a.ld_o);
+  {  // dO rows may be a broadcast of one pooled-gradient row (rstride 0)
+    const uint16_t* db = a.dout + (size_t)b * a.dout_bstride + h * D;
+    for (int idx = threadIdx.x; idx < S * D; idx += blockDim.x) {
+      const int i = idx / D, d = idx % D;
+      dO[i * Dp + d] = ld_bf16(db + (size_t)i * a.dout_rstride + d);
+    }
+  }
   __syncthreads();
   const float* lse = a.lse + ((size_t)b * a.Hl + h) * S;
   for (int idx = threadIdx.x; idx < S * S; idx += blockDim.x) {
@@ -134,6 +165,13 @@ __global__ void __launch_bounds__(256) k_attn_bwd(AttnArgs a) {
   uint16_t* gq = a.dqkv + (size_t)b * S * a.ld_qkv + h * D;
   uint16_t* gk = gq + HD;
   uint16_t* gv = gq + 2 * HD;
+  float* colsum = delta + S;  // 3*D floats: per-block column sums for the QKV bias gradient
+  for (int c = threadIdx.x; c < 3 * D; c += blockDim.x) colsum[c] = 0.f;
+  __syncthreads();
+  // when blockDim is a multiple of D every thread keeps one column d for all its
+  // rows, so the bias column sums accumulate in registers (one LDS atomic per thread)
+  const bool fixed_col = (blockDim.x % D) == 0;
+  float sq = 0.f, sk = 0.f, sv = 0.f;
   for (int idx = threadIdx.x; idx < S * D; idx += blockDim.x) {
     const int i = idx / D, d = idx % D;  // i: query row for dQ, key row for dK / dV
     float dq = 0.f, dk = 0.f, dv = 0.f;
@@ -142,14 +180,38 @@ __global__ void __launch_bounds__(256) k_attn_bwd(AttnArgs a) {
       dk += dS[j * Sp + i] * q[j * Dp + d];
       dv += P[j * Sp + i] * dO[j * Dp + d];
     }
-    st_bf16(gq + (size_t)i * a.ld_qkv + d, dq * a.scale);
-    st_bf16(gk + (size_t)i * a.ld_qkv + d, dk * a.scale);
+    dq *= a.scale;
+    dk *= a.scale;
+    st_bf16(gq + (size_t)i * a.ld_qkv + d, dq);
+    st_bf16(gk + (size_t)i * a.ld_qkv + d, dk);
     st_bf16(gv + (size_t)i * a.ld_qkv + d, dv);
+    if (a.dbias) {
+      if (fixed_col) {
+        sq += dq; sk += dk; sv += dv;
+      } else {
+        atomicAdd(&colsum[d], dq);
+        atomicAdd(&colsum[D + d], dk);
+        atomicAdd(&colsum[2 * D + d], dv);
+      }
+    }
+  }
+  if (a.dbias && fixed_col && threadIdx.x < S * D) {
+    const int d = threadIdx.x % D;
+    atomicAdd(&colsum[d], sq);
+    atomicAdd(&colsum[D + d], sk);
+    atomicAdd(&colsum[2 * D + d], sv);
+  }
+  if (a.dbias) {
+    __syncthreads();
+    for (int c = threadIdx.x; c < 3 * D; c += blockDim.x) {
+      const int part = c / D, d = c % D;
+      atomicAdd(a.dbias + part * HD + h * D + d, colsum[c]);
+    }
   }
 }
 
 size_t fwd_lds(int S, int D) { return sizeof(float) * (3 * S * (D + 1) + S * (S + 1)); }
-size_t bwd_lds(int S, int D) { return sizeof(float) * (5 * S * (D + 1) + 2 * S * (S + 1) + S); }
+size_t bwd_lds(int S, int D) { return sizeof(float) * (5 * S * (D + 1) + 2 * S * (S + 1) + S + 3 * D); }
 
 void check_dims(int S, int D, bool bwd) {
   if (S < 1 || S > 64 || D < 1 || D > 256) throw std::invalid_argument("attn_small: need 1 <= S <= 64, D <= 256");
@@ -157,18 +219,19 @@ void check_dims(int S, int D, bool bwd) {
 }
 
 void attn_fwd(uint64_t qkv, uint64_t o, uint64_t lse, int B, int S, int Hl, int D, int ld_qkv, int ld_o, float scale,
-              uint64_t stream) {
+              uint64_t pool, int ld_pool, uint64_t stream) {
   check_dims(S, D, false);
-  AttnArgs a{(const uint16_t*)qkv, (uint16_t*)o, (float*)lse, nullptr, nullptr, B, S, Hl, D, ld_qkv, ld_o, scale};
+  AttnArgs a{(const uint16_t*)qkv, (uint16_t*)o, (float*)lse, nullptr, nullptr, nullptr, B, S, Hl, D, ld_qkv, ld_o, scale,
+             (uint16_t*)pool, ld_pool, 0, 0};
   hipLaunchKernelGGL(k_attn_fwd, dim3(B * Hl), dim3(256), fwd_lds(S, D), (hipStream_t)stream, a);
   CCMPI_HIP_CHECK(hipGetLastError());
 }
 
-void attn_bwd(uint64_t qkv, uint64_t o, uint64_t lse, uint64_t dout, uint64_t dqkv, int B, int S, int Hl, int D,
-              int ld_qkv, int ld_o, float scale, uint64_t stream) {
+void attn_bwd(uint64_t qkv, uint64_t o, uint64_t lse, uint64_t dout, uint64_t dqkv, uint64_t dbias, int B, int S,
+              int Hl, int D, int ld_qkv, int ld_o, float scale, int dout_bstride, int dout_rstride, uint64_t stream) {
   check_dims(S, D, true);
-  AttnArgs a{(const uint16_t*)qkv, (uint16_t*)o, (float*)lse, (const uint16_t*)dout, (uint16_t*)dqkv,
-             B, S, Hl, D, ld_qkv, ld_o, scale};
+  AttnArgs a{(const uint16_t*)qkv, (uint16_t*)o, (float*)lse, (const uint16_t*)dout, (uint16_t*)dqkv, (float*)dbias,
+             B, S, Hl, D, ld_qkv, ld_o, scale, nullptr, 0, dout_bstride, dout_rstride};
   hipLaunchKernelGGL(k_attn_bwd, dim3(B * Hl), dim3(256), bwd_lds(S, D), (hipStream_t)stream, a);
   CCMPI_HIP_CHECK(hipGetLastError());
 }
@@ -192,6 +255,42 @@ __global__ void __launch_bounds__(256) k_adamw(float* __restrict__ p, const floa
     p[i] = pi;
     if (p16) p16[i] = (uint16_t)f32_to_bf16_bits(pi);
   }
+}
+
+// MNIST patchify: x[B][img*img] fp32 -> xp[B*S][kp] bf16 with, per token row,
+// the patch pixels (p*p), a constant 1 (folds the embedding bias into the
+// GEMM) and a one-hot position (folds the learned position embedding into the
+// GEMM), zero-padded to kp.  One thread per output element.
+__global__ void __launch_bounds__(256) k_patchify(const float* __restrict__ x, uint16_t* __restrict__ xp, int B, int img,
+                                                  int p, int kp) {
+  const int g = img / p, S = g * g, pp = p * p;
+  const uint64_t total = (uint64_t)B * S * kp;
+  for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (uint64_t)gridDim.x * blockDim.x) {
+    const int c = (int)(e % kp);
+    const uint64_t row = e / kp;
+    const int s = (int)(row % S);
+    const uint64_t b = row / S;
+    float v = 0.f;
+    if (c < pp) {
+      const int py = (s / g) * p + c / p, px = (s % g) * p + c % p;
+      v = x[b * img * img + py * img + px];
+    } else if (c == pp) {
+      v = 1.f;
+    } else if (c == pp + 1 + s) {
+      v = 1.f;
+    }
+    xp[e] = (uint16_t)f32_to_bf16_bits(v);
+  }
+}
+
+void patchify(uint64_t x, uint64_t xp, int B, int img, int p, int kp, uint64_t stream) {
+  const int S = (img / p) * (img / p);
+  if (kp < p * p + 1 + S) throw std::invalid_argument("patchify: kp too small for pixels + bias + position columns");
+  const uint64_t total = (uint64_t)B * S * kp;
+  const int grid = (int)std::min<uint64_t>((total + 255) / 256, 4096);
+  hipLaunchKernelGGL(k_patchify, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const float*)x, (uint16_t*)xp, B, img,
+                     p, kp);
+  CCMPI_HIP_CHECK(hipGetLastError());
 }
 
 __global__ void __launch_bounds__(256) k_cast_bf16(const float* __restrict__ x, uint16_t* __restrict__ y, uint64_t n) {
@@ -222,6 +321,7 @@ void register_attn_ops(pybind11::module_& m) {
   m.def("attn_small_bwd", &attn_bwd, py::call_guard<py::gil_scoped_release>());
   m.def("adamw_step", &adamw, py::call_guard<py::gil_scoped_release>());
   m.def("cast_bf16", &cast_bf16, py::call_guard<py::gil_scoped_release>());
+  m.def("patchify", &patchify, py::call_guard<py::gil_scoped_release>());
 }
 
 }  // namespace dev

@@ -15,6 +15,7 @@ PYBIND11_MODULE(_device, m) {
   m.attr("ALGO_ONESHOT") = (int)ALGO_ONESHOT;
   m.attr("ALGO_TWOSHOT") = (int)ALGO_TWOSHOT;
   m.attr("ALGO_REDUCE_BCAST") = (int)ALGO_REDUCE_BCAST;
+  m.attr("ALGO_TWOSHOT_PUSH") = (int)ALGO_TWOSHOT_PUSH;
   m.attr("MAX_RANKS") = kMaxRanks;
   m.attr("MAX_BLOCKS") = kMaxBlocks;
   m.def("reduce_supported", &device_reduce_supported);
@@ -45,6 +46,8 @@ PYBIND11_MODULE(_device, m) {
       .def("alltoall", &DeviceComm::alltoall, py::call_guard<py::gil_scoped_release>())
       .def("bcast", &DeviceComm::bcast, py::call_guard<py::gil_scoped_release>())
       .def("local_reduce", &DeviceComm::local_reduce, py::call_guard<py::gil_scoped_release>())
+      .def("allgather_lastaxis", &DeviceComm::allgather_lastaxis, py::call_guard<py::gil_scoped_release>())
+      .def("reduce_scatter_lastaxis", &DeviceComm::reduce_scatter_lastaxis, py::call_guard<py::gil_scoped_release>())
       .def("rccl_init", [](DeviceComm& d, py::bytes uid) {
         std::string u = uid;
         py::gil_scoped_release g;
@@ -61,6 +64,9 @@ PYBIND11_MODULE(_device, m) {
       .def("p2p_pairwise_alltoall", &DeviceComm::p2p_pairwise_alltoall, py::call_guard<py::gil_scoped_release>())
       .def("error_code", &DeviceComm::error_code, py::call_guard<py::gil_scoped_release>())
       .def("clear_error", &DeviceComm::clear_error)
+      .def("reset_state", &DeviceComm::reset_state, py::call_guard<py::gil_scoped_release>())
+      .def("set_inbox", &DeviceComm::set_inbox)
+      .def_property_readonly("inbox_bytes", &DeviceComm::inbox_bytes)
       .def("set_timeout_seconds", &DeviceComm::set_timeout_seconds)
       .def("set_copy_engine", &DeviceComm::set_copy_engine);
 

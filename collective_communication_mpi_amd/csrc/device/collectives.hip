@@ -261,6 +261,60 @@ __device__ void gather_spans(const char* const* srcs, char* const* dsts, int nr,
   }
 }
 
+
+// Reduce `nr` slots at base + j*stride (this rank's memory) and store the
+// result into every outs[j] (local or peer-mapped).
+template <int DT, int OP, int NRM>
+__device__ void reduce_fanout(const char* base, uint64_t stride, int nr, uint64_t len, char* const* outs) {
+  const uint64_t vbytes = len & ~15ull;
+  const uint64_t kWin = 1ull << 30;
+  for (uint64_t w = 0; w < vbytes; w += kWin) {
+    const uint32_t wl = (uint32_t)min(kWin, vbytes - w);
+    Rsrc src[NRM], dst[NRM];
+#pragma unroll
+    for (int j = 0; j < NRM; ++j) {
+      if (j < nr) {
+        src[j] = make_rsrc(uniform_ptr(const_cast<char*>(base) + j * stride + w), wl);
+        dst[j] = make_rsrc(uniform_ptr(outs[j] + w), wl);
+      }
+    }
+    const uint32_t nv = wl / 16;
+    for (uint32_t v = threadIdx.x; v < nv; v += kThreads * kUnroll) {
+      u32x4 x[kUnroll][NRM];
+#pragma unroll
+      for (int j = 0; j < NRM; ++j)
+        if (j < nr)
+#pragma unroll
+          for (int u = 0; u < kUnroll; ++u)
+            if (v + u * kThreads < nv) x[u][j] = ld16(src[j], (v + u * kThreads) * 16);
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u) {
+        if (v + u * kThreads < nv) {
+          VecAcc<DT> acc;
+          acc.load(x[u][0]);
+#pragma unroll
+          for (int j = 1; j < NRM; ++j)
+            if (j < nr) acc.template acc<OP>(x[u][j]);
+          const u32x4 r = acc.store();
+#pragma unroll
+          for (int j = 0; j < NRM; ++j)
+            if (j < nr) st16(dst[j], (v + u * kThreads) * 16, r);
+        }
+      }
+    }
+  }
+  const uint64_t tail = len - vbytes;
+  if (tail && threadIdx.x == 0) {
+    using E = Elem<DT>;
+    for (uint32_t o = 0; o < tail; o += E::B) {
+      typename E::A acc = E::ld(make_rsrc(const_cast<char*>(base) + vbytes, (uint32_t)tail), o);
+      for (int j = 1; j < nr; ++j)
+        acc = apply_op<OP>(acc, E::ld(make_rsrc(const_cast<char*>(base) + j * stride + vbytes, (uint32_t)tail), o));
+      for (int j = 0; j < nr; ++j) E::st(make_rsrc(outs[j] + vbytes, (uint32_t)tail), o, acc);
+    }
+  }
+}
+
 // Element-aligned partition of `nbytes` into `parts` pieces whose boundaries
 // are multiples of 16 B (except the end).
 __device__ __forceinline__ BlockRange part16(uint64_t nbytes, int parts, int idx) {
@@ -334,6 +388,58 @@ __global__ void __launch_bounds__(kThreads) k_allreduce_twoshot(CollArgs a) {
   finish(a, e);
 }
 
+
+// Push two-shot: phase 1 writes my slice of shard j into rank j's inbox slot
+// [me] (remote 16-B sc0|sc1 stores: posted writes, no round trip); after the
+// phase flag, rank j reduces its p inbox slots (local reads, rank order) and
+// writes the reduced slice into EVERY rank's output (the all-gather is pushed
+// too).  Same bytes on the wire as the pull form; which one a fabric prefers
+// is measured at run time (bench/autotune candidates).
+template <int DT, int OP, int NRM>
+__global__ void __launch_bounds__(kThreads) k_allreduce_twoshot_push(CollArgs a) {
+  __shared__ uint64_t s_epoch;
+  __shared__ uint64_t codes[2][kMaxRanks];
+  if (!start_phase(a, &s_epoch, codes)) return;
+  const uint64_t e = s_epoch;
+  const PeerTable* pt = a.pt;
+  const int me = pt->rank, nr = pt->size;
+  const char* src = resolve(pt, me, a.src_code);
+  const uint64_t shard = (((a.nbytes + nr - 1) / nr) + 15) / 16 * 16;  // inbox slot stride
+  // ---- phase 1: scatter my input shards into the owners' inboxes
+  {
+    __shared__ char* dsts[kMaxRanks];
+    __shared__ const char* srcs[kMaxRanks];
+    __shared__ uint64_t lens[kMaxRanks];
+    if (threadIdx.x < nr) {
+      const int j = threadIdx.x;
+      BlockRange sj = part16(a.nbytes, nr, j);
+      BlockRange bj = part16(sj.hi - sj.lo, gridDim.x, blockIdx.x);
+      srcs[j] = src + sj.lo + bj.lo;
+      dsts[j] = resolve(pt, j, a.aux_code) + (uint64_t)me * shard + bj.lo;
+      lens[j] = bj.hi - bj.lo;
+    }
+    __syncthreads();
+    uint64_t common = lens[0];
+    for (int j = 1; j < nr; ++j) common = min(common, lens[j]);
+    if (common) gather_spans<NRM>(srcs, dsts, nr, -1, common);
+    for (int j = 0; j < nr; ++j)
+      if (lens[j] > common) copy_span(srcs[j] + common, dsts[j] + common, lens[j] - common);
+  }
+  if (!sync_phase(a, 1, e)) return;
+  // ---- phase 2: reduce my inbox slots (rank order), store the result slice into
+  //      every rank's output directly (local + 7 remote posted writes)
+  BlockRange mys = part16(a.nbytes, nr, me);
+  BlockRange sub = part16(mys.hi - mys.lo, gridDim.x, blockIdx.x);
+  if (sub.hi > sub.lo) {
+    __shared__ char* outs[kMaxRanks];
+    if (threadIdx.x < nr) outs[threadIdx.x] = resolve(pt, threadIdx.x, codes[1][threadIdx.x]) + mys.lo + sub.lo;
+    __syncthreads();
+    reduce_fanout<DT, OP, NRM>(resolve(pt, me, a.aux_code) + sub.lo, shard, nr, sub.hi - sub.lo, outs);
+  }
+  if (!sync_phase(a, 3, e)) return;
+  finish(a, e);
+}
+
 // Reference algorithm (mpi_wrapper/comm.py:63-107): the root reduces every
 // rank's buffer in rank order, then every other rank copies the root's result.
 template <int DT, int OP, int NRM>
@@ -397,6 +503,59 @@ __global__ void __launch_bounds__(kThreads) k_move(CollArgs a) {
       }
       __syncthreads();
       gather_spans<NRM>(srcs, dsts, nr, -1, r.hi - r.lo);
+    }
+  }
+  if (!sync_phase(a, 3, e)) return;
+  finish(a, e);
+}
+
+
+// Last-axis collectives for tensor parallelism (fused layout transform):
+//   MODE 0 all-gather : out[m][j*k + c] = in_j[m][c]                (M x k shards -> M x p*k)
+//   MODE 1 reduce-scat: out[m][c] = sum_j in_j[m][me*k + c]          (M x p*k      -> M x k)
+// The (row, 16-B vector) index space is flattened so short rows still keep
+// every lane busy; every peer's vector is loaded before any is used.
+// Requires k * elem_size % 16 == 0 (checked on the host).
+template <int MODE, int DT, int OP, int NRM>
+__global__ void __launch_bounds__(kThreads) k_lastaxis(CollArgs a) {
+  __shared__ uint64_t s_epoch;
+  __shared__ uint64_t codes[2][kMaxRanks];
+  if (!start_phase(a, &s_epoch, codes)) return;
+  const uint64_t e = s_epoch;
+  const PeerTable* pt = a.pt;
+  const int me = pt->rank, nr = pt->size;
+  const uint64_t rowv = a.nbytes / 16;        // vectors per k-row (nbytes = k * elem)
+  const uint64_t rows = (uint64_t)a.root;     // M (passed in `root`)
+  const uint64_t total = rows * rowv;
+  BlockRange r = split_range(total, gridDim.x, blockIdx.x);
+  __shared__ const char* base[kMaxRanks];
+  if (threadIdx.x < nr) base[threadIdx.x] = resolve(pt, threadIdx.x, codes[0][threadIdx.x]);
+  __syncthreads();
+  // one descriptor per peer (uniform base, per-lane 32-bit offsets: host checks < 4 GiB)
+  Rsrc src[NRM];
+#pragma unroll
+  for (int j = 0; j < NRM; ++j)
+    if (j < nr) src[j] = make_rsrc(uniform_ptr(const_cast<char*>(base[j])), 0xFFFFFFF0u);
+  for (uint64_t idx = r.lo + threadIdx.x; idx < r.hi; idx += kThreads) {
+    const uint64_t m = idx / rowv, v = idx % rowv;
+    u32x4 x[NRM];
+    if (MODE == 0) {
+#pragma unroll
+      for (int j = 0; j < NRM; ++j)
+        if (j < nr) x[j] = ld16(src[j], (uint32_t)((m * rowv + v) * 16));
+#pragma unroll
+      for (int j = 0; j < NRM; ++j)
+        if (j < nr) *reinterpret_cast<u32x4*>(a.out + ((m * nr + j) * rowv + v) * 16) = x[j];
+    } else {
+#pragma unroll
+      for (int j = 0; j < NRM; ++j)
+        if (j < nr) x[j] = ld16(src[j], (uint32_t)(((m * nr + me) * rowv + v) * 16));
+      VecAcc<DT> acc;
+      acc.load(x[0]);
+#pragma unroll
+      for (int j = 1; j < NRM; ++j)
+        if (j < nr) acc.template acc<OP>(x[j]);
+      *reinterpret_cast<u32x4*>(a.out + (m * rowv + v) * 16) = acc.store();
     }
   }
   if (!sync_phase(a, 3, e)) return;
@@ -486,6 +645,7 @@ void launch_allreduce(int algo, const CollArgs& a, int nranks, int dtype, int op
         case ALGO_ONESHOT: hipLaunchKernelGGL((k_allreduce_oneshot<D, O, R>), dim3(grid), dim3(kThreads), 0, s, a); break;
         case ALGO_TWOSHOT: hipLaunchKernelGGL((k_allreduce_twoshot<D, O, R>), dim3(grid), dim3(kThreads), 0, s, a); break;
         case ALGO_REDUCE_BCAST: hipLaunchKernelGGL((k_allreduce_reduce_bcast<D, O, R>), dim3(grid), dim3(kThreads), 0, s, a); break;
+        case ALGO_TWOSHOT_PUSH: hipLaunchKernelGGL((k_allreduce_twoshot_push<D, O, R>), dim3(grid), dim3(kThreads), 0, s, a); break;
         default: throw std::invalid_argument("ccmpi: bad allreduce algo");
       }
     });
@@ -498,6 +658,19 @@ void launch_reduce_scatter(const CollArgs& a, int nranks, int dtype, int op, int
     dispatch_dt_op(dtype, op, [&]<int D, int O>() {
       hipLaunchKernelGGL((k_reduce_scatter<D, O, R>), dim3(grid), dim3(kThreads), 0, s, a);
     });
+  });
+  CCMPI_HIP_CHECK(hipGetLastError());
+}
+
+void launch_lastaxis(int mode, const CollArgs& a, int nranks, int dtype, int op, int grid, hipStream_t s) {
+  with_nrm(nranks, [&]<int R>() {
+    if (mode == 0) {
+      hipLaunchKernelGGL((k_lastaxis<0, DT_F32, OP_SUM, R>), dim3(grid), dim3(kThreads), 0, s, a);
+    } else {
+      dispatch_dt_op(dtype, op, [&]<int D, int O>() {
+        hipLaunchKernelGGL((k_lastaxis<1, D, O, R>), dim3(grid), dim3(kThreads), 0, s, a);
+      });
+    }
   });
   CCMPI_HIP_CHECK(hipGetLastError());
 }

@@ -13,6 +13,7 @@ enum AllreduceAlgo : int {
   ALGO_ONESHOT = 0,       // every rank reads everything (small messages)
   ALGO_TWOSHOT = 1,       // reduce-scatter + all-gather over all links (large)
   ALGO_REDUCE_BCAST = 2,  // reference algorithm: reduce to root, broadcast
+  ALGO_TWOSHOT_PUSH = 3,  // two-shot with remote writes (scatter into peers' inboxes, push results)
 };
 
 enum MoveMode : int { MOVE_ALLGATHER = 0, MOVE_ALLTOALL = 1, MOVE_BCAST = 2 };
@@ -27,6 +28,7 @@ struct CollArgs {
   uint64_t timeout_ticks;  // bounded spins, 100 MHz ticks
   int root;
   int pad;
+  uint64_t aux_code;       // symmetric inbox (push two-shot): same code on every rank
 };
 
 struct LocalReduceArgs {
@@ -42,6 +44,8 @@ void launch_copy(const void* src, void* dst, uint64_t nbytes, hipStream_t s);
 void launch_allreduce(int algo, const CollArgs& a, int nranks, int dtype, int op, int grid, hipStream_t s);
 void launch_reduce_scatter(const CollArgs& a, int nranks, int dtype, int op, int grid, hipStream_t s);
 void launch_move(int mode, const CollArgs& a, int nranks, int grid, hipStream_t s);
+// mode 0: last-axis all-gather, 1: last-axis reduce-scatter; rows passed in CollArgs::root
+void launch_lastaxis(int mode, const CollArgs& a, int nranks, int dtype, int op, int grid, hipStream_t s);
 void launch_local_reduce(const LocalReduceArgs& a, int dtype, int op, hipStream_t s);
 
 }  // namespace dev

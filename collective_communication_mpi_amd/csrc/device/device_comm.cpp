@@ -217,6 +217,19 @@ void DeviceComm::allreduce(uint64_t in, uint64_t out, uint64_t count, int dtype,
     }
     return;
   }
+  if (algo == ALGO_TWOSHOT_PUSH) {
+    // needs registered in/out and an inbox of p shards; otherwise the pull form
+    const uint64_t shard = ((nbytes + size_ - 1) / size_ + 15) / 16 * 16;
+    const uint64_t ic = inbox_ptr_ ? code_of_(inbox_ptr_, inbox_bytes_) : 0;
+    uint64_t sc = code_of_(in, nbytes), rc = code_of_(out, nbytes);
+    if (symmetric && sc && rc && ic && in != out && inbox_bytes_ >= shard * size_) {
+      CollArgs a = args_(sc, rc, (char*)out, nbytes, 0);
+      a.aux_code = ic;
+      launch_allreduce(ALGO_TWOSHOT_PUSH, a, size_, dtype, op, grid_(nbytes / size_, max_blocks), st);
+      return;
+    }
+    algo = ALGO_TWOSHOT;
+  }
   const bool needs_res = algo != ALGO_ONESHOT;
   if (symmetric && !(algo == ALGO_ONESHOT && in == out)) {
     uint64_t sc = code_of_(in, nbytes), rc = needs_res ? code_of_(out, nbytes) : 0;
@@ -379,6 +392,46 @@ void DeviceComm::bcast(uint64_t buf, uint64_t nbytes, int root, uint64_t stream,
     if (!out_ok && rank_ != root)
       CCMPI_HIP_CHECK(hipMemcpyAsync((void*)(buf + off), dst, n, hipMemcpyDeviceToDevice, st));
   }
+}
+
+void DeviceComm::allgather_lastaxis(uint64_t in, uint64_t out, uint64_t rows, uint64_t row_bytes, uint64_t stream,
+                                    int max_blocks, bool symmetric) {
+  if (rows == 0 || row_bytes == 0) return;
+  if (row_bytes % 16 || out % 16) throw std::invalid_argument("ccmpi: last-axis all-gather needs 16-B rows/output");
+  const uint64_t nbytes = rows * row_bytes;
+  if (nbytes * size_ >= 0xFFFFFFF0ull) throw std::invalid_argument("ccmpi: last-axis all-gather > 4 GiB");
+  CCMPI_HIP_CHECK(hipSetDevice(device_));
+  hipStream_t st = S(stream);
+  uint64_t sc = code_of_(in, nbytes);
+  if (!sc) {
+    if (symmetric) throw std::invalid_argument("ccmpi: symmetric last-axis all-gather needs a registered input");
+    if (nbytes > scratch_bytes()) throw std::runtime_error("ccmpi: last-axis all-gather input exceeds scratch");
+    CCMPI_HIP_CHECK(hipMemcpyAsync(reinterpret_cast<void*>(scratch_ptr()), (void*)in, nbytes, hipMemcpyDeviceToDevice, st));
+    sc = addr_code(0, 0);
+  }
+  CollArgs a = args_(sc, 0, (char*)out, row_bytes, (int)rows);
+  launch_lastaxis(0, a, size_, DT_F32, OP_SUM, grid_(nbytes * size_, max_blocks), st);
+}
+
+void DeviceComm::reduce_scatter_lastaxis(uint64_t in, uint64_t out, uint64_t rows, uint64_t k, int dtype, int op,
+                                         uint64_t stream, int max_blocks, bool symmetric) {
+  const uint64_t es = dtype_bytes(dtype), row_bytes = k * es;
+  if (rows == 0 || k == 0) return;
+  if (!device_reduce_supported(dtype, op)) throw std::invalid_argument("ccmpi: unsupported device reduction");
+  if (row_bytes % 16 || out % 16) throw std::invalid_argument("ccmpi: last-axis reduce-scatter needs 16-B rows/output");
+  const uint64_t nbytes = rows * row_bytes * size_;
+  if (nbytes >= 0xFFFFFFF0ull) throw std::invalid_argument("ccmpi: last-axis reduce-scatter > 4 GiB");
+  CCMPI_HIP_CHECK(hipSetDevice(device_));
+  hipStream_t st = S(stream);
+  uint64_t sc = code_of_(in, nbytes);
+  if (!sc) {
+    if (symmetric) throw std::invalid_argument("ccmpi: symmetric last-axis reduce-scatter needs a registered input");
+    if (nbytes > scratch_bytes()) throw std::runtime_error("ccmpi: last-axis reduce-scatter input exceeds scratch");
+    CCMPI_HIP_CHECK(hipMemcpyAsync(reinterpret_cast<void*>(scratch_ptr()), (void*)in, nbytes, hipMemcpyDeviceToDevice, st));
+    sc = addr_code(0, 0);
+  }
+  CollArgs a = args_(sc, 0, (char*)out, row_bytes, (int)rows);
+  launch_lastaxis(1, a, size_, dtype, op, grid_(rows * row_bytes, max_blocks), st);
 }
 
 void DeviceComm::local_reduce(const std::vector<uint64_t>& ins, uint64_t out, uint64_t count, int dtype, int op,
@@ -594,6 +647,21 @@ uint32_t DeviceComm::error_code() {
   uint32_t e = 0;
   CCMPI_HIP_CHECK(hipMemcpy(&e, &sig_->error, sizeof(e), hipMemcpyDeviceToHost));
   return e;
+}
+
+void DeviceComm::set_inbox(uint64_t ptr, uint64_t bytes) {
+  if (ptr && (ptr % 16 || find(ptr, bytes, nullptr) <= 0))
+    throw std::invalid_argument("ccmpi: the push inbox must be an aligned symmetric allocation");
+  inbox_ptr_ = ptr;
+  inbox_bytes_ = bytes;
+}
+
+void DeviceComm::reset_state() {
+  CCMPI_HIP_CHECK(hipSetDevice(device_));
+  CCMPI_HIP_CHECK(hipDeviceSynchronize());
+  CCMPI_HIP_CHECK(hipMemset(sig_, 0, sizeof(Signals)));
+  CCMPI_HIP_CHECK(hipMemset(epochs_, 0, sizeof(uint64_t) * kMaxBlocks));
+  CCMPI_HIP_CHECK(hipDeviceSynchronize());
 }
 
 void DeviceComm::clear_error() {

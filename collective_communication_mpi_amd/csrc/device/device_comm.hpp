@@ -66,6 +66,11 @@ class DeviceComm {
   void bcast(uint64_t buf, uint64_t nbytes, int root, uint64_t stream, int max_blocks, bool symmetric);
   void local_reduce(const std::vector<uint64_t>& ins, uint64_t out, uint64_t count, int dtype, int op,
                     uint64_t stream);
+  // TP layout-fused collectives: rows x k shards <-> rows x p*k (last axis)
+  void allgather_lastaxis(uint64_t in, uint64_t out, uint64_t rows, uint64_t row_bytes, uint64_t stream,
+                          int max_blocks, bool symmetric);
+  void reduce_scatter_lastaxis(uint64_t in, uint64_t out, uint64_t rows, uint64_t k, int dtype, int op,
+                               uint64_t stream, int max_blocks, bool symmetric);
 
   // ---- RCCL (vendor library: baseline + P2P transport) ---------------------
   static std::string rccl_unique_id();
@@ -87,6 +92,11 @@ class DeviceComm {
   // ---- health ------------------------------------------------------------
   uint32_t error_code();  // synchronises; 0 = ok
   void clear_error();
+  // zero flags + epochs (call on every rank between host barriers, no kernel in flight)
+  void reset_state();
+  // symmetric inbox for the push two-shot all-reduce (>= p shards)
+  void set_inbox(uint64_t ptr, uint64_t bytes);
+  uint64_t inbox_bytes() const { return inbox_bytes_; }
   uint64_t timeout_ticks() const { return timeout_ticks_; }
   void set_timeout_seconds(double s) { timeout_ticks_ = (uint64_t)(s * 1e8); }
   void set_copy_engine(bool on) { copy_engine_ = on; }
@@ -107,6 +117,7 @@ class DeviceComm {
   uint64_t* epochs_ = nullptr;
   uint64_t timeout_ticks_ = 2000000000ull;  // 20 s
   ncclComm_t nccl_ = nullptr;
+  uint64_t inbox_ptr_ = 0, inbox_bytes_ = 0;
   bool copy_engine_ = true;               // single-rank copies: runtime blit (measured faster than k_copy)
   std::vector<std::string> opened_;      // handles we opened (for release)
 };

@@ -55,8 +55,115 @@ __device__ __forceinline__ float gelu_tanh(float x) {
   return 0.5f * x * (1.f + tanhf(k0 * (x + k1 * x * x * x)));
 }
 
+// Shared epilogue of both GEMM kernels (see the comment inside).
+__device__ __forceinline__ void store_tile(const GemmArgs& g, floatx4 (&acc)[4][4], unsigned char* smem, int bm,
+                                           int bn, int wm, int wn, int split, int t, int lane) {
+  // epilogue: lane holds D[4*(lane>>4) + r][lane & 15] of each 16x16 tile.
+  // Stage the (alpha, bias, act)-applied fp32 tile through LDS (the A/B
+  // buffers are dead now), then write whole rows with 16-B vectors (or, for
+  // split-K, lane-consecutive fp32 atomics: 256 contiguous bytes per wave
+  // instruction).  Falls back to per-element stores when C rows are not
+  // 16-B aligned.
+  float* tile = reinterpret_cast<float*>(smem);
+  constexpr int TS = BN + 4;  // fp32 row stride in LDS
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int cl = wn + j * 16 + (lane & 15);
+    const int col = bn + cl;
+    float b = 0.f;
+    if (split == 0 && col < g.N) {
+      if (g.bias_kind == 1) b = reinterpret_cast<const float*>(g.bias)[col];
+      else if (g.bias_kind == 2) b = bf2f(reinterpret_cast<const uint16_t*>(g.bias)[col]);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int rl = wm + i * 16 + (lane >> 4) * 4 + r;
+        float v = g.alpha * acc[i][j][r] + b;
+        if (g.act == 1) v = fmaxf(v, 0.f);
+        else if (g.act == 2) v = gelu_tanh(v);
+        tile[rl * TS + cl] = v;
+      }
+    }
+  }
+  __syncthreads();
+  const int es = g.out_bf16 ? 2 : 4;
+  const bool vec_ok = (((uint64_t)g.C | ((uint64_t)g.ldc * es)) % 16) == 0;
+  if (g.splitk > 1) {
+    // 64 lanes -> 64 consecutive columns of one row
+    for (int idx = t; idx < BM * BN; idx += NT) {
+      const int rl = idx / BN, cl = idx % BN;
+      const int row = bm + rl, col = bn + cl;
+      if (row < g.M && col < g.N) atomicAdd(reinterpret_cast<float*>(g.C) + (size_t)row * g.ldc + col, tile[rl * TS + cl]);
+    }
+  } else if (vec_ok) {
+    const int per_vec = 16 / es;             // elements per 16-B vector
+    const int vecs_row = BN / per_vec;
+    for (int idx = t; idx < BM * vecs_row; idx += NT) {
+      const int rl = idx / vecs_row, cl = (idx % vecs_row) * per_vec;
+      const int row = bm + rl, col = bn + cl;
+      if (row >= g.M || col >= g.N) continue;
+      const float* src = tile + rl * TS + cl;
+      if (col + per_vec <= g.N) {
+        if (g.out_bf16) {
+          uint16_t* C = reinterpret_cast<uint16_t*>(g.C) + (size_t)row * g.ldc + col;
+          uint4 o;
+          uint32_t w[4];
+          if (g.accumulate) {
+            const uint4 old = *reinterpret_cast<const uint4*>(C);
+            const uint32_t ow[4] = {old.x, old.y, old.z, old.w};
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+              w[q] = f32_to_bf16_bits(src[2 * q] + bf16_lo(ow[q])) | (f32_to_bf16_bits(src[2 * q + 1] + bf16_hi(ow[q])) << 16);
+          } else {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) w[q] = f32_to_bf16_bits(src[2 * q]) | (f32_to_bf16_bits(src[2 * q + 1]) << 16);
+          }
+          o.x = w[0]; o.y = w[1]; o.z = w[2]; o.w = w[3];
+          *reinterpret_cast<uint4*>(C) = o;
+        } else {
+          float* C = reinterpret_cast<float*>(g.C) + (size_t)row * g.ldc + col;
+          float4 v = make_float4(src[0], src[1], src[2], src[3]);
+          if (g.accumulate) {
+            const float4 old = *reinterpret_cast<const float4*>(C);
+            v.x += old.x; v.y += old.y; v.z += old.z; v.w += old.w;
+          }
+          *reinterpret_cast<float4*>(C) = v;
+        }
+      } else {
+        for (int q = 0; q < per_vec && col + q < g.N; ++q) {
+          const size_t o = (size_t)row * g.ldc + col + q;
+          if (g.out_bf16) {
+            uint16_t* C = reinterpret_cast<uint16_t*>(g.C);
+            C[o] = (uint16_t)f32_to_bf16_bits(src[q] + (g.accumulate ? bf2f(C[o]) : 0.f));
+          } else {
+            float* C = reinterpret_cast<float*>(g.C);
+            C[o] = src[q] + (g.accumulate ? C[o] : 0.f);
+          }
+        }
+      }
+    }
+  } else {
+    for (int idx = t; idx < BM * BN; idx += NT) {
+      const int rl = idx / BN, cl = idx % BN;
+      const int row = bm + rl, col = bn + cl;
+      if (row >= g.M || col >= g.N) continue;
+      const size_t o = (size_t)row * g.ldc + col;
+      const float v = tile[rl * TS + cl];
+      if (g.out_bf16) {
+        uint16_t* C = reinterpret_cast<uint16_t*>(g.C);
+        C[o] = (uint16_t)f32_to_bf16_bits(v + (g.accumulate ? bf2f(C[o]) : 0.f));
+      } else {
+        float* C = reinterpret_cast<float*>(g.C);
+        C[o] = v + (g.accumulate ? C[o] : 0.f);
+      }
+    }
+  }
+}
+
 __global__ void __launch_bounds__(NT) k_gemm_nt(GemmArgs g) {
-  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * (BM + BN) * kRowBytes];
+  __shared__ __attribute__((aligned(16))) unsigned char smem[(2 * (BM + BN) * kRowBytes > BM * (BN + 4) * 4) ? 2 * (BM + BN) * kRowBytes : BM * (BN + 4) * 4];
   const int tiles_n = (g.N + BN - 1) / BN, tiles_m = (g.M + BM - 1) / BM;
   const int nwg = tiles_n * tiles_m * g.splitk;
   // bijective XCD-aware remap: blocks b, b+8, b+16, ... (same XCD) get consecutive ids;
@@ -135,44 +242,9 @@ __global__ void __launch_bounds__(NT) k_gemm_nt(GemmArgs g) {
     __syncthreads();
   }
 
-  // epilogue: lane holds D[4*(lane>>4) + r][lane & 15] of each 16x16 tile
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int col = bn + wn + j * 16 + (lane & 15);
-    if (col >= g.N) continue;
-    float b = 0.f;
-    if (split == 0) {
-      if (g.bias_kind == 1) b = reinterpret_cast<const float*>(g.bias)[col];
-      else if (g.bias_kind == 2) b = bf2f(reinterpret_cast<const uint16_t*>(g.bias)[col]);
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = bm + wm + i * 16 + (lane >> 4) * 4 + r;
-        if (row >= g.M) continue;
-        float v = g.alpha * acc[i][j][r] + b;
-        if (g.splitk > 1) {  // partial sums of K slices meet in C (fp32, pre-initialised)
-          atomicAdd(reinterpret_cast<float*>(g.C) + (size_t)row * g.ldc + col, v);
-          continue;
-        }
-        if (g.act == 1) v = fmaxf(v, 0.f);
-        else if (g.act == 2) v = gelu_tanh(v);
-        const size_t o = (size_t)row * g.ldc + col;
-        if (g.out_bf16) {
-          uint16_t* C = reinterpret_cast<uint16_t*>(g.C);
-          if (g.accumulate) v += bf2f(C[o]);
-          C[o] = (uint16_t)f32_to_bf16_bits(v);
-        } else {
-          float* C = reinterpret_cast<float*>(g.C);
-          if (g.accumulate) v += C[o];
-          C[o] = v;
-        }
-      }
-    }
-  }
+  __syncthreads();
+  store_tile(g, acc, smem, bm, bn, wm, wn, split, t, lane);
 }
-
 
 // ---------------------------------------------------------------------------
 // "TN" GEMM for weight gradients: C[N1,N2] (+)= alpha * sum_m A[m,n1] * B[m,n2]
@@ -275,24 +347,8 @@ __global__ void __launch_bounds__(NT) k_gemm_tn(GemmArgs g) {
     if (kt + 1 < nk) swrite(cur ^ 1);
     __syncthreads();
   }
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int col = bn + wn + j * 16 + (lane & 15);
-    if (col >= g.N) continue;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = bm + wm + i * 16 + (lane >> 4) * 4 + r;
-        if (row >= g.M) continue;
-        const float v = g.alpha * acc[i][j][r];
-        const size_t o = (size_t)row * g.ldc + col;
-        float* C = reinterpret_cast<float*>(g.C);
-        if (g.splitk > 1) atomicAdd(C + o, v);
-        else C[o] = g.accumulate ? C[o] + v : v;
-      }
-    }
-  }
+  __syncthreads();
+  store_tile(g, acc, smem, bm, bn, wm, wn, split, t, lane);
 }
 
 // 2-D transpose of 16-bit elements through a padded 64x65 LDS tile.

@@ -31,6 +31,7 @@ import threading
 from typing import Dict, List, Optional, Sequence, Tuple
 
 from . import _native
+from .utils.trace import trace_call
 
 _OPS = {"SUM": 0, "PROD": 1, "MIN": 2, "MAX": 3}
 
@@ -151,6 +152,17 @@ class DeviceGroup:
         seg, _ = self.dc.find(t.data_ptr(), t.numel() * t.element_size())
         return seg > 0
 
+    def _ensure_inbox(self, nbytes: int) -> None:
+        """Collective (all ranks call with the same size): symmetric inbox of
+        p shards for the push two-shot all-reduce, grown on demand."""
+        shard = ((nbytes + self.size - 1) // self.size + 15) // 16 * 16
+        need = shard * self.size
+        if self.dc.inbox_bytes >= need:
+            return
+        cap = max(need, 64 << 20)
+        buf = self.empty(cap, self.torch.uint8)
+        self.dc.set_inbox(buf.data_ptr(), cap)
+
     # -------------------------------------------------------------------- rccl
     def ensure_rccl(self) -> None:
         """Collective: create the RCCL communicator on first use."""
@@ -187,7 +199,9 @@ class DeviceGroup:
         return "oneshot" if nbytes <= self.oneshot_max else "twoshot"
 
     # ------------------------------------------------------------- collectives
-    def allreduce(self, src, dst=None, op="SUM", algo: str = "auto", rings: int = 0) -> object:
+    @trace_call("allreduce")
+    def allreduce(self, src, dst=None, op="SUM", algo: str = "auto", rings: int = 0,
+                  max_blocks: Optional[int] = None) -> object:
         dst = src if dst is None else dst
         self._check(src, "src")
         self._check(dst, "dst")
@@ -197,12 +211,17 @@ class DeviceGroup:
         nbytes = src.numel() * src.element_size()
         if algo == "auto":
             algo = self.pick_allreduce(nbytes)
+        if ":" in algo:  # "twoshot:512" = algorithm with an explicit CTA budget
+            algo, mb = algo.split(":", 1)
+            max_blocks = int(mb)
         s = self._stream()
-        if algo in ("oneshot", "twoshot", "reduce_bcast"):
+        if algo == "push":
+            self._ensure_inbox(nbytes)
+        if algo in ("oneshot", "twoshot", "reduce_bcast", "push"):
             a = {"oneshot": self.D.ALGO_ONESHOT, "twoshot": self.D.ALGO_TWOSHOT,
-                 "reduce_bcast": self.D.ALGO_REDUCE_BCAST}[algo]
-            self.dc.allreduce(src.data_ptr(), dst.data_ptr(), src.numel(), dt, opc, a, s, self.max_blocks,
-                              self._symm(src, dst))
+                 "reduce_bcast": self.D.ALGO_REDUCE_BCAST, "push": self.D.ALGO_TWOSHOT_PUSH}[algo]
+            self.dc.allreduce(src.data_ptr(), dst.data_ptr(), src.numel(), dt, opc, a, s,
+                              max_blocks or self.max_blocks, self._symm(src, dst))
         elif algo == "rccl":
             self.ensure_rccl()
             self.dc.rccl_allreduce(src.data_ptr(), dst.data_ptr(), src.numel(), dt, opc, s)
@@ -221,6 +240,7 @@ class DeviceGroup:
             raise ValueError(f"unknown allreduce algorithm {algo!r}")
         return dst
 
+    @trace_call("reduce_scatter")
     def reduce_scatter(self, src, dst, op="SUM", algo: str = "direct"):
         self._check(src, "src")
         self._check(dst, "dst")
@@ -236,6 +256,7 @@ class DeviceGroup:
                                    self._symm(src))
         return dst
 
+    @trace_call("allgather")
     def allgather(self, src, dst, algo: str = "direct"):
         self._check(src, "src")
         self._check(dst, "dst")
@@ -250,6 +271,7 @@ class DeviceGroup:
             self.dc.allgather(src.data_ptr(), dst.data_ptr(), nb, s, self.max_blocks, self._symm(src) and dst.data_ptr() % 16 == 0)
         return dst
 
+    @trace_call("alltoall")
     def alltoall(self, src, dst, algo: str = "direct"):
         self._check(src, "src")
         self._check(dst, "dst")
@@ -267,6 +289,7 @@ class DeviceGroup:
             self.dc.alltoall(src.data_ptr(), dst.data_ptr(), blk, s, self.max_blocks, self._symm(src))
         return dst
 
+    @trace_call("bcast")
     def bcast(self, buf, root: int = 0, algo: str = "direct"):
         self._check(buf, "buf")
         s = self._stream()
@@ -277,10 +300,72 @@ class DeviceGroup:
             self.dc.bcast(buf.data_ptr(), buf.numel() * buf.element_size(), root, s, self.max_blocks, self._symm(buf))
         return buf
 
+    def allgather_lastaxis(self, src, dst, rows: int, row_bytes: int):
+        """dst[m][j*k:(j+1)*k] = src_j[m]  (TP forward collect, fused layout)."""
+        self.dc.allgather_lastaxis(src.data_ptr(), dst.data_ptr(), rows, row_bytes, self._stream(), self.max_blocks,
+                                   self._symm(src))
+        return dst
+
+    def reduce_scatter_lastaxis(self, src, dst, rows: int, k: int, op="SUM"):
+        """dst[m] = sum_j src_j[m][me*k:(me+1)*k]  (TP backward grad_x, fused layout)."""
+        self.dc.reduce_scatter_lastaxis(src.data_ptr(), dst.data_ptr(), rows, k, dtype_code(src.dtype), op_code(op),
+                                        self._stream(), self.max_blocks, self._symm(src))
+        return dst
+
     def local_reduce(self, inputs: Sequence, out, op="SUM"):
         self.dc.local_reduce([t.data_ptr() for t in inputs], out.data_ptr(), out.numel(), dtype_code(out.dtype),
                              op_code(op), self._stream())
         return out
+
+    # ------------------------------------------------------------------- tuning
+    def tune(self, max_bytes: int = 256 << 20, min_bytes: int = 4 << 10, algos: Sequence[str] = (),
+             iters: int = 5, dtype=None) -> Dict[Tuple[int, int], str]:
+        """Collective: time every all-reduce algorithm at powers of 4 between
+        ``min_bytes`` and ``max_bytes`` (after an exactness check) and make
+        ``algo="auto"`` use the fastest per size class.  Algorithms that fail or
+        time out on any rank are discarded everywhere."""
+        import time
+
+        torch = self.torch
+        dtype = dtype or torch.float32
+        if not algos:
+            algos = ["oneshot", "twoshot"] + ([] if self.shared_device else ["rccl"])
+        es = torch.empty((), dtype=dtype).element_size()
+        x = self.empty(max_bytes // es, dtype)
+        y = self.empty(max_bytes // es, dtype)
+        x.fill_(float(self.rank + 1))
+        expect = float(self.size * (self.size + 1) // 2)
+        b = min_bytes
+        while b <= max_bytes:
+            n = b // es
+            best, best_t = None, None
+            for algo in algos:
+                if algo == "oneshot" and b > (16 << 20):
+                    continue
+                ok = 1
+                try:
+                    self.allreduce(x[:n], y[:n], "SUM", algo)
+                    torch.cuda.synchronize(self.device)
+                    self.check()
+                    ok = int(bool(torch.all(y[:n] == expect).item()))
+                except Exception:  # noqa: BLE001 - disqualify the algorithm
+                    ok = 0
+                if not self.host.allreduce(ok, op=_host_min()):
+                    continue
+                torch.cuda.synchronize(self.device)
+                self.host.Barrier()
+                t0 = time.perf_counter()
+                for _ in range(iters):
+                    self.allreduce(x[:n], y[:n], "SUM", algo)
+                torch.cuda.synchronize(self.device)
+                t = self.host.allreduce(time.perf_counter() - t0, op=_host_max())
+                if best_t is None or t < best_t:
+                    best, best_t = algo, t
+            if best is not None:
+                self.tuned[(self.size, max(0, b.bit_length() - 1))] = best
+                self.tuned[(self.size, max(0, b.bit_length() - 1) + 1)] = best
+            b *= 4
+        return dict(self.tuned)
 
     # ------------------------------------------------------------------ health
     def check(self) -> None:
@@ -291,6 +376,27 @@ class DeviceGroup:
             raise RuntimeError(f"device collective timeout/fault code 0x{code:x} on rank {self.rank} "
                                f"(phase {code >> 8}, peer {code & 0xff})")
 
+    def reset(self) -> None:
+        """Collective recovery after a device timeout: once no kernel is in
+        flight anywhere, every rank zeroes its flags and epochs."""
+        self.torch.cuda.synchronize(self.device)
+        self.host.Barrier()
+        self.dc.reset_state()
+        self.dc.clear_error()
+        self.host.Barrier()
+
     def barrier(self) -> None:
         self.torch.cuda.synchronize(self.device)
         self.host.Barrier()
+
+
+def _host_min():
+    from . import mpi as MPI
+
+    return MPI.MIN
+
+
+def _host_max():
+    from . import mpi as MPI
+
+    return MPI.MAX

@@ -60,7 +60,7 @@ def bench_forward(comm, tp: int = 2, batch: int = 2048, steps: int = 20, warmup:
     xp_static = patchify(xb, cfg)
 
     def fwd():
-        xp_static.copy_(patchify(xb, cfg))
+        patchify(xb, cfg, out=xp_static)
         return layer.forward(xp_static, cfg.batch)
 
     for _ in range(3):

@@ -3,8 +3,8 @@ reference assumes but does not ship (README.md:173-181: "transformer compute,
 training loop and MNIST data were taken care of"; the layer dims come from its
 tests: fc_q/k/v 768 -> 256 column-parallel, fc_o 256 -> 10, test_get_info.py:68-69,152-153).
 
-Model (per image): 28x28 -> 16 patches of 7x7 (49 px, zero-padded to 64) ->
-patch embedding 64 -> 768 (+ bias + learned position) -> fused QKV projection
+Model (per image): 28x28 -> 16 patches of 7x7 (49 px) -> patch embedding
+49 -> 768 (+ bias + learned position) -> fused QKV projection
 768 -> 3x256 (4 heads x 64) -> softmax attention over the 16 patches ->
 fc_o 256 -> 10 -> mean over patches -> cross-entropy.
 
@@ -14,7 +14,9 @@ Parallelism: mp-major 2-D grid from ``get_info`` (rank = dp_idx * tp + tp_idx).
 * fc_o is row-parallel (``fc_o_mode="row"``, default): each rank multiplies its
   local attention output by its input-dim shard of W_o, and ONE TP all-reduce
   (hand-written device kernel, symmetric buffers, graph-capturable) sums the
-  partial outputs.  ``fc_o_mode="naive"`` runs the reference's collects instead
+  partial outputs.  Because fc_o and the mean over patches are both linear,
+  the attention kernel emits the patch-mean of its output and fc_o runs on B
+  rows instead of B*S: the fc_o GEMMs and the TP all-reduce shrink 16x.  ``fc_o_mode="naive"`` runs the reference's collects instead
   (model/func_impl.py:76-187): all-gather the input, out-sharded fc_o, all-gather
   the output; backward slices the output gradient and reduce-scatters grad_x.
 * the embedding input gradient is TP-partial and is all-reduced (Megatron's
@@ -23,8 +25,20 @@ Parallelism: mp-major 2-D grid from ``get_info`` (rank = dp_idx * tp + tp_idx).
   three buckets in backward order, all-reduced on a side stream while the
   remaining backward GEMMs run (parallel/dp.py).
 
-All GEMMs are the hand-written MFMA kernel (ops.gemm_nt); attention is the
-fused short-sequence kernel; the optimizer is one fused AdamW pass.
+All GEMMs are the hand-written MFMA kernels (ops.gemm_nt forward / input
+gradients, ops.gemm_tn weight gradients); attention is the fused short-sequence
+kernel; the optimizer is one fused AdamW pass.  Fusions that remove whole passes:
+
+* the patchify kernel appends a constant-1 column and a one-hot position
+  column block to every token row, so the embedding bias and the learned
+  position embedding are columns of W_emb: the embedding is ONE GEMM (no bias
+  add, no position add) and their gradients come out of the W_emb gradient GEMM;
+* the attention backward kernel accumulates the QKV bias gradient (column sums
+  of dQ/dK/dV) in-kernel;
+* with TP > 1 the embedding needs only the TP-sum of its *weight* gradient
+  (d_model x 72 fp32, 221 KB), not an all-reduce of the TP-partial activation
+  gradient dH (tokens x d_model): W_emb's gradient is linear in dH and the
+  embedding input needs no gradient.
 """
 from __future__ import annotations
 
@@ -50,7 +64,6 @@ class LayerConfig:
     n_classes: int = 10
     img: int = 28
     patch: int = 7
-    patch_pad: int = 64
     out_pad: int = 16        # fc_o output rows padded to 16 (MFMA-friendly K for dX = dZ . W_o)
     batch: int = 2048        # images per DP replica
     tp: int = 1
@@ -70,25 +83,38 @@ class LayerConfig:
     def head_dim(self) -> int:
         return self.d_attn // self.n_heads
 
+    @property
+    def pixels(self) -> int:
+        return self.patch * self.patch
 
-def patchify(x: torch.Tensor, cfg: LayerConfig) -> torch.Tensor:
-    """(B, 784) float -> (B*16, 64) bf16 patches (7x7 pixels, zero-padded)."""
+    @property
+    def kp(self) -> int:
+        """Embedding GEMM K: pixels + bias column + one-hot positions, rounded to 8."""
+        return (self.pixels + 1 + self.seq + 7) // 8 * 8
+
+
+def patchify(x: torch.Tensor, cfg: LayerConfig, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """(B, 784) fp32 -> (B*16, kp) bf16 token rows: 49 pixels | 1 | one-hot(position) | 0 pad."""
     B = x.shape[0]
-    g = cfg.img // cfg.patch
-    p = x.view(B, g, cfg.patch, g, cfg.patch).permute(0, 1, 3, 2, 4).reshape(B * g * g, cfg.patch * cfg.patch)
-    out = torch.zeros(B * g * g, cfg.patch_pad, dtype=torch.bfloat16, device=x.device)
-    out[:, : cfg.patch * cfg.patch] = p
+    if out is None:
+        out = torch.empty(B * cfg.seq, cfg.kp, dtype=torch.bfloat16, device=x.device)
+    x = x.contiguous().float()
+    _native.device().patchify(x.data_ptr(), out.data_ptr(), B, cfg.img, cfg.patch, cfg.kp,
+                              torch.cuda.current_stream(x.device).cuda_stream)
     return out
 
 
 def full_init(cfg: LayerConfig):
-    """Unsharded fp32 weights from a seeded CPU generator (identical on all ranks)."""
+    """Unsharded fp32 weights from a seeded CPU generator (identical on all ranks).
+    W_emb columns: [pixels | bias | position one-hot | pad]."""
     g = torch.Generator().manual_seed(cfg.seed)
-    d, a, pp = cfg.d_model, cfg.d_attn, cfg.patch * cfg.patch
+    d, a, pp = cfg.d_model, cfg.d_attn, cfg.pixels
+    emb = torch.zeros(d, cfg.kp)
+    emb[:, :pp] = torch.randn(d, pp, generator=g) / math.sqrt(pp)
+    emb[:, pp] = 0.0                                                    # bias
+    emb[:, pp + 1:pp + 1 + cfg.seq] = (torch.randn(cfg.seq, d, generator=g) * 0.02).T  # positions
     w = {
-        "emb_w": torch.randn(d, cfg.patch_pad, generator=g) / math.sqrt(pp),
-        "emb_b": torch.zeros(d),
-        "pos": torch.randn(cfg.seq, d, generator=g) * 0.02,
+        "emb_w": emb,
         "q_w": torch.randn(a, d, generator=g) / math.sqrt(d),
         "k_w": torch.randn(a, d, generator=g) / math.sqrt(d),
         "v_w": torch.randn(a, d, generator=g) / math.sqrt(d),
@@ -96,7 +122,6 @@ def full_init(cfg: LayerConfig):
         "o_w": torch.randn(cfg.n_classes, a, generator=g) / math.sqrt(a),
         "o_b": torch.zeros(cfg.n_classes),
     }
-    w["emb_w"][:, pp:] = 0.0  # padding columns of each patch never carry signal
     return w
 
 
@@ -120,12 +145,12 @@ class MnistTPLayer:
         specs = [  # backward order -> bucket layout
             ("o_w", (cfg.out_pad, self.hd)), ("o_b", (cfg.out_pad,)),
             ("qkv_w", (3 * self.hd, d)), ("qkv_b", (3 * self.hd,)),
-            ("emb_w", (d, cfg.patch_pad)), ("emb_b", (d,)), ("pos", (cfg.seq, d)),
+            ("emb_w", (d, cfg.kp)),
         ]
         grad_alloc = (lambda n: self.dp_dev.zeros(n, torch.float32)) if self.dp_dev is not None else None
         self.flat = FlatParams(specs, self.device, grad_alloc)
         self.buckets = GradBuckets(self.flat, self.dp_dev, [["o_w", "o_b"], ["qkv_w", "qkv_b"],
-                                                            ["emb_w", "emb_b", "pos"]],
+                                                            ["emb_w"]],
                                    algo=cfg.dp_algo, overlap=cfg.overlap)
         self._load(full_init(cfg))
         self._bufs = {}
@@ -136,8 +161,6 @@ class MnistTPLayer:
         sl = slice(t * self.hd, (t + 1) * self.hd)
         P = self.flat.param
         P("emb_w").copy_(w["emb_w"])
-        P("emb_b").copy_(w["emb_b"])
-        P("pos").copy_(w["pos"])
         P("qkv_w").copy_(torch.cat([w["q_w"][sl], w["k_w"][sl], w["v_w"][sl]]))
         P("qkv_b").copy_(torch.cat([w["q_b"][sl], w["k_b"][sl], w["v_b"][sl]]))
         ow = torch.zeros(cfg.out_pad, self.hd)
@@ -175,25 +198,31 @@ class MnistTPLayer:
         M = B * S
         P16 = self.flat.param16
         h = self._buf("h", (M, d), torch.bfloat16)
-        gemm_nt(xp, P16("emb_w"), out=h, bias=self.flat.param("emb_b"))
-        h.view(B, S, d).add_(P16("pos"))
+        gemm_nt(xp, P16("emb_w"), out=h)  # bias + position are columns of W_emb
         qkv = self._buf("qkv", (M, 3 * self.hd), torch.bfloat16)
         gemm_nt(h, P16("qkv_w"), out=qkv, bias=self.flat.param("qkv_b"))
         att = self._buf("att", (M, self.hd), torch.bfloat16)
         lse = self._buf("lse", (B * self.hl, S), torch.float32)
         D = _native.device()
         st = torch.cuda.current_stream(self.device).cuda_stream
+        naive = cfg.fc_o_mode == "naive" and cfg.tp > 1
+        pool = None if naive else self._buf("pool", (B, self.hd), torch.bfloat16)
         D.attn_small_fwd(qkv.data_ptr(), att.data_ptr(), lse.data_ptr(), B, S, self.hl, cfg.head_dim,
-                         qkv.stride(0), att.stride(0), 1.0 / math.sqrt(cfg.head_dim), st)
-        if cfg.fc_o_mode == "naive" and cfg.tp > 1:
+                         qkv.stride(0), att.stride(0), 1.0 / math.sqrt(cfg.head_dim),
+                         0 if pool is None else pool.data_ptr(), 0 if pool is None else pool.stride(0), st)
+        if naive:
             z = self._forward_naive_fc_o(att, B)
+            logits = z.view(B, S, cfg.out_pad)[:, :, : cfg.n_classes].mean(dim=1)
         else:
-            z = self._buf("z", (M, cfg.out_pad), torch.float32, self.tp_dev)
-            gemm_nt(att, P16("o_w"), out=z, out_dtype=torch.float32)
+            # fc_o and the mean over patches are linear: pool first (fused in the
+            # attention kernel), so fc_o and its TP all-reduce work on B rows, not B*S
+            zp = self._buf("zp", (B, cfg.out_pad), torch.float32, self.tp_dev)
+            gemm_nt(pool, P16("o_w"), out=zp, out_dtype=torch.float32, splitk=1)
             if self.tp_dev is not None:
-                self.tp_dev.allreduce(z, z, "SUM")  # row-parallel: one TP all-reduce
-        logits = z.view(B, S, cfg.out_pad)[:, :, : cfg.n_classes].mean(dim=1) + self.flat.param("o_b")[: cfg.n_classes]
-        self._saved = (xp, h, qkv, att, lse, B)
+                self.tp_dev.allreduce(zp, zp, "SUM")  # row-parallel: one TP all-reduce (B x 16 fp32)
+            logits = zp[:, : cfg.n_classes]
+        logits = logits + self.flat.param("o_b")[: cfg.n_classes]
+        self._saved = (xp, h, qkv, att, lse, B, pool)
         return logits
 
     def _forward_naive_fc_o(self, att, B):
@@ -229,44 +258,51 @@ class MnistTPLayer:
 
     def backward(self, dlogits: torch.Tensor) -> None:
         cfg = self.cfg
-        xp, h, qkv, att, lse, B = self._saved
+        xp, h, qkv, att, lse, B, pool = self._saved
         S, d = cfg.seq, cfg.d_model
         M = B * S
         G = self.flat.grad
         P16 = self.flat.param16
         D = _native.device()
         st = torch.cuda.current_stream(self.device).cuda_stream
-        # ---- output head: z[b,s,c] -> logits[b,c] = mean_s z + o_b
+        # ---- output head: logits[b,c] = mean_s z[b,s,c] + o_b  (z = att . W_o^T)
         G("o_b")[: cfg.n_classes].add_(dlogits.sum(0))
-        dz = self._buf("dz", (M, cfg.out_pad), torch.bfloat16)
-        dz.zero_()
-        dz.view(B, S, cfg.out_pad)[:, :, : cfg.n_classes] = (dlogits / S).unsqueeze(1).to(torch.bfloat16)
-        datt = self._buf("datt", (M, self.hd), torch.bfloat16)
         if cfg.fc_o_mode == "naive" and cfg.tp > 1:
+            dz = self._buf("dz", (M, cfg.out_pad), torch.bfloat16)
+            dz.zero_()
+            dz.view(B, S, cfg.out_pad)[:, :, : cfg.n_classes] = (dlogits / S).unsqueeze(1).to(torch.bfloat16)
+            datt = self._buf("datt", (M, self.hd), torch.bfloat16)
             self._backward_naive_fc_o(dz, datt, B)
+            dout, dout_b, dout_r = datt, S * datt.stride(0), datt.stride(0)
         else:
-            # row-parallel fc_o: dz is replicated on every TP rank (identity backward of the reduce)
-            gemm_tn(dz, att, out=G("o_w"), accumulate=True)      # dW_o = dZ^T . att
-            oT = transpose(P16("o_w"))                            # [hd, out_pad] (tiny)
-            gemm_nt(dz, oT, out=datt)
+            # pooled row-parallel fc_o: dZ is replicated on every TP rank (identity backward
+            # of the reduce); d(att[b,s]) = dpool[b] / S for every s, broadcast in the kernel
+            dzp = self._buf("dzp", (B, cfg.out_pad), torch.bfloat16)
+            dzp.zero_()
+            dzp[:, : cfg.n_classes] = dlogits.to(torch.bfloat16)
+            gemm_tn(dzp, pool, out=G("o_w"), accumulate=True)    # dW_o = dZ^T . pooled
+            dpool = self._buf("dpool", (B, self.hd), torch.bfloat16)
+            gemm_nt(dzp, transpose(P16("o_w")), out=dpool, alpha=1.0 / S)
+            dout, dout_b, dout_r = dpool, dpool.stride(0), 0
         self.buckets.ready(0)
         # ---- attention
         dqkv = self._buf("dqkv", (M, 3 * self.hd), torch.bfloat16)
-        D.attn_small_bwd(qkv.data_ptr(), att.data_ptr(), lse.data_ptr(), datt.data_ptr(), dqkv.data_ptr(), B, S,
-                         self.hl, cfg.head_dim, qkv.stride(0), att.stride(0), 1.0 / math.sqrt(cfg.head_dim), st)
+        D.attn_small_bwd(qkv.data_ptr(), att.data_ptr(), lse.data_ptr(), dout.data_ptr(), dqkv.data_ptr(),
+                         G("qkv_b").data_ptr(), B, S, self.hl, cfg.head_dim, qkv.stride(0), att.stride(0),
+                         1.0 / math.sqrt(cfg.head_dim), dout_b, dout_r, st)  # + QKV bias grad in-kernel
         # ---- fused QKV projection (column-parallel)
         gemm_tn(dqkv, h, out=G("qkv_w"), accumulate=True)      # dW_qkv = dQKV^T . h
-        G("qkv_b").add_(dqkv.float().sum(0))
         self.buckets.ready(1)
-        dh = self._buf("dh", (M, d), torch.bfloat16, self.tp_dev)
+        dh = self._buf("dh", (M, d), torch.bfloat16)            # TP-partial input gradient
         gemm_nt(dqkv, transpose(P16("qkv_w")), out=dh)
+        # ---- embedding (replicated across TP): only its weight gradient needs the TP sum
         if self.tp_dev is not None:
-            self.tp_dev.allreduce(dh, dh, "SUM")  # column-parallel input grad is TP-partial (fp32 sum inside)
-        # ---- embedding (replicated across TP)
-        gemm_tn(dh, xp, out=G("emb_w"), accumulate=True)       # dW_emb = dH^T . patches
-        dh32 = dh.float()
-        G("emb_b").add_(dh32.sum(0))
-        G("pos").add_(dh32.view(B, S, d).sum(0))
+            gpart = self._buf("gemb", (d, cfg.kp), torch.float32, self.tp_dev)
+            gemm_tn(dh, xp, out=gpart)                           # partial dW_emb on this TP rank
+            self.tp_dev.allreduce(gpart, gpart, "SUM")           # 221 KB instead of tokens x d_model
+            G("emb_w").add_(gpart)
+        else:
+            gemm_tn(dh, xp, out=G("emb_w"), accumulate=True)     # dW_emb = dH^T . [patches | 1 | onehot]
         self.buckets.ready(2)
 
     def _backward_naive_fc_o(self, dz, datt, B):

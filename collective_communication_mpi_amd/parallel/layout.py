@@ -128,22 +128,32 @@ def _host_reduce_scatter_lastaxis(g: np.ndarray, mp_comm, mp_size: int) -> np.nd
 # device helpers
 # --------------------------------------------------------------------------
 def _dev_allgather_lastaxis(x, mp_comm, mp_size: int):
+    """(.., k) shards -> (.., p*k): one device kernel pulls every peer's rows straight
+    into the strided destination (no staging buffer, no interleave pass)."""
     import torch
 
     g = device_group_for(mp_comm)
     p = g.size
     xc = x.contiguous()
     k = xc.shape[-1]
-    M = xc.numel() // max(k, 1)
-    stage = torch.empty((p,) + tuple(xc.shape), dtype=xc.dtype, device=xc.device)
-    g.allgather(xc.reshape(-1), stage.reshape(-1))
+    rows = xc.numel() // max(k, 1)
     out = torch.empty(tuple(xc.shape[:-1]) + (p * k,), dtype=xc.dtype, device=xc.device)
-    g.D.interleave_lastaxis(stage.data_ptr(), out.data_ptr(), M, p, k * xc.element_size(),
-                            torch.cuda.current_stream(xc.device).cuda_stream)
+    rb = k * xc.element_size()
+    if p == 1:
+        out.copy_(xc)
+    elif rb % 16 == 0:
+        g.allgather_lastaxis(xc, out, rows, rb)
+    else:  # rows not 16-B multiples: contiguous all-gather + interleave kernel
+        stage = torch.empty((p,) + tuple(xc.shape), dtype=xc.dtype, device=xc.device)
+        g.allgather(xc.reshape(-1), stage.reshape(-1))
+        g.D.interleave_lastaxis(stage.data_ptr(), out.data_ptr(), rows, p, rb,
+                                torch.cuda.current_stream(xc.device).cuda_stream)
     return out
 
 
 def _dev_reduce_scatter_lastaxis(gx, mp_comm, mp_size: int):
+    """(.., p*k) partial sums -> (.., k) reduced shard: one kernel reads each peer's
+    strided last-axis slice and sums in registers (no pack pass)."""
     import torch
 
     g = device_group_for(mp_comm)
@@ -153,12 +163,17 @@ def _dev_reduce_scatter_lastaxis(gx, mp_comm, mp_size: int):
     if n % p:
         raise ValueError("last axis must be divisible by mp_size")
     k = n // p
-    M = gc.numel() // max(n, 1)
-    packed = torch.empty((p,) + tuple(gc.shape[:-1]) + (k,), dtype=gc.dtype, device=gc.device)
-    g.D.deinterleave_lastaxis(gc.data_ptr(), packed.data_ptr(), M, p, k * gc.element_size(),
-                              torch.cuda.current_stream(gc.device).cuda_stream)
+    rows = gc.numel() // max(n, 1)
     out = torch.empty(tuple(gc.shape[:-1]) + (k,), dtype=gc.dtype, device=gc.device)
-    g.reduce_scatter(packed.reshape(-1), out.reshape(-1))
+    if p == 1:
+        out.copy_(gc)
+    elif (k * gc.element_size()) % 16 == 0:
+        g.reduce_scatter_lastaxis(gc, out, rows, k)
+    else:
+        packed = torch.empty((p,) + tuple(gc.shape[:-1]) + (k,), dtype=gc.dtype, device=gc.device)
+        g.D.deinterleave_lastaxis(gc.data_ptr(), packed.data_ptr(), rows, p, k * gc.element_size(),
+                                  torch.cuda.current_stream(gc.device).cuda_stream)
+        g.reduce_scatter(packed.reshape(-1), out.reshape(-1))
     return out
 
 

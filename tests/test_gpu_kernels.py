@@ -135,3 +135,78 @@ def test_gemm_nt_splitk(splitk):
     bias = torch.randn(192, device="cuda")
     y = gemm_nt(a, b, bias=bias, out_dtype=torch.float32, splitk=splitk)
     torch.testing.assert_close(y, _ref(a, b, bias), rtol=2e-3, atol=0.15)
+
+
+def _attn_ref(qkv, B, S, H, D):
+    q, k, v = qkv.float().view(B, S, 3, H, D).unbind(2)
+    q, k, v = (t.transpose(1, 2) for t in (q, k, v))  # B,H,S,D
+    p = torch.softmax(q @ k.transpose(-1, -2) / D ** 0.5, dim=-1)
+    return (p @ v).transpose(1, 2).reshape(B * S, H * D)
+
+
+@pytest.mark.parametrize("B,S,H,D", [(3, 16, 2, 64), (2, 7, 1, 32), (4, 64, 2, 64)])
+def test_attn_small_fwd_bwd(B, S, H, D):
+    from collective_communication_mpi_amd import _native
+
+    dev = _native.device()
+    st = torch.cuda.current_stream().cuda_stream
+    qkv = (torch.randn(B * S, 3 * H * D, device="cuda") * 0.5).bfloat16()
+    o = torch.empty(B * S, H * D, device="cuda", dtype=torch.bfloat16)
+    lse = torch.empty(B * H, S, device="cuda")
+    pool = torch.empty(B, H * D, device="cuda", dtype=torch.bfloat16)
+    dev.attn_small_fwd(qkv.data_ptr(), o.data_ptr(), lse.data_ptr(), B, S, H, D, qkv.stride(0), o.stride(0),
+                       D ** -0.5, pool.data_ptr(), pool.stride(0), st)
+    ref_in = qkv.float().requires_grad_(True)
+    ref = _attn_ref(ref_in, B, S, H, D)
+    torch.testing.assert_close(o.float(), ref.detach(), rtol=2e-2, atol=2e-2)
+    torch.testing.assert_close(pool.float(), ref.detach().view(B, S, H * D).mean(1), rtol=2e-2, atol=2e-2)
+    do = torch.randn(B * S, H * D, device="cuda").bfloat16()
+    ref.backward(do.float())
+    dqkv = torch.empty_like(qkv)
+    dbias = torch.zeros(3 * H * D, device="cuda")
+    dev.attn_small_bwd(qkv.data_ptr(), o.data_ptr(), lse.data_ptr(), do.data_ptr(), dqkv.data_ptr(),
+                       dbias.data_ptr(), B, S, H, D, qkv.stride(0), o.stride(0), D ** -0.5, S * do.stride(0),
+                       do.stride(0), st)
+    torch.testing.assert_close(dqkv.float(), ref_in.grad, rtol=3e-2, atol=3e-2)
+    torch.testing.assert_close(dbias, dqkv.float().sum(0), rtol=1e-2, atol=1e-2)
+    # broadcast form: dO[b, s] = g[b] for every s (pooled-gradient path, row stride 0)
+    gpool = torch.randn(B, H * D, device="cuda").bfloat16()
+    ref_in.grad = None
+    ref2 = _attn_ref(ref_in, B, S, H, D)
+    ref2.backward(gpool.float().repeat_interleave(S, dim=0))
+    dev.attn_small_bwd(qkv.data_ptr(), o.data_ptr(), lse.data_ptr(), gpool.data_ptr(), dqkv.data_ptr(), 0, B, S,
+                       H, D, qkv.stride(0), o.stride(0), D ** -0.5, gpool.stride(0), 0, st)
+    torch.testing.assert_close(dqkv.float(), ref_in.grad, rtol=3e-2, atol=3e-2)
+
+
+def test_patchify_columns():
+    from collective_communication_mpi_amd.models.mnist_tp import LayerConfig, patchify
+
+    cfg = LayerConfig()
+    x = torch.rand(5, 784, device="cuda")
+    xp = patchify(x, cfg).float()
+    g = cfg.img // cfg.patch
+    ref = x.view(5, g, cfg.patch, g, cfg.patch).permute(0, 1, 3, 2, 4).reshape(5 * g * g, cfg.pixels)
+    torch.testing.assert_close(xp[:, : cfg.pixels], ref.bfloat16().float())
+    assert torch.all(xp[:, cfg.pixels] == 1)
+    onehot = xp[:, cfg.pixels + 1:cfg.pixels + 1 + cfg.seq]
+    torch.testing.assert_close(onehot, torch.eye(cfg.seq, device="cuda").repeat(5, 1))
+    assert torch.all(xp[:, cfg.pixels + 1 + cfg.seq:] == 0)
+
+
+def test_fused_adamw_matches_torch():
+    from collective_communication_mpi_amd.parallel.dp import FlatParams
+
+    fp = FlatParams([("w", (1000,))], "cuda")
+    w0 = torch.randn(1000, device="cuda")
+    fp.param("w").copy_(w0)
+    ref = torch.nn.Parameter(w0.clone())
+    opt = torch.optim.AdamW([ref], lr=1e-2, weight_decay=0.1, eps=1e-8)
+    for _ in range(3):
+        g = torch.randn(1000, device="cuda")
+        fp.grad("w").copy_(g * 2)
+        fp.adamw(1e-2, weight_decay=0.1, grad_scale=0.5)  # grad_scale folds a 1/dp average
+        ref.grad = g
+        opt.step()
+    torch.testing.assert_close(fp.param("w"), ref.detach(), rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(fp.param16("w").float(), ref.detach().bfloat16().float())

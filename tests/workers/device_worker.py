@@ -67,7 +67,7 @@ sizes = [int(s) for s in args.sizes.split(",") if s] or ([1, 7, 1000, 65536 + 3]
                                                           [1, 3, 8, 1000, 4097, 65536 + 3, 1 << 20, (1 << 22) + 5])
 dtypes = [torch.float32, torch.bfloat16] if args.quick else [torch.float32, torch.bfloat16, torch.float16,
                                                               torch.float64, torch.int32, torch.int64]
-algos = ["oneshot", "twoshot", "reduce_bcast"]
+algos = ["oneshot", "twoshot", "reduce_bcast", "push"]
 salt = 0
 t0 = time.time()
 for sym in (False, True):
@@ -127,6 +127,21 @@ for sym in (False, True):
             dev.bcast(b, root)
             check(f"bcast[{dt},n={n},sym={sym}]", b, gen(root, n, dt, salt).to(torch.float64 if dt.is_floating_point else torch.int64), dt)
 
+# TP layout-fused collectives (reference naive collects on device tensors)
+from collective_communication_mpi_amd.parallel.layout import (  # noqa: E402
+    naive_collect_backward_x, naive_collect_forward_input)
+for dt in (torch.float32, torch.bfloat16):
+    for (B, S, k) in [(2, 3, 8), (4, 16, 64), (3, 5, 3)]:
+        salt += 1
+        shards = [gen(r, B * S * k, dt, salt).view(B, S, k) for r in range(p)]
+        got = naive_collect_forward_input(shards[rank].to(dev.device), comm, p)
+        want = torch.cat(shards, dim=-1).to(torch.float64 if dt.is_floating_point else torch.int64)
+        check(f"forward_input_lastaxis[{dt},{B}x{S}x{k}]", got, want, dt)
+        salt += 1
+        full = [gen(r, B * S * k * p, dt, salt).view(B, S, k * p) for r in range(p)]
+        got = naive_collect_backward_x(full[rank].to(dev.device), comm, p)
+        ref = sum(f.to(torch.float64) for f in full)[:, :, rank * k:(rank + 1) * k]
+        check(f"backward_x_lastaxis[{dt},{B}x{S}x{k}]", got, ref, dt, p)
 torch.cuda.synchronize()
 dev.check()
 if args.rccl:
