@@ -46,8 +46,20 @@ struct AttnArgs {
   int dout_rstride;     //      (rstride 0 = the pooled-gradient broadcast over the S rows)
 };
 
-// stage an S x D head tile (bf16, row stride ld) into fp32 LDS [S][D+1]
+// stage an S x D head tile (bf16, row stride ld) into fp32 LDS [S][D+1]; 16-B
+// vector loads (8 bf16 per lane) whenever rows are 16-B aligned (guide G13)
 __device__ __forceinline__ void stage(float* dst, const uint16_t* src, int S, int D, int ld) {
+  if ((D % 8) == 0 && (ld % 8) == 0 && ((uint64_t)src % 16) == 0) {
+    const int vr = D / 8;
+    for (int idx = threadIdx.x; idx < S * vr; idx += blockDim.x) {
+      const int i = idx / vr, c = (idx % vr) * 8;
+      const uint4 w = *reinterpret_cast<const uint4*>(src + (size_t)i * ld + c);
+      float* o = dst + i * (D + 1) + c;
+      o[0] = bf16_lo(w.x); o[1] = bf16_hi(w.x); o[2] = bf16_lo(w.y); o[3] = bf16_hi(w.y);
+      o[4] = bf16_lo(w.z); o[5] = bf16_hi(w.z); o[6] = bf16_lo(w.w); o[7] = bf16_hi(w.w);
+    }
+    return;
+  }
   for (int idx = threadIdx.x; idx < S * D; idx += blockDim.x) {
     const int i = idx / D, d = idx % D;
     dst[i * (D + 1) + d] = ld_bf16(src + (size_t)i * ld + d);
@@ -134,9 +146,15 @@ __global__ void __launch_bounds__(256) k_attn_bwd(AttnArgs a) {
   stage(o, a.o + (size_t)b * S * a.ld_o + h * D, S, D, a.ld_o);
   {  // dO rows may be a broadcast of one pooled-gradient row (rstride 0)
     const uint16_t* db = a.dout + (size_t)b * a.dout_bstride + h * D;
-    for (int idx = threadIdx.x; idx < S * D; idx += blockDim.x) {
-      const int i = idx / D, d = idx % D;
-      dO[i * Dp + d] = ld_bf16(db + (size_t)i * a.dout_rstride + d);
+    if (a.dout_rstride == 0) {
+      stage(dO, db, 1, D, 0);
+      __syncthreads();
+      for (int idx = threadIdx.x; idx < (S - 1) * D; idx += blockDim.x) {
+        const int i = 1 + idx / D, d = idx % D;
+        dO[i * Dp + d] = dO[d];
+      }
+    } else {
+      stage(dO, db, S, D, a.dout_rstride);
     }
   }
   __syncthreads();

@@ -19,6 +19,8 @@
 // tiles land on the same XCD (shared A panel in that XCD's L2).
 #include <pybind11/pybind11.h>
 
+#include <cstdlib>
+
 #include "common.hpp"
 #include "ops.hpp"
 
@@ -31,6 +33,7 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 
 constexpr int BM = 128, BN = 128, BK = 64, NT = 256;
+bool g_use_glds = std::getenv("CCMPI_GEMM_NO_GLDS") == nullptr;  // A/B switch (benchmarks)
 constexpr int kRowBytes = BK * 2;  // 128 B per LDS row
 
 struct GemmArgs {
@@ -246,6 +249,87 @@ __global__ void __launch_bounds__(NT) k_gemm_nt(GemmArgs g) {
   store_tile(g, acc, smem, bm, bn, wm, wn, split, t, lane);
 }
 
+// Same tile / wave layout as k_gemm_nt, staged by LDS-DMA (global_load_lds,
+// 16 B per lane, 1 KiB per wave instruction) instead of registers: the next
+// K-tile streams straight into the other LDS buffer while this one feeds the
+// MFMAs, and the staging costs no VGPRs and no ds_write issue slots.  The LDS
+// image is lane-linear (8 rows of 128 B per instruction), so the (row & 7)
+// chunk swizzle the fragment reads expect is applied to the per-lane SOURCE
+// address (the same involution on both sides).  Rows past M / N re-read the
+// last valid row (their outputs are discarded); used only when K % 64 == 0.
+__global__ void __launch_bounds__(NT) k_gemm_nt_glds(GemmArgs g) {
+  __shared__ __attribute__((aligned(16))) unsigned char smem[(2 * (BM + BN) * kRowBytes > BM * (BN + 4) * 4) ? 2 * (BM + BN) * kRowBytes : BM * (BN + 4) * 4];
+  const int tiles_n = (g.N + BN - 1) / BN, tiles_m = (g.M + BM - 1) / BM;
+  const int nwg = tiles_n * tiles_m * g.splitk;
+  int wg = blockIdx.x;
+  {
+    const int q = nwg / 8, r = nwg % 8, x = wg % 8;
+    wg = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + wg / 8;
+  }
+  const int split = wg % g.splitk;
+  wg /= g.splitk;
+  const int bm = (wg / tiles_n) * BM, bn = (wg % tiles_n) * BN;
+  const int t = threadIdx.x, lane = t & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
+  auto As = [&](int buf) { return smem + buf * ((BM + BN) * kRowBytes); };
+  auto Bs = [&](int buf) { return smem + buf * ((BM + BN) * kRowBytes) + BM * kRowBytes; };
+
+  floatx4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  // per-lane source row / swizzled chunk for the 4 instructions of this wave
+  const int lrow = lane >> 3, pchunk = lane & 7;
+  auto issue = [&](int k0, int buf) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int q = wave * 4 + i;                 // 1 KiB LDS chunk = rows q*8 .. q*8+7
+      const int r = q * 8 + lrow;
+      const int c = pchunk ^ (r & 7);             // logical k-chunk this lane must fetch
+      const int ga = min(bm + r, g.M - 1), gb = min(bn + r, g.N - 1);
+      __builtin_amdgcn_global_load_lds((const void*)(g.A + (size_t)ga * g.lda + k0 + c * 8),
+                                       (__attribute__((address_space(3))) void*)(As(buf) + q * 1024), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(g.B + (size_t)gb * g.ldb + k0 + c * 8),
+                                       (__attribute__((address_space(3))) void*)(Bs(buf) + q * 1024), 16, 0, 0);
+    }
+  };
+  const int nk_all = g.K / BK;
+  const int per = (nk_all + g.splitk - 1) / g.splitk;
+  const int kt0 = split * per;
+  const int nk = max(0, min(nk_all, kt0 + per) - kt0);
+  if (nk > 0) issue(kt0 * BK, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) issue((kt0 + kt + 1) * BK, cur ^ 1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 af[4], bf[4];
+      const int chunk = ks * 4 + (lane >> 4);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int ra_ = wm + i * 16 + (lane & 15);
+        af[i] = *reinterpret_cast<const bf16x8*>(As(cur) + ra_ * kRowBytes + ((chunk ^ (ra_ & 7)) << 4));
+        const int rb_ = wn + i * 16 + (lane & 15);
+        bf[i] = *reinterpret_cast<const bf16x8*>(Bs(cur) + rb_ * kRowBytes + ((chunk ^ (rb_ & 7)) << 4));
+      }
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf[j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  store_tile(g, acc, smem, bm, bn, wm, wn, split, t, lane);
+}
+
 // ---------------------------------------------------------------------------
 // "TN" GEMM for weight gradients: C[N1,N2] (+)= alpha * sum_m A[m,n1] * B[m,n2]
 // with A [M][N1] and B [M][N2] row-major (n contiguous), i.e. dW = dY^T X
@@ -383,7 +467,10 @@ void gemm_nt(uint64_t A, uint64_t B, uint64_t C, uint64_t bias, int M, int N, in
              reinterpret_cast<const void*>(bias), M, N, K, lda, ldb, ldc, alpha, accumulate ? 1 : 0, bias_kind,
              act, out_bf16 ? 1 : 0, splitk};
   const int nwg = ((M + BM - 1) / BM) * ((N + BN - 1) / BN) * splitk;
-  hipLaunchKernelGGL(k_gemm_nt, dim3(nwg), dim3(NT), 0, reinterpret_cast<hipStream_t>(stream), g);
+  if (K % BK == 0 && g_use_glds)
+    hipLaunchKernelGGL(k_gemm_nt_glds, dim3(nwg), dim3(NT), 0, reinterpret_cast<hipStream_t>(stream), g);
+  else
+    hipLaunchKernelGGL(k_gemm_nt, dim3(nwg), dim3(NT), 0, reinterpret_cast<hipStream_t>(stream), g);
   CCMPI_HIP_CHECK(hipGetLastError());
 }
 
@@ -423,6 +510,7 @@ void register_gemm_ops(pybind11::module_& m) {
         pybind11::call_guard<pybind11::gil_scoped_release>());
   m.def("gemm_tn", &gemm_tn, "C[N1,N2] (+)= alpha*A[M,N1]^T.B[M,N2] (fp32 out, split-K atomics)",
         pybind11::call_guard<pybind11::gil_scoped_release>());
+  m.def("gemm_set_glds", [](bool on) { g_use_glds = on; }, "select LDS-DMA (True) or register staging");
   m.def("transpose16", &transpose16, "dst[C,R] = src[R,C]^T for 16-bit elements",
         pybind11::call_guard<pybind11::gil_scoped_release>());
 }
