@@ -133,11 +133,18 @@ class Communicator(object):
             self.comm.Reduce_scatter_block(src_array, dest_array, op)
 
     def Split(self, key, color):
-        """Note the reference's positional order ``(key, color)`` (comm.py:38)."""
+        """Note the reference's positional order ``(key, color)`` (comm.py:38).
+
+        The child starts with a fresh byte counter.  When this communicator
+        already has an RCCL communicator, the child's is derived with
+        ncclCommSplit (collective over this communicator) instead of being
+        bootstrapped from scratch."""
         child = self.comm.Split(key=key, color=color)
-        if child is MPI.COMM_NULL:
-            return None
-        return __class__(child, self._device)
+        out = None if child is MPI.COMM_NULL else __class__(child, self._device)
+        if self._dev is not None and self._dev._rccl:
+            cdev = out.dev if out is not None else None
+            self._dev.split_rccl_into(cdev, -1 if out is None else int(color), int(key))
+        return out
 
     def Alltoall(self, src_array, dest_array, algo: str = "direct"):
         nprocs = self.comm.Get_size()

@@ -54,6 +54,15 @@ PYBIND11_MODULE(_device, m) {
         d.rccl_init(u);
       })
       .def_property_readonly("rccl_ready", &DeviceComm::rccl_ready)
+      .def("rccl_split_from", [](DeviceComm& d, DeviceComm* parent, int color, int key) {
+        py::gil_scoped_release g;
+        d.rccl_split_from(parent, color, key);
+      })
+      .def_static("rccl_split_nocolor", [](DeviceComm* parent) {
+        py::gil_scoped_release g;
+        // a parent rank that joins no child still takes part in the split
+        DeviceComm::rccl_split_leave(parent);
+      })
       .def("rccl_allreduce", &DeviceComm::rccl_allreduce, py::call_guard<py::gil_scoped_release>())
       .def("rccl_reduce_scatter", &DeviceComm::rccl_reduce_scatter, py::call_guard<py::gil_scoped_release>())
       .def("rccl_allgather", &DeviceComm::rccl_allgather, py::call_guard<py::gil_scoped_release>())

@@ -469,6 +469,21 @@ void DeviceComm::rccl_init(const std::string& uid) {
   CCMPI_NCCL_CHECK(ncclCommInitRank(&nccl_, size_, id, rank_));
 }
 
+void DeviceComm::rccl_split_from(DeviceComm* parent, int color, int key) {
+  if (!parent || !parent->nccl_) throw std::runtime_error("ccmpi: parent has no RCCL communicator to split");
+  CCMPI_HIP_CHECK(hipSetDevice(device_));
+  ncclComm_t child = nullptr;
+  CCMPI_NCCL_CHECK(ncclCommSplit(parent->nccl_, color < 0 ? NCCL_SPLIT_NOCOLOR : color, key, &child, nullptr));
+  if (color >= 0) nccl_ = child;
+}
+
+void DeviceComm::rccl_split_leave(DeviceComm* parent) {
+  if (!parent || !parent->nccl_) throw std::runtime_error("ccmpi: parent has no RCCL communicator to split");
+  CCMPI_HIP_CHECK(hipSetDevice(parent->device_));
+  ncclComm_t none = nullptr;
+  CCMPI_NCCL_CHECK(ncclCommSplit(parent->nccl_, NCCL_SPLIT_NOCOLOR, 0, &none, nullptr));
+}
+
 #define CCMPI_NEED_RCCL() \
   if (!nccl_) throw std::runtime_error("ccmpi: RCCL communicator not initialised")
 

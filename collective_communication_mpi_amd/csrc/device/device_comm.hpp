@@ -75,6 +75,9 @@ class DeviceComm {
   // ---- RCCL (vendor library: baseline + P2P transport) ---------------------
   static std::string rccl_unique_id();
   void rccl_init(const std::string& uid);
+  // collective over the PARENT's RCCL comm (every parent rank calls; color < 0 = not a member)
+  void rccl_split_from(DeviceComm* parent, int color, int key);
+  static void rccl_split_leave(DeviceComm* parent);
   bool rccl_ready() const { return nccl_ != nullptr; }
   void rccl_allreduce(uint64_t in, uint64_t out, uint64_t count, int dtype, int op, uint64_t stream);
   void rccl_reduce_scatter(uint64_t in, uint64_t out, uint64_t count, int dtype, int op, uint64_t stream);

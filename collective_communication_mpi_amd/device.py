@@ -173,6 +173,19 @@ class DeviceGroup:
         self.dc.rccl_init(uid)
         self._rccl = True
 
+    def split_rccl_into(self, child: Optional["DeviceGroup"], color: int, key: int) -> None:
+        """Collective over THIS group's ranks: derive the child group's RCCL
+        communicator with ncclCommSplit (shares the parent's RCCL resources)
+        instead of a fresh unique-id bootstrap.  ``child`` is None on ranks
+        that join no child (UNDEFINED color)."""
+        if not self._rccl:
+            return
+        if child is None:
+            self.D.DeviceComm.rccl_split_nocolor(self.dc)
+            return
+        child.dc.rccl_split_from(self.dc, color, key)
+        child._rccl = True
+
     # ----------------------------------------------------------------- helpers
     def _stream(self) -> int:
         return self.torch.cuda.current_stream(self.device).cuda_stream

@@ -99,6 +99,21 @@ def test_single_rank_communicator_paths():
     assert comm.total_bytes_transferred == 0  # p = 1: no traffic in any formula
 
 
+def test_split_derives_rccl_communicator():
+    """Split of a communicator that has RCCL derives the child's via ncclCommSplit."""
+    from collective_communication_mpi_amd import MPI, Communicator
+
+    comm = Communicator(MPI.COMM_WORLD)
+    comm.dev.ensure_rccl()
+    child = comm.Split(key=0, color=0)
+    assert child.dev._rccl
+    x = torch.arange(4096, device="cuda", dtype=torch.float32)
+    y = torch.empty_like(x)
+    child.Allreduce(x, y, MPI.SUM, algo="rccl")
+    torch.cuda.synchronize()
+    torch.testing.assert_close(y, x)
+
+
 @pytest.mark.parametrize("M,N1,N2", [(64, 16, 128), (32768, 384, 768), (32768, 768, 64), (1000, 136, 72), (7, 8, 8)])
 @pytest.mark.parametrize("splitk", [1, 4, None])
 def test_gemm_tn_weight_grad(M, N1, N2, splitk):

@@ -54,3 +54,18 @@ def test_native_reduce_matches_numpy(dt, op, n, seed):
         np.testing.assert_allclose(out, ref, rtol=1e-3 if dt == "float16" else 1e-6)
     else:
         np.testing.assert_array_equal(out, ref)
+
+
+@pytest.mark.skipif(not __import__("os").path.exists("/opt/conda/bin/mpiexec"), reason="no Hydra mpiexec")
+def test_runs_under_hydra_mpiexec():
+    """The host plane bootstraps from Hydra's PMI_RANK/PMI_SIZE too (reference launcher: mpirun/mpiexec)."""
+    import os
+    import subprocess
+
+    from _launch import REPO
+
+    env = dict(os.environ, PYTHONPATH=REPO, CCMPI_TIMEOUT="60")
+    r = subprocess.run(["/opt/conda/bin/mpiexec", "-n", "4", "python", "tests/workers/host_worker.py"], cwd=REPO,
+                       env=env, capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "host plane OK at 4 ranks" in r.stdout
