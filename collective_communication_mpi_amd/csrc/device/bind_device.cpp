@@ -73,6 +73,7 @@ PYBIND11_MODULE(_device, m) {
       .def("p2p_pairwise_alltoall", &DeviceComm::p2p_pairwise_alltoall, py::call_guard<py::gil_scoped_release>())
       .def("error_code", &DeviceComm::error_code, py::call_guard<py::gil_scoped_release>())
       .def("clear_error", &DeviceComm::clear_error)
+      .def("poll_error", &DeviceComm::poll_error)
       .def("reset_state", &DeviceComm::reset_state, py::call_guard<py::gil_scoped_release>())
       .def("set_inbox", &DeviceComm::set_inbox)
       .def_property_readonly("inbox_bytes", &DeviceComm::inbox_bytes)

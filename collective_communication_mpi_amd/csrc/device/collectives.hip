@@ -76,6 +76,7 @@ __device__ bool start_phase(const CollArgs& a, uint64_t* s_epoch, uint64_t (*cod
   bool ok = true;
   if (t < nr) {
     ok = wait_geq(&mine->flag[0][b][t], e, a.timeout_ticks, &mine->error, 0x100 + t);
+    if (!ok) report_host(pt, 0x100 + t);
     if (ok) {
       codes[0][t] = __hip_atomic_load(&mine->addr[0][b][t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       codes[1][t] = __hip_atomic_load(&mine->addr[1][b][t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -98,7 +99,10 @@ __device__ bool sync_phase(const CollArgs& a, int phase, uint64_t e) {
     signal_store(&pt->sig[t]->flag[phase][b][me], e);
   }
   bool ok = true;
-  if (t < nr) ok = wait_geq(&mine->flag[phase][b][t], e, a.timeout_ticks, &mine->error, 0x100 * (phase + 1) + t);
+  if (t < nr) {
+    ok = wait_geq(&mine->flag[phase][b][t], e, a.timeout_ticks, &mine->error, 0x100 * (phase + 1) + t);
+    if (!ok) report_host(pt, 0x100 * (phase + 1) + t);
+  }
   ok = __syncthreads_and(ok);
   return ok;
 }

@@ -71,6 +71,7 @@ struct PeerTable {
   Signals* sig[kMaxRanks];               // sig[j]: rank j's signal buffer (mapped)
   char* seg[kMaxRanks][kMaxSegs];        // seg[j][s]: base of rank j's segment s
   uint64_t seg_bytes[kMaxSegs];
+  uint32_t* host_err;                    // pinned host word mirroring sig[rank]->error (watchdog)
   int rank;
   int size;
   int nsegs;
@@ -134,6 +135,11 @@ __device__ __forceinline__ bool wait_geq(const uint64_t* p, uint64_t want, uint6
     }
   }
   return true;
+}
+
+// Mirror a timeout code into the host-mapped watchdog word (no device sync needed to see it).
+__device__ __forceinline__ void report_host(const PeerTable* pt, uint32_t code) {
+  if (pt->host_err) __hip_atomic_store(pt->host_err, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 __device__ __forceinline__ void signal_store(uint64_t* p, uint64_t v) {

@@ -92,6 +92,10 @@ DeviceComm::DeviceComm(int rank, int size, int device, uint64_t /*scratch_bytes*
   peer_sig_.assign(size, nullptr);
   peer_sig_[rank] = sig_;
   host_pt_.sig[rank] = sig_;
+  CCMPI_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&host_err_), sizeof(uint32_t),
+                                hipHostMallocMapped | hipHostMallocCoherent));
+  *host_err_ = 0;
+  CCMPI_HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&host_pt_.host_err), host_err_, 0));
   if (const char* t = std::getenv("CCMPI_DEVICE_TIMEOUT_S")) set_timeout_seconds(std::atof(t));
   if (const char* c = std::getenv("CCMPI_COPY_ENGINE")) copy_engine_ = std::atoi(c) != 0;
   CCMPI_HIP_CHECK(hipDeviceSynchronize());
@@ -106,6 +110,7 @@ DeviceComm::~DeviceComm() {
   if (sig_) (void)hipFree(sig_);
   if (epochs_) (void)hipFree(epochs_);
   if (dev_pt_) (void)hipFree(dev_pt_);
+  if (host_err_) (void)hipHostFree(host_err_);
 }
 
 void DeviceComm::sync_table_() {
@@ -677,9 +682,15 @@ void DeviceComm::reset_state() {
   CCMPI_HIP_CHECK(hipMemset(sig_, 0, sizeof(Signals)));
   CCMPI_HIP_CHECK(hipMemset(epochs_, 0, sizeof(uint64_t) * kMaxBlocks));
   CCMPI_HIP_CHECK(hipDeviceSynchronize());
+  __atomic_store_n(host_err_, 0u, __ATOMIC_RELEASE);
+}
+
+uint32_t DeviceComm::poll_error() const {
+  return __atomic_load_n(host_err_, __ATOMIC_ACQUIRE);
 }
 
 void DeviceComm::clear_error() {
+  __atomic_store_n(host_err_, 0u, __ATOMIC_RELEASE);
   CCMPI_HIP_CHECK(hipSetDevice(device_));
   CCMPI_HIP_CHECK(hipMemset(&sig_->error, 0, sizeof(uint32_t)));
 }

@@ -94,6 +94,7 @@ class DeviceComm {
 
   // ---- health ------------------------------------------------------------
   uint32_t error_code();  // synchronises; 0 = ok
+  uint32_t poll_error() const;  // non-blocking read of the host-mapped mirror (watchdog)
   void clear_error();
   // zero flags + epochs (call on every rank between host barriers, no kernel in flight)
   void reset_state();
@@ -116,6 +117,7 @@ class DeviceComm {
   std::vector<SegInfo> segs_;            // [0] = scratch
   std::vector<std::vector<char*>> peer_seg_;  // [seg][rank]
   PeerTable host_pt_{};
+  uint32_t* host_err_ = nullptr;         // pinned, device-mapped timeout mirror
   PeerTable* dev_pt_ = nullptr;
   uint64_t* epochs_ = nullptr;
   uint64_t timeout_ticks_ = 2000000000ull;  // 20 s

@@ -104,6 +104,46 @@ class DeviceGroup:
         self.oneshot_max = _env_int("CCMPI_ONESHOT_MAX_BYTES", 256 << 10)
         self.tuned: Dict[Tuple[int, int], str] = {}
         self._lock = threading.Lock()
+        self._watchdog: Optional[threading.Thread] = None
+        mode = os.environ.get("CCMPI_WATCHDOG", "warn").lower()
+        if mode in ("warn", "abort"):
+            self.start_watchdog(mode)
+
+    # ---------------------------------------------------------------- watchdog
+    def start_watchdog(self, mode: str = "warn", period_s: float = 0.2) -> None:
+        """Host-side watchdog.  Device kernels never hang: every
+        spin is bounded (``CCMPI_DEVICE_TIMEOUT_S``) and a timeout writes a
+        rank/phase/peer code into pinned host memory.  This daemon thread polls
+        that word *without* synchronising the device and reports it once per
+        code (``warn``), or prints a rank-tagged message and aborts the whole
+        process (``abort``) so the launcher tears the job down."""
+        if self._watchdog is not None:
+            return
+        dc, rank = self.dc, self.rank
+        stop = self._wd_stop = threading.Event()
+
+        def run():
+            import sys
+
+            last = 0
+            while not stop.wait(period_s):
+                code = dc.poll_error()
+                if code and code != last:
+                    msg = (f"[ccmpi watchdog] rank {rank}: device collective timed out "
+                           f"(code 0x{code:x}: phase {code >> 8}, waiting on peer {code & 0xff})")
+                    print(msg, file=sys.stderr, flush=True)
+                    if mode == "abort":
+                        os._exit(70)
+                last = code
+
+        self._watchdog = threading.Thread(target=run, name=f"ccmpi-watchdog-{rank}", daemon=True)
+        self._watchdog.start()
+
+    def stop_watchdog(self) -> None:
+        if self._watchdog is not None:
+            self._wd_stop.set()
+            self._watchdog.join()
+            self._watchdog = None
 
     # ------------------------------------------------------------------ memory
     def _register(self, t) -> int:

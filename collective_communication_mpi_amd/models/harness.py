@@ -20,6 +20,7 @@ import numpy as np
 import torch
 
 from ..data.preprocess import synthetic_mnist
+from ..utils import checkpoint as ckpt
 from .mnist_tp import LayerConfig, MnistTPLayer, local_batch, patchify
 
 
@@ -134,6 +135,9 @@ def main(argv=None) -> int:
     ap.add_argument("--lr", type=float, default=2e-3)
     ap.add_argument("--fc-o-mode", default="row")
     ap.add_argument("--log", default="")
+    ap.add_argument("--ckpt", default="", help="checkpoint directory (sharded, safetensors)")
+    ap.add_argument("--save-every", type=int, default=0, help="save every K steps (and at the end)")
+    ap.add_argument("--resume", action="store_true", help="continue from --ckpt if it holds a checkpoint")
     args = ap.parse_args(argv)
     comm = Communicator(MPI.COMM_WORLD)
     local = int(os.environ.get("LOCAL_RANK", os.environ.get("CCMPI_LOCAL_RANK", "0")))
@@ -141,13 +145,28 @@ def main(argv=None) -> int:
     cfg, layer, x_all, y_all = build(comm, args.tp, args.batch, lr=args.lr, fc_o_mode=args.fc_o_mode)
     hc = _hc(comm)
     losses = []
-    for step in range(args.steps):
+    start = 0
+    if args.resume and args.ckpt and ckpt.latest(args.ckpt):
+        start = ckpt.load_sharded(args.ckpt, layer.flat, comm, layer.tp_idx, cfg.tp)["step"]
+        if comm.Get_rank() == 0:
+            print(f"resumed from {args.ckpt} at step {start}", flush=True)
+
+    def save():
+        ckpt.save_sharded(args.ckpt, layer.flat, comm, layer.tp_idx, layer.dp_idx, cfg.tp, cfg.dp,
+                          meta={"batch": cfg.batch, "lr": cfg.lr, "fc_o_mode": cfg.fc_o_mode})
+
+    for step in range(start, args.steps):
+        # the data position is a function of the step, so a resumed run sees the same batches
         xb, yb = local_batch(cfg, x_all, y_all, step, comm.Get_rank(), layer.device)
         loss = train_step(layer, cfg, xb, yb)
         lv = hc.allreduce(float(loss.item()), op=MPI.SUM) / cfg.tp
         losses.append(lv)
         if comm.Get_rank() == 0:
             print(f"step {step} loss {lv:.5f}", flush=True)
+        if args.ckpt and args.save_every and (step + 1) % args.save_every == 0:
+            save()
+    if args.ckpt and args.save_every:
+        save()
     if args.log and comm.Get_rank() == 0:
         np.save(args.log, np.array(losses))
     return 0

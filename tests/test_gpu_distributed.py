@@ -21,6 +21,17 @@ def test_device_collectives_multi_rank(n):
     run_ranks(n, py("tests/workers/device_worker.py", "--quick"), timeout=400, env=ENV)
 
 
+@pytest.mark.parametrize("n", [2, 4])
+def test_device_collectives_random_skew(n):
+    """Randomised per-rank host/device delays, back-to-back calls."""
+    run_ranks(n, py("tests/workers/device_worker.py", "--stress", "120"), timeout=300, env=ENV)
+
+
+def test_device_timeout_watchdog_and_recovery():
+    """A rank that skips a collective: bounded spins, host watchdog, reset."""
+    run_ranks(2, py("tests/workers/device_worker.py", "--fault"), timeout=120, env=dict(ENV, CCMPI_WATCHDOG="warn"))
+
+
 @pytest.fixture(scope="module")
 def reference_run(tmp_path_factory):
     out = tmp_path_factory.mktemp("h") / "ref.npz"
@@ -38,3 +49,18 @@ def test_harness_matches_single_rank(reference_run, tmp_path, n, tp, mode):
     for k in ("q_w", "o_w", "emb_w"):
         np.testing.assert_allclose(got[k], reference_run[k], rtol=5e-2, atol=5e-3)
     assert got["losses"][-1] < got["losses"][0]
+
+
+def test_harness_checkpoint_resume(tmp_path):
+    """6 straight steps == 3 steps, checkpoint, resume, 3 more (dp=1 x tp=2)."""
+    H = ["-m", "collective_communication_mpi_amd.models.harness", "--tp", "2", "--batch", "128"]
+    a = tmp_path / "a.npy"
+    c = tmp_path / "c.npy"
+    ck = str(tmp_path / "ck")
+    run_ranks(2, py(*H, "--steps", "6", "--log", str(a)), timeout=300, env=ENV)
+    run_ranks(2, py(*H, "--steps", "3", "--ckpt", ck, "--save-every", "3"), timeout=300, env=ENV)
+    r = run_ranks(2, py(*H, "--steps", "6", "--ckpt", ck, "--resume", "--log", str(c)), timeout=300, env=ENV)
+    assert "resumed from" in r.stdout and "at step 3" in r.stdout
+    la, lc = np.load(a), np.load(c)
+    assert lc.shape == (3,)
+    np.testing.assert_allclose(lc, la[3:], rtol=2e-3, atol=1e-4)

@@ -69,3 +69,12 @@ def test_runs_under_hydra_mpiexec():
                        env=env, capture_output=True, text=True, timeout=180)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "host plane OK at 4 ranks" in r.stdout
+
+
+@pytest.mark.parametrize("n,tp", [(2, 2), (4, 2), (3, 1)])
+def test_sharded_checkpoint_roundtrip(tmp_path, n, tp):
+    """Harness checkpoint/resume: DP replica 0 writes, every rank restores."""
+    from _launch import py, run_ranks
+
+    r = run_ranks(n, py("tests/workers/ckpt_worker.py", str(tmp_path / "ck"), str(tp)), timeout=120)
+    assert r.stdout.count("checkpoint OK") == n

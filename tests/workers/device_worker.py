@@ -3,7 +3,15 @@ share one GPU).  Every device collective is compared with a torch fp64/exact
 oracle built from all ranks' inputs (inputs are generated from per-rank seeds,
 so each rank can rebuild every peer's input locally).
 
-usage: device_worker.py [--quick] [--rccl] [--sizes 1,17,4096,...]
+usage: device_worker.py [--quick] [--rccl] [--sizes 1,17,4096,...] [--stress N] [--fault]
+
+--stress N  SURVEY §5.2: N back-to-back collectives (mixed algorithms and sizes,
+            no host synchronisation in between) with randomised per-rank host
+            sleeps and device-side spin delays, so ranks arrive at each kernel
+            in random order; every result is checked at the end (epoch/ABA safety).
+--fault     SURVEY §5.3: rank p-1 skips one collective; the others must time out
+            (bounded spins), the host watchdog must see the code without a device
+            sync, check() must raise, and reset() must restore a working group.
 """
 import argparse
 import os
@@ -19,6 +27,8 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--quick", action="store_true")
 ap.add_argument("--rccl", action="store_true")
 ap.add_argument("--sizes", default="")
+ap.add_argument("--stress", type=int, default=0)
+ap.add_argument("--fault", action="store_true")
 args = ap.parse_args()
 
 comm = Communicator(MPI.COMM_WORLD)
@@ -62,6 +72,76 @@ def check(name, got, want, dtype, nterms=1):
         fails.append(f"{name}: max diff {diff}")
     return ok
 
+
+def stress(iters):
+    """Random arrival order at every collective; results checked after the burst."""
+    import random
+
+    rng = random.Random(1234 + rank)  # per-rank: delays only
+    shared = random.Random(99)        # identical on every rank: sizes and algorithms
+    pending = []
+    algos_s = ["oneshot", "twoshot", "push", "reduce_bcast"]
+    sym_x = dev.empty(1 << 16, torch.float32)
+    for i in range(iters):
+        n = shared.choice([1, 33, 4096, 1 << 16])
+        algo = shared.choice(algos_s)
+        d = rng.random()
+        if d < 0.3:
+            time.sleep(rng.random() * 0.004)
+        elif d < 0.6:
+            torch.cuda._sleep(rng.randint(1000, 200000))  # device-side skew
+        x = gen(rank, n, torch.float32, 50000 + i).to(dev.device, non_blocking=True)
+        if i % 3 == 0:  # symmetric, zero-copy path
+            xs = sym_x[:n]
+            xs.copy_(x)
+            x = xs
+        y = torch.empty(n, dtype=torch.float32, device=dev.device)
+        dev.allreduce(x, y, "SUM", algo)
+        pending.append((f"stress[{i},{algo},n={n}]", y.clone(), n, 50000 + i))
+    torch.cuda.synchronize()
+    dev.check()
+    for name, y, n, sl in pending:
+        check(name, y, oracle(n, torch.float32, "SUM", sl), torch.float32, p)
+
+
+def fault():
+    """One rank misses a collective; the rest time out, report, and recover."""
+    dev.dc.set_timeout_seconds(0.5)
+    x = dev.empty(4096, torch.float32)
+    x.fill_(1.0)
+    y = dev.empty(4096, torch.float32)
+    torch.cuda.synchronize()
+    comm.comm.Barrier()
+    if rank != p - 1:
+        dev.allreduce(x, y, "SUM", "twoshot")
+        t0 = time.time()
+        while not dev.dc.poll_error() and time.time() - t0 < 10:
+            time.sleep(0.05)  # the watchdog word is host-mapped: no device sync here
+        if not dev.dc.poll_error():
+            fails.append("fault: host-mapped watchdog word never set")
+        try:
+            dev.check()
+            fails.append("fault: check() did not raise after a timeout")
+        except RuntimeError as e:
+            if f"rank {rank}" not in str(e):
+                fails.append(f"fault: message not rank-tagged: {e}")
+    dev.reset()
+    dev.dc.set_timeout_seconds(20.0)
+    dev.allreduce(x, y, "SUM", "twoshot")
+    check("fault_recovery_allreduce", y, torch.full((4096,), float(p), dtype=torch.float64), torch.float32)
+
+
+if args.stress or args.fault:
+    t0 = time.time()
+    if args.stress:
+        stress(args.stress)
+    if args.fault:
+        fault()
+    comm.Barrier()
+    print(f"[rank {rank}/{p}] stress/fault checks: {len(fails)} failures, {time.time() - t0:.1f}s", flush=True)
+    for f in fails[:20]:
+        print(f"[rank {rank}] FAIL {f}", flush=True)
+    sys.exit(1 if fails else 0)
 
 sizes = [int(s) for s in args.sizes.split(",") if s] or ([1, 7, 1000, 65536 + 3] if args.quick else
                                                           [1, 3, 8, 1000, 4097, 65536 + 3, 1 << 20, (1 << 22) + 5])
