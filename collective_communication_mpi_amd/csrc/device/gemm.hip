@@ -22,147 +22,39 @@
 #include <cstdlib>
 
 #include "common.hpp"
+#include "gemm_common.hpp"
 #include "ops.hpp"
 
 namespace ccmpi {
 namespace dev {
 
 namespace {
-
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef float floatx4 __attribute__((ext_vector_type(4)));
+using namespace gemm;
 
 constexpr int BM = 128, BN = 128, BK = 64, NT = 256;
 bool g_use_glds = std::getenv("CCMPI_GEMM_NO_GLDS") == nullptr;  // A/B switch (benchmarks)
+// kernel choice for gemm_nt: 0 auto, 1 = 128x128 only, 2 = 256x256 / 3 = 256x128 whenever legal
+int g_kernel = std::getenv("CCMPI_GEMM_KERNEL") ? std::atoi(std::getenv("CCMPI_GEMM_KERNEL")) : 0;
 constexpr int kRowBytes = BK * 2;  // 128 B per LDS row
 
-struct GemmArgs {
-  const uint16_t* A;
-  const uint16_t* B;
-  void* C;
-  const void* bias;
-  int M, N, K;
-  int lda, ldb, ldc;
-  float alpha;
-  int accumulate;  // C += result
-  int bias_kind;   // 0 none, 1 fp32, 2 bf16
-  int act;         // 0 none, 1 relu, 2 gelu(tanh)
-  int out_bf16;    // 0 fp32 out, 1 bf16 out
-  int splitk;      // >1: K split over workgroups, fp32 atomic-add epilogue into C
-};
-
-__device__ __forceinline__ float bf2f(uint16_t h) { return __uint_as_float((uint32_t)h << 16); }
-
-__device__ __forceinline__ float gelu_tanh(float x) {
-  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
-  return 0.5f * x * (1.f + tanhf(k0 * (x + k1 * x * x * x)));
-}
-
-// Shared epilogue of both GEMM kernels (see the comment inside).
+// Shared epilogue of the 128x128 kernels: lane holds D[4*(lane>>4) + r][lane & 15]
+// of each 16x16 tile.  Stage the (alpha, bias, act)-applied fp32 tile through
+// LDS (the A/B buffers are dead now), then write whole rows (store_rows).
 __device__ __forceinline__ void store_tile(const GemmArgs& g, floatx4 (&acc)[4][4], unsigned char* smem, int bm,
                                            int bn, int wm, int wn, int split, int t, int lane) {
-  // epilogue: lane holds D[4*(lane>>4) + r][lane & 15] of each 16x16 tile.
-  // Stage the (alpha, bias, act)-applied fp32 tile through LDS (the A/B
-  // buffers are dead now), then write whole rows with 16-B vectors (or, for
-  // split-K, lane-consecutive fp32 atomics: 256 contiguous bytes per wave
-  // instruction).  Falls back to per-element stores when C rows are not
-  // 16-B aligned.
   float* tile = reinterpret_cast<float*>(smem);
   constexpr int TS = BN + 4;  // fp32 row stride in LDS
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int cl = wn + j * 16 + (lane & 15);
-    const int col = bn + cl;
-    float b = 0.f;
-    if (split == 0 && col < g.N) {
-      if (g.bias_kind == 1) b = reinterpret_cast<const float*>(g.bias)[col];
-      else if (g.bias_kind == 2) b = bf2f(reinterpret_cast<const uint16_t*>(g.bias)[col]);
-    }
+    const float b = load_bias(g, bn + cl, split);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int rl = wm + i * 16 + (lane >> 4) * 4 + r;
-        float v = g.alpha * acc[i][j][r] + b;
-        if (g.act == 1) v = fmaxf(v, 0.f);
-        else if (g.act == 2) v = gelu_tanh(v);
-        tile[rl * TS + cl] = v;
-      }
-    }
+      for (int r = 0; r < 4; ++r) tile[(wm + i * 16 + (lane >> 4) * 4 + r) * TS + cl] = epi(g, acc[i][j][r], b);
   }
   __syncthreads();
-  const int es = g.out_bf16 ? 2 : 4;
-  const bool vec_ok = (((uint64_t)g.C | ((uint64_t)g.ldc * es)) % 16) == 0;
-  if (g.splitk > 1) {
-    // 64 lanes -> 64 consecutive columns of one row
-    for (int idx = t; idx < BM * BN; idx += NT) {
-      const int rl = idx / BN, cl = idx % BN;
-      const int row = bm + rl, col = bn + cl;
-      if (row < g.M && col < g.N) atomicAdd(reinterpret_cast<float*>(g.C) + (size_t)row * g.ldc + col, tile[rl * TS + cl]);
-    }
-  } else if (vec_ok) {
-    const int per_vec = 16 / es;             // elements per 16-B vector
-    const int vecs_row = BN / per_vec;
-    for (int idx = t; idx < BM * vecs_row; idx += NT) {
-      const int rl = idx / vecs_row, cl = (idx % vecs_row) * per_vec;
-      const int row = bm + rl, col = bn + cl;
-      if (row >= g.M || col >= g.N) continue;
-      const float* src = tile + rl * TS + cl;
-      if (col + per_vec <= g.N) {
-        if (g.out_bf16) {
-          uint16_t* C = reinterpret_cast<uint16_t*>(g.C) + (size_t)row * g.ldc + col;
-          uint4 o;
-          uint32_t w[4];
-          if (g.accumulate) {
-            const uint4 old = *reinterpret_cast<const uint4*>(C);
-            const uint32_t ow[4] = {old.x, old.y, old.z, old.w};
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-              w[q] = f32_to_bf16_bits(src[2 * q] + bf16_lo(ow[q])) | (f32_to_bf16_bits(src[2 * q + 1] + bf16_hi(ow[q])) << 16);
-          } else {
-#pragma unroll
-            for (int q = 0; q < 4; ++q) w[q] = f32_to_bf16_bits(src[2 * q]) | (f32_to_bf16_bits(src[2 * q + 1]) << 16);
-          }
-          o.x = w[0]; o.y = w[1]; o.z = w[2]; o.w = w[3];
-          *reinterpret_cast<uint4*>(C) = o;
-        } else {
-          float* C = reinterpret_cast<float*>(g.C) + (size_t)row * g.ldc + col;
-          float4 v = make_float4(src[0], src[1], src[2], src[3]);
-          if (g.accumulate) {
-            const float4 old = *reinterpret_cast<const float4*>(C);
-            v.x += old.x; v.y += old.y; v.z += old.z; v.w += old.w;
-          }
-          *reinterpret_cast<float4*>(C) = v;
-        }
-      } else {
-        for (int q = 0; q < per_vec && col + q < g.N; ++q) {
-          const size_t o = (size_t)row * g.ldc + col + q;
-          if (g.out_bf16) {
-            uint16_t* C = reinterpret_cast<uint16_t*>(g.C);
-            C[o] = (uint16_t)f32_to_bf16_bits(src[q] + (g.accumulate ? bf2f(C[o]) : 0.f));
-          } else {
-            float* C = reinterpret_cast<float*>(g.C);
-            C[o] = src[q] + (g.accumulate ? C[o] : 0.f);
-          }
-        }
-      }
-    }
-  } else {
-    for (int idx = t; idx < BM * BN; idx += NT) {
-      const int rl = idx / BN, cl = idx % BN;
-      const int row = bm + rl, col = bn + cl;
-      if (row >= g.M || col >= g.N) continue;
-      const size_t o = (size_t)row * g.ldc + col;
-      const float v = tile[rl * TS + cl];
-      if (g.out_bf16) {
-        uint16_t* C = reinterpret_cast<uint16_t*>(g.C);
-        C[o] = (uint16_t)f32_to_bf16_bits(v + (g.accumulate ? bf2f(C[o]) : 0.f));
-      } else {
-        float* C = reinterpret_cast<float*>(g.C);
-        C[o] = v + (g.accumulate ? C[o] : 0.f);
-      }
-    }
-  }
+  store_rows<BM, BN, NT>(g, tile, TS, bm, bn, t);
 }
 
 __global__ void __launch_bounds__(NT) k_gemm_nt(GemmArgs g) {
@@ -467,6 +359,22 @@ void gemm_nt(uint64_t A, uint64_t B, uint64_t C, uint64_t bias, int M, int N, in
              reinterpret_cast<const void*>(bias), M, N, K, lda, ldb, ldc, alpha, accumulate ? 1 : 0, bias_kind,
              act, out_bf16 ? 1 : 0, splitk};
   const int nwg = ((M + BM - 1) / BM) * ((N + BN - 1) / BN) * splitk;
+  // 256 x {256, 128} ping-pong kernels: need K % 128 and enough tiles to
+  // occupy the 256 CUs (one block per CU); smaller grids keep 128x128.
+  const bool big_ok = K % (2 * BK) == 0 && g_use_glds;
+  if (big_ok && g_kernel != 1) {
+    int bn = 0;
+    if (g_kernel == 2) bn = 256;
+    else if (g_kernel == 3) bn = 128;
+    // measured (benchmarks/gemm_bench.py): 256x256 wins from ~4096^2 outputs up;
+    // narrow N (<= 1024) stays on 128x128 (2 blocks/CU balance better)
+    else if (gemm256_tiles(M, N, 256) * splitk >= 256 && M >= 1024 && N >= 1024) bn = 256;
+    if (bn) {
+      launch_gemm_nt_256(g, bn, reinterpret_cast<hipStream_t>(stream));
+      CCMPI_HIP_CHECK(hipGetLastError());
+      return;
+    }
+  }
   if (K % BK == 0 && g_use_glds)
     hipLaunchKernelGGL(k_gemm_nt_glds, dim3(nwg), dim3(NT), 0, reinterpret_cast<hipStream_t>(stream), g);
   else
@@ -511,6 +419,8 @@ void register_gemm_ops(pybind11::module_& m) {
   m.def("gemm_tn", &gemm_tn, "C[N1,N2] (+)= alpha*A[M,N1]^T.B[M,N2] (fp32 out, split-K atomics)",
         pybind11::call_guard<pybind11::gil_scoped_release>());
   m.def("gemm_set_glds", [](bool on) { g_use_glds = on; }, "select LDS-DMA (True) or register staging");
+  m.def("gemm_set_kernel", [](int k) { g_kernel = k; }, "gemm_nt tile choice: 0 auto, 1 128x128, 2 256x256, 3 256x128");
+  m.def("gemm_set_ablation", [](int e) { g_pp_exp = e; }, "ping-pong kernel ablation bits (benchmarks only)");
   m.def("transpose16", &transpose16, "dst[C,R] = src[R,C]^T for 16-bit elements",
         pybind11::call_guard<pybind11::gil_scoped_release>());
 }

@@ -1,0 +1,319 @@
+// Large-tile bf16 "NT" GEMM: 8 waves in two ping-pong groups, LDS-DMA
+// (global_load_lds) staging with four half-tiles in flight, one MFMA quadrant
+// per phase.  Same contract and epilogue as k_gemm_nt (gemm.hip); requires
+// K % 128 == 0 (two K-tiles per main-loop iteration).  Two shapes:
+//   BN = 256: 256x256 tile, waves 2(M) x 4(N)   (large square-ish problems)
+//   BN = 128: 256x128 tile, waves 4(M) x 2(N)   (narrow N, e.g. N = 768)
+//
+// Block tile 256(M) x BN(N) x 64(K), 512 threads = 8 waves.
+//   * LDS: 2 buffers x {A rows 0-127, A rows 128-255, B rows 0..BN/2-1,
+//     B rows BN/2..BN-1} half-tiles (A: 16 KiB, B: BN/2 x 128 B).
+//   * Wave (wr, wc) owns rows {mh*128 + wr*(128/WR) + ...} and columns
+//     {nh*BN/2 + wc*32 + 0..31} for mh, nh in {0, 1}: every wave reads the
+//     SAME half-tiles in the same phase, so a half-tile is free to be restaged
+//     as soon as all waves are past its last read.
+//   * One K-tile = 4 phases, one (mh, nh) output quadrant (K = 64,
+//     v_mfma_f32_16x16x32_bf16) per phase, in the order (0,0) (0,1) (1,1)
+//     (1,0).  LDS reads per phase: A0+B0 | B1 | A1 | - (A and B0 fragments
+//     stay in registers across phases).
+//   * Every phase issues one half-tile of LDS-DMA and then waits with
+//     vmcnt(2*gA + 2*gB) (gA, gB = DMA instructions per wave for an A / B
+//     half-tile): the stage pattern repeats B,A,A,B, so exactly the half-tile
+//     issued four phases earlier is retired.  The stage order (below) puts each restage >= 2 phases after its
+//     half's last read and each retire >= 1 phase before its first read, which
+//     is what the ping-pong barrier pattern requires (analysis in gemm256_schedule
+//     comment).
+//   * Tile order: XCD-aware remap, then group-M (8 tile rows) so the 32 tiles an
+//     XCD runs at once form an 8 x 4 block (A and B panels shared in its L2).
+//   * Ping-pong: waves 4-7 execute one extra s_barrier up front, so while one
+//     group runs its 16 MFMAs between two barriers the other group issues its
+//     LDS reads and DMA; the MFMA cluster runs at s_setprio 1.
+//   * Epilogue: the fp32 tile goes through LDS in two 128-row halves and is
+//     written with the shared row store (bias / act / bf16 / accumulate /
+//     split-K atomics).
+//
+// gemm256_schedule: let phase p of group 0 sit between barriers #(2p-1) and
+// #(2p) and of group 1 between #2p and #(2p+1).  A wave's DMA is visible to a
+// reader once the issuing wave waited on it and the reader passed a later
+// barrier: retire at phase w -> readable from phase w+1 on.  A restage at
+// phase s may overwrite data last read at phase r when s >= r+2.  With
+// per-iteration phases P0..P7 (two K-tiles, buffers 0 then 1), the half-tile
+// staged at each phase is
+//   P0 buf1.B1(t+1) P1 buf1.A1(t+1) P2 buf0.A0(t+2) P3 buf0.B0(t+2)
+//   P4 buf0.B1(t+2) P5 buf0.A1(t+2) P6 buf1.A0(t+3) P7 buf1.B0(t+3)
+// (t = 2*iteration).  Last reads: buf0 A0,B0@P0 B1@P1 A1@P2; buf1 A0,B0@P4
+// B1@P5 A1@P6; first reads one iteration later at the same phases.  Each half
+// is staged 2 phases after its last read and retired 4 phases after staging,
+// at or before the phase preceding its first read.
+#include <hip/hip_runtime.h>
+
+#include "gemm_common.hpp"
+
+namespace ccmpi {
+namespace dev {
+namespace gemm {
+namespace {
+
+constexpr int PM = 256, PK = 64, PNT = 512, kGroupM = 8;
+constexpr int kAHalf = 128 * 128;                // bytes per A half-tile
+
+template <int BN>
+struct Geo {
+  static constexpr int WR = BN == 256 ? 2 : 4;   // wave rows
+  static constexpr int WC = 8 / WR;              // wave cols
+  static constexpr int MI = 8 / WR;              // 16-row MFMA tiles per wave strip and half
+  static constexpr int BHalf = (BN / 2) * 128;   // bytes per B half-tile
+  static constexpr int GA = 2, GB = BHalf / 1024 / 8;  // DMA instr per wave per half-tile
+  static constexpr int VM = 2 * GA + 2 * GB;     // steady-state vmcnt
+  static constexpr int Buf = 2 * kAHalf + 2 * BHalf;
+  static constexpr int EpiTS = BN + 4;
+  static constexpr int Lds = (2 * Buf > 128 * EpiTS * 4) ? 2 * Buf : 128 * EpiTS * 4;
+};
+
+enum Slot { A0 = 0, A1 = 1, B0 = 2, B1 = 3 };
+
+__device__ __forceinline__ void bar() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_barrier" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// EXP: ablation bits for benchmarks only (0 = production):
+//   1 = lax vmcnt (wait for nothing: WRONG results, isolates DMA-latency stalls)
+//   2 = no s_setprio around the MFMA cluster
+//   4 = no ping-pong stagger (both groups in lockstep)
+template <int BN, int EXP = 0>
+__global__ void __launch_bounds__(PNT, 1) k_gemm_nt_pp(GemmArgs g) {
+  using G = Geo<BN>;
+  extern __shared__ __attribute__((aligned(1024))) unsigned char smem[];
+  const int tiles_n = (g.N + BN - 1) / BN, tiles_m = (g.M + PM - 1) / PM;
+  const int nwg = tiles_n * tiles_m * g.splitk;
+  int wg = xcd_remap(blockIdx.x, nwg);
+  const int split = wg % g.splitk;
+  wg /= g.splitk;
+  int tm, tn;
+  {  // group-M order
+    const int per_group = kGroupM * tiles_n;
+    const int first_m = (wg / per_group) * kGroupM;
+    const int gm = min(tiles_m - first_m, kGroupM);
+    tm = first_m + (wg % per_group) % gm;
+    tn = (wg % per_group) / gm;
+  }
+  const int bm = tm * PM, bn = tn * BN;
+  const int t = threadIdx.x, lane = t & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wr = wave / G::WC, wc = wave % G::WC, grp = wave >> 2;
+
+  const int nk_all = g.K / PK;
+  const int per = ((nk_all + g.splitk - 1) / g.splitk + 1) & ~1;  // even K-tiles per split
+  const int kt0 = split * per;
+  const int nk = max(0, min(nk_all, kt0 + per) - kt0);             // even (K % 128 == 0)
+
+  auto lds = [&](int buf, int slot) {
+    return smem + buf * G::Buf + (slot < 2 ? slot * kAHalf : 2 * kAHalf + (slot - 2) * G::BHalf);
+  };
+
+  // DMA of one half-tile in 1 KiB pieces (8 rows x 128 B, one wave instruction).
+  // Lane-linear LDS image; the (row & 7) chunk swizzle is applied to the source.
+  const int lrow = lane >> 3, pchunk = lane & 7;
+  auto stage = [&](int buf, int slot, int kt) {
+    const bool isA = slot < 2;
+    const uint16_t* base = isA ? g.A : g.B;
+    const int ld = isA ? g.lda : g.ldb, lim = (isA ? g.M : g.N) - 1;
+    const int r0 = isA ? bm + (slot & 1) * 128 : bn + (slot & 1) * (BN / 2);
+    const int k0 = (kt0 + kt) * PK;
+    const int n = isA ? G::GA : G::GB;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      if (i < n) {
+        const int q = wave * n + i;
+        const int r = q * 8 + lrow;
+        const int c = pchunk ^ (r & 7);
+        const int gr = min(r0 + r, lim);
+        __builtin_amdgcn_global_load_lds((const void*)(base + (size_t)gr * ld + k0 + c * 8),
+                                         (__attribute__((address_space(3))) void*)(lds(buf, slot) + q * 1024), 16, 0,
+                                         0);
+      }
+    }
+  };
+
+  floatx4 acc[2][2][G::MI][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int i = 0; i < G::MI; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[a][b][i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  bf16x8 fa[G::MI][2], fb0[2][2], fb1[2][2];
+  auto read_a = [&](int buf, int h) {
+    const unsigned char* base = lds(buf, h);
+#pragma unroll
+    for (int i = 0; i < G::MI; ++i)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int row = wr * (128 / G::WR) + i * 16 + (lane & 15);
+        const int chunk = ks * 4 + (lane >> 4);
+        fa[i][ks] = *reinterpret_cast<const bf16x8*>(base + row * 128 + ((chunk ^ (row & 7)) << 4));
+      }
+  };
+  auto read_b = [&](int buf, int h, bf16x8 (&fb)[2][2]) {
+    const unsigned char* base = lds(buf, 2 + h);
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int row = wc * 32 + j * 16 + (lane & 15);
+        const int chunk = ks * 4 + (lane >> 4);
+        fb[j][ks] = *reinterpret_cast<const bf16x8*>(base + row * 128 + ((chunk ^ (row & 7)) << 4));
+      }
+  };
+  auto mma = [&](int mh, int nh, bf16x8 (&fb)[2][2]) {
+    bar();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (!(EXP & 2)) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < G::MI; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[mh][nh][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][ks], fb[j][ks], acc[mh][nh][i][j], 0, 0, 0);
+    if constexpr (!(EXP & 2)) __builtin_amdgcn_s_setprio(0);
+    bar();
+  };
+  // retire the half-tile issued four phases ago (steady state) or everything (tail)
+  auto retire = [&](bool tail) {
+    if constexpr (EXP & 1) {
+      if (tail) wait_vm<0>();
+    } else {
+      if (tail) wait_vm<0>();
+      else wait_vm<G::VM>();
+    }
+  };
+
+  if (nk > 0) {
+    // prologue: tile 0 complete in buffer 0, tile 1's A0/B0 in flight
+    stage(0, A0, 0);
+    stage(0, B0, 0);
+    stage(0, B1, 0);
+    stage(0, A1, 0);
+    stage(1, A0, 1);
+    stage(1, B0, 1);
+    wait_vm<G::VM>();  // buf0 A0, B0 landed
+  }
+  __syncthreads();
+  if (!(EXP & 4) && grp == 1) bar();  // group 1 runs one barrier behind group 0
+
+  for (int kt = 0; kt < nk; kt += 2) {
+    const bool tail = kt + 2 >= nk;  // no tiles beyond this pair: drain instead of counting
+    // ---- K-tile kt (buffer 0)
+    read_a(0, 0);
+    read_b(0, 0, fb0);
+    stage(1, B1, kt + 1);
+    retire(tail);
+    mma(0, 0, fb0);
+
+    read_b(0, 1, fb1);
+    stage(1, A1, kt + 1);
+    retire(tail);
+    mma(0, 1, fb1);
+
+    read_a(0, 1);
+    if (!tail) stage(0, A0, kt + 2);
+    retire(tail);
+    mma(1, 1, fb1);
+
+    if (!tail) stage(0, B0, kt + 2);
+    retire(tail);
+    mma(1, 0, fb0);
+
+    // ---- K-tile kt + 1 (buffer 1)
+    read_a(1, 0);
+    read_b(1, 0, fb0);
+    if (!tail) stage(0, B1, kt + 2);
+    retire(tail);
+    mma(0, 0, fb0);
+
+    read_b(1, 1, fb1);
+    if (!tail) stage(0, A1, kt + 2);
+    retire(tail);
+    mma(0, 1, fb1);
+
+    read_a(1, 1);
+    if (kt + 3 < nk) stage(1, A0, kt + 3);
+    retire(tail);
+    mma(1, 1, fb1);
+
+    if (kt + 3 < nk) stage(1, B0, kt + 3);
+    retire(tail);
+    mma(1, 0, fb0);
+  }
+  if (!(EXP & 4) && grp == 0) bar();  // re-align the groups
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  // epilogue: two passes of 128 rows through LDS
+  float* tile = reinterpret_cast<float*>(smem);
+#pragma unroll
+  for (int mh = 0; mh < 2; ++mh) {
+#pragma unroll
+    for (int nh = 0; nh < 2; ++nh)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int cl = nh * (BN / 2) + wc * 32 + j * 16 + (lane & 15);
+        const float b = load_bias(g, bn + cl, split);
+#pragma unroll
+        for (int i = 0; i < G::MI; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            tile[(wr * (128 / G::WR) + i * 16 + (lane >> 4) * 4 + r) * G::EpiTS + cl] =
+                epi(g, acc[mh][nh][i][j][r], b);
+      }
+    __syncthreads();
+    store_rows<128, BN, PNT>(g, tile, G::EpiTS, bm + mh * 128, bn, t);
+    __syncthreads();
+  }
+}
+
+}  // namespace
+
+int gemm256_tiles(int M, int N, int bn) { return ((M + PM - 1) / PM) * ((N + bn - 1) / bn); }
+
+template <int BN, int EXP>
+static void launch_pp(const GemmArgs& g, hipStream_t stream) {
+  static bool attr = [] {
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(k_gemm_nt_pp<BN, EXP>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, Geo<BN>::Lds) == hipSuccess;
+  }();
+  (void)attr;
+  const int nwg = gemm256_tiles(g.M, g.N, BN) * g.splitk;
+  hipLaunchKernelGGL((k_gemm_nt_pp<BN, EXP>), dim3(nwg), dim3(PNT), Geo<BN>::Lds, stream, g);
+}
+
+int g_pp_exp = 0;  // ablation variant (benchmarks only)
+
+void launch_gemm_nt_256(const GemmArgs& g, int bn, hipStream_t stream) {
+  if (bn == 128) return launch_pp<128, 0>(g, stream);
+  switch (g_pp_exp) {
+    case 1: return launch_pp<256, 1>(g, stream);
+    case 2: return launch_pp<256, 2>(g, stream);
+    case 4: return launch_pp<256, 4>(g, stream);
+    case 6: return launch_pp<256, 6>(g, stream);
+    default: return launch_pp<256, 0>(g, stream);
+  }
+}
+
+}  // namespace gemm
+}  // namespace dev
+}  // namespace ccmpi

@@ -1,0 +1,142 @@
+// Shared pieces of the MFMA GEMM kernels (gemm.hip, gemm256.hip): argument
+// block, epilogue math and the LDS-staged row store.
+#pragma once
+#include <cstdint>
+
+#include "common.hpp"
+
+namespace ccmpi {
+namespace dev {
+namespace gemm {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+struct GemmArgs {
+  const uint16_t* A;
+  const uint16_t* B;
+  void* C;
+  const void* bias;
+  int M, N, K;
+  int lda, ldb, ldc;
+  float alpha;
+  int accumulate;  // C += result
+  int bias_kind;   // 0 none, 1 fp32, 2 bf16
+  int act;         // 0 none, 1 relu, 2 gelu(tanh)
+  int out_bf16;    // 0 fp32 out, 1 bf16 out
+  int splitk;      // >1: K split over workgroups, fp32 atomic-add epilogue into C
+};
+
+__device__ __forceinline__ float bf2f(uint16_t h) { return __uint_as_float((uint32_t)h << 16); }
+
+__device__ __forceinline__ float gelu_tanh(float x) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  return 0.5f * x * (1.f + tanhf(k0 * (x + k1 * x * x * x)));
+}
+
+__device__ __forceinline__ float load_bias(const GemmArgs& g, int col, int split) {
+  if (split != 0 || col >= g.N) return 0.f;
+  if (g.bias_kind == 1) return reinterpret_cast<const float*>(g.bias)[col];
+  if (g.bias_kind == 2) return bf2f(reinterpret_cast<const uint16_t*>(g.bias)[col]);
+  return 0.f;
+}
+
+__device__ __forceinline__ float epi(const GemmArgs& g, float acc, float b) {
+  float v = g.alpha * acc + b;
+  if (g.act == 1) v = fmaxf(v, 0.f);
+  else if (g.act == 2) v = gelu_tanh(v);
+  return v;
+}
+
+// Write a ROWS x COLS fp32 tile staged in LDS (row stride TS floats, values
+// already alpha/bias/act-applied) to C at (row0, col0) with NT threads: whole
+// rows as 16-B vectors when C allows it, lane-consecutive fp32 atomics for
+// split-K, per-element stores otherwise.
+template <int ROWS, int COLS, int NT>
+__device__ __forceinline__ void store_rows(const GemmArgs& g, const float* tile, int TS, int row0, int col0, int t) {
+  const int es = g.out_bf16 ? 2 : 4;
+  const bool vec_ok = (((uint64_t)g.C | ((uint64_t)g.ldc * es)) % 16) == 0;
+  if (g.splitk > 1) {
+    for (int idx = t; idx < ROWS * COLS; idx += NT) {
+      const int rl = idx / COLS, cl = idx % COLS;
+      const int row = row0 + rl, col = col0 + cl;
+      if (row < g.M && col < g.N) atomicAdd(reinterpret_cast<float*>(g.C) + (size_t)row * g.ldc + col, tile[rl * TS + cl]);
+    }
+  } else if (vec_ok) {
+    const int per_vec = 16 / es;
+    const int vecs_row = COLS / per_vec;
+    for (int idx = t; idx < ROWS * vecs_row; idx += NT) {
+      const int rl = idx / vecs_row, cl = (idx % vecs_row) * per_vec;
+      const int row = row0 + rl, col = col0 + cl;
+      if (row >= g.M || col >= g.N) continue;
+      const float* src = tile + rl * TS + cl;
+      if (col + per_vec <= g.N) {
+        if (g.out_bf16) {
+          uint16_t* C = reinterpret_cast<uint16_t*>(g.C) + (size_t)row * g.ldc + col;
+          uint32_t w[4];
+          if (g.accumulate) {
+            const uint4 old = *reinterpret_cast<const uint4*>(C);
+            const uint32_t ow[4] = {old.x, old.y, old.z, old.w};
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+              w[q] = f32_to_bf16_bits(src[2 * q] + bf16_lo(ow[q])) | (f32_to_bf16_bits(src[2 * q + 1] + bf16_hi(ow[q])) << 16);
+          } else {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) w[q] = f32_to_bf16_bits(src[2 * q]) | (f32_to_bf16_bits(src[2 * q + 1]) << 16);
+          }
+          *reinterpret_cast<uint4*>(C) = uint4{w[0], w[1], w[2], w[3]};
+        } else {
+          float* C = reinterpret_cast<float*>(g.C) + (size_t)row * g.ldc + col;
+          float4 v = make_float4(src[0], src[1], src[2], src[3]);
+          if (g.accumulate) {
+            const float4 old = *reinterpret_cast<const float4*>(C);
+            v.x += old.x; v.y += old.y; v.z += old.z; v.w += old.w;
+          }
+          *reinterpret_cast<float4*>(C) = v;
+        }
+      } else {
+        for (int q = 0; q < per_vec && col + q < g.N; ++q) {
+          const size_t o = (size_t)row * g.ldc + col + q;
+          if (g.out_bf16) {
+            uint16_t* C = reinterpret_cast<uint16_t*>(g.C);
+            C[o] = (uint16_t)f32_to_bf16_bits(src[q] + (g.accumulate ? bf2f(C[o]) : 0.f));
+          } else {
+            float* C = reinterpret_cast<float*>(g.C);
+            C[o] = src[q] + (g.accumulate ? C[o] : 0.f);
+          }
+        }
+      }
+    }
+  } else {
+    for (int idx = t; idx < ROWS * COLS; idx += NT) {
+      const int rl = idx / COLS, cl = idx % COLS;
+      const int row = row0 + rl, col = col0 + cl;
+      if (row >= g.M || col >= g.N) continue;
+      const size_t o = (size_t)row * g.ldc + col;
+      const float v = tile[rl * TS + cl];
+      if (g.out_bf16) {
+        uint16_t* C = reinterpret_cast<uint16_t*>(g.C);
+        C[o] = (uint16_t)f32_to_bf16_bits(v + (g.accumulate ? bf2f(C[o]) : 0.f));
+      } else {
+        float* C = reinterpret_cast<float*>(g.C);
+        C[o] = v + (g.accumulate ? C[o] : 0.f);
+      }
+    }
+  }
+}
+
+// XCD-aware bijective workgroup remap: blocks b, b+8, b+16, ... (dispatched
+// round-robin to the same XCD) get consecutive logical ids.
+__device__ __forceinline__ int xcd_remap(int wg, int nwg) {
+  const int q = nwg / 8, r = nwg % 8, x = wg % 8;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + wg / 8;
+}
+
+// 256 x bn (bn = 256 or 128) 8-wave ping-pong kernel (gemm256.hip); requires K % 128 == 0.
+void launch_gemm_nt_256(const GemmArgs& g, int bn, hipStream_t stream);
+int gemm256_tiles(int M, int N, int bn);
+extern int g_pp_exp;  // ablation variant of the ping-pong kernel (benchmarks only; 0 = production)
+
+}  // namespace gemm
+}  // namespace dev
+}  // namespace ccmpi

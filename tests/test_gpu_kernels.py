@@ -35,6 +35,49 @@ def test_gemm_nt_shapes(M, N, K):
     torch.testing.assert_close(y, ref, rtol=2e-3, atol=2e-3 * K ** 0.5)
 
 
+@pytest.fixture(params=[2, 3], ids=["256x256", "256x128"])
+def gemm256(request):
+    """Force a large-tile ping-pong kernel whenever legal (K % 128 == 0)."""
+    from collective_communication_mpi_amd import _native
+
+    D = _native.device()
+    D.gemm_set_kernel(request.param)
+    yield
+    D.gemm_set_kernel(0)
+
+
+@pytest.mark.parametrize("M,N,K", [(256, 256, 128), (1, 8, 128), (300, 520, 256), (777, 1000, 512),
+                                   (4096, 768, 768), (2048, 2048, 4096), (32768, 768, 768)])
+def test_gemm256_shapes(gemm256, M, N, K):
+    from collective_communication_mpi_amd.ops import gemm_nt
+
+    g = torch.Generator(device="cuda").manual_seed(M * 5 + N * 11 + K)
+    a = torch.randn(M, K, device="cuda", generator=g).bfloat16()
+    b = torch.randn(N, K, device="cuda", generator=g).bfloat16()
+    for splitk in (1, 3):
+        y = gemm_nt(a, b, out_dtype=torch.float32, splitk=splitk)
+        torch.testing.assert_close(y, _ref(a, b), rtol=2e-3, atol=2e-3 * K ** 0.5)
+    # repeated launches: an intermittent race shows up as a mismatch between runs
+    y0 = gemm_nt(a, b, out_dtype=torch.float32, splitk=1)
+    for _ in range(3):
+        torch.testing.assert_close(gemm_nt(a, b, out_dtype=torch.float32, splitk=1), y0, rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("act", [None, "gelu"])
+def test_gemm256_epilogue(gemm256, act):
+    from collective_communication_mpi_amd.ops import gemm_nt
+
+    a = torch.randn(600, 384, device="cuda").bfloat16()
+    b = torch.randn(520, 384, device="cuda").bfloat16()
+    bias = torch.randn(520, device="cuda").bfloat16()
+    y = gemm_nt(a, b, bias=bias, act=act, alpha=0.5)
+    torch.testing.assert_close(y.float(), _ref(a, b, bias, act, 0.5), rtol=2e-2, atol=8e-2)
+    c = torch.randn(600, 520, device="cuda")
+    c0 = c.clone()
+    gemm_nt(a, b, out=c, accumulate=True, splitk=1)
+    torch.testing.assert_close(c, c0 + _ref(a, b), rtol=2e-3, atol=5e-2)
+
+
 def test_gemm_asymmetric_identity():
     """A = I with an asymmetric B catches a transposed C write (guide §3)."""
     from collective_communication_mpi_amd.ops import gemm_nt
@@ -43,6 +86,18 @@ def test_gemm_asymmetric_identity():
     a = torch.eye(n, device="cuda").bfloat16()
     b = torch.arange(n * n, device="cuda", dtype=torch.float32).reshape(n, n).remainder(97).bfloat16()
     y = gemm_nt(a, b, out_dtype=torch.float32)
+    torch.testing.assert_close(y, b.float().T)
+    # same check through the 256x256 kernel (K % 128 == 0)
+    from collective_communication_mpi_amd import _native
+
+    n = 256
+    a = torch.eye(n, device="cuda").bfloat16()
+    b = torch.arange(n * n, device="cuda", dtype=torch.float32).reshape(n, n).remainder(97).bfloat16()
+    _native.device().gemm_set_kernel(2)
+    try:
+        y = gemm_nt(a, b, out_dtype=torch.float32, splitk=1)
+    finally:
+        _native.device().gemm_set_kernel(0)
     torch.testing.assert_close(y, b.float().T)
 
 
