@@ -1,0 +1,34 @@
+// Argument block shared by the short-sequence attention kernels
+// (attn_small.hip: scalar fallback; attn_mfma.hip: MFMA path for S <= 16).
+#pragma once
+#include <cstdint>
+
+#include <hip/hip_runtime.h>
+
+namespace ccmpi {
+namespace dev {
+namespace attn {
+
+struct AttnArgs {
+  const uint16_t* qkv;  // [B*S][ld_qkv]
+  uint16_t* o;          // [B*S][ld_o]
+  float* lse;           // [B*Hl][S]
+  const uint16_t* dout; // [B*S][ld_o]   (bwd)
+  uint16_t* dqkv;       // [B*S][ld_qkv] (bwd)
+  float* dbias;         // [3*Hl*D] fp32, += column sums of dqkv (bwd, optional)
+  int B, S, Hl, D, ld_qkv, ld_o;
+  float scale;
+  uint16_t* pool;       // fwd, optional: [B][ld_pool] bf16 mean over the S rows of O
+  int ld_pool;
+  int dout_bstride;     // bwd: dO row (b, i) at dout + b*dout_bstride + i*dout_rstride + h*D
+  int dout_rstride;     //      (rstride 0 = the pooled-gradient broadcast over the S rows)
+};
+
+// MFMA path (attn_mfma.hip): S <= 16, D in {32, 64, 128}, 16-B aligned rows.
+bool mfma_supported(const AttnArgs& a, bool bwd);
+void launch_fwd_mfma(const AttnArgs& a, hipStream_t stream);
+void launch_bwd_mfma(const AttnArgs& a, hipStream_t stream);
+
+}  // namespace attn
+}  // namespace dev
+}  // namespace ccmpi

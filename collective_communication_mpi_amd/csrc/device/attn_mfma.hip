@@ -1,0 +1,313 @@
+// Short-sequence attention on matrix cores (S <= 16 keys/queries per
+// sequence, head_dim D in {32, 64, 128}): the MNIST harness's 16-patch
+// attention, forward and backward.  One wave per (sequence, local head), four
+// waves per workgroup, grid-strided over the (b, h) pairs.
+//
+// Everything stays in MFMA register layouts (16x16 tiles; g = lane >> 4,
+// c = lane & 15; an accumulator holds element [4g + r][c] in register r):
+//   * Q, K, V, dO, O rows are read straight from the fused QKV buffer with one
+//     16-B load per lane per 32 columns: lane (c, g) holds row c, columns
+//     32kk + 8g .. +7 -- the A/B operand layout of v_mfma_f32_16x16x32_bf16.
+//   * S^T = K Q^T (2 MFMAs at D = 64) leaves column i = query on the lane and
+//     the 16 keys j = 4g + r in registers, so the softmax over j is 4 register
+//     ops plus two cross-lane-group shuffles, and the probabilities P[i][4g + r]
+//     ARE the A operand of v_mfma_f32_16x16x16_bf16 for O = P V (no lane
+//     movement).  The V operand (4 consecutive keys of one column per lane) is
+//     read from a per-wave LDS copy of the tile.
+//   * Backward recomputes both S and S^T (and dP, dP^T), so each of
+//     dV = P^T dO, dK = scale dS^T Q and dQ = scale dS K contracts over an
+//     accumulator's row index: the accumulator is the A operand, the other
+//     factor comes from the per-wave LDS tile.  delta_i = rowsum(dO * O).
+//   * Outputs are staged per wave through LDS and written as 16-B row
+//     vectors.  The pooled forward output (mean over the S rows, for the
+//     pooled row-parallel fc_o) and the QKV bias gradient (column sums of dQ,
+//     dK, dV) are reduced in registers; bias sums are flushed with one atomic
+//     per column per wave (and whenever a wave's head changes).
+// The kernel is memory bound (a few KiB moved per ~10 MFMAs): its cost is the
+// QKV read and the O / dQKV write.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+#include "attn_common.hpp"
+#include "common.hpp"
+
+namespace ccmpi {
+namespace dev {
+namespace attn {
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef short s4 __attribute__((ext_vector_type(4)));
+typedef float f4 __attribute__((ext_vector_type(4)));
+constexpr int WPB = 4;  // waves per workgroup
+
+__device__ __forceinline__ s4 pack4(float a, float b, float c, float d) {
+  const uint2 u{f32_to_bf16_bits(a) | (f32_to_bf16_bits(b) << 16), f32_to_bf16_bits(c) | (f32_to_bf16_bits(d) << 16)};
+  return __builtin_bit_cast(s4, u);
+}
+__device__ __forceinline__ bf16x8 ld_row16(const uint16_t* p, bool ok) {
+  const uint4 z = ok ? *reinterpret_cast<const uint4*>(p) : uint4{0, 0, 0, 0};
+  return __builtin_bit_cast(bf16x8, z);
+}
+__device__ __forceinline__ f4 mma32(bf16x8 a, bf16x8 b, f4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ f4 mma16(s4 a, s4 b, f4 c) { return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, b, c, 0, 0, 0); }
+
+// B operand of the 16x16x16 MFMA from a row-major [16][LD] bf16 LDS tile:
+// lane (c, g) takes rows 4g..4g+3 of column col.
+template <int LD>
+__device__ __forceinline__ s4 tile_b(const uint16_t* T, int g, int col) {
+  s4 r;
+  r[0] = (short)T[(4 * g + 0) * LD + col];
+  r[1] = (short)T[(4 * g + 1) * LD + col];
+  r[2] = (short)T[(4 * g + 2) * LD + col];
+  r[3] = (short)T[(4 * g + 3) * LD + col];
+  return r;
+}
+
+// lane (c, g) wrote rows of a [16][D] result as accumulators [4g + r][16nt + c]:
+// stage them as bf16 and store rows < S as 16-B vectors.
+template <int D, int LD>
+__device__ __forceinline__ void store_tile(uint16_t* T, const f4 (&v)[D / 16], float mul, uint16_t* dst, int ld, int S,
+                                           int lane) {
+  const int c = lane & 15, g = lane >> 4;
+#pragma unroll
+  for (int nt = 0; nt < D / 16; ++nt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) T[(4 * g + r) * LD + 16 * nt + c] = (uint16_t)f32_to_bf16_bits(v[nt][r] * mul);
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int t = 0; t < (16 * D / 8) / 64; ++t) {
+    const int p = lane + 64 * t, row = p / (D / 8), col = (p % (D / 8)) * 8;
+    if (row < S) *reinterpret_cast<uint4*>(dst + (size_t)row * ld + col) = *reinterpret_cast<const uint4*>(T + row * LD + col);
+  }
+  __builtin_amdgcn_wave_barrier();
+}
+
+// copy register rows (lane (c, g): row c, columns 32kk + 8g..) into an LDS tile
+template <int D, int LD>
+__device__ __forceinline__ void put_rows(uint16_t* T, const bf16x8 (&x)[D / 32], int lane) {
+  const int c = lane & 15, g = lane >> 4;
+#pragma unroll
+  for (int kk = 0; kk < D / 32; ++kk) *reinterpret_cast<bf16x8*>(T + c * LD + 32 * kk + 8 * g) = x[kk];
+}
+
+template <int D>
+__global__ void __launch_bounds__(256) k_attn16_fwd(AttnArgs a) {
+  constexpr int LD = D + 8, NK = D / 32, NT = D / 16;
+  __shared__ __attribute__((aligned(16))) uint16_t vt[WPB][16 * LD];
+  __shared__ __attribute__((aligned(16))) uint16_t ot[WPB][16 * LD];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
+  const int S = a.S, HD = a.Hl * D, npairs = a.B * a.Hl;
+  uint16_t* V = vt[wave];
+  uint16_t* O = ot[wave];
+  for (int pr = blockIdx.x * WPB + wave; pr < npairs; pr += gridDim.x * WPB) {
+    const int b = pr / a.Hl, h = pr % a.Hl;
+    const uint16_t* qb = a.qkv + (size_t)b * S * a.ld_qkv + h * D;
+    bf16x8 qr[NK], kr[NK], vr[NK];
+#pragma unroll
+    for (int kk = 0; kk < NK; ++kk) {
+      const size_t off = (size_t)c * a.ld_qkv + 32 * kk + 8 * g;
+      qr[kk] = ld_row16(qb + off, c < S);
+      kr[kk] = ld_row16(qb + HD + off, c < S);
+      vr[kk] = ld_row16(qb + 2 * HD + off, c < S);
+    }
+    put_rows<D, LD>(V, vr, lane);
+    f4 st = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kk = 0; kk < NK; ++kk) st = mma32(kr[kk], qr[kk], st);  // S^T[j = 4g + r][i = c]
+    float x[4], m = -INFINITY;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      x[r] = (4 * g + r < S) ? st[r] * a.scale : -INFINITY;
+      m = fmaxf(m, x[r]);
+    }
+    m = fmaxf(m, __shfl_xor(m, 16));
+    m = fmaxf(m, __shfl_xor(m, 32));
+    float e[4], s = 0.f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      e[r] = __expf(x[r] - m);
+      s += e[r];
+    }
+    s += __shfl_xor(s, 16);
+    s += __shfl_xor(s, 32);
+    const float inv = 1.f / s;
+    if (g == 0 && c < S) a.lse[(size_t)pr * S + c] = m + __logf(s);
+    const s4 pa = pack4(e[0] * inv, e[1] * inv, e[2] * inv, e[3] * inv);  // A[i = c][j = 4g + jj]
+    __builtin_amdgcn_wave_barrier();
+    f4 o[NT];
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) o[nt] = mma16(pa, tile_b<LD>(V, g, 16 * nt + c), f4{0.f, 0.f, 0.f, 0.f});
+    if (a.pool) {
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        float cs = 0.f;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) cs += (4 * g + r < S) ? o[nt][r] : 0.f;
+        cs += __shfl_xor(cs, 16);
+        cs += __shfl_xor(cs, 32);
+        if (g == 0) a.pool[(size_t)b * a.ld_pool + h * D + 16 * nt + c] = (uint16_t)f32_to_bf16_bits(cs / (float)S);
+      }
+    }
+    store_tile<D, LD>(O, o, 1.f, a.o + (size_t)b * S * a.ld_o + h * D, a.ld_o, S, lane);
+  }
+}
+
+template <int D>
+__global__ void __launch_bounds__(256) k_attn16_bwd(AttnArgs a) {
+  constexpr int LD = D + 8, NK = D / 32, NT = D / 16, TILE = 16 * LD;
+  extern __shared__ __attribute__((aligned(16))) uint16_t sm[];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
+  uint16_t* Qt = sm + wave * 4 * TILE;
+  uint16_t* Kt = Qt + TILE;
+  uint16_t* Dt = Kt + TILE;
+  uint16_t* Ot = Dt + TILE;
+  const int S = a.S, HD = a.Hl * D, npairs = a.B * a.Hl;
+  float bq[NT], bk[NT], bv[NT];
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) bq[nt] = bk[nt] = bv[nt] = 0.f;
+  int hcur = -1;
+  auto flush = [&](int h) {  // column sums of dQ, dK, dV for head h -> dbias
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      float q = bq[nt], k = bk[nt], v = bv[nt];
+      q += __shfl_xor(q, 16); q += __shfl_xor(q, 32);
+      k += __shfl_xor(k, 16); k += __shfl_xor(k, 32);
+      v += __shfl_xor(v, 16); v += __shfl_xor(v, 32);
+      if (g == 0) {
+        atomicAdd(a.dbias + h * D + 16 * nt + c, q);
+        atomicAdd(a.dbias + HD + h * D + 16 * nt + c, k);
+        atomicAdd(a.dbias + 2 * HD + h * D + 16 * nt + c, v);
+      }
+      bq[nt] = bk[nt] = bv[nt] = 0.f;
+    }
+  };
+  for (int pr = blockIdx.x * WPB + wave; pr < npairs; pr += gridDim.x * WPB) {
+    const int b = pr / a.Hl, h = pr % a.Hl;
+    if (a.dbias && h != hcur) {
+      if (hcur >= 0) flush(hcur);
+      hcur = h;
+    }
+    const uint16_t* qb = a.qkv + (size_t)b * S * a.ld_qkv + h * D;
+    const uint16_t* ob = a.o + (size_t)b * S * a.ld_o + h * D;
+    const uint16_t* db = a.dout + (size_t)b * a.dout_bstride + h * D;
+    bf16x8 qr[NK], kr[NK], vr[NK], dr[NK], orr[NK];
+#pragma unroll
+    for (int kk = 0; kk < NK; ++kk) {
+      const size_t off = (size_t)c * a.ld_qkv + 32 * kk + 8 * g;
+      qr[kk] = ld_row16(qb + off, c < S);
+      kr[kk] = ld_row16(qb + HD + off, c < S);
+      vr[kk] = ld_row16(qb + 2 * HD + off, c < S);
+      dr[kk] = ld_row16(db + (size_t)c * a.dout_rstride + 32 * kk + 8 * g, c < S);
+      orr[kk] = ld_row16(ob + (size_t)c * a.ld_o + 32 * kk + 8 * g, c < S);
+    }
+    put_rows<D, LD>(Qt, qr, lane);
+    put_rows<D, LD>(Kt, kr, lane);
+    put_rows<D, LD>(Dt, dr, lane);
+    const float* lse = a.lse + (size_t)pr * S;
+    const float lse_c = c < S ? lse[c] : 0.f;
+    float lse_r[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) lse_r[r] = (4 * g + r < S) ? lse[4 * g + r] : 0.f;
+    f4 sT = {0.f, 0.f, 0.f, 0.f}, sM = sT, dpT = sT, dpM = sT;
+#pragma unroll
+    for (int kk = 0; kk < NK; ++kk) {
+      sT = mma32(kr[kk], qr[kk], sT);    // S^T[j = 4g + r][i = c]
+      sM = mma32(qr[kk], kr[kk], sM);    // S[i = 4g + r][j = c]
+      dpT = mma32(vr[kk], dr[kk], dpT);  // dP^T[j = 4g + r][i = c]
+      dpM = mma32(dr[kk], vr[kk], dpM);  // dP[i = 4g + r][j = c]
+    }
+    // delta_i = sum_d dO[i][d] O[i][d] for i = c, then for rows i = 4g + r
+    float dl = 0.f;
+#pragma unroll
+    for (int kk = 0; kk < NK; ++kk)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) dl += (float)dr[kk][e] * (float)orr[kk][e];
+    dl += __shfl_xor(dl, 16);
+    dl += __shfl_xor(dl, 32);
+    float P[4], PT[4], dS[4], dST[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const bool ok = (4 * g + r < S) && (c < S);
+      PT[r] = ok ? __expf(sT[r] * a.scale - lse_c) : 0.f;
+      P[r] = ok ? __expf(sM[r] * a.scale - lse_r[r]) : 0.f;
+      const float dl_r = __shfl(dl, 4 * g + r);
+      dST[r] = PT[r] * (dpT[r] - dl);
+      dS[r] = P[r] * (dpM[r] - dl_r);
+    }
+    __builtin_amdgcn_wave_barrier();
+    const s4 aP = pack4(P[0], P[1], P[2], P[3]);        // A[j = c][i = 4g + jj] = P^T
+    const s4 aDS = pack4(dS[0], dS[1], dS[2], dS[3]);   // A[j = c][i = 4g + jj] = dS^T
+    const s4 aDST = pack4(dST[0], dST[1], dST[2], dST[3]);  // A[i = c][j = 4g + jj] = dS
+    f4 acc[NT];
+    uint16_t* gq = a.dqkv + (size_t)b * S * a.ld_qkv + h * D;
+    // dV = P^T dO
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      acc[nt] = mma16(aP, tile_b<LD>(Dt, g, 16 * nt + c), f4{0.f, 0.f, 0.f, 0.f});
+      bv[nt] += acc[nt][0] + acc[nt][1] + acc[nt][2] + acc[nt][3];
+    }
+    store_tile<D, LD>(Ot, acc, 1.f, gq + 2 * HD, a.ld_qkv, S, lane);
+    // dK = scale dS^T Q
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      acc[nt] = mma16(aDS, tile_b<LD>(Qt, g, 16 * nt + c), f4{0.f, 0.f, 0.f, 0.f});
+      bk[nt] += a.scale * (acc[nt][0] + acc[nt][1] + acc[nt][2] + acc[nt][3]);
+    }
+    store_tile<D, LD>(Ot, acc, a.scale, gq + HD, a.ld_qkv, S, lane);
+    // dQ = scale dS K
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      acc[nt] = mma16(aDST, tile_b<LD>(Kt, g, 16 * nt + c), f4{0.f, 0.f, 0.f, 0.f});
+      bq[nt] += a.scale * (acc[nt][0] + acc[nt][1] + acc[nt][2] + acc[nt][3]);
+    }
+    store_tile<D, LD>(Ot, acc, a.scale, gq, a.ld_qkv, S, lane);
+  }
+  if (a.dbias && hcur >= 0) flush(hcur);
+}
+
+template <int D>
+constexpr size_t bwd_lds_bytes() {
+  return (size_t)WPB * 4 * 16 * (D + 8) * sizeof(uint16_t);
+}
+
+int grid_for(int npairs, int cap) { return std::max(1, std::min((npairs + WPB - 1) / WPB, cap)); }
+
+}  // namespace
+
+bool mfma_supported(const AttnArgs& a, bool bwd) {
+  if (a.S < 1 || a.S > 16 || !(a.D == 32 || a.D == 64 || a.D == 128)) return false;
+  if (a.ld_qkv % 8 || a.ld_o % 8 || ((uint64_t)a.qkv % 16) || ((uint64_t)a.o % 16)) return false;
+  if (bwd && (a.dout_bstride % 8 || a.dout_rstride % 8 || ((uint64_t)a.dout % 16) || ((uint64_t)a.dqkv % 16))) return false;
+  return true;
+}
+
+void launch_fwd_mfma(const AttnArgs& a, hipStream_t stream) {
+  const int grid = grid_for(a.B * a.Hl, 4096);
+  if (a.D == 32) hipLaunchKernelGGL(k_attn16_fwd<32>, dim3(grid), dim3(256), 0, stream, a);
+  else if (a.D == 64) hipLaunchKernelGGL(k_attn16_fwd<64>, dim3(grid), dim3(256), 0, stream, a);
+  else hipLaunchKernelGGL(k_attn16_fwd<128>, dim3(grid), dim3(256), 0, stream, a);
+}
+
+void launch_bwd_mfma(const AttnArgs& a, hipStream_t stream) {
+  // fewer, longer-lived waves: every wave flushes its bias column sums once
+  const int grid = grid_for(a.B * a.Hl, a.dbias ? 1024 : 4096);
+  if (a.D == 32) {
+    hipLaunchKernelGGL(k_attn16_bwd<32>, dim3(grid), dim3(256), bwd_lds_bytes<32>(), stream, a);
+  } else if (a.D == 64) {
+    hipLaunchKernelGGL(k_attn16_bwd<64>, dim3(grid), dim3(256), bwd_lds_bytes<64>(), stream, a);
+  } else {
+    static bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(k_attn16_bwd<128>),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           (int)bwd_lds_bytes<128>()) == hipSuccess;
+    (void)attr;
+    hipLaunchKernelGGL(k_attn16_bwd<128>, dim3(grid), dim3(256), bwd_lds_bytes<128>(), stream, a);
+  }
+}
+
+}  // namespace attn
+}  // namespace dev
+}  // namespace ccmpi

@@ -11,6 +11,7 @@
 // fp32 VALU dot products from LDS rather than MFMA tiles (which need >= 16x16x32).
 #include <pybind11/pybind11.h>
 
+#include "attn_common.hpp"
 #include "common.hpp"
 #include "ops.hpp"
 
@@ -18,6 +19,7 @@ namespace ccmpi {
 namespace dev {
 
 namespace {
+using attn::AttnArgs;
 
 __device__ __forceinline__ float ld_bf16(const uint16_t* p) { return __uint_as_float((uint32_t)(*p) << 16); }
 __device__ __forceinline__ void st_bf16(uint16_t* p, float v) { *p = (uint16_t)f32_to_bf16_bits(v); }
@@ -31,20 +33,7 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
-struct AttnArgs {
-  const uint16_t* qkv;  // [B*S][ld_qkv]
-  uint16_t* o;          // [B*S][ld_o]
-  float* lse;           // [B*Hl][S]
-  const uint16_t* dout; // [B*S][ld_o]   (bwd)
-  uint16_t* dqkv;       // [B*S][ld_qkv] (bwd)
-  float* dbias;         // [3*Hl*D] fp32, += column sums of dqkv (bwd, optional)
-  int B, S, Hl, D, ld_qkv, ld_o;
-  float scale;
-  uint16_t* pool;       // fwd, optional: [B][ld_pool] bf16 mean over the S rows of O
-  int ld_pool;
-  int dout_bstride;     // bwd: dO row (b, i) at dout + b*dout_bstride + i*dout_rstride + h*D
-  int dout_rstride;     //      (rstride 0 = the pooled-gradient broadcast over the S rows)
-};
+
 
 // stage an S x D head tile (bf16, row stride ld) into fp32 LDS [S][D+1]; 16-B
 // vector loads (8 bf16 per lane) whenever rows are 16-B aligned (guide G13)
@@ -241,6 +230,11 @@ void attn_fwd(uint64_t qkv, uint64_t o, uint64_t lse, int B, int S, int Hl, int 
   check_dims(S, D, false);
   AttnArgs a{(const uint16_t*)qkv, (uint16_t*)o, (float*)lse, nullptr, nullptr, nullptr, B, S, Hl, D, ld_qkv, ld_o, scale,
              (uint16_t*)pool, ld_pool, 0, 0};
+  if (attn::mfma_supported(a, false)) {
+    attn::launch_fwd_mfma(a, (hipStream_t)stream);
+    CCMPI_HIP_CHECK(hipGetLastError());
+    return;
+  }
   hipLaunchKernelGGL(k_attn_fwd, dim3(B * Hl), dim3(256), fwd_lds(S, D), (hipStream_t)stream, a);
   CCMPI_HIP_CHECK(hipGetLastError());
 }
@@ -250,6 +244,11 @@ void attn_bwd(uint64_t qkv, uint64_t o, uint64_t lse, uint64_t dout, uint64_t dq
   check_dims(S, D, true);
   AttnArgs a{(const uint16_t*)qkv, (uint16_t*)o, (float*)lse, (const uint16_t*)dout, (uint16_t*)dqkv, (float*)dbias,
              B, S, Hl, D, ld_qkv, ld_o, scale, nullptr, 0, dout_bstride, dout_rstride};
+  if (attn::mfma_supported(a, true)) {
+    attn::launch_bwd_mfma(a, (hipStream_t)stream);
+    CCMPI_HIP_CHECK(hipGetLastError());
+    return;
+  }
   hipLaunchKernelGGL(k_attn_bwd, dim3(B * Hl), dim3(256), bwd_lds(S, D), (hipStream_t)stream, a);
   CCMPI_HIP_CHECK(hipGetLastError());
 }

@@ -214,7 +214,8 @@ def _attn_ref(qkv, B, S, H, D):
     return (p @ v).transpose(1, 2).reshape(B * S, H * D)
 
 
-@pytest.mark.parametrize("B,S,H,D", [(3, 16, 2, 64), (2, 7, 1, 32), (4, 64, 2, 64)])
+@pytest.mark.parametrize("B,S,H,D", [(3, 16, 2, 64), (2, 7, 1, 32), (4, 64, 2, 64), (9, 1, 2, 32), (5, 16, 3, 128),
+                                     (2048, 16, 4, 64), (4096, 16, 3, 32), (6, 12, 4, 64), (3, 33, 2, 64)])
 def test_attn_small_fwd_bwd(B, S, H, D):
     from collective_communication_mpi_amd import _native
 
@@ -238,7 +239,10 @@ def test_attn_small_fwd_bwd(B, S, H, D):
                        dbias.data_ptr(), B, S, H, D, qkv.stride(0), o.stride(0), D ** -0.5, S * do.stride(0),
                        do.stride(0), st)
     torch.testing.assert_close(dqkv.float(), ref_in.grad, rtol=3e-2, atol=3e-2)
-    torch.testing.assert_close(dbias, dqkv.float().sum(0), rtol=1e-2, atol=1e-2)
+    # bias gradient = column sums of the fp32 gradient (not of the bf16-rounded dqkv:
+    # rounding noise over B*S rows would dominate at large B)
+    ref_b = ref_in.grad.sum(0)
+    assert (dbias - ref_b).norm() <= 2e-2 * ref_b.norm() + 1e-3, ((dbias - ref_b).abs().max(), ref_b.abs().max())
     # broadcast form: dO[b, s] = g[b] for every s (pooled-gradient path, row stride 0)
     gpool = torch.randn(B, H * D, device="cuda").bfloat16()
     ref_in.grad = None
