@@ -54,11 +54,11 @@ def main():
                 gemm_nt(a, b, out=c)
             return f
 
-        variants = {"k128": ours(1), "k256": ours(2), "k256x128": ours(3), "auto": ours(0),
+        variants = {"k128": ours(1), "k256": ours(2), "k256x192": ours(4), "auto": ours(0),
                     "hipblaslt": lambda: torch.matmul(a, b.T, out=c)}
         # correctness of both kernels on this shape against hipBLASLt
         ref = (a @ b.T).float()
-        for k in ("k128", "k256", "k256x128"):
+        for k in ("k128", "k256", "k256x192"):
             variants[k]()
             err = (c.float() - ref).abs().max().item()
             assert err < 0.05 * K ** 0.5, f"{k} {shp}: max err {err}"

@@ -277,34 +277,41 @@ __global__ void __launch_bounds__(256) k_adamw(float* __restrict__ p, const floa
 // MNIST patchify: x[B][img*img] fp32 -> xp[B*S][kp] bf16 with, per token row,
 // the patch pixels (p*p), a constant 1 (folds the embedding bias into the
 // GEMM) and a one-hot position (folds the learned position embedding into the
-// GEMM), zero-padded to kp.  One thread per output element.
+// GEMM), zero-padded to kp.  One thread per 8-column chunk of a token row
+// (one 16-B store); kp % 8 == 0.
 __global__ void __launch_bounds__(256) k_patchify(const float* __restrict__ x, uint16_t* __restrict__ xp, int B, int img,
                                                   int p, int kp) {
-  const int g = img / p, S = g * g, pp = p * p;
-  const uint64_t total = (uint64_t)B * S * kp;
+  const int g = img / p, S = g * g, pp = p * p, nch = kp / 8;
+  const uint64_t total = (uint64_t)B * S * nch;
   for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (uint64_t)gridDim.x * blockDim.x) {
-    const int c = (int)(e % kp);
-    const uint64_t row = e / kp;
+    const int ch = (int)(e % nch);
+    const uint64_t row = e / nch;
     const int s = (int)(row % S);
-    const uint64_t b = row / S;
-    float v = 0.f;
-    if (c < pp) {
-      const int py = (s / g) * p + c / p, px = (s % g) * p + c % p;
-      v = x[b * img * img + py * img + px];
-    } else if (c == pp) {
-      v = 1.f;
-    } else if (c == pp + 1 + s) {
-      v = 1.f;
+    const float* xb = x + (row / S) * img * img + (s / g) * p * img + (s % g) * p;
+    uint32_t w[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float v2[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int c = ch * 8 + 2 * q + h;
+        float v = 0.f;
+        if (c < pp) v = xb[(c / p) * img + c % p];
+        else if (c == pp || c == pp + 1 + s) v = 1.f;
+        v2[h] = v;
+      }
+      w[q] = f32_to_bf16_bits(v2[0]) | (f32_to_bf16_bits(v2[1]) << 16);
     }
-    xp[e] = (uint16_t)f32_to_bf16_bits(v);
+    *reinterpret_cast<uint4*>(xp + row * kp + ch * 8) = uint4{w[0], w[1], w[2], w[3]};
   }
 }
 
 void patchify(uint64_t x, uint64_t xp, int B, int img, int p, int kp, uint64_t stream) {
   const int S = (img / p) * (img / p);
   if (kp < p * p + 1 + S) throw std::invalid_argument("patchify: kp too small for pixels + bias + position columns");
-  const uint64_t total = (uint64_t)B * S * kp;
-  const int grid = (int)std::min<uint64_t>((total + 255) / 256, 4096);
+  if (kp % 8 || xp % 16) throw std::invalid_argument("patchify: kp % 8 == 0 and a 16-B aligned output required");
+  const uint64_t total = (uint64_t)B * S * (kp / 8);
+  const int grid = (int)std::min<uint64_t>((total + 255) / 256, 8192);
   hipLaunchKernelGGL(k_patchify, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const float*)x, (uint16_t*)xp, B, img,
                      p, kp);
   CCMPI_HIP_CHECK(hipGetLastError());

@@ -19,6 +19,7 @@
 // tiles land on the same XCD (shared A panel in that XCD's L2).
 #include <pybind11/pybind11.h>
 
+#include <algorithm>
 #include <cstdlib>
 
 #include "common.hpp"
@@ -33,7 +34,7 @@ using namespace gemm;
 
 constexpr int BM = 128, BN = 128, BK = 64, NT = 256;
 bool g_use_glds = std::getenv("CCMPI_GEMM_NO_GLDS") == nullptr;  // A/B switch (benchmarks)
-// kernel choice for gemm_nt: 0 auto, 1 = 128x128 only, 2 = 256x256 / 3 = 256x128 whenever legal
+// kernel choice for gemm_nt: 0 auto, 1 = 128x128 only, 2 = 256x256 / 3 = 256x128 / 4 = 256x192 whenever legal
 int g_kernel = std::getenv("CCMPI_GEMM_KERNEL") ? std::atoi(std::getenv("CCMPI_GEMM_KERNEL")) : 0;
 constexpr int kRowBytes = BK * 2;  // 128 B per LDS row
 
@@ -327,6 +328,162 @@ __global__ void __launch_bounds__(NT) k_gemm_tn(GemmArgs g) {
   store_tile(g, acc, smem, bm, bn, wm, wn, split, t, lane);
 }
 
+
+// ---------------------------------------------------------------------------
+// Small-K "NT" GEMM (K <= 128, e.g. the K = 72 patch embedding): the output
+// write dominates, so the kernel is built around it.  Each 256-thread block
+// owns a 256-column slice of B, kept in LDS for the whole launch, and walks
+// 64-row tiles of A (grid-strided), prefetching the next A tile into
+// registers while the current one is multiplied.  The MFMA operands are
+// swapped (first = B rows, second = A rows), so the accumulator of a 16x16
+// tile holds C[m = lane & 15][tile row 4*(lane >> 4) + r]; the tile rows of a
+// PAIR of tiles are mapped to 32 output columns as n = 8*(i >> 2) + 4*half +
+// (i & 3), so each lane ends up with 8 consecutive columns of one row and
+// stores them as one 16-B (bf16) vector -- no LDS round trip, no narrow
+// stores.  LDS rows are padded to an odd number of 16-B slots so 16-row
+// fragment reads are conflict-free.
+// ---------------------------------------------------------------------------
+constexpr int SK_BM = 64, SK_NT = 256;
+int g_sk_bn = std::getenv("CCMPI_SK_BN") ? std::atoi(std::getenv("CCMPI_SK_BN")) : 128;      // tuning knobs
+int g_sk_grid = std::getenv("CCMPI_SK_GRID") ? std::atoi(std::getenv("CCMPI_SK_GRID")) : 2048;
+
+template <int SK_BN>
+__global__ void __launch_bounds__(SK_NT) k_gemm_smallk(GemmArgs g, int kp) {
+  constexpr int WN = SK_BN / 4;  // columns per wave
+  constexpr int NP = WN / 32;    // column pairs (32 columns) per wave
+  constexpr int NJ = 2 * NP;     // 16-col MFMA tiles per wave
+  extern __shared__ __attribute__((aligned(16))) unsigned char sks[];
+  const int stride = kp * 2 + 16;                   // bytes per LDS row (odd # of 16-B slots)
+  unsigned char* Bs = sks;                          // SK_BN rows
+  unsigned char* As = sks + SK_BN * stride;         // 2 x SK_BM rows
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, c = lane & 15, gq = lane >> 4;
+  const int nchunk = kp / 8, kchunks = g.K / 8;     // 16-B chunks per LDS row / per global row
+  const int tiles_n = (g.N + SK_BN - 1) / SK_BN, tiles_m = (g.M + SK_BM - 1) / SK_BM;
+  const int tn = blockIdx.x % tiles_n;
+  const int bn = tn * SK_BN;
+  const int mstep = gridDim.x / tiles_n;            // blocks sharing this N slice
+  int tm = blockIdx.x / tiles_n;
+  if (tm >= tiles_m) return;
+  // B slice -> LDS (zero rows past N and chunks past K)
+  for (int idx = t; idx < SK_BN * nchunk; idx += SK_NT) {
+    const int r = idx / nchunk, ch = idx % nchunk;
+    uint4 v{0, 0, 0, 0};
+    if (bn + r < g.N && ch < kchunks) v = *reinterpret_cast<const uint4*>(g.B + (size_t)(bn + r) * g.ldb + ch * 8);
+    *reinterpret_cast<uint4*>(Bs + r * stride + ch * 16) = v;
+  }
+  constexpr int kMaxPer = SK_BM * 16 / SK_NT;       // A chunks per thread at kp = 128
+  uint4 ra[kMaxPer];
+  const int per = (SK_BM * nchunk + SK_NT - 1) / SK_NT;
+  auto gload = [&](int m0) {
+#pragma unroll
+    for (int i = 0; i < kMaxPer; ++i) {
+      const int idx = t + i * SK_NT, r = idx / nchunk, ch = idx % nchunk;
+      ra[i] = uint4{0, 0, 0, 0};
+      if (i < per && r < SK_BM && m0 + r < g.M && ch < kchunks)
+        ra[i] = *reinterpret_cast<const uint4*>(g.A + (size_t)(m0 + r) * g.lda + ch * 8);
+    }
+  };
+  auto swrite = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < kMaxPer; ++i) {
+      const int idx = t + i * SK_NT, r = idx / nchunk, ch = idx % nchunk;
+      if (i < per && r < SK_BM) *reinterpret_cast<uint4*>(As + (buf * SK_BM + r) * stride + ch * 16) = ra[i];
+    }
+  };
+  gload(tm * SK_BM);
+  swrite(0);
+  __syncthreads();
+  // this lane's output columns: pair p (32 columns) -> bn + WN*wave + 32p + 8*gq + 0..7
+  float bias[NP][8];
+#pragma unroll
+  for (int pr = 0; pr < NP; ++pr)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) bias[pr][e] = load_bias(g, bn + wave * WN + pr * 32 + 8 * gq + e, 0);
+  // B row feeding tile j's MFMA row c (the column permutation described above)
+  int brow[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) brow[j] = wave * WN + (j >> 1) * 32 + 8 * (c >> 2) + 4 * (j & 1) + (c & 3);
+  const int es = g.out_bf16 ? 2 : 4;
+  const bool vec_ok = (((uint64_t)g.C | ((uint64_t)g.ldc * es)) % 16) == 0;
+  int buf = 0;
+  for (; tm < tiles_m; tm += mstep) {
+    const int m0 = tm * SK_BM;
+    const bool more = tm + mstep < tiles_m;
+    if (more) gload((tm + mstep) * SK_BM);
+    floatx4 acc[4][NJ];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+    const unsigned char* A = As + buf * SK_BM * stride;
+    for (int ks = 0; ks < kp / 32; ++ks) {
+      const int ch = 4 * ks + gq;
+      bf16x8 fb[NJ], fa[4];
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) fb[j] = *reinterpret_cast<const bf16x8*>(Bs + brow[j] * stride + ch * 16);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) fa[i] = *reinterpret_cast<const bf16x8*>(A + (i * 16 + c) * stride + ch * 16);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
+    }
+    // epilogue: lane holds C[m0 + 16i + c][bn + WN*wave + 32p + 8*gq + e], e = 4*half + r
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = m0 + i * 16 + c;
+      if (row >= g.M) continue;
+#pragma unroll
+      for (int pr = 0; pr < NP; ++pr) {
+        const int col = bn + wave * WN + pr * 32 + 8 * gq;
+        if (col >= g.N) continue;
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = epi(g, acc[i][2 * pr + (e >> 2)][e & 3], bias[pr][e]);
+        if (vec_ok && col + 8 <= g.N) {
+          if (g.out_bf16) {
+            uint16_t* C = reinterpret_cast<uint16_t*>(g.C) + (size_t)row * g.ldc + col;
+            if (g.accumulate) {
+              const uint4 o = *reinterpret_cast<const uint4*>(C);
+              const uint32_t ow[4] = {o.x, o.y, o.z, o.w};
+#pragma unroll
+              for (int q = 0; q < 4; ++q) { v[2 * q] += bf16_lo(ow[q]); v[2 * q + 1] += bf16_hi(ow[q]); }
+            }
+            uint32_t w[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) w[q] = f32_to_bf16_bits(v[2 * q]) | (f32_to_bf16_bits(v[2 * q + 1]) << 16);
+            *reinterpret_cast<uint4*>(C) = uint4{w[0], w[1], w[2], w[3]};
+          } else {
+            float4* C = reinterpret_cast<float4*>(reinterpret_cast<float*>(g.C) + (size_t)row * g.ldc + col);
+            float4 o0 = make_float4(v[0], v[1], v[2], v[3]), o1 = make_float4(v[4], v[5], v[6], v[7]);
+            if (g.accumulate) {
+              const float4 p0 = C[0], p1 = C[1];
+              o0.x += p0.x; o0.y += p0.y; o0.z += p0.z; o0.w += p0.w;
+              o1.x += p1.x; o1.y += p1.y; o1.z += p1.z; o1.w += p1.w;
+            }
+            C[0] = o0;
+            C[1] = o1;
+          }
+        } else {
+          for (int e = 0; e < 8 && col + e < g.N; ++e) {
+            const size_t o = (size_t)row * g.ldc + col + e;
+            if (g.out_bf16) {
+              uint16_t* C = reinterpret_cast<uint16_t*>(g.C);
+              C[o] = (uint16_t)f32_to_bf16_bits(v[e] + (g.accumulate ? bf2f(C[o]) : 0.f));
+            } else {
+              float* C = reinterpret_cast<float*>(g.C);
+              C[o] = v[e] + (g.accumulate ? C[o] : 0.f);
+            }
+          }
+        }
+      }
+    }
+    if (more) swrite(buf ^ 1);
+    __syncthreads();
+    buf ^= 1;
+  }
+}
+
 // 2-D transpose of 16-bit elements through a padded 64x65 LDS tile.
 __global__ void __launch_bounds__(256) k_transpose16(const uint16_t* __restrict__ src, uint16_t* __restrict__ dst,
                                                      int R, int C, int lds, int ldd) {
@@ -359,13 +516,36 @@ void gemm_nt(uint64_t A, uint64_t B, uint64_t C, uint64_t bias, int M, int N, in
              reinterpret_cast<const void*>(bias), M, N, K, lda, ldb, ldc, alpha, accumulate ? 1 : 0, bias_kind,
              act, out_bf16 ? 1 : 0, splitk};
   const int nwg = ((M + BM - 1) / BM) * ((N + BN - 1) / BN) * splitk;
-  // 256 x {256, 128} ping-pong kernels: need K % 128 and enough tiles to
+  // small K (patch embedding): B slice resident in LDS, A tiles streamed, direct stores
+  // measured (benchmarks/smallk_sweep.py): wins over the 128x128 kernel up to K ~ 96
+  if (K <= 96 && splitk == 1 && g_kernel != 1 && g_sk_bn > 0 && M >= 4 * SK_BM) {
+    const int kp = (K + 31) / 32 * 32;
+    const int skbn = g_sk_bn == 256 ? 256 : 128;
+    const int tiles_n = (N + skbn - 1) / skbn, tiles_m = (M + SK_BM - 1) / SK_BM;
+    const int mblocks = std::max(1, std::min(tiles_m, std::max(1, g_sk_grid / tiles_n)));
+    const size_t lds = (size_t)(skbn + 2 * SK_BM) * (kp * 2 + 16);
+    static bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(k_gemm_smallk<256>),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess &&
+                       hipFuncSetAttribute(reinterpret_cast<const void*>(k_gemm_smallk<128>),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
+    (void)attr;
+    if (skbn == 256)
+      hipLaunchKernelGGL(k_gemm_smallk<256>, dim3(tiles_n * mblocks), dim3(SK_NT), lds,
+                         reinterpret_cast<hipStream_t>(stream), g, kp);
+    else
+      hipLaunchKernelGGL(k_gemm_smallk<128>, dim3(tiles_n * mblocks), dim3(SK_NT), lds,
+                         reinterpret_cast<hipStream_t>(stream), g, kp);
+    CCMPI_HIP_CHECK(hipGetLastError());
+    return;
+  }
+  // 256 x {256, 192, 128} ping-pong kernels: need K % 128 and enough tiles to
   // occupy the 256 CUs (one block per CU); smaller grids keep 128x128.
   const bool big_ok = K % (2 * BK) == 0 && g_use_glds;
   if (big_ok && g_kernel != 1) {
     int bn = 0;
     if (g_kernel == 2) bn = 256;
     else if (g_kernel == 3) bn = 128;
+    else if (g_kernel == 4) bn = 192;
     // measured (benchmarks/gemm_bench.py): 256x256 wins from ~4096^2 outputs up;
     // narrow N (<= 1024) stays on 128x128 (2 blocks/CU balance better)
     else if (gemm256_tiles(M, N, 256) * splitk >= 256 && M >= 1024 && N >= 1024) bn = 256;
@@ -419,8 +599,10 @@ void register_gemm_ops(pybind11::module_& m) {
   m.def("gemm_tn", &gemm_tn, "C[N1,N2] (+)= alpha*A[M,N1]^T.B[M,N2] (fp32 out, split-K atomics)",
         pybind11::call_guard<pybind11::gil_scoped_release>());
   m.def("gemm_set_glds", [](bool on) { g_use_glds = on; }, "select LDS-DMA (True) or register staging");
-  m.def("gemm_set_kernel", [](int k) { g_kernel = k; }, "gemm_nt tile choice: 0 auto, 1 128x128, 2 256x256, 3 256x128");
+  m.def("gemm_set_kernel", [](int k) { g_kernel = k; }, "gemm_nt tile choice: 0 auto, 1 128x128, 2 256x256, 3 256x128, 4 256x192");
   m.def("gemm_set_ablation", [](int e) { g_pp_exp = e; }, "ping-pong kernel ablation bits (benchmarks only)");
+  m.def("gemm_set_smallk", [](int bn, int grid) { g_sk_bn = bn; g_sk_grid = grid; },
+        "small-K kernel: N slice (128 / 256, 0 = off) and grid cap (tuning)");
   m.def("transpose16", &transpose16, "dst[C,R] = src[R,C]^T for 16-bit elements",
         pybind11::call_guard<pybind11::gil_scoped_release>());
 }

@@ -3,7 +3,8 @@
 // per phase.  Same contract and epilogue as k_gemm_nt (gemm.hip); requires
 // K % 128 == 0 (two K-tiles per main-loop iteration).  Two shapes:
 //   BN = 256: 256x256 tile, waves 2(M) x 4(N)   (large square-ish problems)
-//   BN = 128: 256x128 tile, waves 4(M) x 2(N)   (narrow N, e.g. N = 768)
+//   BN = 192: 256x192 tile, waves 4(M) x 2(N)   (N = 384 / 768: whole tiles per CU)
+//   BN = 128: 256x128 tile, waves 4(M) x 2(N)
 //
 // Block tile 256(M) x BN(N) x 64(K), 512 threads = 8 waves.
 //   * LDS: 2 buffers x {A rows 0-127, A rows 128-255, B rows 0..BN/2-1,
@@ -16,10 +17,10 @@
 //     v_mfma_f32_16x16x32_bf16) per phase, in the order (0,0) (0,1) (1,1)
 //     (1,0).  LDS reads per phase: A0+B0 | B1 | A1 | - (A and B0 fragments
 //     stay in registers across phases).
-//   * Every phase issues one half-tile of LDS-DMA and then waits with
-//     vmcnt(2*gA + 2*gB) (gA, gB = DMA instructions per wave for an A / B
-//     half-tile): the stage pattern repeats B,A,A,B, so exactly the half-tile
-//     issued four phases earlier is retired.  The stage order (below) puts each restage >= 2 phases after its
+//   * Every phase issues one half-tile of LDS-DMA (1 KiB piece q by wave
+//     q % 8) and then waits with vmcnt(2*2 + 2*nB) (nB = this wave's pieces of
+//     a B half-tile, 1 or 2): the stage pattern repeats B,A,A,B, so exactly the
+//     half-tile issued four phases earlier is retired.  The stage order (below) puts each restage >= 2 phases after its
 //     half's last read and each retire >= 1 phase before its first read, which
 //     is what the ping-pong barrier pattern requires (analysis in gemm256_schedule
 //     comment).
@@ -59,15 +60,17 @@ constexpr int kAHalf = 128 * 128;                // bytes per A half-tile
 
 template <int BN>
 struct Geo {
-  static constexpr int WR = BN == 256 ? 2 : 4;   // wave rows
-  static constexpr int WC = 8 / WR;              // wave cols
-  static constexpr int MI = 8 / WR;              // 16-row MFMA tiles per wave strip and half
-  static constexpr int BHalf = (BN / 2) * 128;   // bytes per B half-tile
-  static constexpr int GA = 2, GB = BHalf / 1024 / 8;  // DMA instr per wave per half-tile
-  static constexpr int VM = 2 * GA + 2 * GB;     // steady-state vmcnt
+  static constexpr int WR = BN == 256 ? 2 : 4;    // wave rows
+  static constexpr int WC = 8 / WR;               // wave cols
+  static constexpr int MI = 8 / WR;               // 16-row MFMA tiles per wave strip and half
+  static constexpr int NS = (BN / 2) / WC;        // wave column strip per B half
+  static constexpr int NJ = NS / 16;              // 16-col MFMA tiles per strip
+  static constexpr int BHalf = (BN / 2) * 128;    // bytes per B half-tile
+  static constexpr int BPieces = BHalf / 1024;    // 1 KiB DMA pieces per B half-tile (piece q -> wave q % 8)
   static constexpr int Buf = 2 * kAHalf + 2 * BHalf;
   static constexpr int EpiTS = BN + 4;
   static constexpr int Lds = (2 * Buf > 128 * EpiTS * 4) ? 2 * Buf : 128 * EpiTS * 4;
+  static_assert(NS % 16 == 0 && BPieces >= 8 && BPieces <= 16, "unsupported BN");
 };
 
 enum Slot { A0 = 0, A1 = 1, B0 = 2, B1 = 3 };
@@ -83,6 +86,11 @@ __device__ __forceinline__ void wait_vm() {
   if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
   else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+// steady state: this wave's DMA pieces of the last four stages (2 A + 2 B)
+__device__ __forceinline__ void wait_steady(int b_pieces) {
+  if (b_pieces == 2) wait_vm<8>();
+  else wait_vm<6>();
 }
 
 // EXP: ablation bits for benchmarks only (0 = production):
@@ -129,11 +137,11 @@ __global__ void __launch_bounds__(PNT, 1) k_gemm_nt_pp(GemmArgs g) {
     const int ld = isA ? g.lda : g.ldb, lim = (isA ? g.M : g.N) - 1;
     const int r0 = isA ? bm + (slot & 1) * 128 : bn + (slot & 1) * (BN / 2);
     const int k0 = (kt0 + kt) * PK;
-    const int n = isA ? G::GA : G::GB;
+    const int npieces = isA ? 16 : G::BPieces;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      if (i < n) {
-        const int q = wave * n + i;
+      const int q = i * 8 + wave;
+      if (q < npieces) {
         const int r = q * 8 + lrow;
         const int c = pchunk ^ (r & 7);
         const int gr = min(r0 + r, lim);
@@ -144,7 +152,8 @@ __global__ void __launch_bounds__(PNT, 1) k_gemm_nt_pp(GemmArgs g) {
     }
   };
 
-  floatx4 acc[2][2][G::MI][2];
+  const int b_pieces = (wave + 8 < G::BPieces) ? 2 : 1;  // this wave's share of a B half-tile
+  floatx4 acc[2][2][G::MI][G::NJ];
 #pragma unroll
   for (int a = 0; a < 2; ++a)
 #pragma unroll
@@ -152,9 +161,9 @@ __global__ void __launch_bounds__(PNT, 1) k_gemm_nt_pp(GemmArgs g) {
 #pragma unroll
       for (int i = 0; i < G::MI; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[a][b][i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+        for (int j = 0; j < G::NJ; ++j) acc[a][b][i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
 
-  bf16x8 fa[G::MI][2], fb0[2][2], fb1[2][2];
+  bf16x8 fa[G::MI][2], fb0[G::NJ][2], fb1[G::NJ][2];
   auto read_a = [&](int buf, int h) {
     const unsigned char* base = lds(buf, h);
 #pragma unroll
@@ -166,18 +175,18 @@ __global__ void __launch_bounds__(PNT, 1) k_gemm_nt_pp(GemmArgs g) {
         fa[i][ks] = *reinterpret_cast<const bf16x8*>(base + row * 128 + ((chunk ^ (row & 7)) << 4));
       }
   };
-  auto read_b = [&](int buf, int h, bf16x8 (&fb)[2][2]) {
+  auto read_b = [&](int buf, int h, bf16x8 (&fb)[G::NJ][2]) {
     const unsigned char* base = lds(buf, 2 + h);
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < G::NJ; ++j)
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
-        const int row = wc * 32 + j * 16 + (lane & 15);
+        const int row = wc * G::NS + j * 16 + (lane & 15);
         const int chunk = ks * 4 + (lane >> 4);
         fb[j][ks] = *reinterpret_cast<const bf16x8*>(base + row * 128 + ((chunk ^ (row & 7)) << 4));
       }
   };
-  auto mma = [&](int mh, int nh, bf16x8 (&fb)[2][2]) {
+  auto mma = [&](int mh, int nh, bf16x8 (&fb)[G::NJ][2]) {
     bar();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
@@ -187,7 +196,7 @@ __global__ void __launch_bounds__(PNT, 1) k_gemm_nt_pp(GemmArgs g) {
 #pragma unroll
       for (int i = 0; i < G::MI; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
+        for (int j = 0; j < G::NJ; ++j)
           acc[mh][nh][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][ks], fb[j][ks], acc[mh][nh][i][j], 0, 0, 0);
     if constexpr (!(EXP & 2)) __builtin_amdgcn_s_setprio(0);
     bar();
@@ -198,7 +207,7 @@ __global__ void __launch_bounds__(PNT, 1) k_gemm_nt_pp(GemmArgs g) {
       if (tail) wait_vm<0>();
     } else {
       if (tail) wait_vm<0>();
-      else wait_vm<G::VM>();
+      else wait_steady(b_pieces);
     }
   };
 
@@ -210,7 +219,7 @@ __global__ void __launch_bounds__(PNT, 1) k_gemm_nt_pp(GemmArgs g) {
     stage(0, A1, 0);
     stage(1, A0, 1);
     stage(1, B0, 1);
-    wait_vm<G::VM>();  // buf0 A0, B0 landed
+    wait_steady(b_pieces);  // buf0 A0, B0 landed (the 4 younger stages may stay in flight)
   }
   __syncthreads();
   if (!(EXP & 4) && grp == 1) bar();  // group 1 runs one barrier behind group 0
@@ -270,8 +279,8 @@ __global__ void __launch_bounds__(PNT, 1) k_gemm_nt_pp(GemmArgs g) {
 #pragma unroll
     for (int nh = 0; nh < 2; ++nh)
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int cl = nh * (BN / 2) + wc * 32 + j * 16 + (lane & 15);
+      for (int j = 0; j < G::NJ; ++j) {
+        const int cl = nh * (BN / 2) + wc * G::NS + j * 16 + (lane & 15);
         const float b = load_bias(g, bn + cl, split);
 #pragma unroll
         for (int i = 0; i < G::MI; ++i)
@@ -305,6 +314,7 @@ int g_pp_exp = 0;  // ablation variant (benchmarks only)
 
 void launch_gemm_nt_256(const GemmArgs& g, int bn, hipStream_t stream) {
   if (bn == 128) return launch_pp<128, 0>(g, stream);
+  if (bn == 192) return launch_pp<192, 0>(g, stream);
   switch (g_pp_exp) {
     case 1: return launch_pp<256, 1>(g, stream);
     case 2: return launch_pp<256, 2>(g, stream);

@@ -23,6 +23,7 @@ def _ref(a, b, bias=None, act=None, alpha=1.0):
 
 
 @pytest.mark.parametrize("M,N,K", [(1, 1, 8), (16, 16, 32), (128, 128, 64), (130, 70, 72), (2048, 768, 64),
+                                   (32768, 768, 72), (1000, 300, 40), (513, 1000, 128), (300, 7, 8),
                                    (4096, 768, 768), (32768, 384, 768), (777, 1000, 520)])
 def test_gemm_nt_shapes(M, N, K):
     from collective_communication_mpi_amd.ops import gemm_nt
@@ -35,7 +36,7 @@ def test_gemm_nt_shapes(M, N, K):
     torch.testing.assert_close(y, ref, rtol=2e-3, atol=2e-3 * K ** 0.5)
 
 
-@pytest.fixture(params=[2, 3], ids=["256x256", "256x128"])
+@pytest.fixture(params=[2, 3, 4], ids=["256x256", "256x128", "256x192"])
 def gemm256(request):
     """Force a large-tile ping-pong kernel whenever legal (K % 128 == 0)."""
     from collective_communication_mpi_amd import _native
@@ -47,7 +48,8 @@ def gemm256(request):
 
 
 @pytest.mark.parametrize("M,N,K", [(256, 256, 128), (1, 8, 128), (300, 520, 256), (777, 1000, 512),
-                                   (4096, 768, 768), (2048, 2048, 4096), (32768, 768, 768)])
+                                   (4096, 768, 768), (2048, 2048, 4096), (32768, 768, 768), (32768, 384, 768),
+                                   (512, 200, 384)])
 def test_gemm256_shapes(gemm256, M, N, K):
     from collective_communication_mpi_amd.ops import gemm_nt
 
@@ -111,6 +113,26 @@ def test_gemm_epilogue(act, bias_dtype):
     bias = torch.randn(200, device="cuda").to(bias_dtype)
     y = gemm_nt(a, b, bias=bias, act=act, alpha=0.5)
     torch.testing.assert_close(y.float(), _ref(a, b, bias, act, 0.5), rtol=2e-2, atol=5e-2)
+
+
+@pytest.mark.parametrize("out_dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("slice_bn", [128, 256])
+def test_gemm_smallk_epilogue(out_dtype, slice_bn):
+    """K <= 96 path (LDS-resident B, direct vector stores): bias, act, accumulate, both outputs."""
+    from collective_communication_mpi_amd import _native
+    from collective_communication_mpi_amd.ops import gemm_nt
+
+    _native.device().gemm_set_smallk(slice_bn, 2048)
+    a = torch.randn(700, 72, device="cuda").bfloat16()
+    b = torch.randn(520, 72, device="cuda").bfloat16()
+    bias = torch.randn(520, device="cuda")
+    y = gemm_nt(a, b, bias=bias, act="gelu", alpha=0.5, out_dtype=out_dtype)
+    torch.testing.assert_close(y.float(), _ref(a, b, bias, "gelu", 0.5), rtol=2e-2, atol=5e-2)
+    c = torch.randn(700, 520, device="cuda").to(out_dtype)
+    c0 = c.float().clone()
+    gemm_nt(a, b, out=c, accumulate=True, splitk=1)
+    _native.device().gemm_set_smallk(128, 2048)
+    torch.testing.assert_close(c.float(), c0 + _ref(a, b), rtol=2e-2, atol=8e-2)
 
 
 def test_gemm_accumulate_strided():
