@@ -54,6 +54,7 @@ PYBIND11_MODULE(_device, m) {
         d.rccl_init(u);
       })
       .def_property_readonly("rccl_ready", &DeviceComm::rccl_ready)
+      .def("rccl_register_segments", &DeviceComm::rccl_register_segments, py::call_guard<py::gil_scoped_release>())
       .def("rccl_split_from", [](DeviceComm& d, DeviceComm* parent, int color, int key) {
         py::gil_scoped_release g;
         d.rccl_split_from(parent, color, key);

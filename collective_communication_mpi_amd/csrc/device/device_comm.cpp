@@ -98,6 +98,7 @@ DeviceComm::DeviceComm(int rank, int size, int device, uint64_t /*scratch_bytes*
   CCMPI_HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&host_pt_.host_err), host_err_, 0));
   if (const char* t = std::getenv("CCMPI_DEVICE_TIMEOUT_S")) set_timeout_seconds(std::atof(t));
   if (const char* c = std::getenv("CCMPI_COPY_ENGINE")) copy_engine_ = std::atoi(c) != 0;
+  if (const char* c = std::getenv("CCMPI_CHUNK_BYTES")) chunk_cap_ = std::strtoull(c, nullptr, 10);
   CCMPI_HIP_CHECK(hipDeviceSynchronize());
   sync_table_();
 }
@@ -105,6 +106,8 @@ DeviceComm::DeviceComm(int rank, int size, int device, uint64_t /*scratch_bytes*
 DeviceComm::~DeviceComm() {
   (void)hipSetDevice(device_);
   (void)hipDeviceSynchronize();
+  for (void* h : rccl_regs_)
+    if (nccl_ && h) ncclCommDeregister(nccl_, h);
   if (nccl_) ncclCommDestroy(nccl_);
   for (auto& h : opened_) ipc_close(h);
   if (sig_) (void)hipFree(sig_);
@@ -246,7 +249,7 @@ void DeviceComm::allreduce(uint64_t in, uint64_t out, uint64_t count, int dtype,
   }
   if (scratch_bytes() < 64 * es) throw std::runtime_error("ccmpi: scratch segment missing or too small");
   // chunk size identical on all ranks: half the scratch, 16-B and element aligned
-  uint64_t chunk = (scratch_bytes() / 2) / (16 * es) * (16 * es);
+  uint64_t chunk = staging_chunk_(scratch_bytes() / 2, 16 * es);
   char* stage = reinterpret_cast<char*>(scratch_ptr());
   for (uint64_t off = 0; off < nbytes; off += chunk) {
     const uint64_t n = std::min(chunk, nbytes - off);
@@ -288,7 +291,7 @@ void DeviceComm::reduce_scatter(uint64_t in, uint64_t out, uint64_t count_per_ra
     launch_reduce_scatter(args_(sc, 0, (char*)out, blk, 0), size_, dtype, op, grid_(blk, max_blocks), st);
     return;
   }
-  uint64_t chunk = (scratch_bytes() / 2 / size_) / (16 * es) * (16 * es);
+  uint64_t chunk = staging_chunk_(scratch_bytes() / 2 / size_, 16 * es);
   if (chunk == 0) throw std::runtime_error("ccmpi: scratch too small for reduce_scatter");
   char* stage = reinterpret_cast<char*>(scratch_ptr());
   for (uint64_t off = 0; off < blk; off += chunk) {
@@ -324,7 +327,7 @@ void DeviceComm::allgather(uint64_t in, uint64_t out, uint64_t bytes_per_rank, u
   // chunk over the per-rank block; destination blocks are strided by
   // bytes_per_rank so each chunk gathers into a [p][n] staging area first
   // unless the output layout can take it directly (n == bytes_per_rank).
-  uint64_t chunk = (scratch_bytes() / 2 / (size_ + 1)) / 16 * 16;
+  uint64_t chunk = staging_chunk_(scratch_bytes() / 2 / (size_ + 1), 16);
   if (chunk == 0) throw std::runtime_error("ccmpi: scratch too small for allgather");
   char* stage = reinterpret_cast<char*>(scratch_ptr());
   char* gath = stage + chunk;
@@ -359,7 +362,7 @@ void DeviceComm::alltoall(uint64_t in, uint64_t out, uint64_t bytes_per_peer, ui
     launch_move(MOVE_ALLTOALL, args_(sc, 0, (char*)out, bytes_per_peer, 0), size_, grid_(total, max_blocks), st);
     return;
   }
-  uint64_t chunk = (scratch_bytes() / 2 / size_) / 16 * 16;
+  uint64_t chunk = staging_chunk_(scratch_bytes() / 2 / size_, 16);
   if (chunk == 0) throw std::runtime_error("ccmpi: scratch too small for alltoall");
   char* stage = reinterpret_cast<char*>(scratch_ptr());
   char* gath = stage + scratch_bytes() / 2;
@@ -472,6 +475,25 @@ void DeviceComm::rccl_init(const std::string& uid) {
   std::memcpy(&id, uid.data(), sizeof(id));
   CCMPI_HIP_CHECK(hipSetDevice(device_));
   CCMPI_NCCL_CHECK(ncclCommInitRank(&nccl_, size_, id, rank_));
+}
+
+int DeviceComm::rccl_register_segments() {
+  if (!nccl_) return 0;
+  CCMPI_HIP_CHECK(hipSetDevice(device_));
+  for (size_t s = rccl_regs_.size(); s < segs_.size(); ++s) {
+    void* h = nullptr;
+    if (ncclCommRegister(nccl_, segs_[s].local, segs_[s].bytes, &h) != ncclSuccess) h = nullptr;  // best effort
+    rccl_regs_.push_back(h);
+  }
+  int n = 0;
+  for (void* h : rccl_regs_) n += h != nullptr;
+  return n;
+}
+
+uint64_t DeviceComm::staging_chunk_(uint64_t budget, uint64_t align) const {
+  uint64_t c = budget;
+  if (chunk_cap_ && chunk_cap_ < c) c = chunk_cap_;
+  return c / align * align;
 }
 
 void DeviceComm::rccl_split_from(DeviceComm* parent, int color, int key) {

@@ -75,6 +75,9 @@ class DeviceComm {
   // ---- RCCL (vendor library: baseline + P2P transport) ---------------------
   static std::string rccl_unique_id();
   void rccl_init(const std::string& uid);
+  // best-effort ncclCommRegister of every symmetric segment (zero-copy RCCL
+  // collectives on them); returns how many segments are registered
+  int rccl_register_segments();
   // collective over the PARENT's RCCL comm (every parent rank calls; color < 0 = not a member)
   void rccl_split_from(DeviceComm* parent, int color, int key);
   static void rccl_split_leave(DeviceComm* parent);
@@ -118,6 +121,9 @@ class DeviceComm {
   std::vector<std::vector<char*>> peer_seg_;  // [seg][rank]
   PeerTable host_pt_{};
   uint32_t* host_err_ = nullptr;         // pinned, device-mapped timeout mirror
+  std::vector<void*> rccl_regs_;         // ncclCommRegister handles, one per registered segment
+  uint64_t chunk_cap_ = 0;               // CCMPI_CHUNK_BYTES: cap on staging chunks (0 = scratch-sized)
+  uint64_t staging_chunk_(uint64_t budget, uint64_t align) const;
   PeerTable* dev_pt_ = nullptr;
   uint64_t* epochs_ = nullptr;
   uint64_t timeout_ticks_ = 2000000000ull;  // 20 s

@@ -153,7 +153,12 @@ class DeviceGroup:
         seg = self.dc.add_segment(t.data_ptr(), t.numel() * t.element_size(),
                                   [x[0] for x in allh], [x[1] for x in allh])
         self._keep.append(t)
+        if self._rccl_registering():
+            self.dc.rccl_register_segments()
         return seg
+
+    def _rccl_registering(self) -> bool:
+        return getattr(self, "_rccl", False) and os.environ.get("CCMPI_RCCL_REGISTER") == "1"
 
     def empty(self, shape, dtype=None, pool_bytes: int = 64 << 20):
         """Collective symmetric allocation (same call sequence on every rank).
@@ -212,6 +217,8 @@ class DeviceGroup:
         uid = self.host.bcast(uid, root=0)
         self.dc.rccl_init(uid)
         self._rccl = True
+        if os.environ.get("CCMPI_RCCL_REGISTER") == "1":  # user-buffer registration of the symmetric heap
+            self.dc.rccl_register_segments()
 
     def split_rccl_into(self, child: Optional["DeviceGroup"], color: int, key: int) -> None:
         """Collective over THIS group's ranks: derive the child group's RCCL

@@ -35,7 +35,8 @@ parser.add_argument("--device", default="cpu", choices=["cpu", "cuda"])
 parser.add_argument("--size", type=int, default=100, help="elements for myallreduce (reference: 100)")
 parser.add_argument("--dtype", default="int64")
 parser.add_argument("--algo", default="", help="myAllreduce/myAlltoall algorithm (default: reference algorithm)")
-parser.add_argument("--runs", type=int, default=100)
+parser.add_argument("--runs", "--iters", type=int, default=100, help="timed runs (reference: 100)")
+parser.add_argument("--warmup", type=int, default=0, help="untimed runs before the timed ones")
 parser.add_argument("--seed", type=int, default=0)
 
 
@@ -85,6 +86,12 @@ def timed_compare(comm, bufs, args, make_input, library, mine, label, lib_label)
     rng = np.random.default_rng(args.seed + rank)
     lib_times, my_times = [], []
     all_ok = True
+    for _ in range(args.warmup):  # untimed: first-touch, RCCL/IPC setup, kernel loads
+        src, n, dtype = make_input(rng)
+        library(src, bufs.empty(n, dtype))
+        mine(src, bufs.empty(n, dtype))
+        bufs.sync()
+    comm.Barrier()
     for run in range(args.runs):
         src, n, dtype = make_input(rng)
         a = bufs.empty(n, dtype)
