@@ -69,17 +69,26 @@ _NP2DT = {
 }
 
 
+_DT_CACHE: dict = {}
+
+
 def dtype_code(dt) -> int:
     """Native dtype code for a numpy dtype (``"bfloat16"`` for bf16 payloads)."""
+    code = _DT_CACHE.get(dt) if isinstance(dt, np.dtype) else None
+    if code is not None:
+        return code
     if isinstance(dt, str) and dt == "bfloat16":
         return DT_BF16
     d = np.dtype(dt)
     if d.byteorder not in ("=", "|"):
         d = d.newbyteorder("=")
     try:
-        return _NP2DT[d]
+        code = _NP2DT[d]
     except KeyError:
         raise TypeError(f"MPI: unsupported buffer dtype {dt!r}") from None
+    if isinstance(dt, np.dtype):
+        _DT_CACHE[dt] = code
+    return code
 
 
 class Datatype:
@@ -213,6 +222,12 @@ def _as_array(x, writable: bool):
 def _parse(spec, writable: bool) -> Optional[_Buf]:
     """Accept ``arr``, ``[arr, Datatype]``, ``[arr, count, Datatype]`` or
     ``[arr, (counts, displs), Datatype]`` / ``[arr, counts, displs, Datatype]``."""
+    if type(spec) is np.ndarray:  # fast path: a plain contiguous NumPy buffer (the common case)
+        f = spec.flags
+        if f.c_contiguous and (f.writeable or not writable):
+            code = _DT_CACHE.get(spec.dtype)
+            if code is not None:
+                return _Buf(spec, code)
     if spec is None or spec is IN_PLACE:
         return None
     counts = displs = None
@@ -281,6 +296,8 @@ class Status:
 
 class Request:
     """Wraps a native request and keeps its buffer alive until completion."""
+
+    __slots__ = ("_comm", "_native", "_keep", "_decode", "_done", "_result")
 
     def __init__(self, comm: "Comm", native, keep, decode=None) -> None:
         self._comm, self._native, self._keep, self._decode = comm, native, keep, decode
