@@ -34,6 +34,9 @@ using namespace gemm;
 
 constexpr int BM = 128, BN = 128, BK = 64, NT = 256;
 bool g_use_glds = std::getenv("CCMPI_GEMM_NO_GLDS") == nullptr;  // A/B switch (benchmarks)
+bool g_direct_epi = std::getenv("CCMPI_GEMM_STAGED_EPI") == nullptr;  // LDS-free epilogue (A/B switch)
+bool g_persist = std::getenv("CCMPI_GEMM_PERSIST") != nullptr;       // persistent 128x128 kernel (A/B switch; measured no gain)
+int g_persist_grid = 512;                                            // 2 workgroups per CU
 // kernel choice for gemm_nt: 0 auto, 1 = 128x128 only, 2 = 256x256 / 3 = 256x128 / 4 = 256x192 whenever legal
 int g_kernel = std::getenv("CCMPI_GEMM_KERNEL") ? std::atoi(std::getenv("CCMPI_GEMM_KERNEL")) : 0;
 constexpr int kRowBytes = BK * 2;  // 128 B per LDS row
@@ -56,6 +59,78 @@ __device__ __forceinline__ void store_tile(const GemmArgs& g, floatx4 (&acc)[4][
   }
   __syncthreads();
   store_rows<BM, BN, NT>(g, tile, TS, bm, bn, t);
+}
+
+// Direct (LDS-free) epilogue for kernels that swap the MFMA operands and stage
+// B rows in the "pair" permutation: LDS row 32p + 16h + q of the B tile holds
+// output column 32p + 8*(q >> 2) + 4h + (q & 3).  The accumulator of tile
+// (i, j = 2p + h) then holds C[row0 + 16i + (lane & 15)][col0 + 32p + 8*(lane >> 4) + 4h + r],
+// i.e. 8 consecutive columns of one row per lane and pair: one 16-B vector store
+// (bf16) or two (fp32).  Split-K partials go out as fp32 atomics.
+__device__ __forceinline__ int pair_perm(int r) {
+  return (r & ~31) | (((r & 15) >> 2) << 3) | (((r >> 4) & 1) << 2) | (r & 3);
+}
+
+__device__ __forceinline__ void store_direct(const GemmArgs& g, const floatx4 (&acc)[4][4], int row0, int col0, int split,
+                                             int lane) {
+  const int c = lane & 15, gq = lane >> 4;
+  const int es = g.out_bf16 ? 2 : 4;
+  const bool vec_ok = (((uint64_t)g.C | ((uint64_t)g.ldc * es)) % 16) == 0;
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const int col = col0 + 32 * p + 8 * gq;
+    if (col >= g.N) continue;
+    float bias[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) bias[e] = load_bias(g, col + e, split);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = row0 + 16 * i + c;
+      if (row >= g.M) continue;
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = epi(g, acc[i][2 * p + (e >> 2)][e & 3], bias[e]);
+      if (g.splitk > 1) {
+        float* C = reinterpret_cast<float*>(g.C) + (size_t)row * g.ldc + col;
+        for (int e = 0; e < 8 && col + e < g.N; ++e) atomicAdd(C + e, v[e]);
+      } else if (vec_ok && col + 8 <= g.N) {
+        if (g.out_bf16) {
+          uint16_t* C = reinterpret_cast<uint16_t*>(g.C) + (size_t)row * g.ldc + col;
+          if (g.accumulate) {
+            const uint4 o = *reinterpret_cast<const uint4*>(C);
+            const uint32_t ow[4] = {o.x, o.y, o.z, o.w};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) { v[2 * q] += bf16_lo(ow[q]); v[2 * q + 1] += bf16_hi(ow[q]); }
+          }
+          uint32_t w[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) w[q] = f32_to_bf16_bits(v[2 * q]) | (f32_to_bf16_bits(v[2 * q + 1]) << 16);
+          *reinterpret_cast<uint4*>(C) = uint4{w[0], w[1], w[2], w[3]};
+        } else {
+          float4* C = reinterpret_cast<float4*>(reinterpret_cast<float*>(g.C) + (size_t)row * g.ldc + col);
+          float4 o0 = make_float4(v[0], v[1], v[2], v[3]), o1 = make_float4(v[4], v[5], v[6], v[7]);
+          if (g.accumulate) {
+            const float4 p0 = C[0], p1 = C[1];
+            o0.x += p0.x; o0.y += p0.y; o0.z += p0.z; o0.w += p0.w;
+            o1.x += p1.x; o1.y += p1.y; o1.z += p1.z; o1.w += p1.w;
+          }
+          C[0] = o0;
+          C[1] = o1;
+        }
+      } else {
+        for (int e = 0; e < 8 && col + e < g.N; ++e) {
+          const size_t o = (size_t)row * g.ldc + col + e;
+          if (g.out_bf16) {
+            uint16_t* C = reinterpret_cast<uint16_t*>(g.C);
+            C[o] = (uint16_t)f32_to_bf16_bits(v[e] + (g.accumulate ? bf2f(C[o]) : 0.f));
+          } else {
+            float* C = reinterpret_cast<float*>(g.C);
+            C[o] = v[e] + (g.accumulate ? C[o] : 0.f);
+          }
+        }
+      }
+    }
+  }
 }
 
 __global__ void __launch_bounds__(NT) k_gemm_nt(GemmArgs g) {
@@ -150,8 +225,14 @@ __global__ void __launch_bounds__(NT) k_gemm_nt(GemmArgs g) {
 // chunk swizzle the fragment reads expect is applied to the per-lane SOURCE
 // address (the same involution on both sides).  Rows past M / N re-read the
 // last valid row (their outputs are discarded); used only when K % 64 == 0.
+__constant__ int g_pp_exp_dev = 0;
+
+// DIRECT: swapped MFMA operands + pair-permuted B staging + LDS-free epilogue
+// (store_direct); otherwise the LDS-staged row epilogue (store_tile).
+template <bool DIRECT>
 __global__ void __launch_bounds__(NT) k_gemm_nt_glds(GemmArgs g) {
-  __shared__ __attribute__((aligned(16))) unsigned char smem[(2 * (BM + BN) * kRowBytes > BM * (BN + 4) * 4) ? 2 * (BM + BN) * kRowBytes : BM * (BN + 4) * 4];
+  constexpr int kLoop = 2 * (BM + BN) * kRowBytes, kEpi = DIRECT ? 0 : BM * (BN + 4) * 4;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[kLoop > kEpi ? kLoop : kEpi];
   const int tiles_n = (g.N + BN - 1) / BN, tiles_m = (g.M + BM - 1) / BM;
   const int nwg = tiles_n * tiles_m * g.splitk;
   int wg = blockIdx.x;
@@ -182,7 +263,7 @@ __global__ void __launch_bounds__(NT) k_gemm_nt_glds(GemmArgs g) {
       const int q = wave * 4 + i;                 // 1 KiB LDS chunk = rows q*8 .. q*8+7
       const int r = q * 8 + lrow;
       const int c = pchunk ^ (r & 7);             // logical k-chunk this lane must fetch
-      const int ga = min(bm + r, g.M - 1), gb = min(bn + r, g.N - 1);
+      const int ga = min(bm + r, g.M - 1), gb = min(bn + (DIRECT ? pair_perm(r) : r), g.N - 1);
       __builtin_amdgcn_global_load_lds((const void*)(g.A + (size_t)ga * g.lda + k0 + c * 8),
                                        (__attribute__((address_space(3))) void*)(As(buf) + q * 1024), 16, 0, 0);
       __builtin_amdgcn_global_load_lds((const void*)(g.B + (size_t)gb * g.ldb + k0 + c * 8),
@@ -198,29 +279,183 @@ __global__ void __launch_bounds__(NT) k_gemm_nt_glds(GemmArgs g) {
   __syncthreads();
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
-    if (kt + 1 < nk) issue((kt0 + kt + 1) * BK, cur ^ 1);
+    // all fragment reads of this K-tile BEFORE the next tile's DMA is issued:
+    // the compiler cannot prove the DMA target disjoint from the reads and
+    // would otherwise wait for the DMA before the remaining ds_reads
+    bf16x8 af[2][4], bf[2][4];
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      bf16x8 af[4], bf[4];
       const int chunk = ks * 4 + (lane >> 4);
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int ra_ = wm + i * 16 + (lane & 15);
-        af[i] = *reinterpret_cast<const bf16x8*>(As(cur) + ra_ * kRowBytes + ((chunk ^ (ra_ & 7)) << 4));
+        af[ks][i] = *reinterpret_cast<const bf16x8*>(As(cur) + ra_ * kRowBytes + ((chunk ^ (ra_ & 7)) << 4));
         const int rb_ = wn + i * 16 + (lane & 15);
-        bf[i] = *reinterpret_cast<const bf16x8*>(Bs(cur) + rb_ * kRowBytes + ((chunk ^ (rb_ & 7)) << 4));
+        bf[ks][i] = *reinterpret_cast<const bf16x8*>(Bs(cur) + rb_ * kRowBytes + ((chunk ^ (rb_ & 7)) << 4));
       }
-      __builtin_amdgcn_s_setprio(1);
+    }
+    if (kt + 1 < nk) issue((kt0 + kt + 1) * BK, cur ^ 1);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf[j], acc[i][j], 0, 0, 0);
-      __builtin_amdgcn_s_setprio(0);
-    }
+        for (int j = 0; j < 4; ++j) {
+          if constexpr (DIRECT) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[ks][j], af[ks][i], acc[i][j], 0, 0, 0);
+          else acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ks][i], bf[ks][j], acc[i][j], 0, 0, 0);
+        }
+    __builtin_amdgcn_s_setprio(0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
-  store_tile(g, acc, smem, bm, bn, wm, wn, split, t, lane);
+  if (g_pp_exp_dev & 8) {  // ablation (benchmarks only): no epilogue, accumulators kept live
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(acc[i][j]));
+    return;
+  }
+  if constexpr (DIRECT) store_direct(g, acc, bm + wm, bn + wn, split, lane);
+  else store_tile(g, acc, smem, bm, bn, wm, wn, split, t, lane);
+}
+
+
+// Persistent form of k_gemm_nt_glds<DIRECT = true> (LDS-free epilogue): each
+// workgroup walks tiles blockIdx.x, +gridDim.x, ... (XCD-remapped), and issues
+// the NEXT tile's first K-tile DMA before this tile's epilogue stores, so the
+// stores drain while the next tile computes (two co-resident workgroups on a CU
+// otherwise reach their store phases in lockstep and the stores serialize with
+// the MFMA work).  vmcnt retires in issue order, so waiting for that prefetch
+// must skip exactly the younger stores: on the fast path (full tiles, splitk 1,
+// no accumulate, 16-B aligned C) a wave issues 8 (bf16) or 16 (fp32) of them;
+// otherwise it waits for everything.
+// workgroup barrier WITHOUT the release/acquire fences of __syncthreads(): those
+// lower to s_waitcnt vmcnt(0), i.e. they would wait for every in-flight global
+// store.  LDS ordering comes from the explicit waits placed before each call.
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_barrier" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+__device__ __forceinline__ void wait_vm_stores(int n) {
+  if (n == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if (n == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// FULL: M % 128 == 0 and N % 128 == 0 -- no row clamping, so the DMA
+// addresses are a uniform (SGPR) tile base plus per-lane offsets computed once:
+// no VGPR that an in-flight DMA reads is rewritten between tiles (the compiler
+// would otherwise wait for every outstanding memory operation, stores included).
+template <bool FULL>
+__global__ void __launch_bounds__(NT) k_gemm_nt_persist(GemmArgs g) {
+  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * (BM + BN) * kRowBytes];
+  const int tiles_n = (g.N + BN - 1) / BN, tiles_m = (g.M + BM - 1) / BM;
+  const int ntiles = tiles_n * tiles_m;
+  const int t = threadIdx.x, lane = t & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
+  auto As = [&](int buf) { return smem + buf * ((BM + BN) * kRowBytes); };
+  auto Bs = [&](int buf) { return smem + buf * ((BM + BN) * kRowBytes) + BM * kRowBytes; };
+  const int es = g.out_bf16 ? 2 : 4;
+  const bool fast = g.splitk == 1 && !g.accumulate && g.M % BM == 0 && g.N % BN == 0 &&
+                    (((uint64_t)g.C | ((uint64_t)g.ldc * es)) % 16) == 0;
+  const int nstores = fast ? (g.out_bf16 ? 8 : 16) : 0;
+  const int lrow = lane >> 3, pchunk = lane & 7;
+  auto coords = [&](int L, int& bm, int& bn) {
+    const int wg = xcd_remap(L, ntiles);
+    bm = (wg / tiles_n) * BM;
+    bn = (wg % tiles_n) * BN;
+  };
+  uint32_t aoff[4], boff[4];  // per-lane BYTE offsets within a tile (FULL path; saddr + voffset form)
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = (wave * 4 + i) * 8 + lrow, c = pchunk ^ (r & 7);
+    aoff[i] = (uint32_t)(r * g.lda + c * 8) * 2u;
+    boff[i] = (uint32_t)(pair_perm(r) * g.ldb + c * 8) * 2u;
+  }
+  auto issue = [&](int bm, int bn, int k0, int buf) {
+    const char* Ab = reinterpret_cast<const char*>(g.A + (size_t)bm * g.lda + k0);
+    const char* Bb = reinterpret_cast<const char*>(g.B + (size_t)bn * g.ldb + k0);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int q = wave * 4 + i;
+      const void *pa, *pb;
+      if constexpr (FULL) {
+        pa = Ab + aoff[i];
+        pb = Bb + boff[i];
+      } else {
+        const int r = q * 8 + lrow, c = pchunk ^ (r & 7);
+        pa = g.A + (size_t)min(bm + r, g.M - 1) * g.lda + k0 + c * 8;
+        pb = g.B + (size_t)min(bn + pair_perm(r), g.N - 1) * g.ldb + k0 + c * 8;
+      }
+      __builtin_amdgcn_global_load_lds(pa, (__attribute__((address_space(3))) void*)(As(buf) + q * 1024),
+                                       16, 0, 0);
+      __builtin_amdgcn_global_load_lds(pb, (__attribute__((address_space(3))) void*)(Bs(buf) + q * 1024),
+                                       16, 0, 0);
+    }
+  };
+  const int nk = g.K / BK;
+  int L = blockIdx.x;
+  if (L >= ntiles || nk == 0) return;
+  int bm, bn;
+  coords(L, bm, bn);
+  int buf = 0;
+  issue(bm, bn, 0, buf);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (;;) {
+    const int Ln = L + gridDim.x;
+    const bool more = Ln < ntiles;
+    int bmn = 0, bnn = 0;
+    if (more) coords(Ln, bmn, bnn);
+    floatx4 acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+    for (int kt = 0; kt < nk; ++kt) {
+      const int cur = buf;
+      bf16x8 af[2][4], bf[2][4];  // all fragment reads before the DMA (see k_gemm_nt_glds)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int chunk = ks * 4 + (lane >> 4);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int ra_ = wm + i * 16 + (lane & 15);
+          af[ks][i] = *reinterpret_cast<const bf16x8*>(As(cur) + ra_ * kRowBytes + ((chunk ^ (ra_ & 7)) << 4));
+          const int rb_ = wn + i * 16 + (lane & 15);
+          bf[ks][i] = *reinterpret_cast<const bf16x8*>(Bs(cur) + rb_ * kRowBytes + ((chunk ^ (rb_ & 7)) << 4));
+        }
+      }
+      if (kt + 1 < nk) issue(bm, bn, (kt + 1) * BK, cur ^ 1);
+      else if (more) issue(bmn, bnn, 0, cur ^ 1);  // next tile's first K-tile, ahead of our stores
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[ks][j], af[ks][i], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      buf ^= 1;
+      if (kt + 1 < nk) {
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        lds_barrier();
+      }
+    }
+    store_direct(g, acc, bm + wm, bn + wn, 0, lane);
+    if (!more) break;
+    wait_vm_stores(nstores);  // the prefetched K-tile has landed; this tile's stores may still be in flight
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    lds_barrier();
+    L = Ln;
+    bm = bmn;
+    bn = bnn;
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -555,8 +790,18 @@ void gemm_nt(uint64_t A, uint64_t B, uint64_t C, uint64_t bias, int M, int N, in
       return;
     }
   }
-  if (K % BK == 0 && g_use_glds)
-    hipLaunchKernelGGL(k_gemm_nt_glds, dim3(nwg), dim3(NT), 0, reinterpret_cast<hipStream_t>(stream), g);
+  if (K % BK == 0 && g_use_glds) {
+    if (g_direct_epi && splitk == 1 && g_persist) {
+      int grid = std::min(nwg, g_persist_grid);
+      if (M % BM == 0 && N % BN == 0)
+        hipLaunchKernelGGL(k_gemm_nt_persist<true>, dim3(grid), dim3(NT), 0, reinterpret_cast<hipStream_t>(stream), g);
+      else
+        hipLaunchKernelGGL(k_gemm_nt_persist<false>, dim3(grid), dim3(NT), 0, reinterpret_cast<hipStream_t>(stream), g);
+    } else if (g_direct_epi)
+      hipLaunchKernelGGL(k_gemm_nt_glds<true>, dim3(nwg), dim3(NT), 0, reinterpret_cast<hipStream_t>(stream), g);
+    else
+      hipLaunchKernelGGL(k_gemm_nt_glds<false>, dim3(nwg), dim3(NT), 0, reinterpret_cast<hipStream_t>(stream), g);
+  }
   else
     hipLaunchKernelGGL(k_gemm_nt, dim3(nwg), dim3(NT), 0, reinterpret_cast<hipStream_t>(stream), g);
   CCMPI_HIP_CHECK(hipGetLastError());
@@ -599,8 +844,15 @@ void register_gemm_ops(pybind11::module_& m) {
   m.def("gemm_tn", &gemm_tn, "C[N1,N2] (+)= alpha*A[M,N1]^T.B[M,N2] (fp32 out, split-K atomics)",
         pybind11::call_guard<pybind11::gil_scoped_release>());
   m.def("gemm_set_glds", [](bool on) { g_use_glds = on; }, "select LDS-DMA (True) or register staging");
+  m.def("gemm_set_persistent", [](bool on, int grid) { g_persist = on; g_persist_grid = grid > 0 ? grid : 512; },
+        "persistent 128x128 kernel (next-tile prefetch ahead of the epilogue stores) and its grid");
+  m.def("gemm_set_direct_epilogue", [](bool on) { g_direct_epi = on; },
+        "128x128 LDS-DMA kernel: LDS-free epilogue (True) or LDS-staged rows");
   m.def("gemm_set_kernel", [](int k) { g_kernel = k; }, "gemm_nt tile choice: 0 auto, 1 128x128, 2 256x256, 3 256x128, 4 256x192");
-  m.def("gemm_set_ablation", [](int e) { g_pp_exp = e; }, "ping-pong kernel ablation bits (benchmarks only)");
+  m.def("gemm_set_ablation", [](int e) {
+    g_pp_exp = e;
+    CCMPI_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_pp_exp_dev), &e, sizeof(int)));
+  }, "GEMM ablation bits (benchmarks only): 1/2/4 ping-pong kernel, 8 = skip the 128x128 epilogue");
   m.def("gemm_set_smallk", [](int bn, int grid) { g_sk_bn = bn; g_sk_grid = grid; },
         "small-K kernel: N slice (128 / 256, 0 = off) and grid cap (tuning)");
   m.def("transpose16", &transpose16, "dst[C,R] = src[R,C]^T for 16-bit elements",
