@@ -1,0 +1,89 @@
+// Fused classifier head of the harness training step: softmax cross-entropy
+// on z + b (z = pooled fc_o output, fp32 [B][ld_z], b = output bias), in one
+// launch instead of ~9 PyTorch kernels (log_softmax, gather, sum, exp,
+// index_put, div, column sum, zero + scatter of the bf16 gradient):
+//
+//   loss      += sum_b -log softmax(z_b + bias)[y_b] * scale
+//   dz[b][c]   = (softmax(z_b + bias)[c] - [c == y_b]) * scale   (bf16, 0 for c >= n_classes)
+//   dbias[c]  += sum_b dz[b][c]                                  (fp32)
+//
+// scale = 1 / global batch.  One thread per row (n_classes is small); the
+// per-class bias gradient and the loss are reduced in LDS per workgroup and
+// added with one atomic per class per workgroup.
+#include <pybind11/pybind11.h>
+
+#include "common.hpp"
+#include "ops.hpp"
+
+namespace ccmpi {
+namespace dev {
+
+namespace {
+
+constexpr int kMaxClasses = 64;
+
+__global__ void __launch_bounds__(256) k_xent_head(const float* __restrict__ z, int ld_z, const float* __restrict__ bias,
+                                                   const void* __restrict__ y, int y64, int B, int C, int Cpad, float scale,
+                                                   float* __restrict__ loss, uint16_t* __restrict__ dz, int ld_dz,
+                                                   float* __restrict__ dbias) {
+  __shared__ float s_db[kMaxClasses];
+  __shared__ float s_loss;
+  const int t = threadIdx.x;
+  for (int c = t; c < C; c += blockDim.x) s_db[c] = 0.f;
+  if (t == 0) s_loss = 0.f;
+  __syncthreads();
+  const int b = blockIdx.x * blockDim.x + t;
+  const bool live = b < B;  // every lane takes part in the wave reductions
+  const float* zr = z + (size_t)(live ? b : 0) * ld_z;
+  auto logit = [&](int c) { return zr[c] + (bias ? bias[c] : 0.f); };
+  float m = -INFINITY;
+  for (int c = 0; c < C; ++c) m = fmaxf(m, logit(c));
+  float s = 0.f;
+  for (int c = 0; c < C; ++c) s += __expf(logit(c) - m);
+  const float inv = 1.f / s;
+  const int label = !live ? -1 : y64 ? (int)reinterpret_cast<const int64_t*>(y)[b] : reinterpret_cast<const int32_t*>(y)[b];
+  const float lse = m + __logf(s);
+  const float zy = (label >= 0 && label < C) ? logit(label) : lse;
+  auto wsum = [](float x) {
+    for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
+    return x;
+  };
+  const float l = wsum(live ? (lse - zy) * scale : 0.f);
+  if ((t & 63) == 0) atomicAdd(&s_loss, l);
+  uint16_t* dr = dz + (size_t)b * ld_dz;
+  for (int c = 0; c < Cpad; ++c) {
+    float g = 0.f;
+    if (c < C) {
+      g = live ? (__expf(logit(c) - m) * inv - (c == label ? 1.f : 0.f)) * scale : 0.f;
+      const float gs = wsum(g);
+      if ((t & 63) == 0) atomicAdd(&s_db[c], gs);
+    }
+    if (live) dr[c] = (uint16_t)f32_to_bf16_bits(g);
+  }
+  __syncthreads();
+  if (dbias)
+    for (int c = t; c < C; c += blockDim.x) atomicAdd(dbias + c, s_db[c]);
+  if (t == 0) atomicAdd(loss, s_loss);
+}
+
+void xent_head(uint64_t z, int ld_z, uint64_t bias, uint64_t y, bool y64, int B, int C, int Cpad, float scale,
+               uint64_t loss, uint64_t dz, int ld_dz, uint64_t dbias, uint64_t stream) {
+  if (C < 1 || C > kMaxClasses || Cpad < C) throw std::invalid_argument("xent_head: need 1 <= n_classes <= 64 <= pad");
+  if (B <= 0) return;
+  CCMPI_HIP_CHECK(hipMemsetAsync(reinterpret_cast<void*>(loss), 0, sizeof(float), (hipStream_t)stream));
+  hipLaunchKernelGGL(k_xent_head, dim3((B + 255) / 256), dim3(256), 0, (hipStream_t)stream, (const float*)z, ld_z,
+                     (const float*)bias, (const void*)y, y64 ? 1 : 0, B, C, Cpad, scale, (float*)loss, (uint16_t*)dz, ld_dz,
+                     (float*)dbias);
+  CCMPI_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace
+
+void register_head_ops(pybind11::module_& m) {
+  m.def("xent_head", &xent_head,
+        "fused softmax cross-entropy head: loss (+=, zeroed first), bf16 dz, dbias += column sums",
+        pybind11::call_guard<pybind11::gil_scoped_release>());
+}
+
+}  // namespace dev
+}  // namespace ccmpi

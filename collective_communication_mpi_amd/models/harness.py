@@ -44,9 +44,13 @@ def build(comm, tp: int, batch: int, **kw):
 def train_step(layer: MnistTPLayer, cfg: LayerConfig, xb, yb):
     xp = patchify(xb, cfg)
     logits = layer.forward(xp, xb.shape[0])
-    loss, dlogits = layer.loss_and_grad(logits, yb, cfg.batch * cfg.dp)
     layer.zero_grad()
-    layer.backward(dlogits)
+    if cfg.fc_o_mode == "row" or cfg.tp == 1:
+        loss = layer.loss_and_grad_fused(yb, cfg.batch * cfg.dp)  # one kernel: loss, dZ, d o_b
+        layer.backward(None)
+    else:
+        loss, dlogits = layer.loss_and_grad(logits, yb, cfg.batch * cfg.dp)
+        layer.backward(dlogits)
     layer.step()
     return loss
 

@@ -74,6 +74,7 @@ class LayerConfig:
     seed: int = 1234
     dp_algo: str = "auto"
     overlap: bool = True
+    plain_gemm: str = "hipblaslt"  # backward dH = dQKV . W_qkv (no epilogue): "hipblaslt" | "own"
 
     @property
     def seq(self) -> int:
@@ -248,6 +249,26 @@ class MnistTPLayer:
         return torch.cat(list(parts), dim=1).contiguous()
 
     # ------------------------------------------------------------ backward
+    def loss_and_grad_fused(self, y: torch.Tensor, global_batch: int) -> torch.Tensor:
+        """Row (pooled) fc_o mode: softmax cross-entropy on the saved pooled logits in ONE
+        HIP kernel (csrc/device/head.hip).  Writes the bf16 head gradient dZ (read by
+        backward) and adds dL/d o_b to the flat gradient; returns the local loss sum /
+        global batch as a 1-element tensor."""
+        cfg = self.cfg
+        B = y.numel()
+        zp = self._buf("zp", (B, cfg.out_pad), torch.float32, self.tp_dev)
+        dzp = self._buf("dzp", (B, cfg.out_pad), torch.bfloat16)
+        loss = self._buf("loss", (1,), torch.float32)
+        if y.dtype not in (torch.int32, torch.int64) or not y.is_contiguous():
+            y = y.to(torch.int32).contiguous()
+        _native.device().xent_head(zp.data_ptr(), zp.stride(0), self.flat.param("o_b").data_ptr(), y.data_ptr(),
+                                   y.dtype == torch.int64, B,
+                                   cfg.n_classes, cfg.out_pad, 1.0 / global_batch, loss.data_ptr(), dzp.data_ptr(),
+                                   dzp.stride(0), self.flat.grad("o_b").data_ptr(),
+                                   torch.cuda.current_stream(self.device).cuda_stream)
+        self._dz_ready = True
+        return loss[0]
+
     def loss_and_grad(self, logits: torch.Tensor, y: torch.Tensor, global_batch: int):
         """Cross-entropy (mean over the global batch); returns (local loss sum / global batch, dlogits)."""
         lp = torch.log_softmax(logits, dim=1)
@@ -256,7 +277,8 @@ class MnistTPLayer:
         dlogits[torch.arange(y.numel(), device=y.device), y.long()] -= 1.0
         return loss, dlogits / global_batch
 
-    def backward(self, dlogits: torch.Tensor) -> None:
+    def backward(self, dlogits: Optional[torch.Tensor]) -> None:
+        """dlogits=None: the fused head (loss_and_grad_fused) already wrote dZ and dL/d o_b."""
         cfg = self.cfg
         xp, h, qkv, att, lse, B, pool = self._saved
         S, d = cfg.seq, cfg.d_model
@@ -266,7 +288,9 @@ class MnistTPLayer:
         D = _native.device()
         st = torch.cuda.current_stream(self.device).cuda_stream
         # ---- output head: logits[b,c] = mean_s z[b,s,c] + o_b  (z = att . W_o^T)
-        G("o_b")[: cfg.n_classes].add_(dlogits.sum(0))
+        fused = dlogits is None
+        if not fused:
+            G("o_b")[: cfg.n_classes].add_(dlogits.sum(0))
         if cfg.fc_o_mode == "naive" and cfg.tp > 1:
             dz = self._buf("dz", (M, cfg.out_pad), torch.bfloat16)
             dz.zero_()
@@ -278,8 +302,9 @@ class MnistTPLayer:
             # pooled row-parallel fc_o: dZ is replicated on every TP rank (identity backward
             # of the reduce); d(att[b,s]) = dpool[b] / S for every s, broadcast in the kernel
             dzp = self._buf("dzp", (B, cfg.out_pad), torch.bfloat16)
-            dzp.zero_()
-            dzp[:, : cfg.n_classes] = dlogits.to(torch.bfloat16)
+            if not fused:
+                dzp.zero_()
+                dzp[:, : cfg.n_classes] = dlogits.to(torch.bfloat16)
             gemm_tn(dzp, pool, out=G("o_w"), accumulate=True)    # dW_o = dZ^T . pooled
             dpool = self._buf("dpool", (B, self.hd), torch.bfloat16)
             gemm_nt(dzp, transpose(P16("o_w")), out=dpool, alpha=1.0 / S)
@@ -294,7 +319,10 @@ class MnistTPLayer:
         gemm_tn(dqkv, h, out=G("qkv_w"), accumulate=True)      # dW_qkv = dQKV^T . h
         self.buckets.ready(1)
         dh = self._buf("dh", (M, d), torch.bfloat16)            # TP-partial input gradient
-        gemm_nt(dqkv, transpose(P16("qkv_w")), out=dh)
+        if cfg.plain_gemm == "hipblaslt":
+            torch.matmul(dqkv, P16("qkv_w"), out=dh)            # plain GEMM, weight in its stored layout
+        else:
+            gemm_nt(dqkv, transpose(P16("qkv_w")), out=dh)
         # ---- embedding (replicated across TP): only its weight gradient needs the TP sum
         if self.tp_dev is not None:
             gpart = self._buf("gemb", (d, cfg.kp), torch.float32, self.tp_dev)

@@ -306,3 +306,28 @@ def test_fused_adamw_matches_torch():
         opt.step()
     torch.testing.assert_close(fp.param("w"), ref.detach(), rtol=1e-5, atol=1e-6)
     torch.testing.assert_close(fp.param16("w").float(), ref.detach().bfloat16().float())
+
+
+@pytest.mark.parametrize("ydtype", [torch.int32, torch.int64])
+def test_xent_head_fused(ydtype):
+    """Fused softmax cross-entropy head vs torch (loss, dZ incl. zero padding, d bias)."""
+    from collective_communication_mpi_amd import _native
+
+    B, C, Cp, gb = 777, 10, 16, 3000
+    z = torch.randn(B, Cp, device="cuda") * 3
+    bias = torch.randn(Cp, device="cuda")
+    y = torch.randint(0, C, (B,), device="cuda").to(ydtype)
+    loss = torch.empty(1, device="cuda")
+    dz = torch.full((B, Cp), 7.0, device="cuda").bfloat16()
+    db = torch.ones(Cp, device="cuda")
+    _native.device().xent_head(z.data_ptr(), z.stride(0), bias.data_ptr(), y.data_ptr(), ydtype == torch.int64, B, C,
+                               Cp, 1.0 / gb, loss.data_ptr(), dz.data_ptr(), dz.stride(0), db.data_ptr(),
+                               torch.cuda.current_stream().cuda_stream)
+    logits = (z[:, :C] + bias[:C]).requires_grad_(True)
+    ref = torch.nn.functional.cross_entropy(logits, y.long(), reduction="sum") / gb
+    ref.backward()
+    torch.testing.assert_close(loss[0], ref.detach(), rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(dz[:, :C].float(), logits.grad, rtol=1e-2, atol=1e-5)
+    assert torch.all(dz[:, C:] == 0)
+    torch.testing.assert_close(db[:C], 1 + logits.grad.sum(0), rtol=1e-4, atol=1e-6)
+    torch.testing.assert_close(db[C:], torch.ones(Cp - C, device="cuda"))
