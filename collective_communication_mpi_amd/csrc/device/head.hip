@@ -22,7 +22,7 @@ namespace {
 
 constexpr int kMaxClasses = 64;
 
-__global__ void __launch_bounds__(256) k_xent_head(const float* __restrict__ z, int ld_z, const float* __restrict__ bias,
+__global__ void __launch_bounds__(64) k_xent_head(const float* __restrict__ z, int ld_z, const float* __restrict__ bias,
                                                    const void* __restrict__ y, int y64, int B, int C, int Cpad, float scale,
                                                    float* __restrict__ loss, uint16_t* __restrict__ dz, int ld_dz,
                                                    float* __restrict__ dbias) {
@@ -71,7 +71,8 @@ void xent_head(uint64_t z, int ld_z, uint64_t bias, uint64_t y, bool y64, int B,
   if (C < 1 || C > kMaxClasses || Cpad < C) throw std::invalid_argument("xent_head: need 1 <= n_classes <= 64 <= pad");
   if (B <= 0) return;
   CCMPI_HIP_CHECK(hipMemsetAsync(reinterpret_cast<void*>(loss), 0, sizeof(float), (hipStream_t)stream));
-  hipLaunchKernelGGL(k_xent_head, dim3((B + 255) / 256), dim3(256), 0, (hipStream_t)stream, (const float*)z, ld_z,
+  // one wave per workgroup: the kernel is latency bound, so spread rows over many CUs
+  hipLaunchKernelGGL(k_xent_head, dim3((B + 63) / 64), dim3(64), 0, (hipStream_t)stream, (const float*)z, ld_z,
                      (const float*)bias, (const void*)y, y64 ? 1 : 0, B, C, Cpad, scale, (float*)loss, (uint16_t*)dz, ld_dz,
                      (float*)dbias);
   CCMPI_HIP_CHECK(hipGetLastError());
