@@ -28,6 +28,7 @@ struct AttnArgs {
 bool mfma_supported(const AttnArgs& a, bool bwd);
 void launch_fwd_mfma(const AttnArgs& a, hipStream_t stream);
 void launch_bwd_mfma(const AttnArgs& a, hipStream_t stream);
+extern int g_bwd_grid_cap;  // workgroups of the backward kernel when it also reduces the bias gradient
 
 }  // namespace attn
 }  // namespace dev

@@ -165,32 +165,16 @@ __global__ void __launch_bounds__(256) k_attn16_bwd(AttnArgs a) {
   uint16_t* Kt = Qt + TILE;
   uint16_t* Dt = Kt + TILE;
   uint16_t* Ot = Dt + TILE;
-  const int S = a.S, HD = a.Hl * D, npairs = a.B * a.Hl;
+  const int S = a.S, HD = a.Hl * D;
   float bq[NT], bk[NT], bv[NT];
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt) bq[nt] = bk[nt] = bv[nt] = 0.f;
-  int hcur = -1;
-  auto flush = [&](int h) {  // column sums of dQ, dK, dV for head h -> dbias
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt) {
-      float q = bq[nt], k = bk[nt], v = bv[nt];
-      q += __shfl_xor(q, 16); q += __shfl_xor(q, 32);
-      k += __shfl_xor(k, 16); k += __shfl_xor(k, 32);
-      v += __shfl_xor(v, 16); v += __shfl_xor(v, 32);
-      if (g == 0) {
-        atomicAdd(a.dbias + h * D + 16 * nt + c, q);
-        atomicAdd(a.dbias + HD + h * D + 16 * nt + c, k);
-        atomicAdd(a.dbias + 2 * HD + h * D + 16 * nt + c, v);
-      }
-      bq[nt] = bk[nt] = bv[nt] = 0.f;
-    }
-  };
-  for (int pr = blockIdx.x * WPB + wave; pr < npairs; pr += gridDim.x * WPB) {
-    const int b = pr / a.Hl, h = pr % a.Hl;
-    if (a.dbias && h != hcur) {
-      if (hcur >= 0) flush(hcur);
-      hcur = h;
-    }
+  // workgroup k owns head h = k % Hl; its waves stride over the batch, so the
+  // bias column sums of the 4 waves meet in LDS and leave with one atomic per
+  // column per workgroup (per-wave atomics on the same 3*D addresses contend)
+  const int h = blockIdx.x % a.Hl, nbh = gridDim.x / a.Hl;
+  for (int b = (blockIdx.x / a.Hl) * WPB + wave; b < a.B; b += nbh * WPB) {
+    const int pr = b * a.Hl + h;
     const uint16_t* qb = a.qkv + (size_t)b * S * a.ld_qkv + h * D;
     const uint16_t* ob = a.o + (size_t)b * S * a.ld_o + h * D;
     const uint16_t* db = a.dout + (size_t)b * a.dout_bstride + h * D;
@@ -266,7 +250,29 @@ __global__ void __launch_bounds__(256) k_attn16_bwd(AttnArgs a) {
     }
     store_tile<D, LD>(Ot, acc, a.scale, gq, a.ld_qkv, S, lane);
   }
-  if (a.dbias && hcur >= 0) flush(hcur);
+  if (a.dbias) {
+    float* red = reinterpret_cast<float*>(sm);  // reuse the tiles: [WPB][3][D] fp32
+    __syncthreads();
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      float q = bq[nt], k = bk[nt], v = bv[nt];
+      q += __shfl_xor(q, 16); q += __shfl_xor(q, 32);
+      k += __shfl_xor(k, 16); k += __shfl_xor(k, 32);
+      v += __shfl_xor(v, 16); v += __shfl_xor(v, 32);
+      if (g == 0) {
+        red[(wave * 3 + 0) * D + 16 * nt + c] = q;
+        red[(wave * 3 + 1) * D + 16 * nt + c] = k;
+        red[(wave * 3 + 2) * D + 16 * nt + c] = v;
+      }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < 3 * D; i += blockDim.x) {
+      float acc = 0.f;
+#pragma unroll
+      for (int w = 0; w < WPB; ++w) acc += red[w * 3 * D + i];
+      atomicAdd(a.dbias + (i / D) * HD + h * D + i % D, acc);
+    }
+  }
 }
 
 template <int D>
@@ -292,9 +298,13 @@ void launch_fwd_mfma(const AttnArgs& a, hipStream_t stream) {
   else hipLaunchKernelGGL(k_attn16_fwd<128>, dim3(grid), dim3(256), 0, stream, a);
 }
 
+int g_bwd_grid_cap = 0;  // tuning knob (attn_set_bwd_grid); 0 = 256 workgroups per head (measured best)
+
 void launch_bwd_mfma(const AttnArgs& a, hipStream_t stream) {
-  // fewer, longer-lived waves: every wave flushes its bias column sums once
-  const int grid = grid_for(a.B * a.Hl, a.dbias ? 1024 : 4096);
+  // a multiple of Hl workgroups (each owns one head); with the bias gradient,
+  // fewer longer-lived workgroups keep its atomics few
+  int grid = grid_for(a.B * a.Hl, a.dbias ? (g_bwd_grid_cap > 0 ? g_bwd_grid_cap : 256 * a.Hl) : 4096);
+  grid = std::max(a.Hl, grid / a.Hl * a.Hl);
   if (a.D == 32) {
     hipLaunchKernelGGL(k_attn16_bwd<32>, dim3(grid), dim3(256), bwd_lds_bytes<32>(), stream, a);
   } else if (a.D == 64) {

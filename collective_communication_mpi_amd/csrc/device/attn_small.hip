@@ -340,6 +340,8 @@ void cast_bf16(uint64_t x, uint64_t y, uint64_t n, uint64_t stream) {
 }  // namespace
 
 void register_attn_ops(pybind11::module_& m) {
+  m.def("attn_set_bwd_grid", [](int cap) { attn::g_bwd_grid_cap = cap > 0 ? cap : 0; },
+        "backward kernel grid cap (tuning)");
   namespace py = pybind11;
   m.def("attn_small_fwd", &attn_fwd, py::call_guard<py::gil_scoped_release>());
   m.def("attn_small_bwd", &attn_bwd, py::call_guard<py::gil_scoped_release>());
