@@ -11,6 +11,7 @@ from collective_communication_mpi_amd.ops import gemm_nt  # noqa: E402
 
 D = _native.device()
 D.gemm_set_kernel(1)
+D.gemm_set_bk32(False)
 
 
 def t(fn, iters=20):
@@ -32,15 +33,13 @@ for M, N, K in [(32768, 768, 768), (32768, 768, 2304), (8192, 8192, 1024)]:
     for _ in range(3):
         for od in (torch.bfloat16, torch.float32):
             c = torch.empty(M, N, device="cuda", dtype=od)
-            for ab in (0, 8, 16, 32):
+            for ab in (0, 8, 16):
                 D.gemm_set_ablation(ab & 8)
                 D.gemm_set_direct_epilogue(ab != 16)
-                D.gemm_set_persistent(ab not in (8, 32), 512)
-                tag = {0: "-persist", 8: "-noepi", 16: "-staged", 32: "-direct"}[ab]
+                tag = {0: "-fast", 8: "-noepi", 16: "-staged"}[ab]
                 res.setdefault(f"{'bf16' if od == torch.bfloat16 else 'fp32'}{tag}", []).append(
                     t(lambda: gemm_nt(a, b, out=c, splitk=1)))
             D.gemm_set_direct_epilogue(True)
-            D.gemm_set_persistent(True, 512)
     D.gemm_set_ablation(0)
     fl = 2 * M * N * K
     print(f"{M}x{N}x{K}: " + "  ".join(f"{k} {sorted(v)[1]:.1f}us ({fl / sorted(v)[1] / 1e6:.0f}TF)" for k, v in res.items()),

@@ -37,6 +37,7 @@ bool g_use_glds = std::getenv("CCMPI_GEMM_NO_GLDS") == nullptr;  // A/B switch (
 bool g_direct_epi = std::getenv("CCMPI_GEMM_STAGED_EPI") == nullptr;  // LDS-free epilogue (A/B switch)
 bool g_persist = std::getenv("CCMPI_GEMM_PERSIST") != nullptr;       // persistent 128x128 kernel (A/B switch; measured no gain)
 int g_persist_grid = 512;                                            // 2 workgroups per CU
+bool g_bk32 = std::getenv("CCMPI_GEMM_BK64") == nullptr;             // BK = 32 / 32 KiB LDS variant (A/B switch)
 // kernel choice for gemm_nt: 0 auto, 1 = 128x128 only, 2 = 256x256 / 3 = 256x128 / 4 = 256x192 whenever legal
 int g_kernel = std::getenv("CCMPI_GEMM_KERNEL") ? std::atoi(std::getenv("CCMPI_GEMM_KERNEL")) : 0;
 constexpr int kRowBytes = BK * 2;  // 128 B per LDS row
@@ -127,6 +128,47 @@ __device__ __forceinline__ void store_direct(const GemmArgs& g, const floatx4 (&
             float* C = reinterpret_cast<float*>(g.C);
             C[o] = v[e] + (g.accumulate ? C[o] : 0.f);
           }
+        }
+      }
+    }
+  }
+}
+
+// Branch-free specialization of store_direct for the common case (splitk 1, no
+// accumulate, no activation, 16-B aligned C, N % 8 == 0): output type and bias
+// kind are compile-time, so the epilogue is straight-line code (the generic one
+// unrolls every runtime combination into ~12k instructions).
+template <bool OUT_BF16, int BIAS>
+__device__ __forceinline__ void store_direct_fast(const GemmArgs& g, const floatx4 (&acc)[4][4], int row0, int col0,
+                                                  int lane) {
+  const int c = lane & 15, gq = lane >> 4;
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const int col = col0 + 32 * p + 8 * gq;
+    float bias[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      if constexpr (BIAS == 1) bias[e] = col < g.N ? reinterpret_cast<const float*>(g.bias)[col + e] : 0.f;
+      else if constexpr (BIAS == 2) bias[e] = col < g.N ? bf2f(reinterpret_cast<const uint16_t*>(g.bias)[col + e]) : 0.f;
+      else bias[e] = 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = row0 + 16 * i + c;
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = g.alpha * acc[i][2 * p + (e >> 2)][e & 3] + bias[e];
+      if (row < g.M && col < g.N) {
+        if constexpr (OUT_BF16) {
+          uint32_t w[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) w[q] = f32_to_bf16_bits(v[2 * q]) | (f32_to_bf16_bits(v[2 * q + 1]) << 16);
+          *reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(g.C) + (size_t)row * g.ldc + col) =
+              uint4{w[0], w[1], w[2], w[3]};
+        } else {
+          float4* C = reinterpret_cast<float4*>(reinterpret_cast<float*>(g.C) + (size_t)row * g.ldc + col);
+          C[0] = make_float4(v[0], v[1], v[2], v[3]);
+          C[1] = make_float4(v[4], v[5], v[6], v[7]);
         }
       }
     }
@@ -229,7 +271,7 @@ __constant__ int g_pp_exp_dev = 0;
 
 // DIRECT: swapped MFMA operands + pair-permuted B staging + LDS-free epilogue
 // (store_direct); otherwise the LDS-staged row epilogue (store_tile).
-template <bool DIRECT>
+template <bool DIRECT, int FAST = 0>  // FAST = 1 + out_bf16 + 2 * bias_kind (store_direct_fast), 0 = generic
 __global__ void __launch_bounds__(NT) k_gemm_nt_glds(GemmArgs g) {
   constexpr int kLoop = 2 * (BM + BN) * kRowBytes, kEpi = DIRECT ? 0 : BM * (BN + 4) * 4;
   __shared__ __attribute__((aligned(16))) unsigned char smem[kLoop > kEpi ? kLoop : kEpi];
@@ -316,10 +358,86 @@ __global__ void __launch_bounds__(NT) k_gemm_nt_glds(GemmArgs g) {
       for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(acc[i][j]));
     return;
   }
-  if constexpr (DIRECT) store_direct(g, acc, bm + wm, bn + wn, split, lane);
+  constexpr bool kFastBf16 = ((FAST - 1) & 1) != 0;
+  constexpr int kFastBias = (FAST - 1) / 2;
+  if constexpr (DIRECT && FAST > 0) store_direct_fast<kFastBf16, kFastBias>(g, acc, bm + wm, bn + wn, lane);
+  else if constexpr (DIRECT) store_direct(g, acc, bm + wm, bn + wn, split, lane);
   else store_tile(g, acc, smem, bm, bn, wm, wn, split, t, lane);
 }
 
+
+
+// BK = 32 variant of k_gemm_nt_glds<DIRECT = true>: a 32 KiB double buffer
+// instead of 64 KiB, so 4-5 workgroups share a CU and their epilogue store
+// phases de-synchronize from the MFMA phases of the others (with 2 per CU they
+// run in lockstep and the stores serialize with the compute).  LDS rows are
+// 64 B; the 16-B chunk index is XOR-swizzled with (row >> 2) & 3 so the 16 rows
+// of a fragment read land on 16 distinct bank slots.
+constexpr int BK32 = 32, kRow32 = BK32 * 2;
+
+__global__ void __launch_bounds__(NT) k_gemm_nt_glds32(GemmArgs g) {
+  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * (BM + BN) * kRow32];
+  const int tiles_n = (g.N + BN - 1) / BN, tiles_m = (g.M + BM - 1) / BM;
+  const int nwg = tiles_n * tiles_m * g.splitk;
+  int wg = xcd_remap(blockIdx.x, nwg);
+  const int split = wg % g.splitk;
+  wg /= g.splitk;
+  const int bm = (wg / tiles_n) * BM, bn = (wg % tiles_n) * BN;
+  const int t = threadIdx.x, lane = t & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
+  auto As = [&](int buf) { return smem + buf * ((BM + BN) * kRow32); };
+  auto Bs = [&](int buf) { return smem + buf * ((BM + BN) * kRow32) + BM * kRow32; };
+  floatx4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+  // a 1 KiB DMA piece = 16 rows x 64 B; 8 pieces per operand, 2 + 2 per wave
+  const int lrow = lane >> 2, pchunk = lane & 3;
+  auto issue = [&](int k0, int buf) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int q = wave * 2 + i;
+      const int r = q * 16 + lrow;
+      const int c = pchunk ^ ((r >> 2) & 3);
+      const int ga = min(bm + r, g.M - 1), gb = min(bn + pair_perm(r), g.N - 1);
+      __builtin_amdgcn_global_load_lds((const void*)(g.A + (size_t)ga * g.lda + k0 + c * 8),
+                                       (__attribute__((address_space(3))) void*)(As(buf) + q * 1024), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(g.B + (size_t)gb * g.ldb + k0 + c * 8),
+                                       (__attribute__((address_space(3))) void*)(Bs(buf) + q * 1024), 16, 0, 0);
+    }
+  };
+  const int nk_all = g.K / BK32;
+  const int per = (nk_all + g.splitk - 1) / g.splitk;
+  const int kt0 = split * per;
+  const int nk = max(0, min(nk_all, kt0 + per) - kt0);
+  if (nk > 0) issue(kt0 * BK32, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    bf16x8 af[4], bf[4];
+    const int chunk = lane >> 4;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int ra_ = wm + i * 16 + (lane & 15);
+      af[i] = *reinterpret_cast<const bf16x8*>(As(cur) + ra_ * kRow32 + ((chunk ^ ((ra_ >> 2) & 3)) << 4));
+      const int rb_ = wn + i * 16 + (lane & 15);
+      bf[i] = *reinterpret_cast<const bf16x8*>(Bs(cur) + rb_ * kRow32 + ((chunk ^ ((rb_ >> 2) & 3)) << 4));
+    }
+    if (kt + 1 < nk) issue((kt0 + kt + 1) * BK32, cur ^ 1);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j], af[i], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  store_direct(g, acc, bm + wm, bn + wn, split, lane);
+}
 
 // Persistent form of k_gemm_nt_glds<DIRECT = true> (LDS-free epilogue): each
 // workgroup walks tiles blockIdx.x, +gridDim.x, ... (XCD-remapped), and issues
@@ -582,7 +700,7 @@ constexpr int SK_BM = 64, SK_NT = 256;
 int g_sk_bn = std::getenv("CCMPI_SK_BN") ? std::atoi(std::getenv("CCMPI_SK_BN")) : 128;      // tuning knobs
 int g_sk_grid = std::getenv("CCMPI_SK_GRID") ? std::atoi(std::getenv("CCMPI_SK_GRID")) : 2048;
 
-template <int SK_BN>
+template <int SK_BN, int FAST = 0>  // FAST = 1 + out_bf16 (no accumulate / act, aligned C, N % 8 == 0), 0 = generic
 __global__ void __launch_bounds__(SK_NT) k_gemm_smallk(GemmArgs g, int kp) {
   constexpr int WN = SK_BN / 4;  // columns per wave
   constexpr int NP = WN / 32;    // column pairs (32 columns) per wave
@@ -664,6 +782,32 @@ __global__ void __launch_bounds__(SK_NT) k_gemm_smallk(GemmArgs g, int kp) {
         for (int j = 0; j < NJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
     }
     // epilogue: lane holds C[m0 + 16i + c][bn + WN*wave + 32p + 8*gq + e], e = 4*half + r
+    if constexpr (FAST > 0) {  // straight-line: one 16-B (bf16) / 2 x 16-B (fp32) store per row and pair
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = m0 + i * 16 + c;
+#pragma unroll
+        for (int pr = 0; pr < NP; ++pr) {
+          const int col = bn + wave * WN + pr * 32 + 8 * gq;
+          float v[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = g.alpha * acc[i][2 * pr + (e >> 2)][e & 3] + bias[pr][e];
+          if (row < g.M && col < g.N) {
+            if constexpr (FAST == 2) {
+              uint32_t w[4];
+#pragma unroll
+              for (int q = 0; q < 4; ++q) w[q] = f32_to_bf16_bits(v[2 * q]) | (f32_to_bf16_bits(v[2 * q + 1]) << 16);
+              *reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(g.C) + (size_t)row * g.ldc + col) =
+                  uint4{w[0], w[1], w[2], w[3]};
+            } else {
+              float4* C = reinterpret_cast<float4*>(reinterpret_cast<float*>(g.C) + (size_t)row * g.ldc + col);
+              C[0] = make_float4(v[0], v[1], v[2], v[3]);
+              C[1] = make_float4(v[4], v[5], v[6], v[7]);
+            }
+          }
+        }
+      }
+    } else
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int row = m0 + i * 16 + c;
@@ -759,17 +903,27 @@ void gemm_nt(uint64_t A, uint64_t B, uint64_t C, uint64_t bias, int M, int N, in
     const int tiles_n = (N + skbn - 1) / skbn, tiles_m = (M + SK_BM - 1) / SK_BM;
     const int mblocks = std::max(1, std::min(tiles_m, std::max(1, g_sk_grid / tiles_n)));
     const size_t lds = (size_t)(skbn + 2 * SK_BM) * (kp * 2 + 16);
-    static bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(k_gemm_smallk<256>),
+    static bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(k_gemm_smallk<256, 0>),
                                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess &&
-                       hipFuncSetAttribute(reinterpret_cast<const void*>(k_gemm_smallk<128>),
+                       hipFuncSetAttribute(reinterpret_cast<const void*>(k_gemm_smallk<128, 0>),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess &&
+                       hipFuncSetAttribute(reinterpret_cast<const void*>(k_gemm_smallk<128, 1>),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess &&
+                       hipFuncSetAttribute(reinterpret_cast<const void*>(k_gemm_smallk<128, 2>),
                                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
     (void)attr;
+    const bool fast = !accumulate && act == 0 && N % 8 == 0 && ldc % 8 == 0 && (C % 16) == 0;
+    const int id = fast ? 1 + (out_bf16 ? 1 : 0) : 0;
+    auto st = reinterpret_cast<hipStream_t>(stream);
+    const dim3 grid(tiles_n * mblocks);
     if (skbn == 256)
-      hipLaunchKernelGGL(k_gemm_smallk<256>, dim3(tiles_n * mblocks), dim3(SK_NT), lds,
-                         reinterpret_cast<hipStream_t>(stream), g, kp);
+      hipLaunchKernelGGL((k_gemm_smallk<256, 0>), grid, dim3(SK_NT), lds, st, g, kp);
+    else if (id == 1)
+      hipLaunchKernelGGL((k_gemm_smallk<128, 1>), grid, dim3(SK_NT), lds, st, g, kp);
+    else if (id == 2)
+      hipLaunchKernelGGL((k_gemm_smallk<128, 2>), grid, dim3(SK_NT), lds, st, g, kp);
     else
-      hipLaunchKernelGGL(k_gemm_smallk<128>, dim3(tiles_n * mblocks), dim3(SK_NT), lds,
-                         reinterpret_cast<hipStream_t>(stream), g, kp);
+      hipLaunchKernelGGL((k_gemm_smallk<128, 0>), grid, dim3(SK_NT), lds, st, g, kp);
     CCMPI_HIP_CHECK(hipGetLastError());
     return;
   }
@@ -791,14 +945,28 @@ void gemm_nt(uint64_t A, uint64_t B, uint64_t C, uint64_t bias, int M, int N, in
     }
   }
   if (K % BK == 0 && g_use_glds) {
-    if (g_direct_epi && splitk == 1 && g_persist) {
+    if (g_direct_epi && g_bk32) {
+      hipLaunchKernelGGL(k_gemm_nt_glds32, dim3(nwg), dim3(NT), 0, reinterpret_cast<hipStream_t>(stream), g);
+    } else if (g_direct_epi && splitk == 1 && g_persist) {
       int grid = std::min(nwg, g_persist_grid);
       if (M % BM == 0 && N % BN == 0)
         hipLaunchKernelGGL(k_gemm_nt_persist<true>, dim3(grid), dim3(NT), 0, reinterpret_cast<hipStream_t>(stream), g);
       else
         hipLaunchKernelGGL(k_gemm_nt_persist<false>, dim3(grid), dim3(NT), 0, reinterpret_cast<hipStream_t>(stream), g);
-    } else if (g_direct_epi)
-      hipLaunchKernelGGL(k_gemm_nt_glds<true>, dim3(nwg), dim3(NT), 0, reinterpret_cast<hipStream_t>(stream), g);
+    } else if (g_direct_epi) {
+      const bool fast = splitk == 1 && !accumulate && act == 0 && N % 8 == 0 && ldc % 8 == 0 && (C % 16) == 0;
+      const int id = fast ? 1 + (out_bf16 ? 1 : 0) + 2 * bias_kind : 0;
+      auto st = reinterpret_cast<hipStream_t>(stream);
+      switch (id) {
+        case 1: hipLaunchKernelGGL((k_gemm_nt_glds<true, 1>), dim3(nwg), dim3(NT), 0, st, g); break;
+        case 2: hipLaunchKernelGGL((k_gemm_nt_glds<true, 2>), dim3(nwg), dim3(NT), 0, st, g); break;
+        case 3: hipLaunchKernelGGL((k_gemm_nt_glds<true, 3>), dim3(nwg), dim3(NT), 0, st, g); break;
+        case 4: hipLaunchKernelGGL((k_gemm_nt_glds<true, 4>), dim3(nwg), dim3(NT), 0, st, g); break;
+        case 5: hipLaunchKernelGGL((k_gemm_nt_glds<true, 5>), dim3(nwg), dim3(NT), 0, st, g); break;
+        case 6: hipLaunchKernelGGL((k_gemm_nt_glds<true, 6>), dim3(nwg), dim3(NT), 0, st, g); break;
+        default: hipLaunchKernelGGL((k_gemm_nt_glds<true, 0>), dim3(nwg), dim3(NT), 0, st, g); break;
+      }
+    }
     else
       hipLaunchKernelGGL(k_gemm_nt_glds<false>, dim3(nwg), dim3(NT), 0, reinterpret_cast<hipStream_t>(stream), g);
   }
@@ -844,6 +1012,7 @@ void register_gemm_ops(pybind11::module_& m) {
   m.def("gemm_tn", &gemm_tn, "C[N1,N2] (+)= alpha*A[M,N1]^T.B[M,N2] (fp32 out, split-K atomics)",
         pybind11::call_guard<pybind11::gil_scoped_release>());
   m.def("gemm_set_glds", [](bool on) { g_use_glds = on; }, "select LDS-DMA (True) or register staging");
+  m.def("gemm_set_bk32", [](bool on) { g_bk32 = on; }, "128x128 kernel: BK = 32 (32 KiB LDS) or BK = 64");
   m.def("gemm_set_persistent", [](bool on, int grid) { g_persist = on; g_persist_grid = grid > 0 ? grid : 512; },
         "persistent 128x128 kernel (next-tile prefetch ahead of the epilogue stores) and its grid");
   m.def("gemm_set_direct_epilogue", [](bool on) { g_direct_epi = on; },

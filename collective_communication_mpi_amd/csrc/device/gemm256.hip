@@ -97,7 +97,7 @@ __device__ __forceinline__ void wait_steady(int b_pieces) {
 //   1 = lax vmcnt (wait for nothing: WRONG results, isolates DMA-latency stalls)
 //   2 = no s_setprio around the MFMA cluster
 //   4 = no ping-pong stagger (both groups in lockstep)
-template <int BN, int EXP = 0>
+template <int BN, int EXP = 0, int FAST = 0>  // FAST: fast_epilogue_id (gemm_common.hpp), 0 = generic
 __global__ void __launch_bounds__(PNT, 1) k_gemm_nt_pp(GemmArgs g) {
   using G = Geo<BN>;
   extern __shared__ __attribute__((aligned(1024))) unsigned char smem[];
@@ -287,10 +287,11 @@ __global__ void __launch_bounds__(PNT, 1) k_gemm_nt_pp(GemmArgs g) {
 #pragma unroll
           for (int r = 0; r < 4; ++r)
             tile[(wr * (128 / G::WR) + i * 16 + (lane >> 4) * 4 + r) * G::EpiTS + cl] =
-                epi(g, acc[mh][nh][i][j][r], b);
+                (FAST > 0 ? g.alpha * acc[mh][nh][i][j][r] + b : epi(g, acc[mh][nh][i][j][r], b));
       }
     __syncthreads();
-    store_rows<128, BN, PNT>(g, tile, G::EpiTS, bm + mh * 128, bn, t);
+    if constexpr (FAST > 0) store_rows_fast<128, BN, PNT, ((FAST - 1) & 1) != 0>(g, tile, G::EpiTS, bm + mh * 128, bn, t);
+    else store_rows<128, BN, PNT>(g, tile, G::EpiTS, bm + mh * 128, bn, t);
     __syncthreads();
   }
 }
@@ -299,28 +300,39 @@ __global__ void __launch_bounds__(PNT, 1) k_gemm_nt_pp(GemmArgs g) {
 
 int gemm256_tiles(int M, int N, int bn) { return ((M + PM - 1) / PM) * ((N + bn - 1) / bn); }
 
-template <int BN, int EXP>
+template <int BN, int EXP, int FAST = 0>
 static void launch_pp(const GemmArgs& g, hipStream_t stream) {
   static bool attr = [] {
-    return hipFuncSetAttribute(reinterpret_cast<const void*>(k_gemm_nt_pp<BN, EXP>),
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(k_gemm_nt_pp<BN, EXP, FAST>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, Geo<BN>::Lds) == hipSuccess;
   }();
   (void)attr;
   const int nwg = gemm256_tiles(g.M, g.N, BN) * g.splitk;
-  hipLaunchKernelGGL((k_gemm_nt_pp<BN, EXP>), dim3(nwg), dim3(PNT), Geo<BN>::Lds, stream, g);
+  hipLaunchKernelGGL((k_gemm_nt_pp<BN, EXP, FAST>), dim3(nwg), dim3(PNT), Geo<BN>::Lds, stream, g);
+}
+
+// production launches: the common epilogues get branch-free instantiations
+template <int BN>
+static void launch_pp_prod(const GemmArgs& g, hipStream_t stream) {
+  switch (fast_epilogue_id(g)) {
+    case 1: return launch_pp<BN, 0, 1>(g, stream);  // fp32 out, no bias
+    case 2: return launch_pp<BN, 0, 2>(g, stream);  // bf16 out, no bias
+    case 4: return launch_pp<BN, 0, 4>(g, stream);  // bf16 out, fp32 bias
+    default: return launch_pp<BN, 0, 0>(g, stream);
+  }
 }
 
 int g_pp_exp = 0;  // ablation variant (benchmarks only)
 
 void launch_gemm_nt_256(const GemmArgs& g, int bn, hipStream_t stream) {
-  if (bn == 128) return launch_pp<128, 0>(g, stream);
-  if (bn == 192) return launch_pp<192, 0>(g, stream);
+  if (bn == 128) return launch_pp_prod<128>(g, stream);
+  if (bn == 192) return launch_pp_prod<192>(g, stream);
   switch (g_pp_exp) {
     case 1: return launch_pp<256, 1>(g, stream);
     case 2: return launch_pp<256, 2>(g, stream);
     case 4: return launch_pp<256, 4>(g, stream);
     case 6: return launch_pp<256, 6>(g, stream);
-    default: return launch_pp<256, 0>(g, stream);
+    default: return launch_pp_prod<256>(g, stream);
   }
 }
 

@@ -125,6 +125,38 @@ __device__ __forceinline__ void store_rows(const GemmArgs& g, const float* tile,
   }
 }
 
+// Branch-free form of store_rows for the common case (no split-K, no
+// accumulate, 16-B aligned C, N % 8 == 0): whole 16-B row vectors only.
+template <int ROWS, int COLS, int NT, bool OUT_BF16>
+__device__ __forceinline__ void store_rows_fast(const GemmArgs& g, const float* tile, int TS, int row0, int col0, int t) {
+  constexpr int per_vec = OUT_BF16 ? 8 : 4;
+  constexpr int vecs_row = COLS / per_vec;
+  for (int idx = t; idx < ROWS * vecs_row; idx += NT) {
+    const int rl = idx / vecs_row, cl = (idx % vecs_row) * per_vec;
+    const int row = row0 + rl, col = col0 + cl;
+    if (row >= g.M || col >= g.N) continue;
+    const float* src = tile + rl * TS + cl;
+    if constexpr (OUT_BF16) {
+      uint32_t w[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) w[q] = f32_to_bf16_bits(src[2 * q]) | (f32_to_bf16_bits(src[2 * q + 1]) << 16);
+      *reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(g.C) + (size_t)row * g.ldc + col) = uint4{w[0], w[1], w[2], w[3]};
+    } else {
+      *reinterpret_cast<float4*>(reinterpret_cast<float*>(g.C) + (size_t)row * g.ldc + col) =
+          make_float4(src[0], src[1], src[2], src[3]);
+    }
+  }
+}
+
+// Fast-epilogue id shared by the kernels: 1 + out_bf16 + 2 * bias_kind when the
+// epilogue needs no split-K, accumulate, activation or unaligned stores; 0 otherwise.
+inline int fast_epilogue_id(const GemmArgs& g) {
+  const int es = g.out_bf16 ? 2 : 4;
+  const bool ok = g.splitk == 1 && !g.accumulate && g.act == 0 && g.N % 8 == 0 &&
+                  (((uint64_t)g.C | ((uint64_t)g.ldc * es)) % 16) == 0;
+  return ok ? 1 + (g.out_bf16 ? 1 : 0) + 2 * g.bias_kind : 0;
+}
+
 // XCD-aware bijective workgroup remap: blocks b, b+8, b+16, ... (dispatched
 // round-robin to the same XCD) get consecutive logical ids.
 __device__ __forceinline__ int xcd_remap(int wg, int nwg) {
