@@ -37,7 +37,7 @@ bool g_use_glds = std::getenv("CCMPI_GEMM_NO_GLDS") == nullptr;  // A/B switch (
 bool g_direct_epi = std::getenv("CCMPI_GEMM_STAGED_EPI") == nullptr;  // LDS-free epilogue (A/B switch)
 bool g_persist = std::getenv("CCMPI_GEMM_PERSIST") != nullptr;       // persistent 128x128 kernel (A/B switch; measured no gain)
 int g_persist_grid = 512;                                            // 2 workgroups per CU
-bool g_bk32 = std::getenv("CCMPI_GEMM_BK64") == nullptr;             // BK = 32 / 32 KiB LDS variant (A/B switch)
+bool g_bk32 = std::getenv("CCMPI_GEMM_BK32") != nullptr;             // BK = 32 / 32 KiB LDS variant (A/B switch; measured slower)
 // kernel choice for gemm_nt: 0 auto, 1 = 128x128 only, 2 = 256x256 / 3 = 256x128 / 4 = 256x192 whenever legal
 int g_kernel = std::getenv("CCMPI_GEMM_KERNEL") ? std::atoi(std::getenv("CCMPI_GEMM_KERNEL")) : 0;
 constexpr int kRowBytes = BK * 2;  // 128 B per LDS row
@@ -60,6 +60,44 @@ __device__ __forceinline__ void store_tile(const GemmArgs& g, floatx4 (&acc)[4][
   }
   __syncthreads();
   store_rows<BM, BN, NT>(g, tile, TS, bm, bn, t);
+}
+
+// Branch-free staged epilogue of the weight-gradient GEMM (fp32 C, alpha only):
+// ATOMIC = split-K partial sums as lane-consecutive fp32 atomics, otherwise
+// plain (or accumulating) 16-B row stores.
+template <bool ATOMIC, bool ACCUM>
+__device__ __forceinline__ void store_tile_f32(const GemmArgs& g, floatx4 (&acc)[4][4], unsigned char* smem, int bm,
+                                              int bn, int wm, int wn, int t, int lane) {
+  float* tile = reinterpret_cast<float*>(smem);
+  constexpr int TS = BN + 4;
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        tile[(wm + i * 16 + (lane >> 4) * 4 + r) * TS + wn + j * 16 + (lane & 15)] = g.alpha * acc[i][j][r];
+  __syncthreads();
+  if constexpr (ATOMIC) {
+    for (int idx = t; idx < BM * BN; idx += NT) {
+      const int rl = idx / BN, cl = idx % BN;
+      const int row = bm + rl, col = bn + cl;
+      if (row < g.M && col < g.N) atomicAdd(reinterpret_cast<float*>(g.C) + (size_t)row * g.ldc + col, tile[rl * TS + cl]);
+    }
+  } else {
+    for (int idx = t; idx < BM * (BN / 4); idx += NT) {
+      const int rl = idx / (BN / 4), cl = (idx % (BN / 4)) * 4;
+      const int row = bm + rl, col = bn + cl;
+      if (row >= g.M || col >= g.N) continue;
+      float4* C = reinterpret_cast<float4*>(reinterpret_cast<float*>(g.C) + (size_t)row * g.ldc + col);
+      float4 v = make_float4(tile[rl * TS + cl], tile[rl * TS + cl + 1], tile[rl * TS + cl + 2], tile[rl * TS + cl + 3]);
+      if constexpr (ACCUM) {
+        const float4 o = *C;
+        v.x += o.x; v.y += o.y; v.z += o.z; v.w += o.w;
+      }
+      *C = v;
+    }
+  }
 }
 
 // Direct (LDS-free) epilogue for kernels that swap the MFMA operands and stage
@@ -595,6 +633,9 @@ constexpr int kTnTile = BK * kTnRow;    // one operand tile
 
 __device__ __forceinline__ int tn_off(int row, int byte) { return row * kTnRow + (byte ^ (((row >> 3) & 1) << 7)); }
 
+// FAST: 0 generic store_tile, 1 split-K atomics, 2 plain stores, 3 accumulating stores
+// (fp32 C, 16-B aligned, N2 % 4 == 0).
+template <int FAST>
 __global__ void __launch_bounds__(NT) k_gemm_tn(GemmArgs g) {
   __shared__ __attribute__((aligned(16))) unsigned char smem[4 * kTnTile];
   // here: g.M = N1 (rows of C), g.N = N2 (cols of C), g.K = M (reduction)
@@ -678,7 +719,10 @@ __global__ void __launch_bounds__(NT) k_gemm_tn(GemmArgs g) {
     __syncthreads();
   }
   __syncthreads();
-  store_tile(g, acc, smem, bm, bn, wm, wn, split, t, lane);
+  if constexpr (FAST == 1) store_tile_f32<true, false>(g, acc, smem, bm, bn, wm, wn, t, lane);
+  else if constexpr (FAST == 2) store_tile_f32<false, false>(g, acc, smem, bm, bn, wm, wn, t, lane);
+  else if constexpr (FAST == 3) store_tile_f32<false, true>(g, acc, smem, bm, bn, wm, wn, t, lane);
+  else store_tile(g, acc, smem, bm, bn, wm, wn, split, t, lane);
 }
 
 
@@ -935,9 +979,10 @@ void gemm_nt(uint64_t A, uint64_t B, uint64_t C, uint64_t bias, int M, int N, in
     if (g_kernel == 2) bn = 256;
     else if (g_kernel == 3) bn = 128;
     else if (g_kernel == 4) bn = 192;
-    // measured (benchmarks/gemm_bench.py): 256x256 wins from ~4096^2 outputs up;
-    // narrow N (<= 1024) stays on 128x128 (2 blocks/CU balance better)
-    else if (gemm256_tiles(M, N, 256) * splitk >= 256 && M >= 1024 && N >= 1024) bn = 256;
+    // measured (benchmarks/gemm_bench.py, profiles/r1_gemm_fastepi): with the branch-free
+    // epilogues the 128x128 kernel matches 256x256 up to ~256 tiles and for short K;
+    // 256x256 wins with >= 2 tiles per CU and K >= 1024
+    else if (gemm256_tiles(M, N, 256) * splitk >= 512 && K >= 1024 && M >= 1024 && N >= 1024) bn = 256;
     if (bn) {
       launch_gemm_nt_256(g, bn, reinterpret_cast<hipStream_t>(stream));
       CCMPI_HIP_CHECK(hipGetLastError());
@@ -988,7 +1033,15 @@ void gemm_tn(uint64_t A, uint64_t B, uint64_t C, int M, int N1, int N2, int lda,
   GemmArgs g{reinterpret_cast<const uint16_t*>(A), reinterpret_cast<const uint16_t*>(B), reinterpret_cast<void*>(C),
              nullptr, N1, N2, M, lda, ldb, ldc, alpha, accumulate ? 1 : 0, 0, 0, 0, splitk};
   const int nwg = ((N1 + BM - 1) / BM) * ((N2 + BN - 1) / BN) * splitk;
-  hipLaunchKernelGGL(k_gemm_tn, dim3(nwg), dim3(NT), 0, reinterpret_cast<hipStream_t>(stream), g);
+  const bool aligned = (C % 16) == 0 && ldc % 4 == 0 && N2 % 4 == 0;
+  const int fast = !aligned ? 0 : splitk > 1 ? 1 : accumulate ? 3 : 2;
+  auto st = reinterpret_cast<hipStream_t>(stream);
+  switch (fast) {
+    case 1: hipLaunchKernelGGL(k_gemm_tn<1>, dim3(nwg), dim3(NT), 0, st, g); break;
+    case 2: hipLaunchKernelGGL(k_gemm_tn<2>, dim3(nwg), dim3(NT), 0, st, g); break;
+    case 3: hipLaunchKernelGGL(k_gemm_tn<3>, dim3(nwg), dim3(NT), 0, st, g); break;
+    default: hipLaunchKernelGGL(k_gemm_tn<0>, dim3(nwg), dim3(NT), 0, st, g); break;
+  }
   CCMPI_HIP_CHECK(hipGetLastError());
 }
 
