@@ -10,6 +10,10 @@
 // few thousand FMAs per head: the kernel is load/latency bound, so it uses
 // fp32 VALU dot products from LDS rather than MFMA tiles (which need >= 16x16x32).
 #include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <tuple>
+#include <vector>
 
 #include "attn_common.hpp"
 #include "common.hpp"
@@ -255,12 +259,33 @@ void attn_bwd(uint64_t qkv, uint64_t o, uint64_t lse, uint64_t dout, uint64_t dq
 
 // ---------------------------------------------------------------------------
 // Fused AdamW on a flat fp32 parameter buffer + bf16 compute copy (one pass).
-// g is the (DP-summed) gradient; grad_scale folds the 1/dp average in.
+// g is the (DP-summed) gradient; grad_scale folds the 1/dp average in.  Up to
+// kMaxT regions of the flat buffer (row-major [rows][cols] weights) also get a
+// TRANSPOSED bf16 copy ([cols][rows]), so backward GEMMs that need W^T read it
+// directly instead of launching a transpose every step.
 // ---------------------------------------------------------------------------
+constexpr int kMaxT = 4;
+struct TRegions {
+  uint64_t off[kMaxT], rows[kMaxT], cols[kMaxT];
+  uint16_t* dst[kMaxT];
+  int n;
+};
+
+__device__ __forceinline__ void write_transposed(const TRegions& tr, uint64_t i, uint16_t v) {
+  for (int k = 0; k < tr.n; ++k) {
+    const uint64_t rel = i - tr.off[k];
+    if (i >= tr.off[k] && rel < tr.rows[k] * tr.cols[k]) {
+      const uint64_t r = rel / tr.cols[k], c = rel % tr.cols[k];
+      tr.dst[k][c * tr.rows[k] + r] = v;
+    }
+  }
+}
+
 __global__ void __launch_bounds__(256) k_adamw(float* __restrict__ p, const float* __restrict__ g,
                                                float* __restrict__ m, float* __restrict__ v,
                                                uint16_t* __restrict__ p16, uint64_t n, float lr, float b1, float b2,
-                                               float eps, float wd, float bc1, float bc2, float grad_scale) {
+                                               float eps, float wd, float bc1, float bc2, float grad_scale,
+                                               TRegions tr) {
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
     const float gi = g[i] * grad_scale;
     const float mi = b1 * m[i] + (1.f - b1) * gi;
@@ -270,7 +295,9 @@ __global__ void __launch_bounds__(256) k_adamw(float* __restrict__ p, const floa
     float pi = p[i] * (1.f - lr * wd);
     pi -= lr * (mi / bc1) / (sqrtf(vi / bc2) + eps);
     p[i] = pi;
-    if (p16) p16[i] = (uint16_t)f32_to_bf16_bits(pi);
+    const uint16_t h = (uint16_t)f32_to_bf16_bits(pi);
+    if (p16) p16[i] = h;
+    if (tr.n) write_transposed(tr, i, h);
   }
 }
 
@@ -317,23 +344,43 @@ void patchify(uint64_t x, uint64_t xp, int B, int img, int p, int kp, uint64_t s
   CCMPI_HIP_CHECK(hipGetLastError());
 }
 
-__global__ void __launch_bounds__(256) k_cast_bf16(const float* __restrict__ x, uint16_t* __restrict__ y, uint64_t n) {
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
-    y[i] = (uint16_t)f32_to_bf16_bits(x[i]);
+__global__ void __launch_bounds__(256) k_cast_bf16(const float* __restrict__ x, uint16_t* __restrict__ y, uint64_t n,
+                                                   TRegions tr) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint16_t h = (uint16_t)f32_to_bf16_bits(x[i]);
+    y[i] = h;
+    if (tr.n) write_transposed(tr, i, h);
+  }
+}
+
+TRegions make_tregions(const std::vector<std::tuple<uint64_t, uint64_t, uint64_t, uint64_t>>& regs) {
+  if (regs.size() > (size_t)kMaxT) throw std::invalid_argument("at most 4 transposed regions");
+  TRegions tr{};
+  tr.n = (int)regs.size();
+  for (int k = 0; k < tr.n; ++k) {
+    tr.off[k] = std::get<0>(regs[k]);
+    tr.rows[k] = std::get<1>(regs[k]);
+    tr.cols[k] = std::get<2>(regs[k]);
+    tr.dst[k] = reinterpret_cast<uint16_t*>(std::get<3>(regs[k]));
+  }
+  return tr;
 }
 
 void adamw(uint64_t p, uint64_t g, uint64_t m, uint64_t v, uint64_t p16, uint64_t n, float lr, float b1, float b2,
-           float eps, float wd, int step, float grad_scale, uint64_t stream) {
+           float eps, float wd, int step, float grad_scale, uint64_t stream,
+           const std::vector<std::tuple<uint64_t, uint64_t, uint64_t, uint64_t>>& tregions) {
   const float bc1 = 1.f - powf(b1, (float)step), bc2 = 1.f - powf(b2, (float)step);
   const int grid = (int)std::min<uint64_t>((n + 255) / 256, 2048);
   hipLaunchKernelGGL(k_adamw, dim3(grid), dim3(256), 0, (hipStream_t)stream, (float*)p, (const float*)g, (float*)m,
-                     (float*)v, (uint16_t*)p16, n, lr, b1, b2, eps, wd, bc1, bc2, grad_scale);
+                     (float*)v, (uint16_t*)p16, n, lr, b1, b2, eps, wd, bc1, bc2, grad_scale, make_tregions(tregions));
   CCMPI_HIP_CHECK(hipGetLastError());
 }
 
-void cast_bf16(uint64_t x, uint64_t y, uint64_t n, uint64_t stream) {
+void cast_bf16(uint64_t x, uint64_t y, uint64_t n, uint64_t stream,
+               const std::vector<std::tuple<uint64_t, uint64_t, uint64_t, uint64_t>>& tregions) {
   const int grid = (int)std::min<uint64_t>((n + 255) / 256, 2048);
-  hipLaunchKernelGGL(k_cast_bf16, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const float*)x, (uint16_t*)y, n);
+  hipLaunchKernelGGL(k_cast_bf16, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const float*)x, (uint16_t*)y, n,
+                     make_tregions(tregions));
   CCMPI_HIP_CHECK(hipGetLastError());
 }
 
@@ -345,8 +392,14 @@ void register_attn_ops(pybind11::module_& m) {
   namespace py = pybind11;
   m.def("attn_small_fwd", &attn_fwd, py::call_guard<py::gil_scoped_release>());
   m.def("attn_small_bwd", &attn_bwd, py::call_guard<py::gil_scoped_release>());
-  m.def("adamw_step", &adamw, py::call_guard<py::gil_scoped_release>());
-  m.def("cast_bf16", &cast_bf16, py::call_guard<py::gil_scoped_release>());
+  m.def("adamw_step", &adamw, py::arg("p"), py::arg("g"), py::arg("m"), py::arg("v"), py::arg("p16"), py::arg("n"),
+        py::arg("lr"), py::arg("b1"), py::arg("b2"), py::arg("eps"), py::arg("wd"), py::arg("step"),
+        py::arg("grad_scale"), py::arg("stream"),
+        py::arg("tregions") = std::vector<std::tuple<uint64_t, uint64_t, uint64_t, uint64_t>>{},
+        py::call_guard<py::gil_scoped_release>());
+  m.def("cast_bf16", &cast_bf16, py::arg("x"), py::arg("y"), py::arg("n"), py::arg("stream"),
+        py::arg("tregions") = std::vector<std::tuple<uint64_t, uint64_t, uint64_t, uint64_t>>{},
+        py::call_guard<py::gil_scoped_release>());
   m.def("patchify", &patchify, py::call_guard<py::gil_scoped_release>());
 }
 

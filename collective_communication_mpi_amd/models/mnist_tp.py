@@ -74,7 +74,7 @@ class LayerConfig:
     seed: int = 1234
     dp_algo: str = "auto"
     overlap: bool = True
-    plain_gemm: str = "hipblaslt"  # backward dH = dQKV . W_qkv (no epilogue): "hipblaslt" | "own"
+    plain_gemm: str = "own"  # backward dH = dQKV . W_qkv: "own" (MFMA kernel, W^T kept by AdamW) | "hipblaslt"
 
     @property
     def seq(self) -> int:
@@ -149,7 +149,9 @@ class MnistTPLayer:
             ("emb_w", (d, cfg.kp)),
         ]
         grad_alloc = (lambda n: self.dp_dev.zeros(n, torch.float32)) if self.dp_dev is not None else None
-        self.flat = FlatParams(specs, self.device, grad_alloc)
+        # W_qkv^T and W_o^T (backward dH and dpool GEMMs) are kept as transposed bf16
+        # copies refreshed by the fused AdamW kernel: no transpose launch per step
+        self.flat = FlatParams(specs, self.device, grad_alloc, transposed=("qkv_w", "o_w"))
         self.buckets = GradBuckets(self.flat, self.dp_dev, [["o_w", "o_b"], ["qkv_w", "qkv_b"],
                                                             ["emb_w"]],
                                    algo=cfg.dp_algo, overlap=cfg.overlap)
@@ -307,7 +309,7 @@ class MnistTPLayer:
                 dzp[:, : cfg.n_classes] = dlogits.to(torch.bfloat16)
             gemm_tn(dzp, pool, out=G("o_w"), accumulate=True)    # dW_o = dZ^T . pooled
             dpool = self._buf("dpool", (B, self.hd), torch.bfloat16)
-            gemm_nt(dzp, transpose(P16("o_w")), out=dpool, alpha=1.0 / S)
+            gemm_nt(dzp, self.flat.param16_t("o_w"), out=dpool, alpha=1.0 / S)
             dout, dout_b, dout_r = dpool, dpool.stride(0), 0
         self.buckets.ready(0)
         # ---- attention
@@ -320,9 +322,9 @@ class MnistTPLayer:
         self.buckets.ready(1)
         dh = self._buf("dh", (M, d), torch.bfloat16)            # TP-partial input gradient
         if cfg.plain_gemm == "hipblaslt":
-            torch.matmul(dqkv, P16("qkv_w"), out=dh)            # plain GEMM, weight in its stored layout
+            torch.matmul(dqkv, P16("qkv_w"), out=dh)            # library GEMM, weight in its stored layout
         else:
-            gemm_nt(dqkv, transpose(P16("qkv_w")), out=dh)
+            gemm_nt(dqkv, self.flat.param16_t("qkv_w"), out=dh)  # W_qkv^T kept by the optimizer
         # ---- embedding (replicated across TP): only its weight gradient needs the TP sum
         if self.tp_dev is not None:
             gpart = self._buf("gemb", (d, cfg.kp), torch.float32, self.tp_dev)

@@ -29,7 +29,14 @@ _ALIGN = 64  # elements: keeps every parameter view 256-B aligned
 
 
 class FlatParams:
-    def __init__(self, specs: Sequence[Tuple[str, Tuple[int, ...]]], device, grad_alloc=None):
+    """Flat fp32 master weights + bf16 compute copy + AdamW moments.
+
+    ``transposed`` names 2-D parameters that also keep a TRANSPOSED bf16 copy
+    (``param16_t``), refreshed by the same fused AdamW / cast kernels, so the
+    backward GEMMs that consume W^T need no per-step transpose launch."""
+
+    def __init__(self, specs: Sequence[Tuple[str, Tuple[int, ...]]], device, grad_alloc=None,
+                 transposed: Sequence[str] = ()):
         self.specs = list(specs)
         self.offsets: Dict[str, Tuple[int, int, Tuple[int, ...]]] = {}
         off = 0
@@ -49,6 +56,14 @@ class FlatParams:
         self.m = torch.zeros_like(self.p32)
         self.v = torch.zeros_like(self.p32)
         self.step_count = 0
+        self.p16_t: Dict[str, torch.Tensor] = {}
+        for name in transposed:
+            off, n, shape = self.offsets[name]
+            if len(shape) != 2:
+                raise ValueError(f"transposed copy needs a 2-D parameter, {name} is {shape}")
+            self.p16_t[name] = torch.zeros((shape[1], shape[0]), dtype=torch.bfloat16, device=self.device)
+        self._tregions = [(self.offsets[nm][0], self.offsets[nm][2][0], self.offsets[nm][2][1], t.data_ptr())
+                          for nm, t in self.p16_t.items()]
 
     def view(self, buf: torch.Tensor, name: str) -> torch.Tensor:
         off, n, shape = self.offsets[name]
@@ -68,16 +83,21 @@ class FlatParams:
         hi = max(self.offsets[n][0] + (self.offsets[n][1] + _ALIGN - 1) // _ALIGN * _ALIGN for n in names)
         return lo, hi
 
+    def param16_t(self, name):
+        """[cols, rows] bf16 copy of a 2-D parameter (see ``transposed``)."""
+        return self.p16_t[name]
+
     def refresh_bf16(self) -> None:
         _native.device().cast_bf16(self.p32.data_ptr(), self.p16.data_ptr(), self.numel,
-                                   torch.cuda.current_stream(self.device).cuda_stream)
+                                   torch.cuda.current_stream(self.device).cuda_stream, self._tregions)
 
     def adamw(self, lr: float, betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0,
               grad_scale: float = 1.0) -> None:
         self.step_count += 1
         _native.device().adamw_step(self.p32.data_ptr(), self.g.data_ptr(), self.m.data_ptr(), self.v.data_ptr(),
                                     self.p16.data_ptr(), self.numel, lr, betas[0], betas[1], eps, weight_decay,
-                                    self.step_count, grad_scale, torch.cuda.current_stream(self.device).cuda_stream)
+                                    self.step_count, grad_scale, torch.cuda.current_stream(self.device).cuda_stream,
+                                    self._tregions)
 
 
 class GradBuckets:

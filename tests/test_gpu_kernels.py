@@ -331,3 +331,19 @@ def test_xent_head_fused(ydtype):
     assert torch.all(dz[:, C:] == 0)
     torch.testing.assert_close(db[:C], 1 + logits.grad.sum(0), rtol=1e-4, atol=1e-6)
     torch.testing.assert_close(db[C:], torch.ones(Cp - C, device="cuda"))
+
+
+def test_flat_params_transposed_copies():
+    """Fused AdamW / cast keep W^T bf16 copies in sync with the flat master weights."""
+    from collective_communication_mpi_amd.parallel.dp import FlatParams
+
+    f = FlatParams([("a", (48, 80)), ("b", (7,)), ("c", (33, 16))], "cuda", transposed=("a", "c"))
+    f.p32.copy_(torch.randn(f.numel, device="cuda"))
+    f.refresh_bf16()
+    for nm in ("a", "c"):
+        torch.testing.assert_close(f.param16_t(nm), f.param16(nm).T)
+    f.g.copy_(torch.randn(f.numel, device="cuda"))
+    f.adamw(1e-2, weight_decay=0.1)
+    for nm in ("a", "c"):
+        torch.testing.assert_close(f.param16_t(nm), f.param16(nm).T)
+        torch.testing.assert_close(f.param16(nm).float(), f.param(nm), rtol=1e-2, atol=1e-2)
