@@ -633,8 +633,8 @@ constexpr int kTnTile = BK * kTnRow;    // one operand tile
 
 __device__ __forceinline__ int tn_off(int row, int byte) { return row * kTnRow + (byte ^ (((row >> 3) & 1) << 7)); }
 
-// FAST: 0 generic store_tile, 1 split-K atomics, 2 plain stores, 3 accumulating stores
-// (fp32 C, 16-B aligned, N2 % 4 == 0).
+// FAST: 0 generic store_tile, 1 split-K atomics, 2 plain stores, 3 accumulating stores,
+// 4 split-K partial into a workspace slice (fp32 C, 16-B aligned, N2 % 4 == 0).
 template <int FAST>
 __global__ void __launch_bounds__(NT) k_gemm_tn(GemmArgs g) {
   __shared__ __attribute__((aligned(16))) unsigned char smem[4 * kTnTile];
@@ -720,7 +720,12 @@ __global__ void __launch_bounds__(NT) k_gemm_tn(GemmArgs g) {
   }
   __syncthreads();
   if constexpr (FAST == 1) store_tile_f32<true, false>(g, acc, smem, bm, bn, wm, wn, t, lane);
-  else if constexpr (FAST == 2) store_tile_f32<false, false>(g, acc, smem, bm, bn, wm, wn, t, lane);
+  else if constexpr (FAST == 4) {  // split-K partial -> workspace slice [split][N1][N2] (plain stores)
+    GemmArgs w = g;
+    w.C = reinterpret_cast<float*>(g.C) + (size_t)split * g.M * g.N;
+    w.ldc = g.N;
+    store_tile_f32<false, false>(w, acc, smem, bm, bn, wm, wn, t, lane);
+  } else if constexpr (FAST == 2) store_tile_f32<false, false>(g, acc, smem, bm, bn, wm, wn, t, lane);
   else if constexpr (FAST == 3) store_tile_f32<false, true>(g, acc, smem, bm, bn, wm, wn, t, lane);
   else store_tile(g, acc, smem, bm, bn, wm, wn, split, t, lane);
 }
@@ -924,6 +929,29 @@ __global__ void __launch_bounds__(256) k_transpose16(const uint16_t* __restrict_
   }
 }
 
+// Sum of the split-K workspace slices into C ([rows][cols] fp32, row stride ldc),
+// 4 columns per thread: C (+)= sum_s ws[s].
+__global__ void __launch_bounds__(256) k_splitk_reduce(const float* __restrict__ ws, int splitk, float* __restrict__ C,
+                                                       int ldc, int rows, int cols, int accumulate) {
+  const size_t slice = (size_t)rows * cols;
+  const int vc = cols / 4;
+  for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < (size_t)rows * vc; e += (size_t)gridDim.x * blockDim.x) {
+    const int r = (int)(e / vc), c = (int)(e % vc) * 4;
+    const float* src = ws + (size_t)r * cols + c;
+    float4 acc = *reinterpret_cast<const float4*>(src);
+    for (int k = 1; k < splitk; ++k) {
+      const float4 v = *reinterpret_cast<const float4*>(src + k * slice);
+      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+    float4* dst = reinterpret_cast<float4*>(C + (size_t)r * ldc + c);
+    if (accumulate) {
+      const float4 o = *dst;
+      acc.x += o.x; acc.y += o.y; acc.z += o.z; acc.w += o.w;
+    }
+    *dst = acc;
+  }
+}
+
 void gemm_nt(uint64_t A, uint64_t B, uint64_t C, uint64_t bias, int M, int N, int K, int lda, int ldb, int ldc,
              float alpha, bool accumulate, int bias_kind, int act, bool out_bf16, int splitk, uint64_t stream) {
   if (M <= 0 || N <= 0) return;
@@ -1022,21 +1050,35 @@ void gemm_nt(uint64_t A, uint64_t B, uint64_t C, uint64_t bias, int M, int N, in
 
 // C[N1,N2] (+)= alpha * A[M,N1]^T . B[M,N2]; fp32 output.
 void gemm_tn(uint64_t A, uint64_t B, uint64_t C, int M, int N1, int N2, int lda, int ldb, int ldc, float alpha,
-             bool accumulate, int splitk, uint64_t stream) {
+             bool accumulate, int splitk, uint64_t stream, uint64_t workspace) {
   if (N1 <= 0 || N2 <= 0 || M <= 0) return;
   if (N1 % 8 || N2 % 8 || lda % 8 || ldb % 8 || (A % 16) || (B % 16))
     throw std::invalid_argument("ccmpi gemm_tn: N1, N2, lda, ldb must be multiples of 8 and A/B 16-B aligned");
   if (splitk < 1) splitk = 1;
-  if (splitk > 1 && !accumulate)
+  // split-K partials: a workspace of splitk fp32 slices summed by k_splitk_reduce
+  // (coalesced stores + one streaming pass) instead of fp32 atomics on C
+  const bool use_ws = splitk > 1 && workspace != 0 && N2 % 4 == 0 && ldc % 4 == 0 && (C % 16) == 0 &&
+                      (workspace % 16) == 0;
+  if (splitk > 1 && !accumulate && !use_ws)
     CCMPI_HIP_CHECK(hipMemset2DAsync(reinterpret_cast<void*>(C), (size_t)ldc * 4, 0, (size_t)N2 * 4, N1,
                                      reinterpret_cast<hipStream_t>(stream)));
-  GemmArgs g{reinterpret_cast<const uint16_t*>(A), reinterpret_cast<const uint16_t*>(B), reinterpret_cast<void*>(C),
-             nullptr, N1, N2, M, lda, ldb, ldc, alpha, accumulate ? 1 : 0, 0, 0, 0, splitk};
+  GemmArgs g{reinterpret_cast<const uint16_t*>(A), reinterpret_cast<const uint16_t*>(B),
+             reinterpret_cast<void*>(use_ws ? workspace : C), nullptr, N1, N2, M, lda, ldb, use_ws ? N2 : ldc, alpha,
+             accumulate ? 1 : 0, 0, 0, 0, splitk};
   const int nwg = ((N1 + BM - 1) / BM) * ((N2 + BN - 1) / BN) * splitk;
   const bool aligned = (C % 16) == 0 && ldc % 4 == 0 && N2 % 4 == 0;
-  const int fast = !aligned ? 0 : splitk > 1 ? 1 : accumulate ? 3 : 2;
+  const int fast = use_ws ? 4 : !aligned ? 0 : splitk > 1 ? 1 : accumulate ? 3 : 2;
   auto st = reinterpret_cast<hipStream_t>(stream);
   switch (fast) {
+    case 4: {
+      hipLaunchKernelGGL(k_gemm_tn<4>, dim3(nwg), dim3(NT), 0, st, g);
+      CCMPI_HIP_CHECK(hipGetLastError());
+      const size_t work = (size_t)N1 * (N2 / 4);
+      const int grid = (int)std::min<size_t>((work + 255) / 256, 4096);
+      hipLaunchKernelGGL(k_splitk_reduce, dim3(grid), dim3(256), 0, st, reinterpret_cast<const float*>(workspace), splitk,
+                         reinterpret_cast<float*>(C), ldc, N1, N2, accumulate ? 1 : 0);
+      break;
+    }
     case 1: hipLaunchKernelGGL(k_gemm_tn<1>, dim3(nwg), dim3(NT), 0, st, g); break;
     case 2: hipLaunchKernelGGL(k_gemm_tn<2>, dim3(nwg), dim3(NT), 0, st, g); break;
     case 3: hipLaunchKernelGGL(k_gemm_tn<3>, dim3(nwg), dim3(NT), 0, st, g); break;
@@ -1062,7 +1104,10 @@ void register_gemm_ops(pybind11::module_& m) {
         pybind11::arg("alpha"), pybind11::arg("accumulate"), pybind11::arg("bias_kind"), pybind11::arg("act"),
         pybind11::arg("out_bf16"), pybind11::arg("splitk"), pybind11::arg("stream"),
         pybind11::call_guard<pybind11::gil_scoped_release>());
-  m.def("gemm_tn", &gemm_tn, "C[N1,N2] (+)= alpha*A[M,N1]^T.B[M,N2] (fp32 out, split-K atomics)",
+  m.def("gemm_tn", &gemm_tn, "C[N1,N2] (+)= alpha*A[M,N1]^T.B[M,N2] (fp32 out; split-K via workspace or atomics)",
+        pybind11::arg("A"), pybind11::arg("B"), pybind11::arg("C"), pybind11::arg("M"), pybind11::arg("N1"),
+        pybind11::arg("N2"), pybind11::arg("lda"), pybind11::arg("ldb"), pybind11::arg("ldc"), pybind11::arg("alpha"),
+        pybind11::arg("accumulate"), pybind11::arg("splitk"), pybind11::arg("stream"), pybind11::arg("workspace") = 0,
         pybind11::call_guard<pybind11::gil_scoped_release>());
   m.def("gemm_set_glds", [](bool on) { g_use_glds = on; }, "select LDS-DMA (True) or register staging");
   m.def("gemm_set_bk32", [](bool on) { g_bk32 = on; }, "128x128 kernel: BK = 32 (32 KiB LDS) or BK = 64");

@@ -66,11 +66,57 @@ __global__ void __launch_bounds__(64) k_xent_head(const float* __restrict__ z, i
   if (t == 0) atomicAdd(loss, s_loss);
 }
 
+
+// Lane-per-class form (C <= Cpad <= 16): 16 lanes per row, 4 rows per wave,
+// 16 rows per 256-thread workgroup.  max / sum over classes are 4-step
+// shuffles, the dZ row is one contiguous 32-B store, and per-class column sums
+// combine the 4 rows of a wave (xor 16, 32) before LDS and one atomic per
+// class per workgroup.
+__global__ void __launch_bounds__(256) k_xent_head16(const float* __restrict__ z, int ld_z,
+                                                     const float* __restrict__ bias, const void* __restrict__ y, int y64,
+                                                     int B, int C, int Cpad, float scale, float* __restrict__ loss,
+                                                     uint16_t* __restrict__ dz, int ld_dz, float* __restrict__ dbias) {
+  __shared__ float s_db[4][16];
+  __shared__ float s_loss[4];
+  const int t = threadIdx.x, wave = t >> 6, lane = t & 63, c = lane & 15;
+  const int b = blockIdx.x * 16 + wave * 4 + (lane >> 4);
+  const bool live = b < B;
+  const float v = (live && c < C) ? z[(size_t)b * ld_z + c] + (bias ? bias[c] : 0.f) : -INFINITY;
+  float m = v;
+#pragma unroll
+  for (int o = 1; o < 16; o <<= 1) m = fmaxf(m, __shfl_xor(m, o));
+  const float e = (c < C) ? __expf(v - m) : 0.f;
+  float s = e;
+#pragma unroll
+  for (int o = 1; o < 16; o <<= 1) s += __shfl_xor(s, o);
+  const int label = !live ? -1 : y64 ? (int)reinterpret_cast<const int64_t*>(y)[b] : reinterpret_cast<const int32_t*>(y)[b];
+  float l = (live && c == label) ? (m + __logf(s) - v) * scale : 0.f;
+  const float gr = (live && c < C) ? (e / s - (c == label ? 1.f : 0.f)) * scale : 0.f;
+  if (live && c < Cpad) dz[(size_t)b * ld_dz + c] = (uint16_t)f32_to_bf16_bits(gr);
+  float cs = gr;
+  cs += __shfl_xor(cs, 16);
+  cs += __shfl_xor(cs, 32);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) l += __shfl_xor(l, o);
+  if (lane < 16) s_db[wave][lane] = cs;
+  if (lane == 0) s_loss[wave] = l;
+  __syncthreads();
+  if (t < C && dbias) atomicAdd(dbias + t, s_db[0][t] + s_db[1][t] + s_db[2][t] + s_db[3][t]);
+  if (t == 0) atomicAdd(loss, s_loss[0] + s_loss[1] + s_loss[2] + s_loss[3]);
+}
+
 void xent_head(uint64_t z, int ld_z, uint64_t bias, uint64_t y, bool y64, int B, int C, int Cpad, float scale,
                uint64_t loss, uint64_t dz, int ld_dz, uint64_t dbias, uint64_t stream) {
   if (C < 1 || C > kMaxClasses || Cpad < C) throw std::invalid_argument("xent_head: need 1 <= n_classes <= 64 <= pad");
   if (B <= 0) return;
   CCMPI_HIP_CHECK(hipMemsetAsync(reinterpret_cast<void*>(loss), 0, sizeof(float), (hipStream_t)stream));
+  if (Cpad <= 16) {
+    hipLaunchKernelGGL(k_xent_head16, dim3((B + 15) / 16), dim3(256), 0, (hipStream_t)stream, (const float*)z, ld_z,
+                       (const float*)bias, (const void*)y, y64 ? 1 : 0, B, C, Cpad, scale, (float*)loss, (uint16_t*)dz,
+                       ld_dz, (float*)dbias);
+    CCMPI_HIP_CHECK(hipGetLastError());
+    return;
+  }
   // one wave per workgroup: the kernel is latency bound, so spread rows over many CUs
   hipLaunchKernelGGL(k_xent_head, dim3((B + 63) / 64), dim3(64), 0, (hipStream_t)stream, (const float*)z, ld_z,
                      (const float*)bias, (const void*)y, y64 ? 1 : 0, B, C, Cpad, scale, (float*)loss, (uint16_t*)dz, ld_dz,
