@@ -39,7 +39,8 @@ def reference_run(tmp_path_factory):
     return np.load(out)
 
 
-@pytest.mark.parametrize("n,tp,mode", [(2, 2, "row"), (2, 2, "naive"), (2, 1, "row"), (4, 2, "row")])
+@pytest.mark.parametrize("n,tp,mode", [(2, 2, "row"), (2, 2, "naive"), (2, 1, "row"), (4, 2, "row"),
+                                       (8, 2, "row"), (8, 1, "row")])  # 8 ranks sharing one GPU: the DP4 x TP2 grid
 def test_harness_matches_single_rank(reference_run, tmp_path, n, tp, mode):
     out = tmp_path / "run.npz"
     run_ranks(n, py("tests/workers/harness_worker.py", "--tp", str(tp), "--mode", mode, "--out", str(out)),
