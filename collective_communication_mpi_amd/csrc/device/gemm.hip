@@ -1050,11 +1050,30 @@ void gemm_nt(uint64_t A, uint64_t B, uint64_t C, uint64_t bias, int M, int N, in
 
 // C[N1,N2] (+)= alpha * A[M,N1]^T . B[M,N2]; fp32 output.
 void gemm_tn(uint64_t A, uint64_t B, uint64_t C, int M, int N1, int N2, int lda, int ldb, int ldc, float alpha,
-             bool accumulate, int splitk, uint64_t stream, uint64_t workspace) {
+             bool accumulate, int splitk, uint64_t stream, uint64_t workspace, int variant) {
   if (N1 <= 0 || N2 <= 0 || M <= 0) return;
   if (N1 % 8 || N2 % 8 || lda % 8 || ldb % 8 || (A % 16) || (B % 16))
     throw std::invalid_argument("ccmpi gemm_tn: N1, N2, lda, ldb must be multiples of 8 and A/B 16-B aligned");
   if (splitk < 1) splitk = 1;
+  // variant 1: 256x256 8-wave ping-pong TN kernel (gemm256.hip); partials of every
+  // split go to workspace slices, then k_splitk_reduce
+  if (variant == 1 && M % 128 == 0 && N1 >= 256 && N2 >= 256 && (C % 16) == 0 && ldc % 4 == 0 &&
+      (splitk == 1 || (workspace != 0 && (workspace % 16) == 0))) {
+    auto st = reinterpret_cast<hipStream_t>(stream);
+    GemmArgs g{reinterpret_cast<const uint16_t*>(A), reinterpret_cast<const uint16_t*>(B),
+               reinterpret_cast<void*>(splitk > 1 ? workspace : C), nullptr, N1, N2, M, lda, ldb,
+               splitk > 1 ? N2 : ldc, alpha, (splitk == 1 && accumulate) ? 1 : 0, 0, 0, 0, splitk};
+    launch_gemm_tn_256(g, st);
+    CCMPI_HIP_CHECK(hipGetLastError());
+    if (splitk > 1) {
+      const size_t work = (size_t)N1 * (N2 / 4);
+      const int grid = (int)std::min<size_t>((work + 255) / 256, 4096);
+      hipLaunchKernelGGL(k_splitk_reduce, dim3(grid), dim3(256), 0, st, reinterpret_cast<const float*>(workspace), splitk,
+                         reinterpret_cast<float*>(C), ldc, N1, N2, accumulate ? 1 : 0);
+      CCMPI_HIP_CHECK(hipGetLastError());
+    }
+    return;
+  }
   // split-K partials: a workspace of splitk fp32 slices summed by k_splitk_reduce
   // (coalesced stores + one streaming pass) instead of fp32 atomics on C
   const bool use_ws = splitk > 1 && workspace != 0 && N2 % 4 == 0 && ldc % 4 == 0 && (C % 16) == 0 &&
@@ -1108,7 +1127,7 @@ void register_gemm_ops(pybind11::module_& m) {
         pybind11::arg("A"), pybind11::arg("B"), pybind11::arg("C"), pybind11::arg("M"), pybind11::arg("N1"),
         pybind11::arg("N2"), pybind11::arg("lda"), pybind11::arg("ldb"), pybind11::arg("ldc"), pybind11::arg("alpha"),
         pybind11::arg("accumulate"), pybind11::arg("splitk"), pybind11::arg("stream"), pybind11::arg("workspace") = 0,
-        pybind11::call_guard<pybind11::gil_scoped_release>());
+        pybind11::arg("variant") = 0, pybind11::call_guard<pybind11::gil_scoped_release>());
   m.def("gemm_set_glds", [](bool on) { g_use_glds = on; }, "select LDS-DMA (True) or register staging");
   m.def("gemm_set_bk32", [](bool on) { g_bk32 = on; }, "128x128 kernel: BK = 32 (32 KiB LDS) or BK = 64");
   m.def("gemm_set_persistent", [](bool on, int grid) { g_persist = on; g_persist_grid = grid > 0 ? grid : 512; },

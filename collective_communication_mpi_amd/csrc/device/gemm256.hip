@@ -75,6 +75,13 @@ struct Geo {
 
 enum Slot { A0 = 0, A1 = 1, B0 = 2, B1 = 3 };
 
+// TN half-tile image: row r (reduction index) = 256 B = 8 granules of 16 output
+// indices; granule g is stored at g ^ tn_swz(r).
+__device__ __forceinline__ int tn_swz(int r) { return (r & 3) | (((r >> 3) & 1) << 2); }
+__device__ __forceinline__ int tn_off(int r, int col) {
+  return r * 256 + ((((col >> 4) ^ tn_swz(r)) << 5) | ((col & 15) << 1));
+}
+
 __device__ __forceinline__ void bar() {
   __builtin_amdgcn_sched_barrier(0);
   asm volatile("s_barrier" ::: "memory");
@@ -97,7 +104,13 @@ __device__ __forceinline__ void wait_steady(int b_pieces) {
 //   1 = lax vmcnt (wait for nothing: WRONG results, isolates DMA-latency stalls)
 //   2 = no s_setprio around the MFMA cluster
 //   4 = no ping-pong stagger (both groups in lockstep)
-template <int BN, int EXP = 0, int FAST = 0>  // FAST: fast_epilogue_id (gemm_common.hpp), 0 = generic
+// TN: weight-gradient form C[N1][N2] = sum_m A[m][n1] B[m][n2] (g.M = N1, g.N = N2,
+// g.K = M).  Half-tiles are 64 reduction rows x 128 output indices, stored as
+// 256-B rows whose 32-B granules are XOR-swizzled by tn_swz(row); operands come
+// out of ds_read_b64_tr_b16 (conflict-free: 16 lanes read rows r..r+3 and, in the
+// other lane group, r+8..r+11 -> 8 distinct granules).  Split-K partials go to
+// workspace slices (g.C + split * N1 * N2) for k_splitk_reduce.
+template <int BN, int EXP = 0, int FAST = 0, bool TN = false>  // FAST: fast_epilogue_id (gemm_common.hpp)
 __global__ void __launch_bounds__(PNT, 1) k_gemm_nt_pp(GemmArgs g) {
   using G = Geo<BN>;
   extern __shared__ __attribute__((aligned(1024))) unsigned char smem[];
@@ -132,6 +145,26 @@ __global__ void __launch_bounds__(PNT, 1) k_gemm_nt_pp(GemmArgs g) {
   // Lane-linear LDS image; the (row & 7) chunk swizzle is applied to the source.
   const int lrow = lane >> 3, pchunk = lane & 7;
   auto stage = [&](int buf, int slot, int kt) {
+    if constexpr (TN) {
+      // a DMA piece = 4 reduction rows x 256 B; lane -> (row, physical granule, half)
+      const bool isA = slot < 2;
+      const uint16_t* base = isA ? g.A : g.B;
+      const int ld = isA ? g.lda : g.ldb, lim = isA ? g.M : g.N;
+      const int r0 = (isA ? bm : bn) + (slot & 1) * 128;
+      const int k0 = (kt0 + kt) * PK;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int q = i * 8 + wave;
+        const int row = q * 4 + (lane >> 4);
+        const int lg = ((lane & 15) >> 1) ^ tn_swz(row);
+        int oc = r0 + lg * 16 + (lane & 1) * 8;
+        if (oc + 8 > lim) oc = 0;  // outside N1 / N2: any valid address (outputs discarded)
+        __builtin_amdgcn_global_load_lds((const void*)(base + (size_t)(k0 + row) * ld + oc),
+                                         (__attribute__((address_space(3))) void*)(lds(buf, slot) + q * 1024), 16, 0,
+                                         0);
+      }
+      return;
+    }
     const bool isA = slot < 2;
     const uint16_t* base = isA ? g.A : g.B;
     const int ld = isA ? g.lda : g.ldb, lim = (isA ? g.M : g.N) - 1;
@@ -164,8 +197,26 @@ __global__ void __launch_bounds__(PNT, 1) k_gemm_nt_pp(GemmArgs g) {
         for (int j = 0; j < G::NJ; ++j) acc[a][b][i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
 
   bf16x8 fa[G::MI][2], fb0[G::NJ][2], fb1[G::NJ][2];
+  const int tq = (lane >> 2) & 3, tp = lane & 3, tgrp = lane >> 4;  // ds_read_b64_tr_b16 lane roles
+  auto tr8 = [&](const unsigned char* base, int n_loc, int ks) {   // 8 reduction rows of output index n_loc + lane
+    typedef short v4s __attribute__((ext_vector_type(4)));
+    typedef short v8s __attribute__((ext_vector_type(8)));
+    const int r = ks * 32 + tgrp * 8 + tq, col = n_loc + 4 * tp;
+    const v4s a0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (__attribute__((address_space(3))) v4s*)(base + tn_off(r, col)));
+    const v4s a1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (__attribute__((address_space(3))) v4s*)(base + tn_off(r + 4, col)));
+    return __builtin_bit_cast(bf16x8, __builtin_shufflevector(a0, a1, 0, 1, 2, 3, 4, 5, 6, 7));
+  };
   auto read_a = [&](int buf, int h) {
     const unsigned char* base = lds(buf, h);
+    if constexpr (TN) {
+#pragma unroll
+      for (int i = 0; i < G::MI; ++i)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) fa[i][ks] = tr8(base, wr * (128 / G::WR) + i * 16, ks);
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < G::MI; ++i)
 #pragma unroll
@@ -177,6 +228,13 @@ __global__ void __launch_bounds__(PNT, 1) k_gemm_nt_pp(GemmArgs g) {
   };
   auto read_b = [&](int buf, int h, bf16x8 (&fb)[G::NJ][2]) {
     const unsigned char* base = lds(buf, 2 + h);
+    if constexpr (TN) {
+#pragma unroll
+      for (int j = 0; j < G::NJ; ++j)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) fb[j][ks] = tr8(base, wc * G::NS + j * 16, ks);
+      return;
+    }
 #pragma unroll
     for (int j = 0; j < G::NJ; ++j)
 #pragma unroll
@@ -274,6 +332,14 @@ __global__ void __launch_bounds__(PNT, 1) k_gemm_nt_pp(GemmArgs g) {
 
   // epilogue: two passes of 128 rows through LDS
   float* tile = reinterpret_cast<float*>(smem);
+  GemmArgs w = g;
+  if constexpr (TN) {
+    if (g.splitk > 1) {  // this split's partial tile -> its workspace slice
+      w.C = reinterpret_cast<float*>(g.C) + (size_t)split * g.M * g.N;
+      w.ldc = g.N;
+      w.splitk = 1;
+    }
+  }
 #pragma unroll
   for (int mh = 0; mh < 2; ++mh) {
 #pragma unroll
@@ -290,8 +356,8 @@ __global__ void __launch_bounds__(PNT, 1) k_gemm_nt_pp(GemmArgs g) {
                 (FAST > 0 ? g.alpha * acc[mh][nh][i][j][r] + b : epi(g, acc[mh][nh][i][j][r], b));
       }
     __syncthreads();
-    if constexpr (FAST > 0) store_rows_fast<128, BN, PNT, ((FAST - 1) & 1) != 0>(g, tile, G::EpiTS, bm + mh * 128, bn, t);
-    else store_rows<128, BN, PNT>(g, tile, G::EpiTS, bm + mh * 128, bn, t);
+    if constexpr (FAST > 0) store_rows_fast<128, BN, PNT, ((FAST - 1) & 1) != 0>(w, tile, G::EpiTS, bm + mh * 128, bn, t);
+    else store_rows<128, BN, PNT>(w, tile, G::EpiTS, bm + mh * 128, bn, t);
     __syncthreads();
   }
 }
@@ -323,6 +389,23 @@ static void launch_pp_prod(const GemmArgs& g, hipStream_t stream) {
 }
 
 int g_pp_exp = 0;  // ablation variant (benchmarks only)
+
+void launch_gemm_tn_256(const GemmArgs& g, hipStream_t stream) {
+  // partial tiles (split-K) or a plain fp32 tile: branch-free epilogue; accumulate -> generic
+  if (g.splitk > 1 || !g.accumulate) {
+    static bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(k_gemm_nt_pp<256, 0, 1, true>),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, Geo<256>::Lds) == hipSuccess;
+    (void)attr;
+    hipLaunchKernelGGL((k_gemm_nt_pp<256, 0, 1, true>), dim3(gemm256_tiles(g.M, g.N, 256) * g.splitk), dim3(PNT),
+                       Geo<256>::Lds, stream, g);
+  } else {
+    static bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(k_gemm_nt_pp<256, 0, 0, true>),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, Geo<256>::Lds) == hipSuccess;
+    (void)attr;
+    hipLaunchKernelGGL((k_gemm_nt_pp<256, 0, 0, true>), dim3(gemm256_tiles(g.M, g.N, 256) * g.splitk), dim3(PNT),
+                       Geo<256>::Lds, stream, g);
+  }
+}
 
 void launch_gemm_nt_256(const GemmArgs& g, int bn, hipStream_t stream) {
   if (bn == 128) return launch_pp_prod<128>(g, stream);

@@ -167,7 +167,10 @@ __device__ __forceinline__ int xcd_remap(int wg, int nwg) {
 // 256 x bn (bn = 256 or 128) 8-wave ping-pong kernel (gemm256.hip); requires K % 128 == 0.
 void launch_gemm_nt_256(const GemmArgs& g, int bn, hipStream_t stream);
 int gemm256_tiles(int M, int N, int bn);
-extern int g_pp_exp;  // ablation variant of the ping-pong kernel (benchmarks only; 0 = production)
+extern int g_pp_exp;
+// TN (weight-gradient) form of the 256x256 ping-pong kernel; K (reduction rows) % 128 == 0,
+// N1, N2 % 8 == 0.  splitk > 1: g.C is a workspace of splitk fp32 [N1][N2] slices.
+void launch_gemm_tn_256(const GemmArgs& g, hipStream_t stream);  // ablation variant of the ping-pong kernel (benchmarks only; 0 = production)
 
 }  // namespace gemm
 }  // namespace dev

@@ -18,6 +18,14 @@ def _stream(t: torch.Tensor) -> int:
     return torch.cuda.current_stream(t.device).cuda_stream
 
 
+_TN_VARIANT = None  # tests / benchmarks: force the TN kernel (0 = 128x128, 1 = 256x256 ping-pong)
+
+
+def set_tn_variant(v):
+    global _TN_VARIANT
+    _TN_VARIANT = v
+
+
 def _auto_splitk(tiles: int, K: int) -> int:
     """Split K until the grid has ~2 workgroups per CU, keeping >= 4 K-tiles per split."""
     nk = (K + 63) // 64
@@ -81,15 +89,24 @@ def gemm_tn(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None
         out = torch.empty((N1, N2), dtype=torch.float32, device=a.device)
     if out.dtype != torch.float32 or out.shape != (N1, N2) or out.stride(1) != 1:
         raise ValueError("gemm_tn output must be fp32 [N1, N2] with unit column stride")
+    # variant 1 (256x256 ping-pong TN) is opt-in: measured slower than the 128x128 TN kernel on
+    # every shape tried (benchmarks/gemm_tn_splitk.py, profiles/r1_gemm_fastepi/tn_variants.txt)
+    variant = _TN_VARIANT if _TN_VARIANT is not None else 0
+    if variant == 1 and not (M % 128 == 0 and N1 >= 256 and N2 >= 256):
+        variant = 0
     if splitk is None:
-        splitk = _auto_splitk(((N1 + 127) // 128) * ((N2 + 127) // 128), M)
+        if variant == 1:  # 256x256 tiles: split K until ~1 workgroup per CU, >= 2 K-tile pairs per split
+            tiles = ((N1 + 255) // 256) * ((N2 + 255) // 256)
+            splitk = int(max(1, min(256 // max(tiles, 1), M // 256, 64)))
+        else:
+            splitk = _auto_splitk(((N1 + 127) // 128) * ((N2 + 127) // 128), M)
     ws = 0
     # large outputs: partials in a workspace + one reduction pass instead of fp32 atomics
     # (dW_qkv 768x768: 80 -> 68 us); small outputs keep the atomics (one launch fewer)
-    if splitk > 1 and N2 % 4 == 0 and N1 * N2 >= (1 << 18):
+    if splitk > 1 and N2 % 4 == 0 and (variant == 1 or N1 * N2 >= (1 << 18)):
         ws = torch.empty(splitk * N1 * N2, dtype=torch.float32, device=a.device).data_ptr()
     _D().gemm_tn(a.data_ptr(), b.data_ptr(), out.data_ptr(), M, N1, N2, a.stride(0), b.stride(0), out.stride(0),
-                 float(alpha), bool(accumulate), int(splitk), _stream(a), ws)
+                 float(alpha), bool(accumulate), int(splitk), _stream(a), ws, int(variant))
     return out
 
 

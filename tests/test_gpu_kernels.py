@@ -348,3 +348,25 @@ def test_flat_params_transposed_copies():
     for nm in ("a", "c"):
         torch.testing.assert_close(f.param16_t(nm), f.param16(nm).T)
         torch.testing.assert_close(f.param16(nm).float(), f.param(nm), rtol=1e-2, atol=1e-2)
+
+
+@pytest.mark.parametrize("M,N1,N2", [(32768, 768, 768), (4096, 512, 1024), (1024, 296, 520), (256, 256, 256)])
+@pytest.mark.parametrize("splitk", [None, 1, 3])
+def test_gemm_tn_pingpong(M, N1, N2, splitk):
+    """256x256 ping-pong TN kernel (transposed LDS reads, workspace split-K)."""
+    from collective_communication_mpi_amd.ops import gemm_tn
+    from collective_communication_mpi_amd.ops.kernels import set_tn_variant
+
+    g = torch.Generator(device="cuda").manual_seed(M + 3 * N1 + N2)
+    a = torch.randn(M, N1, device="cuda", generator=g).bfloat16()
+    b = torch.randn(M, N2, device="cuda", generator=g).bfloat16()
+    ref = a.float().T @ b.float()
+    set_tn_variant(1)
+    try:
+        out = gemm_tn(a, b, splitk=splitk)
+        torch.testing.assert_close(out, ref, rtol=2e-3, atol=2e-3 * M ** 0.5)
+        acc = torch.ones(N1, N2, device="cuda")
+        gemm_tn(a, b, out=acc, accumulate=True, alpha=0.5, splitk=splitk)
+        torch.testing.assert_close(acc, 1 + 0.5 * ref, rtol=2e-3, atol=2e-3 * M ** 0.5)
+    finally:
+        set_tn_variant(None)
