@@ -281,13 +281,14 @@ __device__ __forceinline__ void write_transposed(const TRegions& tr, uint64_t i,
   }
 }
 
-__global__ void __launch_bounds__(256) k_adamw(float* __restrict__ p, const float* __restrict__ g,
+__global__ void __launch_bounds__(256) k_adamw(float* __restrict__ p, float* __restrict__ g,
                                                float* __restrict__ m, float* __restrict__ v,
                                                uint16_t* __restrict__ p16, uint64_t n, float lr, float b1, float b2,
                                                float eps, float wd, float bc1, float bc2, float grad_scale,
-                                               TRegions tr) {
+                                               TRegions tr, int zero_grad) {
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
     const float gi = g[i] * grad_scale;
+    if (zero_grad) g[i] = 0.f;  // ready for the next backward's accumulation
     const float mi = b1 * m[i] + (1.f - b1) * gi;
     const float vi = b2 * v[i] + (1.f - b2) * gi * gi;
     m[i] = mi;
@@ -368,11 +369,12 @@ TRegions make_tregions(const std::vector<std::tuple<uint64_t, uint64_t, uint64_t
 
 void adamw(uint64_t p, uint64_t g, uint64_t m, uint64_t v, uint64_t p16, uint64_t n, float lr, float b1, float b2,
            float eps, float wd, int step, float grad_scale, uint64_t stream,
-           const std::vector<std::tuple<uint64_t, uint64_t, uint64_t, uint64_t>>& tregions) {
+           const std::vector<std::tuple<uint64_t, uint64_t, uint64_t, uint64_t>>& tregions, bool zero_grad) {
   const float bc1 = 1.f - powf(b1, (float)step), bc2 = 1.f - powf(b2, (float)step);
   const int grid = (int)std::min<uint64_t>((n + 255) / 256, 2048);
-  hipLaunchKernelGGL(k_adamw, dim3(grid), dim3(256), 0, (hipStream_t)stream, (float*)p, (const float*)g, (float*)m,
-                     (float*)v, (uint16_t*)p16, n, lr, b1, b2, eps, wd, bc1, bc2, grad_scale, make_tregions(tregions));
+  hipLaunchKernelGGL(k_adamw, dim3(grid), dim3(256), 0, (hipStream_t)stream, (float*)p, (float*)g, (float*)m,
+                     (float*)v, (uint16_t*)p16, n, lr, b1, b2, eps, wd, bc1, bc2, grad_scale, make_tregions(tregions),
+                     zero_grad ? 1 : 0);
   CCMPI_HIP_CHECK(hipGetLastError());
 }
 
@@ -396,7 +398,7 @@ void register_attn_ops(pybind11::module_& m) {
         py::arg("lr"), py::arg("b1"), py::arg("b2"), py::arg("eps"), py::arg("wd"), py::arg("step"),
         py::arg("grad_scale"), py::arg("stream"),
         py::arg("tregions") = std::vector<std::tuple<uint64_t, uint64_t, uint64_t, uint64_t>>{},
-        py::call_guard<py::gil_scoped_release>());
+        py::arg("zero_grad") = false, py::call_guard<py::gil_scoped_release>());
   m.def("cast_bf16", &cast_bf16, py::arg("x"), py::arg("y"), py::arg("n"), py::arg("stream"),
         py::arg("tregions") = std::vector<std::tuple<uint64_t, uint64_t, uint64_t, uint64_t>>{},
         py::call_guard<py::gil_scoped_release>());

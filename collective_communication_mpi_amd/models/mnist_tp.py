@@ -220,11 +220,14 @@ class MnistTPLayer:
             # fc_o and the mean over patches are linear: pool first (fused in the
             # attention kernel), so fc_o and its TP all-reduce work on B rows, not B*S
             zp = self._buf("zp", (B, cfg.out_pad), torch.float32, self.tp_dev)
-            gemm_nt(pool, P16("o_w"), out=zp, out_dtype=torch.float32, splitk=1)
+            # output bias in the GEMM epilogue, added by TP rank 0 only (the TP all-reduce sums ranks)
+            gemm_nt(pool, P16("o_w"), out=zp, out_dtype=torch.float32, splitk=1,
+                    bias=self.flat.param("o_b") if self.tp_idx == 0 else None)
             if self.tp_dev is not None:
                 self.tp_dev.allreduce(zp, zp, "SUM")  # row-parallel: one TP all-reduce (B x 16 fp32)
-            logits = zp[:, : cfg.n_classes]
-        logits = logits + self.flat.param("o_b")[: cfg.n_classes]
+            logits = zp[:, : cfg.n_classes]  # bias already included
+        if naive:
+            logits = logits + self.flat.param("o_b")[: cfg.n_classes]
         self._saved = (xp, h, qkv, att, lse, B, pool)
         return logits
 
@@ -263,7 +266,7 @@ class MnistTPLayer:
         loss = self._buf("loss", (1,), torch.float32)
         if y.dtype not in (torch.int32, torch.int64) or not y.is_contiguous():
             y = y.to(torch.int32).contiguous()
-        _native.device().xent_head(zp.data_ptr(), zp.stride(0), self.flat.param("o_b").data_ptr(), y.data_ptr(),
+        _native.device().xent_head(zp.data_ptr(), zp.stride(0), 0, y.data_ptr(),  # zp already holds + o_b
                                    y.dtype == torch.int64, B,
                                    cfg.n_classes, cfg.out_pad, 1.0 / global_batch, loss.data_ptr(), dzp.data_ptr(),
                                    dzp.stride(0), self.flat.grad("o_b").data_ptr(),
@@ -282,6 +285,7 @@ class MnistTPLayer:
     def backward(self, dlogits: Optional[torch.Tensor]) -> None:
         """dlogits=None: the fused head (loss_and_grad_fused) already wrote dZ and dL/d o_b."""
         cfg = self.cfg
+        self.flat.grad_dirty = True
         xp, h, qkv, att, lse, B, pool = self._saved
         S, d = cfg.seq, cfg.d_model
         M = B * S
@@ -355,7 +359,12 @@ class MnistTPLayer:
         datt.copy_(dx.reshape(B * S, self.hd))
 
     def zero_grad(self) -> None:
-        self.flat.g.zero_()
+        """The fused AdamW clears the gradient it consumes, so this only zeroes a
+        gradient buffer that has not been through a step (first step, or after a
+        backward without step)."""
+        if self.flat.grad_dirty:
+            self.flat.g.zero_()
+            self.flat.grad_dirty = False
 
     def step(self) -> None:
         self.buckets.wait()

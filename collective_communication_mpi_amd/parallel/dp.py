@@ -56,6 +56,7 @@ class FlatParams:
         self.m = torch.zeros_like(self.p32)
         self.v = torch.zeros_like(self.p32)
         self.step_count = 0
+        self.grad_dirty = False  # g holds values a step has not consumed (AdamW zeroes what it reads)
         self.p16_t: Dict[str, torch.Tensor] = {}
         for name in transposed:
             off, n, shape = self.offsets[name]
@@ -97,7 +98,8 @@ class FlatParams:
         _native.device().adamw_step(self.p32.data_ptr(), self.g.data_ptr(), self.m.data_ptr(), self.v.data_ptr(),
                                     self.p16.data_ptr(), self.numel, lr, betas[0], betas[1], eps, weight_decay,
                                     self.step_count, grad_scale, torch.cuda.current_stream(self.device).cuda_stream,
-                                    self._tregions)
+                                    self._tregions, True)
+        self.grad_dirty = False
 
 
 class GradBuckets:
