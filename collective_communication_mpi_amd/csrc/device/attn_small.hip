@@ -264,41 +264,104 @@ void attn_bwd(uint64_t qkv, uint64_t o, uint64_t lse, uint64_t dout, uint64_t dq
 // TRANSPOSED bf16 copy ([cols][rows]), so backward GEMMs that need W^T read it
 // directly instead of launching a transpose every step.
 // ---------------------------------------------------------------------------
-constexpr int kMaxT = 4;
+constexpr int kMaxT = 4, kTT = 32;  // transposed regions, transpose tile (32x32: enough workgroups to fill the chip)
 struct TRegions {
   uint64_t off[kMaxT], rows[kMaxT], cols[kMaxT];
   uint16_t* dst[kMaxT];
+  int tiles[kMaxT + 1];  // prefix sums of 64x64 tiles per region
   int n;
 };
 
-__device__ __forceinline__ void write_transposed(const TRegions& tr, uint64_t i, uint16_t v) {
-  for (int k = 0; k < tr.n; ++k) {
-    const uint64_t rel = i - tr.off[k];
-    if (i >= tr.off[k] && rel < tr.rows[k] * tr.cols[k]) {
-      const uint64_t r = rel / tr.cols[k], c = rel % tr.cols[k];
-      tr.dst[k][c * tr.rows[k] + r] = v;
-    }
-  }
+__device__ __forceinline__ bool in_regions(const TRegions& tr, uint64_t i) {
+  for (int k = 0; k < tr.n; ++k)
+    if (i >= tr.off[k] && i - tr.off[k] < tr.rows[k] * tr.cols[k]) return true;
+  return false;
 }
 
-__global__ void __launch_bounds__(256) k_adamw(float* __restrict__ p, float* __restrict__ g,
-                                               float* __restrict__ m, float* __restrict__ v,
-                                               uint16_t* __restrict__ p16, uint64_t n, float lr, float b1, float b2,
-                                               float eps, float wd, float bc1, float bc2, float grad_scale,
-                                               TRegions tr, int zero_grad) {
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
-    const float gi = g[i] * grad_scale;
-    if (zero_grad) g[i] = 0.f;  // ready for the next backward's accumulation
-    const float mi = b1 * m[i] + (1.f - b1) * gi;
-    const float vi = b2 * v[i] + (1.f - b2) * gi * gi;
-    m[i] = mi;
-    v[i] = vi;
-    float pi = p[i] * (1.f - lr * wd);
-    pi -= lr * (mi / bc1) / (sqrtf(vi / bc2) + eps);
-    p[i] = pi;
-    const uint16_t h = (uint16_t)f32_to_bf16_bits(pi);
-    if (p16) p16[i] = h;
-    if (tr.n) write_transposed(tr, i, h);
+struct AdamArgs {
+  float* p;
+  float* g;
+  float* m;
+  float* v;
+  uint16_t* p16;
+  uint64_t n;
+  float lr, b1, b2, eps, wd, bc1, bc2, grad_scale;
+  int zero_grad;
+};
+
+// one AdamW element update on already-loaded values; returns the new bf16 bits
+__device__ __forceinline__ float adam_math(const AdamArgs& a, float pi, float gi, float& mi, float& vi) {
+  gi *= a.grad_scale;
+  mi = a.b1 * mi + (1.f - a.b1) * gi;
+  vi = a.b2 * vi + (1.f - a.b2) * gi * gi;
+  pi *= 1.f - a.lr * a.wd;
+  return pi - a.lr * (mi / a.bc1) / (sqrtf(vi / a.bc2) + a.eps);
+}
+
+// Workgroups [0, flat) stride over the flat buffer, skipping the transposed
+// regions; every further workgroup owns one 32x32 tile of a region: it updates
+// the tile row-major (coalesced), stages the bf16 values in LDS and writes the
+// transposed tile with coalesced rows.  All four state arrays are distinct
+// (restrict), and a tile's 16 elements per thread are loaded before any store.
+__global__ void __launch_bounds__(256) k_adamw(AdamArgs a, TRegions tr, int flat) {
+  float* __restrict__ P = a.p;
+  float* __restrict__ Gr = a.g;
+  float* __restrict__ Mo = a.m;
+  float* __restrict__ Vo = a.v;
+  uint16_t* __restrict__ P16 = a.p16;
+  if ((int)blockIdx.x < flat) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += (uint64_t)flat * blockDim.x) {
+      if (tr.n && in_regions(tr, i)) continue;
+      float mi = Mo[i], vi = Vo[i];
+      const float pi = adam_math(a, P[i], Gr[i], mi, vi);
+      if (a.zero_grad) Gr[i] = 0.f;
+      Mo[i] = mi;
+      Vo[i] = vi;
+      P[i] = pi;
+      if (P16) P16[i] = (uint16_t)f32_to_bf16_bits(pi);
+    }
+    return;
+  }
+  __shared__ uint16_t tile[kTT][kTT + 1];
+  const int t = (int)blockIdx.x - flat;
+  int k = 0;
+  while (k + 1 < tr.n && t >= tr.tiles[k + 1]) ++k;
+  const int R = (int)tr.rows[k], Cc = (int)tr.cols[k];
+  const int ntc = (Cc + kTT - 1) / kTT, lt = t - tr.tiles[k];
+  const int r0 = (lt / ntc) * kTT, c0 = (lt % ntc) * kTT;
+  const int tx = threadIdx.x & (kTT - 1), ty = threadIdx.x / kTT;
+  constexpr int RS = 256 / kTT;  // rows per pass
+  constexpr int J = kTT / RS;
+  float pv[J], gv[J], mv[J], vv[J];
+#pragma unroll
+  for (int jj = 0; jj < J; ++jj) {
+    const int r = r0 + ty + RS * jj, c = c0 + tx;
+    const uint64_t i = tr.off[k] + (uint64_t)r * Cc + c;
+    const bool ok = r < R && c < Cc;
+    pv[jj] = ok ? P[i] : 0.f;
+    gv[jj] = ok ? Gr[i] : 0.f;
+    mv[jj] = ok ? Mo[i] : 0.f;
+    vv[jj] = ok ? Vo[i] : 0.f;
+  }
+#pragma unroll
+  for (int jj = 0; jj < J; ++jj) {
+    const int r = r0 + ty + RS * jj, c = c0 + tx;
+    if (r < R && c < Cc) {
+      const uint64_t i = tr.off[k] + (uint64_t)r * Cc + c;
+      const float pi = adam_math(a, pv[jj], gv[jj], mv[jj], vv[jj]);
+      if (a.zero_grad) Gr[i] = 0.f;
+      Mo[i] = mv[jj];
+      Vo[i] = vv[jj];
+      P[i] = pi;
+      const uint16_t h = (uint16_t)f32_to_bf16_bits(pi);
+      if (P16) P16[i] = h;
+      tile[ty + RS * jj][tx] = h;
+    }
+  }
+  __syncthreads();
+  for (int j = ty; j < kTT; j += RS) {  // dst[c][r]: consecutive tx -> consecutive r
+    const int c = c0 + j, r = r0 + tx;
+    if (r < R && c < Cc) tr.dst[k][(uint64_t)c * R + r] = tile[tx][j];
   }
 }
 
@@ -350,7 +413,11 @@ __global__ void __launch_bounds__(256) k_cast_bf16(const float* __restrict__ x, 
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
     const uint16_t h = (uint16_t)f32_to_bf16_bits(x[i]);
     y[i] = h;
-    if (tr.n) write_transposed(tr, i, h);
+    for (int k = 0; k < tr.n; ++k) {  // (initialization path only: scattered writes are fine here)
+      const uint64_t rel = i - tr.off[k];
+      if (i >= tr.off[k] && rel < tr.rows[k] * tr.cols[k])
+        tr.dst[k][(rel % tr.cols[k]) * tr.rows[k] + rel / tr.cols[k]] = h;
+    }
   }
 }
 
@@ -358,11 +425,13 @@ TRegions make_tregions(const std::vector<std::tuple<uint64_t, uint64_t, uint64_t
   if (regs.size() > (size_t)kMaxT) throw std::invalid_argument("at most 4 transposed regions");
   TRegions tr{};
   tr.n = (int)regs.size();
+  tr.tiles[0] = 0;
   for (int k = 0; k < tr.n; ++k) {
     tr.off[k] = std::get<0>(regs[k]);
     tr.rows[k] = std::get<1>(regs[k]);
     tr.cols[k] = std::get<2>(regs[k]);
     tr.dst[k] = reinterpret_cast<uint16_t*>(std::get<3>(regs[k]));
+    tr.tiles[k + 1] = tr.tiles[k] + (int)(((tr.rows[k] + kTT - 1) / kTT) * ((tr.cols[k] + kTT - 1) / kTT));
   }
   return tr;
 }
@@ -371,10 +440,11 @@ void adamw(uint64_t p, uint64_t g, uint64_t m, uint64_t v, uint64_t p16, uint64_
            float eps, float wd, int step, float grad_scale, uint64_t stream,
            const std::vector<std::tuple<uint64_t, uint64_t, uint64_t, uint64_t>>& tregions, bool zero_grad) {
   const float bc1 = 1.f - powf(b1, (float)step), bc2 = 1.f - powf(b2, (float)step);
-  const int grid = (int)std::min<uint64_t>((n + 255) / 256, 2048);
-  hipLaunchKernelGGL(k_adamw, dim3(grid), dim3(256), 0, (hipStream_t)stream, (float*)p, (float*)g, (float*)m,
-                     (float*)v, (uint16_t*)p16, n, lr, b1, b2, eps, wd, bc1, bc2, grad_scale, make_tregions(tregions),
-                     zero_grad ? 1 : 0);
+  const int flat = (int)std::min<uint64_t>((n + 255) / 256, 2048);
+  const TRegions tr = make_tregions(tregions);
+  AdamArgs a{(float*)p, (float*)g, (float*)m, (float*)v, (uint16_t*)p16, n, lr, b1, b2, eps, wd, bc1, bc2, grad_scale,
+             zero_grad ? 1 : 0};
+  hipLaunchKernelGGL(k_adamw, dim3(flat + tr.tiles[tr.n]), dim3(256), 0, (hipStream_t)stream, a, tr, flat);
   CCMPI_HIP_CHECK(hipGetLastError());
 }
 

@@ -75,9 +75,11 @@ __global__ void __launch_bounds__(64) k_xent_head(const float* __restrict__ z, i
 __global__ void __launch_bounds__(256) k_xent_head16(const float* __restrict__ z, int ld_z,
                                                      const float* __restrict__ bias, const void* __restrict__ y, int y64,
                                                      int B, int C, int Cpad, float scale, float* __restrict__ loss,
-                                                     uint16_t* __restrict__ dz, int ld_dz, float* __restrict__ dbias) {
+                                                     uint16_t* __restrict__ dz, int ld_dz, float* __restrict__ dbias,
+                                                     float* __restrict__ partial, unsigned* __restrict__ ticket) {
   __shared__ float s_db[4][16];
   __shared__ float s_loss[4];
+  __shared__ bool s_last;
   const int t = threadIdx.x, wave = t >> 6, lane = t & 63, c = lane & 15;
   const int b = blockIdx.x * 16 + wave * 4 + (lane >> 4);
   const bool live = b < B;
@@ -102,18 +104,38 @@ __global__ void __launch_bounds__(256) k_xent_head16(const float* __restrict__ z
   if (lane == 0) s_loss[wave] = l;
   __syncthreads();
   if (t < C && dbias) atomicAdd(dbias + t, s_db[0][t] + s_db[1][t] + s_db[2][t] + s_db[3][t]);
-  if (t == 0) atomicAdd(loss, s_loss[0] + s_loss[1] + s_loss[2] + s_loss[3]);
+  // loss: per-workgroup partial, the last workgroup to finish sums them in a fixed
+  // order and re-arms the ticket (no memset launch, deterministic sum)
+  if (t == 0) {
+    partial[blockIdx.x] = s_loss[0] + s_loss[1] + s_loss[2] + s_loss[3];
+    __threadfence();
+    s_last = atomicAdd(ticket, 1u) == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (s_last && t < 64) {
+    __threadfence();
+    float acc = 0.f;
+    for (int i = t; i < (int)gridDim.x; i += 64) acc += __hip_atomic_load(partial + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+    if (t == 0) {
+      *loss = acc;
+      *ticket = 0u;
+    }
+  }
 }
 
 void xent_head(uint64_t z, int ld_z, uint64_t bias, uint64_t y, bool y64, int B, int C, int Cpad, float scale,
-               uint64_t loss, uint64_t dz, int ld_dz, uint64_t dbias, uint64_t stream) {
+               uint64_t loss, uint64_t dz, int ld_dz, uint64_t dbias, uint64_t stream, uint64_t workspace) {
   if (C < 1 || C > kMaxClasses || Cpad < C) throw std::invalid_argument("xent_head: need 1 <= n_classes <= 64 <= pad");
   if (B <= 0) return;
-  CCMPI_HIP_CHECK(hipMemsetAsync(reinterpret_cast<void*>(loss), 0, sizeof(float), (hipStream_t)stream));
-  if (Cpad <= 16) {
+  if (!(Cpad <= 16 && workspace))
+    CCMPI_HIP_CHECK(hipMemsetAsync(reinterpret_cast<void*>(loss), 0, sizeof(float), (hipStream_t)stream));
+  if (Cpad <= 16 && workspace) {
+    // workspace: [0, 4) ticket (zero on first use, re-armed by the kernel), then one float per workgroup
     hipLaunchKernelGGL(k_xent_head16, dim3((B + 15) / 16), dim3(256), 0, (hipStream_t)stream, (const float*)z, ld_z,
                        (const float*)bias, (const void*)y, y64 ? 1 : 0, B, C, Cpad, scale, (float*)loss, (uint16_t*)dz,
-                       ld_dz, (float*)dbias);
+                       ld_dz, (float*)dbias, reinterpret_cast<float*>(workspace) + 1,
+                       reinterpret_cast<unsigned*>(workspace));
     CCMPI_HIP_CHECK(hipGetLastError());
     return;
   }
@@ -128,8 +150,12 @@ void xent_head(uint64_t z, int ld_z, uint64_t bias, uint64_t y, bool y64, int B,
 
 void register_head_ops(pybind11::module_& m) {
   m.def("xent_head", &xent_head,
-        "fused softmax cross-entropy head: loss (+=, zeroed first), bf16 dz, dbias += column sums",
-        pybind11::call_guard<pybind11::gil_scoped_release>());
+        "fused softmax cross-entropy head: loss (=), bf16 dz, dbias += column sums; workspace: 4 + 4*ceil(B/16) bytes, "
+        "zero-initialized once (lane-per-class kernel), 0 = memset + atomics",
+        pybind11::arg("z"), pybind11::arg("ld_z"), pybind11::arg("bias"), pybind11::arg("y"), pybind11::arg("y64"),
+        pybind11::arg("B"), pybind11::arg("C"), pybind11::arg("Cpad"), pybind11::arg("scale"), pybind11::arg("loss"),
+        pybind11::arg("dz"), pybind11::arg("ld_dz"), pybind11::arg("dbias"), pybind11::arg("stream"),
+        pybind11::arg("workspace") = 0, pybind11::call_guard<pybind11::gil_scoped_release>());
 }
 
 }  // namespace dev

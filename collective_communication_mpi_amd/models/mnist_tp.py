@@ -264,13 +264,18 @@ class MnistTPLayer:
         zp = self._buf("zp", (B, cfg.out_pad), torch.float32, self.tp_dev)
         dzp = self._buf("dzp", (B, cfg.out_pad), torch.bfloat16)
         loss = self._buf("loss", (1,), torch.float32)
+        if "xent_ws" not in self._bufs:  # ticket + per-workgroup partials; the kernel re-arms the ticket
+            self._bufs["xent_ws"] = torch.zeros(1 + (B + 15) // 16 + 64, dtype=torch.float32, device=self.device)
+        ws = self._bufs["xent_ws"]
+        if ws.numel() < 1 + (B + 15) // 16:
+            ws = self._bufs["xent_ws"] = torch.zeros(1 + (B + 15) // 16 + 64, dtype=torch.float32, device=self.device)
         if y.dtype not in (torch.int32, torch.int64) or not y.is_contiguous():
             y = y.to(torch.int32).contiguous()
         _native.device().xent_head(zp.data_ptr(), zp.stride(0), 0, y.data_ptr(),  # zp already holds + o_b
                                    y.dtype == torch.int64, B,
                                    cfg.n_classes, cfg.out_pad, 1.0 / global_batch, loss.data_ptr(), dzp.data_ptr(),
                                    dzp.stride(0), self.flat.grad("o_b").data_ptr(),
-                                   torch.cuda.current_stream(self.device).cuda_stream)
+                                   torch.cuda.current_stream(self.device).cuda_stream, ws.data_ptr())
         self._dz_ready = True
         return loss[0]
 

@@ -321,16 +321,24 @@ def test_xent_head_fused(ydtype, C, Cp):
     loss = torch.empty(1, device="cuda")
     dz = torch.full((B, Cp), 7.0, device="cuda").bfloat16()
     db = torch.ones(Cp, device="cuda")
-    _native.device().xent_head(z.data_ptr(), z.stride(0), bias.data_ptr(), y.data_ptr(), ydtype == torch.int64, B, C,
-                               Cp, 1.0 / gb, loss.data_ptr(), dz.data_ptr(), dz.stride(0), db.data_ptr(),
-                               torch.cuda.current_stream().cuda_stream)
+    ws = torch.zeros(1 + (B + 15) // 16, device="cuda")  # ticket + partials (lane-per-class kernel)
+    for it in range(2):  # the second call checks that the kernel re-armed its ticket
+        db_in = db.clone()
+        _native.device().xent_head(z.data_ptr(), z.stride(0), bias.data_ptr(), y.data_ptr(), ydtype == torch.int64, B,
+                                   C, Cp, 1.0 / gb, loss.data_ptr(), dz.data_ptr(), dz.stride(0), db.data_ptr(),
+                                   torch.cuda.current_stream().cuda_stream, ws.data_ptr())
+        if it == 0:
+            first = loss.clone()
+    torch.testing.assert_close(loss, first)
     logits = (z[:, :C] + bias[:C]).requires_grad_(True)
     ref = torch.nn.functional.cross_entropy(logits, y.long(), reduction="sum") / gb
     ref.backward()
     torch.testing.assert_close(loss[0], ref.detach(), rtol=1e-5, atol=1e-6)
     torch.testing.assert_close(dz[:, :C].float(), logits.grad, rtol=1e-2, atol=1e-5)
     assert torch.all(dz[:, C:] == 0)
-    torch.testing.assert_close(db[:C], 1 + logits.grad.sum(0), rtol=1e-4, atol=1e-6)
+    gsum = logits.grad.sum(0)
+    torch.testing.assert_close(db_in[:C], 1 + gsum, rtol=1e-4, atol=1e-6)   # after one call
+    torch.testing.assert_close(db[:C], 1 + 2 * gsum, rtol=1e-4, atol=1e-6)  # after two
     torch.testing.assert_close(db[C:], torch.ones(Cp - C, device="cuda"))
 
 
