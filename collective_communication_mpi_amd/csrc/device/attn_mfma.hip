@@ -17,7 +17,9 @@
 //   * Backward recomputes both S and S^T (and dP, dP^T), so each of
 //     dV = P^T dO, dK = scale dS^T Q and dQ = scale dS K contracts over an
 //     accumulator's row index: the accumulator is the A operand, the other
-//     factor comes from the per-wave LDS tile.  delta_i = rowsum(dO * O).
+//     factor comes from the per-wave LDS tile.  delta_i = rowsum(dO * O) is
+//     computed as rowsum(P * dP) from registers, so O is not read -- and the
+//     forward skips storing O when the caller passes o = null (pooled mode).
 //   * Outputs are staged per wave through LDS and written as 16-B row
 //     vectors.  The pooled forward output (mean over the S rows, for the
 //     pooled row-parallel fc_o) and the QKV bias gradient (column sums of dQ,
@@ -152,7 +154,7 @@ __global__ void __launch_bounds__(256) k_attn16_fwd(AttnArgs a) {
         if (g == 0) a.pool[(size_t)b * a.ld_pool + h * D + 16 * nt + c] = (uint16_t)f32_to_bf16_bits(cs / (float)S);
       }
     }
-    store_tile<D, LD>(O, o, 1.f, a.o + (size_t)b * S * a.ld_o + h * D, a.ld_o, S, lane);
+    if (a.o) store_tile<D, LD>(O, o, 1.f, a.o + (size_t)b * S * a.ld_o + h * D, a.ld_o, S, lane);
   }
 }
 
@@ -176,9 +178,8 @@ __global__ void __launch_bounds__(256) k_attn16_bwd(AttnArgs a) {
   for (int b = (blockIdx.x / a.Hl) * WPB + wave; b < a.B; b += nbh * WPB) {
     const int pr = b * a.Hl + h;
     const uint16_t* qb = a.qkv + (size_t)b * S * a.ld_qkv + h * D;
-    const uint16_t* ob = a.o + (size_t)b * S * a.ld_o + h * D;
     const uint16_t* db = a.dout + (size_t)b * a.dout_bstride + h * D;
-    bf16x8 qr[NK], kr[NK], vr[NK], dr[NK], orr[NK];
+    bf16x8 qr[NK], kr[NK], vr[NK], dr[NK];
 #pragma unroll
     for (int kk = 0; kk < NK; ++kk) {
       const size_t off = (size_t)c * a.ld_qkv + 32 * kk + 8 * g;
@@ -186,7 +187,6 @@ __global__ void __launch_bounds__(256) k_attn16_bwd(AttnArgs a) {
       kr[kk] = ld_row16(qb + HD + off, c < S);
       vr[kk] = ld_row16(qb + 2 * HD + off, c < S);
       dr[kk] = ld_row16(db + (size_t)c * a.dout_rstride + 32 * kk + 8 * g, c < S);
-      orr[kk] = ld_row16(ob + (size_t)c * a.ld_o + 32 * kk + 8 * g, c < S);
     }
     put_rows<D, LD>(Qt, qr, lane);
     put_rows<D, LD>(Kt, kr, lane);
@@ -204,23 +204,28 @@ __global__ void __launch_bounds__(256) k_attn16_bwd(AttnArgs a) {
       dpT = mma32(vr[kk], dr[kk], dpT);  // dP^T[j = 4g + r][i = c]
       dpM = mma32(dr[kk], vr[kk], dpM);  // dP[i = 4g + r][j = c]
     }
-    // delta_i = sum_d dO[i][d] O[i][d] for i = c, then for rows i = 4g + r
-    float dl = 0.f;
-#pragma unroll
-    for (int kk = 0; kk < NK; ++kk)
-#pragma unroll
-      for (int e = 0; e < 8; ++e) dl += (float)dr[kk][e] * (float)orr[kk][e];
-    dl += __shfl_xor(dl, 16);
-    dl += __shfl_xor(dl, 32);
+    // delta_i = sum_d dO[i][d] O[i][d] = sum_j P[i][j] dP[i][j]: from the probabilities
+    // and dP already in registers, so O is never read (and need not be stored)
     float P[4], PT[4], dS[4], dST[4];
+    float dl = 0.f, dl_r[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const bool ok = (4 * g + r < S) && (c < S);
       PT[r] = ok ? __expf(sT[r] * a.scale - lse_c) : 0.f;
       P[r] = ok ? __expf(sM[r] * a.scale - lse_r[r]) : 0.f;
-      const float dl_r = __shfl(dl, 4 * g + r);
+      dl += PT[r] * dpT[r];          // row i = c: keys j = 4g + r in registers ...
+      dl_r[r] = P[r] * dpM[r];       // row i = 4g + r: keys j = c on the lanes ...
+    }
+    dl += __shfl_xor(dl, 16);        // ... and across the four lane groups
+    dl += __shfl_xor(dl, 32);
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) dl_r[r] += __shfl_xor(dl_r[r], o);  // ... and across the 16 lanes
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
       dST[r] = PT[r] * (dpT[r] - dl);
-      dS[r] = P[r] * (dpM[r] - dl_r);
+      dS[r] = P[r] * (dpM[r] - dl_r[r]);
     }
     __builtin_amdgcn_wave_barrier();
     const s4 aP = pack4(P[0], P[1], P[2], P[3]);        // A[j = c][i = 4g + jj] = P^T

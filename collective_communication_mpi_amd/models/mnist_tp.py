@@ -204,14 +204,18 @@ class MnistTPLayer:
         gemm_nt(xp, P16("emb_w"), out=h)  # bias + position are columns of W_emb
         qkv = self._buf("qkv", (M, 3 * self.hd), torch.bfloat16)
         gemm_nt(h, P16("qkv_w"), out=qkv, bias=self.flat.param("qkv_b"))
-        att = self._buf("att", (M, self.hd), torch.bfloat16)
         lse = self._buf("lse", (B * self.hl, S), torch.float32)
         D = _native.device()
         st = torch.cuda.current_stream(self.device).cuda_stream
         naive = cfg.fc_o_mode == "naive" and cfg.tp > 1
         pool = None if naive else self._buf("pool", (B, self.hd), torch.bfloat16)
-        D.attn_small_fwd(qkv.data_ptr(), att.data_ptr(), lse.data_ptr(), B, S, self.hl, cfg.head_dim,
-                         qkv.stride(0), att.stride(0), 1.0 / math.sqrt(cfg.head_dim),
+        # the per-token attention output is only consumed by the naive fc_o; the pooled
+        # path (and the MFMA backward, which never reads O) skip materializing it
+        mfma_attn = S <= 16 and cfg.head_dim in (32, 64, 128)
+        att = self._buf("att", (M, self.hd), torch.bfloat16) if (naive or not mfma_attn) else None
+        D.attn_small_fwd(qkv.data_ptr(), 0 if att is None else att.data_ptr(), lse.data_ptr(), B, S, self.hl,
+                         cfg.head_dim, qkv.stride(0), self.hd if att is None else att.stride(0),
+                         1.0 / math.sqrt(cfg.head_dim),
                          0 if pool is None else pool.data_ptr(), 0 if pool is None else pool.stride(0), st)
         if naive:
             z = self._forward_naive_fc_o(att, B)
@@ -323,8 +327,9 @@ class MnistTPLayer:
         self.buckets.ready(0)
         # ---- attention
         dqkv = self._buf("dqkv", (M, 3 * self.hd), torch.bfloat16)
-        D.attn_small_bwd(qkv.data_ptr(), att.data_ptr(), lse.data_ptr(), dout.data_ptr(), dqkv.data_ptr(),
-                         G("qkv_b").data_ptr(), B, S, self.hl, cfg.head_dim, qkv.stride(0), att.stride(0),
+        D.attn_small_bwd(qkv.data_ptr(), 0 if att is None else att.data_ptr(), lse.data_ptr(), dout.data_ptr(),
+                         dqkv.data_ptr(), G("qkv_b").data_ptr(), B, S, self.hl, cfg.head_dim, qkv.stride(0),
+                         self.hd if att is None else att.stride(0),
                          1.0 / math.sqrt(cfg.head_dim), dout_b, dout_r, st)  # + QKV bias grad in-kernel
         # ---- fused QKV projection (column-parallel)
         gemm_tn(dqkv, h, out=G("qkv_w"), accumulate=True)      # dW_qkv = dQKV^T . h
