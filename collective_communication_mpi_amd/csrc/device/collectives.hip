@@ -591,25 +591,63 @@ __global__ void __launch_bounds__(kThreads) k_local_reduce(LocalReduceArgs a) {
 
 // Streaming device copy (single-rank "all-reduce" and staging): 16-B
 // non-temporal loads/stores, 4 vectors in flight per lane, grid-stride.
-__global__ void __launch_bounds__(kThreads) k_copy(const u32x4* __restrict__ src, u32x4* __restrict__ dst, uint64_t nv) {
-  const uint64_t stride = (uint64_t)gridDim.x * kThreads;
-  uint64_t v = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
-  for (; v + 3 * stride < nv; v += 4 * stride) {
-    u32x4 a = __builtin_nontemporal_load(src + v);
-    u32x4 b = __builtin_nontemporal_load(src + v + stride);
-    u32x4 c = __builtin_nontemporal_load(src + v + 2 * stride);
-    u32x4 d = __builtin_nontemporal_load(src + v + 3 * stride);
-    __builtin_nontemporal_store(a, dst + v);
-    __builtin_nontemporal_store(b, dst + v + stride);
-    __builtin_nontemporal_store(c, dst + v + 2 * stride);
-    __builtin_nontemporal_store(d, dst + v + 3 * stride);
+// Copy-kernel variants for the bandwidth sweep (benchmarks/copy_sweep.py):
+// U 16-B vectors in flight per lane, non-temporal loads (LNT) / stores (SNT),
+// CONTIG = each workgroup streams one contiguous slice instead of grid-striding.
+template <int U, bool LNT, bool SNT, bool CONTIG>
+__global__ void __launch_bounds__(kThreads) k_copy_v(const u32x4* __restrict__ src, u32x4* __restrict__ dst, uint64_t nv) {
+  uint64_t v, stride, end;
+  if (CONTIG) {
+    const uint64_t per = ((nv + gridDim.x - 1) / gridDim.x + kThreads - 1) / kThreads * kThreads;
+    v = (uint64_t)blockIdx.x * per + threadIdx.x;
+    end = std::min<uint64_t>(nv, (uint64_t)(blockIdx.x + 1) * per);
+    stride = kThreads;
+  } else {
+    v = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
+    end = nv;
+    stride = (uint64_t)gridDim.x * kThreads;
   }
-  for (; v < nv; v += stride) __builtin_nontemporal_store(__builtin_nontemporal_load(src + v), dst + v);
+  for (; v + (U - 1) * stride < end; v += U * stride) {
+    u32x4 r[U];
+#pragma unroll
+    for (int i = 0; i < U; ++i) r[i] = LNT ? __builtin_nontemporal_load(src + v + i * stride) : src[v + i * stride];
+#pragma unroll
+    for (int i = 0; i < U; ++i) {
+      if (SNT) __builtin_nontemporal_store(r[i], dst + v + i * stride);
+      else dst[v + i * stride] = r[i];
+    }
+  }
+  for (; v < end; v += stride) dst[v] = src[v];
 }
 
 // ---------------------------------------------------------------------------
 // host-side launchers
 // ---------------------------------------------------------------------------
+void launch_copy_variant(const void* src, void* dst, uint64_t nbytes, int variant, int grid, hipStream_t s) {
+  if (((uint64_t)src | (uint64_t)dst | nbytes) % 16) throw std::invalid_argument("copy_variant: 16-B aligned only");
+  const uint64_t nv = nbytes / 16;
+  if (grid <= 0) grid = (int)std::min<uint64_t>((nv + kThreads - 1) / kThreads, 4096);
+  auto* a = (const u32x4*)src;
+  auto* b = (u32x4*)dst;
+  switch (variant) {
+    case 0: hipLaunchKernelGGL((k_copy_v<4, true, true, false>), dim3(grid), dim3(kThreads), 0, s, a, b, nv); break;
+    case 1: hipLaunchKernelGGL((k_copy_v<8, true, true, false>), dim3(grid), dim3(kThreads), 0, s, a, b, nv); break;
+    case 2: hipLaunchKernelGGL((k_copy_v<4, false, false, false>), dim3(grid), dim3(kThreads), 0, s, a, b, nv); break;
+    case 3: hipLaunchKernelGGL((k_copy_v<4, true, false, false>), dim3(grid), dim3(kThreads), 0, s, a, b, nv); break;
+    case 4: hipLaunchKernelGGL((k_copy_v<4, false, true, false>), dim3(grid), dim3(kThreads), 0, s, a, b, nv); break;
+    case 5: hipLaunchKernelGGL((k_copy_v<4, true, true, true>), dim3(grid), dim3(kThreads), 0, s, a, b, nv); break;
+    case 6: hipLaunchKernelGGL((k_copy_v<8, true, true, true>), dim3(grid), dim3(kThreads), 0, s, a, b, nv); break;
+    case 7: hipLaunchKernelGGL((k_copy_v<2, true, true, false>), dim3(grid), dim3(kThreads), 0, s, a, b, nv); break;
+    case 8: hipLaunchKernelGGL((k_copy_v<16, true, true, false>), dim3(grid), dim3(kThreads), 0, s, a, b, nv); break;
+    case 9: hipLaunchKernelGGL((k_copy_v<2, true, true, true>), dim3(grid), dim3(kThreads), 0, s, a, b, nv); break;
+    case 10: hipLaunchKernelGGL((k_copy_v<4, false, true, true>), dim3(grid), dim3(kThreads), 0, s, a, b, nv); break;
+    case 11: hipLaunchKernelGGL((k_copy_v<4, false, false, true>), dim3(grid), dim3(kThreads), 0, s, a, b, nv); break;
+    case 12: hipLaunchKernelGGL((k_copy_v<1, true, true, true>), dim3(grid), dim3(kThreads), 0, s, a, b, nv); break;
+    default: throw std::invalid_argument("copy_variant: variant 0..12");
+  }
+  CCMPI_HIP_CHECK(hipGetLastError());
+}
+
 void launch_copy(const void* src, void* dst, uint64_t nbytes, hipStream_t s) {
   if (nbytes == 0 || src == dst) return;
   const uint64_t a = (uint64_t)src | (uint64_t)dst;
@@ -617,9 +655,15 @@ void launch_copy(const void* src, void* dst, uint64_t nbytes, hipStream_t s) {
     CCMPI_HIP_CHECK(hipMemcpyAsync(dst, src, nbytes, hipMemcpyDeviceToDevice, s));
     return;
   }
+  // One contiguous 4 KiB slice per workgroup (one 16-B non-temporal vector per
+  // lane) up to 2^20 workgroups, longer slices beyond.  Measured on MI355X
+  // (profiles/r1_copy): 3.1-3.2 TB/s algbw at 1 GiB vs 2.4-2.6 for the runtime
+  // blit and 2.2-2.5 for a grid-stride loop, which interleaves every
+  // workgroup's accesses over the whole buffer.
   const uint64_t nv = nbytes / 16;
-  const int grid = (int)std::min<uint64_t>((nv + kThreads - 1) / kThreads, 4096);
-  hipLaunchKernelGGL(k_copy, dim3(grid), dim3(kThreads), 0, s, (const u32x4*)src, (u32x4*)dst, nv);
+  const int grid = (int)std::min<uint64_t>((nv + kThreads - 1) / kThreads, 1u << 20);
+  hipLaunchKernelGGL((k_copy_v<1, true, true, true>), dim3(grid), dim3(kThreads), 0, s, (const u32x4*)src, (u32x4*)dst,
+                     nv);
   CCMPI_HIP_CHECK(hipGetLastError());
   if (nbytes % 16)
     CCMPI_HIP_CHECK(hipMemcpyAsync((char*)dst + nv * 16, (const char*)src + nv * 16, nbytes % 16,

@@ -176,6 +176,24 @@ def test_single_rank_communicator_paths():
     assert comm.total_bytes_transferred == 0  # p = 1: no traffic in any formula
 
 
+@pytest.mark.parametrize("nbytes", [(1 << 20) + 16, (1 << 20) + 6, 48 << 20, (4 << 30) + 4096 + 48])
+def test_single_rank_allreduce_copy(nbytes):
+    """N = 1 all-reduce = the contiguous-slice copy kernel: exact bytes, tails, > 2^20 workgroups' worth."""
+    from collective_communication_mpi_amd import MPI, Communicator, _native
+
+    D = _native.device()
+    x = torch.randn(nbytes // 2, device="cuda", dtype=torch.float16)
+    y = torch.zeros_like(x)
+    Communicator(MPI.COMM_WORLD).Allreduce(x, y, MPI.SUM)
+    assert torch.equal(x, y)
+    if nbytes % 16 == 0 and nbytes < (1 << 30):
+        for v in range(13):
+            y.zero_()
+            D.copy_variant(x.data_ptr(), y.data_ptr(), nbytes, v, 1000, torch.cuda.current_stream().cuda_stream)
+            torch.cuda.synchronize()
+            assert torch.equal(x, y), v
+
+
 def test_split_derives_rccl_communicator():
     """Split of a communicator that has RCCL derives the child's via ncclCommSplit."""
     from collective_communication_mpi_amd import MPI, Communicator
