@@ -32,6 +32,7 @@ ap.add_argument("--layers", type=int, default=32)
 ap.add_argument("--tokens", type=int, default=4096, help="tokens per rank per step")
 ap.add_argument("--iters", type=int, default=3)
 ap.add_argument("--algo", default="auto")
+ap.add_argument("--comm-priority", type=int, default=-1, help="side-stream priority (-1 = high, 0 = normal)")
 args = ap.parse_args()
 comm = Communicator(MPI.COMM_WORLD)
 rank, p = comm.Get_rank(), comm.Get_size()
@@ -46,7 +47,7 @@ per_layer = sum(a * b for a, b in shapes)
 grads = dev.empty(per_layer * args.layers, torch.float32)  # fp32 master grads
 act_in = {k: torch.randn(T, k, device=dev.device).bfloat16() for k in {d, ff}}
 act_out = {k: torch.randn(T, k, device=dev.device).bfloat16() for k in {d, kv, ff}}
-side = torch.cuda.Stream()
+side = torch.cuda.Stream(priority=args.comm_priority)
 events = [torch.cuda.Event() for _ in range(args.layers)]
 
 

@@ -112,7 +112,10 @@ class GradBuckets:
         self.ranges = [flat.range_of(b) for b in buckets]
         self.algo = algo
         self.overlap = overlap
-        self.stream = torch.cuda.Stream(device=flat.device) if (dp_group is not None and overlap) else None
+        # high-priority side stream: a bucket's all-reduce workgroups are dispatched ahead of
+        # the backward GEMM tiles queued behind them, so communication starts as soon as the
+        # bucket is ready instead of after the GEMM drains
+        self.stream = torch.cuda.Stream(device=flat.device, priority=-1) if (dp_group is not None and overlap) else None
         self.events: List[torch.cuda.Event] = [torch.cuda.Event() for _ in self.ranges]
         self.launched = 0
 
