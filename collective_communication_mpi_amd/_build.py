@@ -127,7 +127,7 @@ def build_device(force: bool = False, verbose: bool = False) -> Path:
         objdir = PKG / "build" / "device"
         objdir.mkdir(parents=True, exist_ok=True)
         common = ["-O3", "-std=c++20", "-fPIC", "-fvisibility=hidden", f"--offload-arch={ARCH}",
-                  "-D__HIP_PLATFORM_AMD__=1", f"-I{CSRC / 'device'}", f"-I{ROCM / 'include'}",
+                  f"-I{CSRC / 'device'}", f"-I{ROCM / 'include'}",
                   *_py_includes(), "-Wno-unused-result", "-Wno-unused-command-line-argument"]
         if os.environ.get("CCMPI_SAVE_TEMPS"):
             common += ["-save-temps"]
@@ -139,8 +139,7 @@ def build_device(force: bool = False, verbose: bool = False) -> Path:
             hdrs = _sources("device", (".hpp", ".h", ".cuh", ".inc"))
             if not force and obj.exists() and not _stale(obj, [src, *hdrs]):
                 continue
-            lang = ["-x", "hip"] if src.suffix == ".hip" else ["-x", "hip"]
-            cmd = [hipcc, *lang, *common, "-c", str(src), "-o", str(obj)]
+            cmd = [hipcc, "-x", "hip", *common, "-c", str(src), "-o", str(obj)]
             if verbose:
                 print("[ccmpi build]", " ".join(cmd), flush=True)
             procs.append((cmd, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)))
