@@ -78,3 +78,24 @@ def test_sharded_checkpoint_roundtrip(tmp_path, n, tp):
 
     r = run_ranks(n, py("tests/workers/ckpt_worker.py", str(tmp_path / "ck"), str(tp)), timeout=120)
     assert r.stdout.count("checkpoint OK") == n
+
+
+def test_runs_under_torchrun():
+    """The driver launches bench.py with torch.distributed.run: the host plane must
+    bootstrap from RANK/WORLD_SIZE/MASTER_PORT/TORCHELASTIC_RUN_ID."""
+    import os
+    import socket
+    import subprocess
+    import sys
+
+    from _launch import REPO
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ, PYTHONPATH=REPO, CCMPI_TIMEOUT="60")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "4",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), "tests/workers/host_worker.py"],
+                       cwd=REPO, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    assert "host plane OK at 4 ranks" in r.stdout
