@@ -21,7 +21,12 @@ from typing import Optional
 
 import numpy as np
 
+from . import _native
 from . import mpi as MPI
+
+_h = _native.host()
+_fmy_allreduce, _fmy_alltoall = _h.fmy_allreduce, _h.fmy_alltoall
+_HOST_ALGOS = {"reduce_bcast": 0, "ring": 1, "rhd": 2}
 
 _SUPPORTED_MY_OPS = ("SUM", "PROD", "MIN", "MAX")
 
@@ -49,6 +54,10 @@ def _np_op(op):
     if name == "PROD":
         return np.multiply
     raise NotImplementedError("Only MPI.SUM, MPI.MIN, MPI.MAX and MPI.PROD are supported.")
+
+
+def _op_code(op) -> int:
+    return _SUPPORTED_MY_OPS.index(getattr(op, "name", str(op)).upper())
 
 
 def _validate_op(op) -> None:
@@ -208,6 +217,9 @@ class Communicator(object):
         bytes_transferred = isz * n
         if _is_device(src_array):
             self.dev.allreduce(src_array, dest_array, op, algo)
+        elif algo in _HOST_ALGOS and isinstance(self.comm, MPI.Comm) and \
+                _fmy_allreduce(self.comm._p, src_array, dest_array, _op_code(op), _HOST_ALGOS[algo]) is not NotImplemented:
+            pass  # the same message schedule, run natively (csrc/host/p2p_algos.cpp)
         elif algo == "reduce_bcast":
             self._host_reduce_bcast(src_array, dest_array, op)
         elif algo == "ring":
@@ -310,6 +322,9 @@ class Communicator(object):
         segment_size = n // size
         if _is_device(src_array):
             self.dev.alltoall(src_array, dest_array, algo)
+        elif isinstance(self.comm, MPI.Comm) and \
+                _fmy_alltoall(self.comm._p, src_array, dest_array, False) is not NotImplemented:
+            pass  # Irecv-all / Isend-all / Waitall, run natively (csrc/host/p2p_algos.cpp)
         else:
             src = src_array.reshape(-1)
             dst = dest_array.reshape(-1)
@@ -341,6 +356,9 @@ class Communicator(object):
         chunk_size = n // size
         if _is_device(src_array):
             self.dev.alltoall(src_array, dest_array, algo)
+        elif isinstance(self.comm, MPI.Comm) and \
+                _fmy_alltoall(self.comm._p, src_array, dest_array, True) is not NotImplemented:
+            pass  # pairwise Sendrecv rounds, run natively (csrc/host/p2p_algos.cpp)
         else:
             src = src_array.reshape(-1)
             dst = dest_array.reshape(-1)

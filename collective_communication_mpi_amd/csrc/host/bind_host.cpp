@@ -11,6 +11,10 @@
 namespace py = pybind11;
 using namespace ccmpi;
 
+namespace ccmpi {
+int register_fastcall(PyObject* module);  // fastcall.cpp
+}
+
 namespace {
 
 struct Buf {
@@ -61,6 +65,7 @@ PYBIND11_MODULE(_host, m) {
   m.attr("ANY_TAG") = ANY_TAG;
   m.attr("PROC_NULL") = PROC_NULL;
 
+  if (register_fastcall(m.ptr()) != 0) throw py::error_already_set();
   m.def("wtime", &wtime);
   m.def("job_id", &job_id_from_env);
   m.def("dtype_size", &dtype_size);
@@ -77,6 +82,7 @@ PYBIND11_MODULE(_host, m) {
 
   py::class_<ShmComm, std::shared_ptr<ShmComm>>(m, "HostComm")
       .def_static("world", &ShmComm::world, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("ptr", [](ShmComm& c) { return reinterpret_cast<uintptr_t>(&c); })
       .def_property_readonly("rank", &ShmComm::rank)
       .def_property_readonly("size", &ShmComm::size)
       .def_property_readonly("name", &ShmComm::name)

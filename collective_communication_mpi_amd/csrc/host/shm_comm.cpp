@@ -153,13 +153,26 @@ size_t slot_bytes_for(int p) {
 }
 
 struct Layout {
-  size_t chan_off, ring_off, slot_off, result_off, total;
+  size_t chan_off, flag_off, small_off, ring_off, slot_off, result_off, total;
 };
+
+// per-rank epoch flag (own cache line; written only by its rank)
+struct alignas(64) EpochFlag {
+  std::atomic<uint64_t> epoch;
+  char pad[56];
+};
+static_assert(sizeof(EpochFlag) == 64, "EpochFlag layout");
+
+// single-sync small-message collectives: per rank two (double-buffered by
+// epoch parity) regions of kSmallBytes
+constexpr size_t kSmallBytes = 8192;
 
 Layout layout_for(int p, size_t ring, size_t slot) {
   Layout L;
   L.chan_off = round_up(sizeof(SegHeader), 128);
-  L.ring_off = round_up(L.chan_off + sizeof(ChanCtl) * (size_t)p * p, 4096);
+  L.flag_off = round_up(L.chan_off + sizeof(ChanCtl) * (size_t)p * p, 128);
+  L.small_off = round_up(L.flag_off + sizeof(EpochFlag) * (size_t)p, 4096);
+  L.ring_off = round_up(L.small_off + 2 * kSmallBytes * (size_t)p, 4096);
   L.slot_off = round_up(L.ring_off + ring * (size_t)p * p, 4096);
   L.result_off = L.slot_off + slot * (size_t)p;
   L.total = round_up(L.result_off + slot, 4096);
@@ -173,9 +186,11 @@ ShmComm::ShmComm(const std::string& name, int rank, int size)
   if (size < 1 || rank < 0 || rank >= size)
     throw std::invalid_argument("ccmpi: bad rank/size");
   if (const char* t = envs("CCMPI_TIMEOUT")) timeout_s_ = std::atof(t);
+  small_allreduce_max_ = std::min(env_size("CCMPI_SMALL_ALLREDUCE_BYTES", small_allreduce_max_), kSmallBytes);
   world_ranks_.resize(size);
   for (int i = 0; i < size; ++i) world_ranks_[i] = i;
   send_q_.resize(size);
+  peer_tail_.assign(size, 0);
   unexpected_.resize(size);
   cur_.resize(size);
   attach_();
@@ -224,6 +239,27 @@ void ShmComm::attach_() {
   if (h.size != (uint32_t)size_ || h.ring_bytes != ring || h.slot_bytes != slot)
     throw std::runtime_error("ccmpi: segment geometry mismatch (CCMPI_RING_BYTES/CCMPI_SLOT_BYTES differ across ranks?)");
   if (rank_ == 0) shm_unlink(shm_name.c_str());
+  // cache this rank's channel control blocks and rings (the progress engine
+  // touches them on every poll)
+  auto* ctl = reinterpret_cast<ChanCtl*>(reinterpret_cast<char*>(seg_) + L.chan_off);
+  char* rings = reinterpret_cast<char*>(seg_) + L.ring_off;
+  out_ctl_.resize(size_);
+  in_ctl_.resize(size_);
+  out_ring_.resize(size_);
+  in_ring_.resize(size_);
+  for (int j = 0; j < size_; ++j) {
+    out_ctl_[j] = &ctl[(size_t)rank_ * size_ + j];
+    in_ctl_[j] = &ctl[(size_t)j * size_ + rank_];
+    out_ring_[j] = rings + ring * ((size_t)rank_ * size_ + j);
+    in_ring_[j] = rings + ring * ((size_t)j * size_ + rank_);
+  }
+  ring_cap_ = ring;
+  auto* flags = reinterpret_cast<EpochFlag*>(reinterpret_cast<char*>(seg_) + L.flag_off);
+  flag_.resize(size_);
+  for (int j = 0; j < size_; ++j) flag_[j] = &flags[j].epoch;
+  small_base_ = reinterpret_cast<char*>(seg_) + L.small_off;
+  slot_base_ = reinterpret_cast<char*>(seg_) + L.slot_off;
+  result_base_ = reinterpret_cast<char*>(seg_) + L.result_off;
 }
 
 ShmComm::~ShmComm() {
@@ -261,15 +297,15 @@ std::shared_ptr<ShmComm> ShmComm::world() {
 size_t ShmComm::slot_bytes() const { return seg_->hdr.slot_bytes; }
 size_t ShmComm::ring_bytes() const { return seg_->hdr.ring_bytes; }
 
-char* ShmComm::slot_(int r) {
-  Layout L = layout_for(size_, seg_->hdr.ring_bytes, seg_->hdr.slot_bytes);
-  return reinterpret_cast<char*>(seg_) + L.slot_off + seg_->hdr.slot_bytes * (size_t)r;
+char* ShmComm::slot_(int r) { return slot_base_ + seg_->hdr.slot_bytes * (size_t)r; }
+
+char* ShmComm::result_() { return result_base_; }
+
+char* ShmComm::small_(int r, uint64_t e) {
+  return small_base_ + kSmallBytes * (2 * (size_t)r + (size_t)(e & 1));
 }
 
-char* ShmComm::result_() {
-  Layout L = layout_for(size_, seg_->hdr.ring_bytes, seg_->hdr.slot_bytes);
-  return reinterpret_cast<char*>(seg_) + L.result_off;
-}
+size_t ShmComm::small_bytes() const { return kSmallBytes; }
 
 void ShmComm::backoff_(uint64_t& spins) {
   ++spins;
@@ -295,16 +331,6 @@ void ShmComm::timeout_(const char* what) {
 // ---------------------------------------------------------------------------
 namespace {
 
-inline ChanCtl& chan(Segment* s, int p, int src, int dst) {
-  Layout L = layout_for(p, s->hdr.ring_bytes, s->hdr.slot_bytes);
-  return reinterpret_cast<ChanCtl*>(reinterpret_cast<char*>(s) + L.chan_off)[(size_t)src * p + dst];
-}
-
-inline char* ring(Segment* s, int p, int src, int dst) {
-  Layout L = layout_for(p, s->hdr.ring_bytes, s->hdr.slot_bytes);
-  return reinterpret_cast<char*>(s) + L.ring_off + s->hdr.ring_bytes * ((size_t)src * p + dst);
-}
-
 inline void ring_put(char* r, size_t cap, uint64_t pos, const char* src, size_t n) {
   size_t o = (size_t)(pos & (cap - 1));
   size_t a = std::min(n, cap - o);
@@ -321,21 +347,30 @@ inline void ring_get(const char* r, size_t cap, uint64_t pos, char* dst, size_t 
   }
 }
 
-inline bool tag_match(int want, int got) { return want == ANY_TAG || want == got; }
+// ANY_TAG matches user tags only: the framework's own P2P schedules
+// (p2p_algos.cpp) use negative internal tags that user receives never see.
+inline bool tag_match(int want, int got) { return (want == ANY_TAG && got >= 0) || want == got; }
 
 }  // namespace
 
 bool ShmComm::progress_send_(int dest) {
   bool moved = false;
   auto& q = send_q_[dest];
-  const size_t cap = seg_->hdr.ring_bytes;
-  ChanCtl& c = chan(seg_, size_, rank_, dest);
-  char* rb = ring(seg_, size_, rank_, dest);
+  const size_t cap = ring_cap_;
+  ChanCtl& c = *static_cast<ChanCtl*>(out_ctl_[dest]);
+  char* rb = out_ring_[dest];
+  uint64_t head = c.head.load(std::memory_order_relaxed);
+  // the consumer's tail is re-read only when the cached value shows too little
+  // room: a steady stream of small messages never pulls the consumer's line
+  uint64_t& tail = peer_tail_[dest];
   while (!q.empty()) {
     RequestPtr r = q.front();
-    uint64_t head = c.head.load(std::memory_order_relaxed);
-    uint64_t tail = c.tail.load(std::memory_order_acquire);
     size_t free_b = cap - (size_t)(head - tail);
+    const size_t want = (r->header_sent ? 0 : kHdr) + (r->cap - r->done);
+    if (free_b < want) {
+      tail = c.tail.load(std::memory_order_acquire);
+      free_b = cap - (size_t)(head - tail);
+    }
     if (!r->header_sent) {
       if (free_b < kHdr) return moved;
       char hdr[kHdr];
@@ -348,7 +383,6 @@ bool ShmComm::progress_send_(int dest) {
       head += kHdr;
       free_b -= kHdr;
       r->header_sent = true;
-      c.head.store(head, std::memory_order_release);
       moved = true;
     }
     size_t n = std::min(free_b, r->cap - r->done);
@@ -357,9 +391,11 @@ bool ShmComm::progress_send_(int dest) {
       ring_put(rb, cap, head, src + r->done, n);
       head += n;
       r->done += n;
-      c.head.store(head, std::memory_order_release);
       moved = true;
     }
+    // one publication per (header + payload) that fits: the consumer sees the
+    // whole message at once instead of the header first
+    if (moved) c.head.store(head, std::memory_order_release);
     if (r->done == r->cap) {
       r->complete = true;
       q.pop_front();
@@ -372,9 +408,9 @@ bool ShmComm::progress_send_(int dest) {
 
 bool ShmComm::progress_recv_(int src) {
   bool moved = false;
-  const size_t cap = seg_->hdr.ring_bytes;
-  ChanCtl& c = chan(seg_, size_, src, rank_);
-  const char* rb = ring(seg_, size_, src, rank_);
+  const size_t cap = ring_cap_;
+  ChanCtl& c = *static_cast<ChanCtl*>(in_ctl_[src]);
+  const char* rb = in_ring_[src];
   Cursor& cu = cur_[src];
   for (;;) {
     uint64_t head = c.head.load(std::memory_order_acquire);
@@ -508,6 +544,11 @@ void ShmComm::post_recv_(const RequestPtr& r) {
 }
 
 RequestPtr ShmComm::isend(const void* buf, size_t nbytes, int dest, int tag) {
+  if (tag < 0) throw std::invalid_argument("ccmpi: send tag must be >= 0");
+  return isend_raw(buf, nbytes, dest, tag);
+}
+
+RequestPtr ShmComm::isend_raw(const void* buf, size_t nbytes, int dest, int tag) {
   auto r = std::make_shared<Request>();
   r->kind = Request::SEND;
   r->peer = dest;
@@ -516,7 +557,6 @@ RequestPtr ShmComm::isend(const void* buf, size_t nbytes, int dest, int tag) {
   r->buf = const_cast<char*>(static_cast<const char*>(buf));
   if (dest == PROC_NULL) { r->complete = true; return r; }
   if (dest < 0 || dest >= size_) throw std::invalid_argument("ccmpi: invalid destination rank");
-  if (tag < 0) throw std::invalid_argument("ccmpi: send tag must be >= 0");
   send_q_[dest].push_back(r);
   progress_send_(dest);
   return r;
@@ -616,29 +656,25 @@ void ShmComm::probe(int source, int tag, int* src_out, int* tag_out, size_t* byt
 // ---------------------------------------------------------------------------
 // collectives
 // ---------------------------------------------------------------------------
-void ShmComm::wait_release_(uint64_t target) {
-  SegHeader& h = seg_->hdr;
-  uint64_t spins = 0;
-  double t0 = wtime();
-  while (h.bar_release.load(std::memory_order_acquire) < target) {
-    // keep point-to-point traffic moving while we wait (MPI-style progress)
-    bool moved = false;
-    if (!posted_.empty() || (spins & 63) == 0) moved = progress();
-    if (!moved) backoff_(spins);
-    if ((spins & 1023) == 1023 && wtime() - t0 > timeout_s_) timeout_("barrier");
+// Flat epoch barrier: every rank stores its own flag (no shared counter, no
+// contended line) and waits until every other rank's flag reaches the epoch.
+void ShmComm::sync_epoch_(uint64_t e) {
+  flag_[rank_]->store(e, std::memory_order_release);
+  for (int j = 0; j < size_; ++j) {
+    if (j == rank_ || flag_[j]->load(std::memory_order_acquire) >= e) continue;
+    uint64_t spins = 0;
+    double t0 = wtime();
+    while (flag_[j]->load(std::memory_order_acquire) < e) {
+      // keep point-to-point traffic moving while we wait (MPI-style progress)
+      bool moved = false;
+      if (!posted_.empty() || (spins & 63) == 0) moved = progress();
+      if (!moved) backoff_(spins);
+      if ((spins & 1023) == 1023 && wtime() - t0 > timeout_s_) timeout_("barrier");
+    }
   }
 }
 
-void ShmComm::slot_barrier_() {
-  SegHeader& h = seg_->hdr;
-  const uint64_t e = ++bar_epoch_;
-  const uint64_t v = h.bar_arrive.fetch_add(1, std::memory_order_acq_rel) + 1;
-  if (v == e * (uint64_t)size_) {
-    h.bar_release.store(e, std::memory_order_release);
-  } else {
-    wait_release_(e);
-  }
-}
+void ShmComm::slot_barrier_() { sync_epoch_(++bar_epoch_); }
 
 void ShmComm::barrier() {
   if (size_ == 1) return;
@@ -647,8 +683,15 @@ void ShmComm::barrier() {
 
 void ShmComm::bcast(void* buf, size_t nbytes, int root) {
   if (size_ == 1 || nbytes == 0) return;
-  const size_t S = slot_bytes();
   char* b = static_cast<char*>(buf);
+  if (nbytes <= kSmallBytes) {
+    const uint64_t e = ++bar_epoch_;
+    if (rank_ == root) std::memcpy(small_(root, e), b, nbytes);
+    sync_epoch_(e);
+    if (rank_ != root) std::memcpy(b, small_(root, e), nbytes);
+    return;
+  }
+  const size_t S = slot_bytes();
   for (size_t off = 0; off < nbytes; off += S) {
     size_t c = std::min(S, nbytes - off);
     if (rank_ == root) std::memcpy(result_(), b + off, c);
@@ -665,6 +708,17 @@ void ShmComm::allreduce(const void* sbuf, void* rbuf, size_t count, int dt, int 
   char* dst = static_cast<char*>(rbuf);
   if (size_ == 1) {
     if (src != dst) std::memmove(dst, src, count * es);
+    return;
+  }
+  if (count * es <= small_allreduce_max_) {
+    // one sync: publish, then every rank reduces all p inputs itself in rank
+    // order (bitwise identical everywhere); epoch-parity double buffering makes
+    // the next call safe without a trailing barrier
+    const uint64_t e = ++bar_epoch_;
+    std::memcpy(small_(rank_, e), src, count * es);
+    sync_epoch_(e);
+    if (dst != small_(0, e)) std::memcpy(dst, small_(0, e), count * es);
+    for (int j = 1; j < size_; ++j) reduce_inplace(dst, small_(j, e), count, dt, op);
     return;
   }
   const size_t per = slot_bytes() / es;
@@ -787,6 +841,16 @@ void ShmComm::allgatherv(const void* sbuf, size_t nbytes, void* rbuf,
 }
 
 void ShmComm::allgather(const void* sbuf, size_t nbytes, void* rbuf) {
+  if (size_ > 1 && nbytes <= kSmallBytes) {
+    char* dst = static_cast<char*>(rbuf);
+    const char* src = sbuf ? static_cast<const char*>(sbuf) : dst + nbytes * (size_t)rank_;
+    const uint64_t e = ++bar_epoch_;
+    std::memcpy(small_(rank_, e), src, nbytes);
+    sync_epoch_(e);
+    for (int j = 0; j < size_; ++j)
+      if (dst + nbytes * (size_t)j != small_(j, e)) std::memcpy(dst + nbytes * (size_t)j, small_(j, e), nbytes);
+    return;
+  }
   std::vector<size_t> counts(size_, nbytes), displs(size_);
   for (int i = 0; i < size_; ++i) displs[i] = nbytes * (size_t)i;
   allgatherv(sbuf, nbytes, rbuf, counts, displs);
@@ -886,6 +950,14 @@ void ShmComm::alltoall(const void* sbuf, size_t block_bytes, void* rbuf) {
     return;
   }
   if (!src) src = dst;  // in place: inputs go to the slots before anyone writes
+  if (block_bytes * (size_t)size_ <= kSmallBytes) {
+    const uint64_t e = ++bar_epoch_;
+    std::memcpy(small_(rank_, e), src, block_bytes * (size_t)size_);
+    sync_epoch_(e);
+    for (int j = 0; j < size_; ++j)
+      std::memcpy(dst + (size_t)j * block_bytes, small_(j, e) + (size_t)rank_ * block_bytes, block_bytes);
+    return;
+  }
   const size_t cs = (slot_bytes() / size_) / 64 * 64;
   for (size_t off = 0; off < block_bytes; off += cs) {
     const size_t c = std::min(cs, block_bytes - off);

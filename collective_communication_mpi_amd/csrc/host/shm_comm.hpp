@@ -102,6 +102,18 @@ class ShmComm : public std::enable_shared_from_this<ShmComm> {
   void probe(int source, int tag, int* src_out, int* tag_out, size_t* bytes_out);
   bool iprobe(int source, int tag, int* src_out, int* tag_out, size_t* bytes_out);
 
+  // ---- the reference's hand-written collectives as native P2P schedules --
+  // (p2p_algos.cpp; same message pattern as mpi_wrapper/comm.py, internal tags)
+  // myAllreduce (comm.py:63-107): reduce to rank 0 in rank order, then send back.
+  void my_reduce_bcast(const void* src, void* dst, size_t count, int dt, int op);
+  // myAlltoall (comm.py:110-159): every irecv posted before any isend, waitall.
+  void my_alltoall_nb(const void* src, void* dst, size_t block_bytes);
+  // myAlltoall2 (comm.py:162-199): pairwise sendrecv in rank order.
+  void my_alltoall_pairwise(const void* src, void* dst, size_t block_bytes);
+  // ring reduce-scatter + all-gather, and recursive halving/doubling.
+  void my_ring_allreduce(const void* src, void* dst, size_t count, int dt, int op);
+  void my_rhd_allreduce(const void* src, void* dst, size_t count, int dt, int op);
+
   // ---- collectives (all ranks, same order) ----------------------------
   void barrier();
   void bcast(void* buf, size_t nbytes, int root);
@@ -130,15 +142,18 @@ class ShmComm : public std::enable_shared_from_this<ShmComm> {
   std::shared_ptr<ShmComm> dup() { return split(0, rank_); }
 
   size_t slot_bytes() const;
+  size_t small_bytes() const;
   size_t ring_bytes() const;
 
   // Progress every outstanding request once; returns true if anything moved.
   bool progress();
 
  private:
+  RequestPtr isend_raw(const void* buf, size_t nbytes, int dest, int tag);  // no user-tag check
   void attach_();
-  void wait_release_(uint64_t target);
+  void sync_epoch_(uint64_t e);
   void slot_barrier_();
+  char* small_(int r, uint64_t e);
   char* slot_(int r);
   char* result_();
   bool try_match_unexpected_(const RequestPtr& r);
@@ -166,6 +181,16 @@ class ShmComm : public std::enable_shared_from_this<ShmComm> {
   struct Cursor { bool active = false; int tag = 0; size_t nbytes = 0; size_t done = 0;
                   RequestPtr req; std::shared_ptr<Unexp> ux; };
   std::vector<Cursor> cur_;
+  // this rank's channel control blocks (opaque ChanCtl*) and rings, by peer
+  std::vector<void*> out_ctl_, in_ctl_;
+  std::vector<char*> out_ring_, in_ring_;
+  size_t ring_cap_ = 0;
+  std::vector<std::atomic<uint64_t>*> flag_;  // per-rank epoch flags
+  char* small_base_ = nullptr;
+  size_t small_allreduce_max_ = 1024;  // single-sync all-reduce up to this many bytes (measured crossover)
+  char* slot_base_ = nullptr;
+  char* result_base_ = nullptr;
+  std::vector<uint64_t> peer_tail_;  // last tail read from each out-channel's consumer
 };
 
 double wtime();

@@ -33,6 +33,13 @@ import numpy as np
 from . import _native
 
 _h = _native.host()
+# METH_FASTCALL entry points (csrc/host/fastcall.cpp) for plain contiguous
+# buffers; each returns NotImplemented when the general path is needed
+_fsend, _frecv, _fisend, _firecv = _h.fsend, _h.frecv, _h.fisend, _h.firecv
+_fwait, _ftest, _fwaitall, _fsendrecv = _h.fwait, _h.ftest, _h.fwaitall, _h.fsendrecv
+_fbarrier, _fbcast, _fallreduce, _fallgather = _h.fbarrier, _h.fbcast, _h.fallreduce, _h.fallgather
+_falltoall, _freduce_scatter_block = _h.falltoall, _h.freduce_scatter_block
+_NI = NotImplemented
 
 ANY_SOURCE = _h.ANY_SOURCE
 ANY_TAG = _h.ANY_TAG
@@ -295,7 +302,8 @@ class Status:
 
 
 class Request:
-    """Wraps a native request and keeps its buffer alive until completion."""
+    """Wraps a native request and keeps its buffer alive until completion.
+    ``_native`` is an int handle (fast path, fastcall.cpp) or a pybind11 request."""
 
     __slots__ = ("_comm", "_native", "_keep", "_decode", "_done", "_result")
 
@@ -306,7 +314,10 @@ class Request:
 
     def _finish(self, status: Optional[Status]):
         if self._native is not None and not self._done:
-            st = self._comm._hc.wait(self._native)
+            n = self._native
+            st = _fwait(n) if type(n) is int else self._comm._hc.wait(n)
+            if type(n) is int:
+                self._native = st  # keep the status for a later Get_status
             self._done = True
             if status is not None:
                 status._set(st)
@@ -314,7 +325,7 @@ class Request:
                 self._result = self._decode()
             self._keep = None
         elif status is not None and self._native is not None:
-            status._set(self._native.status)
+            status._set(self._native if type(self._native) is tuple else self._native.status)
         return self._result
 
     def Wait(self, status: Optional[Status] = None) -> bool:
@@ -327,7 +338,8 @@ class Request:
     def Test(self, status: Optional[Status] = None) -> bool:
         if self._done:
             return True
-        if self._comm._hc.test(self._native):
+        n = self._native
+        if (_ftest(n) if type(n) is int else self._comm._hc.test(n)):
             self._finish(status)
             return True
         return False
@@ -345,9 +357,15 @@ class Request:
     def Waitall(requests: Sequence["Request"], statuses: Optional[List[Status]] = None) -> bool:
         reqs = [r for r in requests if r is not None]
         groups = {}
+        handles = []
         for r in reqs:
             if not r._done and r._native is not None:
-                groups.setdefault(id(r._comm), (r._comm, []))[1].append(r._native)
+                if type(r._native) is int:
+                    handles.append(r._native)
+                else:
+                    groups.setdefault(id(r._comm), (r._comm, []))[1].append(r._native)
+        if handles:
+            _fwaitall(handles)
         for comm, natives in groups.values():
             comm._hc.waitall(natives)
         for i, r in enumerate(reqs):
@@ -385,13 +403,16 @@ class Comm:
 
     def __init__(self, native) -> None:
         self._hc = native
+        self._p = native.ptr  # raw pointer for the fastcall entry points (lives as long as _hc)
+        self._rank = native.rank
+        self._size = native.size
 
     # -- identity ----------------------------------------------------------
     def Get_rank(self) -> int:
-        return self._hc.rank
+        return self._rank
 
     def Get_size(self) -> int:
-        return self._hc.size
+        return self._size
 
     rank = property(Get_rank)
     size = property(Get_size)
@@ -415,36 +436,47 @@ class Comm:
 
     # -- sync ----------------------------------------------------------------
     def Barrier(self) -> None:
-        self._hc.barrier()
+        _fbarrier(self._p)
 
     barrier = Barrier
 
     # -- buffer point to point ---------------------------------------------
     def Send(self, buf, dest: int, tag: int = 0) -> None:
-        self._hc.send(_parse(buf, False).arr, dest, tag)
+        if _fsend(self._p, buf, dest, tag) is _NI:
+            self._hc.send(_parse(buf, False).arr, dest, tag)
 
     Ssend = Rsend = Bsend = Send
 
     def Recv(self, buf, source: int = ANY_SOURCE, tag: int = ANY_TAG, status: Optional[Status] = None) -> None:
-        st = self._hc.recv(_parse(buf, True).arr, source, tag)
+        st = _frecv(self._p, buf, source, tag)
+        if st is _NI:
+            st = self._hc.recv(_parse(buf, True).arr, source, tag)
         if status is not None:
             status._set(st)
 
     def Isend(self, buf, dest: int, tag: int = 0) -> Request:
+        h = _fisend(self._p, buf, dest, tag)
+        if h is not _NI:
+            return Request(self, h, buf)
         b = _parse(buf, False)
         return Request(self, self._hc.isend(b.arr, dest, tag), b.arr)
 
     Issend = Irsend = Ibsend = Isend
 
     def Irecv(self, buf, source: int = ANY_SOURCE, tag: int = ANY_TAG) -> Request:
+        h = _firecv(self._p, buf, source, tag)
+        if h is not _NI:
+            return Request(self, h, buf)
         b = _parse(buf, True)
         return Request(self, self._hc.irecv(b.arr, source, tag), b.arr)
 
     def Sendrecv(self, sendbuf, dest: int, sendtag: int = 0, recvbuf=None, source: int = ANY_SOURCE,
                  recvtag: int = ANY_TAG, status: Optional[Status] = None) -> None:
-        s = _parse(sendbuf, False)
-        r = _parse(recvbuf, True)
-        st = self._hc.sendrecv(s.arr, dest, sendtag, r.arr, source, recvtag)
+        st = _fsendrecv(self._p, sendbuf, dest, sendtag, recvbuf, source, recvtag)
+        if st is _NI:
+            s = _parse(sendbuf, False)
+            r = _parse(recvbuf, True)
+            st = self._hc.sendrecv(s.arr, dest, sendtag, r.arr, source, recvtag)
         if status is not None:
             status._set(st)
 
@@ -525,9 +557,12 @@ class Comm:
 
     # -- buffer collectives ---------------------------------------------------
     def Bcast(self, buf, root: int = 0) -> None:
-        self._hc.bcast(_parse(buf, True).arr, root)
+        if _fbcast(self._p, buf, root) is _NI:
+            self._hc.bcast(_parse(buf, True).arr, root)
 
     def Allreduce(self, sendbuf, recvbuf, op: Op = SUM) -> None:
+        if _fallreduce(self._p, sendbuf, recvbuf, op.code) is not _NI:
+            return
         s, r = _parse(sendbuf, False), _parse(recvbuf, True)
         if s is not None and s.arr.dtype != r.arr.dtype:
             s = _parse(s.arr.astype(r.arr.dtype), False)
@@ -542,6 +577,8 @@ class Comm:
         self._hc.reduce(_raw(s), _raw(r), dt, op.code, root)
 
     def Allgather(self, sendbuf, recvbuf) -> None:
+        if _fallgather(self._p, sendbuf, recvbuf) is not _NI:
+            return
         s, r = _parse(sendbuf, False), _parse(recvbuf, True)
         p = self.size
         if r.nbytes % p:
@@ -594,6 +631,8 @@ class Comm:
         self._hc.scatterv(_raw(s), cb, db, _raw(r), root)
 
     def Reduce_scatter_block(self, sendbuf, recvbuf, op: Op = SUM) -> None:
+        if _freduce_scatter_block(self._p, sendbuf, recvbuf, op.code) is not _NI:
+            return
         s, r = _parse(sendbuf, False), _parse(recvbuf, True)
         p = self.size
         if s is not None:
@@ -616,6 +655,8 @@ class Comm:
         self._hc.reduce_scatter(_raw(s), r.arr, [int(c) for c in recvcounts], r.dt, op.code)
 
     def Alltoall(self, sendbuf, recvbuf) -> None:
+        if _falltoall(self._p, sendbuf, recvbuf) is not _NI:
+            return
         s, r = _parse(sendbuf, False), _parse(recvbuf, True)
         self._hc.alltoall(_raw(s), r.arr)
 

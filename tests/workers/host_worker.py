@@ -156,6 +156,38 @@ for n in [p, 4 * p, 1000 * p]:
     C.myAlltoall(x, my)
     C.myAlltoall2(x, my2)
     expect(np.array_equal(lib, my) and np.array_equal(lib, my2), f"myAlltoall n={n}")
+# native schedules (p2p_algos.cpp) vs the Python reference schedules (taken for
+# non-contiguous inputs), in place, multi-dimensional
+for algo in ["reduce_bcast", "ring", "rhd"]:
+    salt += 1
+    x = inp(rank, 2 * 333, np.int64, salt).reshape(333, 2)
+    nat, ref = np.empty_like(x), np.empty_like(x)
+    C.myAllreduce(x, nat, op=MPI.SUM, algo=algo)                    # contiguous -> native
+    for c in range(2):
+        col = np.empty(333, np.int64)
+        C.myAllreduce(x[:, c], col, op=MPI.SUM, algo=algo)          # strided src -> Python schedule
+        ref[:, c] = col
+    expect(np.array_equal(nat, ref), f"myAllreduce native vs python {algo}")
+    inplace = x.copy()
+    C.myAllreduce(inplace, inplace, op=MPI.SUM, algo=algo)
+    expect(np.array_equal(inplace, nat), f"myAllreduce in place {algo}")
+x = (np.arange(6 * p, dtype=np.int32) + 100 * rank).reshape(p, 6)
+lib = np.empty_like(x)
+C.Alltoall(x, lib)
+for f in (C.myAlltoall, C.myAlltoall2):
+    y = x.copy()
+    f(y, y)
+    expect(np.array_equal(y, lib), f"{f.__name__} in place")
+# internal schedule tags never match a user ANY_TAG receive
+if p > 1:
+    box = np.zeros(1, np.int64)
+    req = comm.Irecv(box, source=(rank - 1) % p, tag=MPI.ANY_TAG)
+    C.myAllreduce(np.ones(4, np.int64), np.empty(4, np.int64), op=MPI.SUM)
+    C.myAlltoall(np.zeros(2 * p, np.int64), np.empty(2 * p, np.int64))
+    comm.Send(np.array([4242 + rank], np.int64), dest=(rank + 1) % p, tag=7)
+    st = MPI.Status()
+    req.Wait(st)
+    expect(box[0] == 4242 + (rank - 1) % p and st.Get_tag() == 7, "ANY_TAG isolation from internal tags")
 try:
     C.myAllreduce(np.ones(3), np.ones(3), op=MPI.BAND)
     expect(False, "myAllreduce must reject BAND on every rank")
