@@ -635,8 +635,13 @@ __device__ __forceinline__ int tn_off(int row, int byte) { return row * kTnRow +
 
 // FAST: 0 generic store_tile, 1 split-K atomics, 2 plain stores, 3 accumulating stores,
 // 4 split-K partial into a workspace slice (fp32 C, 16-B aligned, N2 % 4 == 0).
+// split_major = 1: logical id = split * tiles + tile, so after the XCD remap one XCD
+// runs every output tile of a few consecutive K slices: the K slice's rows of A
+// and B are fetched into that XCD's L2 once and shared by all its tiles (with
+// split-minor order each XCD streams whole K panels of its own few tiles, and
+// the same bytes cross the fabric once per tile).
 template <int FAST>
-__global__ void __launch_bounds__(NT) k_gemm_tn(GemmArgs g) {
+__global__ void __launch_bounds__(NT) k_gemm_tn(GemmArgs g, int split_major) {
   __shared__ __attribute__((aligned(16))) unsigned char smem[4 * kTnTile];
   // here: g.M = N1 (rows of C), g.N = N2 (cols of C), g.K = M (reduction)
   const int tiles_n = (g.N + BN - 1) / BN, tiles_m = (g.M + BM - 1) / BM;
@@ -646,8 +651,14 @@ __global__ void __launch_bounds__(NT) k_gemm_tn(GemmArgs g) {
     const int q = nwg / 8, r = nwg % 8, x = wg % 8;
     wg = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + wg / 8;
   }
-  const int split = wg % g.splitk;
-  wg /= g.splitk;
+  int split;
+  if (split_major) {
+    split = wg / (tiles_n * tiles_m);
+    wg %= tiles_n * tiles_m;
+  } else {
+    split = wg % g.splitk;
+    wg /= g.splitk;
+  }
   const int bm = (wg / tiles_n) * BM, bn = (wg % tiles_n) * BN;
   const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
   const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
@@ -1048,6 +1059,8 @@ void gemm_nt(uint64_t A, uint64_t B, uint64_t C, uint64_t bias, int M, int N, in
   CCMPI_HIP_CHECK(hipGetLastError());
 }
 
+int g_tn_split_major = std::getenv("CCMPI_TN_ORDER") ? std::atoi(std::getenv("CCMPI_TN_ORDER")) : 1;
+
 // C[N1,N2] (+)= alpha * A[M,N1]^T . B[M,N2]; fp32 output.
 void gemm_tn(uint64_t A, uint64_t B, uint64_t C, int M, int N1, int N2, int lda, int ldb, int ldc, float alpha,
              bool accumulate, int splitk, uint64_t stream, uint64_t workspace, int variant) {
@@ -1090,7 +1103,7 @@ void gemm_tn(uint64_t A, uint64_t B, uint64_t C, int M, int N1, int N2, int lda,
   auto st = reinterpret_cast<hipStream_t>(stream);
   switch (fast) {
     case 4: {
-      hipLaunchKernelGGL(k_gemm_tn<4>, dim3(nwg), dim3(NT), 0, st, g);
+      hipLaunchKernelGGL(k_gemm_tn<4>, dim3(nwg), dim3(NT), 0, st, g, g_tn_split_major);
       CCMPI_HIP_CHECK(hipGetLastError());
       const size_t work = (size_t)N1 * (N2 / 4);
       const int grid = (int)std::min<size_t>((work + 255) / 256, 4096);
@@ -1098,10 +1111,10 @@ void gemm_tn(uint64_t A, uint64_t B, uint64_t C, int M, int N1, int N2, int lda,
                          reinterpret_cast<float*>(C), ldc, N1, N2, accumulate ? 1 : 0);
       break;
     }
-    case 1: hipLaunchKernelGGL(k_gemm_tn<1>, dim3(nwg), dim3(NT), 0, st, g); break;
-    case 2: hipLaunchKernelGGL(k_gemm_tn<2>, dim3(nwg), dim3(NT), 0, st, g); break;
-    case 3: hipLaunchKernelGGL(k_gemm_tn<3>, dim3(nwg), dim3(NT), 0, st, g); break;
-    default: hipLaunchKernelGGL(k_gemm_tn<0>, dim3(nwg), dim3(NT), 0, st, g); break;
+    case 1: hipLaunchKernelGGL(k_gemm_tn<1>, dim3(nwg), dim3(NT), 0, st, g, g_tn_split_major); break;
+    case 2: hipLaunchKernelGGL(k_gemm_tn<2>, dim3(nwg), dim3(NT), 0, st, g, g_tn_split_major); break;
+    case 3: hipLaunchKernelGGL(k_gemm_tn<3>, dim3(nwg), dim3(NT), 0, st, g, g_tn_split_major); break;
+    default: hipLaunchKernelGGL(k_gemm_tn<0>, dim3(nwg), dim3(NT), 0, st, g, g_tn_split_major); break;
   }
   CCMPI_HIP_CHECK(hipGetLastError());
 }

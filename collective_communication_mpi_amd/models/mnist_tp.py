@@ -75,6 +75,7 @@ class LayerConfig:
     dp_algo: str = "auto"
     overlap: bool = True
     plain_gemm: str = "own"  # backward dH = dQKV . W_qkv: "own" (MFMA kernel, W^T kept by AdamW) | "hipblaslt"
+    emb_grad: str = "reassoc"  # "reassoc": dW_emb = W_qkv^T (dQKV^T Xp), no dH; "dh": materialize dH first
 
     @property
     def seq(self) -> int:
@@ -334,6 +335,10 @@ class MnistTPLayer:
         # ---- fused QKV projection (column-parallel)
         gemm_tn(dqkv, h, out=G("qkv_w"), accumulate=True)      # dW_qkv = dQKV^T . h
         self.buckets.ready(1)
+        if cfg.emb_grad == "reassoc":
+            self._emb_grad_reassoc(dqkv, xp)
+            self.buckets.ready(2)
+            return
         dh = self._buf("dh", (M, d), torch.bfloat16)            # TP-partial input gradient
         if cfg.plain_gemm == "hipblaslt":
             torch.matmul(dqkv, P16("qkv_w"), out=dh)            # library GEMM, weight in its stored layout
@@ -348,6 +353,28 @@ class MnistTPLayer:
         else:
             gemm_tn(dh, xp, out=G("emb_w"), accumulate=True)     # dW_emb = dH^T . [patches | 1 | onehot]
         self.buckets.ready(2)
+
+    def _emb_grad_reassoc(self, dqkv, xp) -> None:
+        """dW_emb = dH^T . Xp with dH = dQKV . W_qkv.  The embedding input takes no
+        gradient, so dH (tokens x d_model) is only ever contracted with Xp: compute
+        A = dQKV^T . Xp (3*hd x kp, reduction over the tokens, fp32) and then
+        dW_emb = W_qkv^T . A (d_model x kp).  Same gradient, contracted in the cheap
+        order: the dH GEMM (tokens x d x 3hd) and its 50 MB round trip disappear.
+        With TP > 1 each rank's product is its heads' partial sum, TP-all-reduced
+        exactly like the dH path's partial weight gradient."""
+        cfg = self.cfg
+        d = cfg.d_model
+        a = self._buf("a_emb", (3 * self.hd, cfg.kp), torch.float32)
+        gemm_tn(dqkv, xp, out=a)                                 # A = dQKV^T . Xp (MFMA, fp32 accumulate)
+        w = self.flat.param("qkv_w")                              # fp32 [3hd, d]
+        G = self.flat.grad
+        if self.tp_dev is not None:
+            gpart = self._buf("gemb", (d, cfg.kp), torch.float32, self.tp_dev)
+            torch.mm(w.t(), a, out=gpart)                         # plain 768x768x72 library GEMM
+            self.tp_dev.allreduce(gpart, gpart, "SUM")
+            G("emb_w").add_(gpart)
+        else:
+            G("emb_w").addmm_(w.t(), a)
 
     def _backward_naive_fc_o(self, dz, datt, B):
         """Reference backward collects: slice the output grad, local dX, reduce-scatter dX."""

@@ -1,0 +1,62 @@
+"""The DP x TP harness layer (single rank) against a plain PyTorch fp32 autograd
+reference of the same model: loss and every parameter gradient, for both ways
+of forming the embedding weight gradient (re-associated / through dH)."""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _reference(cfg, xp, y, P):
+    """fp32 autograd: patch embedding -> QKV -> softmax attention over the 16
+    patches -> mean over patches -> fc_o -> cross-entropy (mean over batch)."""
+    B = y.numel()
+    S, H, hd = cfg.seq, cfg.n_heads, cfg.head_dim
+    w = {k: v.detach().clone().requires_grad_(True) for k, v in P.items()}
+    h = xp @ w["emb_w"].t()
+    qkv = h @ w["qkv_w"].t() + w["qkv_b"]
+    q, k, v = qkv.split(H * hd, dim=1)
+    q, k, v = (t.reshape(B, S, H, hd).transpose(1, 2) for t in (q, k, v))
+    att = torch.softmax(q @ k.transpose(-1, -2) / math.sqrt(hd), dim=-1) @ v   # (B, H, S, hd)
+    pooled = att.transpose(1, 2).reshape(B, S, H * hd).mean(dim=1)
+    z = pooled @ w["o_w"].t() + w["o_b"]
+    loss = torch.nn.functional.cross_entropy(z[:, : cfg.n_classes], y.long())
+    loss.backward()
+    return loss.detach(), {k: t.grad for k, t in w.items()}
+
+
+@pytest.mark.parametrize("emb_grad", ["reassoc", "dh"])
+def test_harness_grads_match_torch_fp32(emb_grad):
+    from collective_communication_mpi_amd import MPI, Communicator
+    from collective_communication_mpi_amd.models.harness import build
+    from collective_communication_mpi_amd.models.mnist_tp import local_batch, patchify
+
+    comm = Communicator(MPI.COMM_WORLD)
+    cfg, layer, x_all, y_all = build(comm, 1, 128, emb_grad=emb_grad)
+    # non-trivial biases so their gradients and the bias epilogues are exercised
+    g = torch.Generator().manual_seed(7)
+    layer.flat.param("qkv_b").copy_(torch.randn(layer.flat.param("qkv_b").shape, generator=g) * 0.1)
+    ob = torch.zeros(cfg.out_pad)
+    ob[: cfg.n_classes] = torch.randn(cfg.n_classes, generator=g) * 0.1
+    layer.flat.param("o_b").copy_(ob)
+    layer.flat.refresh_bf16()
+    xb, yb = local_batch(cfg, x_all, y_all, 0, 0, layer.device)
+    xp = patchify(xb, cfg)
+    layer.forward(xp, cfg.batch)
+    layer.zero_grad()
+    loss = layer.loss_and_grad_fused(yb, cfg.batch)
+    layer.backward(None)
+    torch.cuda.synchronize()
+    names = ["emb_w", "qkv_w", "qkv_b", "o_w", "o_b"]
+    # the reference sees the same bf16-rounded weights the kernels multiply with
+    P = {k: layer.flat.param(k).detach().clone() for k in names}
+    for k in ("emb_w", "qkv_w", "o_w"):
+        P[k] = P[k].bfloat16().float()
+    ref_loss, ref = _reference(cfg, xp.float(), yb, P)
+    assert abs(loss.item() - ref_loss.item()) < 2e-2 * max(1.0, abs(ref_loss.item())), (loss.item(), ref_loss.item())
+    for k in names:
+        got = layer.flat.grad(k).detach().float()
+        err = (got - ref[k]).norm() / ref[k].norm().clamp_min(1e-12)
+        assert err < 4e-2, f"{emb_grad}: grad {k} rel err {err:.3e}"
