@@ -24,7 +24,7 @@ comm = Communicator(MPI.COMM_WORLD)
 torch.cuda.set_device(int(os.environ.get("CCMPI_LOCAL_RANK", "0")) % torch.cuda.device_count())
 cfg, layer, x_all, y_all = build(comm, args.tp, args.batch)
 xb, yb = local_batch(cfg, x_all, y_all, 0, comm.Get_rank(), layer.device)
-xp = patchify(xb, cfg)
+xp = patchify(xb, cfg, out=layer.input_buffer(cfg.batch))
 for _ in range(args.steps):
     if args.mode == "fwd":
         patchify(xb, cfg, out=xp)

@@ -369,9 +369,11 @@ __global__ void __launch_bounds__(256) k_adamw(AdamArgs a, TRegions tr, int flat
 // the patch pixels (p*p), a constant 1 (folds the embedding bias into the
 // GEMM) and a one-hot position (folds the learned position embedding into the
 // GEMM), zero-padded to kp.  One thread per 8-column chunk of a token row
-// (one 16-B store); kp % 8 == 0.
+// (one 16-B store); kp % 8 == 0.  Rows are ldo elements apart (ldo >= kp), so
+// the patches can be written as the right-hand column block of a wider
+// activation buffer ([h | xp], models/mnist_tp.py).
 __global__ void __launch_bounds__(256) k_patchify(const float* __restrict__ x, uint16_t* __restrict__ xp, int B, int img,
-                                                  int p, int kp) {
+                                                  int p, int kp, int ldo) {
   const int g = img / p, S = g * g, pp = p * p, nch = kp / 8;
   const uint64_t total = (uint64_t)B * S * nch;
   for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (uint64_t)gridDim.x * blockDim.x) {
@@ -393,18 +395,20 @@ __global__ void __launch_bounds__(256) k_patchify(const float* __restrict__ x, u
       }
       w[q] = f32_to_bf16_bits(v2[0]) | (f32_to_bf16_bits(v2[1]) << 16);
     }
-    *reinterpret_cast<uint4*>(xp + row * kp + ch * 8) = uint4{w[0], w[1], w[2], w[3]};
+    *reinterpret_cast<uint4*>(xp + row * ldo + ch * 8) = uint4{w[0], w[1], w[2], w[3]};
   }
 }
 
-void patchify(uint64_t x, uint64_t xp, int B, int img, int p, int kp, uint64_t stream) {
+void patchify(uint64_t x, uint64_t xp, int B, int img, int p, int kp, uint64_t stream, int ldo) {
   const int S = (img / p) * (img / p);
+  if (ldo <= 0) ldo = kp;
   if (kp < p * p + 1 + S) throw std::invalid_argument("patchify: kp too small for pixels + bias + position columns");
-  if (kp % 8 || xp % 16) throw std::invalid_argument("patchify: kp % 8 == 0 and a 16-B aligned output required");
+  if (kp % 8 || ldo % 8 || ldo < kp || xp % 16)
+    throw std::invalid_argument("patchify: kp % 8 == 0, ldo % 8 == 0, ldo >= kp and a 16-B aligned output required");
   const uint64_t total = (uint64_t)B * S * (kp / 8);
   const int grid = (int)std::min<uint64_t>((total + 255) / 256, 8192);
   hipLaunchKernelGGL(k_patchify, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const float*)x, (uint16_t*)xp, B, img,
-                     p, kp);
+                     p, kp, ldo);
   CCMPI_HIP_CHECK(hipGetLastError());
 }
 
@@ -472,7 +476,8 @@ void register_attn_ops(pybind11::module_& m) {
   m.def("cast_bf16", &cast_bf16, py::arg("x"), py::arg("y"), py::arg("n"), py::arg("stream"),
         py::arg("tregions") = std::vector<std::tuple<uint64_t, uint64_t, uint64_t, uint64_t>>{},
         py::call_guard<py::gil_scoped_release>());
-  m.def("patchify", &patchify, py::call_guard<py::gil_scoped_release>());
+  m.def("patchify", &patchify, py::arg("x"), py::arg("xp"), py::arg("B"), py::arg("img"), py::arg("p"), py::arg("kp"),
+        py::arg("stream"), py::arg("ldo") = 0, py::call_guard<py::gil_scoped_release>());
 }
 
 }  // namespace dev

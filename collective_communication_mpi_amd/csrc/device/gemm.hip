@@ -941,9 +941,13 @@ __global__ void __launch_bounds__(256) k_transpose16(const uint16_t* __restrict_
 }
 
 // Sum of the split-K workspace slices into C ([rows][cols] fp32, row stride ldc),
-// 4 columns per thread: C (+)= sum_s ws[s].
+// 4 columns per thread: C (+)= sum_s ws[s].  Columns >= csplit (a multiple of 4)
+// go to a second destination instead, C2[r][c - csplit] = sum (overwritten):
+// one GEMM over a row-concatenated operand [X | Y] yields A^T X accumulated
+// into one buffer and A^T Y into another, with no copy pass.
 __global__ void __launch_bounds__(256) k_splitk_reduce(const float* __restrict__ ws, int splitk, float* __restrict__ C,
-                                                       int ldc, int rows, int cols, int accumulate) {
+                                                       int ldc, int rows, int cols, int accumulate,
+                                                       float* __restrict__ C2, int ldc2, int csplit) {
   const size_t slice = (size_t)rows * cols;
   const int vc = cols / 4;
   for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < (size_t)rows * vc; e += (size_t)gridDim.x * blockDim.x) {
@@ -953,6 +957,10 @@ __global__ void __launch_bounds__(256) k_splitk_reduce(const float* __restrict__
     for (int k = 1; k < splitk; ++k) {
       const float4 v = *reinterpret_cast<const float4*>(src + k * slice);
       acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+    if (c >= csplit) {
+      *reinterpret_cast<float4*>(C2 + (size_t)r * ldc2 + (c - csplit)) = acc;
+      continue;
     }
     float4* dst = reinterpret_cast<float4*>(C + (size_t)r * ldc + c);
     if (accumulate) {
@@ -1063,8 +1071,15 @@ int g_tn_split_major = std::getenv("CCMPI_TN_ORDER") ? std::atoi(std::getenv("CC
 
 // C[N1,N2] (+)= alpha * A[M,N1]^T . B[M,N2]; fp32 output.
 void gemm_tn(uint64_t A, uint64_t B, uint64_t C, int M, int N1, int N2, int lda, int ldb, int ldc, float alpha,
-             bool accumulate, int splitk, uint64_t stream, uint64_t workspace, int variant) {
+             bool accumulate, int splitk, uint64_t stream, uint64_t workspace, int variant, uint64_t C2, int ldc2,
+             int csplit) {
   if (N1 <= 0 || N2 <= 0 || M <= 0) return;
+  if (csplit <= 0 || csplit >= N2) {
+    csplit = N2;  // no second destination
+  } else if (C2 == 0 || csplit % 4 || ldc2 % 4 || (C2 % 16) || splitk < 2 || workspace == 0) {
+    throw std::invalid_argument("ccmpi gemm_tn: a column-split output needs split-K with a workspace, "
+                                "csplit % 4 == 0 and a 16-B aligned second output");
+  }
   if (N1 % 8 || N2 % 8 || lda % 8 || ldb % 8 || (A % 16) || (B % 16))
     throw std::invalid_argument("ccmpi gemm_tn: N1, N2, lda, ldb must be multiples of 8 and A/B 16-B aligned");
   if (splitk < 1) splitk = 1;
@@ -1082,7 +1097,8 @@ void gemm_tn(uint64_t A, uint64_t B, uint64_t C, int M, int N1, int N2, int lda,
       const size_t work = (size_t)N1 * (N2 / 4);
       const int grid = (int)std::min<size_t>((work + 255) / 256, 4096);
       hipLaunchKernelGGL(k_splitk_reduce, dim3(grid), dim3(256), 0, st, reinterpret_cast<const float*>(workspace), splitk,
-                         reinterpret_cast<float*>(C), ldc, N1, N2, accumulate ? 1 : 0);
+                         reinterpret_cast<float*>(C), ldc, N1, N2, accumulate ? 1 : 0,
+                         reinterpret_cast<float*>(C2), ldc2, csplit);
       CCMPI_HIP_CHECK(hipGetLastError());
     }
     return;
@@ -1108,7 +1124,8 @@ void gemm_tn(uint64_t A, uint64_t B, uint64_t C, int M, int N1, int N2, int lda,
       const size_t work = (size_t)N1 * (N2 / 4);
       const int grid = (int)std::min<size_t>((work + 255) / 256, 4096);
       hipLaunchKernelGGL(k_splitk_reduce, dim3(grid), dim3(256), 0, st, reinterpret_cast<const float*>(workspace), splitk,
-                         reinterpret_cast<float*>(C), ldc, N1, N2, accumulate ? 1 : 0);
+                         reinterpret_cast<float*>(C), ldc, N1, N2, accumulate ? 1 : 0,
+                         reinterpret_cast<float*>(C2), ldc2, csplit);
       break;
     }
     case 1: hipLaunchKernelGGL(k_gemm_tn<1>, dim3(nwg), dim3(NT), 0, st, g, g_tn_split_major); break;
@@ -1140,7 +1157,8 @@ void register_gemm_ops(pybind11::module_& m) {
         pybind11::arg("A"), pybind11::arg("B"), pybind11::arg("C"), pybind11::arg("M"), pybind11::arg("N1"),
         pybind11::arg("N2"), pybind11::arg("lda"), pybind11::arg("ldb"), pybind11::arg("ldc"), pybind11::arg("alpha"),
         pybind11::arg("accumulate"), pybind11::arg("splitk"), pybind11::arg("stream"), pybind11::arg("workspace") = 0,
-        pybind11::arg("variant") = 0, pybind11::call_guard<pybind11::gil_scoped_release>());
+        pybind11::arg("variant") = 0, pybind11::arg("C2") = 0, pybind11::arg("ldc2") = 0, pybind11::arg("csplit") = 0,
+        pybind11::call_guard<pybind11::gil_scoped_release>());
   m.def("gemm_set_glds", [](bool on) { g_use_glds = on; }, "select LDS-DMA (True) or register staging");
   m.def("gemm_set_bk32", [](bool on) { g_bk32 = on; }, "128x128 kernel: BK = 32 (32 KiB LDS) or BK = 64");
   m.def("gemm_set_persistent", [](bool on, int grid) { g_persist = on; g_persist_grid = grid > 0 ? grid : 512; },

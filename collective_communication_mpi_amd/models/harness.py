@@ -42,7 +42,7 @@ def build(comm, tp: int, batch: int, **kw):
 
 
 def train_step(layer: MnistTPLayer, cfg: LayerConfig, xb, yb):
-    xp = patchify(xb, cfg)
+    xp = patchify(xb, cfg, out=layer.input_buffer(xb.shape[0]))
     logits = layer.forward(xp, xb.shape[0])
     layer.zero_grad()
     if cfg.fc_o_mode == "row" or cfg.tp == 1:
@@ -62,7 +62,7 @@ def bench_forward(comm, tp: int = 2, batch: int = 2048, steps: int = 20, warmup:
     rank = comm.Get_rank()
     cfg, layer, x_all, y_all = build(comm, tp, batch)
     xb, yb = local_batch(cfg, x_all, y_all, 0, rank, layer.device)
-    xp_static = patchify(xb, cfg)
+    xp_static = patchify(xb, cfg, out=layer.input_buffer(cfg.batch))
 
     def fwd():
         patchify(xb, cfg, out=xp_static)

@@ -100,9 +100,11 @@ def patchify(x: torch.Tensor, cfg: LayerConfig, out: Optional[torch.Tensor] = No
     B = x.shape[0]
     if out is None:
         out = torch.empty(B * cfg.seq, cfg.kp, dtype=torch.bfloat16, device=x.device)
+    if out.shape != (B * cfg.seq, cfg.kp) or out.stride(1) != 1:
+        raise ValueError("patchify: out must be [B*S, kp] with unit column stride")
     x = x.contiguous().float()
     _native.device().patchify(x.data_ptr(), out.data_ptr(), B, cfg.img, cfg.patch, cfg.kp,
-                              torch.cuda.current_stream(x.device).cuda_stream)
+                              torch.cuda.current_stream(x.device).cuda_stream, out.stride(0))
     return out
 
 
@@ -158,6 +160,11 @@ class MnistTPLayer:
                                    algo=cfg.dp_algo, overlap=cfg.overlap)
         self._load(full_init(cfg))
         self._bufs = {}
+        self._hx = None
+        # [h | xp] rows padded to a multiple of 64 elements (128 B): every row of h
+        # and of xp starts on a cache-line boundary (an 840-wide row costs the
+        # embedding and QKV GEMMs ~8 us in straddled lines)
+        self._hx_ld = (cfg.d_model + cfg.kp + 63) // 64 * 64
 
     # ------------------------------------------------------------- params
     def _load(self, w):
@@ -195,13 +202,26 @@ class MnistTPLayer:
         return b
 
     # ------------------------------------------------------------ forward
+    def input_buffer(self, B: int) -> torch.Tensor:
+        """Where patchify should write a batch of B images: the right-hand column
+        block of the activation buffer hx = [h | xp] (M x (d_model + kp) bf16).
+        With both the embedding output h and its input xp in one row, the
+        backward reads dQKV once for dQKV^T . [h | xp]: dW_qkv and the
+        embedding-gradient contraction A = dQKV^T . xp come out of one GEMM."""
+        cfg = self.cfg
+        hx = self._buf("hx", (B * cfg.seq, self._hx_ld), torch.bfloat16)
+        return hx[:, cfg.d_model:cfg.d_model + cfg.kp]
+
     def forward(self, xp: torch.Tensor, B: int) -> torch.Tensor:
-        """xp: (B*S, 64) bf16 patches -> logits (B, n_classes) fp32.  Saves activations."""
+        """xp: (B*S, kp) bf16 patches -> logits (B, n_classes) fp32.  Saves activations.
+        xp is either ``input_buffer(B)`` (fused [h | xp] layout) or any other tensor."""
         cfg = self.cfg
         S, d = cfg.seq, cfg.d_model
         M = B * S
         P16 = self.flat.param16
-        h = self._buf("h", (M, d), torch.bfloat16)
+        hx = self._bufs.get(("hx", (M, self._hx_ld), torch.bfloat16))
+        fused = hx is not None and xp.data_ptr() == hx.data_ptr() + 2 * d and xp.stride(0) == hx.stride(0)
+        h = hx[:, :d] if fused else self._buf("h", (M, d), torch.bfloat16)
         gemm_nt(xp, P16("emb_w"), out=h)  # bias + position are columns of W_emb
         qkv = self._buf("qkv", (M, 3 * self.hd), torch.bfloat16)
         gemm_nt(h, P16("qkv_w"), out=qkv, bias=self.flat.param("qkv_b"))
@@ -234,6 +254,7 @@ class MnistTPLayer:
         if naive:
             logits = logits + self.flat.param("o_b")[: cfg.n_classes]
         self._saved = (xp, h, qkv, att, lse, B, pool)
+        self._hx = hx[:, : d + cfg.kp] if fused else None
         return logits
 
     def _forward_naive_fc_o(self, att, B):
@@ -333,6 +354,15 @@ class MnistTPLayer:
                          self.hd if att is None else att.stride(0),
                          1.0 / math.sqrt(cfg.head_dim), dout_b, dout_r, st)  # + QKV bias grad in-kernel
         # ---- fused QKV projection (column-parallel)
+        if cfg.emb_grad == "reassoc" and self._hx is not None:
+            # one GEMM over the fused activation rows: dQKV^T . [h | xp]; the split-K
+            # reduction adds the h columns into dW_qkv and writes the xp columns to A
+            a = self._buf("a_emb", (3 * self.hd, cfg.kp), torch.float32)
+            gemm_tn(dqkv, self._hx, out=G("qkv_w"), accumulate=True, tail=a)
+            self.buckets.ready(1)
+            self._emb_grad_reassoc(dqkv, xp, a=a)
+            self.buckets.ready(2)
+            return
         gemm_tn(dqkv, h, out=G("qkv_w"), accumulate=True)      # dW_qkv = dQKV^T . h
         self.buckets.ready(1)
         if cfg.emb_grad == "reassoc":
@@ -354,7 +384,7 @@ class MnistTPLayer:
             gemm_tn(dh, xp, out=G("emb_w"), accumulate=True)     # dW_emb = dH^T . [patches | 1 | onehot]
         self.buckets.ready(2)
 
-    def _emb_grad_reassoc(self, dqkv, xp) -> None:
+    def _emb_grad_reassoc(self, dqkv, xp, a=None) -> None:
         """dW_emb = dH^T . Xp with dH = dQKV . W_qkv.  The embedding input takes no
         gradient, so dH (tokens x d_model) is only ever contracted with Xp: compute
         A = dQKV^T . Xp (3*hd x kp, reduction over the tokens, fp32) and then
@@ -364,8 +394,9 @@ class MnistTPLayer:
         exactly like the dH path's partial weight gradient."""
         cfg = self.cfg
         d = cfg.d_model
-        a = self._buf("a_emb", (3 * self.hd, cfg.kp), torch.float32)
-        gemm_tn(dqkv, xp, out=a)                                 # A = dQKV^T . Xp (MFMA, fp32 accumulate)
+        if a is None:
+            a = self._buf("a_emb", (3 * self.hd, cfg.kp), torch.float32)
+            gemm_tn(dqkv, xp, out=a)                             # A = dQKV^T . Xp (MFMA, fp32 accumulate)
         w = self.flat.param("qkv_w")                              # fp32 [3hd, d]
         G = self.flat.grad
         if self.tp_dev is not None:

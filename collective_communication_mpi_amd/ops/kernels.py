@@ -74,20 +74,35 @@ def gemm_nt(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None
 
 
 def gemm_tn(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None, alpha: float = 1.0,
-            accumulate: bool = False, splitk: Optional[int] = None) -> torch.Tensor:
+            accumulate: bool = False, splitk: Optional[int] = None, tail: Optional[torch.Tensor] = None) -> torch.Tensor:
     """``out[N1, N2] (+)= alpha * a[M, N1].T @ b[M, N2]`` (weight gradients dW = dY^T X) in fp32,
-    reading both operands M-major through ds_read_b64_tr_b16 (no transposes)."""
+    reading both operands M-major through ds_read_b64_tr_b16 (no transposes).
+
+    ``tail``: split the result by columns -- ``out`` (``[N1, c]``, accumulated if
+    ``accumulate``) receives columns ``< c`` and ``tail`` (``[N1, N2 - c]``,
+    overwritten) the rest, straight from the split-K reduction (one GEMM over a
+    row-concatenated operand ``b = [X | Y]`` gives ``a^T X`` and ``a^T Y``)."""
     if a.dtype != torch.bfloat16 or b.dtype != torch.bfloat16:
         raise TypeError("gemm_tn expects bf16 operands")
     if a.dim() != 2 or b.dim() != 2 or a.shape[0] != b.shape[0] or a.stride(1) != 1 or b.stride(1) != 1:
         raise ValueError(f"gemm_tn shape mismatch: {tuple(a.shape)}^T x {tuple(b.shape)}")
     M, N1 = a.shape
     N2 = b.shape[1]
-    if out is None:
+    csplit = 0
+    if tail is not None:
+        if out is None:
+            raise ValueError("gemm_tn: tail needs an explicit out")
+        csplit = out.shape[1]
+        if (tail.dtype != torch.float32 or tail.shape != (N1, N2 - csplit) or tail.stride(1) != 1
+                or csplit % 4 or tail.stride(0) % 4 or tail.data_ptr() % 16):
+            raise ValueError("gemm_tn tail must be fp32 [N1, N2 - out cols], 16-B aligned rows, out cols % 4 == 0")
+        if out.dtype != torch.float32 or out.shape[0] != N1 or out.stride(1) != 1:
+            raise ValueError("gemm_tn output must be fp32 [N1, c] with unit column stride")
+    elif out is None:
         if accumulate:
             raise ValueError("accumulate needs an output tensor")
         out = torch.empty((N1, N2), dtype=torch.float32, device=a.device)
-    if out.dtype != torch.float32 or out.shape != (N1, N2) or out.stride(1) != 1:
+    if tail is None and (out.dtype != torch.float32 or out.shape != (N1, N2) or out.stride(1) != 1):
         raise ValueError("gemm_tn output must be fp32 [N1, N2] with unit column stride")
     # variant 1 (256x256 ping-pong TN) is opt-in: measured slower than the 128x128 TN kernel on
     # every shape tried (benchmarks/gemm_tn_splitk.py, profiles/r1_gemm_fastepi/tn_variants.txt)
@@ -100,13 +115,16 @@ def gemm_tn(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None
             splitk = int(max(1, min(256 // max(tiles, 1), M // 256, 64)))
         else:
             splitk = _auto_splitk(((N1 + 127) // 128) * ((N2 + 127) // 128), M)
+    if tail is not None:
+        splitk = max(2, splitk)  # the column split happens in the split-K reduction
     ws = 0
     # large outputs: partials in a workspace + one reduction pass instead of fp32 atomics
     # (dW_qkv 768x768: 80 -> 68 us); small outputs keep the atomics (one launch fewer)
-    if splitk > 1 and N2 % 4 == 0 and (variant == 1 or N1 * N2 >= (1 << 18)):
+    if splitk > 1 and N2 % 4 == 0 and (variant == 1 or N1 * N2 >= (1 << 18) or tail is not None):
         ws = torch.empty(splitk * N1 * N2, dtype=torch.float32, device=a.device).data_ptr()
     _D().gemm_tn(a.data_ptr(), b.data_ptr(), out.data_ptr(), M, N1, N2, a.stride(0), b.stride(0), out.stride(0),
-                 float(alpha), bool(accumulate), int(splitk), _stream(a), ws, int(variant))
+                 float(alpha), bool(accumulate), int(splitk), _stream(a), ws, int(variant),
+                 0 if tail is None else tail.data_ptr(), 0 if tail is None else tail.stride(0), csplit)
     return out
 
 

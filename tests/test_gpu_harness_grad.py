@@ -27,8 +27,8 @@ def _reference(cfg, xp, y, P):
     return loss.detach(), {k: t.grad for k, t in w.items()}
 
 
-@pytest.mark.parametrize("emb_grad", ["reassoc", "dh"])
-def test_harness_grads_match_torch_fp32(emb_grad):
+@pytest.mark.parametrize("emb_grad,fused", [("reassoc", True), ("reassoc", False), ("dh", True), ("dh", False)])
+def test_harness_grads_match_torch_fp32(emb_grad, fused):
     from collective_communication_mpi_amd import MPI, Communicator
     from collective_communication_mpi_amd.models.harness import build
     from collective_communication_mpi_amd.models.mnist_tp import local_batch, patchify
@@ -43,7 +43,7 @@ def test_harness_grads_match_torch_fp32(emb_grad):
     layer.flat.param("o_b").copy_(ob)
     layer.flat.refresh_bf16()
     xb, yb = local_batch(cfg, x_all, y_all, 0, 0, layer.device)
-    xp = patchify(xb, cfg)
+    xp = patchify(xb, cfg, out=layer.input_buffer(cfg.batch) if fused else None)
     layer.forward(xp, cfg.batch)
     layer.zero_grad()
     loss = layer.loss_and_grad_fused(yb, cfg.batch)

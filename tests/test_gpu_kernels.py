@@ -225,6 +225,26 @@ def test_gemm_tn_weight_grad(M, N1, N2, splitk):
     torch.testing.assert_close(acc, 1 + 0.5 * ref, rtol=2e-3, atol=2e-3 * M ** 0.5)
 
 
+@pytest.mark.parametrize("M,N1,c,N2,ldb", [(32768, 768, 768, 840, 896), (4096, 256, 128, 200, 264),
+                                            (1000, 136, 64, 72, 72)])
+def test_gemm_tn_column_split(M, N1, c, N2, ldb):
+    """gemm_tn(tail=...): columns < c accumulate into out, the rest overwrite tail,
+    with b a column window of a wider (padded) row buffer."""
+    from collective_communication_mpi_amd.ops import gemm_tn
+
+    g = torch.Generator(device="cuda").manual_seed(M + c)
+    a = torch.randn(M, N1, device="cuda", generator=g).bfloat16()
+    wide = torch.randn(M, ldb, device="cuda", generator=g).bfloat16()
+    b = wide[:, :N2]
+    ref = a.float().T @ b.float()
+    out = torch.full((N1, c), 2.0, device="cuda")
+    tail = torch.full((N1, N2 - c), 7.0, device="cuda")
+    gemm_tn(a, b, out=out, accumulate=True, tail=tail)
+    tol = dict(rtol=2e-3, atol=2e-3 * M ** 0.5)
+    torch.testing.assert_close(out, 2 + ref[:, :c], **tol)
+    torch.testing.assert_close(tail, ref[:, c:], **tol)
+
+
 def test_gemm_tn_asymmetric():
     """A^T with A = I and asymmetric B catches row/column swaps in the tr-read path."""
     from collective_communication_mpi_amd.ops import gemm_tn
