@@ -1,0 +1,181 @@
+"""Data-parallel gradient synchronisation for any torch model: gradients live in
+flat, byte-capped buckets and each bucket is all-reduced as soon as autograd has
+produced all of its gradients, on a communication stream that overlaps the rest
+of the backward pass.
+
+The reference only shards the data (data_parallel_preprocess.py:45-59) and
+builds ``dp_comm`` (func_impl.py:61-62).  ``DistributedDataParallel`` adds the
+gradient all-reduce on that DP communicator:
+
+* buckets are filled in reverse parameter-registration order (roughly the order
+  backward produces gradients) up to ``bucket_bytes`` each; xGMI is
+  point-to-point, so a bucket must be large enough to keep all 7 links busy
+  (default 64 MiB: ~9 MiB per link in flight at 8 ranks) and small enough that
+  the first all-reduce starts early in the backward;
+* every parameter's ``.grad`` is a view into its bucket (allocated from the DP
+  device group's symmetric heap on the GPU, so the hand-written two-shot
+  kernel runs zero-copy), so autograd accumulates straight into the buckets;
+* a post-accumulate-grad hook counts a bucket's ready gradients; the last one
+  records an event on the compute stream and launches the bucket's all-reduce
+  on a high-priority side stream (its workgroups are dispatched ahead of the
+  backward GEMM tiles queued behind them);
+* ``finish()`` (call after ``backward()``, before the optimizer) launches
+  buckets whose parameters got no gradient, joins the side stream and applies
+  the 1/dp average.
+
+CPU tensors are reduced by the C++ host plane (the reference's CPU setting).
+"""
+from __future__ import annotations
+
+from typing import Dict, List
+
+import torch
+
+from .layout import _host_comm, device_group_for
+
+
+class _Bucket:
+    __slots__ = ("params", "buf", "pending", "launched", "event")
+
+    def __init__(self, params, buf):
+        self.params = params
+        self.buf = buf
+        self.pending = len(params)
+        self.launched = False
+        self.event = None
+
+
+class DistributedDataParallel(torch.nn.Module):
+    """Wraps ``module``; ``comm`` is the DP communicator (Communicator or host Comm)."""
+
+    def __init__(self, module: torch.nn.Module, comm, bucket_bytes: int = 64 << 20, algo: str = "auto",
+                 average: bool = True, overlap: bool = True, broadcast_params: bool = True):
+        super().__init__()
+        self.module = module
+        self.comm = comm
+        self.hc = _host_comm(comm)
+        self.p = self.hc.Get_size()
+        self.algo = algo
+        self.average = average
+        params = [q for q in module.parameters() if q.requires_grad]
+        if not params:
+            raise ValueError("DistributedDataParallel: the module has no trainable parameters")
+        dev = params[0].device
+        self.device = dev
+        self.dev = device_group_for(comm) if dev.type == "cuda" and self.p > 1 else None
+        if broadcast_params and self.p > 1:
+            self._broadcast_params(params)
+        # ---- buckets: reverse registration order, <= bucket_bytes, one dtype each
+        self.buckets: List[_Bucket] = []
+        self._view_of: Dict[int, torch.Tensor] = {}
+        cur: List[torch.nn.Parameter] = []
+        cur_bytes = 0
+        for q in reversed(params):
+            nb = q.numel() * q.element_size()
+            if cur and (cur_bytes + nb > bucket_bytes or q.dtype != cur[0].dtype):
+                self._make_bucket(cur)
+                cur, cur_bytes = [], 0
+            cur.append(q)
+            cur_bytes += nb
+        if cur:
+            self._make_bucket(cur)
+        self._bucket_of: Dict[int, _Bucket] = {id(q): b for b in self.buckets for q in b.params}
+        self.stream = (torch.cuda.Stream(device=dev, priority=-1)
+                       if (dev.type == "cuda" and overlap and self.p > 1) else None)
+        self._hooks = [q.register_post_accumulate_grad_hook(self._on_grad) for q in params]
+
+    # ------------------------------------------------------------------ setup
+    def _broadcast_params(self, params) -> None:
+        """Rank 0's parameters everywhere (the replicas start identical)."""
+        with torch.no_grad():
+            for q in params:
+                if q.is_cuda:
+                    t = q.data.contiguous()
+                    self.dev.bcast(t, 0)
+                    if t.data_ptr() != q.data.data_ptr():
+                        q.data.copy_(t)
+                else:
+                    q.data.copy_(torch.as_tensor(self.hc.bcast(q.data.numpy() if self.hc.Get_rank() == 0 else None)))
+
+    def _make_bucket(self, params) -> None:
+        n = sum(q.numel() for q in params)
+        dt = params[0].dtype
+        if self.dev is not None:
+            buf = self.dev.empty(n, dt)   # symmetric heap: zero-copy device collectives
+            buf.zero_()
+        else:
+            buf = torch.zeros(n, dtype=dt, device=params[0].device)
+        off = 0
+        for q in params:
+            q.grad = buf[off:off + q.numel()].view_as(q)
+            self._view_of[id(q)] = q.grad
+            off += q.numel()
+        self.buckets.append(_Bucket(params, buf))
+
+    # --------------------------------------------------------------- forward
+    def forward(self, *args, **kwargs):
+        return self.module(*args, **kwargs)
+
+    # --------------------------------------------------------------- backward
+    def _on_grad(self, q) -> None:
+        v = self._view_of[id(q)]
+        if q.grad is not v and q.grad.data_ptr() != v.data_ptr():
+            # the user dropped the grad (zero_grad(set_to_none=True)): autograd made a
+            # fresh tensor -- move it into the bucket and re-attach the view
+            v.copy_(q.grad)
+            q.grad = v
+        b = self._bucket_of[id(q)]
+        b.pending -= 1
+        if b.pending == 0:
+            self._launch(b)
+
+    def _launch(self, b: _Bucket) -> None:
+        if b.launched or self.p == 1:
+            b.launched = True
+            return
+        b.launched = True
+        if self.dev is None:  # host plane
+            from .. import mpi as MPI
+
+            self.hc.Allreduce(MPI.IN_PLACE, b.buf.numpy(), op=MPI.SUM)
+            return
+        if self.stream is None:
+            self.dev.allreduce(b.buf, b.buf, "SUM", self.algo)
+            return
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.device))
+        self.stream.wait_event(ev)
+        with torch.cuda.stream(self.stream):
+            self.dev.allreduce(b.buf, b.buf, "SUM", self.algo)
+
+    def finish(self) -> None:
+        """Complete the gradient synchronisation (after backward, before the step)."""
+        for b in self.buckets:  # parameters that received no gradient this step
+            if not b.launched:
+                self._launch(b)
+        if self.stream is not None:
+            torch.cuda.current_stream(self.device).wait_stream(self.stream)
+        if self.average and self.p > 1:
+            for b in self.buckets:
+                b.buf.mul_(1.0 / self.p)
+        for b in self.buckets:
+            b.pending = len(b.params)
+            b.launched = False
+
+    def zero_grad(self, set_to_none: bool = False) -> None:
+        """Zero the buckets and re-attach every ``.grad`` view (``set_to_none`` is ignored)."""
+        for b in self.buckets:
+            b.buf.zero_()
+            for q in b.params:
+                q.grad = self._view_of[id(q)]
+
+    @property
+    def bucket_sizes(self) -> List[int]:
+        return [b.buf.numel() * b.buf.element_size() for b in self.buckets]
+
+
+def ddp_wrap(module: torch.nn.Module, comm, **kw) -> DistributedDataParallel:
+    return DistributedDataParallel(module, comm, **kw)
+
+
+__all__ = ["DistributedDataParallel", "ddp_wrap"]

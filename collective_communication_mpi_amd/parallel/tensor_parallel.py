@@ -1,0 +1,272 @@
+"""Megatron-style tensor-parallel layers for any torch model, on this framework's
+collectives.
+
+The reference splits ``fc_q/k/v`` by output features and ``fc_o`` by input
+features (model/func_impl.py:65-70) and moves activations with its naive
+collects (:76-187).  These autograd-aware modules generalise that to any
+``torch.nn.Module``:
+
+* ``ColumnParallelLinear`` -- weight rows (output features) sharded over the TP
+  group; the input is replicated (backward: TP all-reduce of dX, Megatron's
+  "f"); optional ``gather_output`` = the reference's forward all-gather
+  (``naive_collect_forward_output``; backward = the local slice,
+  ``naive_collect_backward_output``).
+* ``RowParallelLinear`` -- weight columns (input features) sharded; the
+  sharded input gives a partial output summed by ONE TP all-reduce (Megatron's
+  "g", forward) instead of the reference's two all-gathers; with
+  ``input_is_parallel=False`` the input is split here (backward: all-gather).
+
+Collectives run on the tensors' plane: CUDA tensors use the device plane
+(hand-written xGMI kernels, ``device_group_for``), CPU tensors the C++ host
+plane -- the reference's own CPU/NumPy setting.  CUDA bf16 GEMMs run on the
+MFMA kernels (``ops.gemm_nt`` forward / input gradient, ``ops.gemm_tn``
+weight gradient, fp32 accumulation); other dtypes use ``torch.matmul``.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from ..ops import gemm_nt, gemm_tn, transpose
+from .layout import _host_comm, device_group_for
+
+
+def _size_rank(comm):
+    hc = _host_comm(comm)
+    return hc.Get_size(), hc.Get_rank()
+
+
+def all_reduce_(t: torch.Tensor, comm) -> torch.Tensor:
+    """In-place SUM over ``comm`` of a contiguous tensor (device or host plane)."""
+    p, _ = _size_rank(comm)
+    if p == 1:
+        return t
+    if not t.is_contiguous():
+        raise ValueError("all_reduce_ needs a contiguous tensor")
+    if t.is_cuda:
+        device_group_for(comm).allreduce(t, t, "SUM")
+    else:
+        from .. import mpi as MPI
+
+        _host_comm(comm).Allreduce(MPI.IN_PLACE, t.detach().numpy(), op=MPI.SUM)
+    return t
+
+
+def _gather_last(x: torch.Tensor, comm) -> torch.Tensor:
+    p, _ = _size_rank(comm)
+    if p == 1:
+        return x
+    from .layout import _dev_allgather_lastaxis, _host_allgather_lastaxis
+
+    if x.is_cuda:
+        return _dev_allgather_lastaxis(x, comm, p)
+    lead = x.shape[:-1]
+    x3 = x.detach().contiguous().reshape(1, -1, x.shape[-1]).numpy()
+    out = _host_allgather_lastaxis(x3, comm)
+    return torch.from_numpy(out).reshape(*lead, out.shape[-1])
+
+
+def _slice_last(x: torch.Tensor, comm) -> torch.Tensor:
+    p, r = _size_rank(comm)
+    if p == 1:
+        return x
+    k = x.shape[-1] // p
+    return x[..., r * k:(r + 1) * k].contiguous()
+
+
+class _CopyToTP(torch.autograd.Function):
+    """Identity forward, TP all-reduce of the gradient (Megatron "f")."""
+
+    @staticmethod
+    def forward(ctx, x, comm):
+        ctx.comm = comm
+        return x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        return all_reduce_(g.contiguous().clone(), ctx.comm), None
+
+
+class _ReduceFromTP(torch.autograd.Function):
+    """TP all-reduce forward, identity backward (Megatron "g")."""
+
+    @staticmethod
+    def forward(ctx, x, comm):
+        return all_reduce_(x.contiguous().clone(), comm)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g, None
+
+
+class _GatherLastTP(torch.autograd.Function):
+    """Last-axis all-gather forward (reference naive_collect_forward_*), own-slice backward
+    (reference naive_collect_backward_output)."""
+
+    @staticmethod
+    def forward(ctx, x, comm):
+        ctx.comm = comm
+        return _gather_last(x, comm)
+
+    @staticmethod
+    def backward(ctx, g):
+        return _slice_last(g, ctx.comm), None
+
+
+class _ScatterLastTP(torch.autograd.Function):
+    """Own last-axis slice forward, all-gather backward."""
+
+    @staticmethod
+    def forward(ctx, x, comm):
+        ctx.comm = comm
+        return _slice_last(x, comm)
+
+    @staticmethod
+    def backward(ctx, g):
+        return _gather_last(g.contiguous(), ctx.comm), None
+
+
+def copy_to_tensor_parallel_region(x, comm):
+    return _CopyToTP.apply(x, comm)
+
+
+def reduce_from_tensor_parallel_region(x, comm):
+    return _ReduceFromTP.apply(x, comm)
+
+
+def gather_from_tensor_parallel_region(x, comm):
+    return _GatherLastTP.apply(x, comm)
+
+
+def scatter_to_tensor_parallel_region(x, comm):
+    return _ScatterLastTP.apply(x, comm)
+
+
+def _mfma_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
+    return (x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16
+            and x.shape[-1] % 8 == 0 and w.shape[0] % 8 == 0 and w.shape[1] % 8 == 0)
+
+
+class _LinearFn(torch.autograd.Function):
+    """y = x W^T (+ b): MFMA bf16 kernels on CUDA bf16, torch.matmul otherwise."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        x2 = x.reshape(-1, x.shape[-1])
+        if not x2.is_contiguous():
+            x2 = x2.contiguous()
+        ctx.save_for_backward(x2, w)
+        ctx.has_bias = b is not None
+        ctx.lead = x.shape[:-1]
+        if _mfma_ok(x2, w):
+            y = gemm_nt(x2, w, bias=b)
+        else:
+            y = x2 @ w.t()
+            if b is not None:
+                y = y + b
+        return y.reshape(*x.shape[:-1], w.shape[0])
+
+    @staticmethod
+    def backward(ctx, g):
+        x2, w = ctx.saved_tensors
+        g2 = g.reshape(-1, g.shape[-1]).contiguous()
+        dx = dw = db = None
+        if _mfma_ok(x2, w) and g2.dtype == torch.bfloat16:
+            if ctx.needs_input_grad[0]:
+                dx = gemm_nt(g2, transpose(w))                      # dX = dY . W
+            if ctx.needs_input_grad[1]:
+                dw = gemm_tn(g2, x2).to(w.dtype)                    # dW = dY^T . X (fp32 accumulate)
+        else:
+            if ctx.needs_input_grad[0]:
+                dx = g2 @ w
+            if ctx.needs_input_grad[1]:
+                dw = g2.t() @ x2
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            db = g2.float().sum(0).to(g.dtype)
+        if dx is not None:
+            dx = dx.reshape(*ctx.lead, w.shape[1])
+        return dx, dw, db
+
+
+def _init_full(out_f: int, in_f: int, seed: int, dtype, bias: bool):
+    """Full (unsharded) weights from a seeded CPU generator: identical on every rank."""
+    gen = torch.Generator().manual_seed(seed)
+    bound = 1.0 / math.sqrt(in_f)
+    w = (torch.rand(out_f, in_f, generator=gen) * 2 - 1) * bound
+    b = (torch.rand(out_f, generator=gen) * 2 - 1) * bound if bias else None
+    return w.to(dtype), (b.to(dtype) if b is not None else None)
+
+
+class ColumnParallelLinear(torch.nn.Module):
+    """``y = x W^T + b`` with W's rows (output features) sharded over ``comm`` (TP group).
+
+    ``gather_output=False`` returns this rank's ``out_features / p`` columns
+    (feed a ``RowParallelLinear``); ``True`` all-gathers the full output."""
+
+    def __init__(self, in_features: int, out_features: int, comm, bias: bool = True, gather_output: bool = False,
+                 device=None, dtype=torch.float32, seed: int = 0):
+        super().__init__()
+        p, r = _size_rank(comm)
+        if out_features % p:
+            raise ValueError(f"out_features {out_features} not divisible by TP size {p}")
+        self.comm, self.p, self.r = comm, p, r
+        self.in_features, self.out_features = in_features, out_features
+        self.gather_output = gather_output
+        k = out_features // p
+        w, b = _init_full(out_features, in_features, seed, dtype, bias)
+        self.weight = torch.nn.Parameter(w[r * k:(r + 1) * k].contiguous().to(device))
+        self.bias = torch.nn.Parameter(b[r * k:(r + 1) * k].contiguous().to(device)) if bias else None
+
+    def forward(self, x):
+        x = copy_to_tensor_parallel_region(x, self.comm)
+        y = _LinearFn.apply(x, self.weight, self.bias)
+        return gather_from_tensor_parallel_region(y, self.comm) if self.gather_output else y
+
+
+class RowParallelLinear(torch.nn.Module):
+    """``y = x W^T + b`` with W's columns (input features) sharded over ``comm``.
+
+    The partial products are summed by one TP all-reduce; the bias is added once,
+    after the reduction.  ``input_is_parallel=False`` splits a full input here."""
+
+    def __init__(self, in_features: int, out_features: int, comm, bias: bool = True, input_is_parallel: bool = True,
+                 device=None, dtype=torch.float32, seed: int = 0):
+        super().__init__()
+        p, r = _size_rank(comm)
+        if in_features % p:
+            raise ValueError(f"in_features {in_features} not divisible by TP size {p}")
+        self.comm, self.p, self.r = comm, p, r
+        self.in_features, self.out_features = in_features, out_features
+        self.input_is_parallel = input_is_parallel
+        k = in_features // p
+        w, b = _init_full(out_features, in_features, seed, dtype, bias)
+        self.weight = torch.nn.Parameter(w[:, r * k:(r + 1) * k].contiguous().to(device))
+        self.bias = torch.nn.Parameter(b.to(device)) if bias else None
+
+    def forward(self, x):
+        if not self.input_is_parallel:
+            x = scatter_to_tensor_parallel_region(x, self.comm)
+        y = reduce_from_tensor_parallel_region(_LinearFn.apply(x, self.weight, None), self.comm)
+        return y + self.bias if self.bias is not None else y
+
+
+def full_weight(layer, comm) -> torch.Tensor:
+    """Reassemble the unsharded weight of a Column/RowParallelLinear (collective)."""
+    w = layer.weight.detach()
+    dim = 0 if isinstance(layer, ColumnParallelLinear) else 1
+    parts = _host_comm(comm).allgather(w.float().cpu())
+    return torch.cat(parts, dim=dim)
+
+
+def sharded_grad_full(layer, comm) -> torch.Tensor:
+    """Reassemble the unsharded weight gradient (collective), for checks."""
+    g = layer.weight.grad.detach()
+    dim = 0 if isinstance(layer, ColumnParallelLinear) else 1
+    parts = _host_comm(comm).allgather(g.float().cpu())
+    return torch.cat(parts, dim=dim)
+
+
+__all__ = ["ColumnParallelLinear", "RowParallelLinear", "all_reduce_", "copy_to_tensor_parallel_region",
+           "reduce_from_tensor_parallel_region", "gather_from_tensor_parallel_region",
+           "scatter_to_tensor_parallel_region", "full_weight", "sharded_grad_full"]

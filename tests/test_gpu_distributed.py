@@ -65,3 +65,11 @@ def test_harness_checkpoint_resume(tmp_path):
     la, lc = np.load(a), np.load(c)
     assert lc.shape == (3,)
     np.testing.assert_allclose(lc, la[3:], rtol=2e-3, atol=1e-4)
+
+
+@pytest.mark.parametrize("n", [2, 4])
+def test_tensor_parallel_layers_and_ddp_gpu(n):
+    """Column/RowParallelLinear (MFMA bf16 GEMMs, device TP collectives) + bucketed DDP
+    on the device plane vs a single-process fp32 reference (tests/workers/tp_ddp_worker.py)."""
+    r = run_ranks(n, py("tests/workers/tp_ddp_worker.py", "--device", "cuda"), timeout=300, env=ENV)
+    assert "tp/ddp OK" in r.stdout

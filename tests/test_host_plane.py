@@ -99,3 +99,11 @@ def test_runs_under_torchrun():
                        cwd=REPO, env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     assert "host plane OK at 4 ranks" in r.stdout
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 4, 8])
+def test_tensor_parallel_layers_and_ddp_cpu(n):
+    """Column/RowParallelLinear + bucketed DistributedDataParallel on the host plane
+    (CPU tensors) vs a single-process fp32 reference, over the mp-major grid."""
+    r = run_ranks(n, py("tests/workers/tp_ddp_worker.py", "--device", "cpu"), timeout=300)
+    assert "tp/ddp OK" in r.stdout
