@@ -22,6 +22,17 @@ struct AttnArgs {
   int ld_pool;
   int dout_bstride;     // bwd: dO row (b, i) at dout + b*dout_bstride + i*dout_rstride + h*D
   int dout_rstride;     //      (rstride 0 = the pooled-gradient broadcast over the S rows)
+  // Pooled row-parallel fc_o fused into the MFMA kernels (optional; Hl must divide
+  // the 4 waves of a workgroup, n_out <= 16).  W_o is [n_out][ld_wo] bf16 whose
+  // columns are this rank's attention features (h*D + d).
+  const uint16_t* wo;
+  int ld_wo, n_out;
+  float* zp;            // fwd: zp[b][0..n_out) = pool[b] . W_o^T (+ bo), fp32, row stride ld_zp
+  int ld_zp;
+  const float* bo;      // fwd: optional output bias [n_out]
+  const uint16_t* dz;   // bwd: dO rows of sequence b = dz_scale * (dz[b] . W_o), broadcast over the S
+  int ld_dz;            //      rows (replaces dout; dz is [B][ld_dz] bf16)
+  float dz_scale;
 };
 
 // MFMA path (attn_mfma.hip): S <= 16, D in {32, 64, 128}, 16-B aligned rows.

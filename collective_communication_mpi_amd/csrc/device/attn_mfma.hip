@@ -101,11 +101,33 @@ __global__ void __launch_bounds__(256) k_attn16_fwd(AttnArgs a) {
   constexpr int LD = D + 8, NK = D / 32, NT = D / 16;
   __shared__ __attribute__((aligned(16))) uint16_t vt[WPB][16 * LD];
   __shared__ __attribute__((aligned(16))) uint16_t ot[WPB][16 * LD];
+  __shared__ float zpart[2][WPB][16];  // fused fc_o: per-wave (= per-head) partial logits, double-buffered
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
   const int S = a.S, HD = a.Hl * D, npairs = a.B * a.Hl;
   uint16_t* V = vt[wave];
   uint16_t* O = ot[wave];
-  for (int pr = blockIdx.x * WPB + wave; pr < npairs; pr += gridDim.x * WPB) {
+  // workgroup-uniform trip count (the fused fc_o reduces across the waves of an iteration);
+  // with Hl | WPB the Hl heads of a sequence are consecutive waves of one workgroup
+  // fused fc_o: with Hl | WPB this wave always serves head h = wave % Hl, so its W_o
+  // entries (classes 4g..4g+3, features 16nt + c) are loaded once, packed as bf16 pairs
+  uint32_t wpk[NT][2];
+  if (a.zp) {
+    const int hw = wave % a.Hl;
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        uint32_t lo = 0, hi = 0;
+        const uint16_t* w = a.wo + (size_t)(4 * g + 2 * q) * a.ld_wo + hw * D + 16 * nt + c;
+        if (4 * g + 2 * q < a.n_out) lo = w[0];
+        if (4 * g + 2 * q + 1 < a.n_out) hi = w[a.ld_wo];
+        wpk[nt][q] = lo | (hi << 16);
+      }
+  }
+  int it = 0;
+  for (int base = blockIdx.x * WPB; base < npairs; base += gridDim.x * WPB, it ^= 1) {
+   const int pr = base + wave;
+   if (pr < npairs) {
     const int b = pr / a.Hl, h = pr % a.Hl;
     const uint16_t* qb = a.qkv + (size_t)b * S * a.ld_qkv + h * D;
     bf16x8 qr[NK], kr[NK], vr[NK];
@@ -144,6 +166,10 @@ __global__ void __launch_bounds__(256) k_attn16_fwd(AttnArgs a) {
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) o[nt] = mma16(pa, tile_b<LD>(V, g, 16 * nt + c), f4{0.f, 0.f, 0.f, 0.f});
     if (a.pool) {
+      // pooled features 16nt + c; with the fused fc_o each one is folded into this head's
+      // share of the logits right away (lane (c, g) takes classes 4g..4g+3), keeping few
+      // registers live
+      float zacc[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) {
         float cs = 0.f;
@@ -151,15 +177,44 @@ __global__ void __launch_bounds__(256) k_attn16_fwd(AttnArgs a) {
         for (int r = 0; r < 4; ++r) cs += (4 * g + r < S) ? o[nt][r] : 0.f;
         cs += __shfl_xor(cs, 16);
         cs += __shfl_xor(cs, 32);
-        if (g == 0) a.pool[(size_t)b * a.ld_pool + h * D + 16 * nt + c] = (uint16_t)f32_to_bf16_bits(cs / (float)S);
+        const uint32_t pb = f32_to_bf16_bits(cs / (float)S);
+        if (g == 0) a.pool[(size_t)b * a.ld_pool + h * D + 16 * nt + c] = (uint16_t)pb;
+        if (a.zp) {
+          const float pv = __uint_as_float(pb << 16);  // the bf16 value a separate fc_o GEMM would read
+#pragma unroll
+          for (int q = 0; q < 2; ++q) {
+            zacc[2 * q] += pv * bf16_lo(wpk[nt][q]);
+            zacc[2 * q + 1] += pv * bf16_hi(wpk[nt][q]);
+          }
+        }
+      }
+      if (a.zp) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          float acc = zacc[j];
+#pragma unroll
+          for (int off = 1; off < 16; off <<= 1) acc += __shfl_xor(acc, off);
+          if (c == 0) zpart[it][wave][4 * g + j] = acc;
+        }
       }
     }
     if (a.o) store_tile<D, LD>(O, o, 1.f, a.o + (size_t)b * S * a.ld_o + h * D, a.ld_o, S, lane);
+   }
+   if (a.zp) {  // sum the Hl heads of each sequence in rank order (deterministic) and add the bias
+    __syncthreads();  // (the next iteration writes the other buffer: one barrier per iteration)
+    const int t = threadIdx.x, w = t >> 4, cls = t & 15, prw = base + w;
+    if (t < WPB * 16 && prw < npairs && prw % a.Hl == 0 && cls < a.n_out) {
+      float acc = 0.f;
+      for (int k = 0; k < a.Hl; ++k) acc += zpart[it][w + k][cls];
+      if (a.bo) acc += a.bo[cls];
+      a.zp[(size_t)(prw / a.Hl) * a.ld_zp + cls] = acc;
+    }
+   }
   }
 }
 
 template <int D>
-__global__ void __launch_bounds__(256) k_attn16_bwd(AttnArgs a) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D == 128 ? 2 : 4))) k_attn16_bwd(AttnArgs a) {
   constexpr int LD = D + 8, NK = D / 32, NT = D / 16, TILE = 16 * LD;
   extern __shared__ __attribute__((aligned(16))) uint16_t sm[];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
@@ -175,10 +230,19 @@ __global__ void __launch_bounds__(256) k_attn16_bwd(AttnArgs a) {
   // bias column sums of the 4 waves meet in LDS and leave with one atomic per
   // column per workgroup (per-wave atomics on the same 3*D addresses contend)
   const int h = blockIdx.x % a.Hl, nbh = gridDim.x / a.Hl;
+  // fused pooled fc_o input gradient: this head's slice of W_o, fp32, for every sequence
+  // (bf16, 2 KiB at D = 64: the workgroup stays within 40 KiB of LDS, 4 per CU)
+  __shared__ uint16_t wos[16 * D];
+  if (a.dz) {
+    for (int i = threadIdx.x; i < 16 * D; i += blockDim.x) {
+      const int cls = i / D;
+      wos[i] = cls < a.n_out ? a.wo[(size_t)cls * a.ld_wo + h * D + i % D] : (uint16_t)0;
+    }
+    __syncthreads();
+  }
   for (int b = (blockIdx.x / a.Hl) * WPB + wave; b < a.B; b += nbh * WPB) {
     const int pr = b * a.Hl + h;
     const uint16_t* qb = a.qkv + (size_t)b * S * a.ld_qkv + h * D;
-    const uint16_t* db = a.dout + (size_t)b * a.dout_bstride + h * D;
     bf16x8 qr[NK], kr[NK], vr[NK], dr[NK];
 #pragma unroll
     for (int kk = 0; kk < NK; ++kk) {
@@ -186,7 +250,32 @@ __global__ void __launch_bounds__(256) k_attn16_bwd(AttnArgs a) {
       qr[kk] = ld_row16(qb + off, c < S);
       kr[kk] = ld_row16(qb + HD + off, c < S);
       vr[kk] = ld_row16(qb + 2 * HD + off, c < S);
-      dr[kk] = ld_row16(db + (size_t)c * a.dout_rstride + 32 * kk + 8 * g, c < S);
+    }
+    if (a.dz) {
+      // dO row (every one of the S rows) = dz_scale * dz[b] . W_o[:, h*D .. h*D + D),
+      // rounded to bf16 like the separate dpool GEMM's output
+      // the dz row is wave-uniform: keep its 8 words in scalar registers
+      const uint32_t* zrow = reinterpret_cast<const uint32_t*>(a.dz + (size_t)__builtin_amdgcn_readfirstlane(b) * a.ld_dz);
+      uint32_t zw[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) zw[q] = __builtin_amdgcn_readfirstlane(zrow[q]);
+      for (int col = lane; col < D; col += 64) {
+        float v = 0.f;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          v += bf16_lo(zw[q]) * __uint_as_float((uint32_t)wos[(2 * q) * D + col] << 16);
+          v += bf16_hi(zw[q]) * __uint_as_float((uint32_t)wos[(2 * q + 1) * D + col] << 16);
+        }
+        Dt[col] = (uint16_t)f32_to_bf16_bits(v * a.dz_scale);  // row 0 of this wave's dO tile
+      }
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int kk = 0; kk < NK; ++kk) dr[kk] = ld_row16(Dt + 32 * kk + 8 * g, c < S);
+      __builtin_amdgcn_wave_barrier();  // put_rows below rewrites the tile
+    } else {
+      const uint16_t* db = a.dout + (size_t)b * a.dout_bstride + h * D;
+#pragma unroll
+      for (int kk = 0; kk < NK; ++kk) dr[kk] = ld_row16(db + (size_t)c * a.dout_rstride + 32 * kk + 8 * g, c < S);
     }
     put_rows<D, LD>(Qt, qr, lane);
     put_rows<D, LD>(Kt, kr, lane);

@@ -229,11 +229,23 @@ void check_dims(int S, int D, bool bwd) {
   if ((bwd ? bwd_lds(S, D) : fwd_lds(S, D)) > 160 * 1024) throw std::invalid_argument("attn_small: tile exceeds LDS");
 }
 
+// Fused pooled fc_o (fwd: logits from the pooled attention output; bwd: the
+// pooled output's gradient from dZ) needs the MFMA kernels' workgroup layout.
+static void check_fused_fc(const AttnArgs& a, bool bwd) {
+  if (!attn::mfma_supported(a, bwd) || a.n_out < 1 || a.n_out > 16 || 4 % a.Hl || !a.wo)
+    throw std::invalid_argument("attention: fused fc_o needs S <= 16, D in {32, 64, 128}, Hl | 4, n_out <= 16");
+  if (bwd && (a.ld_dz < 16 || a.ld_dz % 8 || ((uint64_t)a.dz % 16)))
+    throw std::invalid_argument("attention: fused fc_o backward needs dz rows of >= 16 bf16, 16-B aligned");
+  if (!bwd && !a.pool) throw std::invalid_argument("attention: fused fc_o forward needs the pooled output");
+}
+
 void attn_fwd(uint64_t qkv, uint64_t o, uint64_t lse, int B, int S, int Hl, int D, int ld_qkv, int ld_o, float scale,
-              uint64_t pool, int ld_pool, uint64_t stream) {
+              uint64_t pool, int ld_pool, uint64_t stream, uint64_t wo, int ld_wo, int n_out, uint64_t zp, int ld_zp,
+              uint64_t bo) {
   check_dims(S, D, false);
   AttnArgs a{(const uint16_t*)qkv, (uint16_t*)o, (float*)lse, nullptr, nullptr, nullptr, B, S, Hl, D, ld_qkv, ld_o, scale,
-             (uint16_t*)pool, ld_pool, 0, 0};
+             (uint16_t*)pool, ld_pool, 0, 0, (const uint16_t*)wo, ld_wo, n_out, (float*)zp, ld_zp, (const float*)bo};
+  if (zp) check_fused_fc(a, false);
   if (attn::mfma_supported(a, false)) {
     attn::launch_fwd_mfma(a, (hipStream_t)stream);
     CCMPI_HIP_CHECK(hipGetLastError());
@@ -244,10 +256,13 @@ void attn_fwd(uint64_t qkv, uint64_t o, uint64_t lse, int B, int S, int Hl, int 
 }
 
 void attn_bwd(uint64_t qkv, uint64_t o, uint64_t lse, uint64_t dout, uint64_t dqkv, uint64_t dbias, int B, int S,
-              int Hl, int D, int ld_qkv, int ld_o, float scale, int dout_bstride, int dout_rstride, uint64_t stream) {
+              int Hl, int D, int ld_qkv, int ld_o, float scale, int dout_bstride, int dout_rstride, uint64_t stream,
+              uint64_t dz, int ld_dz, uint64_t wo, int ld_wo, int n_out, float dz_scale) {
   check_dims(S, D, true);
   AttnArgs a{(const uint16_t*)qkv, (uint16_t*)o, (float*)lse, (const uint16_t*)dout, (uint16_t*)dqkv, (float*)dbias,
-             B, S, Hl, D, ld_qkv, ld_o, scale, nullptr, 0, dout_bstride, dout_rstride};
+             B, S, Hl, D, ld_qkv, ld_o, scale, nullptr, 0, dout_bstride, dout_rstride, (const uint16_t*)wo, ld_wo,
+             n_out, nullptr, 0, nullptr, (const uint16_t*)dz, ld_dz, dz_scale};
+  if (dz) check_fused_fc(a, true);
   if (attn::mfma_supported(a, true)) {
     attn::launch_bwd_mfma(a, (hipStream_t)stream);
     CCMPI_HIP_CHECK(hipGetLastError());
@@ -466,8 +481,15 @@ void register_attn_ops(pybind11::module_& m) {
   m.def("attn_set_bwd_grid", [](int cap) { attn::g_bwd_grid_cap = cap > 0 ? cap : 0; },
         "backward kernel grid cap (tuning)");
   namespace py = pybind11;
-  m.def("attn_small_fwd", &attn_fwd, py::call_guard<py::gil_scoped_release>());
-  m.def("attn_small_bwd", &attn_bwd, py::call_guard<py::gil_scoped_release>());
+  m.def("attn_small_fwd", &attn_fwd, py::arg("qkv"), py::arg("o"), py::arg("lse"), py::arg("B"), py::arg("S"),
+        py::arg("Hl"), py::arg("D"), py::arg("ld_qkv"), py::arg("ld_o"), py::arg("scale"), py::arg("pool"),
+        py::arg("ld_pool"), py::arg("stream"), py::arg("wo") = 0, py::arg("ld_wo") = 0, py::arg("n_out") = 0,
+        py::arg("zp") = 0, py::arg("ld_zp") = 0, py::arg("bo") = 0, py::call_guard<py::gil_scoped_release>());
+  m.def("attn_small_bwd", &attn_bwd, py::arg("qkv"), py::arg("o"), py::arg("lse"), py::arg("dout"), py::arg("dqkv"),
+        py::arg("dbias"), py::arg("B"), py::arg("S"), py::arg("Hl"), py::arg("D"), py::arg("ld_qkv"), py::arg("ld_o"),
+        py::arg("scale"), py::arg("dout_bstride"), py::arg("dout_rstride"), py::arg("stream"), py::arg("dz") = 0,
+        py::arg("ld_dz") = 0, py::arg("wo") = 0, py::arg("ld_wo") = 0, py::arg("n_out") = 0,
+        py::arg("dz_scale") = 1.0f, py::call_guard<py::gil_scoped_release>());
   m.def("adamw_step", &adamw, py::arg("p"), py::arg("g"), py::arg("m"), py::arg("v"), py::arg("p16"), py::arg("n"),
         py::arg("lr"), py::arg("b1"), py::arg("b2"), py::arg("eps"), py::arg("wd"), py::arg("step"),
         py::arg("grad_scale"), py::arg("stream"),

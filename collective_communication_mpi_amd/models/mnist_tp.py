@@ -76,6 +76,7 @@ class LayerConfig:
     overlap: bool = True
     plain_gemm: str = "own"  # backward dH = dQKV . W_qkv: "own" (MFMA kernel, W^T kept by AdamW) | "hipblaslt"
     emb_grad: str = "reassoc"  # "reassoc": dW_emb = W_qkv^T (dQKV^T Xp), no dH; "dh": materialize dH first
+    fuse_fc_o: bool = True   # pooled fc_o inside the attention kernels (fwd logits, bwd dpool) instead of GEMMs
 
     @property
     def seq(self) -> int:
@@ -234,20 +235,31 @@ class MnistTPLayer:
         # path (and the MFMA backward, which never reads O) skip materializing it
         mfma_attn = S <= 16 and cfg.head_dim in (32, 64, 128)
         att = self._buf("att", (M, self.hd), torch.bfloat16) if (naive or not mfma_attn) else None
+        fc_fused = self._fused_fc_o()
+        zp = None
+        fc = {}
+        if fc_fused:
+            # logits straight from the attention kernel: per head the pooled features times
+            # this rank's W_o columns, heads summed in the workgroup, bias by TP rank 0
+            zp = self._buf("zp", (B, cfg.out_pad), torch.float32, self.tp_dev)
+            wo = self.flat.param16("o_w")
+            fc = dict(wo=wo.data_ptr(), ld_wo=wo.stride(0), n_out=cfg.out_pad, zp=zp.data_ptr(), ld_zp=zp.stride(0),
+                      bo=self.flat.param("o_b").data_ptr() if self.tp_idx == 0 else 0)
         D.attn_small_fwd(qkv.data_ptr(), 0 if att is None else att.data_ptr(), lse.data_ptr(), B, S, self.hl,
                          cfg.head_dim, qkv.stride(0), self.hd if att is None else att.stride(0),
                          1.0 / math.sqrt(cfg.head_dim),
-                         0 if pool is None else pool.data_ptr(), 0 if pool is None else pool.stride(0), st)
+                         0 if pool is None else pool.data_ptr(), 0 if pool is None else pool.stride(0), st, **fc)
         if naive:
             z = self._forward_naive_fc_o(att, B)
             logits = z.view(B, S, cfg.out_pad)[:, :, : cfg.n_classes].mean(dim=1)
         else:
             # fc_o and the mean over patches are linear: pool first (fused in the
             # attention kernel), so fc_o and its TP all-reduce work on B rows, not B*S
-            zp = self._buf("zp", (B, cfg.out_pad), torch.float32, self.tp_dev)
-            # output bias in the GEMM epilogue, added by TP rank 0 only (the TP all-reduce sums ranks)
-            gemm_nt(pool, P16("o_w"), out=zp, out_dtype=torch.float32, splitk=1,
-                    bias=self.flat.param("o_b") if self.tp_idx == 0 else None)
+            if not fc_fused:
+                zp = self._buf("zp", (B, cfg.out_pad), torch.float32, self.tp_dev)
+                # output bias in the GEMM epilogue, added by TP rank 0 only (the TP all-reduce sums ranks)
+                gemm_nt(pool, P16("o_w"), out=zp, out_dtype=torch.float32, splitk=1,
+                        bias=self.flat.param("o_b") if self.tp_idx == 0 else None)
             if self.tp_dev is not None:
                 self.tp_dev.allreduce(zp, zp, "SUM")  # row-parallel: one TP all-reduce (B x 16 fp32)
             logits = zp[:, : cfg.n_classes]  # bias already included
@@ -256,6 +268,11 @@ class MnistTPLayer:
         self._saved = (xp, h, qkv, att, lse, B, pool)
         self._hx = hx[:, : d + cfg.kp] if fused else None
         return logits
+
+    def _fused_fc_o(self) -> bool:
+        cfg = self.cfg
+        return (cfg.fuse_fc_o and not (cfg.fc_o_mode == "naive" and cfg.tp > 1) and cfg.seq <= 16
+                and cfg.head_dim in (32, 64, 128) and 4 % self.hl == 0 and cfg.out_pad <= 16)
 
     def _forward_naive_fc_o(self, att, B):
         """Reference collects: gather fc_o's input, out-sharded fc_o, gather its output."""
@@ -343,16 +360,26 @@ class MnistTPLayer:
                 dzp.zero_()
                 dzp[:, : cfg.n_classes] = dlogits.to(torch.bfloat16)
             gemm_tn(dzp, pool, out=G("o_w"), accumulate=True)    # dW_o = dZ^T . pooled
-            dpool = self._buf("dpool", (B, self.hd), torch.bfloat16)
-            gemm_nt(dzp, self.flat.param16_t("o_w"), out=dpool, alpha=1.0 / S)
-            dout, dout_b, dout_r = dpool, dpool.stride(0), 0
+            if self._fused_fc_o():
+                dout, dout_b, dout_r = None, 0, 0                   # dpool formed inside the attention bwd
+            else:
+                dpool = self._buf("dpool", (B, self.hd), torch.bfloat16)
+                gemm_nt(dzp, self.flat.param16_t("o_w"), out=dpool, alpha=1.0 / S)
+                dout, dout_b, dout_r = dpool, dpool.stride(0), 0
         self.buckets.ready(0)
         # ---- attention
         dqkv = self._buf("dqkv", (M, 3 * self.hd), torch.bfloat16)
-        D.attn_small_bwd(qkv.data_ptr(), 0 if att is None else att.data_ptr(), lse.data_ptr(), dout.data_ptr(),
+        fc = {}
+        if dout is None:
+            dzp = self._buf("dzp", (B, cfg.out_pad), torch.bfloat16)
+            wo = P16("o_w")
+            fc = dict(dz=dzp.data_ptr(), ld_dz=dzp.stride(0), wo=wo.data_ptr(), ld_wo=wo.stride(0), n_out=cfg.out_pad,
+                      dz_scale=1.0 / S)
+        D.attn_small_bwd(qkv.data_ptr(), 0 if att is None else att.data_ptr(), lse.data_ptr(),
+                         0 if dout is None else dout.data_ptr(),
                          dqkv.data_ptr(), G("qkv_b").data_ptr(), B, S, self.hl, cfg.head_dim, qkv.stride(0),
                          self.hd if att is None else att.stride(0),
-                         1.0 / math.sqrt(cfg.head_dim), dout_b, dout_r, st)  # + QKV bias grad in-kernel
+                         1.0 / math.sqrt(cfg.head_dim), dout_b, dout_r, st, **fc)  # + QKV bias grad in-kernel
         # ---- fused QKV projection (column-parallel)
         if cfg.emb_grad == "reassoc" and self._hx is not None:
             # one GEMM over the fused activation rows: dQKV^T . [h | xp]; the split-K

@@ -320,6 +320,46 @@ def test_attn_small_fwd_bwd(B, S, H, D):
     torch.testing.assert_close(dqkv.float(), ref_in.grad, rtol=3e-2, atol=3e-2)
 
 
+@pytest.mark.parametrize("B,S,H,D,n_out", [(2048, 16, 4, 64, 16), (37, 16, 2, 128, 10), (13, 9, 1, 32, 16),
+                                            (7, 16, 4, 64, 3)])
+def test_attn_fused_fc_o(B, S, H, D, n_out):
+    """Pooled fc_o inside the attention kernels: forward logits zp = pool . W_o^T + b_o
+    (heads summed in the workgroup) and backward dO = (dz . W_o) / S formed in-kernel,
+    against torch fp32 and against the explicit-dO kernel path."""
+    from collective_communication_mpi_amd import _native
+
+    dev = _native.device()
+    st = torch.cuda.current_stream().cuda_stream
+    g = torch.Generator(device="cuda").manual_seed(B * 31 + D)
+    qkv = (torch.randn(B * S, 3 * H * D, device="cuda", generator=g) * 0.5).bfloat16()
+    lse = torch.empty(B * H, S, device="cuda")
+    pool = torch.empty(B, H * D, device="cuda", dtype=torch.bfloat16)
+    wo = (torch.randn(n_out, H * D, device="cuda", generator=g) * 0.1).bfloat16()
+    bo = torch.randn(n_out, device="cuda", generator=g)
+    zp = torch.full((B, 16), float("nan"), device="cuda")
+    dev.attn_small_fwd(qkv.data_ptr(), 0, lse.data_ptr(), B, S, H, D, qkv.stride(0), H * D, D ** -0.5,
+                       pool.data_ptr(), pool.stride(0), st, wo=wo.data_ptr(), ld_wo=wo.stride(0), n_out=n_out,
+                       zp=zp.data_ptr(), ld_zp=zp.stride(0), bo=bo.data_ptr())
+    ref_pool = _attn_ref(qkv, B, S, H, D).view(B, S, H * D).mean(1)
+    torch.testing.assert_close(pool.float(), ref_pool, rtol=2e-2, atol=2e-2)
+    ref_z = pool.float() @ wo.float().T + bo          # from the kernel's own bf16 pooled output
+    torch.testing.assert_close(zp[:, :n_out], ref_z, rtol=1e-4, atol=1e-4)
+    # backward: in-kernel dO vs the explicit broadcast dO the separate GEMM would produce
+    dz = torch.randn(B, 16, device="cuda", generator=g).bfloat16()
+    dpool = ((dz[:, :n_out].float() @ wo.float()) / S).bfloat16()
+    d1, d2 = torch.empty_like(qkv), torch.empty_like(qkv)
+    b1, b2 = torch.zeros(3 * H * D, device="cuda"), torch.zeros(3 * H * D, device="cuda")
+    dev.attn_small_bwd(qkv.data_ptr(), 0, lse.data_ptr(), dpool.data_ptr(), d1.data_ptr(), b1.data_ptr(), B, S, H, D,
+                       qkv.stride(0), H * D, D ** -0.5, dpool.stride(0), 0, st)
+    dev.attn_small_bwd(qkv.data_ptr(), 0, lse.data_ptr(), 0, d2.data_ptr(), b2.data_ptr(), B, S, H, D,
+                       qkv.stride(0), H * D, D ** -0.5, 0, 0, st, dz=dz.data_ptr(), ld_dz=dz.stride(0),
+                       wo=wo.data_ptr(), ld_wo=wo.stride(0), n_out=n_out, dz_scale=1.0 / S)
+    torch.cuda.synchronize()
+    # dO rounding can differ in the last bf16 bit (fp32 summation order), nothing more
+    torch.testing.assert_close(d2.float(), d1.float(), rtol=2e-2, atol=2e-2)
+    assert (b2 - b1).norm() <= 1e-2 * b1.norm() + 1e-3
+
+
 def test_patchify_columns():
     from collective_communication_mpi_amd.models.mnist_tp import LayerConfig, patchify
 
