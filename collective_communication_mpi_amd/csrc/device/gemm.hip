@@ -758,10 +758,54 @@ __global__ void __launch_bounds__(NT) k_gemm_tn(GemmArgs g, int split_major) {
 // ---------------------------------------------------------------------------
 constexpr int SK_BM = 64, SK_NT = 256;
 int g_sk_bn = std::getenv("CCMPI_SK_BN") ? std::atoi(std::getenv("CCMPI_SK_BN")) : 128;      // tuning knobs
-int g_sk_grid = std::getenv("CCMPI_SK_GRID") ? std::atoi(std::getenv("CCMPI_SK_GRID")) : 2048;
+// grid cap; 0 = one balanced round (below)
+int g_sk_grid = std::getenv("CCMPI_SK_GRID") ? std::atoi(std::getenv("CCMPI_SK_GRID")) : 0;
 
-template <int SK_BN, int FAST = 0>  // FAST = 1 + out_bf16 (no accumulate / act, aligned C, N % 8 == 0), 0 = generic
-__global__ void __launch_bounds__(SK_NT) k_gemm_smallk(GemmArgs g, int kp) {
+int device_cus() {
+  static int cus = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      return 256;
+    return n > 0 ? n : 256;
+  }();
+  return cus;
+}
+
+// Patch source for the fused embedding (PATCH = true): the A rows are generated
+// from the fp32 images instead of read -- token row m = (image m / S, patch m % S)
+// holds the patch's p*p pixels, a constant 1 (bias column) and a one-hot patch
+// position, exactly like k_patchify (attn_small.hip) -- and the blocks of the
+// first N slice also store those rows to xp (the backward's copy of the input).
+struct PatchSrc {
+  const float* x;   // [B][img*img]
+  int img, p;
+  uint16_t* xp;     // [M][ld_xp] bf16 (may be null)
+  int ld_xp;
+};
+
+__device__ __forceinline__ uint4 patch_chunk(const PatchSrc& ps, int m, int ch) {
+  const int gp = ps.img / ps.p, S = gp * gp, pp = ps.p * ps.p;
+  const int s = m % S;
+  const float* xb = ps.x + (size_t)(m / S) * ps.img * ps.img + (s / gp) * ps.p * ps.img + (s % gp) * ps.p;
+  uint32_t w[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    float v2[2];
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      const int cc = ch * 8 + 2 * q + hh;
+      float v = 0.f;
+      if (cc < pp) v = xb[(cc / ps.p) * ps.img + cc % ps.p];
+      else if (cc == pp || cc == pp + 1 + s) v = 1.f;
+      v2[hh] = v;
+    }
+    w[q] = f32_to_bf16_bits(v2[0]) | (f32_to_bf16_bits(v2[1]) << 16);
+  }
+  return uint4{w[0], w[1], w[2], w[3]};
+}
+
+template <int SK_BN, int FAST = 0, bool PATCH = false>  // FAST = 1 + out_bf16 (no accumulate / act, aligned C, N % 8 == 0), 0 = generic
+__global__ void __launch_bounds__(SK_NT) k_gemm_smallk(GemmArgs g, int kp, PatchSrc ps) {
   constexpr int WN = SK_BN / 4;  // columns per wave
   constexpr int NP = WN / 32;    // column pairs (32 columns) per wave
   constexpr int NJ = 2 * NP;     // 16-col MFMA tiles per wave
@@ -792,8 +836,14 @@ __global__ void __launch_bounds__(SK_NT) k_gemm_smallk(GemmArgs g, int kp) {
     for (int i = 0; i < kMaxPer; ++i) {
       const int idx = t + i * SK_NT, r = idx / nchunk, ch = idx % nchunk;
       ra[i] = uint4{0, 0, 0, 0};
-      if (i < per && r < SK_BM && m0 + r < g.M && ch < kchunks)
-        ra[i] = *reinterpret_cast<const uint4*>(g.A + (size_t)(m0 + r) * g.lda + ch * 8);
+      if (i < per && r < SK_BM && m0 + r < g.M && ch < kchunks) {
+        if constexpr (PATCH) {
+          ra[i] = patch_chunk(ps, m0 + r, ch);
+          if (tn == 0 && ps.xp) *reinterpret_cast<uint4*>(ps.xp + (size_t)(m0 + r) * ps.ld_xp + ch * 8) = ra[i];
+        } else {
+          ra[i] = *reinterpret_cast<const uint4*>(g.A + (size_t)(m0 + r) * g.lda + ch * 8);
+        }
+      }
     }
   };
   auto swrite = [&](int buf) {
@@ -971,6 +1021,71 @@ __global__ void __launch_bounds__(256) k_splitk_reduce(const float* __restrict__
   }
 }
 
+// Small-K launcher (patch embedding, K <= 96): B slice resident in LDS, A tiles streamed
+// (or generated from the images, PATCH), direct stores.  id = FAST variant (0 generic,
+// 1 fp32 out, 2 bf16 out); patch sources need id 2.
+void launch_smallk(const GemmArgs& g, int id, const PatchSrc& ps, hipStream_t st) {
+  const int kp = (g.K + 31) / 32 * 32;
+  const int skbn = (g_sk_bn == 256 && !ps.x) ? 256 : 128;
+  const int tiles_n = (g.N + skbn - 1) / skbn, tiles_m = (g.M + SK_BM - 1) / SK_BM;
+  const size_t lds = (size_t)(skbn + 2 * SK_BM) * (kp * 2 + 16);
+  // Every block loads its B slice once, then walks M tiles: the grid is one round of
+  // resident blocks (LDS-limited per CU) with the same number of M tiles in every block
+  // (an uneven split leaves half the blocks idle for the last tile).  Measured on the
+  // 32768 x 768 x 72 embedding: 3 blocks per CU, 768 blocks x 4 tiles: 23.6 us; a
+  // 2048-block grid (1-2 tiles each): 28-29 us (benchmarks/emb_write_probe.py).
+  int mblocks;
+  if (g_sk_grid > 0) {
+    mblocks = std::max(1, std::min(tiles_m, std::max(1, g_sk_grid / tiles_n)));
+  } else {
+    const int per_cu = std::max(1, (int)((160u * 1024u) / lds));
+    const int cap = std::max(1, per_cu * device_cus() / tiles_n);   // resident blocks per N slice
+    const int rounds = (tiles_m + cap - 1) / cap;                    // M tiles per block
+    mblocks = (tiles_m + rounds - 1) / rounds;
+  }
+  static bool attr = [] {
+    bool ok = true;
+    for (const void* f : {reinterpret_cast<const void*>(k_gemm_smallk<256, 0>),
+                          reinterpret_cast<const void*>(k_gemm_smallk<128, 0>),
+                          reinterpret_cast<const void*>(k_gemm_smallk<128, 1>),
+                          reinterpret_cast<const void*>(k_gemm_smallk<128, 2>),
+                          reinterpret_cast<const void*>(k_gemm_smallk<128, 2, true>)})
+      ok = ok && hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
+    return ok;
+  }();
+  (void)attr;
+  const dim3 grid(tiles_n * mblocks);
+  if (ps.x) {
+    if (id != 2) throw std::invalid_argument("ccmpi: the fused patch embedding needs the bf16 fast epilogue");
+    hipLaunchKernelGGL((k_gemm_smallk<128, 2, true>), grid, dim3(SK_NT), lds, st, g, kp, ps);
+  } else if (skbn == 256) {
+    hipLaunchKernelGGL((k_gemm_smallk<256, 0>), grid, dim3(SK_NT), lds, st, g, kp, ps);
+  } else if (id == 1) {
+    hipLaunchKernelGGL((k_gemm_smallk<128, 1>), grid, dim3(SK_NT), lds, st, g, kp, ps);
+  } else if (id == 2) {
+    hipLaunchKernelGGL((k_gemm_smallk<128, 2>), grid, dim3(SK_NT), lds, st, g, kp, ps);
+  } else {
+    hipLaunchKernelGGL((k_gemm_smallk<128, 0>), grid, dim3(SK_NT), lds, st, g, kp, ps);
+  }
+  CCMPI_HIP_CHECK(hipGetLastError());
+}
+
+// Fused MNIST patch embedding: h[M][N] = patches(x)[M][K] . W[N][K]^T, bf16 out, with the
+// patch rows (pixels | 1 | one-hot position | 0 pad, K = kp of the model) generated from
+// the fp32 images inside the GEMM and also stored to xp (row stride ld_xp) for the backward.
+void embed_patches(uint64_t x, uint64_t W, uint64_t C, int B, int img, int p, int N, int K, int ldw, int ldc,
+                   uint64_t xp, int ld_xp, uint64_t stream) {
+  const int S = (img / p) * (img / p), M = B * S;
+  if (M <= 0 || N <= 0) return;
+  if (K % 8 || K > 96 || K < p * p + 1 + S || ldw % 8 || ldc % 8 || N % 8 || (W % 16) || (C % 16) ||
+      (xp && (ld_xp % 8 || (xp % 16))) || M < 4 * SK_BM)
+    throw std::invalid_argument("ccmpi embed_patches: K % 8 == 0, p*p + 1 + S <= K <= 96, 16-B aligned rows, N % 8 == 0");
+  GemmArgs g{nullptr, reinterpret_cast<const uint16_t*>(W), reinterpret_cast<void*>(C), nullptr, M, N, K, K, ldw, ldc,
+             1.f, 0, 0, 0, 1, 1};
+  launch_smallk(g, 2, PatchSrc{reinterpret_cast<const float*>(x), img, p, reinterpret_cast<uint16_t*>(xp), ld_xp},
+                reinterpret_cast<hipStream_t>(stream));
+}
+
 void gemm_nt(uint64_t A, uint64_t B, uint64_t C, uint64_t bias, int M, int N, int K, int lda, int ldb, int ldc,
              float alpha, bool accumulate, int bias_kind, int act, bool out_bf16, int splitk, uint64_t stream) {
   if (M <= 0 || N <= 0) return;
@@ -989,33 +1104,8 @@ void gemm_nt(uint64_t A, uint64_t B, uint64_t C, uint64_t bias, int M, int N, in
   // small K (patch embedding): B slice resident in LDS, A tiles streamed, direct stores
   // measured (benchmarks/smallk_sweep.py): wins over the 128x128 kernel up to K ~ 96
   if (K <= 96 && splitk == 1 && g_kernel != 1 && g_sk_bn > 0 && M >= 4 * SK_BM) {
-    const int kp = (K + 31) / 32 * 32;
-    const int skbn = g_sk_bn == 256 ? 256 : 128;
-    const int tiles_n = (N + skbn - 1) / skbn, tiles_m = (M + SK_BM - 1) / SK_BM;
-    const int mblocks = std::max(1, std::min(tiles_m, std::max(1, g_sk_grid / tiles_n)));
-    const size_t lds = (size_t)(skbn + 2 * SK_BM) * (kp * 2 + 16);
-    static bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(k_gemm_smallk<256, 0>),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess &&
-                       hipFuncSetAttribute(reinterpret_cast<const void*>(k_gemm_smallk<128, 0>),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess &&
-                       hipFuncSetAttribute(reinterpret_cast<const void*>(k_gemm_smallk<128, 1>),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess &&
-                       hipFuncSetAttribute(reinterpret_cast<const void*>(k_gemm_smallk<128, 2>),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
-    (void)attr;
     const bool fast = !accumulate && act == 0 && N % 8 == 0 && ldc % 8 == 0 && (C % 16) == 0;
-    const int id = fast ? 1 + (out_bf16 ? 1 : 0) : 0;
-    auto st = reinterpret_cast<hipStream_t>(stream);
-    const dim3 grid(tiles_n * mblocks);
-    if (skbn == 256)
-      hipLaunchKernelGGL((k_gemm_smallk<256, 0>), grid, dim3(SK_NT), lds, st, g, kp);
-    else if (id == 1)
-      hipLaunchKernelGGL((k_gemm_smallk<128, 1>), grid, dim3(SK_NT), lds, st, g, kp);
-    else if (id == 2)
-      hipLaunchKernelGGL((k_gemm_smallk<128, 2>), grid, dim3(SK_NT), lds, st, g, kp);
-    else
-      hipLaunchKernelGGL((k_gemm_smallk<128, 0>), grid, dim3(SK_NT), lds, st, g, kp);
-    CCMPI_HIP_CHECK(hipGetLastError());
+    launch_smallk(g, fast ? 1 + (out_bf16 ? 1 : 0) : 0, PatchSrc{}, reinterpret_cast<hipStream_t>(stream));
     return;
   }
   // 256 x {256, 192, 128} ping-pong kernels: need K % 128 and enough tiles to
@@ -1170,6 +1260,11 @@ void register_gemm_ops(pybind11::module_& m) {
     g_pp_exp = e;
     CCMPI_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_pp_exp_dev), &e, sizeof(int)));
   }, "GEMM ablation bits (benchmarks only): 1/2/4 ping-pong kernel, 8 = skip the 128x128 epilogue");
+  m.def("embed_patches", &embed_patches, "h = patches(x) . W^T (bf16), patch rows generated in-kernel and stored to xp",
+        pybind11::arg("x"), pybind11::arg("W"), pybind11::arg("C"), pybind11::arg("B"), pybind11::arg("img"),
+        pybind11::arg("p"), pybind11::arg("N"), pybind11::arg("K"), pybind11::arg("ldw"), pybind11::arg("ldc"),
+        pybind11::arg("xp"), pybind11::arg("ld_xp"), pybind11::arg("stream"),
+        pybind11::call_guard<pybind11::gil_scoped_release>());
   m.def("gemm_set_smallk", [](int bn, int grid) { g_sk_bn = bn; g_sk_grid = grid; },
         "small-K kernel: N slice (128 / 256, 0 = off) and grid cap (tuning)");
   m.def("transpose16", &transpose16, "dst[C,R] = src[R,C]^T for 16-bit elements",

@@ -691,12 +691,16 @@ void ShmComm::bcast(void* buf, size_t nbytes, int root) {
     if (rank_ != root) std::memcpy(b, small_(root, e), nbytes);
     return;
   }
+  // staged through the root's slot, not `result`: slots are only read between the
+  // two barriers of a collective, while a rooted collective's root may still be
+  // copying `result` out after the previous call's last barrier (Reduce, then a
+  // Bcast from another root, overwrote the Reduce result under load)
   const size_t S = slot_bytes();
   for (size_t off = 0; off < nbytes; off += S) {
     size_t c = std::min(S, nbytes - off);
-    if (rank_ == root) std::memcpy(result_(), b + off, c);
+    if (rank_ == root) std::memcpy(slot_(root), b + off, c);
     slot_barrier_();
-    if (rank_ != root) std::memcpy(b + off, result_(), c);
+    if (rank_ != root) std::memcpy(b + off, slot_(root), c);
     slot_barrier_();
   }
 }

@@ -38,7 +38,12 @@ kernel; the optimizer is one fused AdamW pass.  Fusions that remove whole passes
 * with TP > 1 the embedding needs only the TP-sum of its *weight* gradient
   (d_model x 72 fp32, 221 KB), not an all-reduce of the TP-partial activation
   gradient dH (tokens x d_model): W_emb's gradient is linear in dH and the
-  embedding input needs no gradient.
+  embedding input needs no gradient;
+* both weight gradients of the embedding -> QKV chain come from ONE token-length
+  contraction A = dQKV^T . Xp (3hd x 72): dW_emb = W_qkv^T A and, because
+  h = Xp W_emb^T, dW_qkv = dQKV^T h = A W_emb^T (``qkv_grad="reassoc"``).  The
+  840-column dQKV^T . [h | xp] GEMM (65 us) becomes a 72-column one (~25 us) plus
+  two 72-deep fp32 GEMMs on weight-sized matrices.
 """
 from __future__ import annotations
 
@@ -76,6 +81,9 @@ class LayerConfig:
     overlap: bool = True
     plain_gemm: str = "own"  # backward dH = dQKV . W_qkv: "own" (MFMA kernel, W^T kept by AdamW) | "hipblaslt"
     emb_grad: str = "reassoc"  # "reassoc": dW_emb = W_qkv^T (dQKV^T Xp), no dH; "dh": materialize dH first
+    # with emb_grad="reassoc": "reassoc": dW_qkv = (dQKV^T Xp) W_emb^T (h is not read in backward);
+    # "direct": dW_qkv = dQKV^T h (one TN GEMM over the fused [h | xp] rows)
+    qkv_grad: str = "reassoc"
     fuse_fc_o: bool = True   # pooled fc_o inside the attention kernels (fwd logits, bwd dpool) instead of GEMMs
 
     @property
@@ -213,9 +221,12 @@ class MnistTPLayer:
         hx = self._buf("hx", (B * cfg.seq, self._hx_ld), torch.bfloat16)
         return hx[:, cfg.d_model:cfg.d_model + cfg.kp]
 
-    def forward(self, xp: torch.Tensor, B: int) -> torch.Tensor:
+    def forward(self, xp: torch.Tensor, B: int, images: Optional[torch.Tensor] = None) -> torch.Tensor:
         """xp: (B*S, kp) bf16 patches -> logits (B, n_classes) fp32.  Saves activations.
-        xp is either ``input_buffer(B)`` (fused [h | xp] layout) or any other tensor."""
+        xp is either ``input_buffer(B)`` (fused [h | xp] layout) or any other tensor.
+        With ``images`` ((B, 784) fp32) and the fused layout, the patch rows are
+        generated inside the embedding GEMM (and stored to xp for the backward):
+        no separate patchify pass."""
         cfg = self.cfg
         S, d = cfg.seq, cfg.d_model
         M = B * S
@@ -223,7 +234,17 @@ class MnistTPLayer:
         hx = self._bufs.get(("hx", (M, self._hx_ld), torch.bfloat16))
         fused = hx is not None and xp.data_ptr() == hx.data_ptr() + 2 * d and xp.stride(0) == hx.stride(0)
         h = hx[:, :d] if fused else self._buf("h", (M, d), torch.bfloat16)
-        gemm_nt(xp, P16("emb_w"), out=h)  # bias + position are columns of W_emb
+        if images is not None and not fused:
+            patchify(images, cfg, out=xp)
+            images = None
+        if images is not None:
+            x = images.contiguous().float()
+            w = P16("emb_w")
+            _native.device().embed_patches(x.data_ptr(), w.data_ptr(), h.data_ptr(), B, cfg.img, cfg.patch, d, cfg.kp,
+                                           w.stride(0), h.stride(0), xp.data_ptr(), xp.stride(0),
+                                           torch.cuda.current_stream(self.device).cuda_stream)
+        else:
+            gemm_nt(xp, P16("emb_w"), out=h)  # bias + position are columns of W_emb
         qkv = self._buf("qkv", (M, 3 * self.hd), torch.bfloat16)
         gemm_nt(h, P16("qkv_w"), out=qkv, bias=self.flat.param("qkv_b"))
         lse = self._buf("lse", (B * self.hl, S), torch.float32)
@@ -359,7 +380,9 @@ class MnistTPLayer:
             if not fused:
                 dzp.zero_()
                 dzp[:, : cfg.n_classes] = dlogits.to(torch.bfloat16)
-            gemm_tn(dzp, pool, out=G("o_w"), accumulate=True)    # dW_o = dZ^T . pooled
+            # dW_o = dZ^T . pooled: 16 x hd over B rows, latency-bound; 32 K-splits measured fastest
+            # (benchmarks/tn_small.py: 9.6 us at 8 splits, 7.2 us at 32)
+            gemm_tn(dzp, pool, out=G("o_w"), accumulate=True, splitk=max(1, min(32, B // 64)))
             if self._fused_fc_o():
                 dout, dout_b, dout_r = None, 0, 0                   # dpool formed inside the attention bwd
             else:
@@ -381,6 +404,18 @@ class MnistTPLayer:
                          self.hd if att is None else att.stride(0),
                          1.0 / math.sqrt(cfg.head_dim), dout_b, dout_r, st, **fc)  # + QKV bias grad in-kernel
         # ---- fused QKV projection (column-parallel)
+        if cfg.emb_grad == "reassoc" and cfg.qkv_grad == "reassoc":
+            # h = Xp . W_emb^T, so dW_qkv = dQKV^T . h = (dQKV^T . Xp) . W_emb^T: the one
+            # token-length contraction is A = dQKV^T . Xp (3hd x kp, 72 columns instead of
+            # the 840 of dQKV^T . [h | xp]); A then yields both weight gradients through
+            # two 72-deep fp32 GEMMs on [3hd x d] / [d x kp] matrices
+            a = self._buf("a_emb", (3 * self.hd, cfg.kp), torch.float32)
+            gemm_tn(dqkv, xp, out=a)                              # A = dQKV^T . Xp (MFMA, fp32 accumulate)
+            G("qkv_w").addmm_(a, self.flat.param("emb_w").t())    # dW_qkv += A . W_emb^T
+            self.buckets.ready(1)
+            self._emb_grad_reassoc(dqkv, xp, a=a)
+            self.buckets.ready(2)
+            return
         if cfg.emb_grad == "reassoc" and self._hx is not None:
             # one GEMM over the fused activation rows: dQKV^T . [h | xp]; the split-K
             # reduction adds the h columns into dW_qkv and writes the xp columns to A

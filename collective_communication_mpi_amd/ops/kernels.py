@@ -74,14 +74,18 @@ def gemm_nt(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None
 
 
 def gemm_tn(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None, alpha: float = 1.0,
-            accumulate: bool = False, splitk: Optional[int] = None, tail: Optional[torch.Tensor] = None) -> torch.Tensor:
+            accumulate: bool = False, splitk: Optional[int] = None, tail: Optional[torch.Tensor] = None,
+            workspace: Optional[bool] = None) -> torch.Tensor:
     """``out[N1, N2] (+)= alpha * a[M, N1].T @ b[M, N2]`` (weight gradients dW = dY^T X) in fp32,
     reading both operands M-major through ds_read_b64_tr_b16 (no transposes).
 
     ``tail``: split the result by columns -- ``out`` (``[N1, c]``, accumulated if
     ``accumulate``) receives columns ``< c`` and ``tail`` (``[N1, N2 - c]``,
     overwritten) the rest, straight from the split-K reduction (one GEMM over a
-    row-concatenated operand ``b = [X | Y]`` gives ``a^T X`` and ``a^T Y``)."""
+    row-concatenated operand ``b = [X | Y]`` gives ``a^T X`` and ``a^T Y``).
+
+    ``workspace``: split-K partials through a workspace + one reduction pass (True)
+    or fp32 atomics into ``out`` (False); default by output size."""
     if a.dtype != torch.bfloat16 or b.dtype != torch.bfloat16:
         raise TypeError("gemm_tn expects bf16 operands")
     if a.dim() != 2 or b.dim() != 2 or a.shape[0] != b.shape[0] or a.stride(1) != 1 or b.stride(1) != 1:
@@ -120,7 +124,8 @@ def gemm_tn(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None
     ws = 0
     # large outputs: partials in a workspace + one reduction pass instead of fp32 atomics
     # (dW_qkv 768x768: 80 -> 68 us); small outputs keep the atomics (one launch fewer)
-    if splitk > 1 and N2 % 4 == 0 and (variant == 1 or N1 * N2 >= (1 << 18) or tail is not None):
+    use_ws = workspace if workspace is not None else (variant == 1 or N1 * N2 >= (1 << 18) or tail is not None)
+    if splitk > 1 and N2 % 4 == 0 and (use_ws or tail is not None):
         ws = torch.empty(splitk * N1 * N2, dtype=torch.float32, device=a.device).data_ptr()
     _D().gemm_tn(a.data_ptr(), b.data_ptr(), out.data_ptr(), M, N1, N2, a.stride(0), b.stride(0), out.stride(0),
                  float(alpha), bool(accumulate), int(splitk), _stream(a), ws, int(variant),

@@ -27,15 +27,17 @@ def _reference(cfg, xp, y, P):
     return loss.detach(), {k: t.grad for k, t in w.items()}
 
 
-@pytest.mark.parametrize("emb_grad,fused,fuse_fc_o", [("reassoc", True, True), ("reassoc", True, False),
-                                                      ("reassoc", False, True), ("dh", True, True), ("dh", False, False)])
-def test_harness_grads_match_torch_fp32(emb_grad, fused, fuse_fc_o):
+@pytest.mark.parametrize("emb_grad,qkv_grad,fused,fuse_fc_o", [
+    ("reassoc", "reassoc", True, True), ("reassoc", "reassoc", True, False), ("reassoc", "reassoc", False, True),
+    ("reassoc", "direct", True, True), ("reassoc", "direct", False, True),
+    ("dh", "direct", True, True), ("dh", "direct", False, False)])
+def test_harness_grads_match_torch_fp32(emb_grad, qkv_grad, fused, fuse_fc_o):
     from collective_communication_mpi_amd import MPI, Communicator
     from collective_communication_mpi_amd.models.harness import build
     from collective_communication_mpi_amd.models.mnist_tp import local_batch, patchify
 
     comm = Communicator(MPI.COMM_WORLD)
-    cfg, layer, x_all, y_all = build(comm, 1, 128, emb_grad=emb_grad, fuse_fc_o=fuse_fc_o)
+    cfg, layer, x_all, y_all = build(comm, 1, 128, emb_grad=emb_grad, qkv_grad=qkv_grad, fuse_fc_o=fuse_fc_o)
     # non-trivial biases so their gradients and the bias epilogues are exercised
     g = torch.Generator().manual_seed(7)
     layer.flat.param("qkv_b").copy_(torch.randn(layer.flat.param("qkv_b").shape, generator=g) * 0.1)

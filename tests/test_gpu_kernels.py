@@ -375,6 +375,30 @@ def test_patchify_columns():
     assert torch.all(xp[:, cfg.pixels + 1 + cfg.seq:] == 0)
 
 
+def test_embed_patches_fused_matches_patchify_gemm():
+    """Patch rows generated inside the small-K GEMM (and stored to xp) == patchify, then the GEMM."""
+    from collective_communication_mpi_amd import _native
+    from collective_communication_mpi_amd.models.mnist_tp import LayerConfig, patchify
+    from collective_communication_mpi_amd.ops import gemm_nt
+
+    cfg = LayerConfig()
+    B, d = 37, cfg.d_model  # M = 592: a partial last M tile
+    x = torch.rand(B, 784, device="cuda")
+    w = (torch.randn(d, cfg.kp, device="cuda") * 0.2).bfloat16()
+    ld = d + cfg.kp + 56  # [h | xp] rows, 16-B aligned
+    hx = torch.full((B * cfg.seq, ld), float("nan"), device="cuda").bfloat16()
+    h, xp = hx[:, :d], hx[:, d:d + cfg.kp]
+    _native.device().embed_patches(x.data_ptr(), w.data_ptr(), h.data_ptr(), B, cfg.img, cfg.patch, d, cfg.kp,
+                                   w.stride(0), h.stride(0), xp.data_ptr(), xp.stride(0),
+                                   torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    xp_ref = patchify(x, cfg)
+    assert torch.equal(xp, xp_ref)
+    torch.testing.assert_close(h.float(), gemm_nt(xp_ref, w).float(), rtol=1e-2, atol=1e-2)
+    torch.testing.assert_close(h.float(), xp_ref.float() @ w.float().t(), rtol=2e-2, atol=3e-2)
+    assert torch.isnan(hx[:, d + cfg.kp:].float()).all()  # padding columns untouched
+
+
 def test_fused_adamw_matches_torch():
     from collective_communication_mpi_amd.parallel.dp import FlatParams
 
