@@ -760,6 +760,7 @@ constexpr int SK_BM = 64, SK_NT = 256;
 int g_sk_bn = std::getenv("CCMPI_SK_BN") ? std::atoi(std::getenv("CCMPI_SK_BN")) : 128;      // tuning knobs
 // grid cap; 0 = one balanced round (below)
 int g_sk_grid = std::getenv("CCMPI_SK_GRID") ? std::atoi(std::getenv("CCMPI_SK_GRID")) : 0;
+bool g_sk_nt = std::getenv("CCMPI_SK_NT") != nullptr;  // non-temporal bf16 stores (A/B knob)
 
 int device_cus() {
   static int cus = [] {
@@ -804,7 +805,7 @@ __device__ __forceinline__ uint4 patch_chunk(const PatchSrc& ps, int m, int ch) 
   return uint4{w[0], w[1], w[2], w[3]};
 }
 
-template <int SK_BN, int FAST = 0, bool PATCH = false>  // FAST = 1 + out_bf16 (no accumulate / act, aligned C, N % 8 == 0), 0 = generic
+template <int SK_BN, int FAST = 0, bool PATCH = false>  // FAST = 1 + out_bf16 (no accumulate / act, aligned C, N % 8 == 0), 0 = generic; 3 = bf16 non-temporal
 __global__ void __launch_bounds__(SK_NT) k_gemm_smallk(GemmArgs g, int kp, PatchSrc ps) {
   constexpr int WN = SK_BN / 4;  // columns per wave
   constexpr int NP = WN / 32;    // column pairs (32 columns) per wave
@@ -903,12 +904,17 @@ __global__ void __launch_bounds__(SK_NT) k_gemm_smallk(GemmArgs g, int kp, Patch
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] = g.alpha * acc[i][2 * pr + (e >> 2)][e & 3] + bias[pr][e];
           if (row < g.M && col < g.N) {
-            if constexpr (FAST == 2) {
+            if constexpr (FAST >= 2) {
               uint32_t w[4];
 #pragma unroll
               for (int q = 0; q < 4; ++q) w[q] = f32_to_bf16_bits(v[2 * q]) | (f32_to_bf16_bits(v[2 * q + 1]) << 16);
-              *reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(g.C) + (size_t)row * g.ldc + col) =
-                  uint4{w[0], w[1], w[2], w[3]};
+              uint4* dst = reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(g.C) + (size_t)row * g.ldc + col);
+              if constexpr (FAST == 3) {  // streaming (non-temporal) store: A/B knob for the write-bound case
+                typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+                __builtin_nontemporal_store(u32x4v{w[0], w[1], w[2], w[3]}, reinterpret_cast<u32x4v*>(dst));
+              } else {
+                *dst = uint4{w[0], w[1], w[2], w[3]};
+              }
             } else {
               float4* C = reinterpret_cast<float4*>(reinterpret_cast<float*>(g.C) + (size_t)row * g.ldc + col);
               C[0] = make_float4(v[0], v[1], v[2], v[3]);
@@ -1049,6 +1055,7 @@ void launch_smallk(const GemmArgs& g, int id, const PatchSrc& ps, hipStream_t st
                           reinterpret_cast<const void*>(k_gemm_smallk<128, 0>),
                           reinterpret_cast<const void*>(k_gemm_smallk<128, 1>),
                           reinterpret_cast<const void*>(k_gemm_smallk<128, 2>),
+                          reinterpret_cast<const void*>(k_gemm_smallk<128, 3>),
                           reinterpret_cast<const void*>(k_gemm_smallk<128, 2, true>)})
       ok = ok && hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
     return ok;
@@ -1063,7 +1070,8 @@ void launch_smallk(const GemmArgs& g, int id, const PatchSrc& ps, hipStream_t st
   } else if (id == 1) {
     hipLaunchKernelGGL((k_gemm_smallk<128, 1>), grid, dim3(SK_NT), lds, st, g, kp, ps);
   } else if (id == 2) {
-    hipLaunchKernelGGL((k_gemm_smallk<128, 2>), grid, dim3(SK_NT), lds, st, g, kp, ps);
+    if (g_sk_nt) hipLaunchKernelGGL((k_gemm_smallk<128, 3>), grid, dim3(SK_NT), lds, st, g, kp, ps);
+    else hipLaunchKernelGGL((k_gemm_smallk<128, 2>), grid, dim3(SK_NT), lds, st, g, kp, ps);
   } else {
     hipLaunchKernelGGL((k_gemm_smallk<128, 0>), grid, dim3(SK_NT), lds, st, g, kp, ps);
   }
@@ -1265,6 +1273,7 @@ void register_gemm_ops(pybind11::module_& m) {
         pybind11::arg("p"), pybind11::arg("N"), pybind11::arg("K"), pybind11::arg("ldw"), pybind11::arg("ldc"),
         pybind11::arg("xp"), pybind11::arg("ld_xp"), pybind11::arg("stream"),
         pybind11::call_guard<pybind11::gil_scoped_release>());
+  m.def("gemm_set_smallk_nt", [](bool on) { g_sk_nt = on; }, "small-K kernel: non-temporal bf16 output stores");
   m.def("gemm_set_smallk", [](int bn, int grid) { g_sk_bn = bn; g_sk_grid = grid; },
         "small-K kernel: N slice (128 / 256, 0 = off) and grid cap (tuning)");
   m.def("transpose16", &transpose16, "dst[C,R] = src[R,C]^T for 16-bit elements",
