@@ -1,0 +1,228 @@
+// Weight gradients of the harness's embedding -> QKV chain from the one
+// token-length contraction A = dQKV^T . Xp (fp32 [R][kp], R = 3*hd rows of this
+// TP rank, kp = 72 patch columns), in ONE launch:
+//
+//   Gq[R][d]  += A . We^T      (dW_qkv; h = Xp . We^T, so dQKV^T . h = A . We^T)
+//   Ge[d][kp] += Wq^T . A      (dW_emb, or this TP rank's partial of it)
+//   Z[R][kp]   = 0             (next step's A buffer: the split-K GEMM that forms A
+//                               accumulates with atomics into a zeroed buffer, so
+//                               no memset launch per step)
+//
+// Both products are tiny (85 and 42 MFLOP fp32) and latency-bound; two library
+// sgemm launches took 6.7 + 9.0 us, plus a 5 us memset for A.
+//
+//   * Gq: 64 x 64 output tiles (144 workgroups at R = d = 768).  Both operand
+//     tiles are staged K-major in LDS ([k][64 + 4] fp32), so a thread's 4 rows /
+//     4 columns at one k are two 16-B LDS reads feeding 16 FMAs.
+//   * Ge: 64-column tiles of d x 96-row splits of the R reduction (96 workgroups
+//     at R = d = 768), operand slabs staged in LDS; the splits meet through fp32
+//     atomic adds.
+//   Every global operand load of a workgroup is issued before the first use (the
+//   kernel is latency-bound: one serial load per loop trip cost 85 us).
+#include <pybind11/pybind11.h>
+
+#include "common.hpp"
+#include "ops.hpp"
+
+namespace ccmpi {
+namespace dev {
+
+namespace {
+
+constexpr int kT = 64;          // Gq tile edge, Ge tile height (d columns)
+constexpr int kLdT = kT + 4;    // LDS row stride (floats) of the K-major Gq tiles
+constexpr int kMaxKp = 96;      // patch columns (kp % 4 == 0)
+constexpr int kGeRows = 96;     // Ge: rows of the R reduction per workgroup
+constexpr int kNT = 256;
+
+struct WgradArgs {
+  const float* A;
+  int ld_a;
+  const float* We;
+  int ld_we;
+  const float* Wq;
+  int ld_wq;
+  float* Gq;
+  int ld_gq;
+  float* Ge;
+  int ld_ge;
+  float* Z;
+  int ld_z;
+  int R, d, kp;
+  int gq_blocks;   // workgroups [0, gq_blocks) do Gq tiles, the rest Ge partials
+  int splits;      // Ge: R-splits per d tile
+};
+
+// Gq[r0.., c0..] += sum_k A[r][k] We[c][k] for a 64 x 64 tile.  Operand tiles are
+// fetched with every float4 load in flight, then stored K-major to LDS so one
+// thread's 4 rows / 4 columns at a k are two 16-B LDS reads for 16 FMAs.
+__device__ void gq_tile(const WgradArgs& a, int blk, float* smem) {
+  float* At = smem;                  // [kp][kLdT]: At[k][r] = A[r0 + r][k]
+  float* Wt = smem + kMaxKp * kLdT;  // [kp][kLdT]: Wt[k][c] = We[c0 + c][k]
+  const int tiles_c = (a.d + kT - 1) / kT;
+  const int r0 = (blk / tiles_c) * kT, c0 = (blk % tiles_c) * kT;
+  const int t = threadIdx.x, nv = a.kp / 4;
+  constexpr int kPer = kT * (kMaxKp / 4) / kNT;  // float4 per thread per operand at kp = 96
+  float4 ra[kPer], rw[kPer];
+#pragma unroll
+  for (int u = 0; u < kPer; ++u) {
+    const int idx = t + u * kNT, r = idx / nv, q = idx % nv;
+    const bool ok = idx < kT * nv;
+    ra[u] = (ok && r0 + r < a.R) ? *reinterpret_cast<const float4*>(a.A + (size_t)(r0 + r) * a.ld_a + 4 * q)
+                                 : make_float4(0.f, 0.f, 0.f, 0.f);
+    rw[u] = (ok && c0 + r < a.d) ? *reinterpret_cast<const float4*>(a.We + (size_t)(c0 + r) * a.ld_we + 4 * q)
+                                 : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+#pragma unroll
+  for (int u = 0; u < kPer; ++u) {
+    const int idx = t + u * kNT, r = idx / nv, q = idx % nv;
+    if (idx < kT * nv) {
+      float* pa = At + 4 * q * kLdT + r;
+      float* pw = Wt + 4 * q * kLdT + r;
+      pa[0] = ra[u].x; pa[kLdT] = ra[u].y; pa[2 * kLdT] = ra[u].z; pa[3 * kLdT] = ra[u].w;
+      pw[0] = rw[u].x; pw[kLdT] = rw[u].y; pw[2 * kLdT] = rw[u].z; pw[3 * kLdT] = rw[u].w;
+    }
+  }
+  __syncthreads();
+  const int tx = t & 15, ty = t >> 4;  // rows 4*ty.., columns 4*tx..
+  float acc[4][4] = {};
+  for (int k = 0; k < a.kp; ++k) {
+    const float4 av = *reinterpret_cast<const float4*>(At + k * kLdT + 4 * ty);
+    const float4 wv = *reinterpret_cast<const float4*>(Wt + k * kLdT + 4 * tx);
+    const float ar[4] = {av.x, av.y, av.z, av.w}, wr[4] = {wv.x, wv.y, wv.z, wv.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = fmaf(ar[i], wr[j], acc[i][j]);
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = r0 + 4 * ty + i;
+    if (r >= a.R) continue;
+    float* g = a.Gq + (size_t)r * a.ld_gq + c0 + 4 * tx;
+    if (c0 + 4 * tx + 3 < a.d && ((reinterpret_cast<uintptr_t>(g) & 15) == 0)) {
+      float4 o = *reinterpret_cast<float4*>(g);
+      o.x += acc[i][0]; o.y += acc[i][1]; o.z += acc[i][2]; o.w += acc[i][3];
+      *reinterpret_cast<float4*>(g) = o;
+    } else {
+      for (int j = 0; j < 4; ++j)
+        if (c0 + 4 * tx + j < a.d) g[j] += acc[i][j];
+    }
+  }
+}
+
+// Ge partial of one (d tile, R split): P[i][j] = sum_{r in split} Wq[r][i0 + i] A[r][j]
+// for 64 d columns x kp, both operand slabs staged row-major in LDS (all loads in
+// flight); thread (i4, jg) owns d columns 4*i4.. and patch columns jg + 16m.
+__device__ void ge_tile(const WgradArgs& a, int blk, float* smem) {
+  constexpr int kLdW = kT + 4, kLdA = kMaxKp + 4;
+  float* Ws = smem;                   // [kGeRows][kLdW]
+  float* As = smem + kGeRows * kLdW;  // [kGeRows][kLdA]
+  const int itile = blk / a.splits, split = blk % a.splits;
+  const int i0 = itile * kT, rlo = split * kGeRows, rows = max(0, min(kGeRows, a.R - rlo));
+  const int t = threadIdx.x, nv = a.kp / 4;
+  constexpr int kPerW = kGeRows * (kT / 4) / kNT, kPerA = (kGeRows * (kMaxKp / 4) + kNT - 1) / kNT;
+  float4 rw[kPerW], ra[kPerA];
+#pragma unroll
+  for (int u = 0; u < kPerW; ++u) {
+    const int idx = t + u * kNT, r = idx / (kT / 4), q = idx % (kT / 4);
+    rw[u] = (r < rows && i0 + 4 * q + 3 < a.d)
+                ? *reinterpret_cast<const float4*>(a.Wq + (size_t)(rlo + r) * a.ld_wq + i0 + 4 * q)
+                : make_float4(0.f, 0.f, 0.f, 0.f);
+    if (r < rows && i0 + 4 * q < a.d && i0 + 4 * q + 3 >= a.d) {  // ragged d edge
+      const float* w = a.Wq + (size_t)(rlo + r) * a.ld_wq + i0 + 4 * q;
+      rw[u].x = w[0];
+      if (i0 + 4 * q + 1 < a.d) rw[u].y = w[1];
+      if (i0 + 4 * q + 2 < a.d) rw[u].z = w[2];
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < kPerA; ++u) {
+    const int idx = t + u * kNT, r = idx / nv, q = idx % nv;
+    ra[u] = (idx < kGeRows * nv && r < rows)
+                ? *reinterpret_cast<const float4*>(a.A + (size_t)(rlo + r) * a.ld_a + 4 * q)
+                : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+#pragma unroll
+  for (int u = 0; u < kPerW; ++u) {
+    const int idx = t + u * kNT, r = idx / (kT / 4), q = idx % (kT / 4);
+    *reinterpret_cast<float4*>(Ws + r * kLdW + 4 * q) = rw[u];
+  }
+#pragma unroll
+  for (int u = 0; u < kPerA; ++u) {
+    const int idx = t + u * kNT, r = idx / nv, q = idx % nv;
+    if (idx < kGeRows * nv) *reinterpret_cast<float4*>(As + r * kLdA + 4 * q) = ra[u];
+  }
+  __syncthreads();
+  const int i4 = t & 15, jg = t >> 4;
+  float acc[6][4] = {};
+  for (int r = 0; r < rows; ++r) {
+    const float4 w4 = *reinterpret_cast<const float4*>(Ws + r * kLdW + 4 * i4);
+#pragma unroll
+    for (int m = 0; m < 6; ++m) {
+      const float x = As[r * kLdA + jg + 16 * m];  // columns >= kp hold junk, never stored
+      acc[m][0] = fmaf(w4.x, x, acc[m][0]);
+      acc[m][1] = fmaf(w4.y, x, acc[m][1]);
+      acc[m][2] = fmaf(w4.z, x, acc[m][2]);
+      acc[m][3] = fmaf(w4.w, x, acc[m][3]);
+    }
+  }
+  // fp32 atomic adds into Ge (hardware global_atomic_add_f32, no return): the R
+  // splits meet in memory.  A ticket-and-last-workgroup reduction (fixed order)
+  // cost ~20 us here -- agent-coherent hand-off plus a serial partial read -- and
+  // A itself is already a split-K atomic sum, so order-exact sums bought nothing.
+#pragma unroll
+  for (int m = 0; m < 6; ++m) {
+    const int j = jg + 16 * m;
+    if (j >= a.kp) continue;
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      if (i0 + 4 * i4 + e < a.d) unsafeAtomicAdd(a.Ge + (size_t)(i0 + 4 * i4 + e) * a.ld_ge + j, acc[m][e]);
+  }
+}
+
+constexpr size_t kSmemFloats = 2 * kMaxKp * kLdT > kGeRows * (kT + 4 + kMaxKp + 4)
+                                   ? 2 * kMaxKp * kLdT : kGeRows * (kT + 4 + kMaxKp + 4);
+
+__global__ void __launch_bounds__(kNT) k_emb_qkv_wgrad(WgradArgs a) {
+  __shared__ __attribute__((aligned(16))) float smem[kSmemFloats];
+  const int blk = blockIdx.x;
+  if (blk < a.gq_blocks) gq_tile(a, blk, smem);
+  else if (a.Ge) ge_tile(a, blk - a.gq_blocks, smem);
+  if (a.Z) {  // zero the next A buffer, spread over every workgroup
+    const size_t n = (size_t)a.R * a.kp;
+    for (size_t e = (size_t)blk * blockDim.x + threadIdx.x; e < n; e += (size_t)gridDim.x * blockDim.x)
+      a.Z[(e / a.kp) * a.ld_z + e % a.kp] = 0.f;
+  }
+}
+
+void emb_qkv_wgrad(uint64_t A, int ld_a, uint64_t We, int ld_we, uint64_t Wq, int ld_wq, uint64_t Gq, int ld_gq,
+                   uint64_t Ge, int ld_ge, uint64_t Z, int ld_z, int R, int d, int kp, uint64_t stream) {
+  if (R <= 0 || d <= 0 || kp <= 0) return;
+  if (kp > kMaxKp || kp % 4 || ld_a % 4 || ld_we % 4 || ld_wq % 4 || (A % 16) || (We % 16) || (Wq % 16))
+    throw std::invalid_argument("emb_qkv_wgrad: kp <= 96, kp and row strides % 4 == 0, 16-B aligned operands");
+  if (!A || !We || !Gq || (Z && Z == A)) throw std::invalid_argument("emb_qkv_wgrad: A, We, Gq required; Z must differ from A");
+  if (Ge && !Wq) throw std::invalid_argument("emb_qkv_wgrad: Ge needs Wq");
+  const int splits = (R + kGeRows - 1) / kGeRows, dtiles = (d + kT - 1) / kT;
+  WgradArgs a{reinterpret_cast<const float*>(A), ld_a, reinterpret_cast<const float*>(We), ld_we,
+              reinterpret_cast<const float*>(Wq), ld_wq, reinterpret_cast<float*>(Gq), ld_gq,
+              reinterpret_cast<float*>(Ge), ld_ge, reinterpret_cast<float*>(Z), ld_z, R, d, kp, 0, splits};
+  a.gq_blocks = ((R + kT - 1) / kT) * dtiles;
+  const int ge_blocks = Ge ? dtiles * splits : 0;
+  hipLaunchKernelGGL(k_emb_qkv_wgrad, dim3(a.gq_blocks + ge_blocks), dim3(kNT), 0, (hipStream_t)stream, a);
+  CCMPI_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace
+
+void register_wgrad_ops(pybind11::module_& m) {
+  m.def("emb_qkv_wgrad", &emb_qkv_wgrad,
+        "Gq += A . We^T (fixed order); Ge += Wq^T . A (fp32 atomics; Ge = 0: skipped); Z = 0 (Z = 0: skipped)",
+        pybind11::arg("A"), pybind11::arg("ld_a"), pybind11::arg("We"), pybind11::arg("ld_we"), pybind11::arg("Wq"),
+        pybind11::arg("ld_wq"), pybind11::arg("Gq"), pybind11::arg("ld_gq"), pybind11::arg("Ge"), pybind11::arg("ld_ge"),
+        pybind11::arg("Z"), pybind11::arg("ld_z"), pybind11::arg("R"), pybind11::arg("d"), pybind11::arg("kp"),
+        pybind11::arg("stream"), pybind11::call_guard<pybind11::gil_scoped_release>());
+}
+
+}  // namespace dev
+}  // namespace ccmpi

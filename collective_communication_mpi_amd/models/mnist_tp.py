@@ -42,8 +42,9 @@ kernel; the optimizer is one fused AdamW pass.  Fusions that remove whole passes
 * both weight gradients of the embedding -> QKV chain come from ONE token-length
   contraction A = dQKV^T . Xp (3hd x 72): dW_emb = W_qkv^T A and, because
   h = Xp W_emb^T, dW_qkv = dQKV^T h = A W_emb^T (``qkv_grad="reassoc"``).  The
-  840-column dQKV^T . [h | xp] GEMM (65 us) becomes a 72-column one (~25 us) plus
-  two 72-deep fp32 GEMMs on weight-sized matrices.
+  840-column dQKV^T . [h | xp] GEMM (65 us) becomes a 72-column one (~20 us) plus
+  one fp32 kernel for both weight-sized products (csrc/device/wgrad.hip), which
+  also zeroes the next step's A buffer (the split-K GEMM accumulates into it).
 """
 from __future__ import annotations
 
@@ -409,11 +410,28 @@ class MnistTPLayer:
             # token-length contraction is A = dQKV^T . Xp (3hd x kp, 72 columns instead of
             # the 840 of dQKV^T . [h | xp]); A then yields both weight gradients through
             # two 72-deep fp32 GEMMs on [3hd x d] / [d x kp] matrices
-            a = self._buf("a_emb", (3 * self.hd, cfg.kp), torch.float32)
-            gemm_tn(dqkv, xp, out=a)                              # A = dQKV^T . Xp (MFMA, fp32 accumulate)
-            G("qkv_w").addmm_(a, self.flat.param("emb_w").t())    # dW_qkv += A . W_emb^T
+            # A lives in a zeroed double buffer: the split-K GEMM accumulates into it with
+            # atomics (no memset launch) and the weight-gradient kernel zeroes the other half
+            key = ("a_emb2", 3 * self.hd, cfg.kp)
+            if key not in self._bufs:
+                self._bufs[key] = torch.zeros(2, 3 * self.hd, cfg.kp, dtype=torch.float32, device=self.device)
+                self._a_idx = 0
+            a, a_next = self._bufs[key][self._a_idx], self._bufs[key][self._a_idx ^ 1]
+            self._a_idx ^= 1
+            gemm_tn(dqkv, xp, out=a, accumulate=True, workspace=False)  # A = dQKV^T . Xp (MFMA, fp32)
+            tp = self.tp_dev is not None
+            ge = self._buf("gemb", (d, cfg.kp), torch.float32, self.tp_dev) if tp else G("emb_w")
+            we, wq, gq = self.flat.param("emb_w"), self.flat.param("qkv_w"), G("qkv_w")
+            if tp:
+                ge.zero_()  # this rank's partial, accumulated by atomics, then TP-summed
+            # dW_qkv += A . W_emb^T and dW_emb += W_qkv^T . A (TP: the partial) in one launch
+            D.emb_qkv_wgrad(a.data_ptr(), a.stride(0), we.data_ptr(), we.stride(0), wq.data_ptr(), wq.stride(0),
+                            gq.data_ptr(), gq.stride(0), ge.data_ptr(), ge.stride(0), a_next.data_ptr(),
+                            a_next.stride(0), 3 * self.hd, d, cfg.kp, st)
             self.buckets.ready(1)
-            self._emb_grad_reassoc(dqkv, xp, a=a)
+            if tp:
+                self.tp_dev.allreduce(ge, ge, "SUM")              # 221 KB instead of tokens x d_model
+                G("emb_w").add_(ge)
             self.buckets.ready(2)
             return
         if cfg.emb_grad == "reassoc" and self._hx is not None:

@@ -487,3 +487,35 @@ def test_gemm_tn_pingpong(M, N1, N2, splitk):
         torch.testing.assert_close(acc, 1 + 0.5 * ref, rtol=2e-3, atol=2e-3 * M ** 0.5)
     finally:
         set_tn_variant(None)
+
+
+@pytest.mark.parametrize("R,d,kp", [(768, 768, 72), (200, 136, 72), (96, 68, 40), (384, 768, 72), (1000, 132, 96)])
+def test_emb_qkv_wgrad_matches_torch(R, d, kp):
+    """dW_qkv += A . W_emb^T, dW_emb += W_qkv^T . A and the next-A zeroing, one launch (fp32)."""
+    from collective_communication_mpi_amd import _native
+
+    g = torch.Generator(device="cuda").manual_seed(3)
+    A = torch.randn(R, kp, device="cuda", generator=g)
+    We = torch.randn(d, kp, device="cuda", generator=g)
+    Wq = torch.randn(R, d, device="cuda", generator=g)
+    Gq = torch.randn(R, d, device="cuda", generator=g)
+    Ge = torch.randn(d, kp, device="cuda", generator=g)
+    Z = torch.randn(R, kp, device="cuda", generator=g)
+    gq0, ge0 = Gq.clone(), Ge.clone()
+    st = torch.cuda.current_stream().cuda_stream
+    D = _native.device()
+    D.emb_qkv_wgrad(A.data_ptr(), kp, We.data_ptr(), kp, Wq.data_ptr(), d, Gq.data_ptr(), d, Ge.data_ptr(), kp,
+                    Z.data_ptr(), kp, R, d, kp, st)
+    torch.cuda.synchronize()
+    torch.testing.assert_close(Gq, gq0 + A @ We.t(), rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(Ge, ge0 + Wq.t() @ A, rtol=1e-4, atol=1e-3)
+    assert torch.all(Z == 0)
+    # Gq only (Ge and Z skipped), repeated: Gq's tiles sum in a fixed order
+    g1 = torch.zeros(R, d, device="cuda")
+    g2 = torch.zeros(R, d, device="cuda")
+    for out in (g1, g2):
+        D.emb_qkv_wgrad(A.data_ptr(), kp, We.data_ptr(), kp, Wq.data_ptr(), d, out.data_ptr(), d, 0, kp, 0, kp, R, d,
+                        kp, st)
+    torch.cuda.synchronize()
+    assert torch.equal(g1, g2)
+    torch.testing.assert_close(g1, A @ We.t(), rtol=1e-4, atol=1e-3)
