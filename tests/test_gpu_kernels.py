@@ -519,3 +519,34 @@ def test_emb_qkv_wgrad_matches_torch(R, d, kp):
     torch.cuda.synchronize()
     assert torch.equal(g1, g2)
     torch.testing.assert_close(g1, A @ We.t(), rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.parametrize("stages", [3, 4, 5])
+@pytest.mark.parametrize("M,N,K", [(32768, 768, 768), (300, 520, 64), (129, 200, 128), (1000, 384, 320)])
+def test_gemm_multistage(stages, M, N, K):
+    """Multi-stage BK = 32 pipeline of the 128x128 kernel: plain, bias/bf16 fast epilogue, accumulate."""
+    from collective_communication_mpi_amd import _native
+    from collective_communication_mpi_amd.ops import gemm_nt
+
+    D = _native.device()
+    g = torch.Generator(device="cuda").manual_seed(M + N + K + stages)
+    a = torch.randn(M, K, device="cuda", generator=g).bfloat16()
+    b = torch.randn(N, K, device="cuda", generator=g).bfloat16()
+    bias = torch.randn(N, device="cuda", generator=g)
+    D.gemm_set_kernel(1)
+    D.gemm_set_stages(stages)
+    try:
+        y = gemm_nt(a, b, out_dtype=torch.float32, splitk=1)
+        yb = gemm_nt(a, b, bias=bias)
+        c = torch.randn(M, N, device="cuda", generator=g)
+        c0 = c.clone()
+        gemm_nt(a, b, out=c, accumulate=True, splitk=1)
+        y2 = gemm_nt(a, b, out_dtype=torch.float32, splitk=2)
+    finally:
+        D.gemm_set_stages(0)
+        D.gemm_set_kernel(0)
+    ref = _ref(a, b)
+    torch.testing.assert_close(y, ref, rtol=2e-3, atol=2e-3 * K ** 0.5)
+    torch.testing.assert_close(y2, ref, rtol=2e-3, atol=2e-3 * K ** 0.5)
+    torch.testing.assert_close(yb.float(), ref + bias, rtol=2e-2, atol=5e-2 * K ** 0.5 / 8)
+    torch.testing.assert_close(c, c0 + ref, rtol=2e-3, atol=2e-3 * K ** 0.5)
