@@ -360,11 +360,12 @@ def test_attn_fused_fc_o(B, S, H, D, n_out):
     assert (b2 - b1).norm() <= 1e-2 * b1.norm() + 1e-3
 
 
-def test_patchify_columns():
+@pytest.mark.parametrize("img,patch,misalign", [(28, 7, 0), (28, 7, 1), (24, 6, 0)])  # LDS / plain / runtime sizes
+def test_patchify_columns(img, patch, misalign):
     from collective_communication_mpi_amd.models.mnist_tp import LayerConfig, patchify
 
-    cfg = LayerConfig()
-    x = torch.rand(5, 784, device="cuda")
+    cfg = LayerConfig(img=img, patch=patch)
+    x = torch.rand(5 * img * img + misalign, device="cuda")[misalign:].view(5, img * img)
     xp = patchify(x, cfg).float()
     g = cfg.img // cfg.patch
     ref = x.view(5, g, cfg.patch, g, cfg.patch).permute(0, 1, 3, 2, 4).reshape(5 * g * g, cfg.pixels)
