@@ -12,7 +12,7 @@ import torch  # noqa: E402
 
 from collective_communication_mpi_amd import MPI, Communicator  # noqa: E402
 from collective_communication_mpi_amd.models.harness import build, train_step  # noqa: E402
-from collective_communication_mpi_amd.models.mnist_tp import local_batch, patchify  # noqa: E402
+from collective_communication_mpi_amd.models.mnist_tp import local_batch  # noqa: E402
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--mode", default="fwd")
@@ -24,11 +24,9 @@ comm = Communicator(MPI.COMM_WORLD)
 torch.cuda.set_device(int(os.environ.get("CCMPI_LOCAL_RANK", "0")) % torch.cuda.device_count())
 cfg, layer, x_all, y_all = build(comm, args.tp, args.batch)
 xb, yb = local_batch(cfg, x_all, y_all, 0, comm.Get_rank(), layer.device)
-xp = patchify(xb, cfg, out=layer.input_buffer(cfg.batch))
 for _ in range(args.steps):
     if args.mode == "fwd":
-        patchify(xb, cfg, out=xp)
-        layer.forward(xp, cfg.batch)
+        layer.forward_images(xb, cfg.batch)
     else:
         train_step(layer, cfg, xb, yb)
 torch.cuda.synchronize()

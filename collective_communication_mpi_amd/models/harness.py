@@ -21,7 +21,7 @@ import torch
 
 from ..data.preprocess import synthetic_mnist
 from ..utils import checkpoint as ckpt
-from .mnist_tp import LayerConfig, MnistTPLayer, local_batch, patchify
+from .mnist_tp import LayerConfig, MnistTPLayer, local_batch
 
 
 def _hc(comm):
@@ -35,6 +35,8 @@ def _sync_barrier(comm):
 
 def build(comm, tp: int, batch: int, **kw):
     world = comm.Get_size()
+    if "fwd_chunks" not in kw and os.environ.get("CCMPI_FWD_CHUNKS"):
+        kw["fwd_chunks"] = int(os.environ["CCMPI_FWD_CHUNKS"])
     cfg = LayerConfig(batch=batch, tp=tp, dp=world // tp, **kw)
     layer = MnistTPLayer(comm, cfg)
     x_all, y_all = synthetic_mnist(cfg.batch * cfg.dp * 2, seed=cfg.seed)
@@ -42,8 +44,7 @@ def build(comm, tp: int, batch: int, **kw):
 
 
 def train_step(layer: MnistTPLayer, cfg: LayerConfig, xb, yb):
-    xp = patchify(xb, cfg, out=layer.input_buffer(xb.shape[0]))
-    logits = layer.forward(xp, xb.shape[0])
+    logits = layer.forward_images(xb, xb.shape[0])  # patchify + forward (cfg.fwd_chunks streams)
     layer.zero_grad()
     if cfg.fc_o_mode == "row" or cfg.tp == 1:
         loss = layer.loss_and_grad_fused(yb, cfg.batch * cfg.dp)  # one kernel: loss, dZ, d o_b
@@ -62,11 +63,9 @@ def bench_forward(comm, tp: int = 2, batch: int = 2048, steps: int = 20, warmup:
     rank = comm.Get_rank()
     cfg, layer, x_all, y_all = build(comm, tp, batch)
     xb, yb = local_batch(cfg, x_all, y_all, 0, rank, layer.device)
-    xp_static = patchify(xb, cfg, out=layer.input_buffer(cfg.batch))
 
     def fwd():
-        patchify(xb, cfg, out=xp_static)
-        return layer.forward(xp_static, cfg.batch)
+        return layer.forward_images(xb, cfg.batch)
 
     for _ in range(3):
         fwd()
