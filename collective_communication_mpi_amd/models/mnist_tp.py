@@ -219,12 +219,17 @@ class MnistTPLayer:
 
     # ------------------------------------------------------------ forward
     def input_buffer(self, B: int) -> torch.Tensor:
-        """Where patchify should write a batch of B images: the right-hand column
-        block of the activation buffer hx = [h | xp] (M x (d_model + kp) bf16).
-        With both the embedding output h and its input xp in one row, the
-        backward reads dQKV once for dQKV^T . [h | xp]: dW_qkv and the
-        embedding-gradient contraction A = dQKV^T . xp come out of one GEMM."""
+        """Where patchify should write a batch of B images.  With ``qkv_grad="direct"``
+        (or ``emb_grad="dh"``): the right-hand column block of the activation buffer
+        hx = [h | xp] (M x (d_model + kp) bf16); with both the embedding output h and
+        its input xp in one row, the backward reads dQKV once for dQKV^T . [h | xp].
+        The default re-associated backward never reads h: then xp is its own
+        contiguous buffer."""
         cfg = self.cfg
+        if cfg.emb_grad == "reassoc" and cfg.qkv_grad == "reassoc":
+            # the backward never reads h, so h and xp need not share rows: separate
+            # contiguous buffers write/read ~2 us faster (profiles/r1_qkv_reassoc/layout_probe.txt)
+            return self._buf("xp", (B * cfg.seq, cfg.kp), torch.bfloat16)
         hx = self._buf("hx", (B * cfg.seq, self._hx_ld), torch.bfloat16)
         return hx[:, cfg.d_model:cfg.d_model + cfg.kp]
 
@@ -319,8 +324,8 @@ class MnistTPLayer:
         d, hl, hd = cfg.d_model, self.hl, self.hd
         M = B * S
         P16 = self.flat.param16
-        hx = self._bufs[("hx", (M, self._hx_ld), torch.bfloat16)]
-        h = hx[:, :d]
+        hx = self._bufs.get(("hx", (M, self._hx_ld), torch.bfloat16))
+        h = hx[:, :d] if hx is not None else self._buf("h", (M, d), torch.bfloat16)
         qkv = self._buf("qkv", (M, 3 * hd), torch.bfloat16)
         lse = self._buf("lse", (B * hl, S), torch.float32)
         pool = self._buf("pool", (B, hd), torch.bfloat16)
@@ -351,7 +356,7 @@ class MnistTPLayer:
         if self.tp_dev is not None:
             self.tp_dev.allreduce(zp, zp, "SUM")  # row-parallel: one TP all-reduce (B x 16 fp32)
         self._saved = (xp, h, qkv, None, lse, B, pool)
-        self._hx = hx[:, : d + cfg.kp]
+        self._hx = hx[:, : d + cfg.kp] if hx is not None else None
         return zp[:, : cfg.n_classes]
 
     def _fused_fc_o(self) -> bool:
