@@ -66,6 +66,18 @@ for n in [3, SLOT // 8 + 5]:
     ag = np.empty(p * n)
     comm.Allgather(xs[rank], ag)
     expect(np.array_equal(ag, np.concatenate(xs)), f"Allgather n={n}")
+# ---- Reduce immediately followed by a Bcast from another root, repeatedly: the Bcast
+# once staged through the shared result buffer that a slow Reduce root was still
+# copying out of (seen as a wrong Reduce result under CPU load)
+n = SLOT // 8 + 5
+for it in range(30):
+    out = np.empty(n) if rank == p - 1 else None
+    comm.Reduce(np.full(n, float(rank + it)), out, op=MPI.SUM, root=p - 1)
+    b = np.full(n, -float(it)) if rank == 1 % p else np.zeros(n)
+    comm.Bcast(b, root=1 % p)
+    if rank == p - 1:
+        expect(bool(np.all(out == sum(float(r + it) for r in range(p)))), f"Reduce then Bcast it={it}")
+    expect(bool(np.all(b == -float(it))), f"Bcast after Reduce it={it}")
     g = np.empty(p * n) if rank == 0 else None
     comm.Gather(xs[rank], g, root=0)
     if rank == 0:
