@@ -86,6 +86,9 @@ __device__ void gq_tile(const WgradArgs& a, int blk, float* smem) {
   __syncthreads();
   const int tx = t & 15, ty = t >> 4;  // rows 4*ty.., columns 4*tx..
   float acc[4][4] = {};
+  // unrolled so the LDS reads of several k are in flight (one k per trip waited out
+  // the LDS latency every 16 FMAs)
+#pragma unroll 8
   for (int k = 0; k < a.kp; ++k) {
     const float4 av = *reinterpret_cast<const float4*>(At + k * kLdT + 4 * ty);
     const float4 wv = *reinterpret_cast<const float4*>(Wt + k * kLdT + 4 * tx);
@@ -156,6 +159,7 @@ __device__ void ge_tile(const WgradArgs& a, int blk, float* smem) {
   __syncthreads();
   const int i4 = t & 15, jg = t >> 4;
   float acc[6][4] = {};
+#pragma unroll 8
   for (int r = 0; r < rows; ++r) {
     const float4 w4 = *reinterpret_cast<const float4*>(Ws + r * kLdW + 4 * i4);
 #pragma unroll
@@ -171,13 +175,23 @@ __device__ void ge_tile(const WgradArgs& a, int blk, float* smem) {
   // splits meet in memory.  A ticket-and-last-workgroup reduction (fixed order)
   // cost ~20 us here -- agent-coherent hand-off plus a serial partial read -- and
   // A itself is already a split-K atomic sum, so order-exact sums bought nothing.
+  // The tile goes through LDS first so each wave-instruction adds 64 consecutive
+  // floats of a row: straight from the accumulator layout an instruction touched 16
+  // rows x 16 B, and the adds ran ~8x below the atomic rate (8 of the kernel's 15 us).
+  constexpr int kLdP = kMaxKp + 1;
+  __syncthreads();  // every wave is done with the operand slabs
+  float* tile = smem;  // [kT][kLdP]
 #pragma unroll
   for (int m = 0; m < 6; ++m) {
     const int j = jg + 16 * m;
-    if (j >= a.kp) continue;
+    if (j < a.kp)
 #pragma unroll
-    for (int e = 0; e < 4; ++e)
-      if (i0 + 4 * i4 + e < a.d) unsafeAtomicAdd(a.Ge + (size_t)(i0 + 4 * i4 + e) * a.ld_ge + j, acc[m][e]);
+      for (int e = 0; e < 4; ++e) tile[(4 * i4 + e) * kLdP + j] = acc[m][e];
+  }
+  __syncthreads();
+  for (int idx = t; idx < kT * a.kp; idx += kNT) {
+    const int i = idx / a.kp, j = idx % a.kp;
+    if (i0 + i < a.d) unsafeAtomicAdd(a.Ge + (size_t)(i0 + i) * a.ld_ge + j, tile[i * kLdP + j]);
   }
 }
 
