@@ -918,39 +918,59 @@ __device__ __forceinline__ uint4 patch_chunk(const PatchSrc& ps, int m, int ch) 
   return uint4{w[0], w[1], w[2], w[3]};
 }
 
+// LDS row of the small-K kernel: the K / 8 data chunks (16 B), plus one spare chunk when
+// K is not a multiple of 32, rounded up to a chunk count u with u % 4 == 2, so the 16
+// consecutive rows of a fragment read (lane groups of ds_read_b128) land on 16 distinct
+// 4-bank groups.  Reads of chunks past K go to ONE zero chunk (B row 0's spare chunk,
+// a broadcast) instead of zero-padded row columns.  Measured: the former rows of
+// round_up(K, 32) + 8 elements had 44 % of LDS cycles in bank conflicts
+// (SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE) and room for 3 workgroups per CU, not 4.
+__host__ __device__ inline int sk_row_chunks(int K) {
+  int u = K / 8 + (K % 32 ? 1 : 0);
+  while (u % 4 != 2) ++u;
+  return u;
+}
+inline size_t sk_lds_bytes(int skbn, int K) { return (size_t)(skbn + 2 * SK_BM) * sk_row_chunks(K) * 16; }
+
 template <int SK_BN, int FAST = 0, bool PATCH = false>  // FAST = 1 + out_bf16 (no accumulate / act, aligned C, N % 8 == 0), 0 = generic; 3 = bf16 non-temporal
 __global__ void __launch_bounds__(SK_NT) k_gemm_smallk(GemmArgs g, int kp, PatchSrc ps) {
   constexpr int WN = SK_BN / 4;  // columns per wave
   constexpr int NP = WN / 32;    // column pairs (32 columns) per wave
   constexpr int NJ = 2 * NP;     // 16-col MFMA tiles per wave
   extern __shared__ __attribute__((aligned(16))) unsigned char sks[];
-  const int stride = kp * 2 + 16;                   // bytes per LDS row (odd # of 16-B slots)
-  unsigned char* Bs = sks;                          // SK_BN rows
+  const int stride = sk_row_chunks(g.K) * 16;       // bytes per LDS row
+  unsigned char* Bs = sks;                          // SK_BN rows (fragment-order permuted, below)
   unsigned char* As = sks + SK_BN * stride;         // 2 x SK_BM rows
+  const unsigned char* zchunk = sks + (g.K / 8) * 16;  // B row 0's spare chunk: 16 zero bytes
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6, c = lane & 15, gq = lane >> 4;
-  const int nchunk = kp / 8, kchunks = g.K / 8;     // 16-B chunks per LDS row / per global row
+  const int kchunks = g.K / 8;                      // 16-B data chunks per row
   const int tiles_n = (g.N + SK_BN - 1) / SK_BN, tiles_m = (g.M + SK_BM - 1) / SK_BM;
   const int tn = blockIdx.x % tiles_n;
   const int bn = tn * SK_BN;
   const int mstep = gridDim.x / tiles_n;            // blocks sharing this N slice
   int tm = blockIdx.x / tiles_n;
   if (tm >= tiles_m) return;
-  // B slice -> LDS (zero rows past N and chunks past K)
-  for (int idx = t; idx < SK_BN * nchunk; idx += SK_NT) {
-    const int r = idx / nchunk, ch = idx % nchunk;
+  if (t == 0) *reinterpret_cast<uint4*>(const_cast<unsigned char*>(zchunk)) = uint4{0, 0, 0, 0};
+  // B slice -> LDS (zero rows past N).  Slice row r = 32p + 8*(c >> 2) + 4h + (c & 3) feeds
+  // MFMA row c of tile j = 2p + h (the column permutation described above); it is stored
+  // at LDS row 32p + 16h + c, so a tile's 16 fragment rows are 16 consecutive LDS rows,
+  // read as conflict-free as the A rows.
+  for (int idx = t; idx < SK_BN * kchunks; idx += SK_NT) {
+    const int r = idx / kchunks, ch = idx % kchunks;
+    const int rl = r & 31, pos = (r & ~31) | (((rl >> 2) & 1) << 4) | ((rl >> 3) << 2) | (rl & 3);
     uint4 v{0, 0, 0, 0};
-    if (bn + r < g.N && ch < kchunks) v = *reinterpret_cast<const uint4*>(g.B + (size_t)(bn + r) * g.ldb + ch * 8);
-    *reinterpret_cast<uint4*>(Bs + r * stride + ch * 16) = v;
+    if (bn + r < g.N) v = *reinterpret_cast<const uint4*>(g.B + (size_t)(bn + r) * g.ldb + ch * 8);
+    *reinterpret_cast<uint4*>(Bs + pos * stride + ch * 16) = v;
   }
-  constexpr int kMaxPer = SK_BM * 16 / SK_NT;       // A chunks per thread at kp = 128
+  constexpr int kMaxPer = SK_BM * 16 / SK_NT;       // A chunks per thread at K = 128
   uint4 ra[kMaxPer];
-  const int per = (SK_BM * nchunk + SK_NT - 1) / SK_NT;
+  const int per = (SK_BM * kchunks + SK_NT - 1) / SK_NT;
   auto gload = [&](int m0) {
 #pragma unroll
     for (int i = 0; i < kMaxPer; ++i) {
-      const int idx = t + i * SK_NT, r = idx / nchunk, ch = idx % nchunk;
+      const int idx = t + i * SK_NT, r = idx / kchunks, ch = idx % kchunks;
       ra[i] = uint4{0, 0, 0, 0};
-      if (i < per && r < SK_BM && m0 + r < g.M && ch < kchunks) {
+      if (i < per && r < SK_BM && m0 + r < g.M) {
         if constexpr (PATCH) {
           ra[i] = patch_chunk(ps, m0 + r, ch);
           if (tn == 0 && ps.xp) *reinterpret_cast<uint4*>(ps.xp + (size_t)(m0 + r) * ps.ld_xp + ch * 8) = ra[i];
@@ -963,7 +983,7 @@ __global__ void __launch_bounds__(SK_NT) k_gemm_smallk(GemmArgs g, int kp, Patch
   auto swrite = [&](int buf) {
 #pragma unroll
     for (int i = 0; i < kMaxPer; ++i) {
-      const int idx = t + i * SK_NT, r = idx / nchunk, ch = idx % nchunk;
+      const int idx = t + i * SK_NT, r = idx / kchunks, ch = idx % kchunks;
       if (i < per && r < SK_BM) *reinterpret_cast<uint4*>(As + (buf * SK_BM + r) * stride + ch * 16) = ra[i];
     }
   };
@@ -976,10 +996,6 @@ __global__ void __launch_bounds__(SK_NT) k_gemm_smallk(GemmArgs g, int kp, Patch
   for (int pr = 0; pr < NP; ++pr)
 #pragma unroll
     for (int e = 0; e < 8; ++e) bias[pr][e] = load_bias(g, bn + wave * WN + pr * 32 + 8 * gq + e, 0);
-  // B row feeding tile j's MFMA row c (the column permutation described above)
-  int brow[NJ];
-#pragma unroll
-  for (int j = 0; j < NJ; ++j) brow[j] = wave * WN + (j >> 1) * 32 + 8 * (c >> 2) + 4 * (j & 1) + (c & 3);
   const int es = g.out_bf16 ? 2 : 4;
   const bool vec_ok = (((uint64_t)g.C | ((uint64_t)g.ldc * es)) % 16) == 0;
   int buf = 0;
@@ -995,11 +1011,14 @@ __global__ void __launch_bounds__(SK_NT) k_gemm_smallk(GemmArgs g, int kp, Patch
     const unsigned char* A = As + buf * SK_BM * stride;
     for (int ks = 0; ks < kp / 32; ++ks) {
       const int ch = 4 * ks + gq;
+      const bool z = ch >= kchunks;  // past K: the shared zero chunk
       bf16x8 fb[NJ], fa[4];
 #pragma unroll
-      for (int j = 0; j < NJ; ++j) fb[j] = *reinterpret_cast<const bf16x8*>(Bs + brow[j] * stride + ch * 16);
+      for (int j = 0; j < NJ; ++j)
+        fb[j] = *reinterpret_cast<const bf16x8*>(z ? zchunk : Bs + (wave * WN + 16 * j + c) * stride + ch * 16);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) fa[i] = *reinterpret_cast<const bf16x8*>(A + (i * 16 + c) * stride + ch * 16);
+      for (int i = 0; i < 4; ++i)
+        fa[i] = *reinterpret_cast<const bf16x8*>(z ? zchunk : A + (i * 16 + c) * stride + ch * 16);
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -1147,7 +1166,7 @@ void launch_smallk(const GemmArgs& g, int id, const PatchSrc& ps, hipStream_t st
   const int kp = (g.K + 31) / 32 * 32;
   const int skbn = (g_sk_bn == 256 && !ps.x) ? 256 : 128;
   const int tiles_n = (g.N + skbn - 1) / skbn, tiles_m = (g.M + SK_BM - 1) / SK_BM;
-  const size_t lds = (size_t)(skbn + 2 * SK_BM) * (kp * 2 + 16);
+  const size_t lds = sk_lds_bytes(skbn, g.K);
   // Every block loads its B slice once, then walks M tiles: the grid is one round of
   // resident blocks (LDS-limited per CU) with the same number of M tiles in every block
   // (an uneven split leaves half the blocks idle for the last tile).  Measured on the
