@@ -227,9 +227,133 @@ void emb_qkv_wgrad(uint64_t A, int ld_a, uint64_t We, int ld_we, uint64_t Wq, in
   CCMPI_HIP_CHECK(hipGetLastError());
 }
 
+// Forward weight fold of the same chain: h = Xp . We^T feeds only qkv = h . Wq^T + b
+// (no nonlinearity between), so qkv = Xp . Weff^T + b with
+//
+//   Weff[R][kp] = Wq[R][d] . We[d][kp]   (fp32 accumulate, bf16 out)
+//
+// and the forward runs one K = kp GEMM instead of K = kp plus K = d (the d = 768
+// QKV GEMM was 54 of the 184 us train step).  Same role as the weight-side
+// contractions above: a tiny, latency-bound fp32 product (42 MFLOP at 768 x 72).
+//   * one 512-thread workgroup per kFoldRows (3) rows of Weff; their Wq rows are staged
+//     in LDS;
+//   * thread (slice, cg): patch columns 4*cg.. (one float4 of a We row per k),
+//     k = slice, slice + ns, ... (interleaved, so the slices' LDS reads of one Wq
+//     row hit distinct banks; the column groups of one slice broadcast);
+//   * every global load of a thread -- its Wq chunks and its kFoldBatch We rows --
+//     is issued before the first use: at d = 768 that is ONE memory round trip
+//     (one load per loop trip: 19 us; 16 rows per trip: 13.7 us);
+//   * the ns slice partials meet in LDS in two fixed-order halves (deterministic).
+constexpr int kFoldNT = 512;
+constexpr int kFoldRows = 3;  // 256 workgroups at R = 768: every CU (8 rows: 96 CUs, 10.2 us)
+constexpr int kFoldBatch = 28;  // d = 768: 28 slices x 28 rows, one trip (32 spilled VGPRs)
+constexpr int kFoldMaxD = 1024;
+constexpr int kFoldWqPer = (kFoldRows * kFoldMaxD / 4 + kFoldNT - 1) / kFoldNT;  // float4 of Wq per thread
+
+__global__ void __launch_bounds__(kFoldNT) k_fold_emb_qkv(const float* __restrict__ Wq, int ld_wq,
+                                                          const float* __restrict__ We, int ld_we,
+                                                          uint16_t* __restrict__ Weff, int ld_eff, int R, int d, int kp) {
+  extern __shared__ __attribute__((aligned(16))) float fsm[];
+  const int t = threadIdx.x, r0 = blockIdx.x * kFoldRows, nv = d / 4;
+  const int ng = kp / 4, ns = kFoldNT / ng, slice = t / ng, cg = t % ng;
+  const bool act = slice < ns;
+  float4 wq[kFoldWqPer];
+#pragma unroll
+  for (int u = 0; u < kFoldWqPer; ++u) {
+    const int idx = t + u * kFoldNT, r = idx / nv, q = idx % nv;
+    wq[u] = (idx < kFoldRows * nv && r0 + r < R) ? *reinterpret_cast<const float4*>(Wq + (size_t)(r0 + r) * ld_wq + 4 * q)
+                                                  : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  float4 w[kFoldBatch];
+  auto fetch = [&](int kb) {
+#pragma unroll
+    for (int u = 0; u < kFoldBatch; ++u) {
+      const int k = kb + u * ns;
+      w[u] = (act && k < d) ? *reinterpret_cast<const float4*>(We + (size_t)k * ld_we + 4 * cg) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  int kb = slice;
+  fetch(kb);
+#pragma unroll
+  for (int u = 0; u < kFoldWqPer; ++u) {
+    const int idx = t + u * kFoldNT;
+    if (idx < kFoldRows * nv) *reinterpret_cast<float4*>(fsm + 4 * idx) = wq[u];  // row r at fsm + r * d
+  }
+  __syncthreads();
+  float acc[kFoldRows][4] = {};
+  while (true) {
+#pragma unroll
+    for (int u = 0; u < kFoldBatch; ++u) {
+      const int k = min(kb + u * ns, d - 1);  // past d: w[u] == 0, any in-range row
+#pragma unroll
+      for (int r = 0; r < kFoldRows; ++r) {
+        const float x = fsm[r * d + k];
+        acc[r][0] = fmaf(x, w[u].x, acc[r][0]);
+        acc[r][1] = fmaf(x, w[u].y, acc[r][1]);
+        acc[r][2] = fmaf(x, w[u].z, acc[r][2]);
+        acc[r][3] = fmaf(x, w[u].w, acc[r][3]);
+      }
+    }
+    kb += kFoldBatch * ns;
+    if (kb >= d) break;
+    fetch(kb);
+  }
+  // partials: slices [half, ns) write position slice - half, then slices [0, half) add
+  // theirs in place; the half positions are summed in order
+  const int half = (ns + 1) / 2;
+  __syncthreads();  // every slice is done with the Wq rows: reuse the LDS
+  auto slot = [&](int pos, int r) { return reinterpret_cast<float4*>(fsm + (pos * kFoldRows + r) * kp + 4 * cg); };
+  if (act && slice >= half)
+#pragma unroll
+    for (int r = 0; r < kFoldRows; ++r) *slot(slice - half, r) = make_float4(acc[r][0], acc[r][1], acc[r][2], acc[r][3]);
+  __syncthreads();
+  if (slice < half) {
+    const bool pair = slice + half < ns;
+#pragma unroll
+    for (int r = 0; r < kFoldRows; ++r) {
+      float4 v = make_float4(acc[r][0], acc[r][1], acc[r][2], acc[r][3]);
+      if (pair) {
+        const float4 o = *slot(slice, r);
+        v.x += o.x; v.y += o.y; v.z += o.z; v.w += o.w;
+      }
+      *slot(slice, r) = v;
+    }
+  }
+  __syncthreads();
+  for (int idx = t; idx < kFoldRows * kp; idx += kFoldNT) {
+    const int r = idx / kp, c = idx % kp;
+    if (r0 + r >= R) continue;
+    float s = 0.f;
+    for (int p = 0; p < half; ++p) s += fsm[(p * kFoldRows + r) * kp + c];
+    Weff[(size_t)(r0 + r) * ld_eff + c] = static_cast<uint16_t>(f32_to_bf16_bits(s));
+  }
+}
+
+size_t fold_lds_bytes(int d, int kp) {
+  const int half = (kFoldNT / (kp / 4) + 1) / 2;
+  return sizeof(float) * std::max<size_t>((size_t)kFoldRows * d, (size_t)half * kFoldRows * kp);
+}
+
+void fold_emb_qkv(uint64_t Wq, int ld_wq, uint64_t We, int ld_we, uint64_t Weff, int ld_eff, int R, int d, int kp,
+                  uint64_t stream) {
+  if (R <= 0 || d <= 0 || kp <= 0) return;
+  if (kp > kMaxKp || kp % 4 || d % 4 || d > kFoldMaxD || ld_wq % 4 || ld_we % 4 || (Wq % 16) || (We % 16) || !Weff)
+    throw std::invalid_argument("fold_emb_qkv: kp <= 96, d <= 1024, kp / d / fp32 row strides % 4 == 0, 16-B aligned fp32 operands");
+  const size_t lds = fold_lds_bytes(d, kp);
+  if (lds > 64 * 1024) throw std::invalid_argument("fold_emb_qkv: LDS staging exceeds 64 KiB");
+  hipLaunchKernelGGL(k_fold_emb_qkv, dim3((R + kFoldRows - 1) / kFoldRows), dim3(kFoldNT), lds, (hipStream_t)stream,
+                     reinterpret_cast<const float*>(Wq), ld_wq, reinterpret_cast<const float*>(We), ld_we,
+                     reinterpret_cast<uint16_t*>(Weff), ld_eff, R, d, kp);
+  CCMPI_HIP_CHECK(hipGetLastError());
+}
+
 }  // namespace
 
 void register_wgrad_ops(pybind11::module_& m) {
+  m.def("fold_emb_qkv", &fold_emb_qkv, "Weff (bf16) = Wq . We, fp32 accumulate, fixed summation order",
+        pybind11::arg("Wq"), pybind11::arg("ld_wq"), pybind11::arg("We"), pybind11::arg("ld_we"), pybind11::arg("Weff"),
+        pybind11::arg("ld_eff"), pybind11::arg("R"), pybind11::arg("d"), pybind11::arg("kp"), pybind11::arg("stream"),
+        pybind11::call_guard<pybind11::gil_scoped_release>());
   m.def("emb_qkv_wgrad", &emb_qkv_wgrad,
         "Gq += A . We^T (fixed order); Ge += Wq^T . A (fp32 atomics; Ge = 0: skipped); Z = 0 (Z = 0: skipped)",
         pybind11::arg("A"), pybind11::arg("ld_a"), pybind11::arg("We"), pybind11::arg("ld_we"), pybind11::arg("Wq"),

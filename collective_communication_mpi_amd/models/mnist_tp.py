@@ -44,7 +44,12 @@ kernel; the optimizer is one fused AdamW pass.  Fusions that remove whole passes
   h = Xp W_emb^T, dW_qkv = dQKV^T h = A W_emb^T (``qkv_grad="reassoc"``).  The
   840-column dQKV^T . [h | xp] GEMM (65 us) becomes a 72-column one (~20 us) plus
   one fp32 kernel for both weight-sized products (csrc/device/wgrad.hip), which
-  also zeroes the next step's A buffer (the split-K GEMM accumulates into it).
+  also zeroes the next step's A buffer (the split-K GEMM accumulates into it);
+* the forward folds the same chain (``fold_emb``): h feeds nothing but the QKV
+  projection, so qkv = Xp . W_eff^T + b with W_eff = W_qkv W_emb (3hd x 72, one
+  fp32 kernel per forward, 42 MFLOP).  The 32768 x 768 x 768 QKV GEMM (54 us)
+  and the 32768 x 768 x 72 embedding GEMM become ONE 72-deep GEMM; h (50 MB)
+  is neither written nor read.
 """
 from __future__ import annotations
 
@@ -87,6 +92,9 @@ class LayerConfig:
     qkv_grad: str = "reassoc"
     fuse_fc_o: bool = True   # pooled fc_o inside the attention kernels (fwd logits, bwd dpool) instead of GEMMs
     fwd_chunks: int = 1      # forward_images: row blocks run on that many HIP streams (1 = one stream)
+    # forward: qkv = Xp . (W_qkv W_emb)^T + b -- h is never formed (needs the re-associated
+    # backward, which does not read h); False: h = Xp . W_emb^T, then qkv = h . W_qkv^T + b
+    fold_emb: bool = True
 
     @property
     def seq(self) -> int:
@@ -233,7 +241,25 @@ class MnistTPLayer:
         hx = self._buf("hx", (B * cfg.seq, self._hx_ld), torch.bfloat16)
         return hx[:, cfg.d_model:cfg.d_model + cfg.kp]
 
-    def forward(self, xp: torch.Tensor, B: int, images: Optional[torch.Tensor] = None) -> torch.Tensor:
+    def _folds(self) -> bool:
+        cfg = self.cfg
+        return cfg.fold_emb and cfg.emb_grad == "reassoc" and cfg.qkv_grad == "reassoc"
+
+    def folded_qkv_weight(self, stream=None) -> torch.Tensor:
+        """W_eff = W_qkv . W_emb (3hd x kp bf16) from the fp32 master weights (fp32
+        accumulation, fixed summation order), recomputed on every forward so it always
+        follows the optimizer (and is captured into the step's HIP graph)."""
+        cfg = self.cfg
+        R = 3 * self.hd
+        weff = self._buf("weff", (R, cfg.kp), torch.bfloat16)
+        wq, we = self.flat.param("qkv_w"), self.flat.param("emb_w")
+        st = stream if stream is not None else torch.cuda.current_stream(self.device).cuda_stream
+        _native.device().fold_emb_qkv(wq.data_ptr(), wq.stride(0), we.data_ptr(), we.stride(0), weff.data_ptr(),
+                                      weff.stride(0), R, cfg.d_model, cfg.kp, st)
+        return weff
+
+    def forward(self, xp: torch.Tensor, B: int, images: Optional[torch.Tensor] = None,
+                weff: Optional[torch.Tensor] = None) -> torch.Tensor:
         """xp: (B*S, kp) bf16 patches -> logits (B, n_classes) fp32.  Saves activations.
         xp is either ``input_buffer(B)`` (fused [h | xp] layout) or any other tensor.
         With ``images`` ((B, 784) fp32) and the fused layout, the patch rows are
@@ -245,8 +271,16 @@ class MnistTPLayer:
         P16 = self.flat.param16
         hx = self._bufs.get(("hx", (M, self._hx_ld), torch.bfloat16))
         fused = hx is not None and xp.data_ptr() == hx.data_ptr() + 2 * d and xp.stride(0) == hx.stride(0)
-        h = hx[:, :d] if fused else self._buf("h", (M, d), torch.bfloat16)
-        if images is not None and not fused:
+        qkv = self._buf("qkv", (M, 3 * self.hd), torch.bfloat16)
+        h = None
+        if self._folds():
+            if images is not None:
+                patchify(images, cfg, out=xp)
+            gemm_nt(xp, weff if weff is not None else self.folded_qkv_weight(), out=qkv, bias=self.flat.param("qkv_b"))
+            images = None
+        else:
+            h = hx[:, :d] if fused else self._buf("h", (M, d), torch.bfloat16)
+        if h is not None and images is not None and not fused:
             patchify(images, cfg, out=xp)
             images = None
         if images is not None:
@@ -255,10 +289,10 @@ class MnistTPLayer:
             _native.device().embed_patches(x.data_ptr(), w.data_ptr(), h.data_ptr(), B, cfg.img, cfg.patch, d, cfg.kp,
                                            w.stride(0), h.stride(0), xp.data_ptr(), xp.stride(0),
                                            torch.cuda.current_stream(self.device).cuda_stream)
-        else:
+        elif h is not None:
             gemm_nt(xp, P16("emb_w"), out=h)  # bias + position are columns of W_emb
-        qkv = self._buf("qkv", (M, 3 * self.hd), torch.bfloat16)
-        gemm_nt(h, P16("qkv_w"), out=qkv, bias=self.flat.param("qkv_b"))
+        if h is not None:
+            gemm_nt(h, P16("qkv_w"), out=qkv, bias=self.flat.param("qkv_b"))
         lse = self._buf("lse", (B * self.hl, S), torch.float32)
         D = _native.device()
         st = torch.cuda.current_stream(self.device).cuda_stream
@@ -319,13 +353,17 @@ class MnistTPLayer:
         S = cfg.seq
         if (c == 1 or B % c or not self._fused_fc_o() or not (S <= 16 and cfg.head_dim in (32, 64, 128))
                 or (B // c) * S < 256):
+            # (running the weight fold on a side stream concurrent with patchify measured
+            # slower: train step 0.140 -> 0.159 ms, forward 0.061 -> 0.066 ms)
             patchify(images, cfg, out=xp)
             return self.forward(xp, B)
         d, hl, hd = cfg.d_model, self.hl, self.hd
         M = B * S
         P16 = self.flat.param16
         hx = self._bufs.get(("hx", (M, self._hx_ld), torch.bfloat16))
-        h = hx[:, :d] if hx is not None else self._buf("h", (M, d), torch.bfloat16)
+        folds = self._folds()
+        h = None if folds else (hx[:, :d] if hx is not None else self._buf("h", (M, d), torch.bfloat16))
+        weff = self.folded_qkv_weight() if folds else None  # on the main stream, before the fork
         qkv = self._buf("qkv", (M, 3 * hd), torch.bfloat16)
         lse = self._buf("lse", (B * hl, S), torch.float32)
         pool = self._buf("pool", (B, hd), torch.bfloat16)
@@ -345,8 +383,11 @@ class MnistTPLayer:
             r0, r1 = b0 * S, b1 * S
             with torch.cuda.stream(s):
                 patchify(images[b0:b1], cfg, out=xp[r0:r1])
-                gemm_nt(xp[r0:r1], P16("emb_w"), out=h[r0:r1])
-                gemm_nt(h[r0:r1], P16("qkv_w"), out=qkv[r0:r1], bias=bias)
+                if folds:
+                    gemm_nt(xp[r0:r1], weff, out=qkv[r0:r1], bias=bias)
+                else:
+                    gemm_nt(xp[r0:r1], P16("emb_w"), out=h[r0:r1])
+                    gemm_nt(h[r0:r1], P16("qkv_w"), out=qkv[r0:r1], bias=bias)
                 D.attn_small_fwd(qkv[r0:r1].data_ptr(), 0, lse[b0 * hl:b1 * hl].data_ptr(), Bc, S, hl, cfg.head_dim,
                                  qkv.stride(0), hd, 1.0 / math.sqrt(cfg.head_dim), pool[b0:b1].data_ptr(),
                                  pool.stride(0), s.cuda_stream, wo=wo.data_ptr(), ld_wo=wo.stride(0),

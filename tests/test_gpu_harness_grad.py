@@ -27,17 +27,19 @@ def _reference(cfg, xp, y, P):
     return loss.detach(), {k: t.grad for k, t in w.items()}
 
 
-@pytest.mark.parametrize("emb_grad,qkv_grad,fused,fuse_fc_o", [
-    ("reassoc", "reassoc", True, True), ("reassoc", "reassoc", True, False), ("reassoc", "reassoc", False, True),
-    ("reassoc", "direct", True, True), ("reassoc", "direct", False, True),
-    ("dh", "direct", True, True), ("dh", "direct", False, False)])
-def test_harness_grads_match_torch_fp32(emb_grad, qkv_grad, fused, fuse_fc_o):
+@pytest.mark.parametrize("emb_grad,qkv_grad,fused,fuse_fc_o,fold_emb", [
+    ("reassoc", "reassoc", True, True, True), ("reassoc", "reassoc", True, False, True),
+    ("reassoc", "reassoc", False, True, True), ("reassoc", "reassoc", False, True, False),
+    ("reassoc", "direct", True, True, True), ("reassoc", "direct", False, True, True),
+    ("dh", "direct", True, True, True), ("dh", "direct", False, False, True)])
+def test_harness_grads_match_torch_fp32(emb_grad, qkv_grad, fused, fuse_fc_o, fold_emb):
     from collective_communication_mpi_amd import MPI, Communicator
     from collective_communication_mpi_amd.models.harness import build
     from collective_communication_mpi_amd.models.mnist_tp import local_batch, patchify
 
     comm = Communicator(MPI.COMM_WORLD)
-    cfg, layer, x_all, y_all = build(comm, 1, 128, emb_grad=emb_grad, qkv_grad=qkv_grad, fuse_fc_o=fuse_fc_o)
+    cfg, layer, x_all, y_all = build(comm, 1, 128, emb_grad=emb_grad, qkv_grad=qkv_grad, fuse_fc_o=fuse_fc_o,
+                                     fold_emb=fold_emb)
     # non-trivial biases so their gradients and the bias epilogues are exercised
     g = torch.Generator().manual_seed(7)
     layer.flat.param("qkv_b").copy_(torch.randn(layer.flat.param("qkv_b").shape, generator=g) * 0.1)
@@ -84,7 +86,8 @@ def test_chunked_multistream_forward_is_bitwise_identical(chunks):
         layer.loss_and_grad_fused(yb, cfg.batch)
         layer.backward(None)
         torch.cuda.synchronize()
-        out[c] = (logits, h.clone(), qkv.clone(), lse.clone(), pool.clone(), layer.flat.g.clone())
+        assert (h is None) == layer._folds()  # the folded forward never forms h
+        out[c] = (logits, qkv.clone(), lse.clone(), pool.clone(), layer.flat.g.clone())
     for a, b in zip(out[1][:-1], out[chunks][:-1]):
         assert torch.equal(a, b)
     # the weight gradients go through split-K fp32 atomics: equal up to summation order

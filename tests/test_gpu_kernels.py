@@ -551,3 +551,21 @@ def test_gemm_multistage(stages, M, N, K):
     torch.testing.assert_close(y2, ref, rtol=2e-3, atol=2e-3 * K ** 0.5)
     torch.testing.assert_close(yb.float(), ref + bias, rtol=2e-2, atol=5e-2 * K ** 0.5 / 8)
     torch.testing.assert_close(c, c0 + ref, rtol=2e-3, atol=2e-3 * K ** 0.5)
+
+
+@pytest.mark.parametrize("R,d,kp", [(768, 768, 72), (384, 768, 72), (20, 36, 16), (7, 100, 96)])
+def test_fold_emb_qkv_matches_fp32(R, d, kp):
+    """W_eff = W_qkv . W_emb (fp32 accumulate, bf16 out) against torch fp32, incl. a
+    ragged last row block and strided operands."""
+    from collective_communication_mpi_amd import _native
+
+    torch.manual_seed(R + d)
+    wq = torch.randn(R, d + 4, device="cuda")[:, :d]
+    we = torch.randn(d, kp + 8, device="cuda")[:, :kp]
+    out = torch.full((R, kp + 8), float("nan"), device="cuda").bfloat16()
+    _native.device().fold_emb_qkv(wq.data_ptr(), wq.stride(0), we.data_ptr(), we.stride(0), out.data_ptr(),
+                                  out.stride(0), R, d, kp, torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    ref = wq.double() @ we.double()
+    torch.testing.assert_close(out[:, :kp].double(), ref, rtol=8e-3, atol=8e-3 * ref.abs().max().item())
+    assert torch.isnan(out[:, kp:].float()).all()  # columns past kp untouched
