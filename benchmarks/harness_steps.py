@@ -26,7 +26,7 @@ cfg, layer, x_all, y_all = build(comm, args.tp, args.batch)
 xb, yb = local_batch(cfg, x_all, y_all, 0, comm.Get_rank(), layer.device)
 for _ in range(args.steps):
     if args.mode == "fwd":
-        layer.forward_images(xb, cfg.batch)
+        layer.forward_images(xb, cfg.batch, save=False)  # inference forward, as bench.py times it
     else:
         train_step(layer, cfg, xb, yb)
 torch.cuda.synchronize()

@@ -252,7 +252,8 @@ constexpr int kFoldWqPer = (kFoldRows * kFoldMaxD / 4 + kFoldNT - 1) / kFoldNT; 
 
 __global__ void __launch_bounds__(kFoldNT) k_fold_emb_qkv(const float* __restrict__ Wq, int ld_wq,
                                                           const float* __restrict__ We, int ld_we,
-                                                          uint16_t* __restrict__ Weff, int ld_eff, int R, int d, int kp) {
+                                                          uint16_t* __restrict__ Weff, int ld_eff, int R, int d, int kp,
+                                                          const float* __restrict__ bias, int bias_col) {
   extern __shared__ __attribute__((aligned(16))) float fsm[];
   const int t = threadIdx.x, r0 = blockIdx.x * kFoldRows, nv = d / 4;
   const int ng = kp / 4, ns = kFoldNT / ng, slice = t / ng, cg = t % ng;
@@ -325,6 +326,7 @@ __global__ void __launch_bounds__(kFoldNT) k_fold_emb_qkv(const float* __restric
     if (r0 + r >= R) continue;
     float s = 0.f;
     for (int p = 0; p < half; ++p) s += fsm[(p * kFoldRows + r) * kp + c];
+    if (bias && c == bias_col) s += bias[r0 + r];  // Xp's constant-1 column carries the QKV bias
     Weff[(size_t)(r0 + r) * ld_eff + c] = static_cast<uint16_t>(f32_to_bf16_bits(s));
   }
 }
@@ -335,7 +337,8 @@ size_t fold_lds_bytes(int d, int kp) {
 }
 
 void fold_emb_qkv(uint64_t Wq, int ld_wq, uint64_t We, int ld_we, uint64_t Weff, int ld_eff, int R, int d, int kp,
-                  uint64_t stream) {
+                  uint64_t stream, uint64_t bias, int bias_col) {
+  if (bias && (bias_col < 0 || bias_col >= kp)) throw std::invalid_argument("fold_emb_qkv: bias_col outside [0, kp)");
   if (R <= 0 || d <= 0 || kp <= 0) return;
   if (kp > kMaxKp || kp % 4 || d % 4 || d > kFoldMaxD || ld_wq % 4 || ld_we % 4 || (Wq % 16) || (We % 16) || !Weff)
     throw std::invalid_argument("fold_emb_qkv: kp <= 96, d <= 1024, kp / d / fp32 row strides % 4 == 0, 16-B aligned fp32 operands");
@@ -343,17 +346,18 @@ void fold_emb_qkv(uint64_t Wq, int ld_wq, uint64_t We, int ld_we, uint64_t Weff,
   if (lds > 64 * 1024) throw std::invalid_argument("fold_emb_qkv: LDS staging exceeds 64 KiB");
   hipLaunchKernelGGL(k_fold_emb_qkv, dim3((R + kFoldRows - 1) / kFoldRows), dim3(kFoldNT), lds, (hipStream_t)stream,
                      reinterpret_cast<const float*>(Wq), ld_wq, reinterpret_cast<const float*>(We), ld_we,
-                     reinterpret_cast<uint16_t*>(Weff), ld_eff, R, d, kp);
+                     reinterpret_cast<uint16_t*>(Weff), ld_eff, R, d, kp, reinterpret_cast<const float*>(bias), bias_col);
   CCMPI_HIP_CHECK(hipGetLastError());
 }
 
 }  // namespace
 
 void register_wgrad_ops(pybind11::module_& m) {
-  m.def("fold_emb_qkv", &fold_emb_qkv, "Weff (bf16) = Wq . We, fp32 accumulate, fixed summation order",
+  m.def("fold_emb_qkv", &fold_emb_qkv,
+        "Weff (bf16) = Wq . We (+ bias in column bias_col), fp32 accumulate, fixed summation order",
         pybind11::arg("Wq"), pybind11::arg("ld_wq"), pybind11::arg("We"), pybind11::arg("ld_we"), pybind11::arg("Weff"),
         pybind11::arg("ld_eff"), pybind11::arg("R"), pybind11::arg("d"), pybind11::arg("kp"), pybind11::arg("stream"),
-        pybind11::call_guard<pybind11::gil_scoped_release>());
+        pybind11::arg("bias") = 0, pybind11::arg("bias_col") = -1, pybind11::call_guard<pybind11::gil_scoped_release>());
   m.def("emb_qkv_wgrad", &emb_qkv_wgrad,
         "Gq += A . We^T (fixed order); Ge += Wq^T . A (fp32 atomics; Ge = 0: skipped); Z = 0 (Z = 0: skipped)",
         pybind11::arg("A"), pybind11::arg("ld_a"), pybind11::arg("We"), pybind11::arg("ld_we"), pybind11::arg("Wq"),

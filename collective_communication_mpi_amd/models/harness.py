@@ -64,8 +64,8 @@ def bench_forward(comm, tp: int = 2, batch: int = 2048, steps: int = 20, warmup:
     cfg, layer, x_all, y_all = build(comm, tp, batch)
     xb, yb = local_batch(cfg, x_all, y_all, 0, rank, layer.device)
 
-    def fwd():
-        return layer.forward_images(xb, cfg.batch)
+    def fwd():  # inference forward: no activations kept for a backward
+        return layer.forward_images(xb, cfg.batch, save=False)
 
     for _ in range(3):
         fwd()
@@ -114,7 +114,8 @@ def bench_forward(comm, tp: int = 2, batch: int = 2048, steps: int = 20, warmup:
     loss_v = hc.allreduce(float(loss.item()), op=MPI.SUM) / cfg.tp  # sum over DP of per-replica shares
     return {"tp": cfg.tp, "dp": cfg.dp, "fwd_ms": fwd_s * 1e3, "train_ms": train_s * 1e3,
             "global_batch": cfg.batch * cfg.dp, "seq_len": cfg.seq, "tokens_per_step": cfg.batch * cfg.dp * cfg.seq,
-            "hip_graph": used_graph, "fc_o_mode": cfg.fc_o_mode, "loss": round(loss_v, 5)}
+            "hip_graph": used_graph, "fc_o_mode": cfg.fc_o_mode,
+            "fwd_saves_activations": False, "qkv_in_attention": layer._fuses_proj(), "loss": round(loss_v, 5)}
 
 
 def smoke_step(comm) -> None:

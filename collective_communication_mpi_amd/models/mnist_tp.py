@@ -95,6 +95,13 @@ class LayerConfig:
     # forward: qkv = Xp . (W_qkv W_emb)^T + b -- h is never formed (needs the re-associated
     # backward, which does not read h); False: h = Xp . W_emb^T, then qkv = h . W_qkv^T + b
     fold_emb: bool = True
+    # with fold_emb: the projection qkv = Xp . W_eff^T runs inside the attention forward
+    # kernel (W_eff rows in registers); qkv is written only when the forward saves
+    # activations for a backward.  Off by default: measured slower (rocprofv3, 32768
+    # tokens): 41.9 us inference / 53.6 us saving vs 16.6 us attention + 23.0 us GEMM --
+    # the 144 W registers per wave leave one wave per SIMD and the persistent waves
+    # run their 8 sequences back to back, latency-bound (profiles/r1_fold/)
+    fuse_qkv_attn: bool = False
 
     @property
     def seq(self) -> int:
@@ -245,21 +252,28 @@ class MnistTPLayer:
         cfg = self.cfg
         return cfg.fold_emb and cfg.emb_grad == "reassoc" and cfg.qkv_grad == "reassoc"
 
-    def folded_qkv_weight(self, stream=None) -> torch.Tensor:
+    def _fuses_proj(self) -> bool:
+        cfg = self.cfg
+        return (cfg.fuse_qkv_attn and self._folds() and self._fused_fc_o() and cfg.seq <= 16
+                and cfg.head_dim in (32, 64) and 4 % self.hl == 0)
+
+    def folded_qkv_weight(self, stream=None, with_bias: bool = False) -> torch.Tensor:
         """W_eff = W_qkv . W_emb (3hd x kp bf16) from the fp32 master weights (fp32
         accumulation, fixed summation order), recomputed on every forward so it always
-        follows the optimizer (and is captured into the step's HIP graph)."""
+        follows the optimizer (and is captured into the step's HIP graph).  with_bias:
+        b_qkv is added to the column that multiplies Xp's constant-1 column."""
         cfg = self.cfg
         R = 3 * self.hd
-        weff = self._buf("weff", (R, cfg.kp), torch.bfloat16)
+        weff = self._buf("weff_b" if with_bias else "weff", (R, cfg.kp), torch.bfloat16)
         wq, we = self.flat.param("qkv_w"), self.flat.param("emb_w")
         st = stream if stream is not None else torch.cuda.current_stream(self.device).cuda_stream
+        bias = self.flat.param("qkv_b").data_ptr() if with_bias else 0
         _native.device().fold_emb_qkv(wq.data_ptr(), wq.stride(0), we.data_ptr(), we.stride(0), weff.data_ptr(),
-                                      weff.stride(0), R, cfg.d_model, cfg.kp, st)
+                                      weff.stride(0), R, cfg.d_model, cfg.kp, st, bias=bias, bias_col=cfg.pixels)
         return weff
 
     def forward(self, xp: torch.Tensor, B: int, images: Optional[torch.Tensor] = None,
-                weff: Optional[torch.Tensor] = None) -> torch.Tensor:
+                weff: Optional[torch.Tensor] = None, save: bool = True) -> torch.Tensor:
         """xp: (B*S, kp) bf16 patches -> logits (B, n_classes) fp32.  Saves activations.
         xp is either ``input_buffer(B)`` (fused [h | xp] layout) or any other tensor.
         With ``images`` ((B, 784) fp32) and the fused layout, the patch rows are
@@ -273,7 +287,14 @@ class MnistTPLayer:
         fused = hx is not None and xp.data_ptr() == hx.data_ptr() + 2 * d and xp.stride(0) == hx.stride(0)
         qkv = self._buf("qkv", (M, 3 * self.hd), torch.bfloat16)
         h = None
-        if self._folds():
+        proj = self._fuses_proj()
+        if proj:
+            # projection inside the attention kernel (below); W_eff carries b_qkv
+            if images is not None:
+                patchify(images, cfg, out=xp)
+            weff = self.folded_qkv_weight(with_bias=True)
+            images = None
+        elif self._folds():
             if images is not None:
                 patchify(images, cfg, out=xp)
             gemm_nt(xp, weff if weff is not None else self.folded_qkv_weight(), out=qkv, bias=self.flat.param("qkv_b"))
@@ -312,7 +333,12 @@ class MnistTPLayer:
             wo = self.flat.param16("o_w")
             fc = dict(wo=wo.data_ptr(), ld_wo=wo.stride(0), n_out=cfg.out_pad, zp=zp.data_ptr(), ld_zp=zp.stride(0),
                       bo=self.flat.param("o_b").data_ptr() if self.tp_idx == 0 else 0)
-        D.attn_small_fwd(qkv.data_ptr(), 0 if att is None else att.data_ptr(), lse.data_ptr(), B, S, self.hl,
+        if proj:
+            if xp.stride(1) != 1:
+                raise ValueError("forward: xp needs unit column stride")
+            fc.update(xp=xp.data_ptr(), ld_xp=xp.stride(0), kp=cfg.kp, weff=weff.data_ptr(), ld_weff=weff.stride(0),
+                      qkv_out=qkv.data_ptr() if save else 0)
+        D.attn_small_fwd(0 if proj else qkv.data_ptr(), 0 if att is None else att.data_ptr(), lse.data_ptr(), B, S, self.hl,
                          cfg.head_dim, qkv.stride(0), self.hd if att is None else att.stride(0),
                          1.0 / math.sqrt(cfg.head_dim),
                          0 if pool is None else pool.data_ptr(), 0 if pool is None else pool.stride(0), st, **fc)
@@ -332,11 +358,11 @@ class MnistTPLayer:
             logits = zp[:, : cfg.n_classes]  # bias already included
         if naive:
             logits = logits + self.flat.param("o_b")[: cfg.n_classes]
-        self._saved = (xp, h, qkv, att, lse, B, pool)
+        self._saved = (xp, h, qkv, att, lse, B, pool) if save else None
         self._hx = hx[:, : d + cfg.kp] if fused else None
         return logits
 
-    def forward_images(self, images: torch.Tensor, B: int) -> torch.Tensor:
+    def forward_images(self, images: torch.Tensor, B: int, save: bool = True) -> torch.Tensor:
         """(B, 784) fp32 images -> logits: patchify into the fused [h | xp] rows, then
         ``forward``.  With ``cfg.fwd_chunks = c > 1`` the batch is cut into c row blocks
         whose patchify -> embedding GEMM -> QKV GEMM -> attention chains run on c HIP
@@ -356,14 +382,16 @@ class MnistTPLayer:
             # (running the weight fold on a side stream concurrent with patchify measured
             # slower: train step 0.140 -> 0.159 ms, forward 0.061 -> 0.066 ms)
             patchify(images, cfg, out=xp)
-            return self.forward(xp, B)
+            return self.forward(xp, B, save=save)
         d, hl, hd = cfg.d_model, self.hl, self.hd
         M = B * S
         P16 = self.flat.param16
         hx = self._bufs.get(("hx", (M, self._hx_ld), torch.bfloat16))
         folds = self._folds()
         h = None if folds else (hx[:, :d] if hx is not None else self._buf("h", (M, d), torch.bfloat16))
-        weff = self.folded_qkv_weight() if folds else None  # on the main stream, before the fork
+        proj = self._fuses_proj()
+        # on the main stream, before the fork
+        weff = self.folded_qkv_weight(with_bias=proj) if folds else None
         qkv = self._buf("qkv", (M, 3 * hd), torch.bfloat16)
         lse = self._buf("lse", (B * hl, S), torch.float32)
         pool = self._buf("pool", (B, hd), torch.bfloat16)
@@ -383,20 +411,24 @@ class MnistTPLayer:
             r0, r1 = b0 * S, b1 * S
             with torch.cuda.stream(s):
                 patchify(images[b0:b1], cfg, out=xp[r0:r1])
-                if folds:
+                pj = {}
+                if proj:  # projection inside the attention kernel
+                    pj = dict(xp=xp[r0:r1].data_ptr(), ld_xp=xp.stride(0), kp=cfg.kp, weff=weff.data_ptr(),
+                              ld_weff=weff.stride(0), qkv_out=qkv[r0:r1].data_ptr() if save else 0)
+                elif folds:
                     gemm_nt(xp[r0:r1], weff, out=qkv[r0:r1], bias=bias)
                 else:
                     gemm_nt(xp[r0:r1], P16("emb_w"), out=h[r0:r1])
                     gemm_nt(h[r0:r1], P16("qkv_w"), out=qkv[r0:r1], bias=bias)
-                D.attn_small_fwd(qkv[r0:r1].data_ptr(), 0, lse[b0 * hl:b1 * hl].data_ptr(), Bc, S, hl, cfg.head_dim,
-                                 qkv.stride(0), hd, 1.0 / math.sqrt(cfg.head_dim), pool[b0:b1].data_ptr(),
+                D.attn_small_fwd(0 if proj else qkv[r0:r1].data_ptr(), 0, lse[b0 * hl:b1 * hl].data_ptr(), Bc, S, hl,
+                                 cfg.head_dim, qkv.stride(0), hd, 1.0 / math.sqrt(cfg.head_dim), pool[b0:b1].data_ptr(),
                                  pool.stride(0), s.cuda_stream, wo=wo.data_ptr(), ld_wo=wo.stride(0),
-                                 n_out=cfg.out_pad, zp=zp[b0:b1].data_ptr(), ld_zp=zp.stride(0), bo=bo)
+                                 n_out=cfg.out_pad, zp=zp[b0:b1].data_ptr(), ld_zp=zp.stride(0), bo=bo, **pj)
         for s in self._bufs[key]:
             main.wait_stream(s)
         if self.tp_dev is not None:
             self.tp_dev.allreduce(zp, zp, "SUM")  # row-parallel: one TP all-reduce (B x 16 fp32)
-        self._saved = (xp, h, qkv, None, lse, B, pool)
+        self._saved = (xp, h, qkv, None, lse, B, pool) if save else None
         self._hx = hx[:, : d + cfg.kp] if hx is not None else None
         return zp[:, : cfg.n_classes]
 
@@ -465,6 +497,8 @@ class MnistTPLayer:
         """dlogits=None: the fused head (loss_and_grad_fused) already wrote dZ and dL/d o_b."""
         cfg = self.cfg
         self.flat.grad_dirty = True
+        if self._saved is None:
+            raise RuntimeError("backward: the last forward ran with save=False (no activations kept)")
         xp, h, qkv, att, lse, B, pool = self._saved
         S, d = cfg.seq, cfg.d_model
         M = B * S

@@ -27,19 +27,20 @@ def _reference(cfg, xp, y, P):
     return loss.detach(), {k: t.grad for k, t in w.items()}
 
 
-@pytest.mark.parametrize("emb_grad,qkv_grad,fused,fuse_fc_o,fold_emb", [
-    ("reassoc", "reassoc", True, True, True), ("reassoc", "reassoc", True, False, True),
-    ("reassoc", "reassoc", False, True, True), ("reassoc", "reassoc", False, True, False),
-    ("reassoc", "direct", True, True, True), ("reassoc", "direct", False, True, True),
-    ("dh", "direct", True, True, True), ("dh", "direct", False, False, True)])
-def test_harness_grads_match_torch_fp32(emb_grad, qkv_grad, fused, fuse_fc_o, fold_emb):
+@pytest.mark.parametrize("emb_grad,qkv_grad,fused,fuse_fc_o,fold_emb,fuse_qkv_attn", [
+    ("reassoc", "reassoc", True, True, True, True), ("reassoc", "reassoc", True, False, True, True),
+    ("reassoc", "reassoc", False, True, True, True), ("reassoc", "reassoc", False, True, True, False),
+    ("reassoc", "reassoc", False, True, False, False),
+    ("reassoc", "direct", True, True, True, True), ("reassoc", "direct", False, True, True, True),
+    ("dh", "direct", True, True, True, True), ("dh", "direct", False, False, True, True)])
+def test_harness_grads_match_torch_fp32(emb_grad, qkv_grad, fused, fuse_fc_o, fold_emb, fuse_qkv_attn):
     from collective_communication_mpi_amd import MPI, Communicator
     from collective_communication_mpi_amd.models.harness import build
     from collective_communication_mpi_amd.models.mnist_tp import local_batch, patchify
 
     comm = Communicator(MPI.COMM_WORLD)
     cfg, layer, x_all, y_all = build(comm, 1, 128, emb_grad=emb_grad, qkv_grad=qkv_grad, fuse_fc_o=fuse_fc_o,
-                                     fold_emb=fold_emb)
+                                     fold_emb=fold_emb, fuse_qkv_attn=fuse_qkv_attn)
     # non-trivial biases so their gradients and the bias epilogues are exercised
     g = torch.Generator().manual_seed(7)
     layer.flat.param("qkv_b").copy_(torch.randn(layer.flat.param("qkv_b").shape, generator=g) * 0.1)
@@ -92,3 +93,22 @@ def test_chunked_multistream_forward_is_bitwise_identical(chunks):
         assert torch.equal(a, b)
     # the weight gradients go through split-K fp32 atomics: equal up to summation order
     torch.testing.assert_close(out[chunks][-1], out[1][-1], rtol=1e-4, atol=1e-6)
+
+
+def test_inference_forward_matches_training_forward():
+    """forward_images(save=False) (no qkv written, nothing kept) gives the same logits as
+    the saving forward, and a backward after it fails loudly."""
+    from collective_communication_mpi_amd import MPI, Communicator
+    from collective_communication_mpi_amd.models.harness import build
+    from collective_communication_mpi_amd.models.mnist_tp import local_batch
+
+    comm = Communicator(MPI.COMM_WORLD)
+    cfg, layer, x_all, y_all = build(comm, 1, 256, fuse_qkv_attn=True)
+    assert layer._fuses_proj()
+    xb, _ = local_batch(cfg, x_all, y_all, 0, 0, layer.device)
+    a = layer.forward_images(xb, cfg.batch).clone()
+    b = layer.forward_images(xb, cfg.batch, save=False).clone()
+    torch.cuda.synchronize()
+    assert torch.equal(a, b)
+    with pytest.raises(RuntimeError):
+        layer.backward(None)

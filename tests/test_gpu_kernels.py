@@ -569,3 +569,42 @@ def test_fold_emb_qkv_matches_fp32(R, d, kp):
     ref = wq.double() @ we.double()
     torch.testing.assert_close(out[:, :kp].double(), ref, rtol=8e-3, atol=8e-3 * ref.abs().max().item())
     assert torch.isnan(out[:, kp:].float()).all()  # columns past kp untouched
+
+
+@pytest.mark.parametrize("B,Hl,D", [(300, 4, 64), (97, 2, 64), (64, 4, 32), (33, 1, 64)])
+def test_attention_fused_projection(B, Hl, D):
+    """Attention forward with the QKV projection inside the kernel (Xp . Weff^T, W rows in
+    registers) against the same kernel fed a torch-projected qkv: the written-out qkv rows,
+    lse, pooled output and fused fc_o logits."""
+    from collective_communication_mpi_amd import _native
+
+    dev = _native.device()
+    torch.manual_seed(B * Hl + D)
+    S, kp, nout = 16, 72, 16
+    HD = Hl * D
+    xp = (torch.rand(B * S, kp, device="cuda") * 2 - 1).bfloat16()
+    xp[:, 50:] = 0
+    weff = (torch.randn(3 * HD, kp, device="cuda") * 0.2).bfloat16()
+    wo = (torch.randn(nout, HD, device="cuda") * 0.1).bfloat16()
+    bo = torch.randn(nout, device="cuda")
+    qkv_ref = (xp.float() @ weff.float().t()).bfloat16()
+    st = torch.cuda.current_stream().cuda_stream
+    outs = []
+    for proj in (False, True):
+        qkv_out = torch.full((B * S, 3 * HD), float("nan"), device="cuda").bfloat16()
+        lse = torch.empty(B * Hl, S, device="cuda")
+        pool = torch.empty(B, HD, device="cuda").bfloat16()
+        zp = torch.empty(B, nout, device="cuda")
+        kw = dict(wo=wo.data_ptr(), ld_wo=wo.stride(0), n_out=nout, zp=zp.data_ptr(), ld_zp=zp.stride(0),
+                  bo=bo.data_ptr())
+        if proj:
+            kw.update(xp=xp.data_ptr(), ld_xp=xp.stride(0), kp=kp, weff=weff.data_ptr(), ld_weff=weff.stride(0),
+                      qkv_out=qkv_out.data_ptr())
+        dev.attn_small_fwd(0 if proj else qkv_ref.data_ptr(), 0, lse.data_ptr(), B, S, Hl, D, 3 * HD, HD,
+                           D ** -0.5, pool.data_ptr(), pool.stride(0), st, **kw)
+        torch.cuda.synchronize()
+        outs.append((qkv_out, lse, pool, zp))
+    qkv_out = outs[1][0]
+    torch.testing.assert_close(qkv_out.float(), qkv_ref.float(), rtol=1e-2, atol=1e-2)
+    for x, y in zip(outs[0][1:], outs[1][1:]):
+        torch.testing.assert_close(y.float(), x.float(), rtol=2e-2, atol=2e-2)
