@@ -136,7 +136,7 @@ def build_device(force: bool = False, verbose: bool = False) -> Path:
         for src in hip_srcs + cpp_srcs:
             obj = objdir / (src.stem + ".o")
             objs.append(obj)
-            hdrs = _sources("device", (".hpp", ".h", ".cuh", ".inc"))
+            hdrs = _local_includes(src)
             if not force and obj.exists() and not _stale(obj, [src, *hdrs]):
                 continue
             cmd = [hipcc, "-x", "hip", *common, "-c", str(src), "-o", str(obj)]
@@ -153,6 +153,22 @@ def build_device(force: bool = False, verbose: bool = False) -> Path:
             _run(cmd, verbose)
             shutil.move(str(tmp), str(target))
     return target
+
+
+def _local_includes(src: Path) -> list[Path]:
+    """Headers a source depends on: its `#include "..."` closure inside csrc/."""
+    seen: set[Path] = set()
+    todo = [src]
+    while todo:
+        f = todo.pop()
+        for line in f.read_text(errors="ignore").splitlines():
+            line = line.strip()
+            if line.startswith("#include \""):
+                h = (f.parent / line.split('"')[1]).resolve()
+                if h.exists() and h not in seen:
+                    seen.add(h)
+                    todo.append(h)
+    return sorted(seen)
 
 
 def _drain(procs: list) -> None:

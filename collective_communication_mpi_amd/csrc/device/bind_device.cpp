@@ -16,6 +16,12 @@ PYBIND11_MODULE(_device, m) {
   m.attr("ALGO_TWOSHOT") = (int)ALGO_TWOSHOT;
   m.attr("ALGO_REDUCE_BCAST") = (int)ALGO_REDUCE_BCAST;
   m.attr("ALGO_TWOSHOT_PUSH") = (int)ALGO_TWOSHOT_PUSH;
+  m.attr("ALGO_RING") = (int)ALGO_RING;
+  m.attr("ALGO_RHD") = (int)ALGO_RHD;
+  m.attr("A2A_PULL") = (int)A2A_PULL;
+  m.attr("A2A_PUSH") = (int)A2A_PUSH;
+  m.attr("MAX_RINGS") = kMaxRings;
+  m.def("ring_slot_bytes", &DeviceComm::ring_slot_bytes);
   m.attr("MAX_RANKS") = kMaxRanks;
   m.attr("MAX_BLOCKS") = kMaxBlocks;
   m.def("reduce_supported", &device_reduce_supported);
@@ -50,7 +56,9 @@ PYBIND11_MODULE(_device, m) {
       .def("allreduce", &DeviceComm::allreduce, py::call_guard<py::gil_scoped_release>())
       .def("reduce_scatter", &DeviceComm::reduce_scatter, py::call_guard<py::gil_scoped_release>())
       .def("allgather", &DeviceComm::allgather, py::call_guard<py::gil_scoped_release>())
-      .def("alltoall", &DeviceComm::alltoall, py::call_guard<py::gil_scoped_release>())
+      .def("alltoall", &DeviceComm::alltoall, py::arg("inp"), py::arg("out"), py::arg("bytes_per_peer"),
+           py::arg("stream"), py::arg("max_blocks"), py::arg("symmetric"), py::arg("mode") = 0,
+           py::call_guard<py::gil_scoped_release>())
       .def("bcast", &DeviceComm::bcast, py::call_guard<py::gil_scoped_release>())
       .def("local_reduce", &DeviceComm::local_reduce, py::call_guard<py::gil_scoped_release>())
       .def("allgather_lastaxis", &DeviceComm::allgather_lastaxis, py::call_guard<py::gil_scoped_release>())
@@ -86,7 +94,9 @@ PYBIND11_MODULE(_device, m) {
       .def("set_inbox", &DeviceComm::set_inbox)
       .def_property_readonly("inbox_bytes", &DeviceComm::inbox_bytes)
       .def("set_timeout_seconds", &DeviceComm::set_timeout_seconds)
-      .def("set_copy_engine", &DeviceComm::set_copy_engine);
+      .def("set_copy_engine", &DeviceComm::set_copy_engine)
+      .def("set_rings", &DeviceComm::set_rings)
+      .def_property_readonly("rings", &DeviceComm::rings);
 
   register_ops(m);
 }

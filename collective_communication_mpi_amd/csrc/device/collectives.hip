@@ -24,6 +24,8 @@
 // barrier; grids are sized identically on all ranks from (bytes, nranks).
 // Reductions through LDS would add a round trip without reuse (each byte is
 // read once), so partial sums stay in VGPRs.
+#include <cstdlib>
+
 #include "common.hpp"
 #include "collectives.hpp"
 
@@ -481,9 +483,16 @@ __global__ void __launch_bounds__(kThreads) k_reduce_scatter(CollArgs a) {
   finish(a, e);
 }
 
-// All-gather: out[j*nbytes ...] = in_j.  (mode 0)
-// All-to-all: out[j*nbytes ...] = in_j[me*nbytes ...].  (mode 1)
-// Broadcast : out = in_root.  (mode 2)
+// Per-peer block moves; `nbytes` = bytes per peer block, block strides
+// src_stride / dst_stride (0 = nbytes) so staged chunks of a larger tensor
+// land in place without an unpack pass.
+//   MODE 0 all-gather      (pull): out[j*ds] = in_j
+//   MODE 1 all-to-all      (pull): out[j*ds] = in_j[me*ss]
+//   MODE 2 broadcast       (pull): out = in_root
+//   MODE 3 all-to-all      (push): out_j[me*ds] = in[j*ss]   (reference myAlltoall,
+//          mpi_wrapper/comm.py:130-155: each segment goes straight into its
+//          destination; the input never leaves this rank's memory except as
+//          posted peer writes, so it needs no registration)
 template <int MODE, int NRM>
 __global__ void __launch_bounds__(kThreads) k_move(CollArgs a) {
   __shared__ uint64_t s_epoch;
@@ -492,6 +501,8 @@ __global__ void __launch_bounds__(kThreads) k_move(CollArgs a) {
   const uint64_t e = s_epoch;
   const PeerTable* pt = a.pt;
   const int me = pt->rank, nr = pt->size;
+  const uint64_t ss = a.src_stride ? a.src_stride : a.nbytes;
+  const uint64_t ds = a.dst_stride ? a.dst_stride : a.nbytes;
   BlockRange r = part16(a.nbytes, gridDim.x, blockIdx.x);
   if (r.hi > r.lo) {
     if (MODE == 2) {
@@ -500,16 +511,243 @@ __global__ void __launch_bounds__(kThreads) k_move(CollArgs a) {
       __shared__ const char* srcs[kMaxRanks];
       __shared__ char* dsts[kMaxRanks];
       if (threadIdx.x < nr) {
-        int j = threadIdx.x;
-        uint64_t soff = (MODE == 1 ? (uint64_t)me * a.nbytes : 0) + r.lo;
-        srcs[j] = resolve(pt, j, codes[0][j]) + soff;
-        dsts[j] = a.out + (uint64_t)j * a.nbytes + r.lo;
+        const int j = threadIdx.x;
+        if (MODE == 3) {
+          srcs[j] = a.in + (uint64_t)j * ss + r.lo;
+          dsts[j] = resolve(pt, j, codes[1][j]) + (uint64_t)me * ds + r.lo;
+        } else {
+          srcs[j] = resolve(pt, j, codes[0][j]) + (MODE == 1 ? (uint64_t)me * ss : 0) + r.lo;
+          dsts[j] = a.out + (uint64_t)j * ds + r.lo;
+        }
       }
       __syncthreads();
       gather_spans<NRM>(srcs, dsts, nr, -1, r.hi - r.lo);
     }
   }
   if (!sync_phase(a, 3, e)) return;
+  finish(a, e);
+}
+
+// ---------------------------------------------------------------------------
+// pipelined schedules: ring and recursive halving/doubling
+// ---------------------------------------------------------------------------
+// Both push: every byte that crosses to a peer is a posted remote store into
+// the peer's inbox (reduce-scatter) or its result buffer (all-gather); every
+// load is local.  The buffer is cut into p chunks (part16) and every chunk
+// into gridDim.x sub-slices; CTA b owns sub-slice b of every chunk, so CTA b
+// of a rank only ever waits for CTA b of its ring/partner neighbours (one
+// monotonic step word per (block, source): epoch * kStepsPerEpoch + step).
+// Only the start barrier is all-to-all: it guarantees every peer has reached
+// this collective (its previous use of the inbox / result buffer is done)
+// before anybody writes into it.  No end barrier is needed: a rank finishes
+// only after the last write addressed to it has been flagged, and nobody
+// reads another rank's memory.
+
+// o1 (and o2 if TWO) = RED ? op(x, y) : x over [0, len); x, y 16-B aligned.
+template <int DT, int OP, bool RED, bool TWO>
+__device__ void combine_span(const char* x, const char* y, char* o1, char* o2, uint64_t len) {
+  constexpr int U = 4;
+  const uint64_t kWin = 1ull << 30;
+  const uint64_t vbytes = len & ~15ull;
+  for (uint64_t w = 0; w < vbytes; w += kWin) {
+    const uint32_t wl = (uint32_t)min(kWin, vbytes - w);
+    const Rsrc rx = make_rsrc(uniform_ptr(const_cast<char*>(x) + w), wl);
+    const Rsrc ry = make_rsrc(uniform_ptr(const_cast<char*>(RED ? y : x) + w), wl);
+    const Rsrc r1 = make_rsrc(uniform_ptr(o1 + w), wl);
+    const Rsrc r2 = make_rsrc(uniform_ptr((TWO ? o2 : o1) + w), wl);
+    const uint32_t nv = wl / 16;
+    for (uint32_t v = threadIdx.x; v < nv; v += kThreads * U) {
+      u32x4 xa[U], ya[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint32_t vv = v + u * kThreads;
+        if (vv < nv) {
+          xa[u] = ld16(rx, vv * 16);
+          if (RED) ya[u] = ld16(ry, vv * 16);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint32_t vv = v + u * kThreads;
+        if (vv < nv) {
+          u32x4 res = xa[u];
+          if (RED) {
+            VecAcc<DT> acc;
+            acc.load(xa[u]);
+            acc.template acc<OP>(ya[u]);
+            res = acc.store();
+          }
+          st16(r1, vv * 16, res);
+          if (TWO) st16(r2, vv * 16, res);
+        }
+      }
+    }
+  }
+  const uint64_t tail = len - vbytes;
+  if (tail && threadIdx.x == 0) {
+    const Rsrc rx = make_rsrc(const_cast<char*>(x) + vbytes, (uint32_t)tail);
+    const Rsrc r1 = make_rsrc(o1 + vbytes, (uint32_t)tail);
+    const Rsrc r2 = make_rsrc((TWO ? o2 : o1) + vbytes, (uint32_t)tail);
+    if constexpr (RED) {
+      using E = Elem<DT>;
+      const Rsrc ry = make_rsrc(const_cast<char*>(y) + vbytes, (uint32_t)tail);
+      for (uint32_t o = 0; o < tail; o += E::B) {
+        const typename E::A v = apply_op<OP>(E::ld(rx, o), E::ld(ry, o));
+        E::st(r1, o, v);
+        if (TWO) E::st(r2, o, v);
+      }
+    } else {
+      for (uint32_t o = 0; o < tail; ++o) {
+        const auto v = __builtin_amdgcn_raw_buffer_load_b8(rx.r, o, 0, kCachePolicySys);
+        __builtin_amdgcn_raw_buffer_store_b8(v, r1.r, o, 0, kCachePolicySys);
+        if (TWO) __builtin_amdgcn_raw_buffer_store_b8(v, r2.r, o, 0, kCachePolicySys);
+      }
+    }
+  }
+}
+
+// Drain this CTA's stores, then one lane publishes `v` (release, system scope).
+__device__ __forceinline__ void post_step(uint64_t* flag, uint64_t v) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    release_sys();
+    signal_store(flag, v);
+  }
+}
+
+// One lane waits for *flag >= v (bounded); the CTA follows.  False on timeout.
+__device__ __forceinline__ bool await_step(const CollArgs& a, const uint64_t* flag, uint64_t v, int peer) {
+  bool ok = true;
+  if (threadIdx.x == 0) {
+    const PeerTable* pt = a.pt;
+    ok = wait_geq(flag, v, a.timeout_ticks, &pt->sig[pt->rank]->error, 0x800 + peer);
+    if (!ok) report_host(pt, 0x800 + peer);
+  }
+  return __syncthreads_and(ok);
+}
+
+// CTA b's sub-slice of chunk c: absolute byte range, and its offset inside the
+// chunk (= inside an inbox slot).  The split is of the SLOT size, not of the
+// chunk's own length: chunks differ by up to 16 B, and two rings can deliver
+// different chunks into the same slot of one inbox, so the sub-slot of CTA b
+// must not depend on which chunk it carries.
+struct SubSlice {
+  uint64_t lo, len, rel;
+};
+__device__ __forceinline__ SubSlice sub_slice(uint64_t nbytes, int p, int c, uint64_t slot) {
+  const BlockRange ch = part16(nbytes, p, c);
+  const BlockRange r = part16(slot, gridDim.x, blockIdx.x);
+  const uint64_t len = ch.hi - ch.lo;
+  const uint64_t lo = min(r.lo, len), hi = min(r.hi, len);
+  return {ch.lo + lo, hi - lo, lo};
+}
+
+// Ring all-reduce (reduce-scatter then all-gather, 2(p-1) pipelined steps).
+// CTA b runs ring k = b % nrings (i -> i + stride_k); rings with coprime
+// strides use different xGMI links, so k rings drive k links per direction.
+// Ring position q of this rank: chunk (q - t) is forwarded at RS step t;
+// after p-1 steps the rank owns the fully reduced chunk q + 1, writes it to
+// its result and its right neighbour's result, and the all-gather forwards
+// what arrives.  Inbox slot t holds the partial sum received at RS step t.
+template <int DT, int OP>
+__global__ void __launch_bounds__(kThreads) k_allreduce_ring(CollArgs a) {
+  __shared__ uint64_t s_epoch;
+  __shared__ uint64_t codes[2][kMaxRanks];
+  if (!start_phase(a, &s_epoch, codes)) return;
+  const uint64_t e = s_epoch;
+  const PeerTable* pt = a.pt;
+  const int me = pt->rank, p = pt->size, b = blockIdx.x;
+  const int k = b % a.nrings;
+  const int stride = a.ring_stride[k];
+  const int right = (me + stride) % p, left = (me + p - stride) % p;
+  const int q = (me * a.ring_inv[k]) % p;
+  const uint64_t slot = a.inbox_slot, base = e * kStepsPerEpoch;
+  char* out = a.out;
+  char* r_out = resolve(pt, right, codes[1][right]);
+  const char* inbox = resolve(pt, me, a.aux_code);
+  char* r_inbox = resolve(pt, right, a.aux_code);
+  const uint64_t* my_flag = &pt->sig[me]->step[b][left];
+  uint64_t* r_flag = &pt->sig[right]->step[b][me];
+  // reduce-scatter
+  for (int t = 0; t < p - 1; ++t) {
+    const SubSlice s = sub_slice(a.nbytes, p, (q - t + p) % p, slot);
+    if (t == 0) {
+      combine_span<DT, OP, false, false>(a.in + s.lo, nullptr, r_inbox + s.rel, nullptr, s.len);
+    } else {
+      if (!await_step(a, my_flag, base + t, left)) return;
+      combine_span<DT, OP, true, false>(a.in + s.lo, inbox + (t - 1) * slot + s.rel, r_inbox + t * slot + s.rel,
+                                        nullptr, s.len);
+    }
+    post_step(r_flag, base + t + 1);
+  }
+  // last reduction: the owned chunk, written locally and into the right neighbour's result
+  {
+    const SubSlice s = sub_slice(a.nbytes, p, (q + 1) % p, slot);
+    if (!await_step(a, my_flag, base + p - 1, left)) return;
+    combine_span<DT, OP, true, true>(a.in + s.lo, inbox + (p - 2) * slot + s.rel, out + s.lo, r_out + s.lo, s.len);
+    post_step(r_flag, base + p);
+  }
+  // all-gather: forward the chunk that arrived in the previous step
+  for (int t = 1; t < p - 1; ++t) {
+    const SubSlice s = sub_slice(a.nbytes, p, (q - t + 1 + p) % p, slot);
+    if (!await_step(a, my_flag, base + p - 1 + t, left)) return;
+    combine_span<DT, OP, false, false>(out + s.lo, nullptr, r_out + s.lo, nullptr, s.len);
+    post_step(r_flag, base + p + t);
+  }
+  if (!await_step(a, my_flag, base + 2 * p - 2, left)) return;
+  finish(a, e);
+}
+
+// Recursive halving (reduce-scatter) + recursive doubling (all-gather), p = 2^k.
+// Halving step with mask m: partner = me ^ m; the current range of m*2 chunks
+// splits, the half the partner keeps is pushed into its inbox (slot region of
+// this step), the own half is reduced from the partner's push.  Rank r ends
+// owning chunk r; the doubling steps push the owned range into the partner's
+// result buffer.  log2(p) + log2(p) steps, every step on one link.
+template <int DT, int OP>
+__global__ void __launch_bounds__(kThreads) k_allreduce_rhd(CollArgs a) {
+  __shared__ uint64_t s_epoch;
+  __shared__ uint64_t codes[2][kMaxRanks];
+  if (!start_phase(a, &s_epoch, codes)) return;
+  const uint64_t e = s_epoch;
+  const PeerTable* pt = a.pt;
+  const int me = pt->rank, p = pt->size, b = blockIdx.x;
+  const uint64_t slot = a.inbox_slot, base = e * kStepsPerEpoch;
+  char* out = a.out;
+  const char* inbox = resolve(pt, me, a.aux_code);
+  Signals* mine = pt->sig[me];
+  int step = 0, L = 0;
+  uint64_t slot_off = 0;
+  for (int m = p >> 1; m >= 1; m >>= 1, ++step) {
+    const int partner = me ^ m;
+    const int keep = (me & m) ? L + m : L, give = (me & m) ? L : L + m;
+    const char* from = step == 0 ? a.in : out;
+    char* p_inbox = resolve(pt, partner, a.aux_code) + slot_off;
+    for (int i = 0; i < m; ++i) {
+      const SubSlice s = sub_slice(a.nbytes, p, give + i, slot);
+      combine_span<DT, OP, false, false>(from + s.lo, nullptr, p_inbox + i * slot + s.rel, nullptr, s.len);
+    }
+    post_step(&pt->sig[partner]->step[b][me], base + step + 1);
+    if (!await_step(a, &mine->step[b][partner], base + step + 1, partner)) return;
+    for (int i = 0; i < m; ++i) {
+      const SubSlice s = sub_slice(a.nbytes, p, keep + i, slot);
+      combine_span<DT, OP, true, false>(from + s.lo, inbox + slot_off + i * slot + s.rel, out + s.lo, nullptr, s.len);
+    }
+    L = keep;
+    slot_off += (uint64_t)m * slot;
+  }
+  for (int m = 1; m < p; m <<= 1, ++step) {
+    const int partner = me ^ m;
+    const int own = me & ~(m - 1);
+    char* p_out = resolve(pt, partner, codes[1][partner]);
+    for (int i = 0; i < m; ++i) {
+      const SubSlice s = sub_slice(a.nbytes, p, own + i, slot);
+      combine_span<DT, OP, false, false>(out + s.lo, nullptr, p_out + s.lo, nullptr, s.len);
+    }
+    post_step(&pt->sig[partner]->step[b][me], base + step + 1);
+    if (!await_step(a, &mine->step[b][partner], base + step + 1, partner)) return;
+  }
   finish(a, e);
 }
 
@@ -671,8 +909,13 @@ void launch_copy(const void* src, void* dst, uint64_t nbytes, hipStream_t s) {
 }
 
 int grid_for(uint64_t bytes_per_cta_work, int max_blocks) {
-  // ~64 KiB of output per CTA minimum; at most max_blocks CTAs
-  uint64_t g = (bytes_per_cta_work + (64u << 10) - 1) / (64u << 10);
+  // at least kCtaBytes (CCMPI_CTA_BYTES, default 64 KiB) of work per CTA; at most max_blocks CTAs
+  static const uint64_t kCtaBytes = [] {
+    const char* e = std::getenv("CCMPI_CTA_BYTES");
+    const uint64_t v = e ? std::strtoull(e, nullptr, 10) : 0;
+    return v >= 4096 ? v : (uint64_t)(64u << 10);
+  }();
+  uint64_t g = (bytes_per_cta_work + kCtaBytes - 1) / kCtaBytes;
   if (g < 1) g = 1;
   if (g > (uint64_t)max_blocks) g = max_blocks;
   if (g > (uint64_t)kMaxBlocks) g = kMaxBlocks;
@@ -694,6 +937,8 @@ void launch_allreduce(int algo, const CollArgs& a, int nranks, int dtype, int op
         case ALGO_TWOSHOT: hipLaunchKernelGGL((k_allreduce_twoshot<D, O, R>), dim3(grid), dim3(kThreads), 0, s, a); break;
         case ALGO_REDUCE_BCAST: hipLaunchKernelGGL((k_allreduce_reduce_bcast<D, O, R>), dim3(grid), dim3(kThreads), 0, s, a); break;
         case ALGO_TWOSHOT_PUSH: hipLaunchKernelGGL((k_allreduce_twoshot_push<D, O, R>), dim3(grid), dim3(kThreads), 0, s, a); break;
+        case ALGO_RING: hipLaunchKernelGGL((k_allreduce_ring<D, O>), dim3(grid), dim3(kThreads), 0, s, a); break;
+        case ALGO_RHD: hipLaunchKernelGGL((k_allreduce_rhd<D, O>), dim3(grid), dim3(kThreads), 0, s, a); break;
         default: throw std::invalid_argument("ccmpi: bad allreduce algo");
       }
     });
@@ -729,6 +974,7 @@ void launch_move(int mode, const CollArgs& a, int nranks, int grid, hipStream_t 
       case MOVE_ALLGATHER: hipLaunchKernelGGL((k_move<0, R>), dim3(grid), dim3(kThreads), 0, s, a); break;
       case MOVE_ALLTOALL: hipLaunchKernelGGL((k_move<1, R>), dim3(grid), dim3(kThreads), 0, s, a); break;
       case MOVE_BCAST: hipLaunchKernelGGL((k_move<2, R>), dim3(grid), dim3(kThreads), 0, s, a); break;
+      case MOVE_ALLTOALL_PUSH: hipLaunchKernelGGL((k_move<3, R>), dim3(grid), dim3(kThreads), 0, s, a); break;
       default: throw std::invalid_argument("ccmpi: bad move mode");
     }
   });

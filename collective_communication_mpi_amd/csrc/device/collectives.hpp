@@ -14,21 +14,37 @@ enum AllreduceAlgo : int {
   ALGO_TWOSHOT = 1,       // reduce-scatter + all-gather over all links (large)
   ALGO_REDUCE_BCAST = 2,  // reference algorithm: reduce to root, broadcast
   ALGO_TWOSHOT_PUSH = 3,  // two-shot with remote writes (scatter into peers' inboxes, push results)
+  ALGO_RING = 4,          // pipelined ring RS + AG with peer writes, several rings (coprime strides)
+  ALGO_RHD = 5,           // recursive halving (RS) + doubling (AG) with peer writes, p = 2^k
 };
 
-enum MoveMode : int { MOVE_ALLGATHER = 0, MOVE_ALLTOALL = 1, MOVE_BCAST = 2 };
+enum MoveMode : int {
+  MOVE_ALLGATHER = 0,     // pull: out[j] <- in_j
+  MOVE_ALLTOALL = 1,      // pull: out[j] <- in_j[me]
+  MOVE_BCAST = 2,         // pull: out <- in_root
+  MOVE_ALLTOALL_PUSH = 3  // push: out_j[me] <- in[j]  (peer writes, input stays local)
+};
+
+constexpr int kMaxRings = 8;
+enum AlltoallMode : int { A2A_PULL = 0, A2A_PUSH = 1 };
 
 struct CollArgs {
   const PeerTable* pt;     // device-resident peer table
   uint64_t* epochs;        // per-CTA epoch counters (device, local)
   uint64_t src_code;       // this rank's published input  (addr_code)
-  uint64_t res_code;       // this rank's published result buffer (two-shot / reduce_bcast)
+  uint64_t res_code;       // this rank's published result buffer (two-shot / reduce_bcast / ring / rhd / push)
   char* out;               // local output pointer (16-B aligned)
   uint64_t nbytes;         // see each kernel
   uint64_t timeout_ticks;  // bounded spins, 100 MHz ticks
   int root;
-  int pad;
-  uint64_t aux_code;       // symmetric inbox (push two-shot): same code on every rank
+  int nrings;              // ring: number of concurrent rings (CTA b runs ring b % nrings)
+  uint64_t aux_code;       // symmetric inbox (push two-shot, ring, rhd): same code on every rank
+  const char* in;          // local input (ring / rhd / push all-to-all read only their own input)
+  uint64_t src_stride;     // all-to-all: bytes between per-peer blocks of the source (0 = nbytes)
+  uint64_t dst_stride;     // all-to-all: bytes between per-peer blocks of the destination (0 = nbytes)
+  uint64_t inbox_slot;     // ring / rhd: bytes per inbox chunk slot (>= the largest chunk, 16-B multiple)
+  int8_t ring_stride[kMaxRings];  // ring k: i -> i + stride (coprime to p)
+  int8_t ring_inv[kMaxRings];     // stride^-1 mod p: position of rank r in ring k = r * inv % p
 };
 
 struct LocalReduceArgs {

@@ -43,6 +43,7 @@ constexpr int kMaxRanks = 16;     // ranks per device communicator
 constexpr int kMaxSegs = 32;      // registered symmetric segments per rank
 constexpr int kMaxBlocks = 1024;  // max CTAs of one collective launch
 constexpr int kCachePolicySys = 17;  // aux bits: sc0 | sc1 (system coherent)
+constexpr uint64_t kStepsPerEpoch = 64;  // > 2 * (kMaxRanks - 1) signals per call
 
 inline size_t dtype_bytes(int dt) {
   switch (dt) {
@@ -62,6 +63,9 @@ inline size_t dtype_bytes(int dt) {
 struct Signals {
   uint64_t flag[4][kMaxBlocks][kMaxRanks];  // phase x block x source rank
   uint64_t addr[2][kMaxBlocks][kMaxRanks];  // published (seg, offset) codes per block
+  // step counters of the pipelined schedules (ring, recursive halving/doubling):
+  // value = epoch * kStepsPerEpoch + step, so one monotonic word per (block, source)
+  uint64_t step[kMaxBlocks][kMaxRanks];
   uint32_t error;                           // first timeout/ fault code seen
   uint32_t pad[15];
 };
@@ -119,6 +123,20 @@ __device__ __forceinline__ uint64_t now_ticks() { return __builtin_amdgcn_s_memr
 
 // Bounded wait until *p >= want (system scope). Returns false on timeout and
 // records `code` in the local signal buffer's error word.
+//
+// Acquire side of the flag protocol.  The spin itself uses relaxed loads (a
+// system-scope acquire load per iteration would invalidate the caches on
+// every spin).  Once the flag is seen, a system-scope acquire fence orders
+// every later load of this wave after the flag load and invalidates this
+// CU's vector L1 / the XCD's L2 lines that could hold stale copies of peer
+// data (gfx950: `buffer_inv sc0 sc1`).  The waiting lanes then reach
+// __syncthreads() before any other wave of the workgroup touches peer data;
+// the barrier orders those waves after the fence, and their loads are issued
+// system-coherent (sc0 sc1) as well, so they never hit a line the fence did
+// not cover.  The release side is `release_sys()` + the flag store: the
+// writer's data is written through (sc0 sc1), `buffer_wbl2 sc0 sc1` pushes
+// out anything an earlier kernel left dirty in its L2, and vmcnt(0) makes the
+// flag store the last one issued.
 __device__ __forceinline__ bool wait_geq(const uint64_t* p, uint64_t want, uint64_t budget_ticks,
                                          uint32_t* err, uint32_t code) {
   uint64_t t0 = 0;
@@ -134,6 +152,7 @@ __device__ __forceinline__ bool wait_geq(const uint64_t* p, uint64_t want, uint6
       __builtin_amdgcn_s_sleep(1);
     }
   }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
   return true;
 }
 

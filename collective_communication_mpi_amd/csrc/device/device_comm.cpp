@@ -225,6 +225,10 @@ void DeviceComm::allreduce(uint64_t in, uint64_t out, uint64_t count, int dtype,
     }
     return;
   }
+  if (algo == ALGO_RING || algo == ALGO_RHD) {
+    allreduce_pipelined_(algo, in, out, nbytes, es, dtype, op, st, max_blocks, symmetric);
+    return;
+  }
   if (algo == ALGO_TWOSHOT_PUSH) {
     // needs registered in/out and an inbox of p shards; otherwise the pull form
     const uint64_t shard = ((nbytes + size_ - 1) / size_ + 15) / 16 * 16;
@@ -269,6 +273,80 @@ void DeviceComm::allreduce(uint64_t in, uint64_t out, uint64_t count, int dtype,
     const uint64_t work = algo == ALGO_TWOSHOT ? n / size_ : n;
     launch_allreduce(algo, args_(sc, rc, outp, n, 0), size_, dtype, op, grid_(work, max_blocks), st);
     if (!out_ok) CCMPI_HIP_CHECK(hipMemcpyAsync((void*)(out + off), stage + chunk, n, hipMemcpyDeviceToDevice, st));
+  }
+}
+
+namespace {
+int gcd_i(int a, int b) { return b ? gcd_i(b, a % b) : a; }
+int inv_mod(int a, int m) {
+  for (int x = 1; x < m; ++x)
+    if ((a * x) % m == 1) return x;
+  return 1;
+}
+}  // namespace
+
+uint64_t DeviceComm::ring_slot_bytes(uint64_t nbytes, int p) {
+  // largest part16 chunk of nbytes over p ranks
+  const uint64_t nv = (nbytes + 15) / 16;
+  return ((nv + p - 1) / p) * 16;
+}
+
+// `symmetric` (the caller's promise, identical on every rank): every rank's
+// output is registered and its input 16-B aligned, so results are pushed
+// straight into peers' outputs.  Otherwise the result goes through the scratch
+// segment (and a misaligned input is staged too) in pieces of at most half the
+// scratch; piece sizes depend only on values equal on all ranks.
+void DeviceComm::allreduce_pipelined_(int algo, uint64_t in, uint64_t out, uint64_t nbytes, uint64_t es, int dtype,
+                                      int op, hipStream_t st, int max_blocks, bool symmetric) {
+  const int p = size_;
+  if (algo == ALGO_RHD && (p & (p - 1)))
+    throw std::invalid_argument("ccmpi: recursive halving/doubling needs a power-of-two group size");
+  const uint64_t ic = inbox_ptr_ ? code_of_(inbox_ptr_, inbox_bytes_) : 0;
+  if (!ic) throw std::runtime_error("ccmpi: ring/rhd all-reduce needs the symmetric inbox (set_inbox)");
+  // concurrent rings: strides coprime to p (s and p-s are the two directions of the same links)
+  std::vector<int> strides;
+  for (int s = 1; s < p && (int)strides.size() < std::min(rings_, kMaxRings); ++s)
+    if (gcd_i(s, p) == 1) strides.push_back(s);
+  if (strides.empty()) strides.push_back(1);
+  const int R = algo == ALGO_RING ? (int)strides.size() : 1;
+  // piece size: (p-1) inbox slots of the piece's largest chunk must fit; identical on all ranks
+  uint64_t piece = (inbox_bytes_ / (p - 1) / 16) * 16 * p;
+  const uint64_t half = scratch_bytes() / 2 / 16 * 16;
+  const bool in_al = in % 16 == 0;
+  if (symmetric && (!in_al || out % 16 || !code_of_(out, nbytes)))
+    throw std::invalid_argument("ccmpi: symmetric ring/rhd all-reduce needs a registered output and aligned input");
+  const bool out_reg = symmetric;
+  if (!symmetric) piece = std::min(piece, half);
+  piece = staging_chunk_(piece, 16 * es);
+  if (piece == 0) throw std::runtime_error("ccmpi: inbox/scratch too small for ring/rhd");
+  char* stage = reinterpret_cast<char*>(scratch_ptr());
+  for (uint64_t off = 0; off < nbytes; off += piece) {
+    const uint64_t n = std::min(piece, nbytes - off);
+    const char* inp = reinterpret_cast<const char*>(in + off);
+    if (!in_al) {
+      CCMPI_HIP_CHECK(hipMemcpyAsync(stage, inp, n, hipMemcpyDeviceToDevice, st));
+      inp = stage;
+    }
+    char* outp = reinterpret_cast<char*>(out + off);
+    uint64_t rc = out_reg ? code_of_(out + off, n) : 0;
+    if (!rc) {
+      rc = addr_code(0, half);
+      outp = stage + half;
+    }
+    CollArgs a = args_(0, rc, outp, n, 0);
+    a.in = inp;
+    a.aux_code = ic;
+    a.inbox_slot = ring_slot_bytes(n, p);
+    a.nrings = R;
+    for (int k = 0; k < R; ++k) {
+      a.ring_stride[k] = (int8_t)strides[k];
+      a.ring_inv[k] = (int8_t)inv_mod(strides[k], p);
+    }
+    int g = grid_(n / p, max_blocks);
+    g = std::max(R, g / R * R);
+    launch_allreduce(algo, a, size_, dtype, op, g, st);
+    if (outp != reinterpret_cast<char*>(out + off))
+      CCMPI_HIP_CHECK(hipMemcpyAsync((void*)(out + off), outp, n, hipMemcpyDeviceToDevice, st));
   }
 }
 
@@ -338,16 +416,19 @@ void DeviceComm::allgather(uint64_t in, uint64_t out, uint64_t bytes_per_rank, u
       CCMPI_HIP_CHECK(hipMemcpyAsync(stage, (void*)(in + off), n, hipMemcpyDeviceToDevice, st));
       sc = addr_code(0, 0);
     }
-    const bool direct = (n == bytes_per_rank) && out % 16 == 0 && n % 16 == 0;
-    char* dst = direct ? (char*)out : gath;
-    launch_move(MOVE_ALLGATHER, args_(sc, 0, dst, n, 0), size_, grid_(n * size_, max_blocks), st);
+    // chunks land in the strided output directly when it is 16-B aligned
+    const bool direct = (out + off) % 16 == 0 && bytes_per_rank % 16 == 0;
+    char* dst = direct ? (char*)(out + off) : gath;
+    CollArgs a = args_(sc, 0, dst, n, 0);
+    a.dst_stride = direct ? bytes_per_rank : n;
+    launch_move(MOVE_ALLGATHER, a, size_, grid_(n * size_, max_blocks), st);
     if (!direct)
       CCMPI_HIP_CHECK(hipMemcpy2DAsync((void*)(out + off), bytes_per_rank, gath, n, n, size_, hipMemcpyDeviceToDevice, st));
   }
 }
 
 void DeviceComm::alltoall(uint64_t in, uint64_t out, uint64_t bytes_per_peer, uint64_t stream, int max_blocks,
-                          bool symmetric) {
+                          bool symmetric, int mode) {
   if (bytes_per_peer == 0) return;
   CCMPI_HIP_CHECK(hipSetDevice(device_));
   hipStream_t st = S(stream);
@@ -356,22 +437,40 @@ void DeviceComm::alltoall(uint64_t in, uint64_t out, uint64_t bytes_per_peer, ui
     return;
   }
   const uint64_t total = bytes_per_peer * size_;
-  if (symmetric && in != out && out % 16 == 0 && bytes_per_peer % 16 == 0) {
-    uint64_t sc = code_of_(in, total);
+  const bool aligned = in % 16 == 0 && out % 16 == 0 && bytes_per_peer % 16 == 0;
+  if (symmetric && in != out && aligned) {
+    if (mode == A2A_PUSH) {
+      // every rank's OUTPUT is registered: peer writes straight into it, the input stays local
+      const uint64_t rc = code_of_(out, total);
+      if (!rc) throw std::invalid_argument("ccmpi: push alltoall needs a registered output on every rank");
+      CollArgs a = args_(0, rc, (char*)out, bytes_per_peer, 0);
+      a.in = reinterpret_cast<const char*>(in);
+      launch_move(MOVE_ALLTOALL_PUSH, a, size_, grid_(total, max_blocks), st);
+      return;
+    }
+    const uint64_t sc = code_of_(in, total);
     if (!sc) throw std::invalid_argument("ccmpi: symmetric alltoall needs an aligned registered input");
     launch_move(MOVE_ALLTOALL, args_(sc, 0, (char*)out, bytes_per_peer, 0), size_, grid_(total, max_blocks), st);
     return;
   }
+  // Staged pull (in-place calls, unregistered inputs): one pack pass of this
+  // chunk's p blocks into the scratch segment ([p][n]); the kernel pulls block
+  // `me` of every peer's scratch straight into the strided output (no unpack
+  // pass unless the output is misaligned).
   uint64_t chunk = staging_chunk_(scratch_bytes() / 2 / size_, 16);
   if (chunk == 0) throw std::runtime_error("ccmpi: scratch too small for alltoall");
   char* stage = reinterpret_cast<char*>(scratch_ptr());
   char* gath = stage + scratch_bytes() / 2;
   for (uint64_t off = 0; off < bytes_per_peer; off += chunk) {
     const uint64_t n = std::min(chunk, bytes_per_peer - off);
-    // pack [p][n] (always staged: the reader indexes my block at me*n)
     CCMPI_HIP_CHECK(hipMemcpy2DAsync(stage, n, (void*)(in + off), bytes_per_peer, n, size_, hipMemcpyDeviceToDevice, st));
-    launch_move(MOVE_ALLTOALL, args_(addr_code(0, 0), 0, gath, n, 0), size_, grid_(n * size_, max_blocks), st);
-    CCMPI_HIP_CHECK(hipMemcpy2DAsync((void*)(out + off), bytes_per_peer, gath, n, n, size_, hipMemcpyDeviceToDevice, st));
+    const bool direct = (out + off) % 16 == 0 && bytes_per_peer % 16 == 0;
+    CollArgs a = args_(addr_code(0, 0), 0, direct ? (char*)(out + off) : gath, n, 0);
+    a.src_stride = n;
+    a.dst_stride = direct ? bytes_per_peer : n;
+    launch_move(MOVE_ALLTOALL, a, size_, grid_(n * size_, max_blocks), st);
+    if (!direct)
+      CCMPI_HIP_CHECK(hipMemcpy2DAsync((void*)(out + off), bytes_per_peer, gath, n, n, size_, hipMemcpyDeviceToDevice, st));
   }
 }
 

@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <map>
 #include <mutex>
 #include <string>
@@ -61,8 +62,10 @@ class DeviceComm {
                       uint64_t stream, int max_blocks, bool symmetric);
   void allgather(uint64_t in, uint64_t out, uint64_t bytes_per_rank, uint64_t stream, int max_blocks,
                  bool symmetric);
+  // mode: A2A_PULL (default; staged for in-place / unregistered input) or A2A_PUSH
+  // (symmetric only: every rank's output registered, peer writes into it)
   void alltoall(uint64_t in, uint64_t out, uint64_t bytes_per_peer, uint64_t stream, int max_blocks,
-                bool symmetric);
+                bool symmetric, int mode = 0);
   void bcast(uint64_t buf, uint64_t nbytes, int root, uint64_t stream, int max_blocks, bool symmetric);
   void local_reduce(const std::vector<uint64_t>& ins, uint64_t out, uint64_t count, int dtype, int op,
                     uint64_t stream);
@@ -107,9 +110,16 @@ class DeviceComm {
   uint64_t timeout_ticks() const { return timeout_ticks_; }
   void set_timeout_seconds(double s) { timeout_ticks_ = (uint64_t)(s * 1e8); }
   void set_copy_engine(bool on) { copy_engine_ = on; }
+  // concurrent rings of the ring all-reduce (coprime strides, at most kMaxRings)
+  void set_rings(int r) { rings_ = std::max(1, r); }
+  int rings() const { return rings_; }
+  // inbox bytes per chunk slot of the ring / rhd all-reduce of `nbytes` over p ranks
+  static uint64_t ring_slot_bytes(uint64_t nbytes, int p);
 
  private:
   void sync_table_();
+  void allreduce_pipelined_(int algo, uint64_t in, uint64_t out, uint64_t nbytes, uint64_t es, int dtype, int op,
+                            hipStream_t st, int max_blocks, bool symmetric);
   CollArgs args_(uint64_t src_code, uint64_t res_code, char* out, uint64_t nbytes, int root) const;
   int grid_(uint64_t work_bytes, int max_blocks) const;
   uint64_t code_of_(uint64_t ptr, uint64_t nbytes) const;  // 0 if not registered / misaligned
@@ -129,6 +139,7 @@ class DeviceComm {
   uint64_t timeout_ticks_ = 2000000000ull;  // 20 s
   ncclComm_t nccl_ = nullptr;
   uint64_t inbox_ptr_ = 0, inbox_bytes_ = 0;
+  int rings_ = 1;
   bool copy_engine_ = false;              // single-rank copies: contiguous-slice kernel (3.2 vs 2.6 TB/s for the runtime blit)
   std::vector<std::string> opened_;      // handles we opened (for release)
 };

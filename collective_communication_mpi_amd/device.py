@@ -12,9 +12,13 @@ Algorithms (``algo=``):
 ``oneshot``        every rank pulls all peers' buffers and reduces (latency)
 ``twoshot``        reduce-scatter + all-gather, all peers in flight (bandwidth)
 ``reduce_bcast``   the reference myAllreduce algorithm (mpi_wrapper/comm.py:63)
-``ring``           RCCL send/recv rings + our LDS-free reduction kernel;
-                   ``rings=k`` concurrent rings with coprime strides use k links
-``rhd``            recursive halving/doubling over RCCL send/recv
+``push``           two-shot with peer writes (scatter into owners' inboxes, fan the
+                   reduced shard out to every rank's result)
+``ring``           hand-written pipelined ring RS+AG with peer writes on the flag
+                   protocol; ``rings=k`` concurrent rings with coprime strides (k links)
+``rhd``            hand-written recursive halving (RS) + doubling (AG), p = 2^k
+``ring_rccl``      ring schedule on RCCL send/recv + our reduction kernel
+``rhd_rccl``       recursive halving/doubling on RCCL send/recv
 ``rccl``           vendor RCCL collective (the "library" baseline)
 ``auto``           tuned choice (size thresholds; ``tune()`` measures them)
 =================  ============================================================
@@ -34,6 +38,9 @@ from . import _native
 from .utils.trace import trace_call
 
 _OPS = {"SUM": 0, "PROD": 1, "MIN": 2, "MAX": 3}
+# hand-written all-reduce algorithms -> native algorithm codes
+_HAND_ALGOS = {"oneshot": "ALGO_ONESHOT", "twoshot": "ALGO_TWOSHOT", "reduce_bcast": "ALGO_REDUCE_BCAST",
+               "push": "ALGO_TWOSHOT_PUSH", "ring": "ALGO_RING", "rhd": "ALGO_RHD"}
 
 
 def op_code(op) -> int:
@@ -85,13 +92,18 @@ class DeviceGroup:
         self.dc = self.D.DeviceComm(self.rank, self.size, self.device.index or 0)
         self.dc.connect([bytes(h) for h in host_comm.allgather(bytes(self.dc.signal_handle()))])
         # how many ranks share each physical GPU (multi-process-per-GPU testing):
-        # all their CTAs must be co-resident, so the grid is capped.
+        # all their CTAs must be co-resident (CTA b of one rank spins on CTA b
+        # of the others), so the total over the sharing ranks is capped at 512
+        # (~117 VGPRs -> 4 CTAs of 256 threads per CU fit; 2 per CU are used).
+        # Measured (profiles/r2_coll): 512 CTAs in total move 0.65-0.86 of the
+        # HBM roofline on 64-256 MiB collectives, 96 in total only 0.3, 1024 less
+        # than 512.  One rank per GPU gets the same 512 (2 CTAs per CU).
         props = torch.cuda.get_device_properties(self.device)
         key = f"{getattr(props, 'pci_bus_id', 0)}:{getattr(props, 'pci_device_id', 0)}:{props.name}:{self.device.index}"
         keys = host_comm.allgather(key)
         self.ranks_per_device = keys.count(key)
         self.shared_device = self.ranks_per_device > 1
-        default_blocks = 256 if not self.shared_device else max(1, 96 // self.ranks_per_device)
+        default_blocks = max(1, 512 // self.ranks_per_device)
         self.max_blocks = _env_int("CCMPI_MAX_BLOCKS", default_blocks)
         if scratch_bytes is None:
             scratch_bytes = _env_int("CCMPI_SCRATCH_MB", 64 if self.shared_device else 512) << 20
@@ -102,6 +114,11 @@ class DeviceGroup:
         assert seg == 0, "scratch must be segment 0"
         self._rccl = False
         self.oneshot_max = _env_int("CCMPI_ONESHOT_MAX_BYTES", 256 << 10)
+        # concurrent rings of algo="ring": every stride coprime to p, up to 4 (p = 8: strides
+        # 1, 3, 5, 7 -> 4 links per direction); CCMPI_RINGS overrides
+        coprime = [k for k in range(1, self.size) if _gcd(k, self.size) == 1] or [1]
+        self.default_rings = _env_int("CCMPI_RINGS", min(4, len(coprime)))
+        self.inbox_cap = _env_int("CCMPI_INBOX_MAX_MB", 1024) << 20
         self.tuned: Dict[Tuple[int, int], str] = {}
         self._lock = threading.Lock()
         self._watchdog: Optional[threading.Thread] = None
@@ -199,9 +216,11 @@ class DeviceGroup:
 
     def _ensure_inbox(self, nbytes: int) -> None:
         """Collective (all ranks call with the same size): symmetric inbox of
-        p shards for the push two-shot all-reduce, grown on demand."""
+        p shards for the push two-shot all-reduce (p - 1 chunk slots for the
+        ring / rhd schedules), grown on demand up to ``CCMPI_INBOX_MAX_MB``;
+        ring / rhd process larger buffers in inbox-sized pieces."""
         shard = ((nbytes + self.size - 1) // self.size + 15) // 16 * 16
-        need = shard * self.size
+        need = min(shard * self.size, max(self.inbox_cap, 1 << 20))
         if self.dc.inbox_bytes >= need:
             return
         cap = max(need, 64 << 20)
@@ -275,23 +294,26 @@ class DeviceGroup:
             algo, mb = algo.split(":", 1)
             max_blocks = int(mb)
         s = self._stream()
-        if algo == "push":
+        if algo in ("push", "ring", "rhd"):
             self._ensure_inbox(nbytes)
-        if algo in ("oneshot", "twoshot", "reduce_bcast", "push"):
-            a = {"oneshot": self.D.ALGO_ONESHOT, "twoshot": self.D.ALGO_TWOSHOT,
-                 "reduce_bcast": self.D.ALGO_REDUCE_BCAST, "push": self.D.ALGO_TWOSHOT_PUSH}[algo]
-            self.dc.allreduce(src.data_ptr(), dst.data_ptr(), src.numel(), dt, opc, a, s,
-                              max_blocks or self.max_blocks, self._symm(src, dst))
+        if algo == "ring":
+            self.dc.set_rings(rings or self.default_rings)
+        if algo in _HAND_ALGOS:
+            # ring / rhd read only the local input and push into peers' outputs:
+            # "symmetric" there means a registered output (and an aligned input)
+            symm = (self._symm(dst) and src.data_ptr() % 16 == 0) if algo in ("ring", "rhd") else self._symm(src, dst)
+            self.dc.allreduce(src.data_ptr(), dst.data_ptr(), src.numel(), dt, opc, getattr(self.D, _HAND_ALGOS[algo]),
+                              s, max_blocks or self.max_blocks, symm)
         elif algo == "rccl":
             self.ensure_rccl()
             self.dc.rccl_allreduce(src.data_ptr(), dst.data_ptr(), src.numel(), dt, opc, s)
-        elif algo in ("ring", "rhd"):
+        elif algo in ("ring_rccl", "rhd_rccl"):
             self.ensure_rccl()
             if dst.data_ptr() != src.data_ptr():
                 dst.copy_(src)
             need = (nbytes // max(1, self.size) + 4096) * 2
             tmp = self.scratch if need <= self.scratch.numel() else self.torch.empty(need, dtype=self.torch.uint8, device=self.device)
-            if algo == "ring":
+            if algo == "ring_rccl":
                 k = rings or _env_int("CCMPI_RINGS", 1)
                 self.dc.p2p_ring_allreduce(dst.data_ptr(), dst.numel(), dt, opc, s, k, tmp.data_ptr())
             else:
@@ -301,7 +323,7 @@ class DeviceGroup:
         return dst
 
     @trace_call("reduce_scatter")
-    def reduce_scatter(self, src, dst, op="SUM", algo: str = "direct"):
+    def reduce_scatter(self, src, dst, op="SUM", algo: str = "direct", max_blocks: Optional[int] = None):
         self._check(src, "src")
         self._check(dst, "dst")
         if src.numel() != dst.numel() * self.size:
@@ -312,12 +334,12 @@ class DeviceGroup:
             self.ensure_rccl()
             self.dc.rccl_reduce_scatter(src.data_ptr(), dst.data_ptr(), dst.numel(), dt, opc, s)
         else:
-            self.dc.reduce_scatter(src.data_ptr(), dst.data_ptr(), dst.numel(), dt, opc, s, self.max_blocks,
-                                   self._symm(src))
+            self.dc.reduce_scatter(src.data_ptr(), dst.data_ptr(), dst.numel(), dt, opc, s,
+                                   max_blocks or self.max_blocks, self._symm(src))
         return dst
 
     @trace_call("allgather")
-    def allgather(self, src, dst, algo: str = "direct"):
+    def allgather(self, src, dst, algo: str = "direct", max_blocks: Optional[int] = None):
         self._check(src, "src")
         self._check(dst, "dst")
         if dst.numel() != src.numel() * self.size or src.dtype != dst.dtype:
@@ -328,11 +350,17 @@ class DeviceGroup:
             self.ensure_rccl()
             self.dc.rccl_allgather(src.data_ptr(), dst.data_ptr(), nb, 1, s)
         else:
-            self.dc.allgather(src.data_ptr(), dst.data_ptr(), nb, s, self.max_blocks, self._symm(src) and dst.data_ptr() % 16 == 0)
+            self.dc.allgather(src.data_ptr(), dst.data_ptr(), nb, s, max_blocks or self.max_blocks,
+                              self._symm(src) and dst.data_ptr() % 16 == 0)
         return dst
 
     @trace_call("alltoall")
-    def alltoall(self, src, dst, algo: str = "direct"):
+    def alltoall(self, src, dst, algo: str = "direct", max_blocks: Optional[int] = None):
+        """``direct``: every rank pulls its block from all peers (inputs from the
+        symmetric heap: zero staging; otherwise one pack pass); ``push``: every
+        rank writes its segments straight into the peers' outputs (reference
+        myAlltoall, comm.py:130-155; outputs from the symmetric heap on every
+        rank); ``pairwise``: RCCL send/recv rounds (myAlltoall2); ``rccl``."""
         self._check(src, "src")
         self._check(dst, "dst")
         if src.numel() != dst.numel() or src.numel() % self.size:
@@ -345,8 +373,14 @@ class DeviceGroup:
         elif algo == "pairwise":
             self.ensure_rccl()
             self.dc.p2p_pairwise_alltoall(src.data_ptr(), dst.data_ptr(), blk, s)
+        elif algo == "push":
+            self.dc.alltoall(src.data_ptr(), dst.data_ptr(), blk, s, max_blocks or self.max_blocks,
+                             self._symm(dst) and src.data_ptr() % 16 == 0, self.D.A2A_PUSH)
+        elif algo in ("direct", "auto"):
+            self.dc.alltoall(src.data_ptr(), dst.data_ptr(), blk, s, max_blocks or self.max_blocks, self._symm(src),
+                             self.D.A2A_PULL)
         else:
-            self.dc.alltoall(src.data_ptr(), dst.data_ptr(), blk, s, self.max_blocks, self._symm(src))
+            raise ValueError(f"unknown alltoall algorithm {algo!r}")
         return dst
 
     @trace_call("bcast")
@@ -448,6 +482,12 @@ class DeviceGroup:
     def barrier(self) -> None:
         self.torch.cuda.synchronize(self.device)
         self.host.Barrier()
+
+
+def _gcd(a: int, b: int) -> int:
+    while b:
+        a, b = b, a % b
+    return a
 
 
 def _host_min():

@@ -1,6 +1,6 @@
 """Multi-rank GPU tests (ranks share the box's one GPU through IPC).
 
-* every device collective vs a torch oracle at 2 and 4 ranks (tests/workers/device_worker.py);
+* every device collective vs an fp64/int64 oracle at 2, 3, 4 and 8 ranks (tests/workers/device_worker.py);
 * the DP x TP harness: tp=2 (row-parallel and the reference's naive collects),
   dp=2 and dp=2 x tp=2 reproduce the single-rank training run (losses and
   final weights) within bf16 tolerance."""
@@ -16,15 +16,50 @@ pytestmark = pytest.mark.gpu
 ENV = {"CCMPI_DEVICE_TIMEOUT_S": "20"}
 
 
-@pytest.mark.parametrize("n", [2, 4])
-def test_device_collectives_multi_rank(n):
-    run_ranks(n, py("tests/workers/device_worker.py", "--quick"), timeout=400, env=ENV)
+@pytest.mark.parametrize("n,matrix", [(2, "full"), (4, "full"), (8, "wide"), (3, "quick")])
+def test_device_collectives_multi_rank(n, matrix):
+    """Every hand-written collective x algorithm x dtype x op (tests/workers/device_worker.py)
+    against an fp64/int64 oracle; 3 ranks: non-power-of-two ring and the rhd refusal."""
+    r = run_ranks(n, py("tests/workers/device_worker.py", "--matrix", matrix), timeout=600, env=ENV)
+    assert "0 failures" in r.stdout
 
 
 @pytest.mark.parametrize("n", [2, 4])
+def test_device_collectives_big(n):
+    """>= 96 MiB: staging-chunk loops and ring/rhd inbox pieces (inbox capped at 64 MiB)."""
+    r = run_ranks(n, py("tests/workers/device_worker.py", "--big"), timeout=400,
+                  env=dict(ENV, CCMPI_INBOX_MAX_MB="64"))
+    assert "0 failures" in r.stdout
+
+
+@pytest.mark.parametrize("n", [2, 4, 8])
 def test_device_collectives_random_skew(n):
-    """Randomised per-rank host/device delays, back-to-back calls."""
-    run_ranks(n, py("tests/workers/device_worker.py", "--stress", "120"), timeout=300, env=ENV)
+    """Randomised per-rank host/device delays, back-to-back calls, symmetric and staged
+    calls up to 16 MiB."""
+    r = run_ranks(n, py("tests/workers/device_worker.py", "--stress", "120"), timeout=400, env=ENV)
+    assert "0 failures" in r.stdout
+
+
+def test_rccl_same_gpu_behaviour_recorded(tmp_path):
+    """RCCL with two ranks on one GPU: the outcome of every step is recorded, not swallowed
+    (benchmarks/rccl_shared_probe.py; on this pool ncclCommInitRank reports 'invalid usage')."""
+    import json
+
+    out = tmp_path / "probe.json"
+    run_ranks(2, py("benchmarks/rccl_shared_probe.py", "--out", str(out)), timeout=200, env=ENV)
+    rec = json.loads(out.read_text())
+    for r in rec["per_rank"]:
+        init = r["ncclCommInitRank"]
+        assert init["ok"] or "RCCL error" in init["error"]
+
+
+@pytest.mark.parametrize("case", ["myallreduce", "myalltoall"])
+def test_cli_device_cases(case):
+    """The reference CLI cases on device buffers (reference mpi-test.py:42-98,178-239):
+    myAllreduce (int64, MIN) and myAlltoall vs the library path, 4 ranks."""
+    r = run_ranks(4, py("mpi-test.py", "--device", "cuda", "--test_case", case, "--runs", "5", "--warmup", "1"),
+                  timeout=300, env=ENV)
+    assert "All runs produced correct results." in r.stdout
 
 
 def test_device_timeout_watchdog_and_recovery():

@@ -1,12 +1,23 @@
 """Multi-rank device-plane check (launched by scripts/mpirun; several ranks may
-share one GPU).  Every device collective is compared with a torch fp64/exact
-oracle built from all ranks' inputs (inputs are generated from per-rank seeds,
-so each rank can rebuild every peer's input locally).
+share one GPU).  Every device collective is compared with an fp64/int64
+oracle built from all ranks' inputs: inputs come from per-(rank, case) seeded
+device generators, so each rank regenerates every peer's input locally.
 
-usage: device_worker.py [--quick] [--rccl] [--sizes 1,17,4096,...] [--stress N] [--fault]
+usage: device_worker.py [--matrix quick|full|wide] [--big] [--rccl] [--stress N] [--fault]
 
---stress N  SURVEY §5.2: N back-to-back collectives (mixed algorithms and sizes,
-            no host synchronisation in between) with randomised per-rank host
+--matrix    quick: fp32/bf16, SUM, 4 sizes; full: 6 dtypes x SUM/PROD/MIN/MAX x
+            8 sizes; wide: 6 dtypes x 4 ops x 4 sizes (for 8 ranks).  Every
+            hand-written all-reduce algorithm (oneshot, twoshot, push,
+            reduce_bcast, ring, rhd), symmetric and staged, out-of-place and
+            in-place, plus reduce-scatter / all-gather / all-to-all (pull, push,
+            staged, in-place) / bcast / last-axis TP collects.
+--big       >= 96 MiB cases that cross the staging-chunk loop (64 MiB scratch ->
+            32 MiB chunks) and the ring/rhd inbox pieces.
+--rccl      RCCL collectives and the RCCL-P2P ring/rhd/pairwise schedules; fails
+            loudly (RCCL refuses several ranks on one GPU: see
+            benchmarks/rccl_shared_probe.py and profiles/r2_coll/rccl_shared_gpu.json).
+--stress N  SURVEY §5.2: N back-to-back collectives (mixed algorithms, sizes up to
+            16 MiB, symmetric and staged calls) with randomised per-rank host
             sleeps and device-side spin delays, so ranks arrive at each kernel
             in random order; every result is checked at the end (epoch/ABA safety).
 --fault     SURVEY §5.3: rank p-1 skips one collective; the others must time out
@@ -24,32 +35,52 @@ sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", ".."))
 from collective_communication_mpi_amd import MPI, Communicator  # noqa: E402
 
 ap = argparse.ArgumentParser()
-ap.add_argument("--quick", action="store_true")
+ap.add_argument("--matrix", default="", choices=["", "quick", "full", "wide"])
+ap.add_argument("--quick", action="store_true", help="alias of --matrix quick")
+ap.add_argument("--big", action="store_true")
 ap.add_argument("--rccl", action="store_true")
 ap.add_argument("--sizes", default="")
 ap.add_argument("--stress", type=int, default=0)
 ap.add_argument("--fault", action="store_true")
 args = ap.parse_args()
+if args.quick:
+    args.matrix = "quick"
 
 comm = Communicator(MPI.COMM_WORLD)
 rank, p = comm.Get_rank(), comm.Get_size()
 dev = comm.dev
+D = dev.device
 torch.cuda.synchronize()
 fails = []
+ncheck = 0
+POW2 = p & (p - 1) == 0
+AR_ALGOS = ["oneshot", "twoshot", "push", "reduce_bcast", "ring"] + (["rhd"] if POW2 else [])
+WIDE = lambda dt: torch.float64 if dt.is_floating_point else torch.int64  # noqa: E731
 
 
-def gen(r, n, dtype, salt):
-    g = torch.Generator(device="cpu").manual_seed(1000 * r + salt)
+def gen(r, n, dtype, salt, op="SUM"):
+    """Rank r's input of case `salt` (identical on every rank that asks)."""
+    g = torch.Generator(device=D).manual_seed(1_000_003 * salt + 7919 * r + 17)
     if dtype.is_floating_point:
-        return (torch.randn(n, generator=g, dtype=torch.float64) * 3).to(dtype)
-    return torch.randint(-1000, 1000, (n,), generator=g, dtype=torch.int64).to(dtype)
+        if op == "PROD":  # keep p-fold products in range
+            x = torch.rand(n, generator=g, device=D, dtype=torch.float64) + 0.5
+        else:
+            x = torch.randn(n, generator=g, device=D, dtype=torch.float64) * 3
+        return x.to(dtype)
+    if op == "PROD":
+        x = torch.randint(1, 3, (n,), generator=g, device=D, dtype=torch.int64)
+        x = torch.where(torch.rand(n, generator=g, device=D) < 0.5, -x, x)
+        return x.to(dtype)
+    return torch.randint(-1000, 1000, (n,), generator=g, device=D, dtype=torch.int64).to(dtype)
 
 
 def oracle(n, dtype, op, salt):
-    xs = [gen(r, n, dtype, salt).to(torch.float64 if dtype.is_floating_point else torch.int64) for r in range(p)]
-    acc = xs[0].clone()
-    for x in xs[1:]:
-        if op == "SUM":
+    acc = None
+    for r in range(p):  # rank order, in fp64 / int64
+        x = gen(r, n, dtype, salt, op).to(WIDE(dtype))
+        if acc is None:
+            acc = x
+        elif op == "SUM":
             acc = acc + x
         elif op == "MAX":
             acc = torch.maximum(acc, x)
@@ -61,43 +92,53 @@ def oracle(n, dtype, op, salt):
 
 
 def check(name, got, want, dtype, nterms=1):
-    got = got.detach().cpu().to(torch.float64 if dtype.is_floating_point else torch.int64)
+    global ncheck
+    ncheck += 1
+    got = got.detach().reshape(-1).to(WIDE(dtype))
+    want = want.reshape(-1)
+    if got.shape != want.shape:
+        fails.append(f"{name}: shape {tuple(got.shape)} vs {tuple(want.shape)}")
+        return False
     if dtype.is_floating_point:
         tol = {torch.float32: 1e-5, torch.float64: 1e-12, torch.bfloat16: 1e-2, torch.float16: 2e-3}[dtype] * nterms
         ok = torch.allclose(got, want, rtol=tol, atol=tol * 4)
     else:
         ok = torch.equal(got, want)
     if not ok:
-        diff = (got - want).abs().max().item() if got.shape == want.shape else "shape"
+        diff = (got - want).abs().max().item()
         fails.append(f"{name}: max diff {diff}")
     return ok
 
 
 def stress(iters):
-    """Random arrival order at every collective; results checked after the burst."""
+    """Random arrival order at every collective; results checked after the burst.
+    Mixes symmetric (zero-copy) and staged calls, up to 16 MiB."""
     import random
 
     rng = random.Random(1234 + rank)  # per-rank: delays only
-    shared = random.Random(99)        # identical on every rank: sizes and algorithms
+    shared = random.Random(99)        # identical on every rank: sizes, algorithms, symmetric or not
     pending = []
-    algos_s = ["oneshot", "twoshot", "push", "reduce_bcast"]
-    sym_x = dev.empty(1 << 16, torch.float32)
+    algos_s = AR_ALGOS
+    big = 4 << 20  # elements: 16 MiB fp32
+    sym_x = dev.empty(big, torch.float32)
+    sym_y = dev.empty(big, torch.float32)
     for i in range(iters):
-        n = shared.choice([1, 33, 4096, 1 << 16])
+        n = shared.choice([1, 33, 4096, 1 << 16, 1 << 20, big])
         algo = shared.choice(algos_s)
+        sym = shared.random() < 0.5
         d = rng.random()
         if d < 0.3:
             time.sleep(rng.random() * 0.004)
         elif d < 0.6:
             torch.cuda._sleep(rng.randint(1000, 200000))  # device-side skew
-        x = gen(rank, n, torch.float32, 50000 + i).to(dev.device, non_blocking=True)
-        if i % 3 == 0:  # symmetric, zero-copy path
-            xs = sym_x[:n]
-            xs.copy_(x)
-            x = xs
-        y = torch.empty(n, dtype=torch.float32, device=dev.device)
+        x = gen(rank, n, torch.float32, 50000 + i)
+        if sym:
+            sym_x[:n].copy_(x)
+            x, y = sym_x[:n], sym_y[:n]
+        else:
+            y = torch.empty(n, dtype=torch.float32, device=D)
         dev.allreduce(x, y, "SUM", algo)
-        pending.append((f"stress[{i},{algo},n={n}]", y.clone(), n, 50000 + i))
+        pending.append((f"stress[{i},{algo},n={n},sym={sym}]", y.clone(), n, 50000 + i))
     torch.cuda.synchronize()
     dev.check()
     for name, y, n, sl in pending:
@@ -127,124 +168,204 @@ def fault():
                 fails.append(f"fault: message not rank-tagged: {e}")
     dev.reset()
     dev.dc.set_timeout_seconds(20.0)
-    dev.allreduce(x, y, "SUM", "twoshot")
-    check("fault_recovery_allreduce", y, torch.full((4096,), float(p), dtype=torch.float64), torch.float32)
+    for algo in ("twoshot", "ring"):
+        dev.allreduce(x, y, "SUM", algo)
+        check(f"fault_recovery_allreduce[{algo}]", y, torch.full((4096,), float(p), dtype=torch.float64, device=D),
+              torch.float32)
 
 
-if args.stress or args.fault:
-    t0 = time.time()
-    if args.stress:
-        stress(args.stress)
-    if args.fault:
-        fault()
+def finish(t0):
     comm.Barrier()
-    print(f"[rank {rank}/{p}] stress/fault checks: {len(fails)} failures, {time.time() - t0:.1f}s", flush=True)
+    print(f"[rank {rank}/{p}] device checks: {ncheck} checks, {len(fails)} failures, {time.time() - t0:.1f}s", flush=True)
     for f in fails[:20]:
         print(f"[rank {rank}] FAIL {f}", flush=True)
     sys.exit(1 if fails else 0)
 
-sizes = [int(s) for s in args.sizes.split(",") if s] or ([1, 7, 1000, 65536 + 3] if args.quick else
-                                                          [1, 3, 8, 1000, 4097, 65536 + 3, 1 << 20, (1 << 22) + 5])
-dtypes = [torch.float32, torch.bfloat16] if args.quick else [torch.float32, torch.bfloat16, torch.float16,
-                                                              torch.float64, torch.int32, torch.int64]
-algos = ["oneshot", "twoshot", "reduce_bcast", "push"]
-salt = 0
+
 t0 = time.time()
+if args.stress or args.fault:
+    if args.stress:
+        stress(args.stress)
+    if args.fault:
+        fault()
+    finish(t0)
+
+ALL_DT = [torch.float32, torch.bfloat16, torch.float16, torch.float64, torch.int32, torch.int64]
+ALL_OPS = ["SUM", "PROD", "MIN", "MAX"]
+if args.matrix == "quick":
+    sizes, dtypes, ops = [1, 7, 1000, 65536 + 3], [torch.float32, torch.bfloat16], ["SUM"]
+elif args.matrix == "wide":
+    sizes, dtypes, ops = [1, 1000, 65536 + 3, (1 << 20) + 3], ALL_DT, ALL_OPS
+elif args.matrix == "full":
+    sizes, dtypes, ops = [1, 3, 8, 1000, 4097, 65536 + 3, 1 << 20, (1 << 22) + 5], ALL_DT, ALL_OPS
+else:
+    sizes, dtypes, ops = [], [], []
+if args.sizes:
+    sizes = [int(x) for x in args.sizes.split(",") if x]
+salt = 0
+
+
+def sym_copy(t):
+    s_ = dev.empty(t.numel(), t.dtype)
+    s_.copy_(t)
+    return s_
+
+
+# ---------------------------------------------------------------- all-reduce
 for sym in (False, True):
     for n in sizes:
         for dt in dtypes:
-            for op in (["SUM", "MAX"] if not args.quick else ["SUM"]):
-                for algo in algos:
+            for op in ops:
+                for algo in AR_ALGOS:
                     salt += 1
-                    x = gen(rank, n, dt, salt).to(dev.device)
+                    x = gen(rank, n, dt, salt, op)
                     if sym:
-                        xs = dev.empty(n, dt); xs.copy_(x); x = xs
-                        y = dev.empty(n, dt)
+                        x, y = sym_copy(x), dev.empty(n, dt)
                     else:
                         y = torch.empty_like(x)
                     dev.allreduce(x, y, op, algo)
-                    check(f"allreduce[{algo},{dt},{op},n={n},sym={sym}]", y, oracle(n, dt, op, salt), dt, p)
-                    # in-place
-                    z = gen(rank, n, dt, salt).to(dev.device)
+                    want = oracle(n, dt, op, salt)
+                    check(f"allreduce[{algo},{dt},{op},n={n},sym={sym}]", y, want, dt, p)
+                    z = gen(rank, n, dt, salt, op)
+                    if sym:
+                        z = sym_copy(z)
                     dev.allreduce(z, z, op, algo)
-                    check(f"allreduce_inplace[{algo},{dt},{op},n={n}]", z, oracle(n, dt, op, salt), dt, p)
+                    check(f"allreduce_inplace[{algo},{dt},{op},n={n},sym={sym}]", z, want, dt, p)
+if dtypes and not POW2:  # recursive halving/doubling refuses non-power-of-two groups on every rank
+    try:
+        x = torch.ones(64, device=D)
+        dev.allreduce(x, x, "SUM", "rhd")
+        fails.append("rhd accepted a non-power-of-two group")
+    except ValueError:
+        pass
+
+# ------------------------------------------- reduce-scatter / gathers / bcast
+for sym in (False, True):
     for n in sizes[:6]:
-        for dt in dtypes[:2]:
+        for dt in dtypes[:3]:
+            for op in (ops[:1] + ops[2:3]):  # SUM and MIN
+                salt += 1
+                x = gen(rank, p * n, dt, salt, op)
+                if sym:
+                    x = sym_copy(x)
+                y = torch.empty(n, dtype=dt, device=D)
+                dev.reduce_scatter(x, y, op)
+                check(f"reduce_scatter[{dt},{op},n={n},sym={sym}]", y, oracle(p * n, dt, op, salt)[rank * n:(rank + 1) * n],
+                      dt, p)
             salt += 1
-            # reduce_scatter: input p*n, output n (block = rank)
-            x = gen(rank, p * n, dt, salt).to(dev.device)
+            x = gen(rank, n, dt, salt)
             if sym:
-                xs = dev.empty(p * n, dt); xs.copy_(x); x = xs
-            y = torch.empty(n, dtype=dt, device=dev.device)
-            dev.reduce_scatter(x, y, "SUM")
-            full = oracle(p * n, dt, "SUM", salt)
-            check(f"reduce_scatter[{dt},n={n},sym={sym}]", y, full[rank * n:(rank + 1) * n], dt, p)
-            # allgather
-            salt += 1
-            x = gen(rank, n, dt, salt).to(dev.device)
-            if sym:
-                xs = dev.empty(n, dt); xs.copy_(x); x = xs
-            y = torch.empty(p * n, dtype=dt, device=dev.device)
+                x = sym_copy(x)
+            y = torch.empty(p * n, dtype=dt, device=D)
             dev.allgather(x, y)
-            want = torch.cat([gen(r, n, dt, salt) for r in range(p)]).to(torch.float64 if dt.is_floating_point else torch.int64)
+            want = torch.cat([gen(r, n, dt, salt) for r in range(p)]).to(WIDE(dt))
             check(f"allgather[{dt},n={n},sym={sym}]", y, want, dt)
-            # alltoall
+            # all-to-all: pull (symmetric input or staged), push (symmetric output), in-place (staged)
             salt += 1
-            x = gen(rank, p * n, dt, salt).to(dev.device)
+            want = torch.cat([gen(r, p * n, dt, salt)[rank * n:(rank + 1) * n] for r in range(p)]).to(WIDE(dt))
+            x = gen(rank, p * n, dt, salt)
             if sym:
-                xs = dev.empty(p * n, dt); xs.copy_(x); x = xs
-            y = torch.empty(p * n, dtype=dt, device=dev.device)
+                x = sym_copy(x)
+            y = torch.empty(p * n, dtype=dt, device=D)
             dev.alltoall(x, y)
-            want = torch.cat([gen(r, p * n, dt, salt)[rank * n:(rank + 1) * n] for r in range(p)]).to(
-                torch.float64 if dt.is_floating_point else torch.int64)
-            check(f"alltoall[{dt},n={n},sym={sym}]", y, want, dt)
+            check(f"alltoall[direct,{dt},n={n},sym={sym}]", y, want, dt)
+            y2 = dev.empty(p * n, dt) if sym else torch.empty(p * n, dtype=dt, device=D)
+            dev.alltoall(gen(rank, p * n, dt, salt), y2, "push")
+            check(f"alltoall[push,{dt},n={n},sym_out={sym}]", y2, want, dt)
+            z = gen(rank, p * n, dt, salt)
+            if sym:
+                z = sym_copy(z)
+            dev.alltoall(z, z)
+            check(f"alltoall_inplace[{dt},n={n},sym={sym}]", z, want, dt)
             # bcast from root p-1
             salt += 1
             root = p - 1
-            b = gen(rank, n, dt, salt).to(dev.device)
+            b = gen(rank, n, dt, salt)
             if sym:
-                bs = dev.empty(n, dt); bs.copy_(b); b = bs
+                b = sym_copy(b)
             dev.bcast(b, root)
-            check(f"bcast[{dt},n={n},sym={sym}]", b, gen(root, n, dt, salt).to(torch.float64 if dt.is_floating_point else torch.int64), dt)
+            check(f"bcast[{dt},n={n},sym={sym}]", b, gen(root, n, dt, salt).to(WIDE(dt)), dt)
 
-# TP layout-fused collectives (reference naive collects on device tensors)
-from collective_communication_mpi_amd.parallel.layout import (  # noqa: E402
-    naive_collect_backward_x, naive_collect_forward_input)
-for dt in (torch.float32, torch.bfloat16):
-    for (B, S, k) in [(2, 3, 8), (4, 16, 64), (3, 5, 3)]:
-        salt += 1
-        shards = [gen(r, B * S * k, dt, salt).view(B, S, k) for r in range(p)]
-        got = naive_collect_forward_input(shards[rank].to(dev.device), comm, p)
-        want = torch.cat(shards, dim=-1).to(torch.float64 if dt.is_floating_point else torch.int64)
-        check(f"forward_input_lastaxis[{dt},{B}x{S}x{k}]", got, want, dt)
-        salt += 1
-        full = [gen(r, B * S * k * p, dt, salt).view(B, S, k * p) for r in range(p)]
-        got = naive_collect_backward_x(full[rank].to(dev.device), comm, p)
-        ref = sum(f.to(torch.float64) for f in full)[:, :, rank * k:(rank + 1) * k]
-        check(f"backward_x_lastaxis[{dt},{B}x{S}x{k}]", got, ref, dt, p)
+# ------------------------------------- TP layout-fused collectives (func_impl)
+if dtypes:
+    from collective_communication_mpi_amd.parallel.layout import (  # noqa: E402
+        naive_collect_backward_x, naive_collect_forward_input)
+    for dt in (torch.float32, torch.bfloat16):
+        for (B, S, k) in [(2, 3, 8), (4, 16, 64), (3, 5, 3)]:
+            salt += 1
+            shards = [gen(r, B * S * k, dt, salt).view(B, S, k) for r in range(p)]
+            got = naive_collect_forward_input(shards[rank].clone(), comm, p)
+            check(f"forward_input_lastaxis[{dt},{B}x{S}x{k}]", got, torch.cat(shards, dim=-1).to(WIDE(dt)), dt)
+            salt += 1
+            full = [gen(r, B * S * k * p, dt, salt).view(B, S, k * p) for r in range(p)]
+            got = naive_collect_backward_x(full[rank].clone(), comm, p)
+            ref = sum(f.to(torch.float64) for f in full)[:, :, rank * k:(rank + 1) * k]
+            check(f"backward_x_lastaxis[{dt},{B}x{S}x{k}]", got, ref, dt, p)
+
+# ------------------------------------------------------- >= 96 MiB: chunk loops
+if args.big:
+    n = (24 << 20) + 5  # 96 MiB + 20 B of fp32: > 32 MiB staging chunks, odd tail
+    for algo in ("twoshot", "ring") + (("rhd",) if POW2 else ()):
+        for sym in (False, True):
+            salt += 1
+            x = gen(rank, n, torch.float32, salt)
+            if sym:
+                x, y = sym_copy(x), dev.empty(n, torch.float32)
+            else:
+                y = torch.empty_like(x)
+            dev.allreduce(x, y, "SUM", algo)
+            check(f"big_allreduce[{algo},sym={sym}]", y, oracle(n, torch.float32, "SUM", salt), torch.float32, p)
+            del x, y
+    nb = ((24 << 20) // p) + 3
+    salt += 1
+    x = gen(rank, p * nb, torch.float32, salt)
+    y = torch.empty_like(x)
+    dev.alltoall(x, y)
+    want = torch.cat([gen(r, p * nb, torch.float32, salt)[rank * nb:(rank + 1) * nb] for r in range(p)]).double()
+    check("big_alltoall[staged]", y, want, torch.float32)
+    dev.alltoall(x, x)
+    check("big_alltoall[inplace]", x, want, torch.float32)
+    salt += 1
+    x = gen(rank, p * nb, torch.float32, salt)
+    y = torch.empty(nb, device=D)
+    dev.reduce_scatter(x, y)
+    check("big_reduce_scatter[staged]", y, oracle(p * nb, torch.float32, "SUM", salt)[rank * nb:(rank + 1) * nb],
+          torch.float32, p)
+    salt += 1
+    x = gen(rank, nb, torch.float32, salt)
+    y = torch.empty(p * nb, device=D)
+    dev.allgather(x, y)
+    check("big_allgather[staged]", y, torch.cat([gen(r, nb, torch.float32, salt) for r in range(p)]).double(),
+          torch.float32)
+    torch.cuda.empty_cache()
+
 torch.cuda.synchronize()
 dev.check()
+
+# ---------------------------------------------------- RCCL (fails loudly)
 if args.rccl:
-    try:
-        x = gen(rank, 4096, torch.float32, 7).to(dev.device)
-        y = torch.empty_like(x)
-        dev.allreduce(x, y, "SUM", "rccl")
-        check("rccl_allreduce", y, oracle(4096, torch.float32, "SUM", 7), torch.float32, p)
-        for algo in ("ring", "rhd"):
-            x = gen(rank, 10001, torch.float32, 9).to(dev.device)
-            dev.allreduce(x, x, "SUM", algo)
-            check(f"p2p_{algo}", x, oracle(10001, torch.float32, "SUM", 9), torch.float32, p)
-    except Exception as e:  # noqa: BLE001
-        print(f"[rank {rank}] RCCL path unavailable: {e}", flush=True)
+    x = gen(rank, 4096, torch.float32, 7)
+    y = torch.empty_like(x)
+    dev.allreduce(x, y, "SUM", "rccl")
+    check("rccl_allreduce", y, oracle(4096, torch.float32, "SUM", 7), torch.float32, p)
+    for algo in ("ring_rccl",) + (("rhd_rccl",) if POW2 else ()):
+        x = gen(rank, 10001, torch.float32, 9)
+        dev.allreduce(x, x, "SUM", algo)
+        check(f"p2p_{algo}", x, oracle(10001, torch.float32, "SUM", 9), torch.float32, p)
+    x = gen(rank, p * 999, torch.float32, 13)
+    y = torch.empty_like(x)
+    dev.alltoall(x, y, "pairwise")
+    check("p2p_pairwise_alltoall", y,
+          torch.cat([gen(r, p * 999, torch.float32, 13)[rank * 999:(rank + 1) * 999] for r in range(p)]).double(),
+          torch.float32)
 
 # communicator façade + accounting on device tensors
-x = gen(rank, 1024, torch.float32, 11).to(dev.device)
+x = gen(rank, 1024, torch.float32, 11)
 y = torch.empty_like(x)
+before = comm.total_bytes_transferred
 comm.myAllreduce(x, y, MPI.SUM)
 check("myAllreduce(device)", y, oracle(1024, torch.float32, "SUM", 11), torch.float32, p)
-comm.Barrier()
-msg = f"[rank {rank}/{p}] device checks: {len(fails)} failures, {time.time() - t0:.1f}s"
-print(msg, flush=True)
-for f in fails[:20]:
-    print(f"[rank {rank}] FAIL {f}", flush=True)
-sys.exit(1 if fails else 0)
+want_bytes = 2 * 4096 * (p - 1) if rank == 0 else 2 * 4096
+if comm.total_bytes_transferred - before != want_bytes:
+    fails.append(f"myAllreduce accounting {comm.total_bytes_transferred - before} != {want_bytes}")
+finish(t0)
