@@ -4,11 +4,64 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <memory>
+
 #include "device_comm.hpp"
 #include "ops.hpp"
+#include "symheap.hpp"
 
 namespace py = pybind11;
 using namespace ccmpi::dev;
+
+namespace {
+// Minimal DLPack (v0.8 ABI) to hand symmetric-heap blocks to torch with a
+// deleter that returns the block to the heap when the tensor's storage dies.
+struct DLDevice { int32_t device_type; int32_t device_id; };
+struct DLDataType { uint8_t code; uint8_t bits; uint16_t lanes; };
+struct DLTensor {
+  void* data; DLDevice device; int32_t ndim; DLDataType dtype; int64_t* shape; int64_t* strides; uint64_t byte_offset;
+};
+struct DLManagedTensor { DLTensor dl_tensor; void* manager_ctx; void (*deleter)(DLManagedTensor*); };
+constexpr int32_t kDLROCM = 10;
+constexpr uint8_t kDLUInt = 1;
+
+struct BlockCtx {
+  std::shared_ptr<SymHeap> heap;
+  uint64_t ptr;
+  int64_t shape[1];
+};
+
+void block_deleter(DLManagedTensor* t) {  // may run without the GIL: no Python here
+  auto* c = static_cast<BlockCtx*>(t->manager_ctx);
+  c->heap->release(c->ptr);
+  delete c;
+  delete t;
+}
+
+void capsule_destructor(PyObject* cap) {  // only when torch never consumed the capsule
+  if (PyCapsule_IsValid(cap, "dltensor")) {
+    auto* t = static_cast<DLManagedTensor*>(PyCapsule_GetPointer(cap, "dltensor"));
+    if (t && t->deleter) t->deleter(t);
+  }
+}
+
+py::object heap_block(const std::shared_ptr<SymHeap>& heap, uint64_t bytes, int device) {
+  const uint64_t ptr = heap->alloc(bytes);
+  if (!ptr) return py::none();
+  auto* c = new BlockCtx{heap, ptr, {(int64_t)bytes}};
+  auto* t = new DLManagedTensor{};
+  t->dl_tensor.data = reinterpret_cast<void*>(ptr);
+  t->dl_tensor.device = {kDLROCM, device};
+  t->dl_tensor.ndim = 1;
+  t->dl_tensor.dtype = {kDLUInt, 8, 1};
+  t->dl_tensor.shape = c->shape;
+  t->dl_tensor.strides = nullptr;
+  t->dl_tensor.byte_offset = 0;
+  t->manager_ctx = c;
+  t->deleter = block_deleter;
+  return py::reinterpret_steal<py::object>(PyCapsule_New(t, "dltensor", capsule_destructor));
+}
+}  // namespace
 
 PYBIND11_MODULE(_device, m) {
   m.doc() = "ccmpi device plane: hand-written CDNA4 collectives + kernels (HIP, gfx950)";
@@ -33,6 +86,18 @@ PYBIND11_MODULE(_device, m) {
       py::arg("src"), py::arg("dst"), py::arg("nbytes"), py::arg("variant"), py::arg("grid") = 0,
       py::arg("stream") = 0, py::call_guard<py::gil_scoped_release>());
   m.def("rccl_unique_id", []() { return py::bytes(DeviceComm::rccl_unique_id()); });
+
+  py::class_<SymHeap, std::shared_ptr<SymHeap>>(m, "SymHeap")
+      .def(py::init([]() { return std::make_shared<SymHeap>(); }))
+      .def("add_arena", &SymHeap::add_arena)
+      .def("alloc", &SymHeap::alloc)
+      .def("release", &SymHeap::release)
+      // DLPack capsule of a fresh `bytes`-long uint8 block on `device` (None when full)
+      .def("block", [](const std::shared_ptr<SymHeap>& h, uint64_t bytes, int device) { return heap_block(h, bytes, device); })
+      .def_property_readonly("used_bytes", &SymHeap::used_bytes)
+      .def_property_readonly("capacity", &SymHeap::capacity)
+      .def_property_readonly("largest_free", &SymHeap::largest_free)
+      .def_property_readonly("live_blocks", &SymHeap::live_blocks);
 
   py::class_<DeviceComm>(m, "DeviceComm")
       .def(py::init<int, int, int, uint64_t>(), py::arg("rank"), py::arg("size"), py::arg("device"),

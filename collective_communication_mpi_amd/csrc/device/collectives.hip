@@ -409,7 +409,7 @@ __global__ void __launch_bounds__(kThreads) k_allreduce_twoshot_push(CollArgs a)
   const uint64_t e = s_epoch;
   const PeerTable* pt = a.pt;
   const int me = pt->rank, nr = pt->size;
-  const char* src = resolve(pt, me, a.src_code);
+  const char* src = a.in;  // local input; codes[0][j] = rank j's inbox, codes[1][j] = its result
   const uint64_t shard = (((a.nbytes + nr - 1) / nr) + 15) / 16 * 16;  // inbox slot stride
   // ---- phase 1: scatter my input shards into the owners' inboxes
   {
@@ -421,7 +421,7 @@ __global__ void __launch_bounds__(kThreads) k_allreduce_twoshot_push(CollArgs a)
       BlockRange sj = part16(a.nbytes, nr, j);
       BlockRange bj = part16(sj.hi - sj.lo, gridDim.x, blockIdx.x);
       srcs[j] = src + sj.lo + bj.lo;
-      dsts[j] = resolve(pt, j, a.aux_code) + (uint64_t)me * shard + bj.lo;
+      dsts[j] = resolve(pt, j, codes[0][j]) + (uint64_t)me * shard + bj.lo;
       lens[j] = bj.hi - bj.lo;
     }
     __syncthreads();
@@ -440,7 +440,7 @@ __global__ void __launch_bounds__(kThreads) k_allreduce_twoshot_push(CollArgs a)
     __shared__ char* outs[kMaxRanks];
     if (threadIdx.x < nr) outs[threadIdx.x] = resolve(pt, threadIdx.x, codes[1][threadIdx.x]) + mys.lo + sub.lo;
     __syncthreads();
-    reduce_fanout<DT, OP, NRM>(resolve(pt, me, a.aux_code) + sub.lo, shard, nr, sub.hi - sub.lo, outs);
+    reduce_fanout<DT, OP, NRM>(resolve(pt, me, codes[0][me]) + sub.lo, shard, nr, sub.hi - sub.lo, outs);
   }
   if (!sync_phase(a, 3, e)) return;
   finish(a, e);
@@ -665,8 +665,8 @@ __global__ void __launch_bounds__(kThreads) k_allreduce_ring(CollArgs a) {
   const uint64_t slot = a.inbox_slot, base = e * kStepsPerEpoch;
   char* out = a.out;
   char* r_out = resolve(pt, right, codes[1][right]);
-  const char* inbox = resolve(pt, me, a.aux_code);
-  char* r_inbox = resolve(pt, right, a.aux_code);
+  const char* inbox = resolve(pt, me, codes[0][me]);  // inboxes are published in slot 0
+  char* r_inbox = resolve(pt, right, codes[0][right]);
   const uint64_t* my_flag = &pt->sig[me]->step[b][left];
   uint64_t* r_flag = &pt->sig[right]->step[b][me];
   // reduce-scatter
@@ -715,7 +715,7 @@ __global__ void __launch_bounds__(kThreads) k_allreduce_rhd(CollArgs a) {
   const int me = pt->rank, p = pt->size, b = blockIdx.x;
   const uint64_t slot = a.inbox_slot, base = e * kStepsPerEpoch;
   char* out = a.out;
-  const char* inbox = resolve(pt, me, a.aux_code);
+  const char* inbox = resolve(pt, me, codes[0][me]);  // inboxes are published in slot 0
   Signals* mine = pt->sig[me];
   int step = 0, L = 0;
   uint64_t slot_off = 0;
@@ -723,7 +723,7 @@ __global__ void __launch_bounds__(kThreads) k_allreduce_rhd(CollArgs a) {
     const int partner = me ^ m;
     const int keep = (me & m) ? L + m : L, give = (me & m) ? L : L + m;
     const char* from = step == 0 ? a.in : out;
-    char* p_inbox = resolve(pt, partner, a.aux_code) + slot_off;
+    char* p_inbox = resolve(pt, partner, codes[0][partner]) + slot_off;
     for (int i = 0; i < m; ++i) {
       const SubSlice s = sub_slice(a.nbytes, p, give + i, slot);
       combine_span<DT, OP, false, false>(from + s.lo, nullptr, p_inbox + i * slot + s.rel, nullptr, s.len);

@@ -38,8 +38,9 @@ struct CollArgs {
   uint64_t timeout_ticks;  // bounded spins, 100 MHz ticks
   int root;
   int nrings;              // ring: number of concurrent rings (CTA b runs ring b % nrings)
-  uint64_t aux_code;       // symmetric inbox (push two-shot, ring, rhd): same code on every rank
-  const char* in;          // local input (ring / rhd / push all-to-all read only their own input)
+  uint64_t aux_code;       // unused (inboxes are published through src_code)
+  const char* in;          // local input (push two-shot / ring / rhd / push all-to-all read only their own input;
+                           // those kernels publish the inbox in src_code instead)
   uint64_t src_stride;     // all-to-all: bytes between per-peer blocks of the source (0 = nbytes)
   uint64_t dst_stride;     // all-to-all: bytes between per-peer blocks of the destination (0 = nbytes)
   uint64_t inbox_slot;     // ring / rhd: bytes per inbox chunk slot (>= the largest chunk, 16-B multiple)

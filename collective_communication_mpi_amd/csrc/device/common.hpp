@@ -40,7 +40,7 @@ enum DType : int {
 enum ROp : int { OP_SUM = 0, OP_PROD, OP_MIN, OP_MAX };
 
 constexpr int kMaxRanks = 16;     // ranks per device communicator
-constexpr int kMaxSegs = 32;      // registered symmetric segments per rank
+constexpr int kMaxSegs = 64;      // registered symmetric segments (heap arenas) per rank
 constexpr int kMaxBlocks = 1024;  // max CTAs of one collective launch
 constexpr int kCachePolicySys = 17;  // aux bits: sc0 | sc1 (system coherent)
 constexpr uint64_t kStepsPerEpoch = 64;  // > 2 * (kMaxRanks - 1) signals per call

@@ -235,8 +235,8 @@ void DeviceComm::allreduce(uint64_t in, uint64_t out, uint64_t count, int dtype,
     const uint64_t ic = inbox_ptr_ ? code_of_(inbox_ptr_, inbox_bytes_) : 0;
     uint64_t sc = code_of_(in, nbytes), rc = code_of_(out, nbytes);
     if (symmetric && sc && rc && ic && in != out && inbox_bytes_ >= shard * size_) {
-      CollArgs a = args_(sc, rc, (char*)out, nbytes, 0);
-      a.aux_code = ic;
+      CollArgs a = args_(ic, rc, (char*)out, nbytes, 0);  // the inbox is published in slot 0
+      a.in = reinterpret_cast<const char*>(in);
       launch_allreduce(ALGO_TWOSHOT_PUSH, a, size_, dtype, op, grid_(nbytes / size_, max_blocks), st);
       return;
     }
@@ -333,9 +333,8 @@ void DeviceComm::allreduce_pipelined_(int algo, uint64_t in, uint64_t out, uint6
       rc = addr_code(0, half);
       outp = stage + half;
     }
-    CollArgs a = args_(0, rc, outp, n, 0);
+    CollArgs a = args_(ic, rc, outp, n, 0);  // the inbox is published in slot 0
     a.in = inp;
-    a.aux_code = ic;
     a.inbox_slot = ring_slot_bytes(n, p);
     a.nrings = R;
     for (int k = 0; k < R; ++k) {

@@ -107,8 +107,10 @@ class DeviceGroup:
         self.max_blocks = _env_int("CCMPI_MAX_BLOCKS", default_blocks)
         if scratch_bytes is None:
             scratch_bytes = _env_int("CCMPI_SCRATCH_MB", 64 if self.shared_device else 512) << 20
-        self._keep: List = []
-        self._pool: List[Tuple[object, int, int]] = []  # (tensor, used, cap) sub-allocation pools
+        self._keep: List = []   # registered segments (scratch, heap arenas) live as long as the group
+        self.heap = self.D.SymHeap()
+        self.arena_bytes = _env_int("CCMPI_HEAP_ARENA_MB", 256) << 20
+        self._inbox = None
         self.scratch = torch.empty(max(scratch_bytes, 1 << 16), dtype=torch.uint8, device=self.device)
         seg = self._register(self.scratch)
         assert seg == 0, "scratch must be segment 0"
@@ -177,11 +179,15 @@ class DeviceGroup:
     def _rccl_registering(self) -> bool:
         return getattr(self, "_rccl", False) and os.environ.get("CCMPI_RCCL_REGISTER") == "1"
 
-    def empty(self, shape, dtype=None, pool_bytes: int = 64 << 20):
+    def empty(self, shape, dtype=None):
         """Collective symmetric allocation (same call sequence on every rank).
 
-        Large tensors get their own segment; small ones are carved (256-B
-        aligned) from a shared pooled segment.  Memory lives until the group dies.
+        Blocks come from the symmetric heap (csrc/device/symheap.cpp): a
+        best-fit allocator over IPC-registered arenas of ``CCMPI_HEAP_ARENA_MB``
+        (default 256 MiB, or the request if larger), grown collectively when
+        full.  The tensor owns its block through a DLPack deleter: the block
+        returns to the heap when the last view dies (stream-ordered reuse,
+        like torch's caching allocator).
         """
         torch = self.torch
         dtype = dtype or torch.float32
@@ -191,19 +197,21 @@ class DeviceGroup:
         for s in shape:
             n *= int(s)
         nbytes = n * torch.empty((), dtype=dtype).element_size()
-        need = (max(nbytes, 1) + 255) // 256 * 256
-        if need >= pool_bytes // 4:
-            raw = torch.empty(need, dtype=torch.uint8, device=self.device)
-            self._register(raw)
-            return raw[:nbytes].view(dtype).view(shape)
-        for i, (buf, used, cap) in enumerate(self._pool):
-            if used + need <= cap:
-                self._pool[i] = (buf, used + need, cap)
-                return buf[used:used + nbytes].view(dtype).view(shape)
-        buf = torch.empty(pool_bytes, dtype=torch.uint8, device=self.device)
-        self._register(buf)
-        self._pool.append((buf, need, pool_bytes))
-        return buf[:nbytes].view(dtype).view(shape)
+        need = max(nbytes, 1)
+        idx = self.device.index or 0
+        cap = self.heap.block(need, idx)
+        if cap is None:
+            self._grow_heap(need)
+            cap = self.heap.block(need, idx)
+        raw = torch.utils.dlpack.from_dlpack(cap)
+        return raw[:nbytes].view(dtype).view(shape)
+
+    def _grow_heap(self, need: int) -> None:
+        """Collective: register one more arena (every rank grows at the same call)."""
+        arena = max(self.arena_bytes, (need + (2 << 20) - 1) // (2 << 20) * (2 << 20) + 4096)
+        raw = self.torch.empty(arena, dtype=self.torch.uint8, device=self.device)
+        self._register(raw)
+        self.heap.add_arena(raw.data_ptr(), arena)
 
     def zeros(self, shape, dtype=None):
         t = self.empty(shape, dtype)
@@ -224,8 +232,10 @@ class DeviceGroup:
         if self.dc.inbox_bytes >= need:
             return
         cap = max(need, 64 << 20)
-        buf = self.empty(cap, self.torch.uint8)
-        self.dc.set_inbox(buf.data_ptr(), cap)
+        self.dc.set_inbox(0, 0)
+        self._inbox = None  # old inbox back to the heap first (same order on every rank)
+        self._inbox = self.empty(cap, self.torch.uint8)
+        self.dc.set_inbox(self._inbox.data_ptr(), cap)
 
     # -------------------------------------------------------------------- rccl
     def ensure_rccl(self) -> None:
