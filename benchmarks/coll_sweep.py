@@ -167,7 +167,8 @@ blocks = [int(b) for b in args.blocks.split(",")]
 for op in ops:
     algos = DEFAULT_ALGOS[op]
     if args.algos:  # the requested algorithms this op has (lastaxis: gather / rscatter)
-        valid = set(DEFAULT_ALGOS[op]) | {"rccl", "pairwise", "ring_rccl", "rhd_rccl", "ring", "rhd"}
+        valid = set(DEFAULT_ALGOS[op]) | {"rccl"} | ({"ring_rccl", "rhd_rccl"} if op == "allreduce" else set()) \
+            | ({"pairwise"} if op == "alltoall" else set())
         algos = [a for a in args.algos.split(",") if a in valid] or DEFAULT_ALGOS[op]
     for algo in algos:
         for mb in blocks:

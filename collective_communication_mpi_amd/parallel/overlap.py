@@ -1,0 +1,92 @@
+"""DP gradient all-reduce overlapped with the backward (BASELINE config 5:
+"DP8 gradient all-reduce, Llama-3-8B-sized grad (~16 GB bf16) overlapped with
+backward on 8xMI355X").
+
+A synthetic backward over ``layers`` Llama-3-8B decoder layers (d 4096, GQA
+kv 1024, MLP 14336; 218 M weights per layer, 32 layers = 7.0 B weights =
+14 GB of bf16 gradients): per layer the seven weight gradients
+dW = dY^T X are produced by the MFMA GEMM (``gemm_nt`` over the token axis,
+fp32 accumulate, bf16 out) straight into a flat bf16 gradient buffer on the
+symmetric heap.  As soon as a layer's GEMMs are queued, an event hands that
+layer's slice (one bucket) to a high-priority side stream, which all-reduces
+it with the framework's device all-reduce while the next layer's GEMMs run.
+Activations are kept feature-major ([features, tokens]) so every wgrad GEMM
+reads K-contiguous operands, as the real backward's saved activations are.
+
+Reports compute-only, comm-only and overlapped step times (max over ranks),
+and ``comm_hidden_fraction`` = (compute + comm - overlapped) / comm.
+"""
+from __future__ import annotations
+
+import time
+from typing import Dict, List, Tuple
+
+import torch
+
+from ..ops import gemm_nt
+
+LLAMA3_8B = {"d": 4096, "kv": 1024, "ff": 14336}
+
+
+def layer_weight_shapes(d: int, kv: int, ff: int) -> List[Tuple[int, int]]:
+    """(out_features, in_features) of q, k, v, o, gate, up, down."""
+    return [(d, d), (kv, d), (kv, d), (d, d), (ff, d), (ff, d), (d, ff)]
+
+
+def dp_grad_overlap(comm, layers: int = 32, tokens: int = 4096, iters: int = 3, algo: str = "auto",
+                    priority: int = -1, dims: Dict[str, int] = LLAMA3_8B, seed: int = 0) -> Dict:
+    from .. import mpi as MPI
+
+    dev = comm.dev
+    hc = comm.comm
+    p = comm.Get_size()
+    d, kv, ff, T = dims["d"], dims["kv"], dims["ff"], tokens
+    shapes = layer_weight_shapes(d, kv, ff)
+    per_layer = sum(a * b for a, b in shapes)
+    grads = dev.empty(per_layer * layers, torch.bfloat16)  # bf16 grads, symmetric heap (zero-copy all-reduce)
+    g = torch.Generator(device=dev.device).manual_seed(seed + comm.Get_rank())
+    x_t = {k: (torch.randn(k, T, generator=g, device=dev.device) * 0.05).bfloat16() for k in {d, ff}}
+    dy_t = {k: (torch.randn(k, T, generator=g, device=dev.device) * 0.05).bfloat16() for k in {d, kv, ff}}
+    side = torch.cuda.Stream(device=dev.device, priority=priority)
+    events = [torch.cuda.Event() for _ in range(layers)]
+
+    def backward(comm_on: bool, compute_on: bool = True) -> None:
+        for layer in reversed(range(layers)):
+            base = layer * per_layer
+            if compute_on:
+                o = base
+                for fo, fi in shapes:
+                    gemm_nt(dy_t[fo], x_t[fi], out=grads[o:o + fo * fi].view(fo, fi))
+                    o += fo * fi
+            if comm_on:
+                events[layer].record()
+                side.wait_event(events[layer])
+                with torch.cuda.stream(side):
+                    seg = grads[base:base + per_layer]
+                    dev.allreduce(seg, seg, "SUM", algo)
+        torch.cuda.current_stream().wait_stream(side)
+
+    def timed(**kw) -> float:
+        backward(**kw)
+        torch.cuda.synchronize()
+        hc.Barrier()
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            backward(**kw)
+        torch.cuda.synchronize()
+        return hc.allreduce((time.perf_counter() - t0) / iters, op=MPI.MAX)
+
+    t_compute = timed(comm_on=False)
+    t_comm = timed(comm_on=True, compute_on=False) if p > 1 else 0.0
+    t_both = timed(comm_on=True) if p > 1 else t_compute
+    dev.check()
+    hidden = None if p == 1 or t_comm == 0 else max(0.0, min(1.0, (t_compute + t_comm - t_both) / t_comm))
+    flops = 2 * T * per_layer * layers
+    gbytes = per_layer * layers * 2
+    out = {"ranks": p, "layers": layers, "grad_bytes_bf16": gbytes, "tokens_per_rank": T,
+           "compute_ms": round(t_compute * 1e3, 3), "comm_ms": round(t_comm * 1e3, 3),
+           "overlapped_ms": round(t_both * 1e3, 3), "comm_hidden_fraction": None if hidden is None else round(hidden, 3),
+           "wgrad_TFLOPs": round(flops / t_compute / 1e12, 1), "shared_gpu": dev.shared_device,
+           "comm_algbw_GBps": round(gbytes / t_comm / 1e9, 2) if t_comm else None, "algo": algo}
+    del grads, x_t, dy_t
+    return out
