@@ -7,19 +7,31 @@
 Metric (BASELINE.json): "all-reduce algbw (GB/s) @1GiB fp32 + DP4xTP2 fwd step time".
 
 * A step = one out-of-place all-reduce (SUM) of a 1 GiB fp32 buffer through the
-  framework's ``Communicator.Allreduce`` on the GPU.  Buffers come from the
-  symmetric heap (``comm.empty``), the way framework users allocate
-  communication buffers.  ``value`` = algbw = 1 GiB / (time per all-reduce), the
-  NCCL-tests convention: a property of the whole collective, identical for every
-  rank.  Per-GPU work is fixed as N grows (weak scaling).  At N = 1 the
-  all-reduce is a local copy, so that number is a copy bandwidth.
-* The algorithm is picked once per run, like RCCL's tuner does.  Every candidate
-  runs once and is checked for an exact result (rank-valued inputs, so fp32 sums
-  are exact) before it is timed.  Candidates: the hand-written two-shot kernel
-  over IPC-mapped xGMI peer memory, the RCCL-send/recv multi-ring, and the RCCL
-  all-reduce.  The chosen algorithm and every candidate's time are reported.
-* Secondary: the DP x TP transformer-layer forward step time on MNIST-shaped
-  synthetic data.  The grid is TP=2 x DP=N/2 for N >= 2 (DP4xTP2 at N = 8).
+  framework's device all-reduce.  Buffers come from the symmetric heap
+  (``comm.empty``), the way framework users allocate communication buffers.
+  ``value`` = algbw = 1 GiB / (time per all-reduce), the NCCL-tests convention:
+  a property of the whole collective, identical for every rank.  Per-GPU work
+  is fixed as N grows (weak scaling).  At N = 1 the all-reduce is a local copy,
+  so that number is a copy bandwidth (see ``shared_gpu_dry_run`` below).
+* The algorithm is picked once per run, like RCCL's tuner does.  Every
+  candidate runs once and is checked for an exact result (rank-valued inputs,
+  so fp32 sums are exact) before it is timed: RCCL (the library baseline), the
+  hand-written two-shot over IPC-mapped xGMI peer memory at two CTA budgets,
+  the push two-shot, the hand-written multi-ring and recursive
+  halving/doubling kernels.  Every candidate's time is reported.
+* Secondary (BASELINE configs 2-5):
+  - ``bf16_1GiB``: the same all-reduce on a 1 GiB bf16 buffer;
+  - ``alltoall_256MiB``: all-to-all of 256 MiB per rank (pull, push, RCCL, pairwise);
+  - ``harness``: the DP x TP transformer-layer forward (HIP graph) and train step,
+    TP=2 x DP=N/2 for N >= 2 (DP4xTP2 at N = 8);
+  - ``dp_overlap``: Llama-3-8B-sized bf16 gradient all-reduce (32 layers, 14 GB)
+    overlapped with the wgrad GEMMs (parallel/overlap.py), N >= 2;
+  - ``shared_gpu_dry_run`` (N = 1 only): the N >= 2 code path -- the same
+    candidate loop minus RCCL, which refuses ranks sharing a GPU -- run with 8
+    ranks on this one GPU, so the 8-GPU path is exercised before any 8-GPU run.
+    Its numbers measure HBM + protocol, not xGMI.  The DP-overlap part is left
+    out there (8 processes' side-stream collectives next to their GEMMs on one
+    GPU time out; it is measured at 2 ranks: profiles/r2_overlap).
 
 The timed region is W untimed steps, then a barrier + device sync, K steps,
 and another device sync + barrier.  The time is the MAX over ranks.  Rank 0
@@ -37,6 +49,8 @@ import time
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
+GiB = 1 << 30
+
 
 def parse():
     ap = argparse.ArgumentParser()
@@ -44,10 +58,15 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--size-mb", type=int, default=1024)
-    ap.add_argument("--algo", default="auto", help="auto | twoshot | oneshot | rccl | ring | rhd | reduce_bcast")
+    ap.add_argument("--algo", default="auto", help="auto | twoshot | push | ring | rhd | oneshot | rccl | ...")
     ap.add_argument("--tp", type=int, default=0, help="TP degree of the harness step (default 2 if N>=2)")
     ap.add_argument("--batch", type=int, default=2048, help="images per DP replica for the harness step")
+    ap.add_argument("--dp-layers", type=int, default=32, help="Llama-3-8B layers of the DP-overlap measurement")
+    ap.add_argument("--dp-tokens", type=int, default=4096)
+    ap.add_argument("--a2a-mb", type=int, default=256)
+    ap.add_argument("--shared-dry-run", type=int, default=8, help="N=1: ranks of the shared-GPU dry run (0 = off)")
     ap.add_argument("--no-harness", action="store_true")
+    ap.add_argument("--no-secondary", action="store_true")
     ap.add_argument("--verbose", action="store_true")
     return ap.parse_args()
 
@@ -59,6 +78,31 @@ def relaunch(n: int) -> int:
 
     argv = [sys.executable, os.path.abspath(__file__)] + sys.argv[1:]
     return launch(n, argv, env_extra={"CCMPI_BENCH_CHILD": "1"})
+
+
+def shared_dry_run(n: int, steps: int, warmup: int, verbose: bool):
+    """Run this bench with n ranks on this GPU (the N >= 2 path) and return its JSON."""
+    cmd = [sys.executable, "-m", "collective_communication_mpi_amd.launch", "-n", str(n), "--timeout", "420",
+           sys.executable, os.path.abspath(__file__), "--gpus", str(n), "--steps", str(steps), "--warmup", str(warmup),
+           "--dp-layers", "0", "--a2a-mb", "64", "--shared-dry-run", "0"]
+    env = dict(os.environ, CCMPI_BENCH_CHILD="1")
+    try:
+        r = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=480)
+    except subprocess.TimeoutExpired:
+        return {"error": "timeout"}
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    if r.returncode != 0 or not lines:
+        return {"error": f"rc={r.returncode}", "stderr_tail": r.stderr[-800:]}
+    out = json.loads(lines[-1])
+    if verbose:
+        print("[bench] shared dry run:", lines[-1][:400], file=sys.stderr)
+    keep = {k: out[k] for k in ("value", "ms_per_step", "n_gpus")}
+    keep["ranks"] = n
+    keep["note"] = f"{n} ranks sharing ONE GPU through IPC: HBM + protocol, not xGMI"
+    keep.update({k: out["config"].get(k) for k in ("allreduce_algo", "busbw_GBps", "candidates_ms", "result_exact",
+                                                     "bf16_1GiB", "alltoall", "dp_overlap", "tp_fwd_step_ms",
+                                                     "parallelism")})
+    return keep
 
 
 def main() -> int:
@@ -88,100 +132,164 @@ def main() -> int:
         if rank == 0 and args.verbose:
             print("[bench]", *a, file=sys.stderr, flush=True)
 
-    # ------------------------------------------------------------- all-reduce
-    nbytes = args.size_mb << 20
-    n = nbytes // 4
-    x = dev.empty(n, torch.float32)
-    y = dev.empty(n, torch.float32)
-    x.fill_(float(rank + 1))
-    expect = float(world * (world + 1) // 2)
-    torch.cuda.synchronize()
-
-    def run(algo):
-        if algo == "ring4":
-            dev.allreduce(x, y, "SUM", "ring", rings=4)
-        else:
-            dev.allreduce(x, y, "SUM", algo)
-
-    def valid(algo) -> bool:
-        ok = 1
-        try:
-            y.zero_()
-            torch.cuda.synchronize()
-            hc.Barrier()
-            run(algo)
-            torch.cuda.synchronize()
-            dev.check()
-            ok = int(bool(torch.all(y == expect).item()))
-        except Exception as e:  # noqa: BLE001 - any failure disqualifies the candidate
-            log(f"candidate {algo} failed: {e}")
-            ok = 0
-        return bool(hc.allreduce(ok, op=MPI.MIN))
-
-    def timed(algo, iters) -> float:
+    def sync_barrier():
         torch.cuda.synchronize()
         hc.Barrier()
+
+    def timed(fn, iters) -> float:
+        sync_barrier()
         t0 = time.perf_counter()
         for _ in range(iters):
-            run(algo)
-        torch.cuda.synchronize()
-        hc.Barrier()
+            fn()
+        sync_barrier()
         return hc.allreduce(time.perf_counter() - t0, op=MPI.MAX) / iters
 
-    if world == 1:
-        candidates = ["twoshot"]  # single rank: the all-reduce is a device copy
-    elif args.algo != "auto":
-        candidates = [args.algo]
-    elif dev.shared_device:  # several ranks on one GPU (CI): grid is capped, RCCL refuses
-        candidates = ["twoshot", "push"]
-    else:
-        # RCCL first (baseline), then the hand-written two-shot at several CTA
-        # budgets (per-link in-flight bytes differ on xGMI), then RCCL-P2P rings.
-        candidates = ["rccl", "twoshot:128", "twoshot:256", "twoshot:512", "twoshot:1024", "push:256", "push:512", "ring4"]
-    results = {}
-    custom_failed = False
-    for algo in candidates:
-        custom = not algo.startswith(("rccl", "ring"))
-        if custom and custom_failed:
-            # the hand-written kernels share one flag protocol: after one of them failed
-            # (and waited out the device timeout) the others are not tried
-            results[algo] = None
-            continue
-        if not valid(algo):
-            results[algo] = None
-            if not algo.startswith(("rccl", "ring")):
-                custom_failed = True
-                dev.reset()  # a timed-out kernel leaves per-CTA epochs inconsistent
-            continue
-        run(algo)
-        results[algo] = timed(algo, 3)
-        log(f"candidate {algo}: {results[algo] * 1e3:.3f} ms")
-    good = {a: t for a, t in results.items() if t}
-    if not good:
-        raise SystemExit("no all-reduce algorithm produced a correct result")
-    best = min(good, key=good.get)
+    # ------------------------------------------------------------- all-reduce
+    nbytes = args.size_mb << 20
+    x = dev.empty(nbytes // 4, torch.float32)
+    y = dev.empty(nbytes // 4, torch.float32)
 
+    def ar_run(buf_in, buf_out, algo):
+        dev.allreduce(buf_in, buf_out, "SUM", algo)
+
+    def candidates():
+        if world == 1:
+            return ["twoshot"]  # single rank: the all-reduce is a device copy
+        if args.algo != "auto":
+            return [args.algo]
+        hand = ["twoshot:256", "twoshot:512", "push:512", "ring", "rhd" if world & (world - 1) == 0 else None]
+        hand = [a for a in hand if a]
+        # RCCL first (the library baseline); it refuses ranks that share a GPU
+        return hand if dev.shared_device else ["rccl"] + hand
+
+    custom_failed = [False]
+
+    def pick(buf_in, buf_out, expect, cands):
+        results = {}
+        for algo in cands:
+            custom = not algo.startswith("rccl")
+            if custom and custom_failed[0]:
+                # the hand-written kernels share one flag protocol: after one of them failed
+                # (and waited out the device timeout) the others are not tried
+                results[algo] = None
+                continue
+            ok = 1
+            try:
+                buf_out.zero_()
+                sync_barrier()
+                ar_run(buf_in, buf_out, algo)
+                torch.cuda.synchronize()
+                dev.check()
+                ok = int(bool(torch.all(buf_out == expect).item()))
+            except Exception as e:  # noqa: BLE001 - any failure disqualifies the candidate
+                log(f"candidate {algo} failed: {e}")
+                ok = 0
+            if not hc.allreduce(ok, op=MPI.MIN):
+                results[algo] = None
+                if custom:
+                    custom_failed[0] = True
+                    dev.reset()  # a timed-out kernel leaves per-CTA epochs inconsistent
+                continue
+            ar_run(buf_in, buf_out, algo)
+            results[algo] = timed(lambda: ar_run(buf_in, buf_out, algo), 3)
+            log(f"candidate {algo} ({buf_in.dtype}): {results[algo] * 1e3:.3f} ms")
+        good = {a: t for a, t in results.items() if t}
+        if not good:
+            raise SystemExit("no all-reduce algorithm produced a correct result")
+        return results, min(good, key=good.get)
+
+    x.fill_(float(rank + 1))
+    expect = float(world * (world + 1) // 2)
+    results, best = pick(x, y, expect, candidates())
     for _ in range(args.warmup):
-        run(best)
-    t_step = timed(best, args.steps)
+        ar_run(x, y, best)
+    t_step = timed(lambda: ar_run(x, y, best), args.steps)
     torch.cuda.synchronize()
-    final_ok = bool(torch.all(y == expect).item())
-    final_ok = bool(hc.allreduce(int(final_ok), op=MPI.MIN))
+    final_ok = bool(hc.allreduce(int(bool(torch.all(y == expect).item())), op=MPI.MIN))
     algbw = nbytes / t_step / 1e9
     busbw = algbw * (2 * (world - 1) / world) if world > 1 else 0.0
 
+    secondary = {}
+    if not args.no_secondary:
+        # ---- 1 GiB bf16 all-reduce (BASELINE config 2): rank-valued, exact in bf16
+        xb, yb = x.view(torch.bfloat16), y.view(torch.bfloat16)
+        xb.fill_(float(rank + 1))
+        top = sorted((a for a, t in results.items() if t), key=lambda a: results[a])[:3]
+        res16, best16 = pick(xb, yb, expect, top)
+        t16 = timed(lambda: ar_run(xb, yb, best16), max(3, args.steps // 2))
+        secondary["bf16_1GiB"] = {"algo": best16, "ms": round(t16 * 1e3, 4), "algbw_GBps": round(nbytes / t16 / 1e9, 2),
+                                  "busbw_GBps": round(nbytes / t16 / 1e9 * (2 * (world - 1) / world), 2) if world > 1 else 0.0,
+                                  "candidates_ms": {a: (round(t * 1e3, 4) if t else None) for a, t in res16.items()}}
+        # ---- all-to-all, 256 MiB per rank (BASELINE config 3)
+        an = ((args.a2a_mb << 20) // 4) // world * world
+        blk = an // world
+        xa, ya = x[:an], y[:an]
+        xa.view(world, blk).copy_((rank * world + torch.arange(world, device=dev.device, dtype=torch.float32)).view(world, 1).expand(world, blk))
+        want = (torch.arange(world, device=dev.device, dtype=torch.float32) * world + rank).view(world, 1).expand(world, blk)
+        a2a = {}
+        for algo in ["direct", "push"] + ([] if dev.shared_device or world == 1 else ["rccl", "pairwise"]):
+            try:
+                ya.zero_()
+                sync_barrier()
+                dev.alltoall(xa, ya, algo)
+                torch.cuda.synchronize()
+                dev.check()
+                ok = int(torch.equal(ya.view(world, blk), want))
+            except Exception as e:  # noqa: BLE001
+                log(f"alltoall {algo} failed: {e}")
+                ok = 0
+            if not hc.allreduce(ok, op=MPI.MIN):
+                a2a[algo] = None
+                continue
+            a2a[algo] = round(timed(lambda: dev.alltoall(xa, ya, algo), 5) * 1e3, 4)
+        good = {a: t for a, t in a2a.items() if t}
+        ba = min(good, key=good.get) if good else None
+        secondary["alltoall"] = {"bytes_per_rank": an * 4, "algo": ba, "ms": good.get(ba),
+                                 "algbw_GBps": round(an * 4 / (good[ba] / 1e3) / 1e9, 2) if ba else None,
+                                 "candidates_ms": a2a}
+        # ---- DP gradient all-reduce overlapped with the backward (BASELINE config 5).
+        # A failure here must not cost the headline: it is recorded, and the group is
+        # reset collectively before anything else runs.
+        if world > 1 and args.dp_layers > 0:
+            from collective_communication_mpi_amd.parallel.overlap import dp_grad_overlap
+
+            try:
+                secondary["dp_overlap"] = dp_grad_overlap(
+                    comm, layers=args.dp_layers, tokens=args.dp_tokens, iters=2,
+                    algo=best.split(":")[0] if not best.startswith("rccl") else "rccl")
+                ok = 1
+            except Exception as e:  # noqa: BLE001 - recorded in the JSON
+                secondary["dp_overlap"] = {"error": f"{type(e).__name__}: {e}"[:300]}
+                ok = 0
+            if not hc.allreduce(ok, op=MPI.MIN):
+                torch.cuda.synchronize()
+                dev.reset()
+    del x, y
+    torch.cuda.empty_cache()
+
     # -------------------------------------------------------- harness step
     harness = None
-    if custom_failed and results.get("rccl"):
+    if custom_failed[0] and results.get("rccl"):
         os.environ["CCMPI_ALLREDUCE_ALGO"] = "rccl"  # harness TP/DP collectives follow the valid path
     if not args.no_harness:
-        try:
-            from collective_communication_mpi_amd.models.harness import bench_forward
+        from collective_communication_mpi_amd.models.harness import bench_forward
 
-            tp = args.tp or (2 if world >= 2 and world % 2 == 0 else 1)
-            harness = bench_forward(comm, tp=tp, batch=args.batch, steps=args.steps, warmup=args.warmup)
-        except ImportError:
-            harness = None
+        tp = args.tp or (2 if world >= 2 and world % 2 == 0 else 1)
+        harness = bench_forward(comm, tp=tp, batch=args.batch, steps=args.steps, warmup=args.warmup)
+        if tp > 1 and not args.no_secondary:
+            # per-token row-parallel fc_o: the TP all-reduce carries B*S x 16 partial outputs;
+            # 4 row blocks pipeline it under the fc_o GEMM on a side stream (1 block = no overlap)
+            tok = {}
+            for chunks in (1, 4):
+                r = bench_forward(comm, tp=tp, batch=args.batch, steps=args.steps, warmup=args.warmup, train=False,
+                                  fc_o_mode="token", tp_chunks=chunks)
+                tok[f"chunks{chunks}_fwd_ms"] = round(r["fwd_ms"], 4)
+            tok["tp_allreduce_bytes"] = args.batch * 16 * 16 * 4
+            harness["token_fc_o"] = tok
+
+    dry = None
+    if world == 1 and args.shared_dry_run > 1 and not args.no_secondary and torch.cuda.device_count() >= 1:
+        dry = shared_dry_run(args.shared_dry_run, steps=5, warmup=2, verbose=args.verbose)
 
     if rank == 0:
         tp = harness["tp"] if harness else (2 if world >= 2 and world % 2 == 0 else 1)
@@ -209,12 +317,16 @@ def main() -> int:
                 "busbw_GBps": round(busbw, 3),
                 "candidates_ms": {a: (round(t * 1e3, 4) if t else None) for a, t in results.items()},
                 "result_exact": final_ok,
+                "shared_gpu": dev.shared_device,
+                **secondary,
             },
         }
         if harness:
             out["config"]["tp_fwd_step_ms"] = round(harness["fwd_ms"], 4)
             out["config"]["tp_train_step_ms"] = round(harness.get("train_ms", float("nan")), 4)
             out["config"]["harness"] = {k: v for k, v in harness.items() if k not in ("fwd_ms", "train_ms")}
+        if dry is not None:
+            out["config"]["shared_gpu_dry_run"] = dry
         print(json.dumps(out), flush=True)
     return 0
 

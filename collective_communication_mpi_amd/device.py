@@ -105,6 +105,12 @@ class DeviceGroup:
         self.shared_device = self.ranks_per_device > 1
         default_blocks = max(1, 512 // self.ranks_per_device)
         self.max_blocks = _env_int("CCMPI_MAX_BLOCKS", default_blocks)
+        # CTA budget of collectives that run NEXT TO compute (DP gradient buckets, TP
+        # pipelines on side streams): spinning collective CTAs hold CU slots the GEMMs
+        # could use, and with ranks sharing a GPU a 256-CTA bucket all-reduce beside
+        # another rank's GEMMs never became co-resident (timeouts, profiles/r2_overlap);
+        # 64 CTAs keep both the GEMMs and the collective moving
+        self.overlap_blocks = min(self.max_blocks, _env_int("CCMPI_OVERLAP_BLOCKS", 64))
         if scratch_bytes is None:
             scratch_bytes = _env_int("CCMPI_SCRATCH_MB", 64 if self.shared_device else 512) << 20
         self._keep: List = []   # registered segments (scratch, heap arenas) live as long as the group
@@ -273,6 +279,17 @@ class DeviceGroup:
             raise ValueError(f"{name} must be contiguous")
         return t
 
+    def _budget(self, max_blocks: Optional[int]) -> int:
+        """Per-rank CTA budget.  Ranks sharing a GPU spin on each other's CTAs, so
+        their grids must be co-resident.  The kernels' VGPR use allows 4 CTAs per
+        CU, but a grid that needs every slot of every CU (1024 in total) was seen
+        to leave some CTAs undispatched behind spinning ones (timeout): the total
+        is capped at 512 (2 per CU)."""
+        mb = max_blocks or self.max_blocks
+        if self.shared_device:
+            mb = min(mb, max(1, 512 // self.ranks_per_device))
+        return mb
+
     def _symm(self, *ts) -> bool:
         return all(self.is_symmetric(t) and t.data_ptr() % 16 == 0 for t in ts)
 
@@ -313,7 +330,7 @@ class DeviceGroup:
             # "symmetric" there means a registered output (and an aligned input)
             symm = (self._symm(dst) and src.data_ptr() % 16 == 0) if algo in ("ring", "rhd") else self._symm(src, dst)
             self.dc.allreduce(src.data_ptr(), dst.data_ptr(), src.numel(), dt, opc, getattr(self.D, _HAND_ALGOS[algo]),
-                              s, max_blocks or self.max_blocks, symm)
+                              s, self._budget(max_blocks), symm)
         elif algo == "rccl":
             self.ensure_rccl()
             self.dc.rccl_allreduce(src.data_ptr(), dst.data_ptr(), src.numel(), dt, opc, s)
@@ -345,7 +362,7 @@ class DeviceGroup:
             self.dc.rccl_reduce_scatter(src.data_ptr(), dst.data_ptr(), dst.numel(), dt, opc, s)
         else:
             self.dc.reduce_scatter(src.data_ptr(), dst.data_ptr(), dst.numel(), dt, opc, s,
-                                   max_blocks or self.max_blocks, self._symm(src))
+                                   self._budget(max_blocks), self._symm(src))
         return dst
 
     @trace_call("allgather")
@@ -360,7 +377,7 @@ class DeviceGroup:
             self.ensure_rccl()
             self.dc.rccl_allgather(src.data_ptr(), dst.data_ptr(), nb, 1, s)
         else:
-            self.dc.allgather(src.data_ptr(), dst.data_ptr(), nb, s, max_blocks or self.max_blocks,
+            self.dc.allgather(src.data_ptr(), dst.data_ptr(), nb, s, self._budget(max_blocks),
                               self._symm(src) and dst.data_ptr() % 16 == 0)
         return dst
 
@@ -384,10 +401,10 @@ class DeviceGroup:
             self.ensure_rccl()
             self.dc.p2p_pairwise_alltoall(src.data_ptr(), dst.data_ptr(), blk, s)
         elif algo == "push":
-            self.dc.alltoall(src.data_ptr(), dst.data_ptr(), blk, s, max_blocks or self.max_blocks,
+            self.dc.alltoall(src.data_ptr(), dst.data_ptr(), blk, s, self._budget(max_blocks),
                              self._symm(dst) and src.data_ptr() % 16 == 0, self.D.A2A_PUSH)
         elif algo in ("direct", "auto"):
-            self.dc.alltoall(src.data_ptr(), dst.data_ptr(), blk, s, max_blocks or self.max_blocks, self._symm(src),
+            self.dc.alltoall(src.data_ptr(), dst.data_ptr(), blk, s, self._budget(max_blocks), self._symm(src),
                              self.D.A2A_PULL)
         else:
             raise ValueError(f"unknown alltoall algorithm {algo!r}")
@@ -401,19 +418,19 @@ class DeviceGroup:
             self.ensure_rccl()
             self.dc.rccl_bcast(buf.data_ptr(), buf.numel() * buf.element_size(), 1, root, s)
         else:
-            self.dc.bcast(buf.data_ptr(), buf.numel() * buf.element_size(), root, s, self.max_blocks, self._symm(buf))
+            self.dc.bcast(buf.data_ptr(), buf.numel() * buf.element_size(), root, s, self._budget(None), self._symm(buf))
         return buf
 
     def allgather_lastaxis(self, src, dst, rows: int, row_bytes: int):
         """dst[m][j*k:(j+1)*k] = src_j[m]  (TP forward collect, fused layout)."""
-        self.dc.allgather_lastaxis(src.data_ptr(), dst.data_ptr(), rows, row_bytes, self._stream(), self.max_blocks,
+        self.dc.allgather_lastaxis(src.data_ptr(), dst.data_ptr(), rows, row_bytes, self._stream(), self._budget(None),
                                    self._symm(src))
         return dst
 
     def reduce_scatter_lastaxis(self, src, dst, rows: int, k: int, op="SUM"):
         """dst[m] = sum_j src_j[m][me*k:(me+1)*k]  (TP backward grad_x, fused layout)."""
         self.dc.reduce_scatter_lastaxis(src.data_ptr(), dst.data_ptr(), rows, k, dtype_code(src.dtype), op_code(op),
-                                        self._stream(), self.max_blocks, self._symm(src))
+                                        self._stream(), self._budget(None), self._symm(src))
         return dst
 
     def local_reduce(self, inputs: Sequence, out, op="SUM"):

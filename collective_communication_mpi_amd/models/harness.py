@@ -46,7 +46,7 @@ def build(comm, tp: int, batch: int, **kw):
 def train_step(layer: MnistTPLayer, cfg: LayerConfig, xb, yb):
     logits = layer.forward_images(xb, xb.shape[0])  # patchify + forward (cfg.fwd_chunks streams)
     layer.zero_grad()
-    if cfg.fc_o_mode == "row" or cfg.tp == 1:
+    if layer._fused_fc_o() or (cfg.fc_o_mode == "row" and cfg.tp > 1):
         loss = layer.loss_and_grad_fused(yb, cfg.batch * cfg.dp)  # one kernel: loss, dZ, d o_b
         layer.backward(None)
     else:
@@ -56,20 +56,28 @@ def train_step(layer: MnistTPLayer, cfg: LayerConfig, xb, yb):
     return loss
 
 
-def bench_forward(comm, tp: int = 2, batch: int = 2048, steps: int = 20, warmup: int = 5, graph: bool = True):
+def bench_forward(comm, tp: int = 2, batch: int = 2048, steps: int = 20, warmup: int = 5, graph: bool = True,
+                  train: bool = True, **layer_kw):
     from .. import mpi as MPI
 
     hc = _hc(comm)
     rank = comm.Get_rank()
-    cfg, layer, x_all, y_all = build(comm, tp, batch)
+    cfg, layer, x_all, y_all = build(comm, tp, batch, **layer_kw)
     xb, yb = local_batch(cfg, x_all, y_all, 0, rank, layer.device)
 
     def fwd():  # inference forward: no activations kept for a backward
         return layer.forward_images(xb, cfg.batch, save=False)
 
+    verbose = os.environ.get("CCMPI_HARNESS_VERBOSE") == "1"
+
+    def say(msg):
+        if verbose:
+            print(f"[harness rank {rank}] {msg}", file=sys.stderr, flush=True)
+
     for _ in range(3):
         fwd()
     torch.cuda.synchronize()
+    say("eager forward ok")
     used_graph = False
     g = None
     if graph and os.environ.get("CCMPI_NO_GRAPH") != "1":
@@ -85,6 +93,7 @@ def bench_forward(comm, tp: int = 2, batch: int = 2048, steps: int = 20, warmup:
             with torch.cuda.graph(g):
                 fwd()
             used_graph = True
+            say("graph captured")
         except Exception as e:  # noqa: BLE001 - fall back to eager, reported in the result
             if rank == 0:
                 print(f"[harness] graph capture failed, timing eager: {e}", file=sys.stderr)
@@ -99,6 +108,10 @@ def bench_forward(comm, tp: int = 2, batch: int = 2048, steps: int = 20, warmup:
     torch.cuda.synchronize()
     hc.Barrier()
     fwd_s = hc.allreduce(time.perf_counter() - t0, op=MPI.MAX) / steps
+    say(f"timed forward {fwd_s * 1e3:.3f} ms")
+    if not train:
+        return {"tp": cfg.tp, "dp": cfg.dp, "fwd_ms": fwd_s * 1e3, "hip_graph": used_graph, "fc_o_mode": cfg.fc_o_mode,
+                "tp_chunks": cfg.tp_chunks, "tokens_per_step": cfg.batch * cfg.dp * cfg.seq}
     # training step (eager)
     for _ in range(2):
         train_step(layer, cfg, xb, yb)
@@ -137,7 +150,8 @@ def main(argv=None) -> int:
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--lr", type=float, default=2e-3)
-    ap.add_argument("--fc-o-mode", default="row")
+    ap.add_argument("--fc-o-mode", default="row", choices=["row", "token", "naive"])
+    ap.add_argument("--tp-chunks", type=int, default=1)
     ap.add_argument("--log", default="")
     ap.add_argument("--ckpt", default="", help="checkpoint directory (sharded, safetensors)")
     ap.add_argument("--save-every", type=int, default=0, help="save every K steps (and at the end)")
@@ -146,7 +160,8 @@ def main(argv=None) -> int:
     comm = Communicator(MPI.COMM_WORLD)
     local = int(os.environ.get("LOCAL_RANK", os.environ.get("CCMPI_LOCAL_RANK", "0")))
     torch.cuda.set_device(local % torch.cuda.device_count())
-    cfg, layer, x_all, y_all = build(comm, args.tp, args.batch, lr=args.lr, fc_o_mode=args.fc_o_mode)
+    cfg, layer, x_all, y_all = build(comm, args.tp, args.batch, lr=args.lr, fc_o_mode=args.fc_o_mode,
+                                     tp_chunks=args.tp_chunks)
     hc = _hc(comm)
     losses = []
     start = 0

@@ -79,7 +79,17 @@ class LayerConfig:
     batch: int = 2048        # images per DP replica
     tp: int = 1
     dp: int = 1
-    fc_o_mode: str = "row"   # "row" (Megatron, 1 all-reduce) | "naive" (reference collects)
+    # "row": Megatron row-parallel, pooled first (B rows, one B x 16 all-reduce);
+    # "token": row-parallel per token, as model/func_impl.py:94-109 shapes it -- the TP
+    #   all-reduce moves B*S x 16 partial outputs, cut into tp_chunks row blocks whose
+    #   all-reduces run on a side stream under the next block's fc_o GEMM;
+    # "naive": the reference collects (all-gather in, out-sharded fc_o, all-gather out)
+    fc_o_mode: str = "row"
+    # fc_o_mode="token": row blocks of the attention -> fc_o -> TP all-reduce pipeline.  1 by
+    # default: measured with 2 ranks sharing one GPU, 2/4/8 blocks cost 0.47/0.83/1.98 ms
+    # vs 0.22 ms unpipelined (profiles/r2_overlap) -- a 2 MB all-reduce per step is
+    # latency-bound, and per-block attention is too short to hide it
+    tp_chunks: int = 1
     lr: float = 1e-3
     weight_decay: float = 0.0
     seed: int = 1234
@@ -318,11 +328,12 @@ class MnistTPLayer:
         D = _native.device()
         st = torch.cuda.current_stream(self.device).cuda_stream
         naive = cfg.fc_o_mode == "naive" and cfg.tp > 1
-        pool = None if naive else self._buf("pool", (B, self.hd), torch.bfloat16)
+        token = cfg.fc_o_mode == "token"
+        pool = None if (naive or token) else self._buf("pool", (B, self.hd), torch.bfloat16)
         # the per-token attention output is only consumed by the naive fc_o; the pooled
         # path (and the MFMA backward, which never reads O) skip materializing it
         mfma_attn = S <= 16 and cfg.head_dim in (32, 64, 128)
-        att = self._buf("att", (M, self.hd), torch.bfloat16) if (naive or not mfma_attn) else None
+        att = self._buf("att", (M, self.hd), torch.bfloat16) if (naive or token or not mfma_attn) else None
         fc_fused = self._fused_fc_o()
         zp = None
         fc = {}
@@ -338,13 +349,19 @@ class MnistTPLayer:
                 raise ValueError("forward: xp needs unit column stride")
             fc.update(xp=xp.data_ptr(), ld_xp=xp.stride(0), kp=cfg.kp, weff=weff.data_ptr(), ld_weff=weff.stride(0),
                       qkv_out=qkv.data_ptr() if save else 0)
-        D.attn_small_fwd(0 if proj else qkv.data_ptr(), 0 if att is None else att.data_ptr(), lse.data_ptr(), B, S, self.hl,
-                         cfg.head_dim, qkv.stride(0), self.hd if att is None else att.stride(0),
-                         1.0 / math.sqrt(cfg.head_dim),
-                         0 if pool is None else pool.data_ptr(), 0 if pool is None else pool.stride(0), st, **fc)
+        # token fc_o with TP: attention runs per row block inside the TP pipeline below
+        pipelined = token and self._token_chunks(B) > 1
+        if not pipelined:
+            D.attn_small_fwd(0 if proj else qkv.data_ptr(), 0 if att is None else att.data_ptr(), lse.data_ptr(), B, S,
+                             self.hl, cfg.head_dim, qkv.stride(0), self.hd if att is None else att.stride(0),
+                             1.0 / math.sqrt(cfg.head_dim),
+                             0 if pool is None else pool.data_ptr(), 0 if pool is None else pool.stride(0), st, **fc)
         if naive:
             z = self._forward_naive_fc_o(att, B)
             logits = z.view(B, S, cfg.out_pad)[:, :, : cfg.n_classes].mean(dim=1)
+        elif token:
+            z = self._forward_token_fc_o(att, B, qkv=qkv, lse=lse)
+            logits = z.view(B, S, cfg.out_pad)[:, :, : cfg.n_classes].mean(dim=1)  # o_b is in z (TP rank 0)
         else:
             # fc_o and the mean over patches are linear: pool first (fused in the
             # attention kernel), so fc_o and its TP all-reduce work on B rows, not B*S
@@ -432,9 +449,55 @@ class MnistTPLayer:
         self._hx = hx[:, : d + cfg.kp] if hx is not None else None
         return zp[:, : cfg.n_classes]
 
+    def _token_chunks(self, B: int) -> int:
+        c = max(1, int(self.cfg.tp_chunks)) if self.tp_dev is not None else 1
+        return c if (B % c == 0 and (B // c) * self.cfg.seq >= 256) else 1
+
+    def _forward_token_fc_o(self, att, B, qkv=None, lse=None):
+        """Row-parallel fc_o per token: z = att . W_o[:, shard]^T (+ o_b on TP rank 0),
+        summed over the TP group (B*S x 16 fp32 partial outputs).
+
+        With ``tp_chunks = c > 1`` the batch is cut into c row blocks and each
+        block runs attention -> fc_o GEMM on the main stream, then hands its
+        partial z to the TP all-reduce (hand-written kernel, symmetric buffer,
+        ``overlap_blocks`` CTAs) on a high-priority side stream: block i's
+        all-reduce runs under block i+1's attention.  Fork/join by events, so
+        the whole pipeline is captured into the step's HIP graph."""
+        cfg = self.cfg
+        S = cfg.seq
+        M = B * S
+        z = self._buf("ztok", (M, cfg.out_pad), torch.float32, self.tp_dev)
+        wo = self.flat.param16("o_w")
+        bias = self.flat.param("o_b") if self.tp_idx == 0 else None
+        c = self._token_chunks(B)
+        if c == 1:
+            gemm_nt(att, wo, out=z, out_dtype=torch.float32, splitk=1, bias=bias)
+            if self.tp_dev is not None:
+                self.tp_dev.allreduce(z, z, "SUM")
+            return z
+        main = torch.cuda.current_stream(self.device)
+        if "tp_side" not in self._bufs:
+            self._bufs["tp_side"] = torch.cuda.Stream(self.device, priority=-1)
+        side = self._bufs["tp_side"]
+        D = _native.device()
+        hl, Bc = self.hl, B // c
+        for i in range(c):
+            b0, b1 = i * Bc, (i + 1) * Bc
+            r0, r1 = b0 * S, b1 * S
+            D.attn_small_fwd(qkv[r0:r1].data_ptr(), att[r0:r1].data_ptr(), lse[b0 * hl:b1 * hl].data_ptr(), Bc, S, hl,
+                             cfg.head_dim, qkv.stride(0), att.stride(0), 1.0 / math.sqrt(cfg.head_dim), 0, 0,
+                             main.cuda_stream)
+            gemm_nt(att[r0:r1], wo, out=z[r0:r1], out_dtype=torch.float32, splitk=1, bias=bias)
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                self.tp_dev.allreduce(z[r0:r1], z[r0:r1], "SUM", max_blocks=self.tp_dev.overlap_blocks)
+        main.wait_stream(side)
+        return z
+
     def _fused_fc_o(self) -> bool:
         cfg = self.cfg
-        return (cfg.fuse_fc_o and not (cfg.fc_o_mode == "naive" and cfg.tp > 1) and cfg.seq <= 16
+        return (cfg.fuse_fc_o and not (cfg.fc_o_mode == "naive" and cfg.tp > 1) and cfg.fc_o_mode != "token"
+                and cfg.seq <= 16
                 and cfg.head_dim in (32, 64, 128) and 4 % self.hl == 0 and cfg.out_pad <= 16)
 
     def _forward_naive_fc_o(self, att, B):
@@ -510,12 +573,18 @@ class MnistTPLayer:
         fused = dlogits is None
         if not fused:
             G("o_b")[: cfg.n_classes].add_(dlogits.sum(0))
-        if cfg.fc_o_mode == "naive" and cfg.tp > 1:
+        if (cfg.fc_o_mode == "naive" and cfg.tp > 1) or cfg.fc_o_mode == "token":
             dz = self._buf("dz", (M, cfg.out_pad), torch.bfloat16)
             dz.zero_()
             dz.view(B, S, cfg.out_pad)[:, :, : cfg.n_classes] = (dlogits / S).unsqueeze(1).to(torch.bfloat16)
             datt = self._buf("datt", (M, self.hd), torch.bfloat16)
-            self._backward_naive_fc_o(dz, datt, B)
+            if cfg.fc_o_mode == "token":
+                # row-parallel: dZ is replicated (identity backward of the all-reduce), the
+                # input gradient is local to this rank's heads -- no TP communication
+                gemm_tn(dz, att, out=G("o_w"), accumulate=True)          # dW_o[:, shard] = dZ^T att
+                gemm_nt(dz, self.flat.param16_t("o_w"), out=datt)         # dAtt = dZ . W_o[:, shard]
+            else:
+                self._backward_naive_fc_o(dz, datt, B)
             dout, dout_b, dout_r = datt, S * datt.stride(0), datt.stride(0)
         else:
             # pooled row-parallel fc_o: dZ is replicated on every TP rank (identity backward

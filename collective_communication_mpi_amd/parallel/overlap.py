@@ -8,8 +8,10 @@ kv 1024, MLP 14336; 218 M weights per layer, 32 layers = 7.0 B weights =
 dW = dY^T X are produced by the MFMA GEMM (``gemm_nt`` over the token axis,
 fp32 accumulate, bf16 out) straight into a flat bf16 gradient buffer on the
 symmetric heap.  As soon as a layer's GEMMs are queued, an event hands that
-layer's slice (one bucket) to a high-priority side stream, which all-reduces
-it with the framework's device all-reduce while the next layer's GEMMs run.
+layer's slice (one bucket) to a side stream (normal priority: measured better
+than high priority, profiles/r2_overlap), which all-reduces it with the
+framework's device all-reduce (``overlap_blocks`` CTAs) while the next
+layer's GEMMs run.
 Activations are kept feature-major ([features, tokens]) so every wgrad GEMM
 reads K-contiguous operands, as the real backward's saved activations are.
 
@@ -34,7 +36,10 @@ def layer_weight_shapes(d: int, kv: int, ff: int) -> List[Tuple[int, int]]:
 
 
 def dp_grad_overlap(comm, layers: int = 32, tokens: int = 4096, iters: int = 3, algo: str = "auto",
-                    priority: int = -1, dims: Dict[str, int] = LLAMA3_8B, seed: int = 0) -> Dict:
+                    priority: int = 0, dims: Dict[str, int] = LLAMA3_8B, seed: int = 0, verbose: bool = False,
+                    max_blocks: int = 0) -> Dict:
+    """``max_blocks``: CTA budget of the bucket all-reduces (0 = the group's
+    ``overlap_blocks``, the budget for collectives that run beside compute)."""
     from .. import mpi as MPI
 
     dev = comm.dev
@@ -48,6 +53,7 @@ def dp_grad_overlap(comm, layers: int = 32, tokens: int = 4096, iters: int = 3, 
     x_t = {k: (torch.randn(k, T, generator=g, device=dev.device) * 0.05).bfloat16() for k in {d, ff}}
     dy_t = {k: (torch.randn(k, T, generator=g, device=dev.device) * 0.05).bfloat16() for k in {d, kv, ff}}
     side = torch.cuda.Stream(device=dev.device, priority=priority)
+    mb = max_blocks or dev.overlap_blocks
     events = [torch.cuda.Event() for _ in range(layers)]
 
     def backward(comm_on: bool, compute_on: bool = True) -> None:
@@ -63,18 +69,24 @@ def dp_grad_overlap(comm, layers: int = 32, tokens: int = 4096, iters: int = 3, 
                 side.wait_event(events[layer])
                 with torch.cuda.stream(side):
                     seg = grads[base:base + per_layer]
-                    dev.allreduce(seg, seg, "SUM", algo)
+                    dev.allreduce(seg, seg, "SUM", algo, max_blocks=mb)
         torch.cuda.current_stream().wait_stream(side)
 
     def timed(**kw) -> float:
         backward(**kw)
         torch.cuda.synchronize()
+        dev.check()
         hc.Barrier()
         t0 = time.perf_counter()
         for _ in range(iters):
             backward(**kw)
         torch.cuda.synchronize()
-        return hc.allreduce((time.perf_counter() - t0) / iters, op=MPI.MAX)
+        t = hc.allreduce((time.perf_counter() - t0) / iters, op=MPI.MAX)
+        if verbose and comm.Get_rank() == 0:
+            import sys
+
+            print(f"[dp_overlap] {kw}: {t * 1e3:.3f} ms", file=sys.stderr, flush=True)
+        return t
 
     t_compute = timed(comm_on=False)
     t_comm = timed(comm_on=True, compute_on=False) if p > 1 else 0.0
@@ -87,6 +99,7 @@ def dp_grad_overlap(comm, layers: int = 32, tokens: int = 4096, iters: int = 3, 
            "compute_ms": round(t_compute * 1e3, 3), "comm_ms": round(t_comm * 1e3, 3),
            "overlapped_ms": round(t_both * 1e3, 3), "comm_hidden_fraction": None if hidden is None else round(hidden, 3),
            "wgrad_TFLOPs": round(flops / t_compute / 1e12, 1), "shared_gpu": dev.shared_device,
-           "comm_algbw_GBps": round(gbytes / t_comm / 1e9, 2) if t_comm else None, "algo": algo}
+           "comm_algbw_GBps": round(gbytes / t_comm / 1e9, 2) if t_comm else None, "algo": algo,
+           "bucket_ctas": mb, "buckets": layers}
     del grads, x_t, dy_t
     return out

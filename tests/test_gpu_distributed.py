@@ -74,8 +74,8 @@ def reference_run(tmp_path_factory):
     return np.load(out)
 
 
-@pytest.mark.parametrize("n,tp,mode", [(2, 2, "row"), (2, 2, "naive"), (2, 1, "row"), (4, 2, "row"),
-                                       (8, 2, "row"), (8, 1, "row")])  # 8 ranks sharing one GPU: the DP4 x TP2 grid
+@pytest.mark.parametrize("n,tp,mode", [(2, 2, "row"), (2, 2, "naive"), (2, 2, "token"), (2, 1, "row"), (4, 2, "row"),
+                                       (4, 2, "token"), (8, 2, "row"), (8, 1, "row")])  # 8 ranks on one GPU: DP4 x TP2
 def test_harness_matches_single_rank(reference_run, tmp_path, n, tp, mode):
     out = tmp_path / "run.npz"
     run_ranks(n, py("tests/workers/harness_worker.py", "--tp", str(tp), "--mode", mode, "--out", str(out)),
@@ -108,3 +108,27 @@ def test_tensor_parallel_layers_and_ddp_gpu(n):
     on the device plane vs a single-process fp32 reference (tests/workers/tp_ddp_worker.py)."""
     r = run_ranks(n, py("tests/workers/tp_ddp_worker.py", "--device", "cuda"), timeout=300, env=ENV)
     assert "tp/ddp OK" in r.stdout
+
+
+def test_bench_multi_rank_path_shared_gpu():
+    """bench.py's N >= 2 path (candidate loop, bf16, all-to-all, DP overlap, TP harness)
+    with 4 ranks on this GPU, so an 8-GPU run is never the first execution of it."""
+    import json
+    import subprocess
+    import sys
+
+    from _launch import REPO
+
+    e = dict(os.environ, **ENV)
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "4", "--steps", "3", "--warmup", "1", "--size-mb", "64",
+                        "--a2a-mb", "16", "--dp-layers", "1", "--dp-tokens", "1024", "--batch", "256"],
+                       cwd=REPO, env=e, capture_output=True, text=True, timeout=400)
+    assert r.returncode == 0, r.stderr[-4000:]
+    out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    c = out["config"]
+    assert out["n_gpus"] == 4 and c["result_exact"] and c["shared_gpu"]
+    assert set(c["candidates_ms"]) >= {"twoshot:256", "push:512", "ring", "rhd"}
+    assert all(v for v in c["candidates_ms"].values()), c["candidates_ms"]
+    assert c["bf16_1GiB"]["algbw_GBps"] > 0 and c["alltoall"]["ms"] > 0
+    assert 0.0 <= c["dp_overlap"]["comm_hidden_fraction"] <= 1.0
+    assert c["parallelism"] == "dp2xtp2" and c["tp_fwd_step_ms"] > 0
