@@ -11,7 +11,6 @@ from collective_communication_mpi_amd.ops import gemm_nt  # noqa: E402
 
 D = _native.device()
 D.gemm_set_kernel(1)
-D.gemm_set_bk32(False)
 
 
 def t(fn, iters=20):

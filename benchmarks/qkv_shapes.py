@@ -29,20 +29,11 @@ def t(fn, iters=30):
 
 def reset():
     D.gemm_set_kernel(0)
-    D.gemm_set_bk32(False)
-    D.gemm_set_persistent(False, 0)
-    D.gemm_set_stages(0)
-
+    
 
 VARIANTS = {
     "auto": lambda: None,
     "k128": lambda: D.gemm_set_kernel(1),
-    "k128_bk32": lambda: (D.gemm_set_kernel(1), D.gemm_set_bk32(True)),
-    "k128_persist256": lambda: (D.gemm_set_kernel(1), D.gemm_set_persistent(True, 256)),
-    "k128_persist512": lambda: (D.gemm_set_kernel(1), D.gemm_set_persistent(True, 512)),
-    "k128_ms3": lambda: (D.gemm_set_kernel(1), D.gemm_set_stages(3)),
-    "k128_ms4": lambda: (D.gemm_set_kernel(1), D.gemm_set_stages(4)),
-    "k128_ms5": lambda: (D.gemm_set_kernel(1), D.gemm_set_stages(5)),
     "k256x256": lambda: D.gemm_set_kernel(2),
     "k256x128": lambda: D.gemm_set_kernel(3),
     "k256x192": lambda: D.gemm_set_kernel(4),

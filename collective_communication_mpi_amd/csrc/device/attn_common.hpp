@@ -33,24 +33,12 @@ struct AttnArgs {
   const uint16_t* dz;   // bwd: dO rows of sequence b = dz_scale * (dz[b] . W_o), broadcast over the S
   int ld_dz;            //      rows (replaces dout; dz is [B][ld_dz] bf16)
   float dz_scale;
-  // fwd, optional QKV projection fused in (MFMA kernel, D <= 64, fused fc_o): the q/k/v
-  // rows of sequence b are computed in-kernel as Xp_b . Weff^T, where Xp is [B*S][ld_xp]
-  // bf16 token rows with kp <= 96 columns and Weff is [3*Hl*D][ld_weff] bf16 (any bias
-  // folded into the column Xp holds constant 1).  qkv is then not read; qkv_out
-  // (optional, [B*S][ld_qkv]) receives the projected rows for the backward.
-  const uint16_t* xp;
-  int ld_xp, kp;
-  const uint16_t* weff;
-  int ld_weff;
-  uint16_t* qkv_out;
 };
 
 // MFMA path (attn_mfma.hip): S <= 16, D in {32, 64, 128}, 16-B aligned rows.
 bool mfma_supported(const AttnArgs& a, bool bwd);
-bool proj_supported(const AttnArgs& a);
 void launch_fwd_mfma(const AttnArgs& a, hipStream_t stream);
 void launch_bwd_mfma(const AttnArgs& a, hipStream_t stream);
-extern int g_fwd_proj_grid;  // workgroups of the fused-projection forward (0 = default)
 extern int g_bwd_grid_cap;  // workgroups of the backward kernel when it also reduces the bias gradient
 
 }  // namespace attn

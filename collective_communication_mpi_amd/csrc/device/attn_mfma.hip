@@ -96,20 +96,9 @@ __device__ __forceinline__ void put_rows(uint16_t* T, const bf16x8 (&x)[D / 32],
   for (int kk = 0; kk < D / 32; ++kk) *reinterpret_cast<bf16x8*>(T + c * LD + 32 * kk + 8 * g) = x[kk];
 }
 
-// PROJ: the QKV projection runs in the kernel (AttnArgs::xp).  Wave w always serves
-// head h = w % Hl, so its 3 x D rows of Weff stay in registers for the whole grid-stride
-// loop (144 VGPRs at D = 64, read once per wave); per sequence the wave reads its 16
-// token rows of Xp (2.3 KB, prefetched one iteration ahead) and forms
-//   C[feature 16nt + 4g + r][token c] = sum_k Weff[feature][k] Xp[c][k]
-// with 3 MFMAs per 16-feature tile (kp <= 96).  Q and K fragments are built straight
-// from these accumulators: element e of a lane's k-step-kk operand holds feature
-// 32kk + 16(e >> 2) + 4g + (e & 3) instead of 32kk + 8g + e -- the SAME permutation
-// for Q and K, so S = Q K^T is unchanged.  V goes to its LDS tile at the true
-// feature positions (it is indexed by feature in O = P V).  With qkv_out the rows
-// are also written out (16-B row stores via the per-wave LDS tiles) for the backward.
-template <int D, bool PROJ = false>
+template <int D>
 __global__ void __launch_bounds__(256) k_attn16_fwd(AttnArgs a) {
-  constexpr int LD = D + 8, NK = D / 32, NT = D / 16, KS = 3;
+  constexpr int LD = D + 8, NK = D / 32, NT = D / 16;
   __shared__ __attribute__((aligned(16))) uint16_t vt[WPB][16 * LD];
   __shared__ __attribute__((aligned(16))) uint16_t ot[WPB][16 * LD];
   __shared__ float zpart[2][WPB][16];  // fused fc_o: per-wave (= per-head) partial logits, double-buffered
@@ -135,80 +124,14 @@ __global__ void __launch_bounds__(256) k_attn16_fwd(AttnArgs a) {
         wpk[nt][q] = lo | (hi << 16);
       }
   }
-  [[maybe_unused]] bf16x8 wr[PROJ ? 3 : 1][PROJ ? NT : 1][PROJ ? KS : 1];
-  [[maybe_unused]] bf16x8 xr[PROJ ? KS : 1];
   const int stride = gridDim.x * WPB;
-  auto load_xp = [&](int prx) {
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks)
-      xr[ks] = ld_row16(a.xp + ((size_t)(prx / a.Hl) * S + c) * a.ld_xp + 32 * ks + 8 * g,
-                        prx < npairs && c < S && 32 * ks + 8 * g < a.kp);
-  };
-  if constexpr (PROJ) {
-    const int hw = wave % a.Hl;
-#pragma unroll
-    for (int sec = 0; sec < 3; ++sec)
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt)
-#pragma unroll
-        for (int ks = 0; ks < KS; ++ks)
-          wr[sec][nt][ks] = ld_row16(a.weff + (size_t)(sec * HD + hw * D + 16 * nt + c) * a.ld_weff + 32 * ks + 8 * g,
-                                     32 * ks + 8 * g < a.kp);
-    load_xp(blockIdx.x * WPB + wave);
-  }
   int it = 0;
   for (int base = blockIdx.x * WPB; base < npairs; base += stride, it ^= 1) {
    const int pr = base + wave;
-   [[maybe_unused]] bf16x8 xcur[PROJ ? KS : 1];
-   if constexpr (PROJ) {
-#pragma unroll
-     for (int ks = 0; ks < KS; ++ks) xcur[ks] = xr[ks];
-     load_xp(pr + stride);  // next sequence's rows in flight during this one
-   }
    if (pr < npairs) {
     const int b = pr / a.Hl, h = pr % a.Hl;
     bf16x8 qr[NK], kr[NK];
-    if constexpr (PROJ) {
-      uint16_t* ob = a.qkv_out ? a.qkv_out + (size_t)b * S * a.ld_qkv + h * D : nullptr;
-#pragma unroll
-      for (int sec = 0; sec < 3; ++sec) {
-        f4 pj[NT];
-#pragma unroll
-        for (int nt = 0; nt < NT; ++nt) {
-          pj[nt] = f4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-          for (int ks = 0; ks < KS; ++ks) pj[nt] = mma32(wr[sec][nt][ks], xcur[ks], pj[nt]);
-        }
-        // [token c][feature 16nt + 4g + r] into an LDS tile (V's own tile for v; the O
-        // tile stages q and k when they are written out)
-        uint16_t* T = sec == 2 ? V : O;
-        if (sec == 2 || ob) {
-#pragma unroll
-          for (int nt = 0; nt < NT; ++nt)
-            *reinterpret_cast<s4*>(T + c * LD + 16 * nt + 4 * g) = pack4(pj[nt][0], pj[nt][1], pj[nt][2], pj[nt][3]);
-          __builtin_amdgcn_wave_barrier();
-          if (ob) {
-#pragma unroll
-            for (int t = 0; t < (16 * D / 8) / 64; ++t) {
-              const int p = lane + 64 * t, row = p / (D / 8), col = (p % (D / 8)) * 8;
-              if (row < S)
-                *reinterpret_cast<uint4*>(ob + (size_t)row * a.ld_qkv + sec * HD + col) =
-                    *reinterpret_cast<const uint4*>(T + row * LD + col);
-            }
-            __builtin_amdgcn_wave_barrier();
-          }
-        }
-        if (sec < 2) {
-#pragma unroll
-          for (int kk = 0; kk < NK; ++kk) {
-            const s4 lo = pack4(pj[2 * kk][0], pj[2 * kk][1], pj[2 * kk][2], pj[2 * kk][3]);
-            const s4 hi = pack4(pj[2 * kk + 1][0], pj[2 * kk + 1][1], pj[2 * kk + 1][2], pj[2 * kk + 1][3]);
-            const bf16x8 f = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
-            if (sec == 0) qr[kk] = f; else kr[kk] = f;
-          }
-        }
-      }
-    } else {
+    {
       const uint16_t* qb = a.qkv + (size_t)b * S * a.ld_qkv + h * D;
       bf16x8 vr[NK];
 #pragma unroll
@@ -466,23 +389,7 @@ bool mfma_supported(const AttnArgs& a, bool bwd) {
   return true;
 }
 
-bool proj_supported(const AttnArgs& a) {
-  return a.S >= 1 && a.S <= 16 && (a.D == 32 || a.D == 64) && a.zp && a.Hl >= 1 && WPB % a.Hl == 0 && a.kp > 0 &&
-         a.kp <= 96 && a.kp % 8 == 0 && a.ld_xp % 8 == 0 && a.ld_weff % 8 == 0 && a.ld_qkv % 8 == 0 && a.weff &&
-         ((uint64_t)a.xp % 16) == 0 && ((uint64_t)a.weff % 16) == 0 && ((uint64_t)a.qkv_out % 16) == 0 &&
-         ((uint64_t)a.o % 16) == 0 && a.ld_o % 8 == 0;
-}
-
-int g_fwd_proj_grid = 0;  // tuning knob: workgroups of the fused-projection forward (0 = default)
-
 void launch_fwd_mfma(const AttnArgs& a, hipStream_t stream) {
-  if (a.xp) {
-    // persistent: each wave reads its Weff rows once, so fewer, longer-lived waves
-    const int grid = grid_for(a.B * a.Hl, g_fwd_proj_grid > 0 ? g_fwd_proj_grid : 256);
-    if (a.D == 32) hipLaunchKernelGGL((k_attn16_fwd<32, true>), dim3(grid), dim3(256), 0, stream, a);
-    else hipLaunchKernelGGL((k_attn16_fwd<64, true>), dim3(grid), dim3(256), 0, stream, a);
-    return;
-  }
   const int grid = grid_for(a.B * a.Hl, 4096);
   if (a.D == 32) hipLaunchKernelGGL(k_attn16_fwd<32>, dim3(grid), dim3(256), 0, stream, a);
   else if (a.D == 64) hipLaunchKernelGGL(k_attn16_fwd<64>, dim3(grid), dim3(256), 0, stream, a);

@@ -241,20 +241,12 @@ static void check_fused_fc(const AttnArgs& a, bool bwd) {
 
 void attn_fwd(uint64_t qkv, uint64_t o, uint64_t lse, int B, int S, int Hl, int D, int ld_qkv, int ld_o, float scale,
               uint64_t pool, int ld_pool, uint64_t stream, uint64_t wo, int ld_wo, int n_out, uint64_t zp, int ld_zp,
-              uint64_t bo, uint64_t xp, int ld_xp, int kp, uint64_t weff, int ld_weff, uint64_t qkv_out) {
+              uint64_t bo) {
   check_dims(S, D, false);
   AttnArgs a{(const uint16_t*)qkv, (uint16_t*)o, (float*)lse, nullptr, nullptr, nullptr, B, S, Hl, D, ld_qkv, ld_o, scale,
              (uint16_t*)pool, ld_pool, 0, 0, (const uint16_t*)wo, ld_wo, n_out, (float*)zp, ld_zp, (const float*)bo,
-             nullptr, 0, 1.0f, (const uint16_t*)xp, ld_xp, kp, (const uint16_t*)weff, ld_weff, (uint16_t*)qkv_out};
+             nullptr, 0, 1.0f};
   if (zp) check_fused_fc(a, false);
-  if (xp) {  // fused QKV projection: MFMA kernel only, no fallback
-    if (!attn::proj_supported(a))
-      throw std::invalid_argument("attn_small_fwd: fused projection needs S <= 16, D in {32, 64}, the fused fc_o (zp) "
-                                  "with Hl | 4, kp <= 96 and kp / ld_xp / ld_weff / ld_qkv % 8 == 0, 16-B aligned rows");
-    attn::launch_fwd_mfma(a, (hipStream_t)stream);
-    CCMPI_HIP_CHECK(hipGetLastError());
-    return;
-  }
   if (attn::mfma_supported(a, false)) {
     attn::launch_fwd_mfma(a, (hipStream_t)stream);
     CCMPI_HIP_CHECK(hipGetLastError());
@@ -499,17 +491,13 @@ void cast_bf16(uint64_t x, uint64_t y, uint64_t n, uint64_t stream,
 }  // namespace
 
 void register_attn_ops(pybind11::module_& m) {
-  m.def("attn_set_fwd_proj_grid", [](int g) { attn::g_fwd_proj_grid = g > 0 ? g : 0; },
-        "workgroups of the fused-projection attention forward (0 = default)", pybind11::arg("grid"));
   m.def("attn_set_bwd_grid", [](int cap) { attn::g_bwd_grid_cap = cap > 0 ? cap : 0; },
         "backward kernel grid cap (tuning)");
   namespace py = pybind11;
   m.def("attn_small_fwd", &attn_fwd, py::arg("qkv"), py::arg("o"), py::arg("lse"), py::arg("B"), py::arg("S"),
         py::arg("Hl"), py::arg("D"), py::arg("ld_qkv"), py::arg("ld_o"), py::arg("scale"), py::arg("pool"),
         py::arg("ld_pool"), py::arg("stream"), py::arg("wo") = 0, py::arg("ld_wo") = 0, py::arg("n_out") = 0,
-        py::arg("zp") = 0, py::arg("ld_zp") = 0, py::arg("bo") = 0, py::arg("xp") = 0, py::arg("ld_xp") = 0,
-        py::arg("kp") = 0, py::arg("weff") = 0, py::arg("ld_weff") = 0, py::arg("qkv_out") = 0,
-        py::call_guard<py::gil_scoped_release>());
+        py::arg("zp") = 0, py::arg("ld_zp") = 0, py::arg("bo") = 0, py::call_guard<py::gil_scoped_release>());
   m.def("attn_small_bwd", &attn_bwd, py::arg("qkv"), py::arg("o"), py::arg("lse"), py::arg("dout"), py::arg("dqkv"),
         py::arg("dbias"), py::arg("B"), py::arg("S"), py::arg("Hl"), py::arg("D"), py::arg("ld_qkv"), py::arg("ld_o"),
         py::arg("scale"), py::arg("dout_bstride"), py::arg("dout_rstride"), py::arg("stream"), py::arg("dz") = 0,

@@ -78,13 +78,6 @@ PYBIND11_MODULE(_device, m) {
   m.attr("MAX_RANKS") = kMaxRanks;
   m.attr("MAX_BLOCKS") = kMaxBlocks;
   m.def("reduce_supported", &device_reduce_supported);
-  m.def(
-      "copy_variant",
-      [](uint64_t src, uint64_t dst, uint64_t nbytes, int variant, int grid, uint64_t stream) {
-        launch_copy_variant((const void*)src, (void*)dst, nbytes, variant, grid, (hipStream_t)stream);
-      },
-      py::arg("src"), py::arg("dst"), py::arg("nbytes"), py::arg("variant"), py::arg("grid") = 0,
-      py::arg("stream") = 0, py::call_guard<py::gil_scoped_release>());
   m.def("rccl_unique_id", []() { return py::bytes(DeviceComm::rccl_unique_id()); });
 
   py::class_<SymHeap, std::shared_ptr<SymHeap>>(m, "SymHeap")

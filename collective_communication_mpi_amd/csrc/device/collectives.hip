@@ -828,10 +828,10 @@ __global__ void __launch_bounds__(kThreads) k_local_reduce(LocalReduceArgs a) {
 }
 
 // Streaming device copy (single-rank "all-reduce" and staging): 16-B
-// non-temporal loads/stores, 4 vectors in flight per lane, grid-stride.
-// Copy-kernel variants for the bandwidth sweep (benchmarks/copy_sweep.py):
-// U 16-B vectors in flight per lane, non-temporal loads (LNT) / stores (SNT),
-// CONTIG = each workgroup streams one contiguous slice instead of grid-striding.
+// non-temporal loads/stores; one contiguous 4 KiB slice per workgroup
+// (CONTIG) or a grid-stride loop with U vectors in flight per lane.  The
+// round-1 sweep of 13 (U, LNT, SNT, CONTIG) variants is in profiles/r1_copy;
+// only the measured winner is instantiated (launch_copy).
 template <int U, bool LNT, bool SNT, bool CONTIG>
 __global__ void __launch_bounds__(kThreads) k_copy_v(const u32x4* __restrict__ src, u32x4* __restrict__ dst, uint64_t nv) {
   uint64_t v, stride, end;
@@ -861,31 +861,6 @@ __global__ void __launch_bounds__(kThreads) k_copy_v(const u32x4* __restrict__ s
 // ---------------------------------------------------------------------------
 // host-side launchers
 // ---------------------------------------------------------------------------
-void launch_copy_variant(const void* src, void* dst, uint64_t nbytes, int variant, int grid, hipStream_t s) {
-  if (((uint64_t)src | (uint64_t)dst | nbytes) % 16) throw std::invalid_argument("copy_variant: 16-B aligned only");
-  const uint64_t nv = nbytes / 16;
-  if (grid <= 0) grid = (int)std::min<uint64_t>((nv + kThreads - 1) / kThreads, 4096);
-  auto* a = (const u32x4*)src;
-  auto* b = (u32x4*)dst;
-  switch (variant) {
-    case 0: hipLaunchKernelGGL((k_copy_v<4, true, true, false>), dim3(grid), dim3(kThreads), 0, s, a, b, nv); break;
-    case 1: hipLaunchKernelGGL((k_copy_v<8, true, true, false>), dim3(grid), dim3(kThreads), 0, s, a, b, nv); break;
-    case 2: hipLaunchKernelGGL((k_copy_v<4, false, false, false>), dim3(grid), dim3(kThreads), 0, s, a, b, nv); break;
-    case 3: hipLaunchKernelGGL((k_copy_v<4, true, false, false>), dim3(grid), dim3(kThreads), 0, s, a, b, nv); break;
-    case 4: hipLaunchKernelGGL((k_copy_v<4, false, true, false>), dim3(grid), dim3(kThreads), 0, s, a, b, nv); break;
-    case 5: hipLaunchKernelGGL((k_copy_v<4, true, true, true>), dim3(grid), dim3(kThreads), 0, s, a, b, nv); break;
-    case 6: hipLaunchKernelGGL((k_copy_v<8, true, true, true>), dim3(grid), dim3(kThreads), 0, s, a, b, nv); break;
-    case 7: hipLaunchKernelGGL((k_copy_v<2, true, true, false>), dim3(grid), dim3(kThreads), 0, s, a, b, nv); break;
-    case 8: hipLaunchKernelGGL((k_copy_v<16, true, true, false>), dim3(grid), dim3(kThreads), 0, s, a, b, nv); break;
-    case 9: hipLaunchKernelGGL((k_copy_v<2, true, true, true>), dim3(grid), dim3(kThreads), 0, s, a, b, nv); break;
-    case 10: hipLaunchKernelGGL((k_copy_v<4, false, true, true>), dim3(grid), dim3(kThreads), 0, s, a, b, nv); break;
-    case 11: hipLaunchKernelGGL((k_copy_v<4, false, false, true>), dim3(grid), dim3(kThreads), 0, s, a, b, nv); break;
-    case 12: hipLaunchKernelGGL((k_copy_v<1, true, true, true>), dim3(grid), dim3(kThreads), 0, s, a, b, nv); break;
-    default: throw std::invalid_argument("copy_variant: variant 0..12");
-  }
-  CCMPI_HIP_CHECK(hipGetLastError());
-}
-
 void launch_copy(const void* src, void* dst, uint64_t nbytes, hipStream_t s) {
   if (nbytes == 0 || src == dst) return;
   const uint64_t a = (uint64_t)src | (uint64_t)dst;

@@ -58,7 +58,6 @@ struct LocalReduceArgs {
 
 int grid_for(uint64_t bytes_per_cta_work, int max_blocks);
 void launch_copy(const void* src, void* dst, uint64_t nbytes, hipStream_t s);
-void launch_copy_variant(const void* src, void* dst, uint64_t nbytes, int variant, int grid, hipStream_t s);
 void launch_allreduce(int algo, const CollArgs& a, int nranks, int dtype, int op, int grid, hipStream_t s);
 void launch_reduce_scatter(const CollArgs& a, int nranks, int dtype, int op, int grid, hipStream_t s);
 void launch_move(int mode, const CollArgs& a, int nranks, int grid, hipStream_t s);

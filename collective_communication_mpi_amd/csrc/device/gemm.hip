@@ -35,11 +35,9 @@ using namespace gemm;
 constexpr int BM = 128, BN = 128, BK = 64, NT = 256;
 bool g_use_glds = std::getenv("CCMPI_GEMM_NO_GLDS") == nullptr;  // A/B switch (benchmarks)
 bool g_direct_epi = std::getenv("CCMPI_GEMM_STAGED_EPI") == nullptr;  // LDS-free epilogue (A/B switch)
-bool g_persist = std::getenv("CCMPI_GEMM_PERSIST") != nullptr;       // persistent 128x128 kernel (A/B switch; measured no gain)
-int g_persist_grid = 512;                                            // 2 workgroups per CU
-bool g_bk32 = std::getenv("CCMPI_GEMM_BK32") != nullptr;             // BK = 32 / 32 KiB LDS variant (A/B switch; measured slower)
-// multi-stage BK = 32 pipeline depth for the 128x128 kernel (0 = off; 3..5)
-int g_stages = std::getenv("CCMPI_GEMM_STAGES") ? std::atoi(std::getenv("CCMPI_GEMM_STAGES")) : 0;
+// (round 1 also carried a BK = 32, a multi-stage (3-5 x 16 KiB) and a persistent
+// form of the 128x128 kernel; all measured slower or no faster
+// (profiles/r1_qkv_reassoc/qkv_shapes2.txt, profiles/r1_gemm_fastepi) and were removed)
 // kernel choice for gemm_nt: 0 auto, 1 = 128x128 only, 2 = 256x256 / 3 = 256x128 / 4 = 256x192 whenever legal
 int g_kernel = std::getenv("CCMPI_GEMM_KERNEL") ? std::atoi(std::getenv("CCMPI_GEMM_KERNEL")) : 0;
 constexpr int kRowBytes = BK * 2;  // 128 B per LDS row
@@ -406,326 +404,6 @@ __global__ void __launch_bounds__(NT) k_gemm_nt_glds(GemmArgs g) {
 }
 
 
-
-// BK = 32 variant of k_gemm_nt_glds<DIRECT = true>: a 32 KiB double buffer
-// instead of 64 KiB, so 4-5 workgroups share a CU and their epilogue store
-// phases de-synchronize from the MFMA phases of the others (with 2 per CU they
-// run in lockstep and the stores serialize with the compute).  LDS rows are
-// 64 B; the 16-B chunk index is XOR-swizzled with (row >> 2) & 3 so the 16 rows
-// of a fragment read land on 16 distinct bank slots.
-constexpr int BK32 = 32, kRow32 = BK32 * 2;
-
-__global__ void __launch_bounds__(NT) k_gemm_nt_glds32(GemmArgs g) {
-  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * (BM + BN) * kRow32];
-  const int tiles_n = (g.N + BN - 1) / BN, tiles_m = (g.M + BM - 1) / BM;
-  const int nwg = tiles_n * tiles_m * g.splitk;
-  int wg = xcd_remap(blockIdx.x, nwg);
-  const int split = wg % g.splitk;
-  wg /= g.splitk;
-  const int bm = (wg / tiles_n) * BM, bn = (wg % tiles_n) * BN;
-  const int t = threadIdx.x, lane = t & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
-  const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
-  auto As = [&](int buf) { return smem + buf * ((BM + BN) * kRow32); };
-  auto Bs = [&](int buf) { return smem + buf * ((BM + BN) * kRow32) + BM * kRow32; };
-  floatx4 acc[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-  // a 1 KiB DMA piece = 16 rows x 64 B; 8 pieces per operand, 2 + 2 per wave
-  const int lrow = lane >> 2, pchunk = lane & 3;
-  auto issue = [&](int k0, int buf) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int q = wave * 2 + i;
-      const int r = q * 16 + lrow;
-      const int c = pchunk ^ ((r >> 2) & 3);
-      const int ga = min(bm + r, g.M - 1), gb = min(bn + pair_perm(r), g.N - 1);
-      __builtin_amdgcn_global_load_lds((const void*)(g.A + (size_t)ga * g.lda + k0 + c * 8),
-                                       (__attribute__((address_space(3))) void*)(As(buf) + q * 1024), 16, 0, 0);
-      __builtin_amdgcn_global_load_lds((const void*)(g.B + (size_t)gb * g.ldb + k0 + c * 8),
-                                       (__attribute__((address_space(3))) void*)(Bs(buf) + q * 1024), 16, 0, 0);
-    }
-  };
-  const int nk_all = g.K / BK32;
-  const int per = (nk_all + g.splitk - 1) / g.splitk;
-  const int kt0 = split * per;
-  const int nk = max(0, min(nk_all, kt0 + per) - kt0);
-  if (nk > 0) issue(kt0 * BK32, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    bf16x8 af[4], bf[4];
-    const int chunk = lane >> 4;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int ra_ = wm + i * 16 + (lane & 15);
-      af[i] = *reinterpret_cast<const bf16x8*>(As(cur) + ra_ * kRow32 + ((chunk ^ ((ra_ >> 2) & 3)) << 4));
-      const int rb_ = wn + i * 16 + (lane & 15);
-      bf[i] = *reinterpret_cast<const bf16x8*>(Bs(cur) + rb_ * kRow32 + ((chunk ^ ((rb_ >> 2) & 3)) << 4));
-    }
-    if (kt + 1 < nk) issue((kt0 + kt + 1) * BK32, cur ^ 1);
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j], af[i], acc[i][j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-  }
-  store_direct(g, acc, bm + wm, bn + wn, split, lane);
-}
-
-// Multi-stage form of k_gemm_nt_glds32: STAGES 16-KiB LDS buffers, the DMA of
-// K-tile kt + STAGES - 1 is issued while tile kt feeds the MFMAs.  The 128x128
-// kernels are latency-bound on short K (one K-tile in flight per workgroup, two
-// workgroups per CU: ~64 KiB outstanding per CU, while the MFMA rate needs ~150
-// KiB at ~1 us L2/HBM latency); with 5 stages two workgroups keep 128 KiB in
-// flight in 160 KiB of LDS.  One barrier per K-tile, at the top: it publishes
-// tile kt to every wave and proves buffer (kt - 1) % STAGES -- the next DMA
-// target -- fully read.  Measured (benchmarks/qkv_shapes.py,
-// profiles/r1_qkv_reassoc/qkv_shapes2.txt): no gain -- 32768x768x768 52.5 us
-// (BK = 64, 2 stages) vs 59 / 63 / 62 us at 3 / 4 / 5 stages -- so the depth of
-// the load pipeline is not what limits the 128x128 kernel; A/B knob only.
-template <int STAGES, int FAST>
-__global__ void __launch_bounds__(NT) k_gemm_nt_glds32ms(GemmArgs g) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem_ms[];
-  constexpr int kTile = (BM + BN) * kRow32;
-  const int tiles_n = (g.N + BN - 1) / BN, tiles_m = (g.M + BM - 1) / BM;
-  const int nwg = tiles_n * tiles_m * g.splitk;
-  int wg = xcd_remap(blockIdx.x, nwg);
-  const int split = wg % g.splitk;
-  wg /= g.splitk;
-  const int bm = (wg / tiles_n) * BM, bn = (wg % tiles_n) * BN;
-  const int t = threadIdx.x, lane = t & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
-  const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
-  auto As = [&](int buf) { return smem_ms + buf * kTile; };
-  auto Bs = [&](int buf) { return smem_ms + buf * kTile + BM * kRow32; };
-  floatx4 acc[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-  const int lrow = lane >> 2, pchunk = lane & 3;
-  auto issue = [&](int k0, int buf) {  // 4 DMA instructions per thread per K-tile
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int q = wave * 2 + i;
-      const int r = q * 16 + lrow;
-      const int c = pchunk ^ ((r >> 2) & 3);
-      const int ga = min(bm + r, g.M - 1), gb = min(bn + pair_perm(r), g.N - 1);
-      __builtin_amdgcn_global_load_lds((const void*)(g.A + (size_t)ga * g.lda + k0 + c * 8),
-                                       (__attribute__((address_space(3))) void*)(As(buf) + q * 1024), 16, 0, 0);
-      __builtin_amdgcn_global_load_lds((const void*)(g.B + (size_t)gb * g.ldb + k0 + c * 8),
-                                       (__attribute__((address_space(3))) void*)(Bs(buf) + q * 1024), 16, 0, 0);
-    }
-  };
-  const int nk_all = g.K / BK32;
-  const int per = (nk_all + g.splitk - 1) / g.splitk;
-  const int kt0 = split * per;
-  const int nk = max(0, min(nk_all, kt0 + per) - kt0);
-#pragma unroll
-  for (int s = 0; s < STAGES - 1; ++s)
-    if (s < nk) issue((kt0 + s) * BK32, s);
-  for (int kt = 0; kt < nk; ++kt) {
-    // tile kt has landed once at most min(STAGES - 2, nk - 1 - kt) younger tiles are pending
-    const int younger = min(STAGES - 2, nk - 1 - kt);
-    if (younger >= 3) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-    else if (younger == 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    else if (younger == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    const int cur = kt % STAGES;
-    bf16x8 af[4], bf[4];
-    const int chunk = lane >> 4;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int ra_ = wm + i * 16 + (lane & 15);
-      af[i] = *reinterpret_cast<const bf16x8*>(As(cur) + ra_ * kRow32 + ((chunk ^ ((ra_ >> 2) & 3)) << 4));
-      const int rb_ = wn + i * 16 + (lane & 15);
-      bf[i] = *reinterpret_cast<const bf16x8*>(Bs(cur) + rb_ * kRow32 + ((chunk ^ ((rb_ >> 2) & 3)) << 4));
-    }
-    if (kt + STAGES - 1 < nk) issue((kt0 + kt + STAGES - 1) * BK32, (kt + STAGES - 1) % STAGES);
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j], af[i], acc[i][j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-  }
-  constexpr bool kFastBf16 = ((FAST - 1) & 1) != 0;
-  constexpr int kFastBias = (FAST - 1) / 2;
-  if constexpr (FAST > 0) store_direct_fast<kFastBf16, kFastBias>(g, acc, bm + wm, bn + wn, lane);
-  else store_direct(g, acc, bm + wm, bn + wn, split, lane);
-}
-
-template <int STAGES>
-void launch_glds32ms(const GemmArgs& g, int nwg, int id, hipStream_t st) {
-  constexpr size_t lds = (size_t)STAGES * (BM + BN) * kRow32;
-  static bool attr = [] {
-    bool ok = true;
-    for (const void* f : {reinterpret_cast<const void*>(k_gemm_nt_glds32ms<STAGES, 0>),
-                          reinterpret_cast<const void*>(k_gemm_nt_glds32ms<STAGES, 1>),
-                          reinterpret_cast<const void*>(k_gemm_nt_glds32ms<STAGES, 2>),
-                          reinterpret_cast<const void*>(k_gemm_nt_glds32ms<STAGES, 3>),
-                          reinterpret_cast<const void*>(k_gemm_nt_glds32ms<STAGES, 4>),
-                          reinterpret_cast<const void*>(k_gemm_nt_glds32ms<STAGES, 5>),
-                          reinterpret_cast<const void*>(k_gemm_nt_glds32ms<STAGES, 6>)})
-      ok = ok && hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) == hipSuccess;
-    return ok;
-  }();
-  (void)attr;
-  switch (id) {
-    case 1: hipLaunchKernelGGL((k_gemm_nt_glds32ms<STAGES, 1>), dim3(nwg), dim3(NT), lds, st, g); break;
-    case 2: hipLaunchKernelGGL((k_gemm_nt_glds32ms<STAGES, 2>), dim3(nwg), dim3(NT), lds, st, g); break;
-    case 3: hipLaunchKernelGGL((k_gemm_nt_glds32ms<STAGES, 3>), dim3(nwg), dim3(NT), lds, st, g); break;
-    case 4: hipLaunchKernelGGL((k_gemm_nt_glds32ms<STAGES, 4>), dim3(nwg), dim3(NT), lds, st, g); break;
-    case 5: hipLaunchKernelGGL((k_gemm_nt_glds32ms<STAGES, 5>), dim3(nwg), dim3(NT), lds, st, g); break;
-    case 6: hipLaunchKernelGGL((k_gemm_nt_glds32ms<STAGES, 6>), dim3(nwg), dim3(NT), lds, st, g); break;
-    default: hipLaunchKernelGGL((k_gemm_nt_glds32ms<STAGES, 0>), dim3(nwg), dim3(NT), lds, st, g); break;
-  }
-}
-
-// Persistent form of k_gemm_nt_glds<DIRECT = true> (LDS-free epilogue): each
-// workgroup walks tiles blockIdx.x, +gridDim.x, ... (XCD-remapped), and issues
-// the NEXT tile's first K-tile DMA before this tile's epilogue stores, so the
-// stores drain while the next tile computes (two co-resident workgroups on a CU
-// otherwise reach their store phases in lockstep and the stores serialize with
-// the MFMA work).  vmcnt retires in issue order, so waiting for that prefetch
-// must skip exactly the younger stores: on the fast path (full tiles, splitk 1,
-// no accumulate, 16-B aligned C) a wave issues 8 (bf16) or 16 (fp32) of them;
-// otherwise it waits for everything.
-// workgroup barrier WITHOUT the release/acquire fences of __syncthreads(): those
-// lower to s_waitcnt vmcnt(0), i.e. they would wait for every in-flight global
-// store.  LDS ordering comes from the explicit waits placed before each call.
-__device__ __forceinline__ void lds_barrier() {
-  __builtin_amdgcn_sched_barrier(0);
-  asm volatile("s_barrier" ::: "memory");
-  __builtin_amdgcn_sched_barrier(0);
-}
-
-__device__ __forceinline__ void wait_vm_stores(int n) {
-  if (n == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-  else if (n == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
-
-// FULL: M % 128 == 0 and N % 128 == 0 -- no row clamping, so the DMA
-// addresses are a uniform (SGPR) tile base plus per-lane offsets computed once:
-// no VGPR that an in-flight DMA reads is rewritten between tiles (the compiler
-// would otherwise wait for every outstanding memory operation, stores included).
-template <bool FULL>
-__global__ void __launch_bounds__(NT) k_gemm_nt_persist(GemmArgs g) {
-  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * (BM + BN) * kRowBytes];
-  const int tiles_n = (g.N + BN - 1) / BN, tiles_m = (g.M + BM - 1) / BM;
-  const int ntiles = tiles_n * tiles_m;
-  const int t = threadIdx.x, lane = t & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
-  const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
-  auto As = [&](int buf) { return smem + buf * ((BM + BN) * kRowBytes); };
-  auto Bs = [&](int buf) { return smem + buf * ((BM + BN) * kRowBytes) + BM * kRowBytes; };
-  const int es = g.out_bf16 ? 2 : 4;
-  const bool fast = g.splitk == 1 && !g.accumulate && g.M % BM == 0 && g.N % BN == 0 &&
-                    (((uint64_t)g.C | ((uint64_t)g.ldc * es)) % 16) == 0;
-  const int nstores = fast ? (g.out_bf16 ? 8 : 16) : 0;
-  const int lrow = lane >> 3, pchunk = lane & 7;
-  auto coords = [&](int L, int& bm, int& bn) {
-    const int wg = xcd_remap(L, ntiles);
-    bm = (wg / tiles_n) * BM;
-    bn = (wg % tiles_n) * BN;
-  };
-  uint32_t aoff[4], boff[4];  // per-lane BYTE offsets within a tile (FULL path; saddr + voffset form)
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int r = (wave * 4 + i) * 8 + lrow, c = pchunk ^ (r & 7);
-    aoff[i] = (uint32_t)(r * g.lda + c * 8) * 2u;
-    boff[i] = (uint32_t)(pair_perm(r) * g.ldb + c * 8) * 2u;
-  }
-  auto issue = [&](int bm, int bn, int k0, int buf) {
-    const char* Ab = reinterpret_cast<const char*>(g.A + (size_t)bm * g.lda + k0);
-    const char* Bb = reinterpret_cast<const char*>(g.B + (size_t)bn * g.ldb + k0);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int q = wave * 4 + i;
-      const void *pa, *pb;
-      if constexpr (FULL) {
-        pa = Ab + aoff[i];
-        pb = Bb + boff[i];
-      } else {
-        const int r = q * 8 + lrow, c = pchunk ^ (r & 7);
-        pa = g.A + (size_t)min(bm + r, g.M - 1) * g.lda + k0 + c * 8;
-        pb = g.B + (size_t)min(bn + pair_perm(r), g.N - 1) * g.ldb + k0 + c * 8;
-      }
-      __builtin_amdgcn_global_load_lds(pa, (__attribute__((address_space(3))) void*)(As(buf) + q * 1024),
-                                       16, 0, 0);
-      __builtin_amdgcn_global_load_lds(pb, (__attribute__((address_space(3))) void*)(Bs(buf) + q * 1024),
-                                       16, 0, 0);
-    }
-  };
-  const int nk = g.K / BK;
-  int L = blockIdx.x;
-  if (L >= ntiles || nk == 0) return;
-  int bm, bn;
-  coords(L, bm, bn);
-  int buf = 0;
-  issue(bm, bn, 0, buf);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  for (;;) {
-    const int Ln = L + gridDim.x;
-    const bool more = Ln < ntiles;
-    int bmn = 0, bnn = 0;
-    if (more) coords(Ln, bmn, bnn);
-    floatx4 acc[4][4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-    for (int kt = 0; kt < nk; ++kt) {
-      const int cur = buf;
-      bf16x8 af[2][4], bf[2][4];  // all fragment reads before the DMA (see k_gemm_nt_glds)
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        const int chunk = ks * 4 + (lane >> 4);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int ra_ = wm + i * 16 + (lane & 15);
-          af[ks][i] = *reinterpret_cast<const bf16x8*>(As(cur) + ra_ * kRowBytes + ((chunk ^ (ra_ & 7)) << 4));
-          const int rb_ = wn + i * 16 + (lane & 15);
-          bf[ks][i] = *reinterpret_cast<const bf16x8*>(Bs(cur) + rb_ * kRowBytes + ((chunk ^ (rb_ & 7)) << 4));
-        }
-      }
-      if (kt + 1 < nk) issue(bm, bn, (kt + 1) * BK, cur ^ 1);
-      else if (more) issue(bmn, bnn, 0, cur ^ 1);  // next tile's first K-tile, ahead of our stores
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[ks][j], af[ks][i], acc[i][j], 0, 0, 0);
-      __builtin_amdgcn_s_setprio(0);
-      buf ^= 1;
-      if (kt + 1 < nk) {
-        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-        lds_barrier();
-      }
-    }
-    store_direct(g, acc, bm + wm, bn + wn, 0, lane);
-    if (!more) break;
-    wait_vm_stores(nstores);  // the prefetched K-tile has landed; this tile's stores may still be in flight
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    lds_barrier();
-    L = Ln;
-    bm = bmn;
-    bn = bnn;
-  }
-}
 
 // ---------------------------------------------------------------------------
 // "TN" GEMM for weight gradients: C[N1,N2] (+)= alpha * sum_m A[m,n1] * B[m,n2]
@@ -1266,26 +944,8 @@ void gemm_nt(uint64_t A, uint64_t B, uint64_t C, uint64_t bias, int M, int N, in
       return;
     }
   }
-  if (K % BK == 0 && g_use_glds && g_direct_epi && g_stages >= 3) {
-    const bool fast = splitk == 1 && !accumulate && act == 0 && N % 8 == 0 && ldc % 8 == 0 && (C % 16) == 0;
-    const int id = fast ? 1 + (out_bf16 ? 1 : 0) + 2 * bias_kind : 0;
-    auto st = reinterpret_cast<hipStream_t>(stream);
-    if (g_stages == 3) launch_glds32ms<3>(g, nwg, id, st);
-    else if (g_stages == 4) launch_glds32ms<4>(g, nwg, id, st);
-    else launch_glds32ms<5>(g, nwg, id, st);
-    CCMPI_HIP_CHECK(hipGetLastError());
-    return;
-  }
   if (K % BK == 0 && g_use_glds) {
-    if (g_direct_epi && g_bk32) {
-      hipLaunchKernelGGL(k_gemm_nt_glds32, dim3(nwg), dim3(NT), 0, reinterpret_cast<hipStream_t>(stream), g);
-    } else if (g_direct_epi && splitk == 1 && g_persist) {
-      int grid = std::min(nwg, g_persist_grid);
-      if (M % BM == 0 && N % BN == 0)
-        hipLaunchKernelGGL(k_gemm_nt_persist<true>, dim3(grid), dim3(NT), 0, reinterpret_cast<hipStream_t>(stream), g);
-      else
-        hipLaunchKernelGGL(k_gemm_nt_persist<false>, dim3(grid), dim3(NT), 0, reinterpret_cast<hipStream_t>(stream), g);
-    } else if (g_direct_epi) {
+    if (g_direct_epi) {
       const bool fast = splitk == 1 && !accumulate && act == 0 && N % 8 == 0 && ldc % 8 == 0 && (C % 16) == 0;
       const int id = fast ? 1 + (out_bf16 ? 1 : 0) + 2 * bias_kind : 0;
       auto st = reinterpret_cast<hipStream_t>(stream);
@@ -1400,10 +1060,6 @@ void register_gemm_ops(pybind11::module_& m) {
         pybind11::arg("variant") = 0, pybind11::arg("C2") = 0, pybind11::arg("ldc2") = 0, pybind11::arg("csplit") = 0,
         pybind11::call_guard<pybind11::gil_scoped_release>());
   m.def("gemm_set_glds", [](bool on) { g_use_glds = on; }, "select LDS-DMA (True) or register staging");
-  m.def("gemm_set_bk32", [](bool on) { g_bk32 = on; }, "128x128 kernel: BK = 32 (32 KiB LDS) or BK = 64");
-  m.def("gemm_set_stages", [](int s) { g_stages = s; }, "128x128 kernel: multi-stage BK = 32 pipeline depth (0 = off, 3..5)");
-  m.def("gemm_set_persistent", [](bool on, int grid) { g_persist = on; g_persist_grid = grid > 0 ? grid : 512; },
-        "persistent 128x128 kernel (next-tile prefetch ahead of the epilogue stores) and its grid");
   m.def("gemm_set_direct_epilogue", [](bool on) { g_direct_epi = on; },
         "128x128 LDS-DMA kernel: LDS-free epilogue (True) or LDS-staged rows");
   m.def("gemm_set_kernel", [](int k) { g_kernel = k; }, "gemm_nt tile choice: 0 auto, 1 128x128, 2 256x256, 3 256x128, 4 256x192");

@@ -331,73 +331,6 @@ __global__ void __launch_bounds__(kFoldNT) k_fold_emb_qkv(const float* __restric
   }
 }
 
-// MFMA variant of the fold (fold_set_impl(0); measured 9.3 us against 7.3 us for the
-// fp32 kernel above, which stays the default: 64 strided 4-B We loads per lane make it
-// load-issue bound, and its bf16 operands are less precise): one 16 x 16 tile of Weff per workgroup
-// (240 workgroups at 768 x 72), the d contraction split over the 4 waves (k-steps of 32
-// interleaved), every operand load of a wave issued up front: Wq rows as two float4 per
-// lane and k-step, We columns as 8 strided floats (16 lanes = 64 contiguous bytes of a
-// We row), both rounded to bf16 for v_mfma_f32_16x16x32_bf16 with fp32 accumulation.
-// The 4 wave partials meet in LDS and are summed in wave order (deterministic).
-typedef __bf16 fbf16x8 __attribute__((ext_vector_type(8)));
-typedef float ff4 __attribute__((ext_vector_type(4)));
-constexpr int kFoldMfmaSteps = 8;  // k-steps of 32 per wave: d <= 4 * 8 * 32 = 1024
-
-__device__ __forceinline__ fbf16x8 to_bf16x8(const float (&v)[8]) {
-  uint4 u;
-  u.x = f32_to_bf16_bits(v[0]) | (f32_to_bf16_bits(v[1]) << 16);
-  u.y = f32_to_bf16_bits(v[2]) | (f32_to_bf16_bits(v[3]) << 16);
-  u.z = f32_to_bf16_bits(v[4]) | (f32_to_bf16_bits(v[5]) << 16);
-  u.w = f32_to_bf16_bits(v[6]) | (f32_to_bf16_bits(v[7]) << 16);
-  return __builtin_bit_cast(fbf16x8, u);
-}
-
-__global__ void __launch_bounds__(256) k_fold_emb_qkv_mfma(const float* __restrict__ Wq, int ld_wq,
-                                                           const float* __restrict__ We, int ld_we,
-                                                           uint16_t* __restrict__ Weff, int ld_eff, int R, int d, int kp,
-                                                           const float* __restrict__ bias, int bias_col) {
-  __shared__ float part[4][16][17];
-  const int tiles_n = (kp + 15) / 16;
-  const int r0 = (blockIdx.x / tiles_n) * 16, n0 = (blockIdx.x % tiles_n) * 16;
-  const int t = threadIdx.x, wave = t >> 6, lane = t & 63, c = lane & 15, g = lane >> 4;
-  const int nks = (d + 31) / 32;
-  const bool rok = r0 + c < R, nok = n0 + c < kp;
-  float a[kFoldMfmaSteps][8], b[kFoldMfmaSteps][8];
-#pragma unroll
-  for (int u = 0; u < kFoldMfmaSteps; ++u) {
-    const int k0 = 32 * (wave + 4 * u) + 8 * g;
-    const bool full = wave + 4 * u < nks && k0 + 8 <= d;
-    if (full && rok) {
-      const float4 x = *reinterpret_cast<const float4*>(Wq + (size_t)(r0 + c) * ld_wq + k0);
-      const float4 y = *reinterpret_cast<const float4*>(Wq + (size_t)(r0 + c) * ld_wq + k0 + 4);
-      a[u][0] = x.x; a[u][1] = x.y; a[u][2] = x.z; a[u][3] = x.w;
-      a[u][4] = y.x; a[u][5] = y.y; a[u][6] = y.z; a[u][7] = y.w;
-    } else {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) a[u][e] = (rok && wave + 4 * u < nks && k0 + e < d) ? Wq[(size_t)(r0 + c) * ld_wq + k0 + e] : 0.f;
-    }
-#pragma unroll
-    for (int e = 0; e < 8; ++e)
-      b[u][e] = (nok && wave + 4 * u < nks && k0 + e < d) ? We[(size_t)(k0 + e) * ld_we + n0 + c] : 0.f;
-  }
-  ff4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int u = 0; u < kFoldMfmaSteps; ++u)
-    if (wave + 4 * u < nks) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(to_bf16x8(a[u]), to_bf16x8(b[u]), acc, 0, 0, 0);
-  // acc[r] = partial Weff[r0 + 4g + r][n0 + c]
-#pragma unroll
-  for (int r = 0; r < 4; ++r) part[wave][4 * g + r][c] = acc[r];
-  __syncthreads();
-  const int i = t >> 4, j = t & 15;  // one output per thread of the 16 x 16 tile
-  if (r0 + i < R && n0 + j < kp) {
-    float v = part[0][i][j] + part[1][i][j] + part[2][i][j] + part[3][i][j];
-    if (bias && n0 + j == bias_col) v += bias[r0 + i];
-    Weff[(size_t)(r0 + i) * ld_eff + n0 + j] = static_cast<uint16_t>(f32_to_bf16_bits(v));
-  }
-}
-
-int g_fold_impl = 1;  // 0 = MFMA (bf16 operands), 1 = fp32 FMA kernel (default, faster)
-
 size_t fold_lds_bytes(int d, int kp) {
   const int half = (kFoldNT / (kp / 4) + 1) / 2;
   return sizeof(float) * std::max<size_t>((size_t)kFoldRows * d, (size_t)half * kFoldRows * kp);
@@ -409,14 +342,6 @@ void fold_emb_qkv(uint64_t Wq, int ld_wq, uint64_t We, int ld_we, uint64_t Weff,
   if (R <= 0 || d <= 0 || kp <= 0) return;
   if (kp > kMaxKp || kp % 4 || d % 4 || d > kFoldMaxD || ld_wq % 4 || ld_we % 4 || (Wq % 16) || (We % 16) || !Weff)
     throw std::invalid_argument("fold_emb_qkv: kp <= 96, d <= 1024, kp / d / fp32 row strides % 4 == 0, 16-B aligned fp32 operands");
-  if (g_fold_impl == 0) {
-    const int tiles = ((R + 15) / 16) * ((kp + 15) / 16);
-    hipLaunchKernelGGL(k_fold_emb_qkv_mfma, dim3(tiles), dim3(256), 0, (hipStream_t)stream,
-                       reinterpret_cast<const float*>(Wq), ld_wq, reinterpret_cast<const float*>(We), ld_we,
-                       reinterpret_cast<uint16_t*>(Weff), ld_eff, R, d, kp, reinterpret_cast<const float*>(bias), bias_col);
-    CCMPI_HIP_CHECK(hipGetLastError());
-    return;
-  }
   const size_t lds = fold_lds_bytes(d, kp);
   if (lds > 64 * 1024) throw std::invalid_argument("fold_emb_qkv: LDS staging exceeds 64 KiB");
   hipLaunchKernelGGL(k_fold_emb_qkv, dim3((R + kFoldRows - 1) / kFoldRows), dim3(kFoldNT), lds, (hipStream_t)stream,
@@ -433,8 +358,6 @@ void register_wgrad_ops(pybind11::module_& m) {
         pybind11::arg("Wq"), pybind11::arg("ld_wq"), pybind11::arg("We"), pybind11::arg("ld_we"), pybind11::arg("Weff"),
         pybind11::arg("ld_eff"), pybind11::arg("R"), pybind11::arg("d"), pybind11::arg("kp"), pybind11::arg("stream"),
         pybind11::arg("bias") = 0, pybind11::arg("bias_col") = -1, pybind11::call_guard<pybind11::gil_scoped_release>());
-  m.def("fold_set_impl", [](int impl) { g_fold_impl = impl; },
-        "fold_emb_qkv implementation: 0 = MFMA (bf16 operands), 1 = fp32 FMA (default)", pybind11::arg("impl"));
   m.def("emb_qkv_wgrad", &emb_qkv_wgrad,
         "Gq += A . We^T (fixed order); Ge += Wq^T . A (fp32 atomics; Ge = 0: skipped); Z = 0 (Z = 0: skipped)",
         pybind11::arg("A"), pybind11::arg("ld_a"), pybind11::arg("We"), pybind11::arg("ld_we"), pybind11::arg("Wq"),

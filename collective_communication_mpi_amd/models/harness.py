@@ -128,7 +128,7 @@ def bench_forward(comm, tp: int = 2, batch: int = 2048, steps: int = 20, warmup:
     return {"tp": cfg.tp, "dp": cfg.dp, "fwd_ms": fwd_s * 1e3, "train_ms": train_s * 1e3,
             "global_batch": cfg.batch * cfg.dp, "seq_len": cfg.seq, "tokens_per_step": cfg.batch * cfg.dp * cfg.seq,
             "hip_graph": used_graph, "fc_o_mode": cfg.fc_o_mode,
-            "fwd_saves_activations": False, "qkv_in_attention": layer._fuses_proj(), "loss": round(loss_v, 5)}
+            "fwd_saves_activations": False, "loss": round(loss_v, 5)}
 
 
 def smoke_step(comm) -> None:

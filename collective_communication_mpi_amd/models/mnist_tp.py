@@ -105,14 +105,6 @@ class LayerConfig:
     # forward: qkv = Xp . (W_qkv W_emb)^T + b -- h is never formed (needs the re-associated
     # backward, which does not read h); False: h = Xp . W_emb^T, then qkv = h . W_qkv^T + b
     fold_emb: bool = True
-    # with fold_emb: the projection qkv = Xp . W_eff^T runs inside the attention forward
-    # kernel (W_eff rows in registers); qkv is written only when the forward saves
-    # activations for a backward.  Off by default: measured slower (rocprofv3, 32768
-    # tokens): 41.9 us inference / 53.6 us saving vs 16.6 us attention + 23.0 us GEMM --
-    # the 144 W registers per wave leave one wave per SIMD and the persistent waves
-    # run their 8 sequences back to back, latency-bound (profiles/r1_fold/)
-    fuse_qkv_attn: bool = False
-
     @property
     def seq(self) -> int:
         return (self.img // self.patch) ** 2
@@ -259,27 +251,25 @@ class MnistTPLayer:
         return hx[:, cfg.d_model:cfg.d_model + cfg.kp]
 
     def _folds(self) -> bool:
+        """The forward weight fold W_eff = W_qkv W_emb, within the fold kernel's limits
+        (csrc/device/wgrad.hip: d_model <= 1024 staged in LDS, d_model % 4 == 0);
+        other widths fall back to h = Xp W_emb^T, then the QKV GEMM."""
         cfg = self.cfg
-        return cfg.fold_emb and cfg.emb_grad == "reassoc" and cfg.qkv_grad == "reassoc"
+        return (cfg.fold_emb and cfg.emb_grad == "reassoc" and cfg.qkv_grad == "reassoc"
+                and cfg.d_model <= 1024 and cfg.d_model % 4 == 0 and cfg.kp <= 96)
 
-    def _fuses_proj(self) -> bool:
-        cfg = self.cfg
-        return (cfg.fuse_qkv_attn and self._folds() and self._fused_fc_o() and cfg.seq <= 16
-                and cfg.head_dim in (32, 64) and 4 % self.hl == 0)
-
-    def folded_qkv_weight(self, stream=None, with_bias: bool = False) -> torch.Tensor:
+    def folded_qkv_weight(self, stream=None) -> torch.Tensor:
         """W_eff = W_qkv . W_emb (3hd x kp bf16) from the fp32 master weights (fp32
         accumulation, fixed summation order), recomputed on every forward so it always
-        follows the optimizer (and is captured into the step's HIP graph).  with_bias:
-        b_qkv is added to the column that multiplies Xp's constant-1 column."""
+        follows the optimizer (and is captured into the step's HIP graph).  b_qkv is
+        added in the QKV GEMM's fp32 epilogue."""
         cfg = self.cfg
         R = 3 * self.hd
-        weff = self._buf("weff_b" if with_bias else "weff", (R, cfg.kp), torch.bfloat16)
+        weff = self._buf("weff", (R, cfg.kp), torch.bfloat16)
         wq, we = self.flat.param("qkv_w"), self.flat.param("emb_w")
         st = stream if stream is not None else torch.cuda.current_stream(self.device).cuda_stream
-        bias = self.flat.param("qkv_b").data_ptr() if with_bias else 0
         _native.device().fold_emb_qkv(wq.data_ptr(), wq.stride(0), we.data_ptr(), we.stride(0), weff.data_ptr(),
-                                      weff.stride(0), R, cfg.d_model, cfg.kp, st, bias=bias, bias_col=cfg.pixels)
+                                      weff.stride(0), R, cfg.d_model, cfg.kp, st)
         return weff
 
     def forward(self, xp: torch.Tensor, B: int, images: Optional[torch.Tensor] = None,
@@ -297,14 +287,7 @@ class MnistTPLayer:
         fused = hx is not None and xp.data_ptr() == hx.data_ptr() + 2 * d and xp.stride(0) == hx.stride(0)
         qkv = self._buf("qkv", (M, 3 * self.hd), torch.bfloat16)
         h = None
-        proj = self._fuses_proj()
-        if proj:
-            # projection inside the attention kernel (below); W_eff carries b_qkv
-            if images is not None:
-                patchify(images, cfg, out=xp)
-            weff = self.folded_qkv_weight(with_bias=True)
-            images = None
-        elif self._folds():
+        if self._folds():
             if images is not None:
                 patchify(images, cfg, out=xp)
             gemm_nt(xp, weff if weff is not None else self.folded_qkv_weight(), out=qkv, bias=self.flat.param("qkv_b"))
@@ -344,15 +327,10 @@ class MnistTPLayer:
             wo = self.flat.param16("o_w")
             fc = dict(wo=wo.data_ptr(), ld_wo=wo.stride(0), n_out=cfg.out_pad, zp=zp.data_ptr(), ld_zp=zp.stride(0),
                       bo=self.flat.param("o_b").data_ptr() if self.tp_idx == 0 else 0)
-        if proj:
-            if xp.stride(1) != 1:
-                raise ValueError("forward: xp needs unit column stride")
-            fc.update(xp=xp.data_ptr(), ld_xp=xp.stride(0), kp=cfg.kp, weff=weff.data_ptr(), ld_weff=weff.stride(0),
-                      qkv_out=qkv.data_ptr() if save else 0)
         # token fc_o with TP: attention runs per row block inside the TP pipeline below
         pipelined = token and self._token_chunks(B) > 1
         if not pipelined:
-            D.attn_small_fwd(0 if proj else qkv.data_ptr(), 0 if att is None else att.data_ptr(), lse.data_ptr(), B, S,
+            D.attn_small_fwd(qkv.data_ptr(), 0 if att is None else att.data_ptr(), lse.data_ptr(), B, S,
                              self.hl, cfg.head_dim, qkv.stride(0), self.hd if att is None else att.stride(0),
                              1.0 / math.sqrt(cfg.head_dim),
                              0 if pool is None else pool.data_ptr(), 0 if pool is None else pool.stride(0), st, **fc)
@@ -406,9 +384,8 @@ class MnistTPLayer:
         hx = self._bufs.get(("hx", (M, self._hx_ld), torch.bfloat16))
         folds = self._folds()
         h = None if folds else (hx[:, :d] if hx is not None else self._buf("h", (M, d), torch.bfloat16))
-        proj = self._fuses_proj()
         # on the main stream, before the fork
-        weff = self.folded_qkv_weight(with_bias=proj) if folds else None
+        weff = self.folded_qkv_weight() if folds else None
         qkv = self._buf("qkv", (M, 3 * hd), torch.bfloat16)
         lse = self._buf("lse", (B * hl, S), torch.float32)
         pool = self._buf("pool", (B, hd), torch.bfloat16)
@@ -428,19 +405,15 @@ class MnistTPLayer:
             r0, r1 = b0 * S, b1 * S
             with torch.cuda.stream(s):
                 patchify(images[b0:b1], cfg, out=xp[r0:r1])
-                pj = {}
-                if proj:  # projection inside the attention kernel
-                    pj = dict(xp=xp[r0:r1].data_ptr(), ld_xp=xp.stride(0), kp=cfg.kp, weff=weff.data_ptr(),
-                              ld_weff=weff.stride(0), qkv_out=qkv[r0:r1].data_ptr() if save else 0)
-                elif folds:
+                if folds:
                     gemm_nt(xp[r0:r1], weff, out=qkv[r0:r1], bias=bias)
                 else:
                     gemm_nt(xp[r0:r1], P16("emb_w"), out=h[r0:r1])
                     gemm_nt(h[r0:r1], P16("qkv_w"), out=qkv[r0:r1], bias=bias)
-                D.attn_small_fwd(0 if proj else qkv[r0:r1].data_ptr(), 0, lse[b0 * hl:b1 * hl].data_ptr(), Bc, S, hl,
+                D.attn_small_fwd(qkv[r0:r1].data_ptr(), 0, lse[b0 * hl:b1 * hl].data_ptr(), Bc, S, hl,
                                  cfg.head_dim, qkv.stride(0), hd, 1.0 / math.sqrt(cfg.head_dim), pool[b0:b1].data_ptr(),
                                  pool.stride(0), s.cuda_stream, wo=wo.data_ptr(), ld_wo=wo.stride(0),
-                                 n_out=cfg.out_pad, zp=zp[b0:b1].data_ptr(), ld_zp=zp.stride(0), bo=bo, **pj)
+                                 n_out=cfg.out_pad, zp=zp[b0:b1].data_ptr(), ld_zp=zp.stride(0), bo=bo)
         for s in self._bufs[key]:
             main.wait_stream(s)
         if self.tp_dev is not None:

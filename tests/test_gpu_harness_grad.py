@@ -27,20 +27,22 @@ def _reference(cfg, xp, y, P):
     return loss.detach(), {k: t.grad for k, t in w.items()}
 
 
-@pytest.mark.parametrize("emb_grad,qkv_grad,fused,fuse_fc_o,fold_emb,fuse_qkv_attn", [
-    ("reassoc", "reassoc", True, True, True, True), ("reassoc", "reassoc", True, False, True, True),
-    ("reassoc", "reassoc", False, True, True, True), ("reassoc", "reassoc", False, True, True, False),
-    ("reassoc", "reassoc", False, True, False, False),
-    ("reassoc", "direct", True, True, True, True), ("reassoc", "direct", False, True, True, True),
-    ("dh", "direct", True, True, True, True), ("dh", "direct", False, False, True, True)])
-def test_harness_grads_match_torch_fp32(emb_grad, qkv_grad, fused, fuse_fc_o, fold_emb, fuse_qkv_attn):
+@pytest.mark.parametrize("emb_grad,qkv_grad,fused,fuse_fc_o,fold_emb,d_model", [
+    ("reassoc", "reassoc", True, True, True, 768), ("reassoc", "reassoc", True, False, True, 768),
+    ("reassoc", "reassoc", False, True, True, 768), ("reassoc", "reassoc", False, True, False, 768),
+    ("reassoc", "direct", True, True, True, 768), ("reassoc", "direct", False, True, True, 768),
+    ("dh", "direct", True, True, True, 768), ("dh", "direct", False, False, True, 768),
+    # d_model > 1024: beyond the fold kernel's LDS staging -> unfolded embedding + QKV GEMMs
+    ("reassoc", "reassoc", True, True, True, 1280)])
+def test_harness_grads_match_torch_fp32(emb_grad, qkv_grad, fused, fuse_fc_o, fold_emb, d_model):
     from collective_communication_mpi_amd import MPI, Communicator
     from collective_communication_mpi_amd.models.harness import build
     from collective_communication_mpi_amd.models.mnist_tp import local_batch, patchify
 
     comm = Communicator(MPI.COMM_WORLD)
     cfg, layer, x_all, y_all = build(comm, 1, 128, emb_grad=emb_grad, qkv_grad=qkv_grad, fuse_fc_o=fuse_fc_o,
-                                     fold_emb=fold_emb, fuse_qkv_attn=fuse_qkv_attn)
+                                     fold_emb=fold_emb, d_model=d_model)
+    assert layer._folds() == (fold_emb and emb_grad == qkv_grad == "reassoc" and d_model <= 1024)
     # non-trivial biases so their gradients and the bias epilogues are exercised
     g = torch.Generator().manual_seed(7)
     layer.flat.param("qkv_b").copy_(torch.randn(layer.flat.param("qkv_b").shape, generator=g) * 0.1)
@@ -96,15 +98,14 @@ def test_chunked_multistream_forward_is_bitwise_identical(chunks):
 
 
 def test_inference_forward_matches_training_forward():
-    """forward_images(save=False) (no qkv written, nothing kept) gives the same logits as
+    """forward_images(save=False) (nothing kept for a backward) gives the same logits as
     the saving forward, and a backward after it fails loudly."""
     from collective_communication_mpi_amd import MPI, Communicator
     from collective_communication_mpi_amd.models.harness import build
     from collective_communication_mpi_amd.models.mnist_tp import local_batch
 
     comm = Communicator(MPI.COMM_WORLD)
-    cfg, layer, x_all, y_all = build(comm, 1, 256, fuse_qkv_attn=True)
-    assert layer._fuses_proj()
+    cfg, layer, x_all, y_all = build(comm, 1, 256)
     xb, _ = local_batch(cfg, x_all, y_all, 0, 0, layer.device)
     a = layer.forward_images(xb, cfg.batch).clone()
     b = layer.forward_images(xb, cfg.batch, save=False).clone()

@@ -186,12 +186,6 @@ def test_single_rank_allreduce_copy(nbytes):
     y = torch.zeros_like(x)
     Communicator(MPI.COMM_WORLD).Allreduce(x, y, MPI.SUM)
     assert torch.equal(x, y)
-    if nbytes % 16 == 0 and nbytes < (1 << 30):
-        for v in range(13):
-            y.zero_()
-            D.copy_variant(x.data_ptr(), y.data_ptr(), nbytes, v, 1000, torch.cuda.current_stream().cuda_stream)
-            torch.cuda.synchronize()
-            assert torch.equal(x, y), v
 
 
 def test_split_derives_rccl_communicator():
@@ -490,11 +484,10 @@ def test_gemm_tn_pingpong(M, N1, N2, splitk):
         set_tn_variant(None)
 
 
-@pytest.mark.parametrize("impl", [0, 1])
 @pytest.mark.parametrize("R,d,kp", [(768, 768, 72), (384, 768, 72), (20, 36, 16), (7, 100, 96), (50, 1000, 8)])
-def test_fold_emb_qkv_matches_fp32(R, d, kp, impl):
-    """W_eff = W_qkv . W_emb (+ bias in one column) against torch fp32/fp64, incl. ragged
-    row / column / k edges and strided operands; impl 0 = MFMA (bf16 operands), 1 = fp32 FMA."""
+def test_fold_emb_qkv_matches_fp32(R, d, kp):
+    """W_eff = W_qkv . W_emb (+ bias in one column) against torch fp64, incl. ragged
+    row / column / k edges and strided operands (fp32 FMA kernel, fixed order)."""
     from collective_communication_mpi_amd import _native
 
     torch.manual_seed(R + d)
@@ -504,54 +497,10 @@ def test_fold_emb_qkv_matches_fp32(R, d, kp, impl):
     bcol = kp // 2
     out = torch.full((R, kp + 8), float("nan"), device="cuda").bfloat16()
     dev = _native.device()
-    dev.fold_set_impl(impl)
-    try:
-        dev.fold_emb_qkv(wq.data_ptr(), wq.stride(0), we.data_ptr(), we.stride(0), out.data_ptr(), out.stride(0), R, d,
-                         kp, torch.cuda.current_stream().cuda_stream, bias=bias.data_ptr(), bias_col=bcol)
-        torch.cuda.synchronize()
-    finally:
-        dev.fold_set_impl(1)
+    dev.fold_emb_qkv(wq.data_ptr(), wq.stride(0), we.data_ptr(), we.stride(0), out.data_ptr(), out.stride(0), R, d,
+                     kp, torch.cuda.current_stream().cuda_stream, bias=bias.data_ptr(), bias_col=bcol)
+    torch.cuda.synchronize()
     ref = wq.double() @ we.double()
     ref[:, bcol] += bias.double()
-    tol = (8e-3 if impl == 1 else 2e-2) * ref.abs().max().item()
-    torch.testing.assert_close(out[:, :kp].double(), ref, rtol=8e-3, atol=tol)
+    torch.testing.assert_close(out[:, :kp].double(), ref, rtol=8e-3, atol=8e-3 * ref.abs().max().item())
     assert torch.isnan(out[:, kp:].float()).all()  # columns past kp untouched
-
-
-@pytest.mark.parametrize("B,Hl,D", [(300, 4, 64), (97, 2, 64), (64, 4, 32), (33, 1, 64)])
-def test_attention_fused_projection(B, Hl, D):
-    """Attention forward with the QKV projection inside the kernel (Xp . Weff^T, W rows in
-    registers) against the same kernel fed a torch-projected qkv: the written-out qkv rows,
-    lse, pooled output and fused fc_o logits."""
-    from collective_communication_mpi_amd import _native
-
-    dev = _native.device()
-    torch.manual_seed(B * Hl + D)
-    S, kp, nout = 16, 72, 16
-    HD = Hl * D
-    xp = (torch.rand(B * S, kp, device="cuda") * 2 - 1).bfloat16()
-    xp[:, 50:] = 0
-    weff = (torch.randn(3 * HD, kp, device="cuda") * 0.2).bfloat16()
-    wo = (torch.randn(nout, HD, device="cuda") * 0.1).bfloat16()
-    bo = torch.randn(nout, device="cuda")
-    qkv_ref = (xp.float() @ weff.float().t()).bfloat16()
-    st = torch.cuda.current_stream().cuda_stream
-    outs = []
-    for proj in (False, True):
-        qkv_out = torch.full((B * S, 3 * HD), float("nan"), device="cuda").bfloat16()
-        lse = torch.empty(B * Hl, S, device="cuda")
-        pool = torch.empty(B, HD, device="cuda").bfloat16()
-        zp = torch.empty(B, nout, device="cuda")
-        kw = dict(wo=wo.data_ptr(), ld_wo=wo.stride(0), n_out=nout, zp=zp.data_ptr(), ld_zp=zp.stride(0),
-                  bo=bo.data_ptr())
-        if proj:
-            kw.update(xp=xp.data_ptr(), ld_xp=xp.stride(0), kp=kp, weff=weff.data_ptr(), ld_weff=weff.stride(0),
-                      qkv_out=qkv_out.data_ptr())
-        dev.attn_small_fwd(0 if proj else qkv_ref.data_ptr(), 0, lse.data_ptr(), B, S, Hl, D, 3 * HD, HD,
-                           D ** -0.5, pool.data_ptr(), pool.stride(0), st, **kw)
-        torch.cuda.synchronize()
-        outs.append((qkv_out, lse, pool, zp))
-    qkv_out = outs[1][0]
-    torch.testing.assert_close(qkv_out.float(), qkv_ref.float(), rtol=1e-2, atol=1e-2)
-    for x, y in zip(outs[0][1:], outs[1][1:]):
-        torch.testing.assert_close(y.float(), x.float(), rtol=2e-2, atol=2e-2)
