@@ -98,6 +98,7 @@ def shared_dry_run(n: int, steps: int, warmup: int, verbose: bool):
         print("[bench] shared dry run:", lines[-1][:400], file=sys.stderr)
     keep = {k: out[k] for k in ("value", "ms_per_step", "n_gpus")}
     keep["ranks"] = n
+    keep["unit"] = "GB/s (1 GiB fp32 all-reduce algbw)"
     keep["note"] = f"{n} ranks sharing ONE GPU through IPC: HBM + protocol, not xGMI"
     keep.update({k: out["config"].get(k) for k in ("allreduce_algo", "busbw_GBps", "candidates_ms", "result_exact",
                                                      "bf16_1GiB", "alltoall", "dp_overlap", "tp_fwd_step_ms",
@@ -298,7 +299,7 @@ def main() -> int:
             "metric": "all-reduce algbw (GB/s) @1GiB fp32 + DP4xTP2 fwd step time, 1/2/4/8 MI355X",
             "value": round(algbw, 3),
             "unit": "GB/s",
-            "n_gpus": world,
+            "n_gpus": world // dev.ranks_per_device,  # distinct GPUs (ranks sharing one GPU count once)
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(t_step * 1e3, 4),
