@@ -5,7 +5,8 @@
     scripts/mpirun -n 2 python benchmarks/alltoall_moe.py --mb 64      # ranks sharing one GPU
 
 Algorithms: ``direct`` (hand-written kernel: every rank pulls its block from
-all peers at once over xGMI), ``pairwise`` (reference myAlltoall2 schedule on
+all peers at once over xGMI), ``push`` (every rank writes its segments straight
+into the peers' outputs, the reference myAlltoall pattern), ``pairwise`` (reference myAlltoall2 schedule on
 RCCL send/recv rounds), ``rccl`` (ncclAllToAll, the library baseline).  Each is
 checked for exactness, then timed (median of --iters).  Prints one JSON line.
 """
@@ -40,7 +41,7 @@ blk = n // p
 ar = torch.arange(blk, device=dev.device, dtype=torch.float32) % 997
 for j in range(p):
     x[j * blk:(j + 1) * blk] = rank * 1e6 + j * 1e3 + ar
-algos = ["direct"] + ([] if dev.shared_device else ["pairwise", "rccl"])
+algos = ["direct", "push"] + ([] if dev.shared_device else ["pairwise", "rccl"])
 res = {}
 for algo in algos:
     try:
@@ -69,6 +70,7 @@ for algo in algos:
 if rank == 0:
     nbytes = n * 4
     out = {"bench": "alltoall_moe", "ranks": p, "bytes_per_rank": nbytes, "shared_gpu": dev.shared_device,
+           "hbm_bytes_all_ranks": 2 * p * nbytes,
            "results": {a: (None if t is None else {"ms": round(t * 1e3, 4),
                                                    "algbw_GBps": round(nbytes / t / 1e9, 2),
                                                    "busbw_GBps": round(nbytes / t / 1e9 * (p - 1) / p, 2)})

@@ -119,22 +119,22 @@ __device__ __forceinline__ void finish(const CollArgs& a, uint64_t e) {
 template <int DT> struct Elem;
 template <> struct Elem<DT_F32> { using A = float; static constexpr int B = 4;
   __device__ static A ld(Rsrc r, uint32_t o) { return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r.r, o, 0, kCachePolicySys)); }
-  __device__ static void st(Rsrc r, uint32_t o, A v) { __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r.r, o, 0, kCachePolicySys); } };
+  __device__ static void st(Rsrc r, uint32_t o, A v) { __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r.r, o, 0, kStorePolicy); } };
 template <> struct Elem<DT_I32> { using A = int32_t; static constexpr int B = 4;
   __device__ static A ld(Rsrc r, uint32_t o) { return (int32_t)__builtin_amdgcn_raw_buffer_load_b32(r.r, o, 0, kCachePolicySys); }
-  __device__ static void st(Rsrc r, uint32_t o, A v) { __builtin_amdgcn_raw_buffer_store_b32((uint32_t)v, r.r, o, 0, kCachePolicySys); } };
+  __device__ static void st(Rsrc r, uint32_t o, A v) { __builtin_amdgcn_raw_buffer_store_b32((uint32_t)v, r.r, o, 0, kStorePolicy); } };
 template <> struct Elem<DT_BF16> { using A = float; static constexpr int B = 2;
   __device__ static A ld(Rsrc r, uint32_t o) { return __uint_as_float((uint32_t)__builtin_amdgcn_raw_buffer_load_b16(r.r, o, 0, kCachePolicySys) << 16); }
-  __device__ static void st(Rsrc r, uint32_t o, A v) { __builtin_amdgcn_raw_buffer_store_b16((uint16_t)f32_to_bf16_bits(v), r.r, o, 0, kCachePolicySys); } };
+  __device__ static void st(Rsrc r, uint32_t o, A v) { __builtin_amdgcn_raw_buffer_store_b16((uint16_t)f32_to_bf16_bits(v), r.r, o, 0, kStorePolicy); } };
 template <> struct Elem<DT_F16> { using A = float; static constexpr int B = 2;
   __device__ static A ld(Rsrc r, uint32_t o) { return (float)__builtin_bit_cast(_Float16, (uint16_t)__builtin_amdgcn_raw_buffer_load_b16(r.r, o, 0, kCachePolicySys)); }
-  __device__ static void st(Rsrc r, uint32_t o, A v) { __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(uint16_t, (_Float16)v), r.r, o, 0, kCachePolicySys); } };
+  __device__ static void st(Rsrc r, uint32_t o, A v) { __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(uint16_t, (_Float16)v), r.r, o, 0, kStorePolicy); } };
 template <> struct Elem<DT_F64> { using A = double; static constexpr int B = 8;
   __device__ static A ld(Rsrc r, uint32_t o) { auto v = __builtin_amdgcn_raw_buffer_load_b64(r.r, o, 0, kCachePolicySys); return __hiloint2double((int)v[1], (int)v[0]); }
-  __device__ static void st(Rsrc r, uint32_t o, A v) { typedef unsigned u2 __attribute__((ext_vector_type(2))); u2 x; x[0] = (uint32_t)__double2loint(v); x[1] = (uint32_t)__double2hiint(v); __builtin_amdgcn_raw_buffer_store_b64(x, r.r, o, 0, kCachePolicySys); } };
+  __device__ static void st(Rsrc r, uint32_t o, A v) { typedef unsigned u2 __attribute__((ext_vector_type(2))); u2 x; x[0] = (uint32_t)__double2loint(v); x[1] = (uint32_t)__double2hiint(v); __builtin_amdgcn_raw_buffer_store_b64(x, r.r, o, 0, kStorePolicy); } };
 template <> struct Elem<DT_I64> { using A = int64_t; static constexpr int B = 8;
   __device__ static A ld(Rsrc r, uint32_t o) { auto v = __builtin_amdgcn_raw_buffer_load_b64(r.r, o, 0, kCachePolicySys); return (int64_t)(((uint64_t)v[1] << 32) | v[0]); }
-  __device__ static void st(Rsrc r, uint32_t o, A v) { typedef unsigned u2 __attribute__((ext_vector_type(2))); u2 x; x[0] = (uint32_t)v; x[1] = (uint32_t)((uint64_t)v >> 32); __builtin_amdgcn_raw_buffer_store_b64(x, r.r, o, 0, kCachePolicySys); } };
+  __device__ static void st(Rsrc r, uint32_t o, A v) { typedef unsigned u2 __attribute__((ext_vector_type(2))); u2 x; x[0] = (uint32_t)v; x[1] = (uint32_t)((uint64_t)v >> 32); __builtin_amdgcn_raw_buffer_store_b64(x, r.r, o, 0, kStorePolicy); } };
 
 // Reduce bytes [off, off+len) of every rank's buffer (codes[j]) into dst (local).
 // Vector part by all threads; element tail by thread 0.
@@ -218,7 +218,7 @@ __device__ void copy_span(const char* src, char* dst, uint64_t len) {
     Rsrc s = make_rsrc(const_cast<char*>(src) + vbytes, (uint32_t)tail);
     Rsrc d = make_rsrc(dst + vbytes, (uint32_t)tail);
     for (uint32_t o = 0; o < tail; ++o)
-      __builtin_amdgcn_raw_buffer_store_b8(__builtin_amdgcn_raw_buffer_load_b8(s.r, o, 0, kCachePolicySys), d.r, o, 0, kCachePolicySys);
+      __builtin_amdgcn_raw_buffer_store_b8(__builtin_amdgcn_raw_buffer_load_b8(s.r, o, 0, kCachePolicySys), d.r, o, 0, kStorePolicy);
   }
 }
 
@@ -262,7 +262,7 @@ __device__ void gather_spans(const char* const* srcs, char* const* dsts, int nr,
       Rsrc s = make_rsrc(const_cast<char*>(srcs[j]) + vbytes, (uint32_t)tail);
       Rsrc d = make_rsrc(dsts[j] + vbytes, (uint32_t)tail);
       for (uint32_t o = 0; o < tail; ++o)
-        __builtin_amdgcn_raw_buffer_store_b8(__builtin_amdgcn_raw_buffer_load_b8(s.r, o, 0, kCachePolicySys), d.r, o, 0, kCachePolicySys);
+        __builtin_amdgcn_raw_buffer_store_b8(__builtin_amdgcn_raw_buffer_load_b8(s.r, o, 0, kCachePolicySys), d.r, o, 0, kStorePolicy);
     }
   }
 }
@@ -599,8 +599,8 @@ __device__ void combine_span(const char* x, const char* y, char* o1, char* o2, u
     } else {
       for (uint32_t o = 0; o < tail; ++o) {
         const auto v = __builtin_amdgcn_raw_buffer_load_b8(rx.r, o, 0, kCachePolicySys);
-        __builtin_amdgcn_raw_buffer_store_b8(v, r1.r, o, 0, kCachePolicySys);
-        if (TWO) __builtin_amdgcn_raw_buffer_store_b8(v, r2.r, o, 0, kCachePolicySys);
+        __builtin_amdgcn_raw_buffer_store_b8(v, r1.r, o, 0, kStorePolicy);
+        if (TWO) __builtin_amdgcn_raw_buffer_store_b8(v, r2.r, o, 0, kStorePolicy);
       }
     }
   }

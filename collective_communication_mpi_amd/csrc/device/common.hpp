@@ -8,7 +8,8 @@
 //    peer produced in this launch, and every load of peer memory, is issued
 //    system-coherent (`sc0 sc1`, aux = 17) so no L1/L2 copy can go stale across
 //    calls; bytes we hand to peers are stored `sc0 sc1` (write-through) and
-//    followed by a system-scope release (`buffer_wbl2 sc0 sc1`) before the flag.
+//    published by a system-scope release (`buffer_wbl2 sc0 sc1` + vmcnt(0))
+//    before the flag.
 //  * flags live in uncached signal buffers (hipDeviceMallocUncached) and are
 //    written/polled with system-scope atomics; every spin is bounded by a
 //    wall-clock budget (s_memrealtime, 100 MHz) and reports a timeout code
@@ -43,6 +44,15 @@ constexpr int kMaxRanks = 16;     // ranks per device communicator
 constexpr int kMaxSegs = 64;      // registered symmetric segments (heap arenas) per rank
 constexpr int kMaxBlocks = 1024;  // max CTAs of one collective launch
 constexpr int kCachePolicySys = 17;  // aux bits: sc0 | sc1 (system coherent)
+// Stores of the collectives: sc0|sc1 write-through (aux 17), so bytes handed to a
+// peer leave the XCD's L2 as they are produced instead of in one write-back burst
+// at the release.  Measured against plain write-back stores (aux 0, compile with
+// -DCCMPI_STORE_POLICY=0): identical TCC WRITE_SIZE and 0-9 % faster at 8 ranks
+// (profiles/r2_coll/store_policy.md).  release_sys() is issued either way.
+#ifndef CCMPI_STORE_POLICY
+#define CCMPI_STORE_POLICY 17
+#endif
+constexpr int kStorePolicy = CCMPI_STORE_POLICY;
 constexpr uint64_t kStepsPerEpoch = 64;  // > 2 * (kMaxRanks - 1) signals per call
 
 inline size_t dtype_bytes(int dt) {
@@ -103,7 +113,7 @@ __device__ __forceinline__ u32x4 ld_sys16(const void* p) {
 }
 __device__ __forceinline__ void st_sys16(void* p, u32x4 v) {
   auto rs = __builtin_amdgcn_make_buffer_rsrc(p, 0, 16, 0x00020000);
-  __builtin_amdgcn_raw_buffer_store_b128(v, rs, 0, 0, kCachePolicySys);
+  __builtin_amdgcn_raw_buffer_store_b128(v, rs, 0, 0, kStorePolicy);
 }
 // Buffer-resource form: one descriptor per base, per-lane byte offsets (< 4 GiB).
 struct Rsrc {
@@ -116,7 +126,7 @@ __device__ __forceinline__ u32x4 ld16(Rsrc r, uint32_t off) {
   return __builtin_amdgcn_raw_buffer_load_b128(r.r, off, 0, kCachePolicySys);
 }
 __device__ __forceinline__ void st16(Rsrc r, uint32_t off, u32x4 v) {
-  __builtin_amdgcn_raw_buffer_store_b128(v, r.r, off, 0, kCachePolicySys);
+  __builtin_amdgcn_raw_buffer_store_b128(v, r.r, off, 0, kStorePolicy);
 }
 
 __device__ __forceinline__ uint64_t now_ticks() { return __builtin_amdgcn_s_memrealtime(); }  // 100 MHz
@@ -133,10 +143,11 @@ __device__ __forceinline__ uint64_t now_ticks() { return __builtin_amdgcn_s_memr
 // __syncthreads() before any other wave of the workgroup touches peer data;
 // the barrier orders those waves after the fence, and their loads are issued
 // system-coherent (sc0 sc1) as well, so they never hit a line the fence did
-// not cover.  The release side is `release_sys()` + the flag store: the
-// writer's data is written through (sc0 sc1), `buffer_wbl2 sc0 sc1` pushes
-// out anything an earlier kernel left dirty in its L2, and vmcnt(0) makes the
-// flag store the last one issued.
+// not cover.  The release side is `release_sys()` + the flag store: every
+// store of the workgroup has completed into its XCD's L2 (vmcnt(0) before the
+// barrier), `buffer_wbl2 sc0 sc1` writes that L2's dirty lines (this kernel's
+// and any earlier kernel's) back to memory, and vmcnt(0) orders the flag
+// store after the write-back.
 __device__ __forceinline__ bool wait_geq(const uint64_t* p, uint64_t want, uint64_t budget_ticks,
                                          uint32_t* err, uint32_t code) {
   uint64_t t0 = 0;
