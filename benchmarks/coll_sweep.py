@@ -57,7 +57,7 @@ maxb = args.max_mb << 20
 ALL_OPS = ["allreduce", "allgather", "reduce_scatter", "alltoall", "lastaxis"]
 ops = ALL_OPS if args.ops == "all" else args.ops.split(",")
 DEFAULT_ALGOS = {
-    "allreduce": ["oneshot", "twoshot", "push", "reduce_bcast", "ring", "rhd"],
+    "allreduce": ["ll", "oneshot", "twoshot", "push", "reduce_bcast", "ring", "rhd"],
     "allgather": ["direct"],
     "reduce_scatter": ["direct"],
     "alltoall": ["direct", "push"],
@@ -77,6 +77,7 @@ def hbm_model(op: str, algo: str, S: int) -> float:
     if op == "allreduce":
         return {
             "oneshot": p * p * S + p * S,            # everyone reads all p buffers, writes S
+            "ll": p * (S + 2 * p * S + 2 * p * S + S),  # read S, push 2pS (8 B per 4 B), poll 2pS, write S
             "twoshot": (2 * p - 1) * S + p * S,       # RS: read pS write S; AG: read (p-1)S write (p-1)S
             "push": 2 * p * S + 2 * p * S,            # scatter: read pS write pS; reduce+fan-out: same
             "reduce_bcast": (2 * p - 1) * S + p * S,  # root reads pS writes S; p-1 copies of S
@@ -176,6 +177,8 @@ for op in ops:
             failed = False
             while S <= maxb and not failed:
                 if op == "allreduce" and algo == "oneshot" and S > (64 << 20):
+                    break
+                if op == "allreduce" and algo == "ll" and S > dev.ll_max:
                     break
                 if op == "allreduce" and algo == "reduce_bcast" and S > (256 << 20):
                     break

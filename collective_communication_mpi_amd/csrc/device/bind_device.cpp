@@ -71,6 +71,7 @@ PYBIND11_MODULE(_device, m) {
   m.attr("ALGO_TWOSHOT_PUSH") = (int)ALGO_TWOSHOT_PUSH;
   m.attr("ALGO_RING") = (int)ALGO_RING;
   m.attr("ALGO_RHD") = (int)ALGO_RHD;
+  m.attr("ALGO_LL") = (int)ALGO_LL;
   m.attr("A2A_PULL") = (int)A2A_PULL;
   m.attr("A2A_PUSH") = (int)A2A_PUSH;
   m.attr("MAX_RINGS") = kMaxRings;
@@ -150,10 +151,14 @@ PYBIND11_MODULE(_device, m) {
       .def("poll_error", &DeviceComm::poll_error)
       .def("reset_state", &DeviceComm::reset_state, py::call_guard<py::gil_scoped_release>())
       .def("set_inbox", &DeviceComm::set_inbox)
+      .def("ll_alloc", [](DeviceComm& d, uint64_t max_bytes) { return py::bytes(d.ll_alloc(max_bytes)); })
+      .def("ll_connect", [](DeviceComm& d, const std::vector<std::string>& hs) { d.ll_connect(hs); })
+      .def_property_readonly("ll_max_bytes", &DeviceComm::ll_max_bytes)
       .def_property_readonly("inbox_bytes", &DeviceComm::inbox_bytes)
       .def("set_timeout_seconds", &DeviceComm::set_timeout_seconds)
       .def("set_copy_engine", &DeviceComm::set_copy_engine)
       .def("set_rings", &DeviceComm::set_rings)
+      .def("set_debug_stamps", &DeviceComm::set_debug_stamps)
       .def_property_readonly("rings", &DeviceComm::rings);
 
   register_ops(m);

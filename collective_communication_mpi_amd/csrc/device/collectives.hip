@@ -529,6 +529,102 @@ __global__ void __launch_bounds__(kThreads) k_move(CollArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// low-latency one-shot all-reduce (small messages)
+// ---------------------------------------------------------------------------
+// The flag travels with the data: every 4-byte payload word is pushed to every
+// peer as one naturally aligned 8-byte store (word, flag), single-copy atomic,
+// into the peer's LL buffer region [parity][my rank].  Each rank then polls its
+// own buffer until every unit of every source carries this call's flag and
+// reduces in rank order.  No start or end barrier: one write latency instead of
+// three flag round trips.  Buffer reuse is safe with two parities: a rank writes
+// call k+2's data into the parity it read in call k only after every peer has
+// pushed call k+1's data, i.e. finished reading call k.  The call epoch is one
+// device word shared by all CTAs (the last CTA to finish advances it), so the
+// parity does not depend on the grid and the kernel stays graph-capturable.
+// The LL buffers are uncached device memory (hipDeviceMallocUncached, like the
+// signal buffers): in coarse-grained memory a peer's 8-byte stores became
+// visible to the poller only after ~20 us per source (measured, 43 us for a
+// 4 KiB all-reduce at 2 ranks), with uncached memory after one write latency.
+template <int DT, int OP>
+__global__ void __launch_bounds__(kThreads) k_allreduce_ll(CollArgs a) {
+  const PeerTable* pt = a.pt;
+  const int me = pt->rank, p = pt->size;
+  __shared__ uint32_t s_e;
+  if (threadIdx.x == 0) s_e = __hip_atomic_load(&a.ll_state[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  const uint32_t E = s_e, flag = E + 1;
+  const uint64_t par = E & 1;
+  const uint64_t nvec = a.nbytes / 16;
+  const bool stamp = a.dbg && blockIdx.x == 0 && threadIdx.x == 0;
+  if (stamp) a.dbg[0] = now_ticks();
+  const BlockRange r = split_range(nvec, gridDim.x, blockIdx.x);
+  typedef unsigned u2 __attribute__((ext_vector_type(2)));
+  // push: 16 B of payload = four (word, flag) units = 32 B per peer
+  // descriptors from wave-uniform bases, per-lane byte offsets (a per-lane base
+  // would make the compiler waterfall every buffer instruction over the 64 lanes)
+  for (uint64_t v = r.lo + threadIdx.x; v < r.hi; v += kThreads) {
+    const u32x4 x = *reinterpret_cast<const u32x4*>(a.in + v * 16);
+    for (int j = 0; j < p; ++j) {
+      const Rsrc rd = make_rsrc(uniform_ptr(pt->ll[j] + (par * p + me) * a.ll_slot), (uint32_t)a.ll_slot);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        u2 w;
+        w[0] = x[i];
+        w[1] = flag;
+        __builtin_amdgcn_raw_buffer_store_b64(w, rd.r, (uint32_t)(v * 32 + 8 * i), 0, kStorePolicy);
+      }
+    }
+  }
+  if (stamp) a.dbg[1] = now_ticks();
+  // poll + reduce (rank order): my LL buffer holds every source's units
+  const char* mine = pt->ll[me];
+  bool ok = true;
+  for (uint64_t v = r.lo + threadIdx.x; v < r.hi && ok; v += kThreads) {
+    VecAcc<DT> acc;
+    for (int j = 0; j < p && ok; ++j) {
+      const Rsrc rs = make_rsrc(uniform_ptr(const_cast<char*>(mine) + (par * p + j) * a.ll_slot), (uint32_t)a.ll_slot);
+      u32x4 x;
+      uint64_t t0 = 0;
+      uint32_t spins = 0;
+      for (;;) {
+        bool ready = true;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const u2 w = __builtin_amdgcn_raw_buffer_load_b64(rs.r, (uint32_t)(v * 32 + 8 * i), 0, kCachePolicySys);
+          x[i] = w[0];
+          ready = ready && (w[1] == flag);
+        }
+        if (ready) break;
+        if ((++spins & 63) == 0) {
+          const uint64_t t = now_ticks();
+          if (t0 == 0) t0 = t;
+          else if (t - t0 > a.timeout_ticks) {
+            __hip_atomic_store(&pt->sig[me]->error, 0x900u + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            report_host(pt, 0x900 + j);
+            ok = false;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+      }
+      if (j == 0) acc.load(x);
+      else acc.template acc<OP>(x);
+      if (stamp && j < 14) a.dbg[2 + j] = now_ticks();
+    }
+    if (ok) *reinterpret_cast<u32x4*>(a.out + v * 16) = acc.store();
+  }
+  // the last CTA out advances the call epoch (visible to the next kernel on the stream)
+  if (stamp) a.dbg[16] = now_ticks();
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if (__hip_atomic_fetch_add(&a.ll_state[1], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1) {
+      __hip_atomic_store(&a.ll_state[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&a.ll_state[0], E + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // pipelined schedules: ring and recursive halving/doubling
 // ---------------------------------------------------------------------------
 // Both push: every byte that crosses to a peer is a posted remote store into
@@ -914,6 +1010,7 @@ void launch_allreduce(int algo, const CollArgs& a, int nranks, int dtype, int op
         case ALGO_TWOSHOT_PUSH: hipLaunchKernelGGL((k_allreduce_twoshot_push<D, O, R>), dim3(grid), dim3(kThreads), 0, s, a); break;
         case ALGO_RING: hipLaunchKernelGGL((k_allreduce_ring<D, O>), dim3(grid), dim3(kThreads), 0, s, a); break;
         case ALGO_RHD: hipLaunchKernelGGL((k_allreduce_rhd<D, O>), dim3(grid), dim3(kThreads), 0, s, a); break;
+        case ALGO_LL: hipLaunchKernelGGL((k_allreduce_ll<D, O>), dim3(grid), dim3(kThreads), 0, s, a); break;
         default: throw std::invalid_argument("ccmpi: bad allreduce algo");
       }
     });

@@ -16,6 +16,7 @@ enum AllreduceAlgo : int {
   ALGO_TWOSHOT_PUSH = 3,  // two-shot with remote writes (scatter into peers' inboxes, push results)
   ALGO_RING = 4,          // pipelined ring RS + AG with peer writes, several rings (coprime strides)
   ALGO_RHD = 5,           // recursive halving (RS) + doubling (AG) with peer writes, p = 2^k
+  ALGO_LL = 6,            // low-latency one-shot: (data, flag) 8-B units pushed to every peer, no barriers
 };
 
 enum MoveMode : int {
@@ -46,6 +47,9 @@ struct CollArgs {
   uint64_t inbox_slot;     // ring / rhd: bytes per inbox chunk slot (>= the largest chunk, 16-B multiple)
   int8_t ring_stride[kMaxRings];  // ring k: i -> i + stride (coprime to p)
   int8_t ring_inv[kMaxRings];     // stride^-1 mod p: position of rank r in ring k = r * inv % p
+  uint32_t* ll_state;      // LL all-reduce: [0] call epoch, [1] finished-CTA count (device, local)
+  uint64_t ll_slot;        // LL all-reduce: bytes of one (parity, source) region of the LL buffer
+  uint64_t* dbg;           // optional: per-phase s_memrealtime stamps of CTA 0 / thread 0 (diagnostics)
 };
 
 struct LocalReduceArgs {

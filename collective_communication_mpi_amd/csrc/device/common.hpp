@@ -85,6 +85,7 @@ struct PeerTable {
   Signals* sig[kMaxRanks];               // sig[j]: rank j's signal buffer (mapped)
   char* seg[kMaxRanks][kMaxSegs];        // seg[j][s]: base of rank j's segment s
   uint64_t seg_bytes[kMaxSegs];
+  char* ll[kMaxRanks];                    // ll[j]: rank j's LL buffer (uncached, mapped; null until set up)
   uint32_t* host_err;                    // pinned host word mirroring sig[rank]->error (watchdog)
   int rank;
   int size;

@@ -86,6 +86,8 @@ DeviceComm::DeviceComm(int rank, int size, int device, uint64_t /*scratch_bytes*
   CCMPI_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&epochs_), sizeof(uint64_t) * kMaxBlocks));
   CCMPI_HIP_CHECK(hipMemset(epochs_, 0, sizeof(uint64_t) * kMaxBlocks));
   CCMPI_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&dev_pt_), sizeof(PeerTable)));
+  CCMPI_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&ll_state_), 2 * sizeof(uint32_t)));
+  CCMPI_HIP_CHECK(hipMemset(ll_state_, 0, 2 * sizeof(uint32_t)));
   std::memset(&host_pt_, 0, sizeof(host_pt_));
   host_pt_.rank = rank;
   host_pt_.size = size;
@@ -113,6 +115,8 @@ DeviceComm::~DeviceComm() {
   if (sig_) (void)hipFree(sig_);
   if (epochs_) (void)hipFree(epochs_);
   if (dev_pt_) (void)hipFree(dev_pt_);
+  if (ll_state_) (void)hipFree(ll_state_);
+  if (ll_buf_) (void)hipFree(ll_buf_);
   if (host_err_) (void)hipHostFree(host_err_);
 }
 
@@ -225,6 +229,14 @@ void DeviceComm::allreduce(uint64_t in, uint64_t out, uint64_t count, int dtype,
     }
     return;
   }
+  if (algo == ALGO_LL) {
+    // global decision (sizes and the LL setup are identical on every rank)
+    if (ll_ready_ && nbytes % 16 == 0 && nbytes <= ll_max_) {
+      allreduce_ll_(in, out, nbytes, dtype, op, st, max_blocks);
+      return;
+    }
+    algo = ALGO_ONESHOT;
+  }
   if (algo == ALGO_RING || algo == ALGO_RHD) {
     allreduce_pipelined_(algo, in, out, nbytes, es, dtype, op, st, max_blocks, symmetric);
     return;
@@ -274,6 +286,59 @@ void DeviceComm::allreduce(uint64_t in, uint64_t out, uint64_t count, int dtype,
     launch_allreduce(algo, args_(sc, rc, outp, n, 0), size_, dtype, op, grid_(work, max_blocks), st);
     if (!out_ok) CCMPI_HIP_CHECK(hipMemcpyAsync((void*)(out + off), stage + chunk, n, hipMemcpyDeviceToDevice, st));
   }
+}
+
+void DeviceComm::allreduce_ll_(uint64_t in, uint64_t out, uint64_t nbytes, int dtype, int op, hipStream_t st,
+                               int max_blocks) {
+  // misaligned local buffers go through the scratch segment (local copies only:
+  // the protocol is the same on every rank)
+  const char* inp = reinterpret_cast<const char*>(in);
+  char* outp = reinterpret_cast<char*>(out);
+  char* stage = reinterpret_cast<char*>(scratch_ptr());
+  if (in % 16) {
+    CCMPI_HIP_CHECK(hipMemcpyAsync(stage, inp, nbytes, hipMemcpyDeviceToDevice, st));
+    inp = stage;
+  }
+  const bool out_staged = out % 16 != 0;
+  if (out_staged) outp = stage + scratch_bytes() / 2 / 16 * 16;
+  CollArgs a = args_(0, 0, outp, nbytes, 0);
+  a.in = inp;
+  a.ll_state = ll_state_;
+  a.dbg = dbg_;
+  a.ll_slot = 2 * ll_max_;
+  const uint64_t nvec = nbytes / 16;
+  int g = (int)std::min<uint64_t>((nvec + 255) / 256, (uint64_t)std::max(1, std::min(max_blocks, kMaxBlocks)));
+  launch_allreduce(ALGO_LL, a, size_, dtype, op, std::max(g, 1), st);
+  if (out_staged) CCMPI_HIP_CHECK(hipMemcpyAsync((void*)out, outp, nbytes, hipMemcpyDeviceToDevice, st));
+}
+
+std::string DeviceComm::ll_alloc(uint64_t max_bytes) {
+  if (ll_buf_) throw std::runtime_error("ccmpi: LL buffers already allocated");
+  if (max_bytes == 0 || max_bytes % 16) throw std::invalid_argument("ccmpi: LL max bytes must be a positive multiple of 16");
+  CCMPI_HIP_CHECK(hipSetDevice(device_));
+  const uint64_t bytes = 2ull * size_ * 2 * max_bytes;
+  CCMPI_HIP_CHECK(hipExtMallocWithFlags(reinterpret_cast<void**>(&ll_buf_), bytes, hipDeviceMallocUncached));
+  CCMPI_HIP_CHECK(hipMemset(ll_buf_, 0, bytes));
+  CCMPI_HIP_CHECK(hipDeviceSynchronize());
+  ll_max_ = max_bytes;
+  hipIpcMemHandle_t h;
+  CCMPI_HIP_CHECK(hipIpcGetMemHandle(&h, ll_buf_));
+  return std::string(reinterpret_cast<const char*>(&h), sizeof(h));
+}
+
+void DeviceComm::ll_connect(const std::vector<std::string>& handles) {
+  if (!ll_buf_ || (int)handles.size() != size_) throw std::invalid_argument("ccmpi: ll_connect needs ll_alloc and one handle per rank");
+  CCMPI_HIP_CHECK(hipSetDevice(device_));
+  for (int j = 0; j < size_; ++j) {
+    if (j == rank_) {
+      host_pt_.ll[j] = ll_buf_;
+      continue;
+    }
+    host_pt_.ll[j] = static_cast<char*>(ipc_open(handles[j]));
+    opened_.push_back(handles[j]);
+  }
+  sync_table_();
+  ll_ready_ = true;
 }
 
 namespace {
@@ -801,6 +866,8 @@ void DeviceComm::reset_state() {
   CCMPI_HIP_CHECK(hipDeviceSynchronize());
   CCMPI_HIP_CHECK(hipMemset(sig_, 0, sizeof(Signals)));
   CCMPI_HIP_CHECK(hipMemset(epochs_, 0, sizeof(uint64_t) * kMaxBlocks));
+  CCMPI_HIP_CHECK(hipMemset(ll_state_, 0, 2 * sizeof(uint32_t)));
+  if (ll_buf_) CCMPI_HIP_CHECK(hipMemset(ll_buf_, 0, 2ull * size_ * 2 * ll_max_));
   CCMPI_HIP_CHECK(hipDeviceSynchronize());
   __atomic_store_n(host_err_, 0u, __ATOMIC_RELEASE);
 }

@@ -106,18 +106,26 @@ class DeviceComm {
   void reset_state();
   // symmetric inbox for the push two-shot all-reduce (>= p shards)
   void set_inbox(uint64_t ptr, uint64_t bytes);
+  // LL (low-latency) all-reduce buffers: 2 parities x p sources x (2 * max_bytes)
+  // of uncached device memory per rank.  ll_alloc returns this rank's IPC handle;
+  // ll_connect maps every peer's (collective bootstrap by the Python layer).
+  std::string ll_alloc(uint64_t max_bytes);
+  void ll_connect(const std::vector<std::string>& handles);
+  uint64_t ll_max_bytes() const { return ll_ready_ ? ll_max_ : 0; }
   uint64_t inbox_bytes() const { return inbox_bytes_; }
   uint64_t timeout_ticks() const { return timeout_ticks_; }
   void set_timeout_seconds(double s) { timeout_ticks_ = (uint64_t)(s * 1e8); }
   void set_copy_engine(bool on) { copy_engine_ = on; }
   // concurrent rings of the ring all-reduce (coprime strides, at most kMaxRings)
   void set_rings(int r) { rings_ = std::max(1, r); }
+  void set_debug_stamps(uint64_t ptr) { dbg_ = reinterpret_cast<uint64_t*>(ptr); }  // LL kernel phase stamps
   int rings() const { return rings_; }
   // inbox bytes per chunk slot of the ring / rhd all-reduce of `nbytes` over p ranks
   static uint64_t ring_slot_bytes(uint64_t nbytes, int p);
 
  private:
   void sync_table_();
+  void allreduce_ll_(uint64_t in, uint64_t out, uint64_t nbytes, int dtype, int op, hipStream_t st, int max_blocks);
   void allreduce_pipelined_(int algo, uint64_t in, uint64_t out, uint64_t nbytes, uint64_t es, int dtype, int op,
                             hipStream_t st, int max_blocks, bool symmetric);
   CollArgs args_(uint64_t src_code, uint64_t res_code, char* out, uint64_t nbytes, int root) const;
@@ -139,7 +147,12 @@ class DeviceComm {
   uint64_t timeout_ticks_ = 2000000000ull;  // 20 s
   ncclComm_t nccl_ = nullptr;
   uint64_t inbox_ptr_ = 0, inbox_bytes_ = 0;
+  uint64_t ll_max_ = 0;
+  char* ll_buf_ = nullptr;                // mine (uncached)
+  bool ll_ready_ = false;
+  uint32_t* ll_state_ = nullptr;          // [epoch, finished CTAs] of the LL kernel
   int rings_ = 1;
+  uint64_t* dbg_ = nullptr;
   bool copy_engine_ = false;              // single-rank copies: contiguous-slice kernel (3.2 vs 2.6 TB/s for the runtime blit)
   std::vector<std::string> opened_;      // handles we opened (for release)
 };

@@ -9,6 +9,8 @@ order with surrounding torch work and can be captured in a HIP graph.
 Algorithms (``algo=``):
 
 =================  ============================================================
+``ll``             low-latency one-shot: (word, flag) 8-B units pushed to every
+                   peer, no barriers (messages up to ``CCMPI_LL_MAX_BYTES``)
 ``oneshot``        every rank pulls all peers' buffers and reduces (latency)
 ``twoshot``        reduce-scatter + all-gather, all peers in flight (bandwidth)
 ``reduce_bcast``   the reference myAllreduce algorithm (mpi_wrapper/comm.py:63)
@@ -40,7 +42,7 @@ from .utils.trace import trace_call
 _OPS = {"SUM": 0, "PROD": 1, "MIN": 2, "MAX": 3}
 # hand-written all-reduce algorithms -> native algorithm codes
 _HAND_ALGOS = {"oneshot": "ALGO_ONESHOT", "twoshot": "ALGO_TWOSHOT", "reduce_bcast": "ALGO_REDUCE_BCAST",
-               "push": "ALGO_TWOSHOT_PUSH", "ring": "ALGO_RING", "rhd": "ALGO_RHD"}
+               "push": "ALGO_TWOSHOT_PUSH", "ring": "ALGO_RING", "rhd": "ALGO_RHD", "ll": "ALGO_LL"}
 
 
 def op_code(op) -> int:
@@ -122,6 +124,8 @@ class DeviceGroup:
         assert seg == 0, "scratch must be segment 0"
         self._rccl = False
         self.oneshot_max = _env_int("CCMPI_ONESHOT_MAX_BYTES", 256 << 10)
+        self.ll_max = (_env_int("CCMPI_LL_MAX_BYTES", 512 << 10) + 15) // 16 * 16
+        self.ll_auto_max = min(self.ll_max, _env_int("CCMPI_LL_AUTO_MAX_BYTES", 64 << 10))
         # concurrent rings of algo="ring": every stride coprime to p, up to 4 (p = 8: strides
         # 1, 3, 5, 7 -> 4 links per direction); CCMPI_RINGS overrides
         coprime = [k for k in range(1, self.size) if _gcd(k, self.size) == 1] or [1]
@@ -228,6 +232,15 @@ class DeviceGroup:
         seg, _ = self.dc.find(t.data_ptr(), t.numel() * t.element_size())
         return seg > 0
 
+    def _ensure_ll(self) -> None:
+        """Collective on first use: every rank allocates its uncached LL buffer
+        (2 parities x p sources x 2 x ``ll_max`` bytes; 16 MiB at p = 8) and maps
+        every peer's through IPC."""
+        if self.dc.ll_max_bytes:
+            return
+        h = bytes(self.dc.ll_alloc(self.ll_max))
+        self.dc.ll_connect([bytes(x) for x in self.host.allgather(h)])
+
     def _ensure_inbox(self, nbytes: int) -> None:
         """Collective (all ranks call with the same size): symmetric inbox of
         p shards for the push two-shot all-reduce (p - 1 chunk slots for the
@@ -302,6 +315,10 @@ class DeviceGroup:
         forced = os.environ.get("CCMPI_ALLREDUCE_ALGO")
         if forced:
             return forced
+        if nbytes <= self.ll_auto_max and nbytes % 16 == 0:
+            # in-kernel latency (rocprofv3, 2 ranks): 6.0 us vs 10.2 us one-shot at 4 KiB,
+            # 7.1 vs 12.8 us at 64 KiB (profiles/r2_coll/ll_latency.md)
+            return "ll"
         return "oneshot" if nbytes <= self.oneshot_max else "twoshot"
 
     # ------------------------------------------------------------- collectives
@@ -323,6 +340,8 @@ class DeviceGroup:
         s = self._stream()
         if algo in ("push", "ring", "rhd"):
             self._ensure_inbox(nbytes)
+        if algo == "ll":
+            self._ensure_ll()
         if algo == "ring":
             self.dc.set_rings(rings or self.default_rings)
         if algo in _HAND_ALGOS:

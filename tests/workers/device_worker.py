@@ -54,7 +54,7 @@ torch.cuda.synchronize()
 fails = []
 ncheck = 0
 POW2 = p & (p - 1) == 0
-AR_ALGOS = ["oneshot", "twoshot", "push", "reduce_bcast", "ring"] + (["rhd"] if POW2 else [])
+AR_ALGOS = ["oneshot", "twoshot", "push", "reduce_bcast", "ring", "ll"] + (["rhd"] if POW2 else [])
 WIDE = lambda dt: torch.float64 if dt.is_floating_point else torch.int64  # noqa: E731
 
 
@@ -193,11 +193,11 @@ if args.stress or args.fault:
 ALL_DT = [torch.float32, torch.bfloat16, torch.float16, torch.float64, torch.int32, torch.int64]
 ALL_OPS = ["SUM", "PROD", "MIN", "MAX"]
 if args.matrix == "quick":
-    sizes, dtypes, ops = [1, 7, 1000, 65536 + 3], [torch.float32, torch.bfloat16], ["SUM"]
+    sizes, dtypes, ops = [1, 7, 1000, 65536 + 3, 1 << 17], [torch.float32, torch.bfloat16], ["SUM"]
 elif args.matrix == "wide":
     sizes, dtypes, ops = [1, 1000, 65536 + 3, (1 << 20) + 3], ALL_DT, ALL_OPS
 elif args.matrix == "full":
-    sizes, dtypes, ops = [1, 3, 8, 1000, 4097, 65536 + 3, 1 << 20, (1 << 22) + 5], ALL_DT, ALL_OPS
+    sizes, dtypes, ops = [1, 3, 8, 1000, 4097, 65536 + 3, 1 << 17, 1 << 20, (1 << 22) + 5], ALL_DT, ALL_OPS
 else:
     sizes, dtypes, ops = [], [], []
 if args.sizes:
