@@ -469,7 +469,7 @@ class DeviceGroup:
         torch = self.torch
         dtype = dtype or torch.float32
         if not algos:
-            algos = ["oneshot", "twoshot"] + ([] if self.shared_device else ["rccl"])
+            algos = ["ll", "oneshot", "twoshot"] + ([] if self.shared_device else ["rccl"])
         es = torch.empty((), dtype=dtype).element_size()
         x = self.empty(max_bytes // es, dtype)
         y = self.empty(max_bytes // es, dtype)
@@ -481,6 +481,8 @@ class DeviceGroup:
             best, best_t = None, None
             for algo in algos:
                 if algo == "oneshot" and b > (16 << 20):
+                    continue
+                if algo == "ll" and (b > self.ll_max or b % 16):
                     continue
                 ok = 1
                 try:
