@@ -40,6 +40,8 @@ from . import _native
 from .utils.trace import trace_call
 
 _OPS = {"SUM": 0, "PROD": 1, "MIN": 2, "MAX": 3}
+# all-reduce algorithms whose summation order is not rank order 0..p-1
+_UNORDERED = ("ring", "rhd", "rccl", "ring_rccl", "rhd_rccl")
 # hand-written all-reduce algorithms -> native algorithm codes
 _HAND_ALGOS = {"oneshot": "ALGO_ONESHOT", "twoshot": "ALGO_TWOSHOT", "reduce_bcast": "ALGO_REDUCE_BCAST",
                "push": "ALGO_TWOSHOT_PUSH", "ring": "ALGO_RING", "rhd": "ALGO_RHD", "ll": "ALGO_LL"}
@@ -125,7 +127,14 @@ class DeviceGroup:
         self._rccl = False
         self.oneshot_max = _env_int("CCMPI_ONESHOT_MAX_BYTES", 256 << 10)
         self.ll_max = (_env_int("CCMPI_LL_MAX_BYTES", 512 << 10) + 15) // 16 * 16
-        self.ll_auto_max = min(self.ll_max, _env_int("CCMPI_LL_AUTO_MAX_BYTES", 64 << 10))
+        # LL pushes 2 x the payload to each of the p-1 peers: up to 256 KiB at 2 ranks,
+        # 64 KiB beyond (profiles/r2_coll/ll_latency.md, small_p*.jsonl)
+        self.ll_auto_max = min(self.ll_max, _env_int("CCMPI_LL_AUTO_MAX_BYTES", (256 << 10) if self.size <= 2 else (64 << 10)))
+        # deterministic mode: only algorithms that reduce in rank order
+        # 0..p-1 (bitwise identical on every rank and to a sequential fp32 sum in rank
+        # order, like the reference's root loop, comm.py:85-93); ring / rhd / RCCL are
+        # replaced by the two-shot kernel
+        self.deterministic = os.environ.get("CCMPI_DETERMINISTIC", "0") not in ("0", "")
         # concurrent rings of algo="ring": every stride coprime to p, up to 4 (p = 8: strides
         # 1, 3, 5, 7 -> 4 links per direction); CCMPI_RINGS overrides
         coprime = [k for k in range(1, self.size) if _gcd(k, self.size) == 1] or [1]
@@ -334,6 +343,8 @@ class DeviceGroup:
         nbytes = src.numel() * src.element_size()
         if algo == "auto":
             algo = self.pick_allreduce(nbytes)
+        if self.deterministic and algo.split(":")[0] in _UNORDERED:
+            algo = "twoshot"
         if ":" in algo:  # "twoshot:512" = algorithm with an explicit CTA budget
             algo, mb = algo.split(":", 1)
             max_blocks = int(mb)

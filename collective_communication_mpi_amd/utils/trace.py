@@ -104,6 +104,8 @@ def trace_call(op: str):
             src = args[0]
             nbytes = src.numel() * src.element_size()
             algo = bound.arguments.get("algo", "default")
+            if op == "allreduce" and algo == "auto":  # record the algorithm actually chosen
+                algo = f"auto->{self.pick_allreduce(nbytes)}"
             tok = TRACE.begin(op, str(algo), nbytes, self.size, self.torch.cuda.current_stream(self.device))
             try:
                 return fn(self, *args, **kw)

@@ -211,6 +211,46 @@ def sym_copy(t):
     return s_
 
 
+def determinism():
+    """Rank-ordered algorithms (oneshot, twoshot, push, reduce_bcast, ll) give results
+    that are bitwise identical to each other and to a sequential fp32 sum in rank order
+    (bf16: fp32 accumulation, one rounding) -- the reference's root loop order
+    (comm.py:85-93).  Checked in-place too, and through CCMPI_DETERMINISTIC's mapping."""
+    ordered = ["oneshot", "twoshot", "push", "reduce_bcast", "ll"]
+    for dt in (torch.float32, torch.bfloat16):
+        for n in (1000, 4096, 65536):
+            xs = [gen(r, n, dt, 777000 + n) for r in range(p)]
+            acc = xs[0].float().cpu()
+            for x in xs[1:]:
+                acc = acc + x.float().cpu()  # sequential fp32 adds, rank order
+            want = acc.to(dt)
+            sym_x = dev.empty(n, dt)
+            for algo in ordered:
+                sym_x.copy_(xs[rank])
+                y = dev.empty(n, dt)
+                dev.allreduce(sym_x, y, "SUM", algo)
+                if not torch.equal(y.cpu(), want):
+                    fails.append(f"determinism[{algo},{dt},n={n}]: not bitwise equal to the rank-order fp32 sum")
+                global ncheck
+                ncheck += 1
+    old = dev.deterministic
+    dev.deterministic = True
+    try:
+        x = gen(rank, 4096, torch.float32, 778001)
+        y = torch.empty_like(x)
+        dev.allreduce(x, y, "SUM", "ring")  # mapped to the rank-ordered two-shot
+        acc = gen(0, 4096, torch.float32, 778001).cpu()
+        for r in range(1, p):
+            acc = acc + gen(r, 4096, torch.float32, 778001).cpu()
+        if not torch.equal(y.cpu(), acc):
+            fails.append("deterministic mode: ring not mapped to a rank-ordered algorithm")
+    finally:
+        dev.deterministic = old
+
+
+if args.matrix:
+    determinism()
+
 # ---------------------------------------------------------------- all-reduce
 for sym in (False, True):
     for n in sizes:
