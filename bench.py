@@ -16,7 +16,8 @@ Metric (BASELINE.json): "all-reduce algbw (GB/s) @1GiB fp32 + DP4xTP2 fwd step t
 * The algorithm is picked once per run, like RCCL's tuner does.  Every
   candidate runs once and is checked for an exact result (rank-valued inputs,
   so fp32 sums are exact) before it is timed: RCCL (the library baseline), the
-  hand-written two-shot over IPC-mapped xGMI peer memory at two CTA budgets,
+  hand-written two-shot and fan-out two-shot over IPC-mapped xGMI peer memory
+  at two CTA budgets,
   the push two-shot, the hand-written multi-ring and recursive
   halving/doubling kernels.  Every candidate's time is reported.
 * Secondary (BASELINE configs 2-5):
@@ -158,7 +159,7 @@ def main() -> int:
             return ["twoshot"]  # single rank: the all-reduce is a device copy
         if args.algo != "auto":
             return [args.algo]
-        hand = ["twoshot:256", "twoshot:512", "push:512", "ring", "rhd" if world & (world - 1) == 0 else None]
+        hand = ["twoshot:256", "twoshot:512", "fanout:256", "fanout:512", "push:512", "ring", "rhd" if world & (world - 1) == 0 else None]
         hand = [a for a in hand if a]
         # RCCL first (the library baseline); it refuses ranks that share a GPU
         return hand if dev.shared_device else ["rccl"] + hand

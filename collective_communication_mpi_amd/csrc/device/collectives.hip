@@ -136,12 +136,15 @@ template <> struct Elem<DT_I64> { using A = int64_t; static constexpr int B = 8;
   __device__ static A ld(Rsrc r, uint32_t o) { auto v = __builtin_amdgcn_raw_buffer_load_b64(r.r, o, 0, kCachePolicySys); return (int64_t)(((uint64_t)v[1] << 32) | v[0]); }
   __device__ static void st(Rsrc r, uint32_t o, A v) { typedef unsigned u2 __attribute__((ext_vector_type(2))); u2 x; x[0] = (uint32_t)v; x[1] = (uint32_t)((uint64_t)v >> 32); __builtin_amdgcn_raw_buffer_store_b64(x, r.r, o, 0, kStorePolicy); } };
 
-// Reduce bytes [off, off+len) of every rank's buffer (codes[j]) into dst (local).
-// Vector part by all threads; element tail by thread 0.
-template <int DT, int OP, int NRM>
-__device__ void reduce_span(const PeerTable* pt, const uint64_t* codes, uint64_t off, uint64_t len,
-                            uint64_t total_bytes, char* dst) {
+// Reduce bytes [off, off+len) of every rank's buffer (codes[j]) and store the
+// result into outs[0] (FAN = false, local) or into every outs[j], j < size
+// (FAN = true: local + peer-mapped outputs, the all-gather done as posted
+// writes).  Vector part by all threads; element tail by thread 0.
+template <int DT, int OP, int NRM, bool FAN>
+__device__ void reduce_span_to(const PeerTable* pt, const uint64_t* codes, uint64_t off, uint64_t len,
+                               char* const* outs) {
   const int nr = pt->size;
+  const int nout = FAN ? nr : 1;
   const uint64_t vbytes = len & ~15ull;
   // process in windows of < 2 GiB so 32-bit voffsets suffice
   const uint64_t kWin = 1ull << 30;
@@ -151,7 +154,10 @@ __device__ void reduce_span(const PeerTable* pt, const uint64_t* codes, uint64_t
 #pragma unroll
     for (int j = 0; j < NRM; ++j)
       if (j < nr) src[j] = make_rsrc(uniform_ptr(resolve(pt, j, codes[j]) + off + w), wl);
-    Rsrc out = make_rsrc(uniform_ptr(dst + w), wl);
+    Rsrc out[FAN ? NRM : 1];
+#pragma unroll
+    for (int j = 0; j < (FAN ? NRM : 1); ++j)
+      if (j < nout) out[j] = make_rsrc(uniform_ptr(outs[j] + w), wl);
     const uint32_t nv = wl / 16;
     for (uint32_t v = threadIdx.x; v < nv; v += kThreads * kUnroll) {
       VecAcc<DT> acc[kUnroll];
@@ -174,7 +180,10 @@ __device__ void reduce_span(const PeerTable* pt, const uint64_t* codes, uint64_t
 #pragma unroll
           for (int j = 1; j < NRM; ++j)
             if (j < nr) acc[u].template acc<OP>(x[u][j]);
-          st16(out, vv * 16, acc[u].store());
+          const u32x4 r = acc[u].store();
+#pragma unroll
+          for (int j = 0; j < (FAN ? NRM : 1); ++j)
+            if (j < nout) st16(out[j], vv * 16, r);
         }
       }
     }
@@ -182,15 +191,20 @@ __device__ void reduce_span(const PeerTable* pt, const uint64_t* codes, uint64_t
   const uint64_t tail = len - vbytes;
   if (tail && threadIdx.x == 0) {
     using E = Elem<DT>;
-    char* base0 = dst + vbytes;
-    Rsrc out = make_rsrc(base0, (uint32_t)tail);
     for (uint32_t o = 0; o < tail; o += E::B) {
       typename E::A acc = E::ld(make_rsrc(resolve(pt, 0, codes[0]) + off + vbytes, (uint32_t)tail), o);
       for (int j = 1; j < nr; ++j)
         acc = apply_op<OP>(acc, E::ld(make_rsrc(resolve(pt, j, codes[j]) + off + vbytes, (uint32_t)tail), o));
-      E::st(out, o, acc);
+      for (int j = 0; j < nout; ++j) E::st(make_rsrc(outs[j] + vbytes, (uint32_t)tail), o, acc);
     }
   }
+}
+
+template <int DT, int OP, int NRM>
+__device__ __forceinline__ void reduce_span(const PeerTable* pt, const uint64_t* codes, uint64_t off, uint64_t len,
+                                            uint64_t total_bytes, char* dst) {
+  char* const outs[1] = {dst};
+  reduce_span_to<DT, OP, NRM, false>(pt, codes, off, len, outs);
   (void)total_bytes;
 }
 
@@ -394,6 +408,34 @@ __global__ void __launch_bounds__(kThreads) k_allreduce_twoshot(CollArgs a) {
   finish(a, e);
 }
 
+
+// Fan-out two-shot: one phase.  Rank r pulls shard r's slice from every rank
+// (reads, rank order), reduces it and stores the result straight into EVERY
+// rank's result buffer (codes[1][j], local + posted peer writes): the
+// all-gather rides on the reduce-scatter's stores, so there is no middle
+// barrier and no second read of the shards.  HBM traffic per rank: S read +
+// S written (pull two-shot: S read + S/p written, then S read + S written
+// again for the all-gather).  In place is safe: only rank r reads or writes
+// region r of any buffer, and each CTA reads its slice before it writes it.
+template <int DT, int OP, int NRM>
+__global__ void __launch_bounds__(kThreads) k_allreduce_twoshot_fanout(CollArgs a) {
+  __shared__ uint64_t s_epoch;
+  __shared__ uint64_t codes[2][kMaxRanks];
+  if (!start_phase(a, &s_epoch, codes)) return;
+  const uint64_t e = s_epoch;
+  const PeerTable* pt = a.pt;
+  const int me = pt->rank, nr = pt->size;
+  BlockRange mys = part16(a.nbytes, nr, me);
+  BlockRange sub = part16(mys.hi - mys.lo, gridDim.x, blockIdx.x);
+  if (sub.hi > sub.lo) {
+    __shared__ char* outs[kMaxRanks];
+    if (threadIdx.x < nr) outs[threadIdx.x] = resolve(pt, threadIdx.x, codes[1][threadIdx.x]) + mys.lo + sub.lo;
+    __syncthreads();
+    reduce_span_to<DT, OP, NRM, true>(pt, codes[0], mys.lo + sub.lo, sub.hi - sub.lo, outs);
+  }
+  if (!sync_phase(a, 3, e)) return;
+  finish(a, e);
+}
 
 // Push two-shot: phase 1 writes my slice of shard j into rank j's inbox slot
 // [me] (remote 16-B sc0|sc1 stores: posted writes, no round trip); after the
@@ -1011,6 +1053,7 @@ void launch_allreduce(int algo, const CollArgs& a, int nranks, int dtype, int op
         case ALGO_RING: hipLaunchKernelGGL((k_allreduce_ring<D, O>), dim3(grid), dim3(kThreads), 0, s, a); break;
         case ALGO_RHD: hipLaunchKernelGGL((k_allreduce_rhd<D, O>), dim3(grid), dim3(kThreads), 0, s, a); break;
         case ALGO_LL: hipLaunchKernelGGL((k_allreduce_ll<D, O>), dim3(grid), dim3(kThreads), 0, s, a); break;
+        case ALGO_TWOSHOT_FANOUT: hipLaunchKernelGGL((k_allreduce_twoshot_fanout<D, O, R>), dim3(grid), dim3(kThreads), 0, s, a); break;
         default: throw std::invalid_argument("ccmpi: bad allreduce algo");
       }
     });

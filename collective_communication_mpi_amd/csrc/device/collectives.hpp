@@ -17,6 +17,7 @@ enum AllreduceAlgo : int {
   ALGO_RING = 4,          // pipelined ring RS + AG with peer writes, several rings (coprime strides)
   ALGO_RHD = 5,           // recursive halving (RS) + doubling (AG) with peer writes, p = 2^k
   ALGO_LL = 6,            // low-latency one-shot: (data, flag) 8-B units pushed to every peer, no barriers
+  ALGO_TWOSHOT_FANOUT = 7,  // one phase: pull-reduce my shard, store it into every rank's result (posted writes)
 };
 
 enum MoveMode : int {

@@ -255,11 +255,15 @@ void DeviceComm::allreduce(uint64_t in, uint64_t out, uint64_t count, int dtype,
     algo = ALGO_TWOSHOT;
   }
   const bool needs_res = algo != ALGO_ONESHOT;
+  // the fan-out kernel stores every shard into the ranks' result buffers
+  // (codes[1]) and never touches `out` itself: a staged result is copied back
+  const bool fan = algo == ALGO_TWOSHOT_FANOUT;
+  const bool sharded = algo == ALGO_TWOSHOT || fan;
   if (symmetric && !(algo == ALGO_ONESHOT && in == out)) {
     uint64_t sc = code_of_(in, nbytes), rc = needs_res ? code_of_(out, nbytes) : 0;
     if (!sc || (needs_res && !rc) || out % 16)
       throw std::invalid_argument("ccmpi: symmetric allreduce needs 16-B aligned registered buffers");
-    const uint64_t work = algo == ALGO_TWOSHOT ? nbytes / size_ : nbytes;
+    const uint64_t work = sharded ? nbytes / size_ : nbytes;
     launch_allreduce(algo, args_(sc, rc, (char*)out, nbytes, 0), size_, dtype, op, grid_(work, max_blocks), st);
     return;
   }
@@ -277,14 +281,19 @@ void DeviceComm::allreduce(uint64_t in, uint64_t out, uint64_t count, int dtype,
     const bool out_ok = (out + off) % 16 == 0;
     uint64_t rc = 0;
     char* outp = (char*)(out + off);
+    bool res_staged = false;
     if (needs_res) {
       rc = out_ok ? code_of_(out + off, n) : 0;
-      if (!rc) rc = addr_code(0, chunk);
+      if (!rc) {
+        rc = addr_code(0, chunk);
+        res_staged = fan;
+      }
     }
     if (!out_ok) outp = stage + chunk;
-    const uint64_t work = algo == ALGO_TWOSHOT ? n / size_ : n;
+    const uint64_t work = sharded ? n / size_ : n;
     launch_allreduce(algo, args_(sc, rc, outp, n, 0), size_, dtype, op, grid_(work, max_blocks), st);
-    if (!out_ok) CCMPI_HIP_CHECK(hipMemcpyAsync((void*)(out + off), stage + chunk, n, hipMemcpyDeviceToDevice, st));
+    if (!out_ok || res_staged)
+      CCMPI_HIP_CHECK(hipMemcpyAsync((void*)(out + off), stage + chunk, n, hipMemcpyDeviceToDevice, st));
   }
 }
 

@@ -13,6 +13,9 @@ Algorithms (``algo=``):
                    peer, no barriers (messages up to ``CCMPI_LL_MAX_BYTES``)
 ``oneshot``        every rank pulls all peers' buffers and reduces (latency)
 ``twoshot``        reduce-scatter + all-gather, all peers in flight (bandwidth)
+``fanout``         one-phase two-shot: pull-reduce my shard from every rank, store it
+                   into every rank's result (the all-gather as posted writes; 2pS
+                   HBM bytes instead of (3p-1)S, no middle barrier; large default)
 ``reduce_bcast``   the reference myAllreduce algorithm (mpi_wrapper/comm.py:63)
 ``push``           two-shot with peer writes (scatter into owners' inboxes, fan the
                    reduced shard out to every rank's result)
@@ -44,7 +47,8 @@ _OPS = {"SUM": 0, "PROD": 1, "MIN": 2, "MAX": 3}
 _UNORDERED = ("ring", "rhd", "rccl", "ring_rccl", "rhd_rccl")
 # hand-written all-reduce algorithms -> native algorithm codes
 _HAND_ALGOS = {"oneshot": "ALGO_ONESHOT", "twoshot": "ALGO_TWOSHOT", "reduce_bcast": "ALGO_REDUCE_BCAST",
-               "push": "ALGO_TWOSHOT_PUSH", "ring": "ALGO_RING", "rhd": "ALGO_RHD", "ll": "ALGO_LL"}
+               "push": "ALGO_TWOSHOT_PUSH", "ring": "ALGO_RING", "rhd": "ALGO_RHD", "ll": "ALGO_LL",
+               "fanout": "ALGO_TWOSHOT_FANOUT"}
 
 
 def op_code(op) -> int:
@@ -125,7 +129,9 @@ class DeviceGroup:
         seg = self._register(self.scratch)
         assert seg == 0, "scratch must be segment 0"
         self._rccl = False
-        self.oneshot_max = _env_int("CCMPI_ONESHOT_MAX_BYTES", 256 << 10)
+        # one-shot reads p x the message; above LL sizes the one-phase fan-out wins
+        # from 2 MiB at 2 ranks and from 64 KiB beyond (profiles/r2_coll/fanout.md)
+        self.oneshot_max = _env_int("CCMPI_ONESHOT_MAX_BYTES", (1 << 20) if self.size <= 2 else (64 << 10))
         self.ll_max = (_env_int("CCMPI_LL_MAX_BYTES", 512 << 10) + 15) // 16 * 16
         # LL pushes 2 x the payload to each of the p-1 peers: up to 256 KiB at 2 ranks,
         # 64 KiB beyond (profiles/r2_coll/ll_latency.md, small_p*.jsonl)
@@ -133,7 +139,7 @@ class DeviceGroup:
         # deterministic mode: only algorithms that reduce in rank order
         # 0..p-1 (bitwise identical on every rank and to a sequential fp32 sum in rank
         # order, like the reference's root loop, comm.py:85-93); ring / rhd / RCCL are
-        # replaced by the two-shot kernel
+        # replaced by the fan-out two-shot kernel
         self.deterministic = os.environ.get("CCMPI_DETERMINISTIC", "0") not in ("0", "")
         # concurrent rings of algo="ring": every stride coprime to p, up to 4 (p = 8: strides
         # 1, 3, 5, 7 -> 4 links per direction); CCMPI_RINGS overrides
@@ -328,7 +334,8 @@ class DeviceGroup:
             # in-kernel latency (rocprofv3, 2 ranks): 6.0 us vs 10.2 us one-shot at 4 KiB,
             # 7.1 vs 12.8 us at 64 KiB (profiles/r2_coll/ll_latency.md)
             return "ll"
-        return "oneshot" if nbytes <= self.oneshot_max else "twoshot"
+        # fanout vs twoshot, 2-8 ranks, 1-256 MiB: 0.8x the time (profiles/r2_coll/fanout.md)
+        return "oneshot" if nbytes <= self.oneshot_max else "fanout"
 
     # ------------------------------------------------------------- collectives
     @trace_call("allreduce")
@@ -344,7 +351,7 @@ class DeviceGroup:
         if algo == "auto":
             algo = self.pick_allreduce(nbytes)
         if self.deterministic and algo.split(":")[0] in _UNORDERED:
-            algo = "twoshot"
+            algo = "fanout"
         if ":" in algo:  # "twoshot:512" = algorithm with an explicit CTA budget
             algo, mb = algo.split(":", 1)
             max_blocks = int(mb)
@@ -480,7 +487,7 @@ class DeviceGroup:
         torch = self.torch
         dtype = dtype or torch.float32
         if not algos:
-            algos = ["ll", "oneshot", "twoshot"] + ([] if self.shared_device else ["rccl"])
+            algos = ["ll", "oneshot", "twoshot", "fanout"] + ([] if self.shared_device else ["rccl"])
         es = torch.empty((), dtype=dtype).element_size()
         x = self.empty(max_bytes // es, dtype)
         y = self.empty(max_bytes // es, dtype)

@@ -127,7 +127,7 @@ def test_bench_multi_rank_path_shared_gpu():
     out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
     c = out["config"]
     assert out["n_gpus"] == 1 and c["result_exact"] and c["shared_gpu"]  # 4 ranks, one GPU
-    assert set(c["candidates_ms"]) >= {"twoshot:256", "push:512", "ring", "rhd"}
+    assert set(c["candidates_ms"]) >= {"twoshot:256", "fanout:512", "push:512", "ring", "rhd"}
     assert all(v for v in c["candidates_ms"].values()), c["candidates_ms"]
     assert c["bf16_1GiB"]["algbw_GBps"] > 0 and c["alltoall"]["ms"] > 0
     assert 0.0 <= c["dp_overlap"]["comm_hidden_fraction"] <= 1.0

@@ -7,7 +7,7 @@ usage: device_worker.py [--matrix quick|full|wide] [--big] [--rccl] [--stress N]
 
 --matrix    quick: fp32/bf16, SUM, 4 sizes; full: 6 dtypes x SUM/PROD/MIN/MAX x
             8 sizes; wide: 6 dtypes x 4 ops x 4 sizes (for 8 ranks).  Every
-            hand-written all-reduce algorithm (oneshot, twoshot, push,
+            hand-written all-reduce algorithm (oneshot, twoshot, fanout, push,
             reduce_bcast, ring, rhd), symmetric and staged, out-of-place and
             in-place, plus reduce-scatter / all-gather / all-to-all (pull, push,
             staged, in-place) / bcast / last-axis TP collects.
@@ -54,7 +54,7 @@ torch.cuda.synchronize()
 fails = []
 ncheck = 0
 POW2 = p & (p - 1) == 0
-AR_ALGOS = ["oneshot", "twoshot", "push", "reduce_bcast", "ring", "ll"] + (["rhd"] if POW2 else [])
+AR_ALGOS = ["oneshot", "twoshot", "fanout", "push", "reduce_bcast", "ring", "ll"] + (["rhd"] if POW2 else [])
 WIDE = lambda dt: torch.float64 if dt.is_floating_point else torch.int64  # noqa: E731
 
 
@@ -212,11 +212,11 @@ def sym_copy(t):
 
 
 def determinism():
-    """Rank-ordered algorithms (oneshot, twoshot, push, reduce_bcast, ll) give results
+    """Rank-ordered algorithms (oneshot, twoshot, fanout, push, reduce_bcast, ll) give results
     that are bitwise identical to each other and to a sequential fp32 sum in rank order
     (bf16: fp32 accumulation, one rounding) -- the reference's root loop order
     (comm.py:85-93).  Checked in-place too, and through CCMPI_DETERMINISTIC's mapping."""
-    ordered = ["oneshot", "twoshot", "push", "reduce_bcast", "ll"]
+    ordered = ["oneshot", "twoshot", "fanout", "push", "reduce_bcast", "ll"]
     for dt in (torch.float32, torch.bfloat16):
         for n in (1000, 4096, 65536):
             xs = [gen(r, n, dt, 777000 + n) for r in range(p)]
@@ -238,7 +238,7 @@ def determinism():
     try:
         x = gen(rank, 4096, torch.float32, 778001)
         y = torch.empty_like(x)
-        dev.allreduce(x, y, "SUM", "ring")  # mapped to the rank-ordered two-shot
+        dev.allreduce(x, y, "SUM", "ring")  # mapped to the rank-ordered fan-out two-shot
         acc = gen(0, 4096, torch.float32, 778001).cpu()
         for r in range(1, p):
             acc = acc + gen(r, 4096, torch.float32, 778001).cpu()
@@ -271,6 +271,16 @@ for sym in (False, True):
                         z = sym_copy(z)
                     dev.allreduce(z, z, op, algo)
                     check(f"allreduce_inplace[{algo},{dt},{op},n={n},sym={sym}]", z, want, dt, p)
+if dtypes:  # misaligned (4-B offset) input and output: staged through the scratch segment
+    for algo in ("oneshot", "twoshot", "fanout", "ll"):
+        salt += 1
+        n = 4099
+        xb = torch.empty(n + 1, dtype=torch.float32, device=D)
+        yb = torch.empty(n + 1, dtype=torch.float32, device=D)
+        x, y = xb[1:], yb[1:]
+        x.copy_(gen(rank, n, torch.float32, salt))
+        dev.allreduce(x, y, "SUM", algo)
+        check(f"allreduce_misaligned[{algo}]", y, oracle(n, torch.float32, "SUM", salt), torch.float32, p)
 if dtypes and not POW2:  # recursive halving/doubling refuses non-power-of-two groups on every rank
     try:
         x = torch.ones(64, device=D)
@@ -345,7 +355,7 @@ if dtypes:
 # ------------------------------------------------------- >= 96 MiB: chunk loops
 if args.big:
     n = (24 << 20) + 5  # 96 MiB + 20 B of fp32: > 32 MiB staging chunks, odd tail
-    for algo in ("twoshot", "ring") + (("rhd",) if POW2 else ()):
+    for algo in ("twoshot", "fanout", "ring") + (("rhd",) if POW2 else ()):
         for sym in (False, True):
             salt += 1
             x = gen(rank, n, torch.float32, salt)
