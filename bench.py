@@ -102,7 +102,7 @@ def shared_dry_run(n: int, steps: int, warmup: int, verbose: bool):
     keep["unit"] = "GB/s (1 GiB fp32 all-reduce algbw)"
     keep["note"] = f"{n} ranks sharing ONE GPU through IPC: HBM + protocol, not xGMI"
     keep.update({k: out["config"].get(k) for k in ("allreduce_algo", "busbw_GBps", "candidates_ms", "result_exact",
-                                                     "bf16_1GiB", "alltoall", "dp_overlap", "tp_fwd_step_ms",
+                                                     "self_test", "bf16_1GiB", "alltoall", "dp_overlap", "tp_fwd_step_ms",
                                                      "parallelism")})
     return keep
 
@@ -145,6 +145,11 @@ def main() -> int:
             fn()
         sync_barrier()
         return hc.allreduce(time.perf_counter() - t0, op=MPI.MAX) / iters
+
+    # bring-up check of the small-message algorithms `auto` uses inside the harness
+    # (LL, one-shot) on this fabric: a failing one is disabled on every rank
+    self_test = dev.self_test() if world > 1 else None
+    log(f"self test: {self_test}")
 
     # ------------------------------------------------------------- all-reduce
     nbytes = args.size_mb << 20
@@ -319,6 +324,7 @@ def main() -> int:
                 "busbw_GBps": round(busbw, 3),
                 "candidates_ms": {a: (round(t * 1e3, 4) if t else None) for a, t in results.items()},
                 "result_exact": final_ok,
+                "self_test": self_test,
                 "shared_gpu": dev.shared_device,
                 **secondary,
             },

@@ -141,6 +141,8 @@ class DeviceGroup:
         # order, like the reference's root loop, comm.py:85-93); ring / rhd / RCCL are
         # replaced by the fan-out two-shot kernel
         self.deterministic = os.environ.get("CCMPI_DETERMINISTIC", "0") not in ("0", "")
+        # algorithms `auto` must not pick (CCMPI_DISABLE_ALGOS, or failed self_test())
+        self.disabled = {a for a in os.environ.get("CCMPI_DISABLE_ALGOS", "").split(",") if a}
         # concurrent rings of algo="ring": every stride coprime to p, up to 4 (p = 8: strides
         # 1, 3, 5, 7 -> 4 links per direction); CCMPI_RINGS overrides
         coprime = [k for k in range(1, self.size) if _gcd(k, self.size) == 1] or [1]
@@ -330,12 +332,19 @@ class DeviceGroup:
         forced = os.environ.get("CCMPI_ALLREDUCE_ALGO")
         if forced:
             return forced
+        prefs = []
         if nbytes <= self.ll_auto_max and nbytes % 16 == 0:
             # in-kernel latency (rocprofv3, 2 ranks): 6.0 us vs 10.2 us one-shot at 4 KiB,
             # 7.1 vs 12.8 us at 64 KiB (profiles/r2_coll/ll_latency.md)
-            return "ll"
+            prefs.append("ll")
+        if nbytes <= self.oneshot_max:
+            prefs.append("oneshot")
         # fanout vs twoshot, 2-8 ranks, 1-256 MiB: 0.8x the time (profiles/r2_coll/fanout.md)
-        return "oneshot" if nbytes <= self.oneshot_max else "fanout"
+        prefs += ["fanout", "twoshot", "reduce_bcast"]
+        for a in prefs:
+            if a not in self.disabled:
+                return a
+        return "rccl"
 
     # ------------------------------------------------------------- collectives
     @trace_call("allreduce")
@@ -511,6 +520,7 @@ class DeviceGroup:
                 except Exception:  # noqa: BLE001 - disqualify the algorithm
                     ok = 0
                 if not self.host.allreduce(ok, op=_host_min()):
+                    self.reset()  # a timed-out kernel leaves the per-CTA epochs inconsistent
                     continue
                 torch.cuda.synchronize(self.device)
                 self.host.Barrier()
@@ -528,6 +538,43 @@ class DeviceGroup:
         return dict(self.tuned)
 
     # ------------------------------------------------------------------ health
+    def self_test(self, sizes: Sequence[int] = (4096, 1 << 20),
+                  algos: Sequence[str] = ("ll", "oneshot", "fanout", "twoshot")) -> Dict[str, bool]:
+        """Collective: run each algorithm ``auto`` can pick once per size on
+        rank-valued fp32 data and check the exact result.  An algorithm that
+        fails or times out on any rank is reset away and added to ``disabled``
+        on every rank, so ``auto`` falls through to the next one (ll -> oneshot
+        -> fanout -> twoshot -> reduce_bcast -> rccl).  Run once after bring-up on
+        a new fabric; returns {algo: passed}."""
+        torch = self.torch
+        if self.size == 1:
+            return {a: True for a in algos}
+        n = max(sizes) // 4
+        x = self.empty(n, torch.float32)
+        y = self.empty(n, torch.float32)
+        x.fill_(float(self.rank + 1))
+        expect = float(self.size * (self.size + 1) // 2)
+        out = {}
+        for algo in algos:
+            ok = 1
+            try:
+                for b in sizes:
+                    m = b // 4
+                    y[:m].zero_()
+                    self.allreduce(x[:m], y[:m], "SUM", algo)
+                    torch.cuda.synchronize(self.device)
+                    self.check()
+                    ok &= int(bool(torch.all(y[:m] == expect).item()))
+            except Exception:  # noqa: BLE001 - any failure disables the algorithm
+                ok = 0
+            passed = bool(self.host.allreduce(ok, op=_host_min()))
+            if not passed:
+                self.reset()
+                self.disabled.add(algo)
+            out[algo] = passed
+        del x, y
+        return out
+
     def check(self) -> None:
         """Synchronise and raise if any device collective timed out."""
         code = self.dc.error_code()

@@ -1,0 +1,46 @@
+"""`auto` all-reduce selection (DeviceGroup.pick_allreduce): size classes
+(LL -> one-shot -> fan-out), group-size-dependent thresholds, tuned overrides,
+and the fall-through past algorithms that failed self_test() / were disabled.
+Host-only: the method is exercised on a stand-in object, no GPU needed."""
+from types import SimpleNamespace
+
+from collective_communication_mpi_amd.device import DeviceGroup
+
+
+def group(size=8, disabled=(), tuned=None):
+    return SimpleNamespace(size=size, tuned=tuned or {}, ll_auto_max=(256 << 10) if size <= 2 else (64 << 10),
+                           oneshot_max=(1 << 20) if size <= 2 else (64 << 10), disabled=set(disabled))
+
+
+def pick(g, n):
+    return DeviceGroup.pick_allreduce(g, n)
+
+
+def test_size_classes(monkeypatch):
+    monkeypatch.delenv("CCMPI_ALLREDUCE_ALGO", raising=False)
+    g = group(8)
+    assert pick(g, 4096) == "ll"
+    assert pick(g, 4100) == "oneshot"          # not a 16-B multiple: no LL
+    assert pick(g, 1 << 20) == "fanout"
+    assert pick(g, 1 << 30) == "fanout"
+    g2 = group(2)
+    assert pick(g2, 128 << 10) == "ll"
+    assert pick(g2, 512 << 10) == "oneshot"
+    assert pick(g2, 4 << 20) == "fanout"
+    assert pick(group(1), 1 << 20) == "twoshot"  # single rank: a copy
+
+
+def test_disabled_fall_through(monkeypatch):
+    monkeypatch.delenv("CCMPI_ALLREDUCE_ALGO", raising=False)
+    assert pick(group(8, {"ll"}), 4096) == "oneshot"
+    assert pick(group(8, {"ll", "oneshot"}), 4096) == "fanout"
+    assert pick(group(8, {"fanout"}), 1 << 30) == "twoshot"
+    assert pick(group(8, {"ll", "oneshot", "fanout", "twoshot", "reduce_bcast"}), 4096) == "rccl"
+
+
+def test_tuned_and_forced(monkeypatch):
+    monkeypatch.delenv("CCMPI_ALLREDUCE_ALGO", raising=False)
+    g = group(4, tuned={(4, 20): "twoshot"})
+    assert pick(g, 1 << 20) == "twoshot"
+    monkeypatch.setenv("CCMPI_ALLREDUCE_ALGO", "push")
+    assert pick(group(4), 1 << 24) == "push"

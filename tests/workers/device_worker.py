@@ -250,6 +250,10 @@ def determinism():
 
 if args.matrix:
     determinism()
+    st = dev.self_test()
+    ncheck += 1
+    if not all(st.values()) or dev.disabled:
+        fails.append(f"self_test: {st}, disabled {dev.disabled}")
 
 # ---------------------------------------------------------------- all-reduce
 for sym in (False, True):
