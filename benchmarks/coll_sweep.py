@@ -58,7 +58,7 @@ ALL_OPS = ["allreduce", "allgather", "reduce_scatter", "alltoall", "lastaxis"]
 ops = ALL_OPS if args.ops == "all" else args.ops.split(",")
 DEFAULT_ALGOS = {
     "allreduce": ["ll", "oneshot", "twoshot", "fanout", "push", "reduce_bcast", "ring", "rhd"],
-    "allgather": ["direct"],
+    "allgather": ["direct", "push"],
     "reduce_scatter": ["direct"],
     "alltoall": ["direct", "push"],
     "lastaxis": ["gather", "rscatter"],
@@ -88,6 +88,8 @@ def hbm_model(op: str, algo: str, S: int) -> float:
             # doubling pushes (p-1)/p S (read + write)
             "rhd": p * 7 * (p - 1) / p * S,
         }.get(algo, 0.0)
+    if op == "allgather" and algo == "push":
+        return (p + 1) * S                            # every rank reads its S/p block once, writes S
     if op in ("allgather", "alltoall"):
         return 2 * p * S                              # every rank reads S, writes S
     if op == "reduce_scatter":

@@ -115,7 +115,9 @@ PYBIND11_MODULE(_device, m) {
       .def_property_readonly("scratch_bytes", &DeviceComm::scratch_bytes)
       .def("allreduce", &DeviceComm::allreduce, py::call_guard<py::gil_scoped_release>())
       .def("reduce_scatter", &DeviceComm::reduce_scatter, py::call_guard<py::gil_scoped_release>())
-      .def("allgather", &DeviceComm::allgather, py::call_guard<py::gil_scoped_release>())
+      .def("allgather", &DeviceComm::allgather, py::arg("inp"), py::arg("out"), py::arg("bytes_per_rank"),
+           py::arg("stream"), py::arg("max_blocks"), py::arg("symmetric"), py::arg("mode") = 0,
+           py::call_guard<py::gil_scoped_release>())
       .def("alltoall", &DeviceComm::alltoall, py::arg("inp"), py::arg("out"), py::arg("bytes_per_peer"),
            py::arg("stream"), py::arg("max_blocks"), py::arg("symmetric"), py::arg("mode") = 0,
            py::call_guard<py::gil_scoped_release>())

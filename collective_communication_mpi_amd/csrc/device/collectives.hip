@@ -281,6 +281,45 @@ __device__ void gather_spans(const char* const* srcs, char* const* dsts, int nr,
   }
 }
 
+// Copy one local span to several destinations (push all-gather): each 16-B
+// vector is loaded once and stored to every dsts[j], j != skip.
+template <int NRM>
+__device__ void fanout_span(const char* src, char* const* dsts, int nr, int skip, uint64_t len) {
+  constexpr int kFanUnroll = 4;  // one load feeds p stores: deeper than kUnroll
+  const uint64_t kWin = 1ull << 30;
+  const uint64_t vbytes = len & ~15ull;
+  for (uint64_t w = 0; w < vbytes; w += kWin) {
+    const uint32_t wl = (uint32_t)min(kWin, vbytes - w);
+    Rsrc s = make_rsrc(uniform_ptr(const_cast<char*>(src) + w), wl);
+    Rsrc d[NRM];
+#pragma unroll
+    for (int j = 0; j < NRM; ++j)
+      if (j < nr && j != skip) d[j] = make_rsrc(uniform_ptr(dsts[j] + w), wl);
+    const uint32_t nv = wl / 16;
+    for (uint32_t v = threadIdx.x; v < nv; v += kThreads * kFanUnroll) {
+      u32x4 x[kFanUnroll];
+#pragma unroll
+      for (int u = 0; u < kFanUnroll; ++u)
+        if (v + u * kThreads < nv) x[u] = ld16(s, (v + u * kThreads) * 16);
+#pragma unroll
+      for (int j = 0; j < NRM; ++j)
+        if (j < nr && j != skip)
+#pragma unroll
+          for (int u = 0; u < kFanUnroll; ++u)
+            if (v + u * kThreads < nv) st16(d[j], (v + u * kThreads) * 16, x[u]);
+    }
+  }
+  const uint64_t tail = len - vbytes;
+  if (tail && threadIdx.x == 0) {
+    Rsrc s = make_rsrc(const_cast<char*>(src) + vbytes, (uint32_t)tail);
+    for (int j = 0; j < nr; ++j) {
+      if (j == skip) continue;
+      Rsrc d = make_rsrc(dsts[j] + vbytes, (uint32_t)tail);
+      for (uint32_t o = 0; o < tail; ++o)
+        __builtin_amdgcn_raw_buffer_store_b8(__builtin_amdgcn_raw_buffer_load_b8(s.r, o, 0, kCachePolicySys), d.r, o, 0, kStorePolicy);
+    }
+  }
+}
 
 // Reduce `nr` slots at base + j*stride (this rank's memory) and store the
 // result into every outs[j] (local or peer-mapped).
@@ -535,6 +574,8 @@ __global__ void __launch_bounds__(kThreads) k_reduce_scatter(CollArgs a) {
 //          mpi_wrapper/comm.py:130-155: each segment goes straight into its
 //          destination; the input never leaves this rank's memory except as
 //          posted peer writes, so it needs no registration)
+//   MODE 4 all-gather      (push): out_j[me*ds] = in          (same, one source block;
+//          in place -- in == out[me*ds] -- skips the self copy)
 template <int MODE, int NRM>
 __global__ void __launch_bounds__(kThreads) k_move(CollArgs a) {
   __shared__ uint64_t s_epoch;
@@ -554,8 +595,8 @@ __global__ void __launch_bounds__(kThreads) k_move(CollArgs a) {
       __shared__ char* dsts[kMaxRanks];
       if (threadIdx.x < nr) {
         const int j = threadIdx.x;
-        if (MODE == 3) {
-          srcs[j] = a.in + (uint64_t)j * ss + r.lo;
+        if (MODE == 3 || MODE == 4) {
+          srcs[j] = a.in + (MODE == 3 ? (uint64_t)j * ss : 0) + r.lo;
           dsts[j] = resolve(pt, j, codes[1][j]) + (uint64_t)me * ds + r.lo;
         } else {
           srcs[j] = resolve(pt, j, codes[0][j]) + (MODE == 1 ? (uint64_t)me * ss : 0) + r.lo;
@@ -563,7 +604,10 @@ __global__ void __launch_bounds__(kThreads) k_move(CollArgs a) {
         }
       }
       __syncthreads();
-      gather_spans<NRM>(srcs, dsts, nr, -1, r.hi - r.lo);
+      if (MODE == 4)
+        fanout_span<NRM>(srcs[0], dsts, nr, srcs[me] == dsts[me] ? me : -1, r.hi - r.lo);
+      else
+        gather_spans<NRM>(srcs, dsts, nr, -1, r.hi - r.lo);
     }
   }
   if (!sync_phase(a, 3, e)) return;
@@ -1090,6 +1134,7 @@ void launch_move(int mode, const CollArgs& a, int nranks, int grid, hipStream_t 
       case MOVE_ALLTOALL: hipLaunchKernelGGL((k_move<1, R>), dim3(grid), dim3(kThreads), 0, s, a); break;
       case MOVE_BCAST: hipLaunchKernelGGL((k_move<2, R>), dim3(grid), dim3(kThreads), 0, s, a); break;
       case MOVE_ALLTOALL_PUSH: hipLaunchKernelGGL((k_move<3, R>), dim3(grid), dim3(kThreads), 0, s, a); break;
+      case MOVE_ALLGATHER_PUSH: hipLaunchKernelGGL((k_move<4, R>), dim3(grid), dim3(kThreads), 0, s, a); break;
       default: throw std::invalid_argument("ccmpi: bad move mode");
     }
   });

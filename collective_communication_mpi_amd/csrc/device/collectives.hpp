@@ -24,7 +24,8 @@ enum MoveMode : int {
   MOVE_ALLGATHER = 0,     // pull: out[j] <- in_j
   MOVE_ALLTOALL = 1,      // pull: out[j] <- in_j[me]
   MOVE_BCAST = 2,         // pull: out <- in_root
-  MOVE_ALLTOALL_PUSH = 3  // push: out_j[me] <- in[j]  (peer writes, input stays local)
+  MOVE_ALLTOALL_PUSH = 3,  // push: out_j[me] <- in[j]  (peer writes, input stays local)
+  MOVE_ALLGATHER_PUSH = 4  // push: out_j[me] <- in     (peer writes, input stays local)
 };
 
 constexpr int kMaxRings = 8;

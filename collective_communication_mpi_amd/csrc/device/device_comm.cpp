@@ -457,12 +457,23 @@ void DeviceComm::reduce_scatter(uint64_t in, uint64_t out, uint64_t count_per_ra
 }
 
 void DeviceComm::allgather(uint64_t in, uint64_t out, uint64_t bytes_per_rank, uint64_t stream, int max_blocks,
-                           bool symmetric) {
+                           bool symmetric, int mode) {
   if (bytes_per_rank == 0) return;
   CCMPI_HIP_CHECK(hipSetDevice(device_));
   hipStream_t st = S(stream);
   if (size_ == 1) {
     if (in != out) CCMPI_HIP_CHECK(hipMemcpyAsync((void*)out, (void*)in, bytes_per_rank, hipMemcpyDeviceToDevice, st));
+    return;
+  }
+  if (mode == A2A_PUSH) {
+    // the protocol differs from the pull form, so this is the caller's global
+    // decision: every rank passes a registered, 16-B aligned output
+    const uint64_t rc = code_of_(out, bytes_per_rank * size_);
+    if (!rc || in % 16 || out % 16 || bytes_per_rank % 16)
+      throw std::invalid_argument("ccmpi: push allgather needs a registered 16-B aligned output and 16-B blocks");
+    CollArgs a = args_(0, rc, (char*)out, bytes_per_rank, 0);
+    a.in = reinterpret_cast<const char*>(in);
+    launch_move(MOVE_ALLGATHER_PUSH, a, size_, grid_(bytes_per_rank * size_, max_blocks), st);
     return;
   }
   if (symmetric) {

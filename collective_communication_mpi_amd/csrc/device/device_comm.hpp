@@ -60,8 +60,10 @@ class DeviceComm {
                  uint64_t stream, int max_blocks, bool symmetric);
   void reduce_scatter(uint64_t in, uint64_t out, uint64_t count_per_rank, int dtype, int op,
                       uint64_t stream, int max_blocks, bool symmetric);
+  // mode: A2A_PULL (default) or A2A_PUSH (every rank's output registered: the
+  // input is written into every peer's output block `me`; the input stays local)
   void allgather(uint64_t in, uint64_t out, uint64_t bytes_per_rank, uint64_t stream, int max_blocks,
-                 bool symmetric);
+                 bool symmetric, int mode = 0);
   // mode: A2A_PULL (default; staged for in-place / unregistered input) or A2A_PUSH
   // (symmetric only: every rank's output registered, peer writes into it)
   void alltoall(uint64_t in, uint64_t out, uint64_t bytes_per_peer, uint64_t stream, int max_blocks,

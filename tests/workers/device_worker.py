@@ -314,6 +314,16 @@ for sym in (False, True):
             dev.allgather(x, y)
             want = torch.cat([gen(r, n, dt, salt) for r in range(p)]).to(WIDE(dt))
             check(f"allgather[{dt},n={n},sym={sym}]", y, want, dt)
+            # push: symmetric output (peer writes), also in place (input = own block of the output)
+            y2 = dev.empty(p * n, dt) if sym else torch.empty(p * n, dtype=dt, device=D)
+            dev.allgather(gen(rank, n, dt, salt), y2, "push")
+            check(f"allgather[push,{dt},n={n},sym_out={sym}]", y2, want, dt)
+            if sym:
+                y3 = dev.empty(p * n, dt)
+                mine = y3[rank * n:(rank + 1) * n]
+                mine.copy_(gen(rank, n, dt, salt))
+                dev.allgather(mine, y3, "push")
+                check(f"allgather_inplace[push,{dt},n={n}]", y3, want, dt)
             # all-to-all: pull (symmetric input or staged), push (symmetric output), in-place (staged)
             salt += 1
             want = torch.cat([gen(r, p * n, dt, salt)[rank * n:(rank + 1) * n] for r in range(p)]).to(WIDE(dt))
