@@ -325,9 +325,9 @@ class Communicator(object):
         elif isinstance(self.comm, MPI.Comm) and \
                 _fmy_alltoall(self.comm._p, src_array, dest_array, False) is not NotImplemented:
             pass  # Irecv-all / Isend-all / Waitall, run natively (csrc/host/p2p_algos.cpp)
-        else:
+        else:  # Python schedule: non-contiguous buffers, or an mpi4py communicator
             src = src_array.reshape(-1)
-            dst = dest_array.reshape(-1)
+            dst = dest_array.reshape(-1) if dest_array.flags.c_contiguous else np.empty(n, dest_array.dtype)
             lo = rank * segment_size
             dst[lo:lo + segment_size] = src[lo:lo + segment_size]
             requests = []
@@ -343,6 +343,8 @@ class Communicator(object):
             for i in range(size):
                 if i != rank:
                     dst[i * segment_size:(i + 1) * segment_size] = recv_buffers[i]
+            if not dest_array.flags.c_contiguous:
+                dest_array[...] = dst.reshape(dest_array.shape)
         bytes_transferred = isz * segment_size
         self.total_bytes_transferred += 2 * bytes_transferred * (size - 1)
 
@@ -359,9 +361,9 @@ class Communicator(object):
         elif isinstance(self.comm, MPI.Comm) and \
                 _fmy_alltoall(self.comm._p, src_array, dest_array, True) is not NotImplemented:
             pass  # pairwise Sendrecv rounds, run natively (csrc/host/p2p_algos.cpp)
-        else:
+        else:  # Python schedule: non-contiguous buffers, or an mpi4py communicator
             src = src_array.reshape(-1)
-            dst = dest_array.reshape(-1)
+            dst = dest_array.reshape(-1) if dest_array.flags.c_contiguous else np.empty(n, dest_array.dtype)
             recv_buffer = np.empty(chunk_size, dtype=dst.dtype)
             for i in range(size):
                 start, end = i * chunk_size, (i + 1) * chunk_size
@@ -371,4 +373,6 @@ class Communicator(object):
                     self.comm.Sendrecv(src[start:end], dest=i, sendtag=rank, recvbuf=recv_buffer, source=i,
                                        recvtag=i)
                     np.copyto(dst[start:end], recv_buffer)
+            if not dest_array.flags.c_contiguous:
+                dest_array[...] = dst.reshape(dest_array.shape)
         self.total_bytes_transferred += 2 * isz * chunk_size * (size - 1)

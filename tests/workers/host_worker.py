@@ -190,6 +190,13 @@ for f in (C.myAlltoall, C.myAlltoall2):
     y = x.copy()
     f(y, y)
     expect(np.array_equal(y, lib), f"{f.__name__} in place")
+    # non-contiguous source and destination -> the Python schedules
+    xs = np.zeros((p * 6, 2), np.int32)
+    xs[:, 1] = x.reshape(-1)
+    ys = np.zeros((p * 3, 3), np.int32)  # 2-D non-contiguous destination: reshape copies
+    f(xs[:, 1], ys[:, 1:])
+    expect(np.array_equal(ys[:, 1:].reshape(-1), lib.reshape(-1)) and not ys[:, 0].any(),
+           f"{f.__name__} strided (Python schedule)")
 # internal schedule tags never match a user ANY_TAG receive
 if p > 1:
     box = np.zeros(1, np.int64)
