@@ -211,6 +211,12 @@ class Communicator(object):
         (``"oneshot" | "twoshot" | "reduce_bcast" | "ring" | "rhd" | "auto"``).
         """
         _validate_op(op)  # on every rank, before communicating
+        if not _is_device(dest_array) and not dest_array.flags.c_contiguous:
+            # every schedule receives into / reduces in a flat view of dest
+            tmp = np.empty(dest_array.shape, dest_array.dtype)
+            self.myAllreduce(src_array, tmp, op, algo)
+            dest_array[...] = tmp
+            return
         rank = self.comm.Get_rank()
         size = self.comm.Get_size()
         isz, n = _nbytes_items(src_array)

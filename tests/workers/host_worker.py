@@ -183,6 +183,9 @@ for algo in ["reduce_bcast", "ring", "rhd"]:
     inplace = x.copy()
     C.myAllreduce(inplace, inplace, op=MPI.SUM, algo=algo)
     expect(np.array_equal(inplace, nat), f"myAllreduce in place {algo}")
+    big = np.zeros((333, 3), np.int64)  # 2-D non-contiguous destination
+    C.myAllreduce(x, big[:, 1:], op=MPI.SUM, algo=algo)
+    expect(np.array_equal(big[:, 1:], nat) and not big[:, 0].any(), f"myAllreduce strided destination {algo}")
 x = (np.arange(6 * p, dtype=np.int32) + 100 * rank).reshape(p, 6)
 lib = np.empty_like(x)
 C.Alltoall(x, lib)
