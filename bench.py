@@ -164,7 +164,7 @@ def main() -> int:
             return ["twoshot"]  # single rank: the all-reduce is a device copy
         if args.algo != "auto":
             return [args.algo]
-        hand = ["twoshot:256", "twoshot:512", "fanout:256", "fanout:512", "push:512", "ring", "rhd" if world & (world - 1) == 0 else None]
+        hand = ["twoshot:256", "twoshot:512", "fanout:256", "fanout:512", "fanout_lds:512", "push:512", "ring", "rhd" if world & (world - 1) == 0 else None]
         hand = [a for a in hand if a]
         # RCCL first (the library baseline); it refuses ranks that share a GPU
         return hand if dev.shared_device else ["rccl"] + hand

@@ -57,7 +57,7 @@ maxb = args.max_mb << 20
 ALL_OPS = ["allreduce", "allgather", "reduce_scatter", "alltoall", "lastaxis"]
 ops = ALL_OPS if args.ops == "all" else args.ops.split(",")
 DEFAULT_ALGOS = {
-    "allreduce": ["ll", "oneshot", "twoshot", "fanout", "push", "reduce_bcast", "ring", "rhd"],
+    "allreduce": ["ll", "oneshot", "twoshot", "fanout", "fanout_lds", "push", "reduce_bcast", "ring", "rhd"],
     "allgather": ["direct", "push"],
     "reduce_scatter": ["direct"],
     "alltoall": ["direct", "push"],
@@ -80,6 +80,7 @@ def hbm_model(op: str, algo: str, S: int) -> float:
             "ll": p * (S + 2 * p * S + 2 * p * S + S),  # read S, push 2pS (8 B per 4 B), poll 2pS, write S
             "twoshot": (2 * p - 1) * S + p * S,       # RS: read pS write S; AG: read (p-1)S write (p-1)S
             "fanout": 2 * p * S,                      # every rank reads S (its shard from all), writes S (to all)
+            "fanout_lds": 2 * p * S,
             "push": 2 * p * S + 2 * p * S,            # scatter: read pS write pS; reduce+fan-out: same
             "reduce_bcast": (2 * p - 1) * S + p * S,  # root reads pS writes S; p-1 copies of S
             # ring, per rank: RS reads (2p-3)/p S + final 2/p S, writes p/p S; AG copies (p-2)/p S

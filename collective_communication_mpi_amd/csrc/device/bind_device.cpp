@@ -73,6 +73,7 @@ PYBIND11_MODULE(_device, m) {
   m.attr("ALGO_RHD") = (int)ALGO_RHD;
   m.attr("ALGO_LL") = (int)ALGO_LL;
   m.attr("ALGO_TWOSHOT_FANOUT") = (int)ALGO_TWOSHOT_FANOUT;
+  m.attr("ALGO_TWOSHOT_FANOUT_LDS") = (int)ALGO_TWOSHOT_FANOUT_LDS;
   m.attr("A2A_PULL") = (int)A2A_PULL;
   m.attr("A2A_PUSH") = (int)A2A_PUSH;
   m.attr("MAX_RINGS") = kMaxRings;

@@ -22,8 +22,10 @@
 //      reads them.
 // Block b only ever waits for block b of its peers, so there is no grid-wide
 // barrier; grids are sized identically on all ranks from (bytes, nranks).
-// Reductions through LDS would add a round trip without reuse (each byte is
-// read once), so partial sums stay in VGPRs.
+// Reductions through LDS add a round trip without reuse (each byte is read
+// once), so partial sums stay in VGPRs; the LDS-DMA-staged variant
+// (reduce_span_lds, algo "fanout_lds") measured even or slower on one GPU
+// (profiles/r2_coll/lds_reduce.md) and is kept as a bench candidate for xGMI.
 #include <cstdlib>
 
 #include "common.hpp"
@@ -185,6 +187,76 @@ __device__ void reduce_span_to(const PeerTable* pt, const uint64_t* codes, uint6
           for (int j = 0; j < (FAN ? NRM : 1); ++j)
             if (j < nout) st16(out[j], vv * 16, r);
         }
+      }
+    }
+  }
+  const uint64_t tail = len - vbytes;
+  if (tail && threadIdx.x == 0) {
+    using E = Elem<DT>;
+    for (uint32_t o = 0; o < tail; o += E::B) {
+      typename E::A acc = E::ld(make_rsrc(resolve(pt, 0, codes[0]) + off + vbytes, (uint32_t)tail), o);
+      for (int j = 1; j < nr; ++j)
+        acc = apply_op<OP>(acc, E::ld(make_rsrc(resolve(pt, j, codes[j]) + off + vbytes, (uint32_t)tail), o));
+      for (int j = 0; j < nout; ++j) E::st(make_rsrc(outs[j] + vbytes, (uint32_t)tail), o, acc);
+    }
+  }
+}
+
+// LDS-staged variant of reduce_span_to (algo "fanout_lds"): every
+// source's 16-B vectors go peer HBM -> LDS by DMA (buffer_load_dwordx4 ... lds,
+// no VGPRs held while in flight), double-buffered one tile (kThreads vectors per
+// source) ahead; each lane reads back only the vectors its own DMA lane wrote, so
+// no barrier is needed.  LDS: 2 x NRM x 4 KiB per CTA.  Measured against the
+// register path in profiles/r2_coll/lds_reduce.md.
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+template <int DT, int OP, int NRM, bool FAN>
+__device__ void reduce_span_lds(const PeerTable* pt, const uint64_t* codes, uint64_t off, uint64_t len,
+                                char* const* outs) {
+  __shared__ __attribute__((aligned(16))) char stage[2][NRM][kThreads * 16];
+  const int nr = pt->size;
+  const int nout = FAN ? nr : 1;
+  const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const uint32_t my = threadIdx.x * 16;
+  const uint64_t vbytes = len & ~15ull;
+  const uint64_t kWin = 1ull << 30;
+  for (uint64_t w = 0; w < vbytes; w += kWin) {
+    const uint32_t wl = (uint32_t)min(kWin, vbytes - w);
+    Rsrc src[NRM];
+#pragma unroll
+    for (int j = 0; j < NRM; ++j)
+      if (j < nr) src[j] = make_rsrc(uniform_ptr(resolve(pt, j, codes[j]) + off + w), wl);
+    Rsrc out[FAN ? NRM : 1];
+#pragma unroll
+    for (int j = 0; j < (FAN ? NRM : 1); ++j)
+      if (j < nout) out[j] = make_rsrc(uniform_ptr(outs[j] + w), wl);
+    const uint32_t nv = wl / 16, ntiles = (nv + kThreads - 1) / kThreads;
+    auto issue = [&](uint32_t t, int buf) {
+#pragma unroll
+      for (int j = 0; j < NRM; ++j)
+        if (j < nr)  // out-of-range lanes read 0 (buffer bounds), never stored
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(src[j].r, (lds_ptr_t)&stage[buf][j][wave * 1024], 16,
+                                                   t * kThreads * 16 + my, 0, 0, kCachePolicySys);
+    };
+    if (ntiles) issue(0, 0);
+    for (uint32_t t = 0; t < ntiles; ++t) {
+      const int buf = t & 1;
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      u32x4 x[NRM];
+#pragma unroll
+      for (int j = 0; j < NRM; ++j)
+        if (j < nr) x[j] = *reinterpret_cast<const u32x4*>(&stage[buf][j][my]);
+      if (t + 1 < ntiles) issue(t + 1, buf ^ 1);
+      const uint32_t vv = t * kThreads + threadIdx.x;
+      if (vv < nv) {
+        VecAcc<DT> acc;
+        acc.load(x[0]);
+#pragma unroll
+        for (int j = 1; j < NRM; ++j)
+          if (j < nr) acc.template acc<OP>(x[j]);
+        const u32x4 r = acc.store();
+#pragma unroll
+        for (int j = 0; j < (FAN ? NRM : 1); ++j)
+          if (j < nout) st16(out[j], vv * 16, r);
       }
     }
   }
@@ -456,7 +528,7 @@ __global__ void __launch_bounds__(kThreads) k_allreduce_twoshot(CollArgs a) {
 // S written (pull two-shot: S read + S/p written, then S read + S written
 // again for the all-gather).  In place is safe: only rank r reads or writes
 // region r of any buffer, and each CTA reads its slice before it writes it.
-template <int DT, int OP, int NRM>
+template <int DT, int OP, int NRM, bool LDS = false>
 __global__ void __launch_bounds__(kThreads) k_allreduce_twoshot_fanout(CollArgs a) {
   __shared__ uint64_t s_epoch;
   __shared__ uint64_t codes[2][kMaxRanks];
@@ -470,7 +542,10 @@ __global__ void __launch_bounds__(kThreads) k_allreduce_twoshot_fanout(CollArgs 
     __shared__ char* outs[kMaxRanks];
     if (threadIdx.x < nr) outs[threadIdx.x] = resolve(pt, threadIdx.x, codes[1][threadIdx.x]) + mys.lo + sub.lo;
     __syncthreads();
-    reduce_span_to<DT, OP, NRM, true>(pt, codes[0], mys.lo + sub.lo, sub.hi - sub.lo, outs);
+    if constexpr (LDS)
+      reduce_span_lds<DT, OP, NRM, true>(pt, codes[0], mys.lo + sub.lo, sub.hi - sub.lo, outs);
+    else
+      reduce_span_to<DT, OP, NRM, true>(pt, codes[0], mys.lo + sub.lo, sub.hi - sub.lo, outs);
   }
   if (!sync_phase(a, 3, e)) return;
   finish(a, e);
@@ -1098,6 +1173,9 @@ void launch_allreduce(int algo, const CollArgs& a, int nranks, int dtype, int op
         case ALGO_RHD: hipLaunchKernelGGL((k_allreduce_rhd<D, O>), dim3(grid), dim3(kThreads), 0, s, a); break;
         case ALGO_LL: hipLaunchKernelGGL((k_allreduce_ll<D, O>), dim3(grid), dim3(kThreads), 0, s, a); break;
         case ALGO_TWOSHOT_FANOUT: hipLaunchKernelGGL((k_allreduce_twoshot_fanout<D, O, R>), dim3(grid), dim3(kThreads), 0, s, a); break;
+        case ALGO_TWOSHOT_FANOUT_LDS:
+          hipLaunchKernelGGL((k_allreduce_twoshot_fanout<D, O, R, true>), dim3(grid), dim3(kThreads), 0, s, a);
+          break;
         default: throw std::invalid_argument("ccmpi: bad allreduce algo");
       }
     });

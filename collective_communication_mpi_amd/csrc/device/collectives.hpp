@@ -18,6 +18,7 @@ enum AllreduceAlgo : int {
   ALGO_RHD = 5,           // recursive halving (RS) + doubling (AG) with peer writes, p = 2^k
   ALGO_LL = 6,            // low-latency one-shot: (data, flag) 8-B units pushed to every peer, no barriers
   ALGO_TWOSHOT_FANOUT = 7,  // one phase: pull-reduce my shard, store it into every rank's result (posted writes)
+  ALGO_TWOSHOT_FANOUT_LDS = 8,  // the same, peer vectors staged through LDS by DMA (no VGPRs held in flight)
 };
 
 enum MoveMode : int {

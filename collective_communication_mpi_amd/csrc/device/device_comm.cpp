@@ -257,7 +257,7 @@ void DeviceComm::allreduce(uint64_t in, uint64_t out, uint64_t count, int dtype,
   const bool needs_res = algo != ALGO_ONESHOT;
   // the fan-out kernel stores every shard into the ranks' result buffers
   // (codes[1]) and never touches `out` itself: a staged result is copied back
-  const bool fan = algo == ALGO_TWOSHOT_FANOUT;
+  const bool fan = algo == ALGO_TWOSHOT_FANOUT || algo == ALGO_TWOSHOT_FANOUT_LDS;
   const bool sharded = algo == ALGO_TWOSHOT || fan;
   if (symmetric && !(algo == ALGO_ONESHOT && in == out)) {
     uint64_t sc = code_of_(in, nbytes), rc = needs_res ? code_of_(out, nbytes) : 0;

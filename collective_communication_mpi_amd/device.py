@@ -16,6 +16,9 @@ Algorithms (``algo=``):
 ``fanout``         one-phase two-shot: pull-reduce my shard from every rank, store it
                    into every rank's result (the all-gather as posted writes; 2pS
                    HBM bytes instead of (3p-1)S, no middle barrier; large default)
+``fanout_lds``     the same with the peer vectors staged through LDS by DMA (buffer
+                   loads into LDS: nothing held in VGPRs while in flight); measured
+                   even with ``fanout`` on one GPU, a bench candidate for xGMI
 ``reduce_bcast``   the reference myAllreduce algorithm (mpi_wrapper/comm.py:63)
 ``push``           two-shot with peer writes (scatter into owners' inboxes, fan the
                    reduced shard out to every rank's result)
@@ -48,7 +51,7 @@ _UNORDERED = ("ring", "rhd", "rccl", "ring_rccl", "rhd_rccl")
 # hand-written all-reduce algorithms -> native algorithm codes
 _HAND_ALGOS = {"oneshot": "ALGO_ONESHOT", "twoshot": "ALGO_TWOSHOT", "reduce_bcast": "ALGO_REDUCE_BCAST",
                "push": "ALGO_TWOSHOT_PUSH", "ring": "ALGO_RING", "rhd": "ALGO_RHD", "ll": "ALGO_LL",
-               "fanout": "ALGO_TWOSHOT_FANOUT"}
+               "fanout": "ALGO_TWOSHOT_FANOUT", "fanout_lds": "ALGO_TWOSHOT_FANOUT_LDS"}
 
 
 def op_code(op) -> int:

@@ -54,7 +54,7 @@ torch.cuda.synchronize()
 fails = []
 ncheck = 0
 POW2 = p & (p - 1) == 0
-AR_ALGOS = ["oneshot", "twoshot", "fanout", "push", "reduce_bcast", "ring", "ll"] + (["rhd"] if POW2 else [])
+AR_ALGOS = ["oneshot", "twoshot", "fanout", "fanout_lds", "push", "reduce_bcast", "ring", "ll"] + (["rhd"] if POW2 else [])
 WIDE = lambda dt: torch.float64 if dt.is_floating_point else torch.int64  # noqa: E731
 
 
@@ -216,7 +216,7 @@ def determinism():
     that are bitwise identical to each other and to a sequential fp32 sum in rank order
     (bf16: fp32 accumulation, one rounding) -- the reference's root loop order
     (comm.py:85-93).  Checked in-place too, and through CCMPI_DETERMINISTIC's mapping."""
-    ordered = ["oneshot", "twoshot", "fanout", "push", "reduce_bcast", "ll"]
+    ordered = ["oneshot", "twoshot", "fanout", "fanout_lds", "push", "reduce_bcast", "ll"]
     for dt in (torch.float32, torch.bfloat16):
         for n in (1000, 4096, 65536):
             xs = [gen(r, n, dt, 777000 + n) for r in range(p)]
@@ -276,7 +276,7 @@ for sym in (False, True):
                     dev.allreduce(z, z, op, algo)
                     check(f"allreduce_inplace[{algo},{dt},{op},n={n},sym={sym}]", z, want, dt, p)
 if dtypes:  # misaligned (4-B offset) input and output: staged through the scratch segment
-    for algo in ("oneshot", "twoshot", "fanout", "ll"):
+    for algo in ("oneshot", "twoshot", "fanout", "fanout_lds", "ll"):
         salt += 1
         n = 4099
         xb = torch.empty(n + 1, dtype=torch.float32, device=D)
@@ -369,7 +369,7 @@ if dtypes:
 # ------------------------------------------------------- >= 96 MiB: chunk loops
 if args.big:
     n = (24 << 20) + 5  # 96 MiB + 20 B of fp32: > 32 MiB staging chunks, odd tail
-    for algo in ("twoshot", "fanout", "ring") + (("rhd",) if POW2 else ()):
+    for algo in ("twoshot", "fanout", "fanout_lds", "ring") + (("rhd",) if POW2 else ()):
         for sym in (False, True):
             salt += 1
             x = gen(rank, n, torch.float32, salt)
