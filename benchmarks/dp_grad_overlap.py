@@ -23,11 +23,13 @@ ap.add_argument("--algo", default="auto")
 ap.add_argument("--comm-priority", type=int, default=0, help="side-stream priority (-1 = high, 0 = normal)")
 ap.add_argument("--verbose", action="store_true")
 ap.add_argument("--blocks", type=int, default=0, help="CTA budget of the bucket all-reduces (0 = overlap_blocks)")
+ap.add_argument("--bucket-mb", type=int, default=0, help="max bucket size in MiB (0 = one bucket per layer)")
 args = ap.parse_args()
 comm = Communicator(MPI.COMM_WORLD)
 local = int(os.environ.get("LOCAL_RANK", os.environ.get("CCMPI_LOCAL_RANK", "0")))
 torch.cuda.set_device(local % torch.cuda.device_count())
 res = dp_grad_overlap(comm, layers=args.layers, tokens=args.tokens, iters=args.iters, algo=args.algo,
-                      priority=args.comm_priority, verbose=args.verbose, max_blocks=args.blocks)
+                      priority=args.comm_priority, verbose=args.verbose, max_blocks=args.blocks,
+                      bucket_mb=args.bucket_mb)
 if comm.Get_rank() == 0:
     print(json.dumps({"bench": "dp_grad_overlap", "comm_priority": args.comm_priority, **res}), flush=True)

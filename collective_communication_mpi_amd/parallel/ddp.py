@@ -27,7 +27,8 @@ CPU tensors are reduced by the C++ host plane (the reference's CPU setting).
 """
 from __future__ import annotations
 
-from typing import Dict, List
+import os
+from typing import Dict, List, Optional
 
 import torch
 
@@ -48,9 +49,13 @@ class _Bucket:
 class DistributedDataParallel(torch.nn.Module):
     """Wraps ``module``; ``comm`` is the DP communicator (Communicator or host Comm)."""
 
-    def __init__(self, module: torch.nn.Module, comm, bucket_bytes: int = 64 << 20, algo: str = "auto",
+    def __init__(self, module: torch.nn.Module, comm, bucket_bytes: Optional[int] = None, algo: str = "auto",
                  average: bool = True, overlap: bool = True, broadcast_params: bool = True):
         super().__init__()
+        if bucket_bytes is None:
+            # bucket sweep (profiles/r2_overlap/buckets.md): per-call cost makes buckets
+            # below ~64 MiB expensive (16 MiB: 2.3x the comm time of 416 MiB buckets)
+            bucket_bytes = int(os.environ.get("CCMPI_DP_BUCKET_MB", "64")) << 20
         self.module = module
         self.comm = comm
         self.hc = _host_comm(comm)

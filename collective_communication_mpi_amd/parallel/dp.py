@@ -8,7 +8,7 @@ and builds ``dp_comm`` (func_impl.py:61-62); "we simply just split the batch"
 * every parameter lives in one flat fp32 master buffer (+ a bf16 compute copy
   + AdamW moments); gradients live in one flat fp32 buffer allocated from the
   DP device group's *symmetric heap*, so bucket all-reduces run zero-copy
-  (no staging) with the hand-written two-shot kernel over all xGMI links;
+  (no staging) with the hand-written fan-out two-shot kernel over all xGMI links;
 * the layout is in backward order, so each bucket is a contiguous range that
   becomes ready as soon as its layer's weight-gradient GEMMs are issued;
 * ``GradBuckets.ready(i)`` records an event on the compute stream and launches

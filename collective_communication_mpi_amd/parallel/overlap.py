@@ -37,9 +37,12 @@ def layer_weight_shapes(d: int, kv: int, ff: int) -> List[Tuple[int, int]]:
 
 def dp_grad_overlap(comm, layers: int = 32, tokens: int = 4096, iters: int = 3, algo: str = "auto",
                     priority: int = 0, dims: Dict[str, int] = LLAMA3_8B, seed: int = 0, verbose: bool = False,
-                    max_blocks: int = 0) -> Dict:
+                    max_blocks: int = 0, bucket_mb: int = 0) -> Dict:
     """``max_blocks``: CTA budget of the bucket all-reduces (0 = the group's
-    ``overlap_blocks``, the budget for collectives that run beside compute)."""
+    ``overlap_blocks``, the budget for collectives that run beside compute).
+    ``bucket_mb``: split each layer's gradient range into all-reduces of at most
+    this many MiB, each launched once the layer's GEMMs are queued (0 = one
+    bucket per layer, 436 MB for Llama-3-8B)."""
     from .. import mpi as MPI
 
     dev = comm.dev
@@ -55,6 +58,8 @@ def dp_grad_overlap(comm, layers: int = 32, tokens: int = 4096, iters: int = 3, 
     side = torch.cuda.Stream(device=dev.device, priority=priority)
     mb = max_blocks or dev.overlap_blocks
     events = [torch.cuda.Event() for _ in range(layers)]
+    # bucket length in elements, a multiple of 8 (16-B aligned bf16 buckets)
+    step = per_layer if bucket_mb <= 0 else max(8, ((bucket_mb << 20) // 2) // 8 * 8)
 
     def backward(comm_on: bool, compute_on: bool = True) -> None:
         for layer in reversed(range(layers)):
@@ -68,8 +73,9 @@ def dp_grad_overlap(comm, layers: int = 32, tokens: int = 4096, iters: int = 3, 
                 events[layer].record()
                 side.wait_event(events[layer])
                 with torch.cuda.stream(side):
-                    seg = grads[base:base + per_layer]
-                    dev.allreduce(seg, seg, "SUM", algo, max_blocks=mb)
+                    for lo in range(0, per_layer, step):
+                        seg = grads[base + lo:base + min(per_layer, lo + step)]
+                        dev.allreduce(seg, seg, "SUM", algo, max_blocks=mb)
         torch.cuda.current_stream().wait_stream(side)
 
     def timed(**kw) -> float:
@@ -100,6 +106,7 @@ def dp_grad_overlap(comm, layers: int = 32, tokens: int = 4096, iters: int = 3, 
            "overlapped_ms": round(t_both * 1e3, 3), "comm_hidden_fraction": None if hidden is None else round(hidden, 3),
            "wgrad_TFLOPs": round(flops / t_compute / 1e12, 1), "shared_gpu": dev.shared_device,
            "comm_algbw_GBps": round(gbytes / t_comm / 1e9, 2) if t_comm else None, "algo": algo,
-           "bucket_ctas": mb, "buckets": layers}
+           "bucket_ctas": mb, "buckets": layers * ((per_layer + step - 1) // step),
+           "bucket_MiB": round(min(step, per_layer) * 2 / (1 << 20), 1)}
     del grads, x_t, dy_t
     return out
