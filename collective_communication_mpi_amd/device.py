@@ -137,8 +137,11 @@ class DeviceGroup:
         self.oneshot_max = _env_int("CCMPI_ONESHOT_MAX_BYTES", (1 << 20) if self.size <= 2 else (64 << 10))
         self.ll_max = (_env_int("CCMPI_LL_MAX_BYTES", 512 << 10) + 15) // 16 * 16
         # LL pushes 2 x the payload to each of the p-1 peers: up to 256 KiB at 2 ranks,
-        # 64 KiB beyond (profiles/r2_coll/ll_latency.md, small_p*.jsonl)
-        self.ll_auto_max = min(self.ll_max, _env_int("CCMPI_LL_AUTO_MAX_BYTES", (256 << 10) if self.size <= 2 else (64 << 10)))
+        # 64 KiB beyond (profiles/r2_coll/ll_latency.md).  With > 2 ranks SHARING a GPU
+        # the polling ranks compete with their peers' pushes for the same CUs and LL
+        # loses to one-shot from 8 KiB (small_p4/p8.jsonl): 4 KiB there
+        ll_default = (256 << 10) if self.size <= 2 else ((4 << 10) if self.shared_device else (64 << 10))
+        self.ll_auto_max = min(self.ll_max, _env_int("CCMPI_LL_AUTO_MAX_BYTES", ll_default))
         # deterministic mode: only algorithms that reduce in rank order
         # 0..p-1 (bitwise identical on every rank and to a sequential fp32 sum in rank
         # order, like the reference's root loop, comm.py:85-93); ring / rhd / RCCL are
