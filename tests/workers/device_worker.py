@@ -248,8 +248,54 @@ def determinism():
         dev.deterministic = old
 
 
+def graphs():
+    """Collectives captured once in a HIP graph and replayed with new data: the
+    protocol state (per-CTA epochs, the LL call epoch) lives in device memory, so
+    replays stay in step with the peers' replays.  Staged (unregistered) buffers
+    too: their copies through the scratch segment are captured as well."""
+    global ncheck
+    n = 4096 + 8
+    cases = [("allreduce", a) for a in ("ll", "oneshot", "twoshot", "fanout", "push", "ring")] + \
+        [("allgather", "push"), ("allgather", "direct"), ("alltoall", "direct")]
+    for sym in (True, False):
+        for op, algo in cases:
+            mk = (lambda m: dev.empty(m, torch.float32)) if sym else (lambda m: torch.empty(m, dtype=torch.float32, device=D))
+            if op == "allreduce":
+                x, y = mk(n), mk(n)
+                run = lambda: dev.allreduce(x, y, "SUM", algo)
+            elif op == "allgather":
+                x, y = mk(n), mk(n * p)
+                run = lambda: dev.allgather(x, y, algo)
+            else:
+                x, y = mk(n * p), mk(n * p)
+                run = lambda: dev.alltoall(x, y, algo)
+            x.fill_(1.0)
+            run()  # eager first: lazy allocations (inbox, LL buffers) happen outside the capture
+            torch.cuda.synchronize()
+            comm.comm.Barrier()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                run()
+            for it in range(3):
+                if op == "allreduce":
+                    x.fill_(float(rank + 1 + it))
+                    want = torch.full((n,), float(p * (p + 1) // 2 + p * it), dtype=torch.float64, device=D)
+                elif op == "allgather":
+                    x.fill_(float(rank + 10 * it))
+                    want = (torch.arange(p, device=D, dtype=torch.float64) + 10 * it).repeat_interleave(n)
+                else:
+                    x.view(p, n).copy_((rank * p + torch.arange(p, device=D, dtype=torch.float32) + 100 * it).view(p, 1).expand(p, n))
+                    want = (torch.arange(p, device=D, dtype=torch.float64) * p + rank + 100 * it).repeat_interleave(n)
+                g.replay()
+                torch.cuda.synchronize()
+                dev.check()
+                check(f"graph_replay[{op},{algo},sym={sym},it={it}]", y, want, torch.float32)
+            del g
+
+
 if args.matrix:
     determinism()
+    graphs()
     st = dev.self_test()
     ncheck += 1
     if not all(st.values()) or dev.disabled:
