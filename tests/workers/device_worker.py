@@ -112,7 +112,8 @@ def check(name, got, want, dtype, nterms=1):
 
 def stress(iters):
     """Random arrival order at every collective; results checked after the burst.
-    Mixes symmetric (zero-copy) and staged calls, up to 16 MiB."""
+    Mixes symmetric (zero-copy) and staged calls, up to 16 MiB, all-reduces of every
+    algorithm with push / pull all-gathers and all-to-alls."""
     import random
 
     rng = random.Random(1234 + rank)  # per-rank: delays only
@@ -131,6 +132,33 @@ def stress(iters):
             time.sleep(rng.random() * 0.004)
         elif d < 0.6:
             torch.cuda._sleep(rng.randint(1000, 200000))  # device-side skew
+        kind = shared.random()
+        if kind < 0.15:  # all-gather of n // p elements per rank, push or pull
+            m = max(1, n // p)
+            ag = shared.choice(["direct", "push"])
+            x = gen(rank, m, torch.float32, 50000 + i)
+            if sym:
+                sym_x[:m].copy_(x)
+                x, y = sym_x[:m], sym_y[:m * p]
+            else:
+                y = torch.empty(m * p, dtype=torch.float32, device=D)
+            dev.allgather(x, y, ag)
+            want = torch.cat([gen(r, m, torch.float32, 50000 + i) for r in range(p)]).double()
+            pending.append((f"stress[{i},allgather-{ag},m={m},sym={sym}]", y.clone(), want, 1))
+            continue
+        if kind < 0.3:  # all-to-all of n // p elements per peer block, push or pull
+            m = max(1, n // p)
+            aa = shared.choice(["direct", "push"])
+            x = gen(rank, m * p, torch.float32, 50000 + i)
+            if sym:
+                sym_x[:m * p].copy_(x)
+                x, y = sym_x[:m * p], sym_y[:m * p]
+            else:
+                y = torch.empty(m * p, dtype=torch.float32, device=D)
+            dev.alltoall(x, y, aa)
+            want = torch.cat([gen(r, m * p, torch.float32, 50000 + i)[rank * m:(rank + 1) * m] for r in range(p)]).double()
+            pending.append((f"stress[{i},alltoall-{aa},m={m},sym={sym}]", y.clone(), want, 1))
+            continue
         x = gen(rank, n, torch.float32, 50000 + i)
         if sym:
             sym_x[:n].copy_(x)
@@ -138,11 +166,13 @@ def stress(iters):
         else:
             y = torch.empty(n, dtype=torch.float32, device=D)
         dev.allreduce(x, y, "SUM", algo)
-        pending.append((f"stress[{i},{algo},n={n},sym={sym}]", y.clone(), n, 50000 + i))
+        pending.append((f"stress[{i},{algo},n={n},sym={sym}]", y.clone(), (n, 50000 + i), p))
     torch.cuda.synchronize()
     dev.check()
-    for name, y, n, sl in pending:
-        check(name, y, oracle(n, torch.float32, "SUM", sl), torch.float32, p)
+    for name, y, want, nt in pending:
+        if isinstance(want, tuple):
+            want = oracle(want[0], torch.float32, "SUM", want[1])
+        check(name, y, want, torch.float32, nt)
 
 
 def fault():
