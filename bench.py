@@ -166,8 +166,10 @@ def main() -> int:
             return [args.algo]
         hand = ["twoshot:256", "twoshot:512", "fanout:256", "fanout:512", "fanout_lds:512", "push:512", "ring", "rhd" if world & (world - 1) == 0 else None]
         hand = [a for a in hand if a]
-        # RCCL first (the library baseline); it refuses ranks that share a GPU
-        return hand if dev.shared_device else ["rccl"] + hand
+        # RCCL first (the library baseline); it refuses ranks that share a GPU.  With one
+        # rank per GPU all 1024 CTA slots (4 per CU) are this rank's: more reads in flight
+        # over the links
+        return hand if dev.shared_device else ["rccl"] + hand + ["fanout:1024"]
 
     custom_failed = [False]
 
