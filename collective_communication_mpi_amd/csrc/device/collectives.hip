@@ -661,6 +661,27 @@ __global__ void __launch_bounds__(kThreads) k_move(CollArgs a) {
   const int me = pt->rank, nr = pt->size;
   const uint64_t ss = a.src_stride ? a.src_stride : a.nbytes;
   const uint64_t ds = a.dst_stride ? a.dst_stride : a.nbytes;
+  if ((MODE == 0 || MODE == 1 || MODE == 3) && (a.flags & 1)) {
+    // peer-major: CTA b streams one peer's block (j = b % p, slice b / p of
+    // gridDim / p), one source and one destination stream per CTA
+    const int j = blockIdx.x % nr;
+    BlockRange q = part16(a.nbytes, gridDim.x / nr, blockIdx.x / nr);
+    if (q.hi > q.lo) {
+      const char* src;
+      char* dst;
+      if (MODE == 3 || MODE == 4) {
+        src = a.in + (MODE == 3 ? (uint64_t)j * ss : 0) + q.lo;
+        dst = resolve(pt, j, codes[1][j]) + (uint64_t)me * ds + q.lo;
+      } else {
+        src = resolve(pt, j, codes[0][j]) + (MODE == 1 ? (uint64_t)me * ss : 0) + q.lo;
+        dst = a.out + (uint64_t)j * ds + q.lo;
+      }
+      if (src != dst) copy_span(src, dst, q.hi - q.lo);
+    }
+    if (!sync_phase(a, 3, e)) return;
+    finish(a, e);
+    return;
+  }
   BlockRange r = part16(a.nbytes, gridDim.x, blockIdx.x);
   if (r.hi > r.lo) {
     if (MODE == 2) {

@@ -42,7 +42,7 @@ struct CollArgs {
   uint64_t timeout_ticks;  // bounded spins, 100 MHz ticks
   int root;
   int nrings;              // ring: number of concurrent rings (CTA b runs ring b % nrings)
-  uint64_t aux_code;       // unused (inboxes are published through src_code)
+  uint64_t flags;          // k_move bit 0: peer-major CTA mapping (CTA b moves only peer b % p's block)
   const char* in;          // local input (push two-shot / ring / rhd / push all-to-all read only their own input;
                            // those kernels publish the inbox in src_code instead)
   uint64_t src_stride;     // all-to-all: bytes between per-peer blocks of the source (0 = nbytes)

@@ -456,6 +456,24 @@ void DeviceComm::reduce_scatter(uint64_t in, uint64_t out, uint64_t count_per_ra
   }
 }
 
+// Peer-major CTA mapping for the pull all-gather and both all-to-alls: CTA b
+// streams only peer (b % p)'s block (grid rounded to a multiple of p), one source
+// and one destination stream per CTA instead of p interleaved ones.  Measured
+// 6-10% faster for all-to-all and 23-31% for the pull all-gather at 256 MiB
+// (profiles/r2_coll/peer_major.md); CCMPI_PEER_MAJOR=0 restores the all-peers
+// mapping.  The push all-gather keeps it: one load there feeds p stores.
+static void launch_move_m(int mode, CollArgs a, int p, int grid, hipStream_t st) {
+  static const bool pm = [] {
+    const char* e = std::getenv("CCMPI_PEER_MAJOR");
+    return !(e && e[0] == '0');
+  }();
+  if (pm && (mode == MOVE_ALLGATHER || mode == MOVE_ALLTOALL || mode == MOVE_ALLTOALL_PUSH)) {
+    a.flags |= 1;
+    grid = std::max(p, grid / p * p);
+  }
+  launch_move(mode, a, p, grid, st);
+}
+
 void DeviceComm::allgather(uint64_t in, uint64_t out, uint64_t bytes_per_rank, uint64_t stream, int max_blocks,
                            bool symmetric, int mode) {
   if (bytes_per_rank == 0) return;
@@ -482,7 +500,7 @@ void DeviceComm::allgather(uint64_t in, uint64_t out, uint64_t bytes_per_rank, u
       if (!sc) throw std::invalid_argument("ccmpi: symmetric allgather needs an aligned registered input");
     }
     if (out % 16 == 0 && bytes_per_rank % 16 == 0) {
-      launch_move(MOVE_ALLGATHER, args_(sc, 0, (char*)out, bytes_per_rank, 0), size_, grid_(bytes_per_rank * size_, max_blocks), st);
+      launch_move_m(MOVE_ALLGATHER, args_(sc, 0, (char*)out, bytes_per_rank, 0), size_, grid_(bytes_per_rank * size_, max_blocks), st);
       return;
     }
   }
@@ -505,7 +523,7 @@ void DeviceComm::allgather(uint64_t in, uint64_t out, uint64_t bytes_per_rank, u
     char* dst = direct ? (char*)(out + off) : gath;
     CollArgs a = args_(sc, 0, dst, n, 0);
     a.dst_stride = direct ? bytes_per_rank : n;
-    launch_move(MOVE_ALLGATHER, a, size_, grid_(n * size_, max_blocks), st);
+    launch_move_m(MOVE_ALLGATHER, a, size_, grid_(n * size_, max_blocks), st);
     if (!direct)
       CCMPI_HIP_CHECK(hipMemcpy2DAsync((void*)(out + off), bytes_per_rank, gath, n, n, size_, hipMemcpyDeviceToDevice, st));
   }
@@ -529,12 +547,12 @@ void DeviceComm::alltoall(uint64_t in, uint64_t out, uint64_t bytes_per_peer, ui
       if (!rc) throw std::invalid_argument("ccmpi: push alltoall needs a registered output on every rank");
       CollArgs a = args_(0, rc, (char*)out, bytes_per_peer, 0);
       a.in = reinterpret_cast<const char*>(in);
-      launch_move(MOVE_ALLTOALL_PUSH, a, size_, grid_(total, max_blocks), st);
+      launch_move_m(MOVE_ALLTOALL_PUSH, a, size_, grid_(total, max_blocks), st);
       return;
     }
     const uint64_t sc = code_of_(in, total);
     if (!sc) throw std::invalid_argument("ccmpi: symmetric alltoall needs an aligned registered input");
-    launch_move(MOVE_ALLTOALL, args_(sc, 0, (char*)out, bytes_per_peer, 0), size_, grid_(total, max_blocks), st);
+    launch_move_m(MOVE_ALLTOALL, args_(sc, 0, (char*)out, bytes_per_peer, 0), size_, grid_(total, max_blocks), st);
     return;
   }
   // Staged pull (in-place calls, unregistered inputs): one pack pass of this
@@ -552,7 +570,7 @@ void DeviceComm::alltoall(uint64_t in, uint64_t out, uint64_t bytes_per_peer, ui
     CollArgs a = args_(addr_code(0, 0), 0, direct ? (char*)(out + off) : gath, n, 0);
     a.src_stride = n;
     a.dst_stride = direct ? bytes_per_peer : n;
-    launch_move(MOVE_ALLTOALL, a, size_, grid_(n * size_, max_blocks), st);
+    launch_move_m(MOVE_ALLTOALL, a, size_, grid_(n * size_, max_blocks), st);
     if (!direct)
       CCMPI_HIP_CHECK(hipMemcpy2DAsync((void*)(out + off), bytes_per_peer, gath, n, n, size_, hipMemcpyDeviceToDevice, st));
   }

@@ -41,6 +41,10 @@ class _Trace:
 
         name = f"ccmpi.{op}.{algo}.{nbytes}B"
         torch.cuda.nvtx.range_push(name)
+        if torch.cuda.is_current_stream_capturing():
+            # inside a HIP graph capture an event record becomes a graph node whose
+            # timestamps cannot be read back: keep the range, skip the timing
+            return (op, algo, nbytes, ranks, None, None, stream)
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         s.record(stream)
         return (op, algo, nbytes, ranks, s, e, stream)
@@ -50,14 +54,24 @@ class _Trace:
             return
         import torch
 
-        tok[5].record(tok[6])
         torch.cuda.nvtx.range_pop()
+        if tok[4] is None:
+            return
+        tok[5].record(tok[6])
         with self._lock:
             self._pending.append(tok)
+            drain = len(self._pending) >= 4096
+        if drain:  # bound the pending events of long runs: resolve the completed ones
+            self.flush(completed_only=True)
 
-    def flush(self) -> None:
+    def flush(self, completed_only: bool = False) -> None:
         with self._lock:
-            pend, self._pending = self._pending, []
+            if completed_only:
+                pend = [t for t in self._pending if t[5].query()]
+                done = {id(t) for t in pend}
+                self._pending = [t for t in self._pending if id(t) not in done]
+            else:
+                pend, self._pending = self._pending, []
         for op, algo, nbytes, ranks, s, e, _ in pend:
             e.synchronize()
             ms = s.elapsed_time(e)

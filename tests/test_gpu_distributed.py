@@ -40,6 +40,25 @@ def test_device_collectives_random_skew(n):
     assert "0 failures" in r.stdout
 
 
+def test_trace_records_collectives_and_survives_graph_capture(tmp_path):
+    """CCMPI_TRACE=1 over the quick matrix (which also captures collectives in HIP
+    graphs): one JSON record per eager call per rank, with device time and bandwidths;
+    calls made during a capture keep their roctx range but are not timed."""
+    import glob
+    import json
+
+    path = str(tmp_path / "trace_{pid}.jsonl")
+    r = run_ranks(2, py("tests/workers/device_worker.py", "--matrix", "quick", "--sizes", "1000"), timeout=300,
+                  env=dict(ENV, CCMPI_TRACE="1", CCMPI_TRACE_FILE=path))
+    assert "0 failures" in r.stdout
+    files = glob.glob(str(tmp_path / "trace_*.jsonl"))
+    assert len(files) == 2
+    recs = [json.loads(ln) for f in files for ln in open(f)]
+    assert {"allreduce", "allgather", "alltoall"} <= {x["op"] for x in recs}
+    assert all(x["ms"] >= 0 and x["bytes"] >= 0 for x in recs)
+    assert {"ll", "fanout", "push"} <= {x["algo"] for x in recs}
+
+
 def test_rccl_same_gpu_behaviour_recorded(tmp_path):
     """RCCL with two ranks on one GPU: the outcome of every step is recorded, not swallowed
     (benchmarks/rccl_shared_probe.py; on this pool ncclCommInitRank reports 'invalid usage')."""
