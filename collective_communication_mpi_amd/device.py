@@ -219,8 +219,11 @@ class DeviceGroup:
         best-fit allocator over IPC-registered arenas of ``CCMPI_HEAP_ARENA_MB``
         (default 256 MiB, or the request if larger), grown collectively when
         full.  The tensor owns its block through a DLPack deleter: the block
-        returns to the heap when the last view dies (stream-ordered reuse,
-        like torch's caching allocator).
+        returns to the heap when the last view dies.  As with torch's caching
+        allocator, reuse is ordered only with work on the allocating (current)
+        stream: keep a tensor used on a side stream alive until that stream has
+        been joined.  Peers' writes into a block never outlive the collective
+        that made them (every kernel ends with a barrier over all ranks).
         """
         torch = self.torch
         dtype = dtype or torch.float32
