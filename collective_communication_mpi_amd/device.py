@@ -223,7 +223,8 @@ class DeviceGroup:
         allocator, reuse is ordered only with work on the allocating (current)
         stream: keep a tensor used on a side stream alive until that stream has
         been joined.  Peers' writes into a block never outlive the collective
-        that made them (every kernel ends with a barrier over all ranks).
+        that made them: a rank's kernel ends only after every peer write into
+        its buffers has landed (end barrier, or the per-step flags it awaits).
         """
         torch = self.torch
         dtype = dtype or torch.float32
