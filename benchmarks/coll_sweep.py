@@ -54,7 +54,7 @@ dt = getattr(torch, args.dtype)
 es = torch.empty((), dtype=dt).element_size()
 maxb = args.max_mb << 20
 
-ALL_OPS = ["allreduce", "allgather", "reduce_scatter", "alltoall", "lastaxis"]
+ALL_OPS = ["allreduce", "allgather", "reduce_scatter", "alltoall", "lastaxis", "bcast"]
 ops = ALL_OPS if args.ops == "all" else args.ops.split(",")
 DEFAULT_ALGOS = {
     "allreduce": ["ll", "oneshot", "twoshot", "fanout", "fanout_lds", "push", "reduce_bcast", "ring", "rhd"],
@@ -62,6 +62,7 @@ DEFAULT_ALGOS = {
     "reduce_scatter": ["direct"],
     "alltoall": ["direct", "push"],
     "lastaxis": ["gather", "rscatter"],
+    "bcast": ["direct", "push"],
 }
 if not dev.shared_device:
     DEFAULT_ALGOS["allreduce"].append("rccl")
@@ -97,12 +98,16 @@ def hbm_model(op: str, algo: str, S: int) -> float:
         return p * S + S                              # every rank reads S, writes S/p
     if op == "lastaxis":
         return 2 * p * S if algo == "gather" else p * S + S
+    if op == "bcast":  # pull: p-1 ranks read S and write S; push: the root reads S once, p-1 writes of S
+        return 2 * (p - 1) * S if algo == "direct" else p * S
     return 0.0
 
 
 def bus_factor(op: str) -> float:
     if p == 1:
         return 0.0
+    if op == "bcast":
+        return 1.0
     return 2 * (p - 1) / p if op == "allreduce" else (p - 1) / p
 
 
@@ -150,6 +155,10 @@ def make(op: str, algo: str, S: int, mb: int):
         yo = arena_out[: rows * k]
         want = p * (p + 1) / 2
         return (lambda: dev.reduce_scatter_lastaxis(xi, yo, rows, k)), (lambda: bool(torch.all(yo == want).item()))
+    if op == "bcast":
+        root = p - 1
+        x.fill_(rank + 1)
+        return (lambda: dev.bcast(x, root, algo)), (lambda: bool(torch.all(x == root + 1).item()))
     raise ValueError(op)
 
 

@@ -122,7 +122,8 @@ PYBIND11_MODULE(_device, m) {
       .def("alltoall", &DeviceComm::alltoall, py::arg("inp"), py::arg("out"), py::arg("bytes_per_peer"),
            py::arg("stream"), py::arg("max_blocks"), py::arg("symmetric"), py::arg("mode") = 0,
            py::call_guard<py::gil_scoped_release>())
-      .def("bcast", &DeviceComm::bcast, py::call_guard<py::gil_scoped_release>())
+      .def("bcast", &DeviceComm::bcast, py::arg("buf"), py::arg("nbytes"), py::arg("root"), py::arg("stream"),
+           py::arg("max_blocks"), py::arg("symmetric"), py::arg("mode") = 0, py::call_guard<py::gil_scoped_release>())
       .def("local_reduce", &DeviceComm::local_reduce, py::call_guard<py::gil_scoped_release>())
       .def("allgather_lastaxis", &DeviceComm::allgather_lastaxis, py::call_guard<py::gil_scoped_release>())
       .def("reduce_scatter_lastaxis", &DeviceComm::reduce_scatter_lastaxis, py::call_guard<py::gil_scoped_release>())

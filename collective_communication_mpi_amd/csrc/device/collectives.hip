@@ -651,6 +651,9 @@ __global__ void __launch_bounds__(kThreads) k_reduce_scatter(CollArgs a) {
 //          posted peer writes, so it needs no registration)
 //   MODE 4 all-gather      (push): out_j[me*ds] = in          (same, one source block;
 //          in place -- in == out[me*ds] -- skips the self copy)
+//   MODE 5 broadcast       (push): out_j = in on the root, which loads each vector
+//          once and stores it to the p-1 peers; the other ranks only publish
+//          their buffer and wait at the end barrier
 template <int MODE, int NRM>
 __global__ void __launch_bounds__(kThreads) k_move(CollArgs a) {
   __shared__ uint64_t s_epoch;
@@ -686,6 +689,13 @@ __global__ void __launch_bounds__(kThreads) k_move(CollArgs a) {
   if (r.hi > r.lo) {
     if (MODE == 2) {
       if (me != a.root) copy_span(resolve(pt, a.root, codes[0][a.root]) + r.lo, a.out + r.lo, r.hi - r.lo);
+    } else if (MODE == 5) {
+      if (me == a.root) {
+        __shared__ char* bdst[kMaxRanks];
+        if (threadIdx.x < nr) bdst[threadIdx.x] = resolve(pt, threadIdx.x, codes[1][threadIdx.x]) + r.lo;
+        __syncthreads();
+        fanout_span<NRM>(a.in + r.lo, bdst, nr, me, r.hi - r.lo);
+      }
     } else {
       __shared__ const char* srcs[kMaxRanks];
       __shared__ char* dsts[kMaxRanks];
@@ -1234,6 +1244,7 @@ void launch_move(int mode, const CollArgs& a, int nranks, int grid, hipStream_t 
       case MOVE_BCAST: hipLaunchKernelGGL((k_move<2, R>), dim3(grid), dim3(kThreads), 0, s, a); break;
       case MOVE_ALLTOALL_PUSH: hipLaunchKernelGGL((k_move<3, R>), dim3(grid), dim3(kThreads), 0, s, a); break;
       case MOVE_ALLGATHER_PUSH: hipLaunchKernelGGL((k_move<4, R>), dim3(grid), dim3(kThreads), 0, s, a); break;
+      case MOVE_BCAST_PUSH: hipLaunchKernelGGL((k_move<5, R>), dim3(grid), dim3(kThreads), 0, s, a); break;
       default: throw std::invalid_argument("ccmpi: bad move mode");
     }
   });

@@ -26,7 +26,8 @@ enum MoveMode : int {
   MOVE_ALLTOALL = 1,      // pull: out[j] <- in_j[me]
   MOVE_BCAST = 2,         // pull: out <- in_root
   MOVE_ALLTOALL_PUSH = 3,  // push: out_j[me] <- in[j]  (peer writes, input stays local)
-  MOVE_ALLGATHER_PUSH = 4  // push: out_j[me] <- in     (peer writes, input stays local)
+  MOVE_ALLGATHER_PUSH = 4,  // push: out_j[me] <- in     (peer writes, input stays local)
+  MOVE_BCAST_PUSH = 5       // push: out_j <- in_root    (the root's CTAs fan each vector out)
 };
 
 constexpr int kMaxRings = 8;

@@ -576,13 +576,20 @@ void DeviceComm::alltoall(uint64_t in, uint64_t out, uint64_t bytes_per_peer, ui
   }
 }
 
-void DeviceComm::bcast(uint64_t buf, uint64_t nbytes, int root, uint64_t stream, int max_blocks, bool symmetric) {
+void DeviceComm::bcast(uint64_t buf, uint64_t nbytes, int root, uint64_t stream, int max_blocks, bool symmetric,
+                       int mode) {
   if (nbytes == 0 || size_ == 1) return;
   CCMPI_HIP_CHECK(hipSetDevice(device_));
   hipStream_t st = S(stream);
   if (symmetric && buf % 16 == 0) {
     uint64_t sc = code_of_(buf, nbytes);
     if (!sc) throw std::invalid_argument("ccmpi: symmetric bcast needs an aligned registered buffer");
+    if (mode == A2A_PUSH) {
+      CollArgs a = args_(0, sc, (char*)buf, nbytes, root);  // every rank publishes its buffer as the result
+      a.in = reinterpret_cast<const char*>(buf);
+      launch_move(MOVE_BCAST_PUSH, a, size_, grid_(nbytes, max_blocks), st);
+      return;
+    }
     launch_move(MOVE_BCAST, args_(sc, 0, (char*)buf, nbytes, root), size_, grid_(nbytes, max_blocks), st);
     return;
   }

@@ -68,7 +68,8 @@ class DeviceComm {
   // (symmetric only: every rank's output registered, peer writes into it)
   void alltoall(uint64_t in, uint64_t out, uint64_t bytes_per_peer, uint64_t stream, int max_blocks,
                 bool symmetric, int mode = 0);
-  void bcast(uint64_t buf, uint64_t nbytes, int root, uint64_t stream, int max_blocks, bool symmetric);
+  // mode A2A_PUSH: symmetric buffers only, the root writes into every peer's buffer
+  void bcast(uint64_t buf, uint64_t nbytes, int root, uint64_t stream, int max_blocks, bool symmetric, int mode = 0);
   void local_reduce(const std::vector<uint64_t>& ins, uint64_t out, uint64_t count, int dtype, int op,
                     uint64_t stream);
   // TP layout-fused collectives: rows x k shards <-> rows x p*k (last axis)

@@ -477,14 +477,24 @@ class DeviceGroup:
         return dst
 
     @trace_call("bcast")
-    def bcast(self, buf, root: int = 0, algo: str = "direct"):
+    def bcast(self, buf, root: int = 0, algo: str = "auto"):
+        """``direct`` (= ``auto``): every rank pulls the root's buffer; ``push``:
+        the root loads each vector once and writes it into every peer's buffer
+        (symmetric buffers on every rank, else the pull form) -- only the root's
+        CTAs work there, which measured slower than the pull form at 4 / 8 ranks
+        (profiles/r2_coll/bcast_push.md); ``rccl``."""
         self._check(buf, "buf")
         s = self._stream()
+        nb = buf.numel() * buf.element_size()
         if algo == "rccl":
             self.ensure_rccl()
-            self.dc.rccl_bcast(buf.data_ptr(), buf.numel() * buf.element_size(), 1, root, s)
+            self.dc.rccl_bcast(buf.data_ptr(), nb, 1, root, s)
+        elif algo in ("direct", "auto", "push"):
+            symm = self._symm(buf)
+            mode = self.D.A2A_PUSH if (algo == "push" and symm) else self.D.A2A_PULL
+            self.dc.bcast(buf.data_ptr(), nb, root, s, self._budget(None), symm, mode)
         else:
-            self.dc.bcast(buf.data_ptr(), buf.numel() * buf.element_size(), root, s, self._budget(None), self._symm(buf))
+            raise ValueError(f"unknown bcast algorithm {algo!r}")
         return buf
 
     def allgather_lastaxis(self, src, dst, rows: int, row_bytes: int):

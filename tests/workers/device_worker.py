@@ -417,14 +417,15 @@ for sym in (False, True):
                 z = sym_copy(z)
             dev.alltoall(z, z)
             check(f"alltoall_inplace[{dt},n={n},sym={sym}]", z, want, dt)
-            # bcast from root p-1
-            salt += 1
-            root = p - 1
-            b = gen(rank, n, dt, salt)
-            if sym:
-                b = sym_copy(b)
-            dev.bcast(b, root)
-            check(f"bcast[{dt},n={n},sym={sym}]", b, gen(root, n, dt, salt).to(WIDE(dt)), dt)
+            # bcast from root p-1: pull (auto) and push (symmetric buffers; else pull)
+            for balgo in ("auto", "push"):
+                salt += 1
+                root = p - 1
+                b = gen(rank, n, dt, salt)
+                if sym:
+                    b = sym_copy(b)
+                dev.bcast(b, root, balgo)
+                check(f"bcast[{balgo},{dt},n={n},sym={sym}]", b, gen(root, n, dt, salt).to(WIDE(dt)), dt)
 
 # ------------------------------------- TP layout-fused collectives (func_impl)
 if dtypes:
