@@ -78,6 +78,43 @@ def dtype_code(torch_dtype) -> int:
         raise TypeError(f"unsupported device dtype {torch_dtype}") from None
 
 
+def tuning_key(size: int, ranks_per_device: int, device_name: str) -> str:
+    """Identity of a tuning table: group size, GPU sharing and device model."""
+    return f"p{size}-share{ranks_per_device}-{device_name}"
+
+
+def load_tuning(path: str, key: str) -> Dict[Tuple[int, int], str]:
+    """{(size, log2 bytes): algo} saved by ``save_tuning`` for ``key``; {} if absent."""
+    import json
+
+    try:
+        with open(path) as f:
+            tables = json.load(f)
+    except (OSError, ValueError):
+        return {}
+    out = {}
+    for k, algo in tables.get(key, {}).items():
+        size, lg = (int(v) for v in k.split(","))
+        out[(size, lg)] = str(algo)
+    return out
+
+
+def save_tuning(path: str, key: str, table: Dict[Tuple[int, int], str]) -> None:
+    """Merge ``table`` into the JSON file at ``path`` under ``key`` (atomic rename)."""
+    import json
+
+    try:
+        with open(path) as f:
+            tables = json.load(f)
+    except (OSError, ValueError):
+        tables = {}
+    tables[key] = {f"{s},{lg}": a for (s, lg), a in sorted(table.items())}
+    tmp = f"{path}.tmp{os.getpid()}"
+    with open(tmp, "w") as f:
+        json.dump(tables, f, indent=1, sort_keys=True)
+    os.replace(tmp, path)
+
+
 def _env_int(name: str, default: int) -> int:
     v = os.environ.get(name)
     return int(v) if v else default
@@ -155,6 +192,11 @@ class DeviceGroup:
         self.default_rings = _env_int("CCMPI_RINGS", min(4, len(coprime)))
         self.inbox_cap = _env_int("CCMPI_INBOX_MAX_MB", 1024) << 20
         self.tuned: Dict[Tuple[int, int], str] = {}
+        # persisted tune() results (CCMPI_TUNE_FILE), keyed by group size, GPU sharing and model
+        self.tune_key = tuning_key(self.size, self.ranks_per_device, props.name)
+        self.tune_file = os.environ.get("CCMPI_TUNE_FILE")
+        if self.tune_file:
+            self.tuned.update(load_tuning(self.tune_file, self.tune_key))
         self._lock = threading.Lock()
         self._watchdog: Optional[threading.Thread] = None
         mode = os.environ.get("CCMPI_WATCHDOG", "warn").lower()
@@ -516,11 +558,13 @@ class DeviceGroup:
 
     # ------------------------------------------------------------------- tuning
     def tune(self, max_bytes: int = 256 << 20, min_bytes: int = 4 << 10, algos: Sequence[str] = (),
-             iters: int = 5, dtype=None) -> Dict[Tuple[int, int], str]:
+             iters: int = 5, dtype=None, save: Optional[str] = None) -> Dict[Tuple[int, int], str]:
         """Collective: time every all-reduce algorithm at powers of 4 between
         ``min_bytes`` and ``max_bytes`` (after an exactness check) and make
         ``algo="auto"`` use the fastest per size class.  Algorithms that fail or
-        time out on any rank are discarded everywhere."""
+        time out on any rank are discarded everywhere.  The table is written by
+        rank 0 to ``save`` (default ``CCMPI_TUNE_FILE``), from which later
+        groups of the same size / sharing / GPU model load it at start-up."""
         import time
 
         torch = self.torch
@@ -565,6 +609,10 @@ class DeviceGroup:
                 self.tuned[(self.size, max(0, b.bit_length() - 1))] = best
                 self.tuned[(self.size, max(0, b.bit_length() - 1) + 1)] = best
             b *= 4
+        path = save or self.tune_file
+        if path and self.rank == 0:
+            save_tuning(path, self.tune_key, self.tuned)
+        self.host.Barrier()
         return dict(self.tuned)
 
     # ------------------------------------------------------------------ health

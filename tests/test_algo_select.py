@@ -44,3 +44,19 @@ def test_tuned_and_forced(monkeypatch):
     assert pick(g, 1 << 20) == "twoshot"
     monkeypatch.setenv("CCMPI_ALLREDUCE_ALGO", "push")
     assert pick(group(4), 1 << 24) == "push"
+
+
+def test_tuning_file_roundtrip(tmp_path):
+    from collective_communication_mpi_amd.device import load_tuning, save_tuning, tuning_key
+
+    path = str(tmp_path / "tune.json")
+    k8 = tuning_key(8, 1, "AMD Instinct MI355X")
+    k2 = tuning_key(2, 2, "AMD Instinct MI355X")
+    assert load_tuning(path, k8) == {}  # no file yet
+    save_tuning(path, k8, {(8, 20): "fanout", (8, 12): "ll"})
+    save_tuning(path, k2, {(2, 20): "oneshot"})  # merged, not overwritten
+    assert load_tuning(path, k8) == {(8, 20): "fanout", (8, 12): "ll"}
+    assert load_tuning(path, k2) == {(2, 20): "oneshot"}
+    assert load_tuning(path, tuning_key(4, 1, "x")) == {}
+    g = SimpleNamespace(size=8, tuned=load_tuning(path, k8), ll_auto_max=64 << 10, oneshot_max=64 << 10, disabled=set())
+    assert pick(g, 1 << 20) == "fanout" and pick(g, 4096) == "ll"

@@ -323,9 +323,35 @@ def graphs():
             del g
 
 
+def tuning():
+    """tune() -> per-size table used by auto, persisted through CCMPI_TUNE_FILE-style save."""
+    import tempfile
+
+    global ncheck
+    path = os.path.join(tempfile.gettempdir(), f"ccmpi_tune_test_{os.getppid()}.json")
+    table = dev.tune(max_bytes=1 << 20, min_bytes=4096, iters=2, save=path)
+    ncheck += 1
+    if not table or any(a not in ("ll", "oneshot", "twoshot", "fanout", "rccl") for a in table.values()):
+        fails.append(f"tune: unexpected table {table}")
+    from collective_communication_mpi_amd.device import load_tuning
+    if rank == 0 and load_tuning(path, dev.tune_key) != table:
+        fails.append("tune: saved table differs")
+    for n in (1024, 16384, 1 << 18):  # auto now follows the table
+        x = gen(rank, n, torch.float32, 91000 + n)
+        y = torch.empty_like(x)
+        dev.allreduce(x, y, "SUM", "auto")
+        check(f"tuned_auto[n={n}]", y, oracle(n, torch.float32, "SUM", 91000 + n), torch.float32, p)
+    comm.comm.Barrier()
+    if rank == 0:
+        os.unlink(path)
+    dev.tuned.clear()
+
+
 if args.matrix:
     determinism()
     graphs()
+    if args.matrix == "quick":
+        tuning()
     st = dev.self_test()
     ncheck += 1
     if not all(st.values()) or dev.disabled:
