@@ -377,16 +377,25 @@ for sym in (False, True):
                         z = sym_copy(z)
                     dev.allreduce(z, z, op, algo)
                     check(f"allreduce_inplace[{algo},{dt},{op},n={n},sym={sym}]", z, want, dt, p)
-if dtypes:  # misaligned (4-B offset) input and output: staged through the scratch segment
-    for algo in ("oneshot", "twoshot", "fanout", "fanout_lds", "ll"):
+if dtypes:  # misaligned (one-element offset: 4 B fp32, 2 B bf16) input and output
+    for mdt in (torch.float32, torch.bfloat16):
+        for algo in ("oneshot", "twoshot", "fanout", "fanout_lds", "push", "reduce_bcast", "ring", "ll"):
+            salt += 1
+            n = 4099
+            xb = torch.empty(n + 1, dtype=mdt, device=D)
+            yb = torch.empty(n + 1, dtype=mdt, device=D)
+            x, y = xb[1:], yb[1:]
+            x.copy_(gen(rank, n, mdt, salt))
+            dev.allreduce(x, y, "SUM", algo)
+            check(f"allreduce_misaligned[{algo},{mdt}]", y, oracle(n, mdt, "SUM", salt), mdt, p)
         salt += 1
-        n = 4099
-        xb = torch.empty(n + 1, dtype=torch.float32, device=D)
-        yb = torch.empty(n + 1, dtype=torch.float32, device=D)
+        n = 1001
+        xb = torch.empty(n + 1, dtype=mdt, device=D)
+        yb = torch.empty(p * n + 1, dtype=mdt, device=D)
         x, y = xb[1:], yb[1:]
-        x.copy_(gen(rank, n, torch.float32, salt))
-        dev.allreduce(x, y, "SUM", algo)
-        check(f"allreduce_misaligned[{algo}]", y, oracle(n, torch.float32, "SUM", salt), torch.float32, p)
+        x.copy_(gen(rank, n, mdt, salt))
+        dev.allgather(x, y)
+        check(f"allgather_misaligned[{mdt}]", y, torch.cat([gen(r, n, mdt, salt) for r in range(p)]).to(WIDE(mdt)), mdt)
 if dtypes and not POW2:  # recursive halving/doubling refuses non-power-of-two groups on every rank
     try:
         x = torch.ones(64, device=D)
