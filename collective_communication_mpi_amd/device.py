@@ -78,6 +78,31 @@ def dtype_code(torch_dtype) -> int:
         raise TypeError(f"unsupported device dtype {torch_dtype}") from None
 
 
+class Work:
+    """Handle of a collective started with ``DeviceGroup.start``."""
+
+    def __init__(self, group: "DeviceGroup", done, result, keep) -> None:
+        self.group, self.done, self.result, self._keep = group, done, result, keep
+
+    def is_completed(self) -> bool:
+        return self.done.query()
+
+    def wait(self):
+        """Order the current stream after the collective (no host sync); returns
+        the collective's output tensor."""
+        torch = self.group.torch
+        torch.cuda.current_stream(self.group.device).wait_event(self.done)
+        self._keep = None
+        return self.result
+
+    def synchronize(self):
+        """Block the host until the collective finished; raises on a device timeout."""
+        self.done.synchronize()
+        self.group.check()
+        self._keep = None
+        return self.result
+
+
 def tuning_key(size: int, ranks_per_device: int, device_name: str) -> str:
     """Identity of a tuning table: group size, GPU sharing and device model."""
     return f"p{size}-share{ranks_per_device}-{device_name}"
@@ -614,6 +639,43 @@ class DeviceGroup:
             save_tuning(path, self.tune_key, self.tuned)
         self.host.Barrier()
         return dict(self.tuned)
+
+    # ------------------------------------------------------------- async issue
+    def start(self, op: str, *args, stream=None, **kw) -> "Work":
+        """Non-blocking collective: ``op`` ("allreduce", "allgather", "alltoall",
+        "reduce_scatter", "bcast") runs on ``stream`` (default: this group's
+        communication stream, normal priority) after the work queued so far on
+        the current stream; returns a ``Work`` whose ``wait()`` makes the current
+        stream wait for it.  The tensors stay referenced by the ``Work`` until it
+        is waited on, so their blocks cannot be reused under the collective (the
+        device-side analogue of the reference's Isend/Irecv + Waitall,
+        mpi_wrapper/comm.py:136-150).  Every rank must start the same
+        collectives in the same order on the same stream kind.
+
+        With more than 2 ranks sharing one GPU (this repo's test setup) the
+        default is the current stream: one extra stream in each of 8 processes
+        oversubscribes the GPU's hardware queues, the scheduler then time-slices
+        them and every later cross-process barrier waits for a queue switch
+        (measured: all collectives ~10x slower for the rest of the run)."""
+        torch = self.torch
+        fn = getattr(self, op)
+        if stream is None:
+            if self.shared_device and self.ranks_per_device > 2:
+                stream = torch.cuda.current_stream(self.device)
+            else:
+                if getattr(self, "_comm_stream", None) is None:
+                    self._comm_stream = torch.cuda.Stream(device=self.device)
+                stream = self._comm_stream
+        ready = torch.cuda.Event()
+        ready.record(torch.cuda.current_stream(self.device))
+        stream.wait_event(ready)
+        with torch.cuda.stream(stream):
+            if op in ("allreduce", "allgather", "alltoall", "reduce_scatter"):
+                kw.setdefault("max_blocks", self.overlap_blocks)  # runs beside compute
+            out = fn(*args, **kw)
+            done = torch.cuda.Event()
+            done.record(stream)
+        return Work(self, done, out, args)
 
     # ------------------------------------------------------------------ health
     def self_test(self, sizes: Sequence[int] = (4096, 1 << 20),

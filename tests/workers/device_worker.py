@@ -323,6 +323,40 @@ def graphs():
             del g
 
 
+def async_ops():
+    """DeviceGroup.start(): collectives on the communication stream overlapped with
+    compute on the current stream; Work.wait() orders the consumer after them."""
+    global ncheck
+    n = 1 << 16
+    a = torch.randn(512, 512, device=D)
+    works, wants = [], []
+    for i, (op, algo) in enumerate([("allreduce", "fanout"), ("allreduce", "auto"), ("allgather", "push"),
+                                    ("alltoall", "direct")]):
+        sl = 93000 + i
+        if op == "allreduce":
+            x, y = gen(rank, n, torch.float32, sl), dev.empty(n, torch.float32)
+            works.append(dev.start(op, x, y, "SUM", algo))
+            wants.append(oracle(n, torch.float32, "SUM", sl))
+        elif op == "allgather":
+            x, y = gen(rank, n, torch.float32, sl), dev.empty(n * p, torch.float32)
+            works.append(dev.start(op, x, y, algo))
+            wants.append(torch.cat([gen(r, n, torch.float32, sl) for r in range(p)]).double())
+        else:
+            x, y = gen(rank, n * p, torch.float32, sl), torch.empty(n * p, dtype=torch.float32, device=D)
+            works.append(dev.start(op, x, y, algo))
+            wants.append(torch.cat([gen(r, n * p, torch.float32, sl)[rank * n:(rank + 1) * n] for r in range(p)]).double())
+        del x  # the Work keeps the input alive
+        a = a @ a * 1e-3  # compute on the current stream meanwhile
+    for i, (w, want) in enumerate(zip(works, wants)):
+        out = w.wait()
+        check(f"async[{i}]", out, want, torch.float32, p)
+    w = dev.start("allreduce", gen(rank, 1000, torch.float32, 93100), torch.empty(1000, device=D))
+    check("async_sync", w.synchronize(), oracle(1000, torch.float32, "SUM", 93100), torch.float32, p)
+    ncheck += 1
+    if not w.is_completed():
+        fails.append("async: is_completed() false after synchronize()")
+
+
 def tuning():
     """tune() -> per-size table used by auto, persisted through CCMPI_TUNE_FILE-style save."""
     import tempfile
@@ -347,11 +381,22 @@ def tuning():
     dev.tuned.clear()
 
 
+_LAP = [time.time()]
+
+
+def _lap(label):
+    if rank == 0 and os.environ.get("CCMPI_WORKER_VERBOSE") == "1":
+        print(f"[worker] {label}: {time.time() - _LAP[0]:.2f}s", flush=True)
+    _LAP[0] = time.time()
+
+
+_lap("setup")
 if args.matrix:
-    determinism()
-    graphs()
-    if args.matrix == "quick":
-        tuning()
+    for fn in (determinism, graphs) + ((tuning,) if args.matrix == "quick" else ()):
+        t_s = time.time()
+        fn()
+        if rank == 0 and os.environ.get("CCMPI_WORKER_VERBOSE") == "1":
+            print(f"[worker] {fn.__name__}: {time.time() - t_s:.2f}s", flush=True)
     st = dev.self_test()
     ncheck += 1
     if not all(st.values()) or dev.disabled:
@@ -404,6 +449,7 @@ if dtypes and not POW2:  # recursive halving/doubling refuses non-power-of-two g
     except ValueError:
         pass
 
+_lap("allreduce matrix + misaligned")
 # ------------------------------------------- reduce-scatter / gathers / bcast
 for sym in (False, True):
     for n in sizes[:6]:
@@ -462,6 +508,7 @@ for sym in (False, True):
                 dev.bcast(b, root, balgo)
                 check(f"bcast[{balgo},{dt},n={n},sym={sym}]", b, gen(root, n, dt, salt).to(WIDE(dt)), dt)
 
+_lap("rs/ag/a2a/bcast matrix")
 # ------------------------------------- TP layout-fused collectives (func_impl)
 if dtypes:
     from collective_communication_mpi_amd.parallel.layout import (  # noqa: E402
@@ -478,6 +525,7 @@ if dtypes:
             ref = sum(f.to(torch.float64) for f in full)[:, :, rank * k:(rank + 1) * k]
             check(f"backward_x_lastaxis[{dt},{B}x{S}x{k}]", got, ref, dt, p)
 
+_lap("lastaxis")
 # ------------------------------------------------------- >= 96 MiB: chunk loops
 if args.big:
     n = (24 << 20) + 5  # 96 MiB + 20 B of fp32: > 32 MiB staging chunks, odd tail
@@ -544,4 +592,8 @@ check("myAllreduce(device)", y, oracle(1024, torch.float32, "SUM", 11), torch.fl
 want_bytes = 2 * 4096 * (p - 1) if rank == 0 else 2 * 4096
 if comm.total_bytes_transferred - before != want_bytes:
     fails.append(f"myAllreduce accounting {comm.total_bytes_transferred - before} != {want_bytes}")
+_lap("big/rccl")
+if args.matrix:
+    async_ops()  # last: an extra stream per process slows 8 processes sharing a GPU (DeviceGroup.start)
+    _lap("async_ops")
 finish(t0)
