@@ -85,8 +85,10 @@ class DistributedDataParallel(torch.nn.Module):
         if cur:
             self._make_bucket(cur)
         self._bucket_of: Dict[int, _Bucket] = {id(q): b for b in self.buckets for q in b.params}
+        # > 2 ranks sharing one GPU (test setup): no side stream (DeviceGroup.start)
+        crowded = self.dev is not None and self.dev.shared_device and self.dev.ranks_per_device > 2
         self.stream = (torch.cuda.Stream(device=dev, priority=-1)
-                       if (dev.type == "cuda" and overlap and self.p > 1) else None)
+                       if (dev.type == "cuda" and overlap and self.p > 1 and not crowded) else None)
         self._hooks = [q.register_post_accumulate_grad_hook(self._on_grad) for q in params]
 
     # ------------------------------------------------------------------ setup
@@ -150,8 +152,8 @@ class DistributedDataParallel(torch.nn.Module):
         ev = torch.cuda.Event()
         ev.record(torch.cuda.current_stream(self.device))
         self.stream.wait_event(ev)
-        with torch.cuda.stream(self.stream):
-            self.dev.allreduce(b.buf, b.buf, "SUM", self.algo)
+        with torch.cuda.stream(self.stream):  # beside the backward: the overlap CTA budget
+            self.dev.allreduce(b.buf, b.buf, "SUM", self.algo, max_blocks=self.dev.overlap_blocks)
 
     def finish(self) -> None:
         """Complete the gradient synchronisation (after backward, before the step)."""

@@ -118,7 +118,11 @@ class GradBuckets:
         # dispatched ahead of the GEMM tiles and wait for the peer's bucket -- vs 35% at normal
         # priority; CCMPI_DP_STREAM_PRIORITY=-1 restores the high-priority stream
         prio = int(os.environ.get("CCMPI_DP_STREAM_PRIORITY", "0"))
-        self.stream = torch.cuda.Stream(device=flat.device, priority=prio) if (dp_group is not None and overlap) else None
+        # > 2 ranks sharing one GPU (test setup): no side stream -- one extra stream per
+        # process oversubscribes the hardware queues (see DeviceGroup.start)
+        crowded = dp_group is not None and dp_group.shared_device and dp_group.ranks_per_device > 2
+        self.stream = torch.cuda.Stream(device=flat.device, priority=prio) \
+            if (dp_group is not None and overlap and not crowded) else None
         self.events: List[torch.cuda.Event] = [torch.cuda.Event() for _ in self.ranges]
         self.launched = 0
 
