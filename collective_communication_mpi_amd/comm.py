@@ -66,6 +66,39 @@ def _validate_op(op) -> None:
         raise NotImplementedError("Only MPI.SUM, MPI.MIN, MPI.MAX and MPI.PROD are supported.")
 
 
+class DeviceRequest(MPI.Request):
+    """MPI-style handle of a device collective started on the communication
+    stream (``DeviceGroup.start``).  CUDA-aware-MPI semantics: ``Wait()`` orders
+    the caller's current stream after the collective (no host sync), ``Test()``
+    polls completion, ``synchronize()`` blocks the host and raises on a device
+    timeout.  ``MPI.Request.Waitall`` accepts it mixed with host requests."""
+
+    __slots__ = ()
+
+    def __init__(self, comm, work) -> None:
+        super().__init__(comm, work, None)
+        self._done = False
+
+    def _finish(self, status=None):
+        if not self._done:
+            self._result = self._native.wait()
+            self._done = True
+        return self._result
+
+    def Test(self, status=None) -> bool:
+        if self._done:
+            return True
+        if self._native.is_completed():
+            self._finish(status)
+            return True
+        return False
+
+    def synchronize(self):
+        out = self._native.synchronize()
+        self._done = True
+        return out
+
+
 class Communicator(object):
     """Reference-compatible communicator with a GPU fast path."""
 
@@ -180,6 +213,55 @@ class Communicator(object):
             self.dev.bcast(buf, root)
         else:
             self.comm.Bcast(buf, root)
+
+    # ------------------------------------------- non-blocking collectives
+    # MPI-3 style: each returns a Request (``Wait`` / ``Test`` / ``Request.Waitall``).
+    # NumPy buffers run as round schedules on the host plane (csrc/host/nbcoll.cpp),
+    # advanced by every progress call; CUDA tensors run on the device plane's
+    # communication stream beside the caller's compute (``DeviceGroup.start``).
+    # Byte accounting is that of the blocking call.
+    def Iallreduce(self, src_array, dest_array, op=MPI.SUM, algo: str = "auto"):
+        isz, n = _nbytes_items(src_array)
+        self.total_bytes_transferred += isz * n * 2 * (self.comm.Get_size() - 1)
+        if _is_device(src_array):
+            return DeviceRequest(self.comm, self.dev.start("allreduce", src_array, dest_array, op, algo))
+        return self.comm.Iallreduce(src_array, dest_array, op)
+
+    def Iallgather(self, src_array, dest_array, algo: str = "direct"):
+        sisz, sn = _nbytes_items(src_array)
+        disz, dn = _nbytes_items(dest_array)
+        self.total_bytes_transferred += (sisz * sn + disz * dn) * (self.comm.Get_size() - 1)
+        if _is_device(src_array):
+            return DeviceRequest(self.comm, self.dev.start("allgather", src_array, dest_array, algo))
+        return self.comm.Iallgather(src_array, dest_array)
+
+    def Ireduce_scatter(self, src_array, dest_array, op=MPI.SUM, algo: str = "direct"):
+        sisz, sn = _nbytes_items(src_array)
+        disz, dn = _nbytes_items(dest_array)
+        self.total_bytes_transferred += (sisz * sn + disz * dn) * (self.comm.Get_size() - 1)
+        if _is_device(src_array):
+            return DeviceRequest(self.comm, self.dev.start("reduce_scatter", src_array, dest_array, op, algo))
+        return self.comm.Ireduce_scatter_block(src_array, dest_array, op)
+
+    def Ialltoall(self, src_array, dest_array, algo: str = "direct"):
+        nprocs = self.comm.Get_size()
+        sisz, sn = _nbytes_items(src_array)
+        disz, dn = _nbytes_items(dest_array)
+        assert sn % nprocs == 0 and dn % nprocs == 0, "buffer sizes must be divisible by the number of processes"
+        self.total_bytes_transferred += (sisz * (sn // nprocs) + disz * (dn // nprocs)) * (nprocs - 1)
+        if _is_device(src_array):
+            return DeviceRequest(self.comm, self.dev.start("alltoall", src_array, dest_array, algo))
+        return self.comm.Ialltoall(src_array, dest_array)
+
+    def Ibcast(self, buf, root: int = 0):
+        isz, n = _nbytes_items(buf)
+        self.total_bytes_transferred += isz * n * ((self.comm.Get_size() - 1) if self.comm.Get_rank() == root else 1)
+        if _is_device(buf):
+            return DeviceRequest(self.comm, self.dev.start("bcast", buf, root))
+        return self.comm.Ibcast(buf, root)
+
+    def Ibarrier(self):
+        return self.comm.Ibarrier()
 
     # object collectives (the reference calls these on raw mpi4py comms:
     # model/func_impl.py:89,107,184) -- provided here too so a Communicator

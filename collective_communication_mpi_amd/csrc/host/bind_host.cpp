@@ -80,6 +80,9 @@ PYBIND11_MODULE(_host, m) {
       .def_property_readonly("complete", [](const Request& r) { return r.complete; })
       .def_property_readonly("status", [](const RequestPtr& r) { return status_of(r); });
 
+  // opaque handle of a started non-blocking collective (nbcoll.cpp)
+  py::class_<NbColl, NbCollPtr>(m, "CollRequest");
+
   py::class_<ShmComm, std::shared_ptr<ShmComm>>(m, "HostComm")
       .def_static("world", &ShmComm::world, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("ptr", [](ShmComm& c) { return reinterpret_cast<uintptr_t>(&c); })
@@ -145,6 +148,61 @@ PYBIND11_MODULE(_host, m) {
         if (!c.iprobe(source, tag, &s, &t, &n)) return py::none();
         return py::make_tuple(s, t, n);
       })
+      // ---- non-blocking collectives (None send buffer == IN_PLACE) ----
+      .def("ibarrier", [](ShmComm& c) {
+        py::gil_scoped_release g;
+        return c.ibarrier();
+      })
+      .def("ibcast", [](ShmComm& c, py::object buf, int root) {
+        Buf b = get_buf(buf, true);
+        py::gil_scoped_release g;
+        return c.ibcast(b.ptr, b.nbytes, root);
+      })
+      .def("iallreduce", [](ShmComm& c, py::object sbuf, py::object rbuf, int dt, int op) {
+        Buf s = get_buf(sbuf, false), r = get_buf(rbuf, true);
+        if (s.ptr && s.nbytes != r.nbytes) throw std::invalid_argument("ccmpi: Iallreduce buffer size mismatch");
+        py::gil_scoped_release g;
+        return c.iallreduce(s.ptr, r.ptr, r.nbytes / dtype_size(dt), dt, op);
+      })
+      .def("iallgather", [](ShmComm& c, py::object sbuf, py::object rbuf) {
+        Buf s = get_buf(sbuf, false), r = get_buf(rbuf, true);
+        if (r.nbytes % c.size()) throw std::invalid_argument("ccmpi: Iallgather receive buffer not divisible by comm size");
+        const size_t blk = r.nbytes / c.size();
+        if (s.ptr && s.nbytes != blk) throw std::invalid_argument("ccmpi: Iallgather send size != receive block");
+        py::gil_scoped_release g;
+        return c.iallgather(s.ptr, blk, r.ptr);
+      })
+      .def("ialltoall", [](ShmComm& c, py::object sbuf, py::object rbuf) {
+        Buf s = get_buf(sbuf, false), r = get_buf(rbuf, true);
+        if (r.nbytes % c.size()) throw std::invalid_argument("ccmpi: Ialltoall buffer not divisible by comm size");
+        if (s.ptr && s.nbytes != r.nbytes) throw std::invalid_argument("ccmpi: Ialltoall buffer size mismatch");
+        py::gil_scoped_release g;
+        return c.ialltoall(s.ptr, r.nbytes / c.size(), r.ptr);
+      })
+      .def("ireduce_scatter_block", [](ShmComm& c, py::object sbuf, py::object rbuf, int dt, int op) {
+        Buf s = get_buf(sbuf, false), r = get_buf(rbuf, true);
+        const size_t es = dtype_size(dt);
+        size_t count;
+        if (s.ptr) {
+          if (s.nbytes % (es * c.size())) throw std::invalid_argument("ccmpi: Ireduce_scatter_block send count not divisible by comm size");
+          count = s.nbytes / es / c.size();
+          if (r.nbytes < count * es) throw std::invalid_argument("ccmpi: Ireduce_scatter_block receive buffer too small");
+        } else {
+          if (r.nbytes % (es * c.size())) throw std::invalid_argument("ccmpi: Ireduce_scatter_block in-place buffer not divisible by comm size");
+          count = r.nbytes / es / c.size();
+        }
+        py::gil_scoped_release g;
+        return c.ireduce_scatter_block(s.ptr, r.ptr, count, dt, op);
+      })
+      .def("nb_test", [](ShmComm& c, const NbCollPtr& r) {
+        py::gil_scoped_release g;
+        return c.nb_test(r);
+      })
+      .def("nb_wait", [](ShmComm& c, const NbCollPtr& r) {
+        py::gil_scoped_release g;
+        c.nb_wait(r);
+      })
+      .def_property_readonly("nb_active", &ShmComm::nb_active)
       // ---- collectives on raw buffers (None send buffer == IN_PLACE) ----
       .def("bcast", [](ShmComm& c, py::object buf, int root) {
         Buf b = get_buf(buf, true);

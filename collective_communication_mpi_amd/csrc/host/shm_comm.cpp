@@ -492,7 +492,9 @@ bool ShmComm::progress() {
   for (int d = 0; d < size_; ++d)
     if (!send_q_[d].empty()) moved |= progress_send_(d);
   for (int s = 0; s < size_; ++s) moved |= progress_recv_(s);
-  // hand completed unexpected messages to receivers that bound to them
+  // advance started non-blocking collectives (nbcoll.cpp): a rank waiting on
+  // anything still forwards its collective rounds
+  if (!nb_active_.empty()) nb_progress_();
   return moved;
 }
 

@@ -50,6 +50,29 @@ void reduce_inplace(void* dst, const void* src, size_t n, int dt, int op);
 bool reduce_supported(int dt, int op);
 
 struct Segment;  // opaque shm layout
+class ShmComm;
+
+// A started non-blocking collective: a schedule of P2P rounds (nbcoll.cpp).
+class NbColl {
+ public:
+  virtual ~NbColl() = default;
+  // Post round k's messages; false when the schedule has no round k.
+  virtual bool post(ShmComm& c, int k) = 0;
+  // Local work once round k's messages completed.
+  virtual void finish(int /*k*/) {}
+
+  std::vector<std::shared_ptr<struct Request>> reqs;
+  int round = -1;
+  bool done = false;
+  std::string err;
+  int tag = 0;  // internal tag base; round k uses tag - k
+  std::vector<char> tmp;
+
+ protected:
+  void recv(ShmComm& c, void* b, size_t n, int src, int k);
+  void send(ShmComm& c, const void* b, size_t n, int dst, int k);
+};
+using NbCollPtr = std::shared_ptr<NbColl>;
 
 struct Request {
   enum Kind { SEND, RECV } kind;
@@ -137,6 +160,20 @@ class ShmComm : public std::enable_shared_from_this<ShmComm> {
                  const std::vector<size_t>& rcounts, const std::vector<size_t>& rdispls);
   void scan(const void* sbuf, void* rbuf, size_t count, int dt, int op, bool exclusive);
 
+  // ---- non-blocking collectives (nbcoll.cpp): schedules of P2P rounds on
+  // internal tags, advanced by every progress() call until complete
+  NbCollPtr ibarrier();
+  NbCollPtr ibcast(void* buf, size_t nbytes, int root);
+  NbCollPtr iallreduce(const void* sbuf, void* rbuf, size_t count, int dt, int op);
+  NbCollPtr iallgather(const void* sbuf, size_t nbytes, void* rbuf);
+  NbCollPtr ialltoall(const void* sbuf, size_t block_bytes, void* rbuf);
+  // sbuf == nullptr: in place, rbuf holds the p*count input and receives block rank()
+  NbCollPtr ireduce_scatter_block(const void* sbuf, void* rbuf, size_t count, int dt, int op);
+  bool nb_test(const NbCollPtr& c);
+  void nb_wait(const NbCollPtr& c);
+  size_t nb_active() const { return nb_active_.size(); }
+  RequestPtr isend_internal(const void* buf, size_t nbytes, int dest, int tag);  // tag < 0
+
   // Collective: split by (color, key).  Returns nullptr for color < 0 (UNDEFINED).
   std::shared_ptr<ShmComm> split(int color, int key);
   std::shared_ptr<ShmComm> dup() { return split(0, rank_); }
@@ -162,6 +199,9 @@ class ShmComm : public std::enable_shared_from_this<ShmComm> {
   bool progress_recv_(int src);
   void backoff_(uint64_t& spins);
   [[noreturn]] void timeout_(const char* what);
+  NbCollPtr nb_start_(NbCollPtr c);
+  bool nb_advance_(NbColl& c);
+  void nb_progress_();
 
   std::string name_;
   int rank_, size_;
@@ -191,6 +231,11 @@ class ShmComm : public std::enable_shared_from_this<ShmComm> {
   char* slot_base_ = nullptr;
   char* result_base_ = nullptr;
   std::vector<uint64_t> peer_tail_;  // last tail read from each out-channel's consumer
+
+  // started non-blocking collectives (held until complete), tag sequence
+  std::vector<NbCollPtr> nb_active_;
+  uint64_t nb_seq_ = 0;
+  bool nb_in_progress_ = false;
 };
 
 double wtime();

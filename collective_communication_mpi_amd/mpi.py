@@ -362,6 +362,9 @@ class Request:
             if not r._done and r._native is not None:
                 if type(r._native) is int:
                     handles.append(r._native)
+                elif not isinstance(r._native, _h.Request):
+                    continue  # collective / device request: finished below (collective
+                    # rounds advance during the other waits)
                 else:
                     groups.setdefault(id(r._comm), (r._comm, []))[1].append(r._native)
         if handles:
@@ -385,6 +388,31 @@ class Request:
     @staticmethod
     def Testall(requests: Sequence["Request"], statuses=None) -> bool:
         return all(r.Test() for r in requests if r is not None)
+
+
+class _CollRequest(Request):
+    """Request of a non-blocking collective (``Comm.Iallreduce`` & co.,
+    csrc/host/nbcoll.cpp): a schedule of P2P rounds that every progress call on
+    the communicator advances; ``Wait`` finishes it."""
+
+    __slots__ = ()
+
+    def _finish(self, status: Optional[Status]):
+        if not self._done:
+            self._comm._hc.nb_wait(self._native)
+            self._done = True
+            self._keep = None
+            if self._decode is not None:
+                self._result = self._decode()
+        return self._result
+
+    def Test(self, status: Optional[Status] = None) -> bool:
+        if self._done:
+            return True
+        if self._comm._hc.nb_test(self._native):
+            self._finish(status)
+            return True
+        return False
 
 
 # --------------------------------------------------------------------------
@@ -659,6 +687,34 @@ class Comm:
             return
         s, r = _parse(sendbuf, False), _parse(recvbuf, True)
         self._hc.alltoall(_raw(s), r.arr)
+
+    # -- non-blocking collectives (MPI-3; csrc/host/nbcoll.cpp) ------------------
+    # Buffers must stay untouched until the request completes; the request keeps
+    # them referenced.  Every rank starts the same collectives in the same order.
+    def Ibarrier(self) -> Request:
+        return _CollRequest(self, self._hc.ibarrier(), None)
+
+    def Ibcast(self, buf, root: int = 0) -> Request:
+        b = _parse(buf, True)
+        return _CollRequest(self, self._hc.ibcast(b.arr, root), b.arr)
+
+    def Iallreduce(self, sendbuf, recvbuf, op: Op = SUM) -> Request:
+        s, r = _parse(sendbuf, False), _parse(recvbuf, True)
+        if s is not None and s.arr.dtype != r.arr.dtype:
+            s = _parse(s.arr.astype(r.arr.dtype), False)
+        return _CollRequest(self, self._hc.iallreduce(_raw(s), r.arr, r.dt, op.code), (_raw(s), r.arr))
+
+    def Iallgather(self, sendbuf, recvbuf) -> Request:
+        s, r = _parse(sendbuf, False), _parse(recvbuf, True)
+        return _CollRequest(self, self._hc.iallgather(_raw(s), r.arr), (_raw(s), r.arr))
+
+    def Ialltoall(self, sendbuf, recvbuf) -> Request:
+        s, r = _parse(sendbuf, False), _parse(recvbuf, True)
+        return _CollRequest(self, self._hc.ialltoall(_raw(s), r.arr), (_raw(s), r.arr))
+
+    def Ireduce_scatter_block(self, sendbuf, recvbuf, op: Op = SUM) -> Request:
+        s, r = _parse(sendbuf, False), _parse(recvbuf, True)
+        return _CollRequest(self, self._hc.ireduce_scatter_block(_raw(s), r.arr, r.dt, op.code), (_raw(s), r.arr))
 
     def Alltoallv(self, sendbuf, recvbuf) -> None:
         s, r = _parse(sendbuf, False), _parse(recvbuf, True)

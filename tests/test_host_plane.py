@@ -14,6 +14,16 @@ def test_host_plane_all_ops(n):
     assert "host plane OK" in r.stdout
 
 
+@pytest.mark.parametrize("n", [1, 2, 3, 5, 8])
+def test_nonblocking_collectives(n):
+    """MPI-3 Ibarrier/Ibcast/Iallreduce/Iallgather/Ialltoall/Ireduce_scatter_block
+    (csrc/host/nbcoll.cpp) and the Communicator I* façade: results, in-place forms,
+    many in flight, progress inside unrelated waits, mixed Waitall."""
+    r = run_ranks(n, py("tests/workers/nb_worker.py"), timeout=240,
+                  env={"CCMPI_RING_BYTES": str(16 << 10)})
+    assert f"nonblocking collectives OK ({n} ranks)" in r.stdout
+
+
 def test_mpi_test_cli_cases():
     for case in ["allreduce", "allgather", "reduce_scatter", "split", "alltoall"]:
         r = run_ranks(8, py("mpi-test.py", "--test_case", case), timeout=120)

@@ -29,6 +29,7 @@ import os
 import sys
 import time
 
+import numpy as np
 import torch
 
 sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", ".."))
@@ -355,6 +356,20 @@ def async_ops():
     ncheck += 1
     if not w.is_completed():
         fails.append("async: is_completed() false after synchronize()")
+    # MPI-style façade: Communicator.I* on CUDA tensors -> DeviceRequest, completed by
+    # Request.Waitall together with a host-plane non-blocking collective
+    x, y = gen(rank, n, torch.float32, 93200), dev.empty(n, torch.float32)
+    xa, ya = gen(rank, n * p, torch.float32, 93201), torch.empty(n * p, device=D)
+    hx, hy = np.full(4, rank, np.int64), np.zeros(4, np.int64)
+    reqs = [comm.Iallreduce(x, y, MPI.SUM), comm.Ialltoall(xa, ya), comm.comm.Iallreduce(hx, hy, MPI.SUM)]
+    MPI.Request.Waitall(reqs)
+    check("facade_Iallreduce", y, oracle(n, torch.float32, "SUM", 93200), torch.float32, p)
+    check("facade_Ialltoall", ya,
+          torch.cat([gen(r, n * p, torch.float32, 93201)[rank * n:(rank + 1) * n] for r in range(p)]).double(),
+          torch.float32)
+    ncheck += 1
+    if not np.array_equal(hy, np.full(4, p * (p - 1) // 2)):
+        fails.append("facade: host Iallreduce mixed with device requests")
 
 
 def tuning():
