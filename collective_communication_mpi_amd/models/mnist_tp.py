@@ -54,6 +54,7 @@ kernel; the optimizer is one fused AdamW pass.  Fusions that remove whole passes
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass
 from typing import Optional
 
@@ -433,7 +434,7 @@ class MnistTPLayer:
         With ``tp_chunks = c > 1`` the batch is cut into c row blocks and each
         block runs attention -> fc_o GEMM on the main stream, then hands its
         partial z to the TP all-reduce (hand-written kernel, symmetric buffer,
-        ``overlap_blocks`` CTAs) on a high-priority side stream: block i's
+        ``overlap_blocks`` CTAs) on a normal-priority side stream: block i's
         all-reduce runs under block i+1's attention.  Fork/join by events, so
         the whole pipeline is captured into the step's HIP graph."""
         cfg = self.cfg
@@ -450,7 +451,10 @@ class MnistTPLayer:
             return z
         main = torch.cuda.current_stream(self.device)
         if "tp_side" not in self._bufs:
-            self._bufs["tp_side"] = torch.cuda.Stream(self.device, priority=-1)
+            # CCMPI_TP_STREAM_PRIORITY: 0 = normal (default: 3-24x faster than -1 with 2 ranks
+            # sharing a GPU, profiles/r2_overlap/tp2_priority.md), -1 = high priority
+            prio = int(os.environ.get("CCMPI_TP_STREAM_PRIORITY", "0"))
+            self._bufs["tp_side"] = torch.cuda.Stream(self.device, priority=prio)
         side = self._bufs["tp_side"]
         D = _native.device()
         hl, Bc = self.hl, B // c
