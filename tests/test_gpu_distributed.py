@@ -40,6 +40,15 @@ def test_device_collectives_random_skew(n):
     assert "0 failures" in r.stdout
 
 
+def test_device_collectives_serialized_launches():
+    """the quick matrix with every kernel launch serialized
+    (AMD_SERIALIZE_KERNEL=3 / AMD_SERIALIZE_COPY=3, HIP's CUDA_LAUNCH_BLOCKING): the flag
+    protocol may not depend on launch overlap within a rank."""
+    r = run_ranks(2, py("tests/workers/device_worker.py", "--matrix", "quick", "--sizes", "1,1000,65539"),
+                  timeout=300, env=dict(ENV, AMD_SERIALIZE_KERNEL="3", AMD_SERIALIZE_COPY="3"))
+    assert "0 failures" in r.stdout
+
+
 def test_trace_records_collectives_and_survives_graph_capture(tmp_path):
     """CCMPI_TRACE=1 over the quick matrix (which also captures collectives in HIP
     graphs): one JSON record per eager call per rank, with device time and bandwidths;

@@ -407,7 +407,10 @@ def _lap(label):
 
 _lap("setup")
 if args.matrix:
-    for fn in (determinism, graphs) + ((tuning,) if args.matrix == "quick" else ()):
+    # serialized launches (AMD_SERIALIZE_KERNEL, HIP's CUDA_LAUNCH_BLOCKING) synchronise
+    # around every kernel, which stream capture forbids: graphs are skipped there
+    serialized = os.environ.get("AMD_SERIALIZE_KERNEL", "0") not in ("", "0")
+    for fn in (determinism,) + (() if serialized else (graphs,)) + ((tuning,) if args.matrix == "quick" else ()):
         t_s = time.time()
         fn()
         if rank == 0 and os.environ.get("CCMPI_WORKER_VERBOSE") == "1":
