@@ -81,7 +81,8 @@ PYBIND11_MODULE(_host, m) {
       .def_property_readonly("status", [](const RequestPtr& r) { return status_of(r); });
 
   // opaque handle of a started non-blocking collective (nbcoll.cpp)
-  py::class_<NbColl, NbCollPtr>(m, "CollRequest");
+  py::class_<NbColl, NbCollPtr>(m, "CollRequest")
+      .def_property_readonly("done", [](const NbColl& c) { return c.done; });
 
   py::class_<ShmComm, std::shared_ptr<ShmComm>>(m, "HostComm")
       .def_static("world", &ShmComm::world, py::call_guard<py::gil_scoped_release>())

@@ -669,6 +669,13 @@ class DeviceGroup:
         ready = torch.cuda.Event()
         ready.record(torch.cuda.current_stream(self.device))
         stream.wait_event(ready)
+        if stream != torch.cuda.current_stream(self.device):
+            # a caller that drops the Work unwaited must not see the caching allocator
+            # hand these blocks out while the collective still reads/writes them
+            # (no-op for symmetric-heap tensors, which are not allocator blocks)
+            for t in args:
+                if isinstance(t, torch.Tensor) and t.is_cuda:
+                    t.record_stream(stream)
         with torch.cuda.stream(stream):
             if op in ("allreduce", "allgather", "alltoall", "reduce_scatter"):
                 kw.setdefault("max_blocks", self.overlap_blocks)  # runs beside compute

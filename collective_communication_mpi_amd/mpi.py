@@ -434,6 +434,7 @@ class Comm:
         self._p = native.ptr  # raw pointer for the fastcall entry points (lives as long as _hc)
         self._rank = native.rank
         self._size = native.size
+        self._nb_keep = []  # (started collective, its buffers) until the schedule is done
 
     # -- identity ----------------------------------------------------------
     def Get_rank(self) -> int:
@@ -691,30 +692,38 @@ class Comm:
     # -- non-blocking collectives (MPI-3; csrc/host/nbcoll.cpp) ------------------
     # Buffers must stay untouched until the request completes; the request keeps
     # them referenced.  Every rank starts the same collectives in the same order.
+    def _nb(self, native, keep) -> Request:
+        # the communicator keeps the buffers alive until the schedule finished, even
+        # if the caller drops the request unwaited (its rounds keep progressing)
+        pend = [e for e in self._nb_keep if not e[0].done] if self._nb_keep else []
+        pend.append((native, keep))
+        self._nb_keep = pend
+        return _CollRequest(self, native, keep)
+
     def Ibarrier(self) -> Request:
-        return _CollRequest(self, self._hc.ibarrier(), None)
+        return self._nb(self._hc.ibarrier(), None)
 
     def Ibcast(self, buf, root: int = 0) -> Request:
         b = _parse(buf, True)
-        return _CollRequest(self, self._hc.ibcast(b.arr, root), b.arr)
+        return self._nb(self._hc.ibcast(b.arr, root), b.arr)
 
     def Iallreduce(self, sendbuf, recvbuf, op: Op = SUM) -> Request:
         s, r = _parse(sendbuf, False), _parse(recvbuf, True)
         if s is not None and s.arr.dtype != r.arr.dtype:
             s = _parse(s.arr.astype(r.arr.dtype), False)
-        return _CollRequest(self, self._hc.iallreduce(_raw(s), r.arr, r.dt, op.code), (_raw(s), r.arr))
+        return self._nb(self._hc.iallreduce(_raw(s), r.arr, r.dt, op.code), (_raw(s), r.arr))
 
     def Iallgather(self, sendbuf, recvbuf) -> Request:
         s, r = _parse(sendbuf, False), _parse(recvbuf, True)
-        return _CollRequest(self, self._hc.iallgather(_raw(s), r.arr), (_raw(s), r.arr))
+        return self._nb(self._hc.iallgather(_raw(s), r.arr), (_raw(s), r.arr))
 
     def Ialltoall(self, sendbuf, recvbuf) -> Request:
         s, r = _parse(sendbuf, False), _parse(recvbuf, True)
-        return _CollRequest(self, self._hc.ialltoall(_raw(s), r.arr), (_raw(s), r.arr))
+        return self._nb(self._hc.ialltoall(_raw(s), r.arr), (_raw(s), r.arr))
 
     def Ireduce_scatter_block(self, sendbuf, recvbuf, op: Op = SUM) -> Request:
         s, r = _parse(sendbuf, False), _parse(recvbuf, True)
-        return _CollRequest(self, self._hc.ireduce_scatter_block(_raw(s), r.arr, r.dt, op.code), (_raw(s), r.arr))
+        return self._nb(self._hc.ireduce_scatter_block(_raw(s), r.arr, r.dt, op.code), (_raw(s), r.arr))
 
     def Alltoallv(self, sendbuf, recvbuf) -> None:
         s, r = _parse(sendbuf, False), _parse(recvbuf, True)

@@ -152,6 +152,20 @@ if p > 1:
     check(np.array_equal(rb, np.full(3, (rank - 1) % p)) and np.array_equal(ar, np.full(5, p * (p - 1) // 2)),
           "Waitall mixed")
 
+# ---- a request dropped unwaited: the communicator keeps its buffers alive and later
+# waits keep progressing it to completion (no use-after-free, nothing left active)
+import gc  # noqa: E402
+
+comm.Iallreduce(np.arange(100000, dtype=np.float64) * (rank + 1), np.zeros(100000), MPI.SUM)
+gc.collect()
+junk = [np.full(100000, 7.0) for _ in range(8)]  # reuse freed memory if it had been freed
+for _ in range(1000):
+    comm.Ibarrier().Wait()
+    if comm.allreduce(comm._hc.nb_active, op=MPI.MAX) == 0:  # collective exit decision
+        break
+check(comm._hc.nb_active == 0, "dropped request never completed")
+del junk
+
 # ---- Communicator façade: same results and byte accounting as the blocking calls
 cm = Communicator(comm)
 x = data(rank, 1000, "float32", 30)
