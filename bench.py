@@ -62,6 +62,8 @@ def parse():
     ap.add_argument("--algo", default="auto", help="auto | twoshot | push | ring | rhd | oneshot | rccl | ...")
     ap.add_argument("--tp", type=int, default=0, help="TP degree of the harness step (default 2 if N>=2)")
     ap.add_argument("--batch", type=int, default=2048, help="images per DP replica for the harness step")
+    ap.add_argument("--fc-o-mode", default="token", choices=["token", "row"],
+                    help="harness fc_o: per-token row-parallel (reference shape) or pooled")
     ap.add_argument("--dp-layers", type=int, default=32, help="Llama-3-8B layers of the DP-overlap measurement")
     ap.add_argument("--dp-tokens", type=int, default=4096)
     ap.add_argument("--a2a-mb", type=int, default=256)
@@ -284,17 +286,26 @@ def main() -> int:
         from collective_communication_mpi_amd.models.harness import bench_forward
 
         tp = args.tp or (2 if world >= 2 and world % 2 == 0 else 1)
-        harness = bench_forward(comm, tp=tp, batch=args.batch, steps=args.steps, warmup=args.warmup)
-        if tp > 1 and not args.no_secondary:
-            # per-token row-parallel fc_o: the TP all-reduce carries B*S x 16 partial outputs;
-            # 4 row blocks pipeline it under the fc_o GEMM on a side stream (1 block = no overlap)
-            tok = {}
-            for chunks in (1, 4):
+        # headline: the reference's layer shape -- per-token row-parallel fc_o with (B, S, out)
+        # outputs (reference model/func_impl.py:94-109), so the TP all-reduce carries
+        # B*S x 16 partial outputs every step
+        harness = bench_forward(comm, tp=tp, batch=args.batch, steps=args.steps, warmup=args.warmup,
+                                fc_o_mode=args.fc_o_mode)
+        harness["tp_allreduce_bytes"] = (args.batch * 16 * 16 * 4 if args.fc_o_mode == "token" else args.batch * 16 * 4) \
+            if tp > 1 else 0
+        if not args.no_secondary:
+            # the other fc_o forms: pooled row-parallel (B x 16 TP all-reduce), and the token
+            # pipeline in 4 row blocks whose all-reduces run on a side stream under the next
+            # block's attention
+            other = {}
+            variants = [("pooled", "row", 1)] if args.fc_o_mode == "token" else [("token", "token", 1)]
+            if tp > 1:
+                variants.append(("token_chunks4", "token", 4))
+            for name, mode, chunks in variants:
                 r = bench_forward(comm, tp=tp, batch=args.batch, steps=args.steps, warmup=args.warmup, train=False,
-                                  fc_o_mode="token", tp_chunks=chunks)
-                tok[f"chunks{chunks}_fwd_ms"] = round(r["fwd_ms"], 4)
-            tok["tp_allreduce_bytes"] = args.batch * 16 * 16 * 4
-            harness["token_fc_o"] = tok
+                                  fc_o_mode=mode, tp_chunks=chunks)
+                other[f"{name}_fwd_ms"] = round(r["fwd_ms"], 4)
+            harness["fc_o_variants"] = other
 
     dry = None
     if world == 1 and args.shared_dry_run > 1 and not args.no_secondary and torch.cuda.device_count() >= 1:
@@ -317,7 +328,7 @@ def main() -> int:
             "dtype": "fp32",
             "data": "synthetic (rank-valued 1 GiB fp32 buffer; MNIST-shaped random images, random-init weights)",
             "config": {
-                "model": "allreduce-1GiB-fp32 + MNIST-shaped TP transformer layer (768->256 qkv, 256->10 fc_o)",
+                "model": "allreduce-1GiB-fp32 + MNIST-shaped TP transformer layer (768->256 qkv, 256->10 fc_o per token)",
                 "global_batch": (harness or {}).get("global_batch"),
                 "seq_len": (harness or {}).get("seq_len"),
                 "parallelism": f"dp{dp}xtp{tp}" if harness else f"allreduce-world{world}",

@@ -1,7 +1,7 @@
 """Run the harness forward (eager, no graph) or full train step N times, for
 rocprofv3 kernel statistics.
 
-    python benchmarks/harness_steps.py --mode fwd|train --steps 20 [--tp 1 --batch 2048]
+    python benchmarks/harness_steps.py --mode fwd|train --steps 20 [--tp 1 --batch 2048 --fc-o-mode token]
 """
 import argparse
 import os
@@ -19,10 +19,11 @@ ap.add_argument("--mode", default="fwd")
 ap.add_argument("--steps", type=int, default=20)
 ap.add_argument("--tp", type=int, default=1)
 ap.add_argument("--batch", type=int, default=2048)
+ap.add_argument("--fc-o-mode", default="row", choices=["row", "token", "naive"])
 args = ap.parse_args()
 comm = Communicator(MPI.COMM_WORLD)
 torch.cuda.set_device(int(os.environ.get("CCMPI_LOCAL_RANK", "0")) % torch.cuda.device_count())
-cfg, layer, x_all, y_all = build(comm, args.tp, args.batch)
+cfg, layer, x_all, y_all = build(comm, args.tp, args.batch, fc_o_mode=args.fc_o_mode)
 xb, yb = local_batch(cfg, x_all, y_all, 0, comm.Get_rank(), layer.device)
 for _ in range(args.steps):
     if args.mode == "fwd":

@@ -46,7 +46,8 @@ def build(comm, tp: int, batch: int, **kw):
 def train_step(layer: MnistTPLayer, cfg: LayerConfig, xb, yb):
     logits = layer.forward_images(xb, xb.shape[0])  # patchify + forward (cfg.fwd_chunks streams)
     layer.zero_grad()
-    if layer._fused_fc_o() or (cfg.fc_o_mode == "row" and cfg.tp > 1):
+    if layer._fused_fc_o() or (cfg.fc_o_mode == "row" and cfg.tp > 1) or \
+            (cfg.fc_o_mode == "token" and layer._fused_fc_o_bwd()):
         loss = layer.loss_and_grad_fused(yb, cfg.batch * cfg.dp)  # one kernel: loss, dZ, d o_b
         layer.backward(None)
     else:

@@ -187,7 +187,7 @@ class MnistTPLayer:
         # gradient and the in-kernel dpool read neither), and the transposed tiles are
         # the slow part of the AdamW kernel
         transposed = [n for n, used in (("qkv_w", cfg.emb_grad == "dh" and cfg.plain_gemm == "own"),
-                                         ("o_w", not self._fused_fc_o())) if used]
+                                         ("o_w", not self._fused_fc_o_bwd())) if used]
         self.flat = FlatParams(specs, self.device, grad_alloc, transposed=transposed)
         self.buckets = GradBuckets(self.flat, self.dp_dev, [["o_w", "o_b"], ["qkv_w", "qkv_b"],
                                                             ["emb_w"]],
@@ -313,7 +313,8 @@ class MnistTPLayer:
         st = torch.cuda.current_stream(self.device).cuda_stream
         naive = cfg.fc_o_mode == "naive" and cfg.tp > 1
         token = cfg.fc_o_mode == "token"
-        pool = None if (naive or token) else self._buf("pool", (B, self.hd), torch.bfloat16)
+        tok_fused = token and self._fused_fc_o_bwd()
+        pool = None if (naive or (token and not tok_fused)) else self._buf("pool", (B, self.hd), torch.bfloat16)
         # the per-token attention output is only consumed by the naive fc_o; the pooled
         # path (and the MFMA backward, which never reads O) skip materializing it
         mfma_attn = S <= 16 and cfg.head_dim in (32, 64, 128)
@@ -339,8 +340,15 @@ class MnistTPLayer:
             z = self._forward_naive_fc_o(att, B)
             logits = z.view(B, S, cfg.out_pad)[:, :, : cfg.n_classes].mean(dim=1)
         elif token:
-            z = self._forward_token_fc_o(att, B, qkv=qkv, lse=lse)
-            logits = z.view(B, S, cfg.out_pad)[:, :, : cfg.n_classes].mean(dim=1)  # o_b is in z (TP rank 0)
+            z = self._forward_token_fc_o(att, B, qkv=qkv, lse=lse, pool=pool)
+            if tok_fused:
+                # logits = mean over the S tokens of the all-reduced z (o_b is in z, TP rank 0),
+                # kept in zp for the fused loss head
+                zp = self._buf("zp", (B, cfg.out_pad), torch.float32, self.tp_dev)
+                torch.mean(z.view(B, S, cfg.out_pad), dim=1, out=zp)
+                logits = zp[:, : cfg.n_classes]
+            else:
+                logits = z.view(B, S, cfg.out_pad)[:, :, : cfg.n_classes].mean(dim=1)
         else:
             # fc_o and the mean over patches are linear: pool first (fused in the
             # attention kernel), so fc_o and its TP all-reduce work on B rows, not B*S
@@ -427,7 +435,7 @@ class MnistTPLayer:
         c = max(1, int(self.cfg.tp_chunks)) if self.tp_dev is not None else 1
         return c if (B % c == 0 and (B // c) * self.cfg.seq >= 256) else 1
 
-    def _forward_token_fc_o(self, att, B, qkv=None, lse=None):
+    def _forward_token_fc_o(self, att, B, qkv=None, lse=None, pool=None):
         """Row-parallel fc_o per token: z = att . W_o[:, shard]^T (+ o_b on TP rank 0),
         summed over the TP group (B*S x 16 fp32 partial outputs).
 
@@ -462,7 +470,8 @@ class MnistTPLayer:
             b0, b1 = i * Bc, (i + 1) * Bc
             r0, r1 = b0 * S, b1 * S
             D.attn_small_fwd(qkv[r0:r1].data_ptr(), att[r0:r1].data_ptr(), lse[b0 * hl:b1 * hl].data_ptr(), Bc, S, hl,
-                             cfg.head_dim, qkv.stride(0), att.stride(0), 1.0 / math.sqrt(cfg.head_dim), 0, 0,
+                             cfg.head_dim, qkv.stride(0), att.stride(0), 1.0 / math.sqrt(cfg.head_dim),
+                             0 if pool is None else pool[b0:b1].data_ptr(), 0 if pool is None else pool.stride(0),
                              main.cuda_stream)
             gemm_nt(att[r0:r1], wo, out=z[r0:r1], out_dtype=torch.float32, splitk=1, bias=bias)
             side.wait_stream(main)
@@ -472,8 +481,17 @@ class MnistTPLayer:
         return z
 
     def _fused_fc_o(self) -> bool:
+        return self.cfg.fc_o_mode != "token" and self._fused_fc_o_bwd()
+
+    def _fused_fc_o_bwd(self) -> bool:
+        """The fc_o input gradient formed inside the attention backward, from the
+        (B x out) head gradient and W_o.  Also legal for the per-token fc_o: its loss
+        reads the mean over the S tokens of z, so dZ[b, s] = dlogits[b] / S for every
+        s and dW_o = sum_s dZ^T att = dlogits^T pool / S -- the same products as the
+        pooled form, without the B*S x out dZ, the dW_o GEMM over B*S rows and the
+        B*S x hd dAtt.  The forward still produces and all-reduces every token's z."""
         cfg = self.cfg
-        return (cfg.fuse_fc_o and not (cfg.fc_o_mode == "naive" and cfg.tp > 1) and cfg.fc_o_mode != "token"
+        return (cfg.fuse_fc_o and not (cfg.fc_o_mode == "naive" and cfg.tp > 1)
                 and cfg.seq <= 16
                 and cfg.head_dim in (32, 64, 128) and 4 % self.hl == 0 and cfg.out_pad <= 16)
 
@@ -550,7 +568,7 @@ class MnistTPLayer:
         fused = dlogits is None
         if not fused:
             G("o_b")[: cfg.n_classes].add_(dlogits.sum(0))
-        if (cfg.fc_o_mode == "naive" and cfg.tp > 1) or cfg.fc_o_mode == "token":
+        if (cfg.fc_o_mode == "naive" and cfg.tp > 1) or (cfg.fc_o_mode == "token" and not self._fused_fc_o_bwd()):
             dz = self._buf("dz", (M, cfg.out_pad), torch.bfloat16)
             dz.zero_()
             dz.view(B, S, cfg.out_pad)[:, :, : cfg.n_classes] = (dlogits / S).unsqueeze(1).to(torch.bfloat16)
@@ -573,7 +591,7 @@ class MnistTPLayer:
             # dW_o = dZ^T . pooled: 16 x hd over B rows, latency-bound; 32 K-splits measured fastest
             # (benchmarks/tn_small.py: 9.6 us at 8 splits, 7.2 us at 32)
             gemm_tn(dzp, pool, out=G("o_w"), accumulate=True, splitk=max(1, min(32, B // 64)))
-            if self._fused_fc_o():
+            if self._fused_fc_o_bwd():
                 dout, dout_b, dout_r = None, 0, 0                   # dpool formed inside the attention bwd
             else:
                 dpool = self._buf("dpool", (B, self.hd), torch.bfloat16)

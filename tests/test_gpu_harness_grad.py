@@ -70,6 +70,48 @@ def test_harness_grads_match_torch_fp32(emb_grad, qkv_grad, fused, fuse_fc_o, fo
         assert err < 4e-2, f"{emb_grad}: grad {k} rel err {err:.3e}"
 
 
+@pytest.mark.parametrize("fuse_fc_o,fused_head", [(True, True), (True, False), (False, False)])
+def test_token_fc_o_grads_match_torch_fp32(fuse_fc_o, fused_head):
+    """Per-token fc_o (the reference's (B, S, out) layer shape): fused loss head + in-kernel
+    fc_o backward (fuse_fc_o) and the dZ / dW_o / dAtt GEMM backward both match fp32
+    autograd (the mean over tokens of z equals fc_o of the pooled features); the eager loss
+    head (dlogits given to backward) also takes the in-kernel backward when it is legal."""
+    from collective_communication_mpi_amd import MPI, Communicator
+    from collective_communication_mpi_amd.models.harness import build
+    from collective_communication_mpi_amd.models.mnist_tp import local_batch, patchify
+
+    comm = Communicator(MPI.COMM_WORLD)
+    cfg, layer, x_all, y_all = build(comm, 1, 128, fc_o_mode="token", fuse_fc_o=fuse_fc_o)
+    assert layer._fused_fc_o_bwd() == fuse_fc_o
+    g = torch.Generator().manual_seed(11)
+    layer.flat.param("qkv_b").copy_(torch.randn(layer.flat.param("qkv_b").shape, generator=g) * 0.1)
+    ob = torch.zeros(cfg.out_pad)
+    ob[: cfg.n_classes] = torch.randn(cfg.n_classes, generator=g) * 0.1
+    layer.flat.param("o_b").copy_(ob)
+    layer.flat.refresh_bf16()
+    xb, yb = local_batch(cfg, x_all, y_all, 0, 0, layer.device)
+    xp = patchify(xb, cfg, out=layer.input_buffer(cfg.batch))
+    logits = layer.forward(xp, cfg.batch)
+    layer.zero_grad()
+    if fused_head:
+        loss = layer.loss_and_grad_fused(yb, cfg.batch)
+        layer.backward(None)
+    else:
+        loss, dlogits = layer.loss_and_grad(logits, yb, cfg.batch)
+        layer.backward(dlogits)
+    torch.cuda.synchronize()
+    names = ["emb_w", "qkv_w", "qkv_b", "o_w", "o_b"]
+    P = {k: layer.flat.param(k).detach().clone() for k in names}
+    for k in ("emb_w", "qkv_w", "o_w"):
+        P[k] = P[k].bfloat16().float()
+    ref_loss, ref = _reference(cfg, xp.float(), yb, P)
+    assert abs(loss.item() - ref_loss.item()) < 2e-2 * max(1.0, abs(ref_loss.item())), (loss.item(), ref_loss.item())
+    for k in names:
+        got = layer.flat.grad(k).detach().float()
+        err = (got - ref[k]).norm() / ref[k].norm().clamp_min(1e-12)
+        assert err < 4e-2, f"token fuse_fc_o={fuse_fc_o} fused_head={fused_head}: grad {k} rel err {err:.3e}"
+
+
 @pytest.mark.parametrize("chunks", [2, 4])
 def test_chunked_multistream_forward_is_bitwise_identical(chunks):
     """forward_images on c HIP streams == the single-stream forward: logits and the saved
