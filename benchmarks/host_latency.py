@@ -7,7 +7,8 @@ Per op: median and p10 over ``--reps`` repetitions of ``--iters`` back-to-back
 calls (no barrier inside the timed loop; one barrier before each repetition).
 Ops: one-way Send/Recv latency between ranks 0 and 1 (ping-pong / 2), Barrier,
 Allreduce (library path), myAllreduce (reference reduce->bcast schedule, plus
-ring and rhd), Alltoall and myAlltoall/myAlltoall2, all on the float32 buffer
+ring and rhd), Alltoall and myAlltoall/myAlltoall2, the non-blocking
+Iallreduce/Ialltoall/Ibarrier (+ Wait), all on the float32 buffer
 of ``--count`` elements (alltoall: ``--count`` per rank in total).  Rank 0
 prints one JSON line.
 """
@@ -67,6 +68,10 @@ for algo in ("reduce_bcast", "ring", "rhd"):
 res["Alltoall"] = timeit(lambda: C.Alltoall(xa, ya))
 res["myAlltoall"] = timeit(lambda: C.myAlltoall(xa, ya), args.iters // 4)
 res["myAlltoall2"] = timeit(lambda: C.myAlltoall2(xa, ya), args.iters // 4)
+# MPI-3 non-blocking collectives (csrc/host/nbcoll.cpp), started and waited at once
+res["Iallreduce+Wait"] = timeit(lambda: comm.Iallreduce(x, y, MPI.SUM).Wait(), args.iters // 4)
+res["Ialltoall+Wait"] = timeit(lambda: comm.Ialltoall(xa, ya).Wait(), args.iters // 4)
+res["Ibarrier+Wait"] = timeit(lambda: comm.Ibarrier().Wait(), args.iters // 4)
 if rank == 0:
     print(json.dumps({"bench": "host_latency", "ranks": p, "count": args.count, "dtype": "float32",
                       "cpus": os.cpu_count(), "results_us": res}), flush=True)
