@@ -92,6 +92,9 @@ class Work:
         the collective's output tensor."""
         torch = self.group.torch
         torch.cuda.current_stream(self.group.device).wait_event(self.done)
+        pend = self.group._async_done
+        if pend is not None and pend[1] is self.done:
+            self.group._async_done = None  # the current stream is now ordered after it
         self._keep = None
         return self.result
 
@@ -176,6 +179,7 @@ class DeviceGroup:
         keys = host_comm.allgather(key)
         self.ranks_per_device = keys.count(key)
         self.shared_device = self.ranks_per_device > 1
+        self._async_done = None  # (stream, event) of the last start()ed collective, until ordered
         default_blocks = max(1, 512 // self.ranks_per_device)
         self.max_blocks = _env_int("CCMPI_MAX_BLOCKS", default_blocks)
         # CTA budget of collectives that run NEXT TO compute (DP gradient buckets, TP
@@ -377,7 +381,20 @@ class DeviceGroup:
 
     # ----------------------------------------------------------------- helpers
     def _stream(self) -> int:
-        return self.torch.cuda.current_stream(self.device).cuda_stream
+        cur = self.torch.cuda.current_stream(self.device)
+        if self._async_done is not None and self._async_done[0] != cur.cuda_stream:
+            self._order_after_async(cur)
+        return cur.cuda_stream
+
+    def _order_after_async(self, cur) -> None:
+        """A collective issued on another stream than the last ``start()``ed one waits
+        for it on the device: one collective of a group at a time (they share the
+        per-CTA epochs, flags and the staging scratch), while compute on that stream
+        still overlaps the started collective."""
+        if self.torch.cuda.is_current_stream_capturing():
+            raise RuntimeError("wait() on the started collective before capturing another collective of this group")
+        cur.wait_event(self._async_done[1])
+        self._async_done = None
 
     def _check(self, t, name: str):
         if not (hasattr(t, "is_cuda") and t.is_cuda):
@@ -682,6 +699,7 @@ class DeviceGroup:
             out = fn(*args, **kw)
             done = torch.cuda.Event()
             done.record(stream)
+        self._async_done = (stream.cuda_stream, done)
         return Work(self, done, out, args)
 
     # ------------------------------------------------------------------ health

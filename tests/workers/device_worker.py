@@ -356,6 +356,16 @@ def async_ops():
     ncheck += 1
     if not w.is_completed():
         fails.append("async: is_completed() false after synchronize()")
+    # a blocking collective issued on the current stream before the started one was
+    # waited on: the group orders it after the started one (shared epochs/flags/scratch);
+    # both staged (non-heap) so they would also share the scratch segment
+    big = 1 << 20
+    xs, ys = gen(rank, big, torch.float32, 93300), torch.empty(big, device=D)
+    xb, yb = gen(rank, big, torch.float32, 93301), torch.empty(big, device=D)
+    w = dev.start("allreduce", xs, ys, "SUM", "twoshot")
+    dev.allreduce(xb, yb, "SUM", "twoshot")
+    check("async_then_blocking[blocking]", yb, oracle(big, torch.float32, "SUM", 93301), torch.float32, p)
+    check("async_then_blocking[started]", w.wait(), oracle(big, torch.float32, "SUM", 93300), torch.float32, p)
     # MPI-style façade: Communicator.I* on CUDA tensors -> DeviceRequest, completed by
     # Request.Waitall together with a host-plane non-blocking collective
     x, y = gen(rank, n, torch.float32, 93200), dev.empty(n, torch.float32)
