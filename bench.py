@@ -51,6 +51,7 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 GiB = 1 << 30
+XGMI_LINK_GBPS = 153.6  # MI355X xGMI, per link and direction (7 links x 153.6 = 1075 GB/s per GPU)
 
 
 def parse():
@@ -335,6 +336,10 @@ def main() -> int:
                 "allreduce_algo": best,
                 "allreduce_bytes": nbytes,
                 "busbw_GBps": round(busbw, 3),
+                # one xGMI link per GPU pair (fully connected, <= 7 per GPU), ~153.6 GB/s each per
+                # direction: the all-reduce's bus bandwidth as a fraction of the links it can drive
+                "xgmi_link_frac": (round(busbw / (min(world - 1, 7) * XGMI_LINK_GBPS), 3)
+                                   if world > 1 and not dev.shared_device else None),
                 "candidates_ms": {a: (round(t * 1e3, 4) if t else None) for a, t in results.items()},
                 "result_exact": final_ok,
                 "self_test": self_test,
