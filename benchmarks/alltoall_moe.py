@@ -8,7 +8,9 @@ Algorithms: ``direct`` (hand-written kernel: every rank pulls its block from
 all peers at once over xGMI), ``push`` (every rank writes its segments straight
 into the peers' outputs, the reference myAlltoall pattern), ``pairwise`` (reference myAlltoall2 schedule on
 RCCL send/recv rounds), ``rccl`` (ncclAllToAll, the library baseline).  Each is
-checked for exactness, then timed (median of --iters).  Prints one JSON line.
+checked for exactness, then timed (median of --iters).  Also the ragged
+all-to-all (``alltoallv``: equal counts, and skewed MoE-like counts whose
+correctness the device tests cover).  Prints one JSON line.
 """
 import argparse
 import json
@@ -67,12 +69,52 @@ for algo in algos:
         torch.cuda.synchronize()
         ts.append(time.perf_counter() - t0)
     res[algo] = hc.allreduce(statistics.median(ts), op=MPI.MAX)
+# ragged (MoE routing with imbalanced experts): alltoallv with counts drawn from a
+# skewed distribution around the uniform block (same total per rank on average);
+# "uniform" = alltoallv with equal counts, to compare against the push all-to-all
+import random  # noqa: E402
+
+rg = random.Random(7)
+W = [[rg.choice([0.25, 0.5, 1.0, 1.0, 1.5, 2.0]) for _ in range(p)] for _ in range(p)]
+Cr = [[int(blk * w / 2) // 4 * 4 for w in row] for row in W]  # 16-B segments (fp32 x 4)
+for name, C in (("alltoallv_uniform", [[blk] * p for _ in range(p)]), ("alltoallv_ragged", Cr)):
+    sc, rc = C[rank], [C[i][rank] for i in range(p)]
+    xs, ys = x[:sum(sc)], y[:max(1, sum(rc))]
+    try:
+        dev.alltoallv(xs, sc, ys, rc)
+        torch.cuda.synchronize()
+        dev.check()
+        o, ok = 0, True
+        for i in range(p):  # from rank i: its send elements [sum(C[i][:rank]), + rc[i])
+            g = torch.arange(sum(C[i][:rank]), sum(C[i][:rank]) + rc[i], device=dev.device)
+            want = i * 1e6 + (g // blk).float() * 1e3 + (g % blk % 997).float()
+            ok = ok and torch.equal(ys[o:o + rc[i]], want)
+            o += rc[i]
+    except Exception as e:  # noqa: BLE001
+        ok = False
+        if rank == 0:
+            print(f"# {name}: {e}", file=sys.stderr)
+    if not hc.allreduce(int(ok), op=MPI.MIN):
+        res[name] = None
+        continue
+    for _ in range(args.warmup):
+        dev.alltoallv(xs, sc, ys, rc)
+    ts = []
+    for _ in range(args.iters):
+        torch.cuda.synchronize()
+        hc.Barrier()
+        t0 = time.perf_counter()
+        dev.alltoallv(xs, sc, ys, rc)
+        torch.cuda.synchronize()
+        ts.append(time.perf_counter() - t0)
+    res[name] = hc.allreduce(statistics.median(ts), op=MPI.MAX)
+    res[name + "_max_send_bytes"] = max(sum(r) for r in C) * 4
 if rank == 0:
     nbytes = n * 4
     out = {"bench": "alltoall_moe", "ranks": p, "bytes_per_rank": nbytes, "shared_gpu": dev.shared_device,
            "hbm_bytes_all_ranks": 2 * p * nbytes,
-           "results": {a: (None if t is None else {"ms": round(t * 1e3, 4),
-                                                   "algbw_GBps": round(nbytes / t / 1e9, 2),
-                                                   "busbw_GBps": round(nbytes / t / 1e9 * (p - 1) / p, 2)})
+           "results": {a: (None if t is None else t if a.endswith("_bytes") else
+                               {"ms": round(t * 1e3, 4), "algbw_GBps": round(nbytes / t / 1e9, 2),
+                                "busbw_GBps": round(nbytes / t / 1e9 * (p - 1) / p, 2)})
                        for a, t in res.items()}}
     print(json.dumps(out), flush=True)

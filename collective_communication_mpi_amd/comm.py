@@ -203,6 +203,19 @@ class Communicator(object):
         else:
             self.comm.Alltoall(src_array, dest_array)
 
+    def Alltoallv(self, src_array, send_counts, dest_array, recv_counts, algo: str = "auto"):
+        """All-to-all with per-rank element counts, packed in rank order on both sides
+        (MPI Alltoallv without explicit displacements; the MoE dispatch shape).
+        Accounting: the bytes this rank sends to and receives from the other ranks."""
+        rank, p = self.comm.Get_rank(), self.comm.Get_size()
+        isz, _ = _nbytes_items(src_array)
+        self.total_bytes_transferred += isz * (sum(int(c) for j, c in enumerate(send_counts) if j != rank) +
+                                               sum(int(c) for i, c in enumerate(recv_counts) if i != rank))
+        if _is_device(src_array):
+            self.dev.alltoallv(src_array, send_counts, dest_array, recv_counts)
+        else:
+            self.comm.Alltoallv([src_array, list(send_counts)], [dest_array, list(recv_counts)])
+
     def Bcast(self, buf, root: int = 0):
         isz, n = _nbytes_items(buf)
         if self.comm.Get_rank() == root:

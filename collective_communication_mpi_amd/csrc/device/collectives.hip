@@ -720,6 +720,29 @@ __global__ void __launch_bounds__(kThreads) k_move(CollArgs a) {
   finish(a, e);
 }
 
+// All-to-all with per-peer sizes (MoE token dispatch): CTA b takes a 16-B slice
+// of the concatenated send buffer and writes the part of every peer segment it
+// covers straight into that peer's output (posted xGMI writes, the input never
+// leaves local memory) -- MODE 3's push generalised to ragged segments.  The
+// grid is the same on every rank (the per-CTA flags pair CTA b with CTA b), so
+// ranks with less to send run idle CTAs through the two barriers.
+__global__ void __launch_bounds__(kThreads) k_alltoallv_push(VArgs v) {
+  __shared__ uint64_t s_epoch;
+  __shared__ uint64_t codes[2][kMaxRanks];
+  const CollArgs& a = v.a;
+  if (!start_phase(a, &s_epoch, codes)) return;
+  const uint64_t e = s_epoch;
+  const PeerTable* pt = a.pt;
+  const int nr = pt->size;
+  const BlockRange r = part16(a.nbytes, gridDim.x, blockIdx.x);
+  for (int j = 0; j < nr; ++j) {
+    const uint64_t lo = max(r.lo, v.soff[j]), hi = min(r.hi, v.soff[j] + v.len[j]);
+    if (hi > lo) copy_span(a.in + lo, resolve(pt, j, codes[1][j]) + v.doff[j] + (lo - v.soff[j]), hi - lo);
+  }
+  if (!sync_phase(a, 3, e)) return;
+  finish(a, e);
+}
+
 // ---------------------------------------------------------------------------
 // low-latency one-shot all-reduce (small messages)
 // ---------------------------------------------------------------------------
@@ -1248,6 +1271,11 @@ void launch_move(int mode, const CollArgs& a, int nranks, int grid, hipStream_t 
       default: throw std::invalid_argument("ccmpi: bad move mode");
     }
   });
+  CCMPI_HIP_CHECK(hipGetLastError());
+}
+
+void launch_alltoallv(const VArgs& v, int grid, hipStream_t s) {
+  hipLaunchKernelGGL(k_alltoallv_push, dim3(grid), dim3(kThreads), 0, s, v);
   CCMPI_HIP_CHECK(hipGetLastError());
 }
 

@@ -56,6 +56,16 @@ struct CollArgs {
   uint64_t* dbg;           // optional: per-phase s_memrealtime stamps of CTA 0 / thread 0 (diagnostics)
 };
 
+// All-to-all with per-peer sizes (push): bytes [soff[j], soff[j] + len[j]) of the
+// local input go to peer j's registered output at doff[j].  a.nbytes = this rank's
+// total send bytes; every offset and length is a multiple of 16 B.
+struct VArgs {
+  CollArgs a;
+  uint64_t soff[kMaxRanks];
+  uint64_t doff[kMaxRanks];
+  uint64_t len[kMaxRanks];
+};
+
 struct LocalReduceArgs {
   const char* in[kMaxRanks];
   char* out;
@@ -72,6 +82,7 @@ void launch_move(int mode, const CollArgs& a, int nranks, int grid, hipStream_t 
 // mode 0: last-axis all-gather, 1: last-axis reduce-scatter; rows passed in CollArgs::root
 void launch_lastaxis(int mode, const CollArgs& a, int nranks, int dtype, int op, int grid, hipStream_t s);
 void launch_local_reduce(const LocalReduceArgs& a, int dtype, int op, hipStream_t s);
+void launch_alltoallv(const VArgs& v, int grid, hipStream_t s);
 
 }  // namespace dev
 }  // namespace ccmpi

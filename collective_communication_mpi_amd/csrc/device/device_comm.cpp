@@ -576,6 +576,34 @@ void DeviceComm::alltoall(uint64_t in, uint64_t out, uint64_t bytes_per_peer, ui
   }
 }
 
+void DeviceComm::alltoallv(uint64_t in, uint64_t out, uint64_t out_bytes, const std::vector<uint64_t>& soff,
+                           const std::vector<uint64_t>& doff, const std::vector<uint64_t>& len, uint64_t grid_bytes,
+                           uint64_t stream, int max_blocks) {
+  if ((int)soff.size() != size_ || (int)doff.size() != size_ || (int)len.size() != size_)
+    throw std::invalid_argument("ccmpi: alltoallv needs one offset/length per rank");
+  if (grid_bytes == 0) return;  // nobody sends anything: every rank sees the same
+  CCMPI_HIP_CHECK(hipSetDevice(device_));
+  hipStream_t st = S(stream);
+  uint64_t total = 0;
+  for (int j = 0; j < size_; ++j) {
+    if ((soff[j] | doff[j] | len[j]) % 16) throw std::invalid_argument("ccmpi: alltoallv segments must be 16-B multiples");
+    if (soff[j] != total) throw std::invalid_argument("ccmpi: alltoallv send segments must be packed in peer order");
+    total += len[j];
+  }
+  if (in % 16 || out % 16) throw std::invalid_argument("ccmpi: alltoallv buffers must be 16-B aligned");
+  const uint64_t rc = code_of_(out, std::max<uint64_t>(out_bytes, 16));
+  if (!rc) throw std::invalid_argument("ccmpi: alltoallv needs a registered (symmetric-heap) output on every rank");
+  VArgs v{};
+  v.a = args_(0, rc, (char*)out, total, 0);
+  v.a.in = reinterpret_cast<const char*>(in);
+  for (int j = 0; j < size_; ++j) {
+    v.soff[j] = soff[j];
+    v.doff[j] = doff[j];
+    v.len[j] = len[j];
+  }
+  launch_alltoallv(v, grid_(grid_bytes, max_blocks), st);
+}
+
 void DeviceComm::bcast(uint64_t buf, uint64_t nbytes, int root, uint64_t stream, int max_blocks, bool symmetric,
                        int mode) {
   if (nbytes == 0 || size_ == 1) return;

@@ -66,6 +66,12 @@ class DeviceComm {
                  bool symmetric, int mode = 0);
   // mode: A2A_PULL (default; staged for in-place / unregistered input) or A2A_PUSH
   // (symmetric only: every rank's output registered, peer writes into it)
+  // Ragged all-to-all (push into every rank's registered output): per-peer byte
+  // offsets / lengths, all multiples of 16; grid_bytes = the largest total send of
+  // any rank (the grid must match across ranks).
+  void alltoallv(uint64_t in, uint64_t out, uint64_t out_bytes, const std::vector<uint64_t>& soff,
+                 const std::vector<uint64_t>& doff, const std::vector<uint64_t>& len, uint64_t grid_bytes,
+                 uint64_t stream, int max_blocks);
   void alltoall(uint64_t in, uint64_t out, uint64_t bytes_per_peer, uint64_t stream, int max_blocks,
                 bool symmetric, int mode = 0);
   // mode A2A_PUSH: symmetric buffers only, the root writes into every peer's buffer

@@ -42,6 +42,8 @@ import os
 import threading
 from typing import Dict, List, Optional, Sequence, Tuple
 
+import numpy as np
+
 from . import _native
 from .utils.trace import trace_call
 
@@ -558,6 +560,71 @@ class DeviceGroup:
                              self.D.A2A_PULL)
         else:
             raise ValueError(f"unknown alltoall algorithm {algo!r}")
+        return dst
+
+    @trace_call("alltoallv")
+    def alltoallv(self, src, send_counts, dst, recv_counts=None, max_blocks: Optional[int] = None):
+        """Ragged all-to-all (MPI Alltoallv with packed displacements; the MoE token
+        dispatch/combine shape): ``src`` holds ``send_counts[j]`` elements for rank j
+        back to back in rank order; ``dst`` receives ``recv_counts[i]`` elements from
+        rank i back to back in rank order.  One host all-gather of every rank's count
+        row (p integers) gives each rank the whole count matrix, so every offset is
+        known locally.  When every segment is a 16-B multiple and every rank's
+        output lives in the symmetric heap, one push kernel writes each segment
+        straight into its destination (``k_alltoallv_push``); otherwise the call
+        runs as a padded all-to-all (blocks of the largest count) plus pack/unpack
+        copies.  Returns ``dst``."""
+        torch = self.torch
+        self._check(src, "src")
+        self._check(dst, "dst")
+        if src.dtype != dst.dtype:
+            raise ValueError("alltoallv: src/dst dtypes differ")
+        p, me = self.size, self.rank
+        sc = [int(c) for c in send_counts]
+        if len(sc) != p or min(sc) < 0:
+            raise ValueError("alltoallv: need one non-negative send count per rank")
+        if sum(sc) > src.numel():
+            raise ValueError("alltoallv: send counts exceed src")
+        es = src.element_size()
+        # one host all-gather carries every rank's count row plus whether its buffers
+        # allow the kernel path (16-B aligned input, output in the symmetric heap): a
+        # local property every rank must agree on before choosing a path
+        ok_local = src.data_ptr() % 16 == 0 and (dst.numel() == 0 or (dst.data_ptr() % 16 == 0 and self.is_symmetric(dst)))
+        mat = np.zeros((p, p + 1), np.int64)
+        self.host.Allgather(np.array(sc + [int(ok_local)], np.int64), mat)
+        counts = mat[:, :p]  # counts[i, j]: elements rank i sends to rank j
+        rc = counts[:, me].tolist()
+        if recv_counts is not None and [int(c) for c in recv_counts] != rc:
+            raise ValueError(f"alltoallv: recv_counts {list(recv_counts)} != what the peers send {rc}")
+        rtot_local = sum(rc)
+        if rtot_local > dst.numel():
+            raise ValueError("alltoallv: dst too small for the received segments")
+        fast = bool(mat[:, p].all()) and not np.any((counts * es) % 16)
+        s = self._stream()
+        if fast:
+            b = counts * es
+            soff = np.concatenate([[0], np.cumsum(b[me])[:-1]]).astype(np.uint64).tolist()
+            doff = [int(b[:me, j].sum()) for j in range(p)]
+            grid_bytes = int(b.sum(axis=1).max())
+            out = dst if rtot_local else self.scratch
+            self.dc.alltoallv(src.data_ptr(), out.data_ptr(), max(16, rtot_local * es), [int(x) for x in soff], doff,
+                              [int(x) for x in b[me]], grid_bytes, s, self._budget(max_blocks))
+            return dst
+        # padded fallback: blocks of the largest count through the regular all-to-all
+        m = int(counts.max())
+        if m == 0:
+            return dst
+        ps = torch.zeros(p * m, dtype=src.dtype, device=self.device)
+        pr = torch.empty(p * m, dtype=src.dtype, device=self.device)
+        o = 0
+        for j in range(p):
+            ps[j * m:j * m + sc[j]].copy_(src[o:o + sc[j]])
+            o += sc[j]
+        self.alltoall(ps, pr, "direct", max_blocks)
+        o = 0
+        for i in range(p):
+            dst[o:o + rc[i]].copy_(pr[i * m:i * m + rc[i]])
+            o += rc[i]
         return dst
 
     @trace_call("bcast")

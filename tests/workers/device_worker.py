@@ -382,6 +382,46 @@ def async_ops():
         fails.append("facade: host Iallreduce mixed with device requests")
 
 
+def ragged():
+    """alltoallv: random ragged count matrices (shared RNG), kernel path (16-B segments,
+    heap output), padded fallback (odd counts / non-heap output), empty rows/columns,
+    and the Communicator façade (accounting as Alltoallv)."""
+    import random
+
+    global ncheck
+    shared = random.Random(4242)
+    for it, (dtype, mult, heap) in enumerate([(torch.float32, 4, True), (torch.bfloat16, 8, True),
+                                              (torch.float32, 1, True), (torch.float32, 4, False),
+                                              (torch.int64, 2, True)]):
+        C = [[shared.randint(0, 40) * mult * shared.choice([0, 1, 1, 3, 100]) for _ in range(p)] for _ in range(p)]
+        if it == 0:
+            C[0] = [0] * p  # rank 0 sends nothing
+            for i in range(p):
+                C[i][p - 1] = 0  # rank p-1 receives nothing
+        sc = C[rank]
+        rcv = [C[i][rank] for i in range(p)]
+        x = torch.cat([gen(rank, sc[j], dtype, 94000 + 100 * it + j) for j in range(p)])
+        want = torch.cat([gen(i, C[i][rank], dtype, 94000 + 100 * it + rank) for i in range(p)])
+        n_out = max(1, sum(rcv))
+        y = dev.empty(n_out, dtype) if heap else torch.empty(n_out, dtype=dtype, device=D)
+        y.zero_()
+        dev.alltoallv(x, sc, y, rcv)
+        check(f"alltoallv[{it},{dtype},heap={heap}]", y[:sum(rcv)], want.to(WIDE(dtype)), dtype)
+    # façade: Communicator.Alltoallv on CUDA tensors
+    C = [[(i + 2 * j) % 5 * 4 for j in range(p)] for i in range(p)]
+    x = torch.cat([gen(rank, C[rank][j], torch.float32, 94900 + j) for j in range(p)])
+    y = dev.empty(max(1, sum(C[i][rank] for i in range(p))), torch.float32)
+    before = comm.total_bytes_transferred
+    comm.Alltoallv(x, C[rank], y, [C[i][rank] for i in range(p)])
+    want = torch.cat([gen(i, C[i][rank], torch.float32, 94900 + rank) for i in range(p)])
+    check("facade_Alltoallv", y[:want.numel()], want.double(), torch.float32)
+    sent = sum(C[rank][j] for j in range(p) if j != rank) * 4
+    got = sum(C[i][rank] for i in range(p) if i != rank) * 4
+    ncheck += 1
+    if comm.total_bytes_transferred - before != sent + got:
+        fails.append(f"Alltoallv accounting {comm.total_bytes_transferred - before} != {sent + got}")
+
+
 def tuning():
     """tune() -> per-size table used by auto, persisted through CCMPI_TUNE_FILE-style save."""
     import tempfile
@@ -420,7 +460,7 @@ if args.matrix:
     # serialized launches (AMD_SERIALIZE_KERNEL, HIP's CUDA_LAUNCH_BLOCKING) synchronise
     # around every kernel, which stream capture forbids: graphs are skipped there
     serialized = os.environ.get("AMD_SERIALIZE_KERNEL", "0") not in ("", "0")
-    for fn in (determinism,) + (() if serialized else (graphs,)) + ((tuning,) if args.matrix == "quick" else ()):
+    for fn in (determinism, ragged) + (() if serialized else (graphs,)) + ((tuning,) if args.matrix == "quick" else ()):
         t_s = time.time()
         fn()
         if rank == 0 and os.environ.get("CCMPI_WORKER_VERBOSE") == "1":

@@ -188,6 +188,16 @@ cm.Reduce_scatter(a, r1, MPI.SUM)
 cm.Ireduce_scatter(a, r2, MPI.SUM).Wait()
 check(np.array_equal(r1, r2), "Communicator.Ireduce_scatter")
 cm.Ibarrier().Wait()
+# Alltoallv on the host plane (ragged counts, packed in rank order)
+C = [[(3 * i + j) % 4 for j in range(p)] for i in range(p)]
+src = np.concatenate([np.full(C[rank][j], 100 * rank + j, np.int32) for j in range(p)] or [np.zeros(0, np.int32)])
+dst = np.full(max(1, sum(C[i][rank] for i in range(p))), -1, np.int32)
+b0 = cm.total_bytes_transferred
+cm.Alltoallv(src, C[rank], dst, [C[i][rank] for i in range(p)])
+want = np.concatenate([np.full(C[i][rank], 100 * i + rank, np.int32) for i in range(p)])
+check(np.array_equal(dst[:want.size], want), "Communicator.Alltoallv (host)")
+check(cm.total_bytes_transferred - b0 == 4 * (sum(C[rank]) - C[rank][rank] + sum(C[i][rank] for i in range(p)) - C[rank][rank]),
+      "Alltoallv accounting")
 
 bad = comm.allgather(fails)
 if rank == 0:
