@@ -119,6 +119,7 @@ PYBIND11_MODULE(_device, m) {
       .def("allgather", &DeviceComm::allgather, py::arg("inp"), py::arg("out"), py::arg("bytes_per_rank"),
            py::arg("stream"), py::arg("max_blocks"), py::arg("symmetric"), py::arg("mode") = 0,
            py::call_guard<py::gil_scoped_release>())
+      .def("alltoallv_dev", &DeviceComm::alltoallv_dev, py::call_guard<py::gil_scoped_release>())
       .def("alltoallv", &DeviceComm::alltoallv, py::call_guard<py::gil_scoped_release>())
       .def("alltoall", &DeviceComm::alltoall, py::arg("inp"), py::arg("out"), py::arg("bytes_per_peer"),
            py::arg("stream"), py::arg("max_blocks"), py::arg("symmetric"), py::arg("mode") = 0,

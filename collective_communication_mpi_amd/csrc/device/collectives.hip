@@ -743,6 +743,58 @@ __global__ void __launch_bounds__(kThreads) k_alltoallv_push(VArgs v) {
   finish(a, e);
 }
 
+// The same with the count matrix read on the device: after the start barrier
+// every CTA loads every rank's staged count row (p + 1 int64: counts, output
+// capacity) from the peers' scratch segments into LDS, derives the packed
+// offsets, and pushes its slice.  A segment that is not a 16-B multiple, or that
+// would overrun the receiver's capacity, is not written: the kernel records a
+// fault code (0x900 + peer) that DeviceGroup.check() raises.  The grid is fixed
+// by the caller (sizes are unknown on the host).
+__global__ void __launch_bounds__(kThreads) k_alltoallv_dev(VDevArgs v) {
+  __shared__ uint64_t s_epoch;
+  __shared__ uint64_t codes[2][kMaxRanks];
+  __shared__ int64_t C[kMaxRanks][kMaxRanks + 1];
+  const CollArgs& a = v.a;
+  if (threadIdx.x == 0) {  // published with the start barrier (thread 0 releases before its flag)
+    int64_t* mine = reinterpret_cast<int64_t*>(resolve(a.pt, a.pt->rank, a.src_code));
+    __hip_atomic_store(mine + a.pt->size, v.cap, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  if (!start_phase(a, &s_epoch, codes)) return;
+  const uint64_t e = s_epoch;
+  const PeerTable* pt = a.pt;
+  const int me = pt->rank, nr = pt->size;
+  for (int t = threadIdx.x; t < nr * (nr + 1); t += kThreads) {
+    const int i = t / (nr + 1), j = t % (nr + 1);
+    const int64_t* row = reinterpret_cast<const int64_t*>(resolve(pt, i, codes[0][i]));
+    C[i][j] = __hip_atomic_load(row + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  __syncthreads();
+  if (blockIdx.x == 0 && threadIdx.x < nr) v.recv_counts[threadIdx.x] = C[threadIdx.x][me];
+  const uint64_t es = v.es;
+  uint64_t total = 0;
+  for (int j = 0; j < nr; ++j) total += (uint64_t)max(C[me][j], (int64_t)0) * es;
+  const BlockRange r = part16(total, gridDim.x, blockIdx.x);
+  uint64_t soff = 0;
+  for (int j = 0; j < nr; ++j) {
+    uint64_t doff = 0;
+    for (int i = 0; i < me; ++i) doff += (uint64_t)max(C[i][j], (int64_t)0) * es;
+    const uint64_t len = (uint64_t)max(C[me][j], (int64_t)0) * es;
+    const bool ok = C[me][j] >= 0 && (soff | doff | len) % 16 == 0 && doff + len <= (uint64_t)C[j][nr] * es;
+    if (!ok) {
+      if (threadIdx.x == 0 && blockIdx.x == 0) {
+        __hip_atomic_store(&pt->sig[me]->error, 0x900u + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        report_host(pt, 0x900u + j);
+      }
+    } else {
+      const uint64_t lo = max(r.lo, soff), hi = min(r.hi, soff + len);
+      if (hi > lo) copy_span(a.in + lo, resolve(pt, j, codes[1][j]) + doff + (lo - soff), hi - lo);
+    }
+    soff += len;
+  }
+  if (!sync_phase(a, 3, e)) return;
+  finish(a, e);
+}
+
 // ---------------------------------------------------------------------------
 // low-latency one-shot all-reduce (small messages)
 // ---------------------------------------------------------------------------
@@ -1276,6 +1328,11 @@ void launch_move(int mode, const CollArgs& a, int nranks, int grid, hipStream_t 
 
 void launch_alltoallv(const VArgs& v, int grid, hipStream_t s) {
   hipLaunchKernelGGL(k_alltoallv_push, dim3(grid), dim3(kThreads), 0, s, v);
+  CCMPI_HIP_CHECK(hipGetLastError());
+}
+
+void launch_alltoallv_dev(const VDevArgs& v, int grid, hipStream_t s) {
+  hipLaunchKernelGGL(k_alltoallv_dev, dim3(grid), dim3(kThreads), 0, s, v);
   CCMPI_HIP_CHECK(hipGetLastError());
 }
 

@@ -66,6 +66,17 @@ struct VArgs {
   uint64_t len[kMaxRanks];
 };
 
+// Ragged all-to-all with the counts on the device (no host round trip; graph
+// capturable): every rank's row [count to rank 0 .. count to rank p-1, output
+// capacity in elements] (p + 1 int64) lives at the start of its scratch segment:
+// the counts copied there before the kernel, the capacity written by the kernel.
+struct VDevArgs {
+  CollArgs a;                // src_code = scratch (segment 0) code, res_code = output code
+  int64_t* recv_counts;      // out: elements received from each rank
+  uint32_t es;               // element size in bytes
+  int64_t cap;               // this rank's output capacity in elements (written into its row)
+};
+
 struct LocalReduceArgs {
   const char* in[kMaxRanks];
   char* out;
@@ -83,6 +94,7 @@ void launch_move(int mode, const CollArgs& a, int nranks, int grid, hipStream_t 
 void launch_lastaxis(int mode, const CollArgs& a, int nranks, int dtype, int op, int grid, hipStream_t s);
 void launch_local_reduce(const LocalReduceArgs& a, int dtype, int op, hipStream_t s);
 void launch_alltoallv(const VArgs& v, int grid, hipStream_t s);
+void launch_alltoallv_dev(const VDevArgs& v, int grid, hipStream_t s);
 
 }  // namespace dev
 }  // namespace ccmpi

@@ -604,6 +604,28 @@ void DeviceComm::alltoallv(uint64_t in, uint64_t out, uint64_t out_bytes, const 
   launch_alltoallv(v, grid_(grid_bytes, max_blocks), st);
 }
 
+void DeviceComm::alltoallv_dev(uint64_t in, uint64_t counts, uint64_t out, uint64_t out_elems, uint64_t recv_counts,
+                               int elem_bytes, uint64_t stream, int max_blocks) {
+  CCMPI_HIP_CHECK(hipSetDevice(device_));
+  hipStream_t st = S(stream);
+  if (in % 16 || out % 16) throw std::invalid_argument("ccmpi: alltoallv buffers must be 16-B aligned");
+  const uint64_t row_bytes = 8ull * (size_ + 1);
+  if (scratch_bytes() < row_bytes) throw std::runtime_error("ccmpi: scratch too small for alltoallv counts");
+  const uint64_t rc = code_of_(out, std::max<uint64_t>(out_elems * elem_bytes, 16));
+  if (!rc) throw std::invalid_argument("ccmpi: alltoallv needs a registered (symmetric-heap) output on every rank");
+  // stage the counts at the start of scratch (stream-ordered before the kernel; the
+  // previous collective that used scratch passed its final barrier on every rank)
+  char* row = reinterpret_cast<char*>(scratch_ptr());
+  CCMPI_HIP_CHECK(hipMemcpyAsync(row, (void*)counts, 8ull * size_, hipMemcpyDeviceToDevice, st));
+  VDevArgs v{};
+  v.a = args_(addr_code(0, 0), rc, (char*)out, 0, 0);
+  v.a.in = reinterpret_cast<const char*>(in);
+  v.recv_counts = reinterpret_cast<int64_t*>(recv_counts);
+  v.es = (uint32_t)elem_bytes;
+  v.cap = (int64_t)out_elems;
+  launch_alltoallv_dev(v, std::max(1, std::min(max_blocks > 0 ? max_blocks : 256, kMaxBlocks)), st);
+}
+
 void DeviceComm::bcast(uint64_t buf, uint64_t nbytes, int root, uint64_t stream, int max_blocks, bool symmetric,
                        int mode) {
   if (nbytes == 0 || size_ == 1) return;

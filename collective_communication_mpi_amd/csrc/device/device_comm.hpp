@@ -72,6 +72,11 @@ class DeviceComm {
   void alltoallv(uint64_t in, uint64_t out, uint64_t out_bytes, const std::vector<uint64_t>& soff,
                  const std::vector<uint64_t>& doff, const std::vector<uint64_t>& len, uint64_t grid_bytes,
                  uint64_t stream, int max_blocks);
+  // Ragged all-to-all with device-resident counts: `counts` (p int64, this rank's
+  // send counts) and the output capacity are staged into scratch, the kernel
+  // exchanges them; `recv_counts` (p int64, device) receives what arrived.
+  void alltoallv_dev(uint64_t in, uint64_t counts, uint64_t out, uint64_t out_elems, uint64_t recv_counts,
+                     int elem_bytes, uint64_t stream, int max_blocks);
   void alltoall(uint64_t in, uint64_t out, uint64_t bytes_per_peer, uint64_t stream, int max_blocks,
                 bool symmetric, int mode = 0);
   // mode A2A_PUSH: symmetric buffers only, the root writes into every peer's buffer

@@ -573,13 +573,16 @@ class DeviceGroup:
         output lives in the symmetric heap, one push kernel writes each segment
         straight into its destination (``k_alltoallv_push``); otherwise the call
         runs as a padded all-to-all (blocks of the largest count) plus pack/unpack
-        copies.  Returns ``dst``."""
+        copies.  With ``send_counts`` a CUDA tensor the counts never leave the device
+        (``_alltoallv_dev``; ``recv_counts`` is then an output tensor).  Returns ``dst``."""
         torch = self.torch
         self._check(src, "src")
         self._check(dst, "dst")
         if src.dtype != dst.dtype:
             raise ValueError("alltoallv: src/dst dtypes differ")
         p, me = self.size, self.rank
+        if isinstance(send_counts, torch.Tensor) and send_counts.is_cuda:
+            return self._alltoallv_dev(src, send_counts, dst, recv_counts, max_blocks)
         sc = [int(c) for c in send_counts]
         if len(sc) != p or min(sc) < 0:
             raise ValueError("alltoallv: need one non-negative send count per rank")
@@ -625,6 +628,32 @@ class DeviceGroup:
         for i in range(p):
             dst[o:o + rc[i]].copy_(pr[i * m:i * m + rc[i]])
             o += rc[i]
+        return dst
+
+    def _alltoallv_dev(self, src, send_counts, dst, recv_counts, max_blocks):
+        """alltoallv with the counts in device memory (e.g. an MoE router's per-expert
+        token counts): no host round trip, capturable in a HIP graph.  The kernel
+        exchanges the count rows itself (``k_alltoallv_dev``); ``recv_counts`` (a
+        CUDA int64 tensor of p elements, allocated if None) receives the counts that
+        arrived.  ``dst`` must be in the symmetric heap on every rank and every segment
+        a 16-B multiple; a violating or overflowing segment is not written and
+        ``check()`` raises (fault code 0x900 + peer)."""
+        torch = self.torch
+        p = self.size
+        if send_counts.numel() != p:
+            raise ValueError("alltoallv: need one send count per rank")
+        if not (self.is_symmetric(dst) and dst.data_ptr() % 16 == 0 and src.data_ptr() % 16 == 0):
+            raise ValueError("alltoallv with device counts: dst must come from the symmetric heap (comm.empty), "
+                             "src and dst 16-B aligned")
+        counts = send_counts.to(torch.int64).contiguous()
+        if recv_counts is None:
+            recv_counts = torch.empty(p, dtype=torch.int64, device=self.device)
+        elif not (recv_counts.is_cuda and recv_counts.dtype == torch.int64 and recv_counts.numel() == p
+                  and recv_counts.is_contiguous()):
+            raise ValueError("alltoallv: recv_counts must be a contiguous CUDA int64 tensor of p elements")
+        s = self._stream()
+        self.dc.alltoallv_dev(src.data_ptr(), counts.data_ptr(), dst.data_ptr(), dst.numel(), recv_counts.data_ptr(),
+                              src.element_size(), s, self._budget(max_blocks))
         return dst
 
     @trace_call("bcast")

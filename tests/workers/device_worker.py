@@ -407,6 +407,67 @@ def ragged():
         y.zero_()
         dev.alltoallv(x, sc, y, rcv)
         check(f"alltoallv[{it},{dtype},heap={heap}]", y[:sum(rcv)], want.to(WIDE(dtype)), dtype)
+    # device-resident counts: no host exchange; recv counts come back in a device tensor
+    for it, (dtype, mult) in enumerate([(torch.float32, 4), (torch.bfloat16, 8), (torch.int64, 2)]):
+        C = [[shared.randint(0, 30) * mult for _ in range(p)] for _ in range(p)]
+        sc = C[rank]
+        x = torch.cat([gen(rank, sc[j], dtype, 94500 + 100 * it + j) for j in range(p)])
+        xs = dev.empty(max(1, x.numel()), dtype)
+        xs[:x.numel()].copy_(x)
+        want = torch.cat([gen(i, C[i][rank], dtype, 94500 + 100 * it + rank) for i in range(p)])
+        y = dev.zeros(max(1, want.numel()), dtype)
+        rcnt = torch.full((p,), -1, dtype=torch.int64, device=D)
+        dev.alltoallv(xs, torch.tensor(sc, device=D), y, rcnt)
+        torch.cuda.synchronize()
+        dev.check()
+        check(f"alltoallv_dev[{dtype}]", y[:want.numel()], want.to(WIDE(dtype)), dtype)
+        ncheck += 1
+        if rcnt.tolist() != [C[i][rank] for i in range(p)]:
+            fails.append(f"alltoallv_dev[{dtype}] recv counts {rcnt.tolist()}")
+    # captured once in a HIP graph, replayed with new counts and data in the same buffers
+    # (the capture stream is one more HW queue per process: skipped with > 2 ranks per GPU)
+    if not serialized and dev.ranks_per_device <= 2:
+        cnt = torch.zeros(p, dtype=torch.int64, device=D)
+        xs = dev.empty(64 * p, torch.float32)
+        y = dev.zeros(64 * p, torch.float32)
+        rcnt = torch.zeros(p, dtype=torch.int64, device=D)
+        cs = torch.cuda.Stream()
+        cs.wait_stream(torch.cuda.current_stream())
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.stream(cs):
+            with torch.cuda.graph(g, stream=cs):
+                dev.alltoallv(xs, cnt, y, rcnt)
+        torch.cuda.current_stream().wait_stream(cs)
+        for rep in range(3):
+            C = [[shared.randint(0, 16) * 4 for _ in range(p)] for _ in range(p)]
+            cnt.copy_(torch.tensor(C[rank], device=D))
+            x = torch.cat([gen(rank, C[rank][j], torch.float32, 94800 + 10 * rep + j) for j in range(p)])
+            xs[:x.numel()].copy_(x)
+            torch.cuda.synchronize()
+            dev.host.Barrier()
+            g.replay()
+            torch.cuda.synchronize()
+            dev.check()
+            want = torch.cat([gen(i, C[i][rank], torch.float32, 94800 + 10 * rep + rank) for i in range(p)])
+            check(f"alltoallv_dev_graph[{rep}]", y[:want.numel()], want.double(), torch.float32)
+            ncheck += 1
+            if rcnt.tolist() != [C[i][rank] for i in range(p)]:
+                fails.append(f"alltoallv_dev_graph[{rep}] recv counts {rcnt.tolist()}")
+        del g
+    # a segment that is not a 16-B multiple is refused on the device and reported
+    y = dev.zeros(64, torch.float32)
+    bad = torch.tensor([3] * p, device=D)
+    xs = dev.empty(3 * p, torch.float32)
+    dev.alltoallv(xs, bad, y, None)
+    torch.cuda.synchronize()
+    ncheck += 1
+    try:
+        dev.check()
+        fails.append("alltoallv_dev: misaligned segment not reported")
+    except RuntimeError as e:
+        if "0x90" not in str(e):
+            fails.append(f"alltoallv_dev: unexpected error {e}")
+    dev.host.Barrier()
     # façade: Communicator.Alltoallv on CUDA tensors
     C = [[(i + 2 * j) % 5 * 4 for j in range(p)] for i in range(p)]
     x = torch.cat([gen(rank, C[rank][j], torch.float32, 94900 + j) for j in range(p)])
