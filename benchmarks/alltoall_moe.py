@@ -109,6 +109,34 @@ for name, C in (("alltoallv_uniform", [[blk] * p for _ in range(p)]), ("alltoall
         ts.append(time.perf_counter() - t0)
     res[name] = hc.allreduce(statistics.median(ts), op=MPI.MAX)
     res[name + "_max_send_bytes"] = max(sum(r) for r in C) * 4
+# the ragged counts kept on the device (no host exchange): kernel-side count exchange
+C = Cr
+sc_dev = torch.tensor(C[rank], dtype=torch.int64, device=dev.device)
+rc_dev = torch.empty(p, dtype=torch.int64, device=dev.device)
+xs = x[:sum(C[rank])]
+try:
+    dev.alltoallv(xs, sc_dev, y, rc_dev)
+    torch.cuda.synchronize()
+    dev.check()
+    ok = rc_dev.tolist() == [C[i][rank] for i in range(p)]
+except Exception as e:  # noqa: BLE001
+    ok = False
+    if rank == 0:
+        print(f"# alltoallv_devcounts: {e}", file=sys.stderr)
+if hc.allreduce(int(ok), op=MPI.MIN):
+    for _ in range(args.warmup):
+        dev.alltoallv(xs, sc_dev, y, rc_dev)
+    ts = []
+    for _ in range(args.iters):
+        torch.cuda.synchronize()
+        hc.Barrier()
+        t0 = time.perf_counter()
+        dev.alltoallv(xs, sc_dev, y, rc_dev)
+        torch.cuda.synchronize()
+        ts.append(time.perf_counter() - t0)
+    res["alltoallv_ragged_devcounts"] = hc.allreduce(statistics.median(ts), op=MPI.MAX)
+else:
+    res["alltoallv_ragged_devcounts"] = None
 if rank == 0:
     nbytes = n * 4
     out = {"bench": "alltoall_moe", "ranks": p, "bytes_per_rank": nbytes, "shared_gpu": dev.shared_device,
