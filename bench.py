@@ -290,9 +290,21 @@ def main() -> int:
         # headline: the reference's layer shape -- per-token row-parallel fc_o with (B, S, out)
         # outputs (reference model/func_impl.py:94-109), so the TP all-reduce carries
         # B*S x 16 partial outputs every step
-        harness = bench_forward(comm, tp=tp, batch=args.batch, steps=args.steps, warmup=args.warmup,
-                                fc_o_mode=args.fc_o_mode)
-        harness["tp_allreduce_bytes"] = (args.batch * 16 * 16 * 4 if args.fc_o_mode == "token" else args.batch * 16 * 4) \
+        mode = args.fc_o_mode
+        try:
+            harness = bench_forward(comm, tp=tp, batch=args.batch, steps=args.steps, warmup=args.warmup,
+                                    fc_o_mode=mode)
+            herr, hok = None, 1
+        except Exception as e:  # noqa: BLE001 - recorded; the pooled form is measured instead
+            harness, herr, hok = None, f"{type(e).__name__}: {e}"[:300], 0
+            log(f"harness ({mode}) failed: {herr}")
+        if not hc.allreduce(hok, op=MPI.MIN) and mode != "row":
+            torch.cuda.synchronize()
+            mode = "row"
+            harness = bench_forward(comm, tp=tp, batch=args.batch, steps=args.steps, warmup=args.warmup,
+                                    fc_o_mode=mode)
+            harness["token_error"] = herr
+        harness["tp_allreduce_bytes"] = (args.batch * 16 * 16 * 4 if mode == "token" else args.batch * 16 * 4) \
             if tp > 1 else 0
         if not args.no_secondary:
             # the other fc_o forms: pooled row-parallel (B x 16 TP all-reduce), and the token
@@ -302,10 +314,13 @@ def main() -> int:
             variants = [("pooled", "row", 1)] if args.fc_o_mode == "token" else [("token", "token", 1)]
             if tp > 1:
                 variants.append(("token_chunks4", "token", 4))
-            for name, mode, chunks in variants:
-                r = bench_forward(comm, tp=tp, batch=args.batch, steps=args.steps, warmup=args.warmup, train=False,
-                                  fc_o_mode=mode, tp_chunks=chunks)
-                other[f"{name}_fwd_ms"] = round(r["fwd_ms"], 4)
+            for name, vmode, chunks in variants:
+                try:
+                    r = bench_forward(comm, tp=tp, batch=args.batch, steps=args.steps, warmup=args.warmup,
+                                      train=False, fc_o_mode=vmode, tp_chunks=chunks)
+                    other[f"{name}_fwd_ms"] = round(r["fwd_ms"], 4)
+                except Exception as e:  # noqa: BLE001 - a secondary number must not cost the line
+                    other[f"{name}_error"] = f"{type(e).__name__}: {e}"[:200]
             harness["fc_o_variants"] = other
 
     dry = None
