@@ -208,7 +208,8 @@ def _as_array(x, writable: bool):
     torch = sys.modules.get("torch")  # never import torch from the host plane
     if torch is not None and isinstance(x, torch.Tensor):
         if x.device.type != "cpu":
-            raise TypeError("MPI host buffers must live in host memory; use Communicator for device tensors")
+            raise TypeError("MPI: this call takes host buffers; CUDA tensors work with Allreduce, Allgather, "
+                            "Reduce_scatter_block, Alltoall and Bcast (and with Communicator)")
         x = x.detach().numpy()
     if isinstance(x, (bytes, bytearray, memoryview)):
         a = np.frombuffer(x, dtype=np.uint8)
@@ -266,6 +267,12 @@ def _parse(spec, writable: bool) -> Optional[_Buf]:
     if displs is not None:
         displs = [int(d) for d in np.asarray(displs).ravel()]
     return _Buf(a, dt, counts, displs)
+
+
+def _cuda(*xs) -> bool:
+    """True when a buffer argument is a CUDA tensor (CUDA-aware-MPI calls)."""
+    torch = sys.modules.get("torch")
+    return torch is not None and any(isinstance(x, torch.Tensor) and x.is_cuda for x in xs)
 
 
 def _raw(b: Optional[_Buf]):
@@ -435,6 +442,17 @@ class Comm:
         self._rank = native.rank
         self._size = native.size
         self._nb_keep = []  # (started collective, its buffers) until the schedule is done
+        self._devgrp = None  # device plane of this communicator (first CUDA-tensor call)
+
+    def _dev(self):
+        """CUDA-aware MPI: buffer collectives given CUDA tensors run on this
+        communicator's device plane (IPC / xGMI kernels, created collectively on the
+        first such call, like any collective)."""
+        if self._devgrp is None:
+            from .device import DeviceGroup
+
+            self._devgrp = DeviceGroup(self)
+        return self._devgrp
 
     # -- identity ----------------------------------------------------------
     def Get_rank(self) -> int:
@@ -586,11 +604,17 @@ class Comm:
 
     # -- buffer collectives ---------------------------------------------------
     def Bcast(self, buf, root: int = 0) -> None:
+        if _cuda(buf):
+            self._dev().bcast(buf, root)
+            return
         if _fbcast(self._p, buf, root) is _NI:
             self._hc.bcast(_parse(buf, True).arr, root)
 
     def Allreduce(self, sendbuf, recvbuf, op: Op = SUM) -> None:
         if _fallreduce(self._p, sendbuf, recvbuf, op.code) is not _NI:
+            return
+        if _cuda(sendbuf, recvbuf):
+            self._dev().allreduce(recvbuf if sendbuf is IN_PLACE else sendbuf, recvbuf, op)
             return
         s, r = _parse(sendbuf, False), _parse(recvbuf, True)
         if s is not None and s.arr.dtype != r.arr.dtype:
@@ -607,6 +631,12 @@ class Comm:
 
     def Allgather(self, sendbuf, recvbuf) -> None:
         if _fallgather(self._p, sendbuf, recvbuf) is not _NI:
+            return
+        if _cuda(sendbuf, recvbuf):
+            if sendbuf is IN_PLACE:
+                blk = recvbuf.numel() // self.size
+                sendbuf = recvbuf.view(-1)[self.rank * blk:(self.rank + 1) * blk]
+            self._dev().allgather(sendbuf, recvbuf)
             return
         s, r = _parse(sendbuf, False), _parse(recvbuf, True)
         p = self.size
@@ -662,6 +692,11 @@ class Comm:
     def Reduce_scatter_block(self, sendbuf, recvbuf, op: Op = SUM) -> None:
         if _freduce_scatter_block(self._p, sendbuf, recvbuf, op.code) is not _NI:
             return
+        if _cuda(sendbuf, recvbuf):
+            if sendbuf is IN_PLACE:
+                raise ValueError("MPI.Reduce_scatter_block: IN_PLACE is not supported for CUDA tensors")
+            self._dev().reduce_scatter(sendbuf, recvbuf.view(-1)[:sendbuf.numel() // self.size], op)
+            return
         s, r = _parse(sendbuf, False), _parse(recvbuf, True)
         p = self.size
         if s is not None:
@@ -685,6 +720,9 @@ class Comm:
 
     def Alltoall(self, sendbuf, recvbuf) -> None:
         if _falltoall(self._p, sendbuf, recvbuf) is not _NI:
+            return
+        if _cuda(sendbuf, recvbuf):
+            self._dev().alltoall(recvbuf.clone() if sendbuf is IN_PLACE else sendbuf, recvbuf)
             return
         s, r = _parse(sendbuf, False), _parse(recvbuf, True)
         self._hc.alltoall(_raw(s), r.arr)

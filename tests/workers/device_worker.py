@@ -483,6 +483,35 @@ def ragged():
         fails.append(f"Alltoallv accounting {comm.total_bytes_transferred - before} != {sent + got}")
 
 
+def cuda_aware_mpi():
+    """CUDA-aware MPI: the raw MPI communicator's buffer collectives accept CUDA tensors
+    (its own device plane, created on the first such call)."""
+    global ncheck
+    w = MPI.COMM_WORLD
+    n = 4096
+    x, y = gen(rank, n, torch.float32, 95000), torch.empty(n, device=D)
+    w.Allreduce(x, y, op=MPI.SUM)
+    check("mpi_cuda_Allreduce", y, oracle(n, torch.float32, "SUM", 95000), torch.float32, p)
+    z = gen(rank, n, torch.float32, 95001)
+    w.Allreduce(MPI.IN_PLACE, z, op=MPI.MAX)
+    check("mpi_cuda_Allreduce_inplace", z, oracle(n, torch.float32, "MAX", 95001), torch.float32)
+    g = torch.empty(n * p, device=D)
+    w.Allgather(x, g)
+    check("mpi_cuda_Allgather", g, torch.cat([gen(r, n, torch.float32, 95000) for r in range(p)]).double(), torch.float32)
+    a = gen(rank, n * p, torch.float32, 95002)
+    b = torch.empty(n * p, device=D)
+    w.Alltoall(a, b)
+    check("mpi_cuda_Alltoall", b, torch.cat([gen(r, n * p, torch.float32, 95002)[rank * n:(rank + 1) * n]
+                                             for r in range(p)]).double(), torch.float32)
+    rs = torch.empty(n, device=D)
+    w.Reduce_scatter_block(a, rs, op=MPI.SUM)
+    check("mpi_cuda_Reduce_scatter_block", rs, oracle(n * p, torch.float32, "SUM", 95002)[rank * n:(rank + 1) * n],
+          torch.float32, p)
+    bb = gen(p - 1, n, torch.float32, 95003) if rank == p - 1 else torch.zeros(n, device=D)
+    w.Bcast(bb, root=p - 1)
+    check("mpi_cuda_Bcast", bb, gen(p - 1, n, torch.float32, 95003).double(), torch.float32)
+
+
 def tuning():
     """tune() -> per-size table used by auto, persisted through CCMPI_TUNE_FILE-style save."""
     import tempfile
@@ -521,7 +550,7 @@ if args.matrix:
     # serialized launches (AMD_SERIALIZE_KERNEL, HIP's CUDA_LAUNCH_BLOCKING) synchronise
     # around every kernel, which stream capture forbids: graphs are skipped there
     serialized = os.environ.get("AMD_SERIALIZE_KERNEL", "0") not in ("", "0")
-    for fn in (determinism, ragged) + (() if serialized else (graphs,)) + ((tuning,) if args.matrix == "quick" else ()):
+    for fn in (determinism, ragged, cuda_aware_mpi) + (() if serialized else (graphs,)) + ((tuning,) if args.matrix == "quick" else ()):
         t_s = time.time()
         fn()
         if rank == 0 and os.environ.get("CCMPI_WORKER_VERBOSE") == "1":
