@@ -20,11 +20,14 @@ Collectives run on the tensors' plane: CUDA tensors use the device plane
 (hand-written xGMI kernels, ``device_group_for``), CPU tensors the C++ host
 plane -- the reference's own CPU/NumPy setting.  CUDA bf16 GEMMs run on the
 MFMA kernels (``ops.gemm_nt`` forward / input gradient, ``ops.gemm_tn``
-weight gradient, fp32 accumulation); other dtypes use ``torch.matmul``.
+weight gradient, fp32 accumulation) up to ~2^33 multiply-adds and on hipBLASLt
+(``torch.matmul``) above, where the library GEMM measured faster; other dtypes
+use ``torch.matmul``.
 """
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 
@@ -143,9 +146,35 @@ def scatter_to_tensor_parallel_region(x, comm):
     return _ScatterLastTP.apply(x, comm)
 
 
+# Plain (unfused) GEMMs of these layers: the hand-written MFMA kernels below ~2^33
+# multiply-adds, hipBLASLt (torch.matmul) above -- measured on the Llama-3-8B MLP shapes
+# (profiles/r2_tp_mlp/gemm_ab_mlp_shapes.txt: hipBLASLt 1.5-1.6 PF/s vs 1.1-1.3 for our
+# 256x256 kernel at 4096 x {4096..28672} x {4096..28672}); CCMPI_TP_GEMM=own|blas forces one.
+# Not with several ranks on one GPU: a rank's spinning collective CTAs next to the other
+# rank's hipBLASLt kernels stalled the TP = 2 step for seconds (profiles/r2_tp_mlp), while
+# the hand-written GEMMs co-run with them.
+_TP_GEMM = os.environ.get("CCMPI_TP_GEMM", "auto")
+_BLAS_MIN_MACS = 1 << 33
+_GPU_SHARED = None
+
+
+def _gpu_shared() -> bool:
+    global _GPU_SHARED
+    if _GPU_SHARED is None:
+        local = int(os.environ.get("CCMPI_LOCAL_SIZE", os.environ.get("LOCAL_WORLD_SIZE", "1")))
+        _GPU_SHARED = local > max(1, torch.cuda.device_count())
+    return _GPU_SHARED
+
+
 def _mfma_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
-    return (x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16
-            and x.shape[-1] % 8 == 0 and w.shape[0] % 8 == 0 and w.shape[1] % 8 == 0)
+    if not (x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16
+            and x.shape[-1] % 8 == 0 and w.shape[0] % 8 == 0 and w.shape[1] % 8 == 0):
+        return False
+    if _TP_GEMM == "own":
+        return True
+    if _TP_GEMM == "blas":
+        return False
+    return x.numel() * w.shape[0] < _BLAS_MIN_MACS or _gpu_shared()
 
 
 class _LinearFn(torch.autograd.Function):
