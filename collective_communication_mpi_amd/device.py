@@ -108,6 +108,19 @@ class Work:
         return self.result
 
 
+def alltoallv_plan(counts, me: int, es: int):
+    """Byte offsets of rank ``me``'s ragged all-to-all from the p x p count matrix
+    (``counts[i][j]`` = elements rank i sends to rank j; both sides packed in rank
+    order): (send offset of each peer's segment, offset in each peer's output where
+    this rank's segment lands, segment lengths, the largest total send of any rank,
+    which sizes the grid identically on every rank)."""
+    b = np.asarray(counts, dtype=np.int64) * int(es)
+    p = b.shape[0]
+    soff = [int(x) for x in np.concatenate([[0], np.cumsum(b[me])[:-1]])]
+    doff = [int(b[:me, j].sum()) for j in range(p)]
+    return soff, doff, [int(x) for x in b[me]], int(b.sum(axis=1).max())
+
+
 def tuning_key(size: int, ranks_per_device: int, device_name: str) -> str:
     """Identity of a tuning table: group size, GPU sharing and device model."""
     return f"p{size}-share{ranks_per_device}-{device_name}"
@@ -605,13 +618,10 @@ class DeviceGroup:
         fast = bool(mat[:, p].all()) and not np.any((counts * es) % 16)
         s = self._stream()
         if fast:
-            b = counts * es
-            soff = np.concatenate([[0], np.cumsum(b[me])[:-1]]).astype(np.uint64).tolist()
-            doff = [int(b[:me, j].sum()) for j in range(p)]
-            grid_bytes = int(b.sum(axis=1).max())
+            soff, doff, lens, grid_bytes = alltoallv_plan(counts, me, es)
             out = dst if rtot_local else self.scratch
-            self.dc.alltoallv(src.data_ptr(), out.data_ptr(), max(16, rtot_local * es), [int(x) for x in soff], doff,
-                              [int(x) for x in b[me]], grid_bytes, s, self._budget(max_blocks))
+            self.dc.alltoallv(src.data_ptr(), out.data_ptr(), max(16, rtot_local * es), soff, doff, lens, grid_bytes, s,
+                              self._budget(max_blocks))
             return dst
         # padded fallback: blocks of the largest count through the regular all-to-all
         m = int(counts.max())

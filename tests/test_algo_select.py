@@ -60,3 +60,51 @@ def test_tuning_file_roundtrip(tmp_path):
     assert load_tuning(path, tuning_key(4, 1, "x")) == {}
     g = SimpleNamespace(size=8, tuned=load_tuning(path, k8), ll_auto_max=64 << 10, oneshot_max=64 << 10, disabled=set())
     assert pick(g, 1 << 20) == "fanout" and pick(g, 4096) == "ll"
+
+
+def test_alltoallv_plan_offsets():
+    """Ragged all-to-all offsets (DeviceGroup.alltoallv): every rank's segment for rank j
+    lands right after the segments of ranks < it in j's output, and the per-rank plans
+    tile every output exactly once."""
+    import numpy as np
+
+    from collective_communication_mpi_amd.device import alltoallv_plan
+
+    rng = np.random.default_rng(0)
+    for p in (1, 2, 3, 8):
+        C = rng.integers(0, 9, (p, p)) * 4
+        es = 4
+        plans = [alltoallv_plan(C, me, es) for me in range(p)]
+        for me, (soff, doff, lens, grid) in enumerate(plans):
+            assert lens == [int(c) * es for c in C[me]]
+            assert soff == [int(C[me, :j].sum()) * es for j in range(p)]
+            assert grid == int(C.sum(axis=1).max()) * es
+        for j in range(p):  # rank j's output: [sum_i C[i, j]] covered once, in source order
+            segs = sorted((plans[i][1][j], plans[i][2][j]) for i in range(p))
+            pos = 0
+            for off, ln in segs:
+                assert off == pos
+                pos += ln
+            assert pos == int(C[:, j].sum()) * es
+
+
+def test_tp_gemm_routing(monkeypatch):
+    """TP layers: hand-written MFMA GEMMs below 2^33 multiply-adds and whenever ranks
+    share a GPU, hipBLASLt (torch.matmul) above; CCMPI_TP_GEMM forces either."""
+    import torch
+
+    from collective_communication_mpi_amd.parallel import tensor_parallel as tpm
+
+    x = SimpleNamespace(is_cuda=True, dtype=torch.bfloat16, shape=(4096, 4096), numel=lambda: 4096 * 4096)
+    w_big = SimpleNamespace(dtype=torch.bfloat16, shape=(28672, 4096))
+    w_small = SimpleNamespace(dtype=torch.bfloat16, shape=(256, 4096))
+    monkeypatch.setattr(tpm, "_TP_GEMM", "auto")
+    monkeypatch.setattr(tpm, "_GPU_SHARED", False)
+    assert tpm._mfma_ok(x, w_small) and not tpm._mfma_ok(x, w_big)
+    monkeypatch.setattr(tpm, "_GPU_SHARED", True)
+    assert tpm._mfma_ok(x, w_big)
+    monkeypatch.setattr(tpm, "_GPU_SHARED", False)
+    monkeypatch.setattr(tpm, "_TP_GEMM", "own")
+    assert tpm._mfma_ok(x, w_big)
+    monkeypatch.setattr(tpm, "_TP_GEMM", "blas")
+    assert not tpm._mfma_ok(x, w_small)
