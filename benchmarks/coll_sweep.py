@@ -60,7 +60,7 @@ DEFAULT_ALGOS = {
     "allreduce": ["ll", "oneshot", "twoshot", "fanout", "fanout_lds", "push", "reduce_bcast", "ring", "rhd"],
     "allgather": ["direct", "push"],
     "reduce_scatter": ["direct"],
-    "alltoall": ["direct", "push"],
+    "alltoall": ["direct", "push", "pairwise"],  # pairwise: same bytes, one peer per round
     "lastaxis": ["gather", "rscatter"],
     "bcast": ["direct", "push"],
 }
@@ -181,7 +181,7 @@ blocks = [int(b) for b in args.blocks.split(",")]
 for op in ops:
     algos = DEFAULT_ALGOS[op]
     if args.algos:  # the requested algorithms this op has (lastaxis: gather / rscatter)
-        valid = set(DEFAULT_ALGOS[op]) | {"rccl"} | ({"ring_rccl", "rhd_rccl"} if op == "allreduce" else set()) \
+        valid = set(DEFAULT_ALGOS[op]) | {"rccl"} \
             | ({"pairwise"} if op == "alltoall" else set())
         algos = [a for a in args.algos.split(",") if a in valid] or DEFAULT_ALGOS[op]
     for algo in algos:

@@ -37,6 +37,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--shapes", default=",".join(DEFAULT))
     ap.add_argument("--json", default="")
+    ap.add_argument("--all", action="store_true", help="also the 128x128 and 256x192 kernels")
     args = ap.parse_args()
     D = _native.device()
     out = []
@@ -54,11 +55,20 @@ def main():
                 gemm_nt(a, b, out=c)
             return f
 
-        variants = {"k128": ours(1), "k256": ours(2), "k256x192": ours(4), "auto": ours(0),
+        def w4(sched):
+            def f():
+                D.gemm_set_kernel(5)
+                D.gemm_set_w4_sched(sched)
+                gemm_nt(a, b, out=c)
+            return f
+
+        variants = {"k256": ours(2), "w4s0": w4(0), "w4s1": w4(1), "auto": ours(0),
                     "hipblaslt": lambda: torch.matmul(a, b.T, out=c)}
+        if args.all:
+            variants.update({"k128": ours(1), "k256x192": ours(4)})
         # correctness of both kernels on this shape against hipBLASLt
         ref = (a @ b.T).float()
-        for k in ("k128", "k256", "k256x192"):
+        for k in [v for v in variants if v not in ("auto", "hipblaslt")]:
             variants[k]()
             err = (c.float() - ref).abs().max().item()
             assert err < 0.05 * K ** 0.5, f"{k} {shp}: max err {err}"

@@ -71,8 +71,6 @@ def a2a():
 res["ranks_per_device"] = dev.ranks_per_device
 if step("ncclCommInitRank", init):
     step("ncclAllReduce", ar("rccl"))
-    step("ring_rccl", ar("ring_rccl"))
-    step("rhd_rccl", ar("rhd_rccl"))
     step("pairwise_alltoall", a2a)
 allres = comm.comm.gather(res, root=0)
 if rank == 0:

@@ -415,8 +415,9 @@ class Communicator(object):
     def myAlltoall(self, src_array, dest_array, algo: str = "direct"):
         """Non-blocking all-to-all (reference comm.py:110-159): every Irecv is posted
         before any Isend, then Waitall.  (The reference docstring says Sendrecv;
-        it is Irecv/Isend.)  On device tensors: direct peer-read kernel, or
-        ``algo="pairwise"`` (RCCL P2P rounds) / ``"rccl"``."""
+        it is Irecv/Isend.)  On device tensors: direct peer-read kernel, ``"push"``
+        (peer writes), ``"pairwise"`` (hand-written pairwise rounds),
+        ``"pairwise_rccl"`` (RCCL P2P rounds) or ``"rccl"``."""
         rank = self.comm.Get_rank()
         size = self.comm.Get_size()
         isz, n = _nbytes_items(src_array)
@@ -452,7 +453,9 @@ class Communicator(object):
     def myAlltoall2(self, src_array, dest_array, algo: str = "pairwise"):
         """Pairwise blocking all-to-all (reference comm.py:162-199): for i in rank
         order, Sendrecv with rank i (deadlock-free: the pair (a, b) is handled at
-        step b on rank a and step a on rank b)."""
+        step b on rank a and step a on rank b).  On device tensors the hand-written
+        pairwise kernel (round k: push to rank + k, wait for rank - k; one peer per
+        round over the flag protocol), or ``algo="pairwise_rccl"`` / ``"rccl"``."""
         rank = self.comm.Get_rank()
         size = self.comm.Get_size()
         isz, n = _nbytes_items(src_array)

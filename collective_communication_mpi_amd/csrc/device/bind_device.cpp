@@ -76,6 +76,7 @@ PYBIND11_MODULE(_device, m) {
   m.attr("ALGO_TWOSHOT_FANOUT_LDS") = (int)ALGO_TWOSHOT_FANOUT_LDS;
   m.attr("A2A_PULL") = (int)A2A_PULL;
   m.attr("A2A_PUSH") = (int)A2A_PUSH;
+  m.attr("A2A_PAIRWISE") = (int)A2A_PAIRWISE;
   m.attr("MAX_RINGS") = kMaxRings;
   m.def("ring_slot_bytes", &DeviceComm::ring_slot_bytes);
   m.attr("MAX_RANKS") = kMaxRanks;
@@ -150,8 +151,6 @@ PYBIND11_MODULE(_device, m) {
       .def("rccl_allgather", &DeviceComm::rccl_allgather, py::call_guard<py::gil_scoped_release>())
       .def("rccl_alltoall", &DeviceComm::rccl_alltoall, py::call_guard<py::gil_scoped_release>())
       .def("rccl_bcast", &DeviceComm::rccl_bcast, py::call_guard<py::gil_scoped_release>())
-      .def("p2p_ring_allreduce", &DeviceComm::p2p_ring_allreduce, py::call_guard<py::gil_scoped_release>())
-      .def("p2p_rhd_allreduce", &DeviceComm::p2p_rhd_allreduce, py::call_guard<py::gil_scoped_release>())
       .def("p2p_pairwise_alltoall", &DeviceComm::p2p_pairwise_alltoall, py::call_guard<py::gil_scoped_release>())
       .def("error_code", &DeviceComm::error_code, py::call_guard<py::gil_scoped_release>())
       .def("clear_error", &DeviceComm::clear_error)

@@ -1115,6 +1115,38 @@ __global__ void __launch_bounds__(kThreads) k_allreduce_rhd(CollArgs a) {
 }
 
 
+// Pairwise all-to-all (reference myAlltoall2, mpi_wrapper/comm.py:162-199): p - 1
+// rounds after the local block; in round k rank r pushes its block for
+// to = r + k into to's output (posted peer writes, one peer in flight per round),
+// flags it, and waits for the block from r - k before the next round -- the
+// reference's Sendrecv pairing, exchange by exchange.  Every CTA moves its
+// 16-B slice of each block and pairs its flags with CTA b of the peers (one
+// monotonic step word per (block, source), like the ring).  The start barrier
+// guarantees every peer has entered the call before anything lands in its
+// output; no end barrier: a rank returns once every block addressed to it is
+// flagged, and it never reads peer memory.
+__global__ void __launch_bounds__(kThreads) k_alltoall_pairwise(CollArgs a) {
+  __shared__ uint64_t s_epoch;
+  __shared__ uint64_t codes[2][kMaxRanks];
+  if (!start_phase(a, &s_epoch, codes)) return;
+  const uint64_t e = s_epoch;
+  const PeerTable* pt = a.pt;
+  const int me = pt->rank, p = pt->size, b = blockIdx.x;
+  const uint64_t ss = a.src_stride ? a.src_stride : a.nbytes;
+  const uint64_t ds = a.dst_stride ? a.dst_stride : a.nbytes;
+  const uint64_t base = e * kStepsPerEpoch;
+  const BlockRange q = part16(a.nbytes, gridDim.x, b);
+  const uint64_t len = q.hi - q.lo;
+  if (len) copy_span(a.in + (uint64_t)me * ss + q.lo, resolve(pt, me, codes[1][me]) + (uint64_t)me * ds + q.lo, len);
+  for (int k = 1; k < p; ++k) {
+    const int to = (me + k) % p, from = (me + p - k) % p;
+    if (len) copy_span(a.in + (uint64_t)to * ss + q.lo, resolve(pt, to, codes[1][to]) + (uint64_t)me * ds + q.lo, len);
+    post_step(&pt->sig[to]->step[b][me], base + k);
+    if (!await_step(a, &pt->sig[me]->step[b][from], base + k, from)) return;
+  }
+  finish(a, e);
+}
+
 // Last-axis collectives for tensor parallelism (fused layout transform):
 //   MODE 0 all-gather : out[m][j*k + c] = in_j[m][c]                (M x k shards -> M x p*k)
 //   MODE 1 reduce-scat: out[m][c] = sum_j in_j[m][me*k + c]          (M x p*k      -> M x k)
@@ -1323,6 +1355,11 @@ void launch_move(int mode, const CollArgs& a, int nranks, int grid, hipStream_t 
       default: throw std::invalid_argument("ccmpi: bad move mode");
     }
   });
+  CCMPI_HIP_CHECK(hipGetLastError());
+}
+
+void launch_alltoall_pairwise(const CollArgs& a, int grid, hipStream_t s) {
+  hipLaunchKernelGGL(k_alltoall_pairwise, dim3(grid), dim3(kThreads), 0, s, a);
   CCMPI_HIP_CHECK(hipGetLastError());
 }
 

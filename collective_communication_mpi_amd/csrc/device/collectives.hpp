@@ -31,7 +31,7 @@ enum MoveMode : int {
 };
 
 constexpr int kMaxRings = 8;
-enum AlltoallMode : int { A2A_PULL = 0, A2A_PUSH = 1 };
+enum AlltoallMode : int { A2A_PULL = 0, A2A_PUSH = 1, A2A_PAIRWISE = 2 };
 
 struct CollArgs {
   const PeerTable* pt;     // device-resident peer table
@@ -94,6 +94,9 @@ void launch_move(int mode, const CollArgs& a, int nranks, int grid, hipStream_t 
 void launch_lastaxis(int mode, const CollArgs& a, int nranks, int dtype, int op, int grid, hipStream_t s);
 void launch_local_reduce(const LocalReduceArgs& a, int dtype, int op, hipStream_t s);
 void launch_alltoallv(const VArgs& v, int grid, hipStream_t s);
+// pairwise rounds (push, one peer per round): a.in local input, a.res_code the
+// registered output (or scratch), nbytes per block, src/dst strides as k_move
+void launch_alltoall_pairwise(const CollArgs& a, int grid, hipStream_t s);
 void launch_alltoallv_dev(const VDevArgs& v, int grid, hipStream_t s);
 
 }  // namespace dev

@@ -368,8 +368,9 @@ uint64_t DeviceComm::ring_slot_bytes(uint64_t nbytes, int p) {
 // `symmetric` (the caller's promise, identical on every rank): every rank's
 // output is registered and its input 16-B aligned, so results are pushed
 // straight into peers' outputs.  Otherwise the result goes through the scratch
-// segment (and a misaligned input is staged too) in pieces of at most half the
-// scratch; piece sizes depend only on values equal on all ranks.
+// segment (and a misaligned input is staged too).  Pieces are at most half the
+// scratch either way, so the launch sequence depends only on values equal on
+// all ranks (inbox and scratch sizes, nbytes), never on `symmetric`.
 void DeviceComm::allreduce_pipelined_(int algo, uint64_t in, uint64_t out, uint64_t nbytes, uint64_t es, int dtype,
                                       int op, hipStream_t st, int max_blocks, bool symmetric) {
   const int p = size_;
@@ -390,7 +391,9 @@ void DeviceComm::allreduce_pipelined_(int algo, uint64_t in, uint64_t out, uint6
   if (symmetric && (!in_al || out % 16 || !code_of_(out, nbytes)))
     throw std::invalid_argument("ccmpi: symmetric ring/rhd all-reduce needs a registered output and aligned input");
   const bool out_reg = symmetric;
-  if (!symmetric) piece = std::min(piece, half);
+  // the piece size must not depend on `symmetric` (a per-rank view of the caller's
+  // buffers): every rank splits into the same launches even if one rank stages
+  piece = std::min(piece, half);
   piece = staging_chunk_(piece, 16 * es);
   if (piece == 0) throw std::runtime_error("ccmpi: inbox/scratch too small for ring/rhd");
   char* stage = reinterpret_cast<char*>(scratch_ptr());
@@ -540,6 +543,10 @@ void DeviceComm::alltoall(uint64_t in, uint64_t out, uint64_t bytes_per_peer, ui
   }
   const uint64_t total = bytes_per_peer * size_;
   const bool aligned = in % 16 == 0 && out % 16 == 0 && bytes_per_peer % 16 == 0;
+  if (mode == A2A_PAIRWISE) {
+    alltoall_pairwise_(in, out, bytes_per_peer, st, max_blocks, symmetric && in != out && aligned);
+    return;
+  }
   if (symmetric && in != out && aligned) {
     if (mode == A2A_PUSH) {
       // every rank's OUTPUT is registered: peer writes straight into it, the input stays local
@@ -573,6 +580,48 @@ void DeviceComm::alltoall(uint64_t in, uint64_t out, uint64_t bytes_per_peer, ui
     launch_move_m(MOVE_ALLTOALL, a, size_, grid_(n * size_, max_blocks), st);
     if (!direct)
       CCMPI_HIP_CHECK(hipMemcpy2DAsync((void*)(out + off), bytes_per_peer, gath, n, n, size_, hipMemcpyDeviceToDevice, st));
+  }
+}
+
+// Pairwise rounds push into every peer's output: registered outputs on every rank
+// (`symmetric`, the caller's global promise) take the blocks directly; otherwise
+// they land in the peers' scratch segments ([p][chunk], identical chunking on every
+// rank) and a strided copy moves them out.  In place is always staged (a peer's
+// block could overwrite input not yet sent).
+void DeviceComm::alltoall_pairwise_(uint64_t in, uint64_t out, uint64_t bytes_per_peer, hipStream_t st,
+                                    int max_blocks, bool symmetric) {
+  const uint64_t total = bytes_per_peer * size_;
+  if (symmetric) {
+    const uint64_t rc = code_of_(out, total);
+    if (!rc) throw std::invalid_argument("ccmpi: symmetric pairwise alltoall needs a registered output on every rank");
+    CollArgs a = args_(0, rc, (char*)out, bytes_per_peer, 0);
+    a.in = reinterpret_cast<const char*>(in);
+    launch_alltoall_pairwise(a, grid_(bytes_per_peer, max_blocks), st);
+    return;
+  }
+  uint64_t chunk = staging_chunk_(scratch_bytes() / 2 / size_, 16);
+  if (chunk == 0) throw std::runtime_error("ccmpi: scratch too small for alltoall");
+  char* stage = reinterpret_cast<char*>(scratch_ptr());
+  char* src = reinterpret_cast<char*>(in);
+  if (in == out || in % 16) {
+    // the input must stay intact until sent and be 16-B aligned: second half of scratch
+    chunk = staging_chunk_(scratch_bytes() / 4 / size_, 16);
+  }
+  char* pack = stage + scratch_bytes() / 2;
+  for (uint64_t off = 0; off < bytes_per_peer; off += chunk) {
+    const uint64_t n = std::min(chunk, bytes_per_peer - off);
+    CollArgs a = args_(0, addr_code(0, 0), stage, n, 0);
+    if (in == out || in % 16) {
+      CCMPI_HIP_CHECK(hipMemcpy2DAsync(pack, n, src + off, bytes_per_peer, n, size_, hipMemcpyDeviceToDevice, st));
+      a.in = pack;
+      a.src_stride = n;
+    } else {
+      a.in = src + off;
+      a.src_stride = bytes_per_peer;
+    }
+    a.dst_stride = n;
+    launch_alltoall_pairwise(a, grid_(n, max_blocks), st);
+    CCMPI_HIP_CHECK(hipMemcpy2DAsync((void*)(out + off), bytes_per_peer, stage, n, n, size_, hipMemcpyDeviceToDevice, st));
   }
 }
 
@@ -795,132 +844,6 @@ void DeviceComm::rccl_alltoall(uint64_t in, uint64_t out, uint64_t count, int dt
 void DeviceComm::rccl_bcast(uint64_t buf, uint64_t count, int dtype, int root, uint64_t stream) {
   CCMPI_NEED_RCCL();
   CCMPI_NCCL_CHECK(ncclBroadcast((void*)buf, (void*)buf, count, nccl_dt(dtype), root, nccl_, S(stream)));
-}
-
-namespace {
-int gcd(int a, int b) { return b ? gcd(b, a % b) : a; }
-int modinv(int a, int m) {
-  for (int x = 1; x < m; ++x)
-    if ((a * x) % m == 1) return x;
-  return 1;
-}
-}  // namespace
-
-void DeviceComm::p2p_ring_allreduce(uint64_t buf, uint64_t count, int dtype, int op, uint64_t stream, int rings,
-                                    uint64_t tmp) {
-  CCMPI_NEED_RCCL();
-  const int p = size_;
-  if (p == 1 || count == 0) return;
-  const uint64_t es = dtype_bytes(dtype);
-  const uint64_t q = std::max<uint64_t>(1, 16 / es);  // elements per 16 B
-  hipStream_t st = S(stream);
-  ncclDataType_t ndt = nccl_dt(dtype);
-  // strides coprime to p -> Hamiltonian rings i -> i+s (mod p)
-  std::vector<int> strides;
-  for (int s = 1; s < p && (int)strides.size() < std::max(1, rings); ++s)
-    if (gcd(s, p) == 1) strides.push_back(s);
-  const int R = (int)strides.size();
-  // element layout: ring k owns part k; each part has p chunks (16-B aligned)
-  std::vector<uint64_t> part_lo(R + 1);
-  for (int k = 0; k <= R; ++k) part_lo[k] = (count * k / R) / q * q;
-  part_lo[R] = count;
-  auto chunk_of = [&](int k, int c, uint64_t* lo, uint64_t* n) {
-    uint64_t plo = part_lo[k], pn = part_lo[k + 1] - plo;
-    uint64_t a = (pn * c / p) / q * q, b = c + 1 == p ? pn : (pn * (c + 1) / p) / q * q;
-    *lo = plo + a;
-    *n = b - a;
-  };
-  // temp area per ring: the largest chunk of that ring
-  std::vector<uint64_t> tmp_off(R + 1, 0);
-  for (int k = 0; k < R; ++k) {
-    uint64_t mx = 0;
-    for (int c = 0; c < p; ++c) { uint64_t lo, n; chunk_of(k, c, &lo, &n); mx = std::max(mx, n); }
-    tmp_off[k + 1] = tmp_off[k] + (mx * es + 15) / 16 * 16;
-  }
-  std::vector<int> idx(R), right(R), left(R);
-  for (int k = 0; k < R; ++k) {
-    int s = strides[k];
-    idx[k] = (rank_ * modinv(s, p)) % p;  // position in ring 0, s, 2s, ...
-    right[k] = (rank_ + s) % p;
-    left[k] = (rank_ - s + p) % p;
-  }
-  char* b = reinterpret_cast<char*>(buf);
-  char* t = reinterpret_cast<char*>(tmp);
-  // reduce-scatter
-  for (int step = 0; step < p - 1; ++step) {
-    CCMPI_NCCL_CHECK(ncclGroupStart());
-    for (int k = 0; k < R; ++k) {
-      uint64_t slo, sn, rlo, rn;
-      chunk_of(k, ((idx[k] - step) % p + p) % p, &slo, &sn);
-      chunk_of(k, ((idx[k] - step - 1) % p + p) % p, &rlo, &rn);
-      if (sn) CCMPI_NCCL_CHECK(ncclSend(b + slo * es, sn, ndt, right[k], nccl_, st));
-      if (rn) CCMPI_NCCL_CHECK(ncclRecv(t + tmp_off[k], rn, ndt, left[k], nccl_, st));
-    }
-    CCMPI_NCCL_CHECK(ncclGroupEnd());
-    for (int k = 0; k < R; ++k) {
-      uint64_t rlo, rn;
-      chunk_of(k, ((idx[k] - step - 1) % p + p) % p, &rlo, &rn);
-      if (rn) local_reduce({(uint64_t)(b + rlo * es), (uint64_t)(t + tmp_off[k])}, (uint64_t)(b + rlo * es), rn, dtype, op, stream);
-    }
-  }
-  // all-gather: rank holds reduced chunk idx+1
-  for (int step = 0; step < p - 1; ++step) {
-    CCMPI_NCCL_CHECK(ncclGroupStart());
-    for (int k = 0; k < R; ++k) {
-      uint64_t slo, sn, rlo, rn;
-      chunk_of(k, ((idx[k] + 1 - step) % p + p) % p, &slo, &sn);
-      chunk_of(k, ((idx[k] - step) % p + p) % p, &rlo, &rn);
-      if (sn) CCMPI_NCCL_CHECK(ncclSend(b + slo * es, sn, ndt, right[k], nccl_, st));
-      if (rn) CCMPI_NCCL_CHECK(ncclRecv(b + rlo * es, rn, ndt, left[k], nccl_, st));
-    }
-    CCMPI_NCCL_CHECK(ncclGroupEnd());
-  }
-}
-
-void DeviceComm::p2p_rhd_allreduce(uint64_t buf, uint64_t count, int dtype, int op, uint64_t stream, uint64_t tmp) {
-  CCMPI_NEED_RCCL();
-  const int p = size_;
-  if (p == 1 || count == 0) return;
-  if (p & (p - 1)) throw std::invalid_argument("ccmpi: recursive halving-doubling needs a power-of-two rank count");
-  const uint64_t es = dtype_bytes(dtype);
-  const uint64_t q = std::max<uint64_t>(1, 16 / es);
-  hipStream_t st = S(stream);
-  ncclDataType_t ndt = nccl_dt(dtype);
-  char* b = reinterpret_cast<char*>(buf);
-  char* t = reinterpret_cast<char*>(tmp);
-  auto cut = [&](uint64_t lo, uint64_t hi) { uint64_t m = lo + ((hi - lo) / 2) / q * q; return m; };
-  uint64_t lo = 0, hi = count;
-  std::vector<std::pair<uint64_t, uint64_t>> hist;
-  for (int mask = p / 2; mask >= 1; mask /= 2) {
-    const int partner = rank_ ^ mask;
-    const uint64_t mid = cut(lo, hi);
-    uint64_t keep_lo, keep_hi, send_lo, send_hi;
-    if (rank_ & mask) { keep_lo = mid; keep_hi = hi; send_lo = lo; send_hi = mid; }
-    else { keep_lo = lo; keep_hi = mid; send_lo = mid; send_hi = hi; }
-    CCMPI_NCCL_CHECK(ncclGroupStart());
-    if (send_hi > send_lo) CCMPI_NCCL_CHECK(ncclSend(b + send_lo * es, send_hi - send_lo, ndt, partner, nccl_, st));
-    if (keep_hi > keep_lo) CCMPI_NCCL_CHECK(ncclRecv(t, keep_hi - keep_lo, ndt, partner, nccl_, st));
-    CCMPI_NCCL_CHECK(ncclGroupEnd());
-    if (keep_hi > keep_lo)
-      local_reduce({(uint64_t)(b + keep_lo * es), (uint64_t)t}, (uint64_t)(b + keep_lo * es), keep_hi - keep_lo, dtype, op, stream);
-    hist.push_back({lo, hi});
-    lo = keep_lo;
-    hi = keep_hi;
-  }
-  for (int mask = 1; mask <= p / 2; mask *= 2) {
-    const int partner = rank_ ^ mask;
-    auto prev = hist.back();
-    hist.pop_back();
-    // partner owns the other half of `prev`
-    uint64_t olo = (lo == prev.first) ? hi : prev.first;
-    uint64_t ohi = (lo == prev.first) ? prev.second : lo;
-    CCMPI_NCCL_CHECK(ncclGroupStart());
-    if (hi > lo) CCMPI_NCCL_CHECK(ncclSend(b + lo * es, hi - lo, ndt, partner, nccl_, st));
-    if (ohi > olo) CCMPI_NCCL_CHECK(ncclRecv(b + olo * es, ohi - olo, ndt, partner, nccl_, st));
-    CCMPI_NCCL_CHECK(ncclGroupEnd());
-    lo = prev.first;
-    hi = prev.second;
-  }
 }
 
 void DeviceComm::p2p_pairwise_alltoall(uint64_t in, uint64_t out, uint64_t bytes_per_peer, uint64_t stream) {

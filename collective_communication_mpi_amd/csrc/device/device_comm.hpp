@@ -104,12 +104,7 @@ class DeviceComm {
   void rccl_allgather(uint64_t in, uint64_t out, uint64_t count, int dtype, uint64_t stream);
   void rccl_alltoall(uint64_t in, uint64_t out, uint64_t count, int dtype, uint64_t stream);
   void rccl_bcast(uint64_t buf, uint64_t count, int dtype, int root, uint64_t stream);
-  // Ring / recursive-halving-doubling all-reduce built from RCCL send/recv plus
-  // our local reduction kernel (north-star "hand-written on RCCL P2P").
-  // `rings` concurrent rings with strides coprime to p use that many links.
-  void p2p_ring_allreduce(uint64_t buf, uint64_t count, int dtype, int op, uint64_t stream, int rings,
-                          uint64_t tmp);
-  void p2p_rhd_allreduce(uint64_t buf, uint64_t count, int dtype, int op, uint64_t stream, uint64_t tmp);
+  // reference myAlltoall2 rounds as grouped RCCL send/recv (the library form of algo="pairwise")
   void p2p_pairwise_alltoall(uint64_t in, uint64_t out, uint64_t bytes_per_peer, uint64_t stream);
 
   // ---- health ------------------------------------------------------------
@@ -139,6 +134,8 @@ class DeviceComm {
 
  private:
   void sync_table_();
+  void alltoall_pairwise_(uint64_t in, uint64_t out, uint64_t bytes_per_peer, hipStream_t st, int max_blocks,
+                          bool symmetric);
   void allreduce_ll_(uint64_t in, uint64_t out, uint64_t nbytes, int dtype, int op, hipStream_t st, int max_blocks);
   void allreduce_pipelined_(int algo, uint64_t in, uint64_t out, uint64_t nbytes, uint64_t es, int dtype, int op,
                             hipStream_t st, int max_blocks, bool symmetric);

@@ -928,6 +928,11 @@ void gemm_nt(uint64_t A, uint64_t B, uint64_t C, uint64_t bias, int M, int N, in
   }
   // 256 x {256, 192, 128} ping-pong kernels: need K % 128 and enough tiles to
   // occupy the 256 CUs (one block per CU); smaller grids keep 128x128.
+  if (g_kernel == 5 && gemm_w4_ok(g)) {
+    launch_gemm_nt_w4(g, reinterpret_cast<hipStream_t>(stream));
+    CCMPI_HIP_CHECK(hipGetLastError());
+    return;
+  }
   const bool big_ok = K % (2 * BK) == 0 && g_use_glds;
   if (big_ok && g_kernel != 1) {
     int bn = 0;
@@ -1062,7 +1067,9 @@ void register_gemm_ops(pybind11::module_& m) {
   m.def("gemm_set_glds", [](bool on) { g_use_glds = on; }, "select LDS-DMA (True) or register staging");
   m.def("gemm_set_direct_epilogue", [](bool on) { g_direct_epi = on; },
         "128x128 LDS-DMA kernel: LDS-free epilogue (True) or LDS-staged rows");
-  m.def("gemm_set_kernel", [](int k) { g_kernel = k; }, "gemm_nt tile choice: 0 auto, 1 128x128, 2 256x256, 3 256x128, 4 256x192");
+  m.def("gemm_set_kernel", [](int k) { g_kernel = k; },
+        "gemm_nt tile choice: 0 auto, 1 128x128, 2 256x256, 3 256x128, 4 256x192, 5 256x256 four-wave");
+  m.def("gemm_set_w4_sched", [](int v) { g_w4_sched = v; }, "four-wave kernel main-loop schedule (benchmarks)");
   m.def("gemm_set_ablation", [](int e) {
     g_pp_exp = e;
     CCMPI_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_pp_exp_dev), &e, sizeof(int)));

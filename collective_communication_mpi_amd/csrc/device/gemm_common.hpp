@@ -170,7 +170,11 @@ int gemm256_tiles(int M, int N, int bn);
 extern int g_pp_exp;
 // TN (weight-gradient) form of the 256x256 ping-pong kernel; K (reduction rows) % 128 == 0,
 // N1, N2 % 8 == 0.  splitk > 1: g.C is a workspace of splitk fp32 [N1][N2] slices.
-void launch_gemm_tn_256(const GemmArgs& g, hipStream_t stream);  // ablation variant of the ping-pong kernel (benchmarks only; 0 = production)
+void launch_gemm_tn_256(const GemmArgs& g, hipStream_t stream);
+// 256 x 256 four-wave kernel (gemm_w4.hip): 128 x 128 per wave, K % 64 == 0, no split-K
+bool gemm_w4_ok(const GemmArgs& g);
+extern int g_w4_sched;  // main-loop schedule variant of the four-wave kernel (benchmarks)
+void launch_gemm_nt_w4(const GemmArgs& g, hipStream_t stream);  // ablation variant of the ping-pong kernel (benchmarks only; 0 = production)
 
 }  // namespace gemm
 }  // namespace dev

@@ -1,0 +1,307 @@
+// 256x256 bf16 "NT" GEMM with four waves of 128x128 each (one wave per SIMD).
+//
+// Why this shape (profiles/r3_gemm): hipBLASLt's kernel on the Llama-3-8B MLP
+// shapes is MT256x256x64 with four 16x16 MFMA waves (256-thread workgroups, one per
+// CU, 130 KB LDS) and keeps the matrix pipe busy 84 % of the time; our 8-wave
+// ping-pong kernel (gemm256.hip) gives every wave a 128x64 tile, pays two
+// barriers per 16 MFMAs and sits at 54 %.  A 128x128 wave tile halves the LDS
+// bytes read per MFMA (16 fragment reads feed 64 MFMAs) and needs one barrier
+// per 128 MFMAs.
+//
+// Per workgroup: C tile 256(M) x 256(N), K-tiles of 64, two LDS stages of
+// 64 KiB (A 256 x 128 B + B 256 x 128 B rows, 16-B chunks XOR-swizzled by
+// row & 7).  Staging is LDS-DMA (buffer_load ... lds) through one buffer
+// descriptor per operand and tile: rows past M / N read as zero (buffer bounds),
+// one VGPR of per-lane offset, the K and piece offsets in SGPRs.
+//
+// Main loop, K-tile t (fragment sets F0 = k 0..31, F1 = k 32..63 of a tile):
+//   X: DMA tile t+1 into the other stage | read F0(t)       | 64 MFMA on F1(t-1)
+//   Y:                                     read F1(t)       | 64 MFMA on F0(t)
+//      vmcnt(0) + lgkmcnt(0) + barrier   (tile t+1 landed; every wave is done
+//                                          reading stage t, which the DMA of
+//                                          tile t+2 overwrites next)
+// so each DMA has two MFMA phases (~2k cycles) to land and each fragment read one.
+// Epilogue: per wave, two 64-row halves staged through LDS as fp32, written
+// as whole 16-B row vectors (alpha, bias, activation, accumulate, fp32/bf16 out).
+#include <hip/hip_runtime.h>
+
+#include "gemm_common.hpp"
+
+namespace ccmpi {
+namespace dev {
+namespace gemm {
+namespace {
+
+constexpr int WM = 256, WNB = 256, WK = 64, WNT = 256, kGroupM4 = 8;
+constexpr int kOpBytes = 256 * 128;           // one operand's K-tile (256 rows x 64 bf16)
+constexpr int kStage4 = 2 * kOpBytes;         // A + B
+constexpr int kEpiTS = 132;                   // epilogue fp32 row stride (128 + 4 pad)
+constexpr int kEpiWave = 64 * kEpiTS * 4;     // one wave's 64-row half
+constexpr int kLds4 = (2 * kStage4 > 4 * kEpiWave) ? 2 * kStage4 : 4 * kEpiWave;
+
+typedef __attribute__((address_space(3))) void* lds_vptr;
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t op_rsrc(const uint16_t* base, long rows, int ld) {
+  // rows <= 0: an empty descriptor (every load reads 0)
+  long bytes = rows > 0 ? rows * (long)ld * 2 : 0;
+  if (bytes > 0x7ffffff0l) bytes = 0x7ffffff0l;
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(base), 0, (int)bytes, 0x00020000);
+}
+
+template <int SCHED>
+__global__ void __launch_bounds__(WNT, 1) k_gemm_w4(GemmArgs g) {
+  extern __shared__ __attribute__((aligned(1024))) unsigned char smem[];
+  const int tiles_n = (g.N + WNB - 1) / WNB, tiles_m = (g.M + WM - 1) / WM;
+  const int nwg = tiles_n * tiles_m;
+  int wg = xcd_remap(blockIdx.x, nwg);
+  int tm, tn;
+  {  // group-M order: the 32 tiles an XCD runs at once form an 8 x 4 block
+    const int per_group = kGroupM4 * tiles_n;
+    const int first_m = (wg / per_group) * kGroupM4;
+    const int gm = min(tiles_m - first_m, kGroupM4);
+    tm = first_m + (wg % per_group) % gm;
+    tn = (wg % per_group) / gm;
+  }
+  const int bm = tm * WM, bn = tn * WNB;
+  const int t = threadIdx.x, lane = t & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wr = wave >> 1, wc = wave & 1;
+
+  // ---- staging: 32 pieces of 1 KiB (8 rows x 128 B) per operand and K-tile;
+  // wave w issues pieces q = 4 i + w.  Lane l of a piece: row q*8 + (l >> 3),
+  // physical chunk l & 7 holding logical chunk (l & 7) ^ (l >> 3).
+  const __amdgpu_buffer_rsrc_t ra = op_rsrc(g.A + (size_t)bm * g.lda, (long)g.M - bm, g.lda);
+  const __amdgpu_buffer_rsrc_t rb = op_rsrc(g.B + (size_t)bn * g.ldb, (long)g.N - bn, g.ldb);
+  const int prow = wave * 8 + (lane >> 3);
+  const int pchunk = ((lane & 7) ^ ((lane >> 3) & 7)) << 4;
+  const int va = prow * g.lda * 2 + pchunk, vb = prow * g.ldb * 2 + pchunk;
+  const int sa = 32 * g.lda * 2, sb = 32 * g.ldb * 2;  // byte step between a wave's pieces
+  auto stage = [&](int buf, int kt) {
+    unsigned char* base = smem + buf * kStage4;
+    const int k0 = kt * WK * 2;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_vptr)(base + (i * 4 + wave) * 1024), 16, va,
+                                               k0 + i * sa, 0, 0);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_vptr)(base + kOpBytes + (i * 4 + wave) * 1024), 16, vb,
+                                               k0 + i * sb, 0, 0);
+  };
+
+  auto stage_piece = [&](int buf, int kt, int i) {
+    unsigned char* base = smem + buf * kStage4;
+    const int k0 = kt * WK * 2;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_vptr)(base + (i * 4 + wave) * 1024), 16, va, k0 + i * sa, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_vptr)(base + kOpBytes + (i * 4 + wave) * 1024), 16, vb,
+                                             k0 + i * sb, 0, 0);
+  };
+
+  // ---- fragments (v_mfma_f32_16x16x32_bf16): lane l holds row (l & 15) of a
+  // 16-row block, k = 8 (l >> 4) .. +7 of the 32-deep half `ks`
+  const int frow = lane & 15;
+  auto rd = [&](int buf, int ks, bf16x8 (&fa)[8], bf16x8 (&fb)[8]) {
+    const unsigned char* A = smem + buf * kStage4;
+    const unsigned char* B = A + kOpBytes;
+    const int chunk = ks * 4 + (lane >> 4);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int row = wr * 128 + i * 16 + frow;
+      fa[i] = *reinterpret_cast<const bf16x8*>(A + row * 128 + ((chunk ^ (row & 7)) << 4));
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int row = wc * 128 + j * 16 + frow;
+      fb[j] = *reinterpret_cast<const bf16x8*>(B + row * 128 + ((chunk ^ (row & 7)) << 4));
+    }
+  };
+
+  // group g of a phase reads two fragments of the next set: B blocks 2g, 2g+1 for
+  // g < 4, then A blocks 2(g-4), 2(g-4)+1, so the next phase's first MFMAs (A block
+  // 0 against every B block) find their operands landed
+  auto rd2 = [&](int buf, int ks, int grp, bf16x8 (&fa)[8], bf16x8 (&fb)[8]) {
+    const unsigned char* base = smem + buf * kStage4 + (grp < 4 ? kOpBytes : 0);
+    const int chunk = ks * 4 + (lane >> 4);
+    const int b0_ = (grp < 4 ? wc : wr) * 128 + (grp & 3) * 32 + frow;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int row = b0_ + u * 16;
+      const bf16x8 v = *reinterpret_cast<const bf16x8*>(base + row * 128 + ((chunk ^ (row & 7)) << 4));
+      if (grp < 4) fb[(grp & 3) * 2 + u] = v;
+      else fa[(grp & 3) * 2 + u] = v;
+    }
+  };
+
+  floatx4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+  auto mma = [&](const bf16x8 (&fa)[8], const bf16x8 (&fb)[8]) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+  };
+  // Phase schedules: one fragment read (and in X one DMA piece) per 3 MFMAs, the
+  // last 16 MFMAs bare, so the reads (and the DMA issue, ~60 cycles each) hide
+  // under matrix work and have landed before the phase's barrier / next use.
+  auto sched_x = [&]() {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);
+      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+    }
+    __builtin_amdgcn_sched_group_barrier(0x008, 16, 0);
+  };
+  auto sched_y = [&]() {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+    }
+    __builtin_amdgcn_sched_group_barrier(0x008, 16, 0);
+  };
+
+  const int nk = g.K / WK;
+  bf16x8 a0[8], b0[8], a1[8], b1[8];
+  stage(0, 0);
+  __syncthreads();  // vmcnt(0) + barrier: tile 0 landed
+  // t = 0
+  if (nk > 1) stage(1, 1);
+  rd(0, 0, a0, b0);
+  rd(0, 1, a1, b1);
+  mma(a0, b0);
+  sched_y();
+  __syncthreads();
+  for (int kt = 1; kt < nk; ++kt) {
+    const int buf = kt & 1;
+    const int skt = min(kt + 1, nk - 1);  // unconditional: one basic block (last: a harmless re-load)
+    if constexpr (SCHED == 0) {
+      stage(buf ^ 1, skt);
+      rd(buf, 0, a0, b0);
+      mma(a1, b1);
+      sched_x();
+      __builtin_amdgcn_sched_barrier(0);
+      rd(buf, 1, a1, b1);
+      mma(a0, b0);
+      sched_y();
+    } else {
+      // explicit groups: 8 MFMAs + 2 DMA pieces + 2 fragment reads, fenced
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[i], b1[j], acc[i][j], 0, 0, 0);
+        stage_piece(buf ^ 1, skt, i);
+        rd2(buf, 0, i, a0, b0);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[i], b0[j], acc[i][j], 0, 0, 0);
+        rd2(buf, 1, i, a1, b1);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    __syncthreads();
+  }
+  mma(a1, b1);
+
+  // ---- epilogue: per wave, two 64-row halves through its own LDS slab
+  float* tile = reinterpret_cast<float*>(smem + wave * kEpiWave);
+  const int es = g.out_bf16 ? 2 : 4;
+  const bool vec_ok = (((uint64_t)g.C | ((uint64_t)g.ldc * es)) % 16) == 0 && g.N % 8 == 0;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          tile[(i * 16 + (lane >> 4) * 4 + r) * kEpiTS + j * 16 + (lane & 15)] = acc[h * 4 + i][j][r];
+    // the slab is this wave's own and a wave's LDS accesses run in order: no barrier
+    __builtin_amdgcn_wave_barrier();
+    const int cl = (lane & 15) * 8;
+    const int col = bn + wc * 128 + cl;
+    float bias[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) bias[q] = load_bias(g, col + q, 0);
+#pragma unroll 4
+    for (int it = 0; it < 16; ++it) {
+      const int rl = it * 4 + (lane >> 4);
+      const int row = bm + wr * 128 + h * 64 + rl;
+      if (row >= g.M || col >= g.N) continue;
+      float v[8];
+      const float4 x0 = *reinterpret_cast<const float4*>(tile + rl * kEpiTS + cl);
+      const float4 x1 = *reinterpret_cast<const float4*>(tile + rl * kEpiTS + cl + 4);
+      v[0] = x0.x; v[1] = x0.y; v[2] = x0.z; v[3] = x0.w; v[4] = x1.x; v[5] = x1.y; v[6] = x1.z; v[7] = x1.w;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v[q] = epi(g, v[q], bias[q]);
+      if (vec_ok) {
+        if (g.out_bf16) {
+          uint16_t* C = reinterpret_cast<uint16_t*>(g.C) + (size_t)row * g.ldc + col;
+          if (g.accumulate) {
+            const uint4 o = *reinterpret_cast<const uint4*>(C);
+            const uint32_t ow[4] = {o.x, o.y, o.z, o.w};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) { v[2 * q] += bf16_lo(ow[q]); v[2 * q + 1] += bf16_hi(ow[q]); }
+          }
+          uint32_t w[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) w[q] = f32_to_bf16_bits(v[2 * q]) | (f32_to_bf16_bits(v[2 * q + 1]) << 16);
+          *reinterpret_cast<uint4*>(C) = uint4{w[0], w[1], w[2], w[3]};
+        } else {
+          float* C = reinterpret_cast<float*>(g.C) + (size_t)row * g.ldc + col;
+          float4 y0 = make_float4(v[0], v[1], v[2], v[3]), y1 = make_float4(v[4], v[5], v[6], v[7]);
+          if (g.accumulate) {
+            const float4 o0 = *reinterpret_cast<const float4*>(C), o1 = *reinterpret_cast<const float4*>(C + 4);
+            y0.x += o0.x; y0.y += o0.y; y0.z += o0.z; y0.w += o0.w;
+            y1.x += o1.x; y1.y += o1.y; y1.z += o1.z; y1.w += o1.w;
+          }
+          *reinterpret_cast<float4*>(C) = y0;
+          *reinterpret_cast<float4*>(C + 4) = y1;
+        }
+      } else {
+        for (int q = 0; q < 8 && col + q < g.N; ++q) {
+          const size_t o = (size_t)row * g.ldc + col + q;
+          if (g.out_bf16) {
+            uint16_t* C = reinterpret_cast<uint16_t*>(g.C);
+            C[o] = (uint16_t)f32_to_bf16_bits(v[q] + (g.accumulate ? bf2f(C[o]) : 0.f));
+          } else {
+            float* C = reinterpret_cast<float*>(g.C);
+            C[o] = v[q] + (g.accumulate ? C[o] : 0.f);
+          }
+        }
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+}  // namespace
+
+int g_w4_sched = 1;
+
+bool gemm_w4_ok(const GemmArgs& g) {
+  // one descriptor per operand tile: the bytes from a tile's first row must fit 2 GiB
+  return g.splitk == 1 && g.K % WK == 0 && g.K >= WK && g.lda % 8 == 0 && g.ldb % 8 == 0 &&
+         (long)g.M * g.lda * 2 < 0x7ffffff0l && (long)g.N * g.ldb * 2 < 0x7ffffff0l;
+}
+
+void launch_gemm_nt_w4(const GemmArgs& g, hipStream_t stream) {
+  static bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(k_gemm_w4<0>),
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, kLds4) == hipSuccess &&
+                     hipFuncSetAttribute(reinterpret_cast<const void*>(k_gemm_w4<1>),
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, kLds4) == hipSuccess;
+  (void)attr;
+  const int nwg = ((g.M + WM - 1) / WM) * ((g.N + WNB - 1) / WNB);
+  if (g_w4_sched == 1) hipLaunchKernelGGL((k_gemm_w4<1>), dim3(nwg), dim3(WNT), kLds4, stream, g);
+  else hipLaunchKernelGGL((k_gemm_w4<0>), dim3(nwg), dim3(WNT), kLds4, stream, g);
+}
+
+}  // namespace gemm
+}  // namespace dev
+}  // namespace ccmpi

@@ -25,8 +25,6 @@ Algorithms (``algo=``):
 ``ring``           hand-written pipelined ring RS+AG with peer writes on the flag
                    protocol; ``rings=k`` concurrent rings with coprime strides (k links)
 ``rhd``            hand-written recursive halving (RS) + doubling (AG), p = 2^k
-``ring_rccl``      ring schedule on RCCL send/recv + our reduction kernel
-``rhd_rccl``       recursive halving/doubling on RCCL send/recv
 ``rccl``           vendor RCCL collective (the "library" baseline)
 ``auto``           tuned choice (size thresholds; ``tune()`` measures them)
 =================  ============================================================
@@ -49,7 +47,7 @@ from .utils.trace import trace_call
 
 _OPS = {"SUM": 0, "PROD": 1, "MIN": 2, "MAX": 3}
 # all-reduce algorithms whose summation order is not rank order 0..p-1
-_UNORDERED = ("ring", "rhd", "rccl", "ring_rccl", "rhd_rccl")
+_UNORDERED = ("ring", "rhd", "rccl")
 # hand-written all-reduce algorithms -> native algorithm codes
 _HAND_ALGOS = {"oneshot": "ALGO_ONESHOT", "twoshot": "ALGO_TWOSHOT", "reduce_bcast": "ALGO_REDUCE_BCAST",
                "push": "ALGO_TWOSHOT_PUSH", "ring": "ALGO_RING", "rhd": "ALGO_RHD", "ll": "ALGO_LL",
@@ -195,6 +193,7 @@ class DeviceGroup:
         self.ranks_per_device = keys.count(key)
         self.shared_device = self.ranks_per_device > 1
         self._async_done = None  # (stream, event) of the last start()ed collective, until ordered
+        self._inflight: List = []  # (done event, tensors) of start()ed collectives not yet known complete
         default_blocks = max(1, 512 // self.ranks_per_device)
         self.max_blocks = _env_int("CCMPI_MAX_BLOCKS", default_blocks)
         # CTA budget of collectives that run NEXT TO compute (DP gradient buckets, TP
@@ -323,14 +322,22 @@ class DeviceGroup:
         need = max(nbytes, 1)
         idx = self.device.index or 0
         cap = self.heap.block(need, idx)
-        if cap is None:
-            self._grow_heap(need)
-            cap = self.heap.block(need, idx)
+        # Whether the heap grows is decided collectively: blocks return to the heap
+        # when their last view dies, which can happen at different times on different
+        # ranks (GC, autograd, unwaited work), so a local "no block" must not start
+        # the registration all-gather on one rank only.  Every rank grows when any
+        # rank needs to, by the largest request.
+        grow = self.host.allreduce(0 if cap is not None else need, op=_host_max())
+        if grow:
+            self._grow_heap(grow)
+            if cap is None:
+                cap = self.heap.block(need, idx)
         raw = torch.utils.dlpack.from_dlpack(cap)
         return raw[:nbytes].view(dtype).view(shape)
 
     def _grow_heap(self, need: int) -> None:
-        """Collective: register one more arena (every rank grows at the same call)."""
+        """Collective: register one more arena (every rank grows at the same call,
+        by the same ``need``)."""
         arena = max(self.arena_bytes, (need + (2 << 20) - 1) // (2 << 20) * (2 << 20) + 4096)
         raw = self.torch.empty(arena, dtype=self.torch.uint8, device=self.device)
         self._register(raw)
@@ -489,17 +496,6 @@ class DeviceGroup:
         elif algo == "rccl":
             self.ensure_rccl()
             self.dc.rccl_allreduce(src.data_ptr(), dst.data_ptr(), src.numel(), dt, opc, s)
-        elif algo in ("ring_rccl", "rhd_rccl"):
-            self.ensure_rccl()
-            if dst.data_ptr() != src.data_ptr():
-                dst.copy_(src)
-            need = (nbytes // max(1, self.size) + 4096) * 2
-            tmp = self.scratch if need <= self.scratch.numel() else self.torch.empty(need, dtype=self.torch.uint8, device=self.device)
-            if algo == "ring_rccl":
-                k = rings or _env_int("CCMPI_RINGS", 1)
-                self.dc.p2p_ring_allreduce(dst.data_ptr(), dst.numel(), dt, opc, s, k, tmp.data_ptr())
-            else:
-                self.dc.p2p_rhd_allreduce(dst.data_ptr(), dst.numel(), dt, opc, s, tmp.data_ptr())
         else:
             raise ValueError(f"unknown allreduce algorithm {algo!r}")
         return dst
@@ -552,7 +548,11 @@ class DeviceGroup:
         symmetric heap: zero staging; otherwise one pack pass); ``push``: every
         rank writes its segments straight into the peers' outputs (reference
         myAlltoall, comm.py:130-155; outputs from the symmetric heap on every
-        rank); ``pairwise``: RCCL send/recv rounds (myAlltoall2); ``rccl``."""
+        rank); ``pairwise``: the reference myAlltoall2 schedule (comm.py:162-199)
+        hand-written -- round k pushes the block for rank + k into its output and
+        waits for the block from rank - k, one peer in flight per round (outputs
+        from the symmetric heap: zero staging; otherwise through the scratch
+        segment); ``pairwise_rccl``: the same rounds as RCCL send/recv; ``rccl``."""
         self._check(src, "src")
         self._check(dst, "dst")
         if src.numel() != dst.numel() or src.numel() % self.size:
@@ -563,6 +563,10 @@ class DeviceGroup:
             self.ensure_rccl()
             self.dc.rccl_alltoall(src.data_ptr(), dst.data_ptr(), blk, 1, s)
         elif algo == "pairwise":
+            # hand-written pairwise rounds on the flag protocol (myAlltoall2's schedule)
+            self.dc.alltoall(src.data_ptr(), dst.data_ptr(), blk, s, self._budget(max_blocks),
+                             self._symm(dst) and src.data_ptr() % 16 == 0, self.D.A2A_PAIRWISE)
+        elif algo == "pairwise_rccl":
             self.ensure_rccl()
             self.dc.p2p_pairwise_alltoall(src.data_ptr(), dst.data_ptr(), blk, s)
         elif algo == "push":
@@ -606,15 +610,25 @@ class DeviceGroup:
         # allow the kernel path (16-B aligned input, output in the symmetric heap): a
         # local property every rank must agree on before choosing a path
         ok_local = src.data_ptr() % 16 == 0 and (dst.numel() == 0 or (dst.data_ptr() % 16 == 0 and self.is_symmetric(dst)))
-        mat = np.zeros((p, p + 1), np.int64)
-        self.host.Allgather(np.array(sc + [int(ok_local)], np.int64), mat)
+        # row: [send counts (p) | kernel path ok | expected recv counts (p, -1 = unchecked) | dst capacity].
+        # Every rank validates every rank's expectations against the gathered matrix, so a
+        # bad call raises on ALL ranks before any kernel is launched (no lone waiter).
+        given = [-1] * p if recv_counts is None else [int(c) for c in recv_counts]
+        if len(given) != p:
+            raise ValueError("alltoallv: need one recv count per rank")
+        mat = np.zeros((p, 2 * p + 2), np.int64)
+        self.host.Allgather(np.array(sc + [int(ok_local)] + given + [dst.numel()], np.int64), mat)
         counts = mat[:, :p]  # counts[i, j]: elements rank i sends to rank j
+        for i in range(p):
+            want_i = counts[:, i]
+            if mat[i, p + 1] >= 0 and not np.array_equal(mat[i, p + 1:2 * p + 1], want_i):
+                raise ValueError(f"alltoallv: rank {i} expects recv_counts {mat[i, p + 1:2 * p + 1].tolist()} "
+                                 f"but the peers send {want_i.tolist()}")
+            if int(want_i.sum()) > int(mat[i, 2 * p + 1]):
+                raise ValueError(f"alltoallv: rank {i}'s dst ({int(mat[i, 2 * p + 1])} elements) is too small for "
+                                 f"the {int(want_i.sum())} it receives")
         rc = counts[:, me].tolist()
-        if recv_counts is not None and [int(c) for c in recv_counts] != rc:
-            raise ValueError(f"alltoallv: recv_counts {list(recv_counts)} != what the peers send {rc}")
         rtot_local = sum(rc)
-        if rtot_local > dst.numel():
-            raise ValueError("alltoallv: dst too small for the received segments")
         fast = bool(mat[:, p].all()) and not np.any((counts * es) % 16)
         s = self._stream()
         if fast:
@@ -806,6 +820,11 @@ class DeviceGroup:
             done = torch.cuda.Event()
             done.record(stream)
         self._async_done = (stream.cuda_stream, done)
+        # keep the tensors (symmetric-heap blocks are not caching-allocator blocks, so
+        # record_stream does not protect them) until the collective has completed, even
+        # if the caller drops the Work unwaited -- the host plane does the same (Comm._nb)
+        self._inflight = [(e, k) for e, k in self._inflight if not e.query()]
+        self._inflight.append((done, args))
         return Work(self, done, out, args)
 
     # ------------------------------------------------------------------ health

@@ -149,7 +149,7 @@ def stress(iters):
             continue
         if kind < 0.3:  # all-to-all of n // p elements per peer block, push or pull
             m = max(1, n // p)
-            aa = shared.choice(["direct", "push"])
+            aa = shared.choice(["direct", "push", "pairwise"])
             x = gen(rank, m * p, torch.float32, 50000 + i)
             if sym:
                 sym_x[:m * p].copy_(x)
@@ -651,6 +651,18 @@ for sym in (False, True):
             y2 = dev.empty(p * n, dt) if sym else torch.empty(p * n, dtype=dt, device=D)
             dev.alltoall(gen(rank, p * n, dt, salt), y2, "push")
             check(f"alltoall[push,{dt},n={n},sym_out={sym}]", y2, want, dt)
+            # pairwise rounds (myAlltoall2): symmetric output (direct pushes) or staged
+            y4 = dev.empty(p * n, dt) if sym else torch.empty(p * n, dtype=dt, device=D)
+            dev.alltoall(gen(rank, p * n, dt, salt), y4, "pairwise")
+            check(f"alltoall[pairwise,{dt},n={n},sym_out={sym}]", y4, want, dt)
+            y5 = torch.empty(p * n, dtype=dt, device=D)
+            comm.myAlltoall2(gen(rank, p * n, dt, salt), y5)
+            check(f"myAlltoall2(device)[{dt},n={n}]", y5, want, dt)
+            z2 = gen(rank, p * n, dt, salt)
+            if sym:
+                z2 = sym_copy(z2)
+            dev.alltoall(z2, z2, "pairwise")
+            check(f"alltoall_inplace[pairwise,{dt},n={n},sym={sym}]", z2, want, dt)
             z = gen(rank, p * n, dt, salt)
             if sym:
                 z = sym_copy(z)
@@ -705,6 +717,10 @@ if args.big:
     dev.alltoall(x, y)
     want = torch.cat([gen(r, p * nb, torch.float32, salt)[rank * nb:(rank + 1) * nb] for r in range(p)]).double()
     check("big_alltoall[staged]", y, want, torch.float32)
+    y2 = torch.empty_like(x)
+    dev.alltoall(x, y2, "pairwise")
+    check("big_alltoall[pairwise,staged]", y2, want, torch.float32)
+    del y2
     dev.alltoall(x, x)
     check("big_alltoall[inplace]", x, want, torch.float32)
     salt += 1
@@ -730,13 +746,9 @@ if args.rccl:
     y = torch.empty_like(x)
     dev.allreduce(x, y, "SUM", "rccl")
     check("rccl_allreduce", y, oracle(4096, torch.float32, "SUM", 7), torch.float32, p)
-    for algo in ("ring_rccl",) + (("rhd_rccl",) if POW2 else ()):
-        x = gen(rank, 10001, torch.float32, 9)
-        dev.allreduce(x, x, "SUM", algo)
-        check(f"p2p_{algo}", x, oracle(10001, torch.float32, "SUM", 9), torch.float32, p)
     x = gen(rank, p * 999, torch.float32, 13)
     y = torch.empty_like(x)
-    dev.alltoall(x, y, "pairwise")
+    dev.alltoall(x, y, "pairwise_rccl")
     check("p2p_pairwise_alltoall", y,
           torch.cat([gen(r, p * 999, torch.float32, 13)[rank * 999:(rank + 1) * 999] for r in range(p)]).double(),
           torch.float32)
