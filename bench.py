@@ -239,8 +239,12 @@ def rccl_phase(args) -> dict:
     _, _, local = _env_rank()
     torch.cuda.set_device(local % torch.cuda.device_count())
     dev, hc = comm.dev, comm.comm
-    if dev.shared_device and os.environ.get("CCMPI_BENCH_RCCL") != "force":
+    mode = os.environ.get("CCMPI_BENCH_RCCL", "")  # tests: "force" RCCL on shared GPUs, simulate a "hang"
+    if dev.shared_device and mode not in ("force", "hang"):
         return {"skipped": f"{dev.ranks_per_device} ranks share one GPU (RCCL refuses duplicate devices)"}
+    if mode == "hang":
+        while True:  # the supervisor's --rccl-timeout must end this phase
+            time.sleep(1)
 
     def sync_barrier():
         torch.cuda.synchronize()

@@ -38,6 +38,8 @@ def main():
     ap.add_argument("--shapes", default=",".join(DEFAULT))
     ap.add_argument("--json", default="")
     ap.add_argument("--all", action="store_true", help="also the 128x128 and 256x192 kernels")
+    ap.add_argument("--w4", default="0:8,1:8,3:8",
+                    help="four-wave kernel variants sched:group_m (sched bit 0 persistent, bit 1 MFMA-first)")
     args = ap.parse_args()
     D = _native.device()
     out = []
@@ -55,15 +57,20 @@ def main():
                 gemm_nt(a, b, out=c)
             return f
 
-        def w4(sched):
+        def w4(sched, gm):
             def f():
                 D.gemm_set_kernel(5)
                 D.gemm_set_w4_sched(sched)
+                D.gemm_set_w4_group_m(gm)
                 gemm_nt(a, b, out=c)
             return f
 
-        variants = {"k256": ours(2), "w4s0": w4(0), "w4s1": w4(1), "auto": ours(0),
-                    "hipblaslt": lambda: torch.matmul(a, b.T, out=c)}
+        variants = {"k256": ours(2)}
+        for v in args.w4.split(","):
+            if v:
+                sc, gm = (int(x) for x in v.split(":"))
+                variants[f"w4s{sc}g{gm}"] = w4(sc, gm)
+        variants.update({"auto": ours(0), "hipblaslt": lambda: torch.matmul(a, b.T, out=c)})
         if args.all:
             variants.update({"k128": ours(1), "k256x192": ours(4)})
         # correctness of both kernels on this shape against hipBLASLt

@@ -151,8 +151,20 @@ def build_device(force: bool = False, verbose: bool = False) -> Path:
             cmd = [hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", *map(str, objs), "-o", str(tmp),
                    f"-L{ROCM / 'lib'}", "-lamdhip64", "-lrccl", f"-Wl,-rpath,{ROCM / 'lib'}"]
             _run(cmd, verbose)
+            _check_own_symbols(tmp)
             shutil.move(str(tmp), str(target))
     return target
+
+
+def _check_own_symbols(so: Path) -> None:
+    """Fail the build when the library references a symbol of our own namespace that
+    no object defines (e.g. a kernel template whose host stub hipcc did not emit):
+    such a library links, then fails only when it is imported on the GPU box."""
+    nm = shutil.which("nm") or "/opt/rocm/lib/llvm/bin/llvm-nm"
+    r = subprocess.run([nm, "-D", "--undefined-only", str(so)], capture_output=True, text=True)
+    missing = [ln.split()[-1] for ln in r.stdout.splitlines() if "_ZN5ccmpi" in ln]
+    if missing:
+        raise RuntimeError("ccmpi device build: undefined own symbols: " + ", ".join(missing[:8]))
 
 
 def _local_includes(src: Path) -> list[Path]:

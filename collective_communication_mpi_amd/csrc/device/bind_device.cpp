@@ -109,6 +109,21 @@ PYBIND11_MODULE(_device, m) {
         return py::make_tuple(py::bytes(r.first), r.second);
       })
       .def("add_segment", &DeviceComm::add_segment)
+      .def("export_alloc", [](const DeviceComm& d, uint64_t ptr) {
+        // (IPC handle bytes, allocation base, allocation bytes) of the allocation holding ptr
+        hipDeviceptr_t base = nullptr;
+        size_t sz = 0;
+        CCMPI_HIP_CHECK(hipMemGetAddressRange(&base, &sz, reinterpret_cast<hipDeviceptr_t>(ptr)));
+        auto r = d.export_range((uint64_t)base);
+        return py::make_tuple(py::bytes(r.first), (uint64_t)base, (uint64_t)sz);
+      })
+      .def("set_segment", [](DeviceComm& d, int s, uint64_t ptr, uint64_t bytes, const std::vector<py::bytes>& hs,
+                             const std::vector<uint64_t>& offs, const std::vector<py::bytes>& ks) {
+        std::vector<std::string> h(hs.begin(), hs.end()), k(ks.begin(), ks.end());
+        return d.set_segment(s, ptr, bytes, h, offs, k);
+      })
+      .def("clear_segment", &DeviceComm::clear_segment)
+      .def_property_readonly("num_segments", &DeviceComm::num_segments)
       .def("find", [](const DeviceComm& d, uint64_t ptr, uint64_t n) {
         uint64_t off = 0;
         int s = d.find(ptr, n, &off);

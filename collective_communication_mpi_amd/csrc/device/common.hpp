@@ -41,7 +41,7 @@ enum DType : int {
 enum ROp : int { OP_SUM = 0, OP_PROD, OP_MIN, OP_MAX };
 
 constexpr int kMaxRanks = 16;     // ranks per device communicator
-constexpr int kMaxSegs = 64;      // registered symmetric segments (heap arenas) per rank
+constexpr int kMaxSegs = 128;     // registered segments per rank: heap arenas + on-demand registrations (< 255)
 constexpr int kMaxBlocks = 1024;  // max CTAs of one collective launch
 constexpr int kCachePolicySys = 17;  // aux bits: sc0 | sc1 (system coherent)
 // Stores of the collectives: sc0|sc1 write-through (aux 17), so bytes handed to a

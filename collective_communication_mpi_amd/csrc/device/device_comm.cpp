@@ -51,9 +51,10 @@ inline hipStream_t S(uint64_t s) { return reinterpret_cast<hipStream_t>(s); }
 
 }  // namespace
 
-void* ipc_open(const std::string& handle) {
+void* ipc_open(const std::string& handle, const std::string& key_in) {
+  const std::string& key = key_in.empty() ? handle : key_in;
   std::lock_guard<std::mutex> g(g_ipc_mu);
-  auto it = g_ipc.find(handle);
+  auto it = g_ipc.find(key);
   if (it != g_ipc.end()) {
     it->second.second++;
     return it->second.first;
@@ -63,7 +64,7 @@ void* ipc_open(const std::string& handle) {
   std::memcpy(&h, handle.data(), sizeof(h));
   void* p = nullptr;
   CCMPI_HIP_CHECK(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess));
-  g_ipc[handle] = {p, 1};
+  g_ipc[key] = {p, 1};
   return p;
 }
 
@@ -112,6 +113,8 @@ DeviceComm::~DeviceComm() {
     if (nccl_ && h) ncclCommDeregister(nccl_, h);
   if (nccl_) ncclCommDestroy(nccl_);
   for (auto& h : opened_) ipc_close(h);
+  for (auto& ks : seg_keys_)
+    for (auto& k : ks) ipc_close(k);
   if (sig_) (void)hipFree(sig_);
   if (epochs_) (void)hipFree(epochs_);
   if (dev_pt_) (void)hipFree(dev_pt_);
@@ -178,8 +181,64 @@ int DeviceComm::add_segment(uint64_t local_ptr, uint64_t bytes, const std::vecto
   return s;
 }
 
-int DeviceComm::find(uint64_t ptr, uint64_t nbytes, uint64_t* off) const {
+// On-demand registration of an ordinary allocation (torch caching-allocator segment):
+// slot `s` (-1 = a new slot) maps every rank's allocation; `keys[j]` identifies rank j's
+// allocation generation (the IPC handle bytes plus the owner's allocator generation),
+// so a freed-and-reallocated segment at the same address is opened afresh.  The
+// previous occupant's peer mappings are released (the caller has synchronised the
+// device: no kernel of this rank still resolves through the slot).
+int DeviceComm::set_segment(int s, uint64_t local_ptr, uint64_t bytes, const std::vector<std::string>& handles,
+                            const std::vector<uint64_t>& offsets, const std::vector<std::string>& keys) {
+  if ((int)handles.size() != size_ || (int)offsets.size() != size_ || (int)keys.size() != size_)
+    throw std::invalid_argument("ccmpi: set_segment needs one handle/offset/key per rank");
+  CCMPI_HIP_CHECK(hipSetDevice(device_));
+  if (s < 0) {
+    if ((int)segs_.size() >= kMaxSegs) throw std::runtime_error("ccmpi: too many registered segments");
+    s = (int)segs_.size();
+    segs_.push_back(SegInfo{});
+    peer_seg_.emplace_back(size_, nullptr);
+    seg_keys_.resize(segs_.size());
+  } else if (s == 0 || s >= (int)segs_.size()) {
+    throw std::invalid_argument("ccmpi: set_segment: bad slot");
+  }
+  seg_keys_.resize(segs_.size());
+  for (auto& k : seg_keys_[s]) ipc_close(k);
+  seg_keys_[s].clear();
+  segs_[s] = SegInfo{reinterpret_cast<char*>(local_ptr), bytes, false, true};
+  for (int j = 0; j < size_; ++j) {
+    char* p;
+    if (j == rank_) {
+      p = reinterpret_cast<char*>(local_ptr);
+    } else {
+      p = static_cast<char*>(ipc_open(handles[j], keys[j])) + offsets[j];
+      seg_keys_[s].push_back(keys[j]);
+    }
+    peer_seg_[s][j] = p;
+    host_pt_.seg[j][s] = p;
+  }
+  host_pt_.seg_bytes[s] = bytes;
+  host_pt_.nsegs = (int)segs_.size();
+  sync_table_();
+  return s;
+}
+
+void DeviceComm::clear_segment(int s) {
+  if (s <= 0 || s >= (int)segs_.size()) throw std::invalid_argument("ccmpi: clear_segment: bad slot");
+  seg_keys_.resize(segs_.size());
+  for (auto& k : seg_keys_[s]) ipc_close(k);
+  seg_keys_[s].clear();
+  segs_[s] = SegInfo{nullptr, 0, false, true};  // local range empty: find() never matches it
+  for (int j = 0; j < size_; ++j) {
+    peer_seg_[s][j] = nullptr;
+    host_pt_.seg[j][s] = nullptr;
+  }
+  host_pt_.seg_bytes[s] = 0;
+  sync_table_();
+}
+
+int DeviceComm::find(uint64_t ptr, uint64_t nbytes, uint64_t* off, bool dynamic) const {
   for (size_t s = 0; s < segs_.size(); ++s) {
+    if (segs_[s].dynamic && !dynamic) continue;
     uint64_t b = (uint64_t)segs_[s].local;
     if (ptr >= b && ptr + nbytes <= b + segs_[s].bytes) {
       if (off) *off = ptr - b;
@@ -192,7 +251,7 @@ int DeviceComm::find(uint64_t ptr, uint64_t nbytes, uint64_t* off) const {
 uint64_t DeviceComm::code_of_(uint64_t ptr, uint64_t nbytes) const {
   if (ptr % 16) return 0;
   uint64_t off = 0;
-  int s = find(ptr, nbytes, &off);
+  int s = find(ptr, nbytes, &off, search_dynamic_);
   if (s < 0) return 0;
   return addr_code(s, off);
 }
@@ -217,6 +276,7 @@ int DeviceComm::grid_(uint64_t work_bytes, int max_blocks) const {
 
 void DeviceComm::allreduce(uint64_t in, uint64_t out, uint64_t count, int dtype, int op, int algo,
                            uint64_t stream, int max_blocks, bool symmetric) {
+  DynScope dyn_scope(this, symmetric);
   const uint64_t es = dtype_bytes(dtype), nbytes = count * es;
   if (!device_reduce_supported(dtype, op)) throw std::invalid_argument("ccmpi: unsupported device reduction");
   if (nbytes == 0) return;
@@ -428,6 +488,7 @@ void DeviceComm::allreduce_pipelined_(int algo, uint64_t in, uint64_t out, uint6
 
 void DeviceComm::reduce_scatter(uint64_t in, uint64_t out, uint64_t count_per_rank, int dtype, int op,
                                 uint64_t stream, int max_blocks, bool symmetric) {
+  DynScope dyn_scope(this, symmetric);
   const uint64_t es = dtype_bytes(dtype), blk = count_per_rank * es;
   if (!device_reduce_supported(dtype, op)) throw std::invalid_argument("ccmpi: unsupported device reduction");
   if (blk == 0) return;
@@ -479,6 +540,7 @@ static void launch_move_m(int mode, CollArgs a, int p, int grid, hipStream_t st)
 
 void DeviceComm::allgather(uint64_t in, uint64_t out, uint64_t bytes_per_rank, uint64_t stream, int max_blocks,
                            bool symmetric, int mode) {
+  DynScope dyn_scope(this, symmetric);
   if (bytes_per_rank == 0) return;
   CCMPI_HIP_CHECK(hipSetDevice(device_));
   hipStream_t st = S(stream);
@@ -534,6 +596,7 @@ void DeviceComm::allgather(uint64_t in, uint64_t out, uint64_t bytes_per_rank, u
 
 void DeviceComm::alltoall(uint64_t in, uint64_t out, uint64_t bytes_per_peer, uint64_t stream, int max_blocks,
                           bool symmetric, int mode) {
+  DynScope dyn_scope(this, symmetric);
   if (bytes_per_peer == 0) return;
   CCMPI_HIP_CHECK(hipSetDevice(device_));
   hipStream_t st = S(stream);
@@ -677,6 +740,7 @@ void DeviceComm::alltoallv_dev(uint64_t in, uint64_t counts, uint64_t out, uint6
 
 void DeviceComm::bcast(uint64_t buf, uint64_t nbytes, int root, uint64_t stream, int max_blocks, bool symmetric,
                        int mode) {
+  DynScope dyn_scope(this, symmetric);
   if (nbytes == 0 || size_ == 1) return;
   CCMPI_HIP_CHECK(hipSetDevice(device_));
   hipStream_t st = S(stream);
@@ -711,6 +775,7 @@ void DeviceComm::bcast(uint64_t buf, uint64_t nbytes, int root, uint64_t stream,
 
 void DeviceComm::allgather_lastaxis(uint64_t in, uint64_t out, uint64_t rows, uint64_t row_bytes, uint64_t stream,
                                     int max_blocks, bool symmetric) {
+  DynScope dyn_scope(this, symmetric);
   if (rows == 0 || row_bytes == 0) return;
   if (row_bytes % 16 || out % 16) throw std::invalid_argument("ccmpi: last-axis all-gather needs 16-B rows/output");
   const uint64_t nbytes = rows * row_bytes;
@@ -730,6 +795,7 @@ void DeviceComm::allgather_lastaxis(uint64_t in, uint64_t out, uint64_t rows, ui
 
 void DeviceComm::reduce_scatter_lastaxis(uint64_t in, uint64_t out, uint64_t rows, uint64_t k, int dtype, int op,
                                          uint64_t stream, int max_blocks, bool symmetric) {
+  DynScope dyn_scope(this, symmetric);
   const uint64_t es = dtype_bytes(dtype), row_bytes = k * es;
   if (rows == 0 || k == 0) return;
   if (!device_reduce_supported(dtype, op)) throw std::invalid_argument("ccmpi: unsupported device reduction");

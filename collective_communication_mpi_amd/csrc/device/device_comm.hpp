@@ -27,6 +27,7 @@ struct SegInfo {
   char* local = nullptr;   // this rank's base
   uint64_t bytes = 0;
   bool owned = false;      // allocated by us (freed in dtor)
+  bool dynamic = false;    // on-demand registration slot (searched only by calls that registered)
 };
 
 class DeviceComm {
@@ -46,11 +47,17 @@ class DeviceComm {
   std::pair<std::string, uint64_t> export_range(uint64_t ptr) const;
   int add_segment(uint64_t local_ptr, uint64_t bytes,
                   const std::vector<std::string>& handles, const std::vector<uint64_t>& offsets);
+  // on-demand registration slot (see device_comm.cpp); returns the slot index
+  int set_segment(int s, uint64_t local_ptr, uint64_t bytes, const std::vector<std::string>& handles,
+                  const std::vector<uint64_t>& offsets, const std::vector<std::string>& keys);
+  void clear_segment(int s);
+  int num_segments() const { return (int)segs_.size(); }
   int scratch_segment() const { return 0; }
   uint64_t scratch_bytes() const { return segs_.empty() ? 0 : segs_[0].bytes; }
   uint64_t scratch_ptr() const { return segs_.empty() ? 0 : (uint64_t)segs_[0].local; }
-  // (segment, offset) of a local pointer, or -1 if not inside a segment
-  int find(uint64_t ptr, uint64_t nbytes, uint64_t* off) const;
+  // (segment, offset) of a local pointer, or -1 if not inside a segment; on-demand
+  // slots count only with `dynamic` (a call whose tensors were registered for it)
+  int find(uint64_t ptr, uint64_t nbytes, uint64_t* off, bool dynamic = false) const;
 
   // ---- hand-written collectives (stream-ordered, graph-capturable) ----------
   // `symmetric`: caller guarantees every rank passes registered buffers, so
@@ -142,6 +149,15 @@ class DeviceComm {
   CollArgs args_(uint64_t src_code, uint64_t res_code, char* out, uint64_t nbytes, int root) const;
   int grid_(uint64_t work_bytes, int max_blocks) const;
   uint64_t code_of_(uint64_t ptr, uint64_t nbytes) const;  // 0 if not registered / misaligned
+  // true while a collective whose caller passed symmetric=true runs: its tensors are
+  // heap blocks or were registered on demand for this call, so on-demand slots may
+  // resolve them; any other call (staging paths included) sees heap segments only
+  bool search_dynamic_ = false;
+  struct DynScope {
+    DeviceComm* d;
+    DynScope(DeviceComm* c, bool on) : d(c) { d->search_dynamic_ = on; }
+    ~DynScope() { d->search_dynamic_ = false; }
+  };
 
   int rank_, size_, device_;
   Signals* sig_ = nullptr;               // mine (uncached)
@@ -166,10 +182,11 @@ class DeviceComm {
   uint64_t* dbg_ = nullptr;
   bool copy_engine_ = false;              // single-rank copies: contiguous-slice kernel (3.2 vs 2.6 TB/s for the runtime blit)
   std::vector<std::string> opened_;      // handles we opened (for release)
+  std::vector<std::vector<std::string>> seg_keys_;  // per slot: IPC keys opened for on-demand segments
 };
 
 // Process-wide registry so a handle opened by two communicators maps once.
-void* ipc_open(const std::string& handle);
+void* ipc_open(const std::string& handle, const std::string& key = std::string());
 void ipc_close(const std::string& handle);
 
 }  // namespace dev

@@ -32,14 +32,22 @@ namespace dev {
 namespace gemm {
 namespace {
 
-constexpr int WM = 256, WNB = 256, WK = 64, WNT = 256, kGroupM4 = 8;
+constexpr int WM = 256, WNB = 256, WK = 64, WNT = 256;
 constexpr int kOpBytes = 256 * 128;           // one operand's K-tile (256 rows x 64 bf16)
 constexpr int kStage4 = 2 * kOpBytes;         // A + B
+constexpr int kEpiRows = 32;                  // epilogue pass: 32 rows x 128 columns per wave
 constexpr int kEpiTS = 132;                   // epilogue fp32 row stride (128 + 4 pad)
-constexpr int kEpiWave = 64 * kEpiTS * 4;     // one wave's 64-row half
-constexpr int kLds4 = (2 * kStage4 > 4 * kEpiWave) ? 2 * kStage4 : 4 * kEpiWave;
+constexpr int kEpiWave = kEpiRows * kEpiTS * 4;
+// stage 0 | stage 1, the epilogue slabs overlay stage 1 (and a little beyond) so
+// a persistent workgroup can prefetch its next tile into stage 0 meanwhile
+constexpr int kLds4 = kStage4 + ((kStage4 > 4 * kEpiWave) ? kStage4 : 4 * kEpiWave);
 
 typedef __attribute__((address_space(3))) void* lds_vptr;
+
+struct W4Args {
+  GemmArgs g;
+  int group_m;  // tile rows per group of the group-M order
+};
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t op_rsrc(const uint16_t* base, long rows, int ld) {
   // rows <= 0: an empty descriptor (every load reads 0)
@@ -48,53 +56,57 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t op_rsrc(const uint16_t* base, 
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(base), 0, (int)bytes, 0x00020000);
 }
 
-template <int SCHED>
-__global__ void __launch_bounds__(WNT, 1) k_gemm_w4(GemmArgs g) {
+// logical tile -> (tile row, tile column) in group-M order
+__device__ __forceinline__ void tile_coords(int wg, int tiles_m, int tiles_n, int group_m, int& tm, int& tn) {
+  const int per_group = group_m * tiles_n;
+  const int first_m = (wg / per_group) * group_m;
+  const int gm = min(tiles_m - first_m, group_m);
+  tm = first_m + (wg % per_group) % gm;
+  tn = (wg % per_group) / gm;
+}
+
+// PERSIST: grid = min(tiles, CUs); workgroup b runs logical tiles s, s + G, s + 2G, ...
+// (s = XCD-aware remap of b) and prefetches the next tile's first K-tile during the
+// epilogue.  ORDER: MFMA-first issue order inside each fenced group.
+template <int PERSIST, int ORDER>
+__global__ void __launch_bounds__(WNT, 1) k_gemm_w4(W4Args wa) {
+  const GemmArgs& g = wa.g;
   extern __shared__ __attribute__((aligned(1024))) unsigned char smem[];
   const int tiles_n = (g.N + WNB - 1) / WNB, tiles_m = (g.M + WM - 1) / WM;
-  const int nwg = tiles_n * tiles_m;
-  int wg = xcd_remap(blockIdx.x, nwg);
-  int tm, tn;
-  {  // group-M order: the 32 tiles an XCD runs at once form an 8 x 4 block
-    const int per_group = kGroupM4 * tiles_n;
-    const int first_m = (wg / per_group) * kGroupM4;
-    const int gm = min(tiles_m - first_m, kGroupM4);
-    tm = first_m + (wg % per_group) % gm;
-    tn = (wg % per_group) / gm;
-  }
-  const int bm = tm * WM, bn = tn * WNB;
+  const int ntiles = tiles_n * tiles_m;
+  const int slot = xcd_remap(blockIdx.x, gridDim.x);
   const int t = threadIdx.x, lane = t & 63;
   const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
   const int wr = wave >> 1, wc = wave & 1;
+  const int nk = g.K / WK;
 
   // ---- staging: 32 pieces of 1 KiB (8 rows x 128 B) per operand and K-tile;
   // wave w issues pieces q = 4 i + w.  Lane l of a piece: row q*8 + (l >> 3),
   // physical chunk l & 7 holding logical chunk (l & 7) ^ (l >> 3).
-  const __amdgpu_buffer_rsrc_t ra = op_rsrc(g.A + (size_t)bm * g.lda, (long)g.M - bm, g.lda);
-  const __amdgpu_buffer_rsrc_t rb = op_rsrc(g.B + (size_t)bn * g.ldb, (long)g.N - bn, g.ldb);
   const int prow = wave * 8 + (lane >> 3);
   const int pchunk = ((lane & 7) ^ ((lane >> 3) & 7)) << 4;
   const int va = prow * g.lda * 2 + pchunk, vb = prow * g.ldb * 2 + pchunk;
   const int sa = 32 * g.lda * 2, sb = 32 * g.ldb * 2;  // byte step between a wave's pieces
-  auto stage = [&](int buf, int kt) {
-    unsigned char* base = smem + buf * kStage4;
-    const int k0 = kt * WK * 2;
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_vptr)(base + (i * 4 + wave) * 1024), 16, va,
-                                               k0 + i * sa, 0, 0);
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_vptr)(base + kOpBytes + (i * 4 + wave) * 1024), 16, vb,
-                                               k0 + i * sb, 0, 0);
+  __amdgpu_buffer_rsrc_t ra, rb;  // the current tile's operand descriptors
+  auto ops_for = [&](int tm, int tn) {
+    ra = op_rsrc(g.A + (size_t)tm * WM * g.lda, (long)g.M - tm * WM, g.lda);
+    rb = op_rsrc(g.B + (size_t)tn * WNB * g.ldb, (long)g.N - tn * WNB, g.ldb);
   };
-
   auto stage_piece = [&](int buf, int kt, int i) {
     unsigned char* base = smem + buf * kStage4;
+    // the piece offsets are recomputed per use (a few SALU ops) instead of 16
+    // loop-invariant SGPRs, which pushed the kernel past the SGPR budget (spills)
+    int sa_ = sa, sb_ = sb;
+    asm volatile("" : "+s"(sa_), "+s"(sb_));
     const int k0 = kt * WK * 2;
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_vptr)(base + (i * 4 + wave) * 1024), 16, va, k0 + i * sa, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_vptr)(base + (i * 4 + wave) * 1024), 16, va, k0 + i * sa_, 0,
+                                             0);
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_vptr)(base + kOpBytes + (i * 4 + wave) * 1024), 16, vb,
-                                             k0 + i * sb, 0, 0);
+                                             k0 + i * sb_, 0, 0);
+  };
+  auto stage = [&](int buf, int kt) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) stage_piece(buf, kt, i);
   };
 
   // ---- fragments (v_mfma_f32_16x16x32_bf16): lane l holds row (l & 15) of a
@@ -115,7 +127,6 @@ __global__ void __launch_bounds__(WNT, 1) k_gemm_w4(GemmArgs g) {
       fb[j] = *reinterpret_cast<const bf16x8*>(B + row * 128 + ((chunk ^ (row & 7)) << 4));
     }
   };
-
   // group g of a phase reads two fragments of the next set: B blocks 2g, 2g+1 for
   // g < 4, then A blocks 2(g-4), 2(g-4)+1, so the next phase's first MFMAs (A block
   // 0 against every B block) find their operands landed
@@ -133,27 +144,11 @@ __global__ void __launch_bounds__(WNT, 1) k_gemm_w4(GemmArgs g) {
   };
 
   floatx4 acc[8][8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
   auto mma = [&](const bf16x8 (&fa)[8], const bf16x8 (&fb)[8]) {
 #pragma unroll
     for (int i = 0; i < 8; ++i)
 #pragma unroll
       for (int j = 0; j < 8; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
-  };
-  // Phase schedules: one fragment read (and in X one DMA piece) per 3 MFMAs, the
-  // last 16 MFMAs bare, so the reads (and the DMA issue, ~60 cycles each) hide
-  // under matrix work and have landed before the phase's barrier / next use.
-  auto sched_x = [&]() {
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);
-      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-    }
-    __builtin_amdgcn_sched_group_barrier(0x008, 16, 0);
   };
   auto sched_y = [&]() {
 #pragma unroll
@@ -163,31 +158,56 @@ __global__ void __launch_bounds__(WNT, 1) k_gemm_w4(GemmArgs g) {
     }
     __builtin_amdgcn_sched_group_barrier(0x008, 16, 0);
   };
+  // inside one fenced group: MFMAs first, each load behind two of them
+  auto order_x = [&]() {
+    if constexpr (ORDER) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+    }
+  };
+  auto order_y = [&]() {
+    if constexpr (ORDER) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+    }
+  };
 
-  const int nk = g.K / WK;
-  bf16x8 a0[8], b0[8], a1[8], b1[8];
+  const int es = g.out_bf16 ? 2 : 4;
+  const bool vec_ok = (((uint64_t)g.C | ((uint64_t)g.ldc * es)) % 16) == 0 && g.N % 8 == 0;
+  const int step = PERSIST ? (int)gridDim.x : ntiles;
+  int lt = PERSIST ? slot : slot;  // logical tile
+  if (lt >= ntiles) return;
+  int tm, tn;
+  tile_coords(lt, tiles_m, tiles_n, wa.group_m, tm, tn);
+  ops_for(tm, tn);
   stage(0, 0);
-  __syncthreads();  // vmcnt(0) + barrier: tile 0 landed
-  // t = 0
-  if (nk > 1) stage(1, 1);
-  rd(0, 0, a0, b0);
-  rd(0, 1, a1, b1);
-  mma(a0, b0);
-  sched_y();
-  __syncthreads();
-  for (int kt = 1; kt < nk; ++kt) {
-    const int buf = kt & 1;
-    const int skt = min(kt + 1, nk - 1);  // unconditional: one basic block (last: a harmless re-load)
-    if constexpr (SCHED == 0) {
-      stage(buf ^ 1, skt);
-      rd(buf, 0, a0, b0);
-      mma(a1, b1);
-      sched_x();
-      __builtin_amdgcn_sched_barrier(0);
-      rd(buf, 1, a1, b1);
-      mma(a0, b0);
-      sched_y();
-    } else {
+  for (;;) {
+    const int bm = tm * WM, bn = tn * WNB;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+    bf16x8 a0[8], b0[8], a1[8], b1[8];
+    __syncthreads();  // vmcnt(0) + barrier: K-tile 0 landed; the previous epilogue's slab reads are done
+    // K-tile 0
+    stage(1, min(1, nk - 1));
+    rd(0, 0, a0, b0);
+    rd(0, 1, a1, b1);
+    mma(a0, b0);
+    sched_y();
+    __syncthreads();
+    for (int kt = 1; kt < nk; ++kt) {
+      const int buf = kt & 1;
+      const int skt = min(kt + 1, nk - 1);  // unconditional: one basic block (last: a harmless re-load)
       // explicit groups: 8 MFMAs + 2 DMA pieces + 2 fragment reads, fenced
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
@@ -195,6 +215,7 @@ __global__ void __launch_bounds__(WNT, 1) k_gemm_w4(GemmArgs g) {
         for (int j = 0; j < 8; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[i], b1[j], acc[i][j], 0, 0, 0);
         stage_piece(buf ^ 1, skt, i);
         rd2(buf, 0, i, a0, b0);
+        order_x();
         __builtin_amdgcn_sched_barrier(0);
       }
 #pragma unroll
@@ -202,88 +223,102 @@ __global__ void __launch_bounds__(WNT, 1) k_gemm_w4(GemmArgs g) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[i], b0[j], acc[i][j], 0, 0, 0);
         rd2(buf, 1, i, a1, b1);
+        order_y();
         __builtin_amdgcn_sched_barrier(0);
       }
+      __syncthreads();
     }
-    __syncthreads();
-  }
-  mma(a1, b1);
+    // every wave is past its last read of both stages: prefetch the next tile's
+    // K-tile 0 into stage 0 while the last MFMAs and the epilogue run
+    const int next = lt + step;
+    int ntm = 0, ntn = 0;
+    if (PERSIST && next < ntiles) {
+      tile_coords(next, tiles_m, tiles_n, wa.group_m, ntm, ntn);
+      ops_for(ntm, ntn);
+      stage(0, 0);
+    }
+    mma(a1, b1);
 
-  // ---- epilogue: per wave, two 64-row halves through its own LDS slab
-  float* tile = reinterpret_cast<float*>(smem + wave * kEpiWave);
-  const int es = g.out_bf16 ? 2 : 4;
-  const bool vec_ok = (((uint64_t)g.C | ((uint64_t)g.ldc * es)) % 16) == 0 && g.N % 8 == 0;
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          tile[(i * 16 + (lane >> 4) * 4 + r) * kEpiTS + j * 16 + (lane & 15)] = acc[h * 4 + i][j][r];
-    // the slab is this wave's own and a wave's LDS accesses run in order: no barrier
-    __builtin_amdgcn_wave_barrier();
+    // ---- epilogue: per wave, four 32-row passes through its own slab (over stage 1)
+    float* tile = reinterpret_cast<float*>(smem + kStage4 + wave * kEpiWave);
     const int cl = (lane & 15) * 8;
     const int col = bn + wc * 128 + cl;
     float bias[8];
 #pragma unroll
     for (int q = 0; q < 8; ++q) bias[q] = load_bias(g, col + q, 0);
-#pragma unroll 4
-    for (int it = 0; it < 16; ++it) {
-      const int rl = it * 4 + (lane >> 4);
-      const int row = bm + wr * 128 + h * 64 + rl;
-      if (row >= g.M || col >= g.N) continue;
-      float v[8];
-      const float4 x0 = *reinterpret_cast<const float4*>(tile + rl * kEpiTS + cl);
-      const float4 x1 = *reinterpret_cast<const float4*>(tile + rl * kEpiTS + cl + 4);
-      v[0] = x0.x; v[1] = x0.y; v[2] = x0.z; v[3] = x0.w; v[4] = x1.x; v[5] = x1.y; v[6] = x1.z; v[7] = x1.w;
 #pragma unroll
-      for (int q = 0; q < 8; ++q) v[q] = epi(g, v[q], bias[q]);
-      if (vec_ok) {
-        if (g.out_bf16) {
-          uint16_t* C = reinterpret_cast<uint16_t*>(g.C) + (size_t)row * g.ldc + col;
-          if (g.accumulate) {
-            const uint4 o = *reinterpret_cast<const uint4*>(C);
-            const uint32_t ow[4] = {o.x, o.y, o.z, o.w};
+    for (int h = 0; h < 4; ++h) {
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-            for (int q = 0; q < 4; ++q) { v[2 * q] += bf16_lo(ow[q]); v[2 * q + 1] += bf16_hi(ow[q]); }
-          }
-          uint32_t w[4];
+      for (int i = 0; i < 2; ++i)
 #pragma unroll
-          for (int q = 0; q < 4; ++q) w[q] = f32_to_bf16_bits(v[2 * q]) | (f32_to_bf16_bits(v[2 * q + 1]) << 16);
-          *reinterpret_cast<uint4*>(C) = uint4{w[0], w[1], w[2], w[3]};
-        } else {
-          float* C = reinterpret_cast<float*>(g.C) + (size_t)row * g.ldc + col;
-          float4 y0 = make_float4(v[0], v[1], v[2], v[3]), y1 = make_float4(v[4], v[5], v[6], v[7]);
-          if (g.accumulate) {
-            const float4 o0 = *reinterpret_cast<const float4*>(C), o1 = *reinterpret_cast<const float4*>(C + 4);
-            y0.x += o0.x; y0.y += o0.y; y0.z += o0.z; y0.w += o0.w;
-            y1.x += o1.x; y1.y += o1.y; y1.z += o1.z; y1.w += o1.w;
-          }
-          *reinterpret_cast<float4*>(C) = y0;
-          *reinterpret_cast<float4*>(C + 4) = y1;
-        }
-      } else {
-        for (int q = 0; q < 8 && col + q < g.N; ++q) {
-          const size_t o = (size_t)row * g.ldc + col + q;
+        for (int j = 0; j < 8; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            tile[(i * 16 + (lane >> 4) * 4 + r) * kEpiTS + j * 16 + (lane & 15)] = acc[h * 2 + i][j][r];
+      // the slab is this wave's own and a wave's LDS accesses run in order: no barrier
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll 1
+      for (int it = 0; it < 8; ++it) {
+        const int rl = it * 4 + (lane >> 4);
+        const int row = bm + wr * 128 + h * 32 + rl;
+        if (row >= g.M || col >= g.N) continue;
+        float v[8];
+        const float4 x0 = *reinterpret_cast<const float4*>(tile + rl * kEpiTS + cl);
+        const float4 x1 = *reinterpret_cast<const float4*>(tile + rl * kEpiTS + cl + 4);
+        v[0] = x0.x; v[1] = x0.y; v[2] = x0.z; v[3] = x0.w; v[4] = x1.x; v[5] = x1.y; v[6] = x1.z; v[7] = x1.w;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[q] = epi(g, v[q], bias[q]);
+        if (vec_ok) {
           if (g.out_bf16) {
-            uint16_t* C = reinterpret_cast<uint16_t*>(g.C);
-            C[o] = (uint16_t)f32_to_bf16_bits(v[q] + (g.accumulate ? bf2f(C[o]) : 0.f));
+            uint16_t* C = reinterpret_cast<uint16_t*>(g.C) + (size_t)row * g.ldc + col;
+            if (g.accumulate) {
+              const uint4 o = *reinterpret_cast<const uint4*>(C);
+              const uint32_t ow[4] = {o.x, o.y, o.z, o.w};
+#pragma unroll
+              for (int q = 0; q < 4; ++q) { v[2 * q] += bf16_lo(ow[q]); v[2 * q + 1] += bf16_hi(ow[q]); }
+            }
+            uint32_t w[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) w[q] = f32_to_bf16_bits(v[2 * q]) | (f32_to_bf16_bits(v[2 * q + 1]) << 16);
+            *reinterpret_cast<uint4*>(C) = uint4{w[0], w[1], w[2], w[3]};
           } else {
-            float* C = reinterpret_cast<float*>(g.C);
-            C[o] = v[q] + (g.accumulate ? C[o] : 0.f);
+            float* C = reinterpret_cast<float*>(g.C) + (size_t)row * g.ldc + col;
+            float4 y0 = make_float4(v[0], v[1], v[2], v[3]), y1 = make_float4(v[4], v[5], v[6], v[7]);
+            if (g.accumulate) {
+              const float4 o0 = *reinterpret_cast<const float4*>(C), o1 = *reinterpret_cast<const float4*>(C + 4);
+              y0.x += o0.x; y0.y += o0.y; y0.z += o0.z; y0.w += o0.w;
+              y1.x += o1.x; y1.y += o1.y; y1.z += o1.z; y1.w += o1.w;
+            }
+            *reinterpret_cast<float4*>(C) = y0;
+            *reinterpret_cast<float4*>(C + 4) = y1;
+          }
+        } else {
+          for (int q = 0; q < 8 && col + q < g.N; ++q) {
+            const size_t o = (size_t)row * g.ldc + col + q;
+            if (g.out_bf16) {
+              uint16_t* C = reinterpret_cast<uint16_t*>(g.C);
+              C[o] = (uint16_t)f32_to_bf16_bits(v[q] + (g.accumulate ? bf2f(C[o]) : 0.f));
+            } else {
+              float* C = reinterpret_cast<float*>(g.C);
+              C[o] = v[q] + (g.accumulate ? C[o] : 0.f);
+            }
           }
         }
       }
+      __builtin_amdgcn_wave_barrier();
     }
-    __builtin_amdgcn_wave_barrier();
+    if (!PERSIST || next >= ntiles) break;
+    lt = next;
+    tm = ntm;
+    tn = ntn;
   }
 }
 
 }  // namespace
 
-int g_w4_sched = 1;
+int g_w4_sched = 1;   // bit 0: persistent grid, bit 1: MFMA-first order inside groups
+int g_w4_group_m = 8;
 
 bool gemm_w4_ok(const GemmArgs& g) {
   // one descriptor per operand tile: the bytes from a tile's first row must fit 2 GiB
@@ -291,15 +326,34 @@ bool gemm_w4_ok(const GemmArgs& g) {
          (long)g.M * g.lda * 2 < 0x7ffffff0l && (long)g.N * g.ldb * 2 < 0x7ffffff0l;
 }
 
+static void w4_attr(const void* f) {
+  (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kLds4);
+}
+
 void launch_gemm_nt_w4(const GemmArgs& g, hipStream_t stream) {
-  static bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(k_gemm_w4<0>),
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, kLds4) == hipSuccess &&
-                     hipFuncSetAttribute(reinterpret_cast<const void*>(k_gemm_w4<1>),
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, kLds4) == hipSuccess;
+  static int cus = [] {
+    int dev = 0, n = 0;
+    (void)hipGetDevice(&dev);
+    return hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0 ? n : 256;
+  }();
+  const int ntiles = ((g.M + WM - 1) / WM) * ((g.N + WNB - 1) / WNB);
+  W4Args a{g, g_w4_group_m};
+  const bool persist = g_w4_sched & 1;
+  const int grid = persist ? std::min(ntiles, cus) : ntiles;
+  static bool attr = [] {
+    w4_attr(reinterpret_cast<const void*>(k_gemm_w4<0, 0>));
+    w4_attr(reinterpret_cast<const void*>(k_gemm_w4<1, 0>));
+    w4_attr(reinterpret_cast<const void*>(k_gemm_w4<0, 1>));
+    w4_attr(reinterpret_cast<const void*>(k_gemm_w4<1, 1>));
+    return true;
+  }();
   (void)attr;
-  const int nwg = ((g.M + WM - 1) / WM) * ((g.N + WNB - 1) / WNB);
-  if (g_w4_sched == 1) hipLaunchKernelGGL((k_gemm_w4<1>), dim3(nwg), dim3(WNT), kLds4, stream, g);
-  else hipLaunchKernelGGL((k_gemm_w4<0>), dim3(nwg), dim3(WNT), kLds4, stream, g);
+  switch (g_w4_sched & 3) {
+    case 0: hipLaunchKernelGGL((k_gemm_w4<0, 0>), dim3(grid), dim3(WNT), kLds4, stream, a); break;
+    case 1: hipLaunchKernelGGL((k_gemm_w4<1, 0>), dim3(grid), dim3(WNT), kLds4, stream, a); break;
+    case 2: hipLaunchKernelGGL((k_gemm_w4<0, 1>), dim3(grid), dim3(WNT), kLds4, stream, a); break;
+    default: hipLaunchKernelGGL((k_gemm_w4<1, 1>), dim3(grid), dim3(WNT), kLds4, stream, a); break;
+  }
 }
 
 }  // namespace gemm

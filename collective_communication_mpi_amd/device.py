@@ -30,14 +30,21 @@ Algorithms (``algo=``):
 =================  ============================================================
 
 Tensors obtained from :meth:`DeviceGroup.empty` live in symmetric segments
-(same offset on every rank, peer-mapped once), so collectives on them need no
-staging.  Any other CUDA tensor works too: it is staged through the scratch
-segment in identically sized chunks on every rank.
+(peer-mapped once), so collectives on them need no staging.  Any other CUDA
+tensor of at least ``CCMPI_REGISTER_MIN_BYTES`` (1 MiB) is registered on
+demand: one host all-gather per call carries every rank's (IPC handle,
+allocation, allocator generation) of the caching-allocator segment holding
+it, each distinct combination is mapped once into an LRU of
+``CCMPI_REGISTER_SLOTS`` segment slots, and the kernels then read and write
+the caller's tensors in place (no copy in, no copy out).  Smaller tensors are
+staged through the scratch segment in identically sized chunks on every rank.
 """
 from __future__ import annotations
 
 import os
+import struct
 import threading
+from collections import OrderedDict
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -117,6 +124,21 @@ def alltoallv_plan(counts, me: int, es: int):
     soff = [int(x) for x in np.concatenate([[0], np.cumsum(b[me])[:-1]])]
     doff = [int(b[:me, j].sum()) for j in range(p)]
     return soff, doff, [int(x) for x in b[me]], int(b.sum(axis=1).max())
+
+
+def stale_keys(keys, key) -> List[tuple]:
+    """On-demand registration slots that ``key`` invalidates: a slot is keyed by one
+    (IPC handle, allocation base, bytes, allocator generation) per rank; it is stale
+    when, on some rank, its allocation overlaps the new one's address range but is
+    not the same allocation (the range was freed and reallocated).  Pure function of
+    the keys, which every rank holds identically, so every rank drops the same slots."""
+    out = []
+    for k in keys:
+        for a, b in zip(k, key):
+            if a != b and a[1] < b[1] + b[2] and b[1] < a[1] + a[2]:
+                out.append(k)
+                break
+    return out
 
 
 def tuning_key(size: int, ranks_per_device: int, device_name: str) -> str:
@@ -240,6 +262,14 @@ class DeviceGroup:
         self.tune_file = os.environ.get("CCMPI_TUNE_FILE")
         if self.tune_file:
             self.tuned.update(load_tuning(self.tune_file, self.tune_key))
+        # on-demand registration of ordinary CUDA tensors (collectives >= reg_min bytes)
+        self.reg_min = _env_int("CCMPI_REGISTER_MIN_BYTES", 1 << 20)  # 0 = off
+        self.reg_slots = max(1, _env_int("CCMPI_REGISTER_SLOTS", 32))
+        self._dyn: "OrderedDict[tuple, int]" = OrderedDict()  # identity of every rank's allocation -> slot
+        self._exports: Dict[int, Tuple[bytes, int, int]] = {}  # allocation base -> (handle, base, bytes)
+        self._free_slots: List[int] = []  # released slot indices (reused before new ones)
+        self._alloc_gen = None
+        self.registrations = 0  # slots (re)mapped so far (tests, traces)
         self._lock = threading.Lock()
         self._watchdog: Optional[threading.Thread] = None
         mode = os.environ.get("CCMPI_WATCHDOG", "warn").lower()
@@ -439,6 +469,110 @@ class DeviceGroup:
     def _symm(self, *ts) -> bool:
         return all(self.is_symmetric(t) and t.data_ptr() % 16 == 0 for t in ts)
 
+    def _symm_call(self, nbytes: int, *ts) -> bool:
+        """The ``symmetric`` decision of one collective, identical on every rank.
+        Below ``reg_min`` bytes (or with registration off): every tensor from the
+        symmetric heap (the caller's promise).  From ``reg_min`` up: collective
+        on-demand registration of whatever the tensors live in."""
+        if self.size == 1 or self.reg_min <= 0 or nbytes < self.reg_min:
+            return self._symm(*ts)
+        return self._register_call(ts)
+
+    def _alloc_generation(self) -> int:
+        """Segments this process's caching allocator has returned to the driver: a
+        change means an address range may now hold a different allocation."""
+        try:
+            return int(self.torch._C._cuda_memoryStats(self.device.index or 0)["segment"]["all"]["freed"])
+        except Exception:  # noqa: BLE001 - stats unavailable: assume nothing is ever freed
+            return 0
+
+    def _export(self, ptr: int):
+        """(IPC handle, allocation base, allocation bytes) of the allocation holding ``ptr``."""
+        for base, ent in self._exports.items():
+            if base <= ptr < base + ent[2]:
+                return ent
+        ent = tuple(self.dc.export_alloc(ptr))
+        self._exports[ent[1]] = ent
+        return ent
+
+    def _register_call(self, ts) -> bool:
+        """Collective: map the allocations holding ``ts`` on every rank into peer-visible
+        segment slots.  Returns False (staged path, on every rank) when any rank's
+        tensor cannot be exported or is misaligned, or when a new mapping would be
+        needed during a HIP graph capture."""
+        gen = self._alloc_generation()
+        if gen != self._alloc_gen:
+            self._exports.clear()
+            self._alloc_gen = gen
+        mine = []
+        for t in ts:
+            if t.data_ptr() % 16:
+                mine = None
+                break
+            if self.is_symmetric(t):
+                mine.append(None)  # a heap block: already mapped everywhere
+                continue
+            try:
+                h, base, size = self._export(t.data_ptr())
+            except Exception:  # noqa: BLE001 - not an exportable device allocation
+                mine = None
+                break
+            mine.append((h, base, size, gen))
+        rows = self.host.allgather(mine)
+        if any(r is None for r in rows):
+            return False
+        capturing = self.torch.cuda.is_current_stream_capturing()
+        for i in range(len(ts)):
+            if all(r[i] is None for r in rows):
+                continue  # heap blocks on every rank
+            ids = []
+            for j, r in enumerate(rows):
+                if r[i] is None:  # heap on rank j: its arena allocation is the mapping
+                    ids.append(None)
+                else:
+                    ids.append(r[i])
+            if any(x is None for x in ids):
+                # mixed heap / non-heap: every rank maps its own allocation; heap ranks
+                # export their arena (never freed while the group lives)
+                if mine[i] is None:
+                    h, base, size = self._export(ts[i].data_ptr())
+                    mine_i = (h, base, size, gen)
+                else:
+                    mine_i = mine[i]
+                ids = self.host.allgather(mine_i)
+            key = tuple(ids)
+            slot = self._dyn.get(key)
+            if slot is not None:
+                self._dyn.move_to_end(key)
+                continue
+            if capturing:
+                return False
+            self._map_slot(key)
+        return True
+
+    def _map_slot(self, key) -> None:
+        """Collective: map the allocation set ``key`` (one (handle, base, bytes, gen) per
+        rank) into a slot.  Slots holding an older allocation at an overlapping address
+        on any rank are released first (every rank sees the same keys, so the slot
+        table stays identical everywhere)."""
+        torch = self.torch
+        stale = stale_keys(self._dyn.keys(), key)
+        if stale or (not self._free_slots and len(self._dyn) >= self.reg_slots):
+            torch.cuda.synchronize(self.device)  # no queued kernel of this rank still resolves a slot
+        for k in stale:
+            s = self._dyn.pop(k)
+            self.dc.clear_segment(s)
+            self._free_slots.append(s)
+        if not self._free_slots and len(self._dyn) >= self.reg_slots:
+            self._free_slots.append(self._dyn.popitem(last=False)[1])  # least recently used
+        slot = self._free_slots.pop() if self._free_slots else -1
+        me = key[self.rank]
+        handles = [k[0] for k in key]
+        keys = [k[0] + struct.pack("<QQQ", k[1], k[2], k[3]) for k in key]
+        slot = self.dc.set_segment(slot, me[1], me[2], handles, [0] * self.size, keys)
+        self._dyn[key] = slot
+        self.registrations += 1
+
     def pick_allreduce(self, nbytes: int) -> str:
         if self.size == 1:
             return "twoshot"
@@ -490,7 +624,9 @@ class DeviceGroup:
         if algo in _HAND_ALGOS:
             # ring / rhd read only the local input and push into peers' outputs:
             # "symmetric" there means a registered output (and an aligned input)
-            symm = (self._symm(dst) and src.data_ptr() % 16 == 0) if algo in ("ring", "rhd") else self._symm(src, dst)
+            symm = self._symm_call(nbytes, *((dst,) if algo in ("ring", "rhd") else (src, dst)))
+            if algo in ("ring", "rhd"):
+                symm = symm and src.data_ptr() % 16 == 0
             self.dc.allreduce(src.data_ptr(), dst.data_ptr(), src.numel(), dt, opc, getattr(self.D, _HAND_ALGOS[algo]),
                               s, self._budget(max_blocks), symm)
         elif algo == "rccl":
@@ -513,7 +649,7 @@ class DeviceGroup:
             self.dc.rccl_reduce_scatter(src.data_ptr(), dst.data_ptr(), dst.numel(), dt, opc, s)
         else:
             self.dc.reduce_scatter(src.data_ptr(), dst.data_ptr(), dst.numel(), dt, opc, s,
-                                   self._budget(max_blocks), self._symm(src))
+                                   self._budget(max_blocks), self._symm_call(src.numel() * src.element_size(), src))
         return dst
 
     @trace_call("allgather")
@@ -532,12 +668,15 @@ class DeviceGroup:
         if algo == "rccl":
             self.ensure_rccl()
             self.dc.rccl_allgather(src.data_ptr(), dst.data_ptr(), nb, 1, s)
-        elif algo in ("push", "auto") and self._symm(dst) and src.data_ptr() % 16 == 0 and nb % 16 == 0:
-            # push: 0.85x the pull form's time at 64-256 MiB (profiles/r2_coll/allgather_push.md)
-            self.dc.allgather(src.data_ptr(), dst.data_ptr(), nb, s, self._budget(max_blocks), True, self.D.A2A_PUSH)
-        elif algo in ("direct", "auto", "push"):
-            self.dc.allgather(src.data_ptr(), dst.data_ptr(), nb, s, self._budget(max_blocks),
-                              self._symm(src) and dst.data_ptr() % 16 == 0, self.D.A2A_PULL)
+        elif algo in ("push", "auto", "direct"):
+            # one collective decision for the call (registers both tensors when large)
+            symm = self._symm_call(nb * self.size, src, dst)
+            if algo in ("push", "auto") and symm and nb % 16 == 0:
+                # push: 0.85x the pull form's time at 64-256 MiB (profiles/r2_coll/allgather_push.md)
+                self.dc.allgather(src.data_ptr(), dst.data_ptr(), nb, s, self._budget(max_blocks), True, self.D.A2A_PUSH)
+            else:
+                self.dc.allgather(src.data_ptr(), dst.data_ptr(), nb, s, self._budget(max_blocks),
+                                  symm and dst.data_ptr() % 16 == 0, self.D.A2A_PULL)
         else:
             raise ValueError(f"unknown allgather algorithm {algo!r}")
         return dst
@@ -562,19 +701,21 @@ class DeviceGroup:
         if algo == "rccl":
             self.ensure_rccl()
             self.dc.rccl_alltoall(src.data_ptr(), dst.data_ptr(), blk, 1, s)
-        elif algo == "pairwise":
-            # hand-written pairwise rounds on the flag protocol (myAlltoall2's schedule)
-            self.dc.alltoall(src.data_ptr(), dst.data_ptr(), blk, s, self._budget(max_blocks),
-                             self._symm(dst) and src.data_ptr() % 16 == 0, self.D.A2A_PAIRWISE)
         elif algo == "pairwise_rccl":
             self.ensure_rccl()
             self.dc.p2p_pairwise_alltoall(src.data_ptr(), dst.data_ptr(), blk, s)
-        elif algo == "push":
-            self.dc.alltoall(src.data_ptr(), dst.data_ptr(), blk, s, self._budget(max_blocks),
-                             self._symm(dst) and src.data_ptr() % 16 == 0, self.D.A2A_PUSH)
-        elif algo in ("direct", "auto"):
-            self.dc.alltoall(src.data_ptr(), dst.data_ptr(), blk, s, self._budget(max_blocks), self._symm(src),
-                             self.D.A2A_PULL)
+        elif algo in ("pairwise", "push", "direct", "auto"):
+            symm = self._symm_call(blk * self.size, src, dst)
+            if algo == "pairwise":
+                # hand-written pairwise rounds on the flag protocol (myAlltoall2's schedule)
+                self.dc.alltoall(src.data_ptr(), dst.data_ptr(), blk, s, self._budget(max_blocks),
+                                 symm and src.data_ptr() % 16 == 0, self.D.A2A_PAIRWISE)
+            elif algo == "push":
+                self.dc.alltoall(src.data_ptr(), dst.data_ptr(), blk, s, self._budget(max_blocks),
+                                 symm and src.data_ptr() % 16 == 0, self.D.A2A_PUSH)
+            else:
+                self.dc.alltoall(src.data_ptr(), dst.data_ptr(), blk, s, self._budget(max_blocks), symm,
+                                 self.D.A2A_PULL)
         else:
             raise ValueError(f"unknown alltoall algorithm {algo!r}")
         return dst
@@ -694,7 +835,7 @@ class DeviceGroup:
             self.ensure_rccl()
             self.dc.rccl_bcast(buf.data_ptr(), nb, 1, root, s)
         elif algo in ("direct", "auto", "push"):
-            symm = self._symm(buf)
+            symm = self._symm_call(nb, buf)
             mode = self.D.A2A_PUSH if (algo == "push" and symm) else self.D.A2A_PULL
             self.dc.bcast(buf.data_ptr(), nb, root, s, self._budget(None), symm, mode)
         else:
@@ -704,13 +845,14 @@ class DeviceGroup:
     def allgather_lastaxis(self, src, dst, rows: int, row_bytes: int):
         """dst[m][j*k:(j+1)*k] = src_j[m]  (TP forward collect, fused layout)."""
         self.dc.allgather_lastaxis(src.data_ptr(), dst.data_ptr(), rows, row_bytes, self._stream(), self._budget(None),
-                                   self._symm(src))
+                                   self._symm_call(rows * row_bytes, src))
         return dst
 
     def reduce_scatter_lastaxis(self, src, dst, rows: int, k: int, op="SUM"):
         """dst[m] = sum_j src_j[m][me*k:(me+1)*k]  (TP backward grad_x, fused layout)."""
         self.dc.reduce_scatter_lastaxis(src.data_ptr(), dst.data_ptr(), rows, k, dtype_code(src.dtype), op_code(op),
-                                        self._stream(), self._budget(None), self._symm(src))
+                                        self._stream(), self._budget(None),
+                                        self._symm_call(rows * k * self.size * src.element_size(), src))
         return dst
 
     def local_reduce(self, inputs: Sequence, out, op="SUM"):

@@ -79,7 +79,9 @@ def _slice_last(x: torch.Tensor, comm) -> torch.Tensor:
 
 
 class _CopyToTP(torch.autograd.Function):
-    """Identity forward, TP all-reduce of the gradient (Megatron "f")."""
+    """Identity forward, TP all-reduce of the gradient (Megatron "f").  The gradient
+    is reduced in place: autograd hands this node a buffer it owns, and the device
+    plane registers it on demand (no copy in or out, DeviceGroup._register_call)."""
 
     @staticmethod
     def forward(ctx, x, comm):
@@ -88,15 +90,20 @@ class _CopyToTP(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g):
-        return all_reduce_(g.contiguous().clone(), ctx.comm), None
+        return all_reduce_(g.contiguous(), ctx.comm), None
 
 
 class _ReduceFromTP(torch.autograd.Function):
-    """TP all-reduce forward, identity backward (Megatron "g")."""
+    """TP all-reduce forward, identity backward (Megatron "g").  The partial product
+    is reduced in place (it is the fresh output of the row-parallel GEMM, which its
+    backward does not need), so the 32 MiB Llama activation is never cloned."""
 
     @staticmethod
     def forward(ctx, x, comm):
-        return all_reduce_(x.contiguous().clone(), comm)
+        if not x.is_contiguous():
+            return all_reduce_(x.contiguous(), comm)
+        ctx.mark_dirty(x)
+        return all_reduce_(x, comm)
 
     @staticmethod
     def backward(ctx, g):

@@ -6,7 +6,7 @@ cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
 OUT=gpurun_out/r3_gemm_w4${TAG:+_$TAG}
 mkdir -p $OUT
-timeout -k 10 300 python3 benchmarks/gemm_bench.py --rounds 3 \
+timeout -k 10 400 python3 benchmarks/gemm_bench.py --rounds 3 --w4 ${W4:-0:8,1:8,3:8} \
   --shapes ${SHAPES:-4096x4096x14336,4096x28672x4096,4096x4096x28672,4096x14336x4096,8192x8192x8192} \
   > $OUT/gemm_bench.txt 2>&1 || { echo "gemm_bench failed"; tail -20 $OUT/gemm_bench.txt; exit 1; }
 cat $OUT/gemm_bench.txt

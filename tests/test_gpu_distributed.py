@@ -24,11 +24,23 @@ def test_device_collectives_multi_rank(n, matrix):
     assert "0 failures" in r.stdout
 
 
-@pytest.mark.parametrize("n", [2, 4])
-def test_device_collectives_big(n):
-    """>= 96 MiB: staging-chunk loops and ring/rhd inbox pieces (inbox capped at 64 MiB)."""
+@pytest.mark.parametrize("n,reg", [(2, "0"), (4, "0"), (2, str(1 << 20))])
+def test_device_collectives_big(n, reg):
+    """>= 96 MiB: staging-chunk loops and ring/rhd inbox pieces (inbox capped at 64 MiB);
+    with on-demand registration off (reg 0) the ordinary tensors take the staging loops,
+    with it on they are mapped and reduced in place."""
     r = run_ranks(n, py("tests/workers/device_worker.py", "--big"), timeout=400,
-                  env=dict(ENV, CCMPI_INBOX_MAX_MB="64"))
+                  env=dict(ENV, CCMPI_INBOX_MAX_MB="64", CCMPI_REGISTER_MIN_BYTES=reg))
+    assert "0 failures" in r.stdout
+
+
+@pytest.mark.parametrize("n", [2, 3, 4, 8])
+def test_device_ondemand_registration(n):
+    """ordinary torch tensors >= 1 MiB are registered on demand (IPC
+    handle of their allocator segment, one host all-gather per call, LRU of mapped
+    slots) and every collective runs on them in place; slots are reused, and a freed
+    and reallocated range is remapped (allocator generation)."""
+    r = run_ranks(n, py("tests/workers/device_worker.py", "--register"), timeout=400, env=ENV)
     assert "0 failures" in r.stdout
 
 
@@ -68,17 +80,48 @@ def test_trace_records_collectives_and_survives_graph_capture(tmp_path):
     assert {"ll", "fanout", "push"} <= {x["algo"] for x in recs}
 
 
-def test_rccl_same_gpu_behaviour_recorded(tmp_path):
-    """RCCL with two ranks on one GPU: the outcome of every step is recorded, not swallowed
-    (benchmarks/rccl_shared_probe.py; on this pool ncclCommInitRank reports 'invalid usage')."""
+def test_rccl_same_gpu_refused_and_recorded(tmp_path):
+    """RCCL with two ranks on one GPU: ncclCommInitRank refuses the duplicate device
+    ('invalid usage', profiles/r2_coll/rccl_shared_gpu.json) on every rank, and the probe
+    records that outcome instead of hanging or swallowing it."""
     import json
 
     out = tmp_path / "probe.json"
     run_ranks(2, py("benchmarks/rccl_shared_probe.py", "--out", str(out)), timeout=200, env=ENV)
     rec = json.loads(out.read_text())
+    assert len(rec["per_rank"]) == 2
     for r in rec["per_rank"]:
         init = r["ncclCommInitRank"]
-        assert init["ok"] or "RCCL error" in init["error"]
+        assert not init["ok"], init
+        assert "RCCL error" in init["error"] and "invalid usage" in init["error"], init
+
+
+def _bench_line(extra_env, *args):
+    import json
+    import subprocess
+    import sys
+
+    from _launch import REPO
+
+    e = dict(os.environ, **ENV, **extra_env)
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--steps", "2", "--warmup", "1", "--size-mb", "16",
+                        "--a2a-mb", "8", "--dp-layers", "0", "--batch", "128", "--no-secondary", *args],
+                       cwd=REPO, env=e, capture_output=True, text=True, timeout=400)
+    assert r.returncode == 0, r.stderr[-4000:]
+    return json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+
+
+@pytest.mark.parametrize("mode", ["error", "hang"])
+def test_bench_survives_rccl_failure(mode):
+    """the RCCL baseline runs in its own child group after every
+    hand-written number is measured; an RCCL error (forced on ranks that share the GPU)
+    or a hang (killed at --rccl-timeout) costs only the 'rccl' entry, never the line."""
+    env = {"CCMPI_BENCH_RCCL": "force"} if mode == "error" else {"CCMPI_BENCH_RCCL": "hang"}
+    out = _bench_line(env, "--rccl-timeout", "60")
+    c = out["config"]
+    assert out["value"] > 0 and c["result_exact"] and c["tp_fwd_step_ms"] > 0
+    assert "error" in c["rccl"], c["rccl"]
+    assert all(v for v in c["candidates_ms"].values()), c["candidates_ms"]
 
 
 @pytest.mark.parametrize("case", ["myallreduce", "myalltoall"])

@@ -20,6 +20,9 @@ usage: device_worker.py [--matrix quick|full|wide] [--big] [--rccl] [--stress N]
             16 MiB, symmetric and staged calls) with randomised per-rank host
             sleeps and device-side spin delays, so ranks arrive at each kernel
             in random order; every result is checked at the end (epoch/ABA safety).
+--register  on-demand registration of ordinary (caching-allocator) tensors >= 1 MiB:
+            every collective in place on them (no staging), reuse of mapped slots,
+            and a freed-and-reallocated allocation picked up afresh.
 --fault     SURVEY §5.3: rank p-1 skips one collective; the others must time out
             (bounded spins), the host watchdog must see the code without a device
             sync, check() must raise, and reset() must restore a working group.
@@ -43,6 +46,7 @@ ap.add_argument("--rccl", action="store_true")
 ap.add_argument("--sizes", default="")
 ap.add_argument("--stress", type=int, default=0)
 ap.add_argument("--fault", action="store_true")
+ap.add_argument("--register", action="store_true")
 args = ap.parse_args()
 if args.quick:
     args.matrix = "quick"
@@ -696,6 +700,75 @@ if dtypes:
             check(f"backward_x_lastaxis[{dt},{B}x{S}x{k}]", got, ref, dt, p)
 
 _lap("lastaxis")
+# ------------------------------------- on-demand registration of torch tensors
+if args.register:
+    n = (1 << 20) + 4  # 4 MiB + 16 B of fp32 (>= CCMPI_REGISTER_MIN_BYTES)
+    reg0 = dev.registrations
+    for algo in ("oneshot", "twoshot", "fanout", "push", "ring") + (("rhd",) if POW2 else ()):
+        for inplace in (False, True):
+            salt += 1
+            x = gen(rank, n, torch.float32, salt)  # ordinary torch tensor
+            y = x if inplace else torch.empty_like(x)
+            dev.allreduce(x, y, "SUM", algo)
+            check(f"reg_allreduce[{algo},inplace={inplace}]", y, oracle(n, torch.float32, "SUM", salt),
+                  torch.float32, p)
+    nb = (1 << 18) + 4
+    salt += 1
+    x = gen(rank, p * nb, torch.float32, salt)
+    want = torch.cat([gen(r, p * nb, torch.float32, salt)[rank * nb:(rank + 1) * nb] for r in range(p)]).double()
+    for aa in ("direct", "push", "pairwise"):
+        y = torch.empty_like(x)
+        dev.alltoall(x, y, aa)
+        check(f"reg_alltoall[{aa}]", y, want, torch.float32)
+    salt += 1
+    x = gen(rank, nb, torch.float32, salt)
+    y = torch.empty(p * nb, device=D)
+    for ag in ("direct", "push"):
+        y.zero_()
+        dev.allgather(x, y, ag)
+        check(f"reg_allgather[{ag}]", y, torch.cat([gen(r, nb, torch.float32, salt) for r in range(p)]).double(),
+              torch.float32)
+    salt += 1
+    x = gen(rank, p * nb, torch.float32, salt)
+    y = torch.empty(nb, device=D)
+    dev.reduce_scatter(x, y)
+    check("reg_reduce_scatter", y, oracle(p * nb, torch.float32, "SUM", salt)[rank * nb:(rank + 1) * nb],
+          torch.float32, p)
+    if dev.registrations <= reg0:
+        fails.append("registration: no segment was mapped for the large ordinary tensors")
+    # the same tensors again: mapped slots are reused (no new registrations)
+    reg1 = dev.registrations
+    x = gen(rank, n, torch.float32, 424242)
+    y = torch.empty_like(x)
+    dev.allreduce(x, y, "SUM", "fanout")
+    dev.allreduce(x, y, "SUM", "fanout")
+    check("reg_reuse", y, oracle(n, torch.float32, "SUM", 424242), torch.float32, p)
+    if dev.registrations - reg1 > 2:
+        fails.append(f"registration: {dev.registrations - reg1} new slots for two identical calls")
+    # free every cached segment, allocate again (likely at the same addresses): the
+    # allocator generation changes, stale slots are dropped, results stay exact
+    del x, y
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    for it in range(3):
+        salt += 1
+        x = gen(rank, n, torch.float32, salt)
+        y = torch.empty_like(x)
+        dev.allreduce(x, y, "SUM", "fanout")
+        check(f"reg_after_free[{it}]", y, oracle(n, torch.float32, "SUM", salt), torch.float32, p)
+        del x, y
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+    # mixed: heap input on every rank, ordinary output
+    salt += 1
+    xs = sym_copy(gen(rank, n, torch.float32, salt))
+    y = torch.empty(n, device=D)
+    dev.allreduce(xs, y, "SUM", "fanout")
+    check("reg_mixed_heap_ordinary", y, oracle(n, torch.float32, "SUM", salt), torch.float32, p)
+    torch.cuda.synchronize()
+    dev.check()
+
+_lap("register")
 # ------------------------------------------------------- >= 96 MiB: chunk loops
 if args.big:
     n = (24 << 20) + 5  # 96 MiB + 20 B of fp32: > 32 MiB staging chunks, odd tail
