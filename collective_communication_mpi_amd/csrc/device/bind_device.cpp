@@ -173,6 +173,13 @@ PYBIND11_MODULE(_device, m) {
       .def("reset_state", &DeviceComm::reset_state, py::call_guard<py::gil_scoped_release>())
       .def("set_inbox", &DeviceComm::set_inbox)
       .def("ll_alloc", [](DeviceComm& d, uint64_t max_bytes) { return py::bytes(d.ll_alloc(max_bytes)); })
+      .def("fused_alloc", [](DeviceComm& d) { return py::bytes(d.fused_alloc()); })
+      .def("fused_connect", [](DeviceComm& d, const std::vector<std::string>& hs) { d.fused_connect(hs); })
+      .def("set_fused_inbox", &DeviceComm::set_fused_inbox)
+      .def_property_readonly("fused_inbox_bytes", &DeviceComm::fused_inbox_bytes)
+      .def_property_readonly("fused_ready", &DeviceComm::fused_ready)
+      .def("code_of", [](DeviceComm& d, uint64_t ptr, uint64_t n) { return d.code_of_public(ptr, n); })
+      .def("gemm_rowpar", &DeviceComm::gemm_rowpar, py::call_guard<py::gil_scoped_release>())
       .def("ll_connect", [](DeviceComm& d, const std::vector<std::string>& hs) { d.ll_connect(hs); })
       .def_property_readonly("ll_max_bytes", &DeviceComm::ll_max_bytes)
       .def_property_readonly("inbox_bytes", &DeviceComm::inbox_bytes)

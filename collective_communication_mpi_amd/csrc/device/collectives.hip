@@ -52,12 +52,6 @@ __device__ __forceinline__ BlockRange split_range(uint64_t n, int parts, int idx
   return {lo, hi};
 }
 
-__device__ __forceinline__ char* uniform_ptr(char* p) {
-  uint64_t v = (uint64_t)p;
-  uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
-  uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
-  return (char*)(((uint64_t)hi << 32) | lo);
-}
 
 // Per-CTA prologue: bump the epoch, publish up to two buffer codes, barrier.
 // Returns false on timeout.  `codes` (LDS) receives every rank's codes.

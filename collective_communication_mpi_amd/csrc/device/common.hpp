@@ -130,6 +130,15 @@ __device__ __forceinline__ void st16(Rsrc r, uint32_t off, u32x4 v) {
   __builtin_amdgcn_raw_buffer_store_b128(v, r.r, off, 0, kStorePolicy);
 }
 
+// A pointer every lane holds identically, made provably wave-uniform (SGPRs), so
+// buffer descriptors built from it need no waterfall loop.
+__device__ __forceinline__ char* uniform_ptr(char* p) {
+  uint64_t v = (uint64_t)p;
+  uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+  uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  return (char*)(((uint64_t)hi << 32) | lo);
+}
+
 __device__ __forceinline__ uint64_t now_ticks() { return __builtin_amdgcn_s_memrealtime(); }  // 100 MHz
 
 // Bounded wait until *p >= want (system scope). Returns false on timeout and

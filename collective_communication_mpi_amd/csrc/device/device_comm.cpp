@@ -120,6 +120,8 @@ DeviceComm::~DeviceComm() {
   if (dev_pt_) (void)hipFree(dev_pt_);
   if (ll_state_) (void)hipFree(ll_state_);
   if (ll_buf_) (void)hipFree(ll_buf_);
+  if (fused_state_) (void)hipFree(fused_state_);
+  if (fused_tab_dev_) (void)hipFree(fused_tab_dev_);
   if (host_err_) (void)hipHostFree(host_err_);
 }
 
@@ -930,6 +932,74 @@ void DeviceComm::p2p_pairwise_alltoall(uint64_t in, uint64_t out, uint64_t bytes
   }
 }
 
+std::string DeviceComm::fused_alloc() {
+  if (fused_state_) throw std::runtime_error("ccmpi: fused GEMM state already allocated");
+  CCMPI_HIP_CHECK(hipSetDevice(device_));
+  CCMPI_HIP_CHECK(hipExtMallocWithFlags(reinterpret_cast<void**>(&fused_state_), sizeof(gemm::FusedState),
+                                        hipDeviceMallocUncached));
+  CCMPI_HIP_CHECK(hipMemset(fused_state_, 0, sizeof(gemm::FusedState)));
+  CCMPI_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&fused_tab_dev_), sizeof(gemm::FusedTable)));
+  CCMPI_HIP_CHECK(hipDeviceSynchronize());
+  hipIpcMemHandle_t h;
+  CCMPI_HIP_CHECK(hipIpcGetMemHandle(&h, fused_state_));
+  return std::string(reinterpret_cast<const char*>(&h), sizeof(h));
+}
+
+void DeviceComm::fused_connect(const std::vector<std::string>& handles) {
+  if (!fused_state_ || (int)handles.size() != size_)
+    throw std::invalid_argument("ccmpi: fused_connect needs fused_alloc and one handle per rank");
+  CCMPI_HIP_CHECK(hipSetDevice(device_));
+  for (int j = 0; j < size_; ++j) {
+    if (j == rank_) {
+      fused_tab_.state[j] = fused_state_;
+      continue;
+    }
+    fused_tab_.state[j] = static_cast<gemm::FusedState*>(ipc_open(handles[j]));
+    opened_.push_back(handles[j]);
+  }
+  CCMPI_HIP_CHECK(hipMemcpy(fused_tab_dev_, &fused_tab_, sizeof(fused_tab_), hipMemcpyHostToDevice));
+}
+
+void DeviceComm::set_fused_inbox(uint64_t ptr, uint64_t bytes, const std::vector<uint64_t>& codes) {
+  if (!fused_tab_dev_ || (int)codes.size() != size_) throw std::invalid_argument("ccmpi: set_fused_inbox before fused_connect");
+  if (ptr % 16 || find(ptr, bytes, nullptr) <= 0 || codes[rank_] != code_of_(ptr, bytes))
+    throw std::invalid_argument("ccmpi: the fused inbox must be an aligned symmetric allocation");
+  CCMPI_HIP_CHECK(hipSetDevice(device_));
+  CCMPI_HIP_CHECK(hipDeviceSynchronize());  // no fused GEMM in flight reads the old table
+  for (int j = 0; j < size_; ++j) fused_tab_.inbox_code[j] = codes[j];
+  CCMPI_HIP_CHECK(hipMemcpy(fused_tab_dev_, &fused_tab_, sizeof(fused_tab_), hipMemcpyHostToDevice));
+  fused_inbox_bytes_ = bytes;
+}
+
+void DeviceComm::gemm_rowpar(uint64_t A, uint64_t B, uint64_t out, uint64_t bias, int M, int N, int K, int lda,
+                             int ldb, int ldc, float alpha, int bias_kind, uint64_t stream) {
+  if (M <= 0 || N <= 0) return;
+  if (!fused_ready()) throw std::runtime_error("ccmpi: fused row-parallel GEMM not set up");
+  const int tiles = gemm::gemm_w4_tiles(M, N);
+  const uint64_t need = (uint64_t)((tiles + size_ - 1) / size_) * size_ * gemm::kFusedTileBytes;
+  if (tiles > gemm::kFusedMaxTiles || need > fused_inbox_bytes_)
+    throw std::invalid_argument("ccmpi: fused row-parallel GEMM: output too large for the inbox / tile table");
+  if (K % 64 || lda % 8 || ldb % 8 || ldc % 8 || N % 8 || (A % 16) || (B % 16) || (out % 16) ||
+      (uint64_t)M * ldc * 2 >= 0x7ffffff0ull)
+    throw std::invalid_argument("ccmpi: fused row-parallel GEMM needs K % 64 == 0, 16-B aligned rows, N % 8 == 0");
+  CCMPI_HIP_CHECK(hipSetDevice(device_));
+  uint64_t oc = 0;
+  {
+    DynScope dyn_scope(this, true);  // the caller registered `out` (heap block or on-demand slot)
+    oc = code_of_(out, (uint64_t)M * ldc * 2);
+  }
+  if (!oc) throw std::invalid_argument("ccmpi: fused row-parallel GEMM: the output must be registered on every rank");
+  gemm::GemmArgs g{reinterpret_cast<const uint16_t*>(A), reinterpret_cast<const uint16_t*>(B),
+                   reinterpret_cast<void*>(out), reinterpret_cast<const void*>(bias), M, N, K, lda, ldb, ldc, alpha, 0,
+                   bias_kind, 0, 1, 1};
+  gemm::FusedArgs f{dev_pt_, fused_tab_dev_, oc, ++fused_seq_, timeout_ticks_};
+  hipStream_t st = S(stream);
+  gemm::launch_gemm_nt_w4_fused(g, f, st);
+  CCMPI_HIP_CHECK(hipGetLastError());
+  gemm::launch_fused_wait(f, tiles, st);
+  CCMPI_HIP_CHECK(hipGetLastError());
+}
+
 uint32_t DeviceComm::error_code() {
   CCMPI_HIP_CHECK(hipSetDevice(device_));
   CCMPI_HIP_CHECK(hipDeviceSynchronize());
@@ -952,6 +1022,8 @@ void DeviceComm::reset_state() {
   CCMPI_HIP_CHECK(hipMemset(epochs_, 0, sizeof(uint64_t) * kMaxBlocks));
   CCMPI_HIP_CHECK(hipMemset(ll_state_, 0, 2 * sizeof(uint32_t)));
   if (ll_buf_) CCMPI_HIP_CHECK(hipMemset(ll_buf_, 0, 2ull * size_ * 2 * ll_max_));
+  if (fused_state_) CCMPI_HIP_CHECK(hipMemset(fused_state_, 0, sizeof(gemm::FusedState)));
+  fused_seq_ = 0;
   CCMPI_HIP_CHECK(hipDeviceSynchronize());
   __atomic_store_n(host_err_, 0u, __ATOMIC_RELEASE);
 }

@@ -19,6 +19,7 @@
 
 #include "collectives.hpp"
 #include "common.hpp"
+#include "gemm_common.hpp"
 
 namespace ccmpi {
 namespace dev {
@@ -114,6 +115,21 @@ class DeviceComm {
   // reference myAlltoall2 rounds as grouped RCCL send/recv (the library form of algo="pairwise")
   void p2p_pairwise_alltoall(uint64_t in, uint64_t out, uint64_t bytes_per_peer, uint64_t stream);
 
+  // ---- row-parallel GEMM with the TP all-reduce fused into its epilogue ------
+  // (gemm_common.hpp FusedState).  Setup, collective through the Python layer:
+  // fused_alloc() returns this rank's IPC handle, fused_connect() maps the peers'.
+  std::string fused_alloc();
+  void fused_connect(const std::vector<std::string>& handles);
+  // the symmetric inbox (a heap block on every rank) and every rank's code of it
+  void set_fused_inbox(uint64_t ptr, uint64_t bytes, const std::vector<uint64_t>& codes);
+  uint64_t fused_inbox_bytes() const { return fused_inbox_bytes_; }
+  // out[M, N] = sum over the group of A_r[M, K_r] . B_r[N, K_r]^T (+ bias), bf16; `out`
+  // registered (heap or on-demand) on every rank, 16-B aligned, N % 8 == 0
+  void gemm_rowpar(uint64_t A, uint64_t B, uint64_t out, uint64_t bias, int M, int N, int K, int lda, int ldb,
+                   int ldc, float alpha, int bias_kind, uint64_t stream);
+  uint64_t code_of_public(uint64_t ptr, uint64_t nbytes) const { return code_of_(ptr, nbytes); }
+  bool fused_ready() const { return fused_tab_dev_ != nullptr && fused_inbox_bytes_ > 0; }
+
   // ---- health ------------------------------------------------------------
   uint32_t error_code();  // synchronises; 0 = ok
   uint32_t poll_error() const;  // non-blocking read of the host-mapped mirror (watchdog)
@@ -183,6 +199,11 @@ class DeviceComm {
   bool copy_engine_ = false;              // single-rank copies: contiguous-slice kernel (3.2 vs 2.6 TB/s for the runtime blit)
   std::vector<std::string> opened_;      // handles we opened (for release)
   std::vector<std::vector<std::string>> seg_keys_;  // per slot: IPC keys opened for on-demand segments
+  gemm::FusedState* fused_state_ = nullptr;  // mine (uncached)
+  gemm::FusedTable fused_tab_{};            // host copy
+  gemm::FusedTable* fused_tab_dev_ = nullptr;
+  uint64_t fused_inbox_bytes_ = 0;
+  uint64_t fused_seq_ = 0;
 };
 
 // Process-wide registry so a handle opened by two communicators maps once.

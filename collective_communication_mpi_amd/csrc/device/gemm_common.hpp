@@ -164,6 +164,40 @@ __device__ __forceinline__ int xcd_remap(int wg, int nwg) {
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + wg / 8;
 }
 
+// ---- row-parallel GEMM with the TP all-reduce fused into its epilogue (gemm_w4.hip) ----
+// Every rank computes the same output tiles from its K-shard.  Per tile, each rank
+// draws a ticket from the tile owner's counter (owner = tile % p); the first p - 1
+// arrivals store their bf16 partial into the owner's inbox slot and flag it, the
+// last arrival sums all partials in rank order (its own from registers, rounded to
+// bf16 like the others, so the sum does not depend on who arrives last), adds the
+// bias and writes the final tile into every rank's output, then flags it done on
+// every rank.  Nobody waits for a workgroup that has not started (the last arrival
+// waits only for ticket holders), so it cannot deadlock when ranks share a GPU.
+constexpr int kFusedMaxTiles = 4096;
+constexpr uint64_t kFusedTileBytes = 256ull * 256 * 2;  // one bf16 256 x 256 partial
+struct FusedState {                        // per rank, uncached, peer-mapped
+  uint64_t out_code[2];                    // [0] this call's output (addr_code), [1] its call sequence
+  uint64_t pad[6];
+  uint32_t cnt[kFusedMaxTiles];            // owner: tickets drawn for tile t (reset by its reducer)
+  uint64_t ready[kFusedMaxTiles][kMaxRanks];  // owner: slot (t, j) holds call `value`'s partial
+  uint64_t done[kFusedMaxTiles];           // every rank: tile t of call `value` is final here
+};
+struct FusedTable {                        // device-resident, per group (set up once)
+  FusedState* state[kMaxRanks];            // state[j]: rank j's (mapped)
+  uint64_t inbox_code[kMaxRanks];          // rank j's inbox (>= ceil(T / p) * p tile slots)
+};
+struct FusedArgs {
+  const PeerTable* pt;
+  const FusedTable* tab;
+  uint64_t out_code;                       // this rank's output
+  uint64_t seq;                            // call sequence number (identical on every rank)
+  uint64_t timeout_ticks;
+};
+void launch_gemm_nt_w4_fused(const GemmArgs& g, const FusedArgs& f, hipStream_t stream);
+// one workgroup: wait until every tile of call `seq` is done on this rank (bounded)
+void launch_fused_wait(const FusedArgs& f, int tiles, hipStream_t stream);
+int gemm_w4_tiles(int M, int N);
+
 // 256 x bn (bn = 256 or 128) 8-wave ping-pong kernel (gemm256.hip); requires K % 128 == 0.
 void launch_gemm_nt_256(const GemmArgs& g, int bn, hipStream_t stream);
 int gemm256_tiles(int M, int N, int bn);

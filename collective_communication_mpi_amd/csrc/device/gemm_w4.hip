@@ -44,9 +44,12 @@ constexpr int kLds4 = kStage4 + ((kStage4 > 4 * kEpiWave) ? kStage4 : 4 * kEpiWa
 
 typedef __attribute__((address_space(3))) void* lds_vptr;
 
+constexpr int kLdsExtra = 256;  // after the slabs: fused-epilogue ticket + peers' output pointers
+
 struct W4Args {
   GemmArgs g;
   int group_m;  // tile rows per group of the group-M order
+  FusedArgs f;  // FUSED only
 };
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t op_rsrc(const uint16_t* base, long rows, int ld) {
@@ -65,10 +68,163 @@ __device__ __forceinline__ void tile_coords(int wg, int tiles_m, int tiles_n, in
   tn = (wg % per_group) / gm;
 }
 
+__device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {
+  return f32_to_bf16_bits(a) | (f32_to_bf16_bits(b) << 16);
+}
+
+// Fused TP all-reduce epilogue (FusedState comment in gemm_common.hpp).  `to_slab(h)`
+// stages this wave's 32-row pass h of the fp32 tile in `tile` (row stride kEpiTS).
+template <typename ToSlab>
+__device__ void fused_epilogue(const W4Args& wa, int t, int bm, int bn, const float* tile, ToSlab&& to_slab,
+                               const float* bias) {
+  extern __shared__ __attribute__((aligned(1024))) unsigned char smem[];
+  const GemmArgs& g = wa.g;
+  const FusedArgs& f = wa.f;
+  const PeerTable* pt = f.pt;
+  const int p = pt->size, me = pt->rank;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, wr = wave >> 1, wc = wave & 1;
+  const int owner = t % p, lidx = t / p;
+  uint32_t* s_ticket = reinterpret_cast<uint32_t*>(smem + kLds4);
+  char** s_out = reinterpret_cast<char**>(smem + kLds4 + 64);
+  FusedState* own = f.tab->state[me];
+  FusedState* ost = f.tab->state[owner];
+  uint32_t* err = &pt->sig[me]->error;
+  if (threadIdx.x == 0) {
+    // publish this call's output (every workgroup writes the same two words), then
+    // draw the ticket: the release orders the publication before the ticket
+    __hip_atomic_store(&own->out_code[0], f.out_code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&own->out_code[1], f.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    release_sys();
+    *s_ticket = __hip_atomic_fetch_add(&ost->cnt[t], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  __syncthreads();
+  const bool last = *s_ticket == (uint32_t)(p - 1);
+  char* inbox = resolve(pt, owner, f.tab->inbox_code[owner]) + (uint64_t)lidx * p * kFusedTileBytes;
+  const int cl = (lane & 15) * 8;
+  if (!last) {
+    // my bf16 partial -> the owner's slot `me` (write-through stores), then flag it
+    const Rsrc slot = make_rsrc(uniform_ptr(inbox + (uint64_t)me * kFusedTileBytes), (uint32_t)kFusedTileBytes);
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+      to_slab(h);
+#pragma unroll 2
+      for (int it = 0; it < 8; ++it) {
+        const int rl = it * 4 + (lane >> 4);
+        const float4 x0 = *reinterpret_cast<const float4*>(tile + rl * kEpiTS + cl);
+        const float4 x1 = *reinterpret_cast<const float4*>(tile + rl * kEpiTS + cl + 4);
+        u32x4 w;
+        const float al = g.alpha;
+        w[0] = pack_bf16x2(al * x0.x, al * x0.y); w[1] = pack_bf16x2(al * x0.z, al * x0.w);
+        w[2] = pack_bf16x2(al * x1.x, al * x1.y); w[3] = pack_bf16x2(al * x1.z, al * x1.w);
+        const int row = wr * 128 + h * 32 + rl, col = wc * 128 + cl;
+        st16(slot, (uint32_t)((row * 256 + col) * 2), w);
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      release_sys();
+      signal_store(&ost->ready[t][me], f.seq);
+    }
+    __syncthreads();  // the slabs are reused by this workgroup's next tile
+    return;
+  }
+  // last arrival: every other rank's partial is (being) stored into the owner's inbox
+  bool ok = true;
+  if ((int)threadIdx.x < p) {
+    const int j = threadIdx.x;
+    if (j != me) {
+      ok = wait_geq(&ost->ready[t][j], f.seq, f.timeout_ticks, err, 0xA00 + j);
+      if (!ok) report_host(pt, 0xA00 + j);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    FusedState* sj = f.tab->state[j];
+    const uint64_t code = __hip_atomic_load(&sj->out_code[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    const uint64_t cseq = __hip_atomic_load(&sj->out_code[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (cseq != f.seq) {  // cannot happen when every rank runs the same call sequence
+      __hip_atomic_store(err, 0xB00u + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      report_host(pt, 0xB00 + j);
+      ok = false;
+    }
+    s_out[j] = ok ? resolve(pt, j, code) : nullptr;
+  }
+  ok = __syncthreads_and(ok);
+  if (ok) {
+    // per pass: this lane's 8 row vectors of 8 columns; the sum runs over the ranks in
+    // order (own partial from the slab, the others' from the inbox, 8 loads in flight
+    // per rank), then the result is stored into every rank's output
+    const uint32_t out_bytes = (uint32_t)min<uint64_t>((uint64_t)g.M * g.ldc * 2, 0x7ffffff0ull);
+    for (int h = 0; h < 4; ++h) {
+      to_slab(h);
+      float v[8][8];
+      u32x4 mine[8];
+#pragma unroll
+      for (int it = 0; it < 8; ++it) {
+        const int rl = it * 4 + (lane >> 4);
+        const float4 x0 = *reinterpret_cast<const float4*>(tile + rl * kEpiTS + cl);
+        const float4 x1 = *reinterpret_cast<const float4*>(tile + rl * kEpiTS + cl + 4);
+        const float al = g.alpha;
+        mine[it][0] = pack_bf16x2(al * x0.x, al * x0.y); mine[it][1] = pack_bf16x2(al * x0.z, al * x0.w);
+        mine[it][2] = pack_bf16x2(al * x1.x, al * x1.y); mine[it][3] = pack_bf16x2(al * x1.z, al * x1.w);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[it][q] = 0.f;
+      }
+      __builtin_amdgcn_wave_barrier();  // slab reads done before the next pass rewrites it
+#pragma unroll 1
+      for (int j = 0; j < p; ++j) {
+        u32x4 x[8];
+        if (j == me) {
+#pragma unroll
+          for (int it = 0; it < 8; ++it) x[it] = mine[it];
+        } else {
+          const Rsrc rs = make_rsrc(uniform_ptr(inbox + (uint64_t)j * kFusedTileBytes), (uint32_t)kFusedTileBytes);
+#pragma unroll
+          for (int it = 0; it < 8; ++it) {
+            const int trow = wr * 128 + h * 32 + it * 4 + (lane >> 4), tcol = wc * 128 + cl;
+            x[it] = ld16(rs, (uint32_t)((trow * 256 + tcol) * 2));
+          }
+        }
+#pragma unroll
+        for (int it = 0; it < 8; ++it)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            v[it][2 * q] += bf16_lo(x[it][q]);
+            v[it][2 * q + 1] += bf16_hi(x[it][q]);
+          }
+      }
+      u32x4 res[8];
+#pragma unroll
+      for (int it = 0; it < 8; ++it)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          res[it][q] = pack_bf16x2(v[it][2 * q] + bias[2 * q], v[it][2 * q + 1] + bias[2 * q + 1]);
+      const int col = bn + wc * 128 + cl;
+#pragma unroll 1
+      for (int j = 0; j < p; ++j) {
+        const Rsrc ro = make_rsrc(uniform_ptr(s_out[j]), out_bytes);
+#pragma unroll
+        for (int it = 0; it < 8; ++it) {
+          const int row = bm + wr * 128 + h * 32 + it * 4 + (lane >> 4);
+          if (row < g.M && col < g.N) st16(ro, (uint32_t)(((uint64_t)row * g.ldc + col) * 2), res[it]);
+        }
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __hip_atomic_store(&ost->cnt[t], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);  // next call's tickets
+    release_sys();
+    for (int j = 0; j < p; ++j) signal_store(&f.tab->state[j]->done[t], f.seq);
+  }
+  __syncthreads();
+}
+
 // PERSIST: grid = min(tiles, CUs); workgroup b runs logical tiles s, s + G, s + 2G, ...
 // (s = XCD-aware remap of b) and prefetches the next tile's first K-tile during the
 // epilogue.  ORDER: MFMA-first issue order inside each fenced group.
-template <int PERSIST, int ORDER>
+template <int PERSIST, int ORDER, int FUSED = 0>
 __global__ void __launch_bounds__(WNT, 1) k_gemm_w4(W4Args wa) {
   const GemmArgs& g = wa.g;
   extern __shared__ __attribute__((aligned(1024))) unsigned char smem[];
@@ -246,6 +402,19 @@ __global__ void __launch_bounds__(WNT, 1) k_gemm_w4(W4Args wa) {
     float bias[8];
 #pragma unroll
     for (int q = 0; q < 8; ++q) bias[q] = load_bias(g, col + q, 0);
+    auto to_slab = [&](int h) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            tile[(i * 16 + (lane >> 4) * 4 + r) * kEpiTS + j * 16 + (lane & 15)] = acc[h * 2 + i][j][r];
+      __builtin_amdgcn_wave_barrier();  // the slab is this wave's own: its LDS accesses run in order
+    };
+    if constexpr (FUSED) {
+      fused_epilogue(wa, tm * tiles_n + tn, bm, bn, tile, to_slab, bias);
+    } else {
 #pragma unroll
     for (int h = 0; h < 4; ++h) {
       __builtin_amdgcn_sched_barrier(0);
@@ -308,6 +477,7 @@ __global__ void __launch_bounds__(WNT, 1) k_gemm_w4(W4Args wa) {
       }
       __builtin_amdgcn_wave_barrier();
     }
+    }  // !FUSED
     if (!PERSIST || next >= ntiles) break;
     lt = next;
     tm = ntm;
@@ -326,8 +496,22 @@ bool gemm_w4_ok(const GemmArgs& g) {
          (long)g.M * g.lda * 2 < 0x7ffffff0l && (long)g.N * g.ldb * 2 < 0x7ffffff0l;
 }
 
+// After the fused GEMM: this rank's output is final once every tile's reducer has
+// flagged it (bounded spins; a timeout records 0xC00 and the kernel returns).
+__global__ void __launch_bounds__(256) k_fused_wait(FusedArgs f, int tiles) {
+  const PeerTable* pt = f.pt;
+  const int me = pt->rank;
+  FusedState* own = f.tab->state[me];
+  bool ok = true;
+  for (int t = threadIdx.x; t < tiles && ok; t += blockDim.x) {
+    ok = wait_geq(&own->done[t], f.seq, f.timeout_ticks, &pt->sig[me]->error, 0xC00);
+    if (!ok) report_host(pt, 0xC00);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+}
+
 static void w4_attr(const void* f) {
-  (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kLds4);
+  (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kLds4 + kLdsExtra);
 }
 
 void launch_gemm_nt_w4(const GemmArgs& g, hipStream_t stream) {
@@ -337,7 +521,7 @@ void launch_gemm_nt_w4(const GemmArgs& g, hipStream_t stream) {
     return hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0 ? n : 256;
   }();
   const int ntiles = ((g.M + WM - 1) / WM) * ((g.N + WNB - 1) / WNB);
-  W4Args a{g, g_w4_group_m};
+  W4Args a{g, g_w4_group_m, {}};
   const bool persist = g_w4_sched & 1;
   const int grid = persist ? std::min(ntiles, cus) : ntiles;
   static bool attr = [] {
@@ -349,11 +533,35 @@ void launch_gemm_nt_w4(const GemmArgs& g, hipStream_t stream) {
   }();
   (void)attr;
   switch (g_w4_sched & 3) {
-    case 0: hipLaunchKernelGGL((k_gemm_w4<0, 0>), dim3(grid), dim3(WNT), kLds4, stream, a); break;
-    case 1: hipLaunchKernelGGL((k_gemm_w4<1, 0>), dim3(grid), dim3(WNT), kLds4, stream, a); break;
-    case 2: hipLaunchKernelGGL((k_gemm_w4<0, 1>), dim3(grid), dim3(WNT), kLds4, stream, a); break;
-    default: hipLaunchKernelGGL((k_gemm_w4<1, 1>), dim3(grid), dim3(WNT), kLds4, stream, a); break;
+    case 0: hipLaunchKernelGGL((k_gemm_w4<0, 0>), dim3(grid), dim3(WNT), kLds4 + kLdsExtra, stream, a); break;
+    case 1: hipLaunchKernelGGL((k_gemm_w4<1, 0>), dim3(grid), dim3(WNT), kLds4 + kLdsExtra, stream, a); break;
+    case 2: hipLaunchKernelGGL((k_gemm_w4<0, 1>), dim3(grid), dim3(WNT), kLds4 + kLdsExtra, stream, a); break;
+    default: hipLaunchKernelGGL((k_gemm_w4<1, 1>), dim3(grid), dim3(WNT), kLds4 + kLdsExtra, stream, a); break;
   }
+}
+
+int gemm_w4_tiles(int M, int N) { return ((M + WM - 1) / WM) * ((N + WNB - 1) / WNB); }
+
+void launch_gemm_nt_w4_fused(const GemmArgs& g, const FusedArgs& f, hipStream_t stream) {
+  static int cus = [] {
+    int dev = 0, n = 0;
+    (void)hipGetDevice(&dev);
+    return hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0 ? n : 256;
+  }();
+  // one workgroup per tile (the persistent form spills registers with the fused epilogue)
+  static bool attr = [] {
+    w4_attr(reinterpret_cast<const void*>(k_gemm_w4<0, 0, 1>));
+    return true;
+  }();
+  (void)attr;
+  (void)cus;
+  const int ntiles = gemm_w4_tiles(g.M, g.N);
+  W4Args a{g, g_w4_group_m, f};
+  hipLaunchKernelGGL((k_gemm_w4<0, 0, 1>), dim3(ntiles), dim3(WNT), kLds4 + kLdsExtra, stream, a);
+}
+
+void launch_fused_wait(const FusedArgs& f, int tiles, hipStream_t stream) {
+  hipLaunchKernelGGL(k_fused_wait, dim3(1), dim3(256), 0, stream, f, tiles);
 }
 
 }  // namespace gemm

@@ -406,6 +406,53 @@ class DeviceGroup:
         self._inbox = self.empty(cap, self.torch.uint8)
         self.dc.set_inbox(self._inbox.data_ptr(), cap)
 
+    # ------------------------------------------- fused row-parallel GEMM + all-reduce
+    def _ensure_fused(self, tiles: int) -> None:
+        """Collective on first use / growth: the peer-mapped fused-GEMM state (tickets,
+        slot and done flags) and a symmetric inbox of ceil(tiles / p) * p bf16 tile slots."""
+        if self.dc.fused_inbox_bytes == 0 and not getattr(self, "_fused_connected", False):
+            h = bytes(self.dc.fused_alloc())
+            self.dc.fused_connect([bytes(x) for x in self.host.allgather(h)])
+            self._fused_connected = True
+        need = (tiles + self.size - 1) // self.size * self.size * (256 * 256 * 2)
+        if self.dc.fused_inbox_bytes >= need:
+            return
+        self.torch.cuda.synchronize(self.device)
+        self._fused_inbox = None  # back to the heap first (same order on every rank)
+        self._fused_inbox = self.empty(need, self.torch.uint8)
+        ptr = self._fused_inbox.data_ptr()
+        codes = self.host.allgather(int(self.dc.code_of(ptr, need)))
+        self.dc.set_fused_inbox(ptr, need, codes)
+
+    def gemm_allreduce(self, x, w, bias=None, out=None, alpha: float = 1.0):
+        """Row-parallel layer output: ``sum over the group of x_r @ w_r^T (+ bias)`` in bf16,
+        with the all-reduce fused into the GEMM (csrc/device/gemm_w4.hip): every output
+        tile's partials go straight from the GEMM epilogues into the tile owner's inbox,
+        and the last rank to finish the tile reduces it in rank order and writes it into
+        every rank's output.  x: [M, K_r] bf16, w: [N, K_r] bf16 (K_r % 64 == 0), bias: [N]
+        fp32 / bf16.  ``out`` (default: a symmetric-heap block) is registered on demand.
+        Collective: every rank calls with the same M, N."""
+        torch = self.torch
+        if x.dtype != torch.bfloat16 or w.dtype != torch.bfloat16 or x.dim() != 2 or w.dim() != 2:
+            raise TypeError("gemm_allreduce: x [M, K] and w [N, K] must be 2-D bf16")
+        M, K = x.shape
+        N = w.shape[0]
+        if w.shape[1] != K or x.stride(1) != 1 or w.stride(1) != 1:
+            raise ValueError("gemm_allreduce: shape mismatch or non K-contiguous operand")
+        tiles = ((M + 255) // 256) * ((N + 255) // 256)
+        self._ensure_fused(tiles)
+        if out is None:
+            out = self.empty((M, N), torch.bfloat16)
+        elif not self._register_call((out,)):  # collective: heap blocks pass through
+            raise ValueError("gemm_allreduce: out could not be registered")
+        bk, bp = 0, 0
+        if bias is not None:
+            bk = 1 if bias.dtype == torch.float32 else 2
+            bp = bias.data_ptr()
+        self.dc.gemm_rowpar(x.data_ptr(), w.data_ptr(), out.data_ptr(), bp, M, N, K, x.stride(0), w.stride(0),
+                            out.stride(0), float(alpha), bk, self._stream())
+        return out
+
     # -------------------------------------------------------------------- rccl
     def ensure_rccl(self) -> None:
         """Collective: create the RCCL communicator on first use."""

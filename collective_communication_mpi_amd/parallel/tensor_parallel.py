@@ -225,6 +225,47 @@ class _LinearFn(torch.autograd.Function):
         return dx, dw, db
 
 
+_TP_FUSED = os.environ.get("CCMPI_TP_FUSED", "1") != "0"
+
+
+def _fused_ok(x2: torch.Tensor, w: torch.Tensor, comm) -> bool:
+    """The row-parallel GEMM can carry its TP all-reduce in its epilogue (DeviceGroup.
+    gemm_allreduce): CUDA bf16, K shard % 64, N % 8, a group of more than one rank."""
+    if not (_TP_FUSED and x2.is_cuda and x2.dtype == torch.bfloat16 and w.dtype == torch.bfloat16):
+        return False
+    p, _ = _size_rank(comm)
+    return p > 1 and x2.shape[1] % 64 == 0 and w.shape[0] % 8 == 0 and x2.shape[0] > 0
+
+
+class _RowParallelFused(torch.autograd.Function):
+    """y = sum_r x_r W_r^T + b with the all-reduce fused into the GEMM (forward); the
+    backward is local, as for Megatron's "g" (identity gradient of the all-reduce)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, comm):
+        x2 = x.reshape(-1, x.shape[-1])
+        if not x2.is_contiguous():
+            x2 = x2.contiguous()
+        ctx.save_for_backward(x2, w)
+        ctx.has_bias = b is not None
+        ctx.lead = x.shape[:-1]
+        y = device_group_for(comm).gemm_allreduce(x2, w, bias=b)
+        return y.reshape(*x.shape[:-1], w.shape[0])
+
+    @staticmethod
+    def backward(ctx, g):
+        x2, w = ctx.saved_tensors
+        g2 = g.reshape(-1, g.shape[-1]).contiguous()
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = gemm_nt(g2, transpose(w)).reshape(*ctx.lead, w.shape[1])  # dX = dY . W
+        if ctx.needs_input_grad[1]:
+            dw = gemm_tn(g2, x2).to(w.dtype)                                 # dW = dY^T . X
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            db = g2.float().sum(0).to(g.dtype)
+        return dx, dw, db, None
+
+
 def _init_full(out_f: int, in_f: int, seed: int, dtype, bias: bool):
     """Full (unsharded) weights from a seeded CPU generator: identical on every rank."""
     gen = torch.Generator().manual_seed(seed)
@@ -283,6 +324,9 @@ class RowParallelLinear(torch.nn.Module):
     def forward(self, x):
         if not self.input_is_parallel:
             x = scatter_to_tensor_parallel_region(x, self.comm)
+        if _fused_ok(x.reshape(-1, x.shape[-1]), self.weight, self.comm):
+            # the TP all-reduce rides in the GEMM epilogue (tile-granular overlap)
+            return _RowParallelFused.apply(x, self.weight, self.bias, self.comm)
         y = reduce_from_tensor_parallel_region(_LinearFn.apply(x, self.weight, None), self.comm)
         return y + self.bias if self.bias is not None else y
 

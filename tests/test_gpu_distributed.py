@@ -34,6 +34,16 @@ def test_device_collectives_big(n, reg):
     assert "0 failures" in r.stdout
 
 
+@pytest.mark.parametrize("n", [2, 3, 4])
+def test_fused_rowparallel_gemm_allreduce(n):
+    """the TP all-reduce fused into the row-parallel GEMM (tile tickets,
+    last arrival reduces in rank order and writes every rank's output): vs fp32, bitwise
+    vs the unfused rank-order sum, identical on every rank, under rank skew, and through
+    RowParallelLinear forward + backward (tests/workers/fused_worker.py)."""
+    r = run_ranks(n, py("tests/workers/fused_worker.py"), timeout=400, env=ENV)
+    assert "fused OK" in r.stdout
+
+
 @pytest.mark.parametrize("n", [2, 3, 4, 8])
 def test_device_ondemand_registration(n):
     """ordinary torch tensors >= 1 MiB are registered on demand (IPC

@@ -1,0 +1,104 @@
+"""Fused row-parallel GEMM + TP all-reduce (DeviceGroup.gemm_allreduce) on p ranks.
+
+Every rank holds a K-shard x_r [M, K/p], w_r [N, K/p] (seeded per rank, so every rank
+regenerates all shards); the output must equal sum_r x_r w_r^T (+ bias):
+* against an fp32 reference of the whole product (bf16 tolerance);
+* bitwise against the unfused path on the same four-wave kernel (gemm_nt, then the
+  rank-order fan-out all-reduce of the bf16 partials), without bias;
+* identical on every rank (one reducer writes every rank's tile);
+* over repeated calls, changing shapes (edge tiles, tile counts) and random per-rank
+  delays (arrival order of the tile tickets);
+* RowParallelLinear forward/backward through the fused path vs the unfused layer.
+Prints "fused OK" on success."""
+import os
+import random
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", ".."))
+from collective_communication_mpi_amd import MPI, Communicator  # noqa: E402
+from collective_communication_mpi_amd import _native  # noqa: E402
+from collective_communication_mpi_amd.ops import gemm_nt  # noqa: E402
+
+comm = Communicator(MPI.COMM_WORLD)
+rank, p = comm.Get_rank(), comm.Get_size()
+dev = comm.dev
+D = dev.device
+fails = []
+
+
+def shard(r, rows, cols, salt):
+    g = torch.Generator(device=D).manual_seed(7919 * r + 104729 * salt + 1)
+    return (torch.rand(rows, cols, generator=g, device=D) * 2 - 1).bfloat16()
+
+
+rng = random.Random(31 + rank)
+for salt, (M, N, Kr, use_bias) in enumerate([(512, 768, 256, False), (300, 520, 128, True), (1024, 1024, 512, False),
+                                              (256, 256, 64, True), (777, 1032, 192, False), (2048, 4096, 1024, True)]):
+    xs = [shard(r, M, Kr, salt) for r in range(p)]
+    ws = [shard(r + 100, N, Kr, salt) for r in range(p)]
+    bias = (torch.rand(N, device=D, generator=torch.Generator(device=D).manual_seed(salt)) - 0.5) if use_bias else None
+    ref = sum(xs[r].float() @ ws[r].float().T for r in range(p))
+    if bias is not None:
+        ref = ref + bias
+    for rep in range(3):
+        if rng.random() < 0.5:
+            time.sleep(rng.random() * 0.02)  # host skew: ranks reach the kernel in random order
+        y = dev.gemm_allreduce(xs[rank], ws[rank], bias=bias)
+        torch.cuda.synchronize()
+        dev.check()
+        err = (y.float() - ref).abs().max().item()
+        tol = 0.02 * (Kr * p) ** 0.5 + 0.02
+        if err > tol:
+            fails.append(f"fused[{M}x{N}x{Kr},bias={use_bias},rep={rep}]: max err {err:.4f} > {tol:.4f}")
+        # identical on every rank
+        h = float(y.float().sum().item())
+        hs = comm.comm.allgather(h)
+        if any(x != hs[0] for x in hs):
+            fails.append(f"fused[{M}x{N}x{Kr}]: outputs differ between ranks {hs}")
+    if not use_bias:
+        # bitwise vs gemm_nt on the same kernel + rank-order fan-out all-reduce of the bf16 partials
+        D_ = _native.device()
+        D_.gemm_set_kernel(5)
+        part = gemm_nt(xs[rank], ws[rank])
+        D_.gemm_set_kernel(0)
+        unf = torch.empty_like(part)
+        dev.allreduce(part, unf, "SUM", "fanout")
+        torch.cuda.synchronize()
+        if not torch.equal(unf, y):
+            diff = (unf.float() - y.float()).abs().max().item()
+            fails.append(f"fused[{M}x{N}x{Kr}] != unfused rank-order sum (max diff {diff})")
+
+# RowParallelLinear through the fused path vs the unfused one (same weights)
+from collective_communication_mpi_amd.parallel import tensor_parallel as tp  # noqa: E402
+
+IN, OUT, T = 1024, 512, 384
+x_full = shard(999, T, IN, 77)
+layer = tp.RowParallelLinear(IN, OUT, comm, bias=True, input_is_parallel=False, device=D, dtype=torch.bfloat16, seed=5)
+xin = x_full.clone().requires_grad_(True)
+y = layer(xin)
+y.float().pow(2).sum().backward()
+gx_f, gw_f, gb_f = xin.grad.clone(), layer.weight.grad.clone(), layer.bias.grad.clone()
+tp._TP_FUSED = False
+layer.zero_grad()
+xin2 = x_full.clone().requires_grad_(True)
+y2 = layer(xin2)
+y2.float().pow(2).sum().backward()
+tp._TP_FUSED = True
+if (y.float() - y2.float()).abs().max().item() > 0.05:
+    fails.append(f"RowParallelLinear fused vs unfused forward: {(y.float() - y2.float()).abs().max().item()}")
+for name, a, b in (("dx", gx_f, xin2.grad), ("dw", gw_f, layer.weight.grad), ("db", gb_f, layer.bias.grad)):
+    rel = ((a.float() - b.float()).abs().max() / (b.float().abs().max() + 1e-6)).item()
+    if rel > 0.05:
+        fails.append(f"RowParallelLinear fused vs unfused {name}: rel err {rel}")
+
+torch.cuda.synchronize()
+dev.check()
+bad = comm.comm.allreduce(len(fails), op=MPI.SUM)
+if fails:
+    print(f"[rank {rank}] " + "\n".join(fails[:20]), flush=True)
+if rank == 0:
+    print("fused OK" if bad == 0 else f"fused FAILED ({bad})", flush=True)
+sys.exit(1 if bad else 0)
