@@ -77,6 +77,8 @@ def parse():
                     help="harness fc_o: per-token row-parallel (reference shape) or pooled")
     ap.add_argument("--dp-layers", type=int, default=32, help="Llama-3-8B layers of the DP-overlap measurement")
     ap.add_argument("--dp-tokens", type=int, default=4096)
+    ap.add_argument("--dp-vocab", type=int, default=1,
+                    help="DP overlap: include the LM head and token embedding gradients (Llama-3-8B: 16.06 GB total)")
     ap.add_argument("--a2a-mb", type=int, default=256)
     ap.add_argument("--shared-dry-run", type=int, default=8, help="N=1: ranks of the shared-GPU dry run (0 = off)")
     ap.add_argument("--no-harness", action="store_true")
@@ -474,6 +476,7 @@ def main() -> int:
         want = (torch.arange(world, device=dev.device, dtype=torch.float32) * world + rank).view(world, 1).expand(world, blk)
         a2a = {}
         for algo in ["direct", "push", "pairwise"]:
+            log(f"alltoall {algo}")
             try:
                 ya.zero_()
                 sync_barrier()
@@ -499,10 +502,11 @@ def main() -> int:
         if world > 1 and args.dp_layers > 0:
             from collective_communication_mpi_amd.parallel.overlap import dp_grad_overlap
 
+            log(f"dp overlap: {args.dp_layers} layers, vocab {bool(args.dp_vocab)}")
             try:
                 secondary["dp_overlap"] = dp_grad_overlap(
                     comm, layers=args.dp_layers, tokens=args.dp_tokens, iters=2,
-                    algo=best.split(":")[0])
+                    algo=best.split(":")[0], verbose=args.verbose, vocab=args.dp_vocab)
                 ok = 1
             except Exception as e:  # noqa: BLE001 - recorded in the JSON
                 secondary["dp_overlap"] = {"error": f"{type(e).__name__}: {e}"[:300]}
@@ -523,6 +527,7 @@ def main() -> int:
         # outputs (reference model/func_impl.py:94-109), so the TP all-reduce carries
         # B*S x 16 partial outputs every step
         mode = args.fc_o_mode
+        log(f"harness tp={tp} fc_o={mode}")
         try:
             harness = bench_forward(comm, tp=tp, batch=args.batch, steps=args.steps, warmup=args.warmup,
                                     fc_o_mode=mode)

@@ -1,6 +1,7 @@
 """Run one GEMM shape/kernel repeatedly (for rocprofv3 counter collection).
 
-    python benchmarks/gemm_one.py M N K MODE ITERS     (MODE: 0 auto, 1 128x128, 2 256x256, 3 256x128, -1 hipBLASLt)
+    python benchmarks/gemm_one.py M N K MODE ITERS     (MODE: 0 auto, 1 128x128, 2 256x256, 3 256x128,
+                                                       5 four-wave 256x256 (CCMPI_W4_SCHED), -1 hipBLASLt)
 """
 import os
 import sys
@@ -17,6 +18,8 @@ b = (torch.rand(N, K, device="cuda") * 2 - 1).bfloat16()
 c = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
 if mode >= 0:
     _native.device().gemm_set_kernel(mode)
+    if mode == 5 and os.environ.get("CCMPI_W4_SCHED"):
+        _native.device().gemm_set_w4_sched(int(os.environ["CCMPI_W4_SCHED"]))
 for _ in range(iters):
     if mode >= 0:
         gemm_nt(a, b, out=c)

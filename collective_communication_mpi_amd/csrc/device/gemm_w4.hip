@@ -223,8 +223,10 @@ __device__ void fused_epilogue(const W4Args& wa, int t, int bm, int bn, const fl
 
 // PERSIST: grid = min(tiles, CUs); workgroup b runs logical tiles s, s + G, s + 2G, ...
 // (s = XCD-aware remap of b) and prefetches the next tile's first K-tile during the
-// epilogue.  ORDER: MFMA-first issue order inside each fenced group.
-template <int PERSIST, int ORDER, int FUSED = 0>
+// epilogue.  ORDER: MFMA-first issue order inside each fenced group.  FRONT: the next
+// K-tile's 16 DMA pieces go out in the first half of phase X (4 per group) instead of
+// 2 per group over all of it, so each has ~3/4 of a K-tile to land before the barrier.
+template <int PERSIST, int ORDER, int FUSED = 0, int FRONT = 0>
 __global__ void __launch_bounds__(WNT, 1) k_gemm_w4(W4Args wa) {
   const GemmArgs& g = wa.g;
   extern __shared__ __attribute__((aligned(1024))) unsigned char smem[];
@@ -369,9 +371,16 @@ __global__ void __launch_bounds__(WNT, 1) k_gemm_w4(W4Args wa) {
       for (int i = 0; i < 8; ++i) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[i], b1[j], acc[i][j], 0, 0, 0);
-        stage_piece(buf ^ 1, skt, i);
+        if constexpr (FRONT) {
+          if (i < 4) {
+            stage_piece(buf ^ 1, skt, 2 * i);
+            stage_piece(buf ^ 1, skt, 2 * i + 1);
+          }
+        } else {
+          stage_piece(buf ^ 1, skt, i);
+        }
         rd2(buf, 0, i, a0, b0);
-        order_x();
+        if constexpr (!FRONT) order_x();
         __builtin_amdgcn_sched_barrier(0);
       }
 #pragma unroll
@@ -487,7 +496,7 @@ __global__ void __launch_bounds__(WNT, 1) k_gemm_w4(W4Args wa) {
 
 }  // namespace
 
-int g_w4_sched = 1;   // bit 0: persistent grid, bit 1: MFMA-first order inside groups
+int g_w4_sched = 1;   // bit 0: persistent grid, bit 1: MFMA-first order inside groups, bit 2: front-loaded DMA
 int g_w4_group_m = 8;
 
 bool gemm_w4_ok(const GemmArgs& g) {
@@ -529,9 +538,16 @@ void launch_gemm_nt_w4(const GemmArgs& g, hipStream_t stream) {
     w4_attr(reinterpret_cast<const void*>(k_gemm_w4<1, 0>));
     w4_attr(reinterpret_cast<const void*>(k_gemm_w4<0, 1>));
     w4_attr(reinterpret_cast<const void*>(k_gemm_w4<1, 1>));
+    w4_attr(reinterpret_cast<const void*>(k_gemm_w4<0, 0, 0, 1>));
+    w4_attr(reinterpret_cast<const void*>(k_gemm_w4<1, 0, 0, 1>));
     return true;
   }();
   (void)attr;
+  if (g_w4_sched & 4) {
+    if (persist) hipLaunchKernelGGL((k_gemm_w4<1, 0, 0, 1>), dim3(grid), dim3(WNT), kLds4 + kLdsExtra, stream, a);
+    else hipLaunchKernelGGL((k_gemm_w4<0, 0, 0, 1>), dim3(grid), dim3(WNT), kLds4 + kLdsExtra, stream, a);
+    return;
+  }
   switch (g_w4_sched & 3) {
     case 0: hipLaunchKernelGGL((k_gemm_w4<0, 0>), dim3(grid), dim3(WNT), kLds4 + kLdsExtra, stream, a); break;
     case 1: hipLaunchKernelGGL((k_gemm_w4<1, 0>), dim3(grid), dim3(WNT), kLds4 + kLdsExtra, stream, a); break;

@@ -2,12 +2,16 @@
 "DP8 gradient all-reduce, Llama-3-8B-sized grad (~16 GB bf16) overlapped with
 backward on 8xMI355X").
 
-A synthetic backward over ``layers`` Llama-3-8B decoder layers (d 4096, GQA
-kv 1024, MLP 14336; 218 M weights per layer, 32 layers = 7.0 B weights =
-14 GB of bf16 gradients): per layer the seven weight gradients
-dW = dY^T X are produced by the MFMA GEMM (``gemm_nt`` over the token axis,
-fp32 accumulate, bf16 out) straight into a flat bf16 gradient buffer on the
-symmetric heap.  As soon as a layer's GEMMs are queued, an event hands that
+A synthetic backward over the whole Llama-3-8B parameter set: the LM head
+(128256 x 4096), ``layers`` decoder layers (d 4096, GQA kv 1024, MLP 14336;
+218 M weights per layer) and the token embedding (128256 x 4096) -- 8.03 B
+weights = 16.06 GB of bf16 gradients at 32 layers, the "~16 GB" of the config.
+In backward order: the LM-head gradient dW = dLogits^T H first (the first
+bucket ready), then per layer the seven weight gradients dW = dY^T X, then the
+embedding gradient last (a row scatter-add of the first layer's input gradient
+over the token ids, the last bucket ready).  Every GEMM is the MFMA kernel
+(``gemm_nt`` over the token axis, fp32 accumulate, bf16 out) writing straight
+into one flat bf16 gradient buffer on the symmetric heap.  As soon as a layer's GEMMs are queued, an event hands that
 layer's slice (one bucket) to a side stream (normal priority: measured better
 than high priority, profiles/r2_overlap), which all-reduces it with the
 framework's device all-reduce (``overlap_blocks`` CTAs) while the next
@@ -27,7 +31,7 @@ import torch
 
 from ..ops import gemm_nt
 
-LLAMA3_8B = {"d": 4096, "kv": 1024, "ff": 14336}
+LLAMA3_8B = {"d": 4096, "kv": 1024, "ff": 14336, "vocab": 128256}
 
 
 def layer_weight_shapes(d: int, kv: int, ff: int) -> List[Tuple[int, int]]:
@@ -37,48 +41,78 @@ def layer_weight_shapes(d: int, kv: int, ff: int) -> List[Tuple[int, int]]:
 
 def dp_grad_overlap(comm, layers: int = 32, tokens: int = 4096, iters: int = 3, algo: str = "auto",
                     priority: int = 0, dims: Dict[str, int] = LLAMA3_8B, seed: int = 0, verbose: bool = False,
-                    max_blocks: int = 0, bucket_mb: int = 0) -> Dict:
+                    max_blocks: int = 0, bucket_mb: int = 0, vocab: bool = True) -> Dict:
     """``max_blocks``: CTA budget of the bucket all-reduces (0 = the group's
     ``overlap_blocks``, the budget for collectives that run beside compute).
     ``bucket_mb``: split each layer's gradient range into all-reduces of at most
     this many MiB, each launched once the layer's GEMMs are queued (0 = one
-    bucket per layer, 436 MB for Llama-3-8B)."""
+    bucket per layer, 436 MB for Llama-3-8B, and one each for the LM head and
+    the embedding, 1.05 GB).  ``vocab=False`` leaves the LM head and the
+    embedding out (decoder layers only)."""
     from .. import mpi as MPI
 
     dev = comm.dev
     hc = comm.comm
     p = comm.Get_size()
     d, kv, ff, T = dims["d"], dims["kv"], dims["ff"], tokens
+    V = dims.get("vocab", 0) if vocab else 0
     shapes = layer_weight_shapes(d, kv, ff)
     per_layer = sum(a * b for a, b in shapes)
-    grads = dev.empty(per_layer * layers, torch.bfloat16)  # bf16 grads, symmetric heap (zero-copy all-reduce)
+    emb = V * d  # LM head and token embedding: V x d each
+    # flat layout: [LM head | layer L-1 | ... | layer 0 | embedding] = backward order
+    n_total = per_layer * layers + 2 * emb
+    grads = dev.empty(n_total, torch.bfloat16)  # bf16 grads, symmetric heap (zero-copy all-reduce)
     g = torch.Generator(device=dev.device).manual_seed(seed + comm.Get_rank())
     x_t = {k: (torch.randn(k, T, generator=g, device=dev.device) * 0.05).bfloat16() for k in {d, ff}}
     dy_t = {k: (torch.randn(k, T, generator=g, device=dev.device) * 0.05).bfloat16() for k in {d, kv, ff}}
+    if V:
+        dlogits_t = (torch.randn(V, T, generator=g, device=dev.device) * 0.05).bfloat16()  # [vocab, tokens]
+        ids = torch.randint(0, V, (T,), generator=g, device=dev.device)
+        dx0 = (torch.randn(T, d, generator=g, device=dev.device) * 0.05).bfloat16()  # grad of the embedded tokens
     side = torch.cuda.Stream(device=dev.device, priority=priority)
     mb = max_blocks or dev.overlap_blocks
-    events = [torch.cuda.Event() for _ in range(layers)]
+    events = [torch.cuda.Event() for _ in range(layers + 2)]
     # bucket length in elements, a multiple of 8 (16-B aligned bf16 buckets)
-    step = per_layer if bucket_mb <= 0 else max(8, ((bucket_mb << 20) // 2) // 8 * 8)
+    step = None if bucket_mb <= 0 else max(8, ((bucket_mb << 20) // 2) // 8 * 8)
+
+    def reduce_range(ev, lo, hi) -> None:
+        ev.record()
+        side.wait_event(ev)
+        with torch.cuda.stream(side):
+            st = step or (hi - lo)
+            for a in range(lo, hi, st):
+                seg = grads[a:min(hi, a + st)]
+                dev.allreduce(seg, seg, "SUM", algo, max_blocks=mb)
 
     def backward(comm_on: bool, compute_on: bool = True) -> None:
-        for layer in reversed(range(layers)):
-            base = layer * per_layer
+        if V:  # LM head: the first gradient of the backward
+            if compute_on:
+                gemm_nt(dlogits_t, x_t[d], out=grads[:emb].view(V, d))
+            if comm_on:
+                reduce_range(events[layers], 0, emb)
+        for i, layer in enumerate(reversed(range(layers))):
+            base = emb + i * per_layer
             if compute_on:
                 o = base
                 for fo, fi in shapes:
                     gemm_nt(dy_t[fo], x_t[fi], out=grads[o:o + fo * fi].view(fo, fi))
                     o += fo * fi
             if comm_on:
-                events[layer].record()
-                side.wait_event(events[layer])
-                with torch.cuda.stream(side):
-                    for lo in range(0, per_layer, step):
-                        seg = grads[base + lo:base + min(per_layer, lo + step)]
-                        dev.allreduce(seg, seg, "SUM", algo, max_blocks=mb)
+                reduce_range(events[layer], base, base + per_layer)
+        if V:  # token embedding: the last gradient (row scatter-add over the token ids)
+            eg = grads[n_total - emb:].view(V, d)
+            if compute_on:
+                eg.zero_()
+                eg.index_add_(0, ids, dx0)
+            if comm_on:
+                reduce_range(events[layers + 1], n_total - emb, n_total)
         torch.cuda.current_stream().wait_stream(side)
 
     def timed(**kw) -> float:
+        if verbose and comm.Get_rank() == 0:
+            import sys
+
+            print(f"[dp_overlap] timing {kw} ...", file=sys.stderr, flush=True)
         backward(**kw)
         torch.cuda.synchronize()
         dev.check()
@@ -99,14 +133,15 @@ def dp_grad_overlap(comm, layers: int = 32, tokens: int = 4096, iters: int = 3, 
     t_both = timed(comm_on=True) if p > 1 else t_compute
     dev.check()
     hidden = None if p == 1 or t_comm == 0 else max(0.0, min(1.0, (t_compute + t_comm - t_both) / t_comm))
-    flops = 2 * T * per_layer * layers
-    gbytes = per_layer * layers * 2
+    flops = 2 * T * (per_layer * layers + emb)  # the embedding scatter-add is not a GEMM
+    gbytes = n_total * 2
     out = {"ranks": p, "layers": layers, "grad_bytes_bf16": gbytes, "tokens_per_rank": T,
            "compute_ms": round(t_compute * 1e3, 3), "comm_ms": round(t_comm * 1e3, 3),
            "overlapped_ms": round(t_both * 1e3, 3), "comm_hidden_fraction": None if hidden is None else round(hidden, 3),
            "wgrad_TFLOPs": round(flops / t_compute / 1e12, 1), "shared_gpu": dev.shared_device,
            "comm_algbw_GBps": round(gbytes / t_comm / 1e9, 2) if t_comm else None, "algo": algo,
-           "bucket_ctas": mb, "buckets": layers * ((per_layer + step - 1) // step),
-           "bucket_MiB": round(min(step, per_layer) * 2 / (1 << 20), 1)}
+           "bucket_ctas": mb, "params": n_total, "vocab": V,
+           "buckets": sum((n + (step or n) - 1) // (step or n) for n in [per_layer] * layers + ([emb, emb] if V else [])),
+           "bucket_MiB": round(min(step or per_layer, per_layer) * 2 / (1 << 20), 1)}
     del grads, x_t, dy_t
     return out

@@ -162,18 +162,17 @@ def scatter_to_tensor_parallel_region(x, comm):
 # the hand-written GEMMs co-run with them.
 _TP_GEMM = os.environ.get("CCMPI_TP_GEMM", "auto")
 _BLAS_MIN_MACS = 1 << 33
-_GPU_SHARED = None
 
 
-def _gpu_shared() -> bool:
-    global _GPU_SHARED
-    if _GPU_SHARED is None:
-        local = int(os.environ.get("CCMPI_LOCAL_SIZE", os.environ.get("LOCAL_WORLD_SIZE", "1")))
-        _GPU_SHARED = local > max(1, torch.cuda.device_count())
-    return _GPU_SHARED
+def _gpu_shared(comm) -> bool:
+    """Whether this TP group's ranks share a GPU: measured by the group itself (PCI bus
+    ids gathered over the ranks, DeviceGroup.shared_device), per group."""
+    if comm is None:
+        return False
+    return bool(device_group_for(comm).shared_device)
 
 
-def _mfma_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
+def _mfma_ok(x: torch.Tensor, w: torch.Tensor, comm=None) -> bool:
     if not (x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16
             and x.shape[-1] % 8 == 0 and w.shape[0] % 8 == 0 and w.shape[1] % 8 == 0):
         return False
@@ -181,34 +180,39 @@ def _mfma_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
         return True
     if _TP_GEMM == "blas":
         return False
-    return x.numel() * w.shape[0] < _BLAS_MIN_MACS or _gpu_shared()
+    return x.numel() * w.shape[0] < _BLAS_MIN_MACS or _gpu_shared(comm)
 
 
 class _LinearFn(torch.autograd.Function):
     """y = x W^T (+ b): MFMA bf16 kernels on CUDA bf16, torch.matmul otherwise."""
 
     @staticmethod
-    def forward(ctx, x, w, b):
+    def forward(ctx, x, w, b, comm=None):
         x2 = x.reshape(-1, x.shape[-1])
         if not x2.is_contiguous():
             x2 = x2.contiguous()
         ctx.save_for_backward(x2, w)
         ctx.has_bias = b is not None
         ctx.lead = x.shape[:-1]
-        if _mfma_ok(x2, w):
-            y = gemm_nt(x2, w, bias=b)
+        ctx.mfma = _mfma_ok(x2, w, comm)
+        # the output is allocated in its final shape and written through a 2-D view, so
+        # the returned tensor is no view: _ReduceFromTP may reduce it in place (mark_dirty)
+        y = torch.empty(*x.shape[:-1], w.shape[0], device=x.device, dtype=x.dtype)
+        y2 = y.view(-1, w.shape[0])
+        if ctx.mfma:
+            gemm_nt(x2, w, bias=b, out=y2)
         else:
-            y = x2 @ w.t()
+            torch.matmul(x2, w.t(), out=y2)
             if b is not None:
-                y = y + b
-        return y.reshape(*x.shape[:-1], w.shape[0])
+                y2 += b
+        return y
 
     @staticmethod
     def backward(ctx, g):
         x2, w = ctx.saved_tensors
         g2 = g.reshape(-1, g.shape[-1]).contiguous()
         dx = dw = db = None
-        if _mfma_ok(x2, w) and g2.dtype == torch.bfloat16:
+        if ctx.mfma and g2.dtype == torch.bfloat16:
             if ctx.needs_input_grad[0]:
                 dx = gemm_nt(g2, transpose(w))                      # dX = dY . W
             if ctx.needs_input_grad[1]:
@@ -222,7 +226,7 @@ class _LinearFn(torch.autograd.Function):
             db = g2.float().sum(0).to(g.dtype)
         if dx is not None:
             dx = dx.reshape(*ctx.lead, w.shape[1])
-        return dx, dw, db
+        return dx, dw, db, None
 
 
 _TP_FUSED = os.environ.get("CCMPI_TP_FUSED", "1") != "0"
@@ -297,7 +301,7 @@ class ColumnParallelLinear(torch.nn.Module):
 
     def forward(self, x):
         x = copy_to_tensor_parallel_region(x, self.comm)
-        y = _LinearFn.apply(x, self.weight, self.bias)
+        y = _LinearFn.apply(x, self.weight, self.bias, self.comm)
         return gather_from_tensor_parallel_region(y, self.comm) if self.gather_output else y
 
 
@@ -327,7 +331,7 @@ class RowParallelLinear(torch.nn.Module):
         if _fused_ok(x.reshape(-1, x.shape[-1]), self.weight, self.comm):
             # the TP all-reduce rides in the GEMM epilogue (tile-granular overlap)
             return _RowParallelFused.apply(x, self.weight, self.bias, self.comm)
-        y = reduce_from_tensor_parallel_region(_LinearFn.apply(x, self.weight, None), self.comm)
+        y = reduce_from_tensor_parallel_region(_LinearFn.apply(x, self.weight, None, self.comm), self.comm)
         return y + self.bias if self.bias is not None else y
 
 

@@ -1,18 +1,20 @@
 #!/usr/bin/env bash
-# PMC counters for the GEMM kernels (counter collection only: no tracing domains).
+# GEMM counters: rocprofv3 PMC passes (one run per pass) of gemm_one.py for each
+# MODE in $MODES (-1 = hipBLASLt, 5 = four-wave kernel with CCMPI_W4_SCHED) on $SHAPE.
 set -o pipefail
 cd "$(dirname "$0")/.."
-mkdir -p gpurun_out/pmc
 export TMPDIR=/tmp
-rocprofv3 -L > gpurun_out/pmc/avail.txt 2>&1 || true
-run() {  # name M N K MODE counters...
-  local name=$1; shift; local M=$1 N=$2 K=$3 MODE=$4; shift 4
-  timeout -k 10 120 rocprofv3 --kernel-trace --stats --pmc "$@" --output-format csv -d gpurun_out/pmc/$name -o out -- python3 benchmarks/gemm_one.py $M $N $K $MODE 10 > gpurun_out/pmc/$name.log 2>&1
-}
-C1="SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE"
-C2="SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_BF16 SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INST_CYCLES_VMEM"
-for shp in "k256_4096 4096 4096 4096 2" "k128_4096 4096 4096 4096 1" "blas_4096 4096 4096 4096 -1" "k128_qkv 32768 768 768 1" "blas_qkv 32768 768 768 -1"; do
-  set -- $shp
-  run ${1}_c1 $2 $3 $4 $5 $C1 && run ${1}_c2 $2 $3 $4 $5 $C2 || { echo "pmc run $1 failed rc=$?"; exit 1; }
+OUT=gpurun_out/gemm_pmc${TAG:+_$TAG}
+mkdir -p $OUT
+read M N K <<< "$(echo ${SHAPE:-4096x28672x4096} | tr x ' ')"
+P1="SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE"
+P2="SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_LDS SQ_INSTS_VMEM SQ_INSTS_VALU_MFMA_MOPS_BF16 SQ_INSTS_SALU SQ_ACTIVE_INST_VALU"
+for mode in ${MODES:--1 5}; do
+  timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace_m$mode -o out -- \
+    python3 benchmarks/gemm_one.py $M $N $K $mode 20 > $OUT/trace_m$mode.log 2>&1 || { echo "trace $mode failed"; exit 1; }
+  for pass in P1 P2; do
+    timeout -s KILL 90 rocprofv3 --pmc ${!pass} --output-format csv -d $OUT/pmc_m${mode}_$pass -o out -- \
+      python3 benchmarks/gemm_one.py $M $N $K $mode 10 > $OUT/pmc_m${mode}_$pass.log 2>&1 || { echo "pmc $mode $pass failed"; exit 1; }
+  done
 done
-echo pmc done
+echo gemm pmc done

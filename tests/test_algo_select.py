@@ -99,11 +99,12 @@ def test_tp_gemm_routing(monkeypatch):
     w_big = SimpleNamespace(dtype=torch.bfloat16, shape=(28672, 4096))
     w_small = SimpleNamespace(dtype=torch.bfloat16, shape=(256, 4096))
     monkeypatch.setattr(tpm, "_TP_GEMM", "auto")
-    monkeypatch.setattr(tpm, "_GPU_SHARED", False)
+    monkeypatch.setattr(tpm, "_gpu_shared", lambda comm: False)
     assert tpm._mfma_ok(x, w_small) and not tpm._mfma_ok(x, w_big)
-    monkeypatch.setattr(tpm, "_GPU_SHARED", True)
-    assert tpm._mfma_ok(x, w_big)
-    monkeypatch.setattr(tpm, "_GPU_SHARED", False)
+    # the sharing decision is the TP group's own (DeviceGroup.shared_device), per group
+    monkeypatch.setattr(tpm, "_gpu_shared", lambda comm: comm == "shared-group")
+    assert tpm._mfma_ok(x, w_big, "shared-group") and not tpm._mfma_ok(x, w_big, "other-group")
+    monkeypatch.setattr(tpm, "_gpu_shared", lambda comm: False)
     monkeypatch.setattr(tpm, "_TP_GEMM", "own")
     assert tpm._mfma_ok(x, w_big)
     monkeypatch.setattr(tpm, "_TP_GEMM", "blas")

@@ -202,7 +202,7 @@ def test_bench_multi_rank_path_shared_gpu():
 
     e = dict(os.environ, **ENV)
     r = subprocess.run([sys.executable, "bench.py", "--gpus", "4", "--steps", "3", "--warmup", "1", "--size-mb", "64",
-                        "--a2a-mb", "16", "--dp-layers", "1", "--dp-tokens", "1024", "--batch", "256"],
+                        "--a2a-mb", "16", "--dp-layers", "1", "--dp-tokens", "1024", "--dp-vocab", "0", "--batch", "256"],
                        cwd=REPO, env=e, capture_output=True, text=True, timeout=400)
     assert r.returncode == 0, r.stderr[-4000:]
     out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])

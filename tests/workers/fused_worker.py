@@ -74,7 +74,7 @@ for salt, (M, N, Kr, use_bias) in enumerate([(512, 768, 256, False), (300, 520, 
 # RowParallelLinear through the fused path vs the unfused one (same weights)
 from collective_communication_mpi_amd.parallel import tensor_parallel as tp  # noqa: E402
 
-IN, OUT, T = 1024, 512, 384
+IN, OUT, T = 256 * p, 512, 384  # every rank holds a K shard of 256 (the fused path needs K_r % 64 == 0)
 x_full = shard(999, T, IN, 77)
 layer = tp.RowParallelLinear(IN, OUT, comm, bias=True, input_is_parallel=False, device=D, dtype=torch.bfloat16, seed=5)
 xin = x_full.clone().requires_grad_(True)
