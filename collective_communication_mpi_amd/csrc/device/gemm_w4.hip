@@ -24,6 +24,7 @@
 // Epilogue: per wave, two 64-row halves staged through LDS as fp32, written
 // as whole 16-B row vectors (alpha, bias, activation, accumulate, fp32/bf16 out).
 #include <hip/hip_runtime.h>
+#include <type_traits>
 
 #include "gemm_common.hpp"
 
@@ -494,9 +495,215 @@ __global__ void __launch_bounds__(WNT, 1) k_gemm_w4(W4Args wa) {
   }
 }
 
+// ---------------------------------------------------------------------------------
+// Ring variant (profiles/r3_gemm_ring): the same 256x256 tile and 128x128 wave tiles,
+// but LDS is a ring of four 32-KiB slots, each one 32-deep K-step (A 256 x 64 B |
+// B 256 x 64 B).  A phase is one K-step: 64 MFMAs on the previous step's fragments,
+// 16 fragment reads of this step, and the 8 DMA pieces of the step THREE ahead (into
+// the slot read two phases ago), then a counted `s_waitcnt vmcnt(16)` (the next step
+// landed, the two after it still in flight) + lgkmcnt(0) + a raw s_barrier.  The
+// two-stage kernel above waits vmcnt(0) at every barrier, so the DMA of a K-tile has
+// one phase to land; PMC counters of it against hipBLASLt on the same shape showed 6x
+// the wave wait cycles at equal instruction counts (profiles/r3_gemm_pmc).
+//
+// 64-B rows: 16-B chunk c of row r sits at physical chunk c ^ f((r >> 2) & 3),
+// f = {0, 2, 3, 1}: conflict-free for the 16x16x32 fragment reads (ds_read_b128 lane
+// groups {0-3,12-15,20-27}, {4-11,16-19,28-31}, ... each cover the 16 slots of a
+// 256-B bank row).  The DMA keeps LDS lane-linear and permutes the source chunk.
+constexpr int kRing = 32768;   // one ring slot
+constexpr int kRingHalf = 16384;
+__device__ __forceinline__ int ring_swz(int q) { return (0x78 >> (2 * q)) & 3; }
+
+__device__ __forceinline__ void wait_barrier_ring(int later) {
+  // `later` DMA steps (8 pieces each) may stay in flight past this barrier
+  if (later >= 2) asm volatile("s_waitcnt vmcnt(16) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  else if (later == 1) asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+template <int PRIO>
+__global__ void __launch_bounds__(WNT, 1) k_gemm_w4r(W4Args wa) {
+  const GemmArgs& g = wa.g;
+  extern __shared__ __attribute__((aligned(1024))) unsigned char smem[];
+  const int tiles_n = (g.N + WNB - 1) / WNB, tiles_m = (g.M + WM - 1) / WM;
+  const int lt = xcd_remap(blockIdx.x, gridDim.x);
+  if (lt >= tiles_n * tiles_m) return;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wave >> 1, wc = wave & 1;
+  const int nst = g.K / 32;
+  int tm, tn;
+  tile_coords(lt, tiles_m, tiles_n, wa.group_m, tm, tn);
+  const int bm = tm * WM, bn = tn * WNB;
+  const __amdgpu_buffer_rsrc_t ra = op_rsrc(g.A + (size_t)bm * g.lda, (long)g.M - bm, g.lda);
+  const __amdgpu_buffer_rsrc_t rb = op_rsrc(g.B + (size_t)bn * g.ldb, (long)g.N - bn, g.ldb);
+
+  // DMA piece i of a step: 16 rows x 64 B; wave w covers rows (4 i + w) * 16 ..
+  // lane l: row + (l >> 2), physical chunk l & 3 <- logical chunk (l & 3) ^ f((l >> 4) & 3)
+  const int drow = wave * 16 + (lane >> 2);
+  const int dchunk = ((lane & 3) ^ ring_swz((lane >> 4) & 3)) << 4;
+  const int va = drow * g.lda * 2 + dchunk, vb = drow * g.ldb * 2 + dchunk;
+  auto dma = [&](int s, int i) {
+    int sa_ = 64 * g.lda * 2, sb_ = 64 * g.ldb * 2;
+    asm volatile("" : "+s"(sa_), "+s"(sb_));
+    unsigned char* base = smem + (s & 3) * kRing + wave * 1024;
+    const int k0 = s * 64;
+    if (i < 4)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_vptr)(base + i * 4096), 16, va, k0 + i * sa_, 0, 0);
+    else
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_vptr)(base + kRingHalf + (i - 4) * 4096), 16, vb,
+                                               k0 + (i - 4) * sb_, 0, 0);
+  };
+  // fragment (16x16x32): lane l reads row (l & 15) of a 16-row block, logical chunk l >> 4;
+  // the physical chunk depends on the lane only (block rows are multiples of 16)
+  const int rdo = (lane & 15) * 64 + (((lane >> 4) ^ ring_swz((lane >> 2) & 3)) << 4);
+  // group grp (0..7) of a phase reads B blocks 2 grp, 2 grp + 1 (grp < 4), then A blocks
+  auto rd2 = [&](int s, int grp, bf16x8 (&fa)[8], bf16x8 (&fb)[8]) {
+    const unsigned char* base = smem + (s & 3) * kRing + (grp < 4 ? kRingHalf : 0) + rdo;
+    const int r0 = (grp < 4 ? wc : wr) * 128 + (grp & 3) * 32;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const bf16x8 v = *reinterpret_cast<const bf16x8*>(base + (r0 + u * 16) * 64);
+      if (grp < 4) fb[(grp & 3) * 2 + u] = v;
+      else fa[(grp & 3) * 2 + u] = v;
+    }
+  };
+
+  floatx4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 a0[8], b0[8], a1[8], b1[8];
+
+  // one phase: MFMAs on (pa, pb) = step q-1, reads of step q into (ca, cb), DMA of step
+  // q+3 (DMA), then the barrier with LATER steps still in flight (branch-free body)
+  auto phase = [&](auto dma_c, auto later_c, int q, const bf16x8 (&pa)[8], const bf16x8 (&pb)[8],
+                   bf16x8 (&ca)[8], bf16x8 (&cb)[8]) {
+    constexpr bool DMA = decltype(dma_c)::value;
+    constexpr int LATER = decltype(later_c)::value;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa[i], pb[j], acc[i][j], 0, 0, 0);
+      if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
+      rd2(q, i, ca, cb);
+      if constexpr (DMA) dma(q + 3, i);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    wait_barrier_ring(LATER);
+  };
+  using T = std::true_type;
+  using F = std::false_type;
+  using L2 = std::integral_constant<int, 2>;
+  using L1 = std::integral_constant<int, 1>;
+  using L0 = std::integral_constant<int, 0>;
+
+  // prologue: steps 0..2 in flight (nst is even: 2 or >= 4), step 0 landed; then
+  // "phase 0": step 0's fragments read, step 3 into the last free slot, step 1 landed
+  const int pro = min(nst, 3);
+  for (int s = 0; s < pro; ++s)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) dma(s, i);
+  wait_barrier_ring(pro - 1);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    rd2(0, i, a0, b0);
+    if (nst >= 4) dma(3, i);
+  }
+  wait_barrier_ring(nst >= 4 ? 2 : 0);
+  // steady state: phases 1 .. nst-4 in pairs, each prefetching the step three ahead
+  for (int q = 1; q + 3 < nst; q += 2) {
+    phase(T{}, L2{}, q, a0, b0, a1, b1);
+    phase(T{}, L2{}, q + 1, a1, b1, a0, b0);
+  }
+  if (nst >= 4) {  // drain: phases nst-3, nst-2, nst-1
+    phase(F{}, L1{}, nst - 3, a0, b0, a1, b1);
+    phase(F{}, L0{}, nst - 2, a1, b1, a0, b0);
+  }
+  phase(F{}, L0{}, nst - 1, a0, b0, a1, b1);
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[i], b1[j], acc[i][j], 0, 0, 0);
+
+  // ---- epilogue (the ring is idle: the last barrier saw every read and DMA retire)
+  float* tile = reinterpret_cast<float*>(smem + wave * kEpiWave);
+  const int cl = (lane & 15) * 8;
+  const int col = bn + wc * 128 + cl;
+  float bias[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) bias[q] = load_bias(g, col + q, 0);
+  const int es = g.out_bf16 ? 2 : 4;
+  const bool vec_ok = (((uint64_t)g.C | ((uint64_t)g.ldc * es)) % 16) == 0 && g.N % 8 == 0;
+#pragma unroll
+  for (int h = 0; h < 4; ++h) {
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          tile[(i * 16 + (lane >> 4) * 4 + r) * kEpiTS + j * 16 + (lane & 15)] = acc[h * 2 + i][j][r];
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll 1
+    for (int it = 0; it < 8; ++it) {
+      const int rl = it * 4 + (lane >> 4);
+      const int row = bm + wr * 128 + h * 32 + rl;
+      if (row >= g.M || col >= g.N) continue;
+      float v[8];
+      const float4 x0 = *reinterpret_cast<const float4*>(tile + rl * kEpiTS + cl);
+      const float4 x1 = *reinterpret_cast<const float4*>(tile + rl * kEpiTS + cl + 4);
+      v[0] = x0.x; v[1] = x0.y; v[2] = x0.z; v[3] = x0.w; v[4] = x1.x; v[5] = x1.y; v[6] = x1.z; v[7] = x1.w;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v[q] = epi(g, v[q], bias[q]);
+      if (vec_ok) {
+        if (g.out_bf16) {
+          uint16_t* C = reinterpret_cast<uint16_t*>(g.C) + (size_t)row * g.ldc + col;
+          if (g.accumulate) {
+            const uint4 o = *reinterpret_cast<const uint4*>(C);
+            const uint32_t ow[4] = {o.x, o.y, o.z, o.w};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) { v[2 * q] += bf16_lo(ow[q]); v[2 * q + 1] += bf16_hi(ow[q]); }
+          }
+          uint32_t w[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) w[q] = f32_to_bf16_bits(v[2 * q]) | (f32_to_bf16_bits(v[2 * q + 1]) << 16);
+          *reinterpret_cast<uint4*>(C) = uint4{w[0], w[1], w[2], w[3]};
+        } else {
+          float* C = reinterpret_cast<float*>(g.C) + (size_t)row * g.ldc + col;
+          float4 y0 = make_float4(v[0], v[1], v[2], v[3]), y1 = make_float4(v[4], v[5], v[6], v[7]);
+          if (g.accumulate) {
+            const float4 o0 = *reinterpret_cast<const float4*>(C), o1 = *reinterpret_cast<const float4*>(C + 4);
+            y0.x += o0.x; y0.y += o0.y; y0.z += o0.z; y0.w += o0.w;
+            y1.x += o1.x; y1.y += o1.y; y1.z += o1.z; y1.w += o1.w;
+          }
+          *reinterpret_cast<float4*>(C) = y0;
+          *reinterpret_cast<float4*>(C + 4) = y1;
+        }
+      } else {
+        for (int q = 0; q < 8 && col + q < g.N; ++q) {
+          const size_t o = (size_t)row * g.ldc + col + q;
+          if (g.out_bf16) {
+            uint16_t* C = reinterpret_cast<uint16_t*>(g.C);
+            C[o] = (uint16_t)f32_to_bf16_bits(v[q] + (g.accumulate ? bf2f(C[o]) : 0.f));
+          } else {
+            float* C = reinterpret_cast<float*>(g.C);
+            C[o] = v[q] + (g.accumulate ? C[o] : 0.f);
+          }
+        }
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
 }  // namespace
 
-int g_w4_sched = 1;   // bit 0: persistent grid, bit 1: MFMA-first order inside groups, bit 2: front-loaded DMA
+int g_w4_sched = 1;   // bit 0: persistent grid, bit 1: MFMA-first order inside groups, bit 2: front-loaded DMA,
+                      // bit 3: ring kernel (k_gemm_w4r; bit 4 with s_setprio around the MFMA groups)
 int g_w4_group_m = 8;
 
 bool gemm_w4_ok(const GemmArgs& g) {
@@ -543,6 +750,19 @@ void launch_gemm_nt_w4(const GemmArgs& g, hipStream_t stream) {
     return true;
   }();
   (void)attr;
+  if (g_w4_sched & 8) {
+    static bool rattr = [] {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_gemm_w4r<0>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 4 * kRing);
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_gemm_w4r<1>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 4 * kRing);
+      return true;
+    }();
+    (void)rattr;
+    if (g_w4_sched & 16) hipLaunchKernelGGL(k_gemm_w4r<1>, dim3(ntiles), dim3(WNT), 4 * kRing, stream, a);
+    else hipLaunchKernelGGL(k_gemm_w4r<0>, dim3(ntiles), dim3(WNT), 4 * kRing, stream, a);
+    return;
+  }
   if (g_w4_sched & 4) {
     if (persist) hipLaunchKernelGGL((k_gemm_w4<1, 0, 0, 1>), dim3(grid), dim3(WNT), kLds4 + kLdsExtra, stream, a);
     else hipLaunchKernelGGL((k_gemm_w4<0, 0, 0, 1>), dim3(grid), dim3(WNT), kLds4 + kLdsExtra, stream, a);

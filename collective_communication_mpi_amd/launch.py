@@ -134,7 +134,10 @@ def launch(n: int, cmd: List[str], timeout: Optional[float] = None, env_extra=No
             except subprocess.TimeoutExpired:
                 pass
         for s, h in old.items():
-            signal.signal(s, h)
+            # a handler installed outside Python (e.g. by a profiler's preloaded library)
+            # reads back as None and cannot be reinstalled from here
+            if h is not None:
+                signal.signal(s, h)
     return rc
 
 

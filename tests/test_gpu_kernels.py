@@ -80,6 +80,39 @@ def test_gemm256_epilogue(gemm256, act):
     torch.testing.assert_close(c, c0 + _ref(a, b), rtol=2e-3, atol=5e-2)
 
 
+@pytest.mark.parametrize("sched", [0, 1, 3, 4, 5, 24], ids=["w4", "w4p", "w4po", "w4f", "w4pf", "ring"])
+@pytest.mark.parametrize("M,N,K", [(256, 256, 64), (256, 256, 128), (300, 520, 256), (777, 1000, 512),
+                                   (2048, 2048, 4096), (1, 8, 192), (4096, 768, 768)])
+def test_gemm_w4_shapes(sched, M, N, K):
+    """Four-wave 256x256 kernels (gemm_w4.hip), every schedule variant incl. the LDS ring,
+    against an fp32 reference; bias + bf16 out and accumulate on one shape."""
+    from collective_communication_mpi_amd import _native
+    from collective_communication_mpi_amd.ops import gemm_nt
+
+    D = _native.device()
+    D.gemm_set_kernel(5)
+    D.gemm_set_w4_sched(sched)
+    try:
+        g = torch.Generator(device="cuda").manual_seed(M * 3 + N * 7 + K + sched)
+        a = torch.randn(M, K, device="cuda", generator=g).bfloat16()
+        b = torch.randn(N, K, device="cuda", generator=g).bfloat16()
+        y = gemm_nt(a, b, out_dtype=torch.float32)
+        torch.testing.assert_close(y, _ref(a, b), rtol=2e-3, atol=2e-3 * K ** 0.5)
+        for _ in range(2):
+            torch.testing.assert_close(gemm_nt(a, b, out_dtype=torch.float32), y, rtol=0, atol=0)
+        if M == 300:
+            bias = torch.randn(N, device="cuda").bfloat16()
+            yb = gemm_nt(a, b, bias=bias, alpha=0.5)
+            torch.testing.assert_close(yb.float(), _ref(a, b, bias, None, 0.5), rtol=2e-2, atol=8e-2)
+            c = torch.randn(M, N, device="cuda")
+            c0 = c.clone()
+            gemm_nt(a, b, out=c, accumulate=True)
+            torch.testing.assert_close(c, c0 + _ref(a, b), rtol=2e-3, atol=5e-2)
+    finally:
+        D.gemm_set_kernel(0)
+        D.gemm_set_w4_sched(1)
+
+
 def test_gemm_asymmetric_identity():
     """A = I with an asymmetric B catches a transposed C write (guide §3)."""
     from collective_communication_mpi_amd.ops import gemm_nt
