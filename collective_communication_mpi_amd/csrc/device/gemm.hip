@@ -1071,6 +1071,8 @@ void register_gemm_ops(pybind11::module_& m) {
         "gemm_nt tile choice: 0 auto, 1 128x128, 2 256x256, 3 256x128, 4 256x192, 5 256x256 four-wave");
   m.def("gemm_set_w4_sched", [](int v) { g_w4_sched = v; },
         "four-wave kernel variant (benchmarks): bit 0 persistent grid, bit 1 MFMA-first group order");
+  m.def("gemm_set_w4_debug", [](uint64_t p) { g_w4_dbg = reinterpret_cast<unsigned long long*>(p); },
+        "four-wave ring STAMP diagnostic: device buffer of 4 uint64 per wave (benchmarks only)");
   m.def("gemm_set_w4_group_m", [](int v) { g_w4_group_m = v > 0 ? v : 8; }, "four-wave kernel group-M rows");
   m.def("gemm_set_ablation", [](int e) {
     g_pp_exp = e;

@@ -51,6 +51,7 @@ struct W4Args {
   GemmArgs g;
   int group_m;  // tile rows per group of the group-M order
   FusedArgs f;  // FUSED only
+  unsigned long long* dbg;  // STAMP diagnostic builds only: 4 cycle counts per wave
 };
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t op_rsrc(const uint16_t* base, long rows, int ld) {
@@ -71,6 +72,14 @@ __device__ __forceinline__ void tile_coords(int wg, int tiles_m, int tiles_n, in
 
 __device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {
   return f32_to_bf16_bits(a) | (f32_to_bf16_bits(b) << 16);
+}
+
+// two floats -> packed bf16 (RNE, NaN kept) in one v_cvt_pk_bf16_f32
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+typedef float float2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t cvt_pk_bf16(float a, float b) {
+  const bf16x2_t h = __builtin_convertvector(float2_t{a, b}, bf16x2_t);
+  return __builtin_bit_cast(uint32_t, h);
 }
 
 // Fused TP all-reduce epilogue (FusedState comment in gemm_common.hpp).  `to_slab(h)`
@@ -496,15 +505,23 @@ __global__ void __launch_bounds__(WNT, 1) k_gemm_w4(W4Args wa) {
 }
 
 // ---------------------------------------------------------------------------------
-// Ring variant (profiles/r3_gemm_ring): the same 256x256 tile and 128x128 wave tiles,
-// but LDS is a ring of four 32-KiB slots, each one 32-deep K-step (A 256 x 64 B |
-// B 256 x 64 B).  A phase is one K-step: 64 MFMAs on the previous step's fragments,
-// 16 fragment reads of this step, and the 8 DMA pieces of the step THREE ahead (into
-// the slot read two phases ago), then a counted `s_waitcnt vmcnt(16)` (the next step
-// landed, the two after it still in flight) + lgkmcnt(0) + a raw s_barrier.  The
-// two-stage kernel above waits vmcnt(0) at every barrier, so the DMA of a K-tile has
-// one phase to land; PMC counters of it against hipBLASLt on the same shape showed 6x
-// the wave wait cycles at equal instruction counts (profiles/r3_gemm_pmc).
+// Ring kernel (profiles/r3_gemm): the same 256x256 tile and 128x128 wave tiles, but LDS
+// is a ring of four 32-KiB slots, each one 32-deep K-step (A 256 x 64 B | B 256 x 64 B).
+// A phase is one K-step: 64 MFMAs on the previous step's fragments with the 16 fragment
+// reads of this step and the 8 DMA pieces of the step THREE ahead (into the slot read
+// two phases ago) hand-interleaved one per MFMA gap, then a counted `s_waitcnt
+// vmcnt(16)` (the next step landed, the two after it still in flight) + lgkmcnt(0) +
+// a raw s_barrier.
+//
+// The MFMA takes B's fragment as its A operand (D = B_blk . A_blk^T), so a lane's four
+// accumulator values are four CONSECUTIVE output columns of one row: the fast epilogue
+// packs them to bf16 (8 B, v_cvt_pk_bf16_f32 + ds_write_b64) into a 32-row slab in slot 3
+// and reads back whole 16-B row vectors for the global stores.  PERSIST: grid =
+// min(tiles, CUs); after its epilogue a workgroup puts the next tile's first three
+// K-steps in flight (slots 0..2) while its stores drain.
+//
+// In-kernel s_memtime stamps of the previous form (profiles/r3_gemm/stamps.md): 1320-
+// 1400 cycles per 1024-MFMA-cycle phase and a 65k-cycle generic epilogue per tile.
 //
 // 64-B rows: 16-B chunk c of row r sits at physical chunk c ^ f((r >> 2) & 3),
 // f = {0, 2, 3, 1}: conflict-free for the 16x16x32 fragment reads (ds_read_b128 lane
@@ -512,199 +529,328 @@ __global__ void __launch_bounds__(WNT, 1) k_gemm_w4(W4Args wa) {
 // 256-B bank row).  The DMA keeps LDS lane-linear and permutes the source chunk.
 constexpr int kRing = 32768;   // one ring slot
 constexpr int kRingHalf = 16384;
+constexpr int kRingLds = 4 * kRing;
 __device__ __forceinline__ int ring_swz(int q) { return (0x78 >> (2 * q)) & 3; }
 
-__device__ __forceinline__ void wait_barrier_ring(int later) {
-  // `later` DMA steps (8 pieces each) may stay in flight past this barrier
-  if (later >= 2) asm volatile("s_waitcnt vmcnt(16) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-  else if (later == 1) asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+// `younger` vector-memory ops (DMA pieces / epilogue stores) may stay in flight past
+// this barrier; every LDS op of the wave has retired
+__device__ __forceinline__ void ring_wait_barrier(int younger) {
+  switch (younger) {
+    case 48: asm volatile("s_waitcnt vmcnt(48) lgkmcnt(0)\n\ts_barrier" ::: "memory"); break;
+    case 40: asm volatile("s_waitcnt vmcnt(40) lgkmcnt(0)\n\ts_barrier" ::: "memory"); break;
+    case 32: asm volatile("s_waitcnt vmcnt(32) lgkmcnt(0)\n\ts_barrier" ::: "memory"); break;
+    case 16: asm volatile("s_waitcnt vmcnt(16) lgkmcnt(0)\n\ts_barrier" ::: "memory"); break;
+    case 8: asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)\n\ts_barrier" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory"); break;
+  }
+}
+template <int YOUNGER>
+__device__ __forceinline__ void ring_wait_barrier_c() {
+  if constexpr (YOUNGER == 16) asm volatile("s_waitcnt vmcnt(16) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  else if constexpr (YOUNGER == 8) asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)\n\ts_barrier" ::: "memory");
   else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
-template <int PRIO>
+// one K-step's DMA: slot base + this wave's 1 KiB, per-lane byte offsets incl. the K offset
+// (a local struct in the kernel template made hipcc drop the host launch stubs)
+struct DmaStep {
+  unsigned char* lds;
+  int va, vb;
+};
+
+// EPI 1: bf16 out, C = alpha * AB^T, no bias / activation / accumulate (fast epilogue,
+// exactly 32 store instructions per wave and tile); EPI 0: the generic epilogue.
+// ABL (diagnostic ablations, wrong results): bit 0 drops the steady-state DMA, bit 1 the
+// steady-state fragment reads.  STAMP (diagnostic): per wave, s_memtime cycles of the
+// prologue, main loop, epilogue and the phase-end waits -> wa.dbg (first tile only).
+template <int EPI, int PERSIST, int ABL = 0, int STAMP = 0>
 __global__ void __launch_bounds__(WNT, 1) k_gemm_w4r(W4Args wa) {
   const GemmArgs& g = wa.g;
   extern __shared__ __attribute__((aligned(1024))) unsigned char smem[];
   const int tiles_n = (g.N + WNB - 1) / WNB, tiles_m = (g.M + WM - 1) / WM;
-  const int lt = xcd_remap(blockIdx.x, gridDim.x);
-  if (lt >= tiles_n * tiles_m) return;
+  const int ntiles = tiles_n * tiles_m;
+  int lt = xcd_remap(blockIdx.x, gridDim.x);
+  if (lt >= ntiles) return;
+  const unsigned long long t_start = STAMP ? __builtin_amdgcn_s_memtime() : 0;
+  unsigned long long t_wait = 0, t_loop = 0, t_epi = 0;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wr = wave >> 1, wc = wave & 1;
   const int nst = g.K / 32;
+  const int pro = min(nst, 3);  // nst is even: 2 or >= 4
   int tm, tn;
   tile_coords(lt, tiles_m, tiles_n, wa.group_m, tm, tn);
-  const int bm = tm * WM, bn = tn * WNB;
-  const __amdgpu_buffer_rsrc_t ra = op_rsrc(g.A + (size_t)bm * g.lda, (long)g.M - bm, g.lda);
-  const __amdgpu_buffer_rsrc_t rb = op_rsrc(g.B + (size_t)bn * g.ldb, (long)g.N - bn, g.ldb);
+  __amdgpu_buffer_rsrc_t ra, rb;
+  auto ops_for = [&](int tm_, int tn_) {
+    ra = op_rsrc(g.A + (size_t)tm_ * WM * g.lda, (long)g.M - tm_ * WM, g.lda);
+    rb = op_rsrc(g.B + (size_t)tn_ * WNB * g.ldb, (long)g.N - tn_ * WNB, g.ldb);
+  };
+  ops_for(tm, tn);
 
   // DMA piece i of a step: 16 rows x 64 B; wave w covers rows (4 i + w) * 16 ..
   // lane l: row + (l >> 2), physical chunk l & 3 <- logical chunk (l & 3) ^ f((l >> 4) & 3)
   const int drow = wave * 16 + (lane >> 2);
   const int dchunk = ((lane & 3) ^ ring_swz((lane >> 4) & 3)) << 4;
   const int va = drow * g.lda * 2 + dchunk, vb = drow * g.ldb * 2 + dchunk;
-  auto dma = [&](int s, int i) {
-    int sa_ = 64 * g.lda * 2, sb_ = 64 * g.ldb * 2;
-    asm volatile("" : "+s"(sa_), "+s"(sb_));
-    unsigned char* base = smem + (s & 3) * kRing + wave * 1024;
-    const int k0 = s * 64;
-    if (i < 4)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_vptr)(base + i * 4096), 16, va, k0 + i * sa_, 0, 0);
-    else
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_vptr)(base + kRingHalf + (i - 4) * 4096), 16, vb,
-                                               k0 + (i - 4) * sb_, 0, 0);
+  // piece offsets i * 64 rows: loop-invariant SGPRs (the K offset rides in the VGPR
+  // offset, the slot in M0), so a DMA piece costs one M0 write and the load itself
+  const int sa1 = 64 * g.lda * 2, sb1 = 64 * g.ldb * 2;
+  const int sa2 = 2 * sa1, sa3 = 3 * sa1, sb2 = 2 * sb1, sb3 = 3 * sb1;
+  auto dma_step = [&](int s) {
+    return DmaStep{smem + (s & 3) * kRing + wave * 1024, va + s * 64, vb + s * 64};
   };
+  auto dma_piece = [&](const DmaStep& d, int i) {
+    if (i < 4) {
+      const int so = i == 0 ? 0 : i == 1 ? sa1 : i == 2 ? sa2 : sa3;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_vptr)(d.lds + i * 4096), 16, d.va, so, 0, 0);
+    } else {
+      const int so = i == 4 ? 0 : i == 5 ? sb1 : i == 6 ? sb2 : sb3;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_vptr)(d.lds + kRingHalf + (i - 4) * 4096), 16, d.vb, so,
+                                               0, 0);
+    }
+  };
+  auto dma = [&](int s, int i) { dma_piece(dma_step(s), i); };
   // fragment (16x16x32): lane l reads row (l & 15) of a 16-row block, logical chunk l >> 4;
   // the physical chunk depends on the lane only (block rows are multiples of 16)
   const int rdo = (lane & 15) * 64 + (((lane >> 4) ^ ring_swz((lane >> 2) & 3)) << 4);
-  // group grp (0..7) of a phase reads B blocks 2 grp, 2 grp + 1 (grp < 4), then A blocks
-  auto rd2 = [&](int s, int grp, bf16x8 (&fa)[8], bf16x8 (&fb)[8]) {
+  // read u (0, 1) of group grp (0..7): B blocks 2 grp + u (grp < 4), then A blocks
+  auto rd1 = [&](int s, int grp, int u, bf16x8 (&fa)[8], bf16x8 (&fb)[8]) {
     const unsigned char* base = smem + (s & 3) * kRing + (grp < 4 ? kRingHalf : 0) + rdo;
     const int r0 = (grp < 4 ? wc : wr) * 128 + (grp & 3) * 32;
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const bf16x8 v = *reinterpret_cast<const bf16x8*>(base + (r0 + u * 16) * 64);
-      if (grp < 4) fb[(grp & 3) * 2 + u] = v;
-      else fa[(grp & 3) * 2 + u] = v;
-    }
+    const bf16x8 v = *reinterpret_cast<const bf16x8*>(base + (r0 + u * 16) * 64);
+    if (grp < 4) fb[(grp & 3) * 2 + u] = v;
+    else fa[(grp & 3) * 2 + u] = v;
   };
 
   floatx4 acc[8][8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
   bf16x8 a0[8], b0[8], a1[8], b1[8];
+  // acc[i][j] (A block i, B block j): lane l holds C[16 i + (l & 15)][16 j + 4 (l >> 4) + r]
+  auto mfma = [&](int i, int j, const bf16x8& fa, const bf16x8& fb) {
+    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb, fa, acc[i][j], 0, 0, 0);
+  };
 
   // one phase: MFMAs on (pa, pb) = step q-1, reads of step q into (ca, cb), DMA of step
-  // q+3 (DMA), then the barrier with LATER steps still in flight (branch-free body)
-  auto phase = [&](auto dma_c, auto later_c, int q, const bf16x8 (&pa)[8], const bf16x8 (&pb)[8],
+  // q+3 (DMA), one non-MFMA op per gap: MFMA | read | 2 MFMA | DMA | 2 MFMA | read | 3 MFMA
+  auto phase = [&](auto dma_c, auto younger_c, int q, const bf16x8 (&pa)[8], const bf16x8 (&pb)[8],
                    bf16x8 (&ca)[8], bf16x8 (&cb)[8]) {
     constexpr bool DMA = decltype(dma_c)::value;
-    constexpr int LATER = decltype(later_c)::value;
+    constexpr int YOUNGER = decltype(younger_c)::value;
+    const DmaStep ds = dma_step(q + 3);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
+      auto mm = [&](int j0, int j1) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa[i], pb[j], acc[i][j], 0, 0, 0);
-      if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
-      rd2(q, i, ca, cb);
-      if constexpr (DMA) dma(q + 3, i);
+        for (int j = j0; j < j1; ++j) mfma(i, j, pa[i], pb[j]);
+        __builtin_amdgcn_sched_barrier(0);
+      };
+      mm(0, 1);
+      if constexpr (!(ABL & 2)) rd1(q, i, 0, ca, cb);
       __builtin_amdgcn_sched_barrier(0);
+      mm(1, 3);
+      if constexpr (DMA && !(ABL & 1)) dma_piece(ds, i);
+      __builtin_amdgcn_sched_barrier(0);
+      mm(3, 5);
+      if constexpr (!(ABL & 2)) rd1(q, i, 1, ca, cb);
+      __builtin_amdgcn_sched_barrier(0);
+      mm(5, 8);
     }
-    wait_barrier_ring(LATER);
+    if constexpr (STAMP) {
+      const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+      ring_wait_barrier_c<YOUNGER>();
+      t_wait += __builtin_amdgcn_s_memtime() - t0;
+    } else {
+      ring_wait_barrier_c<YOUNGER>();
+    }
   };
   using T = std::true_type;
   using F = std::false_type;
-  using L2 = std::integral_constant<int, 2>;
-  using L1 = std::integral_constant<int, 1>;
-  using L0 = std::integral_constant<int, 0>;
+  using Y16 = std::integral_constant<int, 16>;
+  using Y8 = std::integral_constant<int, 8>;
+  using Y0 = std::integral_constant<int, 0>;
 
-  // prologue: steps 0..2 in flight (nst is even: 2 or >= 4), step 0 landed; then
-  // "phase 0": step 0's fragments read, step 3 into the last free slot, step 1 landed
-  const int pro = min(nst, 3);
+  const int ldc = g.ldc;
+  // prologue of the first tile: steps 0..2 in flight
   for (int s = 0; s < pro; ++s)
 #pragma unroll
     for (int i = 0; i < 8; ++i) dma(s, i);
-  wait_barrier_ring(pro - 1);
+  const int younger = 8 * (pro - 1);  // DMA pieces issued after step 0's
+  for (;;) {
+    const int bm = tm * WM, bn = tn * WNB;
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    rd2(0, i, a0, b0);
-    if (nst >= 4) dma(3, i);
-  }
-  wait_barrier_ring(nst >= 4 ? 2 : 0);
-  // steady state: phases 1 .. nst-4 in pairs, each prefetching the step three ahead
-  for (int q = 1; q + 3 < nst; q += 2) {
-    phase(T{}, L2{}, q, a0, b0, a1, b1);
-    phase(T{}, L2{}, q + 1, a1, b1, a0, b0);
-  }
-  if (nst >= 4) {  // drain: phases nst-3, nst-2, nst-1
-    phase(F{}, L1{}, nst - 3, a0, b0, a1, b1);
-    phase(F{}, L0{}, nst - 2, a1, b1, a0, b0);
-  }
-  phase(F{}, L0{}, nst - 1, a0, b0, a1, b1);
+    for (int i = 0; i < 8; ++i)
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+      for (int j = 0; j < 8; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+    // step 0 landed everywhere (and every wave is done with the previous epilogue's slab);
+    // "phase 0": step 0's fragments read, step 3 into slot 3, step 1 landed
+    ring_wait_barrier(younger);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[i], b1[j], acc[i][j], 0, 0, 0);
+    for (int i = 0; i < 8; ++i) {
+      rd1(0, i, 0, a0, b0);
+      rd1(0, i, 1, a0, b0);
+      if (nst >= 4) dma(3, i);
+    }
+    ring_wait_barrier(nst >= 4 ? 16 : 0);
+    if (STAMP) t_loop = __builtin_amdgcn_s_memtime();
+    // steady state: phases 1 .. nst-4 in pairs, each prefetching the step three ahead
+    for (int q = 1; q + 3 < nst; q += 2) {
+      phase(T{}, Y16{}, q, a0, b0, a1, b1);
+      phase(T{}, Y16{}, q + 1, a1, b1, a0, b0);
+    }
+    if (nst >= 4) {  // drain: phases nst-3, nst-2, nst-1
+      phase(F{}, Y8{}, nst - 3, a0, b0, a1, b1);
+      phase(F{}, Y0{}, nst - 2, a1, b1, a0, b0);
+    }
+    phase(F{}, Y0{}, nst - 1, a0, b0, a1, b1);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) mfma(i, j, a1[i], b1[j]);
+    if (STAMP) t_epi = __builtin_amdgcn_s_memtime();
 
-  // ---- epilogue (the ring is idle: the last barrier saw every read and DMA retire)
-  float* tile = reinterpret_cast<float*>(smem + wave * kEpiWave);
-  const int cl = (lane & 15) * 8;
-  const int col = bn + wc * 128 + cl;
-  float bias[8];
+    if constexpr (EPI == 1) {
+      // ---- fast epilogue: per 32-row pass, bf16 pairs -> slab (slot 3, 8 KiB per wave,
+      // 16-B chunk c of row r at c ^ (r & 15)) -> 16-B row vectors -> buffer stores
+      unsigned char* slab = smem + 3 * kRing + wave * 8192;
+      const int grp = lane >> 4, lr = lane & 15;
+      const float al = g.alpha;
+      const int ccol = bn + wc * 128 + lr * 8;
+      uint16_t* cptr = reinterpret_cast<uint16_t*>(g.C) + (size_t)(bm + wr * 128) * ldc + ccol;
+      const int rows_left = g.M - bm - wr * 128;
+      const bool col_ok = ccol < g.N;
 #pragma unroll
-  for (int q = 0; q < 8; ++q) bias[q] = load_bias(g, col + q, 0);
-  const int es = g.out_bf16 ? 2 : 4;
-  const bool vec_ok = (((uint64_t)g.C | ((uint64_t)g.ldc * es)) % 16) == 0 && g.N % 8 == 0;
+      for (int h = 0; h < 4; ++h) {
 #pragma unroll
-  for (int h = 0; h < 4; ++h) {
-    __builtin_amdgcn_sched_barrier(0);
+        for (int ii = 0; ii < 2; ++ii)
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          tile[(i * 16 + (lane >> 4) * 4 + r) * kEpiTS + j * 16 + (lane & 15)] = acc[h * 2 + i][j][r];
-    __builtin_amdgcn_wave_barrier();
-#pragma unroll 1
-    for (int it = 0; it < 8; ++it) {
-      const int rl = it * 4 + (lane >> 4);
-      const int row = bm + wr * 128 + h * 32 + rl;
-      if (row >= g.M || col >= g.N) continue;
-      float v[8];
-      const float4 x0 = *reinterpret_cast<const float4*>(tile + rl * kEpiTS + cl);
-      const float4 x1 = *reinterpret_cast<const float4*>(tile + rl * kEpiTS + cl + 4);
-      v[0] = x0.x; v[1] = x0.y; v[2] = x0.z; v[3] = x0.w; v[4] = x1.x; v[5] = x1.y; v[6] = x1.z; v[7] = x1.w;
-#pragma unroll
-      for (int q = 0; q < 8; ++q) v[q] = epi(g, v[q], bias[q]);
-      if (vec_ok) {
-        if (g.out_bf16) {
-          uint16_t* C = reinterpret_cast<uint16_t*>(g.C) + (size_t)row * g.ldc + col;
-          if (g.accumulate) {
-            const uint4 o = *reinterpret_cast<const uint4*>(C);
-            const uint32_t ow[4] = {o.x, o.y, o.z, o.w};
-#pragma unroll
-            for (int q = 0; q < 4; ++q) { v[2 * q] += bf16_lo(ow[q]); v[2 * q + 1] += bf16_hi(ow[q]); }
+          for (int j = 0; j < 8; ++j) {
+            const floatx4 v = acc[2 * h + ii][j];
+            const uint32_t lo = cvt_pk_bf16(al * v[0], al * v[1]);
+            const uint32_t hi = cvt_pk_bf16(al * v[2], al * v[3]);
+            const int row = ii * 16 + lr, chunk = 2 * j + (grp >> 1);
+            *reinterpret_cast<uint2*>(slab + row * 256 + ((chunk ^ (row & 15)) << 4) + (grp & 1) * 8) =
+                uint2{lo, hi};
+            __builtin_amdgcn_sched_barrier(0);
           }
-          uint32_t w[4];
 #pragma unroll
-          for (int q = 0; q < 4; ++q) w[q] = f32_to_bf16_bits(v[2 * q]) | (f32_to_bf16_bits(v[2 * q + 1]) << 16);
-          *reinterpret_cast<uint4*>(C) = uint4{w[0], w[1], w[2], w[3]};
-        } else {
-          float* C = reinterpret_cast<float*>(g.C) + (size_t)row * g.ldc + col;
-          float4 y0 = make_float4(v[0], v[1], v[2], v[3]), y1 = make_float4(v[4], v[5], v[6], v[7]);
-          if (g.accumulate) {
-            const float4 o0 = *reinterpret_cast<const float4*>(C), o1 = *reinterpret_cast<const float4*>(C + 4);
-            y0.x += o0.x; y0.y += o0.y; y0.z += o0.z; y0.w += o0.w;
-            y1.x += o1.x; y1.y += o1.y; y1.z += o1.z; y1.w += o1.w;
-          }
-          *reinterpret_cast<float4*>(C) = y0;
-          *reinterpret_cast<float4*>(C + 4) = y1;
+        for (int it = 0; it < 8; ++it) {
+          const int rl = it * 4 + grp;
+          const u32x4 w = *reinterpret_cast<const u32x4*>(slab + rl * 256 + ((lr ^ (rl & 15)) << 4));
+          if (col_ok && h * 32 + rl < rows_left)
+            *reinterpret_cast<u32x4*>(cptr + (size_t)(h * 32 + rl) * ldc) = w;
         }
-      } else {
-        for (int q = 0; q < 8 && col + q < g.N; ++q) {
-          const size_t o = (size_t)row * g.ldc + col + q;
-          if (g.out_bf16) {
-            uint16_t* C = reinterpret_cast<uint16_t*>(g.C);
-            C[o] = (uint16_t)f32_to_bf16_bits(v[q] + (g.accumulate ? bf2f(C[o]) : 0.f));
+      }
+    } else {
+      // ---- generic epilogue (alpha, bias, activation, accumulate, fp32 / bf16 out):
+      // per 32-row pass, fp32 through a slab over slots 0..2, one row vector per lane
+      float* tile = reinterpret_cast<float*>(smem + wave * kEpiWave);
+      const int cl = (lane & 15) * 8;
+      const int col = bn + wc * 128 + cl;
+      float bias[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) bias[q] = load_bias(g, col + q, 0);
+      const int es = g.out_bf16 ? 2 : 4;
+      const bool vec_ok = (((uint64_t)g.C | ((uint64_t)ldc * es)) % 16) == 0 && g.N % 8 == 0;
+#pragma unroll
+      for (int h = 0; h < 4; ++h) {
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              tile[(i * 16 + (lane & 15)) * kEpiTS + j * 16 + (lane >> 4) * 4 + r] = acc[h * 2 + i][j][r];
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll 1
+        for (int it = 0; it < 8; ++it) {
+          const int rl = it * 4 + (lane >> 4);
+          const int row = bm + wr * 128 + h * 32 + rl;
+          if (row >= g.M || col >= g.N) continue;
+          float v[8];
+          const float4 x0 = *reinterpret_cast<const float4*>(tile + rl * kEpiTS + cl);
+          const float4 x1 = *reinterpret_cast<const float4*>(tile + rl * kEpiTS + cl + 4);
+          v[0] = x0.x; v[1] = x0.y; v[2] = x0.z; v[3] = x0.w; v[4] = x1.x; v[5] = x1.y; v[6] = x1.z; v[7] = x1.w;
+#pragma unroll
+          for (int q = 0; q < 8; ++q) v[q] = epi(g, v[q], bias[q]);
+          if (vec_ok) {
+            if (g.out_bf16) {
+              uint16_t* C = reinterpret_cast<uint16_t*>(g.C) + (size_t)row * ldc + col;
+              if (g.accumulate) {
+                const uint4 o = *reinterpret_cast<const uint4*>(C);
+                const uint32_t ow[4] = {o.x, o.y, o.z, o.w};
+#pragma unroll
+                for (int q = 0; q < 4; ++q) { v[2 * q] += bf16_lo(ow[q]); v[2 * q + 1] += bf16_hi(ow[q]); }
+              }
+              uint32_t w[4];
+#pragma unroll
+              for (int q = 0; q < 4; ++q) w[q] = f32_to_bf16_bits(v[2 * q]) | (f32_to_bf16_bits(v[2 * q + 1]) << 16);
+              *reinterpret_cast<uint4*>(C) = uint4{w[0], w[1], w[2], w[3]};
+            } else {
+              float* C = reinterpret_cast<float*>(g.C) + (size_t)row * ldc + col;
+              float4 y0 = make_float4(v[0], v[1], v[2], v[3]), y1 = make_float4(v[4], v[5], v[6], v[7]);
+              if (g.accumulate) {
+                const float4 o0 = *reinterpret_cast<const float4*>(C), o1 = *reinterpret_cast<const float4*>(C + 4);
+                y0.x += o0.x; y0.y += o0.y; y0.z += o0.z; y0.w += o0.w;
+                y1.x += o1.x; y1.y += o1.y; y1.z += o1.z; y1.w += o1.w;
+              }
+              *reinterpret_cast<float4*>(C) = y0;
+              *reinterpret_cast<float4*>(C + 4) = y1;
+            }
           } else {
-            float* C = reinterpret_cast<float*>(g.C);
-            C[o] = v[q] + (g.accumulate ? C[o] : 0.f);
+            for (int q = 0; q < 8 && col + q < g.N; ++q) {
+              const size_t o = (size_t)row * ldc + col + q;
+              if (g.out_bf16) {
+                uint16_t* C = reinterpret_cast<uint16_t*>(g.C);
+                C[o] = (uint16_t)f32_to_bf16_bits(v[q] + (g.accumulate ? bf2f(C[o]) : 0.f));
+              } else {
+                float* C = reinterpret_cast<float*>(g.C);
+                C[o] = v[q] + (g.accumulate ? C[o] : 0.f);
+              }
+            }
           }
+        }
+        __builtin_amdgcn_wave_barrier();
+      }
+    }
+    // the next tile's first steps (slots 0..2; the slab is slot 3): the stores above are
+    // older than them, so the top-of-tile wait for step 0 also retires the stores
+    const int next = lt + (int)gridDim.x;
+    const bool more = PERSIST && EPI == 1 && next < ntiles;
+    int ntm = 0, ntn = 0;
+    if (more) {
+      tile_coords(next, tiles_m, tiles_n, wa.group_m, ntm, ntn);
+      ops_for(ntm, ntn);
+      for (int s = 0; s < pro; ++s)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) dma(s, i);
+    }
+    if constexpr (STAMP) {
+      if (lt == xcd_remap(blockIdx.x, gridDim.x)) {  // first tile of this workgroup
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned long long t_end = __builtin_amdgcn_s_memtime();
+        if (lane == 0) {
+          unsigned long long* d = wa.dbg + ((size_t)blockIdx.x * 4 + wave) * 4;
+          d[0] = t_loop - t_start;
+          d[1] = t_epi - t_loop;
+          d[2] = t_end - t_epi;
+          d[3] = t_wait;
         }
       }
     }
-    __builtin_amdgcn_wave_barrier();
+    if (!more) break;
+    lt = next;
+    tm = ntm;
+    tn = ntn;
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 }  // namespace
 
 int g_w4_sched = 1;   // bit 0: persistent grid, bit 1: MFMA-first order inside groups, bit 2: front-loaded DMA,
-                      // bit 3: ring kernel (k_gemm_w4r; bit 4 with s_setprio around the MFMA groups)
+                      // bit 3: LDS-ring kernel (k_gemm_w4r), bits 5-6 / 9: its ablations / stamps
 int g_w4_group_m = 8;
+unsigned long long* g_w4_dbg = nullptr;
 
 bool gemm_w4_ok(const GemmArgs& g) {
   // one descriptor per operand tile: the bytes from a tile's first row must fit 2 GiB
@@ -730,6 +876,58 @@ static void w4_attr(const void* f) {
   (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kLds4 + kLdsExtra);
 }
 
+// four-slot LDS ring kernel: EPI 1 (fast) when the output is bf16 with no bias, activation
+// or accumulation and C rows are 16-B vectors; persistent grid (g_w4_sched bit 0) then.
+// Diagnostics: sched bits 5-6 ablations, bit 9 s_memtime stamps (g_w4_dbg).
+static void w4r_attr(const void* f) { (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kRingLds); }
+
+bool gemm_w4r_fast(const GemmArgs& g) {
+  return g.out_bf16 && !g.accumulate && g.act == 0 && g.bias_kind == 0 && g.splitk == 1 && g.N % 8 == 0 && g.ldc % 8 == 0 &&
+         ((uint64_t)g.C % 16) == 0 && (uint64_t)g.M * g.ldc * 2 < 0x7ffffff0ull;
+}
+
+void launch_gemm_nt_w4r(const GemmArgs& g, hipStream_t stream) {
+  static int cus = [] {
+    int dev = 0, n = 0;
+    (void)hipGetDevice(&dev);
+    return hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0 ? n : 256;
+  }();
+  static bool attr = [] {
+    w4r_attr(reinterpret_cast<const void*>(k_gemm_w4r<0, 0>));
+    w4r_attr(reinterpret_cast<const void*>(k_gemm_w4r<1, 0>));
+    w4r_attr(reinterpret_cast<const void*>(k_gemm_w4r<1, 1>));
+    w4r_attr(reinterpret_cast<const void*>(k_gemm_w4r<1, 0, 1>));
+    w4r_attr(reinterpret_cast<const void*>(k_gemm_w4r<1, 0, 2>));
+    w4r_attr(reinterpret_cast<const void*>(k_gemm_w4r<1, 0, 3>));
+    w4r_attr(reinterpret_cast<const void*>(k_gemm_w4r<1, 0, 0, 1>));
+    w4r_attr(reinterpret_cast<const void*>(k_gemm_w4r<1, 1, 0, 1>));
+    return true;
+  }();
+  (void)attr;
+  const int ntiles = gemm_w4_tiles(g.M, g.N);
+  W4Args a{g, g_w4_group_m, {}, g_w4_dbg};
+  const bool fast = gemm_w4r_fast(g);
+  const bool persist = fast && (g_w4_sched & 1);
+  const int grid = persist ? std::min(ntiles, cus) : ntiles;
+  const int abl = (g_w4_sched >> 5) & 3;
+  if (!fast) {
+    hipLaunchKernelGGL((k_gemm_w4r<0, 0>), dim3(grid), dim3(WNT), kRingLds, stream, a);
+  } else if (g_w4_sched & 512) {
+    if (persist) hipLaunchKernelGGL((k_gemm_w4r<1, 1, 0, 1>), dim3(grid), dim3(WNT), kRingLds, stream, a);
+    else hipLaunchKernelGGL((k_gemm_w4r<1, 0, 0, 1>), dim3(grid), dim3(WNT), kRingLds, stream, a);
+  } else if (abl == 1) {
+    hipLaunchKernelGGL((k_gemm_w4r<1, 0, 1>), dim3(grid), dim3(WNT), kRingLds, stream, a);
+  } else if (abl == 2) {
+    hipLaunchKernelGGL((k_gemm_w4r<1, 0, 2>), dim3(grid), dim3(WNT), kRingLds, stream, a);
+  } else if (abl == 3) {
+    hipLaunchKernelGGL((k_gemm_w4r<1, 0, 3>), dim3(grid), dim3(WNT), kRingLds, stream, a);
+  } else if (persist) {
+    hipLaunchKernelGGL((k_gemm_w4r<1, 1>), dim3(grid), dim3(WNT), kRingLds, stream, a);
+  } else {
+    hipLaunchKernelGGL((k_gemm_w4r<1, 0>), dim3(grid), dim3(WNT), kRingLds, stream, a);
+  }
+}
+
 void launch_gemm_nt_w4(const GemmArgs& g, hipStream_t stream) {
   static int cus = [] {
     int dev = 0, n = 0;
@@ -737,7 +935,7 @@ void launch_gemm_nt_w4(const GemmArgs& g, hipStream_t stream) {
     return hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0 ? n : 256;
   }();
   const int ntiles = ((g.M + WM - 1) / WM) * ((g.N + WNB - 1) / WNB);
-  W4Args a{g, g_w4_group_m, {}};
+  W4Args a{g, g_w4_group_m, {}, nullptr};
   const bool persist = g_w4_sched & 1;
   const int grid = persist ? std::min(ntiles, cus) : ntiles;
   static bool attr = [] {
@@ -751,16 +949,7 @@ void launch_gemm_nt_w4(const GemmArgs& g, hipStream_t stream) {
   }();
   (void)attr;
   if (g_w4_sched & 8) {
-    static bool rattr = [] {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_gemm_w4r<0>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 4 * kRing);
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_gemm_w4r<1>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 4 * kRing);
-      return true;
-    }();
-    (void)rattr;
-    if (g_w4_sched & 16) hipLaunchKernelGGL(k_gemm_w4r<1>, dim3(ntiles), dim3(WNT), 4 * kRing, stream, a);
-    else hipLaunchKernelGGL(k_gemm_w4r<0>, dim3(ntiles), dim3(WNT), 4 * kRing, stream, a);
+    launch_gemm_nt_w4r(g, stream);
     return;
   }
   if (g_w4_sched & 4) {
@@ -792,7 +981,7 @@ void launch_gemm_nt_w4_fused(const GemmArgs& g, const FusedArgs& f, hipStream_t 
   (void)attr;
   (void)cus;
   const int ntiles = gemm_w4_tiles(g.M, g.N);
-  W4Args a{g, g_w4_group_m, f};
+  W4Args a{g, g_w4_group_m, f, nullptr};
   hipLaunchKernelGGL((k_gemm_w4<0, 0, 1>), dim3(ntiles), dim3(WNT), kLds4 + kLdsExtra, stream, a);
 }
 

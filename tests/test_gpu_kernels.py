@@ -80,7 +80,7 @@ def test_gemm256_epilogue(gemm256, act):
     torch.testing.assert_close(c, c0 + _ref(a, b), rtol=2e-3, atol=5e-2)
 
 
-@pytest.mark.parametrize("sched", [0, 1, 3, 4, 5, 24], ids=["w4", "w4p", "w4po", "w4f", "w4pf", "ring"])
+@pytest.mark.parametrize("sched", [0, 1, 3, 4, 5, 8, 9], ids=["w4", "w4p", "w4po", "w4f", "w4pf", "ring", "ringp"])
 @pytest.mark.parametrize("M,N,K", [(256, 256, 64), (256, 256, 128), (300, 520, 256), (777, 1000, 512),
                                    (2048, 2048, 4096), (1, 8, 192), (4096, 768, 768)])
 def test_gemm_w4_shapes(sched, M, N, K):
@@ -100,6 +100,9 @@ def test_gemm_w4_shapes(sched, M, N, K):
         torch.testing.assert_close(y, _ref(a, b), rtol=2e-3, atol=2e-3 * K ** 0.5)
         for _ in range(2):
             torch.testing.assert_close(gemm_nt(a, b, out_dtype=torch.float32), y, rtol=0, atol=0)
+        # bf16 out, no bias: the ring kernel's fast epilogue (bf16 = RNE of the fp32 result)
+        y16 = gemm_nt(a, b, alpha=0.5)
+        torch.testing.assert_close(y16.float(), (0.5 * y).bfloat16().float(), rtol=1e-2, atol=1e-2)
         if M == 300:
             bias = torch.randn(N, device="cuda").bfloat16()
             yb = gemm_nt(a, b, bias=bias, alpha=0.5)
