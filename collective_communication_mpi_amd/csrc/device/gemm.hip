@@ -933,6 +933,14 @@ void gemm_nt(uint64_t A, uint64_t B, uint64_t C, uint64_t bias, int M, int N, in
     CCMPI_HIP_CHECK(hipGetLastError());
     return;
   }
+  // auto: large bf16-out GEMMs on the four-wave LDS-ring kernel (gemm_w4.hip; measured
+  // against the 256x256 ping-pong kernel in profiles/r3_gemm)
+  if (g_kernel == 0 && splitk == 1 && g_ring_min_macs > 0 && (long long)M * N * K >= g_ring_min_macs &&
+      M >= 1024 && N >= 1024 && gemm_w4_ok(g) && gemm_w4r_fast(g)) {
+    launch_gemm_nt_w4r(g, reinterpret_cast<hipStream_t>(stream));
+    CCMPI_HIP_CHECK(hipGetLastError());
+    return;
+  }
   const bool big_ok = K % (2 * BK) == 0 && g_use_glds;
   if (big_ok && g_kernel != 1) {
     int bn = 0;
@@ -970,6 +978,21 @@ void gemm_nt(uint64_t A, uint64_t B, uint64_t C, uint64_t bias, int M, int N, in
   else
     hipLaunchKernelGGL(k_gemm_nt, dim3(nwg), dim3(NT), 0, reinterpret_cast<hipStream_t>(stream), g);
   CCMPI_HIP_CHECK(hipGetLastError());
+}
+
+
+// LDS-ring GEMM with operand layouts (gemm_w4.hip): C[M,N] (+)= alpha * op(A) op(B)^T,
+// op(A)[m][k] = ta ? A[k*lda + m] : A[m*lda + k], op(B)[n][k] likewise.  Returns false
+// (nothing launched) when the ring kernel does not apply (K % 64, alignment, 2 GiB).
+bool gemm_ring(uint64_t A, uint64_t B, uint64_t C, int M, int N, int K, int lda, int ldb, int ldc, int ta, int tb,
+               float alpha, bool accumulate, bool out_bf16, uint64_t stream) {
+  if (M <= 0 || N <= 0) return true;
+  GemmArgs g{reinterpret_cast<const uint16_t*>(A), reinterpret_cast<const uint16_t*>(B), reinterpret_cast<void*>(C),
+             nullptr, M, N, K, lda, ldb, ldc, alpha, accumulate ? 1 : 0, 0, 0, out_bf16 ? 1 : 0, 1};
+  if (!gemm_ring_ok(g, ta, tb) || (C % 16) || ldc % 8) return false;
+  launch_gemm_ring(g, ta, tb, reinterpret_cast<hipStream_t>(stream));
+  CCMPI_HIP_CHECK(hipGetLastError());
+  return true;
 }
 
 int g_tn_split_major = std::getenv("CCMPI_TN_ORDER") ? std::atoi(std::getenv("CCMPI_TN_ORDER")) : 1;
@@ -1058,6 +1081,12 @@ void register_gemm_ops(pybind11::module_& m) {
         pybind11::arg("alpha"), pybind11::arg("accumulate"), pybind11::arg("bias_kind"), pybind11::arg("act"),
         pybind11::arg("out_bf16"), pybind11::arg("splitk"), pybind11::arg("stream"),
         pybind11::call_guard<pybind11::gil_scoped_release>());
+  m.def("gemm_ring", &gemm_ring,
+        "LDS-ring GEMM, C (+)= alpha*op(A).op(B)^T with K-major (ta/tb=1) or K-contiguous operands; false = n/a",
+        pybind11::arg("A"), pybind11::arg("B"), pybind11::arg("C"), pybind11::arg("M"), pybind11::arg("N"),
+        pybind11::arg("K"), pybind11::arg("lda"), pybind11::arg("ldb"), pybind11::arg("ldc"), pybind11::arg("ta"),
+        pybind11::arg("tb"), pybind11::arg("alpha"), pybind11::arg("accumulate"), pybind11::arg("out_bf16"),
+        pybind11::arg("stream"), pybind11::call_guard<pybind11::gil_scoped_release>());
   m.def("gemm_tn", &gemm_tn, "C[N1,N2] (+)= alpha*A[M,N1]^T.B[M,N2] (fp32 out; split-K via workspace or atomics)",
         pybind11::arg("A"), pybind11::arg("B"), pybind11::arg("C"), pybind11::arg("M"), pybind11::arg("N1"),
         pybind11::arg("N2"), pybind11::arg("lda"), pybind11::arg("ldb"), pybind11::arg("ldc"), pybind11::arg("alpha"),
@@ -1073,6 +1102,8 @@ void register_gemm_ops(pybind11::module_& m) {
         "four-wave kernel variant (benchmarks): bit 0 persistent grid, bit 1 MFMA-first group order");
   m.def("gemm_set_w4_debug", [](uint64_t p) { g_w4_dbg = reinterpret_cast<unsigned long long*>(p); },
         "four-wave ring STAMP diagnostic: device buffer of 4 uint64 per wave (benchmarks only)");
+  m.def("gemm_set_ring_min", [](long long v) { g_ring_min_macs = v; },
+        "gemm_nt auto: LDS-ring kernel from this many multiply-adds up (0 = never)");
   m.def("gemm_set_w4_group_m", [](int v) { g_w4_group_m = v > 0 ? v : 8; }, "four-wave kernel group-M rows");
   m.def("gemm_set_ablation", [](int e) {
     g_pp_exp = e;

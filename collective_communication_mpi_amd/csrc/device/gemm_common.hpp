@@ -210,7 +210,13 @@ bool gemm_w4_ok(const GemmArgs& g);
 extern int g_w4_sched;    // four-wave kernel variant: bit 0 persistent grid, bit 1 MFMA-first group order
 extern unsigned long long* g_w4_dbg;  // four-wave ring STAMP diagnostic output (benchmarks)
 extern int g_w4_group_m;  // four-wave kernel: tile rows per group-M block
-void launch_gemm_nt_w4(const GemmArgs& g, hipStream_t stream);  // ablation variant of the ping-pong kernel (benchmarks only; 0 = production)
+void launch_gemm_nt_w4(const GemmArgs& g, hipStream_t stream);
+bool gemm_w4r_fast(const GemmArgs& g);  // the LDS-ring kernel's fast epilogue applies
+void launch_gemm_nt_w4r(const GemmArgs& g, hipStream_t stream);  // LDS-ring kernel (sched bits from g_w4_sched)
+// LDS-ring kernel with operand layouts: ta / tb = 1 reads A / B K-major ([K][M] / [K][N])
+bool gemm_ring_ok(const GemmArgs& g, int ta, int tb);
+void launch_gemm_ring(const GemmArgs& g, int ta, int tb, hipStream_t stream);
+extern long long g_ring_min_macs;  // gemm_nt auto: the LDS-ring kernel from this many MACs up (0 = never)  // ablation variant of the ping-pong kernel (benchmarks only; 0 = production)
 
 }  // namespace gemm
 }  // namespace dev

@@ -24,6 +24,7 @@
 // Epilogue: per wave, two 64-row halves staged through LDS as fp32, written
 // as whole 16-B row vectors (alpha, bias, activation, accumulate, fp32/bf16 out).
 #include <hip/hip_runtime.h>
+#include <cstdlib>
 #include <type_traits>
 
 #include "gemm_common.hpp"
@@ -555,15 +556,30 @@ __device__ __forceinline__ void ring_wait_barrier_c() {
 // (a local struct in the kernel template made hipcc drop the host launch stubs)
 struct DmaStep {
   unsigned char* lds;
-  int va, vb;
+  int va, vb;    // N layout: every piece; K-major layout: even pieces
+  int va1, vb1;  // K-major layout: odd pieces (the swizzle depends on the piece parity)
 };
+
+// operand tile descriptor of a K-major ("T") operand stored [K][rows] with row stride ld:
+// base at column m0, bounded by the bytes from there to the end of the buffer
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t op_rsrc_t(const uint16_t* X, int m0, int K, int ld) {
+  long bytes = (long)K * ld * 2 - (long)m0 * 2;
+  if (bytes < 0) bytes = 0;
+  if (bytes > 0x7ffffff0l) bytes = 0x7ffffff0l;
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(X + m0), 0, (int)bytes, 0x00020000);
+}
 
 // EPI 1: bf16 out, C = alpha * AB^T, no bias / activation / accumulate (fast epilogue,
 // exactly 32 store instructions per wave and tile); EPI 0: the generic epilogue.
 // ABL (diagnostic ablations, wrong results): bit 0 drops the steady-state DMA, bit 1 the
 // steady-state fragment reads.  STAMP (diagnostic): per wave, s_memtime cycles of the
 // prologue, main loop, epilogue and the phase-end waits -> wa.dbg (first tile only).
-template <int EPI, int PERSIST, int ABL = 0, int STAMP = 0>
+// TA / TB: operand layout.  0 ("N"): rows of K contiguous elements (A[m][k], B[n][k]).
+// 1 ("T", K-major): stored [K][M] / [K][N] (dX = dY W reads W this way, dW = dY^T X both
+// operands).  A K-major slot half is [32 k][256 rows] with 512-B k-rows whose 32-B
+// granules are XOR-swizzled by tn_swz(k) (the 256x256 TN kernel's scheme, gemm256.hip);
+// its fragments come out of two ds_read_b64_tr_b16 each.
+template <int EPI, int PERSIST, int ABL = 0, int STAMP = 0, int TA = 0, int TB = 0>
 __global__ void __launch_bounds__(WNT, 1) k_gemm_w4r(W4Args wa) {
   const GemmArgs& g = wa.g;
   extern __shared__ __attribute__((aligned(1024))) unsigned char smem[];
@@ -582,8 +598,10 @@ __global__ void __launch_bounds__(WNT, 1) k_gemm_w4r(W4Args wa) {
   tile_coords(lt, tiles_m, tiles_n, wa.group_m, tm, tn);
   __amdgpu_buffer_rsrc_t ra, rb;
   auto ops_for = [&](int tm_, int tn_) {
-    ra = op_rsrc(g.A + (size_t)tm_ * WM * g.lda, (long)g.M - tm_ * WM, g.lda);
-    rb = op_rsrc(g.B + (size_t)tn_ * WNB * g.ldb, (long)g.N - tn_ * WNB, g.ldb);
+    if constexpr (TA) ra = op_rsrc_t(g.A, tm_ * WM, g.K, g.lda);
+    else ra = op_rsrc(g.A + (size_t)tm_ * WM * g.lda, (long)g.M - tm_ * WM, g.lda);
+    if constexpr (TB) rb = op_rsrc_t(g.B, tn_ * WNB, g.K, g.ldb);
+    else rb = op_rsrc(g.B + (size_t)tn_ * WNB * g.ldb, (long)g.N - tn_ * WNB, g.ldb);
   };
   ops_for(tm, tn);
 
@@ -592,32 +610,55 @@ __global__ void __launch_bounds__(WNT, 1) k_gemm_w4r(W4Args wa) {
   const int drow = wave * 16 + (lane >> 2);
   const int dchunk = ((lane & 3) ^ ring_swz((lane >> 4) & 3)) << 4;
   const int va = drow * g.lda * 2 + dchunk, vb = drow * g.ldb * 2 + dchunk;
-  // piece offsets i * 64 rows: loop-invariant SGPRs (the K offset rides in the VGPR
-  // offset, the slot in M0), so a DMA piece costs one M0 write and the load itself
-  const int sa1 = 64 * g.lda * 2, sb1 = 64 * g.ldb * 2;
+  // K-major pieces: 2 k-rows x 512 B; wave w, piece i: k-rows 8 i + 2 w + (l >> 5); lane l
+  // lands at granule (l & 31) >> 1, half l & 1, holding logical granule ^ tn_swz(k-row)
+  const int trow = 2 * wave + (lane >> 5);
+  auto vt = [&](int ld, int par) {
+    const int sw = (trow & 3) | (par << 2);
+    return trow * ld * 2 + (((((lane & 31) >> 1) ^ sw) * 16 + (lane & 1) * 8) * 2);
+  };
+  const int ta0 = TA ? vt(g.lda, 0) : va, ta1 = TA ? vt(g.lda, 1) : va;
+  const int tb0 = TB ? vt(g.ldb, 0) : vb, tb1 = TB ? vt(g.ldb, 1) : vb;
+  // piece offsets (N: i * 64 rows, T: i * 8 k-rows): loop-invariant SGPRs (the K offset
+  // rides in the VGPR offset, the slot in M0), so a DMA piece costs one M0 write and the load
+  const int sa1 = TA ? 16 * g.lda : 64 * g.lda * 2, sb1 = TB ? 16 * g.ldb : 64 * g.ldb * 2;
   const int sa2 = 2 * sa1, sa3 = 3 * sa1, sb2 = 2 * sb1, sb3 = 3 * sb1;
+  const int ka = TA ? 64 * g.lda : 64, kb = TB ? 64 * g.ldb : 64;  // bytes per K-step
   auto dma_step = [&](int s) {
-    return DmaStep{smem + (s & 3) * kRing + wave * 1024, va + s * 64, vb + s * 64};
+    return DmaStep{smem + (s & 3) * kRing + wave * 1024, ta0 + s * ka, tb0 + s * kb, ta1 + s * ka, tb1 + s * kb};
   };
   auto dma_piece = [&](const DmaStep& d, int i) {
     if (i < 4) {
       const int so = i == 0 ? 0 : i == 1 ? sa1 : i == 2 ? sa2 : sa3;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_vptr)(d.lds + i * 4096), 16, d.va, so, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_vptr)(d.lds + i * 4096), 16, (TA && (i & 1)) ? d.va1 : d.va,
+                                               so, 0, 0);
     } else {
       const int so = i == 4 ? 0 : i == 5 ? sb1 : i == 6 ? sb2 : sb3;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_vptr)(d.lds + kRingHalf + (i - 4) * 4096), 16, d.vb, so,
-                                               0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_vptr)(d.lds + kRingHalf + (i - 4) * 4096), 16,
+                                               (TB && (i & 1)) ? d.vb1 : d.vb, so, 0, 0);
     }
   };
   auto dma = [&](int s, int i) { dma_piece(dma_step(s), i); };
   // fragment (16x16x32): lane l reads row (l & 15) of a 16-row block, logical chunk l >> 4;
   // the physical chunk depends on the lane only (block rows are multiples of 16)
   const int rdo = (lane & 15) * 64 + (((lane >> 4) ^ ring_swz((lane >> 2) & 3)) << 4);
+  // K-major fragment: ds_read_b64_tr_b16 lane roles (group tg = l >> 4 reads k-rows
+  // 8 tg + tq (+4), columns 4 tp .. +3 of the 16-row block)
+  const int tg = lane >> 4, tq = (lane >> 2) & 3, tp = lane & 3;
+  const int tr_base = (tg * 8 + tq) * 512 + tp * 8, tr_swz = tq | ((tg & 1) << 2);
+  auto rd_t = [&](const unsigned char* half, int r0) {
+    typedef short v4s __attribute__((ext_vector_type(4)));
+    const unsigned char* p = half + tr_base + ((((r0 >> 4) ^ tr_swz)) << 5);
+    const v4s x0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(p));
+    const v4s x1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(p + 2048));
+    return __builtin_bit_cast(bf16x8, __builtin_shufflevector(x0, x1, 0, 1, 2, 3, 4, 5, 6, 7));
+  };
   // read u (0, 1) of group grp (0..7): B blocks 2 grp + u (grp < 4), then A blocks
   auto rd1 = [&](int s, int grp, int u, bf16x8 (&fa)[8], bf16x8 (&fb)[8]) {
-    const unsigned char* base = smem + (s & 3) * kRing + (grp < 4 ? kRingHalf : 0) + rdo;
-    const int r0 = (grp < 4 ? wc : wr) * 128 + (grp & 3) * 32;
-    const bf16x8 v = *reinterpret_cast<const bf16x8*>(base + (r0 + u * 16) * 64);
+    const unsigned char* half = smem + (s & 3) * kRing + (grp < 4 ? kRingHalf : 0);
+    const int r0 = (grp < 4 ? wc : wr) * 128 + (grp & 3) * 32 + u * 16;
+    const bool t = grp < 4 ? TB : TA;
+    const bf16x8 v = t ? rd_t(half, r0) : *reinterpret_cast<const bf16x8*>(half + rdo + r0 * 64);
     if (grp < 4) fb[(grp & 3) * 2 + u] = v;
     else fa[(grp & 3) * 2 + u] = v;
   };
@@ -643,16 +684,30 @@ __global__ void __launch_bounds__(WNT, 1) k_gemm_w4r(W4Args wa) {
         for (int j = j0; j < j1; ++j) mfma(i, j, pa[i], pb[j]);
         __builtin_amdgcn_sched_barrier(0);
       };
-      mm(0, 1);
-      if constexpr (!(ABL & 2)) rd1(q, i, 0, ca, cb);
-      __builtin_amdgcn_sched_barrier(0);
-      mm(1, 3);
-      if constexpr (DMA && !(ABL & 1)) dma_piece(ds, i);
-      __builtin_amdgcn_sched_barrier(0);
-      mm(3, 5);
-      if constexpr (!(ABL & 2)) rd1(q, i, 1, ca, cb);
-      __builtin_amdgcn_sched_barrier(0);
-      mm(5, 8);
+      if constexpr (TA || TB) {
+        // K-major operands need ~16 more VGPRs of read offsets: A fragments are
+        // replaced in place (pa == ca), block i read right after its last MFMA
+        mm(0, 1);
+        if constexpr (!(ABL & 2)) rd1(q, i >> 1, i & 1, ca, cb);  // B block i
+        __builtin_amdgcn_sched_barrier(0);
+        mm(1, 3);
+        if constexpr (DMA && !(ABL & 1)) dma_piece(ds, i);
+        __builtin_amdgcn_sched_barrier(0);
+        mm(3, 8);
+        if constexpr (!(ABL & 2)) rd1(q, 4 + (i >> 1), i & 1, ca, cb);  // A block i
+        __builtin_amdgcn_sched_barrier(0);
+      } else {
+        mm(0, 1);
+        if constexpr (!(ABL & 2)) rd1(q, i, 0, ca, cb);
+        __builtin_amdgcn_sched_barrier(0);
+        mm(1, 3);
+        if constexpr (DMA && !(ABL & 1)) dma_piece(ds, i);
+        __builtin_amdgcn_sched_barrier(0);
+        mm(3, 5);
+        if constexpr (!(ABL & 2)) rd1(q, i, 1, ca, cb);
+        __builtin_amdgcn_sched_barrier(0);
+        mm(5, 8);
+      }
     }
     if constexpr (STAMP) {
       const unsigned long long t0 = __builtin_amdgcn_s_memtime();
@@ -692,19 +747,21 @@ __global__ void __launch_bounds__(WNT, 1) k_gemm_w4r(W4Args wa) {
     ring_wait_barrier(nst >= 4 ? 16 : 0);
     if (STAMP) t_loop = __builtin_amdgcn_s_memtime();
     // steady state: phases 1 .. nst-4 in pairs, each prefetching the step three ahead
+    // (K-major variants: one A set, a1 aliases a0)
+    bf16x8 (&a1r)[8] = (TA || TB) ? a0 : a1;
     for (int q = 1; q + 3 < nst; q += 2) {
-      phase(T{}, Y16{}, q, a0, b0, a1, b1);
-      phase(T{}, Y16{}, q + 1, a1, b1, a0, b0);
+      phase(T{}, Y16{}, q, a0, b0, a1r, b1);
+      phase(T{}, Y16{}, q + 1, a1r, b1, a0, b0);
     }
     if (nst >= 4) {  // drain: phases nst-3, nst-2, nst-1
-      phase(F{}, Y8{}, nst - 3, a0, b0, a1, b1);
-      phase(F{}, Y0{}, nst - 2, a1, b1, a0, b0);
+      phase(F{}, Y8{}, nst - 3, a0, b0, a1r, b1);
+      phase(F{}, Y0{}, nst - 2, a1r, b1, a0, b0);
     }
-    phase(F{}, Y0{}, nst - 1, a0, b0, a1, b1);
+    phase(F{}, Y0{}, nst - 1, a0, b0, a1r, b1);
 #pragma unroll
     for (int i = 0; i < 8; ++i)
 #pragma unroll
-      for (int j = 0; j < 8; ++j) mfma(i, j, a1[i], b1[j]);
+      for (int j = 0; j < 8; ++j) mfma(i, j, a1r[i], b1[j]);
     if (STAMP) t_epi = __builtin_amdgcn_s_memtime();
 
     if constexpr (EPI == 1) {
@@ -851,6 +908,8 @@ int g_w4_sched = 1;   // bit 0: persistent grid, bit 1: MFMA-first order inside 
                       // bit 3: LDS-ring kernel (k_gemm_w4r), bits 5-6 / 9: its ablations / stamps
 int g_w4_group_m = 8;
 unsigned long long* g_w4_dbg = nullptr;
+int g_ring_sched = 8;  // auto dispatch: non-persistent ring (profiles/r3_gemm)
+long long g_ring_min_macs = std::getenv("CCMPI_RING_MIN_MACS") ? std::atoll(std::getenv("CCMPI_RING_MIN_MACS")) : (1ll << 33);
 
 bool gemm_w4_ok(const GemmArgs& g) {
   // one descriptor per operand tile: the bytes from a tile's first row must fit 2 GiB
@@ -886,7 +945,20 @@ bool gemm_w4r_fast(const GemmArgs& g) {
          ((uint64_t)g.C % 16) == 0 && (uint64_t)g.M * g.ldc * 2 < 0x7ffffff0ull;
 }
 
-void launch_gemm_nt_w4r(const GemmArgs& g, hipStream_t stream) {
+void launch_gemm_nt_w4r(const GemmArgs& g, hipStream_t stream) { launch_gemm_ring(g, 0, 0, stream); }
+
+bool gemm_ring_ok(const GemmArgs& g, int ta, int tb) {
+  if (g.splitk != 1 || g.K % WK || g.K < WK || g.lda % 8 || g.ldb % 8 || ((uint64_t)g.A % 16) || ((uint64_t)g.B % 16))
+    return false;
+  const long a_bytes = ta ? (long)g.K * g.lda * 2 : (long)g.M * g.lda * 2;
+  const long b_bytes = tb ? (long)g.K * g.ldb * 2 : (long)g.N * g.ldb * 2;
+  // (a K-major operand's byte offsets, K * ld * 2 at most, are 32-bit buffer offsets)
+  return a_bytes < 0x7ffffff0l && b_bytes < 0x7ffffff0l;
+}
+
+void launch_gemm_ring(const GemmArgs& g, int ta, int tb, hipStream_t stream) {
+  // explicit ring schedule (gemm_set_kernel(5) + sched bit 3) or the auto defaults
+  const int sched = (g_w4_sched & 8) ? g_w4_sched : g_ring_sched;
   static int cus = [] {
     int dev = 0, n = 0;
     (void)hipGetDevice(&dev);
@@ -901,18 +973,36 @@ void launch_gemm_nt_w4r(const GemmArgs& g, hipStream_t stream) {
     w4r_attr(reinterpret_cast<const void*>(k_gemm_w4r<1, 0, 3>));
     w4r_attr(reinterpret_cast<const void*>(k_gemm_w4r<1, 0, 0, 1>));
     w4r_attr(reinterpret_cast<const void*>(k_gemm_w4r<1, 1, 0, 1>));
+    w4r_attr(reinterpret_cast<const void*>(k_gemm_w4r<0, 0, 0, 0, 0, 1>));
+    w4r_attr(reinterpret_cast<const void*>(k_gemm_w4r<1, 0, 0, 0, 0, 1>));
+    w4r_attr(reinterpret_cast<const void*>(k_gemm_w4r<0, 0, 0, 0, 1, 1>));
+    w4r_attr(reinterpret_cast<const void*>(k_gemm_w4r<1, 0, 0, 0, 1, 1>));
+    w4r_attr(reinterpret_cast<const void*>(k_gemm_w4r<0, 0, 0, 0, 1, 0>));
+    w4r_attr(reinterpret_cast<const void*>(k_gemm_w4r<1, 0, 0, 0, 1, 0>));
     return true;
   }();
   (void)attr;
   const int ntiles = gemm_w4_tiles(g.M, g.N);
   W4Args a{g, g_w4_group_m, {}, g_w4_dbg};
   const bool fast = gemm_w4r_fast(g);
-  const bool persist = fast && (g_w4_sched & 1);
+  const bool persist = fast && (sched & 1);
   const int grid = persist ? std::min(ntiles, cus) : ntiles;
-  const int abl = (g_w4_sched >> 5) & 3;
+  const int abl = (sched >> 5) & 3;
+  if (ta || tb) {  // K-major operands: non-persistent, no diagnostics
+    const int v = (ta ? 2 : 0) + (tb ? 1 : 0) + (fast ? 4 : 0);
+    switch (v) {
+      case 1: hipLaunchKernelGGL((k_gemm_w4r<0, 0, 0, 0, 0, 1>), dim3(ntiles), dim3(WNT), kRingLds, stream, a); break;
+      case 5: hipLaunchKernelGGL((k_gemm_w4r<1, 0, 0, 0, 0, 1>), dim3(ntiles), dim3(WNT), kRingLds, stream, a); break;
+      case 2: hipLaunchKernelGGL((k_gemm_w4r<0, 0, 0, 0, 1, 0>), dim3(ntiles), dim3(WNT), kRingLds, stream, a); break;
+      case 6: hipLaunchKernelGGL((k_gemm_w4r<1, 0, 0, 0, 1, 0>), dim3(ntiles), dim3(WNT), kRingLds, stream, a); break;
+      case 3: hipLaunchKernelGGL((k_gemm_w4r<0, 0, 0, 0, 1, 1>), dim3(ntiles), dim3(WNT), kRingLds, stream, a); break;
+      default: hipLaunchKernelGGL((k_gemm_w4r<1, 0, 0, 0, 1, 1>), dim3(ntiles), dim3(WNT), kRingLds, stream, a); break;
+    }
+    return;
+  }
   if (!fast) {
     hipLaunchKernelGGL((k_gemm_w4r<0, 0>), dim3(grid), dim3(WNT), kRingLds, stream, a);
-  } else if (g_w4_sched & 512) {
+  } else if (sched & 512) {
     if (persist) hipLaunchKernelGGL((k_gemm_w4r<1, 1, 0, 1>), dim3(grid), dim3(WNT), kRingLds, stream, a);
     else hipLaunchKernelGGL((k_gemm_w4r<1, 0, 0, 1>), dim3(grid), dim3(WNT), kRingLds, stream, a);
   } else if (abl == 1) {

@@ -5,6 +5,7 @@ violates a kernel precondition; there is no silent eager fallback."""
 from .kernels import (  # noqa: F401
     gemm_nt,
     gemm_tn,
+    gemm_ring,
     linear,
     transpose,
     interleave_lastaxis,

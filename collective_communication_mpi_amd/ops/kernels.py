@@ -142,6 +142,33 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
     return y.reshape(*lead, w.shape[0])
 
 
+def gemm_ring(a: torch.Tensor, b: torch.Tensor, ta: bool, tb: bool, out: Optional[torch.Tensor] = None,
+              alpha: float = 1.0, accumulate: bool = False, out_dtype: torch.dtype = torch.bfloat16) -> Optional[torch.Tensor]:
+    """``out = alpha * op(a) @ op(b).T (+ out)`` on the four-wave LDS-ring MFMA kernel
+    (csrc/device/gemm_w4.hip), with either operand K-major: op(a) = a.T if ``ta`` (a is
+    [K, M]) else a ([M, K]); op(b) = b.T if ``tb`` (b is [K, N]) else b ([N, K]).
+    dX = dY W is ``gemm_ring(dY, W, False, True)``, dW = dY^T X is
+    ``gemm_ring(dY, X, True, True)``: no transposes.  Returns None when the kernel does
+    not apply (K % 64, 16-B alignment, > 2 GiB operands): the caller falls back."""
+    if a.dtype != torch.bfloat16 or b.dtype != torch.bfloat16 or a.dim() != 2 or b.dim() != 2:
+        raise TypeError("gemm_ring expects 2-D bf16 operands")
+    if a.stride(1) != 1 or b.stride(1) != 1:
+        raise ValueError("gemm_ring operands must have unit inner stride")
+    M, K = (a.shape[1], a.shape[0]) if ta else (a.shape[0], a.shape[1])
+    N, Kb = (b.shape[1], b.shape[0]) if tb else (b.shape[0], b.shape[1])
+    if K != Kb:
+        raise ValueError(f"gemm_ring shape mismatch: op(a) {M}x{K}, op(b) {N}x{Kb}")
+    if out is None:
+        if accumulate:
+            raise ValueError("accumulate needs an output tensor")
+        out = torch.empty((M, N), dtype=out_dtype, device=a.device)
+    if out.shape != (M, N) or out.stride(1) != 1 or out.dtype not in (torch.bfloat16, torch.float32):
+        raise ValueError("gemm_ring output must be [M, N] bf16/fp32 with unit column stride")
+    ok = _D().gemm_ring(a.data_ptr(), b.data_ptr(), out.data_ptr(), M, N, K, a.stride(0), b.stride(0), out.stride(0),
+                        int(ta), int(tb), float(alpha), bool(accumulate), out.dtype == torch.bfloat16, _stream(a))
+    return out if ok else None
+
+
 def transpose(x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """2-D transpose of a 16-bit tensor (LDS-tiled kernel)."""
     if x.dim() != 2 or x.element_size() != 2 or x.stride(1) != 1:
