@@ -535,7 +535,10 @@ __device__ __forceinline__ int ring_swz(int q) { return (0x78 >> (2 * q)) & 3; }
 
 // `younger` vector-memory ops (DMA pieces / epilogue stores) may stay in flight past
 // this barrier; every LDS op of the wave has retired
+// (every barrier is fenced with sched_barrier(0): the K-major fragment reads are inline
+// asm the compiler cannot wait for, so no MFMA may be scheduled above the lgkmcnt(0))
 __device__ __forceinline__ void ring_wait_barrier(int younger) {
+  __builtin_amdgcn_sched_barrier(0);
   switch (younger) {
     case 48: asm volatile("s_waitcnt vmcnt(48) lgkmcnt(0)\n\ts_barrier" ::: "memory"); break;
     case 40: asm volatile("s_waitcnt vmcnt(40) lgkmcnt(0)\n\ts_barrier" ::: "memory"); break;
@@ -544,12 +547,15 @@ __device__ __forceinline__ void ring_wait_barrier(int younger) {
     case 8: asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)\n\ts_barrier" ::: "memory"); break;
     default: asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory"); break;
   }
+  __builtin_amdgcn_sched_barrier(0);
 }
 template <int YOUNGER>
 __device__ __forceinline__ void ring_wait_barrier_c() {
+  __builtin_amdgcn_sched_barrier(0);
   if constexpr (YOUNGER == 16) asm volatile("s_waitcnt vmcnt(16) lgkmcnt(0)\n\ts_barrier" ::: "memory");
   else if constexpr (YOUNGER == 8) asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)\n\ts_barrier" ::: "memory");
   else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
 }
 
 // one K-step's DMA: slot base + this wave's 1 KiB, per-lane byte offsets incl. the K offset
@@ -628,14 +634,23 @@ __global__ void __launch_bounds__(WNT, 1) k_gemm_w4r(W4Args wa) {
     return DmaStep{smem + (s & 3) * kRing + wave * 1024, ta0 + s * ka, tb0 + s * kb, ta1 + s * ka, tb1 + s * kb};
   };
   auto dma_piece = [&](const DmaStep& d, int i) {
-    if (i < 4) {
-      const int so = i == 0 ? 0 : i == 1 ? sa1 : i == 2 ? sa2 : sa3;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_vptr)(d.lds + i * 4096), 16, (TA && (i & 1)) ? d.va1 : d.va,
-                                               so, 0, 0);
+    const bool isa = i < 4;
+    const int so = isa ? (i == 0 ? 0 : i == 1 ? sa1 : i == 2 ? sa2 : sa3)
+                       : (i == 4 ? 0 : i == 5 ? sb1 : i == 6 ? sb2 : sb3);
+    unsigned char* dst = d.lds + (isa ? 0 : kRingHalf) + (i & 3) * 4096;
+    const int vo = isa ? ((TA && (i & 1)) ? d.va1 : d.va) : ((TB && (i & 1)) ? d.vb1 : d.vb);
+    if constexpr (TA || TB) {
+      // inline asm: hipcc tracks a builtin LDS-DMA as a pending LDS write and puts
+      // s_waitcnt vmcnt(0) before every ds_read_b64_tr_b16 (no alias info on the
+      // intrinsic), which drained the DMA ring at each transposed read; the ring's
+      // counted waits (ring_wait_barrier*) order these loads instead
+      const uint32_t m0v = (uint32_t)(uintptr_t)(lds_vptr)dst;
+      asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
+                   :
+                   : "s"(m0v), "v"(vo), "s"(isa ? ra : rb), "s"(so)
+                   : "memory", "m0");
     } else {
-      const int so = i == 4 ? 0 : i == 5 ? sb1 : i == 6 ? sb2 : sb3;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_vptr)(d.lds + kRingHalf + (i - 4) * 4096), 16,
-                                               (TB && (i & 1)) ? d.vb1 : d.vb, so, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(isa ? ra : rb, (lds_vptr)dst, 16, vo, so, 0, 0);
     }
   };
   auto dma = [&](int s, int i) { dma_piece(dma_step(s), i); };
@@ -646,12 +661,20 @@ __global__ void __launch_bounds__(WNT, 1) k_gemm_w4r(W4Args wa) {
   // 8 tg + tq (+4), columns 4 tp .. +3 of the 16-row block)
   const int tg = lane >> 4, tq = (lane >> 2) & 3, tp = lane & 3;
   const int tr_base = (tg * 8 + tq) * 512 + tp * 8, tr_swz = tq | ((tg & 1) << 2);
+  // inline asm: with the intrinsic, hipcc put s_waitcnt vmcnt(0) before every transposed
+  // read (draining the DMA ring).  The compiler does not see these loads complete, so a
+  // fragment must only be used after a phase-end barrier (lgkmcnt(0)) -- which is how
+  // the ring consumes every fragment -- and the two halves must land in one register
+  // tuple without copies (checked in the .s: no v_mov between a read and the barrier)
   auto rd_t = [&](const unsigned char* half, int r0) {
-    typedef short v4s __attribute__((ext_vector_type(4)));
+    typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
     const unsigned char* p = half + tr_base + ((((r0 >> 4) ^ tr_swz)) << 5);
-    const v4s x0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(p));
-    const v4s x1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(p + 2048));
-    return __builtin_bit_cast(bf16x8, __builtin_shufflevector(x0, x1, 0, 1, 2, 3, 4, 5, 6, 7));
+    const uint32_t addr = (uint32_t)(uintptr_t)(lds_vptr)p;
+    u32x2_t x0, x1;
+    asm volatile("ds_read_b64_tr_b16 %0, %2\n\tds_read_b64_tr_b16 %1, %2 offset:2048"
+                 : "=&v"(x0), "=&v"(x1)
+                 : "v"(addr));
+    return __builtin_bit_cast(bf16x8, __builtin_shufflevector(x0, x1, 0, 1, 2, 3));
   };
   // read u (0, 1) of group grp (0..7): B blocks 2 grp + u (grp < 4), then A blocks
   auto rd1 = [&](int s, int grp, int u, bf16x8 (&fa)[8], bf16x8 (&fb)[8]) {
