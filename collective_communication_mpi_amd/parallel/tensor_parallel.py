@@ -19,10 +19,12 @@ collects (:76-187).  These autograd-aware modules generalise that to any
 Collectives run on the tensors' plane: CUDA tensors use the device plane
 (hand-written xGMI kernels, ``device_group_for``), CPU tensors the C++ host
 plane -- the reference's own CPU/NumPy setting.  CUDA bf16 GEMMs run on the
-MFMA kernels (``ops.gemm_nt`` forward / input gradient, ``ops.gemm_tn``
-weight gradient, fp32 accumulation) up to ~2^33 multiply-adds and on hipBLASLt
-(``torch.matmul``) above, where the library GEMM measured faster; other dtypes
-use ``torch.matmul``.
+hand-written MFMA kernels: forward ``ops.gemm_nt`` (the four-wave LDS-ring kernel
+for large shapes), input gradient dX = dY W and weight gradient dW = dY^T X on the
+ring kernel with K-major operands (``ops.gemm_ring``, no transposes), fp32
+accumulation, bf16 out (profiles/r3_gemm: 0.95-1.04x hipBLASLt on the Llama MLP
+backward shapes).  ``CCMPI_TP_GEMM=blas`` routes them to hipBLASLt instead; other
+dtypes use ``torch.matmul``.
 """
 from __future__ import annotations
 
@@ -31,7 +33,7 @@ import os
 
 import torch
 
-from ..ops import gemm_nt, gemm_tn, transpose
+from ..ops import gemm_nt, gemm_ring, gemm_tn, transpose
 from .layout import _host_comm, device_group_for
 
 
@@ -153,15 +155,11 @@ def scatter_to_tensor_parallel_region(x, comm):
     return _ScatterLastTP.apply(x, comm)
 
 
-# Plain (unfused) GEMMs of these layers: the hand-written MFMA kernels below ~2^33
-# multiply-adds, hipBLASLt (torch.matmul) above -- measured on the Llama-3-8B MLP shapes
-# (profiles/r2_tp_mlp/gemm_ab_mlp_shapes.txt: hipBLASLt 1.5-1.6 PF/s vs 1.1-1.3 for our
-# 256x256 kernel at 4096 x {4096..28672} x {4096..28672}); CCMPI_TP_GEMM=own|blas forces one.
-# Not with several ranks on one GPU: a rank's spinning collective CTAs next to the other
-# rank's hipBLASLt kernels stalled the TP = 2 step for seconds (profiles/r2_tp_mlp), while
-# the hand-written GEMMs co-run with them.
+# GEMMs of these layers: hand-written MFMA kernels (default, CCMPI_TP_GEMM=own|auto) or
+# hipBLASLt (CCMPI_TP_GEMM=blas, for A/B runs).  Round 2 routed every GEMM above 2^33
+# multiply-adds to hipBLASLt (our 256x256 kernel was at 0.70-0.86x on the Llama MLP
+# shapes); the LDS-ring kernel closed most of that gap (profiles/r3_gemm).
 _TP_GEMM = os.environ.get("CCMPI_TP_GEMM", "auto")
-_BLAS_MIN_MACS = 1 << 33
 
 
 def _gpu_shared(comm) -> bool:
@@ -176,11 +174,23 @@ def _mfma_ok(x: torch.Tensor, w: torch.Tensor, comm=None) -> bool:
     if not (x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16
             and x.shape[-1] % 8 == 0 and w.shape[0] % 8 == 0 and w.shape[1] % 8 == 0):
         return False
-    if _TP_GEMM == "own":
-        return True
-    if _TP_GEMM == "blas":
-        return False
-    return x.numel() * w.shape[0] < _BLAS_MIN_MACS or _gpu_shared(comm)
+    return _TP_GEMM != "blas"
+
+
+def _linear_backward(g2: torch.Tensor, x2: torch.Tensor, w: torch.Tensor, need_dx: bool, need_dw: bool):
+    """dX = dY W and dW = dY^T X (bf16 out, fp32 accumulate) on the LDS-ring kernel with
+    K-major operands; the older routes (transpose + NT kernel, 256x256 TN kernel) when
+    it does not apply (K % 64, alignment)."""
+    dx = dw = None
+    if need_dx:
+        dx = gemm_ring(g2, w, False, True)
+        if dx is None:
+            dx = gemm_nt(g2, transpose(w))
+    if need_dw:
+        dw = gemm_ring(g2, x2, True, True)
+        if dw is None:
+            dw = gemm_tn(g2, x2).to(w.dtype)
+    return dx, dw
 
 
 class _LinearFn(torch.autograd.Function):
@@ -213,10 +223,7 @@ class _LinearFn(torch.autograd.Function):
         g2 = g.reshape(-1, g.shape[-1]).contiguous()
         dx = dw = db = None
         if ctx.mfma and g2.dtype == torch.bfloat16:
-            if ctx.needs_input_grad[0]:
-                dx = gemm_nt(g2, transpose(w))                      # dX = dY . W
-            if ctx.needs_input_grad[1]:
-                dw = gemm_tn(g2, x2).to(w.dtype)                    # dW = dY^T . X (fp32 accumulate)
+            dx, dw = _linear_backward(g2, x2, w, ctx.needs_input_grad[0], ctx.needs_input_grad[1])
         else:
             if ctx.needs_input_grad[0]:
                 dx = g2 @ w
@@ -261,10 +268,9 @@ class _RowParallelFused(torch.autograd.Function):
         x2, w = ctx.saved_tensors
         g2 = g.reshape(-1, g.shape[-1]).contiguous()
         dx = dw = db = None
-        if ctx.needs_input_grad[0]:
-            dx = gemm_nt(g2, transpose(w)).reshape(*ctx.lead, w.shape[1])  # dX = dY . W
-        if ctx.needs_input_grad[1]:
-            dw = gemm_tn(g2, x2).to(w.dtype)                                 # dW = dY^T . X
+        dx, dw = _linear_backward(g2, x2, w, ctx.needs_input_grad[0], ctx.needs_input_grad[1])
+        if dx is not None:
+            dx = dx.reshape(*ctx.lead, w.shape[1])
         if ctx.has_bias and ctx.needs_input_grad[2]:
             db = g2.float().sum(0).to(g.dtype)
         return dx, dw, db, None

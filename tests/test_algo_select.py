@@ -89,8 +89,8 @@ def test_alltoallv_plan_offsets():
 
 
 def test_tp_gemm_routing(monkeypatch):
-    """TP layers: hand-written MFMA GEMMs below 2^33 multiply-adds and whenever ranks
-    share a GPU, hipBLASLt (torch.matmul) above; CCMPI_TP_GEMM forces either."""
+    """TP layers: hand-written MFMA GEMMs for every CUDA bf16 shape by default (the LDS-ring
+    kernel for large ones); CCMPI_TP_GEMM=blas routes to hipBLASLt; other dtypes never MFMA."""
     import torch
 
     from collective_communication_mpi_amd.parallel import tensor_parallel as tpm
@@ -98,14 +98,11 @@ def test_tp_gemm_routing(monkeypatch):
     x = SimpleNamespace(is_cuda=True, dtype=torch.bfloat16, shape=(4096, 4096), numel=lambda: 4096 * 4096)
     w_big = SimpleNamespace(dtype=torch.bfloat16, shape=(28672, 4096))
     w_small = SimpleNamespace(dtype=torch.bfloat16, shape=(256, 4096))
-    monkeypatch.setattr(tpm, "_TP_GEMM", "auto")
-    monkeypatch.setattr(tpm, "_gpu_shared", lambda comm: False)
-    assert tpm._mfma_ok(x, w_small) and not tpm._mfma_ok(x, w_big)
-    # the sharing decision is the TP group's own (DeviceGroup.shared_device), per group
-    monkeypatch.setattr(tpm, "_gpu_shared", lambda comm: comm == "shared-group")
-    assert tpm._mfma_ok(x, w_big, "shared-group") and not tpm._mfma_ok(x, w_big, "other-group")
-    monkeypatch.setattr(tpm, "_gpu_shared", lambda comm: False)
-    monkeypatch.setattr(tpm, "_TP_GEMM", "own")
-    assert tpm._mfma_ok(x, w_big)
+    for mode in ("auto", "own"):
+        monkeypatch.setattr(tpm, "_TP_GEMM", mode)
+        assert tpm._mfma_ok(x, w_small) and tpm._mfma_ok(x, w_big)
     monkeypatch.setattr(tpm, "_TP_GEMM", "blas")
-    assert not tpm._mfma_ok(x, w_small)
+    assert not tpm._mfma_ok(x, w_small) and not tpm._mfma_ok(x, w_big)
+    monkeypatch.setattr(tpm, "_TP_GEMM", "auto")
+    x32 = SimpleNamespace(is_cuda=True, dtype=torch.float32, shape=(4096, 4096), numel=lambda: 4096 * 4096)
+    assert not tpm._mfma_ok(x32, w_small)
