@@ -214,6 +214,13 @@ class DeviceGroup:
         keys = host_comm.allgather(key)
         self.ranks_per_device = keys.count(key)
         self.shared_device = self.ranks_per_device > 1
+        if self.shared_device:
+            # The LDS-ring GEMM needs a whole CU per workgroup (128 KiB LDS, 512 VGPRs a
+            # wave); next to another rank's spinning collective CTAs (one per CU) none of
+            # its workgroups can start, and the two ranks wait on each other (TP = 2 MLP
+            # on one GPU timed out, profiles/r3_tp2).  A process whose GPU is shared uses
+            # the smaller-footprint kernels instead.
+            self.D.gemm_set_ring_min(0)
         self._async_done = None  # (stream, event) of the last start()ed collective, until ordered
         self._inflight: List = []  # (done event, tensors) of start()ed collectives not yet known complete
         default_blocks = max(1, 512 // self.ranks_per_device)

@@ -177,17 +177,21 @@ def _mfma_ok(x: torch.Tensor, w: torch.Tensor, comm=None) -> bool:
     return _TP_GEMM != "blas"
 
 
-def _linear_backward(g2: torch.Tensor, x2: torch.Tensor, w: torch.Tensor, need_dx: bool, need_dw: bool):
+def _linear_backward(g2: torch.Tensor, x2: torch.Tensor, w: torch.Tensor, need_dx: bool, need_dw: bool,
+                     comm=None):
     """dX = dY W and dW = dY^T X (bf16 out, fp32 accumulate) on the LDS-ring kernel with
     K-major operands; the older routes (transpose + NT kernel, 256x256 TN kernel) when
-    it does not apply (K % 64, alignment)."""
+    it does not apply (K % 64, alignment) or when the TP group's ranks share a GPU (a
+    ring workgroup needs a whole CU and cannot start beside a peer's spinning
+    collective CTAs: DeviceGroup disables the ring GEMMs of such a process)."""
+    ring = not _gpu_shared(comm)
     dx = dw = None
     if need_dx:
-        dx = gemm_ring(g2, w, False, True)
+        dx = gemm_ring(g2, w, False, True) if ring else None
         if dx is None:
             dx = gemm_nt(g2, transpose(w))
     if need_dw:
-        dw = gemm_ring(g2, x2, True, True)
+        dw = gemm_ring(g2, x2, True, True) if ring else None
         if dw is None:
             dw = gemm_tn(g2, x2).to(w.dtype)
     return dx, dw
@@ -201,6 +205,7 @@ class _LinearFn(torch.autograd.Function):
         x2 = x.reshape(-1, x.shape[-1])
         if not x2.is_contiguous():
             x2 = x2.contiguous()
+        ctx.comm = comm
         ctx.save_for_backward(x2, w)
         ctx.has_bias = b is not None
         ctx.lead = x.shape[:-1]
@@ -223,7 +228,7 @@ class _LinearFn(torch.autograd.Function):
         g2 = g.reshape(-1, g.shape[-1]).contiguous()
         dx = dw = db = None
         if ctx.mfma and g2.dtype == torch.bfloat16:
-            dx, dw = _linear_backward(g2, x2, w, ctx.needs_input_grad[0], ctx.needs_input_grad[1])
+            dx, dw = _linear_backward(g2, x2, w, ctx.needs_input_grad[0], ctx.needs_input_grad[1], ctx.comm)
         else:
             if ctx.needs_input_grad[0]:
                 dx = g2 @ w
@@ -257,6 +262,7 @@ class _RowParallelFused(torch.autograd.Function):
         x2 = x.reshape(-1, x.shape[-1])
         if not x2.is_contiguous():
             x2 = x2.contiguous()
+        ctx.comm = comm
         ctx.save_for_backward(x2, w)
         ctx.has_bias = b is not None
         ctx.lead = x.shape[:-1]
@@ -268,7 +274,7 @@ class _RowParallelFused(torch.autograd.Function):
         x2, w = ctx.saved_tensors
         g2 = g.reshape(-1, g.shape[-1]).contiguous()
         dx = dw = db = None
-        dx, dw = _linear_backward(g2, x2, w, ctx.needs_input_grad[0], ctx.needs_input_grad[1])
+        dx, dw = _linear_backward(g2, x2, w, ctx.needs_input_grad[0], ctx.needs_input_grad[1], ctx.comm)
         if dx is not None:
             dx = dx.reshape(*ctx.lead, w.shape[1])
         if ctx.has_bias and ctx.needs_input_grad[2]:
