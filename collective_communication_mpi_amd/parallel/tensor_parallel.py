@@ -241,7 +241,11 @@ class _LinearFn(torch.autograd.Function):
         return dx, dw, db, None
 
 
-_TP_FUSED = os.environ.get("CCMPI_TP_FUSED", "1") != "0"
+# The row-parallel GEMM with its TP all-reduce fused into the epilogue (DeviceGroup.
+# gemm_allreduce) is opt-in: at TP = 2 on one shared GPU the Llama MLP forward took
+# 5.1 ms fused against 1.64 ms for GEMM + zero-copy all-reduce (profiles/r3_tp2); over
+# xGMI it is unmeasured.
+_TP_FUSED = os.environ.get("CCMPI_TP_FUSED", "0") == "1"
 
 
 def _fused_ok(x2: torch.Tensor, w: torch.Tensor, comm) -> bool:
