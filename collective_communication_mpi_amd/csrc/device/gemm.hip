@@ -935,8 +935,10 @@ void gemm_nt(uint64_t A, uint64_t B, uint64_t C, uint64_t bias, int M, int N, in
   }
   // auto: large bf16-out GEMMs on the four-wave LDS-ring kernel (gemm_w4.hip; measured
   // against the 256x256 ping-pong kernel in profiles/r3_gemm)
+  // (long K over at most one tile per CU stays on the 256x256 ping-pong kernel: 4096^2 x
+  // 28672 measured 1291-1368 TF/s there against 1224-1252 on the ring)
   if (g_kernel == 0 && splitk == 1 && g_ring_min_macs > 0 && (long long)M * N * K >= g_ring_min_macs &&
-      M >= 1024 && N >= 1024 && gemm_w4_ok(g) && gemm_w4r_fast(g)) {
+      M >= 1024 && N >= 1024 && !(K > 16384 && gemm_w4_tiles(M, N) <= 256) && gemm_w4_ok(g) && gemm_w4r_fast(g)) {
     launch_gemm_nt_w4r(g, reinterpret_cast<hipStream_t>(stream));
     CCMPI_HIP_CHECK(hipGetLastError());
     return;
