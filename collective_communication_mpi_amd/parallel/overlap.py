@@ -61,7 +61,16 @@ def dp_grad_overlap(comm, layers: int = 32, tokens: int = 4096, iters: int = 3, 
     emb = V * d  # LM head and token embedding: V x d each
     # flat layout: [LM head | layer L-1 | ... | layer 0 | embedding] = backward order
     n_total = per_layer * layers + 2 * emb
+
+    def say(msg: str) -> None:
+        if verbose and comm.Get_rank() == 0:
+            import sys
+
+            print(f"[dp_overlap] {msg}", file=sys.stderr, flush=True)
+
+    say(f"allocating {n_total * 2 / 1e9:.2f} GB of bf16 gradients (symmetric heap)")
     grads = dev.empty(n_total, torch.bfloat16)  # bf16 grads, symmetric heap (zero-copy all-reduce)
+    say("gradients registered")
     g = torch.Generator(device=dev.device).manual_seed(seed + comm.Get_rank())
     x_t = {k: (torch.randn(k, T, generator=g, device=dev.device) * 0.05).bfloat16() for k in {d, ff}}
     dy_t = {k: (torch.randn(k, T, generator=g, device=dev.device) * 0.05).bfloat16() for k in {d, kv, ff}}
@@ -109,10 +118,7 @@ def dp_grad_overlap(comm, layers: int = 32, tokens: int = 4096, iters: int = 3, 
         torch.cuda.current_stream().wait_stream(side)
 
     def timed(**kw) -> float:
-        if verbose and comm.Get_rank() == 0:
-            import sys
-
-            print(f"[dp_overlap] timing {kw} ...", file=sys.stderr, flush=True)
+        say(f"timing {kw} ...")
         backward(**kw)
         torch.cuda.synchronize()
         dev.check()

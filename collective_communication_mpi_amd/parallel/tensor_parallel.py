@@ -286,6 +286,16 @@ class _RowParallelFused(torch.autograd.Function):
         return dx, dw, db, None
 
 
+def _bind_device_group(comm, device) -> None:
+    """Collective, at construction (every rank builds the same layers): create the TP group's
+    device plane before the first GEMM, so a process that shares its GPU with other ranks
+    has switched its GEMMs off the whole-CU ring kernel (DeviceGroup) before any runs."""
+    if device is None or torch.device(device).type != "cuda":
+        return
+    if _size_rank(comm)[0] > 1:
+        device_group_for(comm)
+
+
 def _init_full(out_f: int, in_f: int, seed: int, dtype, bias: bool):
     """Full (unsharded) weights from a seeded CPU generator: identical on every rank."""
     gen = torch.Generator().manual_seed(seed)
@@ -311,6 +321,7 @@ class ColumnParallelLinear(torch.nn.Module):
         self.in_features, self.out_features = in_features, out_features
         self.gather_output = gather_output
         k = out_features // p
+        _bind_device_group(comm, device)
         w, b = _init_full(out_features, in_features, seed, dtype, bias)
         self.weight = torch.nn.Parameter(w[r * k:(r + 1) * k].contiguous().to(device))
         self.bias = torch.nn.Parameter(b[r * k:(r + 1) * k].contiguous().to(device)) if bias else None
@@ -337,6 +348,7 @@ class RowParallelLinear(torch.nn.Module):
         self.in_features, self.out_features = in_features, out_features
         self.input_is_parallel = input_is_parallel
         k = in_features // p
+        _bind_device_group(comm, device)
         w, b = _init_full(out_features, in_features, seed, dtype, bias)
         self.weight = torch.nn.Parameter(w[:, r * k:(r + 1) * k].contiguous().to(device))
         self.bias = torch.nn.Parameter(b.to(device)) if bias else None
