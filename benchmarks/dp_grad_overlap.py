@@ -25,6 +25,10 @@ ap.add_argument("--verbose", action="store_true")
 ap.add_argument("--blocks", type=int, default=0, help="CTA budget of the bucket all-reduces (0 = overlap_blocks)")
 ap.add_argument("--bucket-mb", type=int, default=0, help="max bucket size in MiB (0 = one bucket per layer)")
 args = ap.parse_args()
+if args.verbose:  # a stuck setup shows where it is stuck (every rank, every 90 s)
+    import faulthandler
+
+    faulthandler.dump_traceback_later(90, repeat=True)
 comm = Communicator(MPI.COMM_WORLD)
 local = int(os.environ.get("LOCAL_RANK", os.environ.get("CCMPI_LOCAL_RANK", "0")))
 torch.cuda.set_device(local % torch.cuda.device_count())

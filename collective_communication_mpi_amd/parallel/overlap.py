@@ -59,7 +59,7 @@ def dp_grad_overlap(comm, layers: int = 32, tokens: int = 4096, iters: int = 3, 
     shapes = layer_weight_shapes(d, kv, ff)
     per_layer = sum(a * b for a, b in shapes)
     emb = V * d  # LM head and token embedding: V x d each
-    # flat layout: [LM head | layer L-1 | ... | layer 0 | embedding] = backward order
+    # backward order: LM head, layer L-1 .. layer 0, embedding
     n_total = per_layer * layers + 2 * emb
 
     def say(msg: str) -> None:
@@ -68,9 +68,17 @@ def dp_grad_overlap(comm, layers: int = 32, tokens: int = 4096, iters: int = 3, 
 
             print(f"[dp_overlap] {msg}", file=sys.stderr, flush=True)
 
+    # gradients in symmetric-heap blocks of at most 512 MiB (zero-copy all-reduce): one per
+    # decoder layer (436 MB for Llama-3-8B) and row chunks of the LM head and embedding
+    # (one 3.85 GB registration hung in hipIpcOpenMemHandle with 2 ranks on one GPU,
+    # profiles/r3_dp2; ~0.5 GB blocks register fine)
     say(f"allocating {n_total * 2 / 1e9:.2f} GB of bf16 gradients (symmetric heap)")
-    grads = dev.empty(n_total, torch.bfloat16)  # bf16 grads, symmetric heap (zero-copy all-reduce)
-    say("gradients registered")
+    chunk_rows = max(1, (256 << 20) // max(d, 1))  # 512 MiB of bf16 rows
+    vchunks = [(r0, min(V, r0 + chunk_rows)) for r0 in range(0, V, chunk_rows)] if V else []
+    lm_g = [dev.empty((r1 - r0, d), torch.bfloat16) for r0, r1 in vchunks]
+    layer_g = [dev.empty(per_layer, torch.bfloat16) for _ in range(layers)]
+    emb_g = [dev.empty((r1 - r0, d), torch.bfloat16) for r0, r1 in vchunks]
+    say(f"gradients registered ({len(lm_g) + len(layer_g) + len(emb_g)} heap blocks)")
     g = torch.Generator(device=dev.device).manual_seed(seed + comm.Get_rank())
     x_t = {k: (torch.randn(k, T, generator=g, device=dev.device) * 0.05).bfloat16() for k in {d, ff}}
     dy_t = {k: (torch.randn(k, T, generator=g, device=dev.device) * 0.05).bfloat16() for k in {d, kv, ff}}
@@ -78,43 +86,49 @@ def dp_grad_overlap(comm, layers: int = 32, tokens: int = 4096, iters: int = 3, 
         dlogits_t = (torch.randn(V, T, generator=g, device=dev.device) * 0.05).bfloat16()  # [vocab, tokens]
         ids = torch.randint(0, V, (T,), generator=g, device=dev.device)
         dx0 = (torch.randn(T, d, generator=g, device=dev.device) * 0.05).bfloat16()  # grad of the embedded tokens
+        # per embedding chunk: the token positions whose id falls in it (host-side once)
+        sel = [((ids >= r0) & (ids < r1)).nonzero().flatten() for r0, r1 in vchunks]
+        emb_idx = [(ids[s_] - r0, dx0[s_]) for s_, (r0, _) in zip(sel, vchunks)]
     side = torch.cuda.Stream(device=dev.device, priority=priority)
     mb = max_blocks or dev.overlap_blocks
     events = [torch.cuda.Event() for _ in range(layers + 2)]
     # bucket length in elements, a multiple of 8 (16-B aligned bf16 buckets)
     step = None if bucket_mb <= 0 else max(8, ((bucket_mb << 20) // 2) // 8 * 8)
 
-    def reduce_range(ev, lo, hi) -> None:
+    def reduce_tensors(ev, ts) -> None:
         ev.record()
         side.wait_event(ev)
         with torch.cuda.stream(side):
-            st = step or (hi - lo)
-            for a in range(lo, hi, st):
-                seg = grads[a:min(hi, a + st)]
-                dev.allreduce(seg, seg, "SUM", algo, max_blocks=mb)
+            for t in ts:
+                flat = t.view(-1)
+                st = step or flat.numel()
+                for a in range(0, flat.numel(), st):
+                    seg = flat[a:a + st]
+                    dev.allreduce(seg, seg, "SUM", algo, max_blocks=mb)
 
     def backward(comm_on: bool, compute_on: bool = True) -> None:
         if V:  # LM head: the first gradient of the backward
             if compute_on:
-                gemm_nt(dlogits_t, x_t[d], out=grads[:emb].view(V, d))
+                for (r0, r1), gt in zip(vchunks, lm_g):
+                    gemm_nt(dlogits_t[r0:r1], x_t[d], out=gt)
             if comm_on:
-                reduce_range(events[layers], 0, emb)
-        for i, layer in enumerate(reversed(range(layers))):
-            base = emb + i * per_layer
+                reduce_tensors(events[layers], lm_g)
+        for layer in reversed(range(layers)):
+            gl = layer_g[layer]
             if compute_on:
-                o = base
+                o = 0
                 for fo, fi in shapes:
-                    gemm_nt(dy_t[fo], x_t[fi], out=grads[o:o + fo * fi].view(fo, fi))
+                    gemm_nt(dy_t[fo], x_t[fi], out=gl[o:o + fo * fi].view(fo, fi))
                     o += fo * fi
             if comm_on:
-                reduce_range(events[layer], base, base + per_layer)
+                reduce_tensors(events[layer], [gl])
         if V:  # token embedding: the last gradient (row scatter-add over the token ids)
-            eg = grads[n_total - emb:].view(V, d)
             if compute_on:
-                eg.zero_()
-                eg.index_add_(0, ids, dx0)
+                for gt, (rows, src) in zip(emb_g, emb_idx):
+                    gt.zero_()
+                    gt.index_add_(0, rows, src)
             if comm_on:
-                reduce_range(events[layers + 1], n_total - emb, n_total)
+                reduce_tensors(events[layers + 1], emb_g)
         torch.cuda.current_stream().wait_stream(side)
 
     def timed(**kw) -> float:
@@ -147,7 +161,7 @@ def dp_grad_overlap(comm, layers: int = 32, tokens: int = 4096, iters: int = 3, 
            "wgrad_TFLOPs": round(flops / t_compute / 1e12, 1), "shared_gpu": dev.shared_device,
            "comm_algbw_GBps": round(gbytes / t_comm / 1e9, 2) if t_comm else None, "algo": algo,
            "bucket_ctas": mb, "params": n_total, "vocab": V,
-           "buckets": sum((n + (step or n) - 1) // (step or n) for n in [per_layer] * layers + ([emb, emb] if V else [])),
+           "buckets": sum((t.numel() + (step or t.numel()) - 1) // (step or t.numel()) for t in lm_g + layer_g + emb_g),
            "bucket_MiB": round(min(step or per_layer, per_layer) * 2 / (1 << 20), 1)}
-    del grads, x_t, dy_t
+    del lm_g, layer_g, emb_g, x_t, dy_t
     return out
