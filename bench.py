@@ -333,7 +333,8 @@ def shared_dry_run(n: int, steps: int, warmup: int, verbose: bool):
     # the 8 ranks' streams oversubscribe the hardware queue slots and the scheduler time-
     # slices them: the DP4xTP2 forward measured 1.6-2.9 ms (1 queue: 0.60-0.62 ms, same
     # kernels; profiles/r3_dryrun).  One rank per GPU (the real N >= 2 run) keeps the default.
-    env.setdefault("GPU_MAX_HW_QUEUES", "1")
+    # (the box exports GPU_MAX_HW_QUEUES=4 itself, so this is set, not defaulted)
+    env["GPU_MAX_HW_QUEUES"] = os.environ.get("CCMPI_DRYRUN_HW_QUEUES", "1")
     try:
         r = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=480)
     except subprocess.TimeoutExpired:
