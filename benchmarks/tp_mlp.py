@@ -25,7 +25,7 @@ import torch  # noqa: E402
 
 from collective_communication_mpi_amd import MPI, Communicator  # noqa: E402
 from collective_communication_mpi_amd.parallel.tensor_parallel import (  # noqa: E402
-    ColumnParallelLinear, RowParallelLinear, all_reduce_)
+    ParallelSwiGLUMLP, all_reduce_)
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--tokens", type=int, default=4096)
@@ -33,6 +33,8 @@ ap.add_argument("--d", type=int, default=4096)
 ap.add_argument("--ffn", type=int, default=14336)
 ap.add_argument("--iters", type=int, default=10)
 ap.add_argument("--warmup", type=int, default=3)
+ap.add_argument("--eager-gate", action="store_true",
+                help="SwiGLU gate as eager torch ops (A/B against the fused HIP kernel)")
 args = ap.parse_args()
 comm = Communicator(MPI.COMM_WORLD)
 rank, p = comm.Get_rank(), comm.Get_size()
@@ -42,17 +44,14 @@ dev = torch.device("cuda", torch.cuda.current_device())
 hc = comm.comm
 T, d, f = args.tokens, args.d, args.ffn
 
-gate_up = ColumnParallelLinear(d, 2 * f, comm, bias=False, device=dev, dtype=torch.bfloat16, seed=1)
-down = RowParallelLinear(f, d, comm, bias=False, device=dev, dtype=torch.bfloat16, seed=2)
-k = f // p  # this rank's gate (first k) and up (next k) features: the column shard of [gate; up]
-# reorder the [gate; up] rows so each rank's shard holds matching gate and up features
-g0 = torch.Generator().manual_seed(1)
-full = ((torch.rand(2 * f, d, generator=g0) * 2 - 1) / d ** 0.5).to(torch.bfloat16)
-with torch.no_grad():
-    gate_up.weight.copy_(torch.cat([full[rank * k:(rank + 1) * k], full[f + rank * k:f + (rank + 1) * k]]).to(dev))
+mlp = ParallelSwiGLUMLP(d, f, comm, device=dev, dtype=torch.bfloat16, seed=1)
+gate_up, down = mlp.gate_up, mlp.down
+k = f // p
 
 
 def block(x):
+    if not args.eager_gate:
+        return mlp(x)
     h = gate_up(x)
     a = torch.nn.functional.silu(h[:, :k]) * h[:, k:]
     return down(a)
@@ -99,7 +98,7 @@ chk = float(y.float().abs().mean().item())
 flop_f = 2 * T * d * 2 * f + 2 * T * f * d  # whole block (all ranks together)
 if rank == 0:
     print(json.dumps({
-        "bench": "tp_mlp", "tp": p, "tokens": T, "d_model": d, "ffn": f, "dtype": "bf16",
+        "bench": "tp_mlp", "tp": p, "gate": "eager" if args.eager_gate else "fused", "tokens": T, "d_model": d, "ffn": f, "dtype": "bf16",
         "shared_gpu": comm.dev.shared_device if p > 1 else False,
         "fwd_ms": round(t_f * 1e3, 3), "fwd_bwd_ms": round(t_fb * 1e3, 3),
         "fwd_TFLOPs": round(flop_f / t_f / 1e12, 1), "fwd_bwd_TFLOPs": round(3 * flop_f / t_fb / 1e12, 1),

@@ -9,6 +9,7 @@ void register_gemm_ops(pybind11::module_& m);
 void register_attn_ops(pybind11::module_& m);
 void register_head_ops(pybind11::module_& m);
 void register_wgrad_ops(pybind11::module_& m);
+void register_swiglu_ops(pybind11::module_& m);
 
 void register_ops(pybind11::module_& m) {
   register_layout_ops(m);
@@ -16,6 +17,7 @@ void register_ops(pybind11::module_& m) {
   register_attn_ops(m);
   register_head_ops(m);
   register_wgrad_ops(m);
+  register_swiglu_ops(m);
 }
 
 }  // namespace dev

@@ -1,0 +1,113 @@
+// Fused SwiGLU gate for the Llama-style MLP between the column-parallel gate|up GEMM
+// and the row-parallel down GEMM (parallel/tensor_parallel.py ParallelSwiGLUMLP).
+//
+//   forward : a[t, j]  = silu(g) * u,            g = h[t, j], u = h[t, k + j]
+//   backward: dh[t, j] = da * u * s * (1 + g (1 - s)),  dh[t, k + j] = da * silu(g)
+//
+// h is the [T, 2k] bf16 output of the gate|up GEMM (this rank's gate features in the
+// first k columns, the matching up features in the next k).  Eager PyTorch spends
+// ~10 passes on this (strided silu, mul, and in backward two mul, silu_backward, two
+// zero-filled slice gradients and their sum: ~13 % of the TP MLP's GPU time,
+// profiles/r3_gemm/tp_mlp_own_kernel_stats.md); here it is one read of h (+ da) and
+// one write, 16-B vectors, fp32 math, one bf16 rounding per output.
+//
+// Grid: x = row t (no integer division), y = 256-vector column chunks.
+#include <pybind11/pybind11.h>
+
+#include "common.hpp"
+#include "ops.hpp"
+
+namespace ccmpi {
+namespace dev {
+
+namespace {
+
+__device__ __forceinline__ float sigmoid_fast(float x) {
+  return __builtin_amdgcn_rcpf(1.0f + __expf(-x));  // exp -> inf gives 0, exp -> 0 gives 1
+}
+
+__device__ __forceinline__ uint32_t pack_bf16(float lo, float hi) {
+  return f32_to_bf16_bits(lo) | (f32_to_bf16_bits(hi) << 16);
+}
+
+__global__ void __launch_bounds__(256) k_swiglu_fwd(const uint16_t* __restrict__ h, uint16_t* __restrict__ a,
+                                                    int kv, int64_t ldh, int64_t lda) {
+  const int j = blockIdx.y * 256 + threadIdx.x;  // 8-element vector index within the row
+  if (j >= kv) return;
+  const int64_t t = blockIdx.x;
+  const uint16_t* hr = h + t * ldh;
+  const u32x4 g = *reinterpret_cast<const u32x4*>(hr + 8 * (int64_t)j);
+  const u32x4 u = *reinterpret_cast<const u32x4*>(hr + 8 * ((int64_t)kv + j));
+  u32x4 r;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float g0 = bf16_lo(g[i]), g1 = bf16_hi(g[i]);
+    r[i] = pack_bf16(g0 * sigmoid_fast(g0) * bf16_lo(u[i]), g1 * sigmoid_fast(g1) * bf16_hi(u[i]));
+  }
+  *reinterpret_cast<u32x4*>(a + t * lda + 8 * (int64_t)j) = r;
+}
+
+__global__ void __launch_bounds__(256) k_swiglu_bwd(const uint16_t* __restrict__ h, const uint16_t* __restrict__ da,
+                                                    uint16_t* __restrict__ dh, int kv, int64_t ldh, int64_t ldda,
+                                                    int64_t lddh) {
+  const int j = blockIdx.y * 256 + threadIdx.x;
+  if (j >= kv) return;
+  const int64_t t = blockIdx.x;
+  const uint16_t* hr = h + t * ldh;
+  const u32x4 g = *reinterpret_cast<const u32x4*>(hr + 8 * (int64_t)j);
+  const u32x4 u = *reinterpret_cast<const u32x4*>(hr + 8 * ((int64_t)kv + j));
+  const u32x4 d = *reinterpret_cast<const u32x4*>(da + t * ldda + 8 * (int64_t)j);
+  u32x4 rg, ru;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    float dg2[2], du2[2];
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      const float gv = half ? bf16_hi(g[i]) : bf16_lo(g[i]);
+      const float uv = half ? bf16_hi(u[i]) : bf16_lo(u[i]);
+      const float dv = half ? bf16_hi(d[i]) : bf16_lo(d[i]);
+      const float s = sigmoid_fast(gv);
+      du2[half] = dv * gv * s;
+      dg2[half] = dv * uv * s * (1.0f + gv * (1.0f - s));
+    }
+    rg[i] = pack_bf16(dg2[0], dg2[1]);
+    ru[i] = pack_bf16(du2[0], du2[1]);
+  }
+  uint16_t* dr = dh + t * lddh;
+  *reinterpret_cast<u32x4*>(dr + 8 * (int64_t)j) = rg;
+  *reinterpret_cast<u32x4*>(dr + 8 * ((int64_t)kv + j)) = ru;
+}
+
+void check(uint64_t T, uint64_t k, uint64_t ptrs, uint64_t lds) {
+  if (k % 8 || (ptrs | (lds * 2)) % 16)
+    throw std::invalid_argument("swiglu: k % 8 == 0, 16-B aligned pointers and row strides required");
+  if (T > 0x7fffffffull || k / 8 > 256ull * 65535ull)
+    throw std::invalid_argument("swiglu: too many rows or columns for the grid");
+}
+
+}  // namespace
+
+void register_swiglu_ops(pybind11::module_& m) {
+  m.def("swiglu_fwd", [](uint64_t h, uint64_t a, uint64_t T, uint64_t k, int64_t ldh, int64_t lda, uint64_t stream) {
+    check(T, k, h | a, (uint64_t)(ldh | lda));
+    if (T == 0 || k == 0) return;
+    const int kv = (int)(k / 8);
+    hipLaunchKernelGGL(k_swiglu_fwd, dim3((unsigned)T, (kv + 255) / 256), dim3(256), 0,
+                       reinterpret_cast<hipStream_t>(stream), reinterpret_cast<const uint16_t*>(h),
+                       reinterpret_cast<uint16_t*>(a), kv, ldh, lda);
+    CCMPI_HIP_CHECK(hipGetLastError());
+  }, "a[T, k] = silu(h[:, :k]) * h[:, k:2k] (bf16, element strides ldh / lda)");
+  m.def("swiglu_bwd", [](uint64_t h, uint64_t da, uint64_t dh, uint64_t T, uint64_t k, int64_t ldh, int64_t ldda,
+                         int64_t lddh, uint64_t stream) {
+    check(T, k, h | da | dh, (uint64_t)(ldh | ldda | lddh));
+    if (T == 0 || k == 0) return;
+    const int kv = (int)(k / 8);
+    hipLaunchKernelGGL(k_swiglu_bwd, dim3((unsigned)T, (kv + 255) / 256), dim3(256), 0,
+                       reinterpret_cast<hipStream_t>(stream), reinterpret_cast<const uint16_t*>(h),
+                       reinterpret_cast<const uint16_t*>(da), reinterpret_cast<uint16_t*>(dh), kv, ldh, ldda, lddh);
+    CCMPI_HIP_CHECK(hipGetLastError());
+  }, "dh[T, 2k] from h[T, 2k] and da[T, k] (SwiGLU backward, bf16)");
+}
+
+}  // namespace dev
+}  // namespace ccmpi

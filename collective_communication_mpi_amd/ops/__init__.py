@@ -7,6 +7,7 @@ from .kernels import (  # noqa: F401
     gemm_tn,
     gemm_ring,
     linear,
+    swiglu,
     transpose,
     interleave_lastaxis,
     deinterleave_lastaxis,

@@ -180,6 +180,51 @@ def transpose(x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tens
     return out
 
 
+def _swiglu_rows(t: torch.Tensor) -> torch.Tensor:
+    """2-D view ``[rows, cols]`` with unit column stride (copies only if it must)."""
+    t2 = t.reshape(-1, t.shape[-1])
+    ok = t2.stride(1) == 1 and t2.stride(0) % 8 == 0 and t2.data_ptr() % 16 == 0
+    return t2 if ok else t2.contiguous()
+
+
+class _SwiGLU(torch.autograd.Function):
+    """``silu(h[..., :k]) * h[..., k:]`` in one HIP kernel each way (csrc/device/swiglu.hip);
+    saves only ``h`` (the gate|up GEMM output), backward writes ``dh`` in one pass."""
+
+    @staticmethod
+    def forward(ctx, h):
+        h2 = _swiglu_rows(h)
+        k = h2.shape[1] // 2
+        a = torch.empty(*h.shape[:-1], k, dtype=h.dtype, device=h.device)
+        _D().swiglu_fwd(h2.data_ptr(), a.data_ptr(), h2.shape[0], k, h2.stride(0), k, _stream(h2))
+        ctx.save_for_backward(h2)
+        ctx.lead = h.shape[:-1]
+        return a
+
+    @staticmethod
+    def backward(ctx, da):
+        (h2,) = ctx.saved_tensors
+        k = h2.shape[1] // 2
+        da2 = _swiglu_rows(da)
+        dh = torch.empty(*ctx.lead, 2 * k, dtype=h2.dtype, device=h2.device)
+        _D().swiglu_bwd(h2.data_ptr(), da2.data_ptr(), dh.data_ptr(), h2.shape[0], k, h2.stride(0), da2.stride(0),
+                        2 * k, _stream(h2))
+        return dh
+
+
+def swiglu(h: torch.Tensor) -> torch.Tensor:
+    """SwiGLU gate of a ``[..., 2k]`` gate|up tensor: ``silu(h[..., :k]) * h[..., k:]``.
+
+    CUDA bf16 with ``k % 8 == 0`` runs the fused HIP kernels (fp32 math, one bf16
+    rounding); anything else (CPU, other dtypes) is computed by torch ops."""
+    if h.shape[-1] % 2:
+        raise ValueError("swiglu needs an even last dimension (gate | up)")
+    k = h.shape[-1] // 2
+    if h.is_cuda and h.dtype == torch.bfloat16 and k % 8 == 0 and h.data_ptr() % 16 == 0:
+        return _SwiGLU.apply(h)
+    return torch.nn.functional.silu(h[..., :k]) * h[..., k:]
+
+
 def interleave_lastaxis(stage: torch.Tensor, p: int) -> torch.Tensor:
     """``[p, *lead, k] -> [*lead, p*k]`` (np.concatenate(parts, axis=-1))."""
     stage = stage.contiguous()

@@ -33,7 +33,7 @@ import os
 
 import torch
 
-from ..ops import gemm_nt, gemm_ring, gemm_tn, transpose
+from ..ops import gemm_nt, gemm_ring, gemm_tn, swiglu, transpose
 from .layout import _host_comm, device_group_for
 
 
@@ -363,6 +363,33 @@ class RowParallelLinear(torch.nn.Module):
         return y + self.bias if self.bias is not None else y
 
 
+class ParallelSwiGLUMLP(torch.nn.Module):
+    """Llama MLP block ``y = W_down (silu(W_gate x) * W_up x)`` over a TP group.
+
+    ``gate_up`` is one ``ColumnParallelLinear`` whose rank-r shard holds gate features
+    ``[r k, (r+1) k)`` followed by the SAME up features (k = ffn / p), so the SwiGLU gate
+    is local; it runs as one fused HIP kernel each way (``ops.swiglu``).  ``down`` is a
+    ``RowParallelLinear`` over those k features: one TP all-reduce in forward (Megatron
+    "g"), one in backward for dX of ``gate_up`` (Megatron "f").  The reference's TP layer
+    (model/func_impl.py:65-109) on a realistic Llama-3-8B shape."""
+
+    def __init__(self, d_model: int, ffn: int, comm, device=None, dtype=torch.bfloat16, seed: int = 0):
+        super().__init__()
+        p, r = _size_rank(comm)
+        if ffn % p:
+            raise ValueError(f"ffn {ffn} not divisible by TP size {p}")
+        k = ffn // p
+        self.comm, self.p, self.r, self.ffn = comm, p, r, ffn
+        self.gate_up = ColumnParallelLinear(d_model, 2 * ffn, comm, bias=False, device=device, dtype=dtype, seed=seed)
+        full, _ = _init_full(2 * ffn, d_model, seed, dtype, False)
+        with torch.no_grad():  # shard = [gate rows of rank r; up rows of rank r]
+            self.gate_up.weight.copy_(torch.cat([full[r * k:(r + 1) * k], full[ffn + r * k:ffn + (r + 1) * k]]))
+        self.down = RowParallelLinear(ffn, d_model, comm, bias=False, device=device, dtype=dtype, seed=seed + 1)
+
+    def forward(self, x):
+        return self.down(swiglu(self.gate_up(x)))
+
+
 def full_weight(layer, comm) -> torch.Tensor:
     """Reassemble the unsharded weight of a Column/RowParallelLinear (collective)."""
     w = layer.weight.detach()
@@ -379,6 +406,6 @@ def sharded_grad_full(layer, comm) -> torch.Tensor:
     return torch.cat(parts, dim=dim)
 
 
-__all__ = ["ColumnParallelLinear", "RowParallelLinear", "all_reduce_", "copy_to_tensor_parallel_region",
+__all__ = ["ColumnParallelLinear", "RowParallelLinear", "ParallelSwiGLUMLP", "all_reduce_", "copy_to_tensor_parallel_region",
            "reduce_from_tensor_parallel_region", "gather_from_tensor_parallel_region",
            "scatter_to_tensor_parallel_region", "full_weight", "sharded_grad_full"]

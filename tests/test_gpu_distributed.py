@@ -183,6 +183,14 @@ def test_harness_checkpoint_resume(tmp_path):
     np.testing.assert_allclose(lc, la[3:], rtol=2e-3, atol=1e-4)
 
 
+@pytest.mark.parametrize("n", [1, 2])
+def test_parallel_swiglu_mlp_gpu(n):
+    """ParallelSwiGLUMLP on the device plane: MFMA GEMMs, fused SwiGLU HIP kernels, TP
+    all-reduces, vs single-process fp32 autograd (tests/workers/swiglu_mlp_worker.py)."""
+    r = run_ranks(n, py("tests/workers/swiglu_mlp_worker.py", "--device", "cuda"), timeout=300, env=ENV)
+    assert "swiglu mlp OK" in r.stdout
+
+
 @pytest.mark.parametrize("n", [2, 4])
 def test_tensor_parallel_layers_and_ddp_gpu(n):
     """Column/RowParallelLinear (MFMA bf16 GEMMs, device TP collectives) + bucketed DDP

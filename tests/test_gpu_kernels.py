@@ -569,3 +569,32 @@ def test_gemm_ring_layouts(ta, tb, M, N, K):
     c0 = c.clone()
     gemm_ring(a, b, bool(ta), bool(tb), out=c, accumulate=True)
     torch.testing.assert_close(c, c0 + ref, rtol=2e-3, atol=5e-2)
+
+
+@pytest.mark.parametrize("T,k", [(1, 8), (7, 24), (4096, 1792), (3, 2056), (513, 14336 // 8)])
+def test_swiglu_fwd_bwd_vs_fp32(T, k):
+    """Fused SwiGLU kernels (csrc/device/swiglu.hip) against fp32 autograd of silu(g) * u."""
+    from collective_communication_mpi_amd.ops import swiglu
+
+    g = torch.Generator(device="cuda").manual_seed(T * 31 + k)
+    h = (torch.randn(T, 2 * k, device="cuda", generator=g) * 3).bfloat16().requires_grad_(True)
+    da = torch.randn(T, k, device="cuda", generator=g).bfloat16()
+    a = swiglu(h)
+    a.backward(da)
+    hf = h.detach().float().requires_grad_(True)
+    ref = torch.nn.functional.silu(hf[:, :k]) * hf[:, k:]
+    ref.backward(da.float())
+    assert a.dtype == torch.bfloat16 and a.shape == (T, k)
+    torch.testing.assert_close(a.float(), ref, rtol=1.6e-2, atol=1e-2)
+    torch.testing.assert_close(h.grad.float(), hf.grad, rtol=1.6e-2, atol=2e-2)
+
+
+def test_swiglu_strided_and_batched():
+    """3-D input and a row-strided view (the gate|up slice of a wider buffer) take the kernel."""
+    from collective_communication_mpi_amd.ops import swiglu
+
+    g = torch.Generator(device="cuda").manual_seed(5)
+    wide = torch.randn(2, 64, 3 * 128, device="cuda", generator=g).bfloat16()
+    h = wide[..., :256]  # row stride 384 elements, 16-B aligned
+    ref = torch.nn.functional.silu(h[..., :128].float()) * h[..., 128:].float()
+    torch.testing.assert_close(swiglu(h).float(), ref, rtol=1.6e-2, atol=1e-2)

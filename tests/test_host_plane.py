@@ -111,6 +111,14 @@ def test_runs_under_torchrun():
     assert "host plane OK at 4 ranks" in r.stdout
 
 
+@pytest.mark.parametrize("n", [1, 2, 4])
+def test_parallel_swiglu_mlp_cpu(n):
+    """ParallelSwiGLUMLP (gate|up column shard with matching gate and up features, SwiGLU,
+    row-parallel down) on the host plane vs single-process fp32 autograd."""
+    r = run_ranks(n, py("tests/workers/swiglu_mlp_worker.py", "--device", "cpu"), timeout=300)
+    assert "swiglu mlp OK" in r.stdout
+
+
 @pytest.mark.parametrize("n", [1, 2, 3, 4, 8])
 def test_tensor_parallel_layers_and_ddp_cpu(n):
     """Column/RowParallelLinear + bucketed DistributedDataParallel on the host plane
