@@ -953,6 +953,9 @@ void gemm_nt(uint64_t A, uint64_t B, uint64_t C, uint64_t bias, int M, int N, in
     // epilogues the 128x128 kernel matches 256x256 up to ~256 tiles and for short K;
     // 256x256 wins with >= 2 tiles per CU and K >= 1024
     else if (gemm256_tiles(M, N, 256) * splitk >= 512 && K >= 1024 && M >= 1024 && N >= 1024) bn = 256;
+    // the long-K case the ring kernel leaves to this one (above): 4096^2 x 28672 ran 0.99 ms
+    // on the 128x128 kernel against 0.75 ms here (profiles/r3_swiglu/gemm_sweep.txt)
+    else if (splitk == 1 && K > 16384 && M >= 1024 && N >= 1024 && gemm_w4_tiles(M, N) <= 256) bn = 256;
     if (bn) {
       launch_gemm_nt_256(g, bn, reinterpret_cast<hipStream_t>(stream));
       CCMPI_HIP_CHECK(hipGetLastError());
