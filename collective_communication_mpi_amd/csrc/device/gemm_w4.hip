@@ -53,6 +53,8 @@ struct W4Args {
   int group_m;  // tile rows per group of the group-M order
   FusedArgs f;  // FUSED only
   unsigned long long* dbg;  // STAMP diagnostic builds only: 4 cycle counts per wave
+  uint16_t* glu;  // EPI 2 only: silu(gate) * up of each interleaved (gate, up) column pair
+  int ldglu;
 };
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t op_rsrc(const uint16_t* base, long rows, int ld) {
@@ -577,6 +579,9 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t op_rsrc_t(const uint16_t* X, i
 
 // EPI 1: bf16 out, C = alpha * AB^T, no bias / activation / accumulate (fast epilogue,
 // exactly 32 store instructions per wave and tile); EPI 0: the generic epilogue.
+// EPI 2: EPI 1 plus the SwiGLU gate of interleaved (gate, up) output column pairs:
+// glu[r, c / 2] = silu(C[r, c]) * C[r, c + 1] for even c, from the bf16-rounded C (the
+// values the unfused gate would read), one 8-B store next to each 16-B row store.
 // ABL (diagnostic ablations, wrong results): bit 0 drops the steady-state DMA, bit 1 the
 // steady-state fragment reads.  STAMP (diagnostic): per wave, s_memtime cycles of the
 // prologue, main loop, epilogue and the phase-end waits -> wa.dbg (first tile only).
@@ -787,7 +792,7 @@ __global__ void __launch_bounds__(WNT, 1) k_gemm_w4r(W4Args wa) {
       for (int j = 0; j < 8; ++j) mfma(i, j, a1r[i], b1[j]);
     if (STAMP) t_epi = __builtin_amdgcn_s_memtime();
 
-    if constexpr (EPI == 1) {
+    if constexpr (EPI == 1 || EPI == 2) {
       // ---- fast epilogue: per 32-row pass, bf16 pairs -> slab (slot 3, 8 KiB per wave,
       // 16-B chunk c of row r at c ^ (r & 15)) -> 16-B row vectors -> buffer stores
       unsigned char* slab = smem + 3 * kRing + wave * 8192;
@@ -815,8 +820,19 @@ __global__ void __launch_bounds__(WNT, 1) k_gemm_w4r(W4Args wa) {
         for (int it = 0; it < 8; ++it) {
           const int rl = it * 4 + grp;
           const u32x4 w = *reinterpret_cast<const u32x4*>(slab + rl * 256 + ((lr ^ (rl & 15)) << 4));
-          if (col_ok && h * 32 + rl < rows_left)
+          if (col_ok && h * 32 + rl < rows_left) {
             *reinterpret_cast<u32x4*>(cptr + (size_t)(h * 32 + rl) * ldc) = w;
+            if constexpr (EPI == 2) {
+              float gl[4];
+#pragma unroll
+              for (int q = 0; q < 4; ++q) {
+                const float gv = __uint_as_float(w[q] << 16), uv = __uint_as_float(w[q] & 0xffff0000u);
+                gl[q] = gv * __builtin_amdgcn_rcpf(1.0f + __expf(-gv)) * uv;
+              }
+              uint16_t* gp = wa.glu + (size_t)(bm + wr * 128 + h * 32 + rl) * wa.ldglu + (ccol >> 1);
+              *reinterpret_cast<uint2*>(gp) = uint2{cvt_pk_bf16(gl[0], gl[1]), cvt_pk_bf16(gl[2], gl[3])};
+            }
+          }
         }
       }
     } else {
@@ -895,7 +911,7 @@ __global__ void __launch_bounds__(WNT, 1) k_gemm_w4r(W4Args wa) {
     // the next tile's first steps (slots 0..2; the slab is slot 3): the stores above are
     // older than them, so the top-of-tile wait for step 0 also retires the stores
     const int next = lt + (int)gridDim.x;
-    const bool more = PERSIST && EPI == 1 && next < ntiles;
+    const bool more = PERSIST && (EPI == 1 || EPI == 2) && next < ntiles;
     int ntm = 0, ntn = 0;
     if (more) {
       tile_coords(next, tiles_m, tiles_n, wa.group_m, ntm, ntn);
@@ -979,7 +995,7 @@ bool gemm_ring_ok(const GemmArgs& g, int ta, int tb) {
   return a_bytes < 0x7ffffff0l && b_bytes < 0x7ffffff0l;
 }
 
-void launch_gemm_ring(const GemmArgs& g, int ta, int tb, hipStream_t stream) {
+void launch_gemm_ring(const GemmArgs& g, int ta, int tb, hipStream_t stream, uint16_t* glu, int ldglu) {
   // explicit ring schedule (gemm_set_kernel(5) + sched bit 3) or the auto defaults
   const int sched = (g_w4_sched & 8) ? g_w4_sched : g_ring_sched;
   static int cus = [] {
@@ -991,6 +1007,7 @@ void launch_gemm_ring(const GemmArgs& g, int ta, int tb, hipStream_t stream) {
     w4r_attr(reinterpret_cast<const void*>(k_gemm_w4r<0, 0>));
     w4r_attr(reinterpret_cast<const void*>(k_gemm_w4r<1, 0>));
     w4r_attr(reinterpret_cast<const void*>(k_gemm_w4r<1, 1>));
+    w4r_attr(reinterpret_cast<const void*>(k_gemm_w4r<2, 0>));
     w4r_attr(reinterpret_cast<const void*>(k_gemm_w4r<1, 0, 1>));
     w4r_attr(reinterpret_cast<const void*>(k_gemm_w4r<1, 0, 2>));
     w4r_attr(reinterpret_cast<const void*>(k_gemm_w4r<1, 0, 3>));
@@ -1006,8 +1023,13 @@ void launch_gemm_ring(const GemmArgs& g, int ta, int tb, hipStream_t stream) {
   }();
   (void)attr;
   const int ntiles = gemm_w4_tiles(g.M, g.N);
-  W4Args a{g, g_w4_group_m, {}, g_w4_dbg};
+  W4Args a{g, g_w4_group_m, {}, g_w4_dbg, glu, ldglu};
   const bool fast = gemm_w4r_fast(g);
+  if (glu) {  // SwiGLU epilogue (callers check gemm_w4r_fast and the glu layout first)
+    if (!fast || ta || tb) throw std::invalid_argument("gemm ring: the SwiGLU epilogue needs the fast NT form");
+    hipLaunchKernelGGL((k_gemm_w4r<2, 0>), dim3(ntiles), dim3(WNT), kRingLds, stream, a);
+    return;
+  }
   const bool persist = fast && (sched & 1);
   const int grid = persist ? std::min(ntiles, cus) : ntiles;
   const int abl = (sched >> 5) & 3;

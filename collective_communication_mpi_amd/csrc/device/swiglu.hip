@@ -12,9 +12,15 @@
 // one write, 16-B vectors, fp32 math, one bf16 rounding per output.
 //
 // Grid: x = row t (no integer division), y = 256-vector column chunks.
+//
+// Interleaved layout (ParallelSwiGLUMLP): h[t, 2j] = gate j, h[t, 2j + 1] = up j, so
+// the gate|up GEMM's own epilogue can apply the gate (gemm_w4.hip EPI 2,
+// `gemm_nt_swiglu`): each 16-B row vector of C holds 4 whole pairs.  `*_il` kernels are
+// the unfused forms of that layout (other GEMM routes) and its backward.
 #include <pybind11/pybind11.h>
 
 #include "common.hpp"
+#include "gemm_common.hpp"
 #include "ops.hpp"
 
 namespace ccmpi {
@@ -78,6 +84,42 @@ __global__ void __launch_bounds__(256) k_swiglu_bwd(const uint16_t* __restrict__
   *reinterpret_cast<u32x4*>(dr + 8 * ((int64_t)kv + j)) = ru;
 }
 
+// interleaved pairs: thread = 4 pairs (16 B of h, 8 B of a / da)
+__global__ void __launch_bounds__(256) k_swiglu_fwd_il(const uint16_t* __restrict__ h, uint16_t* __restrict__ a,
+                                                       int nv, int64_t ldh, int64_t lda) {
+  const int j = blockIdx.y * 256 + threadIdx.x;
+  if (j >= nv) return;
+  const int64_t t = blockIdx.x;
+  const u32x4 w = *reinterpret_cast<const u32x4*>(h + t * ldh + 8 * (int64_t)j);
+  float r[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const float gv = bf16_lo(w[q]);
+    r[q] = gv * sigmoid_fast(gv) * bf16_hi(w[q]);
+  }
+  *reinterpret_cast<uint2*>(a + t * lda + 4 * (int64_t)j) = uint2{pack_bf16(r[0], r[1]), pack_bf16(r[2], r[3])};
+}
+
+__global__ void __launch_bounds__(256) k_swiglu_bwd_il(const uint16_t* __restrict__ h, const uint16_t* __restrict__ da,
+                                                       uint16_t* __restrict__ dh, int nv, int64_t ldh, int64_t ldda,
+                                                       int64_t lddh) {
+  const int j = blockIdx.y * 256 + threadIdx.x;
+  if (j >= nv) return;
+  const int64_t t = blockIdx.x;
+  const u32x4 w = *reinterpret_cast<const u32x4*>(h + t * ldh + 8 * (int64_t)j);
+  const uint2 d2 = *reinterpret_cast<const uint2*>(da + t * ldda + 4 * (int64_t)j);
+  const uint32_t dd[2] = {d2.x, d2.y};
+  u32x4 r;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const float gv = bf16_lo(w[q]), uv = bf16_hi(w[q]);
+    const float dv = (q & 1) ? bf16_hi(dd[q >> 1]) : bf16_lo(dd[q >> 1]);
+    const float sg = sigmoid_fast(gv);
+    r[q] = pack_bf16(dv * uv * sg * (1.0f + gv * (1.0f - sg)), dv * gv * sg);
+  }
+  *reinterpret_cast<u32x4*>(dh + t * lddh + 8 * (int64_t)j) = r;
+}
+
 void check(uint64_t T, uint64_t k, uint64_t ptrs, uint64_t lds) {
   if (k % 8 || (ptrs | (lds * 2)) % 16)
     throw std::invalid_argument("swiglu: k % 8 == 0, 16-B aligned pointers and row strides required");
@@ -85,9 +127,51 @@ void check(uint64_t T, uint64_t k, uint64_t ptrs, uint64_t lds) {
     throw std::invalid_argument("swiglu: too many rows or columns for the grid");
 }
 
+void check_il(uint64_t T, uint64_t k, uint64_t hptrs, uint64_t hld, uint64_t aptrs, uint64_t ald) {
+  if (k % 4 || (hptrs | (hld * 2)) % 16 || (aptrs | (ald * 2)) % 8)
+    throw std::invalid_argument("swiglu (interleaved): k % 4 == 0, 16-B aligned h rows, 8-B aligned a rows required");
+  if (T > 0x7fffffffull || k / 4 > 256ull * 65535ull)
+    throw std::invalid_argument("swiglu: too many rows or columns for the grid");
+}
+
 }  // namespace
 
 void register_swiglu_ops(pybind11::module_& m) {
+  m.def("swiglu_fwd_il", [](uint64_t h, uint64_t a, uint64_t T, uint64_t k, int64_t ldh, int64_t lda, uint64_t stream) {
+    check_il(T, k, h, (uint64_t)ldh, a, (uint64_t)lda);
+    if (T == 0 || k == 0) return;
+    const int nv = (int)(k / 4);
+    hipLaunchKernelGGL(k_swiglu_fwd_il, dim3((unsigned)T, (nv + 255) / 256), dim3(256), 0,
+                       reinterpret_cast<hipStream_t>(stream), reinterpret_cast<const uint16_t*>(h),
+                       reinterpret_cast<uint16_t*>(a), nv, ldh, lda);
+    CCMPI_HIP_CHECK(hipGetLastError());
+  }, "a[T, k] = silu(h[:, 0::2]) * h[:, 1::2] (interleaved gate/up pairs, bf16)");
+  m.def("swiglu_bwd_il", [](uint64_t h, uint64_t da, uint64_t dh, uint64_t T, uint64_t k, int64_t ldh, int64_t ldda,
+                            int64_t lddh, uint64_t stream) {
+    check_il(T, k, h | dh, (uint64_t)(ldh | lddh), da, (uint64_t)ldda);
+    if (T == 0 || k == 0) return;
+    const int nv = (int)(k / 4);
+    hipLaunchKernelGGL(k_swiglu_bwd_il, dim3((unsigned)T, (nv + 255) / 256), dim3(256), 0,
+                       reinterpret_cast<hipStream_t>(stream), reinterpret_cast<const uint16_t*>(h),
+                       reinterpret_cast<const uint16_t*>(da), reinterpret_cast<uint16_t*>(dh), nv, ldh, ldda, lddh);
+    CCMPI_HIP_CHECK(hipGetLastError());
+  }, "dh[T, 2k] (interleaved pairs) from h[T, 2k] and da[T, k]");
+  // C[M, N] = A[M, K] B[N, K]^T (bf16) on the LDS-ring kernel with the SwiGLU epilogue:
+  // glu[M, N / 2] from C's interleaved (gate, up) column pairs.  False (nothing launched)
+  // when the ring kernel's fast form does not apply; the caller then runs gemm_nt +
+  // swiglu_fwd_il.
+  m.def("gemm_nt_swiglu", [](uint64_t A, uint64_t B, uint64_t C, uint64_t glu, int M, int N, int K, int lda, int ldb,
+                             int ldc, int ldglu, uint64_t stream) {
+    if (M <= 0 || N <= 0) return true;
+    gemm::GemmArgs g{reinterpret_cast<const uint16_t*>(A), reinterpret_cast<const uint16_t*>(B),
+                     reinterpret_cast<void*>(C), nullptr, M, N, K, lda, ldb, ldc, 1.0f, 0, 0, 0, 1, 1};
+    if (N % 8 || glu % 8 || ldglu % 4 || (int64_t)ldglu * 2 < N / 2 * 2 || !gemm::gemm_ring_ok(g, 0, 0) ||
+        !gemm::gemm_w4_ok(g) || !gemm::gemm_w4r_fast(g))
+      return false;
+    gemm::launch_gemm_ring(g, 0, 0, reinterpret_cast<hipStream_t>(stream), reinterpret_cast<uint16_t*>(glu), ldglu);
+    CCMPI_HIP_CHECK(hipGetLastError());
+    return true;
+  }, "bf16 NT GEMM with the SwiGLU gate of interleaved column pairs in its epilogue (ring kernel)");
   m.def("swiglu_fwd", [](uint64_t h, uint64_t a, uint64_t T, uint64_t k, int64_t ldh, int64_t lda, uint64_t stream) {
     check(T, k, h | a, (uint64_t)(ldh | lda));
     if (T == 0 || k == 0) return;

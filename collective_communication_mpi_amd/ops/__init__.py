@@ -8,6 +8,9 @@ from .kernels import (  # noqa: F401
     gemm_ring,
     linear,
     swiglu,
+    swiglu_pairs,
+    swiglu_pairs_backward,
+    gemm_nt_swiglu,
     transpose,
     interleave_lastaxis,
     deinterleave_lastaxis,

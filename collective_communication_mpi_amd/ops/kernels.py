@@ -225,6 +225,39 @@ def swiglu(h: torch.Tensor) -> torch.Tensor:
     return torch.nn.functional.silu(h[..., :k]) * h[..., k:]
 
 
+def swiglu_pairs(h: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """SwiGLU gate of interleaved (gate, up) pairs: ``silu(h[:, 0::2]) * h[:, 1::2]``
+    (``h`` [T, 2k] bf16 CUDA, row-contiguous; one HIP kernel, no autograd)."""
+    T, n = h.shape
+    if out is None:
+        out = torch.empty((T, n // 2), dtype=h.dtype, device=h.device)
+    _D().swiglu_fwd_il(h.data_ptr(), out.data_ptr(), T, n // 2, h.stride(0), out.stride(0), _stream(h))
+    return out
+
+
+def swiglu_pairs_backward(h: torch.Tensor, da: torch.Tensor) -> torch.Tensor:
+    """Gradient of ``swiglu_pairs`` w.r.t. its interleaved input (one HIP kernel)."""
+    T, n = h.shape
+    da = da if (da.stride(1) == 1 and da.stride(0) % 4 == 0) else da.contiguous()
+    dh = torch.empty_like(h)
+    _D().swiglu_bwd_il(h.data_ptr(), da.data_ptr(), dh.data_ptr(), T, n // 2, h.stride(0), da.stride(0),
+                       dh.stride(0), _stream(h))
+    return dh
+
+
+def gemm_nt_swiglu(a: torch.Tensor, b: torch.Tensor, h: torch.Tensor, glu: torch.Tensor) -> bool:
+    """``h = a @ b.T`` (bf16) with the SwiGLU gate of h's interleaved column pairs written
+    to ``glu`` by the GEMM's own epilogue (LDS-ring kernel, csrc/device/gemm_w4.hip EPI 2).
+    Returns False (nothing launched) when the ring kernel's fast form does not apply."""
+    M, K = a.shape
+    N = b.shape[0]
+    if not (a.stride(1) == 1 and b.stride(1) == 1 and h.shape == (M, N) and h.stride(1) == 1
+            and glu.shape == (M, N // 2) and glu.stride(1) == 1):
+        return False
+    return bool(_D().gemm_nt_swiglu(a.data_ptr(), b.data_ptr(), h.data_ptr(), glu.data_ptr(), M, N, K, a.stride(0),
+                                    b.stride(0), h.stride(0), glu.stride(0), _stream(a)))
+
+
 def interleave_lastaxis(stage: torch.Tensor, p: int) -> torch.Tensor:
     """``[p, *lead, k] -> [*lead, p*k]`` (np.concatenate(parts, axis=-1))."""
     stage = stage.contiguous()

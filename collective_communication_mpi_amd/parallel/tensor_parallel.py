@@ -33,7 +33,7 @@ import os
 
 import torch
 
-from ..ops import gemm_nt, gemm_ring, gemm_tn, swiglu, transpose
+from ..ops import gemm_nt, gemm_nt_swiglu, gemm_ring, gemm_tn, swiglu_pairs, swiglu_pairs_backward, transpose
 from .layout import _host_comm, device_group_for
 
 
@@ -363,13 +363,56 @@ class RowParallelLinear(torch.nn.Module):
         return y + self.bias if self.bias is not None else y
 
 
+class _GateUpSwiGLU(torch.autograd.Function):
+    """``a = swiglu_pairs(x W^T)`` for a gate|up weight whose rows are interleaved (gate j,
+    up j) pairs.  Forward: one GEMM whose epilogue also writes the gate (LDS-ring kernel,
+    EPI 2), else GEMM + ``swiglu_pairs``; saves x, W and the GEMM output h.  Backward:
+    ``swiglu_pairs_backward`` (one kernel) then dX / dW as ``_LinearFn``."""
+
+    @staticmethod
+    def forward(ctx, x, w, comm):
+        x2 = x.reshape(-1, x.shape[-1])
+        if not x2.is_contiguous():
+            x2 = x2.contiguous()
+        M, N = x2.shape[0], w.shape[0]
+        h = torch.empty(M, N, device=x.device, dtype=x.dtype)
+        a = torch.empty(*x.shape[:-1], N // 2, device=x.device, dtype=x.dtype)
+        a2 = a.view(M, N // 2)
+        ctx.mfma = _mfma_ok(x2, w, comm)  # False: hipBLASLt GEMMs (CCMPI_TP_GEMM=blas A/B runs)
+        fused = ctx.mfma and M > 0 and not _gpu_shared(comm) and gemm_nt_swiglu(x2, w, h, a2)
+        if not fused:
+            if ctx.mfma:
+                gemm_nt(x2, w, out=h)
+            else:
+                torch.matmul(x2, w.t(), out=h)
+            swiglu_pairs(h, out=a2)
+        ctx.comm = comm
+        ctx.lead = x.shape[:-1]
+        ctx.save_for_backward(x2, w, h)
+        return a
+
+    @staticmethod
+    def backward(ctx, da):
+        x2, w, h = ctx.saved_tensors
+        dh = swiglu_pairs_backward(h, da.reshape(-1, da.shape[-1]))
+        if ctx.mfma:
+            dx, dw = _linear_backward(dh, x2, w, ctx.needs_input_grad[0], ctx.needs_input_grad[1], ctx.comm)
+        else:
+            dx = dh @ w if ctx.needs_input_grad[0] else None
+            dw = dh.t() @ x2 if ctx.needs_input_grad[1] else None
+        if dx is not None:
+            dx = dx.reshape(*ctx.lead, w.shape[1])
+        return dx, dw, None
+
+
 class ParallelSwiGLUMLP(torch.nn.Module):
     """Llama MLP block ``y = W_down (silu(W_gate x) * W_up x)`` over a TP group.
 
-    ``gate_up`` is one ``ColumnParallelLinear`` whose rank-r shard holds gate features
-    ``[r k, (r+1) k)`` followed by the SAME up features (k = ffn / p), so the SwiGLU gate
-    is local; it runs as one fused HIP kernel each way (``ops.swiglu``).  ``down`` is a
-    ``RowParallelLinear`` over those k features: one TP all-reduce in forward (Megatron
+    ``gate_up`` is one ``ColumnParallelLinear`` whose rank-r shard holds the gate and up
+    features ``[r k, (r+1) k)`` (k = ffn / p) as interleaved rows (gate j, up j), so the
+    SwiGLU gate is local and, on CUDA bf16, applied by the gate|up GEMM's own epilogue
+    (``ops.gemm_nt_swiglu``; backward one ``swiglu_pairs_backward`` kernel).  ``down`` is
+    a ``RowParallelLinear`` over those k features: one TP all-reduce in forward (Megatron
     "g"), one in backward for dX of ``gate_up`` (Megatron "f").  The reference's TP layer
     (model/func_impl.py:65-109) on a realistic Llama-3-8B shape."""
 
@@ -382,12 +425,23 @@ class ParallelSwiGLUMLP(torch.nn.Module):
         self.comm, self.p, self.r, self.ffn = comm, p, r, ffn
         self.gate_up = ColumnParallelLinear(d_model, 2 * ffn, comm, bias=False, device=device, dtype=dtype, seed=seed)
         full, _ = _init_full(2 * ffn, d_model, seed, dtype, False)
-        with torch.no_grad():  # shard = [gate rows of rank r; up rows of rank r]
-            self.gate_up.weight.copy_(torch.cat([full[r * k:(r + 1) * k], full[ffn + r * k:ffn + (r + 1) * k]]))
+        with torch.no_grad():  # shard rows: gate r k + j at 2 j, up r k + j at 2 j + 1
+            shard = torch.stack([full[r * k:(r + 1) * k], full[ffn + r * k:ffn + (r + 1) * k]], dim=1)
+            self.gate_up.weight.copy_(shard.reshape(2 * k, d_model))
         self.down = RowParallelLinear(ffn, d_model, comm, bias=False, device=device, dtype=dtype, seed=seed + 1)
 
+    def _fused_ok(self, x) -> bool:
+        w = self.gate_up.weight
+        return (x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16
+                and (w.shape[0] // 2) % 4 == 0)
+
     def forward(self, x):
-        return self.down(swiglu(self.gate_up(x)))
+        if self._fused_ok(x):
+            a = _GateUpSwiGLU.apply(copy_to_tensor_parallel_region(x, self.comm), self.gate_up.weight, self.comm)
+        else:
+            h = self.gate_up(x)
+            a = torch.nn.functional.silu(h[..., 0::2]) * h[..., 1::2]
+        return self.down(a)
 
 
 def full_weight(layer, comm) -> torch.Tensor:

@@ -5,7 +5,7 @@
 set -o pipefail
 cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
-OUT=gpurun_out/r3_swiglu
+OUT=gpurun_out/${OUT_TAG:-r3_swiglu}
 mkdir -p $OUT
 timeout -k 10 400 python -u -m pytest -x -v --timeout 200 --timeout-method thread \
   tests/test_gpu_kernels.py tests/test_gpu_distributed.py -k "swiglu" > $OUT/tests.log 2>&1

@@ -598,3 +598,34 @@ def test_swiglu_strided_and_batched():
     h = wide[..., :256]  # row stride 384 elements, 16-B aligned
     ref = torch.nn.functional.silu(h[..., :128].float()) * h[..., 128:].float()
     torch.testing.assert_close(swiglu(h).float(), ref, rtol=1.6e-2, atol=1e-2)
+
+
+@pytest.mark.parametrize("M,N,K", [(4096, 2048, 512), (300, 520, 128), (1000, 2056, 64), (257, 264, 192)])
+def test_gemm_nt_swiglu_epilogue(M, N, K):
+    """Ring GEMM with the SwiGLU gate of interleaved column pairs in its epilogue (EPI 2):
+    h = A B^T vs fp32, gate vs silu / mul of the bf16 h, edge tiles in M and N."""
+    from collective_communication_mpi_amd.ops import gemm_nt_swiglu
+
+    g = torch.Generator(device="cuda").manual_seed(M + N + K)
+    a = torch.randn(M, K, device="cuda", generator=g).bfloat16()
+    b = (torch.randn(N, K, device="cuda", generator=g) / K ** 0.5).bfloat16()
+    h = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    glu = torch.empty(M, N // 2, device="cuda", dtype=torch.bfloat16)
+    assert gemm_nt_swiglu(a, b, h, glu), "the ring kernel's fast form should apply"
+    torch.testing.assert_close(h.float(), _ref(a, b), rtol=1.6e-2, atol=2e-2)
+    hf = h.float()
+    ref = torch.nn.functional.silu(hf[:, 0::2]) * hf[:, 1::2]
+    torch.testing.assert_close(glu.float(), ref, rtol=1.6e-2, atol=1e-2)
+
+
+def test_swiglu_pairs_fwd_bwd():
+    from collective_communication_mpi_amd.ops import swiglu_pairs, swiglu_pairs_backward
+
+    g = torch.Generator(device="cuda").manual_seed(9)
+    h = (torch.randn(777, 2 * 1028, device="cuda", generator=g) * 3).bfloat16()
+    da = torch.randn(777, 1028, device="cuda", generator=g).bfloat16()
+    hf = h.float().requires_grad_(True)
+    ref = torch.nn.functional.silu(hf[:, 0::2]) * hf[:, 1::2]
+    ref.backward(da.float())
+    torch.testing.assert_close(swiglu_pairs(h).float(), ref.detach(), rtol=1.6e-2, atol=1e-2)
+    torch.testing.assert_close(swiglu_pairs_backward(h, da).float(), hf.grad, rtol=1.6e-2, atol=2e-2)

@@ -4,7 +4,7 @@
     scripts/mpirun -n 2 python tests/workers/swiglu_mlp_worker.py --device cuda
 
 Forward output on every rank, dX, and the gate|up / down weight gradients (reassembled
-from the shards: rank r holds gate rows [r k, (r+1) k) then the matching up rows) against
+from the shards: rank r holds gate and up rows [r k, (r+1) k) as interleaved pairs) against
 fp32 autograd of ``W_down (silu(W_gate x) * W_up x)`` with the unsharded weights.
 Prints "swiglu mlp OK" on success."""
 import argparse
@@ -64,7 +64,7 @@ if rel(x.grad, xr.grad) > tol:
     fails.append(f"dx rel err {rel(x.grad, xr.grad)}")
 k = F // p
 gu = hc.allgather(mlp.gate_up.weight.grad.detach().float().cpu())
-g_full = torch.cat([s[:k] for s in gu] + [s[k:] for s in gu])  # [gate; up] of the full layer
+g_full = torch.cat([s[0::2] for s in gu] + [s[1::2] for s in gu])  # shards interleave (gate j, up j) rows
 if rel(g_full, wgu.grad) > tol:
     fails.append(f"d W_gate_up rel err {rel(g_full, wgu.grad)}")
 gd = torch.cat(hc.allgather(mlp.down.weight.grad.detach().float().cpu()), dim=1)
