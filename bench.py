@@ -80,15 +80,18 @@ def parse():
     ap.add_argument("--dp-vocab", type=int, default=1,
                     help="DP overlap: include the LM head and token embedding gradients (Llama-3-8B: 16.06 GB total)")
     ap.add_argument("--a2a-mb", type=int, default=256)
+    ap.add_argument("--mlp-tokens", type=int, default=4096,
+                    help="tokens of the TP Llama-3-8B MLP record (tp_mlp: TP over all ranks; 0 = off)")
     ap.add_argument("--shared-dry-run", type=int, default=8, help="N=1: ranks of the shared-GPU dry run (0 = off)")
     ap.add_argument("--no-harness", action="store_true")
     ap.add_argument("--no-secondary", action="store_true")
     ap.add_argument("--verbose", action="store_true")
-    ap.add_argument("--phase", default="", choices=["", "custom", "dp", "rccl"],
+    ap.add_argument("--phase", default="", choices=["", "custom", "dp", "mlp", "rccl"],
                     help="internal: which child phase this process runs (set by the supervisor)")
     ap.add_argument("--result", default="", help="internal: where a child phase writes its JSON")
     ap.add_argument("--rccl-timeout", type=float, default=300.0, help="wall-clock budget of the RCCL phase (s)")
     ap.add_argument("--dp-timeout", type=float, default=420.0, help="wall-clock budget of the DP-overlap phase (s)")
+    ap.add_argument("--mlp-timeout", type=float, default=240.0, help="wall-clock budget of the TP MLP phase (s)")
     ap.add_argument("--custom-timeout", type=float, default=1500.0, help="wall-clock budget of phase 1 (s)")
     ap.add_argument("--no-rccl", action="store_true", help="skip the RCCL baseline phase")
     return ap.parse_args()
@@ -163,6 +166,8 @@ def supervise(args) -> int:
     phases = [("custom", args.custom_timeout)]
     if size > 1 and args.dp_layers > 0 and not args.no_secondary:
         phases.append(("dp", args.dp_timeout))
+    if size > 1 and args.mlp_tokens > 0 and not args.no_secondary:
+        phases.append(("mlp", args.mlp_timeout))
     if size > 1 and not args.no_rccl:
         phases.append(("rccl", args.rccl_timeout))
     status = {}
@@ -199,6 +204,10 @@ def supervise(args) -> int:
             dr = load("dp") if status["dp"]["ok"] else None
             out.setdefault("config", {})["dp_overlap"] = dr if dr is not None else {
                 "error": f"DP-overlap phase failed or timed out: {status['dp']}"}
+        if "mlp" in status:
+            mr = load("mlp") if status["mlp"]["ok"] else None
+            out.setdefault("config", {})["tp_mlp"] = mr if mr is not None else {
+                "error": f"TP MLP phase failed or timed out: {status['mlp']}"}
         if "rccl" in status:
             rr = load("rccl") if status["rccl"]["ok"] else None
             merge_rccl(out, rr, status["rccl"])
@@ -251,6 +260,22 @@ def dp_phase(args) -> dict:
     torch.cuda.set_device(local % torch.cuda.device_count())
     return dp_grad_overlap(comm, layers=args.dp_layers, tokens=args.dp_tokens, iters=2, algo="auto",
                            verbose=args.verbose, vocab=bool(args.dp_vocab))
+
+
+def mlp_phase(args) -> dict:
+    """Phase 3: the Llama-3-8B MLP block (ParallelSwiGLUMLP) with TP over every rank on
+    fresh ranks: hand-written MFMA GEMMs (SwiGLU gate in the gate|up epilogue) and the TP
+    all-reduces of the reference's TP layer, over xGMI when each rank has its own GPU."""
+    os.environ.setdefault("CCMPI_DEVICE_TIMEOUT_S", "20")
+    import torch
+
+    from collective_communication_mpi_amd import MPI, Communicator
+    from collective_communication_mpi_amd.parallel.mlp_bench import measure_tp_mlp
+
+    comm = Communicator(MPI.COMM_WORLD)
+    local = int(os.environ.get("LOCAL_RANK", os.environ.get("CCMPI_LOCAL_RANK", "0")))
+    torch.cuda.set_device(local % torch.cuda.device_count())
+    return measure_tp_mlp(comm, tokens=args.mlp_tokens, iters=10, warmup=3)
 
 
 def rccl_phase(args) -> dict:
@@ -327,7 +352,7 @@ def shared_dry_run(n: int, steps: int, warmup: int, verbose: bool):
     """Run this bench with n ranks on this GPU (the N >= 2 path) and return its JSON."""
     cmd = [sys.executable, "-m", "collective_communication_mpi_amd.launch", "-n", str(n), "--timeout", "420",
            sys.executable, os.path.abspath(__file__), "--gpus", str(n), "--steps", str(steps), "--warmup", str(warmup),
-           "--dp-layers", "0", "--a2a-mb", "64", "--shared-dry-run", "0", "--no-rccl"]
+           "--dp-layers", "0", "--a2a-mb", "64", "--shared-dry-run", "0", "--no-rccl", "--mlp-tokens", "0"]
     env = dict(os.environ, CCMPI_BENCH_CHILD="1")
     # Hardware queues per process: with the box default (4) the 8 ranks' streams
     # oversubscribe the queue slots and the DP4xTP2 forward measured 1.6-2.9 ms; one queue
@@ -377,10 +402,10 @@ def main() -> int:
         return relaunch(args.gpus)
     if launched and not args.phase:
         return supervise(args)
-    if args.phase in ("rccl", "dp"):
+    if args.phase in ("rccl", "dp", "mlp"):
         rank = _env_rank()[0]
         try:
-            out = rccl_phase(args) if args.phase == "rccl" else dp_phase(args)
+            out = {"rccl": rccl_phase, "dp": dp_phase, "mlp": mlp_phase}[args.phase](args)
         except Exception as e:  # noqa: BLE001 - recorded in the merged line
             out = {"error": f"{type(e).__name__}: {e}"[:400]}
         _write_result(args, rank, out)
@@ -577,6 +602,17 @@ def main() -> int:
                     other[f"{name}_error"] = f"{type(e).__name__}: {e}"[:200]
             harness["fc_o_variants"] = other
 
+    mlp = None
+    if world == 1 and args.mlp_tokens > 0 and not args.no_secondary:
+        # one rank: the block runs in this process (no collective, nothing that can hang)
+        from collective_communication_mpi_amd.parallel.mlp_bench import measure_tp_mlp
+
+        try:
+            mlp = measure_tp_mlp(comm, tokens=args.mlp_tokens, iters=10, warmup=3)
+        except Exception as e:  # noqa: BLE001 - a secondary number must not cost the line
+            mlp = {"error": f"{type(e).__name__}: {e}"[:300]}
+        log(f"tp_mlp: {mlp}")
+
     dry = None
     if world == 1 and args.shared_dry_run > 1 and not args.no_secondary and torch.cuda.device_count() >= 1:
         dry = shared_dry_run(args.shared_dry_run, steps=5, warmup=2, verbose=args.verbose)
@@ -620,6 +656,8 @@ def main() -> int:
             out["config"]["tp_fwd_step_ms"] = round(harness["fwd_ms"], 4)
             out["config"]["tp_train_step_ms"] = round(harness.get("train_ms", float("nan")), 4)
             out["config"]["harness"] = {k: v for k, v in harness.items() if k not in ("fwd_ms", "train_ms")}
+        if mlp is not None:
+            out["config"]["tp_mlp"] = mlp
         if dry is not None:
             out["config"]["shared_gpu_dry_run"] = dry
         _write_result(args, rank, out)

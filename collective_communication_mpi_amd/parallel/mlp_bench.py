@@ -1,0 +1,79 @@
+"""Tensor-parallel Llama-3-8B MLP block measurement (``ParallelSwiGLUMLP``), shared by
+``benchmarks/tp_mlp.py`` and ``bench.py`` (its ``tp_mlp`` record, one TP group over all
+ranks: over xGMI when each rank has its own GPU).
+
+The block is ``y = W_down (silu(W_gate x) * W_up x)``; the gate|up GEMM carries the SwiGLU
+gate in its epilogue, the down GEMM's partial output is summed by one TP all-reduce
+(forward) and dX of gate|up by another (backward).  This is the reference's TP layer
+(model/func_impl.py:65-109: column-parallel projections, row-parallel output, collective
+between) on a realistic shape."""
+from __future__ import annotations
+
+import statistics
+import time
+from typing import Dict
+
+import torch
+
+from .tensor_parallel import ParallelSwiGLUMLP, all_reduce_
+
+
+def measure_tp_mlp(comm, tokens: int = 4096, d: int = 4096, ffn: int = 14336, iters: int = 10, warmup: int = 3,
+                   eager_gate: bool = False) -> Dict:
+    """Median forward and forward + backward times (max over ranks), the whole group's
+    model TFLOP/s, and the T x d bf16 TP all-reduce alone.  Collective: every rank calls."""
+    from .. import mpi as MPI
+
+    hc = comm.comm
+    p = comm.Get_size()
+    dev = torch.device("cuda", torch.cuda.current_device())
+    mlp = ParallelSwiGLUMLP(d, ffn, comm, device=dev, dtype=torch.bfloat16, seed=1)
+    gate_up, down = mlp.gate_up, mlp.down
+
+    def block(x):
+        if not eager_gate:
+            return mlp(x)
+        h = gate_up(x)
+        return down(torch.nn.functional.silu(h[:, 0::2]) * h[:, 1::2])  # shard rows are (gate, up) pairs
+
+    x = (torch.randn(tokens, d, generator=torch.Generator().manual_seed(3)) * 0.5).to(torch.bfloat16).to(dev)
+    x.requires_grad_(True)
+    gy = (torch.randn(tokens, d, generator=torch.Generator().manual_seed(4)) * 0.01).to(torch.bfloat16).to(dev)
+
+    def timed(fn):
+        for _ in range(warmup):
+            fn()
+        ts = []
+        for _ in range(iters):
+            torch.cuda.synchronize()
+            hc.Barrier()
+            t0 = time.perf_counter()
+            fn()
+            torch.cuda.synchronize()
+            ts.append(time.perf_counter() - t0)
+        return hc.allreduce(statistics.median(ts), op=MPI.MAX)
+
+    def fwd():
+        with torch.no_grad():
+            block(x)
+
+    def fwd_bwd():
+        x.grad = None
+        gate_up.weight.grad = None
+        down.weight.grad = None
+        block(x).backward(gy)
+
+    t_f = timed(fwd)
+    t_fb = timed(fwd_bwd)
+    buf = torch.randn(tokens, d, device=dev).to(torch.bfloat16)
+    t_ar = timed(lambda: all_reduce_(buf, comm)) if p > 1 else 0.0
+    with torch.no_grad():  # checksum: identical across TP degrees up to bf16 rounding
+        chk = float(block(x).float().abs().mean().item())
+    flop_f = 2 * tokens * d * 2 * ffn + 2 * tokens * ffn * d  # whole block (all ranks together)
+    return {
+        "tp": p, "gate": "eager" if eager_gate else "fused", "tokens": tokens, "d_model": d, "ffn": ffn,
+        "dtype": "bf16", "shared_gpu": bool(comm.dev.shared_device) if p > 1 else False,
+        "fwd_ms": round(t_f * 1e3, 3), "fwd_bwd_ms": round(t_fb * 1e3, 3),
+        "fwd_TFLOPs": round(flop_f / t_f / 1e12, 1), "fwd_bwd_TFLOPs": round(3 * flop_f / t_fb / 1e12, 1),
+        "tp_allreduce_bytes": tokens * d * 2, "tp_allreduce_ms": round(t_ar * 1e3, 3),
+        "out_abs_mean": round(chk, 6)}

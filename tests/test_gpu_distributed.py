@@ -200,7 +200,7 @@ def test_tensor_parallel_layers_and_ddp_gpu(n):
 
 
 def test_bench_multi_rank_path_shared_gpu():
-    """bench.py's N >= 2 path (candidate loop, bf16, all-to-all, DP overlap, TP harness)
+    """bench.py's N >= 2 path (candidate loop, bf16, all-to-all, DP overlap, TP harness, TP MLP)
     with 4 ranks on this GPU, so an 8-GPU run is never the first execution of it."""
     import json
     import subprocess
@@ -210,7 +210,8 @@ def test_bench_multi_rank_path_shared_gpu():
 
     e = dict(os.environ, **ENV)
     r = subprocess.run([sys.executable, "bench.py", "--gpus", "4", "--steps", "3", "--warmup", "1", "--size-mb", "64",
-                        "--a2a-mb", "16", "--dp-layers", "1", "--dp-tokens", "1024", "--dp-vocab", "0", "--batch", "256"],
+                        "--a2a-mb", "16", "--dp-layers", "1", "--dp-tokens", "1024", "--dp-vocab", "0", "--batch", "256",
+                        "--mlp-tokens", "512"],
                        cwd=REPO, env=e, capture_output=True, text=True, timeout=400)
     assert r.returncode == 0, r.stderr[-4000:]
     out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
@@ -221,3 +222,4 @@ def test_bench_multi_rank_path_shared_gpu():
     assert c["bf16_1GiB"]["algbw_GBps"] > 0 and c["alltoall"]["ms"] > 0
     assert 0.0 <= c["dp_overlap"]["comm_hidden_fraction"] <= 1.0
     assert c["parallelism"] == "dp2xtp2" and c["tp_fwd_step_ms"] > 0
+    assert c["tp_mlp"]["tp"] == 4 and c["tp_mlp"]["fwd_bwd_ms"] > 0, c["tp_mlp"]  # TP MLP phase over all ranks
