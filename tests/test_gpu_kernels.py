@@ -629,3 +629,16 @@ def test_swiglu_pairs_fwd_bwd():
     ref.backward(da.float())
     torch.testing.assert_close(swiglu_pairs(h).float(), ref.detach(), rtol=1.6e-2, atol=1e-2)
     torch.testing.assert_close(swiglu_pairs_backward(h, da).float(), hf.grad, rtol=1.6e-2, atol=2e-2)
+
+
+def test_gemm_nt_long_k_dispatch():
+    """Long K over at most one 256x256 tile per CU: gemm_nt auto takes the 256x256 kernel
+    (gemm.hip dispatch, profiles/r3_swiglu/gemm_sweep.txt); numerics vs fp32."""
+    from collective_communication_mpi_amd.ops import gemm_nt
+
+    g = torch.Generator(device="cuda").manual_seed(77)
+    M, N, K = 1024, 1280, 16512
+    a = torch.randn(M, K, device="cuda", generator=g).bfloat16()
+    b = (torch.randn(N, K, device="cuda", generator=g) / K ** 0.5).bfloat16()
+    y = gemm_nt(a, b, out_dtype=torch.bfloat16)
+    torch.testing.assert_close(y.float(), _ref(a, b), rtol=1.6e-2, atol=2e-2)
