@@ -7,7 +7,7 @@
 Metric (BASELINE.json): "all-reduce algbw (GB/s) @1GiB fp32 + DP4xTP2 fwd step time".
 
 * A step = one out-of-place all-reduce (SUM) of a 1 GiB fp32 buffer through the
-  framework's device all-reduce.  Buffers come from the symmetric heap
+  framework's HAND-WRITTEN device all-reduce.  Buffers come from the symmetric heap
   (``comm.empty``), the way framework users allocate communication buffers.
   ``value`` = algbw = 1 GiB / (time per all-reduce), the NCCL-tests convention:
   a property of the whole collective, identical for every rank.  Per-GPU work
@@ -18,31 +18,35 @@ Metric (BASELINE.json): "all-reduce algbw (GB/s) @1GiB fp32 + DP4xTP2 fwd step t
   so fp32 sums are exact) before it is timed: the hand-written two-shot and
   fan-out two-shot over IPC-mapped xGMI peer memory at several CTA budgets, the
   push two-shot, the hand-written multi-ring and recursive halving/doubling
-  kernels.  Every candidate's time is reported.
-* RCCL (the library baseline, the role MPI's built-ins play in the reference's
-  mpi-test.py:42-98,178-239) never shares a process with the hand-written
-  measurements.  With N >= 2 every rank's ``bench.py`` process is a supervisor
-  that never touches the GPU: it starts phase 1 (hand-written collectives,
-  harness, DP overlap) as a child process, then phase 2 (RCCL all-reduce fp32 /
-  bf16, all-to-all, pairwise send/recv) as a second child group of N fresh
-  ranks with a hard wall-clock budget (``--rccl-timeout``).  A hang or error in
-  RCCL costs only its own numbers: the line still carries every hand-written
-  number and ``rccl: {"error": ...}``.  ``value`` is the best all-reduce
-  algbw of either phase (the framework exposes both), with the hand-written
-  best and RCCL's reported separately.
-* Secondary (BASELINE configs 2-5):
-  - ``bf16_1GiB``: the same all-reduce on a 1 GiB bf16 buffer;
-  - ``alltoall_256MiB``: all-to-all of 256 MiB per rank (pull, push, RCCL, pairwise);
-  - ``harness``: the DP x TP transformer-layer forward (HIP graph) and train step,
-    TP=2 x DP=N/2 for N >= 2 (DP4xTP2 at N = 8);
-  - ``dp_overlap``: Llama-3-8B-sized bf16 gradient all-reduce (32 layers, 14 GB)
-    overlapped with the wgrad GEMMs (parallel/overlap.py), N >= 2;
-  - ``shared_gpu_dry_run`` (N = 1 only): the N >= 2 code path -- the same
-    candidate loop minus RCCL, which refuses ranks sharing a GPU -- run with 8
-    ranks on this one GPU, so the 8-GPU path is exercised before any 8-GPU run.
-    Its numbers measure HBM + protocol, not xGMI.  The DP-overlap part is left
-    out there (8 processes' side-stream collectives next to their GEMMs on one
-    GPU time out; it is measured at 2 ranks: profiles/r2_overlap).
+  kernels.  Every candidate's time is reported.  At N >= 2 a size sweep
+  (``DeviceGroup.tune``) follows, written as a tuning table that every later
+  phase's device groups load (``CCMPI_TUNE_FILE``), so ``algo="auto"`` in the TP
+  and DDP layers uses what was measured on this node.
+* Every measurement runs in a supervised child phase of fresh processes (the
+  process that ``bench.py`` starts never touches the GPU), each under its own
+  wall-clock budget; rank 0 merges their JSON records into the one output line.
+  A phase that crashes, hangs or errors costs only its own entry:
+
+  ====================  =========================================================
+  ``coll``              the headline (hand-written all-reduce candidates, 1 GiB
+                        fp32) + bf16 + all-to-all 256 MiB/rank + tuning sweep
+  ``harness``           DP x TP transformer-layer forward (HIP graph) and train
+                        step, TP=2 x DP=N/2 for N >= 2 (DP4xTP2 at N = 8)
+  ``mlp``               TP Llama-3-8B MLP block over all ranks (hand-written MFMA
+                        GEMMs, SwiGLU epilogue, TP all-reduces; unfused, chunked-
+                        overlap and fused row-parallel variants)
+  ``dp``                BASELINE config 5: DP over all ranks of a Llama-3-8B-sized
+                        model (16 GB bf16 gradients) through ``DistributedDataParallel``,
+                        bucket all-reduces launched from autograd hooks during a real
+                        backward (parallel/llama_dp.py), N >= 2
+  ``rccl``              the RCCL library baseline (the role MPI's built-ins play in
+                        the reference's mpi-test.py:42-98,178-239), N >= 2.  Reported
+                        in ``config.rccl`` with ``handwritten_vs_rccl``; it never
+                        replaces the hand-written headline.
+  ``shared_gpu_dry_run``  (N = 1 only) the N >= 2 bench, 8 ranks on this one GPU, so
+                        the 8-GPU path is exercised before any 8-GPU run.  Its numbers
+                        measure HBM + protocol, not xGMI.
+  ====================  =========================================================
 
 The timed region is W untimed steps, then a barrier + device sync, K steps,
 and another device sync + barrier.  The time is the MAX over ranks.  Rank 0
@@ -62,41 +66,48 @@ sys.path.insert(0, REPO)
 
 GiB = 1 << 30
 XGMI_LINK_GBPS = 153.6  # MI355X xGMI, per link and direction (7 links x 153.6 = 1075 GB/s per GPU)
+METRIC = "all-reduce algbw (GB/s) @1GiB fp32 + DP4xTP2 fwd step time, 1/2/4/8 MI355X"
+PHASES = ("coll", "harness", "mlp", "dp", "rccl")
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--size-mb", type=int, default=1024)
-    ap.add_argument("--algo", default="auto", help="auto | twoshot | push | ring | rhd | oneshot | rccl | ...")
+    ap.add_argument("--algo", default="auto", help="auto | twoshot | push | ring | rhd | oneshot | fanout | ...")
     ap.add_argument("--tp", type=int, default=0, help="TP degree of the harness step (default 2 if N>=2)")
     ap.add_argument("--batch", type=int, default=2048, help="images per DP replica for the harness step")
     ap.add_argument("--fc-o-mode", default="token", choices=["token", "row"],
                     help="harness fc_o: per-token row-parallel (reference shape) or pooled")
-    ap.add_argument("--dp-layers", type=int, default=32, help="Llama-3-8B layers of the DP-overlap measurement")
-    ap.add_argument("--dp-tokens", type=int, default=4096)
+    ap.add_argument("--dp-layers", type=int, default=32, help="Llama-3-8B decoder layers of the DP-overlap phase")
+    ap.add_argument("--dp-tokens", type=int, default=4096, help="tokens per rank of the DP-overlap phase")
     ap.add_argument("--dp-vocab", type=int, default=1,
-                    help="DP overlap: include the LM head and token embedding gradients (Llama-3-8B: 16.06 GB total)")
+                    help="DP overlap: include the LM head and token embedding (Llama-3-8B: 16.06 GB of gradients)")
+    ap.add_argument("--dp-scripted", type=int, default=1,
+                    help="DP phase: also measure the scripted wgrad-only overlap (parallel/overlap.py) as a secondary")
     ap.add_argument("--a2a-mb", type=int, default=256)
     ap.add_argument("--mlp-tokens", type=int, default=4096,
                     help="tokens of the TP Llama-3-8B MLP record (tp_mlp: TP over all ranks; 0 = off)")
+    ap.add_argument("--tune-max-mb", type=int, default=256, help="N >= 2: largest size of the tuning sweep (0 = off)")
     ap.add_argument("--shared-dry-run", type=int, default=8, help="N=1: ranks of the shared-GPU dry run (0 = off)")
     ap.add_argument("--no-harness", action="store_true")
     ap.add_argument("--no-secondary", action="store_true")
     ap.add_argument("--verbose", action="store_true")
-    ap.add_argument("--phase", default="", choices=["", "custom", "dp", "mlp", "rccl"],
+    ap.add_argument("--phase", default="", choices=("",) + PHASES,
                     help="internal: which child phase this process runs (set by the supervisor)")
     ap.add_argument("--result", default="", help="internal: where a child phase writes its JSON")
+    ap.add_argument("--coll-timeout", type=float, default=900.0, help="wall-clock budget of the collective phase (s)")
+    ap.add_argument("--harness-timeout", type=float, default=300.0, help="wall-clock budget of the harness phase (s)")
     ap.add_argument("--rccl-timeout", type=float, default=300.0, help="wall-clock budget of the RCCL phase (s)")
-    ap.add_argument("--dp-timeout", type=float, default=420.0, help="wall-clock budget of the DP-overlap phase (s)")
-    ap.add_argument("--mlp-timeout", type=float, default=240.0, help="wall-clock budget of the TP MLP phase (s)")
-    ap.add_argument("--custom-timeout", type=float, default=1500.0, help="wall-clock budget of phase 1 (s)")
+    ap.add_argument("--dp-timeout", type=float, default=600.0, help="wall-clock budget of the DP-overlap phase (s)")
+    ap.add_argument("--mlp-timeout", type=float, default=300.0, help="wall-clock budget of the TP MLP phase (s)")
     ap.add_argument("--no-rccl", action="store_true", help="skip the RCCL baseline phase")
-    return ap.parse_args()
+    return ap.parse_args(argv)
 
 
+# ------------------------------------------------------------------ supervision
 def relaunch(n: int) -> int:
     """--gpus N without a launcher: start N ranks with the framework launcher
     (child processes; this process never touches the GPU)."""
@@ -144,13 +155,82 @@ def _run_child(cmd, env, budget: float):
     return rc, time.monotonic() - t0
 
 
+def plan_phases(args, size: int):
+    """(phase, budget) in run order for a job of ``size`` ranks."""
+    out = [("coll", args.coll_timeout)]
+    sec = not args.no_secondary
+    if not args.no_harness:
+        out.append(("harness", args.harness_timeout))
+    if sec and args.mlp_tokens > 0:
+        out.append(("mlp", args.mlp_timeout))
+    if sec and size > 1 and args.dp_layers > 0:
+        out.append(("dp", args.dp_timeout))
+    if size > 1 and not args.no_rccl:
+        out.append(("rccl", args.rccl_timeout))
+    return out
+
+
+def empty_headline(args, size: int, why: str) -> dict:
+    return {"metric": METRIC, "value": 0.0, "unit": "GB/s", "n_gpus": size, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": None, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "fp32", "data": "synthetic", "config": {"error": why}}
+
+
+def merge_results(args, size: int, status: dict, load) -> dict:
+    """Rank 0: the one output line from the phases' records.  ``load(phase)`` returns a
+    phase's JSON or None.  The headline comes only from the ``coll`` phase; every other
+    phase fills its own key and a failed phase leaves an error there, nothing else."""
+    out = load("coll") if status.get("coll", {}).get("ok") else None
+    if out is None:
+        out = empty_headline(args, size, f"collective phase failed: {status.get('coll')}")
+    c = out.setdefault("config", {})
+
+    def rec(phase):
+        r = load(phase) if status[phase]["ok"] else None
+        return r if r is not None else {"error": f"{phase} phase failed or timed out: {status[phase]}"}
+
+    if "harness" in status:
+        h = rec("harness")
+        c["harness"] = h
+        if "error" not in h:
+            c["tp_fwd_step_ms"] = h.pop("fwd_ms", None)
+            c["tp_train_step_ms"] = h.pop("train_ms", None)
+            c["global_batch"] = h.get("global_batch")
+            c["seq_len"] = h.get("seq_len")
+            c["parallelism"] = f"dp{h.get('dp')}xtp{h.get('tp')}"
+    if "mlp" in status:
+        c["tp_mlp"] = rec("mlp")
+    if "dp" in status:
+        c["dp_overlap"] = rec("dp")
+    if "rccl" in status:
+        merge_rccl(out, load("rccl") if status["rccl"]["ok"] else None, status["rccl"])
+    c["phases"] = status
+    return out
+
+
+def merge_rccl(out: dict, rr, status: dict) -> None:
+    """Fold the RCCL phase into the record as the library comparison.  The headline
+    ``value`` stays the hand-written all-reduce (the north star's product); RCCL goes
+    to ``config.rccl`` and ``config.handwritten_vs_rccl`` = hand-written / RCCL algbw."""
+    c = out.setdefault("config", {})
+    if rr is None or "error" in rr:
+        c["rccl"] = {"error": (rr or {}).get("error") or f"RCCL phase failed or timed out: {status}"}
+        return
+    c["rccl"] = rr
+    if rr.get("algbw_GBps") and out.get("value"):
+        c["handwritten_vs_rccl"] = round(out["value"] / rr["algbw_GBps"], 3)
+    b16 = c.get("bf16_1GiB")
+    if b16 and rr.get("bf16_algbw_GBps"):
+        b16["handwritten_vs_rccl"] = round(b16["algbw_GBps"] / rr["bf16_algbw_GBps"], 3)
+    a2a = c.get("alltoall")
+    if a2a and rr.get("alltoall_ms"):
+        a2a["rccl_ms"] = dict(rr["alltoall_ms"])
+
+
 def supervise(args) -> int:
-    """N >= 2 (or any launcher): this process never touches the GPU.  It runs the
-    hand-written phase, the DP-overlap phase (BASELINE config 5: 16 GB of registered
-    gradients) and the RCCL phase as child processes of N fresh ranks (each child
-    group has its own host-plane job id), each under a wall-clock budget, and rank 0
-    merges the JSON records into the one output line: a phase that hangs or fails is
-    recorded and cannot cost the headline."""
+    """This process never touches the GPU.  It runs every phase as a child process
+    group of ``size`` fresh ranks (each with its own host-plane job id) under a
+    wall-clock budget, and rank 0 merges the JSON records into the one output line."""
     import shutil
     import tempfile
     import uuid
@@ -162,19 +242,15 @@ def supervise(args) -> int:
     _, _, local = _env_rank()
     tmp = world.bcast(tempfile.mkdtemp(prefix="ccmpi_bench_") if rank == 0 else None, root=0)
     job = world.bcast(uuid.uuid4().hex[:12] if rank == 0 else None, root=0)
-    argv = [a for a in sys.argv[1:]]
-    phases = [("custom", args.custom_timeout)]
-    if size > 1 and args.dp_layers > 0 and not args.no_secondary:
-        phases.append(("dp", args.dp_timeout))
-    if size > 1 and args.mlp_tokens > 0 and not args.no_secondary:
-        phases.append(("mlp", args.mlp_timeout))
-    if size > 1 and not args.no_rccl:
-        phases.append(("rccl", args.rccl_timeout))
+    # the collective phase's tuning sweep -> every later phase's device groups (auto)
+    tune_file = os.environ.get("CCMPI_TUNE_FILE") or os.path.join(tmp, "tune.json")
+    argv = list(sys.argv[1:])
     status = {}
-    for phase, budget in phases:
+    for phase, budget in plan_phases(args, size):
         env = dict(os.environ, CCMPI_RANK=str(rank), CCMPI_SIZE=str(size), CCMPI_LOCAL_RANK=str(local),
                    CCMPI_LOCAL_SIZE=os.environ.get("LOCAL_WORLD_SIZE", os.environ.get("CCMPI_LOCAL_SIZE", str(size))),
-                   LOCAL_RANK=str(local), CCMPI_JOBID=f"{job}-{phase}", CCMPI_BENCH_WORKER="1")
+                   LOCAL_RANK=str(local), CCMPI_JOBID=f"{job}-{phase}", CCMPI_BENCH_WORKER="1",
+                   CCMPI_TUNE_FILE=tune_file)
         pp = env.get("PYTHONPATH", "")
         env["PYTHONPATH"] = REPO + (os.pathsep + pp if pp else "")
         cmd = [sys.executable, os.path.abspath(__file__), *argv, "--phase", phase,
@@ -193,116 +269,94 @@ def supervise(args) -> int:
             except (OSError, ValueError):
                 return None
 
-        out = load("custom")
-        if out is None:
-            out = {"metric": METRIC, "value": 0.0, "unit": "GB/s", "n_gpus": size, "steps": args.steps,
-                   "warmup": args.warmup, "ms_per_step": None, "higher_is_better": True, "scaling": "weak",
-                   "vs_baseline": None, "dtype": "fp32", "data": "synthetic",
-                   "config": {"error": f"hand-written phase failed: {status['custom']}"}}
+        out = merge_results(args, size, status, load)
+        if not status["coll"]["ok"]:
             rc = 1
-        if "dp" in status:
-            dr = load("dp") if status["dp"]["ok"] else None
-            out.setdefault("config", {})["dp_overlap"] = dr if dr is not None else {
-                "error": f"DP-overlap phase failed or timed out: {status['dp']}"}
-        if "mlp" in status:
-            mr = load("mlp") if status["mlp"]["ok"] else None
-            out.setdefault("config", {})["tp_mlp"] = mr if mr is not None else {
-                "error": f"TP MLP phase failed or timed out: {status['mlp']}"}
-        if "rccl" in status:
-            rr = load("rccl") if status["rccl"]["ok"] else None
-            merge_rccl(out, rr, status["rccl"])
+        if size == 1 and args.shared_dry_run > 1 and not args.no_secondary:
+            out["config"]["shared_gpu_dry_run"] = shared_dry_run(args.shared_dry_run, steps=5, warmup=2,
+                                                                 verbose=args.verbose)
         print(json.dumps(out), flush=True)
         shutil.rmtree(tmp, ignore_errors=True)
     world.Barrier()
     return rc
 
 
-METRIC = "all-reduce algbw (GB/s) @1GiB fp32 + DP4xTP2 fwd step time, 1/2/4/8 MI355X"
+def shared_dry_run(n: int, steps: int, warmup: int, verbose: bool):
+    """Run this bench with n ranks on this GPU (the N >= 2 path) and return its JSON.
+
+    One hardware queue per process (``GPU_MAX_HW_QUEUES=1``): with HIP's default of 4,
+    8 processes ask for up to 32 queues, the scheduler time-slices the ones it cannot
+    map and the DP4xTP2 forward measured 1.6-7.0 ms instead of ~0.6 ms
+    (profiles/r3_dryrun).  ``CCMPI_DRYRUN_HW_QUEUES`` overrides (empty = HIP default)."""
+    cmd = [sys.executable, "-m", "collective_communication_mpi_amd.launch", "-n", str(n), "--timeout", "600",
+           sys.executable, os.path.abspath(__file__), "--gpus", str(n), "--steps", str(steps), "--warmup", str(warmup),
+           "--dp-layers", "0", "--a2a-mb", "64", "--shared-dry-run", "0", "--no-rccl", "--mlp-tokens", "0",
+           "--tune-max-mb", "0"]
+    env = dict(os.environ, CCMPI_BENCH_CHILD="1")
+    q = os.environ.get("CCMPI_DRYRUN_HW_QUEUES", "1")
+    if q:
+        env["GPU_MAX_HW_QUEUES"] = q
+    try:
+        r = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=660)
+    except subprocess.TimeoutExpired:
+        return {"error": "timeout"}
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    if r.returncode != 0 or not lines:
+        return {"error": f"rc={r.returncode}", "stderr_tail": r.stderr[-800:]}
+    out = json.loads(lines[-1])
+    if verbose:
+        print("[bench] shared dry run:", lines[-1][:400], file=sys.stderr)
+    keep = {k: out[k] for k in ("value", "ms_per_step", "n_gpus")}
+    keep["ranks"] = n
+    keep["unit"] = "GB/s (1 GiB fp32 all-reduce algbw)"
+    keep["note"] = f"{n} ranks sharing ONE GPU through IPC: HBM + protocol, not xGMI"
+    keep["hw_queues_per_rank"] = env.get("GPU_MAX_HW_QUEUES", "HIP default")
+    keep.update({k: out["config"].get(k) for k in ("allreduce_algo", "busbw_GBps", "candidates_ms", "result_exact",
+                                                     "self_test", "bf16_1GiB", "alltoall", "tp_fwd_step_ms",
+                                                     "tp_train_step_ms", "parallelism", "phases")})
+    return keep
 
 
-def merge_rccl(out: dict, rr, status: dict) -> None:
-    """Fold the RCCL phase into the hand-written phase's record (rank 0)."""
-    c = out.setdefault("config", {})
-    if rr is None or "error" in rr:
-        c["rccl"] = {"error": (rr or {}).get("error") or f"RCCL phase failed or timed out: {status}"}
-        return
-    c["rccl"] = rr
-    if rr.get("allreduce_ms"):
-        c.setdefault("candidates_ms", {})["rccl"] = rr["allreduce_ms"]
-        c["handwritten_best_GBps"] = out.get("value")
-        c["handwritten_algo"] = c.get("allreduce_algo")
-        if rr["algbw_GBps"] > (out.get("value") or 0):
-            # the framework offers RCCL too (algo="rccl"): the headline is the faster path
-            out["value"] = rr["algbw_GBps"]
-            out["ms_per_step"] = rr["allreduce_ms"]
-            c["allreduce_algo"] = "rccl"
-            c["busbw_GBps"] = rr["busbw_GBps"]
-            if c.get("xgmi_link_frac") is not None:
-                w = out.get("n_gpus") or 1
-                c["xgmi_link_frac"] = round(rr["busbw_GBps"] / (min(w - 1, 7) * XGMI_LINK_GBPS), 3)
-    a2a = c.get("alltoall")
-    if a2a and rr.get("alltoall_ms"):
-        for k, v in rr["alltoall_ms"].items():
-            a2a.setdefault("candidates_ms", {})[k] = v
+# ------------------------------------------------------------------ phase helpers
+def _setup_phase(timeout_s: str):
+    """Common child-phase bring-up: device timeout, crash reporter, communicator, device."""
+    os.environ.setdefault("CCMPI_DEVICE_TIMEOUT_S", timeout_s)
+    import faulthandler
 
+    faulthandler.enable()
+    from collective_communication_mpi_amd import MPI, Communicator, _native
 
-def dp_phase(args) -> dict:
-    """Phase 2: the Llama-3-8B-sized DP gradient all-reduce overlapped with the weight-
-    gradient GEMMs (parallel/overlap.py) on fresh ranks."""
-    os.environ.setdefault("CCMPI_DEVICE_TIMEOUT_S", "20")
+    _native.host().install_crash_handler(2)  # native backtrace if the phase crashes (rc -11 is then explained)
     import torch
 
-    from collective_communication_mpi_amd import MPI, Communicator
-    from collective_communication_mpi_amd.parallel.overlap import dp_grad_overlap
-
     comm = Communicator(MPI.COMM_WORLD)
-    local = int(os.environ.get("LOCAL_RANK", os.environ.get("CCMPI_LOCAL_RANK", "0")))
+    local = _env_rank()[2]
     torch.cuda.set_device(local % torch.cuda.device_count())
-    return dp_grad_overlap(comm, layers=args.dp_layers, tokens=args.dp_tokens, iters=2, algo="auto",
-                           verbose=args.verbose, vocab=bool(args.dp_vocab))
+    return comm
 
 
-def mlp_phase(args) -> dict:
-    """Phase 3: the Llama-3-8B MLP block (ParallelSwiGLUMLP) with TP over every rank on
-    fresh ranks: hand-written MFMA GEMMs (SwiGLU gate in the gate|up epilogue) and the TP
-    all-reduces of the reference's TP layer, over xGMI when each rank has its own GPU."""
-    os.environ.setdefault("CCMPI_DEVICE_TIMEOUT_S", "20")
+def _fault_injection(phase: str) -> None:
+    """Tests: ``CCMPI_BENCH_FAULT=<phase>`` makes that phase's rank 0 die by SIGSEGV
+    after its GPU work started, like the round-3 harness crash."""
+    if os.environ.get("CCMPI_BENCH_FAULT") == phase and _env_rank()[0] == 0:
+        import signal
+
+        os.kill(os.getpid(), signal.SIGSEGV)
+
+
+def _timers(comm):
     import torch
 
-    from collective_communication_mpi_amd import MPI, Communicator
-    from collective_communication_mpi_amd.parallel.mlp_bench import measure_tp_mlp
+    from collective_communication_mpi_amd import MPI
 
-    comm = Communicator(MPI.COMM_WORLD)
-    local = int(os.environ.get("LOCAL_RANK", os.environ.get("CCMPI_LOCAL_RANK", "0")))
-    torch.cuda.set_device(local % torch.cuda.device_count())
-    return measure_tp_mlp(comm, tokens=args.mlp_tokens, iters=10, warmup=3)
-
-
-def rccl_phase(args) -> dict:
-    """Phase 2: the RCCL library collectives on fresh ranks (BASELINE's 'library'
-    comparison).  Exact-result check before timing, like the hand-written phase."""
-    os.environ.setdefault("CCMPI_DEVICE_TIMEOUT_S", "10")
-    import torch
-
-    from collective_communication_mpi_amd import MPI, Communicator
-
-    comm = Communicator(MPI.COMM_WORLD)
-    rank, world = comm.Get_rank(), comm.Get_size()
-    _, _, local = _env_rank()
-    torch.cuda.set_device(local % torch.cuda.device_count())
-    dev, hc = comm.dev, comm.comm
-    mode = os.environ.get("CCMPI_BENCH_RCCL", "")  # tests: "force" RCCL on shared GPUs, simulate a "hang"
-    if dev.shared_device and mode not in ("force", "hang"):
-        return {"skipped": f"{dev.ranks_per_device} ranks share one GPU (RCCL refuses duplicate devices)"}
-    if mode == "hang":
-        while True:  # the supervisor's --rccl-timeout must end this phase
-            time.sleep(1)
+    hc = comm.comm
 
     def sync_barrier():
         torch.cuda.synchronize()
         hc.Barrier()
 
-    def timed(fn, iters):
+    def timed(fn, iters) -> float:
+        """Seconds per call: barrier + device sync on both sides, MAX over ranks."""
         sync_barrier()
         t0 = time.perf_counter()
         for _ in range(iters):
@@ -310,13 +364,318 @@ def rccl_phase(args) -> dict:
         sync_barrier()
         return hc.allreduce(time.perf_counter() - t0, op=MPI.MAX) / iters
 
+    return sync_barrier, timed
+
+
+def allreduce_candidates(world: int, shared: bool, algo: str = "auto"):
+    """Hand-written all-reduce algorithms the headline tries (CTA budgets after the ':')."""
+    if world == 1:
+        return ["twoshot"]  # single rank: the all-reduce is a device copy
+    if algo != "auto":
+        return [algo]
+    hand = ["twoshot:256", "twoshot:512", "fanout:256", "fanout:512", "fanout_lds:512", "push:512", "ring"]
+    if world & (world - 1) == 0:
+        hand.append("rhd")
+    return hand
+
+
+def run_collectives(comm, args, log=lambda *a: None, groups=("ar", "bf16", "a2a")) -> dict:
+    """The hand-written collective measurements of one process (collective: every rank
+    calls).  ``groups`` selects the candidate loop (``ar``, required for the others),
+    the bf16 all-reduce and the all-to-all.  Returns the record's headline fields."""
+    import torch
+
+    from collective_communication_mpi_amd import MPI
+
+    rank, world = comm.Get_rank(), comm.Get_size()
+    dev, hc = comm.dev, comm.comm
+    sync_barrier, timed = _timers(comm)
+    # bring-up check of the small-message algorithms `auto` uses inside the harness
+    # (LL, one-shot) on this fabric: a failing one is disabled on every rank
+    self_test = dev.self_test() if world > 1 else None
+    log(f"self test: {self_test}")
+    nbytes = args.size_mb << 20
+    x = dev.empty(nbytes // 4, torch.float32)
+    y = dev.empty(nbytes // 4, torch.float32)
+    failed = [False]
+
+    def pick(buf_in, buf_out, expect, cands):
+        results = {}
+        for algo in cands:
+            if failed[0]:
+                # the hand-written kernels share one flag protocol: after one of them failed
+                # (and waited out the device timeout) the others are not tried
+                results[algo] = None
+                continue
+            ok = 1
+            try:
+                buf_out.zero_()
+                sync_barrier()
+                dev.allreduce(buf_in, buf_out, "SUM", algo)
+                torch.cuda.synchronize()
+                dev.check()
+                ok = int(bool(torch.all(buf_out == expect).item()))
+            except Exception as e:  # noqa: BLE001 - any failure disqualifies the candidate
+                log(f"candidate {algo} failed: {e}")
+                ok = 0
+            if not hc.allreduce(ok, op=MPI.MIN):
+                results[algo] = None
+                failed[0] = True
+                dev.reset()  # a timed-out kernel leaves per-CTA epochs inconsistent
+                continue
+            dev.allreduce(buf_in, buf_out, "SUM", algo)
+            results[algo] = timed(lambda: dev.allreduce(buf_in, buf_out, "SUM", algo), 3)
+            log(f"candidate {algo} ({buf_in.dtype}): {results[algo] * 1e3:.3f} ms")
+        good = {a: t for a, t in results.items() if t}
+        if not good:
+            raise SystemExit("no all-reduce algorithm produced a correct result")
+        return results, min(good, key=good.get)
+
+    def ms(results):
+        return {a: (round(t * 1e3, 4) if t else None) for a, t in results.items()}
+
+    x.fill_(float(rank + 1))
+    expect = float(world * (world + 1) // 2)
+    results, best = pick(x, y, expect, allreduce_candidates(world, dev.shared_device, args.algo))
+    for _ in range(args.warmup):
+        dev.allreduce(x, y, "SUM", best)
+    t_step = timed(lambda: dev.allreduce(x, y, "SUM", best), args.steps)
+    torch.cuda.synchronize()
+    final_ok = bool(hc.allreduce(int(bool(torch.all(y == expect).item())), op=MPI.MIN))
+    algbw = nbytes / t_step / 1e9
+    busbw = algbw * (2 * (world - 1) / world) if world > 1 else 0.0
+    sec = {}
+    if "bf16" in groups:
+        # ---- 1 GiB bf16 all-reduce (BASELINE config 2): rank-valued, exact in bf16
+        xb, yb = x.view(torch.bfloat16), y.view(torch.bfloat16)
+        xb.fill_(float(rank + 1))
+        top = sorted((a for a, t in results.items() if t), key=lambda a: results[a])[:3]
+        res16, best16 = pick(xb, yb, expect, top)
+        t16 = timed(lambda: dev.allreduce(xb, yb, "SUM", best16), max(3, args.steps // 2))
+        sec["bf16_1GiB"] = {"algo": best16, "ms": round(t16 * 1e3, 4), "algbw_GBps": round(nbytes / t16 / 1e9, 2),
+                            "busbw_GBps": round(nbytes / t16 / 1e9 * (2 * (world - 1) / world), 2) if world > 1 else 0.0,
+                            "candidates_ms": ms(res16)}
+    if "a2a" in groups:
+        # ---- all-to-all, 256 MiB per rank (BASELINE config 3)
+        an = ((args.a2a_mb << 20) // 4) // world * world
+        blk = an // world
+        xa, ya = x[:an], y[:an]
+        xa.view(world, blk).copy_((rank * world + torch.arange(world, device=dev.device, dtype=torch.float32))
+                                  .view(world, 1).expand(world, blk))
+        want = (torch.arange(world, device=dev.device, dtype=torch.float32) * world + rank).view(world, 1).expand(world, blk)
+        a2a = {}
+        for algo in ["direct", "push", "pairwise"]:
+            log(f"alltoall {algo}")
+            try:
+                ya.zero_()
+                sync_barrier()
+                dev.alltoall(xa, ya, algo)
+                torch.cuda.synchronize()
+                dev.check()
+                ok = int(torch.equal(ya.view(world, blk), want))
+            except Exception as e:  # noqa: BLE001
+                log(f"alltoall {algo} failed: {e}")
+                ok = 0
+            if not hc.allreduce(ok, op=MPI.MIN):
+                a2a[algo] = None
+                continue
+            a2a[algo] = round(timed(lambda: dev.alltoall(xa, ya, algo), 5) * 1e3, 4)
+        good = {a: t for a, t in a2a.items() if t}
+        ba = min(good, key=good.get) if good else None
+        sec["alltoall"] = {"bytes_per_rank": an * 4, "algo": ba, "ms": good.get(ba),
+                           "algbw_GBps": round(an * 4 / (good[ba] / 1e3) / 1e9, 2) if ba else None,
+                           "candidates_ms": a2a}
+    del x, y
+    return {"algbw": algbw, "busbw": busbw, "t_step": t_step, "best": best, "results": ms(results),
+            "final_ok": final_ok, "self_test": self_test, "secondary": sec}
+
+
+def tuning_sweep(comm, args, best_1gib: str, log=lambda *a: None) -> dict:
+    """N >= 2: ``DeviceGroup.tune`` over 16 KiB .. ``--tune-max-mb`` with every hand-written
+    algorithm ``auto`` may pick (ring and RHD included), plus the 1 GiB winner, written to
+    ``CCMPI_TUNE_FILE`` for the later phases' groups of the same size."""
+    import torch
+
+    dev = comm.dev
+    if comm.Get_size() == 1 or args.tune_max_mb <= 0:
+        return {}
+    algos = ["ll", "oneshot", "fanout", "twoshot", "ring"] + (["rhd"] if comm.Get_size() & (comm.Get_size() - 1) == 0
+                                                              else [])
+    t0 = time.perf_counter()
+    table = dev.tune(max_bytes=args.tune_max_mb << 20, min_bytes=16 << 10, algos=algos, iters=5, dtype=torch.float32,
+                     save=None)
+    key = (dev.size, (args.size_mb << 20).bit_length() - 1)
+    dev.tuned[key] = best_1gib
+    if dev.rank == 0 and os.environ.get("CCMPI_TUNE_FILE"):
+        from collective_communication_mpi_amd.device import save_tuning
+
+        save_tuning(os.environ["CCMPI_TUNE_FILE"], dev.tune_key, dev.tuned)
+    comm.comm.Barrier()
+    log(f"tuning sweep {time.perf_counter() - t0:.1f}s: {table}")
+    return {"key": dev.tune_key, "table": {f"2^{lg}": a for (_, lg), a in sorted(dev.tuned.items())},
+            "seconds": round(time.perf_counter() - t0, 1)}
+
+
+# ------------------------------------------------------------------ phases
+def coll_phase(args) -> dict:
+    comm = _setup_phase("10")
+    import torch
+
+    rank, world = comm.Get_rank(), comm.Get_size()
+    dev = comm.dev
+
+    def log(*a):
+        if rank == 0 and args.verbose:
+            print("[bench coll]", *a, file=sys.stderr, flush=True)
+
+    groups = ("ar",) if args.no_secondary else ("ar", "bf16", "a2a")
+    r = run_collectives(comm, args, log, groups)
+    _fault_injection("coll")
+    tuning = tuning_sweep(comm, args, r["best"], log) if not args.no_secondary else {}
+    torch.cuda.synchronize()
+    tp = args.tp or (2 if world >= 2 and world % 2 == 0 else 1)
+    return {
+        "metric": METRIC,
+        "value": round(r["algbw"], 3),
+        "unit": "GB/s",
+        "n_gpus": world // dev.ranks_per_device,  # distinct GPUs (ranks sharing one GPU count once)
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(r["t_step"] * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "fp32",
+        "data": "synthetic (rank-valued 1 GiB fp32 buffer; MNIST-shaped random images, random-init weights)",
+        "config": {
+            "model": "allreduce-1GiB-fp32 + MNIST-shaped TP transformer layer (768->256 qkv, 256->10 fc_o per token)",
+            "global_batch": args.batch * max(1, world // tp),
+            "seq_len": 16,
+            "parallelism": f"dp{max(1, world // tp)}xtp{tp}",
+            "allreduce_algo": r["best"],
+            "allreduce_bytes": args.size_mb << 20,
+            "busbw_GBps": round(r["busbw"], 3),
+            # one xGMI link per GPU pair (fully connected, <= 7 per GPU), ~153.6 GB/s each per
+            # direction: the all-reduce's bus bandwidth as a fraction of the links it can drive
+            "xgmi_link_frac": (round(r["busbw"] / (min(world - 1, 7) * XGMI_LINK_GBPS), 3)
+                               if world > 1 and not dev.shared_device else None),
+            "candidates_ms": r["results"],
+            "result_exact": r["final_ok"],
+            "self_test": r["self_test"],
+            "shared_gpu": dev.shared_device,
+            "tuning": tuning,
+            **r["secondary"],
+        },
+    }
+
+
+def harness_phase(args) -> dict:
+    """The DP x TP transformer-layer forward (HIP graph) and train step, plus the other
+    fc_o forms, in a process of its own (a crash here cannot cost the headline)."""
+    comm = _setup_phase("20")
+    import torch
+
+    from collective_communication_mpi_amd import MPI
+    from collective_communication_mpi_amd.models.harness import bench_forward
+
+    world, hc = comm.Get_size(), comm.comm
+    tp = args.tp or (2 if world >= 2 and world % 2 == 0 else 1)
+    mode = args.fc_o_mode
+    _fault_injection("harness")
+    # headline: the reference's layer shape -- per-token row-parallel fc_o with (B, S, out)
+    # outputs (reference model/func_impl.py:94-109), so the TP all-reduce carries
+    # B*S x 16 partial outputs every step
+    try:
+        harness = bench_forward(comm, tp=tp, batch=args.batch, steps=args.steps, warmup=args.warmup, fc_o_mode=mode)
+        herr, hok = None, 1
+    except Exception as e:  # noqa: BLE001 - recorded; the pooled form is measured instead
+        harness, herr, hok = None, f"{type(e).__name__}: {e}"[:300], 0
+    if not hc.allreduce(hok, op=MPI.MIN) and mode != "row":
+        torch.cuda.synchronize()
+        mode = "row"
+        harness = bench_forward(comm, tp=tp, batch=args.batch, steps=args.steps, warmup=args.warmup, fc_o_mode=mode)
+        harness["token_error"] = herr
+    harness["tp_allreduce_bytes"] = (args.batch * 16 * 16 * 4 if mode == "token" else args.batch * 16 * 4) \
+        if tp > 1 else 0
+    if not args.no_secondary:
+        # the other fc_o forms: pooled row-parallel (B x 16 TP all-reduce), and the token
+        # pipeline in 4 row blocks whose all-reduces run on a side stream under the next
+        # block's attention
+        other = {}
+        variants = [("pooled", "row", 1)] if args.fc_o_mode == "token" else [("token", "token", 1)]
+        if tp > 1:
+            variants.append(("token_chunks4", "token", 4))
+        for name, vmode, chunks in variants:
+            try:
+                r = bench_forward(comm, tp=tp, batch=args.batch, steps=args.steps, warmup=args.warmup,
+                                  train=False, fc_o_mode=vmode, tp_chunks=chunks)
+                other[f"{name}_fwd_ms"] = round(r["fwd_ms"], 4)
+            except Exception as e:  # noqa: BLE001 - a secondary number must not cost the record
+                other[f"{name}_error"] = f"{type(e).__name__}: {e}"[:200]
+        harness["fc_o_variants"] = other
+    harness["fwd_ms"] = round(harness["fwd_ms"], 4)
+    harness["train_ms"] = round(harness.get("train_ms", float("nan")), 4)
+    return harness
+
+
+def dp_phase(args) -> dict:
+    """BASELINE config 5: DistributedDataParallel over every rank of a Llama-3-8B-sized
+    model, bucket all-reduces launched by autograd hooks during the real backward
+    (parallel/llama_dp.py); the scripted wgrad-only overlap (parallel/overlap.py) as a
+    secondary number."""
+    comm = _setup_phase("30")
+    from collective_communication_mpi_amd.parallel.llama_dp import measure_ddp_overlap
+
+    out = measure_ddp_overlap(comm, layers=args.dp_layers, tokens=args.dp_tokens, vocab=bool(args.dp_vocab),
+                              iters=2, verbose=args.verbose)
+    if args.dp_scripted:
+        import torch
+
+        from collective_communication_mpi_amd.parallel.overlap import dp_grad_overlap
+
+        torch.cuda.empty_cache()
+        try:
+            out["scripted_wgrad_only"] = dp_grad_overlap(comm, layers=args.dp_layers, tokens=args.dp_tokens, iters=2,
+                                                         algo="auto", verbose=args.verbose, vocab=bool(args.dp_vocab))
+        except Exception as e:  # noqa: BLE001 - secondary
+            out["scripted_wgrad_only"] = {"error": f"{type(e).__name__}: {e}"[:300]}
+    return out
+
+
+def mlp_phase(args) -> dict:
+    """The Llama-3-8B MLP block (ParallelSwiGLUMLP) with TP over every rank: hand-written
+    MFMA GEMMs (SwiGLU gate in the gate|up epilogue) and the TP all-reduces of the
+    reference's TP layer, over xGMI when each rank has its own GPU; the row-parallel
+    variants (plain, chunked overlap, fused epilogue) side by side."""
+    comm = _setup_phase("20")
+    from collective_communication_mpi_amd.parallel.mlp_bench import measure_tp_mlp
+
+    return measure_tp_mlp(comm, tokens=args.mlp_tokens, iters=10, warmup=3, variants=True)
+
+
+def rccl_phase(args) -> dict:
+    """The RCCL library collectives on fresh ranks (BASELINE's 'library' comparison).
+    Exact-result check before timing, like the hand-written phase."""
+    comm = _setup_phase("10")
+    import torch
+
+    from collective_communication_mpi_amd import MPI
+
+    rank, world = comm.Get_rank(), comm.Get_size()
+    dev, hc = comm.dev, comm.comm
+    mode = os.environ.get("CCMPI_BENCH_RCCL", "")  # tests: "force" RCCL on shared GPUs, simulate a "hang"
+    if dev.shared_device and mode not in ("force", "hang"):
+        return {"skipped": f"{dev.ranks_per_device} ranks share one GPU (RCCL refuses duplicate devices)"}
+    if mode == "hang":
+        while True:  # the supervisor's --rccl-timeout must end this phase
+            time.sleep(1)
+    _, timed = _timers(comm)
     t0 = time.perf_counter()
     dev.ensure_rccl()
     res = {"init_s": round(time.perf_counter() - t0, 2)}
     nbytes = args.size_mb << 20
     x = dev.empty(nbytes // 4, torch.float32)
     y = dev.empty(nbytes // 4, torch.float32)
-    x.fill_(float(rank + 1))
     expect = float(world * (world + 1) // 2)
     for name, xs, ys in (("fp32", x, y), ("bf16", x.view(torch.bfloat16), y.view(torch.bfloat16))):
         xs.fill_(float(rank + 1))
@@ -348,41 +707,6 @@ def rccl_phase(args) -> dict:
     return res
 
 
-def shared_dry_run(n: int, steps: int, warmup: int, verbose: bool):
-    """Run this bench with n ranks on this GPU (the N >= 2 path) and return its JSON."""
-    cmd = [sys.executable, "-m", "collective_communication_mpi_amd.launch", "-n", str(n), "--timeout", "420",
-           sys.executable, os.path.abspath(__file__), "--gpus", str(n), "--steps", str(steps), "--warmup", str(warmup),
-           "--dp-layers", "0", "--a2a-mb", "64", "--shared-dry-run", "0", "--no-rccl", "--mlp-tokens", "0"]
-    env = dict(os.environ, CCMPI_BENCH_CHILD="1")
-    # Hardware queues per process: with the box default (4) the 8 ranks' streams
-    # oversubscribe the queue slots and the DP4xTP2 forward measured 1.6-2.9 ms; one queue
-    # each gave 0.60-0.62 ms in benchmarks/harness_dryrun.py (profiles/r3_dryrun), but in
-    # this full bench (collective candidates first) the harness's HIP-graph replay then
-    # segfaulted in the runtime on all 8 ranks (profiles/r3_valid/README.md).  So the
-    # default is kept; CCMPI_DRYRUN_HW_QUEUES=1 opts in to the one-queue measurement.
-    if os.environ.get("CCMPI_DRYRUN_HW_QUEUES"):
-        env["GPU_MAX_HW_QUEUES"] = os.environ["CCMPI_DRYRUN_HW_QUEUES"]
-    try:
-        r = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=480)
-    except subprocess.TimeoutExpired:
-        return {"error": "timeout"}
-    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
-    if r.returncode != 0 or not lines:
-        return {"error": f"rc={r.returncode}", "stderr_tail": r.stderr[-800:]}
-    out = json.loads(lines[-1])
-    if verbose:
-        print("[bench] shared dry run:", lines[-1][:400], file=sys.stderr)
-    keep = {k: out[k] for k in ("value", "ms_per_step", "n_gpus")}
-    keep["ranks"] = n
-    keep["unit"] = "GB/s (1 GiB fp32 all-reduce algbw)"
-    keep["note"] = f"{n} ranks sharing ONE GPU through IPC: HBM + protocol, not xGMI"
-    keep["hw_queues_per_rank"] = env.get("GPU_MAX_HW_QUEUES", "HIP default")
-    keep.update({k: out["config"].get(k) for k in ("allreduce_algo", "busbw_GBps", "candidates_ms", "result_exact",
-                                                     "self_test", "bf16_1GiB", "alltoall", "dp_overlap", "tp_fwd_step_ms",
-                                                     "parallelism")})
-    return keep
-
-
 def _write_result(args, rank: int, out: dict) -> None:
     if rank != 0:
         return
@@ -400,267 +724,18 @@ def main() -> int:
     launched = any(k in os.environ for k in ("RANK", "CCMPI_RANK", "PMI_RANK", "OMPI_COMM_WORLD_RANK"))
     if args.gpus > 1 and not launched:
         return relaunch(args.gpus)
-    if launched and not args.phase:
-        return supervise(args)
-    if args.phase in ("rccl", "dp", "mlp"):
-        rank = _env_rank()[0]
+    if not args.phase:
+        return supervise(args)  # this process never touches the GPU
+    rank = _env_rank()[0]
+    fn = {"coll": coll_phase, "harness": harness_phase, "rccl": rccl_phase, "dp": dp_phase, "mlp": mlp_phase}[args.phase]
+    if args.phase == "coll":
+        out = fn(args)  # the headline: a failure here fails the phase (rc != 0)
+    else:
         try:
-            out = {"rccl": rccl_phase, "dp": dp_phase, "mlp": mlp_phase}[args.phase](args)
+            out = fn(args)
         except Exception as e:  # noqa: BLE001 - recorded in the merged line
             out = {"error": f"{type(e).__name__}: {e}"[:400]}
-        _write_result(args, rank, out)
-        return 0
-
-    # a hand-written candidate that cannot complete gives up after 10 s (default 20 s):
-    # the slowest legitimate 1 GiB all-reduce takes ~0.1 s, and every candidate starts
-    # from a barrier, so rank skew does not count against it
-    os.environ.setdefault("CCMPI_DEVICE_TIMEOUT_S", "10")
-    import torch
-
-    from collective_communication_mpi_amd import MPI, Communicator
-
-    comm = Communicator(MPI.COMM_WORLD)
-    rank, world = comm.Get_rank(), comm.Get_size()
-    if world != args.gpus and rank == 0:
-        print(f"[bench] warning: --gpus {args.gpus} but world size {world}", file=sys.stderr)
-    local = int(os.environ.get("LOCAL_RANK", os.environ.get("CCMPI_LOCAL_RANK", "0")))
-    torch.cuda.set_device(local % torch.cuda.device_count())
-    dev = comm.dev
-    hc = comm.comm
-
-    def log(*a):
-        if rank == 0 and args.verbose:  # noqa: SIM102
-            print("[bench]", *a, file=sys.stderr, flush=True)
-
-    def sync_barrier():
-        torch.cuda.synchronize()
-        hc.Barrier()
-
-    def timed(fn, iters) -> float:
-        sync_barrier()
-        t0 = time.perf_counter()
-        for _ in range(iters):
-            fn()
-        sync_barrier()
-        return hc.allreduce(time.perf_counter() - t0, op=MPI.MAX) / iters
-
-    # bring-up check of the small-message algorithms `auto` uses inside the harness
-    # (LL, one-shot) on this fabric: a failing one is disabled on every rank
-    self_test = dev.self_test() if world > 1 else None
-    log(f"self test: {self_test}")
-
-    # ------------------------------------------------------------- all-reduce
-    nbytes = args.size_mb << 20
-    x = dev.empty(nbytes // 4, torch.float32)
-    y = dev.empty(nbytes // 4, torch.float32)
-
-    def ar_run(buf_in, buf_out, algo):
-        dev.allreduce(buf_in, buf_out, "SUM", algo)
-
-    def candidates():
-        if world == 1:
-            return ["twoshot"]  # single rank: the all-reduce is a device copy
-        if args.algo != "auto":
-            return [args.algo]
-        hand = ["twoshot:256", "twoshot:512", "fanout:256", "fanout:512", "fanout_lds:512", "push:512", "ring", "rhd" if world & (world - 1) == 0 else None]
-        hand = [a for a in hand if a]
-        # RCCL runs in its own child group after this phase (supervise).  With one rank
-        # per GPU all 1024 CTA slots (4 per CU) are this rank's: more reads in flight
-        # over the links
-        return hand if dev.shared_device else hand + ["fanout:1024"]
-
-    custom_failed = [False]
-
-    def pick(buf_in, buf_out, expect, cands):
-        results = {}
-        for algo in cands:
-            custom = True
-            if custom and custom_failed[0]:
-                # the hand-written kernels share one flag protocol: after one of them failed
-                # (and waited out the device timeout) the others are not tried
-                results[algo] = None
-                continue
-            ok = 1
-            try:
-                buf_out.zero_()
-                sync_barrier()
-                ar_run(buf_in, buf_out, algo)
-                torch.cuda.synchronize()
-                dev.check()
-                ok = int(bool(torch.all(buf_out == expect).item()))
-            except Exception as e:  # noqa: BLE001 - any failure disqualifies the candidate
-                log(f"candidate {algo} failed: {e}")
-                ok = 0
-            if not hc.allreduce(ok, op=MPI.MIN):
-                results[algo] = None
-                if custom:
-                    custom_failed[0] = True
-                    dev.reset()  # a timed-out kernel leaves per-CTA epochs inconsistent
-                continue
-            ar_run(buf_in, buf_out, algo)
-            results[algo] = timed(lambda: ar_run(buf_in, buf_out, algo), 3)
-            log(f"candidate {algo} ({buf_in.dtype}): {results[algo] * 1e3:.3f} ms")
-        good = {a: t for a, t in results.items() if t}
-        if not good:
-            raise SystemExit("no all-reduce algorithm produced a correct result")
-        return results, min(good, key=good.get)
-
-    x.fill_(float(rank + 1))
-    expect = float(world * (world + 1) // 2)
-    results, best = pick(x, y, expect, candidates())
-    for _ in range(args.warmup):
-        ar_run(x, y, best)
-    t_step = timed(lambda: ar_run(x, y, best), args.steps)
-    torch.cuda.synchronize()
-    final_ok = bool(hc.allreduce(int(bool(torch.all(y == expect).item())), op=MPI.MIN))
-    algbw = nbytes / t_step / 1e9
-    busbw = algbw * (2 * (world - 1) / world) if world > 1 else 0.0
-
-    secondary = {}
-    if not args.no_secondary:
-        # ---- 1 GiB bf16 all-reduce (BASELINE config 2): rank-valued, exact in bf16
-        xb, yb = x.view(torch.bfloat16), y.view(torch.bfloat16)
-        xb.fill_(float(rank + 1))
-        top = sorted((a for a, t in results.items() if t), key=lambda a: results[a])[:3]
-        res16, best16 = pick(xb, yb, expect, top)
-        t16 = timed(lambda: ar_run(xb, yb, best16), max(3, args.steps // 2))
-        secondary["bf16_1GiB"] = {"algo": best16, "ms": round(t16 * 1e3, 4), "algbw_GBps": round(nbytes / t16 / 1e9, 2),
-                                  "busbw_GBps": round(nbytes / t16 / 1e9 * (2 * (world - 1) / world), 2) if world > 1 else 0.0,
-                                  "candidates_ms": {a: (round(t * 1e3, 4) if t else None) for a, t in res16.items()}}
-        # ---- all-to-all, 256 MiB per rank (BASELINE config 3)
-        an = ((args.a2a_mb << 20) // 4) // world * world
-        blk = an // world
-        xa, ya = x[:an], y[:an]
-        xa.view(world, blk).copy_((rank * world + torch.arange(world, device=dev.device, dtype=torch.float32)).view(world, 1).expand(world, blk))
-        want = (torch.arange(world, device=dev.device, dtype=torch.float32) * world + rank).view(world, 1).expand(world, blk)
-        a2a = {}
-        for algo in ["direct", "push", "pairwise"]:
-            log(f"alltoall {algo}")
-            try:
-                ya.zero_()
-                sync_barrier()
-                dev.alltoall(xa, ya, algo)
-                torch.cuda.synchronize()
-                dev.check()
-                ok = int(torch.equal(ya.view(world, blk), want))
-            except Exception as e:  # noqa: BLE001
-                log(f"alltoall {algo} failed: {e}")
-                ok = 0
-            if not hc.allreduce(ok, op=MPI.MIN):
-                a2a[algo] = None
-                continue
-            a2a[algo] = round(timed(lambda: dev.alltoall(xa, ya, algo), 5) * 1e3, 4)
-        good = {a: t for a, t in a2a.items() if t}
-        ba = min(good, key=good.get) if good else None
-        secondary["alltoall"] = {"bytes_per_rank": an * 4, "algo": ba, "ms": good.get(ba),
-                                 "algbw_GBps": round(an * 4 / (good[ba] / 1e3) / 1e9, 2) if ba else None,
-                                 "candidates_ms": a2a}
-        # (the DP gradient overlap, BASELINE config 5, runs in its own phase: dp_phase)
-    del x, y
-    torch.cuda.empty_cache()
-
-    # -------------------------------------------------------- harness step
-    harness = None
-    if not args.no_harness:
-        from collective_communication_mpi_amd.models.harness import bench_forward
-
-        tp = args.tp or (2 if world >= 2 and world % 2 == 0 else 1)
-        # headline: the reference's layer shape -- per-token row-parallel fc_o with (B, S, out)
-        # outputs (reference model/func_impl.py:94-109), so the TP all-reduce carries
-        # B*S x 16 partial outputs every step
-        mode = args.fc_o_mode
-        log(f"harness tp={tp} fc_o={mode}")
-        try:
-            harness = bench_forward(comm, tp=tp, batch=args.batch, steps=args.steps, warmup=args.warmup,
-                                    fc_o_mode=mode)
-            herr, hok = None, 1
-        except Exception as e:  # noqa: BLE001 - recorded; the pooled form is measured instead
-            harness, herr, hok = None, f"{type(e).__name__}: {e}"[:300], 0
-            log(f"harness ({mode}) failed: {herr}")
-        if not hc.allreduce(hok, op=MPI.MIN) and mode != "row":
-            torch.cuda.synchronize()
-            mode = "row"
-            harness = bench_forward(comm, tp=tp, batch=args.batch, steps=args.steps, warmup=args.warmup,
-                                    fc_o_mode=mode)
-            harness["token_error"] = herr
-        harness["tp_allreduce_bytes"] = (args.batch * 16 * 16 * 4 if mode == "token" else args.batch * 16 * 4) \
-            if tp > 1 else 0
-        if not args.no_secondary:
-            # the other fc_o forms: pooled row-parallel (B x 16 TP all-reduce), and the token
-            # pipeline in 4 row blocks whose all-reduces run on a side stream under the next
-            # block's attention
-            other = {}
-            variants = [("pooled", "row", 1)] if args.fc_o_mode == "token" else [("token", "token", 1)]
-            if tp > 1:
-                variants.append(("token_chunks4", "token", 4))
-            for name, vmode, chunks in variants:
-                try:
-                    r = bench_forward(comm, tp=tp, batch=args.batch, steps=args.steps, warmup=args.warmup,
-                                      train=False, fc_o_mode=vmode, tp_chunks=chunks)
-                    other[f"{name}_fwd_ms"] = round(r["fwd_ms"], 4)
-                except Exception as e:  # noqa: BLE001 - a secondary number must not cost the line
-                    other[f"{name}_error"] = f"{type(e).__name__}: {e}"[:200]
-            harness["fc_o_variants"] = other
-
-    mlp = None
-    if world == 1 and args.mlp_tokens > 0 and not args.no_secondary:
-        # one rank: the block runs in this process (no collective, nothing that can hang)
-        from collective_communication_mpi_amd.parallel.mlp_bench import measure_tp_mlp
-
-        try:
-            mlp = measure_tp_mlp(comm, tokens=args.mlp_tokens, iters=10, warmup=3)
-        except Exception as e:  # noqa: BLE001 - a secondary number must not cost the line
-            mlp = {"error": f"{type(e).__name__}: {e}"[:300]}
-        log(f"tp_mlp: {mlp}")
-
-    dry = None
-    if world == 1 and args.shared_dry_run > 1 and not args.no_secondary and torch.cuda.device_count() >= 1:
-        dry = shared_dry_run(args.shared_dry_run, steps=5, warmup=2, verbose=args.verbose)
-
-    if rank == 0:
-        tp = harness["tp"] if harness else (2 if world >= 2 and world % 2 == 0 else 1)
-        dp = world // tp
-        out = {
-            "metric": "all-reduce algbw (GB/s) @1GiB fp32 + DP4xTP2 fwd step time, 1/2/4/8 MI355X",
-            "value": round(algbw, 3),
-            "unit": "GB/s",
-            "n_gpus": world // dev.ranks_per_device,  # distinct GPUs (ranks sharing one GPU count once)
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(t_step * 1e3, 4),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "fp32",
-            "data": "synthetic (rank-valued 1 GiB fp32 buffer; MNIST-shaped random images, random-init weights)",
-            "config": {
-                "model": "allreduce-1GiB-fp32 + MNIST-shaped TP transformer layer (768->256 qkv, 256->10 fc_o per token)",
-                "global_batch": (harness or {}).get("global_batch"),
-                "seq_len": (harness or {}).get("seq_len"),
-                "parallelism": f"dp{dp}xtp{tp}" if harness else f"allreduce-world{world}",
-                "allreduce_algo": best,
-                "allreduce_bytes": nbytes,
-                "busbw_GBps": round(busbw, 3),
-                # one xGMI link per GPU pair (fully connected, <= 7 per GPU), ~153.6 GB/s each per
-                # direction: the all-reduce's bus bandwidth as a fraction of the links it can drive
-                "xgmi_link_frac": (round(busbw / (min(world - 1, 7) * XGMI_LINK_GBPS), 3)
-                                   if world > 1 and not dev.shared_device else None),
-                "candidates_ms": {a: (round(t * 1e3, 4) if t else None) for a, t in results.items()},
-                "result_exact": final_ok,
-                "self_test": self_test,
-                "shared_gpu": dev.shared_device,
-                **secondary,
-            },
-        }
-        if harness:
-            out["config"]["tp_fwd_step_ms"] = round(harness["fwd_ms"], 4)
-            out["config"]["tp_train_step_ms"] = round(harness.get("train_ms", float("nan")), 4)
-            out["config"]["harness"] = {k: v for k, v in harness.items() if k not in ("fwd_ms", "train_ms")}
-        if mlp is not None:
-            out["config"]["tp_mlp"] = mlp
-        if dry is not None:
-            out["config"]["shared_gpu_dry_run"] = dry
-        _write_result(args, rank, out)
+    _write_result(args, rank, out)
     return 0
 
 

@@ -32,11 +32,13 @@ ap.add_argument("--iters", type=int, default=10)
 ap.add_argument("--warmup", type=int, default=3)
 ap.add_argument("--eager-gate", action="store_true",
                 help="SwiGLU gate as eager torch ops (A/B against the gate fused into the GEMM epilogue)")
+ap.add_argument("--variants", action="store_true", help="p > 1: every row-parallel mode side by side")
+ap.add_argument("--mode", default="", help="row-parallel mode of the main record (plain | chunked | fused)")
 args = ap.parse_args()
 comm = Communicator(MPI.COMM_WORLD)
 local = int(os.environ.get("LOCAL_RANK", os.environ.get("CCMPI_LOCAL_RANK", "0")))
 torch.cuda.set_device(local % torch.cuda.device_count())
 res = measure_tp_mlp(comm, tokens=args.tokens, d=args.d, ffn=args.ffn, iters=args.iters, warmup=args.warmup,
-                     eager_gate=args.eager_gate)
+                     eager_gate=args.eager_gate, variants=args.variants, mode=args.mode)
 if comm.Get_rank() == 0:
     print(json.dumps({"bench": "tp_mlp", **res}), flush=True)

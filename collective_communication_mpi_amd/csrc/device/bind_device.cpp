@@ -117,6 +117,17 @@ PYBIND11_MODULE(_device, m) {
         auto r = d.export_range((uint64_t)base);
         return py::make_tuple(py::bytes(r.first), (uint64_t)base, (uint64_t)sz);
       })
+      .def_static("alloc_id", [](uint64_t ptr) -> uint64_t {
+        // the driver's unique id of the allocation holding ptr (0 if unknown): a range
+        // freed and reallocated at the same address gets a new id
+        unsigned long long id = 0;
+        if (hipPointerGetAttribute(&id, HIP_POINTER_ATTRIBUTE_BUFFER_ID, reinterpret_cast<hipDeviceptr_t>(ptr)) !=
+            hipSuccess) {
+          (void)hipGetLastError();
+          return 0;
+        }
+        return (uint64_t)id;
+      })
       .def("set_segment", [](DeviceComm& d, int s, uint64_t ptr, uint64_t bytes, const std::vector<py::bytes>& hs,
                              const std::vector<uint64_t>& offs, const std::vector<py::bytes>& ks) {
         std::vector<std::string> h(hs.begin(), hs.end()), k(ks.begin(), ks.end());
@@ -131,6 +142,7 @@ PYBIND11_MODULE(_device, m) {
       })
       .def_property_readonly("scratch_bytes", &DeviceComm::scratch_bytes)
       .def("allreduce", &DeviceComm::allreduce, py::call_guard<py::gil_scoped_release>())
+      .def("allreduce_to_local", &DeviceComm::allreduce_to_local, py::call_guard<py::gil_scoped_release>())
       .def("reduce_scatter", &DeviceComm::reduce_scatter, py::call_guard<py::gil_scoped_release>())
       .def("allgather", &DeviceComm::allgather, py::arg("inp"), py::arg("out"), py::arg("bytes_per_rank"),
            py::arg("stream"), py::arg("max_blocks"), py::arg("symmetric"), py::arg("mode") = 0,

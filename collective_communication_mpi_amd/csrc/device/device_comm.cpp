@@ -359,6 +359,27 @@ void DeviceComm::allreduce(uint64_t in, uint64_t out, uint64_t count, int dtype,
   }
 }
 
+void DeviceComm::allreduce_to_local(uint64_t in, uint64_t out, uint64_t count, int dtype, int op, uint64_t stream,
+                                    int max_blocks) {
+  const uint64_t es = dtype_bytes(dtype), nbytes = count * es;
+  if (!device_reduce_supported(dtype, op)) throw std::invalid_argument("ccmpi: unsupported device reduction");
+  if (nbytes == 0) return;
+  CCMPI_HIP_CHECK(hipSetDevice(device_));
+  hipStream_t st = S(stream);
+  if (size_ == 1) {
+    if (in != out) launch_copy((const void*)in, (void*)out, nbytes, st);
+    return;
+  }
+  const uint64_t sc = code_of_(in, nbytes);
+  if (!sc || out % 16 || in == out)
+    throw std::invalid_argument("ccmpi: allreduce_to_local needs a 16-B aligned symmetric source and a distinct 16-B "
+                                "aligned output");
+  // res = src: the reduce-scatter writes shard r into rank r's own source, the
+  // all-gather reads every rank's source shard into the local output
+  launch_allreduce(ALGO_TWOSHOT, args_(sc, sc, (char*)out, nbytes, 0), size_, dtype, op, grid_(nbytes / size_, max_blocks),
+                   st);
+}
+
 void DeviceComm::allreduce_ll_(uint64_t in, uint64_t out, uint64_t nbytes, int dtype, int op, hipStream_t st,
                                int max_blocks) {
   // misaligned local buffers go through the scratch segment (local copies only:

@@ -66,6 +66,13 @@ class DeviceComm {
   // scratch segment in chunks whose size is identical on all ranks.
   void allreduce(uint64_t in, uint64_t out, uint64_t count, int dtype, int op, int algo,
                  uint64_t stream, int max_blocks, bool symmetric);
+  // Two-shot all-reduce whose reduce-scatter lands in the (registered, symmetric)
+  // source itself -- rank r's reduced shard r overwrites its own source shard r,
+  // which no peer reads -- and whose all-gather pulls the shards into `out`, a
+  // LOCAL buffer that needs no registration.  The source is clobbered: it is the
+  // scratch of a GEMM's partial product (TP row-parallel output, dX partial).
+  void allreduce_to_local(uint64_t in, uint64_t out, uint64_t count, int dtype, int op, uint64_t stream,
+                          int max_blocks);
   void reduce_scatter(uint64_t in, uint64_t out, uint64_t count_per_rank, int dtype, int op,
                       uint64_t stream, int max_blocks, bool symmetric);
   // mode: A2A_PULL (default) or A2A_PUSH (every rank's output registered: the

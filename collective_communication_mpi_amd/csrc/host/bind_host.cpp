@@ -13,6 +13,7 @@ using namespace ccmpi;
 
 namespace ccmpi {
 int register_fastcall(PyObject* module);  // fastcall.cpp
+int install_crash_handler(int fd);        // crash.cpp
 }
 
 namespace {
@@ -67,6 +68,8 @@ PYBIND11_MODULE(_host, m) {
 
   if (register_fastcall(m.ptr()) != 0) throw py::error_already_set();
   m.def("wtime", &wtime);
+  m.def("install_crash_handler", &install_crash_handler, py::arg("fd") = 2,
+        "Print a native backtrace on SIGSEGV/SIGBUS/SIGILL/SIGFPE/SIGABRT, then chain to the previous handler");
   m.def("job_id", &job_id_from_env);
   m.def("dtype_size", &dtype_size);
   m.def("reduce_supported", &reduce_supported);

@@ -178,6 +178,31 @@ def save_tuning(path: str, key: str, table: Dict[Tuple[int, int], str]) -> None:
     os.replace(tmp, path)
 
 
+class _CountingComm:
+    """Proxy of the host communicator that counts the host calls the device plane makes
+    (``calls``): a steady-state device collective should make none (tests)."""
+
+    def __init__(self, comm) -> None:
+        self._comm = comm
+        self.calls = 0
+
+    def __getattr__(self, name):
+        attr = getattr(self._comm, name)
+        if not callable(attr):
+            return attr
+
+        def counted(*a, **k):
+            self.calls += 1
+            return attr(*a, **k)
+
+        return counted
+
+
+# set by any DeviceGroup of this process whose ranks share one GPU (tensor_parallel uses it
+# for groups of one rank, which cannot measure sharing themselves)
+SHARED_GPU_IN_PROCESS = False
+
+
 def _env_int(name: str, default: int) -> int:
     v = os.environ.get(name)
     return int(v) if v else default
@@ -190,7 +215,7 @@ class DeviceGroup:
         import torch
 
         self.torch = torch
-        self.host = host_comm
+        self.host = _CountingComm(host_comm)
         self.rank = host_comm.Get_rank()
         self.size = host_comm.Get_size()
         if device is None:
@@ -215,6 +240,8 @@ class DeviceGroup:
         self.ranks_per_device = keys.count(key)
         self.shared_device = self.ranks_per_device > 1
         if self.shared_device:
+            global SHARED_GPU_IN_PROCESS
+            SHARED_GPU_IN_PROCESS = True
             # The LDS-ring GEMM needs a whole CU per workgroup (128 KiB LDS, 512 VGPRs a
             # wave); next to another rank's spinning collective CTAs (one per CU) none of
             # its workgroups can start, and the two ranks wait on each other (TP = 2 MLP
@@ -275,13 +302,26 @@ class DeviceGroup:
         self._dyn: "OrderedDict[tuple, int]" = OrderedDict()  # identity of every rank's allocation -> slot
         self._exports: Dict[int, Tuple[bytes, int, int]] = {}  # allocation base -> (handle, base, bytes)
         self._free_slots: List[int] = []  # released slot indices (reused before new ones)
-        self._alloc_gen = None
         self.registrations = 0  # slots (re)mapped so far (tests, traces)
+        # slots a captured HIP graph resolves: never evicted or cleared (the graph baked
+        # in their (segment, offset) codes); see _register_call / unpin_captured
+        self._pinned: set = set()
+        # persistent symmetric-heap buffers by key (persistent()): allocated once, so the
+        # steady state allocates nothing and makes no host call
+        self._persist: Dict[tuple, object] = {}
+        # CCMPI_VERIFY_SYMMETRIC=1: every heap-only collective >= reg_min checks with one
+        # host all-gather that every rank passed heap blocks (debug; off = no host call)
+        self.verify_symmetric = os.environ.get("CCMPI_VERIFY_SYMMETRIC", "0") not in ("0", "")
         self._lock = threading.Lock()
         self._watchdog: Optional[threading.Thread] = None
         mode = os.environ.get("CCMPI_WATCHDOG", "warn").lower()
         if mode in ("warn", "abort"):
             self.start_watchdog(mode)
+
+    @property
+    def host_calls(self) -> int:
+        """Host-plane calls this group has made (bootstrap, registration, heap growth)."""
+        return self.host.calls
 
     # ---------------------------------------------------------------- watchdog
     def start_watchdog(self, mode: str = "warn", period_s: float = 0.2) -> None:
@@ -380,6 +420,27 @@ class DeviceGroup:
         self._register(raw)
         self.heap.add_arena(raw.data_ptr(), arena)
 
+    def persistent(self, key, shape, dtype=None):
+        """A symmetric-heap buffer cached under ``(key, shape, dtype)``: the first call
+        allocates it (collective, like ``empty``; every rank must ask for the same keys in
+        the same order), later calls return the same tensor with no host call.  For
+        scratch that never escapes its owner -- the TP layers' GEMM partial products,
+        which their all-reduce clobbers (``allreduce_to_local``)."""
+        torch = self.torch
+        dtype = dtype or torch.float32
+        shape = (shape,) if isinstance(shape, int) else tuple(int(s) for s in shape)
+        k = (key, shape, dtype)
+        t = self._persist.get(k)
+        if t is None:
+            t = self._persist[k] = self.empty(shape, dtype)
+        return t
+
+    def release_persistent(self, key=None) -> None:
+        """Drop cached persistent buffers (all, or those of ``key``); their blocks return
+        to the heap when no other reference remains."""
+        for k in [k for k in self._persist if key is None or k[0] == key]:
+            del self._persist[k]
+
     def zeros(self, shape, dtype=None):
         t = self.empty(shape, dtype)
         t.zero_()
@@ -450,7 +511,7 @@ class DeviceGroup:
         self._ensure_fused(tiles)
         if out is None:
             out = self.empty((M, N), torch.bfloat16)
-        elif not self._register_call((out,)):  # collective: heap blocks pass through
+        elif not (self._symm(out) or self._register_call((out,))):  # heap blocks: no host call
             raise ValueError("gemm_allreduce: out could not be registered")
         bk, bp = 0, 0
         if bias is not None:
@@ -530,23 +591,43 @@ class DeviceGroup:
         on-demand registration of whatever the tensors live in."""
         if self.size == 1 or self.reg_min <= 0 or nbytes < self.reg_min:
             return self._symm(*ts)
+        heap = self._symm(*ts)
+        if self.verify_symmetric and len(set(self.host.allgather(heap))) > 1:
+            raise RuntimeError("collective: symmetric-heap tensors on some ranks only")
+        if heap:
+            # every tensor is a symmetric-heap block here: the same contract as below
+            # reg_min (heap blocks on one rank are heap blocks on every rank), so no host
+            # call; CCMPI_VERIFY_SYMMETRIC=1 checks the contract with one all-gather
+            return True
         return self._register_call(ts)
 
     def _alloc_generation(self) -> int:
-        """Segments this process's caching allocator has returned to the driver: a
-        change means an address range may now hold a different allocation."""
+        """Segments this process's caching allocator has returned to the driver (the
+        fallback identity when the driver has no allocation ids)."""
         try:
             return int(self.torch._C._cuda_memoryStats(self.device.index or 0)["segment"]["all"]["freed"])
         except Exception:  # noqa: BLE001 - stats unavailable: assume nothing is ever freed
             return 0
 
+    def _alloc_identity(self, base: int) -> int:
+        """Identity of the allocation at ``base``: the driver's unique buffer id (a range
+        freed and reallocated at the same address gets a new one, an unrelated free
+        changes nothing), or the allocator's global free count if the driver has none."""
+        aid = self.D.DeviceComm.alloc_id(base)
+        return (1 << 63) | aid if aid else self._alloc_generation()
+
     def _export(self, ptr: int):
-        """(IPC handle, allocation base, allocation bytes) of the allocation holding ``ptr``."""
-        for base, ent in self._exports.items():
+        """(IPC handle, allocation base, allocation bytes, identity) of the allocation
+        holding ``ptr``; cached per base while the base's identity is unchanged."""
+        for base, ent in list(self._exports.items()):
             if base <= ptr < base + ent[2]:
-                return ent
-        ent = tuple(self.dc.export_alloc(ptr))
-        self._exports[ent[1]] = ent
+                if self._alloc_identity(base) == ent[3]:
+                    return ent
+                del self._exports[base]  # freed and reallocated: export the new allocation
+                break
+        h, base, size = self.dc.export_alloc(ptr)
+        ent = (h, base, size, self._alloc_identity(base))
+        self._exports[base] = ent
         return ent
 
     def _register_call(self, ts) -> bool:
@@ -554,10 +635,6 @@ class DeviceGroup:
         segment slots.  Returns False (staged path, on every rank) when any rank's
         tensor cannot be exported or is misaligned, or when a new mapping would be
         needed during a HIP graph capture."""
-        gen = self._alloc_generation()
-        if gen != self._alloc_gen:
-            self._exports.clear()
-            self._alloc_gen = gen
         mine = []
         for t in ts:
             if t.data_ptr() % 16:
@@ -567,11 +644,10 @@ class DeviceGroup:
                 mine.append(None)  # a heap block: already mapped everywhere
                 continue
             try:
-                h, base, size = self._export(t.data_ptr())
+                mine.append(self._export(t.data_ptr()))
             except Exception:  # noqa: BLE001 - not an exportable device allocation
                 mine = None
                 break
-            mine.append((h, base, size, gen))
         rows = self.host.allgather(mine)
         if any(r is None for r in rows):
             return False
@@ -588,21 +664,24 @@ class DeviceGroup:
             if any(x is None for x in ids):
                 # mixed heap / non-heap: every rank maps its own allocation; heap ranks
                 # export their arena (never freed while the group lives)
-                if mine[i] is None:
-                    h, base, size = self._export(ts[i].data_ptr())
-                    mine_i = (h, base, size, gen)
-                else:
-                    mine_i = mine[i]
+                mine_i = self._export(ts[i].data_ptr()) if mine[i] is None else mine[i]
                 ids = self.host.allgather(mine_i)
             key = tuple(ids)
             slot = self._dyn.get(key)
             if slot is not None:
                 self._dyn.move_to_end(key)
+                if capturing:
+                    self._pinned.add(key)  # the graph bakes in this slot's codes
                 continue
             if capturing:
                 return False
             self._map_slot(key)
         return True
+
+    def unpin_captured(self) -> None:
+        """Release the slots pinned by HIP-graph captures (call after dropping every graph
+        that captured collectives on registered tensors): they may be evicted again."""
+        self._pinned.clear()
 
     def _map_slot(self, key) -> None:
         """Collective: map the allocation set ``key`` (one (handle, base, bytes, gen) per
@@ -611,14 +690,23 @@ class DeviceGroup:
         table stays identical everywhere)."""
         torch = self.torch
         stale = stale_keys(self._dyn.keys(), key)
-        if stale or (not self._free_slots and len(self._dyn) >= self.reg_slots):
+        pinned = [k for k in stale if k in self._pinned]
+        if pinned:
+            # a captured graph resolves that slot: remapping it would make the next replay
+            # read unmapped memory or another allocation (ADVICE r3)
+            raise RuntimeError("collective: memory a captured HIP graph's collective uses was freed and reallocated; "
+                               "drop the graph and call unpin_captured() first")
+        evictable = [k for k in self._dyn if k not in self._pinned]
+        full = not self._free_slots and len(self._dyn) >= self.reg_slots
+        if stale or (full and evictable):
             torch.cuda.synchronize(self.device)  # no queued kernel of this rank still resolves a slot
         for k in stale:
             s = self._dyn.pop(k)
             self.dc.clear_segment(s)
             self._free_slots.append(s)
-        if not self._free_slots and len(self._dyn) >= self.reg_slots:
-            self._free_slots.append(self._dyn.popitem(last=False)[1])  # least recently used
+        if not self._free_slots and len(self._dyn) >= self.reg_slots and evictable:
+            self._free_slots.append(self._dyn.pop(evictable[0]))  # least recently used unpinned slot
+        # (every slot pinned by captures: a new slot beyond CCMPI_REGISTER_SLOTS)
         slot = self._free_slots.pop() if self._free_slots else -1
         me = key[self.rank]
         handles = [k[0] for k in key]
@@ -688,6 +776,26 @@ class DeviceGroup:
             self.dc.rccl_allreduce(src.data_ptr(), dst.data_ptr(), src.numel(), dt, opc, s)
         else:
             raise ValueError(f"unknown allreduce algorithm {algo!r}")
+        return dst
+
+    @trace_call("allreduce")
+    def allreduce_to_local(self, src, dst, op="SUM", max_blocks: Optional[int] = None):
+        """``dst = sum over ranks of src`` where ``src`` is a symmetric-heap block (on every
+        rank) that the collective CLOBBERS and ``dst`` is any local CUDA tensor (no
+        registration, no host call): two-shot whose reduce-scatter lands in the source's
+        own shard and whose all-gather pulls every rank's shard into ``dst``
+        (``DeviceComm::allreduce_to_local``).  The TP layers' GEMMs write their partial
+        products into persistent heap scratch (``persistent``) and reduce them into
+        fresh outputs this way: zero-copy, and the output is an ordinary tensor."""
+        self._check(src, "src")
+        self._check(dst, "dst")
+        if src.numel() != dst.numel() or src.dtype != dst.dtype:
+            raise ValueError("allreduce_to_local: src/dst must match in size and dtype")
+        if self.size > 1 and not self._symm(src):
+            raise ValueError("allreduce_to_local: src must be a 16-B aligned symmetric-heap block (comm.empty / "
+                             "persistent)")
+        self.dc.allreduce_to_local(src.data_ptr(), dst.data_ptr(), src.numel(), dtype_code(src.dtype), op_code(op),
+                                   self._stream(), self._budget(max_blocks))
         return dst
 
     @trace_call("reduce_scatter")
@@ -1010,7 +1118,7 @@ class DeviceGroup:
                 if isinstance(t, torch.Tensor) and t.is_cuda:
                     t.record_stream(stream)
         with torch.cuda.stream(stream):
-            if op in ("allreduce", "allgather", "alltoall", "reduce_scatter"):
+            if op in ("allreduce", "allreduce_to_local", "allgather", "alltoall", "reduce_scatter"):
                 kw.setdefault("max_blocks", self.overlap_blocks)  # runs beside compute
             out = fn(*args, **kw)
             done = torch.cuda.Event()

@@ -11,7 +11,9 @@ from .layout import (  # noqa: F401
 from .ddp import DistributedDataParallel, ddp_wrap  # noqa: F401,E402
 from .tensor_parallel import (  # noqa: F401,E402
     ColumnParallelLinear,
+    ParallelSwiGLUMLP,
     RowParallelLinear,
+    all_reduce,
     all_reduce_,
     copy_to_tensor_parallel_region,
     gather_from_tensor_parallel_region,

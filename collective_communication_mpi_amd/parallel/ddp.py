@@ -21,7 +21,13 @@ gradient all-reduce on that DP communicator:
   backward GEMM tiles queued behind them);
 * ``finish()`` (call after ``backward()``, before the optimizer) launches
   buckets whose parameters got no gradient, joins the side stream and applies
-  the 1/dp average.
+  the 1/dp average;
+* gradient sinks (``grad_sink=True``, CUDA): the framework's own layers
+  (tensor_parallel: Column/RowParallelLinear, ParallelSwiGLUMLP) write their weight
+  gradients straight into the bucket views from the dW GEMM and notify the bucket
+  themselves -- autograd then has no gradient tensor to accumulate, which saves
+  an extra read-read-write pass over every such gradient (16 GB of bf16 per
+  Llama-3-8B step).  Other parameters go through AccumulateGrad and the hook.
 
 CPU tensors are reduced by the C++ host plane (the reference's CPU setting).
 """
@@ -36,7 +42,7 @@ from .layout import _host_comm, device_group_for
 
 
 class _Bucket:
-    __slots__ = ("params", "buf", "pending", "launched", "event")
+    __slots__ = ("params", "buf", "pending", "launched", "event", "sinks")
 
     def __init__(self, params, buf):
         self.params = params
@@ -44,13 +50,45 @@ class _Bucket:
         self.pending = len(params)
         self.launched = False
         self.event = None
+        self.sinks = []
+
+
+class _GradSink:
+    """Where a layer's backward writes a parameter's gradient (``param._ccmpi_grad_sink``):
+    ``begin()`` returns (bucket view, accumulate?) -- overwrite after ``zero_grad`` (or when
+    the user dropped ``.grad``), add when accumulating micro-batches -- and ``done()``
+    counts the parameter ready in its bucket, exactly like the post-accumulate hook."""
+
+    __slots__ = ("ddp", "param", "view", "fresh")
+
+    def __init__(self, ddp, param, view):
+        self.ddp, self.param, self.view, self.fresh = ddp, param, view, True
+
+    def begin(self):
+        q = self.param
+        if q.grad is None or q.grad.data_ptr() != self.view.data_ptr():
+            # grad dropped (zero_grad(set_to_none=True)) or replaced: the bucket view is the
+            # gradient again, and it is overwritten
+            if q.grad is not None:
+                self.view.copy_(q.grad)
+                self.fresh = False
+            else:
+                self.fresh = True
+            q.grad = self.view
+        acc = not self.fresh
+        self.fresh = False
+        return self.view, acc
+
+    def done(self):
+        self.ddp._ready(self.param)
 
 
 class DistributedDataParallel(torch.nn.Module):
     """Wraps ``module``; ``comm`` is the DP communicator (Communicator or host Comm)."""
 
     def __init__(self, module: torch.nn.Module, comm, bucket_bytes: Optional[int] = None, algo: str = "auto",
-                 average: bool = True, overlap: bool = True, broadcast_params: bool = True):
+                 average: bool = True, overlap: bool = True, broadcast_params: bool = True, grad_sink: bool = True,
+                 max_blocks: Optional[int] = None):
         super().__init__()
         if bucket_bytes is None:
             # bucket sweep (profiles/r2_overlap/buckets.md): per-call cost makes buckets
@@ -62,6 +100,8 @@ class DistributedDataParallel(torch.nn.Module):
         self.p = self.hc.Get_size()
         self.algo = algo
         self.average = average
+        self.require_backward_grad_sync = True  # False: buckets fill but are not reduced (no_sync)
+        self.max_blocks = max_blocks  # CTA budget of the bucket all-reduces (None: the group's overlap_blocks)
         params = [q for q in module.parameters() if q.requires_grad]
         if not params:
             raise ValueError("DistributedDataParallel: the module has no trainable parameters")
@@ -90,6 +130,19 @@ class DistributedDataParallel(torch.nn.Module):
         self.stream = (torch.cuda.Stream(device=dev, priority=-1)
                        if (dev.type == "cuda" and overlap and self.p > 1 and not crowded) else None)
         self._hooks = [q.register_post_accumulate_grad_hook(self._on_grad) for q in params]
+        if grad_sink and dev.type == "cuda":
+            # the weights of the framework's TP layers, whose backward delivers dW itself;
+            # every other parameter (biases, norms, embeddings, foreign modules) keeps the
+            # AccumulateGrad + hook path
+            from .tensor_parallel import ColumnParallelLinear, RowParallelLinear
+
+            capable = {id(m.weight) for m in module.modules() if isinstance(m, (ColumnParallelLinear, RowParallelLinear))}
+            for b in self.buckets:
+                for q in b.params:
+                    if id(q) in capable:
+                        sk = _GradSink(self, q, self._view_of[id(q)])
+                        q._ccmpi_grad_sink = sk
+                        b.sinks.append(sk)
 
     # ------------------------------------------------------------------ setup
     def _broadcast_params(self, params) -> None:
@@ -131,13 +184,22 @@ class DistributedDataParallel(torch.nn.Module):
             # fresh tensor -- move it into the bucket and re-attach the view
             v.copy_(q.grad)
             q.grad = v
+        sk = getattr(q, "_ccmpi_grad_sink", None)
+        if sk is not None:
+            sk.fresh = False  # the bucket view now holds this step's gradient
+        self._ready(q)
+
+    def _ready(self, q) -> None:
         b = self._bucket_of[id(q)]
         b.pending -= 1
+        if b.pending < 0:
+            raise RuntimeError("DistributedDataParallel: a parameter produced two gradients in one backward "
+                               "(shared weight?) -- build DDP with grad_sink=False")
         if b.pending == 0:
             self._launch(b)
 
     def _launch(self, b: _Bucket) -> None:
-        if b.launched or self.p == 1:
+        if b.launched or self.p == 1 or not self.require_backward_grad_sync:
             b.launched = True
             return
         b.launched = True
@@ -153,16 +215,22 @@ class DistributedDataParallel(torch.nn.Module):
         ev.record(torch.cuda.current_stream(self.device))
         self.stream.wait_event(ev)
         with torch.cuda.stream(self.stream):  # beside the backward: the overlap CTA budget
-            self.dev.allreduce(b.buf, b.buf, "SUM", self.algo, max_blocks=self.dev.overlap_blocks)
+            self.dev.allreduce(b.buf, b.buf, "SUM", self.algo, max_blocks=self.max_blocks or self.dev.overlap_blocks)
 
     def finish(self) -> None:
         """Complete the gradient synchronisation (after backward, before the step)."""
         for b in self.buckets:  # parameters that received no gradient this step
             if not b.launched:
+                for sk in b.sinks:
+                    if sk.fresh:  # no gradient since zero_grad: the view must read as zero
+                        sk.view.zero_()
+                        sk.fresh = False
                 self._launch(b)
         if self.stream is not None:
             torch.cuda.current_stream(self.device).wait_stream(self.stream)
-        if self.average and self.p > 1:
+        if self.average and self.p > 1 and self.require_backward_grad_sync:
+            # (no_sync micro-batches: the local sums keep accumulating, the synchronising
+            # backward reduces and averages all of them at once)
             for b in self.buckets:
                 b.buf.mul_(1.0 / self.p)
         for b in self.buckets:
@@ -170,11 +238,29 @@ class DistributedDataParallel(torch.nn.Module):
             b.launched = False
 
     def zero_grad(self, set_to_none: bool = False) -> None:
-        """Zero the buckets and re-attach every ``.grad`` view (``set_to_none`` is ignored)."""
+        """Zero the gradients and re-attach every ``.grad`` view (``set_to_none`` is ignored).
+        Gradients with a sink are not written: the next backward overwrites them (and
+        ``finish`` zeroes the ones it did not reach)."""
         for b in self.buckets:
-            b.buf.zero_()
+            sunk = {id(sk.param) for sk in b.sinks}
+            if not sunk:
+                b.buf.zero_()
+            else:
+                for q in b.params:
+                    if id(q) not in sunk:
+                        self._view_of[id(q)].zero_()
+                for sk in b.sinks:
+                    sk.fresh = True
             for q in b.params:
                 q.grad = self._view_of[id(q)]
+
+    def allreduce_all(self) -> None:
+        """All-reduce every bucket now, back to back on the current stream (the comm-only
+        time of the overlap measurement; no averaging)."""
+        if self.dev is None or self.p == 1:
+            return
+        for b in self.buckets:
+            self.dev.allreduce(b.buf, b.buf, "SUM", self.algo, max_blocks=self.max_blocks or self.dev.overlap_blocks)
 
     @property
     def bucket_sizes(self) -> List[int]:

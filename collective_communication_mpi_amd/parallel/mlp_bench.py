@@ -4,9 +4,9 @@ ranks: over xGMI when each rank has its own GPU).
 
 The block is ``y = W_down (silu(W_gate x) * W_up x)``; the gate|up GEMM carries the SwiGLU
 gate in its epilogue, the down GEMM's partial output is summed by one TP all-reduce
-(forward) and dX of gate|up by another (backward).  This is the reference's TP layer
-(model/func_impl.py:65-109: column-parallel projections, row-parallel output, collective
-between) on a realistic shape."""
+(forward) and dX of gate|up by another (backward, overlapped with the dW GEMM).  This is
+the reference's TP layer (model/func_impl.py:65-109: column-parallel projections,
+row-parallel output, collective between) on a realistic shape."""
 from __future__ import annotations
 
 import statistics
@@ -15,26 +15,25 @@ from typing import Dict
 
 import torch
 
+from . import tensor_parallel as tp
 from .tensor_parallel import ParallelSwiGLUMLP, all_reduce_
 
 
 def measure_tp_mlp(comm, tokens: int = 4096, d: int = 4096, ffn: int = 14336, iters: int = 10, warmup: int = 3,
-                   eager_gate: bool = False) -> Dict:
+                   eager_gate: bool = False, variants: bool = False, mode: str = "") -> Dict:
     """Median forward and forward + backward times (max over ranks), the whole group's
-    model TFLOP/s, and the T x d bf16 TP all-reduce alone.  Collective: every rank calls."""
+    model TFLOP/s, the T x d bf16 TP all-reduce alone, and the host calls the device
+    plane made during one steady-state forward + backward (0 expected).  ``variants``
+    (p > 1): the same block with each row-parallel mode (plain / chunked / fused) side by
+    side.  Collective: every rank calls."""
     from .. import mpi as MPI
 
     hc = comm.comm
     p = comm.Get_size()
     dev = torch.device("cuda", torch.cuda.current_device())
-    mlp = ParallelSwiGLUMLP(d, ffn, comm, device=dev, dtype=torch.bfloat16, seed=1)
-    gate_up, down = mlp.gate_up, mlp.down
 
-    def block(x):
-        if not eager_gate:
-            return mlp(x)
-        h = gate_up(x)
-        return down(torch.nn.functional.silu(h[:, 0::2]) * h[:, 1::2])  # shard rows are (gate, up) pairs
+    def build(m):
+        return ParallelSwiGLUMLP(d, ffn, comm, device=dev, dtype=torch.bfloat16, seed=1, mode=m)
 
     x = (torch.randn(tokens, d, generator=torch.Generator().manual_seed(3)) * 0.5).to(torch.bfloat16).to(dev)
     x.requires_grad_(True)
@@ -53,27 +52,62 @@ def measure_tp_mlp(comm, tokens: int = 4096, d: int = 4096, ffn: int = 14336, it
             ts.append(time.perf_counter() - t0)
         return hc.allreduce(statistics.median(ts), op=MPI.MAX)
 
-    def fwd():
-        with torch.no_grad():
-            block(x)
+    def run(mlp):
+        gate_up, down = mlp.gate_up, mlp.down
 
-    def fwd_bwd():
-        x.grad = None
-        gate_up.weight.grad = None
-        down.weight.grad = None
-        block(x).backward(gy)
+        def block(xx):
+            if not eager_gate:
+                return mlp(xx)
+            h = gate_up(xx)
+            return down(torch.nn.functional.silu(h[:, 0::2]) * h[:, 1::2])  # shard rows are (gate, up) pairs
 
-    t_f = timed(fwd)
-    t_fb = timed(fwd_bwd)
+        def fwd():
+            with torch.no_grad():
+                block(x)
+
+        def fwd_bwd():
+            x.grad = None
+            gate_up.weight.grad = None
+            down.weight.grad = None
+            block(x).backward(gy)
+
+        t_f = timed(fwd)
+        t_fb = timed(fwd_bwd)
+        host = None
+        if p > 1:
+            dg = comm.dev if mlp.comm is comm else tp.device_group_for(mlp.comm)
+            torch.cuda.synchronize()
+            h0 = dg.host_calls
+            fwd_bwd()
+            torch.cuda.synchronize()
+            host = dg.host_calls - h0
+        with torch.no_grad():  # checksum: identical across TP degrees up to bf16 rounding
+            chk = float(block(x).float().abs().mean().item())
+        return t_f, t_fb, host, chk
+
+    flop_f = 2 * tokens * d * 2 * ffn + 2 * tokens * ffn * d  # whole block (all ranks together)
+    default_mode = mode or tp._ROW_MODE
+    calls0 = dict(tp.CALLS)
+    t_f, t_fb, host, chk = run(build(mode))
+    paths = {k: v - calls0.get(k, 0) for k, v in tp.CALLS.items() if v != calls0.get(k, 0)}
     buf = torch.randn(tokens, d, device=dev).to(torch.bfloat16)
     t_ar = timed(lambda: all_reduce_(buf, comm)) if p > 1 else 0.0
-    with torch.no_grad():  # checksum: identical across TP degrees up to bf16 rounding
-        chk = float(block(x).float().abs().mean().item())
-    flop_f = 2 * tokens * d * 2 * ffn + 2 * tokens * ffn * d  # whole block (all ranks together)
-    return {
-        "tp": p, "gate": "eager" if eager_gate else "fused", "tokens": tokens, "d_model": d, "ffn": ffn,
+    out = {
+        "tp": p, "gate": "eager" if eager_gate else "fused", "row_mode": default_mode if p > 1 else "local",
+        "tokens": tokens, "d_model": d, "ffn": ffn,
         "dtype": "bf16", "shared_gpu": bool(comm.dev.shared_device) if p > 1 else False,
         "fwd_ms": round(t_f * 1e3, 3), "fwd_bwd_ms": round(t_fb * 1e3, 3),
         "fwd_TFLOPs": round(flop_f / t_f / 1e12, 1), "fwd_bwd_TFLOPs": round(3 * flop_f / t_fb / 1e12, 1),
         "tp_allreduce_bytes": tokens * d * 2, "tp_allreduce_ms": round(t_ar * 1e3, 3),
-        "out_abs_mean": round(chk, 6)}
+        "host_calls_per_step": host, "tp_paths": paths, "out_abs_mean": round(chk, 6)}
+    if variants and p > 1:
+        var = {}
+        for m in tp.ROW_MODES:
+            try:
+                vf, vfb, vh, vchk = run(build(m))
+                var[m] = {"fwd_ms": round(vf * 1e3, 3), "fwd_bwd_ms": round(vfb * 1e3, 3), "host_calls_per_step": vh,
+                          "out_abs_mean": round(vchk, 6)}
+            except Exception as e:  # noqa: BLE001 - one variant must not cost the record
+                var[m] = {"error": f"{type(e).__name__}: {e}"[:200]}
+        out["row_mode_variants"] = var
+    return out

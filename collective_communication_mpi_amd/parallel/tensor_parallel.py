@@ -28,6 +28,7 @@ dtypes use ``torch.matmul``.
 """
 from __future__ import annotations
 
+import collections
 import math
 import os
 
@@ -43,7 +44,8 @@ def _size_rank(comm):
 
 
 def all_reduce_(t: torch.Tensor, comm) -> torch.Tensor:
-    """In-place SUM over ``comm`` of a contiguous tensor (device or host plane)."""
+    """In-place SUM over ``comm`` of a contiguous tensor (device or host plane): ``t`` is
+    overwritten with the sum (use ``all_reduce`` to keep it)."""
     p, _ = _size_rank(comm)
     if p == 1:
         return t
@@ -56,6 +58,19 @@ def all_reduce_(t: torch.Tensor, comm) -> torch.Tensor:
 
         _host_comm(comm).Allreduce(MPI.IN_PLACE, t.detach().numpy(), op=MPI.SUM)
     return t
+
+
+def all_reduce(t: torch.Tensor, comm) -> torch.Tensor:
+    """SUM over ``comm`` into a new tensor; ``t`` is not modified (device or host plane)."""
+    p, _ = _size_rank(comm)
+    if p == 1:
+        return t
+    out = torch.empty_like(t, memory_format=torch.contiguous_format)
+    if t.is_cuda:
+        device_group_for(comm).allreduce(t.contiguous(), out, "SUM")
+        return out
+    out.copy_(t)
+    return all_reduce_(out, comm)
 
 
 def _gather_last(x: torch.Tensor, comm) -> torch.Tensor:
@@ -81,9 +96,9 @@ def _slice_last(x: torch.Tensor, comm) -> torch.Tensor:
 
 
 class _CopyToTP(torch.autograd.Function):
-    """Identity forward, TP all-reduce of the gradient (Megatron "f").  The gradient
-    is reduced in place: autograd hands this node a buffer it owns, and the device
-    plane registers it on demand (no copy in or out, DeviceGroup._register_call)."""
+    """Identity forward, TP all-reduce of the gradient (Megatron "f").  Out of place: the
+    incoming gradient may be aliased (e.g. handed unchanged to two branches by an add),
+    so it is never modified; the reduced gradient is a fresh tensor."""
 
     @staticmethod
     def forward(ctx, x, comm):
@@ -92,20 +107,18 @@ class _CopyToTP(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g):
-        return all_reduce_(g.contiguous(), ctx.comm), None
+        return all_reduce(g, ctx.comm), None
 
 
 class _ReduceFromTP(torch.autograd.Function):
-    """TP all-reduce forward, identity backward (Megatron "g").  The partial product
-    is reduced in place (it is the fresh output of the row-parallel GEMM, which its
-    backward does not need), so the 32 MiB Llama activation is never cloned."""
+    """TP all-reduce forward (out of place: the caller's tensor is not modified), identity
+    backward (Megatron "g").  The TP layers themselves never go through here: their GEMMs
+    write into persistent symmetric scratch that the all-reduce consumes
+    (``_RowParallelFn``), which needs neither a copy nor a host call."""
 
     @staticmethod
     def forward(ctx, x, comm):
-        if not x.is_contiguous():
-            return all_reduce_(x.contiguous(), comm)
-        ctx.mark_dirty(x)
-        return all_reduce_(x, comm)
+        return all_reduce(x, comm)
 
     @staticmethod
     def backward(ctx, g):
@@ -163,11 +176,16 @@ _TP_GEMM = os.environ.get("CCMPI_TP_GEMM", "auto")
 
 
 def _gpu_shared(comm) -> bool:
-    """Whether this TP group's ranks share a GPU: measured by the group itself (PCI bus
-    ids gathered over the ranks, DeviceGroup.shared_device), per group."""
-    if comm is None:
-        return False
-    return bool(device_group_for(comm).shared_device)
+    """Whether this process shares its GPU with other ranks (multi-process-per-GPU tests):
+    then the whole-CU LDS-ring GEMM must not run, since its workgroups cannot start
+    beside a peer's spinning collective CTAs.  Measured by every device group (PCI bus
+    ids gathered over its ranks); a size-1 group (e.g. the TP group of a pure-DP run)
+    asks whether ANY group of this process found its GPU shared."""
+    from .. import device as _device
+
+    if comm is None or _size_rank(comm)[0] == 1:
+        return _device.SHARED_GPU_IN_PROCESS
+    return bool(device_group_for(comm).shared_device) or _device.SHARED_GPU_IN_PROCESS
 
 
 def _mfma_ok(x: torch.Tensor, w: torch.Tensor, comm=None) -> bool:
@@ -197,11 +215,97 @@ def _linear_backward(g2: torch.Tensor, x2: torch.Tensor, w: torch.Tensor, need_d
     return dx, dw
 
 
-class _LinearFn(torch.autograd.Function):
-    """y = x W^T (+ b): MFMA bf16 kernels on CUDA bf16, torch.matmul otherwise."""
+# How RowParallelLinear produces its all-reduced output (CCMPI_TP_ROW_MODE, or the layer's
+# ``mode``; read at call time):
+# * "plain"   -- the GEMM writes its partial product into persistent symmetric-heap
+#   scratch, one two-shot all-reduce reduces it into the (ordinary, fresh) output;
+# * "chunked" -- the same in CCMPI_TP_CHUNKS row blocks: block i's all-reduce runs on the
+#   communication stream while block i+1's GEMM runs (no CTA spins inside a GEMM);
+# * "fused"   -- the all-reduce in the GEMM epilogue (DeviceGroup.gemm_allreduce): tile
+#   owners spin on peers' tiles inside the GEMM (3.1x slower at TP = 2 on a shared GPU,
+#   profiles/r3_tp2).
+# The default is what the TP MLP measurements chose (profiles/r4_tp, README).
+ROW_MODES = ("plain", "chunked", "fused")
+_ROW_MODE = os.environ.get("CCMPI_TP_ROW_MODE", "plain")
+_TP_CHUNKS = int(os.environ.get("CCMPI_TP_CHUNKS", "2"))
+# which TP paths ran (tests assert the path they meant to exercise actually ran)
+CALLS: "collections.Counter[str]" = collections.Counter()
+
+
+def _scratch(comm, role: str, shape, dtype):
+    """Persistent symmetric-heap scratch of the TP group, shared by every layer (each use
+    is joined before the next layer's GEMM writes it, and a collective ends only after
+    every peer read of it): allocated once per (role, shape, dtype), no host call after."""
+    return device_group_for(comm).persistent(("tp_" + role,), shape, dtype)
+
+
+def _dev_path(x2: torch.Tensor, w: torch.Tensor, comm) -> bool:
+    """The hand-written device path of the TP layers: CUDA bf16 MFMA GEMMs + device TP
+    collectives on a group of more than one rank (16-B aligned rows)."""
+    return _mfma_ok(x2, w, comm) and _size_rank(comm)[0] > 1 and w.shape[0] % 8 == 0
+
+
+def _fused_ok(x2: torch.Tensor, w: torch.Tensor, comm) -> bool:
+    """The row-parallel GEMM can carry its TP all-reduce in its epilogue (DeviceGroup.
+    gemm_allreduce): CUDA bf16, K shard % 64, N % 8, a group of more than one rank."""
+    if not (x2.is_cuda and x2.dtype == torch.bfloat16 and w.dtype == torch.bfloat16):
+        return False
+    p, _ = _size_rank(comm)
+    return p > 1 and x2.shape[1] % 64 == 0 and w.shape[0] % 8 == 0 and x2.shape[0] > 0
+
+
+def _chunk_rows(M: int, c: int) -> list:
+    """Row blocks of the chunked row-parallel output: multiples of 256 rows (whole GEMM
+    tiles), at most ``c`` of them."""
+    step = max(256, -(-M // max(1, c)) // 256 * 256)
+    return [(r0, min(M, r0 + step)) for r0 in range(0, M, step)]
+
+
+def _deliver_wgrad(w: torch.Tensor, dw):
+    """Hand a weight gradient to its DDP bucket directly when the weight has a gradient
+    sink (``DistributedDataParallel(grad_sink=True)``): copied / added into the bucket view,
+    the bucket notified, and None returned (autograd then has nothing to accumulate)."""
+    sink = getattr(w, "_ccmpi_grad_sink", None)
+    if sink is None or dw is None:
+        return dw
+    view, acc = sink.begin()
+    if acc:
+        view.add_(dw.view_as(view))
+    else:
+        view.copy_(dw.view_as(view))
+    sink.done()
+    return None
+
+
+def _wgrad(g2: torch.Tensor, x2: torch.Tensor, w: torch.Tensor, comm):
+    """dW = dY^T X.  With a DDP gradient sink on ``w`` the MFMA kernel writes (or, when
+    accumulating over micro-batches, adds) straight into the bucket view: no gradient
+    tensor, no AccumulateGrad pass over it (16 GB of bf16 gradients read twice and
+    written once per Llama-3-8B step otherwise); returns None then."""
+    sink = getattr(w, "_ccmpi_grad_sink", None)
+    if sink is None or not sink.view.is_contiguous():
+        return _deliver_wgrad(w, _linear_backward(g2, x2, w, False, True, comm)[1])
+    view, acc = sink.begin()
+    if _gpu_shared(comm) or gemm_ring(g2, x2, True, True, out=view.view(w.shape), accumulate=acc) is None:
+        dw = gemm_tn(g2, x2).to(w.dtype)
+        if acc:
+            view.add_(dw.view_as(view))
+        else:
+            view.copy_(dw.view_as(view))
+    CALLS["wgrad_sink"] += 1
+    sink.done()
+    return None
+
+
+class _RowParallelFn(torch.autograd.Function):
+    """``y = sum_r x_r W_r^T (+ b)`` over the TP group (Megatron "g" folded into the layer).
+    Forward on the device path: GEMM -> persistent symmetric scratch -> two-shot all-reduce
+    into a fresh output (``DeviceGroup.allreduce_to_local``); the bias rides in TP rank 0's
+    GEMM epilogue, so it is summed exactly once.  Backward: local (identity gradient of
+    the all-reduce)."""
 
     @staticmethod
-    def forward(ctx, x, w, b, comm=None):
+    def forward(ctx, x, w, b, comm, mode):
         x2 = x.reshape(-1, x.shape[-1])
         if not x2.is_contiguous():
             x2 = x2.contiguous()
@@ -210,8 +314,104 @@ class _LinearFn(torch.autograd.Function):
         ctx.has_bias = b is not None
         ctx.lead = x.shape[:-1]
         ctx.mfma = _mfma_ok(x2, w, comm)
-        # the output is allocated in its final shape and written through a 2-D view, so
-        # the returned tensor is no view: _ReduceFromTP may reduce it in place (mark_dirty)
+        M, N = x2.shape[0], w.shape[0]
+        p, r = _size_rank(comm)
+        y = torch.empty(*x.shape[:-1], N, device=x.device, dtype=x.dtype)
+        y2 = y.view(M, N)
+        if M == 0:
+            return y
+        if not _dev_path(x2, w, comm):
+            # host plane / other dtypes: local product, in-place all-reduce of that fresh tensor
+            CALLS["row_host"] += 1
+            torch.matmul(x2, w.t(), out=y2)
+            all_reduce_(y2, comm)
+            if b is not None:
+                y2 += b
+            return y
+        dev = device_group_for(comm)
+        bias0 = b if r == 0 else None
+        if mode == "fused" and _fused_ok(x2, w, comm):
+            CALLS["row_fused"] += 1
+            out = _scratch(comm, "row_fused", (M, N), torch.bfloat16)
+            dev.gemm_allreduce(x2, w, bias=b, out=out)
+            y2.copy_(out)
+            return y
+        part = _scratch(comm, "row_partial", (M, N), x.dtype)
+        blocks = _chunk_rows(M, _TP_CHUNKS) if mode == "chunked" else [(0, M)]
+        if len(blocks) == 1:
+            CALLS["row_plain"] += 1
+            gemm_nt(x2, w, bias=bias0, out=part)
+            dev.allreduce_to_local(part, y2)
+            return y
+        CALLS["row_chunked"] += 1
+        works = []
+        for r0, r1 in blocks:
+            gemm_nt(x2[r0:r1], w, bias=bias0, out=part[r0:r1])
+            # block i's all-reduce on the communication stream, under block i+1's GEMM
+            works.append(dev.start("allreduce_to_local", part[r0:r1], y2[r0:r1]))
+        for wk in works:
+            wk.wait()
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        x2, w = ctx.saved_tensors
+        g2 = g.reshape(-1, g.shape[-1]).contiguous()
+        dx = dw = db = None
+        if ctx.mfma and g2.dtype == torch.bfloat16:
+            dx, _ = _linear_backward(g2, x2, w, ctx.needs_input_grad[0], False, ctx.comm)
+            if ctx.needs_input_grad[1]:
+                dw = _wgrad(g2, x2, w, ctx.comm)
+        else:
+            if ctx.needs_input_grad[0]:
+                dx = g2 @ w
+            if ctx.needs_input_grad[1]:
+                dw = _deliver_wgrad(w, g2.t() @ x2)
+        if dx is not None:
+            dx = dx.reshape(*ctx.lead, w.shape[1])
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            db = g2.float().sum(0).to(g.dtype)
+        return dx, dw, db, None, None
+
+
+def _column_backward(g2: torch.Tensor, x2: torch.Tensor, w: torch.Tensor, need_dx: bool, need_dw: bool, comm):
+    """Backward of a column-parallel projection with its TP all-reduce of dX (Megatron "f")
+    overlapped with the weight-gradient GEMM: dX's partial product goes into persistent
+    symmetric scratch, its all-reduce into a fresh dX starts on the communication stream,
+    and dW = dY^T X runs on the compute stream meanwhile."""
+    if not (need_dx and _dev_path(g2, w, comm)):
+        dx, _ = _linear_backward(g2, x2, w, need_dx, False, comm)
+        if dx is not None:
+            dx = all_reduce_(dx, comm)  # a fresh tensor of this backward: in place is safe
+        return dx, (_wgrad(g2, x2, w, comm) if need_dw else None)
+    CALLS["col_bwd_overlap"] += 1
+    dev = device_group_for(comm)
+    M, K = g2.shape[0], w.shape[1]
+    part = _scratch(comm, "dx_partial", (M, K), g2.dtype)
+    ring = not _gpu_shared(comm)
+    if not (ring and gemm_ring(g2, w, False, True, out=part) is not None):
+        gemm_nt(g2, transpose(w), out=part)
+    dx = torch.empty(M, K, device=g2.device, dtype=g2.dtype)
+    work = dev.start("allreduce_to_local", part, dx)
+    dw = _wgrad(g2, x2, w, comm) if need_dw else None
+    work.wait()
+    return dx, dw
+
+
+class _ColumnParallelFn(torch.autograd.Function):
+    """``y = x W_r^T (+ b_r)`` with the replicated input's gradient all-reduced over the TP
+    group in the backward, overlapped with the dW GEMM (``_column_backward``)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, comm):
+        x2 = x.reshape(-1, x.shape[-1])
+        if not x2.is_contiguous():
+            x2 = x2.contiguous()
+        ctx.comm = comm
+        ctx.save_for_backward(x2, w)
+        ctx.has_bias = b is not None
+        ctx.lead = x.shape[:-1]
+        ctx.mfma = _mfma_ok(x2, w, comm)
         y = torch.empty(*x.shape[:-1], w.shape[0], device=x.device, dtype=x.dtype)
         y2 = y.view(-1, w.shape[0])
         if ctx.mfma:
@@ -228,57 +428,12 @@ class _LinearFn(torch.autograd.Function):
         g2 = g.reshape(-1, g.shape[-1]).contiguous()
         dx = dw = db = None
         if ctx.mfma and g2.dtype == torch.bfloat16:
-            dx, dw = _linear_backward(g2, x2, w, ctx.needs_input_grad[0], ctx.needs_input_grad[1], ctx.comm)
+            dx, dw = _column_backward(g2, x2, w, ctx.needs_input_grad[0], ctx.needs_input_grad[1], ctx.comm)
         else:
-            if ctx.needs_input_grad[0]:
-                dx = g2 @ w
             if ctx.needs_input_grad[1]:
-                dw = g2.t() @ x2
-        if ctx.has_bias and ctx.needs_input_grad[2]:
-            db = g2.float().sum(0).to(g.dtype)
-        if dx is not None:
-            dx = dx.reshape(*ctx.lead, w.shape[1])
-        return dx, dw, db, None
-
-
-# The row-parallel GEMM with its TP all-reduce fused into the epilogue (DeviceGroup.
-# gemm_allreduce) is opt-in: at TP = 2 on one shared GPU the Llama MLP forward took
-# 5.1 ms fused against 1.64 ms for GEMM + zero-copy all-reduce (profiles/r3_tp2); over
-# xGMI it is unmeasured.
-_TP_FUSED = os.environ.get("CCMPI_TP_FUSED", "0") == "1"
-
-
-def _fused_ok(x2: torch.Tensor, w: torch.Tensor, comm) -> bool:
-    """The row-parallel GEMM can carry its TP all-reduce in its epilogue (DeviceGroup.
-    gemm_allreduce): CUDA bf16, K shard % 64, N % 8, a group of more than one rank."""
-    if not (_TP_FUSED and x2.is_cuda and x2.dtype == torch.bfloat16 and w.dtype == torch.bfloat16):
-        return False
-    p, _ = _size_rank(comm)
-    return p > 1 and x2.shape[1] % 64 == 0 and w.shape[0] % 8 == 0 and x2.shape[0] > 0
-
-
-class _RowParallelFused(torch.autograd.Function):
-    """y = sum_r x_r W_r^T + b with the all-reduce fused into the GEMM (forward); the
-    backward is local, as for Megatron's "g" (identity gradient of the all-reduce)."""
-
-    @staticmethod
-    def forward(ctx, x, w, b, comm):
-        x2 = x.reshape(-1, x.shape[-1])
-        if not x2.is_contiguous():
-            x2 = x2.contiguous()
-        ctx.comm = comm
-        ctx.save_for_backward(x2, w)
-        ctx.has_bias = b is not None
-        ctx.lead = x.shape[:-1]
-        y = device_group_for(comm).gemm_allreduce(x2, w, bias=b)
-        return y.reshape(*x.shape[:-1], w.shape[0])
-
-    @staticmethod
-    def backward(ctx, g):
-        x2, w = ctx.saved_tensors
-        g2 = g.reshape(-1, g.shape[-1]).contiguous()
-        dx = dw = db = None
-        dx, dw = _linear_backward(g2, x2, w, ctx.needs_input_grad[0], ctx.needs_input_grad[1], ctx.comm)
+                dw = _deliver_wgrad(w, g2.t() @ x2)
+            if ctx.needs_input_grad[0]:
+                dx = all_reduce_(g2 @ w, ctx.comm)
         if dx is not None:
             dx = dx.reshape(*ctx.lead, w.shape[1])
         if ctx.has_bias and ctx.needs_input_grad[2]:
@@ -296,12 +451,16 @@ def _bind_device_group(comm, device) -> None:
         device_group_for(comm)
 
 
-def _init_full(out_f: int, in_f: int, seed: int, dtype, bias: bool):
-    """Full (unsharded) weights from a seeded CPU generator: identical on every rank."""
-    gen = torch.Generator().manual_seed(seed)
+def _init_full(out_f: int, in_f: int, seed: int, dtype, bias: bool, device=None):
+    """Full (unsharded) weights from a seeded generator: identical on every rank.  On the
+    CPU by default (tests regenerate them there); ``device`` (CUDA) draws them on the GPU
+    instead -- same values on every rank of one GPU model, and seconds instead of minutes
+    for a Llama-3-8B-sized stack."""
+    dev = torch.device(device) if device is not None else torch.device("cpu")
+    gen = torch.Generator(device=dev).manual_seed(seed)
     bound = 1.0 / math.sqrt(in_f)
-    w = (torch.rand(out_f, in_f, generator=gen) * 2 - 1) * bound
-    b = (torch.rand(out_f, generator=gen) * 2 - 1) * bound if bias else None
+    w = (torch.rand(out_f, in_f, generator=gen, device=dev) * 2 - 1) * bound
+    b = (torch.rand(out_f, generator=gen, device=dev) * 2 - 1) * bound if bias else None
     return w.to(dtype), (b.to(dtype) if b is not None else None)
 
 
@@ -312,7 +471,7 @@ class ColumnParallelLinear(torch.nn.Module):
     (feed a ``RowParallelLinear``); ``True`` all-gathers the full output."""
 
     def __init__(self, in_features: int, out_features: int, comm, bias: bool = True, gather_output: bool = False,
-                 device=None, dtype=torch.float32, seed: int = 0):
+                 device=None, dtype=torch.float32, seed: int = 0, init: str = "cpu"):
         super().__init__()
         p, r = _size_rank(comm)
         if out_features % p:
@@ -322,13 +481,12 @@ class ColumnParallelLinear(torch.nn.Module):
         self.gather_output = gather_output
         k = out_features // p
         _bind_device_group(comm, device)
-        w, b = _init_full(out_features, in_features, seed, dtype, bias)
+        w, b = _init_full(out_features, in_features, seed, dtype, bias, device if init == "device" else None)
         self.weight = torch.nn.Parameter(w[r * k:(r + 1) * k].contiguous().to(device))
         self.bias = torch.nn.Parameter(b[r * k:(r + 1) * k].contiguous().to(device)) if bias else None
 
     def forward(self, x):
-        x = copy_to_tensor_parallel_region(x, self.comm)
-        y = _LinearFn.apply(x, self.weight, self.bias, self.comm)
+        y = _ColumnParallelFn.apply(x, self.weight, self.bias, self.comm)
         return gather_from_tensor_parallel_region(y, self.comm) if self.gather_output else y
 
 
@@ -339,35 +497,35 @@ class RowParallelLinear(torch.nn.Module):
     after the reduction.  ``input_is_parallel=False`` splits a full input here."""
 
     def __init__(self, in_features: int, out_features: int, comm, bias: bool = True, input_is_parallel: bool = True,
-                 device=None, dtype=torch.float32, seed: int = 0):
+                 device=None, dtype=torch.float32, seed: int = 0, mode: str = "", init: str = "cpu"):
         super().__init__()
         p, r = _size_rank(comm)
         if in_features % p:
             raise ValueError(f"in_features {in_features} not divisible by TP size {p}")
+        if mode and mode not in ROW_MODES:
+            raise ValueError(f"RowParallelLinear mode {mode!r} not in {ROW_MODES}")
+        self.mode = mode  # "" = CCMPI_TP_ROW_MODE at call time
         self.comm, self.p, self.r = comm, p, r
         self.in_features, self.out_features = in_features, out_features
         self.input_is_parallel = input_is_parallel
         k = in_features // p
         _bind_device_group(comm, device)
-        w, b = _init_full(out_features, in_features, seed, dtype, bias)
+        w, b = _init_full(out_features, in_features, seed, dtype, bias, device if init == "device" else None)
         self.weight = torch.nn.Parameter(w[:, r * k:(r + 1) * k].contiguous().to(device))
         self.bias = torch.nn.Parameter(b.to(device)) if bias else None
 
     def forward(self, x):
         if not self.input_is_parallel:
             x = scatter_to_tensor_parallel_region(x, self.comm)
-        if _fused_ok(x.reshape(-1, x.shape[-1]), self.weight, self.comm):
-            # the TP all-reduce rides in the GEMM epilogue (tile-granular overlap)
-            return _RowParallelFused.apply(x, self.weight, self.bias, self.comm)
-        y = reduce_from_tensor_parallel_region(_LinearFn.apply(x, self.weight, None, self.comm), self.comm)
-        return y + self.bias if self.bias is not None else y
+        return _RowParallelFn.apply(x, self.weight, self.bias, self.comm, self.mode or _ROW_MODE)
 
 
 class _GateUpSwiGLU(torch.autograd.Function):
-    """``a = swiglu_pairs(x W^T)`` for a gate|up weight whose rows are interleaved (gate j,
-    up j) pairs.  Forward: one GEMM whose epilogue also writes the gate (LDS-ring kernel,
-    EPI 2), else GEMM + ``swiglu_pairs``; saves x, W and the GEMM output h.  Backward:
-    ``swiglu_pairs_backward`` (one kernel) then dX / dW as ``_LinearFn``."""
+    """``a = swiglu_pairs(x W^T)`` for a column-parallel gate|up weight whose rows are
+    interleaved (gate j, up j) pairs.  Forward: one GEMM whose epilogue also writes the
+    gate (LDS-ring kernel, EPI 2), else GEMM + ``swiglu_pairs``; saves x, W and the GEMM
+    output h.  Backward: ``swiglu_pairs_backward`` (one kernel), then dX with its TP
+    all-reduce overlapped with the dW GEMM (``_column_backward``, Megatron "f")."""
 
     @staticmethod
     def forward(ctx, x, w, comm):
@@ -396,10 +554,10 @@ class _GateUpSwiGLU(torch.autograd.Function):
         x2, w, h = ctx.saved_tensors
         dh = swiglu_pairs_backward(h, da.reshape(-1, da.shape[-1]))
         if ctx.mfma:
-            dx, dw = _linear_backward(dh, x2, w, ctx.needs_input_grad[0], ctx.needs_input_grad[1], ctx.comm)
+            dx, dw = _column_backward(dh, x2, w, ctx.needs_input_grad[0], ctx.needs_input_grad[1], ctx.comm)
         else:
-            dx = dh @ w if ctx.needs_input_grad[0] else None
-            dw = dh.t() @ x2 if ctx.needs_input_grad[1] else None
+            dw = _deliver_wgrad(w, dh.t() @ x2) if ctx.needs_input_grad[1] else None
+            dx = all_reduce_(dh @ w, ctx.comm) if ctx.needs_input_grad[0] else None
         if dx is not None:
             dx = dx.reshape(*ctx.lead, w.shape[1])
         return dx, dw, None
@@ -416,19 +574,22 @@ class ParallelSwiGLUMLP(torch.nn.Module):
     "g"), one in backward for dX of ``gate_up`` (Megatron "f").  The reference's TP layer
     (model/func_impl.py:65-109) on a realistic Llama-3-8B shape."""
 
-    def __init__(self, d_model: int, ffn: int, comm, device=None, dtype=torch.bfloat16, seed: int = 0):
+    def __init__(self, d_model: int, ffn: int, comm, device=None, dtype=torch.bfloat16, seed: int = 0,
+                 mode: str = "", init: str = "cpu"):
         super().__init__()
         p, r = _size_rank(comm)
         if ffn % p:
             raise ValueError(f"ffn {ffn} not divisible by TP size {p}")
         k = ffn // p
         self.comm, self.p, self.r, self.ffn = comm, p, r, ffn
-        self.gate_up = ColumnParallelLinear(d_model, 2 * ffn, comm, bias=False, device=device, dtype=dtype, seed=seed)
-        full, _ = _init_full(2 * ffn, d_model, seed, dtype, False)
+        self.gate_up = ColumnParallelLinear(d_model, 2 * ffn, comm, bias=False, device=device, dtype=dtype, seed=seed,
+                                            init=init)
+        full, _ = _init_full(2 * ffn, d_model, seed, dtype, False, device if init == "device" else None)
         with torch.no_grad():  # shard rows: gate r k + j at 2 j, up r k + j at 2 j + 1
             shard = torch.stack([full[r * k:(r + 1) * k], full[ffn + r * k:ffn + (r + 1) * k]], dim=1)
             self.gate_up.weight.copy_(shard.reshape(2 * k, d_model))
-        self.down = RowParallelLinear(ffn, d_model, comm, bias=False, device=device, dtype=dtype, seed=seed + 1)
+        self.down = RowParallelLinear(ffn, d_model, comm, bias=False, device=device, dtype=dtype, seed=seed + 1,
+                                      mode=mode, init=init)
 
     def _fused_ok(self, x) -> bool:
         w = self.gate_up.weight
@@ -437,7 +598,7 @@ class ParallelSwiGLUMLP(torch.nn.Module):
 
     def forward(self, x):
         if self._fused_ok(x):
-            a = _GateUpSwiGLU.apply(copy_to_tensor_parallel_region(x, self.comm), self.gate_up.weight, self.comm)
+            a = _GateUpSwiGLU.apply(x, self.gate_up.weight, self.comm)
         else:
             h = self.gate_up(x)
             a = torch.nn.functional.silu(h[..., 0::2]) * h[..., 1::2]
@@ -460,6 +621,7 @@ def sharded_grad_full(layer, comm) -> torch.Tensor:
     return torch.cat(parts, dim=dim)
 
 
-__all__ = ["ColumnParallelLinear", "RowParallelLinear", "ParallelSwiGLUMLP", "all_reduce_", "copy_to_tensor_parallel_region",
+__all__ = ["ColumnParallelLinear", "RowParallelLinear", "ParallelSwiGLUMLP", "all_reduce", "all_reduce_",
+           "copy_to_tensor_parallel_region", "ROW_MODES",
            "reduce_from_tensor_parallel_region", "gather_from_tensor_parallel_region",
            "scatter_to_tensor_parallel_region", "full_weight", "sharded_grad_full"]

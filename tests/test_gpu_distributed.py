@@ -134,6 +134,17 @@ def test_bench_survives_rccl_failure(mode):
     assert all(v for v in c["candidates_ms"].values()), c["candidates_ms"]
 
 
+def test_bench_harness_crash_keeps_headline():
+    """the harness runs in a supervised phase of its own; a SIGSEGV there
+    (injected: CCMPI_BENCH_FAULT=harness) costs only the harness record, never the
+    hand-written all-reduce headline."""
+    out = _bench_line({"CCMPI_BENCH_FAULT": "harness"}, "--no-rccl")
+    c = out["config"]
+    assert out["value"] > 0 and c["result_exact"], out
+    assert not c["phases"]["harness"]["ok"] and "error" in c["harness"], c["harness"]
+    assert "tp_fwd_step_ms" not in c
+
+
 @pytest.mark.parametrize("case", ["myallreduce", "myalltoall"])
 def test_cli_device_cases(case):
     """The reference CLI cases on device buffers (reference mpi-test.py:42-98,178-239):
@@ -197,6 +208,14 @@ def test_tensor_parallel_layers_and_ddp_gpu(n):
     on the device plane vs a single-process fp32 reference (tests/workers/tp_ddp_worker.py)."""
     r = run_ranks(n, py("tests/workers/tp_ddp_worker.py", "--device", "cuda"), timeout=300, env=ENV)
     assert "tp/ddp OK" in r.stdout
+
+
+def test_llama_ddp_gradient_sinks_gpu():
+    """BASELINE config 5's machinery on a tiny Llama: DDP over 2 ranks with the TP layers'
+    dW GEMMs writing straight into the buckets (gradient sinks), vs the mean of replica
+    gradients; then measure_ddp_overlap's compute / comm / overlapped record."""
+    r = run_ranks(2, py("tests/workers/llama_dp_worker.py", "--device", "cuda", "--measure"), timeout=300, env=ENV)
+    assert "llama dp OK" in r.stdout
 
 
 def test_bench_multi_rank_path_shared_gpu():

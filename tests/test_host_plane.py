@@ -125,3 +125,11 @@ def test_tensor_parallel_layers_and_ddp_cpu(n):
     (CPU tensors) vs a single-process fp32 reference, over the mp-major grid."""
     r = run_ranks(n, py("tests/workers/tp_ddp_worker.py", "--device", "cpu"), timeout=300)
     assert "tp/ddp OK" in r.stdout
+
+
+def test_llama_ddp_cpu():
+    """DistributedDataParallel over a tiny Llama-shaped model of the framework's TP layers
+    (parallel/llama_dp.py) on the host plane: every rank's gradients equal the mean of the
+    per-rank replica gradients, over two steps and a no_sync micro-batch accumulation."""
+    r = run_ranks(2, py("tests/workers/llama_dp_worker.py", "--device", "cpu"), timeout=300)
+    assert "llama dp OK" in r.stdout

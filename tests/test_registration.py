@@ -50,7 +50,7 @@ def group(rank=0, size=2, slots=2):
     syncs = []
     torch = SimpleNamespace(cuda=SimpleNamespace(synchronize=lambda *_: syncs.append(1)))
     return SimpleNamespace(rank=rank, size=size, reg_slots=slots, _dyn=OrderedDict(), _free_slots=[], dc=FakeDC(),
-                           torch=torch, device=None, registrations=0, _syncs=syncs)
+                           torch=torch, device=None, registrations=0, _syncs=syncs, _pinned=set())
 
 
 def test_map_slot_lru_and_stale_reuse():
@@ -86,3 +86,30 @@ def test_slot_tables_identical_on_every_rank():
                 DeviceGroup._map_slot(g, k)
         tables.append(dict(g._dyn))
     assert tables[0] == tables[1]
+
+
+def test_pinned_slots_survive_eviction_and_refuse_remap():
+    """a slot a captured HIP graph resolves is pinned -- LRU eviction
+    skips it, every slot pinned grows the table, and remapping its range raises."""
+    import pytest
+
+    g = group(slots=2)
+    k1 = (alloc(b"a", 0x1000, 0x100), alloc(b"b", 0x1000, 0x100))
+    k2 = (alloc(b"c", 0x2000, 0x100), alloc(b"d", 0x2000, 0x100))
+    k3 = (alloc(b"e", 0x3000, 0x100), alloc(b"f", 0x3000, 0x100))
+    k4 = (alloc(b"g", 0x4000, 0x100), alloc(b"h", 0x4000, 0x100))
+    DeviceGroup._map_slot(g, k1)
+    DeviceGroup._map_slot(g, k2)
+    g._pinned.add(k1)                       # captured while least recently used
+    DeviceGroup._map_slot(g, k3)            # evicts k2, not the pinned k1
+    assert k1 in g._dyn and k2 not in g._dyn and g._dyn[k3] == 2
+    g._pinned.add(k3)
+    DeviceGroup._map_slot(g, k4)            # every slot pinned: a new one
+    assert g._dyn[k4] == 3 and k1 in g._dyn and k3 in g._dyn
+    k1b = (alloc(b"a2", 0x1000, 0x100, 7), alloc(b"b", 0x1000, 0x100))
+    with pytest.raises(RuntimeError, match="captured HIP graph"):
+        DeviceGroup._map_slot(g, k1b)       # k1's range reallocated under a live graph
+    assert g._dyn[k1] == 1 and g.dc.cleared == []
+    DeviceGroup.unpin_captured(g)
+    DeviceGroup._map_slot(g, k1b)           # after unpin the stale slot is reused
+    assert k1 not in g._dyn and g._dyn[k1b] == 1

@@ -71,28 +71,42 @@ for salt, (M, N, Kr, use_bias) in enumerate([(512, 768, 256, False), (300, 520, 
             diff = (unf.float() - y.float()).abs().max().item()
             fails.append(f"fused[{M}x{N}x{Kr}] != unfused rank-order sum (max diff {diff})")
 
-# RowParallelLinear through the fused path vs the unfused one (same weights)
+# RowParallelLinear through every row-parallel mode (same weights): the fused epilogue,
+# the chunked side-stream overlap and the plain path must agree with an fp32 reference,
+# and each mode must really take its own path (tp.CALLS counts the paths that ran)
 from collective_communication_mpi_amd.parallel import tensor_parallel as tp  # noqa: E402
 
-IN, OUT, T = 256 * p, 512, 384  # every rank holds a K shard of 256 (the fused path needs K_r % 64 == 0)
+IN, OUT, T = 256 * p, 512, 1024  # every rank holds a K shard of 256 (the fused path needs K_r % 64 == 0)
 x_full = shard(999, T, IN, 77)
 layer = tp.RowParallelLinear(IN, OUT, comm, bias=True, input_is_parallel=False, device=D, dtype=torch.bfloat16, seed=5)
-xin = x_full.clone().requires_grad_(True)
-y = layer(xin)
-y.float().pow(2).sum().backward()
-gx_f, gw_f, gb_f = xin.grad.clone(), layer.weight.grad.clone(), layer.bias.grad.clone()
-tp._TP_FUSED = False
-layer.zero_grad()
-xin2 = x_full.clone().requires_grad_(True)
-y2 = layer(xin2)
-y2.float().pow(2).sum().backward()
-tp._TP_FUSED = True
-if (y.float() - y2.float()).abs().max().item() > 0.05:
-    fails.append(f"RowParallelLinear fused vs unfused forward: {(y.float() - y2.float()).abs().max().item()}")
-for name, a, b in (("dx", gx_f, xin2.grad), ("dw", gw_f, layer.weight.grad), ("db", gb_f, layer.bias.grad)):
-    rel = ((a.float() - b.float()).abs().max() / (b.float().abs().max() + 1e-6)).item()
-    if rel > 0.05:
-        fails.append(f"RowParallelLinear fused vs unfused {name}: rel err {rel}")
+wf = tp.full_weight(layer, comm).to(D)
+xr = x_full.float().requires_grad_(True)
+yr = xr @ wf.T + layer.bias.float()
+yr.pow(2).sum().backward()
+grads = {}
+for mode, path in (("fused", "row_fused"), ("chunked", "row_chunked"), ("plain", "row_plain")):
+    layer.mode = mode
+    layer.zero_grad()
+    before = tp.CALLS[path]
+    xin = x_full.clone().requires_grad_(True)
+    y = layer(xin)
+    y.float().pow(2).sum().backward()
+    torch.cuda.synchronize()
+    if tp.CALLS[path] != before + 1:
+        fails.append(f"RowParallelLinear mode {mode}: path {path} ran {tp.CALLS[path] - before} times, expected 1")
+    err = ((y.float() - yr).abs().max() / yr.abs().max()).item()
+    if err > 0.02:
+        fails.append(f"RowParallelLinear {mode} forward vs fp32: rel err {err:.4f}")
+    grads[mode] = (xin.grad.clone(), layer.weight.grad.clone(), layer.bias.grad.clone())
+for mode, (gx, gw, gb) in grads.items():
+    for name, a_, b_ in (("dx", gx, xr.grad), ("dw", gw, None), ("db", gb, None)):
+        if b_ is None:
+            a_ref = grads["plain"][1] if name == "dw" else grads["plain"][2]
+            rel = ((a_.float() - a_ref.float()).abs().max() / (a_ref.float().abs().max() + 1e-6)).item()
+        else:
+            rel = ((a_.float() - b_.float()).abs().max() / (b_.float().abs().max() + 1e-6)).item()
+        if rel > 0.05:
+            fails.append(f"RowParallelLinear {mode} {name}: rel err {rel:.4f}")
 
 torch.cuda.synchronize()
 dev.check()

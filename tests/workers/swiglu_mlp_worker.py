@@ -71,6 +71,36 @@ gd = torch.cat(hc.allgather(mlp.down.weight.grad.detach().float().cpu()), dim=1)
 if rel(gd, wd.grad) > tol:
     fails.append(f"d W_down rel err {rel(gd, wd.grad)}")
 
+if args.device == "cuda" and p > 1:
+    # every row-parallel mode through the whole block (forward + backward), its path
+    # really taken, and a steady-state step with no host call from the device plane
+    from collective_communication_mpi_amd.parallel import tensor_parallel as tp  # noqa: E402
+
+    T2 = 512  # two 256-row blocks for the chunked mode
+    x2 = torch.randn(T2, D, generator=torch.Generator().manual_seed(5))
+    g2 = torch.randn(T2, D, generator=torch.Generator().manual_seed(6)) * 0.1
+    xr2 = x2.to(dt).float().requires_grad_(True)
+    h2 = xr2 @ wgu.detach().T
+    yr2 = (torch.nn.functional.silu(h2[:, :F]) * h2[:, F:]) @ wd.detach().T
+    yr2.backward(g2.to(dt).float())
+    for mode, path in (("plain", "row_plain"), ("chunked", "row_chunked"), ("fused", "row_fused")):
+        m = ParallelSwiGLUMLP(D, F, comm, device=dev, dtype=dt, seed=11, mode=mode)
+        dg = tp.device_group_for(comm)
+        for it in range(2):
+            xi = x2.to(dt).to(dev).requires_grad_(True)
+            c0, b0, h0 = tp.CALLS[path], tp.CALLS["col_bwd_overlap"], dg.host_calls
+            yi = m(xi)
+            yi.backward(g2.to(dt).to(dev))
+            torch.cuda.synchronize()
+            if tp.CALLS[path] != c0 + 1 or tp.CALLS["col_bwd_overlap"] != b0 + 1:
+                fails.append(f"{mode}: paths {dict(tp.CALLS)} (expected one {path} and one col_bwd_overlap)")
+            if it == 1 and dg.host_calls != h0:
+                fails.append(f"{mode}: steady-state step made {dg.host_calls - h0} host calls (expected 0)")
+        if rel(yi.detach(), yr2.detach()) > tol:
+            fails.append(f"{mode}: forward rel err {rel(yi.detach(), yr2.detach())}")
+        if rel(xi.grad, xr2.grad) > tol:
+            fails.append(f"{mode}: dx rel err {rel(xi.grad, xr2.grad)}")
+
 bad = hc.allgather(fails)
 if rank == 0:
     flat = [f"rank {r}: {m}" for r, ms in enumerate(bad) for m in ms]
