@@ -59,10 +59,10 @@ class _GradSink:
     the user dropped ``.grad``), add when accumulating micro-batches -- and ``done()``
     counts the parameter ready in its bucket, exactly like the post-accumulate hook."""
 
-    __slots__ = ("ddp", "param", "view", "fresh")
+    __slots__ = ("ddp", "param", "view", "fresh", "reported")
 
     def __init__(self, ddp, param, view):
-        self.ddp, self.param, self.view, self.fresh = ddp, param, view, True
+        self.ddp, self.param, self.view, self.fresh, self.reported = ddp, param, view, True, False
 
     def begin(self):
         q = self.param
@@ -80,6 +80,7 @@ class _GradSink:
         return self.view, acc
 
     def done(self):
+        self.reported = True
         self.ddp._ready(self.param)
 
 
@@ -186,6 +187,10 @@ class DistributedDataParallel(torch.nn.Module):
             q.grad = v
         sk = getattr(q, "_ccmpi_grad_sink", None)
         if sk is not None:
+            if sk.reported:
+                # the layer delivered this gradient itself (and returned None): autograd still
+                # runs the post-accumulate hook for the parameter; it was counted already
+                return
             sk.fresh = False  # the bucket view now holds this step's gradient
         self._ready(q)
 
@@ -236,6 +241,8 @@ class DistributedDataParallel(torch.nn.Module):
         for b in self.buckets:
             b.pending = len(b.params)
             b.launched = False
+            for sk in b.sinks:
+                sk.reported = False
 
     def zero_grad(self, set_to_none: bool = False) -> None:
         """Zero the gradients and re-attach every ``.grad`` view (``set_to_none`` is ignored).

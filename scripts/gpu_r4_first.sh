@@ -7,13 +7,12 @@ cd "$(dirname "$0")/.."
 OUT=gpurun_out/${OUT_TAG:-r4_first}
 mkdir -p $OUT
 export TMPDIR=/tmp
-timeout -k 10 120 python benchmarks/ipc_identity_probe.py > $OUT/ipc_identity.json 2> $OUT/ipc_identity.err
-rc=$?; echo "probe rc=$rc"; cat $OUT/ipc_identity.json; [ $rc -ne 0 ] && { tail -20 $OUT/ipc_identity.err; exit $rc; }
 timeout -k 10 700 python -u -m pytest -x -v --timeout 300 --timeout-method thread \
-  "tests/test_gpu_distributed.py::test_parallel_swiglu_mlp_gpu" \
-  "tests/test_gpu_distributed.py::test_fused_rowparallel_gemm_allreduce[2]" \
-  "tests/test_gpu_distributed.py::test_tensor_parallel_layers_and_ddp_gpu[2]" \
-  "tests/test_gpu_distributed.py::test_device_ondemand_registration[2]" > $OUT/pytest.log 2>&1
+  "tests/test_gpu_distributed.py::test_tensor_parallel_layers_and_ddp_gpu" \
+  "tests/test_gpu_distributed.py::test_llama_ddp_gradient_sinks_gpu" \
+  "tests/test_gpu_distributed.py::test_bench_tuning_table_drives_auto" \
+  "tests/test_gpu_distributed.py::test_device_ondemand_registration[2]" \
+  "tests/test_gpu_distributed.py::test_bench_harness_crash_keeps_headline" > $OUT/pytest.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -8 $OUT/pytest.log; [ $rc -ne 0 ] && exit $rc
 timeout -k 10 600 python bench.py --verbose > $OUT/bench1.json 2> $OUT/bench1.err
 rc=$?; echo "bench rc=$rc"; cut -c1-600 $OUT/bench1.json; [ $rc -ne 0 ] && { tail -30 $OUT/bench1.err; exit $rc; }

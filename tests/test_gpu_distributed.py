@@ -210,6 +210,13 @@ def test_tensor_parallel_layers_and_ddp_gpu(n):
     assert "tp/ddp OK" in r.stdout
 
 
+def test_bench_tuning_table_drives_auto(tmp_path):
+    """the bench's tuning sweep writes CCMPI_TUNE_FILE; a device group
+    created afterwards loads it and ``auto`` runs what the table says (ring, RHD), 4 ranks."""
+    r = run_ranks(4, py("tests/workers/tune_worker.py", "--file", str(tmp_path / "tune.json")), timeout=300, env=ENV)
+    assert "tune OK" in r.stdout
+
+
 def test_llama_ddp_gradient_sinks_gpu():
     """BASELINE config 5's machinery on a tiny Llama: DDP over 2 ranks with the TP layers'
     dW GEMMs writing straight into the buckets (gradient sinks), vs the mean of replica
