@@ -131,27 +131,40 @@ def _env_rank():
     return r, n, local
 
 
-def _run_child(cmd, env, budget: float):
-    """Run one phase child in its own session; kill its process group at the budget.
-    Returns (returncode or None on timeout, seconds)."""
+def _run_child(cmd, env, budget: float, abort_flag: str = ""):
+    """Run one phase child in its own session; kill its process group at the budget, or as
+    soon as ``abort_flag`` exists (another rank's child of this phase failed: its peers
+    would wait for it in their next collective until the budget).  A child that fails
+    creates the flag for the others.  Returns (returncode or None if killed, seconds)."""
     import signal
 
     t0 = time.monotonic()
     p = subprocess.Popen(cmd, env=env, cwd=REPO, start_new_session=True)
-    try:
-        rc = p.wait(timeout=budget)
-    except subprocess.TimeoutExpired:
-        for sig in (signal.SIGTERM, signal.SIGKILL):
-            try:
-                os.killpg(p.pid, sig)
-            except ProcessLookupError:
-                break
-            try:
-                p.wait(timeout=10)
-                break
-            except subprocess.TimeoutExpired:
-                continue
-        rc = None
+    rc = None
+    while True:
+        try:
+            rc = p.wait(timeout=0.25)
+            break
+        except subprocess.TimeoutExpired:
+            pass
+        if time.monotonic() - t0 > budget or (abort_flag and os.path.exists(abort_flag)):
+            for sig in (signal.SIGTERM, signal.SIGKILL):
+                try:
+                    os.killpg(p.pid, sig)
+                except ProcessLookupError:
+                    break
+                try:
+                    p.wait(timeout=10)
+                    break
+                except subprocess.TimeoutExpired:
+                    continue
+            rc = None
+            break
+    if rc != 0 and abort_flag:
+        try:
+            open(abort_flag, "a").close()
+        except OSError:
+            pass
     return rc, time.monotonic() - t0
 
 
@@ -255,7 +268,11 @@ def supervise(args) -> int:
         env["PYTHONPATH"] = REPO + (os.pathsep + pp if pp else "")
         cmd = [sys.executable, os.path.abspath(__file__), *argv, "--phase", phase,
                "--result", os.path.join(tmp, f"{phase}.json")]
-        rc, secs = _run_child(cmd, env, budget)
+        if rank == 0:
+            print(f"[bench] phase {phase} (budget {budget:.0f}s) ...", file=sys.stderr, flush=True)
+        rc, secs = _run_child(cmd, env, budget, abort_flag=os.path.join(tmp, f"{phase}.abort"))
+        if rank == 0:
+            print(f"[bench] phase {phase}: rc {rc}, {secs:.1f}s", file=sys.stderr, flush=True)
         ok = world.allreduce(int(rc == 0), op=MPI.MIN)
         rcs = world.allgather(rc)
         status[phase] = {"ok": bool(ok), "returncodes": rcs, "seconds": round(secs, 1)}

@@ -16,6 +16,8 @@ M, N, K, mode, iters = (int(v) for v in sys.argv[1:6])
 a = (torch.rand(M, K, device="cuda") * 2 - 1).bfloat16()
 b = (torch.rand(N, K, device="cuda") * 2 - 1).bfloat16()
 c = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+if os.environ.get("CCMPI_RING_SCHED"):
+    _native.device().gemm_set_ring_sched(int(os.environ["CCMPI_RING_SCHED"]))
 if mode >= 0:
     _native.device().gemm_set_kernel(mode)
     if mode == 5 and os.environ.get("CCMPI_W4_SCHED"):

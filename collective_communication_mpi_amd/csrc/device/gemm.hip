@@ -1109,6 +1109,8 @@ void register_gemm_ops(pybind11::module_& m) {
         "four-wave ring STAMP diagnostic: device buffer of 4 uint64 per wave (benchmarks only)");
   m.def("gemm_set_ring_min", [](long long v) { g_ring_min_macs = v; },
         "gemm_nt auto: LDS-ring kernel from this many multiply-adds up (0 = never)");
+  m.def("gemm_set_ring_sched", [](int v) { g_ring_sched = v; },
+        "auto-dispatched LDS-ring kernel variant: bit 0 persistent, bit 10 reads-then-DMA phase (PS 1)");
   m.def("gemm_set_w4_group_m", [](int v) { g_w4_group_m = v > 0 ? v : 8; }, "four-wave kernel group-M rows");
   m.def("gemm_set_ablation", [](int e) {
     g_pp_exp = e;

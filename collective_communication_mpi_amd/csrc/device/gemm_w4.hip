@@ -590,7 +590,13 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t op_rsrc_t(const uint16_t* X, i
 // operands).  A K-major slot half is [32 k][256 rows] with 512-B k-rows whose 32-B
 // granules are XOR-swizzled by tn_swz(k) (the 256x256 TN kernel's scheme, gemm256.hip);
 // its fragments come out of two ds_read_b64_tr_b16 each.
-template <int EPI, int PERSIST, int ABL = 0, int STAMP = 0, int TA = 0, int TB = 0>
+// PS (N layout only): placement of a phase's fragment reads and DMA pieces between its 64
+// MFMAs.  0: per 8 MFMAs one read, one DMA piece, one read (interleaved).  1: the 16 reads
+// over the first 32 MFMAs, the 8 DMA pieces over the last 32 -- the LDS-DMA issue kept
+// away from the ds_reads, as hipBLASLt's MT256x256x64 loop places them (an LDS-DMA piece
+// costs 100-185 cycles to issue inside a phase already carrying reads, 25-60 in a
+// read-free stretch: MI355X_MICROARCH.md, per-instruction constants).
+template <int EPI, int PERSIST, int ABL = 0, int STAMP = 0, int TA = 0, int TB = 0, int PS = 0>
 __global__ void __launch_bounds__(WNT, 1) k_gemm_w4r(W4Args wa) {
   const GemmArgs& g = wa.g;
   extern __shared__ __attribute__((aligned(1024))) unsigned char smem[];
@@ -724,6 +730,20 @@ __global__ void __launch_bounds__(WNT, 1) k_gemm_w4r(W4Args wa) {
         mm(3, 8);
         if constexpr (!(ABL & 2)) rd1(q, 4 + (i >> 1), i & 1, ca, cb);  // A block i
         __builtin_amdgcn_sched_barrier(0);
+      } else if constexpr (PS == 1) {
+        // MFMA m = 8 i + j: read r = m / 2 after odd m < 32, DMA piece (m - 33) / 4 after
+        // m = 33, 37, .., 61
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          mm(j, j + 1);
+          const int m = 8 * i + j;
+          if (m < 32 && (m & 1)) {
+            if constexpr (!(ABL & 2)) rd1(q, m >> 2, (m >> 1) & 1, ca, cb);
+          } else if (m >= 33 && ((m - 33) & 3) == 0) {
+            if constexpr (DMA && !(ABL & 1)) dma_piece(ds, (m - 33) >> 2);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
       } else {
         mm(0, 1);
         if constexpr (!(ABL & 2)) rd1(q, i, 0, ca, cb);
@@ -1019,6 +1039,10 @@ void launch_gemm_ring(const GemmArgs& g, int ta, int tb, hipStream_t stream, uin
     w4r_attr(reinterpret_cast<const void*>(k_gemm_w4r<1, 0, 0, 0, 1, 1>));
     w4r_attr(reinterpret_cast<const void*>(k_gemm_w4r<0, 0, 0, 0, 1, 0>));
     w4r_attr(reinterpret_cast<const void*>(k_gemm_w4r<1, 0, 0, 0, 1, 0>));
+    w4r_attr(reinterpret_cast<const void*>(k_gemm_w4r<1, 0, 0, 0, 0, 0, 1>));
+    w4r_attr(reinterpret_cast<const void*>(k_gemm_w4r<1, 1, 0, 0, 0, 0, 1>));
+    w4r_attr(reinterpret_cast<const void*>(k_gemm_w4r<2, 0, 0, 0, 0, 0, 1>));
+    w4r_attr(reinterpret_cast<const void*>(k_gemm_w4r<1, 0, 0, 1, 0, 0, 1>));
     return true;
   }();
   (void)attr;
@@ -1027,7 +1051,8 @@ void launch_gemm_ring(const GemmArgs& g, int ta, int tb, hipStream_t stream, uin
   const bool fast = gemm_w4r_fast(g);
   if (glu) {  // SwiGLU epilogue (callers check gemm_w4r_fast and the glu layout first)
     if (!fast || ta || tb) throw std::invalid_argument("gemm ring: the SwiGLU epilogue needs the fast NT form");
-    hipLaunchKernelGGL((k_gemm_w4r<2, 0>), dim3(ntiles), dim3(WNT), kRingLds, stream, a);
+    if (sched & 1024) hipLaunchKernelGGL((k_gemm_w4r<2, 0, 0, 0, 0, 0, 1>), dim3(ntiles), dim3(WNT), kRingLds, stream, a);
+    else hipLaunchKernelGGL((k_gemm_w4r<2, 0>), dim3(ntiles), dim3(WNT), kRingLds, stream, a);
     return;
   }
   const bool persist = fast && (sched & 1);
@@ -1048,8 +1073,13 @@ void launch_gemm_ring(const GemmArgs& g, int ta, int tb, hipStream_t stream, uin
   if (!fast) {
     hipLaunchKernelGGL((k_gemm_w4r<0, 0>), dim3(grid), dim3(WNT), kRingLds, stream, a);
   } else if (sched & 512) {
-    if (persist) hipLaunchKernelGGL((k_gemm_w4r<1, 1, 0, 1>), dim3(grid), dim3(WNT), kRingLds, stream, a);
+    if (sched & 1024) hipLaunchKernelGGL((k_gemm_w4r<1, 0, 0, 1, 0, 0, 1>), dim3(grid), dim3(WNT), kRingLds, stream, a);
+    else if (persist) hipLaunchKernelGGL((k_gemm_w4r<1, 1, 0, 1>), dim3(grid), dim3(WNT), kRingLds, stream, a);
     else hipLaunchKernelGGL((k_gemm_w4r<1, 0, 0, 1>), dim3(grid), dim3(WNT), kRingLds, stream, a);
+  } else if (sched & 1024) {
+    // reads-then-DMA phase placement (PS 1)
+    if (persist) hipLaunchKernelGGL((k_gemm_w4r<1, 1, 0, 0, 0, 0, 1>), dim3(grid), dim3(WNT), kRingLds, stream, a);
+    else hipLaunchKernelGGL((k_gemm_w4r<1, 0, 0, 0, 0, 0, 1>), dim3(grid), dim3(WNT), kRingLds, stream, a);
   } else if (abl == 1) {
     hipLaunchKernelGGL((k_gemm_w4r<1, 0, 1>), dim3(grid), dim3(WNT), kRingLds, stream, a);
   } else if (abl == 2) {
