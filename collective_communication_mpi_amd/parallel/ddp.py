@@ -59,10 +59,13 @@ class _GradSink:
     the user dropped ``.grad``), add when accumulating micro-batches -- and ``done()``
     counts the parameter ready in its bucket, exactly like the post-accumulate hook."""
 
-    __slots__ = ("ddp", "param", "view", "fresh", "reported")
+    __slots__ = ("ddp", "param", "view", "fresh", "reported", "scale")
 
-    def __init__(self, ddp, param, view):
+    def __init__(self, ddp, param, view, scale: float = 1.0):
         self.ddp, self.param, self.view, self.fresh, self.reported = ddp, param, view, True, False
+        # the DP average folded into the producing GEMM (alpha = 1/p): no scaling pass over
+        # the reduced bucket afterwards
+        self.scale = scale
 
     def begin(self):
         q = self.param
@@ -141,7 +144,8 @@ class DistributedDataParallel(torch.nn.Module):
             for b in self.buckets:
                 for q in b.params:
                     if id(q) in capable:
-                        sk = _GradSink(self, q, self._view_of[id(q)])
+                        sk = _GradSink(self, q, self._view_of[id(q)],
+                                       1.0 / self.p if (self.average and self.p > 1) else 1.0)
                         q._ccmpi_grad_sink = sk
                         b.sinks.append(sk)
 
@@ -235,9 +239,17 @@ class DistributedDataParallel(torch.nn.Module):
             torch.cuda.current_stream(self.device).wait_stream(self.stream)
         if self.average and self.p > 1 and self.require_backward_grad_sync:
             # (no_sync micro-batches: the local sums keep accumulating, the synchronising
-            # backward reduces and averages all of them at once)
+            # backward reduces and averages all of them at once).  Gradients delivered by a
+            # sink are already scaled by 1/p in their GEMM's epilogue: only the others are
+            # scaled here (norms, biases, embeddings: ~1 GB of a Llama-3-8B's 16 GB)
             for b in self.buckets:
-                b.buf.mul_(1.0 / self.p)
+                if not b.sinks:
+                    b.buf.mul_(1.0 / self.p)
+                    continue
+                sunk = {id(sk.param) for sk in b.sinks}
+                for q in b.params:
+                    if id(q) not in sunk:
+                        self._view_of[id(q)].mul_(1.0 / self.p)
         for b in self.buckets:
             b.pending = len(b.params)
             b.launched = False

@@ -270,7 +270,9 @@ def _deliver_wgrad(w: torch.Tensor, dw):
         return dw
     view, acc = sink.begin()
     if acc:
-        view.add_(dw.view_as(view))
+        view.add_(dw.view_as(view), alpha=sink.scale)
+    elif sink.scale != 1.0:
+        torch.mul(dw.view_as(view), sink.scale, out=view)
     else:
         view.copy_(dw.view_as(view))
     sink.done()
@@ -286,8 +288,10 @@ def _wgrad(g2: torch.Tensor, x2: torch.Tensor, w: torch.Tensor, comm):
     if sink is None or not sink.view.is_contiguous():
         return _deliver_wgrad(w, _linear_backward(g2, x2, w, False, True, comm)[1])
     view, acc = sink.begin()
-    if _gpu_shared(comm) or gemm_ring(g2, x2, True, True, out=view.view(w.shape), accumulate=acc) is None:
-        dw = gemm_tn(g2, x2).to(w.dtype)
+    # the DDP average rides in the GEMM's alpha (sink.scale = 1/p)
+    if _gpu_shared(comm) or gemm_ring(g2, x2, True, True, out=view.view(w.shape), alpha=sink.scale,
+                                      accumulate=acc) is None:
+        dw = gemm_tn(g2, x2, alpha=sink.scale).to(w.dtype)
         if acc:
             view.add_(dw.view_as(view))
         else:

@@ -54,6 +54,13 @@ def test_device_ondemand_registration(n):
     assert "0 failures" in r.stdout
 
 
+def test_captured_registration_slot_is_pinned():
+    """a slot a captured HIP graph uses is pinned -- more registrations than
+    CCMPI_REGISTER_SLOTS afterwards do not evict it, and the replay is still exact."""
+    r = run_ranks(2, py("tests/workers/capture_pin_worker.py"), timeout=200, env=ENV)
+    assert "capture pin OK" in r.stdout
+
+
 @pytest.mark.parametrize("n", [2, 4, 8])
 def test_device_collectives_random_skew(n):
     """Randomised per-rank host/device delays, back-to-back calls, symmetric and staged
