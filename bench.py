@@ -85,7 +85,7 @@ def parse(argv=None):
     ap.add_argument("--dp-tokens", type=int, default=4096, help="tokens per rank of the DP-overlap phase")
     ap.add_argument("--dp-vocab", type=int, default=1,
                     help="DP overlap: include the LM head and token embedding (Llama-3-8B: 16.06 GB of gradients)")
-    ap.add_argument("--dp-scripted", type=int, default=1,
+    ap.add_argument("--dp-scripted", type=int, default=0,
                     help="DP phase: also measure the scripted wgrad-only overlap (parallel/overlap.py) as a secondary")
     ap.add_argument("--a2a-mb", type=int, default=256)
     ap.add_argument("--mlp-tokens", type=int, default=4096,
@@ -644,7 +644,7 @@ def dp_phase(args) -> dict:
     from collective_communication_mpi_amd.parallel.llama_dp import measure_ddp_overlap
 
     out = measure_ddp_overlap(comm, layers=args.dp_layers, tokens=args.dp_tokens, vocab=bool(args.dp_vocab),
-                              iters=2, verbose=args.verbose)
+                              iters=2, blocks_sweep=[64, 256], verbose=args.verbose)
     if args.dp_scripted:
         import torch
 
