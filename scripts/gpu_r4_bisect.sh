@@ -9,14 +9,16 @@ OUT=gpurun_out/${OUT_TAG:-r4_bisect}
 mkdir -p $OUT
 export TMPDIR=/tmp
 export GPU_MAX_HW_QUEUES=${Q:-1}
-export CCMPI_DEVICE_TIMEOUT_S=20
-for pre in ${PREFIXES:-none ar ar,free ar,bf16,a2a ar,bf16,a2a,free}; do
+export CCMPI_DEVICE_TIMEOUT_S=20 CCMPI_HARNESS_VERBOSE=1
+# variant = prefix:train (train 0 = the round-3 harness_dryrun.py forward-only run)
+for v in ${VARIANTS:-none:0 none:1 ar:1 ar,bf16,a2a,free:1}; do
+  pre=${v%%:*}; train=${v##*:}
   p=$pre; [ "$p" = none ] && p=""
   timeout -k 10 300 python -m collective_communication_mpi_amd.launch -n 8 --timeout 280 \
-    python benchmarks/graph_replay_repro.py --prefix "$p" > $OUT/$pre.out 2> $OUT/$pre.err
-  rc=$?; echo "prefix '$pre' rc=$rc"; tail -2 $OUT/$pre.out
+    python benchmarks/graph_replay_repro.py --prefix "$p" --train $train > $OUT/${pre}_t$train.out 2> $OUT/${pre}_t$train.err
+  rc=$?; echo "prefix '$pre' train $train rc=$rc"; tail -2 $OUT/${pre}_t$train.out
   if [ $rc -ne 0 ]; then
-    grep -m1 -A60 "ccmpi crash" $OUT/$pre.err || tail -40 $OUT/$pre.err
+    grep -m1 -A60 "ccmpi crash" $OUT/${pre}_t$train.err || tail -40 $OUT/${pre}_t$train.err
     exit $rc
   fi
 done

@@ -9,6 +9,7 @@ mkdir -p $OUT
 export TMPDIR=/tmp
 timeout -k 10 300 python benchmarks/gemm_ps_ab.py --scheds ${SCHEDS:-8,9,1032,1033} > $OUT/ps_ab.jsonl 2> $OUT/ps_ab.err
 rc=$?; echo "ps_ab rc=$rc"; cat $OUT/ps_ab.jsonl; [ $rc -ne 0 ] && { tail -20 $OUT/ps_ab.err; exit $rc; }
+[ "${PMC:-1}" = 0 ] && exit 0
 read M N K <<< "$(echo ${SHAPE:-4096x28672x4096} | tr x ' ')"
 P1="SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE"
 P2="SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_LDS SQ_INSTS_VMEM SQ_INSTS_VALU_MFMA_MOPS_BF16 SQ_INSTS_SALU SQ_ACTIVE_INST_VALU"
