@@ -428,7 +428,7 @@ def run_collectives(comm, args, log=lambda *a: None, groups=("ar", "bf16", "a2a"
             try:
                 buf_out.zero_()
                 sync_barrier()
-                dev.allreduce(buf_in, buf_out, "SUM", algo)
+                dev.allreduce(buf_in, buf_out, "SUM", algo, symmetric=True)
                 torch.cuda.synchronize()
                 dev.check()
                 ok = int(bool(torch.all(buf_out == expect).item()))
@@ -440,8 +440,8 @@ def run_collectives(comm, args, log=lambda *a: None, groups=("ar", "bf16", "a2a"
                 failed[0] = True
                 dev.reset()  # a timed-out kernel leaves per-CTA epochs inconsistent
                 continue
-            dev.allreduce(buf_in, buf_out, "SUM", algo)
-            results[algo] = timed(lambda: dev.allreduce(buf_in, buf_out, "SUM", algo), 3)
+            dev.allreduce(buf_in, buf_out, "SUM", algo, symmetric=True)
+            results[algo] = timed(lambda: dev.allreduce(buf_in, buf_out, "SUM", algo, symmetric=True), 3)
             log(f"candidate {algo} ({buf_in.dtype}): {results[algo] * 1e3:.3f} ms")
         good = {a: t for a, t in results.items() if t}
         if not good:
@@ -455,8 +455,8 @@ def run_collectives(comm, args, log=lambda *a: None, groups=("ar", "bf16", "a2a"
     expect = float(world * (world + 1) // 2)
     results, best = pick(x, y, expect, allreduce_candidates(world, dev.shared_device, args.algo))
     for _ in range(args.warmup):
-        dev.allreduce(x, y, "SUM", best)
-    t_step = timed(lambda: dev.allreduce(x, y, "SUM", best), args.steps)
+        dev.allreduce(x, y, "SUM", best, symmetric=True)
+    t_step = timed(lambda: dev.allreduce(x, y, "SUM", best, symmetric=True), args.steps)
     torch.cuda.synchronize()
     final_ok = bool(hc.allreduce(int(bool(torch.all(y == expect).item())), op=MPI.MIN))
     algbw = nbytes / t_step / 1e9
@@ -468,7 +468,7 @@ def run_collectives(comm, args, log=lambda *a: None, groups=("ar", "bf16", "a2a"
         xb.fill_(float(rank + 1))
         top = sorted((a for a, t in results.items() if t), key=lambda a: results[a])[:3]
         res16, best16 = pick(xb, yb, expect, top)
-        t16 = timed(lambda: dev.allreduce(xb, yb, "SUM", best16), max(3, args.steps // 2))
+        t16 = timed(lambda: dev.allreduce(xb, yb, "SUM", best16, symmetric=True), max(3, args.steps // 2))
         sec["bf16_1GiB"] = {"algo": best16, "ms": round(t16 * 1e3, 4), "algbw_GBps": round(nbytes / t16 / 1e9, 2),
                             "busbw_GBps": round(nbytes / t16 / 1e9 * (2 * (world - 1) / world), 2) if world > 1 else 0.0,
                             "candidates_ms": ms(res16)}

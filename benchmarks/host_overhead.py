@@ -5,7 +5,8 @@
 For a 32 MiB bf16 tensor (the Llama TP all-reduce size at 4096 tokens):
 * ``registered``: an ordinary torch tensor -- on-demand registration, one pickled host
   all-gather per call (the round-3 path of every TP all-reduce);
-* ``heap``: a symmetric-heap block -- no host call;
+* ``heap``: symmetric-heap blocks, symmetric decided collectively (one host all-gather);
+* ``heap_promise``: the same with ``symmetric=True`` (DDP buckets, the bench) -- no host call;
 * ``to_local``: heap scratch reduced into an ordinary tensor (``allreduce_to_local``, the
   TP layers' path now) -- no host call.
 Per variant: host microseconds per call (issue only: the loop queues ``--calls`` calls,
@@ -33,6 +34,7 @@ out = torch.empty(n, dtype=torch.bfloat16, device=dev.device)
 variants = {
     "registered": lambda: dev.allreduce(plain, plain, "SUM", "fanout"),
     "heap": lambda: dev.allreduce(heap, heap2, "SUM", "fanout"),
+    "heap_promise": lambda: dev.allreduce(heap, heap2, "SUM", "fanout", symmetric=True),
     "to_local": lambda: dev.allreduce_to_local(heap, out),
 }
 res = {}

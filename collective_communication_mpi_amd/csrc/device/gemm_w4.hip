@@ -599,6 +599,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t op_rsrc_t(const uint16_t* X, i
 // read-free stretch: MI355X_MICROARCH.md, per-instruction constants); measured no faster
 // (profiles/r4_gemm).  2: PS 0 with the odd waves one MFMA later (hipBLASLt runs two
 // copies of its loop, picked by the SIMD id, whose DMA / read slots differ by one MFMA).
+// 3: PS 0 with the DMA pieces' LDS addresses as one M0 chain (dma_chain).
 template <int EPI, int PERSIST, int ABL = 0, int STAMP = 0, int TA = 0, int TB = 0, int PS = 0>
 __global__ void __launch_bounds__(WNT, 1) k_gemm_w4r(W4Args wa) {
   const GemmArgs& g = wa.g;
@@ -668,6 +669,26 @@ __global__ void __launch_bounds__(WNT, 1) k_gemm_w4r(W4Args wa) {
     }
   };
   auto dma = [&](int s, int i) { dma_piece(dma_step(s), i); };
+  // PS 3 (N layout): the LDS-DMA pieces of a step as one M0 chain -- M0 is set once per
+  // phase and advanced right after each piece, so no piece waits on a just-written M0
+  // (the builtin emits s_mov m0 + s_nop 0 in front of every piece)
+  auto dma_m0_set = [&](const DmaStep& d) {
+    const uint32_t m0v = (uint32_t)(uintptr_t)(lds_vptr)d.lds;
+    asm volatile("s_mov_b32 m0, %0" : : "s"(m0v) : "memory", "m0");
+  };
+  auto dma_chain = [&](const DmaStep& d, int i) {
+    const bool isa = i < 4;
+    const int so = isa ? (i == 0 ? 0 : i == 1 ? sa1 : i == 2 ? sa2 : sa3)
+                       : (i == 4 ? 0 : i == 5 ? sb1 : i == 6 ? sb2 : sb3);
+    const int vo = isa ? d.va : d.vb;
+    // next piece's LDS address: +4 KiB, except A piece 3 -> B piece 0 (the B half)
+    if (i == 3)
+      asm volatile("buffer_load_dwordx4 %0, %1, %2 offen lds\n\ts_add_u32 m0, m0, %3"
+                   : : "v"(vo), "s"(ra), "s"(so), "i"(kRingHalf - 3 * 4096) : "memory", "m0");
+    else
+      asm volatile("buffer_load_dwordx4 %0, %1, %2 offen lds\n\ts_add_u32 m0, m0, 0x1000"
+                   : : "v"(vo), "s"(isa ? ra : rb), "s"(so) : "memory", "m0");
+  };
   // fragment (16x16x32): lane l reads row (l & 15) of a 16-row block, logical chunk l >> 4;
   // the physical chunk depends on the lane only (block rows are multiples of 16)
   const int rdo = (lane & 15) * 64 + (((lane >> 4) ^ ring_swz((lane >> 2) & 3)) << 4);
@@ -748,6 +769,18 @@ __global__ void __launch_bounds__(WNT, 1) k_gemm_w4r(W4Args wa) {
           }
           __builtin_amdgcn_sched_barrier(0);
         }
+      } else if constexpr (PS == 3) {
+        if (i == 0 && DMA && !(ABL & 1)) dma_m0_set(ds);
+        mm(0, 1);
+        if constexpr (!(ABL & 2)) rd1(q, i, 0, ca, cb);
+        __builtin_amdgcn_sched_barrier(0);
+        mm(1, 3);
+        if constexpr (DMA && !(ABL & 1)) dma_chain(ds, i);
+        __builtin_amdgcn_sched_barrier(0);
+        mm(3, 5);
+        if constexpr (!(ABL & 2)) rd1(q, i, 1, ca, cb);
+        __builtin_amdgcn_sched_barrier(0);
+        mm(5, 8);
       } else if constexpr (SHIFT) {
         // PS 2, odd waves: the same order one MFMA later, so the CU's four waves do not
         // hand their LDS-DMA pieces and reads to the shared address unit at the same cycle
@@ -1077,6 +1110,8 @@ void launch_gemm_ring(const GemmArgs& g, int ta, int tb, hipStream_t stream, uin
     w4r_attr(reinterpret_cast<const void*>(k_gemm_w4r<1, 0, 0, 0, 0, 0, 2>));
     w4r_attr(reinterpret_cast<const void*>(k_gemm_w4r<1, 1, 0, 0, 0, 0, 2>));
     w4r_attr(reinterpret_cast<const void*>(k_gemm_w4r<2, 1, 0, 0, 0, 0, 0>));
+    w4r_attr(reinterpret_cast<const void*>(k_gemm_w4r<1, 0, 0, 0, 0, 0, 3>));
+    w4r_attr(reinterpret_cast<const void*>(k_gemm_w4r<2, 0, 0, 0, 0, 0, 3>));
     return true;
   }();
   (void)attr;
@@ -1085,7 +1120,8 @@ void launch_gemm_ring(const GemmArgs& g, int ta, int tb, hipStream_t stream, uin
   const bool fast = gemm_w4r_fast(g);
   if (glu) {  // SwiGLU epilogue (callers check gemm_w4r_fast and the glu layout first)
     if (!fast || ta || tb) throw std::invalid_argument("gemm ring: the SwiGLU epilogue needs the fast NT form");
-    if (sched & 1024) hipLaunchKernelGGL((k_gemm_w4r<2, 0, 0, 0, 0, 0, 1>), dim3(ntiles), dim3(WNT), kRingLds, stream, a);
+    if (sched & 4096) hipLaunchKernelGGL((k_gemm_w4r<2, 0, 0, 0, 0, 0, 3>), dim3(ntiles), dim3(WNT), kRingLds, stream, a);
+    else if (sched & 1024) hipLaunchKernelGGL((k_gemm_w4r<2, 0, 0, 0, 0, 0, 1>), dim3(ntiles), dim3(WNT), kRingLds, stream, a);
     else hipLaunchKernelGGL((k_gemm_w4r<2, 0>), dim3(ntiles), dim3(WNT), kRingLds, stream, a);
     return;
   }
@@ -1110,6 +1146,9 @@ void launch_gemm_ring(const GemmArgs& g, int ta, int tb, hipStream_t stream, uin
     if (sched & 1024) hipLaunchKernelGGL((k_gemm_w4r<1, 0, 0, 1, 0, 0, 1>), dim3(grid), dim3(WNT), kRingLds, stream, a);
     else if (persist) hipLaunchKernelGGL((k_gemm_w4r<1, 1, 0, 1>), dim3(grid), dim3(WNT), kRingLds, stream, a);
     else hipLaunchKernelGGL((k_gemm_w4r<1, 0, 0, 1>), dim3(grid), dim3(WNT), kRingLds, stream, a);
+  } else if (sched & 4096) {
+    // chained-M0 LDS-DMA (PS 3)
+    hipLaunchKernelGGL((k_gemm_w4r<1, 0, 0, 0, 0, 0, 3>), dim3(grid), dim3(WNT), kRingLds, stream, a);
   } else if (sched & 2048) {
     // parity-staggered phase placement (PS 2)
     if (persist) hipLaunchKernelGGL((k_gemm_w4r<1, 1, 0, 0, 0, 0, 2>), dim3(grid), dim3(WNT), kRingLds, stream, a);

@@ -584,21 +584,24 @@ class DeviceGroup:
     def _symm(self, *ts) -> bool:
         return all(self.is_symmetric(t) and t.data_ptr() % 16 == 0 for t in ts)
 
-    def _symm_call(self, nbytes: int, *ts) -> bool:
+    def _symm_call(self, nbytes: int, *ts, promise: Optional[bool] = None) -> bool:
         """The ``symmetric`` decision of one collective, identical on every rank.
         Below ``reg_min`` bytes (or with registration off): every tensor from the
         symmetric heap (the caller's promise).  From ``reg_min`` up: collective
-        on-demand registration of whatever the tensors live in."""
+        on-demand registration of whatever the tensors live in (one host all-gather;
+        a rank-local check is not enough there: a view at a rank-dependent offset can be
+        aligned on one rank and not on another).  ``promise=True``: the caller guarantees
+        heap blocks of the same layout on every rank (DDP buckets, persistent TP scratch,
+        the bench's buffers) -- no host call; ``CCMPI_VERIFY_SYMMETRIC=1`` checks it."""
+        if promise:
+            ok = self._symm(*ts)
+            if self.verify_symmetric and not all(self.host.allgather(ok)):
+                raise RuntimeError("collective: symmetric=True promised, but not every rank passed aligned heap blocks")
+            if not ok:
+                raise ValueError("collective: symmetric=True needs 16-B aligned symmetric-heap tensors")
+            return True
         if self.size == 1 or self.reg_min <= 0 or nbytes < self.reg_min:
             return self._symm(*ts)
-        heap = self._symm(*ts)
-        if self.verify_symmetric and len(set(self.host.allgather(heap))) > 1:
-            raise RuntimeError("collective: symmetric-heap tensors on some ranks only")
-        if heap:
-            # every tensor is a symmetric-heap block here: the same contract as below
-            # reg_min (heap blocks on one rank are heap blocks on every rank), so no host
-            # call; CCMPI_VERIFY_SYMMETRIC=1 checks the contract with one all-gather
-            return True
         return self._register_call(ts)
 
     def _alloc_generation(self) -> int:
@@ -741,7 +744,9 @@ class DeviceGroup:
     # ------------------------------------------------------------- collectives
     @trace_call("allreduce")
     def allreduce(self, src, dst=None, op="SUM", algo: str = "auto", rings: int = 0,
-                  max_blocks: Optional[int] = None) -> object:
+                  max_blocks: Optional[int] = None, symmetric: Optional[bool] = None) -> object:
+        """``symmetric=True``: src / dst are symmetric-heap blocks of the same layout on every
+        rank (no host call; see ``_symm_call``); default: decided collectively."""
         dst = src if dst is None else dst
         self._check(src, "src")
         self._check(dst, "dst")
@@ -766,7 +771,7 @@ class DeviceGroup:
         if algo in _HAND_ALGOS:
             # ring / rhd read only the local input and push into peers' outputs:
             # "symmetric" there means a registered output (and an aligned input)
-            symm = self._symm_call(nbytes, *((dst,) if algo in ("ring", "rhd") else (src, dst)))
+            symm = self._symm_call(nbytes, *((dst,) if algo in ("ring", "rhd") else (src, dst)), promise=symmetric)
             if algo in ("ring", "rhd"):
                 symm = symm and src.data_ptr() % 16 == 0
             self.dc.allreduce(src.data_ptr(), dst.data_ptr(), src.numel(), dt, opc, getattr(self.D, _HAND_ALGOS[algo]),
@@ -1053,7 +1058,7 @@ class DeviceGroup:
                     continue
                 ok = 1
                 try:
-                    self.allreduce(x[:n], y[:n], "SUM", algo)
+                    self.allreduce(x[:n], y[:n], "SUM", algo, symmetric=True)
                     torch.cuda.synchronize(self.device)
                     self.check()
                     ok = int(bool(torch.all(y[:n] == expect).item()))
@@ -1066,7 +1071,7 @@ class DeviceGroup:
                 self.host.Barrier()
                 t0 = time.perf_counter()
                 for _ in range(iters):
-                    self.allreduce(x[:n], y[:n], "SUM", algo)
+                    self.allreduce(x[:n], y[:n], "SUM", algo, symmetric=True)
                 torch.cuda.synchronize(self.device)
                 t = self.host.allreduce(time.perf_counter() - t0, op=_host_max())
                 if best_t is None or t < best_t:

@@ -455,7 +455,7 @@ class MnistTPLayer:
         if c == 1:
             gemm_nt(att, wo, out=z, out_dtype=torch.float32, splitk=1, bias=bias)
             if self.tp_dev is not None:
-                self.tp_dev.allreduce(z, z, "SUM")
+                self.tp_dev.allreduce(z, z, "SUM", symmetric=True)  # z: heap block (_buf), same on every rank
             return z
         main = torch.cuda.current_stream(self.device)
         if "tp_side" not in self._bufs:
@@ -476,7 +476,7 @@ class MnistTPLayer:
             gemm_nt(att[r0:r1], wo, out=z[r0:r1], out_dtype=torch.float32, splitk=1, bias=bias)
             side.wait_stream(main)
             with torch.cuda.stream(side):
-                self.tp_dev.allreduce(z[r0:r1], z[r0:r1], "SUM", max_blocks=self.tp_dev.overlap_blocks)
+                self.tp_dev.allreduce(z[r0:r1], z[r0:r1], "SUM", max_blocks=self.tp_dev.overlap_blocks, symmetric=True)
         main.wait_stream(side)
         return z
 

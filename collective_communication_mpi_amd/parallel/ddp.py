@@ -218,13 +218,14 @@ class DistributedDataParallel(torch.nn.Module):
             self.hc.Allreduce(MPI.IN_PLACE, b.buf.numpy(), op=MPI.SUM)
             return
         if self.stream is None:
-            self.dev.allreduce(b.buf, b.buf, "SUM", self.algo)
+            self.dev.allreduce(b.buf, b.buf, "SUM", self.algo, symmetric=True)
             return
         ev = torch.cuda.Event()
         ev.record(torch.cuda.current_stream(self.device))
         self.stream.wait_event(ev)
         with torch.cuda.stream(self.stream):  # beside the backward: the overlap CTA budget
-            self.dev.allreduce(b.buf, b.buf, "SUM", self.algo, max_blocks=self.max_blocks or self.dev.overlap_blocks)
+            self.dev.allreduce(b.buf, b.buf, "SUM", self.algo, max_blocks=self.max_blocks or self.dev.overlap_blocks,
+                               symmetric=True)
 
     def finish(self) -> None:
         """Complete the gradient synchronisation (after backward, before the step)."""
@@ -279,7 +280,8 @@ class DistributedDataParallel(torch.nn.Module):
         if self.dev is None or self.p == 1:
             return
         for b in self.buckets:
-            self.dev.allreduce(b.buf, b.buf, "SUM", self.algo, max_blocks=self.max_blocks or self.dev.overlap_blocks)
+            self.dev.allreduce(b.buf, b.buf, "SUM", self.algo, max_blocks=self.max_blocks or self.dev.overlap_blocks,
+                               symmetric=True)
 
     @property
     def bucket_sizes(self) -> List[int]:
