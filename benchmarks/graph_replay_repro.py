@@ -33,6 +33,9 @@ ap.add_argument("--batch", type=int, default=2048)
 ap.add_argument("--size-mb", type=int, default=1024)
 ap.add_argument("--steps", type=int, default=5)
 ap.add_argument("--train", type=int, default=1)
+ap.add_argument("--variants", default="token:1",
+                help="harness forwards to run in order, fc_o_mode:tp_chunks (bench's harness phase: "
+                     "token:1,row:1,token:4); the first one also trains (--train)")
 args = ap.parse_args()
 prefix = [p for p in args.prefix.split(",") if p]
 comm = Communicator(MPI.COMM_WORLD)
@@ -56,11 +59,16 @@ if "free" in prefix:
     torch.cuda.empty_cache()
     say("freed")
 say(f"harness tp={args.tp}, dev registrations={comm.dev.registrations}")
-res = bench_forward(comm, tp=args.tp, batch=args.batch, steps=args.steps, warmup=2, train=bool(args.train),
-                    fc_o_mode="token")
+results = []
+for k, v in enumerate(args.variants.split(",")):
+    mode, chunks = v.split(":")
+    say(f"bench_forward fc_o={mode} tp_chunks={chunks}")
+    res = bench_forward(comm, tp=args.tp, batch=args.batch, steps=args.steps, warmup=2,
+                        train=bool(args.train) and k == 0, fc_o_mode=mode, tp_chunks=int(chunks))
+    results.append({"variant": v, "fwd_ms": round(res["fwd_ms"], 4), "hip_graph": res["hip_graph"]})
 torch.cuda.synchronize()
 comm.comm.Barrier()
 if rank == 0:
     print(json.dumps({"prefix": prefix, "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
-                      "fwd_ms": res["fwd_ms"], "hip_graph": res["hip_graph"]}), flush=True)
+                      "graph_queues": os.environ.get("DEBUG_HIP_FORCE_GRAPH_QUEUES"), "results": results}), flush=True)
     print("replay OK", flush=True)

@@ -583,7 +583,8 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t op_rsrc_t(const uint16_t* X, i
 // EPI 2: EPI 1 plus the SwiGLU gate of interleaved (gate, up) output column pairs:
 // glu[r, c / 2] = silu(C[r, c]) * C[r, c + 1] for even c, from the bf16-rounded C (the
 // values the unfused gate would read), one 8-B store next to each 16-B row store.
-// ABL (diagnostic ablations, wrong results): bit 0 drops the steady-state DMA, bit 1 the
+// ABL (diagnostic ablations, wrong results): bit 2 reads whole 128-B lines per DMA piece
+// (8 rows instead of 16 half lines); bit 0 drops the steady-state DMA, bit 1 the
 // steady-state fragment reads.  STAMP (diagnostic): per wave, s_memtime cycles of the
 // prologue, main loop, epilogue and the phase-end waits -> wa.dbg (first tile only).
 // TA / TB: operand layout.  0 ("N"): rows of K contiguous elements (A[m][k], B[n][k]).
@@ -628,8 +629,10 @@ __global__ void __launch_bounds__(WNT, 1) k_gemm_w4r(W4Args wa) {
 
   // DMA piece i of a step: 16 rows x 64 B; wave w covers rows (4 i + w) * 16 ..
   // lane l: row + (l >> 2), physical chunk l & 3 <- logical chunk (l & 3) ^ f((l >> 4) & 3)
-  const int drow = wave * 16 + (lane >> 2);
-  const int dchunk = ((lane & 3) ^ ring_swz((lane >> 4) & 3)) << 4;
+  // (ABL bit 2, diagnostic: each piece reads 8 rows x 128 B -- whole cache lines, as
+  // hipBLASLt's 64-deep K tiles do -- instead of 16 rows x 64 B; wrong results)
+  const int drow = (ABL & 4) ? wave * 16 + (lane >> 3) : wave * 16 + (lane >> 2);
+  const int dchunk = (ABL & 4) ? (lane & 7) << 4 : ((lane & 3) ^ ring_swz((lane >> 4) & 3)) << 4;
   const int va = drow * g.lda * 2 + dchunk, vb = drow * g.ldb * 2 + dchunk;
   // K-major pieces: 2 k-rows x 512 B; wave w, piece i: k-rows 8 i + 2 w + (l >> 5); lane l
   // lands at granule (l & 31) >> 1, half l & 1, holding logical granule ^ tn_swz(k-row)
@@ -646,7 +649,8 @@ __global__ void __launch_bounds__(WNT, 1) k_gemm_w4r(W4Args wa) {
   const int sa2 = 2 * sa1, sa3 = 3 * sa1, sb2 = 2 * sb1, sb3 = 3 * sb1;
   const int ka = TA ? 64 * g.lda : 64, kb = TB ? 64 * g.ldb : 64;  // bytes per K-step
   auto dma_step = [&](int s) {
-    return DmaStep{smem + (s & 3) * kRing + wave * 1024, ta0 + s * ka, tb0 + s * kb, ta1 + s * ka, tb1 + s * kb};
+    const int sk = (ABL & 4) ? (s >> 1) * 2 : s;  // ABL 4: 128-B aligned K windows
+    return DmaStep{smem + (s & 3) * kRing + wave * 1024, ta0 + sk * ka, tb0 + sk * kb, ta1 + sk * ka, tb1 + sk * kb};
   };
   auto dma_piece = [&](const DmaStep& d, int i) {
     const bool isa = i < 4;
@@ -1111,6 +1115,7 @@ void launch_gemm_ring(const GemmArgs& g, int ta, int tb, hipStream_t stream, uin
     w4r_attr(reinterpret_cast<const void*>(k_gemm_w4r<1, 1, 0, 0, 0, 0, 2>));
     w4r_attr(reinterpret_cast<const void*>(k_gemm_w4r<2, 1, 0, 0, 0, 0, 0>));
     w4r_attr(reinterpret_cast<const void*>(k_gemm_w4r<1, 0, 0, 0, 0, 0, 3>));
+    w4r_attr(reinterpret_cast<const void*>(k_gemm_w4r<1, 0, 4>));
     w4r_attr(reinterpret_cast<const void*>(k_gemm_w4r<2, 0, 0, 0, 0, 0, 3>));
     return true;
   }();
@@ -1157,6 +1162,9 @@ void launch_gemm_ring(const GemmArgs& g, int ta, int tb, hipStream_t stream, uin
     // reads-then-DMA phase placement (PS 1)
     if (persist) hipLaunchKernelGGL((k_gemm_w4r<1, 1, 0, 0, 0, 0, 1>), dim3(grid), dim3(WNT), kRingLds, stream, a);
     else hipLaunchKernelGGL((k_gemm_w4r<1, 0, 0, 0, 0, 0, 1>), dim3(grid), dim3(WNT), kRingLds, stream, a);
+  } else if (sched & 8192) {
+    // diagnostic: whole-cache-line DMA pieces (ABL 4, wrong results)
+    hipLaunchKernelGGL((k_gemm_w4r<1, 0, 4>), dim3(grid), dim3(WNT), kRingLds, stream, a);
   } else if (abl == 1) {
     hipLaunchKernelGGL((k_gemm_w4r<1, 0, 1>), dim3(grid), dim3(WNT), kRingLds, stream, a);
   } else if (abl == 2) {

@@ -655,6 +655,7 @@ class DeviceGroup:
         if any(r is None for r in rows):
             return False
         capturing = self.torch.cuda.is_current_stream_capturing()
+        used = set()  # slots this call resolves: not evictable while it maps the others
         for i in range(len(ts)):
             if all(r[i] is None for r in rows):
                 continue  # heap blocks on every rank
@@ -670,6 +671,7 @@ class DeviceGroup:
                 mine_i = self._export(ts[i].data_ptr()) if mine[i] is None else mine[i]
                 ids = self.host.allgather(mine_i)
             key = tuple(ids)
+            used.add(key)
             slot = self._dyn.get(key)
             if slot is not None:
                 self._dyn.move_to_end(key)
@@ -678,7 +680,7 @@ class DeviceGroup:
                 continue
             if capturing:
                 return False
-            self._map_slot(key)
+            self._map_slot(key, keep=used)
         return True
 
     def unpin_captured(self) -> None:
@@ -686,7 +688,7 @@ class DeviceGroup:
         that captured collectives on registered tensors): they may be evicted again."""
         self._pinned.clear()
 
-    def _map_slot(self, key) -> None:
+    def _map_slot(self, key, keep=()) -> None:
         """Collective: map the allocation set ``key`` (one (handle, base, bytes, gen) per
         rank) into a slot.  Slots holding an older allocation at an overlapping address
         on any rank are released first (every rank sees the same keys, so the slot
@@ -699,7 +701,7 @@ class DeviceGroup:
             # read unmapped memory or another allocation
             raise RuntimeError("collective: memory a captured HIP graph's collective uses was freed and reallocated; "
                                "drop the graph and call unpin_captured() first")
-        evictable = [k for k in self._dyn if k not in self._pinned]
+        evictable = [k for k in self._dyn if k not in self._pinned and k not in keep]
         full = not self._free_slots and len(self._dyn) >= self.reg_slots
         if stale or (full and evictable):
             torch.cuda.synchronize(self.device)  # no queued kernel of this rank still resolves a slot

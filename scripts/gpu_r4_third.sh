@@ -5,7 +5,7 @@ set -o pipefail
 cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
 bash scripts/gpu_r4_suite.sh || exit 1
-OUT_TAG=r4_gemm3 SCHEDS=8,4104 PMC=0 bash scripts/gpu_r4_gemm.sh || exit 1
+OUT_TAG=r4_gemm3 SCHEDS=8,4104,8200 PMC=0 bash scripts/gpu_r4_gemm.sh || exit 1
 mkdir -p gpurun_out/r4_host
 for n in 2 8; do
   timeout -k 10 200 python -m collective_communication_mpi_amd.launch -n $n --timeout 180 \

@@ -113,3 +113,19 @@ def test_pinned_slots_survive_eviction_and_refuse_remap():
     DeviceGroup.unpin_captured(g)
     DeviceGroup._map_slot(g, k1b)           # after unpin the stale slot is reused
     assert k1 not in g._dyn and g._dyn[k1b] == 1
+
+
+def test_slots_of_the_current_call_are_not_evicted():
+    """A collective on two new allocations with one evictable slot left: mapping the second
+    must not evict the first (both are resolved by this call's kernel)."""
+    g = group(slots=2)
+    x = (alloc(b"x", 0x1000, 0x100), alloc(b"x1", 0x1000, 0x100))
+    y = (alloc(b"y", 0x2000, 0x100), alloc(b"y1", 0x2000, 0x100))
+    g._pinned.update({x})
+    DeviceGroup._map_slot(g, x)
+    a = (alloc(b"a", 0x3000, 0x100), alloc(b"a1", 0x3000, 0x100))
+    b = (alloc(b"b", 0x4000, 0x100), alloc(b"b1", 0x4000, 0x100))
+    DeviceGroup._map_slot(g, y)
+    DeviceGroup._map_slot(g, a, keep={a})          # evicts y (LRU, unpinned)
+    DeviceGroup._map_slot(g, b, keep={a, b})       # a is this call's: a new slot instead
+    assert a in g._dyn and b in g._dyn and x in g._dyn and y not in g._dyn
