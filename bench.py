@@ -627,6 +627,7 @@ def harness_phase(args) -> dict:
                 r = bench_forward(comm, tp=tp, batch=args.batch, steps=args.steps, warmup=args.warmup,
                                   train=False, fc_o_mode=vmode, tp_chunks=chunks)
                 other[f"{name}_fwd_ms"] = round(r["fwd_ms"], 4)
+                other[f"{name}_hip_graph"] = r["hip_graph"]
             except Exception as e:  # noqa: BLE001 - a secondary number must not cost the record
                 other[f"{name}_error"] = f"{type(e).__name__}: {e}"[:200]
         harness["fc_o_variants"] = other

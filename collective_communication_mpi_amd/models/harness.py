@@ -57,6 +57,33 @@ def train_step(layer: MnistTPLayer, cfg: LayerConfig, xb, yb):
     return loss
 
 
+def multi_stream_graph_hazard(cfg: LayerConfig, layer: MnistTPLayer):
+    """Why a HIP graph of this forward must not be captured here, or None.
+
+    HIP runtime bug (torch's ROCm 7.0 libamdhip64, root-caused in profiles/r4_bisect): a
+    graph with parallel branches (a forward forked over several streams: the token fc_o's
+    side-stream TP all-reduce pipeline, ``tp_chunks > 1``, or ``fwd_chunks > 1``) gets
+    per-branch "parallel streams" at launch; with few hardware queues per process
+    (``GPU_MAX_HW_QUEUES`` 1-2, the 8-ranks-on-one-GPU dry run) creating them fails
+    ("[hipGraph] Failed to create parallel stream!"), the error is dropped, and the
+    stream-assignment loop then reads past the short stream pool: host SIGSEGV inside
+    hipGraphLaunch on every rank.  Single-stream graphs are not affected.  Such forwards
+    are timed eagerly instead (``CCMPI_FORCE_GRAPH=1`` captures anyway)."""
+    branches = 1
+    if cfg.fc_o_mode == "token" and layer.tp_dev is not None and layer._token_chunks(cfg.batch) > 1:
+        branches = 2
+    if int(cfg.fwd_chunks) > 1:
+        branches = max(branches, int(cfg.fwd_chunks))
+    try:
+        queues = int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))
+    except ValueError:
+        queues = 4
+    if branches > 1 and queues < 4 and os.environ.get("CCMPI_FORCE_GRAPH") != "1":
+        return (f"{branches}-stream forward with GPU_MAX_HW_QUEUES={queues}: HIP graph launch would crash "
+                "(short parallel-stream pool), timed eagerly")
+    return None
+
+
 def bench_forward(comm, tp: int = 2, batch: int = 2048, steps: int = 20, warmup: int = 5, graph: bool = True,
                   train: bool = True, **layer_kw):
     from .. import mpi as MPI
@@ -81,7 +108,10 @@ def bench_forward(comm, tp: int = 2, batch: int = 2048, steps: int = 20, warmup:
     say("eager forward ok")
     used_graph = False
     g = None
-    if graph and os.environ.get("CCMPI_NO_GRAPH") != "1":
+    hazard = multi_stream_graph_hazard(cfg, layer) if graph else None
+    if hazard:
+        say(hazard)
+    if graph and not hazard and os.environ.get("CCMPI_NO_GRAPH") != "1":
         try:
             s = torch.cuda.Stream()
             s.wait_stream(torch.cuda.current_stream())
@@ -112,7 +142,8 @@ def bench_forward(comm, tp: int = 2, batch: int = 2048, steps: int = 20, warmup:
     say(f"timed forward {fwd_s * 1e3:.3f} ms")
     if not train:
         return {"tp": cfg.tp, "dp": cfg.dp, "fwd_ms": fwd_s * 1e3, "hip_graph": used_graph, "fc_o_mode": cfg.fc_o_mode,
-                "tp_chunks": cfg.tp_chunks, "tokens_per_step": cfg.batch * cfg.dp * cfg.seq}
+                "tp_chunks": cfg.tp_chunks, "tokens_per_step": cfg.batch * cfg.dp * cfg.seq,
+                **({"graph_skipped": hazard} if hazard else {})}
     # training step (eager)
     for _ in range(2):
         train_step(layer, cfg, xb, yb)

@@ -6,9 +6,9 @@ set -o pipefail
 cd "$(dirname "$0")/.."
 OUT=gpurun_out/${OUT_TAG:-r4_hcrash}
 mkdir -p $OUT
-export TMPDIR=/tmp GPU_MAX_HW_QUEUES=${Q:-1} CCMPI_HARNESS_VERBOSE=1
+export TMPDIR=/tmp GPU_MAX_HW_QUEUES=${Q:-1} CCMPI_HARNESS_VERBOSE=1 AMD_LOG_LEVEL=${LOG:-1}
 timeout -k 10 300 python -m collective_communication_mpi_amd.launch -n 8 --timeout 280 \
-  AMD_LOG_LEVEL=1 python bench.py --gpus 8 --steps 5 --warmup 2 --phase harness --result $OUT/harness.json --verbose \
+  python bench.py --gpus 8 --steps 5 --warmup 2 --phase harness --result $OUT/harness.json --verbose \
   > $OUT/out.txt 2> $OUT/err.txt
 rc=$?; echo "harness phase rc=$rc"; cat $OUT/harness.json 2>/dev/null | cut -c1-400; echo
 grep -E "\[harness rank 0\]" $OUT/err.txt | tail -12

@@ -70,3 +70,24 @@ def test_phase_plan_isolates_harness():
     assert names == ["coll", "harness", "mlp", "dp", "rccl"]
     assert [p for p, _ in bench.plan_phases(args, 1)] == ["coll", "harness", "mlp"]
     assert "fanout:1024" not in bench.allreduce_candidates(8, False)
+
+
+def test_multi_stream_graph_hazard(monkeypatch):
+    """The HIP-graph guard of the harness: multi-stream forwards are not captured with fewer
+    than 4 hardware queues per process (the runtime's parallel-stream crash)."""
+    from types import SimpleNamespace
+
+    from collective_communication_mpi_amd.models.harness import multi_stream_graph_hazard
+
+    layer = SimpleNamespace(tp_dev=object(), _token_chunks=lambda B: 4)
+    cfg = SimpleNamespace(fc_o_mode="token", batch=2048, fwd_chunks=1)
+    monkeypatch.setenv("GPU_MAX_HW_QUEUES", "1")
+    assert multi_stream_graph_hazard(cfg, layer)
+    monkeypatch.setenv("CCMPI_FORCE_GRAPH", "1")
+    assert multi_stream_graph_hazard(cfg, layer) is None
+    monkeypatch.delenv("CCMPI_FORCE_GRAPH")
+    monkeypatch.setenv("GPU_MAX_HW_QUEUES", "4")
+    assert multi_stream_graph_hazard(cfg, layer) is None
+    monkeypatch.setenv("GPU_MAX_HW_QUEUES", "1")
+    single = SimpleNamespace(tp_dev=object(), _token_chunks=lambda B: 1)
+    assert multi_stream_graph_hazard(cfg, single) is None

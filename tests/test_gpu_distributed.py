@@ -54,6 +54,22 @@ def test_device_ondemand_registration(n):
     assert "0 failures" in r.stdout
 
 
+def test_harness_graph_replay_after_collectives_one_queue():
+    """the bench's old one-process sequence -- collective candidates, bf16,
+    all-to-all, empty_cache, then the harness forwards (token, pooled, 4-block token pipeline)
+    as HIP graphs -- with 8 ranks on the GPU and ONE hardware queue each.  The multi-stream
+    pipeline's graph is what crashed the HIP runtime (profiles/r4_bisect); it is timed eagerly
+    under few queues, every other forward replays its graph."""
+    r = run_ranks(8, py("benchmarks/graph_replay_repro.py", "--prefix", "ar,bf16,a2a,free", "--size-mb", "256",
+                        "--variants", "token:1,row:1,token:4"), timeout=400, env=dict(ENV, GPU_MAX_HW_QUEUES="1"))
+    assert "replay OK" in r.stdout
+    import json
+
+    rec = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    graphs = {x["variant"]: x["hip_graph"] for x in rec["results"]}
+    assert graphs == {"token:1": True, "row:1": True, "token:4": False}, graphs
+
+
 def test_captured_registration_slot_is_pinned():
     """a slot a captured HIP graph uses is pinned -- more registrations than
     CCMPI_REGISTER_SLOTS afterwards do not evict it, and the replay is still exact."""
