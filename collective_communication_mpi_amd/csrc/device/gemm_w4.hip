@@ -534,6 +534,11 @@ constexpr int kRing = 32768;   // one ring slot
 constexpr int kRingHalf = 16384;
 constexpr int kRingLds = 4 * kRing;
 __device__ __forceinline__ int ring_swz(int q) { return (0x78 >> (2 * q)) & 3; }
+// pair-slot ring (PAIR): two 64-KiB slots of one 64-deep K pair each (A half, B half:
+// 256 rows x 128 B), the fast epilogue's slab (4 x 8 KiB) behind them -- 160 KiB
+constexpr int kPair = 65536;
+constexpr int kPairHalf = 32768;
+constexpr int kPairLds = 2 * kPair + 4 * 8192;
 
 // `younger` vector-memory ops (DMA pieces / epilogue stores) may stay in flight past
 // this barrier; every LDS op of the wave has retired
@@ -601,8 +606,16 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t op_rsrc_t(const uint16_t* X, i
 // (profiles/r4_gemm).  2: PS 0 with the odd waves one MFMA later (hipBLASLt runs two
 // copies of its loop, picked by the SIMD id, whose DMA / read slots differ by one MFMA).
 // 3: PS 0 with the DMA pieces' LDS addresses as one M0 chain (dma_chain).
-template <int EPI, int PERSIST, int ABL = 0, int STAMP = 0, int TA = 0, int TB = 0, int PS = 0>
+// PAIR (N layout, non-persistent, no diagnostics): the pair-slot ring.  Each DMA piece
+// reads 8 whole 128-B lines (8 rows x 64 k) instead of 16 half lines: the 16 x 64-B
+// pieces of the 4-slot ring cost 13-16 % against hipBLASLt (profiles/r4_gemm, ABL bit 2
+// ablation).  Two slots of one K pair each (kPair): phase q computes step q-1 and reads
+// step q from slot (q >> 1) & 1; even phase 2p issues the 16 pieces of pair p+1 into the
+// other slot, whose last reader was phase 2p-1; only odd phases end in a barrier (pair
+// p+1 landed everywhere, slot p free).
+template <int EPI, int PERSIST, int ABL = 0, int STAMP = 0, int TA = 0, int TB = 0, int PS = 0, int PAIR = 0>
 __global__ void __launch_bounds__(WNT, 1) k_gemm_w4r(W4Args wa) {
+  static_assert(!PAIR || (!PERSIST && !ABL && !STAMP && !TA && !TB && !PS), "pair-slot ring: N layout only");
   const GemmArgs& g = wa.g;
   extern __shared__ __attribute__((aligned(1024))) unsigned char smem[];
   const int tiles_n = (g.N + WNB - 1) / WNB, tiles_m = (g.M + WM - 1) / WM;
@@ -725,6 +738,31 @@ __global__ void __launch_bounds__(WNT, 1) k_gemm_w4r(W4Args wa) {
     else fa[(grp & 3) * 2 + u] = v;
   };
 
+  // ---- PAIR: operand row r at r * 128 B, its 16-B chunk c (k 8 c .. 8 c + 7 of the pair)
+  // at physical chunk c ^ ((r >> 1) & 7) -- conflict-free for the fragment reads (each
+  // 16-lane ds_read_b128 group: 16 rows, one logical chunk, eight distinct physical ones
+  // per row pair).  Piece i (0..7) of an operand, wave w: rows (4 i + w) * 8 .. +7 at LDS
+  // i * 4 KiB + w * 1 KiB; lane l -> row + (l >> 3), physical chunk l & 7 <- logical
+  // chunk (l & 7) ^ ((w & 1) * 4 + (l >> 4)).
+  const int pch = ((lane & 7) ^ (((wave & 1) * 4 + (lane >> 4)) & 7)) << 4;
+  const int pva = (wave * 8 + (lane >> 3)) * g.lda * 2 + pch, pvb = (wave * 8 + (lane >> 3)) * g.ldb * 2 + pch;
+  const int psa = 32 * g.lda * 2, psb = 32 * g.ldb * 2;  // piece stride: 32 rows
+  auto dma_pair = [&](int p, int i) {  // piece i of pair p: 0..7 A, 8..15 B
+    const bool isa = i < 8;
+    unsigned char* dst = smem + (p & 1) * kPair + (isa ? 0 : kPairHalf) + (i & 7) * 4096 + wave * 1024;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(isa ? ra : rb, (lds_vptr)dst, 16, (isa ? pva : pvb) + p * 128,
+                                             (i & 7) * (isa ? psa : psb), 0, 0);
+  };
+  // fragment of K-step h (0, 1) of a pair: row (l & 15), logical chunk 4 h + (l >> 4)
+  const int prd0 = (lane & 15) * 128 + (((lane >> 4) ^ ((lane & 15) >> 1)) << 4);
+  const int prd1 = (lane & 15) * 128 + (((4 + (lane >> 4)) ^ ((lane & 15) >> 1)) << 4);
+  auto rd_pair = [&](const unsigned char* slot, int ro, int grp, int u, bf16x8 (&fa)[8], bf16x8 (&fb)[8]) {
+    const int r0 = (grp < 4 ? wc : wr) * 128 + (grp & 3) * 32 + u * 16;
+    const bf16x8 v = *reinterpret_cast<const bf16x8*>(slot + (grp < 4 ? kPairHalf : 0) + ro + r0 * 128);
+    if (grp < 4) fb[(grp & 3) * 2 + u] = v;
+    else fa[(grp & 3) * 2 + u] = v;
+  };
+
   floatx4 acc[8][8];
   bf16x8 a0[8], b0[8], a1[8], b1[8];
   // acc[i][j] (A block i, B block j): lane l holds C[16 i + (l & 15)][16 j + 4 (l >> 4) + r]
@@ -825,11 +863,43 @@ __global__ void __launch_bounds__(WNT, 1) k_gemm_w4r(W4Args wa) {
   using Y8 = std::integral_constant<int, 8>;
   using Y0 = std::integral_constant<int, 0>;
 
-  const int ldc = g.ldc;
-  // prologue of the first tile: steps 0..2 in flight
-  for (int s = 0; s < pro; ++s)
+  // PAIR phase q: MFMAs on (pa, pb) = step q-1, reads of step q into (ca, cb); even phases
+  // with DMA also issue the 16 pieces of pair (q >> 1) + 1, odd phases end in the barrier.
+  // Per 8 MFMAs: MFMA | DMA | read | 2 MFMA | DMA | 2 MFMA | read | 3 MFMA
+  auto phase_pair = [&](auto dma_c, auto odd_c, int q, const bf16x8 (&pa)[8], const bf16x8 (&pb)[8],
+                        bf16x8 (&ca)[8], bf16x8 (&cb)[8]) {
+    constexpr bool DMA = decltype(dma_c)::value, ODD = decltype(odd_c)::value;
+    const unsigned char* slot = smem + ((q >> 1) & 1) * kPair;
+    const int ro = ODD ? prd1 : prd0;
+    const int np = (q >> 1) + 1;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) dma(s, i);
+    for (int i = 0; i < 8; ++i) {
+      auto mm = [&](int j0, int j1) {
+#pragma unroll
+        for (int j = j0; j < j1; ++j) mfma(i, j, pa[i], pb[j]);
+        __builtin_amdgcn_sched_barrier(0);
+      };
+      mm(0, 1);
+      if constexpr (DMA) dma_pair(np, 2 * i);
+      rd_pair(slot, ro, i, 0, ca, cb);
+      __builtin_amdgcn_sched_barrier(0);
+      mm(1, 3);
+      if constexpr (DMA) dma_pair(np, 2 * i + 1);
+      __builtin_amdgcn_sched_barrier(0);
+      mm(3, 5);
+      rd_pair(slot, ro, i, 1, ca, cb);
+      __builtin_amdgcn_sched_barrier(0);
+      mm(5, 8);
+    }
+    if constexpr (ODD) ring_wait_barrier_c<0>();
+  };
+
+  const int ldc = g.ldc;
+  // prologue of the first tile: steps 0..2 in flight (PAIR: pairs 0 and 1, in the tile)
+  if constexpr (!PAIR)
+    for (int s = 0; s < pro; ++s)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) dma(s, i);
   int younger = 8 * (pro - 1);  // DMA pieces issued after step 0's
   for (;;) {
     const int bm = tm * WM, bn = tn * WNB;
@@ -837,6 +907,40 @@ __global__ void __launch_bounds__(WNT, 1) k_gemm_w4r(W4Args wa) {
     for (int i = 0; i < 8; ++i)
 #pragma unroll
       for (int j = 0; j < 8; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+    const int next = lt + (int)gridDim.x;
+    bool more = false;
+    int ntm = 0, ntn = 0;
+    if constexpr (PAIR) {
+      const int npair = nst >> 1;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) dma_pair(0, i);
+      if (npair > 1) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) dma_pair(1, i);
+        ring_wait_barrier_c<16>();
+      } else {
+        ring_wait_barrier_c<0>();
+      }
+      // "phase 0": step 0's fragments; phase 1 ends with pair 1 landed
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        rd_pair(smem, prd0, i, 0, a0, b0);
+        rd_pair(smem, prd0, i, 1, a0, b0);
+      }
+      phase_pair(F{}, T{}, 1, a0, b0, a1, b1);
+      for (int p = 1; p + 1 < npair; ++p) {
+        phase_pair(T{}, F{}, 2 * p, a1, b1, a0, b0);
+        phase_pair(F{}, T{}, 2 * p + 1, a0, b0, a1, b1);
+      }
+      if (npair > 1) {
+        phase_pair(F{}, F{}, nst - 2, a1, b1, a0, b0);
+        phase_pair(F{}, T{}, nst - 1, a0, b0, a1, b1);
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) mfma(i, j, a1[i], b1[j]);
+    } else {
     // step 0 landed everywhere (and every wave is done with the previous epilogue's slab);
     // "phase 0": step 0's fragments read, step 3 into slot 3, step 1 landed
     ring_wait_barrier(younger);
@@ -867,9 +971,7 @@ __global__ void __launch_bounds__(WNT, 1) k_gemm_w4r(W4Args wa) {
     // persistent, fast epilogue: every wave is past its last fragment read (the last
     // phase's barrier), so slots 0..2 are free -- the next tile's first three steps load
     // into them under the last MFMAs and the epilogue (which uses slot 3 only)
-    const int next = lt + (int)gridDim.x;
-    const bool more = PERSIST && (EPI == 1 || EPI == 2) && next < ntiles;
-    int ntm = 0, ntn = 0;
+    more = PERSIST && (EPI == 1 || EPI == 2) && next < ntiles;
     if (more) {
       tile_coords(next, tiles_m, tiles_n, wa.group_m, ntm, ntn);
       ops_for(ntm, ntn);
@@ -881,12 +983,14 @@ __global__ void __launch_bounds__(WNT, 1) k_gemm_w4r(W4Args wa) {
     for (int i = 0; i < 8; ++i)
 #pragma unroll
       for (int j = 0; j < 8; ++j) mfma(i, j, a1r[i], b1[j]);
+    }
     if (STAMP) t_epi = __builtin_amdgcn_s_memtime();
 
     if constexpr (EPI == 1 || EPI == 2) {
       // ---- fast epilogue: per 32-row pass, bf16 pairs -> slab (slot 3, 8 KiB per wave,
       // 16-B chunk c of row r at c ^ (r & 15)) -> 16-B row vectors -> buffer stores
-      unsigned char* slab = smem + 3 * kRing + wave * 8192;
+      // (PAIR: the slab behind the two pair slots)
+      unsigned char* slab = smem + (PAIR ? 2 * kPair : 3 * kRing) + wave * 8192;
       const int grp = lane >> 4, lr = lane & 15;
       const float al = g.alpha;
       const int ccol = bn + wc * 128 + lr * 8;
@@ -1066,6 +1170,7 @@ static void w4_attr(const void* f) {
 // or accumulation and C rows are 16-B vectors; persistent grid (g_w4_sched bit 0) then.
 // Diagnostics: sched bits 5-6 ablations, bit 9 s_memtime stamps (g_w4_dbg).
 static void w4r_attr(const void* f) { (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kRingLds); }
+static void w4p_attr(const void* f) { (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kPairLds); }
 
 bool gemm_w4r_fast(const GemmArgs& g) {
   return g.out_bf16 && !g.accumulate && g.act == 0 && g.bias_kind == 0 && g.splitk == 1 && g.N % 8 == 0 && g.ldc % 8 == 0 &&
@@ -1117,6 +1222,9 @@ void launch_gemm_ring(const GemmArgs& g, int ta, int tb, hipStream_t stream, uin
     w4r_attr(reinterpret_cast<const void*>(k_gemm_w4r<1, 0, 0, 0, 0, 0, 3>));
     w4r_attr(reinterpret_cast<const void*>(k_gemm_w4r<1, 0, 4>));
     w4r_attr(reinterpret_cast<const void*>(k_gemm_w4r<2, 0, 0, 0, 0, 0, 3>));
+    w4p_attr(reinterpret_cast<const void*>(k_gemm_w4r<0, 0, 0, 0, 0, 0, 0, 1>));
+    w4p_attr(reinterpret_cast<const void*>(k_gemm_w4r<1, 0, 0, 0, 0, 0, 0, 1>));
+    w4p_attr(reinterpret_cast<const void*>(k_gemm_w4r<2, 0, 0, 0, 0, 0, 0, 1>));
     return true;
   }();
   (void)attr;
@@ -1125,7 +1233,8 @@ void launch_gemm_ring(const GemmArgs& g, int ta, int tb, hipStream_t stream, uin
   const bool fast = gemm_w4r_fast(g);
   if (glu) {  // SwiGLU epilogue (callers check gemm_w4r_fast and the glu layout first)
     if (!fast || ta || tb) throw std::invalid_argument("gemm ring: the SwiGLU epilogue needs the fast NT form");
-    if (sched & 4096) hipLaunchKernelGGL((k_gemm_w4r<2, 0, 0, 0, 0, 0, 3>), dim3(ntiles), dim3(WNT), kRingLds, stream, a);
+    if (sched & 16384) hipLaunchKernelGGL((k_gemm_w4r<2, 0, 0, 0, 0, 0, 0, 1>), dim3(ntiles), dim3(WNT), kPairLds, stream, a);
+    else if (sched & 4096) hipLaunchKernelGGL((k_gemm_w4r<2, 0, 0, 0, 0, 0, 3>), dim3(ntiles), dim3(WNT), kRingLds, stream, a);
     else if (sched & 1024) hipLaunchKernelGGL((k_gemm_w4r<2, 0, 0, 0, 0, 0, 1>), dim3(ntiles), dim3(WNT), kRingLds, stream, a);
     else hipLaunchKernelGGL((k_gemm_w4r<2, 0>), dim3(ntiles), dim3(WNT), kRingLds, stream, a);
     return;
@@ -1145,7 +1254,11 @@ void launch_gemm_ring(const GemmArgs& g, int ta, int tb, hipStream_t stream, uin
     }
     return;
   }
-  if (!fast) {
+  if (sched & 16384) {
+    // pair-slot ring: whole-line DMA pieces, 64-deep slots (non-persistent)
+    if (fast) hipLaunchKernelGGL((k_gemm_w4r<1, 0, 0, 0, 0, 0, 0, 1>), dim3(ntiles), dim3(WNT), kPairLds, stream, a);
+    else hipLaunchKernelGGL((k_gemm_w4r<0, 0, 0, 0, 0, 0, 0, 1>), dim3(ntiles), dim3(WNT), kPairLds, stream, a);
+  } else if (!fast) {
     hipLaunchKernelGGL((k_gemm_w4r<0, 0>), dim3(grid), dim3(WNT), kRingLds, stream, a);
   } else if (sched & 512) {
     if (sched & 1024) hipLaunchKernelGGL((k_gemm_w4r<1, 0, 0, 1, 0, 0, 1>), dim3(grid), dim3(WNT), kRingLds, stream, a);

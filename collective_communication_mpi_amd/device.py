@@ -258,6 +258,14 @@ class DeviceGroup:
         # another rank's GEMMs never became co-resident (timeouts, profiles/r2_overlap);
         # 64 CTAs keep both the GEMMs and the collective moving
         self.overlap_blocks = min(self.max_blocks, _env_int("CCMPI_OVERLAP_BLOCKS", 64))
+        # Upper bound of that budget.  With ranks sharing a GPU, one rank's spinning grid
+        # must leave CUs free: a bucket all-reduce of 256 CTAs (one per CU) beside the
+        # other rank's backward blocked every GEMM workgroup of that rank, so the peer
+        # never arrived -- 60 s device timeout, then both processes' queues were torn down
+        # (hipErrorIllegalAddress, profiles/r4_dp).  Half the CUs at most; no bound when
+        # every rank owns its GPU (its peers progress on their own devices).
+        self.overlap_cap = max(1, _cu_count(self.device) // 2) if self.shared_device else self.max_blocks
+        self.overlap_blocks = min(self.overlap_blocks, self.overlap_cap)
         if scratch_bytes is None:
             scratch_bytes = _env_int("CCMPI_SCRATCH_MB", 64 if self.shared_device else 512) << 20
         self._keep: List = []   # registered segments (scratch, heap arenas) live as long as the group
@@ -1196,6 +1204,15 @@ class DeviceGroup:
     def barrier(self) -> None:
         self.torch.cuda.synchronize(self.device)
         self.host.Barrier()
+
+
+def _cu_count(device) -> int:
+    try:
+        import torch
+
+        return int(torch.cuda.get_device_properties(device).multi_processor_count) or 256
+    except Exception:
+        return 256
 
 
 def _gcd(a: int, b: int) -> int:

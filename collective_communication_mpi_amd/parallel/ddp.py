@@ -224,8 +224,13 @@ class DistributedDataParallel(torch.nn.Module):
         ev.record(torch.cuda.current_stream(self.device))
         self.stream.wait_event(ev)
         with torch.cuda.stream(self.stream):  # beside the backward: the overlap CTA budget
-            self.dev.allreduce(b.buf, b.buf, "SUM", self.algo, max_blocks=self.max_blocks or self.dev.overlap_blocks,
+            self.dev.allreduce(b.buf, b.buf, "SUM", self.algo, max_blocks=self._blocks(),
                                symmetric=True)
+
+    def _blocks(self) -> int:
+        """CTA budget of a bucket all-reduce: ``max_blocks`` (default: the group's
+        ``overlap_blocks``), never above the group's ``overlap_cap``."""
+        return min(self.max_blocks or self.dev.overlap_blocks, getattr(self.dev, "overlap_cap", 1 << 30))
 
     def finish(self) -> None:
         """Complete the gradient synchronisation (after backward, before the step)."""
@@ -280,7 +285,7 @@ class DistributedDataParallel(torch.nn.Module):
         if self.dev is None or self.p == 1:
             return
         for b in self.buckets:
-            self.dev.allreduce(b.buf, b.buf, "SUM", self.algo, max_blocks=self.max_blocks or self.dev.overlap_blocks,
+            self.dev.allreduce(b.buf, b.buf, "SUM", self.algo, max_blocks=self._blocks(),
                                symmetric=True)
 
     @property

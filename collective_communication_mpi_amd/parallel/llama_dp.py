@@ -192,7 +192,11 @@ def measure_ddp_overlap(comm, layers: int = 32, tokens: int = 4096, seq: int = 2
     t_comm = timed(ddp.allreduce_all) if p > 1 else 0.0
     say(f"comm-only {t_comm * 1e3:.1f} ms")
     sweep = {}
-    for mb in (blocks_sweep if p > 1 else [0]):
+    # budgets above the group's overlap cap would only be clamped to it (on a shared GPU:
+    # half the CUs, the deadlock bound -- DeviceComm.overlap_cap)
+    cap = getattr(dev, "overlap_cap", None)
+    budgets = sorted({min(mb, cap) if cap else mb for mb in blocks_sweep}) if p > 1 else [0]
+    for mb in budgets:
         ddp.max_blocks = mb or None
         sweep[mb] = timed(step)
         say(f"overlapped, {mb} CTAs per bucket all-reduce: {sweep[mb] * 1e3:.1f} ms")

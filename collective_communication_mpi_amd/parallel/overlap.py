@@ -90,7 +90,7 @@ def dp_grad_overlap(comm, layers: int = 32, tokens: int = 4096, iters: int = 3, 
         sel = [((ids >= r0) & (ids < r1)).nonzero().flatten() for r0, r1 in vchunks]
         emb_idx = [(ids[s_] - r0, dx0[s_]) for s_, (r0, _) in zip(sel, vchunks)]
     side = torch.cuda.Stream(device=dev.device, priority=priority)
-    mb = max_blocks or dev.overlap_blocks
+    mb = min(max_blocks or dev.overlap_blocks, getattr(dev, "overlap_cap", 1 << 30))
     events = [torch.cuda.Event() for _ in range(layers + 2)]
     # bucket length in elements, a multiple of 8 (16-B aligned bf16 buckets)
     step = None if bucket_mb <= 0 else max(8, ((bucket_mb << 20) // 2) // 8 * 8)

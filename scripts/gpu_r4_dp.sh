@@ -11,7 +11,7 @@ export CCMPI_DEVICE_TIMEOUT_S=60 TMPDIR=/tmp
 L="python -m collective_communication_mpi_amd.launch -n 2 --timeout 500"
 timeout -k 10 300 $L python benchmarks/llama_ddp.py --verbose --layers 2 --blocks 64 > $OUT/l2.json 2>> $OUT/progress.log || { echo "l2 rc=$?"; tail -20 $OUT/progress.log; exit 1; }
 cat $OUT/l2.json
-timeout -k 10 560 $L python benchmarks/llama_ddp.py --verbose > $OUT/full.json 2>> $OUT/progress.log || { echo "full rc=$?"; tail -20 $OUT/progress.log; exit 1; }
+timeout -k 10 560 $L python benchmarks/llama_ddp.py --verbose --blocks 32,64,128 > $OUT/full.json 2>> $OUT/progress.log || { echo "full rc=$?"; tail -20 $OUT/progress.log; exit 1; }
 cat $OUT/full.json
 timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $OUT/trace -o run -- \
   python -m collective_communication_mpi_amd.launch -n 2 --timeout 280 python benchmarks/llama_ddp.py --layers 4 --blocks 64 \
