@@ -55,7 +55,7 @@ for shp in args.shapes.split(","):
             res[f"ring{s}"].append(time_ms(lambda: gemm_nt(a, b, out=c), args.iters))
             errs[f"ring{s}"] = float(((c.float() - ref).abs().max() / ref.abs().max()).item())
         res["hipblaslt"].append(time_ms(lambda: torch.matmul(a, b.T, out=c), args.iters))
-    D.gemm_set_ring_sched(8)
+    D.gemm_set_ring_sched(8 | 16384)
     fl = 2 * M * N * K
     out = {"shape": shp}
     for k, v in res.items():

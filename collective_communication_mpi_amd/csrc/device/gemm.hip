@@ -936,9 +936,11 @@ void gemm_nt(uint64_t A, uint64_t B, uint64_t C, uint64_t bias, int M, int N, in
   // auto: large bf16-out GEMMs on the four-wave LDS-ring kernel (gemm_w4.hip; measured
   // against the 256x256 ping-pong kernel in profiles/r3_gemm)
   // (long K over at most one tile per CU stays on the 256x256 ping-pong kernel: 4096^2 x
-  // 28672 measured 1291-1368 TF/s there against 1224-1252 on the ring)
+  // 28672 measured 1291-1368 TF/s there against 1224-1252 on the ring; ring sched bit 15
+  // sends it to the ring too)
   if (g_kernel == 0 && splitk == 1 && g_ring_min_macs > 0 && (long long)M * N * K >= g_ring_min_macs &&
-      M >= 1024 && N >= 1024 && !(K > 16384 && gemm_w4_tiles(M, N) <= 256) && gemm_w4_ok(g) && gemm_w4r_fast(g)) {
+      M >= 1024 && N >= 1024 && ((g_ring_sched & 32768) || !(K > 16384 && gemm_w4_tiles(M, N) <= 256)) &&
+      gemm_w4_ok(g) && gemm_w4r_fast(g)) {
     launch_gemm_nt_w4r(g, reinterpret_cast<hipStream_t>(stream));
     CCMPI_HIP_CHECK(hipGetLastError());
     return;
@@ -1109,6 +1111,7 @@ void register_gemm_ops(pybind11::module_& m) {
         "four-wave ring STAMP diagnostic: device buffer of 4 uint64 per wave (benchmarks only)");
   m.def("gemm_set_ring_min", [](long long v) { g_ring_min_macs = v; },
         "gemm_nt auto: LDS-ring kernel from this many multiply-adds up (0 = never)");
+  m.def("gemm_ring_launches", [] { return g_ring_launches; }, "LDS-ring GEMM launches so far (this process)");
   m.def("gemm_set_ring_sched", [](int v) { g_ring_sched = v; },
         "auto-dispatched LDS-ring kernel variant: bit 0 persistent, bit 10 reads-then-DMA phase (PS 1)");
   m.def("gemm_set_w4_group_m", [](int v) { g_w4_group_m = v > 0 ? v : 8; }, "four-wave kernel group-M rows");

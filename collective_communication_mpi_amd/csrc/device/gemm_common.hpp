@@ -208,6 +208,7 @@ void launch_gemm_tn_256(const GemmArgs& g, hipStream_t stream);
 // 256 x 256 four-wave kernel (gemm_w4.hip): 128 x 128 per wave, K % 64 == 0, no split-K
 bool gemm_w4_ok(const GemmArgs& g);
 extern int g_ring_sched;  // auto-dispatched LDS-ring kernel variant (gemm_w4.hip launch_gemm_ring)
+extern long long g_ring_launches;  // launch_gemm_ring calls (tests: the ring path really ran)
 extern int g_w4_sched;    // four-wave kernel variant: bit 0 persistent grid, bit 1 MFMA-first group order
 extern unsigned long long* g_w4_dbg;  // four-wave ring STAMP diagnostic output (benchmarks)
 extern int g_w4_group_m;  // four-wave kernel: tile rows per group-M block

@@ -879,17 +879,40 @@ __global__ void __launch_bounds__(WNT, 1) k_gemm_w4r(W4Args wa) {
         for (int j = j0; j < j1; ++j) mfma(i, j, pa[i], pb[j]);
         __builtin_amdgcn_sched_barrier(0);
       };
-      mm(0, 1);
-      if constexpr (DMA) dma_pair(np, 2 * i);
-      rd_pair(slot, ro, i, 0, ca, cb);
-      __builtin_amdgcn_sched_barrier(0);
-      mm(1, 3);
-      if constexpr (DMA) dma_pair(np, 2 * i + 1);
-      __builtin_amdgcn_sched_barrier(0);
-      mm(3, 5);
-      rd_pair(slot, ro, i, 1, ca, cb);
-      __builtin_amdgcn_sched_barrier(0);
-      mm(5, 8);
+      if constexpr (PAIR == 2) {
+        // front-loaded: the 16 pieces over the first 32 MFMAs (4 per 8), half a phase
+        // more of HBM latency before the odd phase's barrier needs them
+        const bool d = DMA && i < 4;
+        mm(0, 1);
+        if (d) dma_pair(np, 4 * i);
+        rd_pair(slot, ro, i, 0, ca, cb);
+        __builtin_amdgcn_sched_barrier(0);
+        mm(1, 3);
+        if (d) dma_pair(np, 4 * i + 1);
+        __builtin_amdgcn_sched_barrier(0);
+        mm(3, 4);
+        if (d) dma_pair(np, 4 * i + 2);
+        __builtin_amdgcn_sched_barrier(0);
+        mm(4, 5);
+        rd_pair(slot, ro, i, 1, ca, cb);
+        __builtin_amdgcn_sched_barrier(0);
+        mm(5, 7);
+        if (d) dma_pair(np, 4 * i + 3);
+        __builtin_amdgcn_sched_barrier(0);
+        mm(7, 8);
+      } else {
+        mm(0, 1);
+        if constexpr (DMA) dma_pair(np, 2 * i);
+        rd_pair(slot, ro, i, 0, ca, cb);
+        __builtin_amdgcn_sched_barrier(0);
+        mm(1, 3);
+        if constexpr (DMA) dma_pair(np, 2 * i + 1);
+        __builtin_amdgcn_sched_barrier(0);
+        mm(3, 5);
+        rd_pair(slot, ro, i, 1, ca, cb);
+        __builtin_amdgcn_sched_barrier(0);
+        mm(5, 8);
+      }
     }
     if constexpr (ODD) ring_wait_barrier_c<0>();
   };
@@ -1139,7 +1162,10 @@ int g_w4_sched = 1;   // bit 0: persistent grid, bit 1: MFMA-first order inside 
                       // bit 3: LDS-ring kernel (k_gemm_w4r), bits 5-6 / 9: its ablations / stamps
 int g_w4_group_m = 8;
 unsigned long long* g_w4_dbg = nullptr;
-int g_ring_sched = 8;  // auto dispatch: non-persistent ring (profiles/r3_gemm)
+long long g_ring_launches = 0;
+// auto dispatch: the pair-slot ring (0.93-0.95x hipBLASLt on the Llama MLP shapes against
+// 0.86-0.89x for the 4-slot ring, profiles/r4_pair); CCMPI_RING_SCHED overrides (A/B runs)
+int g_ring_sched = std::getenv("CCMPI_RING_SCHED") ? std::atoi(std::getenv("CCMPI_RING_SCHED")) : (8 | 16384);
 long long g_ring_min_macs = std::getenv("CCMPI_RING_MIN_MACS") ? std::atoll(std::getenv("CCMPI_RING_MIN_MACS")) : (1ll << 33);
 
 bool gemm_w4_ok(const GemmArgs& g) {
@@ -1191,6 +1217,7 @@ bool gemm_ring_ok(const GemmArgs& g, int ta, int tb) {
 void launch_gemm_ring(const GemmArgs& g, int ta, int tb, hipStream_t stream, uint16_t* glu, int ldglu) {
   // explicit ring schedule (gemm_set_kernel(5) + sched bit 3) or the auto defaults
   const int sched = (g_w4_sched & 8) ? g_w4_sched : g_ring_sched;
+  ++g_ring_launches;
   static int cus = [] {
     int dev = 0, n = 0;
     (void)hipGetDevice(&dev);
@@ -1225,6 +1252,9 @@ void launch_gemm_ring(const GemmArgs& g, int ta, int tb, hipStream_t stream, uin
     w4p_attr(reinterpret_cast<const void*>(k_gemm_w4r<0, 0, 0, 0, 0, 0, 0, 1>));
     w4p_attr(reinterpret_cast<const void*>(k_gemm_w4r<1, 0, 0, 0, 0, 0, 0, 1>));
     w4p_attr(reinterpret_cast<const void*>(k_gemm_w4r<2, 0, 0, 0, 0, 0, 0, 1>));
+    w4p_attr(reinterpret_cast<const void*>(k_gemm_w4r<0, 0, 0, 0, 0, 0, 0, 2>));
+    w4p_attr(reinterpret_cast<const void*>(k_gemm_w4r<1, 0, 0, 0, 0, 0, 0, 2>));
+    w4p_attr(reinterpret_cast<const void*>(k_gemm_w4r<2, 0, 0, 0, 0, 0, 0, 2>));
     return true;
   }();
   (void)attr;
@@ -1233,7 +1263,8 @@ void launch_gemm_ring(const GemmArgs& g, int ta, int tb, hipStream_t stream, uin
   const bool fast = gemm_w4r_fast(g);
   if (glu) {  // SwiGLU epilogue (callers check gemm_w4r_fast and the glu layout first)
     if (!fast || ta || tb) throw std::invalid_argument("gemm ring: the SwiGLU epilogue needs the fast NT form");
-    if (sched & 16384) hipLaunchKernelGGL((k_gemm_w4r<2, 0, 0, 0, 0, 0, 0, 1>), dim3(ntiles), dim3(WNT), kPairLds, stream, a);
+    if (sched & 65536) hipLaunchKernelGGL((k_gemm_w4r<2, 0, 0, 0, 0, 0, 0, 2>), dim3(ntiles), dim3(WNT), kPairLds, stream, a);
+    else if (sched & 16384) hipLaunchKernelGGL((k_gemm_w4r<2, 0, 0, 0, 0, 0, 0, 1>), dim3(ntiles), dim3(WNT), kPairLds, stream, a);
     else if (sched & 4096) hipLaunchKernelGGL((k_gemm_w4r<2, 0, 0, 0, 0, 0, 3>), dim3(ntiles), dim3(WNT), kRingLds, stream, a);
     else if (sched & 1024) hipLaunchKernelGGL((k_gemm_w4r<2, 0, 0, 0, 0, 0, 1>), dim3(ntiles), dim3(WNT), kRingLds, stream, a);
     else hipLaunchKernelGGL((k_gemm_w4r<2, 0>), dim3(ntiles), dim3(WNT), kRingLds, stream, a);
@@ -1254,7 +1285,11 @@ void launch_gemm_ring(const GemmArgs& g, int ta, int tb, hipStream_t stream, uin
     }
     return;
   }
-  if (sched & 16384) {
+  if (sched & 65536) {
+    // pair-slot ring, front-loaded DMA
+    if (fast) hipLaunchKernelGGL((k_gemm_w4r<1, 0, 0, 0, 0, 0, 0, 2>), dim3(ntiles), dim3(WNT), kPairLds, stream, a);
+    else hipLaunchKernelGGL((k_gemm_w4r<0, 0, 0, 0, 0, 0, 0, 2>), dim3(ntiles), dim3(WNT), kPairLds, stream, a);
+  } else if (sched & 16384) {
     // pair-slot ring: whole-line DMA pieces, 64-deep slots (non-persistent)
     if (fast) hipLaunchKernelGGL((k_gemm_w4r<1, 0, 0, 0, 0, 0, 0, 1>), dim3(ntiles), dim3(WNT), kPairLds, stream, a);
     else hipLaunchKernelGGL((k_gemm_w4r<0, 0, 0, 0, 0, 0, 0, 1>), dim3(ntiles), dim3(WNT), kPairLds, stream, a);

@@ -239,6 +239,7 @@ class DeviceGroup:
         keys = host_comm.allgather(key)
         self.ranks_per_device = keys.count(key)
         self.shared_device = self.ranks_per_device > 1
+        self.shared_ring = self.shared_device and os.environ.get("CCMPI_SHARED_RING") == "1"
         if self.shared_device:
             global SHARED_GPU_IN_PROCESS
             SHARED_GPU_IN_PROCESS = True
@@ -246,12 +247,18 @@ class DeviceGroup:
             # wave); next to another rank's spinning collective CTAs (one per CU) none of
             # its workgroups can start, and the two ranks wait on each other (TP = 2 MLP
             # on one GPU timed out, profiles/r3_tp2).  A process whose GPU is shared uses
-            # the smaller-footprint kernels instead.
-            self.D.gemm_set_ring_min(0)
+            # the smaller-footprint kernels instead -- unless CCMPI_SHARED_RING=1: then
+            # every collective of every sharing rank stays within half the CUs in total
+            # (below), so the ring GEMM always finds free CUs (the kernels an 8-GPU TP run
+            # uses, exercised beside another rank's collectives on one GPU)
+            if not self.shared_ring:
+                self.D.gemm_set_ring_min(0)
         self._async_done = None  # (stream, event) of the last start()ed collective, until ordered
         self._inflight: List = []  # (done event, tensors) of start()ed collectives not yet known complete
         default_blocks = max(1, 512 // self.ranks_per_device)
         self.max_blocks = _env_int("CCMPI_MAX_BLOCKS", default_blocks)
+        if self.shared_device and self.shared_ring:
+            self.max_blocks = min(self.max_blocks, self._shared_cap())
         # CTA budget of collectives that run NEXT TO compute (DP gradient buckets, TP
         # pipelines on side streams): spinning collective CTAs hold CU slots the GEMMs
         # could use, and with ranks sharing a GPU a 256-CTA bucket all-reduce beside
@@ -586,8 +593,13 @@ class DeviceGroup:
         is capped at 512 (2 per CU)."""
         mb = max_blocks or self.max_blocks
         if self.shared_device:
-            mb = min(mb, max(1, 512 // self.ranks_per_device))
+            mb = min(mb, self._shared_cap() if self.shared_ring else max(1, 512 // self.ranks_per_device))
         return mb
+
+    def _shared_cap(self) -> int:
+        """CCMPI_SHARED_RING: per-rank CTA cap keeping all sharing ranks' collectives on
+        at most half the CUs."""
+        return max(1, (_cu_count(self.device) // 2) // self.ranks_per_device)
 
     def _symm(self, *ts) -> bool:
         return all(self.is_symmetric(t) and t.data_ptr() % 16 == 0 for t in ts)

@@ -180,9 +180,12 @@ def _gpu_shared(comm) -> bool:
     then the whole-CU LDS-ring GEMM must not run, since its workgroups cannot start
     beside a peer's spinning collective CTAs.  Measured by every device group (PCI bus
     ids gathered over its ranks); a size-1 group (e.g. the TP group of a pure-DP run)
-    asks whether ANY group of this process found its GPU shared."""
+    asks whether ANY group of this process found its GPU shared.  CCMPI_SHARED_RING=1
+    keeps the ring (the device groups then hold every collective to half the CUs)."""
     from .. import device as _device
 
+    if os.environ.get("CCMPI_SHARED_RING") == "1":
+        return False
     if comm is None or _size_rank(comm)[0] == 1:
         return _device.SHARED_GPU_IN_PROCESS
     return bool(device_group_for(comm).shared_device) or _device.SHARED_GPU_IN_PROCESS

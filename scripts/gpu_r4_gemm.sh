@@ -13,7 +13,7 @@ rc=$?; echo "ps_ab rc=$rc"; cat $OUT/ps_ab.jsonl; [ $rc -ne 0 ] && { tail -20 $O
 read M N K <<< "$(echo ${SHAPE:-4096x28672x4096} | tr x ' ')"
 P1="SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE"
 P2="SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_LDS SQ_INSTS_VMEM SQ_INSTS_VALU_MFMA_MOPS_BF16 SQ_INSTS_SALU SQ_ACTIVE_INST_VALU"
-for v in "-1:0" "0:8" "0:1032"; do
+for v in ${PMC_VARIANTS:-"-1:0" "0:8" "0:1032"}; do
   mode=${v%%:*}; rs=${v##*:}; tag=m${mode}_s${rs}
   for pass in P1 P2; do
     CCMPI_RING_SCHED=$rs timeout -s KILL 90 rocprofv3 --pmc ${!pass} --output-format csv -d $OUT/pmc_${tag}_$pass -o out -- \
@@ -21,5 +21,7 @@ for v in "-1:0" "0:8" "0:1032"; do
     echo "pmc $tag $pass ok"
   done
 done
-python3 scripts/pmc_table.py $OUT/pmc_m-1_s0_P1 $OUT/pmc_m-1_s0_P2 $OUT/pmc_m0_s8_P1 $OUT/pmc_m0_s8_P2 $OUT/pmc_m0_s1032_P1 $OUT/pmc_m0_s1032_P2 > $OUT/pmc_table.md 2>&1
+dirs=""
+for v in ${PMC_VARIANTS:-"-1:0" "0:8" "0:1032"}; do dirs="$dirs $OUT/pmc_m${v%%:*}_s${v##*:}_P1 $OUT/pmc_m${v%%:*}_s${v##*:}_P2"; done
+python3 scripts/pmc_table.py $dirs > $OUT/pmc_table.md 2>&1
 cat $OUT/pmc_table.md

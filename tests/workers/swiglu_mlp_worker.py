@@ -19,6 +19,9 @@ from collective_communication_mpi_amd.parallel.tensor_parallel import ParallelSw
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--device", default="cpu")
+ap.add_argument("--big", action="store_true",
+                help="shapes that take the LDS-ring GEMM and its SwiGLU epilogue (with CCMPI_SHARED_RING=1 "
+                     "and CCMPI_RING_MIN_MACS=1: beside the other ranks' collectives on one GPU)")
 args = ap.parse_args()
 
 comm = Communicator(MPI.COMM_WORLD)
@@ -31,7 +34,11 @@ if args.device == "cuda":
 else:
     dev, dt, tol = torch.device("cpu"), torch.float32, 1e-4
 
-D, F, T = 128, 64 * p, 48
+D, F, T = (1024, 512 * p, 1024) if args.big else (128, 64 * p, 48)
+if args.big and args.device == "cuda":
+    from collective_communication_mpi_amd import _native  # noqa: E402
+
+    ring0 = _native.device().gemm_ring_launches()
 mlp = ParallelSwiGLUMLP(D, F, comm, device=dev, dtype=dt, seed=11)
 gen = torch.Generator().manual_seed(3)
 x0 = torch.randn(T, D, generator=gen)
@@ -71,7 +78,10 @@ gd = torch.cat(hc.allgather(mlp.down.weight.grad.detach().float().cpu()), dim=1)
 if rel(gd, wd.grad) > tol:
     fails.append(f"d W_down rel err {rel(gd, wd.grad)}")
 
-if args.device == "cuda" and p > 1:
+if args.big and args.device == "cuda" and _native.device().gemm_ring_launches() == ring0:
+    fails.append("--big: no LDS-ring GEMM launched (the path under test did not run)")
+
+if args.device == "cuda" and p > 1 and not args.big:
     # every row-parallel mode through the whole block (forward + backward), its path
     # really taken, and a steady-state step with no host call from the device plane
     from collective_communication_mpi_amd.parallel import tensor_parallel as tp  # noqa: E402
