@@ -806,6 +806,39 @@ __global__ void __launch_bounds__(256) k_transpose16(const uint16_t* __restrict_
   }
 }
 
+// The same with 16-B accesses and no LDS: lane l of wave w takes an 8-row x 16-column
+// block (rows r0 + 8 l .., columns c0 + 16 w ..; 8 x 2 row loads of 16 B), transposes its
+// two 8 x 8 halves in registers and writes 16 destination rows of 16 B.  A workgroup covers
+// 512 x 64: each source row's 128-B line is read whole by its four waves, every store
+// instruction writes 1 KiB of consecutive bytes.  R, C, strides % 8 == 0, 16-B aligned.
+__global__ void __launch_bounds__(256) k_transpose16_v(const uint16_t* __restrict__ src, uint16_t* __restrict__ dst,
+                                                       int R, int C, int lds, int ldd) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r = blockIdx.y * 512 + 8 * lane, c = blockIdx.x * 64 + 16 * wave;
+  if (r >= R) return;
+#pragma unroll
+  for (int b = 0; b < 2; ++b) {
+    const int cb = c + 8 * b;
+    if (cb >= C) break;
+    uint4 q[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) q[i] = *reinterpret_cast<const uint4*>(src + (size_t)(r + i) * lds + cb);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      uint32_t o[4];
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        const uint4& x = q[2 * m];
+        const uint4& y = q[2 * m + 1];
+        const uint32_t xw = (j >> 1) == 0 ? x.x : (j >> 1) == 1 ? x.y : (j >> 1) == 2 ? x.z : x.w;
+        const uint32_t yw = (j >> 1) == 0 ? y.x : (j >> 1) == 1 ? y.y : (j >> 1) == 2 ? y.z : y.w;
+        o[m] = (j & 1) ? ((xw >> 16) | (yw & 0xffff0000u)) : ((xw & 0xffffu) | (yw << 16));
+      }
+      *reinterpret_cast<uint4*>(dst + (size_t)(cb + j) * ldd + r) = uint4{o[0], o[1], o[2], o[3]};
+    }
+  }
+}
+
 // Sum of the split-K workspace slices into C ([rows][cols] fp32, row stride ldc),
 // 4 columns per thread: C (+)= sum_s ws[s].  Columns >= csplit (a multiple of 4)
 // go to a second destination instead, C2[r][c - csplit] = sum (overwritten):
@@ -1073,6 +1106,13 @@ void gemm_tn(uint64_t A, uint64_t B, uint64_t C, int M, int N1, int N2, int lda,
 
 void transpose16(uint64_t src, uint64_t dst, int R, int C, int lds, int ldd, uint64_t stream) {
   if (R <= 0 || C <= 0) return;
+  if (R % 8 == 0 && C % 8 == 0 && lds % 8 == 0 && ldd % 8 == 0 && src % 16 == 0 && dst % 16 == 0) {
+    dim3 grid((C + 63) / 64, (R + 511) / 512);
+    hipLaunchKernelGGL(k_transpose16_v, grid, dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+                       reinterpret_cast<const uint16_t*>(src), reinterpret_cast<uint16_t*>(dst), R, C, lds, ldd);
+    CCMPI_HIP_CHECK(hipGetLastError());
+    return;
+  }
   dim3 grid((C + 63) / 64, (R + 63) / 64);
   hipLaunchKernelGGL(k_transpose16, grid, dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
                      reinterpret_cast<const uint16_t*>(src), reinterpret_cast<uint16_t*>(dst), R, C, lds, ldd);

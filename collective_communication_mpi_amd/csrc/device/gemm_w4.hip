@@ -615,7 +615,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t op_rsrc_t(const uint16_t* X, i
 // p+1 landed everywhere, slot p free).
 template <int EPI, int PERSIST, int ABL = 0, int STAMP = 0, int TA = 0, int TB = 0, int PS = 0, int PAIR = 0>
 __global__ void __launch_bounds__(WNT, 1) k_gemm_w4r(W4Args wa) {
-  static_assert(!PAIR || (!PERSIST && !ABL && !STAMP && !TA && !TB && !PS), "pair-slot ring: N layout only");
+  static_assert(!PAIR || (!ABL && !STAMP && !TA && !TB && !PS), "pair-slot ring: N layout only");
   const GemmArgs& g = wa.g;
   extern __shared__ __attribute__((aligned(1024))) unsigned char smem[];
   const int tiles_n = (g.N + WNB - 1) / WNB, tiles_m = (g.M + WM - 1) / WM;
@@ -918,12 +918,24 @@ __global__ void __launch_bounds__(WNT, 1) k_gemm_w4r(W4Args wa) {
   };
 
   const int ldc = g.ldc;
-  // prologue of the first tile: steps 0..2 in flight (PAIR: pairs 0 and 1, in the tile)
-  if constexpr (!PAIR)
-    for (int s = 0; s < pro; ++s)
+  // prologue of the first tile: steps 0..2 in flight (PAIR: pairs 0 and 1)
+  auto prologue = [&]() {
+    if constexpr (PAIR) {
 #pragma unroll
-      for (int i = 0; i < 8; ++i) dma(s, i);
-  int younger = 8 * (pro - 1);  // DMA pieces issued after step 0's
+      for (int i = 0; i < 16; ++i) dma_pair(0, i);
+      if (nst >= 4)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) dma_pair(1, i);
+    } else {
+      for (int s = 0; s < pro; ++s)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) dma(s, i);
+    }
+  };
+  prologue();
+  // DMA pieces issued after step 0's (PAIR: after pair 0's)
+  const int younger0 = PAIR ? (nst >= 4 ? 16 : 0) : 8 * (pro - 1);
+  int younger = younger0;
   for (;;) {
     const int bm = tm * WM, bn = tn * WNB;
 #pragma unroll
@@ -935,15 +947,8 @@ __global__ void __launch_bounds__(WNT, 1) k_gemm_w4r(W4Args wa) {
     int ntm = 0, ntn = 0;
     if constexpr (PAIR) {
       const int npair = nst >> 1;
-#pragma unroll
-      for (int i = 0; i < 16; ++i) dma_pair(0, i);
-      if (npair > 1) {
-#pragma unroll
-        for (int i = 0; i < 16; ++i) dma_pair(1, i);
-        ring_wait_barrier_c<16>();
-      } else {
-        ring_wait_barrier_c<0>();
-      }
+      // pair 0 landed everywhere, every wave past the previous tile's epilogue
+      ring_wait_barrier(younger);
       // "phase 0": step 0's fragments; phase 1 ends with pair 1 landed
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
@@ -958,6 +963,14 @@ __global__ void __launch_bounds__(WNT, 1) k_gemm_w4r(W4Args wa) {
       if (npair > 1) {
         phase_pair(F{}, F{}, nst - 2, a1, b1, a0, b0);
         phase_pair(F{}, T{}, nst - 1, a0, b0, a1, b1);
+      }
+      // persistent: both slots are free (the last phase's barrier) -- the next tile's
+      // pairs 0 and 1 load under the last MFMAs and the epilogue (whose slab is apart)
+      more = PERSIST && (EPI == 1 || EPI == 2) && next < ntiles;
+      if (more) {
+        tile_coords(next, tiles_m, tiles_n, wa.group_m, ntm, ntn);
+        ops_for(ntm, ntn);
+        prologue();
       }
 #pragma unroll
       for (int i = 0; i < 8; ++i)
@@ -1133,7 +1146,7 @@ __global__ void __launch_bounds__(WNT, 1) k_gemm_w4r(W4Args wa) {
     // then the wait conservatively also retires the stores
     if (more) {
       const bool interior = bm + WM <= g.M && bn + WNB <= g.N;
-      younger = !interior ? 8 * (pro - 1) : (EPI == 2 ? 63 : 8 * (pro - 1) + 32);
+      younger = !interior ? younger0 : (EPI == 2 ? 63 : younger0 + 32);
     }
     if constexpr (STAMP) {
       if (lt == xcd_remap(blockIdx.x, gridDim.x)) {  // first tile of this workgroup
@@ -1252,6 +1265,8 @@ void launch_gemm_ring(const GemmArgs& g, int ta, int tb, hipStream_t stream, uin
     w4p_attr(reinterpret_cast<const void*>(k_gemm_w4r<0, 0, 0, 0, 0, 0, 0, 1>));
     w4p_attr(reinterpret_cast<const void*>(k_gemm_w4r<1, 0, 0, 0, 0, 0, 0, 1>));
     w4p_attr(reinterpret_cast<const void*>(k_gemm_w4r<2, 0, 0, 0, 0, 0, 0, 1>));
+    w4p_attr(reinterpret_cast<const void*>(k_gemm_w4r<1, 1, 0, 0, 0, 0, 0, 1>));
+    w4p_attr(reinterpret_cast<const void*>(k_gemm_w4r<2, 1, 0, 0, 0, 0, 0, 1>));
     w4p_attr(reinterpret_cast<const void*>(k_gemm_w4r<0, 0, 0, 0, 0, 0, 0, 2>));
     w4p_attr(reinterpret_cast<const void*>(k_gemm_w4r<1, 0, 0, 0, 0, 0, 0, 2>));
     w4p_attr(reinterpret_cast<const void*>(k_gemm_w4r<2, 0, 0, 0, 0, 0, 0, 2>));
@@ -1263,7 +1278,9 @@ void launch_gemm_ring(const GemmArgs& g, int ta, int tb, hipStream_t stream, uin
   const bool fast = gemm_w4r_fast(g);
   if (glu) {  // SwiGLU epilogue (callers check gemm_w4r_fast and the glu layout first)
     if (!fast || ta || tb) throw std::invalid_argument("gemm ring: the SwiGLU epilogue needs the fast NT form");
-    if (sched & 65536) hipLaunchKernelGGL((k_gemm_w4r<2, 0, 0, 0, 0, 0, 0, 2>), dim3(ntiles), dim3(WNT), kPairLds, stream, a);
+    if ((sched & 16384) && (sched & 1)) {
+      hipLaunchKernelGGL((k_gemm_w4r<2, 1, 0, 0, 0, 0, 0, 1>), dim3(std::min(ntiles, cus)), dim3(WNT), kPairLds, stream, a);
+    } else if (sched & 65536) hipLaunchKernelGGL((k_gemm_w4r<2, 0, 0, 0, 0, 0, 0, 2>), dim3(ntiles), dim3(WNT), kPairLds, stream, a);
     else if (sched & 16384) hipLaunchKernelGGL((k_gemm_w4r<2, 0, 0, 0, 0, 0, 0, 1>), dim3(ntiles), dim3(WNT), kPairLds, stream, a);
     else if (sched & 4096) hipLaunchKernelGGL((k_gemm_w4r<2, 0, 0, 0, 0, 0, 3>), dim3(ntiles), dim3(WNT), kRingLds, stream, a);
     else if (sched & 1024) hipLaunchKernelGGL((k_gemm_w4r<2, 0, 0, 0, 0, 0, 1>), dim3(ntiles), dim3(WNT), kRingLds, stream, a);
@@ -1290,8 +1307,9 @@ void launch_gemm_ring(const GemmArgs& g, int ta, int tb, hipStream_t stream, uin
     if (fast) hipLaunchKernelGGL((k_gemm_w4r<1, 0, 0, 0, 0, 0, 0, 2>), dim3(ntiles), dim3(WNT), kPairLds, stream, a);
     else hipLaunchKernelGGL((k_gemm_w4r<0, 0, 0, 0, 0, 0, 0, 2>), dim3(ntiles), dim3(WNT), kPairLds, stream, a);
   } else if (sched & 16384) {
-    // pair-slot ring: whole-line DMA pieces, 64-deep slots (non-persistent)
-    if (fast) hipLaunchKernelGGL((k_gemm_w4r<1, 0, 0, 0, 0, 0, 0, 1>), dim3(ntiles), dim3(WNT), kPairLds, stream, a);
+    // pair-slot ring: whole-line DMA pieces, 64-deep slots (bit 0: persistent grid)
+    if (persist) hipLaunchKernelGGL((k_gemm_w4r<1, 1, 0, 0, 0, 0, 0, 1>), dim3(grid), dim3(WNT), kPairLds, stream, a);
+    else if (fast) hipLaunchKernelGGL((k_gemm_w4r<1, 0, 0, 0, 0, 0, 0, 1>), dim3(ntiles), dim3(WNT), kPairLds, stream, a);
     else hipLaunchKernelGGL((k_gemm_w4r<0, 0, 0, 0, 0, 0, 0, 1>), dim3(ntiles), dim3(WNT), kPairLds, stream, a);
   } else if (!fast) {
     hipLaunchKernelGGL((k_gemm_w4r<0, 0>), dim3(grid), dim3(WNT), kRingLds, stream, a);

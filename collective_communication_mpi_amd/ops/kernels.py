@@ -1,6 +1,7 @@
 """Python entry points of the device kernels (csrc/device/*.hip)."""
 from __future__ import annotations
 
+import os
 from typing import Optional
 
 import torch
@@ -164,13 +165,32 @@ def gemm_ring(a: torch.Tensor, b: torch.Tensor, ta: bool, tb: bool, out: Optiona
         out = torch.empty((M, N), dtype=out_dtype, device=a.device)
     if out.shape != (M, N) or out.stride(1) != 1 or out.dtype not in (torch.bfloat16, torch.float32):
         raise ValueError("gemm_ring output must be [M, N] bf16/fp32 with unit column stride")
+    if (ta or tb) and _kmajor_via_transpose(M, N, K, a, b):
+        # K-major operands transposed first (k_transpose16_v, ~6 TB/s), then the N-layout
+        # pair-slot ring: its whole-line DMA pieces and one ds_read_b128 per fragment beat
+        # the K-major ring's two transposed LDS reads per fragment (profiles/r4_bwd)
+        at = transpose(a) if ta else a
+        bt = transpose(b) if tb else b
+        return gemm_ring(at, bt, False, False, out=out, alpha=alpha, accumulate=accumulate, out_dtype=out_dtype)
     ok = _D().gemm_ring(a.data_ptr(), b.data_ptr(), out.data_ptr(), M, N, K, a.stride(0), b.stride(0), out.stride(0),
                         int(ta), int(tb), float(alpha), bool(accumulate), out.dtype == torch.bfloat16, _stream(a))
     return out if ok else None
 
 
+def _kmajor_via_transpose(M: int, N: int, K: int, a: torch.Tensor, b: torch.Tensor) -> bool:
+    """Route a K-major ring GEMM through transposed copies (CCMPI_KMAJOR_ROUTE=transpose,
+    read per call; ``ring`` keeps the K-major kernel): large GEMMs only, and not long K
+    (there the K-major ring measured faster than the N-layout kernels, profiles/r4_pair2)."""
+    if os.environ.get("CCMPI_KMAJOR_ROUTE", "transpose") != "transpose":
+        return False
+    return (M >= 1024 and N >= 1024 and K <= 16384 and K % 8 == 0 and M % 8 == 0 and N % 8 == 0
+            and M * N * K >= (1 << 33) and a.data_ptr() % 16 == 0 and b.data_ptr() % 16 == 0
+            and a.stride(0) % 8 == 0 and b.stride(0) % 8 == 0)
+
+
 def transpose(x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """2-D transpose of a 16-bit tensor (LDS-tiled kernel)."""
+    """2-D transpose of a 16-bit tensor: 16-B register-transpose kernel when the shape and
+    strides are multiples of 8 elements (k_transpose16_v), else the LDS-tiled one."""
     if x.dim() != 2 or x.element_size() != 2 or x.stride(1) != 1:
         raise ValueError("transpose expects a 2-D row-contiguous 16-bit tensor")
     R, C = x.shape

@@ -328,6 +328,11 @@ class _RowParallelFn(torch.autograd.Function):
         if M == 0:
             return y
         if not _dev_path(x2, w, comm):
+            if ctx.mfma and p == 1:
+                # a one-rank TP group on the GPU: the hand-written GEMM, nothing to reduce
+                CALLS["row_local"] += 1
+                gemm_nt(x2, w, bias=b, out=y2)
+                return y
             # host plane / other dtypes: local product, in-place all-reduce of that fresh tensor
             CALLS["row_host"] += 1
             torch.matmul(x2, w.t(), out=y2)

@@ -80,8 +80,8 @@ def test_gemm256_epilogue(gemm256, act):
     torch.testing.assert_close(c, c0 + _ref(a, b), rtol=2e-3, atol=5e-2)
 
 
-@pytest.mark.parametrize("sched", [0, 1, 3, 4, 5, 8, 9, 8 | 16384, 8 | 65536],
-                         ids=["w4", "w4p", "w4po", "w4f", "w4pf", "ring", "ringp", "ringpair", "ringpairfl"])
+@pytest.mark.parametrize("sched", [0, 1, 3, 4, 5, 8, 9, 8 | 16384, 9 | 16384, 8 | 65536],
+                         ids=["w4", "w4p", "w4po", "w4f", "w4pf", "ring", "ringp", "ringpair", "ringpairp", "ringpairfl"])
 @pytest.mark.parametrize("M,N,K", [(256, 256, 64), (256, 256, 128), (300, 520, 256), (777, 1000, 512),
                                    (2048, 2048, 4096), (1, 8, 192), (4096, 768, 768)])
 def test_gemm_w4_shapes(sched, M, N, K):
@@ -194,6 +194,19 @@ def test_transpose_and_interleave():
         inter = interleave_lastaxis(st, 4)
         torch.testing.assert_close(inter, torch.cat(list(st), dim=-1))
         torch.testing.assert_close(deinterleave_lastaxis(inter, 4), st)
+
+
+@pytest.mark.parametrize("R,C", [(8, 8), (520, 72), (4096, 1032), (1000, 16), (24, 4104)])
+def test_transpose_vectorized(R, C):
+    """16-B register-transpose kernel (R, C % 8 == 0): partial workgroups in both
+    dimensions, a strided source view, against torch."""
+    from collective_communication_mpi_amd.ops import transpose
+
+    x = torch.randn(R, C + 8, device="cuda").bfloat16()[:, :C]
+    torch.testing.assert_close(transpose(x), x.T.contiguous(), rtol=0, atol=0)
+    out = torch.empty(C, R + 16, device="cuda", dtype=torch.bfloat16)[:, :R]
+    transpose(x, out=out)
+    torch.testing.assert_close(out, x.T, rtol=0, atol=0)
 
 
 def test_single_rank_communicator_paths():
@@ -543,6 +556,31 @@ def test_fold_emb_qkv_matches_fp32(R, d, kp):
     assert torch.isnan(out[:, kp:].float()).all()  # columns past kp untouched
 
 
+@pytest.mark.parametrize("route", ["transpose", "ring"])
+@pytest.mark.parametrize("ta,tb", [(0, 1), (1, 1), (1, 0)], ids=["kA-tB", "tA-tB", "tA-kB"])
+def test_gemm_ring_kmajor_routes(monkeypatch, route, ta, tb):
+    """A large K-major GEMM both ways: transposed copies + the N-layout pair ring (the
+    default route above 2^33 MACs) and the K-major ring; fp32 reference, bf16 out with
+    alpha, and fp32 accumulate (the DDP gradient-sink forms)."""
+    from collective_communication_mpi_amd import _native
+    from collective_communication_mpi_amd.ops import gemm_ring
+
+    monkeypatch.setenv("CCMPI_KMAJOR_ROUTE", route)
+    M, N, K = 2048, 2048, 2048
+    g = torch.Generator(device="cuda").manual_seed(17 + ta + 2 * tb)
+    a = torch.randn(K, M, device="cuda", generator=g).bfloat16() if ta else torch.randn(M, K, device="cuda", generator=g).bfloat16()
+    b = torch.randn(K, N, device="cuda", generator=g).bfloat16() if tb else torch.randn(N, K, device="cuda", generator=g).bfloat16()
+    ref = (a.float().T if ta else a.float()) @ (b.float().T if tb else b.float()).T
+    n0 = _native.device().gemm_ring_launches()
+    y16 = gemm_ring(a, b, bool(ta), bool(tb), alpha=0.5)
+    assert _native.device().gemm_ring_launches() == n0 + 1
+    torch.testing.assert_close(y16.float(), 0.5 * ref, rtol=1.6e-2, atol=1.6e-2 * K ** 0.5)
+    c = torch.randn(M, N, device="cuda")
+    c0 = c.clone()
+    gemm_ring(a, b, bool(ta), bool(tb), out=c, accumulate=True)
+    torch.testing.assert_close(c, c0 + ref, rtol=2e-3, atol=2e-3 * K ** 0.5)
+
+
 @pytest.mark.parametrize("ta,tb", [(0, 0), (0, 1), (1, 1), (1, 0)], ids=["kA-kB", "kA-tB", "tA-tB", "tA-kB"])
 @pytest.mark.parametrize("M,N,K", [(256, 256, 64), (300, 520, 256), (776, 1000, 512), (2048, 1024, 1024),
                                    (8, 8, 192), (1, 8, 192)])
@@ -601,7 +639,7 @@ def test_swiglu_strided_and_batched():
     torch.testing.assert_close(swiglu(h).float(), ref, rtol=1.6e-2, atol=1e-2)
 
 
-@pytest.mark.parametrize("ring", [8, 8 | 16384, 8 | 65536], ids=["ring", "pair", "pairfl"])
+@pytest.mark.parametrize("ring", [8, 8 | 16384, 9 | 16384, 8 | 65536], ids=["ring", "pair", "pairp", "pairfl"])
 @pytest.mark.parametrize("M,N,K", [(4096, 2048, 512), (300, 520, 128), (1000, 2056, 64), (257, 264, 192)])
 def test_gemm_nt_swiglu_epilogue(M, N, K, ring):
     """Ring GEMM with the SwiGLU gate of interleaved column pairs in its epilogue (EPI 2):
