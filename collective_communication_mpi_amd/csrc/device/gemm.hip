@@ -21,6 +21,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <string>
 
 #include "common.hpp"
 #include "gemm_common.hpp"
@@ -839,6 +840,39 @@ __global__ void __launch_bounds__(256) k_transpose16_v(const uint16_t* __restric
   }
 }
 
+// LDS variant: a workgroup moves a 64 x 64 tile.  Loads: 8 lanes per source row, 16 B
+// each (a wave reads 8 whole 128-B lines); the tile lands in LDS with a 33-word row
+// stride (odd: the column gathers below are bank-conflict free).  Stores: 8 lanes per
+// destination row, each packing 8 source rows of one column (8 ds_read_u16) into 16 B.
+__global__ void __launch_bounds__(256) k_transpose16_l(const uint16_t* __restrict__ src, uint16_t* __restrict__ dst,
+                                                       int R, int C, int lds, int ldd) {
+  constexpr int S = 66;  // row stride in elements (33 words)
+  __shared__ uint32_t tile[64 * S / 2];
+  const int t = threadIdx.x;
+  const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
+  const int lr = t >> 3, lc = (t & 7) * 8;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int row = lr + 32 * h;
+    uint4 v = uint4{0u, 0u, 0u, 0u};
+    if (r0 + row < R && c0 + lc < C) v = *reinterpret_cast<const uint4*>(src + (size_t)(r0 + row) * lds + c0 + lc);
+    uint32_t* d = tile + (row * S + lc) / 2;
+    d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+  }
+  __syncthreads();
+  const uint16_t* t16 = reinterpret_cast<const uint16_t*>(tile);
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int oc = lr + 32 * h, q = t & 7;  // destination row c0 + oc, source rows 8 q ..
+    uint32_t o[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+      o[m] = (uint32_t)t16[(8 * q + 2 * m) * S + oc] | ((uint32_t)t16[(8 * q + 2 * m + 1) * S + oc] << 16);
+    if (c0 + oc < C && r0 + 8 * q < R)
+      *reinterpret_cast<uint4*>(dst + (size_t)(c0 + oc) * ldd + r0 + 8 * q) = uint4{o[0], o[1], o[2], o[3]};
+  }
+}
+
 // Sum of the split-K workspace slices into C ([rows][cols] fp32, row stride ldc),
 // 4 columns per thread: C (+)= sum_s ws[s].  Columns >= csplit (a multiple of 4)
 // go to a second destination instead, C2[r][c - csplit] = sum (overwritten):
@@ -1107,6 +1141,14 @@ void gemm_tn(uint64_t A, uint64_t B, uint64_t C, int M, int N1, int N2, int lda,
 void transpose16(uint64_t src, uint64_t dst, int R, int C, int lds, int ldd, uint64_t stream) {
   if (R <= 0 || C <= 0) return;
   if (R % 8 == 0 && C % 8 == 0 && lds % 8 == 0 && ldd % 8 == 0 && src % 16 == 0 && dst % 16 == 0) {
+    static const bool reg = std::getenv("CCMPI_TRANSPOSE") && std::string(std::getenv("CCMPI_TRANSPOSE")) == "reg";
+    if (!reg) {  // the LDS tile by default; CCMPI_TRANSPOSE=reg picks the register transpose (A/B)
+      dim3 grid((C + 63) / 64, (R + 63) / 64);
+      hipLaunchKernelGGL(k_transpose16_l, grid, dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+                         reinterpret_cast<const uint16_t*>(src), reinterpret_cast<uint16_t*>(dst), R, C, lds, ldd);
+      CCMPI_HIP_CHECK(hipGetLastError());
+      return;
+    }
     dim3 grid((C + 63) / 64, (R + 511) / 512);
     hipLaunchKernelGGL(k_transpose16_v, grid, dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
                        reinterpret_cast<const uint16_t*>(src), reinterpret_cast<uint16_t*>(dst), R, C, lds, ldd);

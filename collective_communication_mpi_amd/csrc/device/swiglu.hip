@@ -120,6 +120,54 @@ __global__ void __launch_bounds__(256) k_swiglu_bwd_il(const uint16_t* __restric
   *reinterpret_cast<u32x4*>(dh + t * lddh + 8 * (int64_t)j) = r;
 }
 
+// The same, plus dh^T [2k, T] for the weight-gradient GEMM dW = dh^T X (which then runs
+// on the N-layout pair ring instead of the K-major one, with no separate transpose pass):
+// a 64-row x 64-column tile of dh per workgroup, written row-major straight away and
+// through an LDS tile (33-word row stride: conflict-free column gathers) transposed,
+// 16-B stores both ways.  T % 8 == 0.
+__global__ void __launch_bounds__(256) k_swiglu_bwd_il_t(const uint16_t* __restrict__ h, const uint16_t* __restrict__ da,
+                                                         uint16_t* __restrict__ dh, uint16_t* __restrict__ dht, int T,
+                                                         int n, int64_t ldh, int64_t ldda, int64_t lddh, int64_t ldt) {
+  constexpr int S = 66;  // LDS row stride, elements
+  __shared__ uint32_t tile[64 * S / 2];
+  const int t = threadIdx.x;
+  const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
+  const int lr = t >> 3, lc = (t & 7) * 8;
+#pragma unroll
+  for (int hh = 0; hh < 2; ++hh) {
+    const int row = lr + 32 * hh;
+    u32x4 r = u32x4{0u, 0u, 0u, 0u};
+    if (r0 + row < T && c0 + lc < n) {
+      const int64_t tr = r0 + row;
+      const u32x4 w = *reinterpret_cast<const u32x4*>(h + tr * ldh + c0 + lc);
+      const uint2 d2 = *reinterpret_cast<const uint2*>(da + tr * ldda + (c0 + lc) / 2);
+      const uint32_t dd[2] = {d2.x, d2.y};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float gv = bf16_lo(w[q]), uv = bf16_hi(w[q]);
+        const float dv = (q & 1) ? bf16_hi(dd[q >> 1]) : bf16_lo(dd[q >> 1]);
+        const float sg = sigmoid_fast(gv);
+        r[q] = pack_bf16(dv * uv * sg * (1.0f + gv * (1.0f - sg)), dv * gv * sg);
+      }
+      *reinterpret_cast<u32x4*>(dh + tr * lddh + c0 + lc) = r;
+    }
+    uint32_t* d = tile + (row * S + lc) / 2;
+    d[0] = r[0]; d[1] = r[1]; d[2] = r[2]; d[3] = r[3];
+  }
+  __syncthreads();
+  const uint16_t* t16 = reinterpret_cast<const uint16_t*>(tile);
+#pragma unroll
+  for (int hh = 0; hh < 2; ++hh) {
+    const int oc = lr + 32 * hh, q = t & 7;  // dh^T row c0 + oc, columns r0 + 8 q ..
+    uint32_t o[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+      o[m] = (uint32_t)t16[(8 * q + 2 * m) * S + oc] | ((uint32_t)t16[(8 * q + 2 * m + 1) * S + oc] << 16);
+    if (c0 + oc < n && r0 + 8 * q < T)
+      *reinterpret_cast<uint4*>(dht + (int64_t)(c0 + oc) * ldt + r0 + 8 * q) = uint4{o[0], o[1], o[2], o[3]};
+  }
+}
+
 void check(uint64_t T, uint64_t k, uint64_t ptrs, uint64_t lds) {
   if (k % 8 || (ptrs | (lds * 2)) % 16)
     throw std::invalid_argument("swiglu: k % 8 == 0, 16-B aligned pointers and row strides required");
@@ -156,6 +204,18 @@ void register_swiglu_ops(pybind11::module_& m) {
                        reinterpret_cast<const uint16_t*>(da), reinterpret_cast<uint16_t*>(dh), nv, ldh, ldda, lddh);
     CCMPI_HIP_CHECK(hipGetLastError());
   }, "dh[T, 2k] (interleaved pairs) from h[T, 2k] and da[T, k]");
+  m.def("swiglu_bwd_il_t", [](uint64_t h, uint64_t da, uint64_t dh, uint64_t dht, uint64_t T, uint64_t k, int64_t ldh,
+                              int64_t ldda, int64_t lddh, int64_t ldt, uint64_t stream) {
+    check_il(T, k, h | dh | dht, (uint64_t)(ldh | lddh | ldt), da, (uint64_t)ldda);
+    if (T % 8) throw std::invalid_argument("swiglu_bwd_il_t: T % 8 == 0 required");
+    if (T == 0 || k == 0) return;
+    const int n = (int)(2 * k);
+    hipLaunchKernelGGL(k_swiglu_bwd_il_t, dim3((n + 63) / 64, (unsigned)((T + 63) / 64)), dim3(256), 0,
+                       reinterpret_cast<hipStream_t>(stream), reinterpret_cast<const uint16_t*>(h),
+                       reinterpret_cast<const uint16_t*>(da), reinterpret_cast<uint16_t*>(dh),
+                       reinterpret_cast<uint16_t*>(dht), (int)T, n, ldh, ldda, lddh, ldt);
+    CCMPI_HIP_CHECK(hipGetLastError());
+  }, "swiglu_bwd_il plus dh^T [2k, T] (the dW GEMM's N-layout operand)");
   // C[M, N] = A[M, K] B[N, K]^T (bf16) on the LDS-ring kernel with the SwiGLU epilogue:
   // glu[M, N / 2] from C's interleaved (gate, up) column pairs.  False (nothing launched)
   // when the ring kernel's fast form does not apply; the caller then runs gemm_nt +

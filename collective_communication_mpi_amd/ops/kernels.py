@@ -144,13 +144,16 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
 
 
 def gemm_ring(a: torch.Tensor, b: torch.Tensor, ta: bool, tb: bool, out: Optional[torch.Tensor] = None,
-              alpha: float = 1.0, accumulate: bool = False, out_dtype: torch.dtype = torch.bfloat16) -> Optional[torch.Tensor]:
+              alpha: float = 1.0, accumulate: bool = False, out_dtype: torch.dtype = torch.bfloat16,
+              a_nt: Optional[torch.Tensor] = None) -> Optional[torch.Tensor]:
     """``out = alpha * op(a) @ op(b).T (+ out)`` on the four-wave LDS-ring MFMA kernel
     (csrc/device/gemm_w4.hip), with either operand K-major: op(a) = a.T if ``ta`` (a is
     [K, M]) else a ([M, K]); op(b) = b.T if ``tb`` (b is [K, N]) else b ([N, K]).
     dX = dY W is ``gemm_ring(dY, W, False, True)``, dW = dY^T X is
     ``gemm_ring(dY, X, True, True)``: no transposes.  Returns None when the kernel does
-    not apply (K % 64, 16-B alignment, > 2 GiB operands): the caller falls back."""
+    not apply (K % 64, 16-B alignment, > 2 GiB operands): the caller falls back.
+    ``a_nt``: op(a) already in N layout (``a.T`` contiguous, e.g. the dh^T the SwiGLU
+    backward writes): the N-layout pair ring runs on it, no transpose of ``a``."""
     if a.dtype != torch.bfloat16 or b.dtype != torch.bfloat16 or a.dim() != 2 or b.dim() != 2:
         raise TypeError("gemm_ring expects 2-D bf16 operands")
     if a.stride(1) != 1 or b.stride(1) != 1:
@@ -165,11 +168,11 @@ def gemm_ring(a: torch.Tensor, b: torch.Tensor, ta: bool, tb: bool, out: Optiona
         out = torch.empty((M, N), dtype=out_dtype, device=a.device)
     if out.shape != (M, N) or out.stride(1) != 1 or out.dtype not in (torch.bfloat16, torch.float32):
         raise ValueError("gemm_ring output must be [M, N] bf16/fp32 with unit column stride")
-    if (ta or tb) and _kmajor_via_transpose(M, N, K, a, b):
+    if ta and (a_nt is not None or _kmajor_via_transpose(M, N, K, a, b)):
         # K-major operands transposed first (k_transpose16_v, ~6 TB/s), then the N-layout
         # pair-slot ring: its whole-line DMA pieces and one ds_read_b128 per fragment beat
         # the K-major ring's two transposed LDS reads per fragment (profiles/r4_bwd)
-        at = transpose(a) if ta else a
+        at = a_nt if a_nt is not None else transpose(a)
         bt = transpose(b) if tb else b
         return gemm_ring(at, bt, False, False, out=out, alpha=alpha, accumulate=accumulate, out_dtype=out_dtype)
     ok = _D().gemm_ring(a.data_ptr(), b.data_ptr(), out.data_ptr(), M, N, K, a.stride(0), b.stride(0), out.stride(0),
@@ -179,8 +182,9 @@ def gemm_ring(a: torch.Tensor, b: torch.Tensor, ta: bool, tb: bool, out: Optiona
 
 def _kmajor_via_transpose(M: int, N: int, K: int, a: torch.Tensor, b: torch.Tensor) -> bool:
     """Route a K-major ring GEMM through transposed copies (CCMPI_KMAJOR_ROUTE=transpose,
-    read per call; ``ring`` keeps the K-major kernel): large GEMMs only, and not long K
-    (there the K-major ring measured faster than the N-layout kernels, profiles/r4_pair2)."""
+    read per call; ``ring`` keeps the K-major kernel): K-major A (the dW = dY^T X form),
+    large GEMMs only, and not long K.  dX = dY W (K-major B only) stays on the ring: a
+    transposed weight copy + the pair ring measured no faster (profiles/r4_bwd)."""
     if os.environ.get("CCMPI_KMAJOR_ROUTE", "transpose") != "transpose":
         return False
     return (M >= 1024 and N >= 1024 and K <= 16384 and K % 8 == 0 and M % 8 == 0 and N % 8 == 0
@@ -255,11 +259,18 @@ def swiglu_pairs(h: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.T
     return out
 
 
-def swiglu_pairs_backward(h: torch.Tensor, da: torch.Tensor) -> torch.Tensor:
-    """Gradient of ``swiglu_pairs`` w.r.t. its interleaved input (one HIP kernel)."""
+def swiglu_pairs_backward(h: torch.Tensor, da: torch.Tensor, transposed: bool = False):
+    """Gradient of ``swiglu_pairs`` w.r.t. its interleaved input (one HIP kernel).  With
+    ``transposed`` (T % 8 == 0): returns ``(dh, dh^T)``, the transposed copy written by the
+    same kernel (the weight-gradient GEMM's N-layout operand, no separate transpose)."""
     T, n = h.shape
     da = da if (da.stride(1) == 1 and da.stride(0) % 4 == 0) else da.contiguous()
     dh = torch.empty_like(h)
+    if transposed:
+        dht = torch.empty(n, T, device=h.device, dtype=h.dtype)
+        _D().swiglu_bwd_il_t(h.data_ptr(), da.data_ptr(), dh.data_ptr(), dht.data_ptr(), T, n // 2, h.stride(0),
+                             da.stride(0), dh.stride(0), dht.stride(0), _stream(h))
+        return dh, dht
     _D().swiglu_bwd_il(h.data_ptr(), da.data_ptr(), dh.data_ptr(), T, n // 2, h.stride(0), da.stride(0),
                        dh.stride(0), _stream(h))
     return dh

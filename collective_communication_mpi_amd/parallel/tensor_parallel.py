@@ -35,6 +35,7 @@ import os
 import torch
 
 from ..ops import gemm_nt, gemm_nt_swiglu, gemm_ring, gemm_tn, swiglu_pairs, swiglu_pairs_backward, transpose
+from ..ops.kernels import _kmajor_via_transpose
 from .layout import _host_comm, device_group_for
 
 
@@ -199,7 +200,7 @@ def _mfma_ok(x: torch.Tensor, w: torch.Tensor, comm=None) -> bool:
 
 
 def _linear_backward(g2: torch.Tensor, x2: torch.Tensor, w: torch.Tensor, need_dx: bool, need_dw: bool,
-                     comm=None):
+                     comm=None, g2t: Optional[torch.Tensor] = None):
     """dX = dY W and dW = dY^T X (bf16 out, fp32 accumulate) on the LDS-ring kernel with
     K-major operands; the older routes (transpose + NT kernel, 256x256 TN kernel) when
     it does not apply (K % 64, alignment) or when the TP group's ranks share a GPU (a
@@ -212,7 +213,7 @@ def _linear_backward(g2: torch.Tensor, x2: torch.Tensor, w: torch.Tensor, need_d
         if dx is None:
             dx = gemm_nt(g2, transpose(w))
     if need_dw:
-        dw = gemm_ring(g2, x2, True, True) if ring else None
+        dw = gemm_ring(g2, x2, True, True, a_nt=g2t) if ring else None
         if dw is None:
             dw = gemm_tn(g2, x2).to(w.dtype)
     return dx, dw
@@ -282,18 +283,18 @@ def _deliver_wgrad(w: torch.Tensor, dw):
     return None
 
 
-def _wgrad(g2: torch.Tensor, x2: torch.Tensor, w: torch.Tensor, comm):
+def _wgrad(g2: torch.Tensor, x2: torch.Tensor, w: torch.Tensor, comm, g2t: Optional[torch.Tensor] = None):
     """dW = dY^T X.  With a DDP gradient sink on ``w`` the MFMA kernel writes (or, when
     accumulating over micro-batches, adds) straight into the bucket view: no gradient
     tensor, no AccumulateGrad pass over it (16 GB of bf16 gradients read twice and
     written once per Llama-3-8B step otherwise); returns None then."""
     sink = getattr(w, "_ccmpi_grad_sink", None)
     if sink is None or not sink.view.is_contiguous():
-        return _deliver_wgrad(w, _linear_backward(g2, x2, w, False, True, comm)[1])
+        return _deliver_wgrad(w, _linear_backward(g2, x2, w, False, True, comm, g2t)[1])
     view, acc = sink.begin()
     # the DDP average rides in the GEMM's alpha (sink.scale = 1/p)
     if _gpu_shared(comm) or gemm_ring(g2, x2, True, True, out=view.view(w.shape), alpha=sink.scale,
-                                      accumulate=acc) is None:
+                                      accumulate=acc, a_nt=g2t) is None:
         dw = gemm_tn(g2, x2, alpha=sink.scale).to(w.dtype)
         if acc:
             view.add_(dw.view_as(view))
@@ -386,7 +387,8 @@ class _RowParallelFn(torch.autograd.Function):
         return dx, dw, db, None, None
 
 
-def _column_backward(g2: torch.Tensor, x2: torch.Tensor, w: torch.Tensor, need_dx: bool, need_dw: bool, comm):
+def _column_backward(g2: torch.Tensor, x2: torch.Tensor, w: torch.Tensor, need_dx: bool, need_dw: bool, comm,
+                     g2t: Optional[torch.Tensor] = None):
     """Backward of a column-parallel projection with its TP all-reduce of dX (Megatron "f")
     overlapped with the weight-gradient GEMM: dX's partial product goes into persistent
     symmetric scratch, its all-reduce into a fresh dX starts on the communication stream,
@@ -395,7 +397,7 @@ def _column_backward(g2: torch.Tensor, x2: torch.Tensor, w: torch.Tensor, need_d
         dx, _ = _linear_backward(g2, x2, w, need_dx, False, comm)
         if dx is not None:
             dx = all_reduce_(dx, comm)  # a fresh tensor of this backward: in place is safe
-        return dx, (_wgrad(g2, x2, w, comm) if need_dw else None)
+        return dx, (_wgrad(g2, x2, w, comm, g2t) if need_dw else None)
     CALLS["col_bwd_overlap"] += 1
     dev = device_group_for(comm)
     M, K = g2.shape[0], w.shape[1]
@@ -405,7 +407,7 @@ def _column_backward(g2: torch.Tensor, x2: torch.Tensor, w: torch.Tensor, need_d
         gemm_nt(g2, transpose(w), out=part)
     dx = torch.empty(M, K, device=g2.device, dtype=g2.dtype)
     work = dev.start("allreduce_to_local", part, dx)
-    dw = _wgrad(g2, x2, w, comm) if need_dw else None
+    dw = _wgrad(g2, x2, w, comm, g2t) if need_dw else None
     work.wait()
     return dx, dw
 
@@ -532,6 +534,14 @@ class RowParallelLinear(torch.nn.Module):
         return _RowParallelFn.apply(x, self.weight, self.bias, self.comm, self.mode or _ROW_MODE)
 
 
+def _dh_transposed(h: torch.Tensor, x2: torch.Tensor, w: torch.Tensor, comm) -> bool:
+    """Whether the gate|up weight gradient dW = dh^T X takes the transposed route (then the
+    SwiGLU backward also writes dh^T): the ring is on, and ops' K-major routing rule holds."""
+    T, n = h.shape
+    return (T % 8 == 0 and not _gpu_shared(comm) and h.stride(1) == 1
+            and _kmajor_via_transpose(n, x2.shape[1], T, h, x2))
+
+
 class _GateUpSwiGLU(torch.autograd.Function):
     """``a = swiglu_pairs(x W^T)`` for a column-parallel gate|up weight whose rows are
     interleaved (gate j, up j) pairs.  Forward: one GEMM whose epilogue also writes the
@@ -564,9 +574,15 @@ class _GateUpSwiGLU(torch.autograd.Function):
     @staticmethod
     def backward(ctx, da):
         x2, w, h = ctx.saved_tensors
-        dh = swiglu_pairs_backward(h, da.reshape(-1, da.shape[-1]))
+        da2 = da.reshape(-1, da.shape[-1])
+        dht = None
+        if ctx.mfma and ctx.needs_input_grad[1] and _dh_transposed(h, x2, w, ctx.comm):
+            # dh^T from the same kernel: dW = dh^T X on the N-layout pair ring, no transpose pass
+            dh, dht = swiglu_pairs_backward(h, da2, transposed=True)
+        else:
+            dh = swiglu_pairs_backward(h, da2)
         if ctx.mfma:
-            dx, dw = _column_backward(dh, x2, w, ctx.needs_input_grad[0], ctx.needs_input_grad[1], ctx.comm)
+            dx, dw = _column_backward(dh, x2, w, ctx.needs_input_grad[0], ctx.needs_input_grad[1], ctx.comm, dht)
         else:
             dw = _deliver_wgrad(w, dh.t() @ x2) if ctx.needs_input_grad[1] else None
             dx = all_reduce_(dh @ w, ctx.comm) if ctx.needs_input_grad[0] else None

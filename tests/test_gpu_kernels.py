@@ -1,6 +1,10 @@
 """Single-rank numerics of the HIP kernels vs plain PyTorch fp32 references."""
+import os
+
 import pytest
 import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 pytestmark = pytest.mark.gpu
 
@@ -196,10 +200,25 @@ def test_transpose_and_interleave():
         torch.testing.assert_close(deinterleave_lastaxis(inter, 4), st)
 
 
+@pytest.mark.parametrize("kind", ["lds", "reg"])
 @pytest.mark.parametrize("R,C", [(8, 8), (520, 72), (4096, 1032), (1000, 16), (24, 4104)])
-def test_transpose_vectorized(R, C):
-    """16-B register-transpose kernel (R, C % 8 == 0): partial workgroups in both
-    dimensions, a strided source view, against torch."""
+def test_transpose_vectorized(R, C, kind):
+    """16-B transpose kernels (R, C % 8 == 0), LDS tile and register transpose (picked by
+    CCMPI_TRANSPOSE at the first call in a process: the reg case runs in a child):
+    partial workgroups in both dimensions, a strided source view, against torch."""
+    if kind == "reg":
+        import subprocess
+        import sys
+
+        code = (f"import torch, tests.test_gpu_kernels as t; t._transpose_check({R}, {C})")
+        env = {**os.environ, "CCMPI_TRANSPOSE": "reg"}
+        r = subprocess.run([sys.executable, "-c", code], cwd=REPO, env=env, capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0, r.stderr[-2000:]
+        return
+    _transpose_check(R, C)
+
+
+def _transpose_check(R, C):
     from collective_communication_mpi_amd.ops import transpose
 
     x = torch.randn(R, C + 8, device="cuda").bfloat16()[:, :C]
@@ -668,6 +687,21 @@ def _swiglu_epilogue_check(M, N, K, gemm_nt_swiglu):
     hf = h.float()
     ref = torch.nn.functional.silu(hf[:, 0::2]) * hf[:, 1::2]
     torch.testing.assert_close(glu.float(), ref, rtol=1.6e-2, atol=1e-2)
+
+
+@pytest.mark.parametrize("T,k", [(8, 4), (4096, 1024), (200, 36), (72, 1000)])
+def test_swiglu_pairs_backward_transposed(T, k):
+    """The SwiGLU backward that also writes dh^T (for dW on the N-layout ring): both outputs
+    bitwise equal to the plain kernel's dh and its transpose; partial tiles both ways."""
+    from collective_communication_mpi_amd.ops import swiglu_pairs_backward
+
+    g = torch.Generator(device="cuda").manual_seed(T + k)
+    h = torch.randn(T, 2 * k, device="cuda", generator=g).bfloat16()
+    da = torch.randn(T, k, device="cuda", generator=g).bfloat16()
+    ref = swiglu_pairs_backward(h, da)
+    dh, dht = swiglu_pairs_backward(h, da, transposed=True)
+    torch.testing.assert_close(dh, ref, rtol=0, atol=0)
+    torch.testing.assert_close(dht, ref.T, rtol=0, atol=0)
 
 
 def test_swiglu_pairs_fwd_bwd():
