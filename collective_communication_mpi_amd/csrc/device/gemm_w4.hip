@@ -615,7 +615,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t op_rsrc_t(const uint16_t* X, i
 // p+1 landed everywhere, slot p free).
 template <int EPI, int PERSIST, int ABL = 0, int STAMP = 0, int TA = 0, int TB = 0, int PS = 0, int PAIR = 0>
 __global__ void __launch_bounds__(WNT, 1) k_gemm_w4r(W4Args wa) {
-  static_assert(!PAIR || (!ABL && !STAMP && !TA && !TB && !PS), "pair-slot ring: N layout only");
+  static_assert(!PAIR || (!ABL && !STAMP && !TA && !PS), "pair-slot ring: N-layout A");
   const GemmArgs& g = wa.g;
   extern __shared__ __attribute__((aligned(1024))) unsigned char smem[];
   const int tiles_n = (g.N + WNB - 1) / WNB, tiles_m = (g.M + WM - 1) / WM;
@@ -747,18 +747,51 @@ __global__ void __launch_bounds__(WNT, 1) k_gemm_w4r(W4Args wa) {
   const int pch = ((lane & 7) ^ (((wave & 1) * 4 + (lane >> 4)) & 7)) << 4;
   const int pva = (wave * 8 + (lane >> 3)) * g.lda * 2 + pch, pvb = (wave * 8 + (lane >> 3)) * g.ldb * 2 + pch;
   const int psa = 32 * g.lda * 2, psb = 32 * g.ldb * 2;  // piece stride: 32 rows
+  // PAIR + TB (dX = dY W): the B half of a pair slot holds the pair's two K-steps in the
+  // K-major layout of the 4-slot ring ([32 k][256 rows], 512-B k-rows -- already whole
+  // lines), step h at + h * 16 KiB.  Every DMA piece is then inline asm (M0 + load) and the
+  // transposed B reads use the builtin, which the compiler tracks: with no builtin LDS-DMA
+  // in the kernel it adds no vmcnt(0) before them, and no manual lgkmcnt is needed.
+  auto dma_asm = [&](unsigned char* dst, __amdgpu_buffer_rsrc_t rs, int vo, int so) {
+    const uint32_t m0v = (uint32_t)(uintptr_t)(lds_vptr)dst;
+    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
+                 :
+                 : "s"(m0v), "v"(vo), "s"(rs), "s"(so)
+                 : "memory", "m0");
+  };
   auto dma_pair = [&](int p, int i) {  // piece i of pair p: 0..7 A, 8..15 B
     const bool isa = i < 8;
-    unsigned char* dst = smem + (p & 1) * kPair + (isa ? 0 : kPairHalf) + (i & 7) * 4096 + wave * 1024;
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(isa ? ra : rb, (lds_vptr)dst, 16, (isa ? pva : pvb) + p * 128,
-                                             (i & 7) * (isa ? psa : psb), 0, 0);
+    unsigned char* slot = smem + (p & 1) * kPair;
+    if constexpr (TB) {
+      if (isa) {
+        dma_asm(slot + (i & 7) * 4096 + wave * 1024, ra, pva + p * 128, (i & 7) * psa);
+      } else {  // K-major B: step 2 p + h, piece j of its 16 KiB (the 4-slot ring's layout)
+        const int j = (i - 8) & 3, h = (i - 8) >> 2;
+        dma_asm(slot + kPairHalf + h * 16384 + j * 4096 + wave * 1024, rb, ((j & 1) ? tb1 : tb0) + (2 * p + h) * kb,
+                j == 0 ? 0 : j == 1 ? sb1 : j == 2 ? sb2 : sb3);
+      }
+    } else {
+      unsigned char* dst = slot + (isa ? 0 : kPairHalf) + (i & 7) * 4096 + wave * 1024;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(isa ? ra : rb, (lds_vptr)dst, 16, (isa ? pva : pvb) + p * 128,
+                                               (i & 7) * (isa ? psa : psb), 0, 0);
+    }
   };
   // fragment of K-step h (0, 1) of a pair: row (l & 15), logical chunk 4 h + (l >> 4)
   const int prd0 = (lane & 15) * 128 + (((lane >> 4) ^ ((lane & 15) >> 1)) << 4);
   const int prd1 = (lane & 15) * 128 + (((4 + (lane >> 4)) ^ ((lane & 15) >> 1)) << 4);
-  auto rd_pair = [&](const unsigned char* slot, int ro, int grp, int u, bf16x8 (&fa)[8], bf16x8 (&fb)[8]) {
+  auto rd_tb = [&](const unsigned char* half, int r0) {
+    typedef short v4s __attribute__((ext_vector_type(4)));
+    typedef __attribute__((address_space(3))) v4s* lds_v4s;
+    const unsigned char* p = half + tr_base + ((((r0 >> 4) ^ tr_swz)) << 5);
+    const v4s x0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s)(lds_vptr)p);
+    const v4s x1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s)(lds_vptr)(p + 2048));
+    return __builtin_bit_cast(bf16x8, __builtin_shufflevector(x0, x1, 0, 1, 2, 3, 4, 5, 6, 7));
+  };
+  auto rd_pair = [&](const unsigned char* slot, int h, int grp, int u, bf16x8 (&fa)[8], bf16x8 (&fb)[8]) {
     const int r0 = (grp < 4 ? wc : wr) * 128 + (grp & 3) * 32 + u * 16;
-    const bf16x8 v = *reinterpret_cast<const bf16x8*>(slot + (grp < 4 ? kPairHalf : 0) + ro + r0 * 128);
+    bf16x8 v;
+    if (TB && grp < 4) v = rd_tb(slot + kPairHalf + h * 16384, r0);
+    else v = *reinterpret_cast<const bf16x8*>(slot + (grp < 4 ? kPairHalf : 0) + (h ? prd1 : prd0) + r0 * 128);
     if (grp < 4) fb[(grp & 3) * 2 + u] = v;
     else fa[(grp & 3) * 2 + u] = v;
   };
@@ -870,7 +903,7 @@ __global__ void __launch_bounds__(WNT, 1) k_gemm_w4r(W4Args wa) {
                         bf16x8 (&ca)[8], bf16x8 (&cb)[8]) {
     constexpr bool DMA = decltype(dma_c)::value, ODD = decltype(odd_c)::value;
     const unsigned char* slot = smem + ((q >> 1) & 1) * kPair;
-    const int ro = ODD ? prd1 : prd0;
+    const int ro = ODD ? 1 : 0;  // K-step within the pair
     const int np = (q >> 1) + 1;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
@@ -952,8 +985,8 @@ __global__ void __launch_bounds__(WNT, 1) k_gemm_w4r(W4Args wa) {
       // "phase 0": step 0's fragments; phase 1 ends with pair 1 landed
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
-        rd_pair(smem, prd0, i, 0, a0, b0);
-        rd_pair(smem, prd0, i, 1, a0, b0);
+        rd_pair(smem, 0, i, 0, a0, b0);
+        rd_pair(smem, 0, i, 1, a0, b0);
       }
       phase_pair(F{}, T{}, 1, a0, b0, a1, b1);
       for (int p = 1; p + 1 < npair; ++p) {
@@ -1268,6 +1301,8 @@ void launch_gemm_ring(const GemmArgs& g, int ta, int tb, hipStream_t stream, uin
     w4p_attr(reinterpret_cast<const void*>(k_gemm_w4r<1, 1, 0, 0, 0, 0, 0, 1>));
     w4p_attr(reinterpret_cast<const void*>(k_gemm_w4r<2, 1, 0, 0, 0, 0, 0, 1>));
     w4p_attr(reinterpret_cast<const void*>(k_gemm_w4r<0, 0, 0, 0, 0, 0, 0, 2>));
+    w4p_attr(reinterpret_cast<const void*>(k_gemm_w4r<1, 0, 0, 0, 0, 1, 0, 1>));
+    w4p_attr(reinterpret_cast<const void*>(k_gemm_w4r<0, 0, 0, 0, 0, 1, 0, 1>));
     w4p_attr(reinterpret_cast<const void*>(k_gemm_w4r<1, 0, 0, 0, 0, 0, 0, 2>));
     w4p_attr(reinterpret_cast<const void*>(k_gemm_w4r<2, 0, 0, 0, 0, 0, 0, 2>));
     return true;
@@ -1290,6 +1325,11 @@ void launch_gemm_ring(const GemmArgs& g, int ta, int tb, hipStream_t stream, uin
   const bool persist = fast && (sched & 1);
   const int grid = persist ? std::min(ntiles, cus) : ntiles;
   const int abl = (sched >> 5) & 3;
+  if (!ta && tb && (sched & 16384)) {  // dX = dY W: pair-slot ring, N-layout A, K-major B
+    if (fast) hipLaunchKernelGGL((k_gemm_w4r<1, 0, 0, 0, 0, 1, 0, 1>), dim3(ntiles), dim3(WNT), kPairLds, stream, a);
+    else hipLaunchKernelGGL((k_gemm_w4r<0, 0, 0, 0, 0, 1, 0, 1>), dim3(ntiles), dim3(WNT), kPairLds, stream, a);
+    return;
+  }
   if (ta || tb) {  // K-major operands: non-persistent, no diagnostics
     const int v = (ta ? 2 : 0) + (tb ? 1 : 0) + (fast ? 4 : 0);
     switch (v) {
