@@ -1,0 +1,34 @@
+"""CPU checks of the backward GEMM routing rule (ops.kernels._kmajor_via_transpose): which
+K-major GEMMs of the Llama MLP backward go through transposed copies into the N-layout
+pair ring, which stay on the K-major ring, and the CCMPI_KMAJOR_ROUTE switch."""
+import torch
+
+from collective_communication_mpi_amd.ops.kernels import _kmajor_via_transpose
+
+
+def _t(*shape):
+    return torch.empty(*shape, dtype=torch.bfloat16)
+
+
+def test_dw_shapes_take_the_transpose_route(monkeypatch):
+    monkeypatch.delenv("CCMPI_KMAJOR_ROUTE", raising=False)
+    T, d, f = 4096, 4096, 14336
+    # gate|up dW = dh^T X: M = 2f, N = d, K = T
+    assert _kmajor_via_transpose(2 * f, d, T, _t(T, 2 * f), _t(T, d))
+    # down dW = dY^T A: M = d, N = f, K = T
+    assert _kmajor_via_transpose(d, f, T, _t(T, d), _t(T, f))
+
+
+def test_long_k_small_and_ragged_stay_on_the_ring(monkeypatch):
+    monkeypatch.delenv("CCMPI_KMAJOR_ROUTE", raising=False)
+    assert not _kmajor_via_transpose(4096, 4096, 28672, _t(28672, 4096), _t(28672, 4096))  # long K
+    assert not _kmajor_via_transpose(512, 4096, 4096, _t(4096, 512), _t(4096, 4096))  # M < 1024
+    assert not _kmajor_via_transpose(1024, 1024, 1024, _t(1024, 1024), _t(1024, 1024))  # < 2^33 MACs
+    assert not _kmajor_via_transpose(4100, 4096, 4096, _t(4096, 4100), _t(4096, 4096))  # M % 8
+
+
+def test_route_switch(monkeypatch):
+    monkeypatch.setenv("CCMPI_KMAJOR_ROUTE", "ring")
+    assert not _kmajor_via_transpose(28672, 4096, 4096, _t(4096, 28672), _t(4096, 4096))
+    monkeypatch.setenv("CCMPI_KMAJOR_ROUTE", "transpose")
+    assert _kmajor_via_transpose(28672, 4096, 4096, _t(4096, 28672), _t(4096, 4096))
