@@ -40,16 +40,21 @@ def measure_tp_mlp(comm, tokens: int = 4096, d: int = 4096, ffn: int = 14336, it
     gy = (torch.randn(tokens, d, generator=torch.Generator().manual_seed(4)) * 0.01).to(torch.bfloat16).to(dev)
 
     def timed(fn):
+        # back-to-back steps between two synchronisations, as a training loop issues them
+        # (the host queues step i+1 while the GPU runs step i); one synchronised call per
+        # sample measured the host's launch latency too (~0.12 ms on a 1.06 ms forward,
+        # profiles/r4_probe).  Median over 3 rounds of `iters` steps, max over ranks.
         for _ in range(warmup):
             fn()
         ts = []
-        for _ in range(iters):
+        for _ in range(3):
             torch.cuda.synchronize()
             hc.Barrier()
             t0 = time.perf_counter()
-            fn()
+            for _ in range(iters):
+                fn()
             torch.cuda.synchronize()
-            ts.append(time.perf_counter() - t0)
+            ts.append((time.perf_counter() - t0) / iters)
         return hc.allreduce(statistics.median(ts), op=MPI.MAX)
 
     def run(mlp):
