@@ -645,7 +645,11 @@ def dp_phase(args) -> dict:
     from collective_communication_mpi_amd.parallel.llama_dp import measure_ddp_overlap
 
     out = measure_ddp_overlap(comm, layers=args.dp_layers, tokens=args.dp_tokens, vocab=bool(args.dp_vocab),
-                              iters=2, blocks_sweep=[64, 256], verbose=args.verbose)
+                              # CTA budgets of the bucket all-reduces: a CU holding one collective CTA
+                              # cannot start a ring-GEMM workgroup (512-VGPR waves take whole SIMDs),
+                              # so 256 (one per CU) would stall the backward; 32 was best on the
+                              # 2-rank rehearsal (profiles/r4_dp)
+                              iters=2, blocks_sweep=[32, 64, 128], verbose=args.verbose)
     if args.dp_scripted:
         import torch
 
