@@ -188,7 +188,8 @@ def _kmajor_via_transpose(M: int, N: int, K: int, a: torch.Tensor, b: torch.Tens
     if os.environ.get("CCMPI_KMAJOR_ROUTE", "transpose") != "transpose":
         return False
     return (M >= 1024 and N >= 1024 and K <= 16384 and K % 8 == 0 and M % 8 == 0 and N % 8 == 0
-            and M * N * K >= (1 << 33) and a.data_ptr() % 16 == 0 and b.data_ptr() % 16 == 0
+            and M * N * K >= int(os.environ.get("CCMPI_KMAJOR_MIN_MACS", 1 << 33))
+            and a.data_ptr() % 16 == 0 and b.data_ptr() % 16 == 0
             and a.stride(0) % 8 == 0 and b.stride(0) % 8 == 0)
 
 

@@ -579,6 +579,7 @@ class _GateUpSwiGLU(torch.autograd.Function):
         if ctx.mfma and ctx.needs_input_grad[1] and _dh_transposed(h, x2, w, ctx.comm):
             # dh^T from the same kernel: dW = dh^T X on the N-layout pair ring, no transpose pass
             dh, dht = swiglu_pairs_backward(h, da2, transposed=True)
+            CALLS["dh_transposed"] += 1
         else:
             dh = swiglu_pairs_backward(h, da2)
         if ctx.mfma:

@@ -80,6 +80,11 @@ if rel(gd, wd.grad) > tol:
 
 if args.big and args.device == "cuda" and _native.device().gemm_ring_launches() == ring0:
     fails.append("--big: no LDS-ring GEMM launched (the path under test did not run)")
+if args.big and args.device == "cuda" and os.environ.get("CCMPI_KMAJOR_MIN_MACS") == "1":
+    from collective_communication_mpi_amd.parallel import tensor_parallel as _tp  # noqa: E402
+
+    if not _tp.CALLS["dh_transposed"]:
+        fails.append("--big: the dW transpose route (dh^T from the SwiGLU backward) did not run")
 
 if args.device == "cuda" and p > 1 and not args.big:
     # every row-parallel mode through the whole block (forward + backward), its path
