@@ -187,7 +187,8 @@ def _kmajor_via_transpose(M: int, N: int, K: int, a: torch.Tensor, b: torch.Tens
     transposed weight copy + the pair ring measured no faster (profiles/r4_bwd)."""
     if os.environ.get("CCMPI_KMAJOR_ROUTE", "transpose") != "transpose":
         return False
-    return (M >= 1024 and N >= 1024 and K <= 16384 and K % 8 == 0 and M % 8 == 0 and N % 8 == 0
+    dmin = int(os.environ.get("CCMPI_KMAJOR_MIN_DIM", 1024))  # (tests lower both thresholds)
+    return (M >= dmin and N >= dmin and K <= 16384 and K % 8 == 0 and M % 8 == 0 and N % 8 == 0
             and M * N * K >= int(os.environ.get("CCMPI_KMAJOR_MIN_MACS", 1 << 33))
             and a.data_ptr() % 16 == 0 and b.data_ptr() % 16 == 0
             and a.stride(0) % 8 == 0 and b.stride(0) % 8 == 0)

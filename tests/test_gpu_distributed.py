@@ -252,11 +252,18 @@ def test_bench_tuning_table_drives_auto(tmp_path):
     assert "tune OK" in r.stdout
 
 
-def test_llama_ddp_gradient_sinks_gpu():
+@pytest.mark.parametrize("route", ["default", "transpose_all"])
+def test_llama_ddp_gradient_sinks_gpu(route):
     """BASELINE config 5's machinery on a tiny Llama: DDP over 2 ranks with the TP layers'
     dW GEMMs writing straight into the buckets (gradient sinks), vs the mean of replica
-    gradients; then measure_ddp_overlap's compute / comm / overlapped record."""
-    r = run_ranks(2, py("tests/workers/llama_dp_worker.py", "--device", "cuda", "--measure"), timeout=300, env=ENV)
+    gradients; then measure_ddp_overlap's compute / comm / overlapped record.
+    ``transpose_all``: every dW takes the transposed route into the pair ring (the sink's
+    1/p alpha and bucket view as its output), as the full-size model's do."""
+    env = dict(ENV)
+    if route == "transpose_all":
+        env.update({"CCMPI_SHARED_RING": "1", "CCMPI_RING_MIN_MACS": "1", "CCMPI_KMAJOR_MIN_MACS": "1",
+                    "CCMPI_KMAJOR_MIN_DIM": "8"})
+    r = run_ranks(2, py("tests/workers/llama_dp_worker.py", "--device", "cuda", "--measure"), timeout=300, env=env)
     assert "llama dp OK" in r.stdout
 
 
