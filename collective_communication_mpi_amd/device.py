@@ -269,9 +269,10 @@ class DeviceGroup:
         # must leave CUs free: a bucket all-reduce of 256 CTAs (one per CU) beside the
         # other rank's backward blocked every GEMM workgroup of that rank, so the peer
         # never arrived -- 60 s device timeout, then both processes' queues were torn down
-        # (hipErrorIllegalAddress, profiles/r4_dp).  Half the CUs at most; no bound when
-        # every rank owns its GPU (its peers progress on their own devices).
-        self.overlap_cap = max(1, _cu_count(self.device) // 2) if self.shared_device else self.max_blocks
+        # (hipErrorIllegalAddress, profiles/r4_dp).  All sharing ranks together on half
+        # the CUs at most; no bound when every rank owns its GPU (its peers progress on
+        # their own devices).
+        self.overlap_cap = self._shared_cap() if self.shared_device else self.max_blocks
         self.overlap_blocks = min(self.overlap_blocks, self.overlap_cap)
         if scratch_bytes is None:
             scratch_bytes = _env_int("CCMPI_SCRATCH_MB", 64 if self.shared_device else 512) << 20
