@@ -372,9 +372,12 @@ class _RowParallelFn(torch.autograd.Function):
         g2 = g.reshape(-1, g.shape[-1]).contiguous()
         dx = dw = db = None
         if ctx.mfma and g2.dtype == torch.bfloat16:
-            dx, _ = _linear_backward(g2, x2, w, ctx.needs_input_grad[0], False, ctx.comm)
-            if ctx.needs_input_grad[1]:
-                dw = _wgrad(g2, x2, w, ctx.comm)
+            if ctx.needs_input_grad[0] and ctx.needs_input_grad[1] and _concurrent_ok(g2, ctx.comm):
+                dx, dw = _concurrent_dx_dw(g2, x2, w, ctx.comm)
+            else:
+                dx, _ = _linear_backward(g2, x2, w, ctx.needs_input_grad[0], False, ctx.comm)
+                if ctx.needs_input_grad[1]:
+                    dw = _wgrad(g2, x2, w, ctx.comm)
         else:
             if ctx.needs_input_grad[0]:
                 dx = g2 @ w
@@ -385,6 +388,36 @@ class _RowParallelFn(torch.autograd.Function):
         if ctx.has_bias and ctx.needs_input_grad[2]:
             db = g2.float().sum(0).to(g.dtype)
         return dx, dw, db, None, None
+
+
+_SIDE_STREAMS: dict = {}
+
+
+def _concurrent_ok(g2: torch.Tensor, comm) -> bool:
+    """dX and dW of a row-parallel layer on two streams (CCMPI_TP_BWD_CONCURRENT, default
+    on): CUDA, the ring GEMMs on (a GPU of its own, or CCMPI_SHARED_RING), no graph capture."""
+    return (g2.is_cuda and os.environ.get("CCMPI_TP_BWD_CONCURRENT", "1") == "1" and not _gpu_shared(comm)
+            and not torch.cuda.is_current_stream_capturing())
+
+
+def _concurrent_dx_dw(g2: torch.Tensor, x2: torch.Tensor, w: torch.Tensor, comm):
+    """dW = dY^T X on a second stream beside dX = dY W.  Two independent GEMMs whose last
+    waves of tiles would each leave CUs idle (the Llama down projection: 896 tiles = 3.5
+    waves of 256 workgroups) fill each other's tails.  A DDP gradient sink in dW records its
+    bucket's ready event on that stream, so the bucket all-reduce still follows the GEMM."""
+    cur = torch.cuda.current_stream(g2.device)
+    side = _SIDE_STREAMS.get(g2.device)
+    if side is None:
+        side = _SIDE_STREAMS[g2.device] = torch.cuda.Stream(device=g2.device)
+    side.wait_stream(cur)
+    with torch.cuda.stream(side):
+        dw = _wgrad(g2, x2, w, comm)
+    dx, _ = _linear_backward(g2, x2, w, True, False, comm)
+    cur.wait_stream(side)
+    if dw is not None:
+        dw.record_stream(cur)
+    CALLS["row_bwd_concurrent"] += 1
+    return dx, dw
 
 
 def _column_backward(g2: torch.Tensor, x2: torch.Tensor, w: torch.Tensor, need_dx: bool, need_dw: bool, comm,
