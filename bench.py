@@ -264,6 +264,10 @@ def supervise(args) -> int:
                    CCMPI_LOCAL_SIZE=os.environ.get("LOCAL_WORLD_SIZE", os.environ.get("CCMPI_LOCAL_SIZE", str(size))),
                    LOCAL_RANK=str(local), CCMPI_JOBID=f"{job}-{phase}", CCMPI_BENCH_WORKER="1",
                    CCMPI_TUNE_FILE=tune_file)
+        if phase in ("mlp", "dp"):
+            # ranks sharing a GPU (a rehearsal) keep the ring GEMMs an 8-GPU run uses, every
+            # collective held within half the CUs (device.py); one rank per GPU: no effect
+            env.setdefault("CCMPI_SHARED_RING", "1")
         pp = env.get("PYTHONPATH", "")
         env["PYTHONPATH"] = REPO + (os.pathsep + pp if pp else "")
         cmd = [sys.executable, os.path.abspath(__file__), *argv, "--phase", phase,
