@@ -1,11 +1,11 @@
-"""LDS-ring NT GEMM phase placements vs hipBLASLt on the Llama-3-8B MLP shapes.
+"""LDS-ring NT GEMM variants vs hipBLASLt on the Llama-3-8B MLP shapes.
 
-    python benchmarks/gemm_ps_ab.py [--rounds 5] [--scheds 8,1032]
+    python benchmarks/gemm_ps_ab.py [--rounds 5] [--scheds 8,16392]
 
-Variants (``gemm_set_ring_sched``; bit 0 persistent grid, bit 10 the reads-then-DMA
-phase placement PS 1) and hipBLASLt (torch.matmul) are timed in interleaved rounds in
-one process (median of per-round medians), bf16 in / out, uniform random operands.
-One JSON line per shape."""
+Variants (``gemm_set_ring_sched``: bit 3 the ring, bit 14 pair slots, bit 0 persistent
+grid, bit 15 long K on the ring too, bit 13 the whole-line ablation) and hipBLASLt
+(torch.matmul) are timed in interleaved rounds in one process (median of per-round
+medians), bf16 in / out, uniform random operands.  One JSON line per shape."""
 import argparse
 import json
 import os
@@ -36,7 +36,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--rounds", type=int, default=5)
 ap.add_argument("--iters", type=int, default=20)
 ap.add_argument("--shapes", default=",".join(SHAPES))
-ap.add_argument("--scheds", default="8,1032")
+ap.add_argument("--scheds", default="8,16392")
 args = ap.parse_args()
 D = _native.device()
 scheds = [int(v) for v in args.scheds.split(",")]

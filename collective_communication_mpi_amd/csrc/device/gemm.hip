@@ -1195,7 +1195,7 @@ void register_gemm_ops(pybind11::module_& m) {
         "gemm_nt auto: LDS-ring kernel from this many multiply-adds up (0 = never)");
   m.def("gemm_ring_launches", [] { return g_ring_launches; }, "LDS-ring GEMM launches so far (this process)");
   m.def("gemm_set_ring_sched", [](int v) { g_ring_sched = v; },
-        "auto-dispatched LDS-ring kernel variant: bit 0 persistent, bit 10 reads-then-DMA phase (PS 1)");
+        "auto-dispatched LDS-ring kernel variant: bit 3 ring, bit 14 pair slots (default), bit 0 persistent, bit 15 long K too; diagnostics: bits 5-6 / 13 ablations, bit 9 stamps");
   m.def("gemm_set_w4_group_m", [](int v) { g_w4_group_m = v > 0 ? v : 8; }, "four-wave kernel group-M rows");
   m.def("gemm_set_ablation", [](int e) {
     g_pp_exp = e;

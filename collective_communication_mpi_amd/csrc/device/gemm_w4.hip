@@ -597,25 +597,19 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t op_rsrc_t(const uint16_t* X, i
 // operands).  A K-major slot half is [32 k][256 rows] with 512-B k-rows whose 32-B
 // granules are XOR-swizzled by tn_swz(k) (the 256x256 TN kernel's scheme, gemm256.hip);
 // its fragments come out of two ds_read_b64_tr_b16 each.
-// PS (N layout only): placement of a phase's fragment reads and DMA pieces between its 64
-// MFMAs.  0: per 8 MFMAs one read, one DMA piece, one read (interleaved).  1: the 16 reads
-// over the first 32 MFMAs, the 8 DMA pieces over the last 32 -- the LDS-DMA issue kept
-// away from the ds_reads, as hipBLASLt's MT256x256x64 loop places them (an LDS-DMA piece
-// costs 100-185 cycles to issue inside a phase already carrying reads, 25-60 in a
-// read-free stretch: MI355X_MICROARCH.md, per-instruction constants); measured no faster
-// (profiles/r4_gemm).  2: PS 0 with the odd waves one MFMA later (hipBLASLt runs two
-// copies of its loop, picked by the SIMD id, whose DMA / read slots differ by one MFMA).
-// 3: PS 0 with the DMA pieces' LDS addresses as one M0 chain (dma_chain).
-// PAIR (N layout, non-persistent, no diagnostics): the pair-slot ring.  Each DMA piece
+// (Phase placements tried and measured no faster -- reads first / DMA last, odd waves one
+// MFMA later, one M0 chain per phase, and for the pair ring front-loaded DMA -- were
+// removed; their A/B records: profiles/r4_gemm, profiles/r4_pair2.)
+// PAIR (N-layout A; B N-layout or K-major; no diagnostics): the pair-slot ring.  Each DMA piece
 // reads 8 whole 128-B lines (8 rows x 64 k) instead of 16 half lines: the 16 x 64-B
 // pieces of the 4-slot ring cost 13-16 % against hipBLASLt (profiles/r4_gemm, ABL bit 2
 // ablation).  Two slots of one K pair each (kPair): phase q computes step q-1 and reads
 // step q from slot (q >> 1) & 1; even phase 2p issues the 16 pieces of pair p+1 into the
 // other slot, whose last reader was phase 2p-1; only odd phases end in a barrier (pair
 // p+1 landed everywhere, slot p free).
-template <int EPI, int PERSIST, int ABL = 0, int STAMP = 0, int TA = 0, int TB = 0, int PS = 0, int PAIR = 0>
+template <int EPI, int PERSIST, int ABL = 0, int STAMP = 0, int TA = 0, int TB = 0, int PAIR = 0>
 __global__ void __launch_bounds__(WNT, 1) k_gemm_w4r(W4Args wa) {
-  static_assert(!PAIR || (!ABL && !STAMP && !TA && !PS), "pair-slot ring: N-layout A");
+  static_assert(!PAIR || (!ABL && !STAMP && !TA), "pair-slot ring: N-layout A");
   const GemmArgs& g = wa.g;
   extern __shared__ __attribute__((aligned(1024))) unsigned char smem[];
   const int tiles_n = (g.N + WNB - 1) / WNB, tiles_m = (g.M + WM - 1) / WM;
@@ -686,26 +680,6 @@ __global__ void __launch_bounds__(WNT, 1) k_gemm_w4r(W4Args wa) {
     }
   };
   auto dma = [&](int s, int i) { dma_piece(dma_step(s), i); };
-  // PS 3 (N layout): the LDS-DMA pieces of a step as one M0 chain -- M0 is set once per
-  // phase and advanced right after each piece, so no piece waits on a just-written M0
-  // (the builtin emits s_mov m0 + s_nop 0 in front of every piece)
-  auto dma_m0_set = [&](const DmaStep& d) {
-    const uint32_t m0v = (uint32_t)(uintptr_t)(lds_vptr)d.lds;
-    asm volatile("s_mov_b32 m0, %0" : : "s"(m0v) : "memory", "m0");
-  };
-  auto dma_chain = [&](const DmaStep& d, int i) {
-    const bool isa = i < 4;
-    const int so = isa ? (i == 0 ? 0 : i == 1 ? sa1 : i == 2 ? sa2 : sa3)
-                       : (i == 4 ? 0 : i == 5 ? sb1 : i == 6 ? sb2 : sb3);
-    const int vo = isa ? d.va : d.vb;
-    // next piece's LDS address: +4 KiB, except A piece 3 -> B piece 0 (the B half)
-    if (i == 3)
-      asm volatile("buffer_load_dwordx4 %0, %1, %2 offen lds\n\ts_add_u32 m0, m0, %3"
-                   : : "v"(vo), "s"(ra), "s"(so), "i"(kRingHalf - 3 * 4096) : "memory", "m0");
-    else
-      asm volatile("buffer_load_dwordx4 %0, %1, %2 offen lds\n\ts_add_u32 m0, m0, 0x1000"
-                   : : "v"(vo), "s"(isa ? ra : rb), "s"(so) : "memory", "m0");
-  };
   // fragment (16x16x32): lane l reads row (l & 15) of a 16-row block, logical chunk l >> 4;
   // the physical chunk depends on the lane only (block rows are multiples of 16)
   const int rdo = (lane & 15) * 64 + (((lane >> 4) ^ ring_swz((lane >> 2) & 3)) << 4);
@@ -805,11 +779,10 @@ __global__ void __launch_bounds__(WNT, 1) k_gemm_w4r(W4Args wa) {
 
   // one phase: MFMAs on (pa, pb) = step q-1, reads of step q into (ca, cb), DMA of step
   // q+3 (DMA), one non-MFMA op per gap: MFMA | read | 2 MFMA | DMA | 2 MFMA | read | 3 MFMA
-  auto phase = [&](auto dma_c, auto younger_c, auto shift_c, int q, const bf16x8 (&pa)[8], const bf16x8 (&pb)[8],
+  auto phase = [&](auto dma_c, auto younger_c, int q, const bf16x8 (&pa)[8], const bf16x8 (&pb)[8],
                    bf16x8 (&ca)[8], bf16x8 (&cb)[8]) {
     constexpr bool DMA = decltype(dma_c)::value;
     constexpr int YOUNGER = decltype(younger_c)::value;
-    constexpr bool SHIFT = decltype(shift_c)::value;
     const DmaStep ds = dma_step(q + 3);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
@@ -830,45 +803,6 @@ __global__ void __launch_bounds__(WNT, 1) k_gemm_w4r(W4Args wa) {
         mm(3, 8);
         if constexpr (!(ABL & 2)) rd1(q, 4 + (i >> 1), i & 1, ca, cb);  // A block i
         __builtin_amdgcn_sched_barrier(0);
-      } else if constexpr (PS == 1) {
-        // MFMA m = 8 i + j: read r = m / 2 after odd m < 32, DMA piece (m - 33) / 4 after
-        // m = 33, 37, .., 61
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          mm(j, j + 1);
-          const int m = 8 * i + j;
-          if (m < 32 && (m & 1)) {
-            if constexpr (!(ABL & 2)) rd1(q, m >> 2, (m >> 1) & 1, ca, cb);
-          } else if (m >= 33 && ((m - 33) & 3) == 0) {
-            if constexpr (DMA && !(ABL & 1)) dma_piece(ds, (m - 33) >> 2);
-          }
-          __builtin_amdgcn_sched_barrier(0);
-        }
-      } else if constexpr (PS == 3) {
-        if (i == 0 && DMA && !(ABL & 1)) dma_m0_set(ds);
-        mm(0, 1);
-        if constexpr (!(ABL & 2)) rd1(q, i, 0, ca, cb);
-        __builtin_amdgcn_sched_barrier(0);
-        mm(1, 3);
-        if constexpr (DMA && !(ABL & 1)) dma_chain(ds, i);
-        __builtin_amdgcn_sched_barrier(0);
-        mm(3, 5);
-        if constexpr (!(ABL & 2)) rd1(q, i, 1, ca, cb);
-        __builtin_amdgcn_sched_barrier(0);
-        mm(5, 8);
-      } else if constexpr (SHIFT) {
-        // PS 2, odd waves: the same order one MFMA later, so the CU's four waves do not
-        // hand their LDS-DMA pieces and reads to the shared address unit at the same cycle
-        mm(0, 2);
-        if constexpr (!(ABL & 2)) rd1(q, i, 0, ca, cb);
-        __builtin_amdgcn_sched_barrier(0);
-        mm(2, 4);
-        if constexpr (DMA && !(ABL & 1)) dma_piece(ds, i);
-        __builtin_amdgcn_sched_barrier(0);
-        mm(4, 6);
-        if constexpr (!(ABL & 2)) rd1(q, i, 1, ca, cb);
-        __builtin_amdgcn_sched_barrier(0);
-        mm(6, 8);
       } else {
         mm(0, 1);
         if constexpr (!(ABL & 2)) rd1(q, i, 0, ca, cb);
@@ -912,40 +846,17 @@ __global__ void __launch_bounds__(WNT, 1) k_gemm_w4r(W4Args wa) {
         for (int j = j0; j < j1; ++j) mfma(i, j, pa[i], pb[j]);
         __builtin_amdgcn_sched_barrier(0);
       };
-      if constexpr (PAIR == 2) {
-        // front-loaded: the 16 pieces over the first 32 MFMAs (4 per 8), half a phase
-        // more of HBM latency before the odd phase's barrier needs them
-        const bool d = DMA && i < 4;
-        mm(0, 1);
-        if (d) dma_pair(np, 4 * i);
-        rd_pair(slot, ro, i, 0, ca, cb);
-        __builtin_amdgcn_sched_barrier(0);
-        mm(1, 3);
-        if (d) dma_pair(np, 4 * i + 1);
-        __builtin_amdgcn_sched_barrier(0);
-        mm(3, 4);
-        if (d) dma_pair(np, 4 * i + 2);
-        __builtin_amdgcn_sched_barrier(0);
-        mm(4, 5);
-        rd_pair(slot, ro, i, 1, ca, cb);
-        __builtin_amdgcn_sched_barrier(0);
-        mm(5, 7);
-        if (d) dma_pair(np, 4 * i + 3);
-        __builtin_amdgcn_sched_barrier(0);
-        mm(7, 8);
-      } else {
-        mm(0, 1);
-        if constexpr (DMA) dma_pair(np, 2 * i);
-        rd_pair(slot, ro, i, 0, ca, cb);
-        __builtin_amdgcn_sched_barrier(0);
-        mm(1, 3);
-        if constexpr (DMA) dma_pair(np, 2 * i + 1);
-        __builtin_amdgcn_sched_barrier(0);
-        mm(3, 5);
-        rd_pair(slot, ro, i, 1, ca, cb);
-        __builtin_amdgcn_sched_barrier(0);
-        mm(5, 8);
-      }
+      mm(0, 1);
+      if constexpr (DMA) dma_pair(np, 2 * i);
+      rd_pair(slot, ro, i, 0, ca, cb);
+      __builtin_amdgcn_sched_barrier(0);
+      mm(1, 3);
+      if constexpr (DMA) dma_pair(np, 2 * i + 1);
+      __builtin_amdgcn_sched_barrier(0);
+      mm(3, 5);
+      rd_pair(slot, ro, i, 1, ca, cb);
+      __builtin_amdgcn_sched_barrier(0);
+      mm(5, 8);
     }
     if constexpr (ODD) ring_wait_barrier_c<0>();
   };
@@ -1024,19 +935,15 @@ __global__ void __launch_bounds__(WNT, 1) k_gemm_w4r(W4Args wa) {
     // steady state: phases 1 .. nst-4 in pairs, each prefetching the step three ahead
     // (K-major variants: one A set, a1 aliases a0)
     bf16x8 (&a1r)[8] = (TA || TB) ? a0 : a1;
-    auto body = [&](auto sh) {
-      for (int q = 1; q + 3 < nst; q += 2) {
-        phase(T{}, Y16{}, sh, q, a0, b0, a1r, b1);
-        phase(T{}, Y16{}, sh, q + 1, a1r, b1, a0, b0);
-      }
-      if (nst >= 4) {  // drain: phases nst-3, nst-2, nst-1
-        phase(F{}, Y8{}, sh, nst - 3, a0, b0, a1r, b1);
-        phase(F{}, Y0{}, sh, nst - 2, a1r, b1, a0, b0);
-      }
-      phase(F{}, Y0{}, sh, nst - 1, a0, b0, a1r, b1);
-    };
-    if (PS == 2 && !(TA || TB) && (wave & 1)) body(T{});
-    else body(F{});
+    for (int q = 1; q + 3 < nst; q += 2) {
+      phase(T{}, Y16{}, q, a0, b0, a1r, b1);
+      phase(T{}, Y16{}, q + 1, a1r, b1, a0, b0);
+    }
+    if (nst >= 4) {  // drain: phases nst-3, nst-2, nst-1
+      phase(F{}, Y8{}, nst - 3, a0, b0, a1r, b1);
+      phase(F{}, Y0{}, nst - 2, a1r, b1, a0, b0);
+    }
+    phase(F{}, Y0{}, nst - 1, a0, b0, a1r, b1);
     // persistent, fast epilogue: every wave is past its last fragment read (the last
     // phase's barrier), so slots 0..2 are free -- the next tile's first three steps load
     // into them under the last MFMAs and the epilogue (which uses slot 3 only)
@@ -1270,6 +1177,7 @@ void launch_gemm_ring(const GemmArgs& g, int ta, int tb, hipStream_t stream, uin
     return hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0 ? n : 256;
   }();
   static bool attr = [] {
+    // 4-slot ring: generic / fast / persistent / SwiGLU epilogues, diagnostics, K-major forms
     w4r_attr(reinterpret_cast<const void*>(k_gemm_w4r<0, 0>));
     w4r_attr(reinterpret_cast<const void*>(k_gemm_w4r<1, 0>));
     w4r_attr(reinterpret_cast<const void*>(k_gemm_w4r<1, 1>));
@@ -1277,6 +1185,7 @@ void launch_gemm_ring(const GemmArgs& g, int ta, int tb, hipStream_t stream, uin
     w4r_attr(reinterpret_cast<const void*>(k_gemm_w4r<1, 0, 1>));
     w4r_attr(reinterpret_cast<const void*>(k_gemm_w4r<1, 0, 2>));
     w4r_attr(reinterpret_cast<const void*>(k_gemm_w4r<1, 0, 3>));
+    w4r_attr(reinterpret_cast<const void*>(k_gemm_w4r<1, 0, 4>));
     w4r_attr(reinterpret_cast<const void*>(k_gemm_w4r<1, 0, 0, 1>));
     w4r_attr(reinterpret_cast<const void*>(k_gemm_w4r<1, 1, 0, 1>));
     w4r_attr(reinterpret_cast<const void*>(k_gemm_w4r<0, 0, 0, 0, 0, 1>));
@@ -1285,52 +1194,36 @@ void launch_gemm_ring(const GemmArgs& g, int ta, int tb, hipStream_t stream, uin
     w4r_attr(reinterpret_cast<const void*>(k_gemm_w4r<1, 0, 0, 0, 1, 1>));
     w4r_attr(reinterpret_cast<const void*>(k_gemm_w4r<0, 0, 0, 0, 1, 0>));
     w4r_attr(reinterpret_cast<const void*>(k_gemm_w4r<1, 0, 0, 0, 1, 0>));
-    w4r_attr(reinterpret_cast<const void*>(k_gemm_w4r<1, 0, 0, 0, 0, 0, 1>));
-    w4r_attr(reinterpret_cast<const void*>(k_gemm_w4r<1, 1, 0, 0, 0, 0, 1>));
-    w4r_attr(reinterpret_cast<const void*>(k_gemm_w4r<2, 0, 0, 0, 0, 0, 1>));
-    w4r_attr(reinterpret_cast<const void*>(k_gemm_w4r<1, 0, 0, 1, 0, 0, 1>));
-    w4r_attr(reinterpret_cast<const void*>(k_gemm_w4r<1, 0, 0, 0, 0, 0, 2>));
-    w4r_attr(reinterpret_cast<const void*>(k_gemm_w4r<1, 1, 0, 0, 0, 0, 2>));
-    w4r_attr(reinterpret_cast<const void*>(k_gemm_w4r<2, 1, 0, 0, 0, 0, 0>));
-    w4r_attr(reinterpret_cast<const void*>(k_gemm_w4r<1, 0, 0, 0, 0, 0, 3>));
-    w4r_attr(reinterpret_cast<const void*>(k_gemm_w4r<1, 0, 4>));
-    w4r_attr(reinterpret_cast<const void*>(k_gemm_w4r<2, 0, 0, 0, 0, 0, 3>));
-    w4p_attr(reinterpret_cast<const void*>(k_gemm_w4r<0, 0, 0, 0, 0, 0, 0, 1>));
-    w4p_attr(reinterpret_cast<const void*>(k_gemm_w4r<1, 0, 0, 0, 0, 0, 0, 1>));
-    w4p_attr(reinterpret_cast<const void*>(k_gemm_w4r<2, 0, 0, 0, 0, 0, 0, 1>));
-    w4p_attr(reinterpret_cast<const void*>(k_gemm_w4r<1, 1, 0, 0, 0, 0, 0, 1>));
-    w4p_attr(reinterpret_cast<const void*>(k_gemm_w4r<2, 1, 0, 0, 0, 0, 0, 1>));
-    w4p_attr(reinterpret_cast<const void*>(k_gemm_w4r<0, 0, 0, 0, 0, 0, 0, 2>));
-    w4p_attr(reinterpret_cast<const void*>(k_gemm_w4r<1, 0, 0, 0, 0, 1, 0, 1>));
-    w4p_attr(reinterpret_cast<const void*>(k_gemm_w4r<0, 0, 0, 0, 0, 1, 0, 1>));
-    w4p_attr(reinterpret_cast<const void*>(k_gemm_w4r<1, 0, 0, 0, 0, 0, 0, 2>));
-    w4p_attr(reinterpret_cast<const void*>(k_gemm_w4r<2, 0, 0, 0, 0, 0, 0, 2>));
+    // pair-slot ring
+    w4p_attr(reinterpret_cast<const void*>(k_gemm_w4r<0, 0, 0, 0, 0, 0, 1>));
+    w4p_attr(reinterpret_cast<const void*>(k_gemm_w4r<1, 0, 0, 0, 0, 0, 1>));
+    w4p_attr(reinterpret_cast<const void*>(k_gemm_w4r<2, 0, 0, 0, 0, 0, 1>));
+    w4p_attr(reinterpret_cast<const void*>(k_gemm_w4r<1, 1, 0, 0, 0, 0, 1>));
+    w4p_attr(reinterpret_cast<const void*>(k_gemm_w4r<2, 1, 0, 0, 0, 0, 1>));
+    w4p_attr(reinterpret_cast<const void*>(k_gemm_w4r<0, 0, 0, 0, 0, 1, 1>));
+    w4p_attr(reinterpret_cast<const void*>(k_gemm_w4r<1, 0, 0, 0, 0, 1, 1>));
     return true;
   }();
   (void)attr;
   const int ntiles = gemm_w4_tiles(g.M, g.N);
   W4Args a{g, g_w4_group_m, {}, g_w4_dbg, glu, ldglu};
   const bool fast = gemm_w4r_fast(g);
+  const bool pair = sched & 16384;
+  const bool persist = fast && (sched & 1);
+  const int grid = persist ? std::min(ntiles, cus) : ntiles;
   if (glu) {  // SwiGLU epilogue (callers check gemm_w4r_fast and the glu layout first)
     if (!fast || ta || tb) throw std::invalid_argument("gemm ring: the SwiGLU epilogue needs the fast NT form");
-    if ((sched & 16384) && (sched & 1)) {
-      hipLaunchKernelGGL((k_gemm_w4r<2, 1, 0, 0, 0, 0, 0, 1>), dim3(std::min(ntiles, cus)), dim3(WNT), kPairLds, stream, a);
-    } else if (sched & 65536) hipLaunchKernelGGL((k_gemm_w4r<2, 0, 0, 0, 0, 0, 0, 2>), dim3(ntiles), dim3(WNT), kPairLds, stream, a);
-    else if (sched & 16384) hipLaunchKernelGGL((k_gemm_w4r<2, 0, 0, 0, 0, 0, 0, 1>), dim3(ntiles), dim3(WNT), kPairLds, stream, a);
-    else if (sched & 4096) hipLaunchKernelGGL((k_gemm_w4r<2, 0, 0, 0, 0, 0, 3>), dim3(ntiles), dim3(WNT), kRingLds, stream, a);
-    else if (sched & 1024) hipLaunchKernelGGL((k_gemm_w4r<2, 0, 0, 0, 0, 0, 1>), dim3(ntiles), dim3(WNT), kRingLds, stream, a);
+    if (pair && persist) hipLaunchKernelGGL((k_gemm_w4r<2, 1, 0, 0, 0, 0, 1>), dim3(grid), dim3(WNT), kPairLds, stream, a);
+    else if (pair) hipLaunchKernelGGL((k_gemm_w4r<2, 0, 0, 0, 0, 0, 1>), dim3(ntiles), dim3(WNT), kPairLds, stream, a);
     else hipLaunchKernelGGL((k_gemm_w4r<2, 0>), dim3(ntiles), dim3(WNT), kRingLds, stream, a);
     return;
   }
-  const bool persist = fast && (sched & 1);
-  const int grid = persist ? std::min(ntiles, cus) : ntiles;
-  const int abl = (sched >> 5) & 3;
-  if (!ta && tb && (sched & 16384)) {  // dX = dY W: pair-slot ring, N-layout A, K-major B
-    if (fast) hipLaunchKernelGGL((k_gemm_w4r<1, 0, 0, 0, 0, 1, 0, 1>), dim3(ntiles), dim3(WNT), kPairLds, stream, a);
-    else hipLaunchKernelGGL((k_gemm_w4r<0, 0, 0, 0, 0, 1, 0, 1>), dim3(ntiles), dim3(WNT), kPairLds, stream, a);
+  if (!ta && tb && pair) {  // dX = dY W: pair-slot ring, N-layout A, K-major B
+    if (fast) hipLaunchKernelGGL((k_gemm_w4r<1, 0, 0, 0, 0, 1, 1>), dim3(ntiles), dim3(WNT), kPairLds, stream, a);
+    else hipLaunchKernelGGL((k_gemm_w4r<0, 0, 0, 0, 0, 1, 1>), dim3(ntiles), dim3(WNT), kPairLds, stream, a);
     return;
   }
-  if (ta || tb) {  // K-major operands: non-persistent, no diagnostics
+  if (ta || tb) {  // K-major operands on the 4-slot ring: non-persistent, no diagnostics
     const int v = (ta ? 2 : 0) + (tb ? 1 : 0) + (fast ? 4 : 0);
     switch (v) {
       case 1: hipLaunchKernelGGL((k_gemm_w4r<0, 0, 0, 0, 0, 1>), dim3(ntiles), dim3(WNT), kRingLds, stream, a); break;
@@ -1342,32 +1235,17 @@ void launch_gemm_ring(const GemmArgs& g, int ta, int tb, hipStream_t stream, uin
     }
     return;
   }
-  if (sched & 65536) {
-    // pair-slot ring, front-loaded DMA
-    if (fast) hipLaunchKernelGGL((k_gemm_w4r<1, 0, 0, 0, 0, 0, 0, 2>), dim3(ntiles), dim3(WNT), kPairLds, stream, a);
-    else hipLaunchKernelGGL((k_gemm_w4r<0, 0, 0, 0, 0, 0, 0, 2>), dim3(ntiles), dim3(WNT), kPairLds, stream, a);
-  } else if (sched & 16384) {
+  const int abl = (sched >> 5) & 3;
+  if (pair) {
     // pair-slot ring: whole-line DMA pieces, 64-deep slots (bit 0: persistent grid)
-    if (persist) hipLaunchKernelGGL((k_gemm_w4r<1, 1, 0, 0, 0, 0, 0, 1>), dim3(grid), dim3(WNT), kPairLds, stream, a);
-    else if (fast) hipLaunchKernelGGL((k_gemm_w4r<1, 0, 0, 0, 0, 0, 0, 1>), dim3(ntiles), dim3(WNT), kPairLds, stream, a);
-    else hipLaunchKernelGGL((k_gemm_w4r<0, 0, 0, 0, 0, 0, 0, 1>), dim3(ntiles), dim3(WNT), kPairLds, stream, a);
+    if (persist) hipLaunchKernelGGL((k_gemm_w4r<1, 1, 0, 0, 0, 0, 1>), dim3(grid), dim3(WNT), kPairLds, stream, a);
+    else if (fast) hipLaunchKernelGGL((k_gemm_w4r<1, 0, 0, 0, 0, 0, 1>), dim3(ntiles), dim3(WNT), kPairLds, stream, a);
+    else hipLaunchKernelGGL((k_gemm_w4r<0, 0, 0, 0, 0, 0, 1>), dim3(ntiles), dim3(WNT), kPairLds, stream, a);
   } else if (!fast) {
     hipLaunchKernelGGL((k_gemm_w4r<0, 0>), dim3(grid), dim3(WNT), kRingLds, stream, a);
-  } else if (sched & 512) {
-    if (sched & 1024) hipLaunchKernelGGL((k_gemm_w4r<1, 0, 0, 1, 0, 0, 1>), dim3(grid), dim3(WNT), kRingLds, stream, a);
-    else if (persist) hipLaunchKernelGGL((k_gemm_w4r<1, 1, 0, 1>), dim3(grid), dim3(WNT), kRingLds, stream, a);
+  } else if (sched & 512) {  // diagnostic: s_memtime stamps
+    if (persist) hipLaunchKernelGGL((k_gemm_w4r<1, 1, 0, 1>), dim3(grid), dim3(WNT), kRingLds, stream, a);
     else hipLaunchKernelGGL((k_gemm_w4r<1, 0, 0, 1>), dim3(grid), dim3(WNT), kRingLds, stream, a);
-  } else if (sched & 4096) {
-    // chained-M0 LDS-DMA (PS 3)
-    hipLaunchKernelGGL((k_gemm_w4r<1, 0, 0, 0, 0, 0, 3>), dim3(grid), dim3(WNT), kRingLds, stream, a);
-  } else if (sched & 2048) {
-    // parity-staggered phase placement (PS 2)
-    if (persist) hipLaunchKernelGGL((k_gemm_w4r<1, 1, 0, 0, 0, 0, 2>), dim3(grid), dim3(WNT), kRingLds, stream, a);
-    else hipLaunchKernelGGL((k_gemm_w4r<1, 0, 0, 0, 0, 0, 2>), dim3(grid), dim3(WNT), kRingLds, stream, a);
-  } else if (sched & 1024) {
-    // reads-then-DMA phase placement (PS 1)
-    if (persist) hipLaunchKernelGGL((k_gemm_w4r<1, 1, 0, 0, 0, 0, 1>), dim3(grid), dim3(WNT), kRingLds, stream, a);
-    else hipLaunchKernelGGL((k_gemm_w4r<1, 0, 0, 0, 0, 0, 1>), dim3(grid), dim3(WNT), kRingLds, stream, a);
   } else if (sched & 8192) {
     // diagnostic: whole-cache-line DMA pieces (ABL 4, wrong results)
     hipLaunchKernelGGL((k_gemm_w4r<1, 0, 4>), dim3(grid), dim3(WNT), kRingLds, stream, a);
