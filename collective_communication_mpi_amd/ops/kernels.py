@@ -65,36 +65,12 @@ def gemm_nt(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None
         if bias.dtype not in (torch.float32, torch.bfloat16) or not bias.is_contiguous() or bias.numel() != N:
             raise ValueError("bias must be a contiguous [N] fp32/bf16 tensor")
         bias_ptr = bias.data_ptr()
-    if (splitk is None and bias is None and act is None and not accumulate and out.dtype == torch.bfloat16
-            and _longk_split(M, N, K)):
-        return _gemm_longk_split(a, b, False, out, alpha)
     if splitk is None:
         fp32_plain = out.dtype == torch.float32 and act is None
         splitk = _auto_splitk(((M + 127) // 128) * ((N + 127) // 128), K) if fp32_plain else 1
     _D().gemm_nt(a.data_ptr(), b.data_ptr(), out.data_ptr(), bias_ptr, M, N, K, a.stride(0), b.stride(0),
                  out.stride(0), float(alpha), bool(accumulate), bias_kind, _ACT[act], out.dtype == torch.bfloat16,
                  int(splitk), _stream(a))
-    return out
-
-
-def _longk_split(M: int, N: int, K: int) -> bool:
-    """Long K over at most one 256x256 tile per CU (CCMPI_LONGK_SPLIT=1): the GEMM runs as two
-    K halves on the pair-slot ring into an fp32 workspace (profiles/r4_longk)."""
-    return (os.environ.get("CCMPI_LONGK_SPLIT", "0") == "1" and K > 16384 and K % 128 == 0 and M >= 1024
-            and N >= 1024 and ((M + 255) // 256) * ((N + 255) // 256) <= 256)
-
-
-def _gemm_longk_split(a: torch.Tensor, b: torch.Tensor, tb: bool, out: torch.Tensor, alpha: float) -> torch.Tensor:
-    """``out (bf16) = alpha * a @ op(b).T`` as two K halves accumulated in fp32 (one rounding
-    to bf16 at the end, as the single GEMM's)."""
-    K = a.shape[1]
-    h = K // 2
-    ws = torch.empty(out.shape, device=out.device, dtype=torch.float32)
-    b0, b1 = (b[:h], b[h:]) if tb else (b[:, :h], b[:, h:])
-    if gemm_ring(a[:, :h], b0, False, tb, out=ws, alpha=alpha) is None or \
-            gemm_ring(a[:, h:], b1, False, tb, out=ws, alpha=alpha, accumulate=True) is None:
-        raise RuntimeError("long-K split: the ring kernel did not apply to the halves")
-    out.copy_(ws)
     return out
 
 
@@ -192,9 +168,6 @@ def gemm_ring(a: torch.Tensor, b: torch.Tensor, ta: bool, tb: bool, out: Optiona
         out = torch.empty((M, N), dtype=out_dtype, device=a.device)
     if out.shape != (M, N) or out.stride(1) != 1 or out.dtype not in (torch.bfloat16, torch.float32):
         raise ValueError("gemm_ring output must be [M, N] bf16/fp32 with unit column stride")
-    if (not ta and tb and not accumulate and out.dtype == torch.bfloat16 and K % 128 == 0 and
-            _longk_split(M, N, K)):
-        return _gemm_longk_split(a, b, True, out, alpha)
     if ta and (a_nt is not None or _kmajor_via_transpose(M, N, K, a, b)):
         # K-major operands transposed first (k_transpose16_v, ~6 TB/s), then the N-layout
         # pair-slot ring: its whole-line DMA pieces and one ds_read_b128 per fragment beat
