@@ -19,6 +19,8 @@
 // the unfused forms of that layout (other GEMM routes) and its backward.
 #include <pybind11/pybind11.h>
 
+#include <cstdlib>
+
 #include "common.hpp"
 #include "gemm_common.hpp"
 #include "ops.hpp"
@@ -125,16 +127,17 @@ __global__ void __launch_bounds__(256) k_swiglu_bwd_il(const uint16_t* __restric
 // a 64-row x 64-column tile of dh per workgroup, written row-major straight away and
 // through an LDS tile (33-word row stride: conflict-free column gathers) transposed,
 // 16-B stores both ways.  T % 8 == 0.
+template <int R>  // rows per tile: 64 or 128
 __global__ void __launch_bounds__(256) k_swiglu_bwd_il_t(const uint16_t* __restrict__ h, const uint16_t* __restrict__ da,
                                                          uint16_t* __restrict__ dh, uint16_t* __restrict__ dht, int T,
                                                          int n, int64_t ldh, int64_t ldda, int64_t lddh, int64_t ldt) {
   constexpr int S = 66;  // LDS row stride, elements
-  __shared__ uint32_t tile[64 * S / 2];
+  __shared__ uint32_t tile[R * S / 2];
   const int t = threadIdx.x;
-  const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
+  const int r0 = blockIdx.y * R, c0 = blockIdx.x * 64;
   const int lr = t >> 3, lc = (t & 7) * 8;
 #pragma unroll
-  for (int hh = 0; hh < 2; ++hh) {
+  for (int hh = 0; hh < R / 32; ++hh) {
     const int row = lr + 32 * hh;
     u32x4 r = u32x4{0u, 0u, 0u, 0u};
     if (r0 + row < T && c0 + lc < n) {
@@ -156,9 +159,11 @@ __global__ void __launch_bounds__(256) k_swiglu_bwd_il_t(const uint16_t* __restr
   }
   __syncthreads();
   const uint16_t* t16 = reinterpret_cast<const uint16_t*>(tile);
+  // dh^T row c0 + oc, columns r0 + 8 q ..: R / 8 lanes per destination row
+  constexpr int QL = R / 8, RPW = 256 / QL;
 #pragma unroll
-  for (int hh = 0; hh < 2; ++hh) {
-    const int oc = lr + 32 * hh, q = t & 7;  // dh^T row c0 + oc, columns r0 + 8 q ..
+  for (int hh = 0; hh < 64 / RPW; ++hh) {
+    const int oc = t / QL + RPW * hh, q = t % QL;
     uint32_t o[4];
 #pragma unroll
     for (int m = 0; m < 4; ++m)
@@ -210,10 +215,16 @@ void register_swiglu_ops(pybind11::module_& m) {
     if (T % 8) throw std::invalid_argument("swiglu_bwd_il_t: T % 8 == 0 required");
     if (T == 0 || k == 0) return;
     const int n = (int)(2 * k);
-    hipLaunchKernelGGL(k_swiglu_bwd_il_t, dim3((n + 63) / 64, (unsigned)((T + 63) / 64)), dim3(256), 0,
-                       reinterpret_cast<hipStream_t>(stream), reinterpret_cast<const uint16_t*>(h),
-                       reinterpret_cast<const uint16_t*>(da), reinterpret_cast<uint16_t*>(dh),
-                       reinterpret_cast<uint16_t*>(dht), (int)T, n, ldh, ldda, lddh, ldt);
+    // 128-row tiles unless CCMPI_SWIGLU_T_ROWS=64 (A/B)
+    static const bool r64 = std::getenv("CCMPI_SWIGLU_T_ROWS") && std::atoi(std::getenv("CCMPI_SWIGLU_T_ROWS")) == 64;
+    auto args = [&](auto kern, int R) {
+      hipLaunchKernelGGL(kern, dim3((n + 63) / 64, (unsigned)((T + R - 1) / R)), dim3(256), 0,
+                         reinterpret_cast<hipStream_t>(stream), reinterpret_cast<const uint16_t*>(h),
+                         reinterpret_cast<const uint16_t*>(da), reinterpret_cast<uint16_t*>(dh),
+                         reinterpret_cast<uint16_t*>(dht), (int)T, n, ldh, ldda, lddh, ldt);
+    };
+    if (r64) args(k_swiglu_bwd_il_t<64>, 64);
+    else args(k_swiglu_bwd_il_t<128>, 128);
     CCMPI_HIP_CHECK(hipGetLastError());
   }, "swiglu_bwd_il plus dh^T [2k, T] (the dW GEMM's N-layout operand)");
   // C[M, N] = A[M, K] B[N, K]^T (bf16) on the LDS-ring kernel with the SwiGLU epilogue:
