@@ -1,5 +1,5 @@
 """The SwiGLU backward of the Llama MLP (T 4096, ffn 14336): dh alone, and dh + dh^T in one
-kernel (CCMPI_SWIGLU_T_ROWS=64 | 128 tile rows, read at the first call).  Bytes moved
+kernel.  Bytes moved
 per second.  One JSON line."""
 import json
 import os
@@ -29,6 +29,5 @@ plain = t_us(lambda: swiglu_pairs_backward(h, da))
 both = t_us(lambda: swiglu_pairs_backward(h, da, transposed=True))
 mb_plain = (T * 2 * k * 2 * 2 + T * k * 2) / 1e6
 mb_both = mb_plain + T * 2 * k * 2 / 1e6
-print(json.dumps({"tile_rows": os.environ.get("CCMPI_SWIGLU_T_ROWS", "128"),
-                  "dh_us": round(plain, 1), "dh_TBps": round(mb_plain / plain, 2),
+print(json.dumps({"dh_us": round(plain, 1), "dh_TBps": round(mb_plain / plain, 2),
                   "dh_and_dht_us": round(both, 1), "dh_and_dht_TBps": round(mb_both / both, 2)}), flush=True)

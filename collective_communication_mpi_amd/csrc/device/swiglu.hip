@@ -127,7 +127,7 @@ __global__ void __launch_bounds__(256) k_swiglu_bwd_il(const uint16_t* __restric
 // a 64-row x 64-column tile of dh per workgroup, written row-major straight away and
 // through an LDS tile (33-word row stride: conflict-free column gathers) transposed,
 // 16-B stores both ways.  T % 8 == 0.
-template <int R>  // rows per tile: 64 or 128
+template <int R>  // rows per tile (a multiple of 32)
 __global__ void __launch_bounds__(256) k_swiglu_bwd_il_t(const uint16_t* __restrict__ h, const uint16_t* __restrict__ da,
                                                          uint16_t* __restrict__ dh, uint16_t* __restrict__ dht, int T,
                                                          int n, int64_t ldh, int64_t ldda, int64_t lddh, int64_t ldt) {
@@ -215,16 +215,12 @@ void register_swiglu_ops(pybind11::module_& m) {
     if (T % 8) throw std::invalid_argument("swiglu_bwd_il_t: T % 8 == 0 required");
     if (T == 0 || k == 0) return;
     const int n = (int)(2 * k);
-    // 128-row tiles unless CCMPI_SWIGLU_T_ROWS=64 (A/B)
-    static const bool r64 = std::getenv("CCMPI_SWIGLU_T_ROWS") && std::atoi(std::getenv("CCMPI_SWIGLU_T_ROWS")) == 64;
-    auto args = [&](auto kern, int R) {
-      hipLaunchKernelGGL(kern, dim3((n + 63) / 64, (unsigned)((T + R - 1) / R)), dim3(256), 0,
-                         reinterpret_cast<hipStream_t>(stream), reinterpret_cast<const uint16_t*>(h),
-                         reinterpret_cast<const uint16_t*>(da), reinterpret_cast<uint16_t*>(dh),
-                         reinterpret_cast<uint16_t*>(dht), (int)T, n, ldh, ldda, lddh, ldt);
-    };
-    if (r64) args(k_swiglu_bwd_il_t<64>, 64);
-    else args(k_swiglu_bwd_il_t<128>, 128);
+    // 64-row tiles: 128-row ones measured 3 % slower (profiles/r4_swiglu_t)
+    constexpr int R = 64;
+    hipLaunchKernelGGL(k_swiglu_bwd_il_t<R>, dim3((n + 63) / 64, (unsigned)((T + R - 1) / R)), dim3(256), 0,
+                       reinterpret_cast<hipStream_t>(stream), reinterpret_cast<const uint16_t*>(h),
+                       reinterpret_cast<const uint16_t*>(da), reinterpret_cast<uint16_t*>(dh),
+                       reinterpret_cast<uint16_t*>(dht), (int)T, n, ldh, ldda, lddh, ldt);
     CCMPI_HIP_CHECK(hipGetLastError());
   }, "swiglu_bwd_il plus dh^T [2k, T] (the dW GEMM's N-layout operand)");
   // C[M, N] = A[M, K] B[N, K]^T (bf16) on the LDS-ring kernel with the SwiGLU epilogue:
