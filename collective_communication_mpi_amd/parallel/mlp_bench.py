@@ -91,14 +91,14 @@ def measure_tp_mlp(comm, tokens: int = 4096, d: int = 4096, ffn: int = 14336, it
         return t_f, t_fb, host, chk
 
     flop_f = 2 * tokens * d * 2 * ffn + 2 * tokens * ffn * d  # whole block (all ranks together)
-    default_mode = mode or tp._ROW_MODE
+    default_mode = tp._row_mode(mode or tp._ROW_MODE, comm) if p > 1 else "local"
     calls0 = dict(tp.CALLS)
     t_f, t_fb, host, chk = run(build(mode))
     paths = {k: v - calls0.get(k, 0) for k, v in tp.CALLS.items() if v != calls0.get(k, 0)}
     buf = torch.randn(tokens, d, device=dev).to(torch.bfloat16)
     t_ar = timed(lambda: all_reduce_(buf, comm)) if p > 1 else 0.0
     out = {
-        "tp": p, "gate": "eager" if eager_gate else "fused", "row_mode": default_mode if p > 1 else "local",
+        "tp": p, "gate": "eager" if eager_gate else "fused", "row_mode": default_mode,
         "tokens": tokens, "d_model": d, "ffn": ffn,
         "dtype": "bf16", "shared_gpu": bool(comm.dev.shared_device) if p > 1 else False,
         "fwd_ms": round(t_f * 1e3, 3), "fwd_bwd_ms": round(t_fb * 1e3, 3),

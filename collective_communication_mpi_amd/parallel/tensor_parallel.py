@@ -228,9 +228,21 @@ def _linear_backward(g2: torch.Tensor, x2: torch.Tensor, w: torch.Tensor, need_d
 # * "fused"   -- the all-reduce in the GEMM epilogue (DeviceGroup.gemm_allreduce): tile
 #   owners spin on peers' tiles inside the GEMM (3.1x slower at TP = 2 on a shared GPU,
 #   profiles/r3_tp2).
-# The default is what the TP MLP measurements chose (profiles/r4_tp, README).
+# * "auto" (default) -- "chunked" when every rank owns its GPU: the all-reduce then crosses
+#   xGMI links while the next row block's GEMM keeps the CUs busy; "plain" when ranks share
+#   a GPU, where both compete for the same HBM and CUs and plain measured fastest
+#   (profiles/r4_first, profiles/r4_shared_ring: 1.18 ms against chunked 1.36 ms at TP = 2).
+#   bench.py's mlp phase records all three (tp_mlp.row_mode_variants).
 ROW_MODES = ("plain", "chunked", "fused")
-_ROW_MODE = os.environ.get("CCMPI_TP_ROW_MODE", "plain")
+_ROW_MODE = os.environ.get("CCMPI_TP_ROW_MODE", "auto")
+
+
+def _row_mode(mode: str, comm) -> str:
+    """The row-parallel mode a call runs (resolves ``auto``)."""
+    if mode != "auto":
+        return mode
+    shared = _size_rank(comm)[0] > 1 and bool(device_group_for(comm).shared_device)
+    return "plain" if shared else "chunked"
 _TP_CHUNKS = int(os.environ.get("CCMPI_TP_CHUNKS", "2"))
 # which TP paths ran (tests assert the path they meant to exercise actually ran)
 CALLS: "collections.Counter[str]" = collections.Counter()
@@ -343,6 +355,7 @@ class _RowParallelFn(torch.autograd.Function):
             return y
         dev = device_group_for(comm)
         bias0 = b if r == 0 else None
+        mode = _row_mode(mode, comm)
         if mode == "fused" and _fused_ok(x2, w, comm):
             CALLS["row_fused"] += 1
             out = _scratch(comm, "row_fused", (M, N), torch.bfloat16)
@@ -549,8 +562,8 @@ class RowParallelLinear(torch.nn.Module):
         p, r = _size_rank(comm)
         if in_features % p:
             raise ValueError(f"in_features {in_features} not divisible by TP size {p}")
-        if mode and mode not in ROW_MODES:
-            raise ValueError(f"RowParallelLinear mode {mode!r} not in {ROW_MODES}")
+        if mode and mode not in ROW_MODES + ("auto",):
+            raise ValueError(f"RowParallelLinear mode {mode!r} not in {ROW_MODES + ('auto',)}")
         self.mode = mode  # "" = CCMPI_TP_ROW_MODE at call time
         self.comm, self.p, self.r = comm, p, r
         self.in_features, self.out_features = in_features, out_features
