@@ -32,3 +32,18 @@ def test_route_switch(monkeypatch):
     assert not _kmajor_via_transpose(28672, 4096, 4096, _t(4096, 28672), _t(4096, 4096))
     monkeypatch.setenv("CCMPI_KMAJOR_ROUTE", "transpose")
     assert _kmajor_via_transpose(28672, 4096, 4096, _t(4096, 28672), _t(4096, 4096))
+
+
+def test_row_parallel_auto_mode(monkeypatch):
+    """``auto``: chunked (the all-reduce of a row block under the next block's GEMM) when
+    every rank owns its GPU, plain when ranks share one; explicit modes pass through."""
+    from types import SimpleNamespace
+
+    from collective_communication_mpi_amd.parallel import tensor_parallel as tp
+
+    monkeypatch.setattr(tp, "_size_rank", lambda comm: (2, 0))
+    monkeypatch.setattr(tp, "device_group_for", lambda comm: SimpleNamespace(shared_device=False))
+    assert tp._row_mode("auto", object()) == "chunked"
+    monkeypatch.setattr(tp, "device_group_for", lambda comm: SimpleNamespace(shared_device=True))
+    assert tp._row_mode("auto", object()) == "plain"
+    assert tp._row_mode("fused", object()) == "fused"
