@@ -91,7 +91,7 @@ def measure_tp_mlp(comm, tokens: int = 4096, d: int = 4096, ffn: int = 14336, it
         return t_f, t_fb, host, chk
 
     flop_f = 2 * tokens * d * 2 * ffn + 2 * tokens * ffn * d  # whole block (all ranks together)
-    default_mode = tp._row_mode(mode or tp._ROW_MODE, comm) if p > 1 else "local"
+    default_mode = tp._row_mode(mode or tp._ROW_MODE, comm, tokens, d) if p > 1 else "local"
     calls0 = dict(tp.CALLS)
     t_f, t_fb, host, chk = run(build(mode))
     paths = {k: v - calls0.get(k, 0) for k, v in tp.CALLS.items() if v != calls0.get(k, 0)}

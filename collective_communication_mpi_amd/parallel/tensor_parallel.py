@@ -228,21 +228,36 @@ def _linear_backward(g2: torch.Tensor, x2: torch.Tensor, w: torch.Tensor, need_d
 # * "fused"   -- the all-reduce in the GEMM epilogue (DeviceGroup.gemm_allreduce): tile
 #   owners spin on peers' tiles inside the GEMM (3.1x slower at TP = 2 on a shared GPU,
 #   profiles/r3_tp2).
-# * "auto" (default) -- "chunked" when every rank owns its GPU: the all-reduce then crosses
-#   xGMI links while the next row block's GEMM keeps the CUs busy; "plain" when ranks share
-#   a GPU, where both compete for the same HBM and CUs and plain measured fastest
-#   (profiles/r4_first, profiles/r4_shared_ring: 1.18 ms against chunked 1.36 ms at TP = 2).
-#   bench.py's mlp phase records all three (tp_mlp.row_mode_variants).
+# * "auto" (default) -- "chunked" when every rank owns its GPU AND each row block's GEMM
+#   still fills the chip (>= one 256x256 tile per CU): the all-reduce then crosses xGMI while
+#   the next block's GEMM keeps every CU busy.  Otherwise "plain": a block of fewer tiles
+#   than CUs takes as long as the whole GEMM (one wave either way), so chunking would double
+#   the GEMM time -- the Llama MLP's 4096 x 4096 output is exactly 256 tiles -- and ranks
+#   sharing a GPU compete for the same HBM and CUs (plain measured fastest there:
+#   profiles/r4_first, profiles/r4_shared_ring, 1.18 ms against chunked 1.36 ms at TP = 2).
+#   bench.py's mlp phase records all three modes (tp_mlp.row_mode_variants).
 ROW_MODES = ("plain", "chunked", "fused")
 _ROW_MODE = os.environ.get("CCMPI_TP_ROW_MODE", "auto")
 
 
-def _row_mode(mode: str, comm) -> str:
-    """The row-parallel mode a call runs (resolves ``auto``)."""
+def _row_mode(mode: str, comm, M: int = 0, N: int = 0) -> str:
+    """The row-parallel mode a call with a [M, N] output runs (resolves ``auto``)."""
     if mode != "auto":
         return mode
-    shared = _size_rank(comm)[0] > 1 and bool(device_group_for(comm).shared_device)
-    return "plain" if shared else "chunked"
+    if _size_rank(comm)[0] > 1 and bool(device_group_for(comm).shared_device):
+        return "plain"
+    blocks = _chunk_rows(M, _TP_CHUNKS) if M else []
+    if len(blocks) < 2:
+        return "plain"
+    tiles = -(-(blocks[0][1] - blocks[0][0]) // 256) * -(-N // 256)
+    return "chunked" if tiles >= _cu_count() else "plain"
+
+
+def _cu_count() -> int:
+    try:
+        return int(torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count) or 256
+    except Exception:  # noqa: BLE001 - no GPU: the MI355X's
+        return 256
 _TP_CHUNKS = int(os.environ.get("CCMPI_TP_CHUNKS", "2"))
 # which TP paths ran (tests assert the path they meant to exercise actually ran)
 CALLS: "collections.Counter[str]" = collections.Counter()
@@ -355,7 +370,7 @@ class _RowParallelFn(torch.autograd.Function):
             return y
         dev = device_group_for(comm)
         bias0 = b if r == 0 else None
-        mode = _row_mode(mode, comm)
+        mode = _row_mode(mode, comm, M, N)
         if mode == "fused" and _fused_ok(x2, w, comm):
             CALLS["row_fused"] += 1
             out = _scratch(comm, "row_fused", (M, N), torch.bfloat16)

@@ -36,14 +36,20 @@ def test_route_switch(monkeypatch):
 
 def test_row_parallel_auto_mode(monkeypatch):
     """``auto``: chunked (the all-reduce of a row block under the next block's GEMM) when
-    every rank owns its GPU, plain when ranks share one; explicit modes pass through."""
+    every rank owns its GPU and each block's GEMM still fills the chip; plain otherwise;
+    explicit modes pass through."""
     from types import SimpleNamespace
 
     from collective_communication_mpi_amd.parallel import tensor_parallel as tp
 
     monkeypatch.setattr(tp, "_size_rank", lambda comm: (2, 0))
+    monkeypatch.setattr(tp, "_cu_count", lambda: 256)
     monkeypatch.setattr(tp, "device_group_for", lambda comm: SimpleNamespace(shared_device=False))
-    assert tp._row_mode("auto", object()) == "chunked"
+    # 16384 x 8192 output: 2 blocks of 32 x 32 tiles (>= one per CU) -> chunked
+    assert tp._row_mode("auto", object(), 16384, 8192) == "chunked"
+    # the Llama MLP's 4096 x 4096 output: 2 blocks of 128 tiles -> plain
+    assert tp._row_mode("auto", object(), 4096, 4096) == "plain"
+    assert tp._row_mode("auto", object(), 256, 8192) == "plain"  # one block
     monkeypatch.setattr(tp, "device_group_for", lambda comm: SimpleNamespace(shared_device=True))
-    assert tp._row_mode("auto", object()) == "plain"
-    assert tp._row_mode("fused", object()) == "fused"
+    assert tp._row_mode("auto", object(), 16384, 8192) == "plain"
+    assert tp._row_mode("fused", object(), 4096, 4096) == "fused"
