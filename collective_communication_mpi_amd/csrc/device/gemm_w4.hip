@@ -846,30 +846,13 @@ __global__ void __launch_bounds__(WNT, 1) k_gemm_w4r(W4Args wa) {
         for (int j = j0; j < j1; ++j) mfma(i, j, pa[i], pb[j]);
         __builtin_amdgcn_sched_barrier(0);
       };
-      if constexpr (PAIR == 3) {
-        // spread: pieces 0..11 in the even phase (2 per group in groups 0-3, 1 in 4-7), the
-        // last 4 in the first half of the odd phase (DMA there means "the tail")
-        mm(0, 1);
-        if constexpr (DMA && !ODD) dma_pair(np, i < 4 ? 2 * i : 4 + i);
-        if constexpr (DMA && ODD) {
-          if (i < 4) dma_pair(np, 12 + i);
-        }
-        rd_pair(slot, ro, i, 0, ca, cb);
-        __builtin_amdgcn_sched_barrier(0);
-        mm(1, 3);
-        if constexpr (DMA && !ODD) {
-          if (i < 4) dma_pair(np, 2 * i + 1);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      } else {
-        mm(0, 1);
-        if constexpr (DMA) dma_pair(np, 2 * i);
-        rd_pair(slot, ro, i, 0, ca, cb);
-        __builtin_amdgcn_sched_barrier(0);
-        mm(1, 3);
-        if constexpr (DMA) dma_pair(np, 2 * i + 1);
-        __builtin_amdgcn_sched_barrier(0);
-      }
+      mm(0, 1);
+      if constexpr (DMA) dma_pair(np, 2 * i);
+      rd_pair(slot, ro, i, 0, ca, cb);
+      __builtin_amdgcn_sched_barrier(0);
+      mm(1, 3);
+      if constexpr (DMA) dma_pair(np, 2 * i + 1);
+      __builtin_amdgcn_sched_barrier(0);
       mm(3, 5);
       rd_pair(slot, ro, i, 1, ca, cb);
       __builtin_amdgcn_sched_barrier(0);
@@ -917,10 +900,9 @@ __global__ void __launch_bounds__(WNT, 1) k_gemm_w4r(W4Args wa) {
         rd_pair(smem, 0, i, 1, a0, b0);
       }
       phase_pair(F{}, T{}, 1, a0, b0, a1, b1);
-      using TAIL = std::integral_constant<bool, PAIR == 3>;
       for (int p = 1; p + 1 < npair; ++p) {
         phase_pair(T{}, F{}, 2 * p, a1, b1, a0, b0);
-        phase_pair(TAIL{}, T{}, 2 * p + 1, a0, b0, a1, b1);
+        phase_pair(F{}, T{}, 2 * p + 1, a0, b0, a1, b1);
       }
       if (npair > 1) {
         phase_pair(F{}, F{}, nst - 2, a1, b1, a0, b0);
@@ -1220,7 +1202,6 @@ void launch_gemm_ring(const GemmArgs& g, int ta, int tb, hipStream_t stream, uin
     w4p_attr(reinterpret_cast<const void*>(k_gemm_w4r<2, 1, 0, 0, 0, 0, 1>));
     w4p_attr(reinterpret_cast<const void*>(k_gemm_w4r<0, 0, 0, 0, 0, 1, 1>));
     w4p_attr(reinterpret_cast<const void*>(k_gemm_w4r<1, 0, 0, 0, 0, 1, 1>));
-    w4p_attr(reinterpret_cast<const void*>(k_gemm_w4r<1, 0, 0, 0, 0, 0, 3>));
     return true;
   }();
   (void)attr;
@@ -1258,8 +1239,6 @@ void launch_gemm_ring(const GemmArgs& g, int ta, int tb, hipStream_t stream, uin
   if (pair) {
     // pair-slot ring: whole-line DMA pieces, 64-deep slots (bit 0: persistent grid)
     if (persist) hipLaunchKernelGGL((k_gemm_w4r<1, 1, 0, 0, 0, 0, 1>), dim3(grid), dim3(WNT), kPairLds, stream, a);
-    else if (fast && (sched & 65536))  // experiment: DMA spread over 1.5 phases (PAIR 3)
-      hipLaunchKernelGGL((k_gemm_w4r<1, 0, 0, 0, 0, 0, 3>), dim3(ntiles), dim3(WNT), kPairLds, stream, a);
     else if (fast) hipLaunchKernelGGL((k_gemm_w4r<1, 0, 0, 0, 0, 0, 1>), dim3(ntiles), dim3(WNT), kPairLds, stream, a);
     else hipLaunchKernelGGL((k_gemm_w4r<0, 0, 0, 0, 0, 0, 1>), dim3(ntiles), dim3(WNT), kPairLds, stream, a);
   } else if (!fast) {
