@@ -600,7 +600,10 @@ class DeviceGroup:
     def _shared_cap(self) -> int:
         """CCMPI_SHARED_RING: per-rank CTA cap keeping all sharing ranks' collectives on
         at most half the CUs."""
-        return max(1, (_cu_count(self.device) // 2) // self.ranks_per_device)
+        cus = getattr(self, "_cus", None)
+        if cus is None:
+            cus = self._cus = _cu_count(self.device)  # one device query per group
+        return max(1, (cus // 2) // self.ranks_per_device)
 
     def _symm(self, *ts) -> bool:
         return all(self.is_symmetric(t) and t.data_ptr() % 16 == 0 for t in ts)

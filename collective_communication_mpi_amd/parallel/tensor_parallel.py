@@ -253,11 +253,18 @@ def _row_mode(mode: str, comm, M: int = 0, N: int = 0) -> str:
     return "chunked" if tiles >= _cu_count() else "plain"
 
 
+_CUS: dict = {}
+
+
 def _cu_count() -> int:
+    """CUs of the current device (cached per device index)."""
     try:
-        return int(torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count) or 256
+        idx = torch.cuda.current_device()
     except Exception:  # noqa: BLE001 - no GPU: the MI355X's
         return 256
+    if idx not in _CUS:
+        _CUS[idx] = int(torch.cuda.get_device_properties(idx).multi_processor_count) or 256
+    return _CUS[idx]
 _TP_CHUNKS = int(os.environ.get("CCMPI_TP_CHUNKS", "2"))
 # which TP paths ran (tests assert the path they meant to exercise actually ran)
 CALLS: "collections.Counter[str]" = collections.Counter()
