@@ -37,8 +37,6 @@ variants = {
     "heap_promise": lambda: dev.allreduce(heap, heap2, "SUM", "fanout", symmetric=True),
     "to_local": lambda: dev.allreduce_to_local(heap, out),
 }
-if os.environ.get("CCMPI_TO_LOCAL") == "fanout":  # the A/B form of allreduce_to_local
-    variants = {"to_local_fanout_copy": variants["to_local"]}
 res = {}
 for name, fn in variants.items():
     heap.fill_(1)

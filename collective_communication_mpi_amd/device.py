@@ -825,15 +825,6 @@ class DeviceGroup:
         if self.size > 1 and not self._symm(src):
             raise ValueError("allreduce_to_local: src must be a 16-B aligned symmetric-heap block (comm.empty / "
                              "persistent)")
-        if self.size > 1 and os.environ.get("CCMPI_TO_LOCAL") == "fanout":
-            # A/B: one-phase fan-out (posted writes of the reduced chunks) into persistent
-            # symmetric scratch, then a local copy.  Safe without double buffering: a peer's
-            # next fan-out writes into this scratch only after its entry handshake with this
-            # rank's next call, which is stream-ordered after this copy.
-            out = self.persistent(("to_local_out",), (src.numel(),), src.dtype)
-            self.allreduce(src.view(-1), out, op, "fanout", max_blocks=max_blocks, symmetric=True)
-            dst.view(-1).copy_(out)
-            return dst
         self.dc.allreduce_to_local(src.data_ptr(), dst.data_ptr(), src.numel(), dtype_code(src.dtype), op_code(op),
                                    self._stream(), self._budget(max_blocks))
         return dst
