@@ -55,7 +55,6 @@ struct W4Args {
   unsigned long long* dbg;  // STAMP diagnostic builds only: 4 cycle counts per wave
   uint16_t* glu;  // EPI 2 only: silu(gate) * up of each interleaved (gate, up) column pair
   int ldglu;
-  int prio = 0;   // PAIR, experiment: s_setprio 1 for odd waves (1), waves 2-3 (2), waves 0-1 (3)
 };
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t op_rsrc(const uint16_t* base, long rows, int ld) {
@@ -892,10 +891,6 @@ __global__ void __launch_bounds__(WNT, 1) k_gemm_w4r(W4Args wa) {
     int ntm = 0, ntn = 0;
     if constexpr (PAIR) {
       const int npair = nst >> 1;
-      if (wa.prio && lt == xcd_remap(blockIdx.x, gridDim.x)) {
-        const bool hi = wa.prio == 1 ? (wave & 1) : wa.prio == 2 ? (wave >= 2) : (wave < 2);
-        if (hi) __builtin_amdgcn_s_setprio(1);
-      }
       // pair 0 landed everywhere, every wave past the previous tile's epilogue
       ring_wait_barrier(younger);
       // "phase 0": step 0's fragments; phase 1 ends with pair 1 landed
@@ -1211,7 +1206,7 @@ void launch_gemm_ring(const GemmArgs& g, int ta, int tb, hipStream_t stream, uin
   }();
   (void)attr;
   const int ntiles = gemm_w4_tiles(g.M, g.N);
-  W4Args a{g, g_w4_group_m, {}, g_w4_dbg, glu, ldglu, (sched >> 17) & 3};
+  W4Args a{g, g_w4_group_m, {}, g_w4_dbg, glu, ldglu};
   const bool fast = gemm_w4r_fast(g);
   const bool pair = sched & 16384;
   const bool persist = fast && (sched & 1);
