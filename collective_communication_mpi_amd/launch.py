@@ -11,8 +11,9 @@ first failing exit code and tears down the remaining ranks (no orphaned
 spinners), and enforces an optional wall-clock ``--timeout``.
 
 Open MPI style flags that make no sense for a single-host shm runtime
-(``--oversubscribe``, ``--allow-run-as-root``, ``--bind-to X``, ``-H host``) are
-accepted and ignored; ``-x VAR[=VAL]`` exports a variable.
+(``--oversubscribe``, ``--allow-run-as-root``, ``-H host``) are accepted and ignored;
+``-x VAR[=VAL]`` exports a variable; ``--bind-to core`` pins rank r to the r-th CPU the
+launcher may use (``CCMPI_BIND=core`` does the same), other levels leave placement to the OS.
 """
 from __future__ import annotations
 
@@ -27,7 +28,7 @@ from typing import List, Optional
 
 REPO = Path(__file__).resolve().parent.parent
 
-_FLAG_WITH_ARG_IGNORED = {"--bind-to", "--map-by", "-H", "--host", "--hostfile", "-hostfile", "--mca", "-ppn"}
+_FLAG_WITH_ARG_IGNORED = {"--map-by", "-H", "--host", "--hostfile", "-hostfile", "--mca", "-ppn"}
 _FLAG_IGNORED = {"--oversubscribe", "--allow-run-as-root", "-l", "--tag-output", "-prepend-rank"}
 
 
@@ -51,6 +52,12 @@ def parse(argv: List[str]):
             else:
                 k, v = kv, os.environ.get(kv, "")
             exports[k] = v
+            i += 2
+        elif a == "--bind-to":
+            # Open MPI semantics for "core": rank r pinned to the r-th CPU this launcher may
+            # use (fewer migrations, shorter tails for the host plane's spin-waits); any other
+            # level ("none", "socket", ...) leaves placement to the OS
+            exports["CCMPI_BIND"] = argv[i + 1]
             i += 2
         elif a in _FLAG_WITH_ARG_IGNORED:
             i += 2
@@ -87,7 +94,12 @@ def launch(n: int, cmd: List[str], timeout: Optional[float] = None, env_extra=No
         # Foreign launcher variables would make the runtime pick the wrong rank.
         for k in ("PMI_RANK", "PMI_SIZE", "OMPI_COMM_WORLD_RANK", "OMPI_COMM_WORLD_SIZE", "RANK", "WORLD_SIZE"):
             env.pop(k, None)
-        procs.append(subprocess.Popen(cmd, env=env, start_new_session=True))
+        pin = None
+        if base.get("CCMPI_BIND") == "core":
+            cpus = sorted(os.sched_getaffinity(0))
+            pin = cpus[r % len(cpus)]
+        procs.append(subprocess.Popen(cmd, env=env, start_new_session=True,
+                                      preexec_fn=(lambda c=pin: os.sched_setaffinity(0, {c})) if pin is not None else None))
 
     def kill_all(sig=signal.SIGTERM):
         for p in procs:

@@ -133,3 +133,25 @@ def test_llama_ddp_cpu():
     per-rank replica gradients, over two steps and a no_sync micro-batch accumulation."""
     r = run_ranks(2, py("tests/workers/llama_dp_worker.py", "--device", "cpu"), timeout=300)
     assert "llama dp OK" in r.stdout
+
+
+def test_launcher_bind_to_core(tmp_path):
+    """``--bind-to core`` (Open MPI semantics): every rank pinned to its own CPU."""
+    import os
+    import subprocess
+    import sys
+
+    if len(os.sched_getaffinity(0)) < 2:
+        import pytest
+
+        pytest.skip("needs 2 CPUs")
+    code = ("import os; print(os.environ['CCMPI_RANK'], sorted(os.sched_getaffinity(0)), flush=True)")
+    r = subprocess.run([sys.executable, "-m", "collective_communication_mpi_amd.launch", "-n", "2", "--bind-to", "core",
+                        sys.executable, "-c", code], capture_output=True, text=True, timeout=120,
+                       cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    assert r.returncode == 0, r.stderr
+    lines = sorted(l.split(" ", 1) for l in r.stdout.strip().splitlines())
+    import ast
+
+    cpus = [ast.literal_eval(c) for _, c in lines]
+    assert all(len(c) == 1 for c in cpus) and cpus[0] != cpus[1], r.stdout
