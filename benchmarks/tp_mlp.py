@@ -33,7 +33,7 @@ ap.add_argument("--warmup", type=int, default=3)
 ap.add_argument("--eager-gate", action="store_true",
                 help="SwiGLU gate as eager torch ops (A/B against the gate fused into the GEMM epilogue)")
 ap.add_argument("--variants", action="store_true", help="p > 1: every row-parallel mode side by side")
-ap.add_argument("--mode", default="", help="row-parallel mode of the main record (plain | chunked | fused)")
+ap.add_argument("--mode", default="", help="row-parallel mode of the main record (plain | chunked | fused | push)")
 args = ap.parse_args()
 comm = Communicator(MPI.COMM_WORLD)
 local = int(os.environ.get("LOCAL_RANK", os.environ.get("CCMPI_LOCAL_RANK", "0")))

@@ -388,9 +388,10 @@ __device__ void fanout_span(const char* src, char* const* dsts, int nr, int skip
 }
 
 // Reduce `nr` slots at base + j*stride (this rank's memory) and store the
-// result into every outs[j] (local or peer-mapped).
-template <int DT, int OP, int NRM>
+// result into every outs[j] (local or peer-mapped); ONE: into outs[0] only.
+template <int DT, int OP, int NRM, bool ONE = false>
 __device__ void reduce_fanout(const char* base, uint64_t stride, int nr, uint64_t len, char* const* outs) {
+  const int nout = ONE ? 1 : nr;
   const uint64_t vbytes = len & ~15ull;
   const uint64_t kWin = 1ull << 30;
   for (uint64_t w = 0; w < vbytes; w += kWin) {
@@ -400,7 +401,7 @@ __device__ void reduce_fanout(const char* base, uint64_t stride, int nr, uint64_
     for (int j = 0; j < NRM; ++j) {
       if (j < nr) {
         src[j] = make_rsrc(uniform_ptr(const_cast<char*>(base) + j * stride + w), wl);
-        dst[j] = make_rsrc(uniform_ptr(outs[j] + w), wl);
+        if (j < nout) dst[j] = make_rsrc(uniform_ptr(outs[j] + w), wl);
       }
     }
     const uint32_t nv = wl / 16;
@@ -423,7 +424,7 @@ __device__ void reduce_fanout(const char* base, uint64_t stride, int nr, uint64_
           const u32x4 r = acc.store();
 #pragma unroll
           for (int j = 0; j < NRM; ++j)
-            if (j < nr) st16(dst[j], (v + u * kThreads) * 16, r);
+            if (j < nout) st16(dst[j], (v + u * kThreads) * 16, r);
         }
       }
     }
@@ -435,7 +436,7 @@ __device__ void reduce_fanout(const char* base, uint64_t stride, int nr, uint64_
       typename E::A acc = E::ld(make_rsrc(const_cast<char*>(base) + vbytes, (uint32_t)tail), o);
       for (int j = 1; j < nr; ++j)
         acc = apply_op<OP>(acc, E::ld(make_rsrc(const_cast<char*>(base) + j * stride + vbytes, (uint32_t)tail), o));
-      for (int j = 0; j < nr; ++j) E::st(make_rsrc(outs[j] + vbytes, (uint32_t)tail), o, acc);
+      for (int j = 0; j < nout; ++j) E::st(make_rsrc(outs[j] + vbytes, (uint32_t)tail), o, acc);
     }
   }
 }
@@ -592,6 +593,54 @@ __global__ void __launch_bounds__(kThreads) k_allreduce_twoshot_push(CollArgs a)
     __syncthreads();
     reduce_fanout<DT, OP, NRM>(resolve(pt, me, codes[0][me]) + sub.lo, shard, nr, sub.hi - sub.lo, outs);
   }
+  if (!sync_phase(a, 3, e)) return;
+  finish(a, e);
+}
+
+// Inbox-to-local two-shot, the collective half of the push row-parallel GEMM
+// (DeviceComm::gemm_push_rowpar): every rank's GEMM epilogue has already stored its
+// partial of shard j (row block j) into rank j's inbox slot [rank] as posted writes,
+// so the reduce-scatter's traffic crossed the fabric under the GEMM.  Here rank r
+// reduces its p slots (local reads, rank order) into its own slot r, and after the
+// phase flag every rank pulls every reduced shard from its owner into `out`
+// (a local tensor).  codes[0][j] = rank j's inbox; slot stride = the shard size.
+template <int DT, int OP, int NRM>
+__global__ void __launch_bounds__(kThreads) k_allreduce_inbox_local(CollArgs a) {
+  __shared__ uint64_t s_epoch;
+  __shared__ uint64_t codes[2][kMaxRanks];
+  if (!start_phase(a, &s_epoch, codes)) return;
+  const uint64_t e = s_epoch;
+  const PeerTable* pt = a.pt;
+  const int me = pt->rank, nr = pt->size;
+  const uint64_t shard = (((a.nbytes + nr - 1) / nr) + 15) / 16 * 16;
+  {
+    BlockRange mys = part16(a.nbytes, nr, me);
+    BlockRange sub = part16(mys.hi - mys.lo, gridDim.x, blockIdx.x);
+    char* inbox = resolve(pt, me, codes[0][me]);
+    if (sub.hi > sub.lo) {
+      char* outs[1] = {inbox + (uint64_t)me * shard + sub.lo};
+      reduce_fanout<DT, OP, NRM, true>(inbox + sub.lo, shard, nr, sub.hi - sub.lo, outs);
+    }
+  }
+  if (!sync_phase(a, 1, e)) return;
+  __shared__ const char* srcs[kMaxRanks];
+  __shared__ char* dsts[kMaxRanks];
+  __shared__ uint64_t lens[kMaxRanks];
+  if (threadIdx.x < nr) {
+    const int j = threadIdx.x;
+    BlockRange sj = part16(a.nbytes, nr, j);
+    BlockRange bj = part16(sj.hi - sj.lo, gridDim.x, blockIdx.x);
+    srcs[j] = resolve(pt, j, codes[0][j]) + (uint64_t)j * shard + bj.lo;
+    dsts[j] = a.out + sj.lo + bj.lo;
+    lens[j] = bj.hi - bj.lo;
+  }
+  __syncthreads();
+  uint64_t common = lens[0];
+  for (int j = 1; j < nr; ++j) common = min(common, lens[j]);
+  if (common) gather_spans<NRM>(srcs, dsts, nr, -1, common);
+  for (int j = 0; j < nr; ++j)
+    if (lens[j] > common) copy_span(srcs[j] + common, dsts[j] + common, lens[j] - common);
+  // no rank's next push may land in an inbox a peer still reads
   if (!sync_phase(a, 3, e)) return;
   finish(a, e);
 }
@@ -1311,6 +1360,15 @@ void launch_allreduce(int algo, const CollArgs& a, int nranks, int dtype, int op
         default: throw std::invalid_argument("ccmpi: bad allreduce algo");
       }
     });
+  });
+  CCMPI_HIP_CHECK(hipGetLastError());
+}
+
+void launch_inbox_to_local(const CollArgs& a, int nranks, int dtype, int grid, hipStream_t s) {
+  with_nrm(nranks, [&]<int R>() {
+    if (dtype == DT_BF16) hipLaunchKernelGGL((k_allreduce_inbox_local<DT_BF16, OP_SUM, R>), dim3(grid), dim3(kThreads), 0, s, a);
+    else if (dtype == DT_F32) hipLaunchKernelGGL((k_allreduce_inbox_local<DT_F32, OP_SUM, R>), dim3(grid), dim3(kThreads), 0, s, a);
+    else throw std::invalid_argument("ccmpi: inbox all-reduce supports bf16 / fp32 sums");
   });
   CCMPI_HIP_CHECK(hipGetLastError());
 }

@@ -88,6 +88,9 @@ struct LocalReduceArgs {
 int grid_for(uint64_t bytes_per_cta_work, int max_blocks);
 void launch_copy(const void* src, void* dst, uint64_t nbytes, hipStream_t s);
 void launch_allreduce(int algo, const CollArgs& a, int nranks, int dtype, int op, int grid, hipStream_t s);
+// the collective half of the push row-parallel GEMM: reduce the inbox slots the GEMM
+// epilogues filled (codes[0] = the inboxes), pull every shard into a.out (bf16 / fp32 sum)
+void launch_inbox_to_local(const CollArgs& a, int nranks, int dtype, int grid, hipStream_t s);
 void launch_reduce_scatter(const CollArgs& a, int nranks, int dtype, int op, int grid, hipStream_t s);
 void launch_move(int mode, const CollArgs& a, int nranks, int grid, hipStream_t s);
 // mode 0: last-axis all-gather, 1: last-axis reduce-scatter; rows passed in CollArgs::root

@@ -1021,6 +1021,40 @@ void DeviceComm::gemm_rowpar(uint64_t A, uint64_t B, uint64_t out, uint64_t bias
   CCMPI_HIP_CHECK(hipGetLastError());
 }
 
+void DeviceComm::gemm_push_rowpar(uint64_t A, uint64_t B, uint64_t out, uint64_t inbox, int M, int N, int K, int lda,
+                                  int ldb, float alpha, uint64_t stream, int max_blocks) {
+  if (M <= 0 || N <= 0) return;
+  if (size_ < 2 || size_ > kMaxRanks) throw std::invalid_argument("ccmpi: push row-parallel GEMM needs 2..16 ranks");
+  const int rows = M / size_;
+  const uint64_t nbytes = (uint64_t)M * N * 2, shard = nbytes / size_;
+  if (rows * size_ != M || rows % 256 || N % 8 || (out % 16) || (inbox % 16) || nbytes >= 0x7ffffff0ull)
+    throw std::invalid_argument("ccmpi: push row-parallel GEMM needs M % (256 p) == 0, N % 8 == 0, 16-B aligned buffers");
+  gemm::GemmArgs g{reinterpret_cast<const uint16_t*>(A), reinterpret_cast<const uint16_t*>(B), nullptr, nullptr, M, N, K,
+                   lda, ldb, N, alpha, 0, 0, 0, 1, 1};
+  if (!gemm::gemm_ring_ok(g, 0, 0)) throw std::invalid_argument("ccmpi: push row-parallel GEMM: K % 64 == 0, 16-B rows");
+  CCMPI_HIP_CHECK(hipSetDevice(device_));
+  uint64_t ic = 0;
+  {
+    DynScope dyn_scope(this, true);
+    ic = code_of_(inbox, nbytes);
+  }
+  if (!ic) throw std::invalid_argument("ccmpi: push row-parallel GEMM: the inbox must be a symmetric heap block");
+  // block j of this rank's partial -> rank j's inbox, slot [rank_] (peer-mapped address)
+  const int s = (int)(ic >> 56) - 1;
+  const uint64_t off = ic & ((1ull << 56) - 1);
+  uint16_t* push[kMaxRanks] = {};
+  for (int j = 0; j < size_; ++j) {
+    char* base = host_pt_.seg[j][s];
+    if (!base) throw std::runtime_error("ccmpi: push row-parallel GEMM: peer segment not mapped");
+    push[j] = reinterpret_cast<uint16_t*>(base + off + (uint64_t)rank_ * shard);
+  }
+  g.C = push[rank_];
+  hipStream_t st = S(stream);
+  gemm::launch_gemm_ring(g, 0, 0, st, nullptr, 0, push, rows);
+  CCMPI_HIP_CHECK(hipGetLastError());
+  launch_inbox_to_local(args_(ic, 0, reinterpret_cast<char*>(out), nbytes, 0), size_, DT_BF16, grid_(shard, max_blocks), st);
+}
+
 uint32_t DeviceComm::error_code() {
   CCMPI_HIP_CHECK(hipSetDevice(device_));
   CCMPI_HIP_CHECK(hipDeviceSynchronize());

@@ -134,6 +134,13 @@ class DeviceComm {
   // registered (heap or on-demand) on every rank, 16-B aligned, N % 8 == 0
   void gemm_rowpar(uint64_t A, uint64_t B, uint64_t out, uint64_t bias, int M, int N, int K, int lda, int ldb,
                    int ldc, float alpha, int bias_kind, uint64_t stream);
+  // Push row-parallel GEMM: out[M, N] = sum over the group of A_r . B_r^T (bf16, no bias).
+  // Each rank's GEMM epilogue stores its partial of row block j (M / p rows) straight into
+  // rank j's slot [rank] of `inbox` (a symmetric heap block of M * N * 2 bytes on every
+  // rank), then one inbox-to-local two-shot reduces the slots and pulls every block into
+  // `out` (any local 16-B aligned tensor).  M % (256 p) == 0, K % 64 == 0, N % 8 == 0.
+  void gemm_push_rowpar(uint64_t A, uint64_t B, uint64_t out, uint64_t inbox, int M, int N, int K, int lda, int ldb,
+                        float alpha, uint64_t stream, int max_blocks);
   uint64_t code_of_public(uint64_t ptr, uint64_t nbytes) const { return code_of_(ptr, nbytes); }
   bool fused_ready() const { return fused_tab_dev_ != nullptr && fused_inbox_bytes_ > 0; }
 

@@ -217,7 +217,9 @@ bool gemm_w4r_fast(const GemmArgs& g);  // the LDS-ring kernel's fast epilogue a
 void launch_gemm_nt_w4r(const GemmArgs& g, hipStream_t stream);  // LDS-ring kernel (sched bits from g_w4_sched)
 // LDS-ring kernel with operand layouts: ta / tb = 1 reads A / B K-major ([K][M] / [K][N])
 bool gemm_ring_ok(const GemmArgs& g, int ta, int tb);
-void launch_gemm_ring(const GemmArgs& g, int ta, int tb, hipStream_t stream, uint16_t* glu = nullptr, int ldglu = 0);
+// push / push_rows: EPI 1 stores output row block j (push_rows rows) at push[j] instead of C
+void launch_gemm_ring(const GemmArgs& g, int ta, int tb, hipStream_t stream, uint16_t* glu = nullptr, int ldglu = 0,
+                      uint16_t* const* push = nullptr, int push_rows = 0);
 extern long long g_ring_min_macs;  // gemm_nt auto: the LDS-ring kernel from this many MACs up (0 = never)  // ablation variant of the ping-pong kernel (benchmarks only; 0 = production)
 
 }  // namespace gemm

@@ -55,6 +55,10 @@ struct W4Args {
   unsigned long long* dbg;  // STAMP diagnostic builds only: 4 cycle counts per wave
   uint16_t* glu;  // EPI 2 only: silu(gate) * up of each interleaved (gate, up) column pair
   int ldglu;
+  // EPI 1 push mode (push_rows > 0): output row block j = rows [j * push_rows, (j + 1) *
+  // push_rows) goes to push[j] (row 0 of the block at push[j]; a peer's inbox slot), not C
+  int push_rows;
+  uint16_t* push[kMaxRanks];
 };
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t op_rsrc(const uint16_t* base, long rows, int ld) {
@@ -970,7 +974,14 @@ __global__ void __launch_bounds__(WNT, 1) k_gemm_w4r(W4Args wa) {
       const int grp = lane >> 4, lr = lane & 15;
       const float al = g.alpha;
       const int ccol = bn + wc * 128 + lr * 8;
-      uint16_t* cptr = reinterpret_cast<uint16_t*>(g.C) + (size_t)(bm + wr * 128) * ldc + ccol;
+      uint16_t* cbase = reinterpret_cast<uint16_t*>(g.C);
+      int crow = bm + wr * 128;
+      if (EPI == 1 && wa.push_rows) {  // whole tiles per block (push_rows % 256 == 0)
+        const int blk = bm / wa.push_rows;
+        cbase = wa.push[blk];
+        crow -= blk * wa.push_rows;
+      }
+      uint16_t* cptr = cbase + (size_t)crow * ldc + ccol;
       const int rows_left = g.M - bm - wr * 128;
       const bool col_ok = ccol < g.N;
 #pragma unroll
@@ -1167,7 +1178,8 @@ bool gemm_ring_ok(const GemmArgs& g, int ta, int tb) {
   return a_bytes < 0x7ffffff0l && b_bytes < 0x7ffffff0l;
 }
 
-void launch_gemm_ring(const GemmArgs& g, int ta, int tb, hipStream_t stream, uint16_t* glu, int ldglu) {
+void launch_gemm_ring(const GemmArgs& g, int ta, int tb, hipStream_t stream, uint16_t* glu, int ldglu,
+                      uint16_t* const* push, int push_rows) {
   // explicit ring schedule (gemm_set_kernel(5) + sched bit 3) or the auto defaults
   const int sched = (g_w4_sched & 8) ? g_w4_sched : g_ring_sched;
   ++g_ring_launches;
@@ -1208,6 +1220,13 @@ void launch_gemm_ring(const GemmArgs& g, int ta, int tb, hipStream_t stream, uin
   const int ntiles = gemm_w4_tiles(g.M, g.N);
   W4Args a{g, g_w4_group_m, {}, g_w4_dbg, glu, ldglu};
   const bool fast = gemm_w4r_fast(g);
+  if (push_rows) {  // row blocks into peers' inboxes: the fast NT epilogue, whole tiles per block
+    const int blocks = push_rows > 0 ? g.M / push_rows : 0;
+    if (!fast || ta || tb || glu || push_rows % 256 || blocks < 1 || blocks > kMaxRanks || blocks * push_rows != g.M)
+      throw std::invalid_argument("gemm ring: push mode needs the fast NT form and M = blocks x push_rows (% 256)");
+    a.push_rows = push_rows;
+    for (int j = 0; j < blocks; ++j) a.push[j] = push[j];
+  }
   const bool pair = sched & 16384;
   const bool persist = fast && (sched & 1);
   const int grid = persist ? std::min(ntiles, cus) : ntiles;

@@ -537,6 +537,29 @@ class DeviceGroup:
                             out.stride(0), float(alpha), bk, self._stream())
         return out
 
+    def gemm_push_allreduce(self, x, w, out, alpha: float = 1.0, max_blocks: Optional[int] = None):
+        """Row-parallel layer output ``out = sum over the group of x_r @ w_r^T`` (bf16, no
+        bias) with the reduce-scatter's traffic inside the GEMM: the GEMM epilogue stores
+        row block j of this rank's partial (M / p rows) straight into rank j's inbox slot
+        as posted writes (over xGMI while the other tiles still compute), then one
+        inbox-to-local two-shot reduces the slots and pulls every block into ``out``
+        (``DeviceComm::gemm_push_rowpar``).  No CTA spins inside the GEMM.  The inbox is a
+        persistent symmetric-heap block of the output's size.  x: [M, K_r], w: [N, K_r];
+        M % (256 p) == 0, K_r % 64 == 0, N % 8 == 0; ``out`` any local [M, N] bf16 tensor.
+        Collective: every rank calls with the same M, N."""
+        torch = self.torch
+        if x.dtype != torch.bfloat16 or w.dtype != torch.bfloat16 or x.dim() != 2 or w.dim() != 2:
+            raise TypeError("gemm_push_allreduce: x [M, K] and w [N, K] must be 2-D bf16")
+        M, K = x.shape
+        N = w.shape[0]
+        if w.shape[1] != K or x.stride(1) != 1 or w.stride(1) != 1 or tuple(out.shape) != (M, N) \
+                or not out.is_contiguous() or out.dtype != torch.bfloat16:
+            raise ValueError("gemm_push_allreduce: shape mismatch, non K-contiguous operand or bad output")
+        inbox = self.persistent("gemm_push_inbox", (M * N,), torch.bfloat16)
+        self.dc.gemm_push_rowpar(x.data_ptr(), w.data_ptr(), out.data_ptr(), inbox.data_ptr(), M, N, K, x.stride(0),
+                                 w.stride(0), float(alpha), self._stream(), self._budget(max_blocks))
+        return out
+
     # -------------------------------------------------------------------- rccl
     def ensure_rccl(self) -> None:
         """Collective: create the RCCL communicator on first use."""

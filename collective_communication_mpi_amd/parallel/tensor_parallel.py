@@ -228,6 +228,10 @@ def _linear_backward(g2: torch.Tensor, x2: torch.Tensor, w: torch.Tensor, need_d
 # * "fused"   -- the all-reduce in the GEMM epilogue (DeviceGroup.gemm_allreduce): tile
 #   owners spin on peers' tiles inside the GEMM (3.1x slower at TP = 2 on a shared GPU,
 #   profiles/r3_tp2).
+# * "push"    -- the GEMM epilogue stores row block j of the partial straight into rank j's
+#   inbox (posted writes under the GEMM, nobody spins), then one inbox-to-local two-shot
+#   (DeviceGroup.gemm_push_allreduce).  Needs M % (256 p) == 0, no bias and the ring GEMM
+#   (a GPU of its own, or CCMPI_SHARED_RING); otherwise plain.
 # * "auto" (default) -- "chunked" when every rank owns its GPU AND each row block's GEMM
 #   still fills the chip (>= one 256x256 tile per CU): the all-reduce then crosses xGMI while
 #   the next block's GEMM keeps every CU busy.  Otherwise "plain": a block of fewer tiles
@@ -236,7 +240,7 @@ def _linear_backward(g2: torch.Tensor, x2: torch.Tensor, w: torch.Tensor, need_d
 #   sharing a GPU compete for the same HBM and CUs (plain measured fastest there:
 #   profiles/r4_first, profiles/r4_shared_ring, 1.18 ms against chunked 1.36 ms at TP = 2).
 #   bench.py's mlp phase records all three modes (tp_mlp.row_mode_variants).
-ROW_MODES = ("plain", "chunked", "fused")
+ROW_MODES = ("plain", "chunked", "fused", "push")
 _ROW_MODE = os.environ.get("CCMPI_TP_ROW_MODE", "auto")
 
 
@@ -290,6 +294,17 @@ def _fused_ok(x2: torch.Tensor, w: torch.Tensor, comm) -> bool:
         return False
     p, _ = _size_rank(comm)
     return p > 1 and x2.shape[1] % 64 == 0 and w.shape[0] % 8 == 0 and x2.shape[0] > 0
+
+
+def _push_ok(x2: torch.Tensor, w: torch.Tensor, b, comm) -> bool:
+    """The push row-parallel form applies (identical answer on every rank of the group):
+    CUDA bf16, no bias, M % (256 p), K shard % 64, N % 8, the ring GEMM allowed."""
+    if not (x2.is_cuda and x2.dtype == torch.bfloat16 and w.dtype == torch.bfloat16) or b is not None:
+        return False
+    p, _ = _size_rank(comm)
+    M, K = x2.shape
+    return (p > 1 and M > 0 and M % (256 * p) == 0 and K % 64 == 0 and w.shape[0] % 8 == 0
+            and x2.stride(0) % 8 == 0 and w.stride(0) % 8 == 0 and not _gpu_shared(comm))
 
 
 def _chunk_rows(M: int, c: int) -> list:
@@ -383,6 +398,10 @@ class _RowParallelFn(torch.autograd.Function):
             out = _scratch(comm, "row_fused", (M, N), torch.bfloat16)
             dev.gemm_allreduce(x2, w, bias=b, out=out)
             y2.copy_(out)
+            return y
+        if mode == "push" and _push_ok(x2, w, b, comm):
+            CALLS["row_push"] += 1
+            dev.gemm_push_allreduce(x2, w, y2)
             return y
         part = _scratch(comm, "row_partial", (M, N), x.dtype)
         blocks = _chunk_rows(M, _TP_CHUNKS) if mode == "chunked" else [(0, M)]

@@ -53,3 +53,25 @@ def test_row_parallel_auto_mode(monkeypatch):
     monkeypatch.setattr(tp, "device_group_for", lambda comm: SimpleNamespace(shared_device=True))
     assert tp._row_mode("auto", object(), 16384, 8192) == "plain"
     assert tp._row_mode("fused", object(), 4096, 4096) == "fused"
+
+
+def test_row_parallel_push_applies(monkeypatch):
+    """``push`` (GEMM epilogue into the owners' inboxes) needs whole 256-row tiles per rank
+    block, no bias, K % 64, N % 8 and the ring GEMM; otherwise the layer runs plain."""
+    from types import SimpleNamespace
+
+    from collective_communication_mpi_amd.parallel import tensor_parallel as tp
+
+    def t(*shape):
+        return SimpleNamespace(is_cuda=True, dtype=torch.bfloat16, shape=shape, stride=lambda d: shape[1])
+
+    monkeypatch.setattr(tp, "_size_rank", lambda comm: (4, 0))
+    monkeypatch.setattr(tp, "_gpu_shared", lambda comm: False)
+    assert "push" in tp.ROW_MODES
+    assert tp._push_ok(t(4096, 3584), t(4096, 3584), None, object())
+    assert not tp._push_ok(t(4096, 3584), t(4096, 3584), object(), object())  # bias
+    assert not tp._push_ok(t(2048 + 256, 3584), t(4096, 3584), None, object())  # M % (256 p)
+    assert not tp._push_ok(t(4096, 3600), t(4096, 3600), None, object())  # K % 64
+    assert not tp._push_ok(t(4096, 3584), t(4100, 3584), None, object())  # N % 8
+    monkeypatch.setattr(tp, "_gpu_shared", lambda comm: True)
+    assert not tp._push_ok(t(4096, 3584), t(4096, 3584), None, object())  # ring GEMM off

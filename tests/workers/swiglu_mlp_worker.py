@@ -86,6 +86,47 @@ if args.big and args.device == "cuda" and os.environ.get("CCMPI_KMAJOR_MIN_MACS"
     if not _tp.CALLS["dh_transposed"]:
         fails.append("--big: the dW transpose route (dh^T from the SwiGLU backward) did not run")
 
+if args.big and args.device == "cuda" and p > 1 and os.environ.get("CCMPI_SHARED_RING") == "1":
+    # the push row-parallel form (the GEMM epilogue stores each row block into its owner's
+    # inbox, then an inbox-to-local two-shot): same bf16 partials and the same rank-order
+    # reduction as plain, so the block's output must match plain bit for bit
+    from collective_communication_mpi_amd.parallel import tensor_parallel as tp  # noqa: E402
+
+    outs = {}
+    dg = tp.device_group_for(comm)
+    for mode in ("plain", "push"):
+        m = ParallelSwiGLUMLP(D, F, comm, device=dev, dtype=dt, seed=11, mode=mode)
+        for it in range(2):
+            xi = x0.to(dt).to(dev).requires_grad_(True)
+            c0, h0 = tp.CALLS["row_" + mode], dg.host_calls
+            yi = m(xi)
+            yi.backward(gy.to(dt).to(dev))
+            torch.cuda.synchronize()
+            if tp.CALLS["row_" + mode] != c0 + 1:
+                fails.append(f"{mode}: row path did not run ({dict(tp.CALLS)})")
+            if it == 1 and dg.host_calls != h0:
+                fails.append(f"{mode}: steady-state step made {dg.host_calls - h0} host calls (expected 0)")
+        outs[mode] = (yi.detach().clone(), xi.grad.clone())
+    if not torch.equal(outs["push"][0], outs["plain"][0]):
+        fails.append(f"push: forward differs from plain (max {(outs['push'][0].float() - outs['plain'][0].float()).abs().max().item()})")
+    if rel(outs["push"][1], xr.grad) > tol:
+        fails.append(f"push: dx rel err {rel(outs['push'][1], xr.grad)}")
+    # the DeviceGroup call itself against an fp32 sum of every rank's product, 2 shapes
+    for (M2, N2, K2) in ((256 * p, 512, 128), (512 * p, 1032, 192)):
+        ga = torch.Generator().manual_seed(40 + rank)
+        xa = (torch.randn(M2, K2, generator=ga) * 0.5).to(dt)
+        wa = (torch.randn(N2, K2, generator=ga) * 0.5).to(dt)
+        ref = sum(a.float() @ b.float().T for a, b in hc.allgather((xa, wa)))
+        out = torch.empty(M2, N2, dtype=dt, device=dev)
+        dg.gemm_push_allreduce(xa.to(dev), wa.to(dev), out)
+        if rel(out, ref) > 0.02:
+            fails.append(f"gemm_push_allreduce {M2}x{N2}x{K2}: rel err {rel(out, ref)}")
+    try:
+        dg.gemm_push_allreduce(xa[:300].to(dev), wa.to(dev), torch.empty(300, N2, dtype=dt, device=dev))
+        fails.append("gemm_push_allreduce accepted M % (256 p) != 0")
+    except (ValueError, RuntimeError):
+        pass
+
 if args.device == "cuda" and p > 1 and not args.big:
     # every row-parallel mode through the whole block (forward + backward), its path
     # really taken, and a steady-state step with no host call from the device plane
