@@ -225,11 +225,13 @@ def test_parallel_swiglu_mlp_gpu(n):
     assert "swiglu mlp OK" in r.stdout
 
 
-@pytest.mark.parametrize("n", [2, 4])
+@pytest.mark.parametrize("n", [2, 4, 8])
 def test_swiglu_mlp_ring_gemm_beside_collectives_gpu(n):
     """the kernels an 8-GPU TP run uses (LDS-ring GEMMs, the SwiGLU
     epilogue, K-major backward rings) next to the other ranks' TP collectives on one GPU:
-    CCMPI_SHARED_RING=1 keeps the ring on and holds every collective to half the CUs."""
+    CCMPI_SHARED_RING=1 keeps the ring on and holds every collective to half the CUs.  The
+    worker also checks the push row mode against plain, bit for bit (8 ranks: the driver's
+    8-GPU mlp phase runs it at TP = 8)."""
     # (CCMPI_KMAJOR_MIN_MACS=1: these small shapes also take the dW transpose route, with
     # dh^T from the fused SwiGLU backward, across TP ranks)
     env = {**ENV, "CCMPI_SHARED_RING": "1", "CCMPI_RING_MIN_MACS": "1", "CCMPI_KMAJOR_MIN_MACS": "1"}

@@ -34,7 +34,7 @@ if args.device == "cuda":
 else:
     dev, dt, tol = torch.device("cpu"), torch.float32, 1e-4
 
-D, F, T = (1024, 512 * p, 1024) if args.big else (128, 64 * p, 48)
+D, F, T = (1024, 512 * p, max(1024, 256 * p)) if args.big else (128, 64 * p, 48)  # push: T % (256 p)
 if args.big and args.device == "cuda":
     from collective_communication_mpi_amd import _native  # noqa: E402
 
