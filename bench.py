@@ -21,7 +21,8 @@ Metric (BASELINE.json): "all-reduce algbw (GB/s) @1GiB fp32 + DP4xTP2 fwd step t
   kernels.  Every candidate's time is reported.  At N >= 2 a size sweep
   (``DeviceGroup.tune``) follows, written as a tuning table that every later
   phase's device groups load (``CCMPI_TUNE_FILE``), so ``algo="auto"`` in the TP
-  and DDP layers uses what was measured on this node.
+  and DDP layers uses what was measured on this node.  At N >= 4 the harness's
+  2-rank TP groups (a table key of their own) are swept as well, up to 16 MiB.
 * Every measurement runs in a supervised child phase of fresh processes (the
   process that ``bench.py`` starts never touches the GPU), each under its own
   wall-clock budget; rank 0 merges their JSON records into the one output line.
@@ -34,7 +35,7 @@ Metric (BASELINE.json): "all-reduce algbw (GB/s) @1GiB fp32 + DP4xTP2 fwd step t
                         step, TP=2 x DP=N/2 for N >= 2 (DP4xTP2 at N = 8)
   ``mlp``               TP Llama-3-8B MLP block over all ranks (hand-written MFMA
                         GEMMs, SwiGLU epilogue, TP all-reduces; unfused, chunked-
-                        overlap and fused row-parallel variants)
+                        overlap, fused and push row-parallel variants)
   ``dp``                BASELINE config 5: DP over all ranks of a Llama-3-8B-sized
                         model (16 GB bf16 gradients) through ``DistributedDataParallel``,
                         bucket all-reduces launched from autograd hooks during a real
@@ -533,8 +534,28 @@ def tuning_sweep(comm, args, best_1gib: str, log=lambda *a: None) -> dict:
         save_tuning(os.environ["CCMPI_TUNE_FILE"], dev.tune_key, dev.tuned)
     comm.comm.Barrier()
     log(f"tuning sweep {time.perf_counter() - t0:.1f}s: {table}")
-    return {"key": dev.tune_key, "table": {f"2^{lg}": a for (_, lg), a in sorted(dev.tuned.items())},
-            "seconds": round(time.perf_counter() - t0, 1)}
+    out = {"key": dev.tune_key, "table": {f"2^{lg}": a for (_, lg), a in sorted(dev.tuned.items())},
+           "seconds": round(time.perf_counter() - t0, 1)}
+    world = comm.Get_size()
+    if world >= 4 and world % 2 == 0:
+        # the harness's TP pairs (mp-major grid: ranks 2k, 2k + 1, reference func_impl.py:53-62)
+        # are 2-rank groups with a table key of their own: sweep them too (every pair at once,
+        # up to 16 MiB -- the TP all-reduce is 2 MiB), so their auto is measured, not a default
+        t1 = time.perf_counter()
+        sub = comm.Split(comm.Get_rank(), comm.Get_rank() // 2)
+        sdev = sub.dev
+        sdev.tune(max_bytes=min(args.tune_max_mb, 16) << 20, min_bytes=16 << 10,
+                  algos=["ll", "oneshot", "fanout", "twoshot", "ring", "rhd"], iters=5, dtype=torch.float32, save=None)
+        if comm.Get_rank() == 0 and os.environ.get("CCMPI_TUNE_FILE"):
+            from collective_communication_mpi_amd.device import save_tuning
+
+            save_tuning(os.environ["CCMPI_TUNE_FILE"], sdev.tune_key, sdev.tuned)
+        comm.comm.Barrier()
+        out["tp_pairs"] = {"key": sdev.tune_key,
+                           "table": {f"2^{lg}": a for (_, lg), a in sorted(sdev.tuned.items())},
+                           "seconds": round(time.perf_counter() - t1, 1)}
+        log(f"TP-pair tuning sweep {out['tp_pairs']['seconds']}s: {out['tp_pairs']['table']}")
+    return out
 
 
 # ------------------------------------------------------------------ phases
