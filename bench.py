@@ -26,7 +26,9 @@ Metric (BASELINE.json): "all-reduce algbw (GB/s) @1GiB fp32 + DP4xTP2 fwd step t
 * Every measurement runs in a supervised child phase of fresh processes (the
   process that ``bench.py`` starts never touches the GPU), each under its own
   wall-clock budget; rank 0 merges their JSON records into the one output line.
-  A phase that crashes, hangs or errors costs only its own entry:
+  A phase that crashes, hangs or errors costs only its own entry (the ``coll`` phase
+  writes its record as soon as the headline is measured, so a failure in its tuning
+  sweep leaves ``value`` in place, marked ``partial``):
 
   ====================  =========================================================
   ``coll``              the headline (hand-written all-reduce candidates, 1 GiB
@@ -196,6 +198,13 @@ def merge_results(args, size: int, status: dict, load) -> dict:
     phase fills its own key and a failed phase leaves an error there, nothing else."""
     out = load("coll") if status.get("coll", {}).get("ok") else None
     if out is None:
+        # the coll phase writes its record once the headline is measured, before the
+        # secondary tuning sweep: a sweep that dies or hangs keeps the headline
+        early = load("coll")
+        if early and early.get("partial"):
+            out = early
+            out.setdefault("config", {})["coll_phase_error"] = f"after the headline: {status.get('coll')}"
+    if out is None:
         out = empty_headline(args, size, f"collective phase failed: {status.get('coll')}")
     c = out.setdefault("config", {})
 
@@ -292,7 +301,7 @@ def supervise(args) -> int:
                 return None
 
         out = merge_results(args, size, status, load)
-        if not status["coll"]["ok"]:
+        if not status["coll"]["ok"] and not out.get("partial"):
             rc = 1
         if size == 1 and args.shared_dry_run > 1 and not args.no_secondary:
             out["config"]["shared_gpu_dry_run"] = shared_dry_run(args.shared_dry_run, steps=5, warmup=2,
@@ -573,8 +582,23 @@ def coll_phase(args) -> dict:
     groups = ("ar",) if args.no_secondary else ("ar", "bf16", "a2a")
     r = run_collectives(comm, args, log, groups)
     _fault_injection("coll")
-    tuning = tuning_sweep(comm, args, r["best"], log) if not args.no_secondary else {}
+    tuning = {}
+    rec = coll_record(args, comm, r, tuning)
+    if not args.no_secondary:
+        _write_result(args, rank, {**rec, "partial": "written before the tuning sweep"})
+        _fault_injection("coll_tuning")
+        try:
+            tuning.update(tuning_sweep(comm, args, r["best"], log))
+        except Exception as e:  # noqa: BLE001 - the sweep is secondary; the headline stands
+            tuning["error"] = f"{type(e).__name__}: {e}"[:300]
     torch.cuda.synchronize()
+    return rec
+
+
+def coll_record(args, comm, r: dict, tuning: dict) -> dict:
+    """The headline record of the coll phase (``tuning`` is filled in place afterwards)."""
+    dev = comm.dev
+    world = comm.Get_size()
     tp = args.tp or (2 if world >= 2 and world % 2 == 0 else 1)
     return {
         "metric": METRIC,

@@ -91,3 +91,16 @@ def test_multi_stream_graph_hazard(monkeypatch):
     monkeypatch.setenv("GPU_MAX_HW_QUEUES", "1")
     single = SimpleNamespace(tp_dev=object(), _token_chunks=lambda B: 1)
     assert multi_stream_graph_hazard(cfg, single) is None
+
+
+def test_tuning_sweep_failure_keeps_headline():
+    """The coll phase writes its record (``partial``) once the headline is measured, before
+    the secondary tuning sweep: a sweep that crashes or hangs costs the table, not ``value``."""
+    args = bench.parse([])
+    early = {**_coll(), "partial": "written before the tuning sweep"}
+    out = bench.merge_results(args, 8, _status(coll=-11), {"coll": early}.get)
+    assert out["value"] == 500.0 and out["config"]["allreduce_algo"] == "fanout:512"
+    assert "-11" in out["config"]["coll_phase_error"]
+    # no record at all: the zero headline, as before
+    out = bench.merge_results(args, 8, _status(coll=-11), {}.get)
+    assert out["value"] == 0.0

@@ -168,6 +168,26 @@ def test_bench_harness_crash_keeps_headline():
     assert "tp_fwd_step_ms" not in c
 
 
+def test_bench_tuning_crash_keeps_headline():
+    """The coll phase writes the headline before its secondary tuning sweep: a SIGSEGV right
+    after it (injected: CCMPI_BENCH_FAULT=coll_tuning) keeps ``value`` and the exit status."""
+    import json
+    import subprocess
+    import sys
+
+    from _launch import REPO
+
+    e = dict(os.environ, **ENV, CCMPI_BENCH_FAULT="coll_tuning")
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--steps", "2", "--warmup", "1", "--size-mb", "16",
+                        "--a2a-mb", "8", "--dp-layers", "0", "--batch", "128", "--tune-max-mb", "1", "--no-rccl",
+                        "--no-harness", "--mlp-tokens", "0"], cwd=REPO, env=e, capture_output=True, text=True, timeout=400)
+    assert r.returncode == 0, r.stderr[-4000:]
+    out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    c = out["config"]
+    assert out["value"] > 0 and c["result_exact"] and out.get("partial"), out
+    assert "-11" in c["coll_phase_error"], c.get("coll_phase_error")
+
+
 @pytest.mark.parametrize("case", ["myallreduce", "myalltoall"])
 def test_cli_device_cases(case):
     """The reference CLI cases on device buffers (reference mpi-test.py:42-98,178-239):
