@@ -488,7 +488,7 @@ def run_collectives(comm, args, log=lambda *a: None, groups=("ar", "bf16", "a2a"
                             "candidates_ms": ms(res16)}
     if "a2a" in groups:
         # ---- all-to-all, 256 MiB per rank (BASELINE config 3)
-        an = ((args.a2a_mb << 20) // 4) // world * world
+        an = min((args.a2a_mb << 20) // 4, x.numel()) // world * world  # within the 1 GiB buffers
         blk = an // world
         xa, ya = x[:an], y[:an]
         xa.view(world, blk).copy_((rank * world + torch.arange(world, device=dev.device, dtype=torch.float32))
