@@ -70,7 +70,7 @@ sys.path.insert(0, REPO)
 GiB = 1 << 30
 XGMI_LINK_GBPS = 153.6  # MI355X xGMI, per link and direction (7 links x 153.6 = 1075 GB/s per GPU)
 METRIC = "all-reduce algbw (GB/s) @1GiB fp32 + DP4xTP2 fwd step time, 1/2/4/8 MI355X"
-PHASES = ("coll", "harness", "mlp", "dp", "rccl")
+PHASES = ("coll", "harness", "mlp", "dp", "rccl", "host")
 
 
 def parse(argv=None):
@@ -107,6 +107,11 @@ def parse(argv=None):
     ap.add_argument("--dp-timeout", type=float, default=600.0, help="wall-clock budget of the DP-overlap phase (s)")
     ap.add_argument("--mlp-timeout", type=float, default=300.0, help="wall-clock budget of the TP MLP phase (s)")
     ap.add_argument("--no-rccl", action="store_true", help="skip the RCCL baseline phase")
+    ap.add_argument("--host-ranks", type=int, default=8,
+                    help="BASELINE config 1: CPU processes of the host-plane phase (0 = off)")
+    ap.add_argument("--host-count", type=int, default=1024, help="host phase: float32 elements per buffer")
+    ap.add_argument("--host-runs", type=int, default=100, help="host phase: timed runs (reference: 100)")
+    ap.add_argument("--host-timeout", type=float, default=180.0, help="wall-clock budget of the host phase (s)")
     return ap.parse_args(argv)
 
 
@@ -183,6 +188,8 @@ def plan_phases(args, size: int):
         out.append(("dp", args.dp_timeout))
     if size > 1 and not args.no_rccl:
         out.append(("rccl", args.rccl_timeout))
+    if sec and args.host_ranks > 1:
+        out.append(("host", args.host_timeout))
     return out
 
 
@@ -227,7 +234,12 @@ def merge_results(args, size: int, status: dict, load) -> dict:
         c["dp_overlap"] = rec("dp")
     if "rccl" in status:
         merge_rccl(out, load("rccl") if status["rccl"]["ok"] else None, status["rccl"])
+    if "host" in status:
+        c["host_cpu"] = rec("host")  # BASELINE config 1 (8 CPU processes, 1k float32)
     c["phases"] = status
+    if out.get("partial") and not status.get("coll", {}).get("ok"):
+        # the headline survived a failure later in the coll phase: say so at the top level
+        out["warning"] = "coll phase failed after the headline was measured (config.coll_phase_error)"
     return out
 
 
@@ -284,7 +296,18 @@ def supervise(args) -> int:
                "--result", os.path.join(tmp, f"{phase}.json")]
         if rank == 0:
             print(f"[bench] phase {phase} (budget {budget:.0f}s) ...", file=sys.stderr, flush=True)
-        rc, secs = _run_child(cmd, env, budget, abort_flag=os.path.join(tmp, f"{phase}.abort"))
+        if phase == "host":
+            # BASELINE config 1 is an 8-process CPU job whatever N is: rank 0 launches it
+            # (host plane only, a job of its own), the other ranks wait
+            rc, secs = 0, 0.0
+            if rank == 0:
+                for k in ("CCMPI_RANK", "CCMPI_SIZE", "CCMPI_LOCAL_RANK", "CCMPI_LOCAL_SIZE", "CCMPI_JOBID"):
+                    env.pop(k, None)
+                cmd = [sys.executable, "-m", "collective_communication_mpi_amd.launch", "-n", str(args.host_ranks),
+                       "--timeout", str(int(budget)), *cmd]
+                rc, secs = _run_child(cmd, env, budget + 15)
+        else:
+            rc, secs = _run_child(cmd, env, budget, abort_flag=os.path.join(tmp, f"{phase}.abort"))
         if rank == 0:
             print(f"[bench] phase {phase}: rc {rc}, {secs:.1f}s", file=sys.stderr, flush=True)
         ok = world.allreduce(int(rc == 0), op=MPI.MIN)
@@ -322,7 +345,7 @@ def shared_dry_run(n: int, steps: int, warmup: int, verbose: bool):
     cmd = [sys.executable, "-m", "collective_communication_mpi_amd.launch", "-n", str(n), "--timeout", "600",
            sys.executable, os.path.abspath(__file__), "--gpus", str(n), "--steps", str(steps), "--warmup", str(warmup),
            "--dp-layers", "0", "--a2a-mb", "64", "--shared-dry-run", "0", "--no-rccl", "--mlp-tokens", "0",
-           "--tune-max-mb", "0"]
+           "--tune-max-mb", "16", "--host-ranks", "0"]
     env = dict(os.environ, CCMPI_BENCH_CHILD="1")
     q = os.environ.get("CCMPI_DRYRUN_HW_QUEUES", "1")
     if q:
@@ -342,9 +365,10 @@ def shared_dry_run(n: int, steps: int, warmup: int, verbose: bool):
     keep["unit"] = "GB/s (1 GiB fp32 all-reduce algbw)"
     keep["note"] = f"{n} ranks sharing ONE GPU through IPC: HBM + protocol, not xGMI"
     keep["hw_queues_per_rank"] = env.get("GPU_MAX_HW_QUEUES", "HIP default")
-    keep.update({k: out["config"].get(k) for k in ("allreduce_algo", "busbw_GBps", "candidates_ms", "result_exact",
-                                                     "self_test", "bf16_1GiB", "alltoall", "tp_fwd_step_ms",
-                                                     "tp_train_step_ms", "parallelism", "phases")})
+    keep.update({k: out["config"].get(k) for k in ("allreduce_algo", "busbw_GBps", "candidates_ms", "candidates",
+                                                     "result_exact", "self_test", "bf16_1GiB", "alltoall",
+                                                     "alltoall_pairwise", "sweep", "tuning", "tp_fwd_step_ms",
+                                                     "tp_train_step_ms", "parallelism", "harness", "phases")})
     return keep
 
 
@@ -410,10 +434,104 @@ def allreduce_candidates(world: int, shared: bool, algo: str = "auto"):
     return hand
 
 
-def run_collectives(comm, args, log=lambda *a: None, groups=("ar", "bf16", "a2a")) -> dict:
-    """The hand-written collective measurements of one process (collective: every rank
-    calls).  ``groups`` selects the candidate loop (``ar``, required for the others),
-    the bf16 all-reduce and the all-to-all.  Returns the record's headline fields."""
+def _base_algo(algo: str) -> str:
+    """The self-test family of a candidate (``fanout_lds:512`` -> ``fanout``)."""
+    b = algo.split(":")[0]
+    return "fanout" if b == "fanout_lds" else b
+
+
+def order_candidates(cands, self_test, disabled):
+    """(candidates in try order, {skipped candidate: reason}).  Candidates whose algorithm
+    family failed the bring-up ``self_test`` (``DeviceGroup.disabled``, also
+    ``CCMPI_DISABLE_ALGOS``) are skipped; those whose family passed it come first, the
+    untested families (push, ring, RHD) after them, each group in the given order."""
+    skipped = {a: "disabled (failed self_test or CCMPI_DISABLE_ALGOS)" for a in cands
+               if a.split(":")[0] in disabled or _base_algo(a) in disabled}
+    st = self_test or {}
+    keep = [a for a in cands if a not in skipped]
+    return sorted(keep, key=lambda a: 0 if st.get(_base_algo(a)) else 1), skipped
+
+
+def pick_candidates(cands, attempt, agree, reset, timer, log=lambda *a: None):
+    """Try every candidate, whatever happened to the ones before it (collective: every rank
+    runs the same sequence).  ``attempt(c)`` runs ``c`` once and returns None or this rank's
+    error text (an exception counts as an error); ``agree(err)`` returns None when every rank
+    succeeded, else the first failing rank's error (host all-gather); ``reset()`` restores
+    the device state after a failure (a timed-out kernel leaves per-CTA epochs
+    inconsistent); ``timer(c)`` returns seconds per call, followed by one more ``agree`` on
+    the device error state after timing.  Returns ({candidate: {"ms", "error"}}, fastest
+    or None).  Like the reference's per-run oracle check (mpi-test.py:75-84): a mismatch
+    is reported, the run goes on."""
+    out = {}
+    for c in cands:
+        try:
+            err = attempt(c)
+        except Exception as e:  # noqa: BLE001 - any failure disqualifies the candidate, not the run
+            err = f"{type(e).__name__}: {e}"
+        err = agree(err)
+        t = None
+        if not err:
+            try:
+                t = timer(c)
+                err = None
+            except Exception as e:  # noqa: BLE001
+                err = f"during timing: {type(e).__name__}: {e}"
+            err = agree(err)
+        if err:
+            log(f"candidate {c} failed: {err}")
+            out[c] = {"ms": None, "error": str(err)[:400]}
+            reset()
+            continue
+        out[c] = {"ms": round(t * 1e3, 4), "error": None}
+        log(f"candidate {c}: {t * 1e3:.3f} ms")
+    good = {c: o["ms"] for c, o in out.items() if o["ms"]}
+    return out, (min(good, key=good.get) if good else None)
+
+
+def _injected(algo: str, kind: str) -> bool:
+    """Tests: ``CCMPI_BENCH_FAULT=candidate:<algo>[,candidate_bf16:<algo>,...]`` makes rank 0
+    skip that candidate's kernel (its peers then time out in theirs, as on a broken link)
+    and report the failure.  ``candidate:`` matches fp32 and bf16, ``candidate_<kind>:``
+    only that kind; ``*`` matches every algorithm."""
+    if _env_rank()[0] != 0:
+        return False
+    for ent in os.environ.get("CCMPI_BENCH_FAULT", "").split(","):
+        pre, _, a = ent.partition(":")
+        if pre in ("candidate", f"candidate_{kind}") and a in ("*", algo):
+            return True
+    return False
+
+
+def _device_agree(comm):
+    """``agree`` of ``pick_candidates`` over the host plane, with the device's error state
+    (a timeout code names phase and peer) folded into this rank's error."""
+    dev, hc = comm.dev, comm.comm
+
+    def agree(err):
+        try:
+            dev.check()
+        except Exception as e:  # noqa: BLE001
+            err = f"{err}; {e}" if err else str(e)
+        errs = hc.allgather(err)
+        bad = [(r, e) for r, e in enumerate(errs) if e]
+        return "; ".join(f"rank {r}: {e}" for r, e in bad[:3]) if bad else None
+
+    return agree
+
+
+def _bw(nbytes: int, ms, world: int, ar: bool = True) -> dict:
+    if not ms:
+        return {"algbw_GBps": None, "busbw_GBps": None}
+    alg = nbytes / (ms / 1e3) / 1e9
+    f = (2 * (world - 1) / world if ar else (world - 1) / world) if world > 1 else 0.0
+    return {"algbw_GBps": round(alg, 2), "busbw_GBps": round(alg * f, 2)}
+
+
+def run_headline(comm, args, log=lambda *a: None) -> dict:
+    """The headline (collective: every rank calls): bring-up self test, every hand-written
+    all-reduce candidate on the 1 GiB fp32 buffer (each checked exact, then timed; a failed
+    one is reset away and the next is tried), then the K timed steps of the fastest.
+    Returns the record fields plus the buffers for the secondaries (``x``, ``y``)."""
     import torch
 
     from collective_communication_mpi_amd import MPI
@@ -421,53 +539,21 @@ def run_collectives(comm, args, log=lambda *a: None, groups=("ar", "bf16", "a2a"
     rank, world = comm.Get_rank(), comm.Get_size()
     dev, hc = comm.dev, comm.comm
     sync_barrier, timed = _timers(comm)
-    # bring-up check of the small-message algorithms `auto` uses inside the harness
-    # (LL, one-shot) on this fabric: a failing one is disabled on every rank
+    # bring-up check of the algorithms `auto` picks on this fabric: a failing one is
+    # disabled on every rank (and its candidates are skipped below)
     self_test = dev.self_test() if world > 1 else None
     log(f"self test: {self_test}")
     nbytes = args.size_mb << 20
     x = dev.empty(nbytes // 4, torch.float32)
     y = dev.empty(nbytes // 4, torch.float32)
-    failed = [False]
-
-    def pick(buf_in, buf_out, expect, cands):
-        results = {}
-        for algo in cands:
-            if failed[0]:
-                # the hand-written kernels share one flag protocol: after one of them failed
-                # (and waited out the device timeout) the others are not tried
-                results[algo] = None
-                continue
-            ok = 1
-            try:
-                buf_out.zero_()
-                sync_barrier()
-                dev.allreduce(buf_in, buf_out, "SUM", algo, symmetric=True)
-                torch.cuda.synchronize()
-                dev.check()
-                ok = int(bool(torch.all(buf_out == expect).item()))
-            except Exception as e:  # noqa: BLE001 - any failure disqualifies the candidate
-                log(f"candidate {algo} failed: {e}")
-                ok = 0
-            if not hc.allreduce(ok, op=MPI.MIN):
-                results[algo] = None
-                failed[0] = True
-                dev.reset()  # a timed-out kernel leaves per-CTA epochs inconsistent
-                continue
-            dev.allreduce(buf_in, buf_out, "SUM", algo, symmetric=True)
-            results[algo] = timed(lambda: dev.allreduce(buf_in, buf_out, "SUM", algo, symmetric=True), 3)
-            log(f"candidate {algo} ({buf_in.dtype}): {results[algo] * 1e3:.3f} ms")
-        good = {a: t for a, t in results.items() if t}
-        if not good:
-            raise SystemExit("no all-reduce algorithm produced a correct result")
-        return results, min(good, key=good.get)
-
-    def ms(results):
-        return {a: (round(t * 1e3, 4) if t else None) for a, t in results.items()}
-
     x.fill_(float(rank + 1))
     expect = float(world * (world + 1) // 2)
-    results, best = pick(x, y, expect, allreduce_candidates(world, dev.shared_device, args.algo))
+    cands, skipped = order_candidates(allreduce_candidates(world, dev.shared_device, args.algo), self_test,
+                                      dev.disabled)
+    outcomes, best = pick_candidates(cands, *allreduce_trial(comm, x, y, expect, "fp32"), log=log)
+    outcomes.update({a: {"ms": None, "error": why} for a, why in skipped.items()})
+    if best is None:
+        raise SystemExit(f"no all-reduce algorithm produced a correct result: {outcomes}")
     for _ in range(args.warmup):
         dev.allreduce(x, y, "SUM", best, symmetric=True)
     t_step = timed(lambda: dev.allreduce(x, y, "SUM", best, symmetric=True), args.steps)
@@ -475,50 +561,101 @@ def run_collectives(comm, args, log=lambda *a: None, groups=("ar", "bf16", "a2a"
     final_ok = bool(hc.allreduce(int(bool(torch.all(y == expect).item())), op=MPI.MIN))
     algbw = nbytes / t_step / 1e9
     busbw = algbw * (2 * (world - 1) / world) if world > 1 else 0.0
+    return {"algbw": algbw, "busbw": busbw, "t_step": t_step, "best": best, "outcomes": outcomes,
+            "results": {a: o["ms"] for a, o in outcomes.items()}, "final_ok": final_ok, "self_test": self_test,
+            "x": x, "y": y, "expect": expect}
+
+
+def allreduce_trial(comm, xin, yout, expect: float, kind: str):
+    """(attempt, agree, reset, timer) of ``pick_candidates`` for all-reduce candidates on the
+    symmetric buffers ``xin`` -> ``yout`` (rank-valued input: the exact result is known)."""
+    import torch
+
+    dev = comm.dev
+    sync_barrier, timed = _timers(comm)
+
+    def attempt(algo):
+        yout.zero_()
+        sync_barrier()
+        if _injected(algo, kind):
+            return "injected fault (CCMPI_BENCH_FAULT): kernel skipped on rank 0"
+        dev.allreduce(xin, yout, "SUM", algo, symmetric=True)
+        torch.cuda.synchronize()
+        dev.check()
+        return None if bool(torch.all(yout == expect).item()) else "wrong result"
+
+    def timer(algo):
+        dev.allreduce(xin, yout, "SUM", algo, symmetric=True)
+        return timed(lambda: dev.allreduce(xin, yout, "SUM", algo, symmetric=True), 3)
+
+    return attempt, _device_agree(comm), dev.reset, timer
+
+
+def run_secondaries(comm, args, h: dict, log=lambda *a: None, groups=("bf16", "a2a")) -> dict:
+    """The secondary device collectives after the headline (collective): the 1 GiB bf16
+    all-reduce (BASELINE config 2: the three fastest fp32 candidates, plus the hand-written
+    ring timed on its own), and the all-to-all of ``--a2a-mb`` per rank (config 3: direct,
+    push and pairwise, the pairwise time reported under its own key).  Every block that
+    fails records an error instead of raising."""
+    import torch
+
+    rank, world = comm.Get_rank(), comm.Get_size()
+    dev = comm.dev
+    _, timed = _timers(comm)
+    x, y, expect = h["x"], h["y"], h["expect"]
+    nbytes = x.numel() * 4
     sec = {}
     if "bf16" in groups:
-        # ---- 1 GiB bf16 all-reduce (BASELINE config 2): rank-valued, exact in bf16
         xb, yb = x.view(torch.bfloat16), y.view(torch.bfloat16)
-        xb.fill_(float(rank + 1))
-        top = sorted((a for a, t in results.items() if t), key=lambda a: results[a])[:3]
-        res16, best16 = pick(xb, yb, expect, top)
-        t16 = timed(lambda: dev.allreduce(xb, yb, "SUM", best16, symmetric=True), max(3, args.steps // 2))
-        sec["bf16_1GiB"] = {"algo": best16, "ms": round(t16 * 1e3, 4), "algbw_GBps": round(nbytes / t16 / 1e9, 2),
-                            "busbw_GBps": round(nbytes / t16 / 1e9 * (2 * (world - 1) / world), 2) if world > 1 else 0.0,
-                            "candidates_ms": ms(res16)}
+        xb.fill_(float(rank + 1))  # rank-valued: exact in bf16
+        good = {a: o["ms"] for a, o in h["outcomes"].items() if o["ms"]}
+        top = sorted(good, key=good.get)[:3]
+        if world > 1 and "ring" not in top and args.algo == "auto":
+            top.append("ring")  # BASELINE config 2 names the ring: always a bf16 point of its own
+        res16, best16 = pick_candidates(top, *allreduce_trial(comm, xb, yb, expect, "bf16"), log=log)
+        b16 = {"candidates": res16, "candidates_ms": {a: o["ms"] for a, o in res16.items()}}
+        if best16 is None:
+            b16["error"] = "no bf16 candidate produced a correct result"
+        else:
+            t16 = timed(lambda: dev.allreduce(xb, yb, "SUM", best16, symmetric=True), max(3, args.steps // 2))
+            b16.update({"algo": best16, "ms": round(t16 * 1e3, 4), **_bw(nbytes, t16 * 1e3, world)})
+        if "ring" in res16:
+            b16["ring"] = {"ms": res16["ring"]["ms"], "error": res16["ring"]["error"],
+                           **_bw(nbytes, res16["ring"]["ms"], world)}
+        sec["bf16_1GiB"] = b16
     if "a2a" in groups:
-        # ---- all-to-all, 256 MiB per rank (BASELINE config 3)
         an = min((args.a2a_mb << 20) // 4, x.numel()) // world * world  # within the 1 GiB buffers
         blk = an // world
         xa, ya = x[:an], y[:an]
         xa.view(world, blk).copy_((rank * world + torch.arange(world, device=dev.device, dtype=torch.float32))
                                   .view(world, 1).expand(world, blk))
         want = (torch.arange(world, device=dev.device, dtype=torch.float32) * world + rank).view(world, 1).expand(world, blk)
-        a2a = {}
-        for algo in ["direct", "push", "pairwise"]:
-            log(f"alltoall {algo}")
-            try:
-                ya.zero_()
-                sync_barrier()
-                dev.alltoall(xa, ya, algo)
-                torch.cuda.synchronize()
-                dev.check()
-                ok = int(torch.equal(ya.view(world, blk), want))
-            except Exception as e:  # noqa: BLE001
-                log(f"alltoall {algo} failed: {e}")
-                ok = 0
-            if not hc.allreduce(ok, op=MPI.MIN):
-                a2a[algo] = None
-                continue
-            a2a[algo] = round(timed(lambda: dev.alltoall(xa, ya, algo), 5) * 1e3, 4)
-        good = {a: t for a, t in a2a.items() if t}
-        ba = min(good, key=good.get) if good else None
-        sec["alltoall"] = {"bytes_per_rank": an * 4, "algo": ba, "ms": good.get(ba),
-                           "algbw_GBps": round(an * 4 / (good[ba] / 1e3) / 1e9, 2) if ba else None,
-                           "candidates_ms": a2a}
-    del x, y
-    return {"algbw": algbw, "busbw": busbw, "t_step": t_step, "best": best, "results": ms(results),
-            "final_ok": final_ok, "self_test": self_test, "secondary": sec}
+        sync_barrier, _ = _timers(comm)
+
+        def attempt(algo):
+            ya.zero_()
+            sync_barrier()
+            if _injected(algo, "a2a"):
+                return "injected fault (CCMPI_BENCH_FAULT): kernel skipped on rank 0"
+            dev.alltoall(xa, ya, algo)
+            torch.cuda.synchronize()
+            dev.check()
+            return None if torch.equal(ya.view(world, blk), want) else "wrong result"
+
+        res, ba = pick_candidates(["direct", "push", "pairwise"], attempt, _device_agree(comm), dev.reset,
+                                  lambda algo: timed(lambda: dev.alltoall(xa, ya, algo), 5), log=log)
+        ms = res[ba]["ms"] if ba else None
+        sec["alltoall"] = {"bytes_per_rank": an * 4, "algo": ba, "ms": ms,
+                           "algbw_GBps": round(an * 4 / (ms / 1e3) / 1e9, 2) if ms else None,
+                           "candidates_ms": {a: o["ms"] for a, o in res.items()}, "candidates": res}
+        if not ba:
+            sec["alltoall"]["error"] = "no all-to-all algorithm produced a correct result"
+        pw = res.get("pairwise", {})
+        # BASELINE config 3 (pairwise all-to-all, 256 MiB/rank) on its own key
+        sec["alltoall_pairwise"] = {"bytes_per_rank": an * 4, "ms": pw.get("ms"), "error": pw.get("error"),
+                                    "algbw_GBps": round(an * 4 / (pw["ms"] / 1e3) / 1e9, 2) if pw.get("ms") else None,
+                                    "busbw_GBps": _bw(an * 4, pw.get("ms"), world, ar=False)["busbw_GBps"]}
+    return sec
 
 
 def tuning_sweep(comm, args, best_1gib: str, log=lambda *a: None) -> dict:
@@ -545,6 +682,14 @@ def tuning_sweep(comm, args, best_1gib: str, log=lambda *a: None) -> dict:
     log(f"tuning sweep {time.perf_counter() - t0:.1f}s: {table}")
     out = {"key": dev.tune_key, "table": {f"2^{lg}": a for (_, lg), a in sorted(dev.tuned.items())},
            "seconds": round(time.perf_counter() - t0, 1)}
+    # BASELINE config 2's algbw sweep: the same sizes in bf16 (measured only: the table above
+    # stays the fp32 one), every algorithm's time per size in both curves
+    try:
+        dev.tune(max_bytes=args.tune_max_mb << 20, min_bytes=16 << 10, algos=algos, iters=5, dtype=torch.bfloat16,
+                 save=None, apply=False)
+    except Exception as e:  # noqa: BLE001 - the bf16 curve is secondary
+        out["bf16_error"] = f"{type(e).__name__}: {e}"[:300]
+    out["sweep"] = {"float32": dev.sweep_curve("float32"), "bfloat16": dev.sweep_curve("bfloat16")}
     world = comm.Get_size()
     if world >= 4 and world % 2 == 0:
         # the harness's TP pairs (mp-major grid: ranks 2k, 2k + 1, reference func_impl.py:53-62)
@@ -579,18 +724,37 @@ def coll_phase(args) -> dict:
         if rank == 0 and args.verbose:
             print("[bench coll]", *a, file=sys.stderr, flush=True)
 
-    groups = ("ar",) if args.no_secondary else ("ar", "bf16", "a2a")
-    r = run_collectives(comm, args, log, groups)
+    r = run_headline(comm, args, log)
     _fault_injection("coll")
     tuning = {}
     rec = coll_record(args, comm, r, tuning)
     if not args.no_secondary:
+        # the fp32 headline is on disk before any secondary runs: a crash or hang in the
+        # bf16 / all-to-all / tuning work below keeps ``value`` (marked partial)
+        _write_result(args, rank, {**rec, "partial": "written after the fp32 headline, before the secondaries"})
+        _fault_injection("coll_secondary")
+        try:
+            rec["config"].update(run_secondaries(comm, args, r, log))
+        except Exception as e:  # noqa: BLE001 - secondary; the headline stands
+            rec["config"]["secondary_error"] = f"{type(e).__name__}: {e}"[:300]
         _write_result(args, rank, {**rec, "partial": "written before the tuning sweep"})
         _fault_injection("coll_tuning")
         try:
             tuning.update(tuning_sweep(comm, args, r["best"], log))
         except Exception as e:  # noqa: BLE001 - the sweep is secondary; the headline stands
             tuning["error"] = f"{type(e).__name__}: {e}"[:300]
+        sw = tuning.pop("sweep", None)
+        if sw:
+            # BASELINE config 2: algbw / busbw vs size (fp32 and bf16), the 1 GiB headline
+            # and its bf16 counterpart as the last points
+            b16 = rec["config"].get("bf16_1GiB", {})
+            sw["float32"].append({"bytes": args.size_mb << 20, "best": r["best"], "ms": r["results"],
+                                  **_bw(args.size_mb << 20, r["t_step"] * 1e3, world)})
+            if b16.get("ms"):
+                sw["bfloat16"].append({"bytes": args.size_mb << 20, "best": b16["algo"], "ms": b16["candidates_ms"],
+                                       **_bw(args.size_mb << 20, b16["ms"], world)})
+            rec["config"]["sweep"] = sw
+    r.pop("x", None), r.pop("y", None)
     torch.cuda.synchronize()
     return rec
 
@@ -626,11 +790,13 @@ def coll_record(args, comm, r: dict, tuning: dict) -> dict:
             "xgmi_link_frac": (round(r["busbw"] / (min(world - 1, 7) * XGMI_LINK_GBPS), 3)
                                if world > 1 and not dev.shared_device else None),
             "candidates_ms": r["results"],
+            # every candidate's outcome: {"ms", "error"} (error: exception / timeout code with
+            # phase and peer, per failing rank; or why it was skipped)
+            "candidates": r["outcomes"],
             "result_exact": r["final_ok"],
             "self_test": r["self_test"],
             "shared_gpu": dev.shared_device,
             "tuning": tuning,
-            **r["secondary"],
         },
     }
 
@@ -642,7 +808,7 @@ def harness_phase(args) -> dict:
     import torch
 
     from collective_communication_mpi_amd import MPI
-    from collective_communication_mpi_amd.models.harness import bench_forward
+    from collective_communication_mpi_amd.models.harness import bench_forward, fc_o_forms_agree
 
     world, hc = comm.Get_size(), comm.comm
     tp = args.tp or (2 if world >= 2 and world % 2 == 0 else 1)
@@ -664,22 +830,39 @@ def harness_phase(args) -> dict:
     harness["tp_allreduce_bytes"] = (args.batch * 16 * 16 * 4 if mode == "token" else args.batch * 16 * 4) \
         if tp > 1 else 0
     if not args.no_secondary:
-        # the other fc_o forms: pooled row-parallel (B x 16 TP all-reduce), and the token
+        # the other fc_o forms: pooled row-parallel (B x 16 TP all-reduce), the token
         # pipeline in 4 row blocks whose all-reduces run on a side stream under the next
-        # block's attention
+        # block's attention, and the per-token kernel's other TP form (push / plain)
         other = {}
-        variants = [("pooled", "row", 1)] if args.fc_o_mode == "token" else [("token", "token", 1)]
+        variants = [("pooled", "row", 1, "")] if args.fc_o_mode == "token" else [("token", "token", 1, "")]
         if tp > 1:
-            variants.append(("token_chunks4", "token", 4))
-        for name, vmode, chunks in variants:
+            variants.append(("token_chunks4", "token", 4, ""))
+            if mode == "token" and harness.get("fc_o_tp_form") in ("plain", "push"):
+                alt = "push" if harness["fc_o_tp_form"] == "plain" else "plain"
+                variants.append((f"token_{alt}", "token", 1, alt))
+                try:
+                    # both forms sum the same partials in rank order: bitwise equal, or the
+                    # push form's numbers are not trusted (and its variant is not timed)
+                    other["push_equals_plain"] = fc_o_forms_agree(comm, tp, args.batch)
+                except Exception as e:  # noqa: BLE001
+                    other["push_equals_plain"] = {"equal": False, "error": f"{type(e).__name__}: {e}"[:200]}
+        for name, vmode, chunks, form in variants:
+            if form == "push" and not other.get("push_equals_plain", {}).get("equal"):
+                other[f"{name}_error"] = "push form not bitwise equal to plain: not timed"
+                continue
             try:
                 r = bench_forward(comm, tp=tp, batch=args.batch, steps=args.steps, warmup=args.warmup,
-                                  train=False, fc_o_mode=vmode, tp_chunks=chunks)
+                                  train=False, fc_o_mode=vmode, tp_chunks=chunks, tp_fc_o_form=form)
                 other[f"{name}_fwd_ms"] = round(r["fwd_ms"], 4)
                 other[f"{name}_hip_graph"] = r["hip_graph"]
             except Exception as e:  # noqa: BLE001 - a secondary number must not cost the record
                 other[f"{name}_error"] = f"{type(e).__name__}: {e}"[:200]
         harness["fc_o_variants"] = other
+        if harness.get("fc_o_tp_form") == "push" and not other.get("push_equals_plain", {}).get("equal"):
+            # the headline ran the push form but it did not check out: re-measure it plain
+            harness = {**bench_forward(comm, tp=tp, batch=args.batch, steps=args.steps, warmup=args.warmup,
+                                       fc_o_mode=mode, tp_fc_o_form="plain"), "fc_o_variants": other,
+                       "push_rejected": True, "tp_allreduce_bytes": harness["tp_allreduce_bytes"]}
     harness["fwd_ms"] = round(harness["fwd_ms"], 4)
     harness["train_ms"] = round(harness.get("train_ms", float("nan")), 4)
     return harness
@@ -693,12 +876,13 @@ def dp_phase(args) -> dict:
     comm = _setup_phase("30")
     from collective_communication_mpi_amd.parallel.llama_dp import measure_ddp_overlap
 
+    # CTA budgets of the bucket all-reduces: a CU holding one collective CTA cannot start a
+    # ring-GEMM workgroup (512-VGPR waves take whole SIMDs), so large budgets can stall the
+    # backward (32 was best on the 2-rank rehearsal, profiles/r4_dp); with one rank per GPU
+    # 7 links may need more CTAs in flight: 256 / 512 are swept there too
+    budgets = [32, 64, 128] + ([] if comm.dev.shared_device else [256, 512])
     out = measure_ddp_overlap(comm, layers=args.dp_layers, tokens=args.dp_tokens, vocab=bool(args.dp_vocab),
-                              # CTA budgets of the bucket all-reduces: a CU holding one collective CTA
-                              # cannot start a ring-GEMM workgroup (512-VGPR waves take whole SIMDs),
-                              # so 256 (one per CU) would stall the backward; 32 was best on the
-                              # 2-rank rehearsal (profiles/r4_dp)
-                              iters=2, blocks_sweep=[32, 64, 128], verbose=args.verbose)
+                              iters=2, blocks_sweep=budgets, verbose=args.verbose)
     if args.dp_scripted:
         import torch
 
@@ -778,6 +962,82 @@ def rccl_phase(args) -> dict:
     return res
 
 
+def host_phase(args) -> dict:
+    """BASELINE config 1: "myAllreduce 8-proc CPU on a 1k-float32 buffer" -- the reference's
+    own benchmark (mpi-test.py:40-98 myallreduce, :178-239 myalltoall) on the C++ host plane:
+    ``--host-runs`` runs, each bracketed by Barrier + Wtime (the reference's timing), the
+    library collective against the hand-written one on the same input, every run checked
+    with ``np.array_equal`` (MIN is exact in any order).  Also the median of back-to-back
+    calls (no barrier inside), the per-call cost without the barrier's.  CPU only."""
+    import statistics
+
+    import numpy as np
+
+    from collective_communication_mpi_amd import MPI, Communicator
+
+    world = MPI.COMM_WORLD
+    comm = Communicator(world)
+    rank, p = comm.Get_rank(), comm.Get_size()
+    n = args.host_count
+    runs = args.host_runs
+    rng = np.random.default_rng(1234 + rank)
+    out = {"ranks": p, "count": n, "dtype": "float32", "runs": runs, "op": "MIN",
+           "timing": "per run: Barrier, Wtime, call, Barrier, Wtime (reference mpi-test.py:59-72); avg over runs"}
+
+    def bench_pair(name_lib, lib, name_my, my, make):
+        t_lib, t_my, ok = [], [], True
+        for _ in range(runs):
+            src, d_lib, d_my = make()
+            comm.Barrier()
+            t0 = MPI.Wtime()
+            lib(src, d_lib)
+            comm.Barrier()
+            t_lib.append(MPI.Wtime() - t0)
+            comm.Barrier()
+            t0 = MPI.Wtime()
+            my(src, d_my)
+            comm.Barrier()
+            t_my.append(MPI.Wtime() - t0)
+            ok &= bool(np.array_equal(d_lib, d_my))
+        ok = bool(world.allreduce(int(ok), op=MPI.MIN))
+        src, d_lib, d_my = make()
+        b2b = {}
+        for nm, fn, d in ((name_lib, lib, d_lib), (name_my, my, d_my)):
+            reps = []
+            for _ in range(5):
+                comm.Barrier()
+                t0 = time.perf_counter()
+                for _ in range(200):
+                    fn(src, d)
+                reps.append((time.perf_counter() - t0) / 200)
+            b2b[nm] = round(max(world.allgather(statistics.median(reps))) * 1e6, 3)
+        return {f"{name_lib}_avg_us": round(max(world.allgather(statistics.mean(t_lib))) * 1e6, 3),
+                f"{name_my}_avg_us": round(max(world.allgather(statistics.mean(t_my))) * 1e6, 3),
+                "back_to_back_median_us": b2b, "all_runs_equal": ok}
+
+    def make_ar():
+        return (rng.standard_normal(n).astype(np.float32), np.empty(n, np.float32), np.empty(n, np.float32))
+
+    out["allreduce"] = bench_pair("Allreduce", lambda s, d: comm.Allreduce(s, d, op=MPI.MIN),
+                                  "myAllreduce", lambda s, d: comm.myAllreduce(s, d, op=MPI.MIN), make_ar)
+    na = n // p * p
+
+    def make_a2a():
+        return (rng.standard_normal(na).astype(np.float32), np.empty(na, np.float32), np.empty(na, np.float32))
+
+    out["alltoall"] = bench_pair("Alltoall", comm.Alltoall, "myAlltoall", comm.myAlltoall, make_a2a)
+    reps = []
+    s, d, _ = make_a2a()
+    for _ in range(5):
+        comm.Barrier()
+        t0 = time.perf_counter()
+        for _ in range(200):
+            comm.myAlltoall2(s, d)
+        reps.append((time.perf_counter() - t0) / 200)
+    out["alltoall"]["myAlltoall2_back_to_back_median_us"] = round(max(world.allgather(statistics.median(reps))) * 1e6, 3)
+    return out
+
+
 def _write_result(args, rank: int, out: dict) -> None:
     if rank != 0:
         return
@@ -798,7 +1058,8 @@ def main() -> int:
     if not args.phase:
         return supervise(args)  # this process never touches the GPU
     rank = _env_rank()[0]
-    fn = {"coll": coll_phase, "harness": harness_phase, "rccl": rccl_phase, "dp": dp_phase, "mlp": mlp_phase}[args.phase]
+    fn = {"coll": coll_phase, "harness": harness_phase, "rccl": rccl_phase, "dp": dp_phase, "mlp": mlp_phase,
+          "host": host_phase}[args.phase]
     if args.phase == "coll":
         out = fn(args)  # the headline: a failure here fails the phase (rc != 0)
     else:

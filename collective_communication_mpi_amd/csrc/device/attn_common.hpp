@@ -33,6 +33,16 @@ struct AttnArgs {
   const uint16_t* dz;   // bwd: dO rows of sequence b = dz_scale * (dz[b] . W_o), broadcast over the S
   int ld_dz;            //      rows (replaces dout; dz is [B][ld_dz] bf16)
   float dz_scale;
+  // Per-token row-parallel fc_o fused into the MFMA forward (the reference layer's shape,
+  // model/func_impl.py:94-109: every token's partial output, not the pooled one):
+  // z[b*S + i][0..16) = bf16(O[b, i]) . W_o^T (+ bo), the Hl local heads summed in head order,
+  // fp32 rows of ld_zt floats.  zrows == 0: into ztok (local).  zrows > 0 (push): row block j
+  // = rows [j zrows, (j+1) zrows) goes to zpush[j] (rank j's inbox slot for this rank, peer-
+  // mapped), stored write-through; DeviceComm::inbox_to_local then completes the TP sum.
+  float* ztok;
+  int ld_zt;
+  int zrows;
+  float* zpush[16];
 };
 
 // MFMA path (attn_mfma.hip): S <= 16, D in {32, 64, 128}, 16-B aligned rows.

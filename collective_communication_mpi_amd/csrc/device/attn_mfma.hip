@@ -102,6 +102,8 @@ __global__ void __launch_bounds__(256) k_attn16_fwd(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) uint16_t vt[WPB][16 * LD];
   __shared__ __attribute__((aligned(16))) uint16_t ot[WPB][16 * LD];
   __shared__ float zpart[2][WPB][16];  // fused fc_o: per-wave (= per-head) partial logits, double-buffered
+  // per-token fused fc_o: per-wave (= per-head) z tiles [16 tokens][16 classes], double-buffered
+  __shared__ float ztp[2][WPB][16 * 16];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
   const int S = a.S, HD = a.Hl * D, npairs = a.B * a.Hl;
   uint16_t* V = vt[wave];
@@ -123,6 +125,15 @@ __global__ void __launch_bounds__(256) k_attn16_fwd(AttnArgs a) {
         if (4 * g + 2 * q + 1 < a.n_out) hi = w[a.ld_wo];
         wpk[nt][q] = lo | (hi << 16);
       }
+  }
+  // per-token fused fc_o: B operand of z = O . W_o^T -- lane (c, g) holds class c, this
+  // wave's head features 32kk + 8g .. +7 (loaded once; classes >= n_out read as zero)
+  bf16x8 wb[NK];
+  if (a.ztok || a.zrows) {
+    const int hw = wave % a.Hl;
+#pragma unroll
+    for (int kk = 0; kk < NK; ++kk)
+      wb[kk] = ld_row16(a.wo + (size_t)c * a.ld_wo + hw * D + 32 * kk + 8 * g, c < a.n_out);
   }
   const int stride = gridDim.x * WPB;
   int it = 0;
@@ -202,7 +213,49 @@ __global__ void __launch_bounds__(256) k_attn16_fwd(AttnArgs a) {
         }
       }
     }
+    if (a.ztok || a.zrows) {
+      // z[i][cls] over this head's features on the MFMA: A = bf16(O) rows (the values a
+      // separate fc_o GEMM would read) from this wave's LDS tile, B = W_o in registers;
+      // the accumulator holds z[i = 4g + r][cls = c]
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) O[(4 * g + r) * LD + 16 * nt + c] = (uint16_t)f32_to_bf16_bits(o[nt][r]);
+      __builtin_amdgcn_wave_barrier();
+      f4 zt = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < NK; ++kk) zt = mma32(*reinterpret_cast<const bf16x8*>(O + c * LD + 32 * kk + 8 * g), wb[kk], zt);
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int r = 0; r < 4; ++r) ztp[it][wave][(4 * g + r) * 16 + c] = zt[r];
+    }
     if (a.o) store_tile<D, LD>(O, o, 1.f, a.o + (size_t)b * S * a.ld_o + h * D, a.ld_o, S, lane);
+   }
+   if (a.ztok || a.zrows) {
+    // the Hl heads of each sequence of this iteration (consecutive waves, Hl | WPB), summed in
+    // head order, + the bias; thread t = (token t >> 4, class t & 15): a 64-B row per 16 lanes
+    __syncthreads();  // (the next iteration writes the other buffer)
+    const int t = threadIdx.x, i = t >> 4, cls = t & 15;
+    for (int w = 0; w < WPB; w += a.Hl) {
+      const int prw = base + w;
+      if (prw >= npairs) break;
+      const int b = prw / a.Hl;
+      if (i < S) {
+        float acc = 0.f;
+        for (int k = 0; k < a.Hl; ++k) acc += ztp[it][w + k][i * 16 + cls];
+        if (a.bo && cls < a.n_out) acc += a.bo[cls];
+        const size_t row = (size_t)b * S + i;
+        if (a.zrows) {
+          // zrows % S == 0: the whole sequence lies in one block, j is workgroup-uniform
+          const int j = (int)((size_t)b * S / a.zrows);
+          float* dst = a.zpush[j] + (row - (size_t)j * a.zrows) * a.ld_zt + cls;
+          __hip_atomic_store(reinterpret_cast<uint32_t*>(dst), __float_as_uint(acc), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_SYSTEM);  // write-through store into the peer's inbox
+        } else {
+          a.ztok[row * a.ld_zt + cls] = acc;
+        }
+      }
+    }
    }
    if (a.zp) {  // sum the Hl heads of each sequence in rank order (deterministic) and add the bias
     __syncthreads();  // (the next iteration writes the other buffer: one barrier per iteration)
@@ -215,6 +268,7 @@ __global__ void __launch_bounds__(256) k_attn16_fwd(AttnArgs a) {
     }
    }
   }
+  if (a.zrows) release_sys();  // pushed rows performed system-wide before the workgroup retires
 }
 
 template <int D>

@@ -241,12 +241,33 @@ static void check_fused_fc(const AttnArgs& a, bool bwd) {
 
 void attn_fwd(uint64_t qkv, uint64_t o, uint64_t lse, int B, int S, int Hl, int D, int ld_qkv, int ld_o, float scale,
               uint64_t pool, int ld_pool, uint64_t stream, uint64_t wo, int ld_wo, int n_out, uint64_t zp, int ld_zp,
-              uint64_t bo) {
+              uint64_t bo, uint64_t ztok, int ld_zt, int zrows, const std::vector<uint64_t>& zpush) {
   check_dims(S, D, false);
   AttnArgs a{(const uint16_t*)qkv, (uint16_t*)o, (float*)lse, nullptr, nullptr, nullptr, B, S, Hl, D, ld_qkv, ld_o, scale,
              (uint16_t*)pool, ld_pool, 0, 0, (const uint16_t*)wo, ld_wo, n_out, (float*)zp, ld_zp, (const float*)bo,
              nullptr, 0, 1.0f};
   if (zp) check_fused_fc(a, false);
+  if (ztok || zrows) {
+    // per-token fused fc_o (local z, or pushed row blocks): the MFMA kernel's workgroup layout
+    if (zp || !attn::mfma_supported(a, false) || n_out < 1 || n_out > 16 || 4 % Hl || !wo || ld_wo % 8 ||
+        (wo % 16) || ld_zt < 16)
+      throw std::invalid_argument("attention: per-token fused fc_o needs S <= 16, D in {32, 64, 128}, Hl | 4, "
+                                  "n_out <= 16, 16-B aligned W_o rows, z rows of >= 16 floats");
+    if (zrows) {
+      const int64_t M = (int64_t)B * S;
+      const int64_t blocks = M / zrows;
+      if (zrows % S || M % zrows || blocks < 1 || blocks > 16 || (int64_t)zpush.size() != blocks)
+        throw std::invalid_argument("attention: push fc_o needs whole sequences per block (zrows % S == 0), "
+                                    "B*S = blocks x zrows and one target per block (<= 16)");
+      for (int64_t j = 0; j < blocks; ++j) {
+        if (!zpush[j] || zpush[j] % 16) throw std::invalid_argument("attention: push fc_o targets must be 16-B aligned");
+        a.zpush[j] = reinterpret_cast<float*>(zpush[j]);
+      }
+    }
+    a.ztok = reinterpret_cast<float*>(ztok);
+    a.ld_zt = ld_zt;
+    a.zrows = zrows;
+  }
   if (attn::mfma_supported(a, false)) {
     attn::launch_fwd_mfma(a, (hipStream_t)stream);
     CCMPI_HIP_CHECK(hipGetLastError());
@@ -497,7 +518,8 @@ void register_attn_ops(pybind11::module_& m) {
   m.def("attn_small_fwd", &attn_fwd, py::arg("qkv"), py::arg("o"), py::arg("lse"), py::arg("B"), py::arg("S"),
         py::arg("Hl"), py::arg("D"), py::arg("ld_qkv"), py::arg("ld_o"), py::arg("scale"), py::arg("pool"),
         py::arg("ld_pool"), py::arg("stream"), py::arg("wo") = 0, py::arg("ld_wo") = 0, py::arg("n_out") = 0,
-        py::arg("zp") = 0, py::arg("ld_zp") = 0, py::arg("bo") = 0, py::call_guard<py::gil_scoped_release>());
+        py::arg("zp") = 0, py::arg("ld_zp") = 0, py::arg("bo") = 0, py::arg("ztok") = 0, py::arg("ld_zt") = 16,
+        py::arg("zrows") = 0, py::arg("zpush") = std::vector<uint64_t>{}, py::call_guard<py::gil_scoped_release>());
   m.def("attn_small_bwd", &attn_bwd, py::arg("qkv"), py::arg("o"), py::arg("lse"), py::arg("dout"), py::arg("dqkv"),
         py::arg("dbias"), py::arg("B"), py::arg("S"), py::arg("Hl"), py::arg("D"), py::arg("ld_qkv"), py::arg("ld_o"),
         py::arg("scale"), py::arg("dout_bstride"), py::arg("dout_rstride"), py::arg("stream"), py::arg("dz") = 0,

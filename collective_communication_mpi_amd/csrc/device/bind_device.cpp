@@ -193,6 +193,8 @@ PYBIND11_MODULE(_device, m) {
       .def("code_of", [](DeviceComm& d, uint64_t ptr, uint64_t n) { return d.code_of_public(ptr, n); })
       .def("gemm_rowpar", &DeviceComm::gemm_rowpar, py::call_guard<py::gil_scoped_release>())
       .def("gemm_push_rowpar", &DeviceComm::gemm_push_rowpar, py::call_guard<py::gil_scoped_release>())
+      .def("push_targets", &DeviceComm::push_targets)
+      .def("inbox_to_local", &DeviceComm::inbox_to_local, py::call_guard<py::gil_scoped_release>())
       .def("ll_connect", [](DeviceComm& d, const std::vector<std::string>& hs) { d.ll_connect(hs); })
       .def_property_readonly("ll_max_bytes", &DeviceComm::ll_max_bytes)
       .def_property_readonly("inbox_bytes", &DeviceComm::inbox_bytes)

@@ -1026,33 +1026,58 @@ void DeviceComm::gemm_push_rowpar(uint64_t A, uint64_t B, uint64_t out, uint64_t
   if (M <= 0 || N <= 0) return;
   if (size_ < 2 || size_ > kMaxRanks) throw std::invalid_argument("ccmpi: push row-parallel GEMM needs 2..16 ranks");
   const int rows = M / size_;
-  const uint64_t nbytes = (uint64_t)M * N * 2, shard = nbytes / size_;
+  const uint64_t nbytes = (uint64_t)M * N * 2;
   if (rows * size_ != M || rows % 256 || N % 8 || (out % 16) || (inbox % 16) || nbytes >= 0x7ffffff0ull)
     throw std::invalid_argument("ccmpi: push row-parallel GEMM needs M % (256 p) == 0, N % 8 == 0, 16-B aligned buffers");
   gemm::GemmArgs g{reinterpret_cast<const uint16_t*>(A), reinterpret_cast<const uint16_t*>(B), nullptr, nullptr, M, N, K,
                    lda, ldb, N, alpha, 0, 0, 0, 1, 1};
   if (!gemm::gemm_ring_ok(g, 0, 0)) throw std::invalid_argument("ccmpi: push row-parallel GEMM: K % 64 == 0, 16-B rows");
   CCMPI_HIP_CHECK(hipSetDevice(device_));
+  const std::vector<uint64_t> tgt = push_targets(inbox, nbytes);
+  uint16_t* push[kMaxRanks] = {};
+  for (int j = 0; j < size_; ++j) push[j] = reinterpret_cast<uint16_t*>(tgt[j]);
+  g.C = push[rank_];
+  hipStream_t st = S(stream);
+  gemm::launch_gemm_ring(g, 0, 0, st, nullptr, 0, push, rows);
+  CCMPI_HIP_CHECK(hipGetLastError());
+  inbox_to_local(inbox, out, nbytes, DT_BF16, stream, max_blocks);
+}
+
+std::vector<uint64_t> DeviceComm::push_targets(uint64_t inbox, uint64_t nbytes) {
+  if (size_ < 2 || nbytes % (16ull * size_) || inbox % 16)
+    throw std::invalid_argument("ccmpi: push inbox needs >= 2 ranks, nbytes % (16 p) == 0, a 16-B aligned block");
   uint64_t ic = 0;
   {
     DynScope dyn_scope(this, true);
     ic = code_of_(inbox, nbytes);
   }
-  if (!ic) throw std::invalid_argument("ccmpi: push row-parallel GEMM: the inbox must be a symmetric heap block");
+  if (!ic) throw std::invalid_argument("ccmpi: push inbox must be a symmetric heap block");
   // block j of this rank's partial -> rank j's inbox, slot [rank_] (peer-mapped address)
   const int s = (int)(ic >> 56) - 1;
-  const uint64_t off = ic & ((1ull << 56) - 1);
-  uint16_t* push[kMaxRanks] = {};
+  const uint64_t off = ic & ((1ull << 56) - 1), shard = nbytes / size_;
+  std::vector<uint64_t> out(size_);
   for (int j = 0; j < size_; ++j) {
     char* base = host_pt_.seg[j][s];
-    if (!base) throw std::runtime_error("ccmpi: push row-parallel GEMM: peer segment not mapped");
-    push[j] = reinterpret_cast<uint16_t*>(base + off + (uint64_t)rank_ * shard);
+    if (!base) throw std::runtime_error("ccmpi: push inbox: peer segment not mapped");
+    out[j] = reinterpret_cast<uint64_t>(base + off + (uint64_t)rank_ * shard);
   }
-  g.C = push[rank_];
-  hipStream_t st = S(stream);
-  gemm::launch_gemm_ring(g, 0, 0, st, nullptr, 0, push, rows);
-  CCMPI_HIP_CHECK(hipGetLastError());
-  launch_inbox_to_local(args_(ic, 0, reinterpret_cast<char*>(out), nbytes, 0), size_, DT_BF16, grid_(shard, max_blocks), st);
+  return out;
+}
+
+void DeviceComm::inbox_to_local(uint64_t inbox, uint64_t out, uint64_t nbytes, int dtype, uint64_t stream,
+                                int max_blocks) {
+  if (size_ < 2 || nbytes % (16ull * size_) || inbox % 16 || out % 16 || nbytes >= 0x7ffffff0ull)
+    throw std::invalid_argument("ccmpi: inbox_to_local needs >= 2 ranks, nbytes % (16 p) == 0, 16-B aligned buffers");
+  if (dtype != DT_BF16 && dtype != DT_F32) throw std::invalid_argument("ccmpi: inbox_to_local sums bf16 / fp32");
+  CCMPI_HIP_CHECK(hipSetDevice(device_));
+  uint64_t ic = 0;
+  {
+    DynScope dyn_scope(this, true);
+    ic = code_of_(inbox, nbytes);
+  }
+  if (!ic) throw std::invalid_argument("ccmpi: inbox_to_local: the inbox must be a symmetric heap block");
+  launch_inbox_to_local(args_(ic, 0, reinterpret_cast<char*>(out), nbytes, 0), size_, dtype,
+                        grid_(nbytes / size_, max_blocks), S(stream));
 }
 
 uint32_t DeviceComm::error_code() {

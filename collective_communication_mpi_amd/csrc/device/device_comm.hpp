@@ -141,6 +141,14 @@ class DeviceComm {
   // `out` (any local 16-B aligned tensor).  M % (256 p) == 0, K % 64 == 0, N % 8 == 0.
   void gemm_push_rowpar(uint64_t A, uint64_t B, uint64_t out, uint64_t inbox, int M, int N, int K, int lda, int ldb,
                         float alpha, uint64_t stream, int max_blocks);
+  // The two halves of any push row-parallel producer (a GEMM epilogue, the harness's
+  // attention + per-token fc_o kernel): push_targets() = where THIS rank's partial of row
+  // block j goes -- rank j's slot [rank] of `inbox` (peer-mapped addresses, p of them; `inbox`
+  // a symmetric heap block of nbytes on every rank, nbytes % (16 p) == 0); inbox_to_local()
+  // = the collective that follows the producer on the same stream: every rank reduces its
+  // p slots in rank order and pulls every reduced block into `out` (a local tensor).
+  std::vector<uint64_t> push_targets(uint64_t inbox, uint64_t nbytes);
+  void inbox_to_local(uint64_t inbox, uint64_t out, uint64_t nbytes, int dtype, uint64_t stream, int max_blocks);
   uint64_t code_of_public(uint64_t ptr, uint64_t nbytes) const { return code_of_(ptr, nbytes); }
   bool fused_ready() const { return fused_tab_dev_ != nullptr && fused_inbox_bytes_ > 0; }
 

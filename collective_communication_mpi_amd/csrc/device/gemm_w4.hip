@@ -982,6 +982,12 @@ __global__ void __launch_bounds__(WNT, 1) k_gemm_w4r(W4Args wa) {
         crow -= blk * wa.push_rows;
       }
       uint16_t* cptr = cbase + (size_t)crow * ldc + ccol;
+      // push mode: the rows go to a peer's inbox over xGMI -- stored write-through (sc0 sc1,
+      // kStorePolicy) like every collective store, through a descriptor on the wave-uniform
+      // row base, so they leave this XCD's L2 as they are produced and the inbox-to-local
+      // collective that follows never depends on an L2 write-back
+      const bool pushed = EPI == 1 && wa.push_rows;
+      const Rsrc prs = make_rsrc(uniform_ptr(reinterpret_cast<char*>(cbase + (size_t)crow * ldc)), 0x7ffffff0u);
       const int rows_left = g.M - bm - wr * 128;
       const bool col_ok = ccol < g.N;
 #pragma unroll
@@ -1003,7 +1009,11 @@ __global__ void __launch_bounds__(WNT, 1) k_gemm_w4r(W4Args wa) {
           const int rl = it * 4 + grp;
           const u32x4 w = *reinterpret_cast<const u32x4*>(slab + rl * 256 + ((lr ^ (rl & 15)) << 4));
           if (col_ok && h * 32 + rl < rows_left) {
-            *reinterpret_cast<u32x4*>(cptr + (size_t)(h * 32 + rl) * ldc) = w;
+            if (pushed)
+              __builtin_amdgcn_raw_buffer_store_b128(w, prs.r, (uint32_t)(((h * 32 + rl) * ldc + ccol) * 2), 0,
+                                                     kStorePolicy);
+            else
+              *reinterpret_cast<u32x4*>(cptr + (size_t)(h * 32 + rl) * ldc) = w;
             if constexpr (EPI == 2) {
               float gl[4];
 #pragma unroll

@@ -178,6 +178,43 @@ def save_tuning(path: str, key: str, table: Dict[Tuple[int, int], str]) -> None:
     os.replace(tmp, path)
 
 
+def row_mode_key(tune_key: str) -> str:
+    """Tuning-file key of the TP row-parallel output modes measured for one group identity."""
+    return f"rowmode:{tune_key}"
+
+
+def load_row_modes(path: str, tune_key: str) -> Dict[Tuple[int, int], str]:
+    """{(M, N): row-parallel mode} measured for groups of ``tune_key`` (``save_row_modes``)."""
+    import json
+
+    try:
+        with open(path) as f:
+            tables = json.load(f)
+    except (OSError, ValueError):
+        return {}
+    out = {}
+    for k, mode in tables.get(row_mode_key(tune_key), {}).items():
+        m, n = (int(v) for v in k.split(","))
+        out[(m, n)] = str(mode)
+    return out
+
+
+def save_row_modes(path: str, tune_key: str, table: Dict[Tuple[int, int], str]) -> None:
+    """Merge the row-mode table into the tuning file (same file as ``save_tuning``)."""
+    import json
+
+    try:
+        with open(path) as f:
+            tables = json.load(f)
+    except (OSError, ValueError):
+        tables = {}
+    tables[row_mode_key(tune_key)] = {f"{m},{n}": mode for (m, n), mode in sorted(table.items())}
+    tmp = f"{path}.tmp{os.getpid()}"
+    with open(tmp, "w") as f:
+        json.dump(tables, f, indent=1, sort_keys=True)
+    os.replace(tmp, path)
+
+
 class _CountingComm:
     """Proxy of the host communicator that counts the host calls the device plane makes
     (``calls``): a steady-state device collective should make none (tests)."""
@@ -310,8 +347,12 @@ class DeviceGroup:
         # persisted tune() results (CCMPI_TUNE_FILE), keyed by group size, GPU sharing and model
         self.tune_key = tuning_key(self.size, self.ranks_per_device, props.name)
         self.tune_file = os.environ.get("CCMPI_TUNE_FILE")
+        # TP row-parallel output mode per (M, N), measured by the bench's mlp phase
+        # (tensor_parallel._row_mode reads it for mode "auto")
+        self.row_modes: Dict[Tuple[int, int], str] = {}
         if self.tune_file:
             self.tuned.update(load_tuning(self.tune_file, self.tune_key))
+            self.row_modes.update(load_row_modes(self.tune_file, self.tune_key))
         # on-demand registration of ordinary CUDA tensors (collectives >= reg_min bytes)
         self.reg_min = _env_int("CCMPI_REGISTER_MIN_BYTES", 1 << 20)  # 0 = off
         self.reg_slots = max(1, _env_int("CCMPI_REGISTER_SLOTS", 32))
@@ -451,10 +492,34 @@ class DeviceGroup:
             t = self._persist[k] = self.empty(shape, dtype)
         return t
 
+    def scratch_view(self, key, shape, dtype=None):
+        """Grow-only persistent symmetric scratch under ``(key, dtype)``: one heap block per
+        key, reallocated (collectively, to the new size) only when a call needs more than it
+        holds; every smaller request is a view of it.  Variable token counts (eval, packing,
+        a last partial batch) then reuse one block instead of leaking one per shape, and the
+        steady state makes no host call.  Every rank must ask for the same keys and sizes in
+        the same order (the TP layers do: same shapes on every rank of the group)."""
+        torch = self.torch
+        dtype = dtype or torch.float32
+        shape = (shape,) if isinstance(shape, int) else tuple(int(s) for s in shape)
+        n = 1
+        for d in shape:
+            n *= d
+        k = ("grow", key, dtype)
+        t = self._persist.get(k)
+        if t is None or t.numel() < n:
+            if t is not None:
+                # the old block returns to the heap: no queued kernel of this rank may still use it
+                torch.cuda.synchronize(self.device)
+                del self._persist[k]
+                t = None
+            t = self._persist[k] = self.empty(max(n, 1), dtype)
+        return t[:n].view(shape)
+
     def release_persistent(self, key=None) -> None:
         """Drop cached persistent buffers (all, or those of ``key``); their blocks return
         to the heap when no other reference remains."""
-        for k in [k for k in self._persist if key is None or k[0] == key]:
+        for k in [k for k in self._persist if key is None or k[0] == key or (k[0] == "grow" and k[1] == key)]:
             del self._persist[k]
 
     def zeros(self, shape, dtype=None):
@@ -555,7 +620,7 @@ class DeviceGroup:
         if w.shape[1] != K or x.stride(1) != 1 or w.stride(1) != 1 or tuple(out.shape) != (M, N) \
                 or not out.is_contiguous() or out.dtype != torch.bfloat16:
             raise ValueError("gemm_push_allreduce: shape mismatch, non K-contiguous operand or bad output")
-        inbox = self.persistent("gemm_push_inbox", (M * N,), torch.bfloat16)
+        inbox = self.scratch_view("gemm_push_inbox", (M * N,), torch.bfloat16)
         self.dc.gemm_push_rowpar(x.data_ptr(), w.data_ptr(), out.data_ptr(), inbox.data_ptr(), M, N, K, x.stride(0),
                                  w.stride(0), float(alpha), self._stream(), self._budget(max_blocks))
         return out
@@ -1078,19 +1143,24 @@ class DeviceGroup:
 
     # ------------------------------------------------------------------- tuning
     def tune(self, max_bytes: int = 256 << 20, min_bytes: int = 4 << 10, algos: Sequence[str] = (),
-             iters: int = 5, dtype=None, save: Optional[str] = None) -> Dict[Tuple[int, int], str]:
+             iters: int = 5, dtype=None, save: Optional[str] = None, apply: bool = True) -> Dict[Tuple[int, int], str]:
         """Collective: time every all-reduce algorithm at powers of 4 between
         ``min_bytes`` and ``max_bytes`` (after an exactness check) and make
         ``algo="auto"`` use the fastest per size class.  Algorithms that fail or
         time out on any rank are discarded everywhere.  The table is written by
         rank 0 to ``save`` (default ``CCMPI_TUNE_FILE``), from which later
-        groups of the same size / sharing / GPU model load it at start-up."""
+        groups of the same size / sharing / GPU model load it at start-up.
+        Every measured time is kept in ``tune_times[(dtype name, bytes)][algo]``
+        (seconds per call, None = failed): the algbw-vs-size curve.  ``apply=False``
+        only measures (e.g. a bf16 curve beside the fp32 table)."""
         import time
 
         torch = self.torch
         dtype = dtype or torch.float32
         if not algos:
             algos = ["ll", "oneshot", "twoshot", "fanout"] + ([] if self.shared_device else ["rccl"])
+        times = self.__dict__.setdefault("tune_times", {})
+        dname = str(dtype).replace("torch.", "")
         es = torch.empty((), dtype=dtype).element_size()
         x = self.empty(max_bytes // es, dtype)
         y = self.empty(max_bytes // es, dtype)
@@ -1100,6 +1170,7 @@ class DeviceGroup:
         while b <= max_bytes:
             n = b // es
             best, best_t = None, None
+            row = times.setdefault((dname, b), {})
             for algo in algos:
                 if algo == "oneshot" and b > (16 << 20):
                     continue
@@ -1114,6 +1185,7 @@ class DeviceGroup:
                 except Exception:  # noqa: BLE001 - disqualify the algorithm
                     ok = 0
                 if not self.host.allreduce(ok, op=_host_min()):
+                    row[algo] = None
                     self.reset()  # a timed-out kernel leaves the per-CTA epochs inconsistent
                     continue
                 torch.cuda.synchronize(self.device)
@@ -1122,18 +1194,36 @@ class DeviceGroup:
                 for _ in range(iters):
                     self.allreduce(x[:n], y[:n], "SUM", algo, symmetric=True)
                 torch.cuda.synchronize(self.device)
-                t = self.host.allreduce(time.perf_counter() - t0, op=_host_max())
+                t = self.host.allreduce(time.perf_counter() - t0, op=_host_max()) / iters
+                row[algo] = t
                 if best_t is None or t < best_t:
                     best, best_t = algo, t
-            if best is not None:
+            if best is not None and apply:
                 self.tuned[(self.size, max(0, b.bit_length() - 1))] = best
                 self.tuned[(self.size, max(0, b.bit_length() - 1) + 1)] = best
             b *= 4
         path = save or self.tune_file
-        if path and self.rank == 0:
+        if path and self.rank == 0 and apply:
             save_tuning(path, self.tune_key, self.tuned)
         self.host.Barrier()
         return dict(self.tuned)
+
+    def sweep_curve(self, dtype_name: str = "float32") -> List[dict]:
+        """The algbw/busbw-vs-size curve of the ``tune`` runs of one dtype: per size, every
+        algorithm's time, the fastest, and its algorithm / bus bandwidth (NCCL-tests
+        conventions: busbw = algbw x 2(p-1)/p)."""
+        out = []
+        f = 2 * (self.size - 1) / self.size if self.size > 1 else 0.0
+        for (dn, b), row in sorted(getattr(self, "tune_times", {}).items(), key=lambda kv: kv[0][1]):
+            if dn != dtype_name:
+                continue
+            good = {a: t for a, t in row.items() if t}
+            best = min(good, key=good.get) if good else None
+            alg = b / good[best] / 1e9 if best else None
+            out.append({"bytes": b, "best": best, "ms": {a: (round(t * 1e3, 4) if t else None) for a, t in row.items()},
+                        "algbw_GBps": round(alg, 2) if alg else None,
+                        "busbw_GBps": round(alg * f, 2) if alg else None})
+        return out
 
     # ------------------------------------------------------------- async issue
     def start(self, op: str, *args, stream=None, **kw) -> "Work":

@@ -140,10 +140,11 @@ def bench_forward(comm, tp: int = 2, batch: int = 2048, steps: int = 20, warmup:
     hc.Barrier()
     fwd_s = hc.allreduce(time.perf_counter() - t0, op=MPI.MAX) / steps
     say(f"timed forward {fwd_s * 1e3:.3f} ms")
+    form = getattr(layer, "_zt_form", None)  # the fused per-token fc_o's TP form, if it ran
     if not train:
         return {"tp": cfg.tp, "dp": cfg.dp, "fwd_ms": fwd_s * 1e3, "hip_graph": used_graph, "fc_o_mode": cfg.fc_o_mode,
                 "tp_chunks": cfg.tp_chunks, "tokens_per_step": cfg.batch * cfg.dp * cfg.seq,
-                **({"graph_skipped": hazard} if hazard else {})}
+                **({"fc_o_tp_form": form} if form else {}), **({"graph_skipped": hazard} if hazard else {})}
     # training step (eager)
     for _ in range(2):
         train_step(layer, cfg, xb, yb)
@@ -159,8 +160,31 @@ def bench_forward(comm, tp: int = 2, batch: int = 2048, steps: int = 20, warmup:
     loss_v = hc.allreduce(float(loss.item()), op=MPI.SUM) / cfg.tp  # sum over DP of per-replica shares
     return {"tp": cfg.tp, "dp": cfg.dp, "fwd_ms": fwd_s * 1e3, "train_ms": train_s * 1e3,
             "global_batch": cfg.batch * cfg.dp, "seq_len": cfg.seq, "tokens_per_step": cfg.batch * cfg.dp * cfg.seq,
-            "hip_graph": used_graph, "fc_o_mode": cfg.fc_o_mode,
+            "hip_graph": used_graph, "fc_o_mode": cfg.fc_o_mode, **({"fc_o_tp_form": form} if form else {}),
             "fwd_saves_activations": False, "loss": round(loss_v, 5)}
+
+
+def fc_o_forms_agree(comm, tp: int, batch: int) -> dict:
+    """Collective: one forward of the per-token fc_o in both TP forms ("plain": kernel +
+    all-reduce of z; "push": kernel pushes row blocks into the owners' inboxes + inbox-to-
+    local) on the same input; the all-reduced z and the logits must be bitwise equal on every
+    rank.  Returns {"equal": bool, "max_abs_diff": float}."""
+    from .. import mpi as MPI
+
+    hc = _hc(comm)
+    cfg, layer, x_all, y_all = build(comm, tp, batch, fc_o_mode="token", tp_fc_o_form="plain")
+    xb, _ = local_batch(cfg, x_all, y_all, 0, comm.Get_rank(), layer.device)
+    out = {}
+    for form in ("plain", "push"):
+        layer.cfg.tp_fc_o_form = form
+        logits = layer.forward_images(xb, cfg.batch, save=False)
+        torch.cuda.synchronize()
+        out[form] = (layer._zt.clone(), logits.clone(), layer._zt_form)
+    zp, lp, fp = out["plain"]
+    zq, lq, fq = out["push"]
+    eq = int(fp == "plain" and fq == "push" and torch.equal(zp, zq) and torch.equal(lp, lq))
+    diff = float((zp - zq).abs().max().item())
+    return {"equal": bool(hc.allreduce(eq, op=MPI.MIN)), "max_abs_diff": hc.allreduce(diff, op=MPI.MAX)}
 
 
 def smoke_step(comm) -> None:

@@ -106,6 +106,18 @@ class LayerConfig:
     # forward: qkv = Xp . (W_qkv W_emb)^T + b -- h is never formed (needs the re-associated
     # backward, which does not read h); False: h = Xp . W_emb^T, then qkv = h . W_qkv^T + b
     fold_emb: bool = True
+    # fc_o_mode="token" with tp_chunks = 1: the per-token fc_o runs inside the attention kernel
+    # (csrc/device/attn_mfma.hip: z = O . W_o^T on the MFMA, heads summed in the workgroup; no
+    # attention output tensor, no fc_o GEMM), and its TP sum takes one of two forms:
+    # * "plain": the kernel writes this rank's partial z, then one TP all-reduce of z;
+    # * "push":  the kernel stores row block j of its partial straight into TP rank j's inbox
+    #   slot (posted writes over xGMI while the other sequences still compute), then the
+    #   inbox-to-local two-shot (DeviceComm::inbox_to_local) -- the all-reduce's reduce-scatter
+    #   traffic is overlapped with the attention.  Bitwise equal to "plain" (both sum the
+    #   ranks' partials in rank order, in fp32).
+    # * "auto" (default; CCMPI_TP_FC_O_FORM overrides): "push" when every TP rank owns its
+    #   GPU, "plain" when the ranks share one (the pushes then only compete for the same HBM).
+    tp_fc_o_form: str = ""
     @property
     def seq(self) -> int:
         return (self.img // self.patch) ** 2
@@ -314,11 +326,14 @@ class MnistTPLayer:
         naive = cfg.fc_o_mode == "naive" and cfg.tp > 1
         token = cfg.fc_o_mode == "token"
         tok_fused = token and self._fused_fc_o_bwd()
-        pool = None if (naive or (token and not tok_fused)) else self._buf("pool", (B, self.hd), torch.bfloat16)
-        # the per-token attention output is only consumed by the naive fc_o; the pooled
-        # path (and the MFMA backward, which never reads O) skip materializing it
+        # the per-token attention output is only consumed by the naive fc_o and the unfused /
+        # pipelined token fc_o; the pooled path, the fused token kernel (and the MFMA backward,
+        # which never reads O) skip materializing it
         mfma_attn = S <= 16 and cfg.head_dim in (32, 64, 128)
-        att = self._buf("att", (M, self.hd), torch.bfloat16) if (naive or token or not mfma_attn) else None
+        tok_kernel_pre = token and tok_fused and mfma_attn and self._token_chunks(B) == 1
+        pool = None if (naive or (token and not tok_fused)) else self._buf("pool", (B, self.hd), torch.bfloat16)
+        att = self._buf("att", (M, self.hd), torch.bfloat16) if (naive or (token and not tok_kernel_pre)
+                                                                   or not mfma_attn) else None
         fc_fused = self._fused_fc_o()
         zp = None
         fc = {}
@@ -331,7 +346,11 @@ class MnistTPLayer:
                       bo=self.flat.param("o_b").data_ptr() if self.tp_idx == 0 else 0)
         # token fc_o with TP: attention runs per row block inside the TP pipeline below
         pipelined = token and self._token_chunks(B) > 1
-        if not pipelined:
+        tok_kernel = token and tok_fused and mfma_attn and not pipelined
+        if tok_kernel:
+            att = None  # the attention kernel forms z itself; O is never stored
+            self._token_fc_o_kernel(qkv, lse, pool, B, st)
+        elif not pipelined:
             D.attn_small_fwd(qkv.data_ptr(), 0 if att is None else att.data_ptr(), lse.data_ptr(), B, S,
                              self.hl, cfg.head_dim, qkv.stride(0), self.hd if att is None else att.stride(0),
                              1.0 / math.sqrt(cfg.head_dim),
@@ -340,7 +359,7 @@ class MnistTPLayer:
             z = self._forward_naive_fc_o(att, B)
             logits = z.view(B, S, cfg.out_pad)[:, :, : cfg.n_classes].mean(dim=1)
         elif token:
-            z = self._forward_token_fc_o(att, B, qkv=qkv, lse=lse, pool=pool)
+            z = self._zt if tok_kernel else self._forward_token_fc_o(att, B, qkv=qkv, lse=lse, pool=pool)
             if tok_fused:
                 # logits = mean over the S tokens of the all-reduced z (o_b is in z, TP rank 0),
                 # kept in zp for the fused loss head
@@ -430,6 +449,50 @@ class MnistTPLayer:
         self._saved = (xp, h, qkv, None, lse, B, pool) if save else None
         self._hx = hx[:, : d + cfg.kp] if hx is not None else None
         return zp[:, : cfg.n_classes]
+
+    def tp_fc_o_form(self, B: int) -> str:
+        """"plain" or "push": how the fused per-token fc_o's TP sum runs (``cfg.tp_fc_o_form``)."""
+        if self.tp_dev is None:
+            return "local"
+        form = self.cfg.tp_fc_o_form or os.environ.get("CCMPI_TP_FC_O_FORM", "auto")
+        if form == "auto":
+            form = "plain" if self.tp_dev.shared_device else "push"
+        if form == "push" and B % self.cfg.tp:
+            form = "plain"  # push needs whole sequences per TP rank's row block
+        return form
+
+    def _token_fc_o_kernel(self, qkv, lse, pool, B: int, st: int) -> None:
+        """Attention + per-token row-parallel fc_o in ONE kernel (``k_attn16_fwd``), then the
+        TP sum of z (B*S x 16 fp32, o_b added by TP rank 0): an all-reduce ("plain"), or the
+        kernel pushes every row block into its owner's inbox and the inbox-to-local two-shot
+        completes it ("push", reference model/func_impl.py:94-109's output path, with the
+        communication under the attention).  Leaves the summed z in ``self._zt``."""
+        cfg = self.cfg
+        S = cfg.seq
+        M = B * S
+        D = _native.device()
+        z = self._buf("ztok", (M, cfg.out_pad), torch.float32, self.tp_dev)
+        wo = self.flat.param16("o_w")
+        kw = dict(wo=wo.data_ptr(), ld_wo=wo.stride(0), n_out=cfg.out_pad, ld_zt=cfg.out_pad,
+                  bo=self.flat.param("o_b").data_ptr() if self.tp_idx == 0 else 0)
+        args = (qkv.data_ptr(), 0, lse.data_ptr(), B, S, self.hl, cfg.head_dim, qkv.stride(0), self.hd,
+                1.0 / math.sqrt(cfg.head_dim), pool.data_ptr(), pool.stride(0))  # pool: dW_o in backward
+        form = self.tp_fc_o_form(B)
+        if form == "push":
+            inbox = self._buf("ztok_inbox", (M, cfg.out_pad), torch.float32, self.tp_dev)
+            key = ("ztok_targets", inbox.data_ptr(), M)
+            if key not in self._bufs:  # peer-mapped slot addresses: resolved once, no host call after
+                self._bufs[key] = self.tp_dev.dc.push_targets(inbox.data_ptr(), inbox.numel() * 4)
+            s = self.tp_dev._stream()
+            D.attn_small_fwd(*args, s, zrows=M // cfg.tp, zpush=self._bufs[key], **kw)
+            self.tp_dev.dc.inbox_to_local(inbox.data_ptr(), z.data_ptr(), inbox.numel() * 4, 10, s,
+                                          self.tp_dev._budget(None))
+        else:
+            D.attn_small_fwd(*args, st, ztok=z.data_ptr(), **kw)
+            if self.tp_dev is not None:
+                self.tp_dev.allreduce(z, z, "SUM", symmetric=True)  # z: heap block (_buf), same on every rank
+        self._zt = z
+        self._zt_form = form
 
     def _token_chunks(self, B: int) -> int:
         c = max(1, int(self.cfg.tp_chunks)) if self.tp_dev is not None else 1

@@ -42,13 +42,14 @@ from .layout import _host_comm, device_group_for
 
 
 class _Bucket:
-    __slots__ = ("params", "buf", "pending", "launched", "event", "sinks")
+    __slots__ = ("params", "buf", "pending", "launched", "reduced", "event", "sinks")
 
     def __init__(self, params, buf):
         self.params = params
         self.buf = buf
         self.pending = len(params)
         self.launched = False
+        self.reduced = False  # its all-reduce was issued this backward (the view is no longer ours)
         self.event = None
         self.sinks = []
 
@@ -70,10 +71,14 @@ class _GradSink:
     def begin(self):
         q = self.param
         if q.grad is None or q.grad.data_ptr() != self.view.data_ptr():
-            # grad dropped (zero_grad(set_to_none=True)) or replaced: the bucket view is the
-            # gradient again, and it is overwritten
+            # grad dropped (zero_grad) or replaced: the bucket view is the gradient again, and
+            # it is overwritten -- a user-supplied gradient is kept, scaled like everything the
+            # sink adds to it (the DDP average rides in every contribution, not in finish)
             if q.grad is not None:
-                self.view.copy_(q.grad)
+                if self.scale != 1.0:
+                    torch.mul(q.grad.view_as(self.view), self.scale, out=self.view)
+                else:
+                    self.view.copy_(q.grad.view_as(self.view))
                 self.fresh = False
             else:
                 self.fresh = True
@@ -91,7 +96,7 @@ class DistributedDataParallel(torch.nn.Module):
     """Wraps ``module``; ``comm`` is the DP communicator (Communicator or host Comm)."""
 
     def __init__(self, module: torch.nn.Module, comm, bucket_bytes: Optional[int] = None, algo: str = "auto",
-                 average: bool = True, overlap: bool = True, broadcast_params: bool = True, grad_sink: bool = True,
+                 average: bool = True, overlap: bool = True, broadcast_params: bool = True, grad_sink="auto",
                  max_blocks: Optional[int] = None):
         super().__init__()
         if bucket_bytes is None:
@@ -134,7 +139,9 @@ class DistributedDataParallel(torch.nn.Module):
         self.stream = (torch.cuda.Stream(device=dev, priority=-1)
                        if (dev.type == "cuda" and overlap and self.p > 1 and not crowded) else None)
         self._hooks = [q.register_post_accumulate_grad_hook(self._on_grad) for q in params]
-        if grad_sink and dev.type == "cuda":
+        self._late: List = []  # (param, scaled gradient) that arrived after its bucket's all-reduce started
+        # grad_sink: "auto" = on CUDA; True also on the CPU (the host plane; tests)
+        if grad_sink is True or (grad_sink == "auto" and dev.type == "cuda"):
             # the weights of the framework's TP layers, whose backward delivers dW itself;
             # every other parameter (biases, norms, embeddings, foreign modules) keeps the
             # AccumulateGrad + hook path
@@ -148,6 +155,7 @@ class DistributedDataParallel(torch.nn.Module):
                                        1.0 / self.p if (self.average and self.p > 1) else 1.0)
                         q._ccmpi_grad_sink = sk
                         b.sinks.append(sk)
+                        self._hooks.append(q.register_hook(self._sink_pre_hook(q, sk, b)))
 
     # ------------------------------------------------------------------ setup
     def _broadcast_params(self, params) -> None:
@@ -182,20 +190,48 @@ class DistributedDataParallel(torch.nn.Module):
         return self.module(*args, **kwargs)
 
     # --------------------------------------------------------------- backward
+    def _sink_pre_hook(self, q, sk: "_GradSink", b: "_Bucket"):
+        """Gradient hook of a sink parameter: a contribution that reaches the weight through
+        autograd (another use of the weight -- a penalty term, a foreign op) instead of the
+        layer's sink.  Autograd runs the weight's AccumulateGrad after every producer's
+        backward, so the layer's sink (if any) has delivered already.  The contribution is
+        scaled like the sink's (1/p, the DDP average in every summand); if the bucket's
+        all-reduce is already in flight it must not touch the bucket view: it is kept aside
+        and all-reduced on its own in ``finish``."""
+
+        def hook(g):
+            if g is None:
+                return None  # only the layer's sink produced this weight's gradient
+            if sk.reported and b.reduced:
+                self._late.append((q, g * sk.scale if sk.scale != 1.0 else g.clone()))
+                q.grad = None  # AccumulateGrad then stores a fresh tensor; _on_grad restores the view
+                return g
+            return g * sk.scale if sk.scale != 1.0 else g
+
+        return hook
+
     def _on_grad(self, q) -> None:
         v = self._view_of[id(q)]
-        if q.grad is not v and q.grad.data_ptr() != v.data_ptr():
-            # the user dropped the grad (zero_grad(set_to_none=True)): autograd made a
-            # fresh tensor -- move it into the bucket and re-attach the view
+        sk = getattr(q, "_ccmpi_grad_sink", None)
+        if sk is not None and sk.reported:
+            # the layer delivered this gradient itself: autograd still runs the post-accumulate
+            # hook for the parameter (it was counted already); a late contribution was set
+            # aside by the gradient hook -- re-attach the bucket view
+            q.grad = v
+            return
+        if q.grad is None:
+            q.grad = v  # no contribution at all
+            if sk is not None and sk.fresh:
+                v.zero_()  # a sink view nothing wrote this step reads as zero
+                sk.fresh = False
+        elif q.grad is not v and q.grad.data_ptr() != v.data_ptr():
+            # the user dropped the grad (zero_grad(set_to_none=True)), or a sink parameter
+            # reached only through autograd after DDP.zero_grad: autograd made a fresh tensor
+            # -- move it into the bucket and re-attach the view
             v.copy_(q.grad)
             q.grad = v
-        sk = getattr(q, "_ccmpi_grad_sink", None)
         if sk is not None:
-            if sk.reported:
-                # the layer delivered this gradient itself (and returned None): autograd still
-                # runs the post-accumulate hook for the parameter; it was counted already
-                return
-            sk.fresh = False  # the bucket view now holds this step's gradient
+            sk.fresh = False  # the bucket view now holds this step's gradient (already 1/p-scaled)
         self._ready(q)
 
     def _ready(self, q) -> None:
@@ -212,6 +248,7 @@ class DistributedDataParallel(torch.nn.Module):
             b.launched = True
             return
         b.launched = True
+        b.reduced = True
         if self.dev is None:  # host plane
             from .. import mpi as MPI
 
@@ -243,11 +280,26 @@ class DistributedDataParallel(torch.nn.Module):
                 self._launch(b)
         if self.stream is not None:
             torch.cuda.current_stream(self.device).wait_stream(self.stream)
+        if self._late:
+            # contributions that reached sink weights after their bucket's all-reduce started
+            # (already 1/p-scaled): every rank has the same list (same model code), each one
+            # is all-reduced on its own and added to the reduced bucket view
+            for q, g in self._late:
+                g = g.contiguous()
+                if self.dev is None:
+                    from .. import mpi as MPI
+
+                    self.hc.Allreduce(MPI.IN_PLACE, g.numpy(), op=MPI.SUM)
+                else:
+                    self.dev.allreduce(g, g, "SUM", self.algo)
+                self._view_of[id(q)].add_(g.view_as(self._view_of[id(q)]))
+            self._late = []
         if self.average and self.p > 1 and self.require_backward_grad_sync:
             # (no_sync micro-batches: the local sums keep accumulating, the synchronising
-            # backward reduces and averages all of them at once).  Gradients delivered by a
-            # sink are already scaled by 1/p in their GEMM's epilogue: only the others are
-            # scaled here (norms, biases, embeddings: ~1 GB of a Llama-3-8B's 16 GB)
+            # backward reduces and averages all of them at once).  Every contribution to a
+            # sink parameter is already scaled by 1/p (the GEMM's alpha, or the gradient
+            # hook): only the others are scaled here (norms, biases, embeddings: ~1 GB of a
+            # Llama-3-8B's 16 GB)
             for b in self.buckets:
                 if not b.sinks:
                     b.buf.mul_(1.0 / self.p)
@@ -259,13 +311,17 @@ class DistributedDataParallel(torch.nn.Module):
         for b in self.buckets:
             b.pending = len(b.params)
             b.launched = False
+            b.reduced = False
             for sk in b.sinks:
                 sk.reported = False
+                sk.param.grad = sk.view
 
     def zero_grad(self, set_to_none: bool = False) -> None:
         """Zero the gradients and re-attach every ``.grad`` view (``set_to_none`` is ignored).
-        Gradients with a sink are not written: the next backward overwrites them (and
-        ``finish`` zeroes the ones it did not reach)."""
+        Gradients with a sink are not written: their ``.grad`` is set to None instead, so the
+        next backward overwrites the bucket view -- through the layer's sink, or through
+        AccumulateGrad and ``_on_grad`` (a weight reached by another op) -- and ``finish``
+        zeroes the ones it did not reach and re-attaches the views."""
         for b in self.buckets:
             sunk = {id(sk.param) for sk in b.sinks}
             if not sunk:
@@ -277,7 +333,7 @@ class DistributedDataParallel(torch.nn.Module):
                 for sk in b.sinks:
                     sk.fresh = True
             for q in b.params:
-                q.grad = self._view_of[id(q)]
+                q.grad = None if id(q) in sunk else self._view_of[id(q)]
 
     def allreduce_all(self) -> None:
         """All-reduce every bucket now, back to back on the current stream (the comm-only

@@ -189,24 +189,41 @@ def measure_ddp_overlap(comm, layers: int = 32, tokens: int = 4096, seq: int = 2
     t_compute = timed(step)
     say(f"compute-only {t_compute * 1e3:.1f} ms")
     ddp.require_backward_grad_sync = True
-    t_comm = timed(ddp.allreduce_all) if p > 1 else 0.0
-    say(f"comm-only {t_comm * 1e3:.1f} ms")
-    sweep = {}
-    # budgets above the group's overlap cap would only be clamped to it (on a shared GPU:
-    # half the CUs, the deadlock bound -- DeviceComm.overlap_cap)
+
+    def hidden_of(t_c: float, t_o: float):
+        return None if p == 1 or t_c == 0 else max(0.0, min(1.0, (t_compute + t_c - t_o) / t_c))
+
+    # comm-only at the group's full CTA budget (max_blocks): the bound the links set, with no
+    # compute beside it
+    t_full = 0.0
+    if p > 1:
+        def allreduce_full():
+            for b in ddp.buckets:
+                dev.allreduce(b.buf, b.buf, "SUM", ddp.algo, max_blocks=dev.max_blocks, symmetric=True)
+
+        t_full = timed(allreduce_full)
+        say(f"comm-only at the full budget ({dev.max_blocks} CTAs) {t_full * 1e3:.1f} ms")
+    # every budget: comm-only and overlapped at the SAME bucket CTA budget, so each hidden
+    # fraction compares like with like; budgets above the group's overlap cap would only be
+    # clamped to it (on a shared GPU: half the CUs, the deadlock bound -- DeviceComm.overlap_cap)
     cap = getattr(dev, "overlap_cap", None)
     budgets = sorted({min(mb, cap) if cap else mb for mb in blocks_sweep}) if p > 1 else [0]
+    sweep, per = {}, {}
     for mb in budgets:
         ddp.max_blocks = mb or None
+        t_c = timed(ddp.allreduce_all) if p > 1 else 0.0
         sweep[mb] = timed(step)
-        say(f"overlapped, {mb} CTAs per bucket all-reduce: {sweep[mb] * 1e3:.1f} ms")
+        per[mb] = {"comm_ms": round(t_c * 1e3, 2), "overlapped_ms": round(sweep[mb] * 1e3, 2),
+                   "hidden": None if hidden_of(t_c, sweep[mb]) is None else round(hidden_of(t_c, sweep[mb]), 3)}
+        say(f"{mb} CTAs per bucket all-reduce: comm-only {t_c * 1e3:.1f} ms, overlapped {sweep[mb] * 1e3:.1f} ms")
     best_mb = min(sweep, key=sweep.get)
     ddp.max_blocks = best_mb or None
     t_both = sweep[best_mb]
+    t_comm = per[best_mb]["comm_ms"] / 1e3
     loss = float(step().item())
     torch.cuda.synchronize()
     dev.check()
-    hidden = None if p == 1 or t_comm == 0 else max(0.0, min(1.0, (t_compute + t_comm - t_both) / t_comm))
+    hidden = hidden_of(t_comm, t_both)
     gbytes = sum(b.buf.numel() * b.buf.element_size() for b in ddp.buckets)
     nonemb = nparams - (c.vocab * c.d if vocab else 0)
     flops = 6 * nonemb * batch * seq  # fwd + bwd GEMM work (attention scores not counted)
@@ -218,6 +235,9 @@ def measure_ddp_overlap(comm, layers: int = 32, tokens: int = 4096, seq: int = 2
            "compute_ms": round(t_compute * 1e3, 2), "comm_ms": round(t_comm * 1e3, 2),
            "overlapped_ms": round(t_both * 1e3, 2), "comm_hidden_fraction": None if hidden is None else round(hidden, 3),
            "comm_algbw_GBps": round(gbytes / t_comm / 1e9, 2) if t_comm else None,
+           "comm_full_ms": round(t_full * 1e3, 2), "comm_full_blocks": dev.max_blocks if p > 1 else None,
+           "comm_full_algbw_GBps": round(gbytes / t_full / 1e9, 2) if t_full else None,
+           "per_budget": {str(k): v for k, v in per.items()},
            "step_TFLOPs_per_rank": round(flops / t_both / 1e12, 1),
            "bucket_MiB": round(max(ddp.bucket_sizes) / (1 << 20), 1), "buckets": len(ddp.buckets),
            "bucket_ctas": best_mb, "bucket_ctas_sweep_ms": {str(k): round(v * 1e3, 2) for k, v in sweep.items()},

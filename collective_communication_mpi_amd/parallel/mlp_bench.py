@@ -24,8 +24,10 @@ def measure_tp_mlp(comm, tokens: int = 4096, d: int = 4096, ffn: int = 14336, it
     """Median forward and forward + backward times (max over ranks), the whole group's
     model TFLOP/s, the T x d bf16 TP all-reduce alone, and the host calls the device
     plane made during one steady-state forward + backward (0 expected).  ``variants``
-    (p > 1): the same block with each row-parallel mode (plain / chunked / fused) side by
-    side.  Collective: every rank calls."""
+    (p > 1): the same block with each row-parallel mode (plain / chunked / fused / push)
+    side by side FIRST; the fastest correct one is recorded as this shape's ``auto`` (the
+    group's ``row_modes``, CCMPI_TUNE_FILE), and the headline then runs ``auto``.
+    Collective: every rank calls."""
     from .. import mpi as MPI
 
     hc = comm.comm
@@ -91,6 +93,46 @@ def measure_tp_mlp(comm, tokens: int = 4096, d: int = 4096, ffn: int = 14336, it
         return t_f, t_fb, host, chk
 
     flop_f = 2 * tokens * d * 2 * ffn + 2 * tokens * ffn * d  # whole block (all ranks together)
+    var = None
+    if variants and p > 1:
+        # every row-parallel mode side by side, each checked against plain on the same input
+        # (push / chunked sum the same partials in rank order: bitwise equal); the fastest
+        # correct forward becomes this (M, N)'s "auto" for groups of this identity -- written
+        # to CCMPI_TUNE_FILE like the collectives' table, and used by the headline below
+        var, ref = {}, None
+        for m in tp.ROW_MODES:
+            try:
+                mlp = build(m)
+                vf, vfb, vh, vchk = run(mlp)
+                calls0 = dict(tp.CALLS)
+                with torch.no_grad():
+                    out_m = mlp(x)
+                ran = [k for k, v in tp.CALLS.items() if v != calls0.get(k, 0) and k.startswith("row_")]
+                if ref is None:
+                    ref = out_m
+                exact = bool(hc.allreduce(int(torch.equal(out_m, ref)), op=MPI.MIN))
+                close = bool(hc.allreduce(int(torch.allclose(out_m.float(), ref.float(), rtol=2e-2, atol=2e-3)),
+                                          op=MPI.MIN))
+                var[m] = {"fwd_ms": round(vf * 1e3, 3), "fwd_bwd_ms": round(vfb * 1e3, 3), "host_calls_per_step": vh,
+                          "out_abs_mean": round(vchk, 6), "bitwise_equal_plain": exact, "close_to_plain": close,
+                          "ran": ran}
+                del mlp, out_m
+            except Exception as e:  # noqa: BLE001 - one variant must not cost the record
+                var[m] = {"error": f"{type(e).__name__}: {e}"[:200]}
+        ok = {m: v["fwd_ms"] for m, v in var.items()
+              if "error" not in v and v["close_to_plain"] and (m != "push" or v["bitwise_equal_plain"])
+              and any(r == f"row_{m}" for r in v["ran"])}  # the mode actually ran (not a fallback)
+        if ok:
+            best = min(ok, key=ok.get)
+            dg = comm.dev
+            dg.row_modes[(tokens, d)] = best
+            path = getattr(dg, "tune_file", None)
+            if path and comm.Get_rank() == 0:
+                from ..device import save_row_modes
+
+                save_row_modes(path, dg.tune_key, dg.row_modes)
+            hc.Barrier()
+            var["auto_choice"] = best
     default_mode = tp._row_mode(mode or tp._ROW_MODE, comm, tokens, d) if p > 1 else "local"
     calls0 = dict(tp.CALLS)
     t_f, t_fb, host, chk = run(build(mode))
@@ -105,14 +147,6 @@ def measure_tp_mlp(comm, tokens: int = 4096, d: int = 4096, ffn: int = 14336, it
         "fwd_TFLOPs": round(flop_f / t_f / 1e12, 1), "fwd_bwd_TFLOPs": round(3 * flop_f / t_fb / 1e12, 1),
         "tp_allreduce_bytes": tokens * d * 2, "tp_allreduce_ms": round(t_ar * 1e3, 3),
         "host_calls_per_step": host, "tp_paths": paths, "out_abs_mean": round(chk, 6)}
-    if variants and p > 1:
-        var = {}
-        for m in tp.ROW_MODES:
-            try:
-                vf, vfb, vh, vchk = run(build(m))
-                var[m] = {"fwd_ms": round(vf * 1e3, 3), "fwd_bwd_ms": round(vfb * 1e3, 3), "host_calls_per_step": vh,
-                          "out_abs_mean": round(vchk, 6)}
-            except Exception as e:  # noqa: BLE001 - one variant must not cost the record
-                var[m] = {"error": f"{type(e).__name__}: {e}"[:200]}
+    if var is not None:
         out["row_mode_variants"] = var
     return out

@@ -31,6 +31,7 @@ from __future__ import annotations
 import collections
 import math
 import os
+from typing import Optional
 
 import torch
 
@@ -232,29 +233,31 @@ def _linear_backward(g2: torch.Tensor, x2: torch.Tensor, w: torch.Tensor, need_d
 #   inbox (posted writes under the GEMM, nobody spins), then one inbox-to-local two-shot
 #   (DeviceGroup.gemm_push_allreduce).  Needs M % (256 p) == 0, no bias and the ring GEMM
 #   (a GPU of its own, or CCMPI_SHARED_RING); otherwise plain.
-# * "auto" (default) -- "chunked" when every rank owns its GPU AND each row block's GEMM
-#   still fills the chip (>= one 256x256 tile per CU): the all-reduce then crosses xGMI while
-#   the next block's GEMM keeps every CU busy.  Otherwise "plain": a block of fewer tiles
-#   than CUs takes as long as the whole GEMM (one wave either way), so chunking would double
-#   the GEMM time -- the Llama MLP's 4096 x 4096 output is exactly 256 tiles -- and ranks
-#   sharing a GPU compete for the same HBM and CUs (plain measured fastest there:
-#   profiles/r4_first, profiles/r4_shared_ring, 1.18 ms against chunked 1.36 ms at TP = 2).
-#   bench.py's mlp phase records all three modes (tp_mlp.row_mode_variants).
+# * "auto" (default) -- the mode the bench's mlp phase MEASURED fastest for this (M, N) on a
+#   group of the same identity (size, GPU sharing, GPU model), read from CCMPI_TUNE_FILE
+#   (``DeviceGroup.row_modes``; every rank loads the same file, so the choice is the same on
+#   every rank); "plain" when nothing was measured.  "chunked" is never the unmeasured
+#   default: a row block of fewer 256x256 tiles than CUs takes as long as the whole GEMM (one
+#   wave either way), so at the Llama shapes (4096 x 4096 = 256 tiles, 128 per half) chunking
+#   doubles the GEMM time; "push" is only chosen when it measured faster AND bitwise equal to
+#   "plain" (parallel/mlp_bench.py).
 ROW_MODES = ("plain", "chunked", "fused", "push")
 _ROW_MODE = os.environ.get("CCMPI_TP_ROW_MODE", "auto")
+
+
+def row_mode_from_table(table: dict, M: int, N: int) -> str:
+    """``auto``'s choice from a measured {(M, N): mode} table (pure: tests)."""
+    mode = table.get((int(M), int(N)))
+    return mode if mode in ROW_MODES else "plain"
 
 
 def _row_mode(mode: str, comm, M: int = 0, N: int = 0) -> str:
     """The row-parallel mode a call with a [M, N] output runs (resolves ``auto``)."""
     if mode != "auto":
         return mode
-    if _size_rank(comm)[0] > 1 and bool(device_group_for(comm).shared_device):
+    if _size_rank(comm)[0] == 1:
         return "plain"
-    blocks = _chunk_rows(M, _TP_CHUNKS) if M else []
-    if len(blocks) < 2:
-        return "plain"
-    tiles = -(-(blocks[0][1] - blocks[0][0]) // 256) * -(-N // 256)
-    return "chunked" if tiles >= _cu_count() else "plain"
+    return row_mode_from_table(getattr(device_group_for(comm), "row_modes", {}), M, N)
 
 
 _CUS: dict = {}
@@ -277,8 +280,10 @@ CALLS: "collections.Counter[str]" = collections.Counter()
 def _scratch(comm, role: str, shape, dtype):
     """Persistent symmetric-heap scratch of the TP group, shared by every layer (each use
     is joined before the next layer's GEMM writes it, and a collective ends only after
-    every peer read of it): allocated once per (role, shape, dtype), no host call after."""
-    return device_group_for(comm).persistent(("tp_" + role,), shape, dtype)
+    every peer read of it): one grow-only block per (role, dtype) -- a view of it for each
+    shape, so varying token counts reuse it (``DeviceGroup.scratch_view``); no host call
+    once it is large enough."""
+    return device_group_for(comm).scratch_view("tp_" + role, shape, dtype)
 
 
 def _dev_path(x2: torch.Tensor, w: torch.Tensor, comm) -> bool:
@@ -328,6 +333,7 @@ def _deliver_wgrad(w: torch.Tensor, dw):
         torch.mul(dw.view_as(view), sink.scale, out=view)
     else:
         view.copy_(dw.view_as(view))
+    CALLS["wgrad_sink"] += 1
     sink.done()
     return None
 

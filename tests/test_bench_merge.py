@@ -67,8 +67,8 @@ def test_faster_rccl_never_replaces_handwritten_value():
 def test_phase_plan_isolates_harness():
     args = bench.parse([])
     names = [p for p, _ in bench.plan_phases(args, 8)]
-    assert names == ["coll", "harness", "mlp", "dp", "rccl"]
-    assert [p for p, _ in bench.plan_phases(args, 1)] == ["coll", "harness", "mlp"]
+    assert names == ["coll", "harness", "mlp", "dp", "rccl", "host"]
+    assert [p for p, _ in bench.plan_phases(args, 1)] == ["coll", "harness", "mlp", "host"]
     assert "fanout:1024" not in bench.allreduce_candidates(8, False)
 
 
@@ -104,3 +104,118 @@ def test_tuning_sweep_failure_keeps_headline():
     # no record at all: the zero headline, as before
     out = bench.merge_results(args, 8, _status(coll=-11), {}.get)
     assert out["value"] == 0.0
+
+
+def _fake_pick(fail, times):
+    """pick_candidates with injected failures (``fail``: candidates whose attempt fails on
+    'rank 1'), a fake agree over 2 ranks and counted resets."""
+    resets = []
+
+    def attempt(c):
+        if c in fail:
+            raise RuntimeError("device collective timeout/fault code 0x301 on rank 1 (phase 3, peer 0)")
+        return None
+
+    def agree(err):
+        return f"rank 1: {err}" if err else None
+
+    return attempt, agree, lambda: resets.append(1), lambda c: times[c], resets
+
+
+def test_failed_first_candidate_keeps_trying():
+    """a failing first candidate is reset away and the rest are still
+    tried; every outcome is recorded with its error text."""
+    cands = ["twoshot:256", "twoshot:512", "fanout:256", "fanout:512", "ring"]
+    times = {"twoshot:512": 4e-3, "fanout:256": 3e-3, "fanout:512": 2.5e-3, "ring": 9e-3}
+    attempt, agree, reset, timer, resets = _fake_pick({"twoshot:256"}, times)
+    out, best = bench.pick_candidates(cands, attempt, agree, reset, timer)
+    assert best == "fanout:512" and len(resets) == 1
+    assert out["twoshot:256"]["ms"] is None and "0x301" in out["twoshot:256"]["error"]
+    assert out["ring"]["ms"] == 9.0 and out["ring"]["error"] is None
+
+
+def test_every_candidate_failing_returns_none():
+    cands = ["fanout:256", "ring"]
+    attempt, agree, reset, timer, resets = _fake_pick(set(cands), {})
+    out, best = bench.pick_candidates(cands, attempt, agree, reset, timer)
+    assert best is None and len(resets) == 2 and all(o["error"] for o in out.values())
+
+
+def test_timing_failure_is_a_candidate_error():
+    def timer(c):
+        if c == "a":
+            raise RuntimeError("boom")
+        return 1e-3
+
+    out, best = bench.pick_candidates(["a", "b"], lambda c: None, lambda e: e, lambda: None, timer)
+    assert best == "b" and "during timing" in out["a"]["error"]
+
+
+def test_candidate_order_follows_self_test():
+    cands = bench.allreduce_candidates(8, False)
+    order, skipped = bench.order_candidates(cands, {"ll": True, "oneshot": True, "fanout": True, "twoshot": False},
+                                            {"twoshot"})
+    assert "twoshot:256" in skipped and "twoshot:512" in skipped
+    assert order[:3] == ["fanout:256", "fanout:512", "fanout_lds:512"]
+    assert order[3:] == ["push:512", "ring", "rhd"]
+    # no self test (one rank) keeps the given order
+    order, skipped = bench.order_candidates(["b", "a"], None, set())
+    assert order == ["b", "a"] and not skipped
+
+
+def test_injected_candidate_fault_spec(monkeypatch):
+    monkeypatch.setenv("CCMPI_RANK", "0")
+    monkeypatch.setenv("CCMPI_SIZE", "2")
+    monkeypatch.setenv("CCMPI_BENCH_FAULT", "candidate:twoshot:256,candidate_bf16:*")
+    assert bench._injected("twoshot:256", "fp32") and bench._injected("twoshot:256", "bf16")
+    assert not bench._injected("fanout:512", "fp32") and bench._injected("fanout:512", "bf16")
+    monkeypatch.setenv("CCMPI_RANK", "1")
+    assert not bench._injected("twoshot:256", "fp32")  # only rank 0 skips its kernel
+
+
+def test_bf16_exhaustion_keeps_fp32_headline():
+    """An exhausted bf16 candidate list records an error in its block; the record (and the
+    fp32 value) survive."""
+    args = bench.parse([])
+    coll = _coll()
+    coll["config"]["bf16_1GiB"] = {"error": "no bf16 candidate produced a correct result",
+                                   "candidates": {"fanout:512": {"ms": None, "error": "rank 0: injected"}}}
+    out = bench.merge_results(args, 8, {"coll": {"ok": True, "returncodes": [0] * 8, "seconds": 1}},
+                              {"coll": coll}.get)
+    assert out["value"] == 500.0 and "error" in out["config"]["bf16_1GiB"] and "warning" not in out
+
+
+def test_partial_headline_sets_top_level_warning():
+    args = bench.parse([])
+    early = {**_coll(), "partial": "written after the fp32 headline, before the secondaries"}
+    out = bench.merge_results(args, 8, _status(coll=-11), {"coll": early}.get)
+    assert out["value"] == 500.0 and "warning" in out
+
+
+def test_host_phase_record_merged():
+    args = bench.parse([])
+    assert [p for p, _ in bench.plan_phases(args, 1)][-1] == "host"
+    assert "host" not in [p for p, _ in bench.plan_phases(bench.parse(["--host-ranks", "0"]), 1)]
+    st = {"coll": {"ok": True, "returncodes": [0], "seconds": 1}, "host": {"ok": True, "returncodes": [0], "seconds": 3}}
+    rec = {"ranks": 8, "allreduce": {"Allreduce_avg_us": 12.0, "myAllreduce_avg_us": 20.0, "all_runs_equal": True}}
+    out = bench.merge_results(args, 1, st, {"coll": _coll(), "host": rec}.get)
+    assert out["config"]["host_cpu"]["allreduce"]["all_runs_equal"]
+
+
+def test_host_phase_runs_on_cpu(tmp_path):
+    """BASELINE config 1 end to end on the CPU: 8 host-plane processes, library vs
+    hand-written all-reduce / all-to-all, every run checked equal."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    res = tmp_path / "host.json"
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-m", "collective_communication_mpi_amd.launch", "-n", "8", "--timeout", "150",
+                        sys.executable, "bench.py", "--phase", "host", "--host-runs", "20", "--result", str(res)],
+                       cwd=repo, capture_output=True, text=True, timeout=200)
+    assert r.returncode == 0, r.stderr[-3000:]
+    rec = json.loads(res.read_text())
+    assert rec["ranks"] == 8 and rec["allreduce"]["all_runs_equal"] and rec["alltoall"]["all_runs_equal"]
+    assert rec["allreduce"]["myAllreduce_avg_us"] > 0 and rec["alltoall"]["myAlltoall_avg_us"] > 0

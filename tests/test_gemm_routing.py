@@ -35,24 +35,42 @@ def test_route_switch(monkeypatch):
 
 
 def test_row_parallel_auto_mode(monkeypatch):
-    """``auto``: chunked (the all-reduce of a row block under the next block's GEMM) when
-    every rank owns its GPU and each block's GEMM still fills the chip; plain otherwise;
-    explicit modes pass through."""
+    """``auto``: the mode the mlp phase measured for this (M, N) on a group
+    of the same identity (the group's ``row_modes`` table, loaded from CCMPI_TUNE_FILE);
+    "plain" when nothing was measured -- "chunked" is never the unmeasured default; explicit
+    modes pass through."""
     from types import SimpleNamespace
 
     from collective_communication_mpi_amd.parallel import tensor_parallel as tp
 
     monkeypatch.setattr(tp, "_size_rank", lambda comm: (2, 0))
-    monkeypatch.setattr(tp, "_cu_count", lambda: 256)
-    monkeypatch.setattr(tp, "device_group_for", lambda comm: SimpleNamespace(shared_device=False))
-    # 16384 x 8192 output: 2 blocks of 32 x 32 tiles (>= one per CU) -> chunked
-    assert tp._row_mode("auto", object(), 16384, 8192) == "chunked"
-    # the Llama MLP's 4096 x 4096 output: 2 blocks of 128 tiles -> plain
-    assert tp._row_mode("auto", object(), 4096, 4096) == "plain"
-    assert tp._row_mode("auto", object(), 256, 8192) == "plain"  # one block
-    monkeypatch.setattr(tp, "device_group_for", lambda comm: SimpleNamespace(shared_device=True))
+    monkeypatch.setattr(tp, "device_group_for", lambda comm: SimpleNamespace(shared_device=False, row_modes={}))
     assert tp._row_mode("auto", object(), 16384, 8192) == "plain"
+    assert tp._row_mode("auto", object(), 4096, 4096) == "plain"
+    table = {(4096, 4096): "push", (8192, 4096): "chunked", (256, 64): "bogus"}
+    monkeypatch.setattr(tp, "device_group_for", lambda comm: SimpleNamespace(shared_device=False, row_modes=table))
+    assert tp._row_mode("auto", object(), 4096, 4096) == "push"
+    assert tp._row_mode("auto", object(), 8192, 4096) == "chunked"
+    assert tp._row_mode("auto", object(), 256, 64) == "plain"  # unknown mode names are ignored
+    assert tp._row_mode("auto", object(), 2048, 4096) == "plain"
     assert tp._row_mode("fused", object(), 4096, 4096) == "fused"
+
+
+def test_row_mode_tune_file_switches_auto_to_push(tmp_path):
+    """A tune-file entry written by the mlp phase (save_row_modes) is what a device group
+    created afterwards loads (load_row_modes) and what ``auto`` then runs; it sits beside the
+    collective tables in the same file without disturbing them."""
+    from collective_communication_mpi_amd.device import load_row_modes, load_tuning, save_row_modes, save_tuning
+    from collective_communication_mpi_amd.parallel import tensor_parallel as tp
+
+    path = str(tmp_path / "tune.json")
+    save_tuning(path, "p8-share1-MI355X", {(8, 20): "fanout"})
+    save_row_modes(path, "p8-share1-MI355X", {(4096, 4096): "push"})
+    assert load_tuning(path, "p8-share1-MI355X") == {(8, 20): "fanout"}
+    table = load_row_modes(path, "p8-share1-MI355X")
+    assert table == {(4096, 4096): "push"} and load_row_modes(path, "p2-share1-MI355X") == {}
+    assert tp.row_mode_from_table(table, 4096, 4096) == "push"
+    assert tp.row_mode_from_table({}, 4096, 4096) == "plain"
 
 
 def test_row_parallel_push_applies(monkeypatch):

@@ -188,6 +188,35 @@ def test_bench_tuning_crash_keeps_headline():
     assert "-11" in c["coll_phase_error"], c.get("coll_phase_error")
 
 
+def test_bench_failing_candidates_keep_headline():
+    """the first fp32 candidate fails (rank 0 skips its kernel, rank 1 times
+    out in it), and so does every bf16 candidate; the bench resets, tries the rest, records
+    each failure with its timeout code, and ``value`` comes from the next working algorithm."""
+    import json
+    import subprocess
+    import sys
+
+    from _launch import REPO
+
+    e = dict(os.environ, **ENV, CCMPI_BENCH_FAULT="candidate:twoshot:256,candidate_bf16:*")
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--steps", "2", "--warmup", "1", "--size-mb", "16",
+                        "--a2a-mb", "8", "--dp-layers", "0", "--tune-max-mb", "1", "--no-rccl", "--no-harness",
+                        "--mlp-tokens", "0", "--host-ranks", "0"],
+                       cwd=REPO, env=e, capture_output=True, text=True, timeout=400)
+    assert r.returncode == 0, r.stderr[-4000:]
+    out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    c = out["config"]
+    assert out["value"] > 0 and c["result_exact"], out
+    cand = c["candidates"]
+    assert cand["twoshot:256"]["ms"] is None and "rank" in cand["twoshot:256"]["error"], cand
+    assert c["allreduce_algo"] != "twoshot:256" and sum(1 for o in cand.values() if o["ms"]) >= 3, cand
+    assert "error" in c["bf16_1GiB"] and all(o["error"] for o in c["bf16_1GiB"]["candidates"].values()), c["bf16_1GiB"]
+    assert c["alltoall_pairwise"]["ms"] > 0 and c["alltoall"]["ms"] > 0
+    sw = c["sweep"]
+    assert sw["float32"] and all(pt["algbw_GBps"] for pt in sw["float32"]), sw
+    assert sw["bfloat16"] and sw["float32"][-1]["bytes"] == 16 << 20
+
+
 @pytest.mark.parametrize("case", ["myallreduce", "myalltoall"])
 def test_cli_device_cases(case):
     """The reference CLI cases on device buffers (reference mpi-test.py:42-98,178-239):
@@ -220,6 +249,26 @@ def test_harness_matches_single_rank(reference_run, tmp_path, n, tp, mode):
     for k in ("q_w", "o_w", "emb_w"):
         np.testing.assert_allclose(got[k], reference_run[k], rtol=5e-2, atol=5e-3)
     assert got["losses"][-1] < got["losses"][0]
+
+
+@pytest.mark.parametrize("n", [2, 8])
+def test_harness_fc_o_push_equals_plain(n):
+    """the per-token fc_o's push form (row blocks stored into the TP
+    owners' inboxes by the attention kernel, then inbox-to-local) is bitwise equal to the
+    plain form (kernel + all-reduce of z), TP = 2 at 2 and 8 ranks on one GPU."""
+    r = run_ranks(n, py("tests/workers/fc_o_push_worker.py"), timeout=300, env=ENV)
+    assert "fc_o push OK" in r.stdout
+
+
+def test_harness_token_push_matches_single_rank(reference_run, tmp_path):
+    """The push form's training run reproduces the single-rank run (dp=1 x tp=2, token fc_o)."""
+    out = tmp_path / "run.npz"
+    run_ranks(2, py("tests/workers/harness_worker.py", "--tp", "2", "--mode", "token", "--out", str(out)),
+              timeout=400, env=dict(ENV, CCMPI_TP_FC_O_FORM="push"))
+    got = np.load(out)
+    np.testing.assert_allclose(got["losses"], reference_run["losses"], rtol=2e-2, atol=2e-3)
+    for k in ("q_w", "o_w", "emb_w"):
+        np.testing.assert_allclose(got[k], reference_run[k], rtol=5e-2, atol=5e-3)
 
 
 def test_harness_checkpoint_resume(tmp_path):
@@ -257,6 +306,13 @@ def test_swiglu_mlp_ring_gemm_beside_collectives_gpu(n):
     env = {**ENV, "CCMPI_SHARED_RING": "1", "CCMPI_RING_MIN_MACS": "1", "CCMPI_KMAJOR_MIN_MACS": "1"}
     r = run_ranks(n, py("tests/workers/swiglu_mlp_worker.py", "--device", "cuda", "--big"), timeout=300, env=env)
     assert "swiglu mlp OK" in r.stdout
+
+
+def test_tp_scratch_reused_across_token_counts():
+    """varying token counts reuse one grow-only scratch block per role (no host
+    call once the largest shape was seen), results vs fp32 at every M."""
+    r = run_ranks(2, py("tests/workers/tp_varm_worker.py"), timeout=300, env=ENV)
+    assert "varm OK" in r.stdout
 
 
 @pytest.mark.parametrize("n", [2, 4])

@@ -423,6 +423,50 @@ def test_attn_fused_fc_o(B, S, H, D, n_out):
     assert (b2 - b1).norm() <= 1e-2 * b1.norm() + 1e-3
 
 
+@pytest.mark.parametrize("B,S,H,D,n_out", [(2048, 16, 2, 64, 16), (2048, 16, 4, 64, 16), (37, 16, 1, 128, 10),
+                                            (12, 9, 2, 32, 16)])
+def test_attn_token_fc_o(B, S, H, D, n_out):
+    """Per-token row-parallel fc_o inside the attention kernel: z[t] = bf16(O[t]) . W_o^T + b_o
+    (heads summed in the workgroup, MFMA) against torch fp32 on the kernel's own O; the push
+    form (row blocks stored write-through to per-block targets, here local buffers) writes
+    bitwise the same rows; the pooled output is still produced."""
+    from collective_communication_mpi_amd import _native
+
+    dev = _native.device()
+    st = torch.cuda.current_stream().cuda_stream
+    g = torch.Generator(device="cuda").manual_seed(B * 7 + H)
+    qkv = (torch.randn(B * S, 3 * H * D, device="cuda", generator=g) * 0.5).bfloat16()
+    lse = torch.empty(B * H, S, device="cuda")
+    o = torch.empty(B * S, H * D, device="cuda", dtype=torch.bfloat16)
+    pool = torch.empty(B, H * D, device="cuda", dtype=torch.bfloat16)
+    wo = torch.zeros(16, H * D, device="cuda").bfloat16()
+    wo[:n_out] = (torch.randn(n_out, H * D, device="cuda", generator=g) * 0.1).bfloat16()
+    bo = torch.zeros(16, device="cuda")
+    bo[:n_out] = torch.randn(n_out, device="cuda", generator=g)
+    z = torch.full((B * S, 16), float("nan"), device="cuda")
+    kw = dict(wo=wo.data_ptr(), ld_wo=wo.stride(0), n_out=n_out, bo=bo.data_ptr(), ld_zt=16)
+    dev.attn_small_fwd(qkv.data_ptr(), o.data_ptr(), lse.data_ptr(), B, S, H, D, qkv.stride(0), o.stride(0), D ** -0.5,
+                       pool.data_ptr(), pool.stride(0), st, ztok=z.data_ptr(), **kw)
+    ref_o = _attn_ref(qkv, B, S, H, D)
+    torch.testing.assert_close(o.float(), ref_o, rtol=2e-2, atol=2e-2)
+    torch.testing.assert_close(pool.float(), ref_o.view(B, S, H * D).mean(1), rtol=2e-2, atol=2e-2)
+    ref_z = o.float() @ wo[:n_out].float().T + bo[:n_out]
+    torch.testing.assert_close(z[:, :n_out], ref_z, rtol=1e-4, atol=1e-4)
+    assert torch.all(z[:, n_out:] == 0)
+    # push form: blocks of whole sequences into separate targets
+    blocks = 4 if B % 4 == 0 else 1
+    zrows = B * S // blocks
+    tg = torch.full((blocks, zrows, 16), float("nan"), device="cuda")
+    dev.attn_small_fwd(qkv.data_ptr(), 0, lse.data_ptr(), B, S, H, D, qkv.stride(0), H * D, D ** -0.5,
+                       pool.data_ptr(), pool.stride(0), st, zrows=zrows,
+                       zpush=[tg[j].data_ptr() for j in range(blocks)], **kw)
+    torch.cuda.synchronize()
+    assert torch.equal(tg.view(B * S, 16), z)
+    with pytest.raises(ValueError):  # a block boundary inside a sequence
+        dev.attn_small_fwd(qkv.data_ptr(), 0, lse.data_ptr(), B, S, H, D, qkv.stride(0), H * D, D ** -0.5,
+                           pool.data_ptr(), pool.stride(0), st, zrows=S + 1, zpush=[tg.data_ptr()], **kw)
+
+
 @pytest.mark.parametrize("img,patch,misalign", [(28, 7, 0), (28, 7, 1), (24, 6, 0)])  # LDS / plain / runtime sizes
 def test_patchify_columns(img, patch, misalign):
     from collective_communication_mpi_amd.models.mnist_tp import LayerConfig, patchify

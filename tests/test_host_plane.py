@@ -135,6 +135,17 @@ def test_llama_ddp_cpu():
     assert "llama dp OK" in r.stdout
 
 
+@pytest.mark.parametrize("penalty", [0.0, 0.05])
+def test_llama_ddp_sinks_cpu(penalty):
+    """DDP gradient sinks on the host plane, with a weight penalty on TP weights
+    whose gradient then arrives through the layer's sink AND through autograd (after the
+    bucket's all-reduce started): averaged exactly once, and zero_grad leaves no stale
+    sink view behind (two steps + a no_sync accumulation)."""
+    r = run_ranks(2, py("tests/workers/llama_dp_worker.py", "--device", "cpu", "--sink", "--penalty", str(penalty)),
+                  timeout=300)
+    assert "llama dp OK" in r.stdout
+
+
 def test_launcher_bind_to_core(tmp_path):
     """``--bind-to core`` (Open MPI semantics): every rank pinned to its own CPU."""
     import os

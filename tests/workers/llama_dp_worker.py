@@ -9,7 +9,10 @@ finish every rank's gradients must equal the mean over ranks of the per-rank gra
 of an unwrapped replica (computed here for every rank's batch), for two steps (the
 second exercises zero_grad's sink reset) and with a micro-batch accumulation step.  On
 CUDA the weight gradients of the TP layers must arrive through the gradient sinks.
-``--measure``: also run measure_ddp_overlap on the tiny model.  Prints "llama dp OK"."""
+``--measure``: also run measure_ddp_overlap on the tiny model.  ``--sink``: gradient sinks on
+the CPU too (host plane); ``--penalty``: a weight penalty on TP weights (their gradient then
+arrives through the layer's sink AND through autograd) -- the sum must still be
+averaged exactly once.  Prints "llama dp OK"."""
 import argparse
 import os
 import sys
@@ -26,6 +29,8 @@ from collective_communication_mpi_amd.parallel.llama_dp import (LlamaConfig, Lla
 ap = argparse.ArgumentParser()
 ap.add_argument("--device", default="cpu")
 ap.add_argument("--measure", action="store_true")
+ap.add_argument("--sink", action="store_true")
+ap.add_argument("--penalty", type=float, default=0.0)
 args = ap.parse_args()
 comm = Communicator(MPI.COMM_WORLD)
 hc = comm.comm
@@ -40,7 +45,20 @@ B, S = 2, 64
 selfc = _self_comm(comm)
 model = LlamaModel(cfg, selfc, device, dtype=dt, seed=3)
 ref = LlamaModel(cfg, selfc, device, dtype=dt, seed=3)
-ddp = DistributedDataParallel(model, comm, bucket_bytes=64 << 10, broadcast_params=False)
+ddp = DistributedDataParallel(model, comm, bucket_bytes=64 << 10, broadcast_params=False,
+                              **({"grad_sink": True} if args.sink else {}))
+
+
+def penalized(m):
+    """Weights with an extra loss term (reach the weight through autograd, beside the sink)."""
+    return [m.blocks[0].wq.weight, m.blocks[-1].mlp.down.weight, m.head.weight]
+
+
+def loss_of(m, ids):
+    loss = m(ids)
+    if args.penalty:
+        loss = loss + args.penalty * sum((w.float() ** 2).sum() for w in penalized(m))
+    return loss
 
 
 def ids_of(r, step):
@@ -54,7 +72,7 @@ def ref_grads(step, micro=1):
     for r in range(p):
         ref.zero_grad(set_to_none=True)
         for m in range(micro):
-            ref(ids_of(r, step * 10 + m)).backward()
+            loss_of(ref, ids_of(r, step * 10 + m)).backward()
         gs = [q.grad.float().clone() for q in ref.parameters()]
         acc = gs if acc is None else [a + b for a, b in zip(acc, gs)]
     return [a / p for a in acc]
@@ -73,10 +91,11 @@ def compare(tag, want):
 for step in range(2):
     sinks0 = tp.CALLS["wgrad_sink"]
     ddp.zero_grad()
-    ddp(ids_of(rank, step * 10)).backward()
+    loss_of(model, ids_of(rank, step * 10)).backward()
     ddp.finish()
-    if device.type == "cuda":
-        torch.cuda.synchronize()
+    if device.type == "cuda" or args.sink:
+        if device.type == "cuda":
+            torch.cuda.synchronize()
         n_tp = 4 * cfg.layers + 2 * cfg.layers + 1  # q k v o + gate_up down per layer + LM head
         if tp.CALLS["wgrad_sink"] - sinks0 != n_tp:
             fails.append(f"step {step}: {tp.CALLS['wgrad_sink'] - sinks0} sink dW GEMMs, expected {n_tp}")
@@ -84,10 +103,10 @@ for step in range(2):
 # micro-batch accumulation: no sync on the first, sync on the second (the sinks add)
 ddp.zero_grad()
 ddp.require_backward_grad_sync = False
-ddp(ids_of(rank, 50)).backward()
+loss_of(model, ids_of(rank, 50)).backward()
 ddp.finish()
 ddp.require_backward_grad_sync = True
-ddp(ids_of(rank, 51)).backward()
+loss_of(model, ids_of(rank, 51)).backward()
 ddp.finish()
 compare("accumulate", ref_grads(5, micro=2))
 if args.measure and device.type == "cuda":
