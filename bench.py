@@ -658,6 +658,17 @@ def run_secondaries(comm, args, h: dict, log=lambda *a: None, groups=("bf16", "a
     return sec
 
 
+def run_collectives(comm, args, log=lambda *a: None, groups=("ar", "bf16", "a2a")) -> dict:
+    """The coll phase's device work in one call (benchmarks/graph_replay_repro.py): the
+    headline, then the secondaries named in ``groups``; the 1 GiB buffers are released before
+    returning.  Returns the headline fields plus ``secondary``."""
+    r = run_headline(comm, args, log)
+    sec = [g for g in groups if g in ("bf16", "a2a")]
+    r["secondary"] = run_secondaries(comm, args, r, log, tuple(sec)) if sec else {}
+    r.pop("x", None), r.pop("y", None)
+    return r
+
+
 def tuning_sweep(comm, args, best_1gib: str, log=lambda *a: None) -> dict:
     """N >= 2: ``DeviceGroup.tune`` over 16 KiB .. ``--tune-max-mb`` with every hand-written
     algorithm ``auto`` may pick (ring and RHD included), plus the 1 GiB winner, written to

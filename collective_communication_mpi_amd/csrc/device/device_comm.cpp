@@ -474,9 +474,12 @@ void DeviceComm::allreduce_pipelined_(int algo, uint64_t in, uint64_t out, uint6
   if (symmetric && (!in_al || out % 16 || !code_of_(out, nbytes)))
     throw std::invalid_argument("ccmpi: symmetric ring/rhd all-reduce needs a registered output and aligned input");
   const bool out_reg = symmetric;
-  // the piece size must not depend on `symmetric` (a per-rank view of the caller's
-  // buffers): every rank splits into the same launches even if one rank stages
-  piece = std::min(piece, half);
+  // `symmetric` is identical on every rank (the Python layer decides it collectively, or the
+  // caller promises it): with it nothing is staged, so the pieces are bounded by the inbox
+  // alone -- a 1 GiB all-reduce is ONE launch, not 32 scratch-sized ones (64 MiB scratch on a
+  // shared GPU: every launch paid the start barrier and the 2(p-1)-step pipeline fill again,
+  // profiles/r5_ring).  Staged calls keep pieces of half the scratch.
+  if (!symmetric) piece = std::min(piece, half);
   piece = staging_chunk_(piece, 16 * es);
   if (piece == 0) throw std::runtime_error("ccmpi: inbox/scratch too small for ring/rhd");
   char* stage = reinterpret_cast<char*>(scratch_ptr());

@@ -613,7 +613,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t op_rsrc_t(const uint16_t* X, i
 // p+1 landed everywhere, slot p free).
 template <int EPI, int PERSIST, int ABL = 0, int STAMP = 0, int TA = 0, int TB = 0, int PAIR = 0>
 __global__ void __launch_bounds__(WNT, 1) k_gemm_w4r(W4Args wa) {
-  static_assert(!PAIR || (!ABL && !STAMP && !TA), "pair-slot ring: N-layout A");
+  static_assert(!PAIR || (!ABL && !STAMP), "pair-slot ring: no diagnostics");
   const GemmArgs& g = wa.g;
   extern __shared__ __attribute__((aligned(1024))) unsigned char smem[];
   const int tiles_n = (g.N + WNB - 1) / WNB, tiles_m = (g.M + WM - 1) / WM;
@@ -725,11 +725,12 @@ __global__ void __launch_bounds__(WNT, 1) k_gemm_w4r(W4Args wa) {
   const int pch = ((lane & 7) ^ (((wave & 1) * 4 + (lane >> 4)) & 7)) << 4;
   const int pva = (wave * 8 + (lane >> 3)) * g.lda * 2 + pch, pvb = (wave * 8 + (lane >> 3)) * g.ldb * 2 + pch;
   const int psa = 32 * g.lda * 2, psb = 32 * g.ldb * 2;  // piece stride: 32 rows
-  // PAIR + TB (dX = dY W): the B half of a pair slot holds the pair's two K-steps in the
-  // K-major layout of the 4-slot ring ([32 k][256 rows], 512-B k-rows -- already whole
-  // lines), step h at + h * 16 KiB.  Every DMA piece is then inline asm (M0 + load) and the
-  // transposed B reads use the builtin, which the compiler tracks: with no builtin LDS-DMA
-  // in the kernel it adds no vmcnt(0) before them, and no manual lgkmcnt is needed.
+  // PAIR + TB (dX = dY W) / TA (dW = dY^T X, with TB: both operands M-major, no transposes):
+  // a K-major operand's half of a pair slot holds the pair's two K-steps in the K-major layout
+  // of the 4-slot ring ([32 k][256 rows], 512-B k-rows -- already whole lines), step h at
+  // + h * 16 KiB.  Every DMA piece is then inline asm (M0 + load) and the transposed reads use
+  // the builtin, which the compiler tracks: with no builtin LDS-DMA in the kernel it adds no
+  // vmcnt(0) before them, and no manual lgkmcnt is needed.
   auto dma_asm = [&](unsigned char* dst, __amdgpu_buffer_rsrc_t rs, int vo, int so) {
     const uint32_t m0v = (uint32_t)(uintptr_t)(lds_vptr)dst;
     asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
@@ -740,13 +741,22 @@ __global__ void __launch_bounds__(WNT, 1) k_gemm_w4r(W4Args wa) {
   auto dma_pair = [&](int p, int i) {  // piece i of pair p: 0..7 A, 8..15 B
     const bool isa = i < 8;
     unsigned char* slot = smem + (p & 1) * kPair;
-    if constexpr (TB) {
+    if constexpr (TA || TB) {
+      // K-major operand: step 2 p + h, piece j of its 16 KiB (the 4-slot ring's layout);
+      // an N-layout operand: the pair layout's whole-line pieces
+      const int j = i & 3, h = (i & 7) >> 2;
       if (isa) {
-        dma_asm(slot + (i & 7) * 4096 + wave * 1024, ra, pva + p * 128, (i & 7) * psa);
-      } else {  // K-major B: step 2 p + h, piece j of its 16 KiB (the 4-slot ring's layout)
-        const int j = (i - 8) & 3, h = (i - 8) >> 2;
-        dma_asm(slot + kPairHalf + h * 16384 + j * 4096 + wave * 1024, rb, ((j & 1) ? tb1 : tb0) + (2 * p + h) * kb,
-                j == 0 ? 0 : j == 1 ? sb1 : j == 2 ? sb2 : sb3);
+        if constexpr (TA)
+          dma_asm(slot + h * 16384 + j * 4096 + wave * 1024, ra, ((j & 1) ? ta1 : ta0) + (2 * p + h) * ka,
+                  j == 0 ? 0 : j == 1 ? sa1 : j == 2 ? sa2 : sa3);
+        else
+          dma_asm(slot + (i & 7) * 4096 + wave * 1024, ra, pva + p * 128, (i & 7) * psa);
+      } else {
+        if constexpr (TB)
+          dma_asm(slot + kPairHalf + h * 16384 + j * 4096 + wave * 1024, rb, ((j & 1) ? tb1 : tb0) + (2 * p + h) * kb,
+                  j == 0 ? 0 : j == 1 ? sb1 : j == 2 ? sb2 : sb3);
+        else
+          dma_asm(slot + kPairHalf + (i & 7) * 4096 + wave * 1024, rb, pvb + p * 128, (i & 7) * psb);
       }
     } else {
       unsigned char* dst = slot + (isa ? 0 : kPairHalf) + (i & 7) * 4096 + wave * 1024;
@@ -769,6 +779,7 @@ __global__ void __launch_bounds__(WNT, 1) k_gemm_w4r(W4Args wa) {
     const int r0 = (grp < 4 ? wc : wr) * 128 + (grp & 3) * 32 + u * 16;
     bf16x8 v;
     if (TB && grp < 4) v = rd_tb(slot + kPairHalf + h * 16384, r0);
+    else if (TA && grp >= 4) v = rd_tb(slot + h * 16384, r0);  // K-major A (dW = dY^T X): same fragment layout
     else v = *reinterpret_cast<const bf16x8*>(slot + (grp < 4 ? kPairHalf : 0) + (h ? prd1 : prd0) + r0 * 128);
     if (grp < 4) fb[(grp & 3) * 2 + u] = v;
     else fa[(grp & 3) * 2 + u] = v;
@@ -1139,6 +1150,9 @@ unsigned long long* g_w4_dbg = nullptr;
 long long g_ring_launches = 0;
 // auto dispatch: the pair-slot ring (0.93-0.95x hipBLASLt on the Llama MLP shapes against
 // 0.86-0.89x for the 4-slot ring, profiles/r4_pair); CCMPI_RING_SCHED overrides (A/B runs)
+// K-major A on the pair ring without K-major B (CCMPI_PAIR_TA=1): the TA + TB form is the
+// default for dW = dY^T X; A alone goes to the 4-slot ring unless asked for
+int g_pair_ta = std::getenv("CCMPI_PAIR_TA") ? std::atoi(std::getenv("CCMPI_PAIR_TA")) : 0;
 int g_ring_sched = std::getenv("CCMPI_RING_SCHED") ? std::atoi(std::getenv("CCMPI_RING_SCHED")) : (8 | 16384);
 long long g_ring_min_macs = std::getenv("CCMPI_RING_MIN_MACS") ? std::atoll(std::getenv("CCMPI_RING_MIN_MACS")) : (1ll << 33);
 
@@ -1224,6 +1238,10 @@ void launch_gemm_ring(const GemmArgs& g, int ta, int tb, hipStream_t stream, uin
     w4p_attr(reinterpret_cast<const void*>(k_gemm_w4r<2, 1, 0, 0, 0, 0, 1>));
     w4p_attr(reinterpret_cast<const void*>(k_gemm_w4r<0, 0, 0, 0, 0, 1, 1>));
     w4p_attr(reinterpret_cast<const void*>(k_gemm_w4r<1, 0, 0, 0, 0, 1, 1>));
+    w4p_attr(reinterpret_cast<const void*>(k_gemm_w4r<0, 0, 0, 0, 1, 0, 1>));
+    w4p_attr(reinterpret_cast<const void*>(k_gemm_w4r<1, 0, 0, 0, 1, 0, 1>));
+    w4p_attr(reinterpret_cast<const void*>(k_gemm_w4r<0, 0, 0, 0, 1, 1, 1>));
+    w4p_attr(reinterpret_cast<const void*>(k_gemm_w4r<1, 0, 0, 0, 1, 1, 1>));
     return true;
   }();
   (void)attr;
@@ -1247,9 +1265,18 @@ void launch_gemm_ring(const GemmArgs& g, int ta, int tb, hipStream_t stream, uin
     else hipLaunchKernelGGL((k_gemm_w4r<2, 0>), dim3(ntiles), dim3(WNT), kRingLds, stream, a);
     return;
   }
-  if (!ta && tb && pair) {  // dX = dY W: pair-slot ring, N-layout A, K-major B
-    if (fast) hipLaunchKernelGGL((k_gemm_w4r<1, 0, 0, 0, 0, 1, 1>), dim3(ntiles), dim3(WNT), kPairLds, stream, a);
-    else hipLaunchKernelGGL((k_gemm_w4r<0, 0, 0, 0, 0, 1, 1>), dim3(ntiles), dim3(WNT), kPairLds, stream, a);
+  if ((ta || tb) && pair && (tb || g_pair_ta)) {
+    // K-major operands on the pair-slot ring: dX = dY W (B), dW = dY^T X (A and B: no
+    // transposes); K-major A alone only on request (CCMPI_PAIR_TA)
+    const int v = (ta ? 2 : 0) + (tb ? 1 : 0) + (fast ? 4 : 0);
+    switch (v) {
+      case 1: hipLaunchKernelGGL((k_gemm_w4r<0, 0, 0, 0, 0, 1, 1>), dim3(ntiles), dim3(WNT), kPairLds, stream, a); break;
+      case 5: hipLaunchKernelGGL((k_gemm_w4r<1, 0, 0, 0, 0, 1, 1>), dim3(ntiles), dim3(WNT), kPairLds, stream, a); break;
+      case 2: hipLaunchKernelGGL((k_gemm_w4r<0, 0, 0, 0, 1, 0, 1>), dim3(ntiles), dim3(WNT), kPairLds, stream, a); break;
+      case 6: hipLaunchKernelGGL((k_gemm_w4r<1, 0, 0, 0, 1, 0, 1>), dim3(ntiles), dim3(WNT), kPairLds, stream, a); break;
+      case 3: hipLaunchKernelGGL((k_gemm_w4r<0, 0, 0, 0, 1, 1, 1>), dim3(ntiles), dim3(WNT), kPairLds, stream, a); break;
+      default: hipLaunchKernelGGL((k_gemm_w4r<1, 0, 0, 0, 1, 1, 1>), dim3(ntiles), dim3(WNT), kPairLds, stream, a); break;
+    }
     return;
   }
   if (ta || tb) {  // K-major operands on the 4-slot ring: non-persistent, no diagnostics

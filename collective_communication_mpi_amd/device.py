@@ -883,11 +883,11 @@ class DeviceGroup:
         if algo == "ring":
             self.dc.set_rings(rings or self.default_rings)
         if algo in _HAND_ALGOS:
-            # ring / rhd read only the local input and push into peers' outputs:
-            # "symmetric" there means a registered output (and an aligned input)
-            symm = self._symm_call(nbytes, *((dst,) if algo in ("ring", "rhd") else (src, dst)), promise=symmetric)
-            if algo in ("ring", "rhd"):
-                symm = symm and src.data_ptr() % 16 == 0
+            # one decision on every rank (ring / rhd split the call into launches by it):
+            # both tensors go through the collective check, which also covers the alignment
+            # of every rank's input (ring / rhd read only the local input, but a rank-local
+            # alignment test could make the ranks disagree)
+            symm = self._symm_call(nbytes, src, dst, promise=symmetric)
             self.dc.allreduce(src.data_ptr(), dst.data_ptr(), src.numel(), dt, opc, getattr(self.D, _HAND_ALGOS[algo]),
                               s, self._budget(max_blocks), symm)
         elif algo == "rccl":

@@ -168,11 +168,25 @@ def gemm_ring(a: torch.Tensor, b: torch.Tensor, ta: bool, tb: bool, out: Optiona
         out = torch.empty((M, N), dtype=out_dtype, device=a.device)
     if out.shape != (M, N) or out.stride(1) != 1 or out.dtype not in (torch.bfloat16, torch.float32):
         raise ValueError("gemm_ring output must be [M, N] bf16/fp32 with unit column stride")
+    route = os.environ.get("CCMPI_KMAJOR_ROUTE", "transpose")
+    if ta and route == "pair":
+        # dW = dY^T X with both operands M-major on the pair-slot ring's TA (+ TB) form: no
+        # transposes at all (an N-layout copy the producer wrote is not needed either)
+        ok = _D().gemm_ring(a.data_ptr(), b.data_ptr(), out.data_ptr(), M, N, K, a.stride(0), b.stride(0),
+                            out.stride(0), 1, int(tb), float(alpha), bool(accumulate), out.dtype == torch.bfloat16,
+                            _stream(a))
+        if ok:
+            return out
     if ta and (a_nt is not None or _kmajor_via_transpose(M, N, K, a, b)):
-        # K-major operands transposed first (k_transpose16_v, ~6 TB/s), then the N-layout
-        # pair-slot ring: its whole-line DMA pieces and one ds_read_b128 per fragment beat
-        # the K-major ring's two transposed LDS reads per fragment (profiles/r4_bwd)
+        # K-major A transposed first (k_transpose16_v, ~6 TB/s) -- or taken from a_nt, the
+        # N-layout copy its producer wrote -- then the pair-slot ring: its whole-line DMA
+        # pieces and one ds_read_b128 per fragment beat the 4-slot K-major ring's two
+        # transposed LDS reads per fragment (profiles/r4_bwd).  A K-major B stays K-major:
+        # the pair ring reads it directly (its dX = dY W form), so dW = dY^T X transposes
+        # at most dY (CCMPI_WGRAD_B=transpose: the old route, both operands transposed)
         at = a_nt if a_nt is not None else transpose(a)
+        if tb and os.environ.get("CCMPI_WGRAD_B", "kmajor") == "kmajor":
+            return gemm_ring(at, b, False, True, out=out, alpha=alpha, accumulate=accumulate, out_dtype=out_dtype)
         bt = transpose(b) if tb else b
         return gemm_ring(at, bt, False, False, out=out, alpha=alpha, accumulate=accumulate, out_dtype=out_dtype)
     ok = _D().gemm_ring(a.data_ptr(), b.data_ptr(), out.data_ptr(), M, N, K, a.stride(0), b.stride(0), out.stride(0),

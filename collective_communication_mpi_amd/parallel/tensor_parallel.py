@@ -190,7 +190,17 @@ def _gpu_shared(comm) -> bool:
         return False
     if comm is None or _size_rank(comm)[0] == 1:
         return _device.SHARED_GPU_IN_PROCESS
-    return bool(device_group_for(comm).shared_device) or _device.SHARED_GPU_IN_PROCESS
+    dg = device_group_for(comm)
+    v = getattr(dg, "_tp_shared_agreed", None)
+    if v is None:
+        # the kernel routes this picks must be the same on every rank of the group (push vs
+        # plain row mode, ring vs fallback GEMMs around a collective): the process-global part
+        # differs between processes, so the group agrees once (one host all-reduce, cached)
+        from .. import mpi as MPI
+
+        local = bool(dg.shared_device) or _device.SHARED_GPU_IN_PROCESS
+        v = dg._tp_shared_agreed = bool(dg.host.allreduce(int(local), op=MPI.MAX))
+    return v
 
 
 def _mfma_ok(x: torch.Tensor, w: torch.Tensor, comm=None) -> bool:

@@ -619,16 +619,19 @@ def test_fold_emb_qkv_matches_fp32(R, d, kp):
     assert torch.isnan(out[:, kp:].float()).all()  # columns past kp untouched
 
 
-@pytest.mark.parametrize("route", ["transpose", "ring"])
+@pytest.mark.parametrize("route", ["transpose", "ring", "pair"])
 @pytest.mark.parametrize("ta,tb", [(0, 1), (1, 1), (1, 0)], ids=["kA-tB", "tA-tB", "tA-kB"])
 def test_gemm_ring_kmajor_routes(monkeypatch, route, ta, tb):
-    """A large K-major GEMM both ways: transposed copies + the N-layout pair ring (the
-    default route above 2^33 MACs) and the K-major ring; fp32 reference, bf16 out with
-    alpha, and fp32 accumulate (the DDP gradient-sink forms)."""
+    """A large K-major GEMM every way: transposed copies + the N-layout pair ring, the
+    K-major operands read straight by the pair ring (TA / TB forms: no transposes), and the
+    4-slot K-major ring; fp32 reference, bf16 out with alpha, and fp32 accumulate (the DDP
+    gradient-sink forms)."""
     from collective_communication_mpi_amd import _native
     from collective_communication_mpi_amd.ops import gemm_ring
 
     monkeypatch.setenv("CCMPI_KMAJOR_ROUTE", route)
+    if route == "pair":
+        _native.device().gemm_set_pair_ta(1)  # the (1, 0) form on the pair ring too
     M, N, K = 2048, 2048, 2048
     g = torch.Generator(device="cuda").manual_seed(17 + ta + 2 * tb)
     a = torch.randn(K, M, device="cuda", generator=g).bfloat16() if ta else torch.randn(M, K, device="cuda", generator=g).bfloat16()
@@ -641,6 +644,7 @@ def test_gemm_ring_kmajor_routes(monkeypatch, route, ta, tb):
     c = torch.randn(M, N, device="cuda")
     c0 = c.clone()
     gemm_ring(a, b, bool(ta), bool(tb), out=c, accumulate=True)
+    _native.device().gemm_set_pair_ta(0)
     torch.testing.assert_close(c, c0 + ref, rtol=2e-3, atol=2e-3 * K ** 0.5)
 
 
