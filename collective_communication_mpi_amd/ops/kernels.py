@@ -168,10 +168,13 @@ def gemm_ring(a: torch.Tensor, b: torch.Tensor, ta: bool, tb: bool, out: Optiona
         out = torch.empty((M, N), dtype=out_dtype, device=a.device)
     if out.shape != (M, N) or out.stride(1) != 1 or out.dtype not in (torch.bfloat16, torch.float32):
         raise ValueError("gemm_ring output must be [M, N] bf16/fp32 with unit column stride")
-    route = os.environ.get("CCMPI_KMAJOR_ROUTE", "transpose")
+    route = os.environ.get("CCMPI_KMAJOR_ROUTE", "pair")
     if ta and route == "pair":
         # dW = dY^T X with both operands M-major on the pair-slot ring's TA (+ TB) form: no
-        # transposes at all (an N-layout copy the producer wrote is not needed either)
+        # transposes at all (an N-layout copy the producer wrote is not needed either).
+        # Llama-3-8B MLP at T = 4096: dW_down 0.369 ms against 0.464 ms for both operands
+        # transposed, the whole block forward + backward 3.334 ms against 3.395 ms
+        # (profiles/r5_fourth).  CCMPI_KMAJOR_ROUTE=transpose: the round-4 route
         ok = _D().gemm_ring(a.data_ptr(), b.data_ptr(), out.data_ptr(), M, N, K, a.stride(0), b.stride(0),
                             out.stride(0), 1, int(tb), float(alpha), bool(accumulate), out.dtype == torch.bfloat16,
                             _stream(a))
@@ -196,10 +199,11 @@ def gemm_ring(a: torch.Tensor, b: torch.Tensor, ta: bool, tb: bool, out: Optiona
 
 def _kmajor_via_transpose(M: int, N: int, K: int, a: torch.Tensor, b: torch.Tensor) -> bool:
     """Route a K-major ring GEMM through transposed copies (CCMPI_KMAJOR_ROUTE=transpose,
-    read per call; ``ring`` keeps the K-major kernel): K-major A (the dW = dY^T X form),
-    large GEMMs only, and not long K.  dX = dY W (K-major B only) stays on the ring: a
-    transposed weight copy + the pair ring measured no faster (profiles/r4_bwd)."""
-    if os.environ.get("CCMPI_KMAJOR_ROUTE", "transpose") != "transpose":
+    read per call; default ``pair``: the pair ring reads K-major operands itself; ``ring``: the
+    4-slot K-major kernel): K-major A (the dW = dY^T X form), large GEMMs only, and not long
+    K.  dX = dY W (K-major B only) stays on the ring: a transposed weight copy + the pair ring
+    measured no faster (profiles/r4_bwd)."""
+    if os.environ.get("CCMPI_KMAJOR_ROUTE", "pair") != "transpose":
         return False
     dmin = int(os.environ.get("CCMPI_KMAJOR_MIN_DIM", 1024))  # (tests lower both thresholds)
     return (M >= dmin and N >= dmin and K <= 16384 and K % 8 == 0 and M % 8 == 0 and N % 8 == 0

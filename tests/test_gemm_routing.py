@@ -10,8 +10,17 @@ def _t(*shape):
     return torch.empty(*shape, dtype=torch.bfloat16)
 
 
-def test_dw_shapes_take_the_transpose_route(monkeypatch):
+def test_dw_default_route_reads_kmajor_operands(monkeypatch):
+    """Default route ``pair``: the pair ring reads both M-major dW operands itself (no
+    transposes, no dh^T); the round-4 transpose route stays selectable."""
     monkeypatch.delenv("CCMPI_KMAJOR_ROUTE", raising=False)
+    T, d, f = 4096, 4096, 14336
+    assert not _kmajor_via_transpose(2 * f, d, T, _t(T, 2 * f), _t(T, d))
+    assert not _kmajor_via_transpose(d, f, T, _t(T, d), _t(T, f))
+
+
+def test_dw_shapes_take_the_transpose_route(monkeypatch):
+    monkeypatch.setenv("CCMPI_KMAJOR_ROUTE", "transpose")
     T, d, f = 4096, 4096, 14336
     # gate|up dW = dh^T X: M = 2f, N = d, K = T
     assert _kmajor_via_transpose(2 * f, d, T, _t(T, 2 * f), _t(T, d))
@@ -20,7 +29,7 @@ def test_dw_shapes_take_the_transpose_route(monkeypatch):
 
 
 def test_long_k_small_and_ragged_stay_on_the_ring(monkeypatch):
-    monkeypatch.delenv("CCMPI_KMAJOR_ROUTE", raising=False)
+    monkeypatch.setenv("CCMPI_KMAJOR_ROUTE", "transpose")
     assert not _kmajor_via_transpose(4096, 4096, 28672, _t(28672, 4096), _t(28672, 4096))  # long K
     assert not _kmajor_via_transpose(512, 4096, 4096, _t(4096, 512), _t(4096, 4096))  # M < 1024
     assert not _kmajor_via_transpose(1024, 1024, 1024, _t(1024, 1024), _t(1024, 1024))  # < 2^33 MACs

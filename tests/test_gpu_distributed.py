@@ -294,16 +294,18 @@ def test_parallel_swiglu_mlp_gpu(n):
     assert "swiglu mlp OK" in r.stdout
 
 
-@pytest.mark.parametrize("n", [2, 4, 8])
-def test_swiglu_mlp_ring_gemm_beside_collectives_gpu(n):
+@pytest.mark.parametrize("n,route", [(2, "pair"), (4, "pair"), (8, "pair"), (2, "transpose")])
+def test_swiglu_mlp_ring_gemm_beside_collectives_gpu(n, route):
     """the kernels an 8-GPU TP run uses (LDS-ring GEMMs, the SwiGLU
     epilogue, K-major backward rings) next to the other ranks' TP collectives on one GPU:
     CCMPI_SHARED_RING=1 keeps the ring on and holds every collective to half the CUs.  The
     worker also checks the push row mode against plain, bit for bit (8 ranks: the driver's
     8-GPU mlp phase runs it at TP = 8)."""
-    # (CCMPI_KMAJOR_MIN_MACS=1: these small shapes also take the dW transpose route, with
-    # dh^T from the fused SwiGLU backward, across TP ranks)
-    env = {**ENV, "CCMPI_SHARED_RING": "1", "CCMPI_RING_MIN_MACS": "1", "CCMPI_KMAJOR_MIN_MACS": "1"}
+    # (route "pair", the default: dW reads both M-major operands on the pair ring; route
+    # "transpose" with CCMPI_KMAJOR_MIN_MACS=1: these small shapes also take the round-4 dW
+    # transpose route, with dh^T from the fused SwiGLU backward, across TP ranks)
+    env = {**ENV, "CCMPI_SHARED_RING": "1", "CCMPI_RING_MIN_MACS": "1", "CCMPI_KMAJOR_MIN_MACS": "1",
+           "CCMPI_KMAJOR_ROUTE": route}
     r = run_ranks(n, py("tests/workers/swiglu_mlp_worker.py", "--device", "cuda", "--big"), timeout=300, env=env)
     assert "swiglu mlp OK" in r.stdout
 
@@ -330,7 +332,7 @@ def test_bench_tuning_table_drives_auto(tmp_path):
     assert "tune OK" in r.stdout
 
 
-@pytest.mark.parametrize("route", ["default", "transpose_all"])
+@pytest.mark.parametrize("route", ["default", "transpose_all", "pair_all"])
 def test_llama_ddp_gradient_sinks_gpu(route):
     """BASELINE config 5's machinery on a tiny Llama: DDP over 2 ranks with the TP layers'
     dW GEMMs writing straight into the buckets (gradient sinks), vs the mean of replica
@@ -340,7 +342,9 @@ def test_llama_ddp_gradient_sinks_gpu(route):
     env = dict(ENV)
     if route == "transpose_all":
         env.update({"CCMPI_SHARED_RING": "1", "CCMPI_RING_MIN_MACS": "1", "CCMPI_KMAJOR_MIN_MACS": "1",
-                    "CCMPI_KMAJOR_MIN_DIM": "8"})
+                    "CCMPI_KMAJOR_MIN_DIM": "8", "CCMPI_KMAJOR_ROUTE": "transpose"})
+    elif route == "pair_all":  # every dW on the pair ring's TA + TB form (the default route), small shapes too
+        env.update({"CCMPI_SHARED_RING": "1", "CCMPI_RING_MIN_MACS": "1"})
     r = run_ranks(2, py("tests/workers/llama_dp_worker.py", "--device", "cuda", "--measure"), timeout=300, env=env)
     assert "llama dp OK" in r.stdout
 

@@ -80,7 +80,8 @@ if rel(gd, wd.grad) > tol:
 
 if args.big and args.device == "cuda" and _native.device().gemm_ring_launches() == ring0:
     fails.append("--big: no LDS-ring GEMM launched (the path under test did not run)")
-if args.big and args.device == "cuda" and os.environ.get("CCMPI_KMAJOR_MIN_MACS") == "1":
+if (args.big and args.device == "cuda" and os.environ.get("CCMPI_KMAJOR_MIN_MACS") == "1"
+        and os.environ.get("CCMPI_KMAJOR_ROUTE") == "transpose"):
     from collective_communication_mpi_amd.parallel import tensor_parallel as _tp  # noqa: E402
 
     if not _tp.CALLS["dh_transposed"]:
