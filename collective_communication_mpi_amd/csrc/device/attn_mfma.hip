@@ -233,26 +233,36 @@ __global__ void __launch_bounds__(256) k_attn16_fwd(AttnArgs a) {
    }
    if (a.ztok || a.zrows) {
     // the Hl heads of each sequence of this iteration (consecutive waves, Hl | WPB), summed in
-    // head order, + the bias; thread t = (token t >> 4, class t & 15): a 64-B row per 16 lanes
+    // head order, + the bias.  Wave s writes sequence s (waves s >= WPB / Hl idle): lane l =
+    // (token l >> 2, classes 4 (l & 3) .. +3), one 16-B store per lane, a sequence's S x 16
+    // fp32 rows as whole lines
     __syncthreads();  // (the next iteration writes the other buffer)
-    const int t = threadIdx.x, i = t >> 4, cls = t & 15;
-    for (int w = 0; w < WPB; w += a.Hl) {
-      const int prw = base + w;
-      if (prw >= npairs) break;
+    const int i = lane >> 2, q = (lane & 3) * 4, w = wave * a.Hl;
+    const int prw = base + w;
+    if (w < WPB && prw < npairs) {
       const int b = prw / a.Hl;
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = (a.bo && q + r < a.n_out) ? a.bo[q + r] : 0.f;
+      float z4[4] = {0.f, 0.f, 0.f, 0.f};
+      for (int k = 0; k < a.Hl; ++k) {
+        const float4 x = *reinterpret_cast<const float4*>(&ztp[it][w + k][i * 16 + q]);
+        z4[0] += x.x; z4[1] += x.y; z4[2] += x.z; z4[3] += x.w;
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = z4[r] + v[r];
+      const u32x4 pk = {__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3])};
+      const size_t row0 = (size_t)b * S;  // the sequence's first row
       if (i < S) {
-        float acc = 0.f;
-        for (int k = 0; k < a.Hl; ++k) acc += ztp[it][w + k][i * 16 + cls];
-        if (a.bo && cls < a.n_out) acc += a.bo[cls];
-        const size_t row = (size_t)b * S + i;
         if (a.zrows) {
-          // zrows % S == 0: the whole sequence lies in one block, j is workgroup-uniform
-          const int j = (int)((size_t)b * S / a.zrows);
-          float* dst = a.zpush[j] + (row - (size_t)j * a.zrows) * a.ld_zt + cls;
-          __hip_atomic_store(reinterpret_cast<uint32_t*>(dst), __float_as_uint(acc), __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_SYSTEM);  // write-through store into the peer's inbox
+          // zrows % S == 0: the whole sequence lies in block j (wave-uniform); rank j's inbox
+          // slot over xGMI, stored write-through (sc0 sc1) like every collective store
+          const int j = __builtin_amdgcn_readfirstlane((int)(row0 / a.zrows));
+          char* seq = reinterpret_cast<char*>(a.zpush[j] + (row0 - (size_t)j * a.zrows) * a.ld_zt);
+          const Rsrc rs = make_rsrc(uniform_ptr(seq), (uint32_t)(S * a.ld_zt * 4));
+          __builtin_amdgcn_raw_buffer_store_b128(pk, rs.r, (uint32_t)((i * a.ld_zt + q) * 4), 0, kStorePolicy);
         } else {
-          a.ztok[row * a.ld_zt + cls] = acc;
+          *reinterpret_cast<u32x4*>(a.ztok + (row0 + i) * a.ld_zt + q) = pk;
         }
       }
     }
@@ -268,7 +278,6 @@ __global__ void __launch_bounds__(256) k_attn16_fwd(AttnArgs a) {
     }
    }
   }
-  if (a.zrows) release_sys();  // pushed rows performed system-wide before the workgroup retires
 }
 
 template <int D>

@@ -250,7 +250,7 @@ void attn_fwd(uint64_t qkv, uint64_t o, uint64_t lse, int B, int S, int Hl, int 
   if (ztok || zrows) {
     // per-token fused fc_o (local z, or pushed row blocks): the MFMA kernel's workgroup layout
     if (zp || !attn::mfma_supported(a, false) || n_out < 1 || n_out > 16 || 4 % Hl || !wo || ld_wo % 8 ||
-        (wo % 16) || ld_zt < 16)
+        (wo % 16) || ld_zt < 16 || ld_zt % 4 || (ztok % 16))
       throw std::invalid_argument("attention: per-token fused fc_o needs S <= 16, D in {32, 64, 128}, Hl | 4, "
                                   "n_out <= 16, 16-B aligned W_o rows, z rows of >= 16 floats");
     if (zrows) {

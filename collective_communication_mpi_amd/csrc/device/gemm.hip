@@ -1194,6 +1194,7 @@ void register_gemm_ops(pybind11::module_& m) {
   m.def("gemm_set_ring_min", [](long long v) { g_ring_min_macs = v; },
         "gemm_nt auto: LDS-ring kernel from this many multiply-adds up (0 = never)");
   m.def("gemm_ring_launches", [] { return g_ring_launches; }, "LDS-ring GEMM launches so far (this process)");
+  m.def("gemm_set_pair_nobar", [](int v) { g_pair_nobar = v; }, "diagnostic: pair ring without its barrier (wrong results)");
   m.def("gemm_set_pair_ta", [](int v) { g_pair_ta = v; }, "K-major A alone on the pair-slot ring (1) or the 4-slot ring (0)");
   m.def("gemm_set_ring_sched", [](int v) { g_ring_sched = v; },
         "auto-dispatched LDS-ring kernel variant: bit 3 ring, bit 14 pair slots (default), bit 0 persistent, bit 15 long K too; diagnostics: bits 5-6 / 13 ablations, bit 9 stamps");

@@ -207,6 +207,7 @@ extern int g_pp_exp;
 void launch_gemm_tn_256(const GemmArgs& g, hipStream_t stream);
 // 256 x 256 four-wave kernel (gemm_w4.hip): 128 x 128 per wave, K % 64 == 0, no split-K
 bool gemm_w4_ok(const GemmArgs& g);
+extern int g_pair_nobar;  // diagnostic: pair ring without its odd-phase barrier (wrong results)
 extern int g_pair_ta;     // K-major A alone on the pair-slot ring (CCMPI_PAIR_TA; gemm_set_pair_ta)
 extern int g_ring_sched;  // auto-dispatched LDS-ring kernel variant (gemm_w4.hip launch_gemm_ring)
 extern long long g_ring_launches;  // launch_gemm_ring calls (tests: the ring path really ran)

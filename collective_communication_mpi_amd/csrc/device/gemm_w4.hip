@@ -59,6 +59,10 @@ struct W4Args {
   // push_rows) goes to push[j] (row 0 of the block at push[j]; a peer's inbox slot), not C
   int push_rows;
   uint16_t* push[kMaxRanks];
+  // diagnostic (gemm_set_pair_nobar, wrong results): the pair ring's odd-phase sync reduced to
+  // the wave's own waits (1), to the barrier without the DMA wait (2), or to neither (3) --
+  // upper bounds of removing the barrier's skew / the DMA latency stalls
+  int nobar;
 };
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t op_rsrc(const uint16_t* base, long rows, int ld) {
@@ -873,7 +877,23 @@ __global__ void __launch_bounds__(WNT, 1) k_gemm_w4r(W4Args wa) {
       __builtin_amdgcn_sched_barrier(0);
       mm(5, 8);
     }
-    if constexpr (ODD) ring_wait_barrier_c<0>();
+    if constexpr (ODD) {
+      if (wa.nobar == 1) {  // own waits only, no barrier
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+      } else if (wa.nobar == 2) {  // barrier, DMA not waited for
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+      } else if (wa.nobar == 3) {  // neither
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+      } else {
+        ring_wait_barrier_c<0>();
+      }
+    }
   };
 
   const int ldc = g.ldc;
@@ -1152,6 +1172,7 @@ long long g_ring_launches = 0;
 // 0.86-0.89x for the 4-slot ring, profiles/r4_pair); CCMPI_RING_SCHED overrides (A/B runs)
 // K-major A on the pair ring without K-major B (CCMPI_PAIR_TA=1): the TA + TB form is the
 // default for dW = dY^T X; A alone goes to the 4-slot ring unless asked for
+int g_pair_nobar = 0;
 int g_pair_ta = std::getenv("CCMPI_PAIR_TA") ? std::atoi(std::getenv("CCMPI_PAIR_TA")) : 0;
 int g_ring_sched = std::getenv("CCMPI_RING_SCHED") ? std::atoi(std::getenv("CCMPI_RING_SCHED")) : (8 | 16384);
 long long g_ring_min_macs = std::getenv("CCMPI_RING_MIN_MACS") ? std::atoll(std::getenv("CCMPI_RING_MIN_MACS")) : (1ll << 33);
@@ -1247,6 +1268,7 @@ void launch_gemm_ring(const GemmArgs& g, int ta, int tb, hipStream_t stream, uin
   (void)attr;
   const int ntiles = gemm_w4_tiles(g.M, g.N);
   W4Args a{g, g_w4_group_m, {}, g_w4_dbg, glu, ldglu};
+  a.nobar = g_pair_nobar;
   const bool fast = gemm_w4r_fast(g);
   if (push_rows) {  // row blocks into peers' inboxes: the fast NT epilogue, whole tiles per block
     const int blocks = push_rows > 0 ? g.M / push_rows : 0;
