@@ -43,12 +43,23 @@ struct AttnArgs {
   int ld_zt;
   int zrows;
   float* zpush[16];
+  // Fused QKV projection (k_qkv_attn16_fwd, the harness forward): qkv = X W^T + b computed in
+  // the attention kernel from the patch rows X ([B*S][ld_xq] bf16, kq <= 96 columns) and the
+  // folded weight W ([3 Hl D][ld_wq] bf16: q rows, then k, then v) with the fp32 bias bq;
+  // qkv_out (optional, [B*S][ld_qkv] bf16): the projection is also stored, for a backward
+  const uint16_t* xq;
+  int ld_xq, kq;
+  const uint16_t* wq;
+  int ld_wq;
+  const float* bq;
+  uint16_t* qkv_out;
 };
 
 // MFMA path (attn_mfma.hip): S <= 16, D in {32, 64, 128}, 16-B aligned rows.
 bool mfma_supported(const AttnArgs& a, bool bwd);
 void launch_fwd_mfma(const AttnArgs& a, hipStream_t stream);
 void launch_bwd_mfma(const AttnArgs& a, hipStream_t stream);
+void launch_qkv_fwd_mfma(const AttnArgs& a, hipStream_t stream);  // fused QKV + attention + token fc_o
 extern int g_bwd_grid_cap;  // workgroups of the backward kernel when it also reduces the bias gradient
 
 }  // namespace attn

@@ -280,6 +280,161 @@ __global__ void __launch_bounds__(256) k_attn16_fwd(AttnArgs a) {
   }
 }
 
+
+// Fused QKV projection + attention + per-token fc_o (the harness forward, fc_o_mode "token"):
+// one wave per sequence (S <= 16 tokens), looping over the Hl local heads.  Per head the
+// workgroup stages that head's rows of the folded QKV weight (3 D rows x kq <= 96 columns,
+// bf16) in LDS; each wave forms its sequence's q | k | v = X W_h^T + b on the MFMA (X = the
+// sequence's patch rows, the A operand read straight from global memory, zero past kq),
+// rounds them to bf16 into its LDS tile (the values the unfused QKV GEMM would store), runs
+// the attention of k_attn16_fwd on them, and adds this head's share of z = O W_o^T to one
+// MFMA accumulator chained over the heads (heads summed in head order).  The qkv tensor's
+// write + read (2 x B*S x 3 Hl D x 2 B) and the QKV GEMM launch disappear; qkv is stored only
+// when a backward needs it (qkv_out).  z rows go to ztok or, pushed, to the TP owners' inbox
+// slots (zrows), as in k_attn16_fwd.
+template <int D>
+__global__ void __launch_bounds__(256) k_qkv_attn16_fwd(AttnArgs a) {
+  constexpr int NK = D / 32, NT = D / 16;
+  constexpr int KQ = 96;           // projection depth: kq <= 96 columns, 3 MFMA k-steps
+  constexpr int LDW = KQ + 8;      // staged W row (bf16)
+  constexpr int LDT = 3 * D + 8;   // per-wave q | k | v tile row (bf16)
+  extern __shared__ __attribute__((aligned(16))) uint16_t sm[];
+  uint16_t* W = sm;  // [3 D][LDW]
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
+  uint16_t* T = sm + 3 * D * LDW + wave * 16 * LDT;  // [16][LDT]
+  const int S = a.S, HD = a.Hl * D;
+  const int stride = gridDim.x * WPB;
+  for (int base = blockIdx.x * WPB; base < a.B; base += stride) {  // workgroup-uniform trip count
+    const int b = base + wave;
+    const bool live = b < a.B;
+    bf16x8 xr[3];  // patch rows: lane (c, g) holds token c, columns 32 kk + 8 g .. +7
+#pragma unroll
+    for (int kk = 0; kk < 3; ++kk) {
+      const int col = 32 * kk + 8 * g;
+      xr[kk] = ld_row16(a.xq + (size_t)(live ? b * S + c : 0) * a.ld_xq + col, live && c < S && col < a.kq);
+    }
+    f4 zt = {0.f, 0.f, 0.f, 0.f};
+    for (int h = 0; h < a.Hl; ++h) {
+      __syncthreads();  // every wave is done with the previous head's W tile
+      for (int q = threadIdx.x; q < 3 * D * (KQ / 8); q += blockDim.x) {
+        const int row = q / (KQ / 8), col = (q % (KQ / 8)) * 8, sel = row / D, f = row % D;
+        uint4 v = {0u, 0u, 0u, 0u};
+        if (col < a.kq) v = *reinterpret_cast<const uint4*>(a.wq + (size_t)(sel * HD + h * D + f) * a.ld_wq + col);
+        *reinterpret_cast<uint4*>(W + row * LDW + col) = v;
+      }
+      __syncthreads();
+      if (!live) continue;
+      // q | k | v of head h: acc[r] = out[token 4 g + r][feature 16 nt + c] (+ bias, bf16)
+#pragma unroll
+      for (int sel = 0; sel < 3; ++sel)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+          f4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int kk = 0; kk < 3; ++kk)
+            acc = mma32(xr[kk], *reinterpret_cast<const bf16x8*>(W + (sel * D + 16 * nt + c) * LDW + 32 * kk + 8 * g),
+                        acc);
+          const float bias = a.bq[sel * HD + h * D + 16 * nt + c];
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            T[(4 * g + r) * LDT + sel * D + 16 * nt + c] = (uint16_t)f32_to_bf16_bits(acc[r] + bias);
+        }
+      __builtin_amdgcn_wave_barrier();
+      if (a.qkv_out) {  // the projection for a backward: rows < S, 16-B vectors
+        for (int p = lane; p < 16 * 3 * (D / 8); p += 64) {
+          const int row = p / (3 * (D / 8)), rem = p % (3 * (D / 8)), sel = rem / (D / 8), ch = rem % (D / 8);
+          if (row < S)
+            *reinterpret_cast<uint4*>(a.qkv_out + (size_t)(b * S + row) * a.ld_qkv + sel * HD + h * D + ch * 8) =
+                *reinterpret_cast<const uint4*>(T + row * LDT + sel * D + ch * 8);
+        }
+      }
+      bf16x8 qr[NK], kr[NK];
+#pragma unroll
+      for (int kk = 0; kk < NK; ++kk) {
+        qr[kk] = *reinterpret_cast<const bf16x8*>(T + c * LDT + 32 * kk + 8 * g);
+        kr[kk] = *reinterpret_cast<const bf16x8*>(T + c * LDT + D + 32 * kk + 8 * g);
+      }
+      f4 st = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < NK; ++kk) st = mma32(kr[kk], qr[kk], st);  // S^T[j = 4g + r][i = c]
+      float x[4], m = -INFINITY;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        x[r] = (4 * g + r < S) ? st[r] * a.scale : -INFINITY;
+        m = fmaxf(m, x[r]);
+      }
+      m = fmaxf(m, __shfl_xor(m, 16));
+      m = fmaxf(m, __shfl_xor(m, 32));
+      float e[4], ssum = 0.f;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        e[r] = __expf(x[r] - m);
+        ssum += e[r];
+      }
+      ssum += __shfl_xor(ssum, 16);
+      ssum += __shfl_xor(ssum, 32);
+      const float inv = 1.f / ssum;
+      const int pr = b * a.Hl + h;
+      if (g == 0 && c < S) a.lse[(size_t)pr * S + c] = m + __logf(ssum);
+      const s4 pa = pack4(e[0] * inv, e[1] * inv, e[2] * inv, e[3] * inv);
+      f4 o[NT];
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) o[nt] = mma16(pa, tile_b<LDT>(T + 2 * D, g, 16 * nt + c), f4{0.f, 0.f, 0.f, 0.f});
+      if (a.pool) {
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+          float cs = 0.f;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) cs += (4 * g + r < S) ? o[nt][r] : 0.f;
+          cs += __shfl_xor(cs, 16);
+          cs += __shfl_xor(cs, 32);
+          if (g == 0) a.pool[(size_t)b * a.ld_pool + h * D + 16 * nt + c] = (uint16_t)f32_to_bf16_bits(cs / (float)S);
+        }
+      }
+      // z += bf16(O_h) W_o,h^T: O staged over the tile's (dead) q columns, the A operand
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) T[(4 * g + r) * LDT + 16 * nt + c] = (uint16_t)f32_to_bf16_bits(o[nt][r]);
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int kk = 0; kk < NK; ++kk) {
+        const bf16x8 wb = ld_row16(a.wo + (size_t)c * a.ld_wo + h * D + 32 * kk + 8 * g, c < a.n_out);
+        zt = mma32(*reinterpret_cast<const bf16x8*>(T + c * LDT + 32 * kk + 8 * g), wb, zt);  // z[4g + r][c]
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+    if (live) {
+      // + the bias, then whole 64-B rows: stage z as fp32 [16][16] in the tile
+      float* Z = reinterpret_cast<float*>(T);
+      const float bo = (a.bo && c < a.n_out) ? a.bo[c] : 0.f;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) Z[(4 * g + r) * 16 + c] = zt[r] + bo;
+      __builtin_amdgcn_wave_barrier();
+      const int i = lane >> 2, q = (lane & 3) * 4;
+      const u32x4 pk = *reinterpret_cast<const u32x4*>(Z + i * 16 + q);
+      const size_t row0 = (size_t)b * S;
+      if (i < S) {
+        if (a.zrows) {
+          const int j = __builtin_amdgcn_readfirstlane((int)(row0 / a.zrows));
+          char* seq = reinterpret_cast<char*>(a.zpush[j] + (row0 - (size_t)j * a.zrows) * a.ld_zt);
+          const Rsrc rs = make_rsrc(uniform_ptr(seq), (uint32_t)(S * a.ld_zt * 4));
+          __builtin_amdgcn_raw_buffer_store_b128(pk, rs.r, (uint32_t)((i * a.ld_zt + q) * 4), 0, kStorePolicy);
+        } else {
+          *reinterpret_cast<u32x4*>(a.ztok + (row0 + i) * a.ld_zt + q) = pk;
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+  }
+}
+
+template <int D>
+constexpr size_t qkv_fwd_lds_bytes() {
+  return (size_t)(3 * D * (96 + 8) + WPB * 16 * (3 * D + 8)) * sizeof(uint16_t);
+}
+
 template <int D>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D == 128 ? 2 : 4))) k_attn16_bwd(AttnArgs a) {
   constexpr int LD = D + 8, NK = D / 32, NT = D / 16, TILE = 16 * LD;
@@ -457,6 +612,26 @@ void launch_fwd_mfma(const AttnArgs& a, hipStream_t stream) {
   if (a.D == 32) hipLaunchKernelGGL(k_attn16_fwd<32>, dim3(grid), dim3(256), 0, stream, a);
   else if (a.D == 64) hipLaunchKernelGGL(k_attn16_fwd<64>, dim3(grid), dim3(256), 0, stream, a);
   else hipLaunchKernelGGL(k_attn16_fwd<128>, dim3(grid), dim3(256), 0, stream, a);
+}
+
+void launch_qkv_fwd_mfma(const AttnArgs& a, hipStream_t stream) {
+  const int grid = grid_for(a.B, 4096);
+  auto go = [&](const void* k, size_t lds) {
+    (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  };
+  if (a.D == 32) {
+    static bool attr = (go(reinterpret_cast<const void*>(k_qkv_attn16_fwd<32>), qkv_fwd_lds_bytes<32>()), true);
+    (void)attr;
+    hipLaunchKernelGGL(k_qkv_attn16_fwd<32>, dim3(grid), dim3(256), qkv_fwd_lds_bytes<32>(), stream, a);
+  } else if (a.D == 64) {
+    static bool attr = (go(reinterpret_cast<const void*>(k_qkv_attn16_fwd<64>), qkv_fwd_lds_bytes<64>()), true);
+    (void)attr;
+    hipLaunchKernelGGL(k_qkv_attn16_fwd<64>, dim3(grid), dim3(256), qkv_fwd_lds_bytes<64>(), stream, a);
+  } else {
+    static bool attr = (go(reinterpret_cast<const void*>(k_qkv_attn16_fwd<128>), qkv_fwd_lds_bytes<128>()), true);
+    (void)attr;
+    hipLaunchKernelGGL(k_qkv_attn16_fwd<128>, dim3(grid), dim3(256), qkv_fwd_lds_bytes<128>(), stream, a);
+  }
 }
 
 int g_bwd_grid_cap = 0;  // tuning knob (attn_set_bwd_grid); 0 = 256 workgroups per head (measured best)

@@ -277,6 +277,42 @@ void attn_fwd(uint64_t qkv, uint64_t o, uint64_t lse, int B, int S, int Hl, int 
   CCMPI_HIP_CHECK(hipGetLastError());
 }
 
+// Fused QKV projection + attention + per-token fc_o (attn_mfma.hip k_qkv_attn16_fwd): the
+// harness forward's QKV GEMM, attention and fc_o in one kernel.
+void attn_qkv_fwd(uint64_t xq, int ld_xq, int kq, uint64_t wq, int ld_wq, uint64_t bq, uint64_t qkv_out, int ld_qkv,
+                  uint64_t lse, int B, int S, int Hl, int D, float scale, uint64_t pool, int ld_pool, uint64_t wo,
+                  int ld_wo, int n_out, uint64_t bo, uint64_t ztok, int ld_zt, int zrows,
+                  const std::vector<uint64_t>& zpush, uint64_t stream) {
+  if (S < 1 || S > 16 || !(D == 32 || D == 64 || D == 128) || Hl < 1 || kq < 8 || kq > 96 || kq % 8 || ld_xq % 8 ||
+      ld_wq % 8 || ld_wo % 8 || (xq % 16) || (wq % 16) || (wo % 16) || !wo || !bq || !lse || n_out < 1 || n_out > 16 ||
+      ld_zt < 16 || ld_zt % 4 || (ztok % 16) || (!ztok && !zrows) || (qkv_out && (ld_qkv % 8 || qkv_out % 16)) ||
+      false)
+    throw std::invalid_argument("attention: fused QKV forward needs S <= 16, D in {32, 64, 128}, kq % 8 == 0 and "
+                                "<= 96, 16-B aligned rows, n_out <= 16, z rows of >= 16 floats (% 4), a z target");
+  AttnArgs a{};
+  a.lse = (float*)lse;
+  a.B = B; a.S = S; a.Hl = Hl; a.D = D; a.ld_qkv = ld_qkv; a.scale = scale;
+  a.pool = (uint16_t*)pool; a.ld_pool = ld_pool;
+  a.wo = (const uint16_t*)wo; a.ld_wo = ld_wo; a.n_out = n_out; a.bo = (const float*)bo;
+  a.xq = (const uint16_t*)xq; a.ld_xq = ld_xq; a.kq = kq;
+  a.wq = (const uint16_t*)wq; a.ld_wq = ld_wq; a.bq = (const float*)bq; a.qkv_out = (uint16_t*)qkv_out;
+  a.ztok = (float*)ztok; a.ld_zt = ld_zt; a.zrows = zrows;
+  if (zrows) {
+    const int64_t M = (int64_t)B * S;
+    const int64_t blocks = M / zrows;
+    if (zrows % S || M % zrows || blocks < 1 || blocks > 16 || (int64_t)zpush.size() != blocks)
+      throw std::invalid_argument("attention: push fc_o needs whole sequences per block (zrows % S == 0), "
+                                  "B*S = blocks x zrows and one target per block (<= 16)");
+    for (int64_t j = 0; j < blocks; ++j) {
+      if (!zpush[j] || zpush[j] % 16) throw std::invalid_argument("attention: push fc_o targets must be 16-B aligned");
+      a.zpush[j] = reinterpret_cast<float*>(zpush[j]);
+    }
+  }
+  if (B == 0) return;
+  attn::launch_qkv_fwd_mfma(a, (hipStream_t)stream);
+  CCMPI_HIP_CHECK(hipGetLastError());
+}
+
 void attn_bwd(uint64_t qkv, uint64_t o, uint64_t lse, uint64_t dout, uint64_t dqkv, uint64_t dbias, int B, int S,
               int Hl, int D, int ld_qkv, int ld_o, float scale, int dout_bstride, int dout_rstride, uint64_t stream,
               uint64_t dz, int ld_dz, uint64_t wo, int ld_wo, int n_out, float dz_scale) {
@@ -520,6 +556,11 @@ void register_attn_ops(pybind11::module_& m) {
         py::arg("ld_pool"), py::arg("stream"), py::arg("wo") = 0, py::arg("ld_wo") = 0, py::arg("n_out") = 0,
         py::arg("zp") = 0, py::arg("ld_zp") = 0, py::arg("bo") = 0, py::arg("ztok") = 0, py::arg("ld_zt") = 16,
         py::arg("zrows") = 0, py::arg("zpush") = std::vector<uint64_t>{}, py::call_guard<py::gil_scoped_release>());
+  m.def("attn_qkv_fwd", &attn_qkv_fwd, py::arg("xq"), py::arg("ld_xq"), py::arg("kq"), py::arg("wq"), py::arg("ld_wq"),
+        py::arg("bq"), py::arg("qkv_out"), py::arg("ld_qkv"), py::arg("lse"), py::arg("B"), py::arg("S"), py::arg("Hl"),
+        py::arg("D"), py::arg("scale"), py::arg("pool"), py::arg("ld_pool"), py::arg("wo"), py::arg("ld_wo"),
+        py::arg("n_out"), py::arg("bo"), py::arg("ztok"), py::arg("ld_zt"), py::arg("zrows"), py::arg("zpush"),
+        py::arg("stream"), py::call_guard<py::gil_scoped_release>());
   m.def("attn_small_bwd", &attn_bwd, py::arg("qkv"), py::arg("o"), py::arg("lse"), py::arg("dout"), py::arg("dqkv"),
         py::arg("dbias"), py::arg("B"), py::arg("S"), py::arg("Hl"), py::arg("D"), py::arg("ld_qkv"), py::arg("ld_o"),
         py::arg("scale"), py::arg("dout_bstride"), py::arg("dout_rstride"), py::arg("stream"), py::arg("dz") = 0,

@@ -118,6 +118,9 @@ class LayerConfig:
     # * "auto" (default; CCMPI_TP_FC_O_FORM overrides): "push" when every TP rank owns its
     #   GPU, "plain" when the ranks share one (the pushes then only compete for the same HBM).
     tp_fc_o_form: str = ""
+    # token mode: the QKV projection inside the attention kernel (k_qkv_attn16_fwd) -- the
+    # B*S x 3hd qkv tensor is neither written (inference) nor read back, and the QKV GEMM goes
+    fuse_qkv: bool = True
     @property
     def seq(self) -> int:
         return (self.img // self.patch) ** 2
@@ -300,10 +303,13 @@ class MnistTPLayer:
         fused = hx is not None and xp.data_ptr() == hx.data_ptr() + 2 * d and xp.stride(0) == hx.stride(0)
         qkv = self._buf("qkv", (M, 3 * self.hd), torch.bfloat16)
         h = None
+        fuse_qkv = self._fuses_qkv(B)
         if self._folds():
             if images is not None:
                 patchify(images, cfg, out=xp)
-            gemm_nt(xp, weff if weff is not None else self.folded_qkv_weight(), out=qkv, bias=self.flat.param("qkv_b"))
+            weff = weff if weff is not None else self.folded_qkv_weight()
+            if not fuse_qkv:
+                gemm_nt(xp, weff, out=qkv, bias=self.flat.param("qkv_b"))
             images = None
         else:
             h = hx[:, :d] if fused else self._buf("h", (M, d), torch.bfloat16)
@@ -349,7 +355,10 @@ class MnistTPLayer:
         tok_kernel = token and tok_fused and mfma_attn and not pipelined
         if tok_kernel:
             att = None  # the attention kernel forms z itself; O is never stored
-            self._token_fc_o_kernel(qkv, lse, pool, B, st)
+            # fused QKV: the kernel also forms q | k | v from the patch rows (stored to qkv only
+            # when a backward will read it)
+            self._token_fc_o_kernel(qkv, lse, pool, B, st,
+                                    qkv_from=(xp, weff, save) if fuse_qkv else None)
         elif not pipelined:
             D.attn_small_fwd(qkv.data_ptr(), 0 if att is None else att.data_ptr(), lse.data_ptr(), B, S,
                              self.hl, cfg.head_dim, qkv.stride(0), self.hd if att is None else att.stride(0),
@@ -461,7 +470,16 @@ class MnistTPLayer:
             form = "plain"  # push needs whole sequences per TP rank's row block
         return form
 
-    def _token_fc_o_kernel(self, qkv, lse, pool, B: int, st: int) -> None:
+    def _fuses_qkv(self, B: int) -> bool:
+        """The token-mode forward runs the QKV projection inside the attention kernel
+        (``k_qkv_attn16_fwd``): folded weights, the fused per-token fc_o, kp <= 96
+        (CCMPI_FUSE_QKV=0: the QKV GEMM + attention kernel instead)."""
+        cfg = self.cfg
+        return (cfg.fuse_qkv and os.environ.get("CCMPI_FUSE_QKV", "1") != "0" and self._folds()
+                and cfg.fc_o_mode == "token" and self._fused_fc_o_bwd() and self._token_chunks(B) == 1
+                and cfg.seq <= 16 and cfg.head_dim in (32, 64, 128) and cfg.kp <= 96)
+
+    def _token_fc_o_kernel(self, qkv, lse, pool, B: int, st: int, qkv_from=None) -> None:
         """Attention + per-token row-parallel fc_o in ONE kernel (``k_attn16_fwd``), then the
         TP sum of z (B*S x 16 fp32, o_b added by TP rank 0): an all-reduce ("plain"), or the
         kernel pushes every row block into its owner's inbox and the inbox-to-local two-shot
@@ -477,6 +495,17 @@ class MnistTPLayer:
                   bo=self.flat.param("o_b").data_ptr() if self.tp_idx == 0 else 0)
         args = (qkv.data_ptr(), 0, lse.data_ptr(), B, S, self.hl, cfg.head_dim, qkv.stride(0), self.hd,
                 1.0 / math.sqrt(cfg.head_dim), pool.data_ptr(), pool.stride(0))  # pool: dW_o in backward
+        fwd = D.attn_small_fwd
+        if qkv_from is not None:
+            xp, weff, keep = qkv_from
+            bq = self.flat.param("qkv_b")
+
+            def fwd(*_a, zrows=0, zpush=(), ztok=0, ld_zt=16, wo=0, ld_wo=0, n_out=0, bo=0):
+                stream = _a[-1]
+                D.attn_qkv_fwd(xp.data_ptr(), xp.stride(0), cfg.kp, weff.data_ptr(), weff.stride(0), bq.data_ptr(),
+                               qkv.data_ptr() if keep else 0, qkv.stride(0), lse.data_ptr(), B, S, self.hl,
+                               cfg.head_dim, 1.0 / math.sqrt(cfg.head_dim), pool.data_ptr(), pool.stride(0), wo, ld_wo,
+                               n_out, bo, ztok, ld_zt, zrows, list(zpush), stream)
         form = self.tp_fc_o_form(B)
         if form == "push":
             inbox = self._buf("ztok_inbox", (M, cfg.out_pad), torch.float32, self.tp_dev)
@@ -484,11 +513,11 @@ class MnistTPLayer:
             if key not in self._bufs:  # peer-mapped slot addresses: resolved once, no host call after
                 self._bufs[key] = self.tp_dev.dc.push_targets(inbox.data_ptr(), inbox.numel() * 4)
             s = self.tp_dev._stream()
-            D.attn_small_fwd(*args, s, zrows=M // cfg.tp, zpush=self._bufs[key], **kw)
+            fwd(*args, s, zrows=M // cfg.tp, zpush=self._bufs[key], **kw)
             self.tp_dev.dc.inbox_to_local(inbox.data_ptr(), z.data_ptr(), inbox.numel() * 4, 10, s,
                                           self.tp_dev._budget(None))
         else:
-            D.attn_small_fwd(*args, st, ztok=z.data_ptr(), **kw)
+            fwd(*args, st, ztok=z.data_ptr(), **kw)
             if self.tp_dev is not None:
                 self.tp_dev.allreduce(z, z, "SUM", symmetric=True)  # z: heap block (_buf), same on every rank
         self._zt = z

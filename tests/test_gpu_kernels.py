@@ -467,6 +467,55 @@ def test_attn_token_fc_o(B, S, H, D, n_out):
                            pool.data_ptr(), pool.stride(0), st, zrows=S + 1, zpush=[tg.data_ptr()], **kw)
 
 
+@pytest.mark.parametrize("B,S,H,D,kp", [(2048, 16, 4, 64, 72), (2048, 16, 2, 64, 72), (37, 16, 1, 128, 96),
+                                        (9, 7, 2, 32, 40), (5, 16, 4, 64, 8)])
+def test_attn_qkv_fused(B, S, H, D, kp):
+    """QKV projection + attention + per-token fc_o in one kernel (the harness forward):
+    q | k | v = bf16(X W^T + b) against torch fp32 (stored when asked), then lse, pool and z
+    against the unfused attention kernel run on that qkv; the push form bitwise equal."""
+    from collective_communication_mpi_amd import _native
+
+    dev = _native.device()
+    st = torch.cuda.current_stream().cuda_stream
+    g = torch.Generator(device="cuda").manual_seed(B * 13 + H * 5 + kp)
+    HD = H * D
+    xp = (torch.randn(B * S, kp, device="cuda", generator=g) * 0.5).bfloat16()
+    w = (torch.randn(3 * HD, kp, device="cuda", generator=g) / kp ** 0.5).bfloat16()
+    bq = torch.randn(3 * HD, device="cuda", generator=g) * 0.1
+    wo = torch.zeros(16, HD, device="cuda").bfloat16()
+    wo[:10] = (torch.randn(10, HD, device="cuda", generator=g) * 0.1).bfloat16()
+    bo = torch.zeros(16, device="cuda")
+    bo[:10] = torch.randn(10, device="cuda", generator=g)
+    qkv = torch.full((B * S, 3 * HD), float("nan"), device="cuda").bfloat16()
+    lse = torch.empty(B * H, S, device="cuda")
+    pool = torch.empty(B, HD, device="cuda", dtype=torch.bfloat16)
+    z = torch.full((B * S, 16), float("nan"), device="cuda")
+    common = dict(lse=lse.data_ptr(), B=B, S=S, Hl=H, D=D, scale=D ** -0.5, pool=pool.data_ptr(), ld_pool=pool.stride(0),
+                  wo=wo.data_ptr(), ld_wo=wo.stride(0), n_out=16, bo=bo.data_ptr(), ld_zt=16, stream=st)
+    dev.attn_qkv_fwd(xq=xp.data_ptr(), ld_xq=xp.stride(0), kq=kp, wq=w.data_ptr(), ld_wq=w.stride(0), bq=bq.data_ptr(),
+                     qkv_out=qkv.data_ptr(), ld_qkv=qkv.stride(0), ztok=z.data_ptr(), zrows=0, zpush=[], **common)
+    ref_qkv = (xp.float() @ w.float().T + bq).bfloat16()
+    torch.testing.assert_close(qkv.float(), ref_qkv.float(), rtol=1e-2, atol=1e-2)
+    # the unfused kernel on the fused kernel's own qkv: same lse / pool, z up to fp32 summation order
+    lse2, pool2 = torch.empty_like(lse), torch.empty_like(pool)
+    z2 = torch.empty_like(z)
+    dev.attn_small_fwd(qkv.data_ptr(), 0, lse2.data_ptr(), B, S, H, D, qkv.stride(0), HD, D ** -0.5, pool2.data_ptr(),
+                       pool2.stride(0), st, wo=wo.data_ptr(), ld_wo=wo.stride(0), n_out=16, bo=bo.data_ptr(),
+                       ztok=z2.data_ptr(), ld_zt=16)
+    torch.testing.assert_close(lse, lse2, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(pool.float(), pool2.float(), rtol=1e-2, atol=1e-2)
+    torch.testing.assert_close(z, z2, rtol=1e-4, atol=1e-4)
+    # push form into per-block targets: bitwise the same rows; no qkv written (inference)
+    blocks = 2 if B % 2 == 0 else 1
+    tg = torch.full((blocks, B * S // blocks, 16), float("nan"), device="cuda")
+    qkv.fill_(float("nan"))
+    dev.attn_qkv_fwd(xq=xp.data_ptr(), ld_xq=xp.stride(0), kq=kp, wq=w.data_ptr(), ld_wq=w.stride(0), bq=bq.data_ptr(),
+                     qkv_out=0, ld_qkv=qkv.stride(0), ztok=0, zrows=B * S // blocks,
+                     zpush=[tg[j].data_ptr() for j in range(blocks)], **common)
+    torch.cuda.synchronize()
+    assert torch.equal(tg.view(B * S, 16), z) and torch.isnan(qkv.float()).all()
+
+
 @pytest.mark.parametrize("img,patch,misalign", [(28, 7, 0), (28, 7, 1), (24, 6, 0)])  # LDS / plain / runtime sizes
 def test_patchify_columns(img, patch, misalign):
     from collective_communication_mpi_amd.models.mnist_tp import LayerConfig, patchify
