@@ -44,7 +44,7 @@ struct AttnArgs {
   int zrows;
   float* zpush[16];
   // Fused QKV projection (k_qkv_attn16_fwd, the harness forward): qkv = X W^T + b computed in
-  // the attention kernel from the patch rows X ([B*S][ld_xq] bf16, kq <= 96 columns) and the
+  // the attention kernel from the patch rows X ([B*S][ld_xq] bf16, kq <= 80 columns) and the
   // folded weight W ([3 Hl D][ld_wq] bf16: q rows, then k, then v) with the fp32 bias bq;
   // qkv_out (optional, [B*S][ld_qkv] bf16): the projection is also stored, for a backward
   const uint16_t* xq;
@@ -53,6 +53,11 @@ struct AttnArgs {
   int ld_wq;
   const float* bq;
   uint16_t* qkv_out;
+  // img (optional, [B][28 * 28] fp32 MNIST images): the kernel builds X itself (7 x 7 patch
+  // pixels, a 1, the one-hot position -- k_patchify's rows, bitwise) and, with xq_out, stores
+  // them ([B*S][ld_xq] bf16) for the backward; xq is then unused
+  const float* img;
+  uint16_t* xq_out;
 };
 
 // MFMA path (attn_mfma.hip): S <= 16, D in {32, 64, 128}, 16-B aligned rows.

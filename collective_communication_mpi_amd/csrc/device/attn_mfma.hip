@@ -96,16 +96,51 @@ __device__ __forceinline__ void put_rows(uint16_t* T, const bf16x8 (&x)[D / 32],
   for (int kk = 0; kk < D / 32; ++kk) *reinterpret_cast<bf16x8*>(T + c * LD + 32 * kk + 8 * g) = x[kk];
 }
 
-template <int D>
-__global__ void __launch_bounds__(256) k_attn16_fwd(AttnArgs a) {
+__device__ __forceinline__ s4 ld_s4(const uint16_t* p, bool ok) {
+  const uint2 z = ok ? *reinterpret_cast<const uint2*>(p) : uint2{0, 0};
+  return __builtin_bit_cast(s4, z);
+}
+
+// copy the rows < S of a per-wave [16][LD] bf16 tile to global memory as 16-B vectors
+template <int D, int LD>
+__device__ __forceinline__ void rows_out(const uint16_t* T, uint16_t* dst, int ld, int S, int lane) {
+#pragma unroll
+  for (int t = 0; t < (16 * D / 8) / 64; ++t) {
+    const int p = lane + 64 * t, row = p / (D / 8), col = (p % (D / 8)) * 8;
+    if (row < S) *reinterpret_cast<uint4*>(dst + (size_t)row * ld + col) = *reinterpret_cast<const uint4*>(T + row * LD + col);
+  }
+}
+
+// The forward body.  QKV = false: q, k, v rows are read from the qkv buffer (k_attn16_fwd).
+// QKV = true (k_qkv_attn16_fwd, the harness forward with fc_o_mode "token"): the wave forms
+// its (sequence, head)'s q | k | v = X W_h^T + b itself on the MFMA from the sequence's patch
+// rows X (B*S x kq bf16, kq <= 80: two 16x16x32 k-steps + one 16x16x16 tail).  With Hl | WPB
+// a wave always serves head h = wave % Hl, so W_h's 3 D x kq operand fragments (120 VGPRs at
+// D = 64) are loaded ONCE and stay in registers for the whole grid-stride loop
+// (workgroups are persistent: two per CU); each iteration loads only X (prefetched one
+// iteration ahead).  q and k are rounded to bf16 (the values the unfused QKV GEMM would store)
+// and turned into row fragments through the wave's O / V tiles, v lands in the V tile the PV
+// product reads; qkv is written only when a backward needs it (qkv_out).  The QKV GEMM's
+// launch, its 2 x B*S x 3 Hl D x 2 B of qkv write + read, and the old per-head W staging
+// (one wave per sequence, two workgroup barriers per head: 38.9 us vs 23.1 + 17.0 us
+// unfused) are gone.
+template <int D, bool QKV, bool IMG = false>
+__device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
   constexpr int LD = D + 8, NK = D / 32, NT = D / 16;
   __shared__ __attribute__((aligned(16))) uint16_t vt[WPB][16 * LD];
   __shared__ __attribute__((aligned(16))) uint16_t ot[WPB][16 * LD];
   __shared__ float zpart[2][WPB][16];  // fused fc_o: per-wave (= per-head) partial logits, double-buffered
   // per-token fused fc_o: per-wave (= per-head) z tiles [16 tokens][16 classes], double-buffered
   __shared__ float ztp[2][WPB][16 * 16];
+  // fused patchify: the WPB / Hl images of an iteration (consecutive in memory), double-buffered
+  // and padded to whole 1-KiB LDS-DMA pieces
+  constexpr int kImgPieces = (WPB * 784 * 4 + 1023) / 1024;
+  __shared__ __attribute__((aligned(16))) float imgs[IMG ? 2 : 1][IMG ? kImgPieces * 256 : 1];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
   const int S = a.S, HD = a.Hl * D, npairs = a.B * a.Hl;
+  // per-token fc_o: z rows stored (ztok), pushed (zrows), or -- fused QKV only -- reduced to
+  // their mean over the S tokens in-kernel (zp: the local TP = 1 form, z never stored)
+  const bool tok = a.ztok || a.zrows || (QKV && a.zp);
   uint16_t* V = vt[wave];
   uint16_t* O = ot[wave];
   // workgroup-uniform trip count (the fused fc_o reduces across the waves of an iteration);
@@ -113,7 +148,7 @@ __global__ void __launch_bounds__(256) k_attn16_fwd(AttnArgs a) {
   // fused fc_o: with Hl | WPB this wave always serves head h = wave % Hl, so its W_o
   // entries (classes 4g..4g+3, features 16nt + c) are loaded once, packed as bf16 pairs
   uint32_t wpk[NT][2];
-  if (a.zp) {
+  if (!QKV && a.zp) {
     const int hw = wave % a.Hl;
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt)
@@ -129,20 +164,158 @@ __global__ void __launch_bounds__(256) k_attn16_fwd(AttnArgs a) {
   // per-token fused fc_o: B operand of z = O . W_o^T -- lane (c, g) holds class c, this
   // wave's head features 32kk + 8g .. +7 (loaded once; classes >= n_out read as zero)
   bf16x8 wb[NK];
-  if (a.ztok || a.zrows) {
+  if (tok) {
     const int hw = wave % a.Hl;
 #pragma unroll
     for (int kk = 0; kk < NK; ++kk)
       wb[kk] = ld_row16(a.wo + (size_t)c * a.ld_wo + hw * D + 32 * kk + 8 * g, c < a.n_out);
   }
   const int stride = gridDim.x * WPB;
-  int it = 0;
+  // fused QKV: W_h's rows as B operands (lane (c, g): feature 16 nt + c of q | k | v, depth
+  // 32 kk + 8 g .. +7, tail 64 + 4 g .. +3; zero past kq) and the bias, loaded once
+  constexpr int WS = QKV ? 3 : 1, WN = QKV ? NT : 1;
+  bf16x8 wf[WS][WN][2];
+  s4 wtl[WS][WN];
+  int it = 0;    // iteration parity: double-buffered LDS (z tiles, images)
+  bf16x8 xn[2];  // the next iteration's patch rows (lane (c, g): token c, depth 32 kk + 8 g ..)
+  s4 xtn;
+  auto load_x = [&](int p) {
+    const bool ok = p < npairs && c < S;
+    if constexpr (IMG) {
+      // MNIST 28 x 28, 7 x 7 patches (S = 16): token c = patch (c / 4, c % 4); column cc < 49
+      // is pixel (cc / 7, cc % 7) of the patch, 49 the bias 1, 50 + c the position one-hot.
+      // The image is this iteration's LDS copy (staged one iteration ahead by LDS-DMA).
+      const float* im = imgs[it] + (wave / a.Hl) * 784 + (c >> 2) * 196 + (c & 3) * 7;
+      // the 20 per-lane pixel offsets are loop-invariant: hide g from the optimizer so they are
+      // recomputed per call rather than hoisted into 20 live registers (which spilled)
+      int g = lane >> 4;
+      asm volatile("" : "+v"(g));
+      auto px = [&](int cc) -> uint32_t {
+        float v = 0.f;
+        if (ok) {
+          if (cc < 49) v = im[(cc / 7) * 28 + cc % 7];
+          else if (cc == 49 || cc == 50 + c) v = 1.f;
+        }
+        return f32_to_bf16_bits(v);
+      };
+      u32x4 w0, w1;
+      uint2 wt;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        w0[q] = px(8 * g + 2 * q) | (px(8 * g + 2 * q + 1) << 16);
+        w1[q] = px(32 + 8 * g + 2 * q) | (px(32 + 8 * g + 2 * q + 1) << 16);
+      }
+      wt.x = px(64 + 4 * g) | (px(64 + 4 * g + 1) << 16);
+      wt.y = px(64 + 4 * g + 2) | (px(64 + 4 * g + 3) << 16);
+      xn[0] = __builtin_bit_cast(bf16x8, w0);
+      xn[1] = __builtin_bit_cast(bf16x8, w1);
+      xtn = __builtin_bit_cast(s4, wt);
+    } else {
+      const uint16_t* row = a.xq + (size_t)(ok ? (p / a.Hl) * S + c : 0) * a.ld_xq;
+      xn[0] = ld_row16(row + 8 * g, ok && 8 * g < a.kq);
+      xn[1] = ld_row16(row + 32 + 8 * g, ok && 32 + 8 * g < a.kq);
+      xtn = ld_s4(row + 64 + 4 * g, ok && 64 + 4 * g < a.kq);
+    }
+  };
+  // LDS-DMA of the images of the iteration starting at pair p0 into buffer buf: straight from
+  // global memory into LDS, no VGPRs held; bytes past the batch read as zero (buffer bounds)
+  auto stage_imgs = [&](int buf, int p0) {
+    if constexpr (IMG) {
+      const int nseq = WPB / a.Hl, pieces = (nseq * 784 * 4 + 1023) / 1024;
+      // (the descriptor starts at the iteration's first image: the bounds check covers
+      // voffset, so the batch end clips exactly)
+      const int b0 = p0 / a.Hl;
+      const Rsrc rs = make_rsrc(uniform_ptr(reinterpret_cast<char*>(const_cast<float*>(a.img + (size_t)b0 * 784))), (uint32_t)((size_t)(a.B - b0) * 784 * 4));
+      for (int pc = wave; pc < pieces; pc += WPB)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs.r, (__attribute__((address_space(3))) void*)(imgs[buf] + pc * 256),
+                                                 16, (pc * 64 + lane) * 16, 0, 0, 0);
+    }
+  };
+  if constexpr (QKV) {
+    const int hw = wave % a.Hl;
+#pragma unroll
+    for (int sel = 0; sel < 3; ++sel)
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        const int f = sel * HD + hw * D + 16 * nt + c;
+        const uint16_t* w = a.wq + (size_t)f * a.ld_wq;
+        wf[sel][nt][0] = ld_row16(w + 8 * g, 8 * g < a.kq);
+        wf[sel][nt][1] = ld_row16(w + 32 + 8 * g, 32 + 8 * g < a.kq);
+        wtl[sel][nt] = ld_s4(w + 64 + 4 * g, 64 + 4 * g < a.kq);
+      }
+    if constexpr (!IMG) load_x(blockIdx.x * WPB + wave);
+    if constexpr (IMG) {
+      stage_imgs(0, blockIdx.x * WPB);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+  }
   for (int base = blockIdx.x * WPB; base < npairs; base += stride, it ^= 1) {
    const int pr = base + wave;
+   bf16x8 xr[2];
+   s4 xt;
+   if constexpr (QKV) {
+    // (image mode builds this iteration's rows now, from LDS: the prefetch is the images' DMA)
+    if constexpr (IMG) load_x(pr);
+    xr[0] = xn[0];
+    xr[1] = xn[1];
+    xt = xtn;
+    if constexpr (!IMG) load_x(pr + stride);
+   }
    if (pr < npairs) {
     const int b = pr / a.Hl, h = pr % a.Hl;
     bf16x8 qr[NK], kr[NK];
-    {
+    if constexpr (QKV) {
+      // sel's [16 tokens][D] block of X W_h^T + b, rounded to bf16, into tile T.  The bias is
+      // re-read per iteration (L1 hits; an opaque pointer keeps the compiler from hoisting 12
+      // more loop-invariant registers)
+      const float* bqp = a.bq + h * D + c;
+      asm volatile("" : "+v"(bqp));
+      auto proj = [&](int sel, uint16_t* T) {
+        float bias[NT];
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) bias[nt] = bqp[sel * HD + 16 * nt];
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+          // (the 16x16x16 tail gets its own accumulator: chaining it onto the 16x16x32
+          // accumulator lost rows -- the compiler emits no wait states for that srcC hazard)
+          const f4 tl = mma16(xt, wtl[sel][nt], f4{0.f, 0.f, 0.f, 0.f});
+          f4 acc = mma32(xr[0], wf[sel][nt][0], f4{0.f, 0.f, 0.f, 0.f});
+          acc = mma32(xr[1], wf[sel][nt][1], acc);  // acc[r] = [token 4g + r][feature 16 nt + c]
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            T[(4 * g + r) * LD + 16 * nt + c] = (uint16_t)f32_to_bf16_bits(acc[r] + tl[r] + bias[nt]);
+        }
+      };
+      if (IMG && a.xq_out && h == 0 && c < S) {  // the patch rows, for the backward (one head's wave)
+        uint16_t* xo = a.xq_out + (size_t)(b * S + c) * a.ld_xq;
+        if (8 * g < a.kq) *reinterpret_cast<bf16x8*>(xo + 8 * g) = xr[0];
+        if (32 + 8 * g < a.kq) *reinterpret_cast<bf16x8*>(xo + 32 + 8 * g) = xr[1];
+        if (64 + 4 * g < a.kq) *reinterpret_cast<s4*>(xo + 64 + 4 * g) = xt;
+      }
+      proj(0, O);
+      proj(1, V);
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int kk = 0; kk < NK; ++kk) {
+        qr[kk] = *reinterpret_cast<const bf16x8*>(O + c * LD + 32 * kk + 8 * g);
+        kr[kk] = *reinterpret_cast<const bf16x8*>(V + c * LD + 32 * kk + 8 * g);
+      }
+      uint16_t* qo = a.qkv_out ? a.qkv_out + (size_t)b * S * a.ld_qkv + h * D : nullptr;
+      if (qo) {
+        rows_out<D, LD>(O, qo, a.ld_qkv, S, lane);
+        rows_out<D, LD>(V, qo + HD, a.ld_qkv, S, lane);
+      }
+      __builtin_amdgcn_wave_barrier();
+      proj(2, V);
+      // the next iteration's images, issued after this iteration's last global loads (the
+      // bias): vmcnt retires in order, so waiting on a later load would wait on the DMA too.
+      // (a wave with no pair now has no next iteration either, so every piece is issued)
+      if constexpr (IMG)
+        if (base + stride < npairs) stage_imgs(it ^ 1, base + stride);
+      __builtin_amdgcn_wave_barrier();
+      if (qo) rows_out<D, LD>(V, qo + 2 * HD, a.ld_qkv, S, lane);
+    } else {
       const uint16_t* qb = a.qkv + (size_t)b * S * a.ld_qkv + h * D;
       bf16x8 vr[NK];
 #pragma unroll
@@ -194,7 +367,7 @@ __global__ void __launch_bounds__(256) k_attn16_fwd(AttnArgs a) {
         cs += __shfl_xor(cs, 32);
         const uint32_t pb = f32_to_bf16_bits(cs / (float)S);
         if (g == 0) a.pool[(size_t)b * a.ld_pool + h * D + 16 * nt + c] = (uint16_t)pb;
-        if (a.zp) {
+        if (!QKV && a.zp) {
           const float pv = __uint_as_float(pb << 16);  // the bf16 value a separate fc_o GEMM would read
 #pragma unroll
           for (int q = 0; q < 2; ++q) {
@@ -203,7 +376,7 @@ __global__ void __launch_bounds__(256) k_attn16_fwd(AttnArgs a) {
           }
         }
       }
-      if (a.zp) {
+      if (!QKV && a.zp) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           float acc = zacc[j];
@@ -213,7 +386,7 @@ __global__ void __launch_bounds__(256) k_attn16_fwd(AttnArgs a) {
         }
       }
     }
-    if (a.ztok || a.zrows) {
+    if (tok) {
       // z[i][cls] over this head's features on the MFMA: A = bf16(O) rows (the values a
       // separate fc_o GEMM would read) from this wave's LDS tile, B = W_o in registers;
       // the accumulator holds z[i = 4g + r][cls = c]
@@ -231,11 +404,12 @@ __global__ void __launch_bounds__(256) k_attn16_fwd(AttnArgs a) {
     }
     if (a.o) store_tile<D, LD>(O, o, 1.f, a.o + (size_t)b * S * a.ld_o + h * D, a.ld_o, S, lane);
    }
-   if (a.ztok || a.zrows) {
+   if (tok) {
     // the Hl heads of each sequence of this iteration (consecutive waves, Hl | WPB), summed in
     // head order, + the bias.  Wave s writes sequence s (waves s >= WPB / Hl idle): lane l =
     // (token l >> 2, classes 4 (l & 3) .. +3), one 16-B store per lane, a sequence's S x 16
     // fp32 rows as whole lines
+    if constexpr (IMG) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next images have landed
     __syncthreads();  // (the next iteration writes the other buffer)
     const int i = lane >> 2, q = (lane & 3) * 4, w = wave * a.Hl;
     const int prw = base + w;
@@ -261,13 +435,26 @@ __global__ void __launch_bounds__(256) k_attn16_fwd(AttnArgs a) {
           char* seq = reinterpret_cast<char*>(a.zpush[j] + (row0 - (size_t)j * a.zrows) * a.ld_zt);
           const Rsrc rs = make_rsrc(uniform_ptr(seq), (uint32_t)(S * a.ld_zt * 4));
           __builtin_amdgcn_raw_buffer_store_b128(pk, rs.r, (uint32_t)((i * a.ld_zt + q) * 4), 0, kStorePolicy);
-        } else {
+        } else if (a.ztok) {
           *reinterpret_cast<u32x4*>(a.ztok + (row0 + i) * a.ld_zt + q) = pk;
+        }
+      }
+      if (QKV && a.zp) {  // logits = mean over the S tokens (lanes 4 i + (q / 4))
+        float m[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          m[r] = i < S ? v[r] : 0.f;
+#pragma unroll
+          for (int off = 4; off < 64; off <<= 1) m[r] += __shfl_xor(m[r], off);
+        }
+        if (i == 0) {
+          const float n = (float)S;
+          *reinterpret_cast<float4*>(a.zp + (size_t)b * a.ld_zp + q) = float4{m[0] / n, m[1] / n, m[2] / n, m[3] / n};
         }
       }
     }
    }
-   if (a.zp) {  // sum the Hl heads of each sequence in rank order (deterministic) and add the bias
+   if (!QKV && a.zp) {  // sum the Hl heads of each sequence in rank order (deterministic) and add the bias
     __syncthreads();  // (the next iteration writes the other buffer: one barrier per iteration)
     const int t = threadIdx.x, w = t >> 4, cls = t & 15, prw = base + w;
     if (t < WPB * 16 && prw < npairs && prw % a.Hl == 0 && cls < a.n_out) {
@@ -281,158 +468,15 @@ __global__ void __launch_bounds__(256) k_attn16_fwd(AttnArgs a) {
 }
 
 
-// Fused QKV projection + attention + per-token fc_o (the harness forward, fc_o_mode "token"):
-// one wave per sequence (S <= 16 tokens), looping over the Hl local heads.  Per head the
-// workgroup stages that head's rows of the folded QKV weight (3 D rows x kq <= 96 columns,
-// bf16) in LDS; each wave forms its sequence's q | k | v = X W_h^T + b on the MFMA (X = the
-// sequence's patch rows, the A operand read straight from global memory, zero past kq),
-// rounds them to bf16 into its LDS tile (the values the unfused QKV GEMM would store), runs
-// the attention of k_attn16_fwd on them, and adds this head's share of z = O W_o^T to one
-// MFMA accumulator chained over the heads (heads summed in head order).  The qkv tensor's
-// write + read (2 x B*S x 3 Hl D x 2 B) and the QKV GEMM launch disappear; qkv is stored only
-// when a backward needs it (qkv_out).  z rows go to ztok or, pushed, to the TP owners' inbox
-// slots (zrows), as in k_attn16_fwd.
 template <int D>
-__global__ void __launch_bounds__(256) k_qkv_attn16_fwd(AttnArgs a) {
-  constexpr int NK = D / 32, NT = D / 16;
-  constexpr int KQ = 96;           // projection depth: kq <= 96 columns, 3 MFMA k-steps
-  constexpr int LDW = KQ + 8;      // staged W row (bf16)
-  constexpr int LDT = 3 * D + 8;   // per-wave q | k | v tile row (bf16)
-  extern __shared__ __attribute__((aligned(16))) uint16_t sm[];
-  uint16_t* W = sm;  // [3 D][LDW]
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
-  uint16_t* T = sm + 3 * D * LDW + wave * 16 * LDT;  // [16][LDT]
-  const int S = a.S, HD = a.Hl * D;
-  const int stride = gridDim.x * WPB;
-  for (int base = blockIdx.x * WPB; base < a.B; base += stride) {  // workgroup-uniform trip count
-    const int b = base + wave;
-    const bool live = b < a.B;
-    bf16x8 xr[3];  // patch rows: lane (c, g) holds token c, columns 32 kk + 8 g .. +7
-#pragma unroll
-    for (int kk = 0; kk < 3; ++kk) {
-      const int col = 32 * kk + 8 * g;
-      xr[kk] = ld_row16(a.xq + (size_t)(live ? b * S + c : 0) * a.ld_xq + col, live && c < S && col < a.kq);
-    }
-    f4 zt = {0.f, 0.f, 0.f, 0.f};
-    for (int h = 0; h < a.Hl; ++h) {
-      __syncthreads();  // every wave is done with the previous head's W tile
-      for (int q = threadIdx.x; q < 3 * D * (KQ / 8); q += blockDim.x) {
-        const int row = q / (KQ / 8), col = (q % (KQ / 8)) * 8, sel = row / D, f = row % D;
-        uint4 v = {0u, 0u, 0u, 0u};
-        if (col < a.kq) v = *reinterpret_cast<const uint4*>(a.wq + (size_t)(sel * HD + h * D + f) * a.ld_wq + col);
-        *reinterpret_cast<uint4*>(W + row * LDW + col) = v;
-      }
-      __syncthreads();
-      if (!live) continue;
-      // q | k | v of head h: acc[r] = out[token 4 g + r][feature 16 nt + c] (+ bias, bf16)
-#pragma unroll
-      for (int sel = 0; sel < 3; ++sel)
-#pragma unroll
-        for (int nt = 0; nt < NT; ++nt) {
-          f4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-          for (int kk = 0; kk < 3; ++kk)
-            acc = mma32(xr[kk], *reinterpret_cast<const bf16x8*>(W + (sel * D + 16 * nt + c) * LDW + 32 * kk + 8 * g),
-                        acc);
-          const float bias = a.bq[sel * HD + h * D + 16 * nt + c];
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            T[(4 * g + r) * LDT + sel * D + 16 * nt + c] = (uint16_t)f32_to_bf16_bits(acc[r] + bias);
-        }
-      __builtin_amdgcn_wave_barrier();
-      if (a.qkv_out) {  // the projection for a backward: rows < S, 16-B vectors
-        for (int p = lane; p < 16 * 3 * (D / 8); p += 64) {
-          const int row = p / (3 * (D / 8)), rem = p % (3 * (D / 8)), sel = rem / (D / 8), ch = rem % (D / 8);
-          if (row < S)
-            *reinterpret_cast<uint4*>(a.qkv_out + (size_t)(b * S + row) * a.ld_qkv + sel * HD + h * D + ch * 8) =
-                *reinterpret_cast<const uint4*>(T + row * LDT + sel * D + ch * 8);
-        }
-      }
-      bf16x8 qr[NK], kr[NK];
-#pragma unroll
-      for (int kk = 0; kk < NK; ++kk) {
-        qr[kk] = *reinterpret_cast<const bf16x8*>(T + c * LDT + 32 * kk + 8 * g);
-        kr[kk] = *reinterpret_cast<const bf16x8*>(T + c * LDT + D + 32 * kk + 8 * g);
-      }
-      f4 st = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int kk = 0; kk < NK; ++kk) st = mma32(kr[kk], qr[kk], st);  // S^T[j = 4g + r][i = c]
-      float x[4], m = -INFINITY;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        x[r] = (4 * g + r < S) ? st[r] * a.scale : -INFINITY;
-        m = fmaxf(m, x[r]);
-      }
-      m = fmaxf(m, __shfl_xor(m, 16));
-      m = fmaxf(m, __shfl_xor(m, 32));
-      float e[4], ssum = 0.f;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        e[r] = __expf(x[r] - m);
-        ssum += e[r];
-      }
-      ssum += __shfl_xor(ssum, 16);
-      ssum += __shfl_xor(ssum, 32);
-      const float inv = 1.f / ssum;
-      const int pr = b * a.Hl + h;
-      if (g == 0 && c < S) a.lse[(size_t)pr * S + c] = m + __logf(ssum);
-      const s4 pa = pack4(e[0] * inv, e[1] * inv, e[2] * inv, e[3] * inv);
-      f4 o[NT];
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt) o[nt] = mma16(pa, tile_b<LDT>(T + 2 * D, g, 16 * nt + c), f4{0.f, 0.f, 0.f, 0.f});
-      if (a.pool) {
-#pragma unroll
-        for (int nt = 0; nt < NT; ++nt) {
-          float cs = 0.f;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) cs += (4 * g + r < S) ? o[nt][r] : 0.f;
-          cs += __shfl_xor(cs, 16);
-          cs += __shfl_xor(cs, 32);
-          if (g == 0) a.pool[(size_t)b * a.ld_pool + h * D + 16 * nt + c] = (uint16_t)f32_to_bf16_bits(cs / (float)S);
-        }
-      }
-      // z += bf16(O_h) W_o,h^T: O staged over the tile's (dead) q columns, the A operand
-      __builtin_amdgcn_wave_barrier();
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) T[(4 * g + r) * LDT + 16 * nt + c] = (uint16_t)f32_to_bf16_bits(o[nt][r]);
-      __builtin_amdgcn_wave_barrier();
-#pragma unroll
-      for (int kk = 0; kk < NK; ++kk) {
-        const bf16x8 wb = ld_row16(a.wo + (size_t)c * a.ld_wo + h * D + 32 * kk + 8 * g, c < a.n_out);
-        zt = mma32(*reinterpret_cast<const bf16x8*>(T + c * LDT + 32 * kk + 8 * g), wb, zt);  // z[4g + r][c]
-      }
-      __builtin_amdgcn_wave_barrier();
-    }
-    if (live) {
-      // + the bias, then whole 64-B rows: stage z as fp32 [16][16] in the tile
-      float* Z = reinterpret_cast<float*>(T);
-      const float bo = (a.bo && c < a.n_out) ? a.bo[c] : 0.f;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) Z[(4 * g + r) * 16 + c] = zt[r] + bo;
-      __builtin_amdgcn_wave_barrier();
-      const int i = lane >> 2, q = (lane & 3) * 4;
-      const u32x4 pk = *reinterpret_cast<const u32x4*>(Z + i * 16 + q);
-      const size_t row0 = (size_t)b * S;
-      if (i < S) {
-        if (a.zrows) {
-          const int j = __builtin_amdgcn_readfirstlane((int)(row0 / a.zrows));
-          char* seq = reinterpret_cast<char*>(a.zpush[j] + (row0 - (size_t)j * a.zrows) * a.ld_zt);
-          const Rsrc rs = make_rsrc(uniform_ptr(seq), (uint32_t)(S * a.ld_zt * 4));
-          __builtin_amdgcn_raw_buffer_store_b128(pk, rs.r, (uint32_t)((i * a.ld_zt + q) * 4), 0, kStorePolicy);
-        } else {
-          *reinterpret_cast<u32x4*>(a.ztok + (row0 + i) * a.ld_zt + q) = pk;
-        }
-      }
-      __builtin_amdgcn_wave_barrier();
-    }
-  }
+__global__ void __launch_bounds__(256) k_attn16_fwd(AttnArgs a) {
+  attn16_fwd_body<D, false>(a);
 }
 
-template <int D>
-constexpr size_t qkv_fwd_lds_bytes() {
-  return (size_t)(3 * D * (96 + 8) + WPB * 16 * (3 * D + 8)) * sizeof(uint16_t);
+// two workgroups (8 waves) per CU: <= 256 VGPRs, W_h's fragments included
+template <int D, bool IMG>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) k_qkv_attn16_fwd(AttnArgs a) {
+  attn16_fwd_body<D, true, IMG>(a);
 }
 
 template <int D>
@@ -614,23 +658,16 @@ void launch_fwd_mfma(const AttnArgs& a, hipStream_t stream) {
   else hipLaunchKernelGGL(k_attn16_fwd<128>, dim3(grid), dim3(256), 0, stream, a);
 }
 
+int g_qkv_grid_cap = 512;  // persistent: two workgroups per CU (W_h loaded once per wave)
+
 void launch_qkv_fwd_mfma(const AttnArgs& a, hipStream_t stream) {
-  const int grid = grid_for(a.B, 4096);
-  auto go = [&](const void* k, size_t lds) {
-    (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  };
-  if (a.D == 32) {
-    static bool attr = (go(reinterpret_cast<const void*>(k_qkv_attn16_fwd<32>), qkv_fwd_lds_bytes<32>()), true);
-    (void)attr;
-    hipLaunchKernelGGL(k_qkv_attn16_fwd<32>, dim3(grid), dim3(256), qkv_fwd_lds_bytes<32>(), stream, a);
-  } else if (a.D == 64) {
-    static bool attr = (go(reinterpret_cast<const void*>(k_qkv_attn16_fwd<64>), qkv_fwd_lds_bytes<64>()), true);
-    (void)attr;
-    hipLaunchKernelGGL(k_qkv_attn16_fwd<64>, dim3(grid), dim3(256), qkv_fwd_lds_bytes<64>(), stream, a);
+  const int grid = grid_for(a.B * a.Hl, g_qkv_grid_cap);
+  if (a.img) {
+    if (a.D == 32) hipLaunchKernelGGL((k_qkv_attn16_fwd<32, true>), dim3(grid), dim3(256), 0, stream, a);
+    else hipLaunchKernelGGL((k_qkv_attn16_fwd<64, true>), dim3(grid), dim3(256), 0, stream, a);
   } else {
-    static bool attr = (go(reinterpret_cast<const void*>(k_qkv_attn16_fwd<128>), qkv_fwd_lds_bytes<128>()), true);
-    (void)attr;
-    hipLaunchKernelGGL(k_qkv_attn16_fwd<128>, dim3(grid), dim3(256), qkv_fwd_lds_bytes<128>(), stream, a);
+    if (a.D == 32) hipLaunchKernelGGL((k_qkv_attn16_fwd<32, false>), dim3(grid), dim3(256), 0, stream, a);
+    else hipLaunchKernelGGL((k_qkv_attn16_fwd<64, false>), dim3(grid), dim3(256), 0, stream, a);
   }
 }
 

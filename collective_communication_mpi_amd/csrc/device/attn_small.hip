@@ -278,17 +278,22 @@ void attn_fwd(uint64_t qkv, uint64_t o, uint64_t lse, int B, int S, int Hl, int 
 }
 
 // Fused QKV projection + attention + per-token fc_o (attn_mfma.hip k_qkv_attn16_fwd): the
-// harness forward's QKV GEMM, attention and fc_o in one kernel.
+// harness forward's QKV GEMM, attention and fc_o in one kernel (W_h held in registers).
 void attn_qkv_fwd(uint64_t xq, int ld_xq, int kq, uint64_t wq, int ld_wq, uint64_t bq, uint64_t qkv_out, int ld_qkv,
                   uint64_t lse, int B, int S, int Hl, int D, float scale, uint64_t pool, int ld_pool, uint64_t wo,
                   int ld_wo, int n_out, uint64_t bo, uint64_t ztok, int ld_zt, int zrows,
-                  const std::vector<uint64_t>& zpush, uint64_t stream) {
-  if (S < 1 || S > 16 || !(D == 32 || D == 64 || D == 128) || Hl < 1 || kq < 8 || kq > 96 || kq % 8 || ld_xq % 8 ||
+                  const std::vector<uint64_t>& zpush, uint64_t stream, uint64_t img, uint64_t xq_out, uint64_t zmean,
+                  int ld_zmean) {
+  if (S < 1 || S > 16 || !(D == 32 || D == 64) || Hl < 1 || 4 % Hl || kq < 8 || kq > 80 || kq % 8 || ld_xq % 8 ||
       ld_wq % 8 || ld_wo % 8 || (xq % 16) || (wq % 16) || (wo % 16) || !wo || !bq || !lse || n_out < 1 || n_out > 16 ||
-      ld_zt < 16 || ld_zt % 4 || (ztok % 16) || (!ztok && !zrows) || (qkv_out && (ld_qkv % 8 || qkv_out % 16)) ||
+      ld_zt < 16 || ld_zt % 4 || (ztok % 16) || (!ztok && !zrows && !zmean) || (qkv_out && (ld_qkv % 8 || qkv_out % 16)) ||
+      (zmean && (zmean % 16 || ld_zmean % 4 || ld_zmean < 16 || zrows)) ||
       false)
-    throw std::invalid_argument("attention: fused QKV forward needs S <= 16, D in {32, 64, 128}, kq % 8 == 0 and "
-                                "<= 96, 16-B aligned rows, n_out <= 16, z rows of >= 16 floats (% 4), a z target");
+    throw std::invalid_argument("attention: fused QKV forward needs S <= 16, D in {32, 64}, Hl | 4, kq % 8 == 0 and "
+                                "<= 80, 16-B aligned rows, n_out <= 16, z rows of >= 16 floats (% 4), a z target");
+  if (img && (S != 16 || kq < 66 || (img % 16) || (xq_out % 16)))
+    throw std::invalid_argument("attention: fused patchify is the MNIST 28x28 / 7x7 case (S = 16, kq >= 66)");
+  if (!img && (xq_out || !xq)) throw std::invalid_argument("attention: patch rows xq needed (xq_out only with img)");
   AttnArgs a{};
   a.lse = (float*)lse;
   a.B = B; a.S = S; a.Hl = Hl; a.D = D; a.ld_qkv = ld_qkv; a.scale = scale;
@@ -296,6 +301,8 @@ void attn_qkv_fwd(uint64_t xq, int ld_xq, int kq, uint64_t wq, int ld_wq, uint64
   a.wo = (const uint16_t*)wo; a.ld_wo = ld_wo; a.n_out = n_out; a.bo = (const float*)bo;
   a.xq = (const uint16_t*)xq; a.ld_xq = ld_xq; a.kq = kq;
   a.wq = (const uint16_t*)wq; a.ld_wq = ld_wq; a.bq = (const float*)bq; a.qkv_out = (uint16_t*)qkv_out;
+  a.img = (const float*)img; a.xq_out = (uint16_t*)xq_out;
+  a.zp = (float*)zmean; a.ld_zp = ld_zmean;  // mean over the tokens of z (the local form's logits)
   a.ztok = (float*)ztok; a.ld_zt = ld_zt; a.zrows = zrows;
   if (zrows) {
     const int64_t M = (int64_t)B * S;
@@ -560,7 +567,8 @@ void register_attn_ops(pybind11::module_& m) {
         py::arg("bq"), py::arg("qkv_out"), py::arg("ld_qkv"), py::arg("lse"), py::arg("B"), py::arg("S"), py::arg("Hl"),
         py::arg("D"), py::arg("scale"), py::arg("pool"), py::arg("ld_pool"), py::arg("wo"), py::arg("ld_wo"),
         py::arg("n_out"), py::arg("bo"), py::arg("ztok"), py::arg("ld_zt"), py::arg("zrows"), py::arg("zpush"),
-        py::arg("stream"), py::call_guard<py::gil_scoped_release>());
+        py::arg("stream"), py::arg("img") = 0, py::arg("xq_out") = 0, py::arg("zmean") = 0, py::arg("ld_zmean") = 16,
+        py::call_guard<py::gil_scoped_release>());
   m.def("attn_small_bwd", &attn_bwd, py::arg("qkv"), py::arg("o"), py::arg("lse"), py::arg("dout"), py::arg("dqkv"),
         py::arg("dbias"), py::arg("B"), py::arg("S"), py::arg("Hl"), py::arg("D"), py::arg("ld_qkv"), py::arg("ld_o"),
         py::arg("scale"), py::arg("dout_bstride"), py::arg("dout_rstride"), py::arg("stream"), py::arg("dz") = 0,

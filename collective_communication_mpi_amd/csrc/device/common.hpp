@@ -200,11 +200,11 @@ __device__ __forceinline__ void acquire_sys() {
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ float bf16_lo(uint32_t w) { return __uint_as_float(w << 16); }
 __device__ __forceinline__ float bf16_hi(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
+// fp32 -> bf16 bits, round to nearest even, NaN stays NaN: gfx950's v_cvt_pk_bf16_f32 (one
+// VALU op; the integer RNE sequence it replaces compiled to an exec-mask branch per value for
+// its NaN test).  Denormals are preserved (the kernels' fp32 denorm mode).
 __device__ __forceinline__ uint32_t f32_to_bf16_bits(float f) {
-  uint32_t u = __float_as_uint(f);
-  if ((u & 0x7fffffffu) > 0x7f800000u) return (u >> 16) | 0x40;  // keep NaN a NaN
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return u >> 16;
+  return __builtin_bit_cast(uint16_t, (__bf16)f);
 }
 
 template <int OP, typename A>

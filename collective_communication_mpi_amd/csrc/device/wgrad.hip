@@ -331,6 +331,65 @@ __global__ void __launch_bounds__(kFoldNT) k_fold_emb_qkv(const float* __restric
   }
 }
 
+// The same fold on the fp32 matrix cores (v_mfma_f32_16x16x4_f32: exact fp32 products, fp32
+// accumulate): one 512-thread workgroup per 16 x 16 tile of Weff (grid R/16 x kp/16 = 240
+// workgroups at 768 x 72), its 8 waves splitting d.  A wave issues ALL its loads first --
+// per 16-deep k chunk j one float4 of its Wq row (k = 16 j + 4 g .. +3: the MFMA's k slot g
+// takes k = 16 j + 4 g + i at step i, the same permutation on both operands) and 4 We values
+// -- so the whole product is one memory round trip, then 4 MFMAs per chunk.  The 8 wave
+// partials meet in LDS in wave order (deterministic), + the bias column, bf16 out.  (A first
+// version with one workgroup per 16 rows x all columns -- 48 workgroups, a load round trip
+// per chunk -- took 17.9 us against the FMA kernel's 7.4 us.)
+constexpr int kFmWaves = 8;
+constexpr int kFmMaxJ = 8;  // chunks per wave: d <= 16 * 8 * 8 = 1024
+
+__global__ void __launch_bounds__(kFmWaves * 64) k_fold_mfma(const float* __restrict__ Wq, int ld_wq,
+                                                            const float* __restrict__ We, int ld_we,
+                                                            uint16_t* __restrict__ Weff, int ld_eff, int R, int d,
+                                                            int kp, const float* __restrict__ bias, int bias_col) {
+  typedef float f4v __attribute__((ext_vector_type(4)));
+  __shared__ __attribute__((aligned(16))) float part[kFmWaves][16][16 + 1];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
+  const int r0 = blockIdx.x * 16, c0 = blockIdx.y * 16, col = c0 + c;
+  const int nj = (d + 15) / 16, per = (nj + kFmWaves - 1) / kFmWaves;
+  const int j0 = wave * per;
+  const bool rok = r0 + c < R, cok = col < kp;
+  const float* arow = Wq + (size_t)(rok ? r0 + c : 0) * ld_wq;
+  float4 a4[kFmMaxJ];
+  float b[kFmMaxJ][4];
+#pragma unroll
+  for (int u = 0; u < kFmMaxJ; ++u) {
+    const int k = 16 * (j0 + u) + 4 * g;  // d % 4 == 0: the float4 is all in range or all out
+    const bool kok = u < per && k < d;
+    a4[u] = (rok && kok) ? *reinterpret_cast<const float4*>(arow + k) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) b[u][i] = (cok && kok) ? We[(size_t)(k + i) * ld_we + col] : 0.f;
+  }
+  f4v acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int u = 0; u < kFmMaxJ; ++u) {
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[u].x, b[u][0], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[u].y, b[u][1], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[u].z, b[u][2], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[u].w, b[u][3], acc, 0, 0, 0);
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) part[wave][4 * g + r][c] = acc[r];  // [row 4g + r][col c]
+  __syncthreads();
+  if (threadIdx.x < 256) {
+    const int r = threadIdx.x >> 4, cc = threadIdx.x & 15;
+    if (r0 + r < R && c0 + cc < kp) {
+      float sum = 0.f;
+#pragma unroll
+      for (int w = 0; w < kFmWaves; ++w) sum += part[w][r][cc];
+      if (bias && c0 + cc == bias_col) sum += bias[r0 + r];  // Xp's constant-1 column carries the QKV bias
+      Weff[(size_t)(r0 + r) * ld_eff + c0 + cc] = static_cast<uint16_t>(f32_to_bf16_bits(sum));
+    }
+  }
+}
+
+int g_fold_variant = -1;  // -1: CCMPI_FOLD (default "mfma"), 0: FMA kernel, 1: MFMA kernel
+
 size_t fold_lds_bytes(int d, int kp) {
   const int half = (kFoldNT / (kp / 4) + 1) / 2;
   return sizeof(float) * std::max<size_t>((size_t)kFoldRows * d, (size_t)half * kFoldRows * kp);
@@ -342,6 +401,17 @@ void fold_emb_qkv(uint64_t Wq, int ld_wq, uint64_t We, int ld_we, uint64_t Weff,
   if (R <= 0 || d <= 0 || kp <= 0) return;
   if (kp > kMaxKp || kp % 4 || d % 4 || d > kFoldMaxD || ld_wq % 4 || ld_we % 4 || (Wq % 16) || (We % 16) || !Weff)
     throw std::invalid_argument("fold_emb_qkv: kp <= 96, d <= 1024, kp / d / fp32 row strides % 4 == 0, 16-B aligned fp32 operands");
+  if (g_fold_variant < 0) {
+    const char* e = std::getenv("CCMPI_FOLD");
+    g_fold_variant = (e && std::string(e) == "fma") ? 0 : 1;
+  }
+  if (g_fold_variant == 1) {
+    hipLaunchKernelGGL(k_fold_mfma, dim3((R + 15) / 16, (kp + 15) / 16), dim3(kFmWaves * 64), 0, (hipStream_t)stream,
+                       reinterpret_cast<const float*>(Wq), ld_wq, reinterpret_cast<const float*>(We), ld_we,
+                       reinterpret_cast<uint16_t*>(Weff), ld_eff, R, d, kp, reinterpret_cast<const float*>(bias), bias_col);
+    CCMPI_HIP_CHECK(hipGetLastError());
+    return;
+  }
   const size_t lds = fold_lds_bytes(d, kp);
   if (lds > 64 * 1024) throw std::invalid_argument("fold_emb_qkv: LDS staging exceeds 64 KiB");
   hipLaunchKernelGGL(k_fold_emb_qkv, dim3((R + kFoldRows - 1) / kFoldRows), dim3(kFoldNT), lds, (hipStream_t)stream,
@@ -358,6 +428,8 @@ void register_wgrad_ops(pybind11::module_& m) {
         pybind11::arg("Wq"), pybind11::arg("ld_wq"), pybind11::arg("We"), pybind11::arg("ld_we"), pybind11::arg("Weff"),
         pybind11::arg("ld_eff"), pybind11::arg("R"), pybind11::arg("d"), pybind11::arg("kp"), pybind11::arg("stream"),
         pybind11::arg("bias") = 0, pybind11::arg("bias_col") = -1, pybind11::call_guard<pybind11::gil_scoped_release>());
+  m.def("fold_set_variant", [](int v) { g_fold_variant = v; },
+        "fold_emb_qkv kernel: 0 = fp32 FMA, 1 = fp32 MFMA, -1 = CCMPI_FOLD (default mfma)", pybind11::arg("v"));
   m.def("emb_qkv_wgrad", &emb_qkv_wgrad,
         "Gq += A . We^T (fixed order); Ge += Wq^T . A (fp32 atomics; Ge = 0: skipped); Z = 0 (Z = 0: skipped)",
         pybind11::arg("A"), pybind11::arg("ld_a"), pybind11::arg("We"), pybind11::arg("ld_we"), pybind11::arg("Wq"),

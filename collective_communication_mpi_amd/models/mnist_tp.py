@@ -304,9 +304,14 @@ class MnistTPLayer:
         qkv = self._buf("qkv", (M, 3 * self.hd), torch.bfloat16)
         h = None
         fuse_qkv = self._fuses_qkv(B)
+        img = None  # images the fused kernel patchifies itself (MNIST 28 x 28 / 7 x 7)
         if self._folds():
             if images is not None:
-                patchify(images, cfg, out=xp)
+                if fuse_qkv and cfg.img == 28 and cfg.patch == 7 and images.dtype == torch.float32 \
+                        and images.is_contiguous() and os.environ.get("CCMPI_FUSE_PATCHIFY", "1") != "0":
+                    img = images
+                else:
+                    patchify(images, cfg, out=xp)
             weff = weff if weff is not None else self.folded_qkv_weight()
             if not fuse_qkv:
                 gemm_nt(xp, weff, out=qkv, bias=self.flat.param("qkv_b"))
@@ -358,7 +363,7 @@ class MnistTPLayer:
             # fused QKV: the kernel also forms q | k | v from the patch rows (stored to qkv only
             # when a backward will read it)
             self._token_fc_o_kernel(qkv, lse, pool, B, st,
-                                    qkv_from=(xp, weff, save) if fuse_qkv else None)
+                                    qkv_from=(xp, weff, save, img) if fuse_qkv else None)
         elif not pipelined:
             D.attn_small_fwd(qkv.data_ptr(), 0 if att is None else att.data_ptr(), lse.data_ptr(), B, S,
                              self.hl, cfg.head_dim, qkv.stride(0), self.hd if att is None else att.stride(0),
@@ -373,7 +378,8 @@ class MnistTPLayer:
                 # logits = mean over the S tokens of the all-reduced z (o_b is in z, TP rank 0),
                 # kept in zp for the fused loss head
                 zp = self._buf("zp", (B, cfg.out_pad), torch.float32, self.tp_dev)
-                torch.mean(z.view(B, S, cfg.out_pad), dim=1, out=zp)
+                if z is not None:  # (None: the fused kernel already wrote the mean into zp)
+                    torch.mean(z.view(B, S, cfg.out_pad), dim=1, out=zp)
                 logits = zp[:, : cfg.n_classes]
             else:
                 logits = z.view(B, S, cfg.out_pad)[:, :, : cfg.n_classes].mean(dim=1)
@@ -413,6 +419,8 @@ class MnistTPLayer:
                 or (B // c) * S < 256):
             # (running the weight fold on a side stream concurrent with patchify measured
             # slower: train step 0.140 -> 0.159 ms, forward 0.061 -> 0.066 ms)
+            if self._fuses_qkv(B):
+                return self.forward(xp, B, images=images, save=save)  # the fused kernel patchifies
             patchify(images, cfg, out=xp)
             return self.forward(xp, B, save=save)
         d, hl, hd = cfg.d_model, self.hl, self.hd
@@ -472,19 +480,21 @@ class MnistTPLayer:
 
     def _fuses_qkv(self, B: int) -> bool:
         """The token-mode forward runs the QKV projection inside the attention kernel
-        (``k_qkv_attn16_fwd``): folded weights, the fused per-token fc_o, kp <= 96
-        (CCMPI_FUSE_QKV=0: the QKV GEMM + attention kernel instead)."""
+        (``k_qkv_attn16_fwd``): folded weights, the fused per-token fc_o
+        (CCMPI_FUSE_QKV=0: the QKV GEMM + attention kernel instead).  The kernel keeps a
+        head's folded weight in registers: head_dim <= 64, kp <= 80, local heads | 4."""
         cfg = self.cfg
         return (cfg.fuse_qkv and os.environ.get("CCMPI_FUSE_QKV", "1") != "0" and self._folds()
                 and cfg.fc_o_mode == "token" and self._fused_fc_o_bwd() and self._token_chunks(B) == 1
-                and cfg.seq <= 16 and cfg.head_dim in (32, 64, 128) and cfg.kp <= 96)
+                and cfg.seq <= 16 and cfg.head_dim in (32, 64) and cfg.kp <= 80 and 4 % self.hl == 0)
 
     def _token_fc_o_kernel(self, qkv, lse, pool, B: int, st: int, qkv_from=None) -> None:
         """Attention + per-token row-parallel fc_o in ONE kernel (``k_attn16_fwd``), then the
         TP sum of z (B*S x 16 fp32, o_b added by TP rank 0): an all-reduce ("plain"), or the
         kernel pushes every row block into its owner's inbox and the inbox-to-local two-shot
         completes it ("push", reference model/func_impl.py:94-109's output path, with the
-        communication under the attention).  Leaves the summed z in ``self._zt``."""
+        communication under the attention).  Leaves the summed z in ``self._zt`` (None when
+        the fused kernel wrote the token mean straight into zp: TP = 1)."""
         cfg = self.cfg
         S = cfg.seq
         M = B * S
@@ -497,15 +507,19 @@ class MnistTPLayer:
                 1.0 / math.sqrt(cfg.head_dim), pool.data_ptr(), pool.stride(0))  # pool: dW_o in backward
         fwd = D.attn_small_fwd
         if qkv_from is not None:
-            xp, weff, keep = qkv_from
+            xp, weff, keep, img = qkv_from
             bq = self.flat.param("qkv_b")
 
-            def fwd(*_a, zrows=0, zpush=(), ztok=0, ld_zt=16, wo=0, ld_wo=0, n_out=0, bo=0):
+            def fwd(*_a, zrows=0, zpush=(), ztok=0, ld_zt=16, wo=0, ld_wo=0, n_out=0, bo=0, zmean=0, ld_zmean=16):
                 stream = _a[-1]
-                D.attn_qkv_fwd(xp.data_ptr(), xp.stride(0), cfg.kp, weff.data_ptr(), weff.stride(0), bq.data_ptr(),
-                               qkv.data_ptr() if keep else 0, qkv.stride(0), lse.data_ptr(), B, S, self.hl,
-                               cfg.head_dim, 1.0 / math.sqrt(cfg.head_dim), pool.data_ptr(), pool.stride(0), wo, ld_wo,
-                               n_out, bo, ztok, ld_zt, zrows, list(zpush), stream)
+                # with img the kernel builds the patch rows itself (stored to xp for a backward)
+                D.attn_qkv_fwd(0 if img is not None else xp.data_ptr(), xp.stride(0), cfg.kp, weff.data_ptr(),
+                               weff.stride(0), bq.data_ptr(), qkv.data_ptr() if keep else 0, qkv.stride(0),
+                               lse.data_ptr(), B, S, self.hl, cfg.head_dim, 1.0 / math.sqrt(cfg.head_dim),
+                               pool.data_ptr(), pool.stride(0), wo, ld_wo, n_out, bo, ztok, ld_zt, zrows, list(zpush),
+                               stream, img=0 if img is None else img.data_ptr(),
+                               xq_out=xp.data_ptr() if (img is not None and keep) else 0, zmean=zmean,
+                               ld_zmean=ld_zmean)
         form = self.tp_fc_o_form(B)
         if form == "push":
             inbox = self._buf("ztok_inbox", (M, cfg.out_pad), torch.float32, self.tp_dev)
@@ -516,6 +530,12 @@ class MnistTPLayer:
             fwd(*args, s, zrows=M // cfg.tp, zpush=self._bufs[key], **kw)
             self.tp_dev.dc.inbox_to_local(inbox.data_ptr(), z.data_ptr(), inbox.numel() * 4, 10, s,
                                           self.tp_dev._budget(None))
+        elif self.tp_dev is None and qkv_from is not None:
+            # local form (TP = 1): nothing to sum across ranks, so the fused kernel reduces z to
+            # the logits (mean over the tokens) itself and z is never stored
+            zp = self._buf("zp", (B, cfg.out_pad), torch.float32, self.tp_dev)
+            fwd(*args, st, zmean=zp.data_ptr(), ld_zmean=zp.stride(0), **kw)
+            z = None
         else:
             fwd(*args, st, ztok=z.data_ptr(), **kw)
             if self.tp_dev is not None:

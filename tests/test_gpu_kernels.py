@@ -467,8 +467,8 @@ def test_attn_token_fc_o(B, S, H, D, n_out):
                            pool.data_ptr(), pool.stride(0), st, zrows=S + 1, zpush=[tg.data_ptr()], **kw)
 
 
-@pytest.mark.parametrize("B,S,H,D,kp", [(2048, 16, 4, 64, 72), (2048, 16, 2, 64, 72), (37, 16, 1, 128, 96),
-                                        (9, 7, 2, 32, 40), (5, 16, 4, 64, 8)])
+@pytest.mark.parametrize("B,S,H,D,kp", [(2048, 16, 4, 64, 72), (2048, 16, 2, 64, 72), (37, 16, 1, 64, 80),
+                                        (9, 7, 2, 32, 40), (5, 16, 4, 64, 8), (3001, 16, 4, 32, 72)])
 def test_attn_qkv_fused(B, S, H, D, kp):
     """QKV projection + attention + per-token fc_o in one kernel (the harness forward):
     q | k | v = bf16(X W^T + b) against torch fp32 (stored when asked), then lse, pool and z
@@ -514,6 +514,60 @@ def test_attn_qkv_fused(B, S, H, D, kp):
                      zpush=[tg[j].data_ptr() for j in range(blocks)], **common)
     torch.cuda.synchronize()
     assert torch.equal(tg.view(B * S, 16), z) and torch.isnan(qkv.float()).all()
+    # local form: the token mean of z (+ bias) straight into the logits, z never stored
+    zm = torch.full((B, 16), float("nan"), device="cuda")
+    dev.attn_qkv_fwd(xq=xp.data_ptr(), ld_xq=xp.stride(0), kq=kp, wq=w.data_ptr(), ld_wq=w.stride(0), bq=bq.data_ptr(),
+                     qkv_out=0, ld_qkv=qkv.stride(0), ztok=0, zrows=0, zpush=[], zmean=zm.data_ptr(), ld_zmean=16,
+                     **common)
+    torch.cuda.synchronize()
+    torch.testing.assert_close(zm, z.view(B, S, 16).mean(dim=1), rtol=1e-5, atol=1e-5)
+    with pytest.raises(ValueError):  # beyond the register-resident weight: kq > 80
+        dev.attn_qkv_fwd(xq=xp.data_ptr(), ld_xq=xp.stride(0), kq=88, wq=w.data_ptr(), ld_wq=w.stride(0),
+                         bq=bq.data_ptr(), qkv_out=0, ld_qkv=qkv.stride(0), ztok=z.data_ptr(), zrows=0, zpush=[],
+                         **common)
+
+
+@pytest.mark.parametrize("B,H,D", [(2048, 4, 64), (2048, 2, 64), (37, 1, 64), (301, 4, 32)])
+def test_attn_qkv_fused_patchify(B, H, D):
+    """Fused patchify: the kernel builds the MNIST patch rows from the fp32 images itself --
+    the rows it stores for the backward are bitwise k_patchify's, and qkv / lse / pool / z are
+    bitwise those of the same kernel reading k_patchify's rows."""
+    from collective_communication_mpi_amd import _native
+
+    dev = _native.device()
+    st = torch.cuda.current_stream().cuda_stream
+    g = torch.Generator(device="cuda").manual_seed(B + H)
+    S, kp, HD = 16, 72, H * D
+    img = torch.rand(B, 784, device="cuda", generator=g)
+    xp = torch.empty(B * S, kp, device="cuda", dtype=torch.bfloat16)
+    dev.patchify(img.data_ptr(), xp.data_ptr(), B, 28, 7, kp, st, kp)
+    w = (torch.randn(3 * HD, kp, device="cuda", generator=g) / kp ** 0.5).bfloat16()
+    bq = torch.randn(3 * HD, device="cuda", generator=g) * 0.1
+    wo = (torch.randn(16, HD, device="cuda", generator=g) * 0.1).bfloat16()
+    bo = torch.randn(16, device="cuda", generator=g)
+    outs = []
+    for mode in ("rows", "img"):
+        qkv = torch.full((B * S, 3 * HD), float("nan"), device="cuda").bfloat16()
+        lse = torch.empty(B * H, S, device="cuda")
+        pool = torch.empty(B, HD, device="cuda", dtype=torch.bfloat16)
+        z = torch.full((B * S, 16), float("nan"), device="cuda")
+        xo = torch.full((B * S, kp), float("nan"), device="cuda").bfloat16()
+        dev.attn_qkv_fwd(xq=xp.data_ptr() if mode == "rows" else 0, ld_xq=kp, kq=kp, wq=w.data_ptr(),
+                         ld_wq=w.stride(0), bq=bq.data_ptr(), qkv_out=qkv.data_ptr(), ld_qkv=qkv.stride(0),
+                         lse=lse.data_ptr(), B=B, S=S, Hl=H, D=D, scale=D ** -0.5, pool=pool.data_ptr(),
+                         ld_pool=pool.stride(0), wo=wo.data_ptr(), ld_wo=wo.stride(0), n_out=16, bo=bo.data_ptr(),
+                         ztok=z.data_ptr(), ld_zt=16, zrows=0, zpush=[], stream=st,
+                         img=img.data_ptr() if mode == "img" else 0, xq_out=xo.data_ptr() if mode == "img" else 0)
+        outs.append((qkv, lse, pool, z, xo))
+    torch.cuda.synchronize()
+    (q0, l0, p0, z0, _), (q1, l1, p1, z1, xo) = outs
+    assert torch.equal(xo, xp)
+    assert torch.equal(q0, q1) and torch.equal(l0, l1) and torch.equal(p0, p1) and torch.equal(z0, z1)
+    with pytest.raises(ValueError):  # image mode is the 16-token MNIST case
+        dev.attn_qkv_fwd(xq=0, ld_xq=kp, kq=kp, wq=w.data_ptr(), ld_wq=w.stride(0), bq=bq.data_ptr(), qkv_out=0,
+                         ld_qkv=3 * HD, lse=l0.data_ptr(), B=B, S=9, Hl=H, D=D, scale=1.0, pool=p0.data_ptr(),
+                         ld_pool=HD, wo=wo.data_ptr(), ld_wo=HD, n_out=16, bo=0, ztok=z0.data_ptr(), ld_zt=16,
+                         zrows=0, zpush=[], stream=st, img=img.data_ptr())
 
 
 @pytest.mark.parametrize("img,patch,misalign", [(28, 7, 0), (28, 7, 1), (24, 6, 0)])  # LDS / plain / runtime sizes
@@ -646,10 +700,22 @@ def test_gemm_tn_pingpong(M, N1, N2, splitk):
         set_tn_variant(None)
 
 
+@pytest.mark.parametrize("variant", [0, 1], ids=["fma", "mfma"])
 @pytest.mark.parametrize("R,d,kp", [(768, 768, 72), (384, 768, 72), (20, 36, 16), (7, 100, 96), (50, 1000, 8)])
-def test_fold_emb_qkv_matches_fp32(R, d, kp):
+def test_fold_emb_qkv_matches_fp32(R, d, kp, variant):
     """W_eff = W_qkv . W_emb (+ bias in one column) against torch fp64, incl. ragged
-    row / column / k edges and strided operands (fp32 FMA kernel, fixed order)."""
+    row / column / k edges and strided operands (fp32 FMA kernel and fp32 MFMA kernel,
+    both fixed order)."""
+    from collective_communication_mpi_amd import _native
+
+    _native.device().fold_set_variant(variant)
+    try:
+        _fold_check(R, d, kp)
+    finally:
+        _native.device().fold_set_variant(-1)
+
+
+def _fold_check(R, d, kp):
     from collective_communication_mpi_amd import _native
 
     torch.manual_seed(R + d)
