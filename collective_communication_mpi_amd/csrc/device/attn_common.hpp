@@ -65,6 +65,7 @@ bool mfma_supported(const AttnArgs& a, bool bwd);
 void launch_fwd_mfma(const AttnArgs& a, hipStream_t stream);
 void launch_bwd_mfma(const AttnArgs& a, hipStream_t stream);
 void launch_qkv_fwd_mfma(const AttnArgs& a, hipStream_t stream);  // fused QKV + attention + token fc_o
+extern int g_qkv_grid_cap;  // workgroups of the fused QKV forward (persistent grid)
 extern int g_bwd_grid_cap;  // workgroups of the backward kernel when it also reduces the bias gradient
 
 }  // namespace attn

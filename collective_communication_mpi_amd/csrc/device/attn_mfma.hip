@@ -45,7 +45,7 @@ typedef float f4 __attribute__((ext_vector_type(4)));
 constexpr int WPB = 4;  // waves per workgroup
 
 __device__ __forceinline__ s4 pack4(float a, float b, float c, float d) {
-  const uint2 u{f32_to_bf16_bits(a) | (f32_to_bf16_bits(b) << 16), f32_to_bf16_bits(c) | (f32_to_bf16_bits(d) << 16)};
+  const uint2 u{pk_bf16(a, b), pk_bf16(c, d)};
   return __builtin_bit_cast(s4, u);
 }
 __device__ __forceinline__ bf16x8 ld_row16(const uint16_t* p, bool ok) {
@@ -163,12 +163,21 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
   }
   // per-token fused fc_o: B operand of z = O . W_o^T -- lane (c, g) holds class c, this
   // wave's head features 32kk + 8g .. +7 (loaded once; classes >= n_out read as zero)
-  bf16x8 wb[NK];
+  bf16x8 wb[QKV ? 1 : NK];
+  // fused QKV: z comes from the transposed O accumulators (features on the K axis), so W_o is
+  // the B operand of the 16x16x16 MFMA -- lane (c, g): class c, features 16 nt + 4 g .. +3
+  s4 wo16[QKV ? NT : 1];
   if (tok) {
     const int hw = wave % a.Hl;
+    if constexpr (QKV) {
 #pragma unroll
-    for (int kk = 0; kk < NK; ++kk)
-      wb[kk] = ld_row16(a.wo + (size_t)c * a.ld_wo + hw * D + 32 * kk + 8 * g, c < a.n_out);
+      for (int nt = 0; nt < NT; ++nt)
+        wo16[nt] = ld_s4(a.wo + (size_t)c * a.ld_wo + hw * D + 16 * nt + 4 * g, c < a.n_out);
+    } else {
+#pragma unroll
+      for (int kk = 0; kk < NK; ++kk)
+        wb[kk] = ld_row16(a.wo + (size_t)c * a.ld_wo + hw * D + 32 * kk + 8 * g, c < a.n_out);
+    }
   }
   const int stride = gridDim.x * WPB;
   // fused QKV: W_h's rows as B operands (lane (c, g): feature 16 nt + c of q | k | v, depth
@@ -190,23 +199,23 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
       // recomputed per call rather than hoisted into 20 live registers (which spilled)
       int g = lane >> 4;
       asm volatile("" : "+v"(g));
-      auto px = [&](int cc) -> uint32_t {
+      auto px = [&](int cc) -> float {
         float v = 0.f;
         if (ok) {
           if (cc < 49) v = im[(cc / 7) * 28 + cc % 7];
           else if (cc == 49 || cc == 50 + c) v = 1.f;
         }
-        return f32_to_bf16_bits(v);
+        return v;
       };
       u32x4 w0, w1;
       uint2 wt;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        w0[q] = px(8 * g + 2 * q) | (px(8 * g + 2 * q + 1) << 16);
-        w1[q] = px(32 + 8 * g + 2 * q) | (px(32 + 8 * g + 2 * q + 1) << 16);
+        w0[q] = pk_bf16(px(8 * g + 2 * q), px(8 * g + 2 * q + 1));
+        w1[q] = pk_bf16(px(32 + 8 * g + 2 * q), px(32 + 8 * g + 2 * q + 1));
       }
-      wt.x = px(64 + 4 * g) | (px(64 + 4 * g + 1) << 16);
-      wt.y = px(64 + 4 * g + 2) | (px(64 + 4 * g + 3) << 16);
+      wt.x = pk_bf16(px(64 + 4 * g), px(64 + 4 * g + 1));
+      wt.y = pk_bf16(px(64 + 4 * g + 2), px(64 + 4 * g + 3));
       xn[0] = __builtin_bit_cast(bf16x8, w0);
       xn[1] = __builtin_bit_cast(bf16x8, w1);
       xtn = __builtin_bit_cast(s4, wt);
@@ -266,25 +275,28 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
     const int b = pr / a.Hl, h = pr % a.Hl;
     bf16x8 qr[NK], kr[NK];
     if constexpr (QKV) {
-      // sel's [16 tokens][D] block of X W_h^T + b, rounded to bf16, into tile T.  The bias is
-      // re-read per iteration (L1 hits; an opaque pointer keeps the compiler from hoisting 12
-      // more loop-invariant registers)
-      const float* bqp = a.bq + h * D + c;
+      // sel's [16 tokens][D] block of X W_h^T + b, rounded to bf16, into tile T -- computed
+      // transposed, (W_h X^T), so a lane's accumulator holds 4 consecutive features of one
+      // token: 2 packed conversions + one 8-B LDS store per 16 x 16 tile instead of 4 + 4
+      // 2-B stores.  The bias is re-read per iteration (L1 hits; an opaque pointer keeps the
+      // compiler from hoisting loop-invariant registers)
+      const float* bqp = a.bq + h * D + 4 * g;
       asm volatile("" : "+v"(bqp));
       auto proj = [&](int sel, uint16_t* T) {
-        float bias[NT];
-#pragma unroll
-        for (int nt = 0; nt < NT; ++nt) bias[nt] = bqp[sel * HD + 16 * nt];
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt) {
+          // (a compiler memory barrier per tile: the 12 bias loads are not all hoisted up front)
+          const float* bp = bqp + sel * HD + 16 * nt;
+          asm volatile("" : "+v"(bp)::"memory");
+          const float4 bz = *reinterpret_cast<const float4*>(bp);
           // (the 16x16x16 tail gets its own accumulator: chaining it onto the 16x16x32
           // accumulator lost rows -- the compiler emits no wait states for that srcC hazard)
-          const f4 tl = mma16(xt, wtl[sel][nt], f4{0.f, 0.f, 0.f, 0.f});
-          f4 acc = mma32(xr[0], wf[sel][nt][0], f4{0.f, 0.f, 0.f, 0.f});
-          acc = mma32(xr[1], wf[sel][nt][1], acc);  // acc[r] = [token 4g + r][feature 16 nt + c]
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            T[(4 * g + r) * LD + 16 * nt + c] = (uint16_t)f32_to_bf16_bits(acc[r] + tl[r] + bias[nt]);
+          const f4 tl = mma16(wtl[sel][nt], xt, f4{0.f, 0.f, 0.f, 0.f});
+          f4 acc = mma32(wf[sel][nt][0], xr[0], f4{0.f, 0.f, 0.f, 0.f});
+          acc = mma32(wf[sel][nt][1], xr[1], acc);  // acc[r] = [feature 16 nt + 4g + r][token c]
+          const uint2 pk = {pk_bf16(acc[0] + tl[0] + bz.x, acc[1] + tl[1] + bz.y),
+                            pk_bf16(acc[2] + tl[2] + bz.z, acc[3] + tl[3] + bz.w)};
+          *reinterpret_cast<uint2*>(T + c * LD + 16 * nt + 4 * g) = pk;
         }
       };
       if (IMG && a.xq_out && h == 0 && c < S) {  // the patch rows, for the backward (one head's wave)
@@ -350,6 +362,34 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
     if (g == 0 && c < S) a.lse[(size_t)pr * S + c] = m + __logf(s);
     const s4 pa = pack4(e[0] * inv, e[1] * inv, e[2] * inv, e[3] * inv);  // A[i = c][j = 4g + jj]
     __builtin_amdgcn_wave_barrier();
+    if constexpr (QKV) {
+      // O^T = V^T P^T: ot[nt][r] = O[query c][feature 16 nt + 4g + r] -- features on the MFMA
+      // K axis, so z = bf16(O) W_o^T chains straight from the registers (no LDS round trip)
+      f4 ot[NT];
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) ot[nt] = mma16(tile_b<LD>(V, g, 16 * nt + c), pa, f4{0.f, 0.f, 0.f, 0.f});
+      f4 zt = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) zt = mma16(pack4(ot[nt][0], ot[nt][1], ot[nt][2], ot[nt][3]), wo16[nt], zt);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) ztp[it][wave][(4 * g + r) * 16 + c] = zt[r];  // z[i = 4g + r][cls = c]
+      if (a.pool) {
+        // pool[f] = mean over the S queries of O[i][f]: recompute O un-transposed (4 more
+        // 16x16x16 MFMAs, one tile live at a time) so the column sum is 4 adds + 2 shuffles per
+        // tile -- and bitwise the unfused kernel's pool.  (A 15-shuffle butterfly over the
+        // transposed accumulators pushed the kernel past 256 VGPRs.)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+          const f4 on = mma16(pa, tile_b<LD>(V, g, 16 * nt + c), f4{0.f, 0.f, 0.f, 0.f});
+          float cs = 0.f;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) cs += (4 * g + r < S) ? on[r] : 0.f;
+          cs += __shfl_xor(cs, 16);
+          cs += __shfl_xor(cs, 32);
+          if (g == 0) a.pool[(size_t)b * a.ld_pool + h * D + 16 * nt + c] = (uint16_t)f32_to_bf16_bits(cs / (float)S);
+        }
+      }
+    } else {
     f4 o[NT];
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) o[nt] = mma16(pa, tile_b<LD>(V, g, 16 * nt + c), f4{0.f, 0.f, 0.f, 0.f});
@@ -403,6 +443,7 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
       for (int r = 0; r < 4; ++r) ztp[it][wave][(4 * g + r) * 16 + c] = zt[r];
     }
     if (a.o) store_tile<D, LD>(O, o, 1.f, a.o + (size_t)b * S * a.ld_o + h * D, a.ld_o, S, lane);
+    }  // !QKV
    }
    if (tok) {
     // the Hl heads of each sequence of this iteration (consecutive waves, Hl | WPB), summed in
@@ -658,7 +699,7 @@ void launch_fwd_mfma(const AttnArgs& a, hipStream_t stream) {
   else hipLaunchKernelGGL(k_attn16_fwd<128>, dim3(grid), dim3(256), 0, stream, a);
 }
 
-int g_qkv_grid_cap = 512;  // persistent: two workgroups per CU (W_h loaded once per wave)
+int g_qkv_grid_cap = 512;  // persistent: two workgroups per CU (W_h loaded once per wave); attn_set_qkv_grid
 
 void launch_qkv_fwd_mfma(const AttnArgs& a, hipStream_t stream) {
   const int grid = grid_for(a.B * a.Hl, g_qkv_grid_cap);

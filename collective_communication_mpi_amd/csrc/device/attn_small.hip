@@ -285,7 +285,8 @@ void attn_qkv_fwd(uint64_t xq, int ld_xq, int kq, uint64_t wq, int ld_wq, uint64
                   const std::vector<uint64_t>& zpush, uint64_t stream, uint64_t img, uint64_t xq_out, uint64_t zmean,
                   int ld_zmean) {
   if (S < 1 || S > 16 || !(D == 32 || D == 64) || Hl < 1 || 4 % Hl || kq < 8 || kq > 80 || kq % 8 || ld_xq % 8 ||
-      ld_wq % 8 || ld_wo % 8 || (xq % 16) || (wq % 16) || (wo % 16) || !wo || !bq || !lse || n_out < 1 || n_out > 16 ||
+      ld_wq % 8 || ld_wo % 8 || (xq % 16) || (wq % 16) || (wo % 16) || !wo || !bq || (bq % 16) || !lse || n_out < 1 ||
+      n_out > 16 ||
       ld_zt < 16 || ld_zt % 4 || (ztok % 16) || (!ztok && !zrows && !zmean) || (qkv_out && (ld_qkv % 8 || qkv_out % 16)) ||
       (zmean && (zmean % 16 || ld_zmean % 4 || ld_zmean < 16 || zrows)) ||
       false)
@@ -478,7 +479,7 @@ __global__ void __launch_bounds__(256) k_patchify(const float* __restrict__ x, u
         else if (c == pp || c == pp + 1 + s) v = 1.f;
         v2[h] = v;
       }
-      w[q] = f32_to_bf16_bits(v2[0]) | (f32_to_bf16_bits(v2[1]) << 16);
+      w[q] = pk_bf16(v2[0], v2[1]);
     }
     *reinterpret_cast<uint4*>(xp + (size_t)row * ldo + ch * 8) = uint4{w[0], w[1], w[2], w[3]};
   }
@@ -501,6 +502,34 @@ void patchify(uint64_t x, uint64_t xp, int B, int img, int p, int kp, uint64_t s
   else
     hipLaunchKernelGGL((k_patchify<0, 0>), dim3(grid), dim3(256), 0, (hipStream_t)stream, (const float*)x, (uint16_t*)xp,
                        B, img, p, kp, ldo);
+  CCMPI_HIP_CHECK(hipGetLastError());
+}
+
+// Mean over each group of S consecutive fp32 rows (the per-token fc_o's logits: z rows ->
+// one row per sequence), one thread per (group, 4 columns), rows summed in order -- the
+// summation order of DeviceComm::inbox_mean, so the "plain" TP form (all-reduce of z, then
+// this) and the "push" form (inbox_mean) give bitwise the same logits.
+__global__ void __launch_bounds__(256) k_rows_mean(const float* __restrict__ z, int ld_z, float* __restrict__ out,
+                                                   int ld_out, int groups, int S, int ncol4) {
+  const int idx = blockIdx.x * 256 + threadIdx.x;
+  if (idx >= groups * ncol4) return;
+  const int gi = idx / ncol4, q = idx % ncol4;
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int i = 0; i < S; ++i) {
+    const float4 v = *reinterpret_cast<const float4*>(z + (size_t)(gi * S + i) * ld_z + 4 * q);
+    acc[0] += v.x; acc[1] += v.y; acc[2] += v.z; acc[3] += v.w;
+  }
+  const float n = (float)S;
+  *reinterpret_cast<float4*>(out + (size_t)gi * ld_out + 4 * q) = float4{acc[0] / n, acc[1] / n, acc[2] / n, acc[3] / n};
+}
+
+void rows_mean(uint64_t z, int ld_z, uint64_t out, int ld_out, int groups, int S, int ncol, uint64_t stream) {
+  if (groups < 0 || S < 1 || ncol % 4 || ld_z % 4 || ld_out % 4 || z % 16 || out % 16 || ncol > ld_z || ncol > ld_out)
+    throw std::invalid_argument("rows_mean: fp32 rows, ncol % 4 == 0, 16-B aligned rows");
+  if (groups == 0) return;
+  const int n = groups * (ncol / 4);
+  hipLaunchKernelGGL(k_rows_mean, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, (const float*)z, ld_z,
+                     (float*)out, ld_out, groups, S, ncol / 4);
   CCMPI_HIP_CHECK(hipGetLastError());
 }
 
@@ -555,6 +584,12 @@ void cast_bf16(uint64_t x, uint64_t y, uint64_t n, uint64_t stream,
 }  // namespace
 
 void register_attn_ops(pybind11::module_& m) {
+  m.def("rows_mean", &rows_mean, "out[g] = mean of fp32 rows z[g S .. g S + S) (ordered sum)", pybind11::arg("z"),
+        pybind11::arg("ld_z"), pybind11::arg("out"), pybind11::arg("ld_out"), pybind11::arg("groups"),
+        pybind11::arg("S"), pybind11::arg("ncol"), pybind11::arg("stream"),
+        pybind11::call_guard<pybind11::gil_scoped_release>());
+  m.def("attn_set_qkv_grid", [](int cap) { attn::g_qkv_grid_cap = cap > 0 ? cap : 512; },
+        "workgroups of the fused QKV forward (default 512: two per CU)", pybind11::arg("cap"));
   m.def("attn_set_bwd_grid", [](int cap) { attn::g_bwd_grid_cap = cap > 0 ? cap : 0; },
         "backward kernel grid cap (tuning)");
   namespace py = pybind11;

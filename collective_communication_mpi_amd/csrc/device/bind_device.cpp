@@ -195,6 +195,7 @@ PYBIND11_MODULE(_device, m) {
       .def("gemm_push_rowpar", &DeviceComm::gemm_push_rowpar, py::call_guard<py::gil_scoped_release>())
       .def("push_targets", &DeviceComm::push_targets)
       .def("inbox_to_local", &DeviceComm::inbox_to_local, py::call_guard<py::gil_scoped_release>())
+      .def("inbox_mean", &DeviceComm::inbox_mean, py::call_guard<py::gil_scoped_release>())
       .def("ll_connect", [](DeviceComm& d, const std::vector<std::string>& hs) { d.ll_connect(hs); })
       .def_property_readonly("ll_max_bytes", &DeviceComm::ll_max_bytes)
       .def_property_readonly("inbox_bytes", &DeviceComm::inbox_bytes)

@@ -645,6 +645,67 @@ __global__ void __launch_bounds__(kThreads) k_allreduce_inbox_local(CollArgs a) 
   finish(a, e);
 }
 
+// Inbox-to-mean: the TP sum of the per-token fc_o output z followed by the mean over each
+// sequence's S rows (the harness logits), as reduce-scatter + mean + all-gather of the means.
+// Every rank's attention kernel has pushed its partial z row block j into rank j's inbox slot
+// [rank] (posted writes under the attention); here rank r sums its p slots per row (rank
+// order), averages each sequence's S rows (row order), and stores the B / p mean rows into
+// EVERY rank's logits buffer (local + peer-mapped write-through stores).  So the fabric
+// carries (p-1)/p of z once plus B x 16 logits -- not z twice (all-reduce) -- and the
+// separate mean kernel disappears.  a.nbytes = the whole z (B*S x 16 fp32), a.root = S,
+// codes[0][j] = rank j's inbox (slot stride nbytes / p), codes[1][j] = rank j's logits
+// (B x 16 fp32, symmetric).
+template <int NRM>
+__global__ void __launch_bounds__(kThreads) k_inbox_mean(CollArgs a) {
+  __shared__ uint64_t s_epoch;
+  __shared__ uint64_t codes[2][kMaxRanks];
+  if (!start_phase(a, &s_epoch, codes)) return;
+  const uint64_t e = s_epoch;
+  const PeerTable* pt = a.pt;
+  const int me = pt->rank, nr = pt->size, S = a.root;
+  const uint32_t shard = (uint32_t)(a.nbytes / nr), ngroups = shard / (uint32_t)(S * 64);
+  {
+    char* inbox = resolve(pt, me, codes[0][me]);
+    Rsrc src[NRM], dst[NRM];
+#pragma unroll
+    for (int j = 0; j < NRM; ++j)
+      if (j < nr) {
+        src[j] = make_rsrc(uniform_ptr(inbox + (uint64_t)j * shard), shard);
+        dst[j] = make_rsrc(uniform_ptr(resolve(pt, j, codes[1][j]) + (uint64_t)me * ngroups * 64), ngroups * 64);
+      }
+    const float n = (float)S;
+    for (uint32_t idx = blockIdx.x * kThreads + threadIdx.x; idx < ngroups * 4; idx += gridDim.x * kThreads) {
+      const uint32_t gl = idx >> 2, q = idx & 3;
+      float acc[4] = {0.f, 0.f, 0.f, 0.f};
+      for (int i = 0; i < S; ++i) {
+        const uint32_t off = (gl * S + i) * 64 + q * 16;
+        float row[4];
+        const u32x4 x0 = ld16(src[0], off);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) row[k] = __uint_as_float(x0[k]);
+#pragma unroll
+        for (int j = 1; j < NRM; ++j)
+          if (j < nr) {
+            const u32x4 xj = ld16(src[j], off);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) row[k] += __uint_as_float(xj[k]);
+          }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) acc[k] += row[k];
+      }
+      const u32x4 m = {__float_as_uint(acc[0] / n), __float_as_uint(acc[1] / n), __float_as_uint(acc[2] / n),
+                       __float_as_uint(acc[3] / n)};
+#pragma unroll
+      for (int j = 0; j < NRM; ++j)
+        if (j < nr) st16(dst[j], gl * 64 + q * 16, m);
+    }
+  }
+  // every rank's means have landed everywhere, and no rank's next push can reach an inbox
+  // that is still being read
+  if (!sync_phase(a, 1, e)) return;
+  finish(a, e);
+}
+
 // Reference algorithm (mpi_wrapper/comm.py:63-107): the root reduces every
 // rank's buffer in rank order, then every other rank copies the root's result.
 template <int DT, int OP, int NRM>
@@ -1370,6 +1431,11 @@ void launch_inbox_to_local(const CollArgs& a, int nranks, int dtype, int grid, h
     else if (dtype == DT_F32) hipLaunchKernelGGL((k_allreduce_inbox_local<DT_F32, OP_SUM, R>), dim3(grid), dim3(kThreads), 0, s, a);
     else throw std::invalid_argument("ccmpi: inbox all-reduce supports bf16 / fp32 sums");
   });
+  CCMPI_HIP_CHECK(hipGetLastError());
+}
+
+void launch_inbox_mean(const CollArgs& a, int nranks, int grid, hipStream_t s) {
+  with_nrm(nranks, [&]<int R>() { hipLaunchKernelGGL((k_inbox_mean<R>), dim3(grid), dim3(kThreads), 0, s, a); });
   CCMPI_HIP_CHECK(hipGetLastError());
 }
 

@@ -91,6 +91,7 @@ void launch_allreduce(int algo, const CollArgs& a, int nranks, int dtype, int op
 // the collective half of the push row-parallel GEMM: reduce the inbox slots the GEMM
 // epilogues filled (codes[0] = the inboxes), pull every shard into a.out (bf16 / fp32 sum)
 void launch_inbox_to_local(const CollArgs& a, int nranks, int dtype, int grid, hipStream_t s);
+void launch_inbox_mean(const CollArgs& a, int nranks, int grid, hipStream_t s);
 void launch_reduce_scatter(const CollArgs& a, int nranks, int dtype, int op, int grid, hipStream_t s);
 void launch_move(int mode, const CollArgs& a, int nranks, int grid, hipStream_t s);
 // mode 0: last-axis all-gather, 1: last-axis reduce-scatter; rows passed in CollArgs::root

@@ -206,6 +206,13 @@ __device__ __forceinline__ float bf16_hi(uint32_t w) { return __uint_as_float(w 
 __device__ __forceinline__ uint32_t f32_to_bf16_bits(float f) {
   return __builtin_bit_cast(uint16_t, (__bf16)f);
 }
+// two fp32 -> packed bf16 pair (lo = a): ONE v_cvt_pk_bf16_f32 (the scalar form above, OR-ed
+// in pairs, compiles to two conversions + shift + or)
+__device__ __forceinline__ uint32_t pk_bf16(float a, float b) {
+  typedef float f2_t __attribute__((ext_vector_type(2)));
+  typedef __bf16 b2_t __attribute__((ext_vector_type(2)));
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f2_t{a, b}), b2_t));
+}
 
 template <int OP, typename A>
 __device__ __forceinline__ A apply_op(A a, A b) {
@@ -244,7 +251,7 @@ template <> struct VecAcc<DT_BF16> {
   }
   __device__ __forceinline__ u32x4 store() const {
     u32x4 r;
-    for (int i = 0; i < 4; ++i) r[i] = f32_to_bf16_bits(v[2 * i]) | (f32_to_bf16_bits(v[2 * i + 1]) << 16);
+    for (int i = 0; i < 4; ++i) r[i] = pk_bf16(v[2 * i], v[2 * i + 1]);
     return r;
   }
 };

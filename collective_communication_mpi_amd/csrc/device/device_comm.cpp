@@ -1083,6 +1083,26 @@ void DeviceComm::inbox_to_local(uint64_t inbox, uint64_t out, uint64_t nbytes, i
                         grid_(nbytes / size_, max_blocks), S(stream));
 }
 
+void DeviceComm::inbox_mean(uint64_t inbox, uint64_t out, uint64_t nbytes, int rows, uint64_t stream, int max_blocks) {
+  // nbytes: the whole fp32 z (rows of 16 floats); every owner's block holds whole sequences
+  const uint64_t shard = nbytes / (size_ > 0 ? size_ : 1);
+  if (size_ < 2 || rows < 1 || nbytes % (64ull * rows * size_) || inbox % 16 || out % 16 || nbytes >= 0x7ffffff0ull)
+    throw std::invalid_argument("ccmpi: inbox_mean needs >= 2 ranks, whole sequences (rows x 16 fp32) per rank, "
+                                "16-B aligned buffers");
+  CCMPI_HIP_CHECK(hipSetDevice(device_));
+  uint64_t ic = 0, oc = 0;
+  const uint64_t out_bytes = nbytes / rows;
+  {
+    DynScope dyn_scope(this, true);
+    ic = code_of_(inbox, nbytes);
+    oc = code_of_(out, out_bytes);
+  }
+  if (!ic || !oc) throw std::invalid_argument("ccmpi: inbox_mean: the inbox and the output must be symmetric heap blocks");
+  const uint64_t groups = shard / (64ull * rows);
+  const int grid = std::max(1, std::min<int>((int)((groups * 4 + 255) / 256), max_blocks > 0 ? max_blocks : 64));
+  launch_inbox_mean(args_(ic, oc, reinterpret_cast<char*>(out), nbytes, rows), size_, grid, S(stream));
+}
+
 uint32_t DeviceComm::error_code() {
   CCMPI_HIP_CHECK(hipSetDevice(device_));
   CCMPI_HIP_CHECK(hipDeviceSynchronize());

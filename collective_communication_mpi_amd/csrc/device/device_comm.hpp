@@ -149,6 +149,9 @@ class DeviceComm {
   // p slots in rank order and pulls every reduced block into `out` (a local tensor).
   std::vector<uint64_t> push_targets(uint64_t inbox, uint64_t nbytes);
   void inbox_to_local(uint64_t inbox, uint64_t out, uint64_t nbytes, int dtype, uint64_t stream, int max_blocks);
+  // TP sum of pushed per-token rows + mean over each group of `rows` rows, fanned out to every
+  // rank's `out` (symmetric, nbytes / rows bytes): the fused-fc_o logits (k_inbox_mean)
+  void inbox_mean(uint64_t inbox, uint64_t out, uint64_t nbytes, int rows, uint64_t stream, int max_blocks);
   uint64_t code_of_public(uint64_t ptr, uint64_t nbytes) const { return code_of_(ptr, nbytes); }
   bool fused_ready() const { return fused_tab_dev_ != nullptr && fused_inbox_bytes_ > 0; }
 

@@ -144,7 +144,7 @@ __device__ __forceinline__ void store_direct(const GemmArgs& g, const floatx4 (&
           }
           uint32_t w[4];
 #pragma unroll
-          for (int q = 0; q < 4; ++q) w[q] = f32_to_bf16_bits(v[2 * q]) | (f32_to_bf16_bits(v[2 * q + 1]) << 16);
+          for (int q = 0; q < 4; ++q) w[q] = pk_bf16(v[2 * q], v[2 * q + 1]);
           *reinterpret_cast<uint4*>(C) = uint4{w[0], w[1], w[2], w[3]};
         } else {
           float4* C = reinterpret_cast<float4*>(reinterpret_cast<float*>(g.C) + (size_t)row * g.ldc + col);
@@ -201,7 +201,7 @@ __device__ __forceinline__ void store_direct_fast(const GemmArgs& g, const float
         if constexpr (OUT_BF16) {
           uint32_t w[4];
 #pragma unroll
-          for (int q = 0; q < 4; ++q) w[q] = f32_to_bf16_bits(v[2 * q]) | (f32_to_bf16_bits(v[2 * q + 1]) << 16);
+          for (int q = 0; q < 4; ++q) w[q] = pk_bf16(v[2 * q], v[2 * q + 1]);
           *reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(g.C) + (size_t)row * g.ldc + col) =
               uint4{w[0], w[1], w[2], w[3]};
         } else {
@@ -592,7 +592,7 @@ __device__ __forceinline__ uint4 patch_chunk(const PatchSrc& ps, int m, int ch) 
       else if (cc == pp || cc == pp + 1 + s) v = 1.f;
       v2[hh] = v;
     }
-    w[q] = f32_to_bf16_bits(v2[0]) | (f32_to_bf16_bits(v2[1]) << 16);
+    w[q] = pk_bf16(v2[0], v2[1]);
   }
   return uint4{w[0], w[1], w[2], w[3]};
 }
@@ -718,7 +718,7 @@ __global__ void __launch_bounds__(SK_NT) k_gemm_smallk(GemmArgs g, int kp, Patch
             if constexpr (FAST >= 2) {
               uint32_t w[4];
 #pragma unroll
-              for (int q = 0; q < 4; ++q) w[q] = f32_to_bf16_bits(v[2 * q]) | (f32_to_bf16_bits(v[2 * q + 1]) << 16);
+              for (int q = 0; q < 4; ++q) w[q] = pk_bf16(v[2 * q], v[2 * q + 1]);
               uint4* dst = reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(g.C) + (size_t)row * g.ldc + col);
               if constexpr (FAST == 3) {  // streaming (non-temporal) store: A/B knob for the write-bound case
                 typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
@@ -757,7 +757,7 @@ __global__ void __launch_bounds__(SK_NT) k_gemm_smallk(GemmArgs g, int kp, Patch
             }
             uint32_t w[4];
 #pragma unroll
-            for (int q = 0; q < 4; ++q) w[q] = f32_to_bf16_bits(v[2 * q]) | (f32_to_bf16_bits(v[2 * q + 1]) << 16);
+            for (int q = 0; q < 4; ++q) w[q] = pk_bf16(v[2 * q], v[2 * q + 1]);
             *reinterpret_cast<uint4*>(C) = uint4{w[0], w[1], w[2], w[3]};
           } else {
             float4* C = reinterpret_cast<float4*>(reinterpret_cast<float*>(g.C) + (size_t)row * g.ldc + col);

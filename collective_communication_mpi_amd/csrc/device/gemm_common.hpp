@@ -79,10 +79,10 @@ __device__ __forceinline__ void store_rows(const GemmArgs& g, const float* tile,
             const uint32_t ow[4] = {old.x, old.y, old.z, old.w};
 #pragma unroll
             for (int q = 0; q < 4; ++q)
-              w[q] = f32_to_bf16_bits(src[2 * q] + bf16_lo(ow[q])) | (f32_to_bf16_bits(src[2 * q + 1] + bf16_hi(ow[q])) << 16);
+              w[q] = pk_bf16(src[2 * q] + bf16_lo(ow[q]), src[2 * q + 1] + bf16_hi(ow[q]));
           } else {
 #pragma unroll
-            for (int q = 0; q < 4; ++q) w[q] = f32_to_bf16_bits(src[2 * q]) | (f32_to_bf16_bits(src[2 * q + 1]) << 16);
+            for (int q = 0; q < 4; ++q) w[q] = pk_bf16(src[2 * q], src[2 * q + 1]);
           }
           *reinterpret_cast<uint4*>(C) = uint4{w[0], w[1], w[2], w[3]};
         } else {
@@ -139,7 +139,7 @@ __device__ __forceinline__ void store_rows_fast(const GemmArgs& g, const float* 
     if constexpr (OUT_BF16) {
       uint32_t w[4];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) w[q] = f32_to_bf16_bits(src[2 * q]) | (f32_to_bf16_bits(src[2 * q + 1]) << 16);
+      for (int q = 0; q < 4; ++q) w[q] = pk_bf16(src[2 * q], src[2 * q + 1]);
       *reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(g.C) + (size_t)row * g.ldc + col) = uint4{w[0], w[1], w[2], w[3]};
     } else {
       *reinterpret_cast<float4*>(reinterpret_cast<float*>(g.C) + (size_t)row * g.ldc + col) =

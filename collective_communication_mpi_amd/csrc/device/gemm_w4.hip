@@ -82,7 +82,7 @@ __device__ __forceinline__ void tile_coords(int wg, int tiles_m, int tiles_n, in
 }
 
 __device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {
-  return f32_to_bf16_bits(a) | (f32_to_bf16_bits(b) << 16);
+  return pk_bf16(a, b);
 }
 
 // two floats -> packed bf16 (RNE, NaN kept) in one v_cvt_pk_bf16_f32
@@ -479,7 +479,7 @@ __global__ void __launch_bounds__(WNT, 1) k_gemm_w4(W4Args wa) {
             }
             uint32_t w[4];
 #pragma unroll
-            for (int q = 0; q < 4; ++q) w[q] = f32_to_bf16_bits(v[2 * q]) | (f32_to_bf16_bits(v[2 * q + 1]) << 16);
+            for (int q = 0; q < 4; ++q) w[q] = pk_bf16(v[2 * q], v[2 * q + 1]);
             *reinterpret_cast<uint4*>(C) = uint4{w[0], w[1], w[2], w[3]};
           } else {
             float* C = reinterpret_cast<float*>(g.C) + (size_t)row * g.ldc + col;
@@ -1102,7 +1102,7 @@ __global__ void __launch_bounds__(WNT, 1) k_gemm_w4r(W4Args wa) {
               }
               uint32_t w[4];
 #pragma unroll
-              for (int q = 0; q < 4; ++q) w[q] = f32_to_bf16_bits(v[2 * q]) | (f32_to_bf16_bits(v[2 * q + 1]) << 16);
+              for (int q = 0; q < 4; ++q) w[q] = pk_bf16(v[2 * q], v[2 * q + 1]);
               *reinterpret_cast<uint4*>(C) = uint4{w[0], w[1], w[2], w[3]};
             } else {
               float* C = reinterpret_cast<float*>(g.C) + (size_t)row * ldc + col;

@@ -35,7 +35,7 @@ __device__ __forceinline__ float sigmoid_fast(float x) {
 }
 
 __device__ __forceinline__ uint32_t pack_bf16(float lo, float hi) {
-  return f32_to_bf16_bits(lo) | (f32_to_bf16_bits(hi) << 16);
+  return pk_bf16(lo, hi);
 }
 
 __global__ void __launch_bounds__(256) k_swiglu_fwd(const uint16_t* __restrict__ h, uint16_t* __restrict__ a,

@@ -166,9 +166,10 @@ def bench_forward(comm, tp: int = 2, batch: int = 2048, steps: int = 20, warmup:
 
 def fc_o_forms_agree(comm, tp: int, batch: int) -> dict:
     """Collective: one forward of the per-token fc_o in both TP forms ("plain": kernel +
-    all-reduce of z; "push": kernel pushes row blocks into the owners' inboxes + inbox-to-
-    local) on the same input; the all-reduced z and the logits must be bitwise equal on every
-    rank.  Returns {"equal": bool, "max_abs_diff": float}."""
+    all-reduce of z + ordered token mean; "push": kernel pushes row blocks into the owners'
+    inboxes, the owners reduce them to the sequences' logits and fan those out) on the same
+    input; the logits (and z, where both forms keep it) must be bitwise equal on every rank.
+    Returns {"equal": bool, "max_abs_diff": float}."""
     from .. import mpi as MPI
 
     hc = _hc(comm)
@@ -179,11 +180,13 @@ def fc_o_forms_agree(comm, tp: int, batch: int) -> dict:
         layer.cfg.tp_fc_o_form = form
         logits = layer.forward_images(xb, cfg.batch, save=False)
         torch.cuda.synchronize()
-        out[form] = (layer._zt.clone(), logits.clone(), layer._zt_form)
+        z = layer._zt
+        out[form] = (None if z is None else z.clone(), logits.clone(), layer._zt_form)
     zp, lp, fp = out["plain"]
     zq, lq, fq = out["push"]
-    eq = int(fp == "plain" and fq == "push" and torch.equal(zp, zq) and torch.equal(lp, lq))
-    diff = float((zp - zq).abs().max().item())
+    z_eq = zp is None or zq is None or torch.equal(zp, zq)
+    eq = int(fp == "plain" and fq == "push" and z_eq and torch.equal(lp, lq))
+    diff = float((lp - lq).abs().max().item())
     return {"equal": bool(hc.allreduce(eq, op=MPI.MIN)), "max_abs_diff": hc.allreduce(diff, op=MPI.MAX)}
 
 

@@ -378,8 +378,9 @@ class MnistTPLayer:
                 # logits = mean over the S tokens of the all-reduced z (o_b is in z, TP rank 0),
                 # kept in zp for the fused loss head
                 zp = self._buf("zp", (B, cfg.out_pad), torch.float32, self.tp_dev)
-                if z is not None:  # (None: the fused kernel already wrote the mean into zp)
-                    torch.mean(z.view(B, S, cfg.out_pad), dim=1, out=zp)
+                if z is not None:  # (None: the kernel / inbox_mean already wrote the mean into zp)
+                    # ordered sum over the tokens: bitwise the push form's inbox_mean
+                    D.rows_mean(z.data_ptr(), z.stride(0), zp.data_ptr(), zp.stride(0), B, S, cfg.out_pad, st)
                 logits = zp[:, : cfg.n_classes]
             else:
                 logits = z.view(B, S, cfg.out_pad)[:, :, : cfg.n_classes].mean(dim=1)
@@ -493,8 +494,10 @@ class MnistTPLayer:
         TP sum of z (B*S x 16 fp32, o_b added by TP rank 0): an all-reduce ("plain"), or the
         kernel pushes every row block into its owner's inbox and the inbox-to-local two-shot
         completes it ("push", reference model/func_impl.py:94-109's output path, with the
-        communication under the attention).  Leaves the summed z in ``self._zt`` (None when
-        the fused kernel wrote the token mean straight into zp: TP = 1)."""
+        communication under the attention; the owners then reduce their row block to the
+        sequences' logits and fan those out -- ``DeviceComm.inbox_mean`` -- so z is never
+        gathered).  Leaves the summed z in ``self._zt`` (None when the logits went straight
+        into zp: the push form, and the fused kernel's in-kernel mean at TP = 1)."""
         cfg = self.cfg
         S = cfg.seq
         M = B * S
@@ -516,7 +519,8 @@ class MnistTPLayer:
                 D.attn_qkv_fwd(0 if img is not None else xp.data_ptr(), xp.stride(0), cfg.kp, weff.data_ptr(),
                                weff.stride(0), bq.data_ptr(), qkv.data_ptr() if keep else 0, qkv.stride(0),
                                lse.data_ptr(), B, S, self.hl, cfg.head_dim, 1.0 / math.sqrt(cfg.head_dim),
-                               pool.data_ptr(), pool.stride(0), wo, ld_wo, n_out, bo, ztok, ld_zt, zrows, list(zpush),
+                               pool.data_ptr() if keep else 0, pool.stride(0),  # pool: only the backward reads it
+                               wo, ld_wo, n_out, bo, ztok, ld_zt, zrows, list(zpush),
                                stream, img=0 if img is None else img.data_ptr(),
                                xq_out=xp.data_ptr() if (img is not None and keep) else 0, zmean=zmean,
                                ld_zmean=ld_zmean)
@@ -528,8 +532,16 @@ class MnistTPLayer:
                 self._bufs[key] = self.tp_dev.dc.push_targets(inbox.data_ptr(), inbox.numel() * 4)
             s = self.tp_dev._stream()
             fwd(*args, s, zrows=M // cfg.tp, zpush=self._bufs[key], **kw)
-            self.tp_dev.dc.inbox_to_local(inbox.data_ptr(), z.data_ptr(), inbox.numel() * 4, 10, s,
+            if self._fused_fc_o_bwd():
+                # the owners sum their row block AND average each sequence's rows, then fan the
+                # B / tp logit rows out to every rank (k_inbox_mean): z itself is never gathered
+                zp = self._buf("zp", (B, cfg.out_pad), torch.float32, self.tp_dev)
+                self.tp_dev.dc.inbox_mean(inbox.data_ptr(), zp.data_ptr(), inbox.numel() * 4, S, s,
                                           self.tp_dev._budget(None))
+                z = None
+            else:
+                self.tp_dev.dc.inbox_to_local(inbox.data_ptr(), z.data_ptr(), inbox.numel() * 4, 10, s,
+                                              self.tp_dev._budget(None))
         elif self.tp_dev is None and qkv_from is not None:
             # local form (TP = 1): nothing to sum across ranks, so the fused kernel reduces z to
             # the logits (mean over the tokens) itself and z is never stored

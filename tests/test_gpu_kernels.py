@@ -891,3 +891,23 @@ def test_gemm_nt_long_k_dispatch():
     b = (torch.randn(N, K, device="cuda", generator=g) / K ** 0.5).bfloat16()
     y = gemm_nt(a, b, out_dtype=torch.bfloat16)
     torch.testing.assert_close(y.float(), _ref(a, b), rtol=1.6e-2, atol=2e-2)
+
+
+@pytest.mark.parametrize("groups,S,ncol,ld", [(2048, 16, 16, 16), (7, 9, 8, 12), (1, 1, 4, 4)])
+def test_rows_mean_ordered(groups, S, ncol, ld):
+    """Token mean of the per-token logits (k_rows_mean): the in-order fp32 sum / S -- the
+    order DeviceComm.inbox_mean uses, so the plain and push TP forms agree bitwise."""
+    from collective_communication_mpi_amd import _native
+
+    z = torch.randn(groups * S, ld, device="cuda")
+    out = torch.full((groups, ld + 4), float("nan"), device="cuda")
+    _native.device().rows_mean(z.data_ptr(), ld, out.data_ptr(), out.stride(0), groups, S, ncol,
+                               torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    zz = z.view(groups, S, ld)[:, :, :ncol]
+    ref = torch.zeros(groups, ncol, device="cuda")
+    for i in range(S):
+        ref = ref + zz[:, i]
+    # (a tensor divisor: torch turns division by a Python scalar into a reciprocal multiply)
+    assert torch.equal(out[:, :ncol], ref / torch.full_like(ref, float(S)))
+    assert torch.isnan(out[:, ncol:]).all()
