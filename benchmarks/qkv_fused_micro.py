@@ -33,6 +33,8 @@ def main():
     ap.add_argument("--B", type=int, default=2048)
     ap.add_argument("--H", type=int, default=4)
     ap.add_argument("--only", default="")
+    ap.add_argument("--grid", type=int, default=0, help="only this persistent grid size")
+    ap.add_argument("--train", type=int, default=-1, help="0/1: only inference / training stores")
     args = ap.parse_args()
     dev = _native.device()
     st = torch.cuda.current_stream().cuda_stream
@@ -73,10 +75,10 @@ def main():
     rows = []
     if not args.only or args.only == "unfused":
         rows.append(dict(kernel="unfused", us=timed(unfused, args.iters)))
-    for cap in (256, 512, 1024, 2048):
+    for cap in ((args.grid,) if args.grid else (256, 512, 1024, 2048)):
         dev.attn_set_qkv_grid(cap)
         for mode in ("rows", "img"):
-            for train in (False, True):
+            for train in ((bool(args.train),) if args.train >= 0 else (False, True)):
                 for mean in (False, True):
                     if args.only and args.only != mode:
                         continue

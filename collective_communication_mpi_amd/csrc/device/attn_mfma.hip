@@ -96,6 +96,28 @@ __device__ __forceinline__ void put_rows(uint16_t* T, const bf16x8 (&x)[D / 32],
   for (int kk = 0; kk < D / 32; ++kk) *reinterpret_cast<bf16x8*>(T + c * LD + 32 * kk + 8 * g) = x[kk];
 }
 
+// Reductions across the 16-lane rows of a wave on gfx950's v_permlane16/32_swap (VALU, no LDS
+// round trip like the ds_bpermute behind __shfl_xor): with both operands = v, the two results
+// hold, on every lane, v and its partner's v (lane ^ 16, resp. lane ^ 32), so op(r0, r1) is
+// the pair reduction -- the same operand order on both partners, bitwise equal to the
+// shuffle form.
+__device__ __forceinline__ float pair16_sum(float v) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float pair32_sum(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float pair16_max(float v) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float pair32_max(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+
 __device__ __forceinline__ s4 ld_s4(const uint16_t* p, bool ok) {
   const uint2 z = ok ? *reinterpret_cast<const uint2*>(p) : uint2{0, 0};
   return __builtin_bit_cast(s4, z);
@@ -138,6 +160,10 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
   __shared__ __attribute__((aligned(16))) float imgs[IMG ? 2 : 1][IMG ? kImgPieces * 256 : 1];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
   const int S = a.S, HD = a.Hl * D, npairs = a.B * a.Hl;
+  // fused QKV: Hl | 4, so pair -> (sequence, head) is a shift and a mask, not a division
+  const int lhl = a.Hl == 4 ? 2 : a.Hl == 2 ? 1 : 0;
+  auto div_hl = [&](int x) { return QKV ? x >> lhl : x / a.Hl; };
+  auto mod_hl = [&](int x) { return QKV ? x & (a.Hl - 1) : x % a.Hl; };
   // per-token fc_o: z rows stored (ztok), pushed (zrows), or -- fused QKV only -- reduced to
   // their mean over the S tokens in-kernel (zp: the local TP = 1 form, z never stored)
   const bool tok = a.ztok || a.zrows || (QKV && a.zp);
@@ -149,7 +175,7 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
   // entries (classes 4g..4g+3, features 16nt + c) are loaded once, packed as bf16 pairs
   uint32_t wpk[NT][2];
   if (!QKV && a.zp) {
-    const int hw = wave % a.Hl;
+    const int hw = mod_hl(wave);
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
@@ -168,7 +194,7 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
   // the B operand of the 16x16x16 MFMA -- lane (c, g): class c, features 16 nt + 4 g .. +3
   s4 wo16[QKV ? NT : 1];
   if (tok) {
-    const int hw = wave % a.Hl;
+    const int hw = mod_hl(wave);
     if constexpr (QKV) {
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt)
@@ -188,13 +214,17 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
   int it = 0;    // iteration parity: double-buffered LDS (z tiles, images)
   bf16x8 xn[2];  // the next iteration's patch rows (lane (c, g): token c, depth 32 kk + 8 g ..)
   s4 xtn;
+  // fused QKV bias: two spare depth columns kb, kb + 1 (kq <= 72) hold X = 1 and W = the fp32
+  // bias split into bf16 hi + lo parts, so the bias rides in the MFMA's fp32 accumulation (to
+  // ~2^-17 relative -- far below the bf16 rounding of q | k | v) instead of 12 per-tile loads
+  const int kb = a.kq > 64 ? a.kq : 64, gb = (kb - 64) >> 2;
   auto load_x = [&](int p) {
     const bool ok = p < npairs && c < S;
     if constexpr (IMG) {
       // MNIST 28 x 28, 7 x 7 patches (S = 16): token c = patch (c / 4, c % 4); column cc < 49
       // is pixel (cc / 7, cc % 7) of the patch, 49 the bias 1, 50 + c the position one-hot.
       // The image is this iteration's LDS copy (staged one iteration ahead by LDS-DMA).
-      const float* im = imgs[it] + (wave / a.Hl) * 784 + (c >> 2) * 196 + (c & 3) * 7;
+      const float* im = imgs[it] + (div_hl(wave)) * 784 + (c >> 2) * 196 + (c & 3) * 7;
       // the 20 per-lane pixel offsets are loop-invariant: hide g from the optimizer so they are
       // recomputed per call rather than hoisted into 20 live registers (which spilled)
       int g = lane >> 4;
@@ -203,7 +233,7 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
         float v = 0.f;
         if (ok) {
           if (cc < 49) v = im[(cc / 7) * 28 + cc % 7];
-          else if (cc == 49 || cc == 50 + c) v = 1.f;
+          else if (cc == 49 || cc == 50 + c) v = 1.f;  // (the fused bias columns are set below)
         }
         return v;
       };
@@ -220,20 +250,24 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
       xn[1] = __builtin_bit_cast(bf16x8, w1);
       xtn = __builtin_bit_cast(s4, wt);
     } else {
-      const uint16_t* row = a.xq + (size_t)(ok ? (p / a.Hl) * S + c : 0) * a.ld_xq;
+      const uint16_t* row = a.xq + (size_t)(ok ? div_hl(p) * S + c : 0) * a.ld_xq;
       xn[0] = ld_row16(row + 8 * g, ok && 8 * g < a.kq);
       xn[1] = ld_row16(row + 32 + 8 * g, ok && 32 + 8 * g < a.kq);
       xtn = ld_s4(row + 64 + 4 * g, ok && 64 + 4 * g < a.kq);
+    }
+    if (g == gb) {  // the bias columns kb, kb + 1 of X are ones
+      xtn[0] = (short)0x3F80;
+      xtn[1] = (short)0x3F80;
     }
   };
   // LDS-DMA of the images of the iteration starting at pair p0 into buffer buf: straight from
   // global memory into LDS, no VGPRs held; bytes past the batch read as zero (buffer bounds)
   auto stage_imgs = [&](int buf, int p0) {
     if constexpr (IMG) {
-      const int nseq = WPB / a.Hl, pieces = (nseq * 784 * 4 + 1023) / 1024;
+      const int nseq = div_hl(WPB), pieces = (nseq * 784 * 4 + 1023) / 1024;
       // (the descriptor starts at the iteration's first image: the bounds check covers
       // voffset, so the batch end clips exactly)
-      const int b0 = p0 / a.Hl;
+      const int b0 = div_hl(p0);
       const Rsrc rs = make_rsrc(uniform_ptr(reinterpret_cast<char*>(const_cast<float*>(a.img + (size_t)b0 * 784))), (uint32_t)((size_t)(a.B - b0) * 784 * 4));
       for (int pc = wave; pc < pieces; pc += WPB)
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rs.r, (__attribute__((address_space(3))) void*)(imgs[buf] + pc * 256),
@@ -241,7 +275,7 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
     }
   };
   if constexpr (QKV) {
-    const int hw = wave % a.Hl;
+    const int hw = mod_hl(wave);
 #pragma unroll
     for (int sel = 0; sel < 3; ++sel)
 #pragma unroll
@@ -251,6 +285,12 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
         wf[sel][nt][0] = ld_row16(w + 8 * g, 8 * g < a.kq);
         wf[sel][nt][1] = ld_row16(w + 32 + 8 * g, 32 + 8 * g < a.kq);
         wtl[sel][nt] = ld_s4(w + 64 + 4 * g, 64 + 4 * g < a.kq);
+        if (g == gb) {
+          const float bias = a.bq[f];
+          const uint32_t hi = f32_to_bf16_bits(bias);
+          wtl[sel][nt][0] = (short)hi;
+          wtl[sel][nt][1] = (short)f32_to_bf16_bits(bias - __uint_as_float(hi << 16));
+        }
       }
     if constexpr (!IMG) load_x(blockIdx.x * WPB + wave);
     if constexpr (IMG) {
@@ -265,37 +305,36 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
    s4 xt;
    if constexpr (QKV) {
     // (image mode builds this iteration's rows now, from LDS: the prefetch is the images' DMA)
-    if constexpr (IMG) load_x(pr);
+    if constexpr (IMG) {
+      load_x(pr);
+      // the next iteration's images (the body issues no further global loads, so nothing
+      // waits on this DMA before the epilogue's vmcnt(0); a wave with no pair now has no next
+      // iteration either, so every piece is issued)
+      if (base + stride < npairs) stage_imgs(it ^ 1, base + stride);
+    }
     xr[0] = xn[0];
     xr[1] = xn[1];
     xt = xtn;
     if constexpr (!IMG) load_x(pr + stride);
    }
    if (pr < npairs) {
-    const int b = pr / a.Hl, h = pr % a.Hl;
+    const int b = div_hl(pr), h = mod_hl(pr);
     bf16x8 qr[NK], kr[NK];
     if constexpr (QKV) {
-      // sel's [16 tokens][D] block of X W_h^T + b, rounded to bf16, into tile T -- computed
-      // transposed, (W_h X^T), so a lane's accumulator holds 4 consecutive features of one
-      // token: 2 packed conversions + one 8-B LDS store per 16 x 16 tile instead of 4 + 4
-      // 2-B stores.  The bias is re-read per iteration (L1 hits; an opaque pointer keeps the
-      // compiler from hoisting loop-invariant registers)
-      const float* bqp = a.bq + h * D + 4 * g;
-      asm volatile("" : "+v"(bqp));
+      // sel's [16 tokens][D] block of X W_h^T + b (the bias via the tail's bias columns),
+      // rounded to bf16, into tile T -- computed transposed, (W_h X^T), so a lane's accumulator
+      // holds 4 consecutive features of one token: 2 packed conversions + one 8-B LDS store
+      // per 16 x 16 tile instead of 4 + 4 2-B stores.  (The first version re-read the bias per
+      // tile: flat loads + vmcnt(0) waits that also drained the X prefetch, 12 per pair.)
       auto proj = [&](int sel, uint16_t* T) {
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt) {
-          // (a compiler memory barrier per tile: the 12 bias loads are not all hoisted up front)
-          const float* bp = bqp + sel * HD + 16 * nt;
-          asm volatile("" : "+v"(bp)::"memory");
-          const float4 bz = *reinterpret_cast<const float4*>(bp);
           // (the 16x16x16 tail gets its own accumulator: chaining it onto the 16x16x32
           // accumulator lost rows -- the compiler emits no wait states for that srcC hazard)
           const f4 tl = mma16(wtl[sel][nt], xt, f4{0.f, 0.f, 0.f, 0.f});
           f4 acc = mma32(wf[sel][nt][0], xr[0], f4{0.f, 0.f, 0.f, 0.f});
           acc = mma32(wf[sel][nt][1], xr[1], acc);  // acc[r] = [feature 16 nt + 4g + r][token c]
-          const uint2 pk = {pk_bf16(acc[0] + tl[0] + bz.x, acc[1] + tl[1] + bz.y),
-                            pk_bf16(acc[2] + tl[2] + bz.z, acc[3] + tl[3] + bz.w)};
+          const uint2 pk = {pk_bf16(acc[0] + tl[0], acc[1] + tl[1]), pk_bf16(acc[2] + tl[2], acc[3] + tl[3])};
           *reinterpret_cast<uint2*>(T + c * LD + 16 * nt + 4 * g) = pk;
         }
       };
@@ -319,14 +358,26 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
         rows_out<D, LD>(V, qo + HD, a.ld_qkv, S, lane);
       }
       __builtin_amdgcn_wave_barrier();
-      proj(2, V);
-      // the next iteration's images, issued after this iteration's last global loads (the
-      // bias): vmcnt retires in order, so waiting on a later load would wait on the DMA too.
-      // (a wave with no pair now has no next iteration either, so every piece is issued)
-      if constexpr (IMG)
-        if (base + stride < npairs) stage_imgs(it ^ 1, base + stride);
+      // v un-transposed (acc[r] = v[token 4g + r][feature 16 nt + c]) into the V^T tile
+      // ([D features][16 tokens], one 8-B store per lane per tile): the PV MFMA's operand
+      // (keys 4g .. 4g+3 of one feature) is then ONE 8-B LDS read instead of four 2-B reads.
+      // For a backward, v also goes row-major into the (free) O tile for the qkv store.
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        const f4 tl = mma16(xt, wtl[2][nt], f4{0.f, 0.f, 0.f, 0.f});
+        f4 acc = mma32(xr[0], wf[2][nt][0], f4{0.f, 0.f, 0.f, 0.f});
+        acc = mma32(xr[1], wf[2][nt][1], acc);
+        const uint2 pk = {pk_bf16(acc[0] + tl[0], acc[1] + tl[1]), pk_bf16(acc[2] + tl[2], acc[3] + tl[3])};
+        *reinterpret_cast<uint2*>(V + (16 * nt + c) * 16 + 4 * g) = pk;
+        if (qo) {
+          O[(4 * g + 0) * LD + 16 * nt + c] = (uint16_t)(pk.x & 0xffffu);
+          O[(4 * g + 1) * LD + 16 * nt + c] = (uint16_t)(pk.x >> 16);
+          O[(4 * g + 2) * LD + 16 * nt + c] = (uint16_t)(pk.y & 0xffffu);
+          O[(4 * g + 3) * LD + 16 * nt + c] = (uint16_t)(pk.y >> 16);
+        }
+      }
       __builtin_amdgcn_wave_barrier();
-      if (qo) rows_out<D, LD>(V, qo + 2 * HD, a.ld_qkv, S, lane);
+      if (qo) rows_out<D, LD>(O, qo + 2 * HD, a.ld_qkv, S, lane);
     } else {
       const uint16_t* qb = a.qkv + (size_t)b * S * a.ld_qkv + h * D;
       bf16x8 vr[NK];
@@ -348,16 +399,14 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
       x[r] = (4 * g + r < S) ? st[r] * a.scale : -INFINITY;
       m = fmaxf(m, x[r]);
     }
-    m = fmaxf(m, __shfl_xor(m, 16));
-    m = fmaxf(m, __shfl_xor(m, 32));
+    m = pair32_max(pair16_max(m));
     float e[4], s = 0.f;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       e[r] = __expf(x[r] - m);
       s += e[r];
     }
-    s += __shfl_xor(s, 16);
-    s += __shfl_xor(s, 32);
+    s = pair32_sum(pair16_sum(s));
     const float inv = 1.f / s;
     if (g == 0 && c < S) a.lse[(size_t)pr * S + c] = m + __logf(s);
     const s4 pa = pack4(e[0] * inv, e[1] * inv, e[2] * inv, e[3] * inv);  // A[i = c][j = 4g + jj]
@@ -367,7 +416,8 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
       // K axis, so z = bf16(O) W_o^T chains straight from the registers (no LDS round trip)
       f4 ot[NT];
 #pragma unroll
-      for (int nt = 0; nt < NT; ++nt) ot[nt] = mma16(tile_b<LD>(V, g, 16 * nt + c), pa, f4{0.f, 0.f, 0.f, 0.f});
+      for (int nt = 0; nt < NT; ++nt)
+        ot[nt] = mma16(*reinterpret_cast<const s4*>(V + (16 * nt + c) * 16 + 4 * g), pa, f4{0.f, 0.f, 0.f, 0.f});
       f4 zt = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) zt = mma16(pack4(ot[nt][0], ot[nt][1], ot[nt][2], ot[nt][3]), wo16[nt], zt);
@@ -380,12 +430,11 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
         // transposed accumulators pushed the kernel past 256 VGPRs.)
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt) {
-          const f4 on = mma16(pa, tile_b<LD>(V, g, 16 * nt + c), f4{0.f, 0.f, 0.f, 0.f});
+          const f4 on = mma16(pa, *reinterpret_cast<const s4*>(V + (16 * nt + c) * 16 + 4 * g), f4{0.f, 0.f, 0.f, 0.f});
           float cs = 0.f;
 #pragma unroll
           for (int r = 0; r < 4; ++r) cs += (4 * g + r < S) ? on[r] : 0.f;
-          cs += __shfl_xor(cs, 16);
-          cs += __shfl_xor(cs, 32);
+          cs = pair32_sum(pair16_sum(cs));
           if (g == 0) a.pool[(size_t)b * a.ld_pool + h * D + 16 * nt + c] = (uint16_t)f32_to_bf16_bits(cs / (float)S);
         }
       }
@@ -403,8 +452,7 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
         float cs = 0.f;
 #pragma unroll
         for (int r = 0; r < 4; ++r) cs += (4 * g + r < S) ? o[nt][r] : 0.f;
-        cs += __shfl_xor(cs, 16);
-        cs += __shfl_xor(cs, 32);
+        cs = pair32_sum(pair16_sum(cs));
         const uint32_t pb = f32_to_bf16_bits(cs / (float)S);
         if (g == 0) a.pool[(size_t)b * a.ld_pool + h * D + 16 * nt + c] = (uint16_t)pb;
         if (!QKV && a.zp) {
@@ -455,7 +503,7 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
     const int i = lane >> 2, q = (lane & 3) * 4, w = wave * a.Hl;
     const int prw = base + w;
     if (w < WPB && prw < npairs) {
-      const int b = prw / a.Hl;
+      const int b = div_hl(prw);
       float v[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) v[r] = (a.bo && q + r < a.n_out) ? a.bo[q + r] : 0.f;
@@ -485,8 +533,9 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           m[r] = i < S ? v[r] : 0.f;
-#pragma unroll
-          for (int off = 4; off < 64; off <<= 1) m[r] += __shfl_xor(m[r], off);
+          m[r] += __shfl_xor(m[r], 4);
+          m[r] += __shfl_xor(m[r], 8);
+          m[r] = pair32_sum(pair16_sum(m[r]));
         }
         if (i == 0) {
           const float n = (float)S;
@@ -498,11 +547,11 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
    if (!QKV && a.zp) {  // sum the Hl heads of each sequence in rank order (deterministic) and add the bias
     __syncthreads();  // (the next iteration writes the other buffer: one barrier per iteration)
     const int t = threadIdx.x, w = t >> 4, cls = t & 15, prw = base + w;
-    if (t < WPB * 16 && prw < npairs && prw % a.Hl == 0 && cls < a.n_out) {
+    if (t < WPB * 16 && prw < npairs && mod_hl(prw) == 0 && cls < a.n_out) {
       float acc = 0.f;
       for (int k = 0; k < a.Hl; ++k) acc += zpart[it][w + k][cls];
       if (a.bo) acc += a.bo[cls];
-      a.zp[(size_t)(prw / a.Hl) * a.ld_zp + cls] = acc;
+      a.zp[(size_t)div_hl(prw) * a.ld_zp + cls] = acc;
     }
    }
   }
@@ -612,8 +661,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D == 1
       dl += PT[r] * dpT[r];          // row i = c: keys j = 4g + r in registers ...
       dl_r[r] = P[r] * dpM[r];       // row i = 4g + r: keys j = c on the lanes ...
     }
-    dl += __shfl_xor(dl, 16);        // ... and across the four lane groups
-    dl += __shfl_xor(dl, 32);
+    dl = pair32_sum(pair16_sum(dl));  // ... and across the four lane groups
 #pragma unroll
     for (int r = 0; r < 4; ++r)
 #pragma unroll
@@ -657,9 +705,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D == 1
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
       float q = bq[nt], k = bk[nt], v = bv[nt];
-      q += __shfl_xor(q, 16); q += __shfl_xor(q, 32);
-      k += __shfl_xor(k, 16); k += __shfl_xor(k, 32);
-      v += __shfl_xor(v, 16); v += __shfl_xor(v, 32);
+      q = pair32_sum(pair16_sum(q));
+      k = pair32_sum(pair16_sum(k));
+      v = pair32_sum(pair16_sum(v));
       if (g == 0) {
         red[(wave * 3 + 0) * D + 16 * nt + c] = q;
         red[(wave * 3 + 1) * D + 16 * nt + c] = k;

@@ -284,14 +284,15 @@ void attn_qkv_fwd(uint64_t xq, int ld_xq, int kq, uint64_t wq, int ld_wq, uint64
                   int ld_wo, int n_out, uint64_t bo, uint64_t ztok, int ld_zt, int zrows,
                   const std::vector<uint64_t>& zpush, uint64_t stream, uint64_t img, uint64_t xq_out, uint64_t zmean,
                   int ld_zmean) {
-  if (S < 1 || S > 16 || !(D == 32 || D == 64) || Hl < 1 || 4 % Hl || kq < 8 || kq > 80 || kq % 8 || ld_xq % 8 ||
+  if (S < 1 || S > 16 || !(D == 32 || D == 64) || Hl < 1 || 4 % Hl || kq < 8 || kq > 72 || kq % 8 || ld_xq % 8 ||
       ld_wq % 8 || ld_wo % 8 || (xq % 16) || (wq % 16) || (wo % 16) || !wo || !bq || (bq % 16) || !lse || n_out < 1 ||
       n_out > 16 ||
       ld_zt < 16 || ld_zt % 4 || (ztok % 16) || (!ztok && !zrows && !zmean) || (qkv_out && (ld_qkv % 8 || qkv_out % 16)) ||
       (zmean && (zmean % 16 || ld_zmean % 4 || ld_zmean < 16 || zrows)) ||
       false)
     throw std::invalid_argument("attention: fused QKV forward needs S <= 16, D in {32, 64}, Hl | 4, kq % 8 == 0 and "
-                                "<= 80, 16-B aligned rows, n_out <= 16, z rows of >= 16 floats (% 4), a z target");
+                                "<= 72 (the bias rides in two spare depth columns), 16-B aligned rows, n_out <= 16, "
+                                "z rows of >= 16 floats (% 4), a z target");
   if (img && (S != 16 || kq < 66 || (img % 16) || (xq_out % 16)))
     throw std::invalid_argument("attention: fused patchify is the MNIST 28x28 / 7x7 case (S = 16, kq >= 66)");
   if (!img && (xq_out || !xq)) throw std::invalid_argument("attention: patch rows xq needed (xq_out only with img)");

@@ -483,11 +483,12 @@ class MnistTPLayer:
         """The token-mode forward runs the QKV projection inside the attention kernel
         (``k_qkv_attn16_fwd``): folded weights, the fused per-token fc_o
         (CCMPI_FUSE_QKV=0: the QKV GEMM + attention kernel instead).  The kernel keeps a
-        head's folded weight in registers: head_dim <= 64, kp <= 80, local heads | 4."""
+        head's folded weight in registers: head_dim <= 64, kp <= 72 (two spare depth columns
+        carry the bias), local heads | 4."""
         cfg = self.cfg
         return (cfg.fuse_qkv and os.environ.get("CCMPI_FUSE_QKV", "1") != "0" and self._folds()
                 and cfg.fc_o_mode == "token" and self._fused_fc_o_bwd() and self._token_chunks(B) == 1
-                and cfg.seq <= 16 and cfg.head_dim in (32, 64) and cfg.kp <= 80 and 4 % self.hl == 0)
+                and cfg.seq <= 16 and cfg.head_dim in (32, 64) and cfg.kp <= 72 and 4 % self.hl == 0)
 
     def _token_fc_o_kernel(self, qkv, lse, pool, B: int, st: int, qkv_from=None) -> None:
         """Attention + per-token row-parallel fc_o in ONE kernel (``k_attn16_fwd``), then the

@@ -8,7 +8,7 @@ OUT=gpurun_out/${OUT_TAG:-r5_fourteenth}
 mkdir -p $OUT
 export TMPDIR=/tmp
 timeout -k 10 300 python3 -u -m pytest -v --timeout 120 --timeout-method thread -m gpu \
-  tests/test_gpu_kernels.py -k "attn or fold_emb or gemm_bias or cast or rows_mean" > $OUT/tests_k.log 2>&1
+  tests/test_gpu_kernels.py -k "attn or fold_emb or gemm_bias or cast or rows_mean or harness" > $OUT/tests_k.log 2>&1
 rc=$?; tail -3 $OUT/tests_k.log; [ $rc -ne 0 ] && { grep -E "FAILED|^E " $OUT/tests_k.log | head -30; exit $rc; }
 timeout -k 10 600 python3 -u -m pytest -x -v --timeout 120 --timeout-method thread -m gpu \
   tests/test_gpu_distributed.py -k "harness" > $OUT/tests.log 2>&1

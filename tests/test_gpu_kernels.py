@@ -467,7 +467,7 @@ def test_attn_token_fc_o(B, S, H, D, n_out):
                            pool.data_ptr(), pool.stride(0), st, zrows=S + 1, zpush=[tg.data_ptr()], **kw)
 
 
-@pytest.mark.parametrize("B,S,H,D,kp", [(2048, 16, 4, 64, 72), (2048, 16, 2, 64, 72), (37, 16, 1, 64, 80),
+@pytest.mark.parametrize("B,S,H,D,kp", [(2048, 16, 4, 64, 72), (2048, 16, 2, 64, 72), (37, 16, 1, 64, 64),
                                         (9, 7, 2, 32, 40), (5, 16, 4, 64, 8), (3001, 16, 4, 32, 72)])
 def test_attn_qkv_fused(B, S, H, D, kp):
     """QKV projection + attention + per-token fc_o in one kernel (the harness forward):
@@ -521,8 +521,8 @@ def test_attn_qkv_fused(B, S, H, D, kp):
                      **common)
     torch.cuda.synchronize()
     torch.testing.assert_close(zm, z.view(B, S, 16).mean(dim=1), rtol=1e-5, atol=1e-5)
-    with pytest.raises(ValueError):  # beyond the register-resident weight: kq > 80
-        dev.attn_qkv_fwd(xq=xp.data_ptr(), ld_xq=xp.stride(0), kq=88, wq=w.data_ptr(), ld_wq=w.stride(0),
+    with pytest.raises(ValueError):  # beyond the register-resident weight + bias columns: kq > 72
+        dev.attn_qkv_fwd(xq=xp.data_ptr(), ld_xq=xp.stride(0), kq=80, wq=w.data_ptr(), ld_wq=w.stride(0),
                          bq=bq.data_ptr(), qkv_out=0, ld_qkv=qkv.stride(0), ztok=z.data_ptr(), zrows=0, zpush=[],
                          **common)
 
