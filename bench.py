@@ -888,6 +888,8 @@ def harness_phase(args) -> dict:
                 harness["train_fc_o_tp_form"] = form
     harness["fwd_ms"] = round(harness["fwd_ms"], 4)
     harness["train_ms"] = round(harness.get("train_ms", float("nan")), 4)
+    if "train_ms_eager" in harness:
+        harness["train_ms_eager"] = round(harness["train_ms_eager"], 4)
     return harness
 
 

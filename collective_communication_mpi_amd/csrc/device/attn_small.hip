@@ -369,7 +369,24 @@ struct AdamArgs {
   uint64_t n;
   float lr, b1, b2, eps, wd, bc1, bc2, grad_scale;
   int zero_grad;
+  // optional [steps done, unused] on the device (a HIP-graph-captured step): t = steps + 1 is
+  // read here and a one-thread kernel launched right after advances the count -- so a
+  // replayed graph applies the right bias corrections without a host-side argument.  (A
+  // last-workgroup ticket instead cost 2000+ contended atomics on one address: 70 us.)
+  int* step_dev;
 };
+
+// the bias corrections of step t = step_dev[0] + 1 (read before this workgroup's ticket)
+__device__ __forceinline__ void adam_device_step(AdamArgs& a) {
+  if (!a.step_dev) return;
+  const float t = (float)(__hip_atomic_load(a.step_dev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1);
+  a.bc1 = 1.f - powf(a.b1, t);
+  a.bc2 = 1.f - powf(a.b2, t);
+}
+
+__global__ void k_adam_step_advance(int* step_dev) {
+  if (threadIdx.x == 0) step_dev[0] += 1;
+}
 
 // one AdamW element update on already-loaded values; returns the new bf16 bits
 __device__ __forceinline__ float adam_math(const AdamArgs& a, float pi, float gi, float& mi, float& vi) {
@@ -386,6 +403,7 @@ __device__ __forceinline__ float adam_math(const AdamArgs& a, float pi, float gi
 // transposed tile with coalesced rows.  All four state arrays are distinct
 // (restrict), and a tile's 16 elements per thread are loaded before any store.
 __global__ void __launch_bounds__(256) k_adamw(AdamArgs a, TRegions tr, int flat) {
+  adam_device_step(a);
   float* __restrict__ P = a.p;
   float* __restrict__ Gr = a.g;
   float* __restrict__ Mo = a.m;
@@ -564,14 +582,20 @@ TRegions make_tregions(const std::vector<std::tuple<uint64_t, uint64_t, uint64_t
 
 void adamw(uint64_t p, uint64_t g, uint64_t m, uint64_t v, uint64_t p16, uint64_t n, float lr, float b1, float b2,
            float eps, float wd, int step, float grad_scale, uint64_t stream,
-           const std::vector<std::tuple<uint64_t, uint64_t, uint64_t, uint64_t>>& tregions, bool zero_grad) {
+           const std::vector<std::tuple<uint64_t, uint64_t, uint64_t, uint64_t>>& tregions, bool zero_grad,
+           uint64_t step_dev) {
   const float bc1 = 1.f - powf(b1, (float)step), bc2 = 1.f - powf(b2, (float)step);
   const int flat = (int)std::min<uint64_t>((n + 255) / 256, 2048);
   const TRegions tr = make_tregions(tregions);
+  if (step_dev % 8) throw std::invalid_argument("adamw: the device step counter must be 8-B aligned");
   AdamArgs a{(float*)p, (float*)g, (float*)m, (float*)v, (uint16_t*)p16, n, lr, b1, b2, eps, wd, bc1, bc2, grad_scale,
-             zero_grad ? 1 : 0};
+             zero_grad ? 1 : 0, reinterpret_cast<int*>(step_dev)};
   hipLaunchKernelGGL(k_adamw, dim3(flat + tr.tiles[tr.n]), dim3(256), 0, (hipStream_t)stream, a, tr, flat);
   CCMPI_HIP_CHECK(hipGetLastError());
+  if (step_dev) {
+    hipLaunchKernelGGL(k_adam_step_advance, dim3(1), dim3(64), 0, (hipStream_t)stream, reinterpret_cast<int*>(step_dev));
+    CCMPI_HIP_CHECK(hipGetLastError());
+  }
 }
 
 void cast_bf16(uint64_t x, uint64_t y, uint64_t n, uint64_t stream,
@@ -614,7 +638,7 @@ void register_attn_ops(pybind11::module_& m) {
         py::arg("lr"), py::arg("b1"), py::arg("b2"), py::arg("eps"), py::arg("wd"), py::arg("step"),
         py::arg("grad_scale"), py::arg("stream"),
         py::arg("tregions") = std::vector<std::tuple<uint64_t, uint64_t, uint64_t, uint64_t>>{},
-        py::arg("zero_grad") = false, py::call_guard<py::gil_scoped_release>());
+        py::arg("zero_grad") = false, py::arg("step_dev") = 0, py::call_guard<py::gil_scoped_release>());
   m.def("cast_bf16", &cast_bf16, py::arg("x"), py::arg("y"), py::arg("n"), py::arg("stream"),
         py::arg("tregions") = std::vector<std::tuple<uint64_t, uint64_t, uint64_t, uint64_t>>{},
         py::call_guard<py::gil_scoped_release>());

@@ -848,7 +848,9 @@ class MnistTPLayer:
 
     def step(self) -> None:
         self.buckets.wait()
-        self.flat.adamw(self.cfg.lr, weight_decay=self.cfg.weight_decay, grad_scale=1.0 / self.cfg.dp)
+        # (graph_step: inside a captured training step the AdamW reads t from the device counter)
+        self.flat.adamw(self.cfg.lr, weight_decay=self.cfg.weight_decay, grad_scale=1.0 / self.cfg.dp,
+                        device_step=getattr(self, "graph_step", False))
 
 
 def local_batch(cfg: LayerConfig, x_all: np.ndarray, y_all: np.ndarray, step: int, rank: int, device):

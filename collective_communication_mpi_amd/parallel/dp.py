@@ -57,6 +57,7 @@ class FlatParams:
         self.m = torch.zeros_like(self.p32)
         self.v = torch.zeros_like(self.p32)
         self.step_count = 0
+        self._step_dev: Optional[torch.Tensor] = None  # [steps done, ticket] for graph-captured steps
         self.grad_dirty = False  # g holds values a step has not consumed (AdamW zeroes what it reads)
         self.p16_t: Dict[str, torch.Tensor] = {}
         for name in transposed:
@@ -93,13 +94,33 @@ class FlatParams:
         _native.device().cast_bf16(self.p32.data_ptr(), self.p16.data_ptr(), self.numel,
                                    torch.cuda.current_stream(self.device).cuda_stream, self._tregions)
 
+    def device_step(self) -> torch.Tensor:
+        """The device-side step counter ([steps done, ticket], int32), seeded from
+        ``step_count``.  An AdamW launched with ``device_step=True`` takes t from it and the
+        kernel's last workgroup advances it, so a HIP graph of whole training steps replays
+        with the right bias corrections; ``sync_step()`` brings ``step_count`` back."""
+        if self._step_dev is None:
+            self._step_dev = torch.zeros(2, dtype=torch.int32, device=self.device)
+        self._step_dev.fill_(0)
+        self._step_dev[0] = self.step_count
+        return self._step_dev
+
+    def sync_step(self) -> int:
+        """step_count <- the device counter (after graph replays)."""
+        if self._step_dev is not None:
+            self.step_count = int(self._step_dev[0].item())
+        return self.step_count
+
     def adamw(self, lr: float, betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0,
-              grad_scale: float = 1.0) -> None:
+              grad_scale: float = 1.0, device_step: bool = False) -> None:
         self.step_count += 1
+        if device_step and self._step_dev is None:
+            raise RuntimeError("adamw(device_step=True): call device_step() first (outside any capture)")
         _native.device().adamw_step(self.p32.data_ptr(), self.g.data_ptr(), self.m.data_ptr(), self.v.data_ptr(),
                                     self.p16.data_ptr(), self.numel, lr, betas[0], betas[1], eps, weight_decay,
                                     self.step_count, grad_scale, torch.cuda.current_stream(self.device).cuda_stream,
-                                    self._tregions, True)
+                                    self._tregions, True,
+                                    step_dev=self._step_dev.data_ptr() if device_step else 0)
         self.grad_dirty = False
 
 

@@ -251,6 +251,16 @@ def test_harness_matches_single_rank(reference_run, tmp_path, n, tp, mode):
     assert got["losses"][-1] < got["losses"][0]
 
 
+@pytest.mark.parametrize("n,tp,mode", [(1, 1, "token"), (2, 2, "token"), (2, 2, "row"), (2, 1, "token")])
+def test_harness_graph_train_matches_eager(n, tp, mode):
+    """Training steps replayed from HIP graphs (two alternating captures, device-side AdamW
+    step counter) reproduce eager steps: losses, weights, step count; TP and DP collectives
+    inside the captured step."""
+    r = run_ranks(n, py("tests/workers/graph_train_worker.py"), timeout=300,
+                  env=dict(ENV, GT_TP=str(tp), GT_MODE=mode))
+    assert "graph train OK" in r.stdout
+
+
 @pytest.mark.parametrize("n", [2, 8])
 def test_harness_fc_o_push_equals_plain(n):
     """the per-token fc_o's push form (row blocks stored into the TP
