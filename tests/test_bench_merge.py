@@ -219,3 +219,22 @@ def test_host_phase_runs_on_cpu(tmp_path):
     rec = json.loads(res.read_text())
     assert rec["ranks"] == 8 and rec["allreduce"]["all_runs_equal"] and rec["alltoall"]["all_runs_equal"]
     assert rec["allreduce"]["myAllreduce_avg_us"] > 0 and rec["alltoall"]["myAlltoall_avg_us"] > 0
+
+
+def test_sweep_curve_from_tune_times():
+    """DeviceGroup.tune keeps every algorithm's time per (dtype, size); sweep_curve turns them
+    into the algbw / busbw-vs-size curve the bench records (NCCL-tests conventions)."""
+    from collective_communication_mpi_amd.device import DeviceGroup
+
+    class G:
+        size = 4
+        tune_times = {("float32", 4 << 20): {"twoshot": 3e-4},
+                      ("float32", 1 << 20): {"twoshot": 1e-4, "ll": None, "fanout": 2e-4},
+                      ("bfloat16", 1 << 20): {"ring": 5e-4}}
+
+    curve = DeviceGroup.sweep_curve(G(), "float32")
+    assert [c["bytes"] for c in curve] == [1 << 20, 4 << 20]
+    assert curve[0]["best"] == "twoshot" and curve[0]["ms"] == {"twoshot": 0.1, "ll": None, "fanout": 0.2}
+    alg = (1 << 20) / 1e-4 / 1e9
+    assert curve[0]["algbw_GBps"] == round(alg, 2) and curve[0]["busbw_GBps"] == round(alg * 1.5, 2)
+    assert [c["best"] for c in DeviceGroup.sweep_curve(G(), "bfloat16")] == ["ring"]
