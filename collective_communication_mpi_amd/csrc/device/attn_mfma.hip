@@ -206,6 +206,14 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
     }
   }
   const int stride = gridDim.x * WPB;
+  // the fc_o bias of this lane's epilogue classes (4 (lane & 3) .. +3), loaded once (the
+  // compiler cannot hoist it past the loop's global stores)
+  float bov[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int cls = (lane & 3) * 4 + r;
+    bov[r] = (tok && a.bo && cls < a.n_out) ? a.bo[cls] : 0.f;
+  }
   // fused QKV: W_h's rows as B operands (lane (c, g): feature 16 nt + c of q | k | v, depth
   // 32 kk + 8 g .. +7, tail 64 + 4 g .. +3; zero past kq) and the bias, loaded once
   constexpr int WS = QKV ? 3 : 1, WN = QKV ? NT : 1;
@@ -506,7 +514,7 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
       const int b = div_hl(prw);
       float v[4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = (a.bo && q + r < a.n_out) ? a.bo[q + r] : 0.f;
+      for (int r = 0; r < 4; ++r) v[r] = bov[r];
       float z4[4] = {0.f, 0.f, 0.f, 0.f};
       for (int k = 0; k < a.Hl; ++k) {
         const float4 x = *reinterpret_cast<const float4*>(&ztp[it][w + k][i * 16 + q]);
