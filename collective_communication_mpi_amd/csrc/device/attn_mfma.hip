@@ -160,6 +160,7 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
   __shared__ __attribute__((aligned(16))) float imgs[IMG ? 2 : 1][IMG ? kImgPieces * 256 : 1];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
   const int S = a.S, HD = a.Hl * D, npairs = a.B * a.Hl;
+  const float inv_s = 1.f / (float)S;  // (fused path: means as multiplies)
   // fused QKV: Hl | 4, so pair -> (sequence, head) is a shift and a mask, not a division
   const int lhl = a.Hl == 4 ? 2 : a.Hl == 2 ? 1 : 0;
   auto div_hl = [&](int x) { return QKV ? x >> lhl : x / a.Hl; };
@@ -336,14 +337,23 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
       // tile: flat loads + vmcnt(0) waits that also drained the X prefetch, 12 per pair.)
       auto proj = [&](int sel, uint16_t* T) {
 #pragma unroll
-        for (int nt = 0; nt < NT; ++nt) {
+        for (int nt = 0; nt < NT; nt += 2) {  // two tiles in flight: the MFMAs overlap the conversions
           // (the 16x16x16 tail gets its own accumulator: chaining it onto the 16x16x32
           // accumulator lost rows -- the compiler emits no wait states for that srcC hazard)
-          const f4 tl = mma16(wtl[sel][nt], xt, f4{0.f, 0.f, 0.f, 0.f});
-          f4 acc = mma32(wf[sel][nt][0], xr[0], f4{0.f, 0.f, 0.f, 0.f});
-          acc = mma32(wf[sel][nt][1], xr[1], acc);  // acc[r] = [feature 16 nt + 4g + r][token c]
-          const uint2 pk = {pk_bf16(acc[0] + tl[0], acc[1] + tl[1]), pk_bf16(acc[2] + tl[2], acc[3] + tl[3])};
-          *reinterpret_cast<uint2*>(T + c * LD + 16 * nt + 4 * g) = pk;
+          f4 tl[2], acc[2];
+#pragma unroll
+          for (int u = 0; u < 2; ++u) {
+            tl[u] = mma16(wtl[sel][nt + u], xt, f4{0.f, 0.f, 0.f, 0.f});
+            acc[u] = mma32(wf[sel][nt + u][0], xr[0], f4{0.f, 0.f, 0.f, 0.f});
+          }
+#pragma unroll
+          for (int u = 0; u < 2; ++u) acc[u] = mma32(wf[sel][nt + u][1], xr[1], acc[u]);  // [feature 16 nt + 4g + r][token c]
+#pragma unroll
+          for (int u = 0; u < 2; ++u) {
+            const uint2 pk = {pk_bf16(acc[u][0] + tl[u][0], acc[u][1] + tl[u][1]),
+                              pk_bf16(acc[u][2] + tl[u][2], acc[u][3] + tl[u][3])};
+            *reinterpret_cast<uint2*>(T + c * LD + 16 * (nt + u) + 4 * g) = pk;
+          }
         }
       };
       if (IMG && a.xq_out && h == 0 && c < S) {  // the patch rows, for the backward (one head's wave)
@@ -415,7 +425,9 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
       s += e[r];
     }
     s = pair32_sum(pair16_sum(s));
-    const float inv = 1.f / s;
+    // (fused path: the hardware reciprocal -- the precise division is ~10 VALU ops, and the
+    // probabilities are rounded to bf16 right after)
+    const float inv = QKV ? __builtin_amdgcn_rcpf(s) : 1.f / s;
     if (g == 0 && c < S) a.lse[(size_t)pr * S + c] = m + __logf(s);
     const s4 pa = pack4(e[0] * inv, e[1] * inv, e[2] * inv, e[3] * inv);  // A[i = c][j = 4g + jj]
     __builtin_amdgcn_wave_barrier();
@@ -443,7 +455,7 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) cs += (4 * g + r < S) ? on[r] : 0.f;
           cs = pair32_sum(pair16_sum(cs));
-          if (g == 0) a.pool[(size_t)b * a.ld_pool + h * D + 16 * nt + c] = (uint16_t)f32_to_bf16_bits(cs / (float)S);
+          if (g == 0) a.pool[(size_t)b * a.ld_pool + h * D + 16 * nt + c] = (uint16_t)f32_to_bf16_bits(cs * inv_s);
         }
       }
     } else {
@@ -546,8 +558,8 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
           m[r] = pair32_sum(pair16_sum(m[r]));
         }
         if (i == 0) {
-          const float n = (float)S;
-          *reinterpret_cast<float4*>(a.zp + (size_t)b * a.ld_zp + q) = float4{m[0] / n, m[1] / n, m[2] / n, m[3] / n};
+          *reinterpret_cast<float4*>(a.zp + (size_t)b * a.ld_zp + q) =
+              float4{m[0] * inv_s, m[1] * inv_s, m[2] * inv_s, m[3] * inv_s};
         }
       }
     }

@@ -496,7 +496,8 @@ def test_attn_qkv_fused(B, S, H, D, kp):
                      qkv_out=qkv.data_ptr(), ld_qkv=qkv.stride(0), ztok=z.data_ptr(), zrows=0, zpush=[], **common)
     ref_qkv = (xp.float() @ w.float().T + bq).bfloat16()
     torch.testing.assert_close(qkv.float(), ref_qkv.float(), rtol=1e-2, atol=1e-2)
-    # the unfused kernel on the fused kernel's own qkv: same lse / pool, z up to fp32 summation order
+    # the unfused kernel on the fused kernel's own qkv: same lse / pool; z up to fp32 summation
+    # order and the fused softmax's hardware reciprocal (1 ulp in P can flip a bf16 rounding of P)
     lse2, pool2 = torch.empty_like(lse), torch.empty_like(pool)
     z2 = torch.empty_like(z)
     dev.attn_small_fwd(qkv.data_ptr(), 0, lse2.data_ptr(), B, S, H, D, qkv.stride(0), HD, D ** -0.5, pool2.data_ptr(),
@@ -504,7 +505,7 @@ def test_attn_qkv_fused(B, S, H, D, kp):
                        ztok=z2.data_ptr(), ld_zt=16)
     torch.testing.assert_close(lse, lse2, rtol=1e-5, atol=1e-5)
     torch.testing.assert_close(pool.float(), pool2.float(), rtol=1e-2, atol=1e-2)
-    torch.testing.assert_close(z, z2, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(z, z2, rtol=1e-2, atol=2e-3)
     # push form into per-block targets: bitwise the same rows; no qkv written (inference)
     blocks = 2 if B % 2 == 0 else 1
     tg = torch.full((blocks, B * S // blocks, 16), float("nan"), device="cuda")
