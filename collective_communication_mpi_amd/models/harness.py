@@ -197,9 +197,35 @@ def bench_forward(comm, tp: int = 2, batch: int = 2048, steps: int = 20, warmup:
     hc.Barrier()
     fwd_s = hc.allreduce(time.perf_counter() - t0, op=MPI.MAX) / steps
     say(f"timed forward {fwd_s * 1e3:.3f} ms")
+    fwd_eager_s = None
+    if g is not None:
+        # the same forward launched eagerly: with two or three kernels per step the host can
+        # stay ahead of the GPU, and a graph replay pays its own launch cost per step -- the
+        # step time is the faster way of running it on this node (both on record)
+        for _ in range(warmup):
+            fwd()
+        _sync_barrier(comm)
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            fwd()
+        torch.cuda.synchronize()
+        hc.Barrier()
+        fwd_eager_s = hc.allreduce(time.perf_counter() - t0, op=MPI.MAX) / steps
+        say(f"timed eager forward {fwd_eager_s * 1e3:.3f} ms")
+    fwd_graph_s = fwd_s if g is not None else None
+    fwd_timed = "graph" if g is not None else "eager"
+    if fwd_eager_s is not None and fwd_eager_s < fwd_s:
+        fwd_s, fwd_timed = fwd_eager_s, "eager"
+    # hip_graph: a graph was captured and replayed; fwd_timed: which launch mode fwd_ms is
+    fwd_modes = {"fwd_timed": fwd_timed}
+    if fwd_graph_s is not None:
+        fwd_modes["fwd_ms_graph"] = round(fwd_graph_s * 1e3, 4)
+    if fwd_eager_s is not None:
+        fwd_modes["fwd_ms_eager"] = round(fwd_eager_s * 1e3, 4)
     form = getattr(layer, "_zt_form", None)  # the fused per-token fc_o's TP form, if it ran
     if not train:
-        return {"tp": cfg.tp, "dp": cfg.dp, "fwd_ms": fwd_s * 1e3, "hip_graph": used_graph, "fc_o_mode": cfg.fc_o_mode,
+        return {"tp": cfg.tp, "dp": cfg.dp, "fwd_ms": fwd_s * 1e3, "hip_graph": used_graph, **fwd_modes,
+                "fc_o_mode": cfg.fc_o_mode,
                 "tp_chunks": cfg.tp_chunks, "tokens_per_step": cfg.batch * cfg.dp * cfg.seq,
                 **({"fc_o_tp_form": form} if form else {}), **({"graph_skipped": hazard} if hazard else {})}
     # training step: eager, then (where safe) replayed from HIP graphs of whole steps
@@ -245,7 +271,7 @@ def bench_forward(comm, tp: int = 2, batch: int = 2048, steps: int = 20, warmup:
                 train_s, train_graph = graph_s, True
             say(f"timed graph train step {graph_s * 1e3:.3f} ms (eager {train_eager_s * 1e3:.3f})")
     loss_v = hc.allreduce(float(loss.item()), op=MPI.SUM) / cfg.tp  # sum over DP of per-replica shares
-    return {"tp": cfg.tp, "dp": cfg.dp, "fwd_ms": fwd_s * 1e3, "train_ms": train_s * 1e3,
+    return {"tp": cfg.tp, "dp": cfg.dp, "fwd_ms": fwd_s * 1e3, **fwd_modes, "train_ms": train_s * 1e3,
             "train_ms_eager": train_eager_s * 1e3, "train_hip_graph": train_graph,
             **({"train_ms_graph": round(train_graph_s * 1e3, 4)} if train_graph_s is not None else {}),
             **({"train_graph_skipped": t_hazard} if (t_hazard and graph) else {}),
