@@ -158,6 +158,10 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
   // and padded to whole 1-KiB LDS-DMA pieces
   constexpr int kImgPieces = (WPB * 784 * 4 + 1023) / 1024;
   __shared__ __attribute__((aligned(16))) float imgs[IMG ? 2 : 1][IMG ? kImgPieces * 256 : 1];
+  // ... and their patch rows X (bf16, 80 columns + pad), built ONCE per sequence by the whole
+  // workgroup (not once per head), double-buffered
+  constexpr int LDX = 88;
+  __shared__ __attribute__((aligned(16))) uint16_t xs[IMG ? 2 : 1][IMG ? WPB : 1][IMG ? 16 * LDX : 1];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
   const int S = a.S, HD = a.Hl * D, npairs = a.B * a.Hl;
   const float inv_s = 1.f / (float)S;  // (fused path: means as multiplies)
@@ -230,34 +234,11 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
   auto load_x = [&](int p) {
     const bool ok = p < npairs && c < S;
     if constexpr (IMG) {
-      // MNIST 28 x 28, 7 x 7 patches (S = 16): token c = patch (c / 4, c % 4); column cc < 49
-      // is pixel (cc / 7, cc % 7) of the patch, 49 the bias 1, 50 + c the position one-hot.
-      // The image is this iteration's LDS copy (staged one iteration ahead by LDS-DMA).
-      const float* im = imgs[it] + (div_hl(wave)) * 784 + (c >> 2) * 196 + (c & 3) * 7;
-      // the 20 per-lane pixel offsets are loop-invariant: hide g from the optimizer so they are
-      // recomputed per call rather than hoisted into 20 live registers (which spilled)
-      int g = lane >> 4;
-      asm volatile("" : "+v"(g));
-      auto px = [&](int cc) -> float {
-        float v = 0.f;
-        if (ok) {
-          if (cc < 49) v = im[(cc / 7) * 28 + cc % 7];
-          else if (cc == 49 || cc == 50 + c) v = 1.f;  // (the fused bias columns are set below)
-        }
-        return v;
-      };
-      u32x4 w0, w1;
-      uint2 wt;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        w0[q] = pk_bf16(px(8 * g + 2 * q), px(8 * g + 2 * q + 1));
-        w1[q] = pk_bf16(px(32 + 8 * g + 2 * q), px(32 + 8 * g + 2 * q + 1));
-      }
-      wt.x = pk_bf16(px(64 + 4 * g), px(64 + 4 * g + 1));
-      wt.y = pk_bf16(px(64 + 4 * g + 2), px(64 + 4 * g + 3));
-      xn[0] = __builtin_bit_cast(bf16x8, w0);
-      xn[1] = __builtin_bit_cast(bf16x8, w1);
-      xtn = __builtin_bit_cast(s4, wt);
+      // this iteration's X tile of the wave's sequence (built at the end of the previous one)
+      const uint16_t* X = xs[it][div_hl(wave)] + c * LDX;
+      xn[0] = *reinterpret_cast<const bf16x8*>(X + 8 * g);
+      xn[1] = *reinterpret_cast<const bf16x8*>(X + 32 + 8 * g);
+      xtn = *reinterpret_cast<const s4*>(X + 64 + 4 * g);
     } else {
       const uint16_t* row = a.xq + (size_t)(ok ? div_hl(p) * S + c : 0) * a.ld_xq;
       xn[0] = ld_row16(row + 8 * g, ok && 8 * g < a.kq);
@@ -283,6 +264,29 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
                                                  16, (pc * 64 + lane) * 16, 0, 0, 0);
     }
   };
+  // the X tiles of the iteration starting at pair p0 from its LDS images, by the whole
+  // workgroup: one 8-column chunk (4 packed conversions, one 16-B LDS store) per thread and
+  // step.  MNIST 28 x 28 with 7 x 7 patches (S = 16): token t = patch (t / 4, t % 4); column
+  // cc < 49 is pixel (cc / 7, cc % 7) of the patch, 49 the embedding bias 1, 50 + t the
+  // position one-hot, the rest zero (the QKV bias columns are set in load_x)
+  auto build_x = [&](int buf, int p0) {
+    if constexpr (IMG) {
+      const int nseq = div_hl(WPB);
+      for (int id = threadIdx.x; id < nseq * 160; id += WPB * 64) {
+        const int sq = id / 160, rem = id - sq * 160, t = rem / 10, ch = rem - t * 10;
+        const float* im = imgs[buf] + sq * 784 + (t >> 2) * 196 + (t & 3) * 7;
+        float v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int cc = 8 * ch + j;
+          v[j] = cc < 49 ? im[(cc / 7) * 28 + cc % 7] : ((cc == 49 || cc == 50 + t) ? 1.f : 0.f);
+        }
+        const u32x4 w = {pk_bf16(v[0], v[1]), pk_bf16(v[2], v[3]), pk_bf16(v[4], v[5]), pk_bf16(v[6], v[7])};
+        *reinterpret_cast<u32x4*>(xs[buf][sq] + t * LDX + 8 * ch) = w;
+      }
+      (void)p0;
+    }
+  };
   if constexpr (QKV) {
     const int hw = mod_hl(wave);
 #pragma unroll
@@ -303,8 +307,13 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
       }
     if constexpr (!IMG) load_x(blockIdx.x * WPB + wave);
     if constexpr (IMG) {
-      stage_imgs(0, blockIdx.x * WPB);
+      // images two iterations deep: the first two now, X of the first one built
+      const int p0 = blockIdx.x * WPB;
+      stage_imgs(0, p0);
+      if (p0 + stride < npairs) stage_imgs(1, p0 + stride);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      build_x(0, p0);
       __syncthreads();
     }
   }
@@ -316,10 +325,11 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
     // (image mode builds this iteration's rows now, from LDS: the prefetch is the images' DMA)
     if constexpr (IMG) {
       load_x(pr);
-      // the next iteration's images (the body issues no further global loads, so nothing
-      // waits on this DMA before the epilogue's vmcnt(0); a wave with no pair now has no next
-      // iteration either, so every piece is issued)
-      if (base + stride < npairs) stage_imgs(it ^ 1, base + stride);
+      // the images of the iteration after next, into the buffer whose images this iteration's
+      // X was built from (the body issues no further global loads, so nothing waits on this
+      // DMA before the epilogue's vmcnt(0); the trip count is workgroup-uniform, so every
+      // piece is issued)
+      if (base + 2 * stride < npairs) stage_imgs(it, base + 2 * stride);
     }
     xr[0] = xn[0];
     xr[1] = xn[1];
@@ -518,7 +528,13 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
     // head order, + the bias.  Wave s writes sequence s (waves s >= WPB / Hl idle): lane l =
     // (token l >> 2, classes 4 (l & 3) .. +3), one 16-B store per lane, a sequence's S x 16
     // fp32 rows as whole lines
-    if constexpr (IMG) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next images have landed
+    if constexpr (IMG) {
+      // this wave's DMA of the images two iterations ahead has landed (visible to every wave
+      // after the barrier below); the next iteration's X, from images that landed one
+      // barrier ago, goes to the other X buffer
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (base + stride < npairs) build_x(it ^ 1, base + stride);
+    }
     __syncthreads();  // (the next iteration writes the other buffer)
     const int i = lane >> 2, q = (lane & 3) * 4, w = wave * a.Hl;
     const int prw = base + w;
