@@ -332,16 +332,16 @@ __global__ void __launch_bounds__(kFoldNT) k_fold_emb_qkv(const float* __restric
 }
 
 // The same fold on the fp32 matrix cores (v_mfma_f32_16x16x4_f32: exact fp32 products, fp32
-// accumulate): one 512-thread workgroup per 16 x 16 tile of Weff (grid R/16 x kp/16 = 240
-// workgroups at 768 x 72), its 8 waves splitting d.  A wave issues ALL its loads first --
+// accumulate): one 1024-thread workgroup per 16 x 16 tile of Weff (grid R/16 x kp/16 = 240
+// workgroups at 768 x 72), its 16 waves splitting d.  A wave issues ALL its loads first --
 // per 16-deep k chunk j one float4 of its Wq row (k = 16 j + 4 g .. +3: the MFMA's k slot g
 // takes k = 16 j + 4 g + i at step i, the same permutation on both operands) and 4 We values
-// -- so the whole product is one memory round trip, then 4 MFMAs per chunk.  The 8 wave
+// -- so the whole product is one memory round trip, then 4 MFMAs per chunk.  The 16 wave
 // partials meet in LDS in wave order (deterministic), + the bias column, bf16 out.  (A first
 // version with one workgroup per 16 rows x all columns -- 48 workgroups, a load round trip
 // per chunk -- took 17.9 us against the FMA kernel's 7.4 us.)
-constexpr int kFmWaves = 8;
-constexpr int kFmMaxJ = 8;  // chunks per wave: d <= 16 * 8 * 8 = 1024
+constexpr int kFmWaves = 16;  // (8: 4.9 us at 768 x 72 x 768, one 6-chunk load chain per wave)
+constexpr int kFmMaxJ = 4;   // chunks per wave: d <= 16 * 4 * 16 = 1024
 
 __global__ void __launch_bounds__(kFmWaves * 64) k_fold_mfma(const float* __restrict__ Wq, int ld_wq,
                                                             const float* __restrict__ We, int ld_we,
