@@ -216,12 +216,33 @@ def bench_forward(comm, tp: int = 2, batch: int = 2048, steps: int = 20, warmup:
     fwd_timed = "graph" if g is not None else "eager"
     if fwd_eager_s is not None and fwd_eager_s < fwd_s:
         fwd_s, fwd_timed = fwd_eager_s, "eager"
+    # the launch plan: the forward's native launches recorded once, re-issued from a loop
+    # (MnistTPLayer.forward_plan; None where the forward is not all-native -- the same on
+    # every rank, so the collective recording forward runs everywhere or nowhere)
+    fwd_plan_s = None
+    plan = layer.forward_plan(xb, cfg.batch) if os.environ.get("CCMPI_NO_PLAN") != "1" else None
+    if plan is not None:
+        for _ in range(warmup):
+            plan()
+        _sync_barrier(comm)
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            plan()
+        torch.cuda.synchronize()
+        hc.Barrier()
+        fwd_plan_s = hc.allreduce(time.perf_counter() - t0, op=MPI.MAX) / steps
+        say(f"timed launch-plan forward {fwd_plan_s * 1e3:.3f} ms")
+        if fwd_plan_s < fwd_s:
+            fwd_s, fwd_timed = fwd_plan_s, "plan"
     # hip_graph: a graph was captured and replayed; fwd_timed: which launch mode fwd_ms is
+    # (graph replay, eager forward_images, or the recorded launch plan)
     fwd_modes = {"fwd_timed": fwd_timed}
     if fwd_graph_s is not None:
         fwd_modes["fwd_ms_graph"] = round(fwd_graph_s * 1e3, 4)
     if fwd_eager_s is not None:
         fwd_modes["fwd_ms_eager"] = round(fwd_eager_s * 1e3, 4)
+    if fwd_plan_s is not None:
+        fwd_modes["fwd_ms_plan"] = round(fwd_plan_s * 1e3, 4)
     form = getattr(layer, "_zt_form", None)  # the fused per-token fc_o's TP form, if it ran
     if not train:
         return {"tp": cfg.tp, "dp": cfg.dp, "fwd_ms": fwd_s * 1e3, "hip_graph": used_graph, **fwd_modes,

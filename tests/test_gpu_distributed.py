@@ -251,6 +251,14 @@ def test_harness_matches_single_rank(reference_run, tmp_path, n, tp, mode):
     assert got["losses"][-1] < got["losses"][0]
 
 
+@pytest.mark.parametrize("n,tp", [(1, 1), (2, 2)])
+def test_harness_forward_plan_matches_forward(n, tp):
+    """The recorded launch plan of the harness forward (local form at TP = 1, push form at
+    TP = 2) reproduces forward_images bitwise, and follows new pixels and new weights."""
+    r = run_ranks(n, py("tests/workers/plan_worker.py"), timeout=300, env=dict(ENV, PL_TP=str(tp)))
+    assert "plan OK" in r.stdout
+
+
 @pytest.mark.parametrize("n,tp,mode", [(1, 1, "token"), (2, 2, "token"), (2, 2, "row"), (2, 1, "token")])
 def test_harness_graph_train_matches_eager(n, tp, mode):
     """Training steps replayed from HIP graphs (two alternating captures, device-side AdamW
