@@ -95,6 +95,46 @@ class GraphedTrainStep:
         return self.layer.flat.sync_step()
 
 
+class TrainPlan:
+    """Whole training steps as recorded launch plans (``MnistTPLayer.forward_plan``'s
+    recorder over a full ``train_step``): two recordings, re-issued alternately (the split-K
+    accumulator parity, as in ``GraphedTrainStep``), AdamW on the device step counter.
+    Only where the step is all-native: TP = 1 and DP = 1 (the TP / DP paths run torch ops
+    and other groups' collectives); ``available`` says so before anything runs."""
+
+    @staticmethod
+    def available(layer: MnistTPLayer, cfg: LayerConfig) -> bool:
+        return (layer.tp_dev is None and layer.buckets.dp is None and cfg.fc_o_mode == "token"
+                and layer._fuses_qkv(cfg.batch) and int(cfg.fwd_chunks) <= 1)
+
+    def __init__(self, layer: MnistTPLayer, cfg: LayerConfig, xb, yb):
+        from .mnist_tp import LaunchPlan, _LaunchRecorder
+
+        self.layer = layer
+        layer.flat.device_step()
+        torch.cuda.synchronize()
+        layer.graph_step = True
+        self.plans = []
+        try:
+            for _ in range(2):
+                rec = _LaunchRecorder(None)
+                with rec.active(layer):
+                    loss = train_step(layer, cfg, xb, yb)
+                self.plans.append(LaunchPlan(rec.calls, loss))
+        finally:
+            layer.graph_step = False
+        self.i = 0
+
+    def replay(self):
+        out = self.plans[self.i]()
+        self.i ^= 1
+        return out
+
+    def close(self) -> int:
+        torch.cuda.synchronize()
+        return self.layer.flat.sync_step()
+
+
 def train_graph_hazard(cfg: LayerConfig, layer: MnistTPLayer):
     """Why the training step must not be graph-captured here, or None: the forward's
     multi-stream hazard, or the DP bucket all-reduce's side stream with few hardware queues
@@ -262,6 +302,7 @@ def bench_forward(comm, tp: int = 2, batch: int = 2048, steps: int = 20, warmup:
     hc.Barrier()
     train_eager_s = hc.allreduce(time.perf_counter() - t0, op=MPI.MAX) / n_train
     train_s, train_graph, train_graph_s = train_eager_s, False, None
+    train_timed = "eager"
     t_hazard = train_graph_hazard(cfg, layer) if graph else "graph disabled"
     if t_hazard is None and os.environ.get("CCMPI_NO_GRAPH") != "1":
         gts = None
@@ -290,11 +331,30 @@ def bench_forward(comm, tp: int = 2, batch: int = 2048, steps: int = 20, warmup:
             # and a replay adds its launch cost -- measured 0.118 eager vs 0.125 ms graph)
             if graph_s < train_eager_s:
                 train_s, train_graph = graph_s, True
+                train_timed = "graph"
             say(f"timed graph train step {graph_s * 1e3:.3f} ms (eager {train_eager_s * 1e3:.3f})")
+    train_plan_s = None
+    if TrainPlan.available(layer, cfg) and os.environ.get("CCMPI_NO_PLAN") != "1":
+        tp_ = TrainPlan(layer, cfg, xb, yb)
+        for _ in range(2):
+            tp_.replay()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(n_train):
+            loss = tp_.replay()
+        torch.cuda.synchronize()
+        train_plan_s = time.perf_counter() - t0
+        train_plan_s = hc.allreduce(train_plan_s, op=MPI.MAX) / n_train
+        tp_.close()
+        say(f"timed launch-plan train step {train_plan_s * 1e3:.3f} ms")
+        if train_plan_s < train_s:
+            train_s, train_graph = train_plan_s, False
+            train_timed = "plan"
     loss_v = hc.allreduce(float(loss.item()), op=MPI.SUM) / cfg.tp  # sum over DP of per-replica shares
     return {"tp": cfg.tp, "dp": cfg.dp, "fwd_ms": fwd_s * 1e3, **fwd_modes, "train_ms": train_s * 1e3,
-            "train_ms_eager": train_eager_s * 1e3, "train_hip_graph": train_graph,
+            "train_ms_eager": train_eager_s * 1e3, "train_hip_graph": train_graph, "train_timed": train_timed,
             **({"train_ms_graph": round(train_graph_s * 1e3, 4)} if train_graph_s is not None else {}),
+            **({"train_ms_plan": round(train_plan_s * 1e3, 4)} if train_plan_s is not None else {}),
             **({"train_graph_skipped": t_hazard} if (t_hazard and graph) else {}),
             "global_batch": cfg.batch * cfg.dp, "seq_len": cfg.seq, "tokens_per_step": cfg.batch * cfg.dp * cfg.seq,
             "hip_graph": used_graph, "fc_o_mode": cfg.fc_o_mode, **({"fc_o_tp_form": form} if form else {}),

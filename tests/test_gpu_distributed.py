@@ -251,6 +251,14 @@ def test_harness_matches_single_rank(reference_run, tmp_path, n, tp, mode):
     assert got["losses"][-1] < got["losses"][0]
 
 
+def test_harness_train_plan_matches_eager():
+    """Training steps re-issued from recorded launch plans (TrainPlan: two alternating
+    recordings, device-side AdamW step counter) reproduce eager steps."""
+    r = run_ranks(1, py("tests/workers/graph_train_worker.py"), timeout=300,
+                  env=dict(ENV, GT_TP="1", GT_MODE="token", GT_PLAN="1"))
+    assert "graph train OK" in r.stdout
+
+
 @pytest.mark.parametrize("n,tp", [(1, 1), (2, 2)])
 def test_harness_forward_plan_matches_forward(n, tp):
     """The recorded launch plan of the harness forward (local form at TP = 1, push form at

@@ -8,7 +8,7 @@ import torch
 
 sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", ".."))
 from collective_communication_mpi_amd import MPI, Communicator  # noqa: E402
-from collective_communication_mpi_amd.models.harness import GraphedTrainStep, build, train_step  # noqa: E402
+from collective_communication_mpi_amd.models.harness import GraphedTrainStep, TrainPlan, build, train_step  # noqa: E402
 from collective_communication_mpi_amd.models.mnist_tp import local_batch  # noqa: E402
 
 comm = Communicator(MPI.COMM_WORLD)
@@ -21,7 +21,11 @@ xb, yb = local_batch(cfg, x_all, y_all, 0, comm.Get_rank(), eager.device)
 for _ in range(2):
     train_step(eager, cfg, xb, yb)
     train_step(graphed, cfg2, xb, yb)
-gts = GraphedTrainStep(graphed, cfg2, xb, yb)
+if os.environ.get("GT_PLAN") == "1":  # the recorded launch plan instead of the graphs
+    assert TrainPlan.available(graphed, cfg2)
+    gts = TrainPlan(graphed, cfg2, xb, yb)
+else:
+    gts = GraphedTrainStep(graphed, cfg2, xb, yb)
 le, lg = [], []
 for _ in range(5):
     le.append(float(train_step(eager, cfg, xb, yb).item()))
