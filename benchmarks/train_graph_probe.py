@@ -8,7 +8,7 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."
 import torch  # noqa: E402
 
 from collective_communication_mpi_amd import MPI, Communicator  # noqa: E402
-from collective_communication_mpi_amd.models.harness import GraphedTrainStep, build, train_step  # noqa: E402
+from collective_communication_mpi_amd.models.harness import GraphedTrainStep, TrainPlan, build, train_step  # noqa: E402
 from collective_communication_mpi_amd.models.mnist_tp import local_batch  # noqa: E402
 
 comm = Communicator(MPI.COMM_WORLD)
@@ -40,4 +40,17 @@ for _ in range(n):
 torch.cuda.synchronize()
 one = (time.perf_counter() - t0) / n * 1e3
 gts.close()
-print({"eager_ms": round(eager, 4), "graph_alternating_ms": round(graph, 4), "graph_same_ms": round(one, 4)}, flush=True)
+res = {"eager_ms": round(eager, 4), "graph_alternating_ms": round(graph, 4), "graph_same_ms": round(one, 4)}
+if TrainPlan.available(layer, cfg):
+    tp_ = TrainPlan(layer, cfg, xb, yb)
+    for _ in range(4):
+        tp_.replay()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(n):
+        tp_.replay()
+    torch.cuda.synchronize()
+    res["plan_ms"] = round((time.perf_counter() - t0) / n * 1e3, 4)
+    res["plan_launches"] = len(tp_.plans[0].calls)
+    tp_.close()
+print(res, flush=True)

@@ -369,23 +369,24 @@ struct AdamArgs {
   uint64_t n;
   float lr, b1, b2, eps, wd, bc1, bc2, grad_scale;
   int zero_grad;
-  // optional [steps done, unused] on the device (a HIP-graph-captured step): t = steps + 1 is
-  // read here and a one-thread kernel launched right after advances the count -- so a
-  // replayed graph applies the right bias corrections without a host-side argument.  (A
-  // last-workgroup ticket instead cost 2000+ contended atomics on one address: 70 us.)
+  // optional device step counter (a HIP-graph-captured or plan-replayed step): two slots of
+  // "steps done" used alternately.  Every workgroup reads t = *step_dev + 1 and workgroup 0
+  // writes t into the other slot (*step_next), which no workgroup of this launch reads; the
+  // next step (the other recording of the pair) reads that slot.  So a replayed step applies
+  // the right bias corrections with no host-side argument and no extra launch.  (A one-thread
+  // advance kernel after this one cost 4-5 us per step; a last-workgroup ticket, 2000+
+  // contended atomics on one address, 70 us.)
   int* step_dev;
+  int* step_next;
 };
 
-// the bias corrections of step t = step_dev[0] + 1 (read before this workgroup's ticket)
+// the bias corrections of step t = step_dev[0] + 1
 __device__ __forceinline__ void adam_device_step(AdamArgs& a) {
   if (!a.step_dev) return;
-  const float t = (float)(__hip_atomic_load(a.step_dev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1);
-  a.bc1 = 1.f - powf(a.b1, t);
-  a.bc2 = 1.f - powf(a.b2, t);
-}
-
-__global__ void k_adam_step_advance(int* step_dev) {
-  if (threadIdx.x == 0) step_dev[0] += 1;
+  const int t = __hip_atomic_load(a.step_dev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
+  if (blockIdx.x == 0 && threadIdx.x == 0) a.step_next[0] = t;
+  a.bc1 = 1.f - powf(a.b1, (float)t);
+  a.bc2 = 1.f - powf(a.b2, (float)t);
 }
 
 // one AdamW element update on already-loaded values; returns the new bf16 bits
@@ -583,19 +584,17 @@ TRegions make_tregions(const std::vector<std::tuple<uint64_t, uint64_t, uint64_t
 void adamw(uint64_t p, uint64_t g, uint64_t m, uint64_t v, uint64_t p16, uint64_t n, float lr, float b1, float b2,
            float eps, float wd, int step, float grad_scale, uint64_t stream,
            const std::vector<std::tuple<uint64_t, uint64_t, uint64_t, uint64_t>>& tregions, bool zero_grad,
-           uint64_t step_dev) {
+           uint64_t step_dev, int step_parity) {
   const float bc1 = 1.f - powf(b1, (float)step), bc2 = 1.f - powf(b2, (float)step);
   const int flat = (int)std::min<uint64_t>((n + 255) / 256, 2048);
   const TRegions tr = make_tregions(tregions);
   if (step_dev % 8) throw std::invalid_argument("adamw: the device step counter must be 8-B aligned");
+  if (step_parity != 0 && step_parity != 1) throw std::invalid_argument("adamw: step_parity must be 0 or 1");
+  int* slots = reinterpret_cast<int*>(step_dev);
   AdamArgs a{(float*)p, (float*)g, (float*)m, (float*)v, (uint16_t*)p16, n, lr, b1, b2, eps, wd, bc1, bc2, grad_scale,
-             zero_grad ? 1 : 0, reinterpret_cast<int*>(step_dev)};
+             zero_grad ? 1 : 0, slots ? slots + step_parity : nullptr, slots ? slots + (step_parity ^ 1) : nullptr};
   hipLaunchKernelGGL(k_adamw, dim3(flat + tr.tiles[tr.n]), dim3(256), 0, (hipStream_t)stream, a, tr, flat);
   CCMPI_HIP_CHECK(hipGetLastError());
-  if (step_dev) {
-    hipLaunchKernelGGL(k_adam_step_advance, dim3(1), dim3(64), 0, (hipStream_t)stream, reinterpret_cast<int*>(step_dev));
-    CCMPI_HIP_CHECK(hipGetLastError());
-  }
 }
 
 void cast_bf16(uint64_t x, uint64_t y, uint64_t n, uint64_t stream,
@@ -638,7 +637,7 @@ void register_attn_ops(pybind11::module_& m) {
         py::arg("lr"), py::arg("b1"), py::arg("b2"), py::arg("eps"), py::arg("wd"), py::arg("step"),
         py::arg("grad_scale"), py::arg("stream"),
         py::arg("tregions") = std::vector<std::tuple<uint64_t, uint64_t, uint64_t, uint64_t>>{},
-        py::arg("zero_grad") = false, py::arg("step_dev") = 0, py::call_guard<py::gil_scoped_release>());
+        py::arg("zero_grad") = false, py::arg("step_dev") = 0, py::arg("step_parity") = 0, py::call_guard<py::gil_scoped_release>());
   m.def("cast_bf16", &cast_bf16, py::arg("x"), py::arg("y"), py::arg("n"), py::arg("stream"),
         py::arg("tregions") = std::vector<std::tuple<uint64_t, uint64_t, uint64_t, uint64_t>>{},
         py::call_guard<py::gil_scoped_release>());

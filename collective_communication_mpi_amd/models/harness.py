@@ -120,6 +120,9 @@ class TrainPlan:
                 rec = _LaunchRecorder(None)
                 with rec.active(layer):
                     loss = train_step(layer, cfg, xb, yb)
+                if rec.allocated:
+                    raise RuntimeError("TrainPlan: the recorded step allocated device memory (a temporary "
+                                       "whose pointer a recorded call may hold): not replayable")
                 self.plans.append(LaunchPlan(rec.calls, loss))
         finally:
             layer.graph_step = False
@@ -334,8 +337,13 @@ def bench_forward(comm, tp: int = 2, batch: int = 2048, steps: int = 20, warmup:
                 train_timed = "graph"
             say(f"timed graph train step {graph_s * 1e3:.3f} ms (eager {train_eager_s * 1e3:.3f})")
     train_plan_s = None
+    tp_ = None
     if TrainPlan.available(layer, cfg) and os.environ.get("CCMPI_NO_PLAN") != "1":
-        tp_ = TrainPlan(layer, cfg, xb, yb)
+        try:
+            tp_ = TrainPlan(layer, cfg, xb, yb)
+        except RuntimeError as e:
+            say(str(e))
+    if tp_ is not None:
         for _ in range(2):
             tp_.replay()
         torch.cuda.synchronize()

@@ -192,11 +192,15 @@ class LaunchPlan:
 
 class _LaunchRecorder:
     """Proxies ``_native.device()`` and a device group's ``dc`` while a forward runs,
-    keeping every native call with its arguments (the call still executes)."""
+    keeping every native call with its arguments (the call still executes).  A plan holds
+    raw pointers, so a recording during which the caching allocator handed out any block
+    (a temporary whose pointer a call may have taken) sets ``allocated`` and must not be
+    replayed."""
 
     def __init__(self, dc):
         self.calls = []
         self.dc = dc
+        self.allocated = False
 
     def _proxy(self, target):
         rec = self
@@ -218,7 +222,12 @@ class _LaunchRecorder:
         def __init__(self, rec, layer):
             self.rec, self.layer = rec, layer
 
+        @staticmethod
+        def _allocs(layer) -> int:
+            return int(torch.cuda.memory_stats(layer.device).get("allocation.all.allocated", 0))
+
         def __enter__(self):
+            self.n0 = self._allocs(self.layer)
             self.orig = _native.device
             dev = self.orig()
             proxy = self.rec._proxy(dev)
@@ -231,6 +240,7 @@ class _LaunchRecorder:
             _native.device = self.orig
             if self.rec.dc is not None:
                 self.layer.tp_dev.dc = self.rec.dc
+            self.rec.allocated = self._allocs(self.layer) != self.n0
             return False
 
     def active(self, layer):
@@ -482,10 +492,11 @@ class MnistTPLayer:
         if not (self._fuses_qkv(B) and cfg.fc_o_mode == "token" and self.tp_fc_o_form(B) in ("local", "push")
                 and images.dtype == torch.float32 and images.is_contiguous() and images.is_cuda):
             return None
+        self.forward_images(images, B, save=False)   # persistent buffers exist before recording
         rec = _LaunchRecorder(self.tp_dev.dc if self.tp_dev is not None else None)
         with rec.active(self):
             logits = self.forward_images(images, B, save=False)
-        return LaunchPlan(rec.calls, logits)
+        return LaunchPlan(rec.calls, logits) if not rec.allocated else None
 
     def forward_images(self, images: torch.Tensor, B: int, save: bool = True) -> torch.Tensor:
         """(B, 784) fp32 images -> logits: patchify into the fused [h | xp] rows, then

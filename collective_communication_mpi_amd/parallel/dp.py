@@ -57,7 +57,8 @@ class FlatParams:
         self.m = torch.zeros_like(self.p32)
         self.v = torch.zeros_like(self.p32)
         self.step_count = 0
-        self._step_dev: Optional[torch.Tensor] = None  # [steps done, ticket] for graph-captured steps
+        self._step_dev: Optional[torch.Tensor] = None  # two "steps done" slots for recorded steps
+        self._step_par = 0
         self.grad_dirty = False  # g holds values a step has not consumed (AdamW zeroes what it reads)
         self.p16_t: Dict[str, torch.Tensor] = {}
         for name in transposed:
@@ -95,20 +96,23 @@ class FlatParams:
                                    torch.cuda.current_stream(self.device).cuda_stream, self._tregions)
 
     def device_step(self) -> torch.Tensor:
-        """The device-side step counter ([steps done, ticket], int32), seeded from
-        ``step_count``.  An AdamW launched with ``device_step=True`` takes t from it and the
-        kernel's last workgroup advances it, so a HIP graph of whole training steps replays
-        with the right bias corrections; ``sync_step()`` brings ``step_count`` back."""
+        """The device-side step counter (two int32 slots of "steps done", used alternately),
+        seeded from ``step_count``.  An AdamW launched with ``device_step=True`` reads
+        t - 1 from slot ``p`` and writes t to slot ``p ^ 1`` (``p`` flips per call), so the
+        alternating pair of recorded training steps (HIP graphs or launch plans) replays with
+        the right bias corrections; ``sync_step()`` brings ``step_count`` back."""
         if self._step_dev is None:
             self._step_dev = torch.zeros(2, dtype=torch.int32, device=self.device)
-        self._step_dev.fill_(0)
-        self._step_dev[0] = self.step_count
+        self._step_dev.fill_(self.step_count)
+        self._step_par = 0
         return self._step_dev
 
     def sync_step(self) -> int:
         """step_count <- the device counter (after graph replays)."""
         if self._step_dev is not None:
-            self.step_count = int(self._step_dev[0].item())
+            newest = int(torch.argmax(self._step_dev).item())     # the slots alternate; the newer is larger
+            self.step_count = int(self._step_dev[newest].item())
+            self._step_par = newest
         return self.step_count
 
     def adamw(self, lr: float, betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0,
@@ -120,7 +124,10 @@ class FlatParams:
                                     self.p16.data_ptr(), self.numel, lr, betas[0], betas[1], eps, weight_decay,
                                     self.step_count, grad_scale, torch.cuda.current_stream(self.device).cuda_stream,
                                     self._tregions, True,
-                                    step_dev=self._step_dev.data_ptr() if device_step else 0)
+                                    step_dev=self._step_dev.data_ptr() if device_step else 0,
+                                    step_parity=self._step_par if device_step else 0)
+        if device_step:
+            self._step_par ^= 1
         self.grad_dirty = False
 
 
