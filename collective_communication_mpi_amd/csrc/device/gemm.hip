@@ -432,8 +432,12 @@ __device__ __forceinline__ int tn_off(int row, int byte) { return row * kTnRow +
 // and B are fetched into that XCD's L2 once and shared by all its tiles (with
 // split-minor order each XCD streams whole K panels of its own few tiles, and
 // the same bytes cross the fabric once per tile).
-template <int FAST>
-__global__ void __launch_bounds__(NT) k_gemm_tn(GemmArgs g, int split_major) {
+// PF: K tiles in flight per workgroup.  PF = 1 issues tile k+1's global loads under tile k's
+// MFMAs, so with few workgroups (a narrow output split over K) every tile waits out most
+// of a memory round trip; PF = 2 keeps tiles k+1 and k+2 in flight in two register sets
+// (the loop unrolled by two so the sets are indexed statically).
+template <int FAST, int PF = 1>
+__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2))) k_gemm_tn(GemmArgs g, int split_major) {
   __shared__ __attribute__((aligned(16))) unsigned char smem[4 * kTnTile];
   // here: g.M = N1 (rows of C), g.N = N2 (cols of C), g.K = M (reduction)
   const int tiles_n = (g.N + BN - 1) / BN, tiles_m = (g.M + BM - 1) / BM;
@@ -463,38 +467,50 @@ __global__ void __launch_bounds__(NT) k_gemm_tn(GemmArgs g, int split_major) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
 
-  uint4 ra[4], rb[4];
+  uint4 ra[PF][4], rb[PF][4];
   const int schunk = t & 15, srow = t >> 4;  // 16 chunks of 16 B per 128-column row
-  auto gload = [&](int m0) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int m = m0 + srow + 16 * i;
-      const int ca = bm + schunk * 8, cb = bn + schunk * 8;
-      ra[i] = (m < g.K && ca < g.M) ? *reinterpret_cast<const uint4*>(g.A + (size_t)m * g.lda + ca) : uint4{0, 0, 0, 0};
-      rb[i] = (m < g.K && cb < g.N) ? *reinterpret_cast<const uint4*>(g.B + (size_t)m * g.ldb + cb) : uint4{0, 0, 0, 0};
-    }
-  };
-  auto swrite = [&](int buf) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int r = srow + 16 * i;
-      *reinterpret_cast<uint4*>(As(buf) + tn_off(r, schunk * 16)) = ra[i];
-      *reinterpret_cast<uint4*>(Bs(buf) + tn_off(r, schunk * 16)) = rb[i];
-    }
-  };
   const int nk_all = (g.K + BK - 1) / BK;
   const int per = (nk_all + g.splitk - 1) / g.splitk;
   const int kt0 = split * per;
   const int nk = max(0, min(nk_all, kt0 + per) - kt0);
-  if (nk > 0) {
-    gload(kt0 * BK);
-    swrite(0);
+  // PF = 2 loads through buffer resources over this split's rows: rows past K read as 0
+  // with no branch, so the loads carry no exec-mask control flow and the compiler can
+  // wait for the older register set alone (with the guarded pointer loads below it
+  // emits vmcnt(0), draining the newer set too).  Columns past N1 / N2 read the row's
+  // neighbours, which only reach outputs that are never stored.
+  const int rows = max(0, min(g.K - kt0 * BK, nk * BK));
+  Rsrc rsa{}, rsb{};
+  if constexpr (PF == 2) {
+    rsa = make_rsrc(uniform_ptr(reinterpret_cast<char*>(const_cast<uint16_t*>(g.A + (size_t)kt0 * BK * g.lda))),
+                    (uint32_t)((size_t)rows * g.lda * 2));
+    rsb = make_rsrc(uniform_ptr(reinterpret_cast<char*>(const_cast<uint16_t*>(g.B + (size_t)kt0 * BK * g.ldb))),
+                    (uint32_t)((size_t)rows * g.ldb * 2));
   }
-  __syncthreads();
+  auto gload = [&](int s, int m0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = m0 + srow + 16 * i;
+      const int ca = bm + schunk * 8, cb = bn + schunk * 8;
+      if constexpr (PF == 2) {
+        const uint32_t ml = (uint32_t)(m - kt0 * BK);
+        ra[s][i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rsa.r, (ml * g.lda + ca) * 2, 0, 0));
+        rb[s][i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rsb.r, (ml * g.ldb + cb) * 2, 0, 0));
+      } else {
+        ra[s][i] = (m < g.K && ca < g.M) ? *reinterpret_cast<const uint4*>(g.A + (size_t)m * g.lda + ca) : uint4{0, 0, 0, 0};
+        rb[s][i] = (m < g.K && cb < g.N) ? *reinterpret_cast<const uint4*>(g.B + (size_t)m * g.ldb + cb) : uint4{0, 0, 0, 0};
+      }
+    }
+  };
+  auto swrite = [&](int buf, int s) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = srow + 16 * i;
+      *reinterpret_cast<uint4*>(As(buf) + tn_off(r, schunk * 16)) = ra[s][i];
+      *reinterpret_cast<uint4*>(Bs(buf) + tn_off(r, schunk * 16)) = rb[s][i];
+    }
+  };
   const int grp = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) gload((kt0 + kt + 1) * BK);
+  auto compute = [&](int cur) {
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       bf16x8 af[4], bf[4];
@@ -518,8 +534,40 @@ __global__ void __launch_bounds__(NT) k_gemm_tn(GemmArgs g, int split_major) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf[j], acc[i][j], 0, 0, 0);
     }
-    if (kt + 1 < nk) swrite(cur ^ 1);
+  };
+  if constexpr (PF == 1) {
+    if (nk > 0) {
+      gload(0, kt0 * BK);
+      swrite(0, 0);
+    }
     __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+      const int cur = kt & 1;
+      if (kt + 1 < nk) gload(0, (kt0 + kt + 1) * BK);
+      compute(cur);
+      if (kt + 1 < nk) swrite(cur ^ 1, 0);
+      __syncthreads();
+    }
+  } else {
+    // tile j is loaded into register set j & 1 and written to LDS buffer j & 1 one
+    // iteration before its MFMAs; set j & 1 is refilled with tile j + 2 right after
+    if (nk > 0) gload(0, kt0 * BK);
+    if (nk > 1) gload(1, (kt0 + 1) * BK);
+    if (nk > 0) swrite(0, 0);
+    __syncthreads();
+    if (nk > 2) gload(0, (kt0 + 2) * BK);
+    for (int kt = 0; kt < nk; kt += 2) {
+      compute(0);
+      if (kt + 1 < nk) swrite(1, 1);
+      __syncthreads();
+      if (kt + 3 < nk) gload(1, (kt0 + kt + 3) * BK);
+      if (kt + 1 < nk) {
+        compute(1);
+        if (kt + 2 < nk) swrite(0, 0);
+        __syncthreads();
+        if (kt + 4 < nk) gload(0, (kt0 + kt + 4) * BK);
+      }
+    }
   }
   __syncthreads();
   if constexpr (FAST == 1) store_tile_f32<true, false>(g, acc, smem, bm, bn, wm, wn, t, lane);
@@ -1070,6 +1118,8 @@ bool gemm_ring(uint64_t A, uint64_t B, uint64_t C, int M, int N, int K, int lda,
 }
 
 int g_tn_split_major = std::getenv("CCMPI_TN_ORDER") ? std::atoi(std::getenv("CCMPI_TN_ORDER")) : 1;
+// K tiles in flight in the 128x128 TN kernel: 0 = auto (two when a split walks >= 4 tiles), 1, 2
+int g_tn_pf = std::getenv("CCMPI_TN_PF") ? std::atoi(std::getenv("CCMPI_TN_PF")) : 0;
 
 // C[N1,N2] (+)= alpha * A[M,N1]^T . B[M,N2]; fp32 output.
 void gemm_tn(uint64_t A, uint64_t B, uint64_t C, int M, int N1, int N2, int lda, int ldb, int ldc, float alpha,
@@ -1119,6 +1169,30 @@ void gemm_tn(uint64_t A, uint64_t B, uint64_t C, int M, int N1, int N2, int lda,
   const bool aligned = (C % 16) == 0 && ldc % 4 == 0 && N2 % 4 == 0;
   const int fast = use_ws ? 4 : !aligned ? 0 : splitk > 1 ? 1 : accumulate ? 3 : 2;
   auto st = reinterpret_cast<hipStream_t>(stream);
+  // two K tiles in flight when each workgroup walks several of them (g_tn_pf: A/B knob)
+  const int nk_split = ((M + BK - 1) / BK + splitk - 1) / splitk;
+  // (PF = 2 addresses a split's rows with 32-bit buffer offsets)
+  const bool fits = (size_t)nk_split * BK * std::max(lda, ldb) * 2 < (1ull << 31);
+  const bool pf2 = fits && (g_tn_pf == 2 || (g_tn_pf == 0 && nk_split >= 4));
+  if (pf2) {
+    switch (fast) {
+      case 4: hipLaunchKernelGGL((k_gemm_tn<4, 2>), dim3(nwg), dim3(NT), 0, st, g, g_tn_split_major); break;
+      case 1: hipLaunchKernelGGL((k_gemm_tn<1, 2>), dim3(nwg), dim3(NT), 0, st, g, g_tn_split_major); break;
+      case 2: hipLaunchKernelGGL((k_gemm_tn<2, 2>), dim3(nwg), dim3(NT), 0, st, g, g_tn_split_major); break;
+      case 3: hipLaunchKernelGGL((k_gemm_tn<3, 2>), dim3(nwg), dim3(NT), 0, st, g, g_tn_split_major); break;
+      default: hipLaunchKernelGGL((k_gemm_tn<0, 2>), dim3(nwg), dim3(NT), 0, st, g, g_tn_split_major); break;
+    }
+    CCMPI_HIP_CHECK(hipGetLastError());
+    if (fast == 4) {
+      const size_t work = (size_t)N1 * (N2 / 4);
+      const int grid = (int)std::min<size_t>((work + 255) / 256, 4096);
+      hipLaunchKernelGGL(k_splitk_reduce, dim3(grid), dim3(256), 0, st, reinterpret_cast<const float*>(workspace), splitk,
+                         reinterpret_cast<float*>(C), ldc, N1, N2, accumulate ? 1 : 0,
+                         reinterpret_cast<float*>(C2), ldc2, csplit);
+      CCMPI_HIP_CHECK(hipGetLastError());
+    }
+    return;
+  }
   switch (fast) {
     case 4: {
       hipLaunchKernelGGL(k_gemm_tn<4>, dim3(nwg), dim3(NT), 0, st, g, g_tn_split_major);
@@ -1183,6 +1257,8 @@ void register_gemm_ops(pybind11::module_& m) {
         pybind11::arg("variant") = 0, pybind11::arg("C2") = 0, pybind11::arg("ldc2") = 0, pybind11::arg("csplit") = 0,
         pybind11::call_guard<pybind11::gil_scoped_release>());
   m.def("gemm_set_glds", [](bool on) { g_use_glds = on; }, "select LDS-DMA (True) or register staging");
+  m.def("gemm_tn_set_prefetch", [](int pf) { g_tn_pf = pf; },
+        "128x128 TN kernel: K tiles in flight (0 auto, 1, 2)", pybind11::arg("pf"));
   m.def("gemm_set_direct_epilogue", [](bool on) { g_direct_epi = on; },
         "128x128 LDS-DMA kernel: LDS-free epilogue (True) or LDS-staged rows");
   m.def("gemm_set_kernel", [](int k) { g_kernel = k; },

@@ -272,20 +272,30 @@ def test_split_derives_rccl_communicator():
     torch.testing.assert_close(y, x)
 
 
-@pytest.mark.parametrize("M,N1,N2", [(64, 16, 128), (32768, 384, 768), (32768, 768, 64), (1000, 136, 72), (7, 8, 8)])
+@pytest.mark.parametrize("M,N1,N2", [(64, 16, 128), (32768, 384, 768), (32768, 768, 64), (1000, 136, 72), (7, 8, 8),
+                                     (320, 128, 72), (32768, 768, 72)])
 @pytest.mark.parametrize("splitk", [1, 4, None])
-def test_gemm_tn_weight_grad(M, N1, N2, splitk):
+@pytest.mark.parametrize("pf", [0, 1, 2])  # K tiles in flight: auto, one, two (odd / even tile counts above)
+def test_gemm_tn_weight_grad(M, N1, N2, splitk, pf):
+    from collective_communication_mpi_amd import _native
     from collective_communication_mpi_amd.ops import gemm_tn
 
-    g = torch.Generator(device="cuda").manual_seed(M + N1 + N2)
-    a = torch.randn(M, N1, device="cuda", generator=g).bfloat16()
-    b = torch.randn(M, N2, device="cuda", generator=g).bfloat16()
-    ref = a.float().T @ b.float()
-    out = gemm_tn(a, b, splitk=splitk)
-    torch.testing.assert_close(out, ref, rtol=2e-3, atol=2e-3 * M ** 0.5)
-    acc = torch.ones(N1, N2, device="cuda")
-    gemm_tn(a, b, out=acc, accumulate=True, alpha=0.5, splitk=splitk)
-    torch.testing.assert_close(acc, 1 + 0.5 * ref, rtol=2e-3, atol=2e-3 * M ** 0.5)
+    _native.device().gemm_tn_set_prefetch(pf)
+    try:
+        g = torch.Generator(device="cuda").manual_seed(M + N1 + N2)
+        a = torch.randn(M, N1, device="cuda", generator=g).bfloat16()
+        b = torch.randn(M, N2, device="cuda", generator=g).bfloat16()
+        ref = a.float().T @ b.float()
+        out = gemm_tn(a, b, splitk=splitk)
+        torch.testing.assert_close(out, ref, rtol=2e-3, atol=2e-3 * M ** 0.5)
+        acc = torch.ones(N1, N2, device="cuda")
+        gemm_tn(a, b, out=acc, accumulate=True, alpha=0.5, splitk=splitk)
+        torch.testing.assert_close(acc, 1 + 0.5 * ref, rtol=2e-3, atol=2e-3 * M ** 0.5)
+        acc.fill_(1.0)
+        gemm_tn(a, b, out=acc, accumulate=True, splitk=splitk, workspace=True)
+        torch.testing.assert_close(acc, 1 + ref, rtol=2e-3, atol=2e-3 * M ** 0.5)
+    finally:
+        _native.device().gemm_tn_set_prefetch(0)
 
 
 @pytest.mark.parametrize("M,N1,c,N2,ldb", [(32768, 768, 768, 840, 896), (4096, 256, 128, 200, 264),
