@@ -62,6 +62,18 @@ __device__ void gq_tile(const WgradArgs& a, int blk, float* smem) {
   const int tiles_c = (a.d + kT - 1) / kT;
   const int r0 = (blk / tiles_c) * kT, c0 = (blk % tiles_c) * kT;
   const int t = threadIdx.x, nv = a.kp / 4;
+  const int tx = t & 15, ty = t >> 4;  // rows 4*ty.., columns 4*tx..
+  // the tile's old Gq values are fetched with the operands (the read-modify-write at the
+  // end would otherwise wait out a second memory round trip)
+  float4 old[4];
+  bool vec[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = r0 + 4 * ty + i;
+    const float* g = a.Gq + (size_t)r * a.ld_gq + c0 + 4 * tx;
+    vec[i] = r < a.R && c0 + 4 * tx + 3 < a.d && ((reinterpret_cast<uintptr_t>(g) & 15) == 0);
+    old[i] = vec[i] ? *reinterpret_cast<const float4*>(g) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
   constexpr int kPer = kT * (kMaxKp / 4) / kNT;  // float4 per thread per operand at kp = 96
   float4 ra[kPer], rw[kPer];
 #pragma unroll
@@ -84,7 +96,6 @@ __device__ void gq_tile(const WgradArgs& a, int blk, float* smem) {
     }
   }
   __syncthreads();
-  const int tx = t & 15, ty = t >> 4;  // rows 4*ty.., columns 4*tx..
   float acc[4][4] = {};
   // unrolled so the LDS reads of several k are in flight (one k per trip waited out
   // the LDS latency every 16 FMAs)
@@ -103,8 +114,8 @@ __device__ void gq_tile(const WgradArgs& a, int blk, float* smem) {
     const int r = r0 + 4 * ty + i;
     if (r >= a.R) continue;
     float* g = a.Gq + (size_t)r * a.ld_gq + c0 + 4 * tx;
-    if (c0 + 4 * tx + 3 < a.d && ((reinterpret_cast<uintptr_t>(g) & 15) == 0)) {
-      float4 o = *reinterpret_cast<float4*>(g);
+    if (vec[i]) {
+      float4 o = old[i];
       o.x += acc[i][0]; o.y += acc[i][1]; o.z += acc[i][2]; o.w += acc[i][3];
       *reinterpret_cast<float4*>(g) = o;
     } else {

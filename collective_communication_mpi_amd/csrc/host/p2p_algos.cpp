@@ -30,12 +30,25 @@ constexpr int kTagAlltoall = -17;
 constexpr int kTagPairwise = -18;
 constexpr int kTagRing = -19;   // ring steps use kTagRing - step (one tag per step)
 constexpr int kTagRhd = -4096;  // rhd rounds use kTagRhd - round
+// reduce_bcast root: pre-post every receive (p scratch slices) up to this many bytes
+constexpr size_t kPrepostMaxBytes = size_t(4) << 20;
 
 // per-thread scratch, grown on demand (the schedules run with the GIL released)
 char* scratch(size_t nbytes) {
   thread_local std::vector<char> buf;
   if (buf.size() < nbytes) buf.resize(std::max(nbytes, (size_t)4096));
   return buf.data();
+}
+
+// Touch every page of [p, p + n) with a write (the bytes written are overwritten by the
+// result afterwards).  A freshly allocated result buffer faults on first touch (~2-5 us
+// per page with the zero fill); doing that while this rank idles waiting for a peer
+// keeps the fault off the schedule's critical path.
+void prefault(void* p, size_t n) {
+  constexpr uintptr_t kPage = 4096;
+  volatile char* c = static_cast<volatile char*>(p);
+  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+  for (uintptr_t o = 0; o < n; o = ((a + o) / kPage + 1) * kPage - a) c[o] = 0;
 }
 
 bool overlaps(const void* a, const void* b, size_t n) {
@@ -50,18 +63,42 @@ void ShmComm::my_reduce_bcast(const void* src, void* dst, size_t count, int dt, 
   if (!reduce_supported(dt, op)) throw std::invalid_argument("ccmpi: unsupported reduction for myAllreduce");
   const size_t nb = count * dtype_size(dt);
   if (rank_ == 0) {
-    if (dst != src) std::memmove(dst, src, nb);
-    char* tmp = scratch(nb);
+    // every receive is posted before the first wait, each into its own scratch slice, so
+    // the contributions land in place as they arrive (a receive posted late finds the
+    // message in the unexpected queue: a heap copy, then a second copy); the reduction
+    // still runs in rank order 1..p-1, as in the reference
+    if (nb * (size_t)size_ > kPrepostMaxBytes) {  // large: one scratch slice, receives in turn
+      if (dst != src) std::memmove(dst, src, nb);
+      char* tmp = scratch(nb);
+      for (int i = 1; i < size_; ++i) {
+        recv(tmp, nb, i, kTagReduceBcast);
+        reduce_inplace(dst, tmp, count, dt, op);
+      }
+      std::vector<RequestPtr> rs;
+      rs.reserve(size_);
+      for (int i = 1; i < size_; ++i) rs.push_back(isend_raw(dst, nb, i, kTagReduceBcast));
+      waitall(rs);
+      return;
+    }
+    // slices 1..p-1 receive, slice 0 accumulates: the sends go out of scratch and the copy
+    // into dst (whose first touch may fault) comes after them
+    char* tmp = scratch(nb * (size_t)size_);
+    char* acc = tmp;
+    std::vector<RequestPtr> rr;
+    rr.reserve(size_);
+    for (int i = 1; i < size_; ++i) rr.push_back(irecv(tmp + nb * (size_t)i, nb, i, kTagReduceBcast));
+    std::memcpy(acc, src, nb);
     for (int i = 1; i < size_; ++i) {
-      recv(tmp, nb, i, kTagReduceBcast);
-      reduce_inplace(dst, tmp, count, dt, op);
+      wait(rr[i - 1]);
+      reduce_inplace(acc, tmp + nb * (size_t)i, count, dt, op);
     }
     // the reference sends in rank order with blocking Sends; posting them all
     // and waiting once keeps that order on every ring and lets small results
     // leave without a round trip per peer
     std::vector<RequestPtr> rs;
     rs.reserve(size_);
-    for (int i = 1; i < size_; ++i) rs.push_back(isend_raw(dst, nb, i, kTagReduceBcast));
+    for (int i = 1; i < size_; ++i) rs.push_back(isend_raw(acc, nb, i, kTagReduceBcast));
+    std::memmove(dst, acc, nb);
     waitall(rs);
   } else {
     if (dst == src) {
@@ -70,7 +107,11 @@ void ShmComm::my_reduce_bcast(const void* src, void* dst, size_t count, int dt, 
       src = tmp;
     }
     auto rr = irecv(dst, nb, 0, kTagReduceBcast);  // posted first: the result lands in place
-    wait(isend_raw(src, nb, 0, kTagReduceBcast));
+    auto rs = isend_raw(src, nb, 0, kTagReduceBcast);
+    // no receive progress has run since the irecv (isend_raw only pushes the send), so
+    // dst holds no result bytes yet: fault its pages in while the root reduces
+    prefault(dst, nb);
+    wait(rs);
     wait(rr);
   }
 }
