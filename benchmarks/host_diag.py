@@ -20,7 +20,16 @@ n = int(os.environ.get("HD_COUNT", "1024"))
 runs = int(os.environ.get("HD_RUNS", "200"))
 
 
+fresh_ranks = os.environ.get("HD_FRESH_RANKS")  # e.g. "0" or "1-7": only these ranks take fresh arrays
+if fresh_ranks:
+    lo, _, hi = fresh_ranks.partition("-")
+    mine = int(lo) <= rank <= int(hi or lo)
+else:
+    mine = True
+
+
 def run(name, fn, fresh):
+    fresh = fresh if mine else False
     call, total = [], []
     s = rng.standard_normal(n).astype(np.float32)
     d = np.empty(n, np.float32)

@@ -167,6 +167,7 @@ PyObject* f_send(PyObject*, PyObject* const* a, Py_ssize_t n) {
   View b;
   if (!view_of(a[1], false, false, b)) return not_impl();
   ShmComm* c = comm_of(a[0]);
+  if (!c) return PyErr_Occurred() ? nullptr : (PyErr_SetString(PyExc_ValueError, "ccmpi: communicator freed"), nullptr);
   int dest = (int)PyLong_AsLong(a[2]), tag = (int)PyLong_AsLong(a[3]);
   if (PyErr_Occurred()) return nullptr;
   RequestPtr r;
@@ -180,6 +181,7 @@ PyObject* f_recv(PyObject*, PyObject* const* a, Py_ssize_t n) {
   View b;
   if (!view_of(a[1], true, false, b)) return not_impl();
   ShmComm* c = comm_of(a[0]);
+  if (!c) return PyErr_Occurred() ? nullptr : (PyErr_SetString(PyExc_ValueError, "ccmpi: communicator freed"), nullptr);
   int src = (int)PyLong_AsLong(a[2]), tag = (int)PyLong_AsLong(a[3]);
   if (PyErr_Occurred()) return nullptr;
   RequestPtr r;
@@ -193,6 +195,7 @@ PyObject* f_isend(PyObject*, PyObject* const* a, Py_ssize_t n) {
   View b;
   if (!view_of(a[1], false, false, b)) return not_impl();
   ShmComm* c = comm_of(a[0]);
+  if (!c) return PyErr_Occurred() ? nullptr : (PyErr_SetString(PyExc_ValueError, "ccmpi: communicator freed"), nullptr);
   int dest = (int)PyLong_AsLong(a[2]), tag = (int)PyLong_AsLong(a[3]);
   if (PyErr_Occurred()) return nullptr;
   RequestPtr r;
@@ -205,6 +208,7 @@ PyObject* f_irecv(PyObject*, PyObject* const* a, Py_ssize_t n) {
   View b;
   if (!view_of(a[1], true, false, b)) return not_impl();
   ShmComm* c = comm_of(a[0]);
+  if (!c) return PyErr_Occurred() ? nullptr : (PyErr_SetString(PyExc_ValueError, "ccmpi: communicator freed"), nullptr);
   int src = (int)PyLong_AsLong(a[2]), tag = (int)PyLong_AsLong(a[3]);
   if (PyErr_Occurred()) return nullptr;
   RequestPtr r;
@@ -267,6 +271,7 @@ PyObject* f_sendrecv(PyObject*, PyObject* const* a, Py_ssize_t n) {
   View s, r;
   if (!view_of(a[1], false, false, s) || !view_of(a[4], true, false, r)) return not_impl();
   ShmComm* c = comm_of(a[0]);
+  if (!c) return PyErr_Occurred() ? nullptr : (PyErr_SetString(PyExc_ValueError, "ccmpi: communicator freed"), nullptr);
   int dest = (int)PyLong_AsLong(a[2]), stag = (int)PyLong_AsLong(a[3]);
   int src = (int)PyLong_AsLong(a[5]), rtag = (int)PyLong_AsLong(a[6]);
   if (PyErr_Occurred()) return nullptr;
@@ -280,6 +285,7 @@ PyObject* f_sendrecv(PyObject*, PyObject* const* a, Py_ssize_t n) {
 PyObject* f_barrier(PyObject*, PyObject* const* a, Py_ssize_t n) {
   if (!nargs_is(n, 1, "fbarrier")) return nullptr;
   ShmComm* c = comm_of(a[0]);
+  if (!c) return PyErr_Occurred() ? nullptr : (PyErr_SetString(PyExc_ValueError, "ccmpi: communicator freed"), nullptr);
   if (!guarded([&] { c->barrier(); })) return nullptr;
   Py_RETURN_NONE;
 }
@@ -289,6 +295,7 @@ PyObject* f_bcast(PyObject*, PyObject* const* a, Py_ssize_t n) {
   View b;
   if (!view_of(a[1], true, false, b)) return not_impl();
   ShmComm* c = comm_of(a[0]);
+  if (!c) return PyErr_Occurred() ? nullptr : (PyErr_SetString(PyExc_ValueError, "ccmpi: communicator freed"), nullptr);
   int root = (int)PyLong_AsLong(a[2]);
   if (PyErr_Occurred()) return nullptr;
   if (!guarded([&] { c->bcast(b.ptr(), b.nbytes(), root); })) return nullptr;
@@ -303,6 +310,7 @@ PyObject* f_allreduce(PyObject*, PyObject* const* a, Py_ssize_t n) {
   const int dt = dtype_of(r);
   if (dt < 0 || dtype_of(s) != dt || s.nbytes() != r.nbytes()) return not_impl();
   ShmComm* c = comm_of(a[0]);
+  if (!c) return PyErr_Occurred() ? nullptr : (PyErr_SetString(PyExc_ValueError, "ccmpi: communicator freed"), nullptr);
   int op = (int)PyLong_AsLong(a[3]);
   if (PyErr_Occurred()) return nullptr;
   if (!reduce_supported(dt, op)) return not_impl();
@@ -315,6 +323,7 @@ PyObject* f_allgather(PyObject*, PyObject* const* a, Py_ssize_t n) {
   View s, r;
   if (!view_of(a[1], false, false, s) || !view_of(a[2], true, false, r)) return not_impl();
   ShmComm* c = comm_of(a[0]);
+  if (!c) return PyErr_Occurred() ? nullptr : (PyErr_SetString(PyExc_ValueError, "ccmpi: communicator freed"), nullptr);
   if (r.nbytes() != s.nbytes() * (size_t)c->size()) return not_impl();
   if (!guarded([&] { c->allgather(s.ptr(), s.nbytes(), r.ptr()); })) return nullptr;
   Py_RETURN_NONE;
@@ -325,6 +334,7 @@ PyObject* f_alltoall(PyObject*, PyObject* const* a, Py_ssize_t n) {
   View s, r;
   if (!view_of(a[1], false, false, s) || !view_of(a[2], true, false, r)) return not_impl();
   ShmComm* c = comm_of(a[0]);
+  if (!c) return PyErr_Occurred() ? nullptr : (PyErr_SetString(PyExc_ValueError, "ccmpi: communicator freed"), nullptr);
   if (s.nbytes() != r.nbytes() || r.nbytes() % (size_t)c->size()) return not_impl();
   if (!guarded([&] { c->alltoall(s.ptr(), r.nbytes() / c->size(), r.ptr()); })) return nullptr;
   Py_RETURN_NONE;
@@ -336,6 +346,7 @@ PyObject* f_reduce_scatter_block(PyObject*, PyObject* const* a, Py_ssize_t n) {
   if (!view_of(a[1], false, true, s) || !view_of(a[2], true, true, r)) return not_impl();
   const int dt = dtype_of(r);
   ShmComm* c = comm_of(a[0]);
+  if (!c) return PyErr_Occurred() ? nullptr : (PyErr_SetString(PyExc_ValueError, "ccmpi: communicator freed"), nullptr);
   if (dt < 0 || dtype_of(s) != dt || s.nbytes() != r.nbytes() * (size_t)c->size()) return not_impl();
   int op = (int)PyLong_AsLong(a[3]);
   if (PyErr_Occurred()) return nullptr;
@@ -354,6 +365,7 @@ PyObject* f_my_allreduce(PyObject*, PyObject* const* a, Py_ssize_t n) {
   const int dt = dtype_of(r);
   if (dt < 0 || dtype_of(s) != dt || s.nbytes() != r.nbytes()) return not_impl();
   ShmComm* c = comm_of(a[0]);
+  if (!c) return PyErr_Occurred() ? nullptr : (PyErr_SetString(PyExc_ValueError, "ccmpi: communicator freed"), nullptr);
   int op = (int)PyLong_AsLong(a[3]), algo = (int)PyLong_AsLong(a[4]);
   if (PyErr_Occurred()) return nullptr;
   if (!reduce_supported(dt, op)) return not_impl();
@@ -376,6 +388,7 @@ PyObject* f_my_alltoall(PyObject*, PyObject* const* a, Py_ssize_t n) {
   View s, r;
   if (!view_of(a[1], false, false, s) || !view_of(a[2], true, false, r)) return not_impl();
   ShmComm* c = comm_of(a[0]);
+  if (!c) return PyErr_Occurred() ? nullptr : (PyErr_SetString(PyExc_ValueError, "ccmpi: communicator freed"), nullptr);
   const int pairwise = PyObject_IsTrue(a[3]);
   if (pairwise < 0) return nullptr;
   if (s.nbytes() != r.nbytes() || r.nbytes() % (size_t)c->size()) return not_impl();

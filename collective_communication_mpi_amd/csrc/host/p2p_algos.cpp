@@ -15,6 +15,7 @@
 // Messages carry negative internal tags, so user receives posted with
 // ANY_TAG never match them (tag_match in shm_comm.cpp).
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <stdexcept>
 #include <vector>
@@ -51,6 +52,19 @@ void prefault(void* p, size_t n) {
   for (uintptr_t o = 0; o < n; o = ((a + o) / kPage + 1) * kPage - a) c[o] = 0;
 }
 
+}  // namespace
+
+// Optional phase timestamps of the reduce->bcast schedule (CCMPI_P2P_TRACE=1), read back
+// with p2p_trace(): a diagnostic for where a call's time goes, off by default.
+bool g_p2p_trace_on = std::getenv("CCMPI_P2P_TRACE") != nullptr;
+std::vector<double> g_p2p_trace;
+
+namespace {
+
+inline void trace_mark() {
+  if (g_p2p_trace_on) g_p2p_trace.push_back(wtime());
+}
+
 bool overlaps(const void* a, const void* b, size_t n) {
   const char* x = static_cast<const char*>(a);
   const char* y = static_cast<const char*>(b);
@@ -82,14 +96,17 @@ void ShmComm::my_reduce_bcast(const void* src, void* dst, size_t count, int dt, 
     }
     // slices 1..p-1 receive, slice 0 accumulates: the sends go out of scratch and the copy
     // into dst (whose first touch may fault) comes after them
+    trace_mark();
     char* tmp = scratch(nb * (size_t)size_);
     char* acc = tmp;
     std::vector<RequestPtr> rr;
     rr.reserve(size_);
     for (int i = 1; i < size_; ++i) rr.push_back(irecv(tmp + nb * (size_t)i, nb, i, kTagReduceBcast));
     std::memcpy(acc, src, nb);
+    trace_mark();
     for (int i = 1; i < size_; ++i) {
       wait(rr[i - 1]);
+      trace_mark();
       reduce_inplace(acc, tmp + nb * (size_t)i, count, dt, op);
     }
     // the reference sends in rank order with blocking Sends; posting them all
@@ -98,21 +115,29 @@ void ShmComm::my_reduce_bcast(const void* src, void* dst, size_t count, int dt, 
     std::vector<RequestPtr> rs;
     rs.reserve(size_);
     for (int i = 1; i < size_; ++i) rs.push_back(isend_raw(acc, nb, i, kTagReduceBcast));
+    trace_mark();
     std::memmove(dst, acc, nb);
     waitall(rs);
+    trace_mark();
   } else {
     if (dst == src) {
       char* tmp = scratch(nb);
       std::memcpy(tmp, src, nb);
       src = tmp;
     }
+    trace_mark();
     auto rr = irecv(dst, nb, 0, kTagReduceBcast);  // posted first: the result lands in place
+    trace_mark();
     auto rs = isend_raw(src, nb, 0, kTagReduceBcast);
+    trace_mark();
     // no receive progress has run since the irecv (isend_raw only pushes the send), so
     // dst holds no result bytes yet: fault its pages in while the root reduces
     prefault(dst, nb);
+    trace_mark();
     wait(rs);
+    trace_mark();
     wait(rr);
+    trace_mark();
   }
 }
 

@@ -240,5 +240,7 @@ class ShmComm : public std::enable_shared_from_this<ShmComm> {
 
 double wtime();
 std::string job_id_from_env();
+extern bool g_p2p_trace_on;              // p2p_algos.cpp: CCMPI_P2P_TRACE
+extern std::vector<double> g_p2p_trace;  // reduce->bcast phase timestamps
 
 }  // namespace ccmpi

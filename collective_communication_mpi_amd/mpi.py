@@ -861,6 +861,7 @@ class Comm:
 
     def Free(self) -> None:
         self._hc = None
+        self._p = None  # the fastcall entry points must not see the freed communicator
 
     def Abort(self, errorcode: int = 1) -> None:
         import os

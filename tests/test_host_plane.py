@@ -37,6 +37,31 @@ def test_mpi_test_cli_cases():
         "This is rank 0.", "This is rank 1.", "This is rank 2."]
 
 
+def test_launcher_binds_ranks_to_distinct_cores():
+    """Default binding (l3): each rank on its own allowed CPU, one per physical core, the
+    launcher's L3 domain first; ``CCMPI_BIND=none`` leaves the affinity alone; more ranks
+    than cores: no binding."""
+    import os
+
+    from collective_communication_mpi_amd.launch import l3_plan
+
+    allowed = sorted(os.sched_getaffinity(0))
+    code = "import os; print('CPU', os.environ['CCMPI_RANK'], sorted(os.sched_getaffinity(0)))"
+    n = min(2, len(allowed))
+    plan = l3_plan(n)
+    r = run_ranks(n, py("-c", code), timeout=60)
+    got = {int(l.split()[1]): eval(l.split(None, 2)[2]) for l in r.stdout.splitlines() if l.startswith("CPU")}
+    assert sorted(got) == list(range(n))
+    if plan is None:
+        assert all(v == allowed for v in got.values())
+    else:  # (the launcher's own CPU picks the domain, so compare properties, not the plan)
+        cpus = [v[0] for v in got.values()]
+        assert all(len(v) == 1 for v in got.values()) and len(set(cpus)) == n and set(cpus) <= set(allowed)
+    r = run_ranks(n, py("-c", code), timeout=60, env={"CCMPI_BIND": "none"})
+    assert all(eval(l.split(None, 2)[2]) == allowed for l in r.stdout.splitlines() if l.startswith("CPU"))
+    assert l3_plan(len(allowed) + 1) is None
+
+
 def test_launcher_propagates_failure():
     r = run_ranks(3, py("-c", "import os,sys; sys.exit(3 if os.environ['CCMPI_RANK']=='1' else 0)"),
                   timeout=60, check=False)
