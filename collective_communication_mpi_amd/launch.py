@@ -14,12 +14,14 @@ Open MPI style flags that make no sense for a single-host shm runtime
 (``--oversubscribe``, ``--allow-run-as-root``, ``-H host``) are accepted and ignored;
 ``-x VAR[=VAL]`` exports a variable.  Binding (``--bind-to`` / ``CCMPI_BIND``):
 
-* ``l3`` (default): rank r runs on one hardware thread of the r-th physical core, filling the
-  L3 domain (CCD) the launcher runs in first, then the next ones.  The host plane's messages
-  are shared-memory cache lines moving between the ranks' cores: on the MI355X box's 2 x
-  64-core EPYC the OS spread 8 ranks over 8 CCDs, and every line crossed the IO die
-  (8-rank library Allreduce of 4 KiB 8.1 us unbound, 3.3 us in one CCD; the reference's
-  myAllreduce loop 26.3 -> 14.8 us; ``profiles/r5_host/``);
+* ``l3`` (default): every rank may run on any hardware thread of the fewest L3 domains
+  (CCDs) that hold one physical core per rank, the launcher's own domain first.  The host
+  plane's messages are shared-memory cache lines moving between the ranks' cores: on the
+  MI355X box's 2 x 64-core EPYC the OS spread 8 ranks over 8 CCDs, and every line crossed
+  the IO die (8-rank library Allreduce of 4 KiB 8.1 us unbound, 3.3-3.9 us in one CCD; the
+  reference's myAllreduce loop 26.3 -> 14.8-17.3 us; ``profiles/r5_host/``).  A set rather
+  than one CPU per rank: a GPU rank's runtime threads (HIP, RCCL proxy) float within it;
+* ``l3core``: rank r on one hardware thread of the r-th physical core of those domains;
 * ``core``: rank r on the r-th CPU the launcher may use;
 * ``none`` (or any other level): placement left to the OS.
 No binding either when there are more ranks than allowed physical cores.
@@ -106,29 +108,52 @@ def _read_cpu_list(path: str) -> List[int]:
     return out
 
 
+def _l3_domains():
+    """(domains in placement order, allowed CPUs by domain): L3 key -> one allowed hardware
+    thread per physical core, the launcher's own domain first."""
+    allowed = set(os.sched_getaffinity(0))
+    sysfs = "/sys/devices/system/cpu"
+    cores, threads = {}, {}
+    seen_core = set()
+    dom_of = {}
+    for c in sorted(allowed):
+        sib = tuple(_read_cpu_list(f"{sysfs}/cpu{c}/topology/thread_siblings_list"))
+        key = tuple(_read_cpu_list(f"{sysfs}/cpu{c}/cache/index3/shared_cpu_list"))
+        dom_of[c] = key
+        threads.setdefault(key, []).append(c)
+        if sib in seen_core:
+            continue
+        seen_core.add(sib)
+        cores.setdefault(key, []).append(c)
+    first = dom_of.get(_current_cpu())
+    order = sorted(cores, key=lambda k: (k != first, min(k)))
+    return order, cores, threads
+
+
 def l3_plan(n: int) -> Optional[List[int]]:
     """CPUs for n ranks: one allowed hardware thread per physical core, the launcher's own L3
     domain first, then the other domains in CPU order; None if that gives fewer than n CPUs
     or the topology is unreadable."""
     try:
-        allowed = set(os.sched_getaffinity(0))
-        sysfs = "/sys/devices/system/cpu"
-        domains = {}   # L3 key -> CPUs (one per core)
-        seen_core = set()
-        dom_of = {}
-        for c in sorted(allowed):
-            sib = tuple(_read_cpu_list(f"{sysfs}/cpu{c}/topology/thread_siblings_list"))
-            key = tuple(_read_cpu_list(f"{sysfs}/cpu{c}/cache/index3/shared_cpu_list"))
-            dom_of[c] = key
-            if sib in seen_core:
-                continue
-            seen_core.add(sib)
-            domains.setdefault(key, []).append(c)
-        cur = _current_cpu()
-        first = dom_of.get(cur)
-        order = sorted(domains, key=lambda k: (k != first, min(k)))
-        plan = [c for k in order for c in domains[k]]
+        order, cores, _ = _l3_domains()
+        plan = [c for k in order for c in cores[k]]
         return plan[:n] if len(plan) >= n else None
+    except (OSError, ValueError):
+        return None
+
+
+def l3_set(n: int) -> Optional[List[int]]:
+    """One CPU set for all n ranks: every allowed hardware thread of the fewest L3 domains
+    (launcher's first) that hold n physical cores; None as for ``l3_plan``."""
+    try:
+        order, cores, threads = _l3_domains()
+        out, ncores = [], 0
+        for k in order:
+            out += threads[k]
+            ncores += len(cores[k])
+            if ncores >= n:
+                return sorted(out)
+        return None
     except (OSError, ValueError):
         return None
 
@@ -142,12 +167,16 @@ def launch(n: int, cmd: List[str], timeout: Optional[float] = None, env_extra=No
     pp = base.get("PYTHONPATH", "")
     base["PYTHONPATH"] = str(REPO) + (os.pathsep + pp if pp else "")
     bind = base.get("CCMPI_BIND", "l3")
-    plan = None
+    plan = None  # per rank: the CPU set it is bound to
     if bind == "l3":
-        plan = l3_plan(n)
+        dom = l3_set(n)
+        plan = [dom] * n if dom is not None else None
+    elif bind == "l3core":
+        cpus = l3_plan(n)
+        plan = [[c] for c in cpus] if cpus is not None else None
     elif bind == "core":
         cpus = sorted(os.sched_getaffinity(0))
-        plan = [cpus[r % len(cpus)] for r in range(n)]
+        plan = [[cpus[r % len(cpus)]] for r in range(n)]
     for r in range(n):
         env = dict(base)
         env.update({
@@ -160,9 +189,9 @@ def launch(n: int, cmd: List[str], timeout: Optional[float] = None, env_extra=No
             env.pop(k, None)
         pin = plan[r] if plan is not None else None
         if pin is not None:
-            env["CCMPI_BOUND_CPU"] = str(pin)
+            env["CCMPI_BOUND_CPUS"] = ",".join(map(str, pin))
         procs.append(subprocess.Popen(cmd, env=env, start_new_session=True,
-                                      preexec_fn=(lambda c=pin: os.sched_setaffinity(0, {c})) if pin is not None else None))
+                                      preexec_fn=(lambda c=pin: os.sched_setaffinity(0, set(c))) if pin is not None else None))
 
     def kill_all(sig=signal.SIGTERM):
         for p in procs:

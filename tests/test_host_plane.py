@@ -38,18 +38,24 @@ def test_mpi_test_cli_cases():
 
 
 def test_launcher_binds_ranks_to_distinct_cores():
-    """Default binding (l3): each rank on its own allowed CPU, one per physical core, the
-    launcher's L3 domain first; ``CCMPI_BIND=none`` leaves the affinity alone; more ranks
-    than cores: no binding."""
+    """``CCMPI_BIND=l3core``: each rank on its own allowed CPU, one per physical core, the
+    launcher's L3 domain first; default ``l3``: all ranks share one set of allowed CPUs
+    holding enough cores; ``none`` leaves the affinity alone; more ranks than cores: no
+    binding."""
     import os
 
-    from collective_communication_mpi_amd.launch import l3_plan
+    from collective_communication_mpi_amd.launch import l3_plan, l3_set
 
     allowed = sorted(os.sched_getaffinity(0))
     code = "import os; print('CPU', os.environ['CCMPI_RANK'], sorted(os.sched_getaffinity(0)))"
     n = min(2, len(allowed))
-    plan = l3_plan(n)
     r = run_ranks(n, py("-c", code), timeout=60)
+    sets = [eval(l.split(None, 2)[2]) for l in r.stdout.splitlines() if l.startswith("CPU")]
+    dom = l3_set(n)
+    assert len(sets) == n and all(v == sets[0] for v in sets)
+    assert sets[0] == allowed if dom is None else (set(sets[0]) <= set(allowed) and len(sets[0]) >= n)
+    plan = l3_plan(n)
+    r = run_ranks(n, py("-c", code), timeout=60, env={"CCMPI_BIND": "l3core"})
     got = {int(l.split()[1]): eval(l.split(None, 2)[2]) for l in r.stdout.splitlines() if l.startswith("CPU")}
     assert sorted(got) == list(range(n))
     if plan is None:
@@ -59,7 +65,7 @@ def test_launcher_binds_ranks_to_distinct_cores():
         assert all(len(v) == 1 for v in got.values()) and len(set(cpus)) == n and set(cpus) <= set(allowed)
     r = run_ranks(n, py("-c", code), timeout=60, env={"CCMPI_BIND": "none"})
     assert all(eval(l.split(None, 2)[2]) == allowed for l in r.stdout.splitlines() if l.startswith("CPU"))
-    assert l3_plan(len(allowed) + 1) is None
+    assert l3_plan(len(allowed) + 1) is None and l3_set(len(allowed) + 1) is None
 
 
 def test_launcher_propagates_failure():
