@@ -124,6 +124,164 @@ __global__ void __launch_bounds__(256) k_xent_head16(const float* __restrict__ z
   }
 }
 
+// Loss head + output-weight gradient in one launch, for the harness's pooled / per-token
+// fc_o (logits z = pool W_o^T + o_b, pool = the sequence mean of the attention output):
+// loss, dz (bf16) and dbias as k_xent_head16 (z already holds + o_b), and
+//
+//   dW_o[c][j] += sum_b dz[b][c] * pool[b][j]      (c < C, j < HD; bf16 dz and pool, fp32 sums)
+//
+// which the backward otherwise runs as a split-K TN GEMM dZ^T pool: a second launch of
+// ~7 us at B = 2048 for 16 x 256 outputs.  Grid (ceil(B / 64), ceil(HD / 64)): workgroup
+// (x, y) forms the gradient of rows 64x.. (every y recomputes that small softmax; y = 0
+// alone stores dz, dbias and the loss partial; 4 lanes per row, 4 classes per lane), then the
+// 16 x 64 dW_o tile of columns 64y..:
+// wave q sums rows 16q..16q+15 for column 64y + lane from pool values fetched before the
+// softmax, the four quarters meet in LDS, and one atomic per (class, column) leaves.
+constexpr int kWoRows = 64;
+
+__global__ void __launch_bounds__(256) k_xent_head_wo(const float* __restrict__ z, int ld_z, const void* __restrict__ y,
+                                                      int y64, int B, int C, int Cpad, float scale,
+                                                      float* __restrict__ loss, uint16_t* __restrict__ dz, int ld_dz,
+                                                      float* __restrict__ dbias, const uint16_t* __restrict__ pool,
+                                                      int ld_pool, int HD, float* __restrict__ dwo, int ld_dwo,
+                                                      float* __restrict__ partial, unsigned* __restrict__ ticket) {
+  __shared__ __attribute__((aligned(16))) float s_g[kWoRows][16];  // the rows' bf16-rounded gradient
+  __shared__ float s_acc[3][16][64];  // row quarters 1..3 of the dW_o tile
+  __shared__ float s_db[4][16];
+  __shared__ float s_loss[4];
+  __shared__ bool s_last;
+  const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
+  const int b0 = blockIdx.x * kWoRows;
+  const bool head = blockIdx.y == 0;
+  const int j = blockIdx.y * 64 + lane;
+  uint16_t pv[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int b = b0 + wave * 16 + r;
+    pv[r] = (b < B && j < HD) ? pool[(size_t)b * ld_pool + j] : (uint16_t)0;
+  }
+  // softmax: 4 lanes per row (classes 4q .. 4q + 3 on lane q of the row), all 64 rows at once
+  const int rl = t >> 2, q = t & 3, c0 = 4 * q;
+  const int b = b0 + rl;
+  const bool live = b < B;
+  float v[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) v[e] = (live && c0 + e < C) ? z[(size_t)b * ld_z + c0 + e] : -INFINITY;
+  const int label = !live ? -1 : y64 ? (int)reinterpret_cast<const int64_t*>(y)[b] : reinterpret_cast<const int32_t*>(y)[b];
+  float m = fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3]));
+  m = fmaxf(m, __shfl_xor(m, 1));
+  m = fmaxf(m, __shfl_xor(m, 2));
+  float ex[4], s = 0.f;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    ex[e] = (c0 + e < C) ? __expf(v[e] - m) : 0.f;
+    s += ex[e];
+  }
+  s += __shfl_xor(s, 1);
+  s += __shfl_xor(s, 2);
+  const float inv = 1.f / s, lse = m + __logf(s);
+  float l = 0.f, gf[4];
+  uint16_t gb[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int c = c0 + e;
+    if (live && c == label) l += (lse - v[e]) * scale;
+    const float gr = (live && c < C) ? (ex[e] * inv - (c == label ? 1.f : 0.f)) * scale : 0.f;
+    gb[e] = (uint16_t)f32_to_bf16_bits(gr);
+    gf[e] = gr;
+  }
+  *reinterpret_cast<float4*>(&s_g[rl][c0]) = float4{__uint_as_float((uint32_t)gb[0] << 16), __uint_as_float((uint32_t)gb[1] << 16),
+                                                    __uint_as_float((uint32_t)gb[2] << 16), __uint_as_float((uint32_t)gb[3] << 16)};
+  if (head && live) {
+    if (c0 + 3 < Cpad) {
+      *reinterpret_cast<uint2*>(dz + (size_t)b * ld_dz + c0) =
+          uint2{(uint32_t)gb[0] | ((uint32_t)gb[1] << 16), (uint32_t)gb[2] | ((uint32_t)gb[3] << 16)};
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (c0 + e < Cpad) dz[(size_t)b * ld_dz + c0 + e] = gb[e];
+    }
+  }
+  __syncthreads();
+  float acc[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) acc[k] = 0.f;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const float p = __uint_as_float((uint32_t)pv[r] << 16);
+    const float4* g = reinterpret_cast<const float4*>(s_g[wave * 16 + r]);
+#pragma unroll
+    for (int k4 = 0; k4 < 4; ++k4) {
+      const float4 w = g[k4];
+      acc[4 * k4 + 0] = fmaf(w.x, p, acc[4 * k4 + 0]);
+      acc[4 * k4 + 1] = fmaf(w.y, p, acc[4 * k4 + 1]);
+      acc[4 * k4 + 2] = fmaf(w.z, p, acc[4 * k4 + 2]);
+      acc[4 * k4 + 3] = fmaf(w.w, p, acc[4 * k4 + 3]);
+    }
+  }
+  if (wave > 0)
+#pragma unroll
+    for (int k = 0; k < 16; ++k) s_acc[wave - 1][k][lane] = acc[k];
+  if (head) {
+    // class sums over the wave's 16 rows (lanes with the same q), loss over the wave
+    float cs[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      cs[e] = gf[e];
+#pragma unroll
+      for (int o = 4; o < 64; o <<= 1) cs[e] += __shfl_xor(cs[e], o);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) l += __shfl_xor(l, o);
+    if (lane < 4)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) s_db[wave][4 * lane + e] = cs[e];
+    if (lane == 0) s_loss[wave] = l;
+  }
+  __syncthreads();
+  if (wave == 0 && j < HD) {
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+      if (k < C)
+        atomicAdd(dwo + (size_t)k * ld_dwo + j, acc[k] + s_acc[0][k][lane] + s_acc[1][k][lane] + s_acc[2][k][lane]);
+  }
+  if (head) {  // workgroup-uniform
+    if (t < C && dbias) atomicAdd(dbias + t, s_db[0][t] + s_db[1][t] + s_db[2][t] + s_db[3][t]);
+    // loss: the head workgroups' partials, summed in a fixed order by the last to finish
+    if (t == 0) {
+      partial[blockIdx.x] = s_loss[0] + s_loss[1] + s_loss[2] + s_loss[3];
+      __threadfence();
+      s_last = atomicAdd(ticket, 1u) == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (s_last && t < 64) {
+      __threadfence();
+      float a = 0.f;
+      for (int i = t; i < (int)gridDim.x; i += 64) a += __hip_atomic_load(partial + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o);
+      if (t == 0) {
+        *loss = a;
+        *ticket = 0u;
+      }
+    }
+  }
+}
+
+void xent_head_wo(uint64_t z, int ld_z, uint64_t y, bool y64, int B, int C, int Cpad, float scale, uint64_t loss,
+                  uint64_t dz, int ld_dz, uint64_t dbias, uint64_t pool, int ld_pool, int HD, uint64_t dwo, int ld_dwo,
+                  uint64_t stream, uint64_t workspace) {
+  if (C < 1 || Cpad < C || Cpad > 16) throw std::invalid_argument("xent_head_wo: need 1 <= n_classes <= pad <= 16");
+  if (!workspace || !pool || !dwo || HD <= 0 || ld_pool < HD || ld_dwo < HD)
+    throw std::invalid_argument("xent_head_wo: workspace, pool [B][>= HD] and dW_o [C][>= HD] required");
+  if (dz % 8 || ld_dz % 4) throw std::invalid_argument("xent_head_wo: dz 8-B aligned with a row stride % 4 == 0");
+  if (B <= 0) return;
+  hipLaunchKernelGGL(k_xent_head_wo, dim3((B + kWoRows - 1) / kWoRows, (HD + 63) / 64), dim3(256), 0,
+                     (hipStream_t)stream, (const float*)z, ld_z, (const void*)y, y64 ? 1 : 0, B, C, Cpad, scale,
+                     (float*)loss, (uint16_t*)dz, ld_dz, (float*)dbias, (const uint16_t*)pool, ld_pool, HD, (float*)dwo,
+                     ld_dwo, reinterpret_cast<float*>(workspace) + 1, reinterpret_cast<unsigned*>(workspace));
+  CCMPI_HIP_CHECK(hipGetLastError());
+}
+
 void xent_head(uint64_t z, int ld_z, uint64_t bias, uint64_t y, bool y64, int B, int C, int Cpad, float scale,
                uint64_t loss, uint64_t dz, int ld_dz, uint64_t dbias, uint64_t stream, uint64_t workspace) {
   if (C < 1 || C > kMaxClasses || Cpad < C) throw std::invalid_argument("xent_head: need 1 <= n_classes <= 64 <= pad");
@@ -156,6 +314,14 @@ void register_head_ops(pybind11::module_& m) {
         pybind11::arg("B"), pybind11::arg("C"), pybind11::arg("Cpad"), pybind11::arg("scale"), pybind11::arg("loss"),
         pybind11::arg("dz"), pybind11::arg("ld_dz"), pybind11::arg("dbias"), pybind11::arg("stream"),
         pybind11::arg("workspace") = 0, pybind11::call_guard<pybind11::gil_scoped_release>());
+  m.def("xent_head_wo", &xent_head_wo,
+        "xent_head (z already + bias, lane-per-class, workspace 4 + 4*ceil(B/64) bytes zeroed once) plus "
+        "dW_o[c][j] += sum_b dz[b][c] pool[b][j] (bf16 pool, fp32 atomics) in one launch",
+        pybind11::arg("z"), pybind11::arg("ld_z"), pybind11::arg("y"), pybind11::arg("y64"), pybind11::arg("B"),
+        pybind11::arg("C"), pybind11::arg("Cpad"), pybind11::arg("scale"), pybind11::arg("loss"), pybind11::arg("dz"),
+        pybind11::arg("ld_dz"), pybind11::arg("dbias"), pybind11::arg("pool"), pybind11::arg("ld_pool"),
+        pybind11::arg("HD"), pybind11::arg("dwo"), pybind11::arg("ld_dwo"), pybind11::arg("stream"),
+        pybind11::arg("workspace"), pybind11::call_guard<pybind11::gil_scoped_release>());
 }
 
 }  // namespace dev

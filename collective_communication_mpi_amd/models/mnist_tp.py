@@ -757,13 +757,41 @@ class MnistTPLayer:
             ws = self._bufs["xent_ws"] = torch.zeros(1 + (B + 15) // 16 + 64, dtype=torch.float32, device=self.device)
         if y.dtype not in (torch.int32, torch.int64) or not y.is_contiguous():
             y = y.to(torch.int32).contiguous()
-        _native.device().xent_head(zp.data_ptr(), zp.stride(0), 0, y.data_ptr(),  # zp already holds + o_b
-                                   y.dtype == torch.int64, B,
-                                   cfg.n_classes, cfg.out_pad, 1.0 / global_batch, loss.data_ptr(), dzp.data_ptr(),
-                                   dzp.stride(0), self.flat.grad("o_b").data_ptr(),
-                                   torch.cuda.current_stream(self.device).cuda_stream, ws.data_ptr())
+        st = torch.cuda.current_stream(self.device).cuda_stream
+        pool = self._head_wo_pool(B)
+        if pool is not None:
+            # + dW_o = dZ^T pool in the same launch (the backward then skips its TN GEMM)
+            gw = self.flat.grad("o_w")
+            _native.device().xent_head_wo(zp.data_ptr(), zp.stride(0), y.data_ptr(), y.dtype == torch.int64, B,
+                                          cfg.n_classes, cfg.out_pad, 1.0 / global_batch, loss.data_ptr(),
+                                          dzp.data_ptr(), dzp.stride(0), self.flat.grad("o_b").data_ptr(),
+                                          pool.data_ptr(), pool.stride(0), pool.shape[1], gw.data_ptr(), gw.stride(0),
+                                          st, ws.data_ptr())
+            self._dwo_done = True
+        else:
+            _native.device().xent_head(zp.data_ptr(), zp.stride(0), 0, y.data_ptr(),  # zp already holds + o_b
+                                       y.dtype == torch.int64, B,
+                                       cfg.n_classes, cfg.out_pad, 1.0 / global_batch, loss.data_ptr(), dzp.data_ptr(),
+                                       dzp.stride(0), self.flat.grad("o_b").data_ptr(), st, ws.data_ptr())
         self._dz_ready = True
         return loss[0]
+
+    def _head_wo_pool(self, B: int):
+        """The saved pooled activations when the backward's output-head branch would form
+        dW_o = dZ^T pool with its TN GEMM (pooled row-parallel / fused per-token fc_o), so the
+        loss head can fold it in (``xent_head_wo``); None otherwise (or CCMPI_HEAD_WO=0)."""
+        cfg = self.cfg
+        if os.environ.get("CCMPI_HEAD_WO", "1") == "0" or self._saved is None or cfg.out_pad > 16:
+            return None
+        if (cfg.fc_o_mode == "naive" and cfg.tp > 1) or (cfg.fc_o_mode == "token" and not self._fused_fc_o_bwd()):
+            return None
+        pool = self._saved[6]
+        if pool is None or self._saved[5] != B or pool.dtype != torch.bfloat16 or pool.stride(1) != 1:
+            return None
+        gw = self.flat.grad("o_w")
+        if gw.dim() != 2 or gw.shape[1] != pool.shape[1] or gw.stride(1) != 1:
+            return None
+        return pool
 
     def loss_and_grad(self, logits: torch.Tensor, y: torch.Tensor, global_batch: int):
         """Cross-entropy (mean over the global batch); returns (local loss sum / global batch, dlogits)."""
@@ -811,8 +839,11 @@ class MnistTPLayer:
                 dzp.zero_()
                 dzp[:, : cfg.n_classes] = dlogits.to(torch.bfloat16)
             # dW_o = dZ^T . pooled: 16 x hd over B rows, latency-bound; 32 K-splits measured fastest
-            # (benchmarks/tn_small.py: 9.6 us at 8 splits, 7.2 us at 32)
-            gemm_tn(dzp, pool, out=G("o_w"), accumulate=True, splitk=max(1, min(32, B // 64)))
+            # (benchmarks/tn_small.py: 9.6 us at 8 splits, 7.2 us at 32) -- unless the fused loss
+            # head already added it (xent_head_wo)
+            if not (fused and getattr(self, "_dwo_done", False)):
+                gemm_tn(dzp, pool, out=G("o_w"), accumulate=True, splitk=max(1, min(32, B // 64)))
+            self._dwo_done = False
             if self._fused_fc_o_bwd():
                 dout, dout_b, dout_r = None, 0, 0                   # dpool formed inside the attention bwd
             else:

@@ -673,6 +673,42 @@ def test_xent_head_fused(ydtype, C, Cp):
     torch.testing.assert_close(db[C:], torch.ones(Cp - C, device="cuda"))
 
 
+@pytest.mark.parametrize("B,HD,C,Cp", [(777, 256, 10, 16), (2048, 128, 10, 16), (130, 100, 5, 8)])
+@pytest.mark.parametrize("ydtype", [torch.int32, torch.int64])
+def test_xent_head_wo_fused(B, HD, C, Cp, ydtype):
+    """Loss head + dW_o = dZ^T pool in one launch vs torch: loss, bf16 dZ (zero padding), d bias,
+    and dW_o accumulated into a non-zero buffer from the bf16 dZ and pool."""
+    from collective_communication_mpi_amd import _native
+
+    gb = 3000
+    g = torch.Generator(device="cuda").manual_seed(B + HD)
+    z = torch.randn(B, Cp, device="cuda", generator=g) * 3
+    y = torch.randint(0, C, (B,), device="cuda", generator=g).to(ydtype)
+    pool = torch.randn(B, HD, device="cuda", generator=g).bfloat16()
+    loss = torch.empty(1, device="cuda")
+    dz = torch.full((B, Cp), 7.0, device="cuda").bfloat16()
+    db = torch.ones(Cp, device="cuda")
+    dwo = torch.full((Cp, HD + 4), 0.5, device="cuda")  # padded rows: ld > HD
+    ws = torch.zeros(1 + (B + 63) // 64, device="cuda")
+    for _ in range(2):  # the second call checks the re-armed ticket
+        _native.device().xent_head_wo(z.data_ptr(), z.stride(0), y.data_ptr(), ydtype == torch.int64, B, C, Cp, 1.0 / gb,
+                                      loss.data_ptr(), dz.data_ptr(), dz.stride(0), db.data_ptr(), pool.data_ptr(),
+                                      pool.stride(0), HD, dwo.data_ptr(), dwo.stride(0),
+                                      torch.cuda.current_stream().cuda_stream, ws.data_ptr())
+    torch.cuda.synchronize()
+    logits = z[:, :C].clone().requires_grad_(True)
+    ref = torch.nn.functional.cross_entropy(logits, y.long(), reduction="sum") / gb
+    ref.backward()
+    torch.testing.assert_close(loss[0], ref.detach(), rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(dz[:, :C].float(), logits.grad, rtol=1e-2, atol=1e-5)
+    assert torch.all(dz[:, C:] == 0)
+    torch.testing.assert_close(db[:C], 1 + 2 * logits.grad.sum(0), rtol=1e-4, atol=1e-6)
+    torch.testing.assert_close(db[C:], torch.ones(Cp - C, device="cuda"))
+    wref = dz[:, :C].float().T @ pool.float()  # from the bf16 gradient the kernel stores
+    torch.testing.assert_close(dwo[:C, :HD], 0.5 + 2 * wref, rtol=1e-4, atol=1e-5)
+    assert torch.all(dwo[C:] == 0.5) and torch.all(dwo[:, HD:] == 0.5)
+
+
 def test_flat_params_transposed_copies():
     """Fused AdamW / cast keep W^T bf16 copies in sync with the flat master weights."""
     from collective_communication_mpi_amd.parallel.dp import FlatParams
