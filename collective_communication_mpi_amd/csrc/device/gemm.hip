@@ -433,11 +433,12 @@ __device__ __forceinline__ int tn_off(int row, int byte) { return row * kTnRow +
 // split-minor order each XCD streams whole K panels of its own few tiles, and
 // the same bytes cross the fabric once per tile).
 // PF: K tiles in flight per workgroup.  PF = 1 issues tile k+1's global loads under tile k's
-// MFMAs, so with few workgroups (a narrow output split over K) every tile waits out most
-// of a memory round trip; PF = 2 keeps tiles k+1 and k+2 in flight in two register sets
-// (the loop unrolled by two so the sets are indexed statically).
+// MFMAs; PF = 2 keeps tiles k+1 and k+2 in flight in two register sets (the loop unrolled so
+// the sets are indexed statically): 5-8 % faster on the dQKV^T Xp and 4096^2 shapes.  PF = 4
+// (one wave per SIMD) measured no faster on the narrow shape and 20 % slower on the wide ones
+// (profiles/r5_train_kernels/gemm_tn_pf4.jsonl), so only 1 and 2 are built.
 template <int FAST, int PF = 1>
-__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2))) k_gemm_tn(GemmArgs g, int split_major) {
+__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(PF >= 4 ? 1 : 2))) k_gemm_tn(GemmArgs g, int split_major) {
   __shared__ __attribute__((aligned(16))) unsigned char smem[4 * kTnTile];
   // here: g.M = N1 (rows of C), g.N = N2 (cols of C), g.K = M (reduction)
   const int tiles_n = (g.N + BN - 1) / BN, tiles_m = (g.M + BM - 1) / BM;
@@ -480,7 +481,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2))) k_
   // neighbours, which only reach outputs that are never stored.
   const int rows = max(0, min(g.K - kt0 * BK, nk * BK));
   Rsrc rsa{}, rsb{};
-  if constexpr (PF == 2) {
+  if constexpr (PF >= 2) {
     rsa = make_rsrc(uniform_ptr(reinterpret_cast<char*>(const_cast<uint16_t*>(g.A + (size_t)kt0 * BK * g.lda))),
                     (uint32_t)((size_t)rows * g.lda * 2));
     rsb = make_rsrc(uniform_ptr(reinterpret_cast<char*>(const_cast<uint16_t*>(g.B + (size_t)kt0 * BK * g.ldb))),
@@ -491,7 +492,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2))) k_
     for (int i = 0; i < 4; ++i) {
       const int m = m0 + srow + 16 * i;
       const int ca = bm + schunk * 8, cb = bn + schunk * 8;
-      if constexpr (PF == 2) {
+      if constexpr (PF >= 2) {
         const uint32_t ml = (uint32_t)(m - kt0 * BK);
         ra[s][i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rsa.r, (ml * g.lda + ca) * 2, 0, 0));
         rb[s][i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rsb.r, (ml * g.ldb + cb) * 2, 0, 0));
@@ -549,23 +550,23 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2))) k_
       __syncthreads();
     }
   } else {
-    // tile j is loaded into register set j & 1 and written to LDS buffer j & 1 one
-    // iteration before its MFMAs; set j & 1 is refilled with tile j + 2 right after
-    if (nk > 0) gload(0, kt0 * BK);
-    if (nk > 1) gload(1, (kt0 + 1) * BK);
+    // tile j is loaded into register set j % PF and written to LDS buffer j & 1 one step
+    // before its MFMAs; set j % PF is refilled with tile j + PF right after that write
+#pragma unroll
+    for (int u = 0; u < PF; ++u)
+      if (u < nk) gload(u, (kt0 + u) * BK);
     if (nk > 0) swrite(0, 0);
     __syncthreads();
-    if (nk > 2) gload(0, (kt0 + 2) * BK);
-    for (int kt = 0; kt < nk; kt += 2) {
-      compute(0);
-      if (kt + 1 < nk) swrite(1, 1);
-      __syncthreads();
-      if (kt + 3 < nk) gload(1, (kt0 + kt + 3) * BK);
-      if (kt + 1 < nk) {
-        compute(1);
-        if (kt + 2 < nk) swrite(0, 0);
-        __syncthreads();
-        if (kt + 4 < nk) gload(0, (kt0 + kt + 4) * BK);
+    if (PF < nk) gload(0, (kt0 + PF) * BK);
+    for (int kt = 0; kt < nk; kt += PF) {
+#pragma unroll
+      for (int u = 0; u < PF; ++u) {
+        if (kt + u < nk) {
+          compute(u & 1);
+          if (kt + u + 1 < nk) swrite((u + 1) & 1, (u + 1) % PF);
+          __syncthreads();
+          if (kt + u + 1 + PF < nk) gload((u + 1) % PF, (kt0 + kt + u + 1 + PF) * BK);
+        }
       }
     }
   }
