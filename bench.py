@@ -1007,7 +1007,9 @@ def host_phase(args) -> dict:
     runs = args.host_runs
     rng = np.random.default_rng(1234 + rank)
     out = {"ranks": p, "count": n, "dtype": "float32", "runs": runs, "op": "MIN",
-           "timing": "per run: Barrier, Wtime, call, Barrier, Wtime (reference mpi-test.py:59-72); avg over runs"}
+           "timing": "per run: Barrier, Wtime, call, Barrier, Wtime (reference mpi-test.py:59-72); avg over runs",
+           # the launcher's CPU binding (default: one shared set of the fewest L3 domains)
+           "binding": os.environ.get("CCMPI_BIND", "l3"), "bound_cpus": os.environ.get("CCMPI_BOUND_CPUS")}
 
     def bench_pair(name_lib, lib, name_my, my, make):
         t_lib, t_my, ok = [], [], True
