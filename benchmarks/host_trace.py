@@ -34,6 +34,16 @@ for fresh in os.environ.get("HT_MODES", "fresh,reuse").split(","):
         elif fresh == "copyfresh":  # new arrays without the random-number work
             s = base.copy()
             d = np.empty(n, np.float32)
+        elif fresh == "fresh_touch_d":  # the reference's loop + the result written before the barrier
+            s = rng.standard_normal(n).astype(np.float32)
+            d = np.empty(n, np.float32)
+            d.fill(0)
+        elif fresh == "pool":  # 64 pre-touched (source, result) pairs in turn: new addresses, warm pages
+            if not hasattr(sys, "_ht_pool"):
+                sys._ht_pool = [(rng.standard_normal(n).astype(np.float32), np.zeros(n, np.float32)) for _ in range(64)]
+                sys._ht_i = 0
+            s, d = sys._ht_pool[sys._ht_i % 64]
+            sys._ht_i += 1
         comm.Barrier()
         t0 = H.wtime()
         comm.myAllreduce(s, d, op=MPI.MIN)
