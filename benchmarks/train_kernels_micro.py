@@ -40,7 +40,7 @@ def emit(**kw):
     print(json.dumps(kw), flush=True)
 
 
-only = sys.argv[1:] or ["wgrad", "gemm_tn_a", "gemm_tn_o"]
+only = sys.argv[1:] or ["wgrad", "gemm_tn_a", "gemm_tn_o", "bwd"]
 B, S, Cp = 2048, 16, 16
 R, d, kp = 768, 768, 72
 if "wgrad" in only:
@@ -84,3 +84,22 @@ if "gemm_tn_o" in only:
     for sk in (4, 8, 16, 32):
         us = t(lambda: gemm_tn(dzp, pool, out=go, accumulate=True, splitk=sk))
         emit(kernel="gemm_tn_o", splitk=sk, us=us)
+if "bwd" in only:
+    # the fused attention backward (token fc_o, dpool formed in-kernel) with / without the
+    # in-kernel QKV bias gradient, over workgroups per head
+    H, Dh, hd = 4, 64, 256
+    qkv = (torch.randn(B * S, 3 * hd, device="cuda") * 0.5).bfloat16()
+    lse = torch.randn(B * H * S, device="cuda").abs() + 2
+    dqkv = torch.empty(B * S, 3 * hd, device="cuda").bfloat16()
+    dbias = torch.zeros(3 * hd, device="cuda")
+    dzp = torch.randn(B, Cp, device="cuda").bfloat16()
+    wo = torch.randn(Cp, hd, device="cuda").bfloat16()
+    for cap in (0, 512, 2048, 4096):
+        D.attn_set_bwd_grid(cap)
+        for with_db in (True, False):
+            us = t(lambda: D.attn_small_bwd(qkv.data_ptr(), 0, lse.data_ptr(), 0, dqkv.data_ptr(),
+                                            dbias.data_ptr() if with_db else 0, B, S, H, Dh, qkv.stride(0), hd,
+                                            Dh ** -0.5, 0, 0, st(), dz=dzp.data_ptr(), ld_dz=dzp.stride(0),
+                                            wo=wo.data_ptr(), ld_wo=wo.stride(0), n_out=Cp, dz_scale=1.0 / S))
+            emit(kernel="attn_bwd", grid_cap=cap, dbias=with_db, us=us)
+    D.attn_set_bwd_grid(0)

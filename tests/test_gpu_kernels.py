@@ -621,22 +621,26 @@ def test_embed_patches_fused_matches_patchify_gemm():
     assert torch.isnan(hx[:, d + cfg.kp:].float()).all()  # padding columns untouched
 
 
-def test_fused_adamw_matches_torch():
+@pytest.mark.parametrize("n", [1000, 1003, 650001])
+def test_fused_adamw_matches_torch(n):
     from collective_communication_mpi_amd.parallel.dp import FlatParams
 
-    fp = FlatParams([("w", (1000,))], "cuda")
-    w0 = torch.randn(1000, device="cuda")
+    fp = FlatParams([("w", (n,))], "cuda")
+    w0 = torch.randn(n, device="cuda")
     fp.param("w").copy_(w0)
     ref = torch.nn.Parameter(w0.clone())
     opt = torch.optim.AdamW([ref], lr=1e-2, weight_decay=0.1, eps=1e-8)
     for _ in range(3):
-        g = torch.randn(1000, device="cuda")
+        g = torch.randn(n, device="cuda")
         fp.grad("w").copy_(g * 2)
         fp.adamw(1e-2, weight_decay=0.1, grad_scale=0.5)  # grad_scale folds a 1/dp average
         ref.grad = g
         opt.step()
+        assert torch.all(fp.grad("w") == 0)  # the kernel zeroes what it consumed
     torch.testing.assert_close(fp.param("w"), ref.detach(), rtol=1e-5, atol=1e-6)
-    torch.testing.assert_close(fp.param16("w").float(), ref.detach().bfloat16().float())
+    # the bf16 copy is the rounding of the kernel's own fp32 result (against torch's, values
+    # within 1e-7 of a bf16 rounding boundary may land one bf16 ulp apart at this n)
+    assert torch.equal(fp.param16("w"), fp.param("w").bfloat16())
 
 
 @pytest.mark.parametrize("ydtype", [torch.int32, torch.int64])
