@@ -58,6 +58,17 @@ struct AttnArgs {
   // them ([B*S][ld_xq] bf16) for the backward; xq is then unused
   const float* img;
   uint16_t* xq_out;
+  // fused QKV in image mode, optional: the NEXT forward's weight fold fold_out = bf16(fold_wq .
+  // fold_we) ([fold_R][fold_kp] from fp32 [fold_R][fold_d] and [fold_d][fold_kp]), computed by
+  // the workgroups once their attention work is done -- bitwise the fold_emb_qkv MFMA
+  // kernel's result (same per-slice MFMA chains, same summation order)
+  const float* fold_wq;
+  int ld_fold_wq;
+  const float* fold_we;
+  int ld_fold_we;
+  uint16_t* fold_out;
+  int ld_fold_out, fold_R, fold_d, fold_kp;
+  int fold_at_start;  // 1: the fold runs before the attention work (its loads under W_h's), 0: after
 };
 
 // MFMA path (attn_mfma.hip): S <= 16, D in {32, 64, 128}, 16-B aligned rows.

@@ -146,6 +146,68 @@ __device__ __forceinline__ void rows_out(const uint16_t* T, uint16_t* dst, int l
 // launch, its 2 x B*S x 3 Hl D x 2 B of qkv write + read, and the old per-head W staging
 // (one wave per sequence, two workgroup barriers per head: 38.9 us vs 23.1 + 17.0 us
 // unfused) are gone.
+// The weight fold W_eff = bf16(Wq . We) as the tail of the fused forward (AttnArgs fold_*):
+// one 16 x 16 output tile per workgroup and trip, the K axis cut into 16 slices exactly as
+// wgrad.hip's k_fold_mfma cuts it over its 16 waves -- here each of the 4 waves runs the MFMA
+// chains of 4 slices, two slices' operands in flight at a time -- and the 16
+// partial tiles summed in slice order in LDS: bitwise that kernel's output, without its launch.
+constexpr int kFoldSlices = 16, kFoldMaxJ = 4;
+
+__device__ __forceinline__ void fold_tail(const AttnArgs& a, float* part /* >= 16 * 16 * 17 floats of LDS */) {
+  typedef float f4v __attribute__((ext_vector_type(4)));
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
+  const int R = a.fold_R, d = a.fold_d, kp = a.fold_kp;
+  const int tiles_c = (kp + 15) / 16, ntiles = ((R + 15) / 16) * tiles_c;
+  const int nj = (d + 15) / 16, per = (nj + kFoldSlices - 1) / kFoldSlices;
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int r0 = (tile / tiles_c) * 16, c0 = (tile % tiles_c) * 16, col = c0 + c;
+    const bool rok = r0 + c < R, cok = col < kp;
+    const float* arow = a.fold_wq + (size_t)(rok ? r0 + c : 0) * a.ld_fold_wq;
+    // two slices' operands at a time (all four at once would take 128 VGPRs and spill)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      float4 a4[2][kFoldMaxJ];
+      float b[2][kFoldMaxJ][4];
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int j0 = (4 * wave + 2 * h + s) * per;
+#pragma unroll
+        for (int u = 0; u < kFoldMaxJ; ++u) {
+          const int k = 16 * (j0 + u) + 4 * g;
+          const bool kok = u < per && k < d;
+          a4[s][u] = (rok && kok) ? *reinterpret_cast<const float4*>(arow + k) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) b[s][u][i] = (cok && kok) ? a.fold_we[(size_t)(k + i) * a.ld_fold_we + col] : 0.f;
+        }
+      }
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        f4v acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int u = 0; u < kFoldMaxJ; ++u) {
+          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[s][u].x, b[s][u][0], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[s][u].y, b[s][u][1], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[s][u].z, b[s][u][2], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[s][u].w, b[s][u][3], acc, 0, 0, 0);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) part[((4 * wave + 2 * h + s) * 16 + 4 * g + r) * 17 + c] = acc[r];
+      }
+    }
+    __syncthreads();
+    {
+      const int r = threadIdx.x >> 4, cc = threadIdx.x & 15;  // 256 threads: one output each
+      if (r0 + r < R && c0 + cc < kp) {
+        float sum = 0.f;
+#pragma unroll
+        for (int w = 0; w < kFoldSlices; ++w) sum += part[(w * 16 + r) * 17 + cc];
+        a.fold_out[(size_t)(r0 + r) * a.ld_fold_out + c0 + cc] = static_cast<uint16_t>(f32_to_bf16_bits(sum));
+      }
+    }
+    __syncthreads();
+  }
+}
+
 template <int D, bool QKV, bool IMG = false>
 __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
   constexpr int LD = D + 8, NK = D / 32, NT = D / 16;
@@ -158,6 +220,7 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
   // and padded to whole 1-KiB LDS-DMA pieces
   constexpr int kImgPieces = (WPB * 784 * 4 + 1023) / 1024;
   __shared__ __attribute__((aligned(16))) float imgs[IMG ? 2 : 1][IMG ? kImgPieces * 256 : 1];
+  static_assert(!IMG || 2 * kImgPieces * 256 >= 16 * 16 * 17, "fold_tail reuses the image buffers");
   // ... and their patch rows X (bf16, 80 columns + pad), built ONCE per sequence by the whole
   // workgroup (not once per head), double-buffered
   constexpr int LDX = 88;
@@ -211,6 +274,11 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
     }
   }
   const int stride = gridDim.x * WPB;
+  if constexpr (QKV && IMG) {
+    // the next forward's weight fold before any image is staged (imgs is free), its operand
+    // loads in flight with W_h's fragment loads below
+    if (a.fold_out && a.fold_at_start) fold_tail(a, &imgs[0][0]);
+  }
   // the fc_o bias of this lane's epilogue classes (4 (lane & 3) .. +3), loaded once (the
   // compiler cannot hoist it past the loop's global stores)
   float bov[4];
@@ -590,6 +658,14 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
       a.zp[(size_t)div_hl(prw) * a.ld_zp + cls] = acc;
     }
    }
+  }
+  if constexpr (QKV && IMG) {
+    // the next forward's weight fold in the images' LDS (every DMA into it has landed: each
+    // trip ends with vmcnt(0) and a barrier, and the trip count is workgroup-uniform)
+    if (a.fold_out && !a.fold_at_start) {
+      __syncthreads();
+      fold_tail(a, &imgs[0][0]);
+    }
   }
 }
 

@@ -283,7 +283,8 @@ void attn_qkv_fwd(uint64_t xq, int ld_xq, int kq, uint64_t wq, int ld_wq, uint64
                   uint64_t lse, int B, int S, int Hl, int D, float scale, uint64_t pool, int ld_pool, uint64_t wo,
                   int ld_wo, int n_out, uint64_t bo, uint64_t ztok, int ld_zt, int zrows,
                   const std::vector<uint64_t>& zpush, uint64_t stream, uint64_t img, uint64_t xq_out, uint64_t zmean,
-                  int ld_zmean) {
+                  int ld_zmean, uint64_t fold_wq, int ld_fold_wq, uint64_t fold_we, int ld_fold_we, uint64_t fold_out,
+                  int ld_fold_out, int fold_R, int fold_d) {
   if (S < 1 || S > 16 || !(D == 32 || D == 64) || Hl < 1 || 4 % Hl || kq < 8 || kq > 72 || kq % 8 || ld_xq % 8 ||
       ld_wq % 8 || ld_wo % 8 || (xq % 16) || (wq % 16) || (wo % 16) || !wo || !bq || (bq % 16) || !lse || n_out < 1 ||
       n_out > 16 ||
@@ -296,6 +297,11 @@ void attn_qkv_fwd(uint64_t xq, int ld_xq, int kq, uint64_t wq, int ld_wq, uint64
   if (img && (S != 16 || kq < 66 || (img % 16) || (xq_out % 16)))
     throw std::invalid_argument("attention: fused patchify is the MNIST 28x28 / 7x7 case (S = 16, kq >= 66)");
   if (!img && (xq_out || !xq)) throw std::invalid_argument("attention: patch rows xq needed (xq_out only with img)");
+  if (fold_out && (!img || !fold_wq || !fold_we || fold_R < 1 || fold_d < 4 || fold_d % 4 || fold_d > 16 * 4 * 16 ||
+                   ld_fold_wq % 4 || ld_fold_wq < fold_d || ld_fold_we < kq || ld_fold_out < kq || (fold_wq % 16) ||
+                   fold_out == wq))
+    throw std::invalid_argument("attention: the fold tail needs image mode, fp32 Wq [R][d] (16-B aligned, d % 4 == 0, "
+                                "d <= 1024) and We [d][kq], and an output other than the W_eff being read");
   AttnArgs a{};
   a.lse = (float*)lse;
   a.B = B; a.S = S; a.Hl = Hl; a.D = D; a.ld_qkv = ld_qkv; a.scale = scale;
@@ -305,6 +311,11 @@ void attn_qkv_fwd(uint64_t xq, int ld_xq, int kq, uint64_t wq, int ld_wq, uint64
   a.wq = (const uint16_t*)wq; a.ld_wq = ld_wq; a.bq = (const float*)bq; a.qkv_out = (uint16_t*)qkv_out;
   a.img = (const float*)img; a.xq_out = (uint16_t*)xq_out;
   a.zp = (float*)zmean; a.ld_zp = ld_zmean;  // mean over the tokens of z (the local form's logits)
+  a.fold_wq = (const float*)fold_wq; a.ld_fold_wq = ld_fold_wq; a.fold_we = (const float*)fold_we;
+  a.ld_fold_we = ld_fold_we; a.fold_out = (uint16_t*)fold_out; a.ld_fold_out = ld_fold_out;
+  a.fold_R = fold_R; a.fold_d = fold_d; a.fold_kp = kq;
+  static const int at_start = std::getenv("CCMPI_FOLD_TAIL_AT") && std::string(std::getenv("CCMPI_FOLD_TAIL_AT")) == "end" ? 0 : 1;
+  a.fold_at_start = at_start;
   a.ztok = (float*)ztok; a.ld_zt = ld_zt; a.zrows = zrows;
   if (zrows) {
     const int64_t M = (int64_t)B * S;
@@ -628,6 +639,8 @@ void register_attn_ops(pybind11::module_& m) {
         py::arg("D"), py::arg("scale"), py::arg("pool"), py::arg("ld_pool"), py::arg("wo"), py::arg("ld_wo"),
         py::arg("n_out"), py::arg("bo"), py::arg("ztok"), py::arg("ld_zt"), py::arg("zrows"), py::arg("zpush"),
         py::arg("stream"), py::arg("img") = 0, py::arg("xq_out") = 0, py::arg("zmean") = 0, py::arg("ld_zmean") = 16,
+        py::arg("fold_wq") = 0, py::arg("ld_fold_wq") = 0, py::arg("fold_we") = 0, py::arg("ld_fold_we") = 0,
+        py::arg("fold_out") = 0, py::arg("ld_fold_out") = 0, py::arg("fold_R") = 0, py::arg("fold_d") = 0,
         py::call_guard<py::gil_scoped_release>());
   m.def("attn_small_bwd", &attn_bwd, py::arg("qkv"), py::arg("o"), py::arg("lse"), py::arg("dout"), py::arg("dqkv"),
         py::arg("dbias"), py::arg("B"), py::arg("S"), py::arg("Hl"), py::arg("D"), py::arg("ld_qkv"), py::arg("ld_o"),

@@ -277,6 +277,23 @@ def bench_forward(comm, tp: int = 2, batch: int = 2048, steps: int = 20, warmup:
         say(f"timed launch-plan forward {fwd_plan_s * 1e3:.3f} ms")
         if fwd_plan_s < fwd_s:
             fwd_s, fwd_timed = fwd_plan_s, "plan"
+    # the same with the weight fold pipelined into the fused kernel's tail (each call folds the
+    # next call's W_eff from the current weights; no fold launch)
+    fwd_pipe_s = None
+    pplan = layer.forward_plan_pipelined(xb, cfg.batch) if plan is not None else None
+    if pplan is not None:
+        for _ in range(warmup):
+            pplan()
+        _sync_barrier(comm)
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            pplan()
+        torch.cuda.synchronize()
+        hc.Barrier()
+        fwd_pipe_s = hc.allreduce(time.perf_counter() - t0, op=MPI.MAX) / steps
+        say(f"timed pipelined-fold launch-plan forward {fwd_pipe_s * 1e3:.3f} ms")
+        if fwd_pipe_s < fwd_s:
+            fwd_s, fwd_timed = fwd_pipe_s, "plan_pipelined_fold"
     # hip_graph: a graph was captured and replayed; fwd_timed: which launch mode fwd_ms is
     # (graph replay, eager forward_images, or the recorded launch plan)
     fwd_modes = {"fwd_timed": fwd_timed}
@@ -286,6 +303,8 @@ def bench_forward(comm, tp: int = 2, batch: int = 2048, steps: int = 20, warmup:
         fwd_modes["fwd_ms_eager"] = round(fwd_eager_s * 1e3, 4)
     if fwd_plan_s is not None:
         fwd_modes["fwd_ms_plan"] = round(fwd_plan_s * 1e3, 4)
+    if fwd_pipe_s is not None:
+        fwd_modes["fwd_ms_plan_pipelined_fold"] = round(fwd_pipe_s * 1e3, 4)
     form = getattr(layer, "_zt_form", None)  # the fused per-token fc_o's TP form, if it ran
     if not train:
         return {"tp": cfg.tp, "dp": cfg.dp, "fwd_ms": fwd_s * 1e3, "hip_graph": used_graph, **fwd_modes,

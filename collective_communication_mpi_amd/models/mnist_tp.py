@@ -190,6 +190,37 @@ class LaunchPlan:
         return [getattr(fn, "__name__", str(fn)) for fn, _, _ in self.calls]
 
 
+class PipelinedFoldPlan:
+    """Two launch plans of the image-mode fused forward used alternately (``MnistTPLayer.
+    forward_plan_pipelined``): plan k reads W_eff buffer k and its kernel tail folds buffer
+    k ^ 1 for the next call.  A call whose weights changed since the previous one (or the
+    first call) folds its own buffer first with the fold kernel."""
+
+    def __init__(self, layer, plans, w):
+        self.layer, self.plans, self.w = layer, plans, w
+        self.k = 0
+        self.stamp = None
+
+    def _stamp(self):
+        f = self.layer.flat
+        return (f.step_count, f.p32._version)
+
+    def invalidate(self) -> None:
+        self.stamp = None
+
+    def names(self):
+        return self.plans[0].names()
+
+    def __call__(self) -> torch.Tensor:
+        st = self._stamp()
+        if st != self.stamp:
+            self.layer._fold_into(self.w[self.k])
+            self.stamp = st
+        out = self.plans[self.k]()
+        self.k ^= 1
+        return out
+
+
 class _LaunchRecorder:
     """Proxies ``_native.device()`` and a device group's ``dc`` while a forward runs,
     keeping every native call with its arguments (the call still executes).  A plan holds
@@ -284,6 +315,7 @@ class MnistTPLayer:
         self._load(full_init(cfg))
         self._bufs = {}
         self._hx = None
+        self._fold_next = None  # (W_qkv, W_emb, W_eff') for the fused kernel's fold tail (pipelined plan)
         # [h | xp] rows padded to a multiple of 64 elements (128 B): every row of h
         # and of xp starts on a cache-line boundary (an 840-wide row costs the
         # embedding and QKV GEMMs ~8 us in straddled lines)
@@ -498,6 +530,50 @@ class MnistTPLayer:
             logits = self.forward_images(images, B, save=False)
         return LaunchPlan(rec.calls, logits) if not rec.allocated else None
 
+    def _fold_into(self, out: torch.Tensor) -> None:
+        """The standalone weight fold (``fold_emb_qkv``) into ``out``."""
+        cfg = self.cfg
+        wq, we = self.flat.param("qkv_w"), self.flat.param("emb_w")
+        _native.device().fold_emb_qkv(wq.data_ptr(), wq.stride(0), we.data_ptr(), we.stride(0), out.data_ptr(),
+                                      out.stride(0), 3 * self.hd, cfg.d_model, cfg.kp,
+                                      torch.cuda.current_stream(self.device).cuda_stream)
+
+    def forward_plan_pipelined(self, images: torch.Tensor, B: int) -> Optional["PipelinedFoldPlan"]:
+        """``forward_plan`` with the weight fold software-pipelined into the fused kernel: call
+        i reads W_eff from buffer i % 2 and, once its attention work is done, each workgroup
+        folds a tile of the NEXT call's W_eff = bf16(W_qkv W_emb) into the other buffer
+        (``attn_qkv_fwd(fold_*)``, bitwise the fold kernel's result).  Every call still does
+        one full fold and one full forward, from the current weights; the fold kernel's
+        launch and its ~5 us (a latency-bound 240-workgroup kernel) leave the step.  When the
+        weights changed since the last call (an optimizer step, a write into the parameters:
+        ``FlatParams.step_count`` / the buffer's version) the call folds its own W_eff
+        first; weights changed only by replayed recordings (``TrainPlan``) are not seen --
+        ``invalidate()`` then.  Image-mode fused forward only; None otherwise."""
+        cfg = self.cfg
+        if not (self._fuses_qkv(B) and cfg.fc_o_mode == "token" and self.tp_fc_o_form(B) in ("local", "push")
+                and images.dtype == torch.float32 and images.is_contiguous() and images.is_cuda
+                and cfg.img == 28 and cfg.patch == 7 and os.environ.get("CCMPI_FUSE_PATCHIFY", "1") != "0"):
+            return None
+        R = 3 * self.hd
+        w = [self._buf("weff_pipe0", (R, cfg.kp), torch.bfloat16), self._buf("weff_pipe1", (R, cfg.kp), torch.bfloat16)]
+        xp = self.input_buffer(B)
+        self.forward_images(images, B, save=False)  # persistent buffers exist before recording
+        wq, we = self.flat.param("qkv_w"), self.flat.param("emb_w")
+        plans = []
+        try:
+            for k in (0, 1):
+                self._fold_into(w[k])
+                self._fold_next = (wq, we, w[k ^ 1])
+                rec = _LaunchRecorder(self.tp_dev.dc if self.tp_dev is not None else None)
+                with rec.active(self):
+                    logits = self.forward(xp, B, images=images, weff=w[k], save=False)
+                if rec.allocated:
+                    return None
+                plans.append(LaunchPlan(rec.calls, logits))
+        finally:
+            self._fold_next = None
+        return PipelinedFoldPlan(self, plans, w)
+
     def forward_images(self, images: torch.Tensor, B: int, save: bool = True) -> torch.Tensor:
         """(B, 784) fp32 images -> logits: patchify into the fused [h | xp] rows, then
         ``forward``.  With ``cfg.fwd_chunks = c > 1`` the batch is cut into c row blocks
@@ -614,6 +690,13 @@ class MnistTPLayer:
             def fwd(*_a, zrows=0, zpush=(), ztok=0, ld_zt=16, wo=0, ld_wo=0, n_out=0, bo=0, zmean=0, ld_zmean=16):
                 stream = _a[-1]
                 # with img the kernel builds the patch rows itself (stored to xp for a backward)
+                fkw = {}
+                fold = self._fold_next
+                if fold is not None and img is not None:  # the next call's W_eff in the kernel's tail
+                    fwq, fwe, fout = fold
+                    fkw = dict(fold_wq=fwq.data_ptr(), ld_fold_wq=fwq.stride(0), fold_we=fwe.data_ptr(),
+                               ld_fold_we=fwe.stride(0), fold_out=fout.data_ptr(), ld_fold_out=fout.stride(0),
+                               fold_R=fwq.shape[0], fold_d=fwq.shape[1])
                 D.attn_qkv_fwd(0 if img is not None else xp.data_ptr(), xp.stride(0), cfg.kp, weff.data_ptr(),
                                weff.stride(0), bq.data_ptr(), qkv.data_ptr() if keep else 0, qkv.stride(0),
                                lse.data_ptr(), B, S, self.hl, cfg.head_dim, 1.0 / math.sqrt(cfg.head_dim),
@@ -621,7 +704,7 @@ class MnistTPLayer:
                                wo, ld_wo, n_out, bo, ztok, ld_zt, zrows, list(zpush),
                                stream, img=0 if img is None else img.data_ptr(),
                                xq_out=xp.data_ptr() if (img is not None and keep) else 0, zmean=zmean,
-                               ld_zmean=ld_zmean)
+                               ld_zmean=ld_zmean, **fkw)
         form = self.tp_fc_o_form(B)
         if form == "push":
             inbox = self._buf("ztok_inbox", (M, cfg.out_pad), torch.float32, self.tp_dev)

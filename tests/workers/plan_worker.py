@@ -1,6 +1,8 @@
 """MnistTPLayer.forward_plan: the forward's recorded native launches re-issued from a loop give
 bitwise the forward_images logits, and keep doing so after new pixels are written into the
-images tensor and a training step changes the weights (the plan reads live buffers)."""
+images tensor and a training step changes the weights (the plan reads live buffers).  The
+pipelined-fold plan (the next call's weight fold in the fused kernel's tail) likewise, over
+several calls and after a weight change."""
 import os
 import sys
 
@@ -33,5 +35,21 @@ ref2 = layer.forward_images(xb, cfg.batch, save=False).clone()
 out2 = plan().clone()
 torch.cuda.synchronize()
 assert torch.equal(out2, ref2) and not torch.equal(out2, out), ((out2 - ref2).abs().max().item())
+# the pipelined-fold plan: every call bitwise forward_images (W_eff folded by the previous
+# call's kernel tail), across calls and after the weights change
+pp = layer.forward_plan_pipelined(xb, cfg.batch)
+assert pp is not None, "forward_plan_pipelined unavailable"
+assert "fold_emb_qkv" not in pp.names(), pp.names()
+ref3 = layer.forward_images(xb, cfg.batch, save=False).clone()
+for i in range(5):
+    o = pp().clone()
+    torch.cuda.synchronize()
+    assert torch.equal(o, ref3), (i, (o - ref3).abs().max().item())
+train_step(layer, cfg, xb, yb)        # new weights: the next call folds its own W_eff first
+ref4 = layer.forward_images(xb, cfg.batch, save=False).clone()
+for i in range(3):
+    o = pp().clone()
+    torch.cuda.synchronize()
+    assert torch.equal(o, ref4) and not torch.equal(o, ref3), (i, (o - ref4).abs().max().item())
 if comm.Get_rank() == 0:
     print("plan OK", names, flush=True)
