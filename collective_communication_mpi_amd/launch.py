@@ -15,7 +15,8 @@ Open MPI style flags that make no sense for a single-host shm runtime
 ``-x VAR[=VAL]`` exports a variable.  Binding (``--bind-to`` / ``CCMPI_BIND``):
 
 * ``l3`` (default): every rank may run on any hardware thread of the fewest L3 domains
-  (CCDs) that hold one physical core per rank, the launcher's own domain first.  The host
+  (CCDs) that hold one physical core per rank, the least busy domain first (a 20 ms
+  ``/proc/stat`` sample; ties: the launcher's own domain).  The host
   plane's messages are shared-memory cache lines moving between the ranks' cores: on the
   MI355X box's 2 x 64-core EPYC the OS spread 8 ranks over 8 CCDs, and every line crossed
   the IO die (8-rank library Allreduce of 4 KiB 8.1 us unbound, 3.3-3.9 us in one CCD; the
@@ -108,9 +109,37 @@ def _read_cpu_list(path: str) -> List[int]:
     return out
 
 
+def _cpu_busy(window_s: float = 0.02) -> dict:
+    """Per-CPU busy fraction over a short window (/proc/stat), {} if unreadable."""
+    def snap():
+        out = {}
+        with open("/proc/stat") as f:
+            for line in f:
+                if line.startswith("cpu") and line[3:4].isdigit():
+                    parts = line.split()
+                    vals = [int(v) for v in parts[1:]]
+                    idle = vals[3] + (vals[4] if len(vals) > 4 else 0)
+                    out[int(parts[0][3:])] = (sum(vals), idle)
+        return out
+    try:
+        a = snap()
+        time.sleep(window_s)
+        b = snap()
+    except (OSError, ValueError):
+        return {}
+    busy = {}
+    for c, (tot, idle) in b.items():
+        if c in a:
+            dt, di = tot - a[c][0], idle - a[c][1]
+            busy[c] = (dt - di) / dt if dt > 0 else 0.0
+    return busy
+
+
 def _l3_domains():
     """(domains in placement order, allowed CPUs by domain): L3 key -> one allowed hardware
-    thread per physical core, the launcher's own domain first."""
+    thread per physical core; the least busy domain first (a short /proc/stat sample: on a
+    shared host another job's ranks may be spinning in the launcher's own domain), ties broken
+    by the launcher's own domain, then CPU order."""
     allowed = set(os.sched_getaffinity(0))
     sysfs = "/sys/devices/system/cpu"
     cores, threads = {}, {}
@@ -126,7 +155,9 @@ def _l3_domains():
         seen_core.add(sib)
         cores.setdefault(key, []).append(c)
     first = dom_of.get(_current_cpu())
-    order = sorted(cores, key=lambda k: (k != first, min(k)))
+    busy = _cpu_busy()
+    load = {k: round(sum(busy.get(c, 0.0) for c in threads[k]), 1) for k in cores}
+    order = sorted(cores, key=lambda k: (load[k], k != first, min(k)))
     return order, cores, threads
 
 
