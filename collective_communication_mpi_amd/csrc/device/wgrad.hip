@@ -51,6 +51,7 @@ struct WgradArgs {
   int R, d, kp;
   int gq_blocks;   // workgroups [0, gq_blocks) do Gq tiles, the rest Ge partials
   int splits;      // Ge: R-splits per d tile
+  int ge_mfma;     // Ge tiles on the matrix cores (ge_tile_mfma) instead of atomic R-splits
 };
 
 // Gq[r0.., c0..] += sum_k A[r][k] We[c][k] for a 64 x 64 tile.  Operand tiles are
@@ -206,6 +207,55 @@ __device__ void ge_tile(const WgradArgs& a, int blk, float* smem) {
   }
 }
 
+// Ge on the fp32 matrix cores (R <= 768): one 16 x 16 tile of Ge = Wq^T A per workgroup over
+// ALL R rows, so no atomics -- the tile is read, added to and written once.  The 4 waves take
+// R / 4 rows each: MFMA m of wave w covers rows 4 (w G + m) .. +3 (G = groups per wave), lane
+// (c, g) supplying Wq[row g][i0 + c] and A[row g][j0 + c] (both 64-B coalesced), every load
+// issued before the first MFMA; the 4 partial tiles are summed in wave order in LDS.  (The
+// 8 R-splits x 64-column atomic tiles of ge_tile cost 5 us of the kernel's 12.)
+constexpr int kGeMaxG = 48;  // 4-row groups per wave: R <= 4 * 4 * 48
+// Ge variant (wgrad_set_ge_mfma / CCMPI_WGRAD_GE=atomic for the R-split atomic tiles)
+bool g_ge_mfma = std::getenv("CCMPI_WGRAD_GE") == nullptr || std::string(std::getenv("CCMPI_WGRAD_GE")) != "atomic";
+
+__device__ void ge_tile_mfma(const WgradArgs& a, int blk, float* smem) {
+  typedef float f4v __attribute__((ext_vector_type(4)));
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
+  const int tiles_j = (a.kp + 15) / 16;
+  const int i0 = (blk / tiles_j) * 16, j0 = (blk % tiles_j) * 16;
+  const int ngroups = (a.R + 3) / 4, G = (ngroups + 3) / 4;
+  const bool iok = i0 + c < a.d, jok = j0 + c < a.kp;
+  // the tile's old values, fetched with the operands (lane: row 4g + r, column c)
+  float old[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int i = i0 + 4 * g + r;
+    old[r] = (wave == 0 && i < a.d && jok) ? a.Ge[(size_t)i * a.ld_ge + j0 + c] : 0.f;
+  }
+  float wv[kGeMaxG], av[kGeMaxG];
+#pragma unroll
+  for (int m = 0; m < kGeMaxG; ++m) {
+    const int row = 4 * (wave * G + m) + g;
+    const bool ok = m < G && row < a.R;
+    wv[m] = (ok && iok) ? a.Wq[(size_t)row * a.ld_wq + i0 + c] : 0.f;
+    av[m] = (ok && jok) ? a.A[(size_t)row * a.ld_a + j0 + c] : 0.f;
+  }
+  f4v acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int m = 0; m < kGeMaxG; ++m) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wv[m], av[m], acc, 0, 0, 0);
+  float* part = smem;  // [4][16][17]
+#pragma unroll
+  for (int r = 0; r < 4; ++r) part[(wave * 16 + 4 * g + r) * 17 + c] = acc[r];
+  __syncthreads();
+  if (wave == 0) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int i = 4 * g + r;
+      const float v = part[i * 17 + c] + part[(16 + i) * 17 + c] + part[(32 + i) * 17 + c] + part[(48 + i) * 17 + c];
+      if (i0 + i < a.d && jok) a.Ge[(size_t)(i0 + i) * a.ld_ge + j0 + c] = old[r] + v;
+    }
+  }
+}
+
 constexpr size_t kSmemFloats = 2 * kMaxKp * kLdT > kGeRows * (kT + 4 + kMaxKp + 4)
                                    ? 2 * kMaxKp * kLdT : kGeRows * (kT + 4 + kMaxKp + 4);
 
@@ -213,6 +263,7 @@ __global__ void __launch_bounds__(kNT) k_emb_qkv_wgrad(WgradArgs a) {
   __shared__ __attribute__((aligned(16))) float smem[kSmemFloats];
   const int blk = blockIdx.x;
   if (blk < a.gq_blocks) gq_tile(a, blk, smem);
+  else if (a.Ge && a.ge_mfma) ge_tile_mfma(a, blk - a.gq_blocks, smem);
   else if (a.Ge) ge_tile(a, blk - a.gq_blocks, smem);
   if (a.Z) {  // zero the next A buffer, spread over every workgroup
     const size_t n = (size_t)a.R * a.kp;
@@ -233,7 +284,8 @@ void emb_qkv_wgrad(uint64_t A, int ld_a, uint64_t We, int ld_we, uint64_t Wq, in
               reinterpret_cast<const float*>(Wq), ld_wq, reinterpret_cast<float*>(Gq), ld_gq,
               reinterpret_cast<float*>(Ge), ld_ge, reinterpret_cast<float*>(Z), ld_z, R, d, kp, 0, splits};
   a.gq_blocks = ((R + kT - 1) / kT) * dtiles;
-  const int ge_blocks = Ge ? dtiles * splits : 0;
+  a.ge_mfma = (g_ge_mfma && R <= 4 * 4 * kGeMaxG) ? 1 : 0;
+  const int ge_blocks = !Ge ? 0 : a.ge_mfma ? ((d + 15) / 16) * ((kp + 15) / 16) : dtiles * splits;
   hipLaunchKernelGGL(k_emb_qkv_wgrad, dim3(a.gq_blocks + ge_blocks), dim3(kNT), 0, (hipStream_t)stream, a);
   CCMPI_HIP_CHECK(hipGetLastError());
 }
@@ -439,6 +491,9 @@ void register_wgrad_ops(pybind11::module_& m) {
         pybind11::arg("Wq"), pybind11::arg("ld_wq"), pybind11::arg("We"), pybind11::arg("ld_we"), pybind11::arg("Weff"),
         pybind11::arg("ld_eff"), pybind11::arg("R"), pybind11::arg("d"), pybind11::arg("kp"), pybind11::arg("stream"),
         pybind11::arg("bias") = 0, pybind11::arg("bias_col") = -1, pybind11::call_guard<pybind11::gil_scoped_release>());
+  m.def("wgrad_set_ge_mfma", [](bool on) { g_ge_mfma = on; },
+        "emb_qkv_wgrad's dW_emb part: matrix-core tiles over all R rows (True) or R-split atomic tiles",
+        pybind11::arg("on"));
   m.def("fold_set_variant", [](int v) { g_fold_variant = v; },
         "fold_emb_qkv kernel: 0 = fp32 FMA, 1 = fp32 MFMA, -1 = CCMPI_FOLD (default mfma)", pybind11::arg("v"));
   m.def("emb_qkv_wgrad", &emb_qkv_wgrad,

@@ -7,7 +7,7 @@ OUT=gpurun_out/${OUT_TAG:-r5_48}
 mkdir -p $OUT
 export TMPDIR=/tmp
 timeout -k 10 300 python3 -u -m pytest -x -v --timeout 120 --timeout-method thread -m gpu \
-  tests/test_gpu_kernels.py -k "xent or adam" > $OUT/tests_k.log 2>&1
+  tests/test_gpu_kernels.py -k "xent or adam or wgrad or fold" > $OUT/tests_k.log 2>&1
 rc=$?; tail -2 $OUT/tests_k.log; [ $rc -ne 0 ] && { grep -E "FAILED|^E |Error" $OUT/tests_k.log | head -30; exit $rc; }
 timeout -k 10 600 python3 -u -m pytest -x -v --timeout 200 --timeout-method thread -m gpu \
   tests/test_gpu_distributed.py tests/test_gpu_harness_grad.py -k "harness or graph or plan or grad" > $OUT/tests_h.log 2>&1

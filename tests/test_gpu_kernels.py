@@ -751,6 +751,38 @@ def test_gemm_tn_pingpong(M, N1, N2, splitk):
         set_tn_variant(None)
 
 
+@pytest.mark.parametrize("ge_mfma", [True, False], ids=["ge-mfma", "ge-atomic"])
+@pytest.mark.parametrize("R,d,kp", [(768, 768, 72), (384, 768, 72), (20, 36, 16), (50, 1000, 8), (1000, 64, 16)])
+def test_emb_qkv_wgrad_matches_fp32(R, d, kp, ge_mfma):
+    """The harness's weight-gradient kernel: Gq += A We^T, Ge += Wq^T A (matrix-core tiles over
+    all R rows, or R-split atomic tiles; R = 1000 exceeds the matrix-core path and takes the
+    atomic one), Z zeroed -- against fp32 torch."""
+    from collective_communication_mpi_amd import _native
+
+    g = torch.Generator(device="cuda").manual_seed(R + d + kp)
+    A = torch.randn(R, kp, device="cuda", generator=g)
+    We = torch.randn(d, kp, device="cuda", generator=g)
+    Wq = torch.randn(R, d, device="cuda", generator=g)
+    Gq = torch.randn(R, d, device="cuda", generator=g)
+    Ge = torch.randn(d, kp + 4, device="cuda", generator=g)  # padded rows
+    Z = torch.ones(R, kp, device="cuda")
+    gq_ref = Gq + A @ We.T
+    ge_ref = Ge[:, :kp] + Wq.T @ A
+    D = _native.device()
+    D.wgrad_set_ge_mfma(ge_mfma)
+    try:
+        D.emb_qkv_wgrad(A.data_ptr(), A.stride(0), We.data_ptr(), We.stride(0), Wq.data_ptr(), Wq.stride(0),
+                        Gq.data_ptr(), Gq.stride(0), Ge.data_ptr(), Ge.stride(0), Z.data_ptr(), Z.stride(0), R, d, kp,
+                        torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+    finally:
+        D.wgrad_set_ge_mfma(True)
+    tol = dict(rtol=1e-4, atol=1e-3 * max(R, d) ** 0.5)
+    torch.testing.assert_close(Gq, gq_ref, **tol)
+    torch.testing.assert_close(Ge[:, :kp], ge_ref, **tol)
+    assert torch.all(Z == 0)
+
+
 @pytest.mark.parametrize("variant", [0, 1], ids=["fma", "mfma"])
 @pytest.mark.parametrize("R,d,kp", [(768, 768, 72), (384, 768, 72), (20, 36, 16), (7, 100, 96), (50, 1000, 8)])
 def test_fold_emb_qkv_matches_fp32(R, d, kp, variant):
