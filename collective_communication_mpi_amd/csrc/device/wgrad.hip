@@ -262,6 +262,8 @@ constexpr size_t kSmemFloats = 2 * kMaxKp * kLdT > kGeRows * (kT + 4 + kMaxKp + 
 __global__ void __launch_bounds__(kNT) k_emb_qkv_wgrad(WgradArgs a) {
   __shared__ __attribute__((aligned(16))) float smem[kSmemFloats];
   const int blk = blockIdx.x;
+  // (dW_qkv on the matrix cores as 2 x 2 MFMA tiles per wave measured 6.8 us alone but 9.4 us
+  // beside the dW_emb tiles, against 7.2 / 8.2 for these FMA tiles: not kept)
   if (blk < a.gq_blocks) gq_tile(a, blk, smem);
   else if (a.Ge && a.ge_mfma) ge_tile_mfma(a, blk - a.gq_blocks, smem);
   else if (a.Ge) ge_tile(a, blk - a.gq_blocks, smem);
