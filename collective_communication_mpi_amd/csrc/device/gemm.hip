@@ -511,19 +511,26 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(PF >= 4
     }
   };
   const int grp = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  // fragment read addresses: tn_off(ks * 32 + grp * 8 + q + 4 h, (w + 16 i + 4 p) * 2) is a
+  // per-lane base plus the constant ks * 32 * kTnRow + h * 4 * kTnRow + 32 i: the half-swap
+  // XOR only flips the 128-B bit that w * 2 (w in {0, 64}) owns (row bit 3 = grp & 1; q + 4h
+  // < 8 never carries into it), so every read is base + an immediate offset
+  const int lrow = (grp * 8 + q) * kTnRow, xsw = (grp & 1) << 7;
+  const int la = lrow + ((wm * 2) ^ xsw) + 8 * p, lb = lrow + ((wn * 2) ^ xsw) + 8 * p;
   auto compute = [&](int cur) {
+    const unsigned char* abase = As(cur) + la;
+    const unsigned char* bbase = Bs(cur) + lb;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       bf16x8 af[4], bf[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         v4s a0, a1, b0, b1;
-        const int r0 = ks * 32 + grp * 8 + q;
-        const int ca = (wm + i * 16 + 4 * p) * 2, cb = (wn + i * 16 + 4 * p) * 2;
-        a0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(As(cur) + tn_off(r0, ca)));
-        a1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(As(cur) + tn_off(r0 + 4, ca)));
-        b0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(Bs(cur) + tn_off(r0, cb)));
-        b1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(Bs(cur) + tn_off(r0 + 4, cb)));
+        const int o = ks * 32 * kTnRow + 32 * i;
+        a0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(abase + o));
+        a1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(abase + o + 4 * kTnRow));
+        b0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(bbase + o));
+        b1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(bbase + o + 4 * kTnRow));
         typedef short v8s __attribute__((ext_vector_type(8)));
         v8s av = __builtin_shufflevector(a0, a1, 0, 1, 2, 3, 4, 5, 6, 7);
         v8s bv = __builtin_shufflevector(b0, b1, 0, 1, 2, 3, 4, 5, 6, 7);
