@@ -198,7 +198,10 @@ def test_bench_failing_candidates_keep_headline():
 
     from _launch import REPO
 
+    # each injected failure waits out the device timeout on the rank left in the kernel: 6 s
+    # here (the collectives themselves take milliseconds at 16 MiB) instead of the suite's 20
     e = dict(os.environ, **ENV, CCMPI_BENCH_FAULT="candidate:twoshot:256,candidate_bf16:*")
+    e["CCMPI_DEVICE_TIMEOUT_S"] = "6"
     r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--steps", "2", "--warmup", "1", "--size-mb", "16",
                         "--a2a-mb", "8", "--dp-layers", "0", "--tune-max-mb", "1", "--no-rccl", "--no-harness",
                         "--mlp-tokens", "0", "--host-ranks", "0"],
