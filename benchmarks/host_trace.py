@@ -13,6 +13,9 @@ from collective_communication_mpi_amd import MPI, Communicator, _native  # noqa:
 
 if os.environ.get("HT_PIN"):  # pin rank r to CPU HT_PIN + r (one L3 domain for 8 ranks)
     os.sched_setaffinity(0, {int(os.environ["HT_PIN"]) + int(os.environ.get("RANK", os.environ.get("CCMPI_RANK", "0")))})
+if os.environ.get("HT_GC") == "0":  # diagnostic: no cyclic-GC passes during the loop
+    import gc
+    gc.disable()
 world = MPI.COMM_WORLD
 comm = Communicator(world)
 rank, p = comm.Get_rank(), comm.Get_size()
