@@ -95,6 +95,9 @@ def parse(argv=None):
                     help="tokens of the TP Llama-3-8B MLP record (tp_mlp: TP over all ranks; 0 = off)")
     ap.add_argument("--tune-max-mb", type=int, default=256, help="N >= 2: largest size of the tuning sweep (0 = off)")
     ap.add_argument("--shared-dry-run", type=int, default=8, help="N=1: ranks of the shared-GPU dry run (0 = off)")
+    ap.add_argument("--variants", default="fast", choices=["fast", "all"],
+                    help="secondary variants: 'fast' skips the ones that cannot win (token_chunks4 fc_o, "
+                         "fused MLP row mode: 11x / 3.4x slower than plain, BENCH_r05 / profiles/r5_rehearse8)")
     ap.add_argument("--no-harness", action="store_true")
     ap.add_argument("--no-secondary", action="store_true")
     ap.add_argument("--verbose", action="store_true")
@@ -122,7 +125,8 @@ def relaunch(n: int) -> int:
     from collective_communication_mpi_amd.launch import launch
 
     argv = [sys.executable, os.path.abspath(__file__)] + sys.argv[1:]
-    return launch(n, argv, env_extra={"CCMPI_BENCH_CHILD": "1"})
+    # rank r on the CPUs local to the GPU it drives, an L3 domain of its own (topology.py)
+    return launch(n, argv, env_extra={"CCMPI_BENCH_CHILD": "1", "CCMPI_BIND": os.environ.get("CCMPI_BIND", "gpu")})
 
 
 def _env_rank():
@@ -139,15 +143,18 @@ def _env_rank():
     return r, n, local
 
 
-def _run_child(cmd, env, budget: float, abort_flag: str = ""):
+def _run_child(cmd, env, budget: float, abort_flag: str = "", cpus=None):
     """Run one phase child in its own session; kill its process group at the budget, or as
     soon as ``abort_flag`` exists (another rank's child of this phase failed: its peers
     would wait for it in their next collective until the budget).  A child that fails
-    creates the flag for the others.  Returns (returncode or None if killed, seconds)."""
+    creates the flag for the others.  ``cpus``: the child's CPU binding (set before it
+    starts, so its GPU runtime's threads inherit it).  Returns (returncode or None if
+    killed, seconds)."""
     import signal
 
     t0 = time.monotonic()
-    p = subprocess.Popen(cmd, env=env, cwd=REPO, start_new_session=True)
+    pre = (lambda c=frozenset(cpus): os.sched_setaffinity(0, c)) if cpus else None
+    p = subprocess.Popen(cmd, env=env, cwd=REPO, start_new_session=True, preexec_fn=pre)
     rc = None
     while True:
         try:
@@ -174,6 +181,32 @@ def _run_child(cmd, env, budget: float, abort_flag: str = ""):
         except OSError:
             pass
     return rc, time.monotonic() - t0
+
+
+def phase_binding(world, rank: int, local: int):
+    """(CPU set for this rank's GPU phase children or None, binding mode).  Launched by
+    ``launch.py`` (``CCMPI_BOUND_CPUS`` set): the children inherit that binding.  Launched by
+    torchrun (nobody bound us): rank 0 reads the GPU-local plan from sysfs once
+    (``topology.gpu_plan``, before any GPU call) and every rank takes its local rank's set,
+    so both launch paths place ranks the same way.  ``CCMPI_BIND=none`` (or anything other
+    than ``gpu``) leaves placement to the OS."""
+    mode = os.environ.get("CCMPI_BIND", "gpu")
+    if os.environ.get("CCMPI_BOUND_CPUS"):
+        return None, os.environ.get("CCMPI_BIND_EFFECTIVE", mode)
+    plan = None
+    if mode == "gpu" and rank == 0:
+        from collective_communication_mpi_amd.launch import _cpu_busy
+        from collective_communication_mpi_amd.topology import gpu_plan
+
+        nloc = int(os.environ.get("LOCAL_WORLD_SIZE", os.environ.get("CCMPI_LOCAL_SIZE", world.Get_size())))
+        try:
+            plan = gpu_plan(nloc, busy=_cpu_busy())
+        except (OSError, ValueError):
+            plan = None
+    plan = world.bcast(plan, root=0) if mode == "gpu" else None
+    if not plan or local >= len(plan):
+        return None, "none"
+    return plan[local], "gpu"
 
 
 def plan_phases(args, size: int):
@@ -280,6 +313,10 @@ def supervise(args) -> int:
     # the collective phase's tuning sweep -> every later phase's device groups (auto)
     tune_file = os.environ.get("CCMPI_TUNE_FILE") or os.path.join(tmp, "tune.json")
     argv = list(sys.argv[1:])
+    from collective_communication_mpi_amd.topology import format_cpu_list
+
+    cpus, bind_mode = phase_binding(world, rank, local)
+    bound = world.allgather(format_cpu_list(cpus if cpus else os.sched_getaffinity(0)))
     status = {}
     for phase, budget in plan_phases(args, size):
         env = dict(os.environ, CCMPI_RANK=str(rank), CCMPI_SIZE=str(size), CCMPI_LOCAL_RANK=str(local),
@@ -303,16 +340,25 @@ def supervise(args) -> int:
             if rank == 0:
                 for k in ("CCMPI_RANK", "CCMPI_SIZE", "CCMPI_LOCAL_RANK", "CCMPI_LOCAL_SIZE", "CCMPI_JOBID"):
                     env.pop(k, None)
+                # CPU ranks exchange shared-memory cache lines: one CCD (launch.py ``l3``)
+                env["CCMPI_BIND"] = os.environ.get("CCMPI_HOST_BIND", "l3")
+                for k in ("CCMPI_BOUND_CPUS", "CCMPI_BIND_EFFECTIVE"):
+                    env.pop(k, None)
                 cmd = [sys.executable, "-m", "collective_communication_mpi_amd.launch", "-n", str(args.host_ranks),
                        "--timeout", str(int(budget)), *cmd]
                 rc, secs = _run_child(cmd, env, budget + 15)
         else:
-            rc, secs = _run_child(cmd, env, budget, abort_flag=os.path.join(tmp, f"{phase}.abort"))
+            if cpus:
+                env["CCMPI_BOUND_CPUS"] = format_cpu_list(cpus)
+                env["CCMPI_BIND_EFFECTIVE"] = bind_mode
+            rc, secs = _run_child(cmd, env, budget, abort_flag=os.path.join(tmp, f"{phase}.abort"), cpus=cpus)
         if rank == 0:
             print(f"[bench] phase {phase}: rc {rc}, {secs:.1f}s", file=sys.stderr, flush=True)
         ok = world.allreduce(int(rc == 0), op=MPI.MIN)
         rcs = world.allgather(rc)
         status[phase] = {"ok": bool(ok), "returncodes": rcs, "seconds": round(secs, 1)}
+        if phase != "host":
+            status[phase].update(binding=bind_mode, bound_cpus=bound)
         world.Barrier()  # no child of this phase is alive anywhere before the next starts
     rc = 0
     if rank == 0:
@@ -347,6 +393,9 @@ def shared_dry_run(n: int, steps: int, warmup: int, verbose: bool):
            "--dp-layers", "0", "--a2a-mb", "64", "--shared-dry-run", "0", "--no-rccl", "--mlp-tokens", "0",
            "--tune-max-mb", "16", "--host-ranks", "0"]
     env = dict(os.environ, CCMPI_BENCH_CHILD="1")
+    # the placement an N-GPU run uses (every rank on its GPU's CPUs, a CCD each);
+    # CCMPI_DRYRUN_BIND=l3|none for the A/B (profiles/r6_bind)
+    env["CCMPI_BIND"] = os.environ.get("CCMPI_DRYRUN_BIND", "gpu")
     q = os.environ.get("CCMPI_DRYRUN_HW_QUEUES", "1")
     if q:
         env["GPU_MAX_HW_QUEUES"] = q
@@ -365,6 +414,8 @@ def shared_dry_run(n: int, steps: int, warmup: int, verbose: bool):
     keep["unit"] = "GB/s (1 GiB fp32 all-reduce algbw)"
     keep["note"] = f"{n} ranks sharing ONE GPU through IPC: HBM + protocol, not xGMI"
     keep["hw_queues_per_rank"] = env.get("GPU_MAX_HW_QUEUES", "HIP default")
+    keep["binding"] = env["CCMPI_BIND"]
+    keep["placement"] = out["config"].get("placement")
     keep.update({k: out["config"].get(k) for k in ("allreduce_algo", "busbw_GBps", "candidates_ms", "candidates",
                                                      "result_exact", "self_test", "bf16_1GiB", "alltoall",
                                                      "alltoall_pairwise", "sweep", "tuning", "tp_fwd_step_ms",
@@ -387,7 +438,27 @@ def _setup_phase(timeout_s: str):
     comm = Communicator(MPI.COMM_WORLD)
     local = _env_rank()[2]
     torch.cuda.set_device(local % torch.cuda.device_count())
+    _PLACEMENT[:] = comm.comm.allgather(_check_placement(torch))
     return comm
+
+
+_PLACEMENT: list = []  # per rank, set by _setup_phase: where the phase child runs
+
+
+def _check_placement(torch) -> str:
+    """This rank's CPU binding against the GPU the runtime opened (topology.check_bound:
+    a binding with no CPU on the GPU's side is moved there, every thread, and reported)."""
+    from collective_communication_mpi_amd.topology import check_bound
+
+    try:
+        props = torch.cuda.get_device_properties(torch.cuda.current_device())
+        r = check_bound(props)
+        gpu = f"{getattr(props, 'pci_domain_id', 0):04x}:{props.pci_bus_id:02x}:{props.pci_device_id:02x}"
+        where = {True: "gpu-local", False: "NOT gpu-local", None: "gpu cpus unknown"}[r.get("gpu_local")]
+        return (f"cpus={r['bound_cpus']} gpu={gpu} {where}"
+                + (f" (re-bound {r['rebound_threads']} threads)" if "rebound_threads" in r else ""))
+    except Exception as e:  # noqa: BLE001 - a record field, never a failure
+        return f"unknown ({type(e).__name__}: {e})"[:200]
 
 
 def _fault_injection(phase: str) -> None:
@@ -808,6 +879,7 @@ def coll_record(args, comm, r: dict, tuning: dict) -> dict:
             "self_test": r["self_test"],
             "shared_gpu": dev.shared_device,
             "tuning": tuning,
+            "placement": list(_PLACEMENT),
         },
     }
 
@@ -847,7 +919,8 @@ def harness_phase(args) -> dict:
         other = {}
         variants = [("pooled", "row", 1, "")] if args.fc_o_mode == "token" else [("token", "token", 1, "")]
         if tp > 1:
-            variants.append(("token_chunks4", "token", 4, ""))
+            if args.variants == "all":
+                variants.append(("token_chunks4", "token", 4, ""))
             if mode == "token" and harness.get("fc_o_tp_form") in ("plain", "push"):
                 alt = "push" if harness["fc_o_tp_form"] == "plain" else "plain"
                 variants.append((f"token_{alt}", "token", 1, alt))
@@ -866,6 +939,10 @@ def harness_phase(args) -> dict:
                                   train=False, fc_o_mode=vmode, tp_chunks=chunks, tp_fc_o_form=form)
                 other[f"{name}_fwd_ms"] = round(r["fwd_ms"], 4)
                 other[f"{name}_hip_graph"] = r["hip_graph"]
+                # how the variant was launched: eager / graph / plan / plan_pipelined_fold, the
+                # fastest reported, every mode's time on record
+                other[f"{name}_fwd_timed"] = r.get("fwd_timed")
+                other[f"{name}_fwd_modes_ms"] = {k[len("fwd_ms_"):]: v for k, v in r.items() if k.startswith("fwd_ms_")}
             except Exception as e:  # noqa: BLE001 - a secondary number must not cost the record
                 other[f"{name}_error"] = f"{type(e).__name__}: {e}"[:200]
         harness["fc_o_variants"] = other
@@ -886,6 +963,8 @@ def harness_phase(args) -> dict:
                 harness["fwd_ms"] = t_alt
                 harness["fc_o_tp_form"] = alt
                 harness["train_fc_o_tp_form"] = form
+                harness[f"fwd_timed_{form}"] = harness.get("fwd_timed")
+                harness["fwd_timed"] = other.get(f"token_{alt}_fwd_timed")
     harness["fwd_ms"] = round(harness["fwd_ms"], 4)
     harness["train_ms"] = round(harness.get("train_ms", float("nan")), 4)
     if "train_ms_eager" in harness:
@@ -930,7 +1009,10 @@ def mlp_phase(args) -> dict:
     comm = _setup_phase("20")
     from collective_communication_mpi_amd.parallel.mlp_bench import measure_tp_mlp
 
-    return measure_tp_mlp(comm, tokens=args.mlp_tokens, iters=10, warmup=3, variants=True)
+    from collective_communication_mpi_amd.parallel.tensor_parallel import ROW_MODES
+
+    modes = ROW_MODES if args.variants == "all" else tuple(m for m in ROW_MODES if m != "fused")
+    return measure_tp_mlp(comm, tokens=args.mlp_tokens, iters=10, warmup=3, variants=True, modes=modes)
 
 
 def rccl_phase(args) -> dict:
@@ -1009,7 +1091,7 @@ def host_phase(args) -> dict:
     out = {"ranks": p, "count": n, "dtype": "float32", "runs": runs, "op": "MIN",
            "timing": "per run: Barrier, Wtime, call, Barrier, Wtime (reference mpi-test.py:59-72); avg over runs",
            # the launcher's CPU binding (default: one shared set of the fewest L3 domains)
-           "binding": os.environ.get("CCMPI_BIND", "l3"), "bound_cpus": os.environ.get("CCMPI_BOUND_CPUS")}
+           "binding": os.environ.get("CCMPI_BIND_EFFECTIVE", os.environ.get("CCMPI_BIND", "l3")), "bound_cpus": os.environ.get("CCMPI_BOUND_CPUS")}
 
     def bench_pair(name_lib, lib, name_my, my, make):
         t_lib, t_my, ok = [], [], True
@@ -1094,6 +1176,8 @@ def main() -> int:
             out = fn(args)
         except Exception as e:  # noqa: BLE001 - recorded in the merged line
             out = {"error": f"{type(e).__name__}: {e}"[:400]}
+    if _PLACEMENT and isinstance(out, dict) and args.phase != "coll":
+        out["placement"] = list(_PLACEMENT)
     _write_result(args, rank, out)
     return 0
 

@@ -5,7 +5,7 @@ import json
 import os
 import sys
 
-os.environ["CCMPI_P2P_TRACE"] = "1"
+os.environ.setdefault("CCMPI_P2P_TRACE", "1")  # 2: also the marks inside isend_raw
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
 import numpy as np  # noqa: E402
 
@@ -22,7 +22,8 @@ rank, p = comm.Get_rank(), comm.Get_size()
 rng = np.random.default_rng(rank)
 n, runs = 1024, 200
 H = _native.host()
-base = rng.standard_normal(n).astype(np.float32)
+src0 = rng.standard_normal(n).astype(np.float32)
+keep = []  # fresh_nofree: every run's arrays stay alive (new addresses and pages every run)
 for fresh in os.environ.get("HT_MODES", "fresh,reuse").split(","):
     s = rng.standard_normal(n).astype(np.float32)
     d = np.empty(n, np.float32)
@@ -35,8 +36,16 @@ for fresh in os.environ.get("HT_MODES", "fresh,reuse").split(","):
         elif fresh == "rngwork":  # the same random-number work, arrays reused
             rng.standard_normal(n).astype(np.float32)
         elif fresh == "copyfresh":  # new arrays without the random-number work
-            s = base.copy()
+            s = src0.copy()
             d = np.empty(n, np.float32)
+        elif fresh == "fresh_nofree":  # nothing freed: every run on never-touched heap memory
+            s = rng.standard_normal(n).astype(np.float32)
+            d = np.empty(n, np.float32)
+            keep.append((s, d))
+        elif fresh == "fresh_touch_s":  # the reference's loop + the source re-read before the barrier
+            s = rng.standard_normal(n).astype(np.float32)
+            d = np.empty(n, np.float32)
+            float(s.sum())
         elif fresh == "fresh_touch_d":  # the reference's loop + the result written before the barrier
             s = rng.standard_normal(n).astype(np.float32)
             d = np.empty(n, np.float32)
@@ -59,8 +68,8 @@ for fresh in os.environ.get("HT_MODES", "fresh,reuse").split(","):
         for r in range(p):
             rel = []
             for k in range(runs):
-                base = min(allrows[q][k][0] for q in range(p))
-                rel.append([x - base for x in allrows[r][k]])
+                t_first = min(allrows[q][k][0] for q in range(p))
+                rel.append([x - t_first for x in allrows[r][k]])
             m = np.mean(np.array(rel[20:]), axis=0) * 1e6
             out[r] = [round(float(x), 2) for x in m]
         print(json.dumps({"fresh": fresh, "timeline_us": out}), flush=True)

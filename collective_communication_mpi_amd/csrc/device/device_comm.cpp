@@ -448,12 +448,14 @@ uint64_t DeviceComm::ring_slot_bytes(uint64_t nbytes, int p) {
   return ((nv + p - 1) / p) * 16;
 }
 
-// `symmetric` (the caller's promise, identical on every rank): every rank's
-// output is registered and its input 16-B aligned, so results are pushed
-// straight into peers' outputs.  Otherwise the result goes through the scratch
-// segment (and a misaligned input is staged too).  Pieces are at most half the
-// scratch either way, so the launch sequence depends only on values equal on
-// all ranks (inbox and scratch sizes, nbytes), never on `symmetric`.
+// `symmetric` (identical on every rank): every rank's output is registered and
+// its input 16-B aligned, so results are pushed straight into peers' outputs, and
+// pieces are bounded by the inbox alone.  Otherwise the result goes through the
+// scratch segment (a misaligned input is staged too) in pieces of at most half the
+// scratch.  The launch sequence therefore DEPENDS on `symmetric` once nbytes
+// exceeds half the scratch: the caller must make the decision identical on all
+// ranks there -- a promise, the collective registration path, or an all-gather of
+// the rank-local check (DeviceGroup._symm_call does the last beyond half the scratch).
 void DeviceComm::allreduce_pipelined_(int algo, uint64_t in, uint64_t out, uint64_t nbytes, uint64_t es, int dtype,
                                       int op, hipStream_t st, int max_blocks, bool symmetric) {
   const int p = size_;

@@ -68,11 +68,7 @@ PYBIND11_MODULE(_host, m) {
 
   if (register_fastcall(m.ptr()) != 0) throw py::error_already_set();
   m.def("wtime", &wtime);
-  m.def("p2p_trace", []() {
-    std::vector<double> v;
-    v.swap(g_p2p_trace);
-    return v;
-  }, "phase timestamps of reduce->bcast calls since the last read (CCMPI_P2P_TRACE=1)");
+  m.def("p2p_trace", []() { return p2p_trace_take(); }, "phase timestamps of reduce->bcast calls since the last read (CCMPI_P2P_TRACE=1)");
   m.def("install_crash_handler", &install_crash_handler, py::arg("fd") = 2,
         "Print a native backtrace on SIGSEGV/SIGBUS/SIGILL/SIGFPE/SIGABRT, then chain to the previous handler");
   m.def("job_id", &job_id_from_env);

@@ -17,6 +17,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <stdexcept>
 #include <vector>
 
@@ -56,13 +57,24 @@ void prefault(void* p, size_t n) {
 
 // Optional phase timestamps of the reduce->bcast schedule (CCMPI_P2P_TRACE=1), read back
 // with p2p_trace(): a diagnostic for where a call's time goes, off by default.
+// The buffer is shared by every thread of the process (schedules run with the GIL
+// released), so it is guarded, and capped: nobody has to read it.
+// CCMPI_P2P_TRACE=2 adds marks inside isend_raw (shm_comm.cpp): entry, request allocated,
+// queued, payload copied into the peer's ring and published.
 bool g_p2p_trace_on = std::getenv("CCMPI_P2P_TRACE") != nullptr;
-std::vector<double> g_p2p_trace;
+bool g_p2p_trace_fine = g_p2p_trace_on && std::atoi(std::getenv("CCMPI_P2P_TRACE")) >= 2;
 
 namespace {
 
+constexpr size_t kTraceCap = size_t(1) << 20;
+std::mutex g_trace_mu;
+std::vector<double> g_trace;
+
 inline void trace_mark() {
-  if (g_p2p_trace_on) g_p2p_trace.push_back(wtime());
+  if (!g_p2p_trace_on) return;
+  const double t = wtime();
+  std::lock_guard<std::mutex> lk(g_trace_mu);
+  if (g_trace.size() < kTraceCap) g_trace.push_back(t);
 }
 
 bool overlaps(const void* a, const void* b, size_t n) {
@@ -72,6 +84,15 @@ bool overlaps(const void* a, const void* b, size_t n) {
 }
 
 }  // namespace
+
+void p2p_trace_mark() { trace_mark(); }
+
+std::vector<double> p2p_trace_take() {
+  std::vector<double> v;
+  std::lock_guard<std::mutex> lk(g_trace_mu);
+  v.swap(g_trace);
+  return v;
+}
 
 void ShmComm::my_reduce_bcast(const void* src, void* dst, size_t count, int dt, int op) {
   if (!reduce_supported(dt, op)) throw std::invalid_argument("ccmpi: unsupported reduction for myAllreduce");
@@ -120,7 +141,9 @@ void ShmComm::my_reduce_bcast(const void* src, void* dst, size_t count, int dt, 
     waitall(rs);
     trace_mark();
   } else {
-    if (dst == src) {
+    if (overlaps(dst, src, nb)) {
+      // any overlap (not only dst == src): the prefault below writes dst while a message
+      // larger than the ring is still being pushed from src during wait(rs)
       char* tmp = scratch(nb);
       std::memcpy(tmp, src, nb);
       src = tmp;

@@ -551,7 +551,9 @@ RequestPtr ShmComm::isend(const void* buf, size_t nbytes, int dest, int tag) {
 }
 
 RequestPtr ShmComm::isend_raw(const void* buf, size_t nbytes, int dest, int tag) {
+  if (g_p2p_trace_fine) p2p_trace_mark();
   auto r = std::make_shared<Request>();
+  if (g_p2p_trace_fine) p2p_trace_mark();
   r->kind = Request::SEND;
   r->peer = dest;
   r->tag = tag;
@@ -560,7 +562,9 @@ RequestPtr ShmComm::isend_raw(const void* buf, size_t nbytes, int dest, int tag)
   if (dest == PROC_NULL) { r->complete = true; return r; }
   if (dest < 0 || dest >= size_) throw std::invalid_argument("ccmpi: invalid destination rank");
   send_q_[dest].push_back(r);
+  if (g_p2p_trace_fine) p2p_trace_mark();
   progress_send_(dest);
+  if (g_p2p_trace_fine) p2p_trace_mark();
   return r;
 }
 

@@ -241,6 +241,8 @@ class ShmComm : public std::enable_shared_from_this<ShmComm> {
 double wtime();
 std::string job_id_from_env();
 extern bool g_p2p_trace_on;              // p2p_algos.cpp: CCMPI_P2P_TRACE
-extern std::vector<double> g_p2p_trace;  // reduce->bcast phase timestamps
+extern bool g_p2p_trace_fine;            // CCMPI_P2P_TRACE=2: marks inside isend_raw
+void p2p_trace_mark();                   // one timestamp (when tracing is on)
+std::vector<double> p2p_trace_take();   // reduce->bcast phase timestamps since the last take
 
 }  // namespace ccmpi

@@ -245,6 +245,18 @@ def _env_int(name: str, default: int) -> int:
     return int(v) if v else default
 
 
+def device_identity(props) -> str:
+    """Identity of a physical GPU across processes: its UUID plus PCI domain:bus:device.
+    Not the device ordinal -- with one visible device per rank (per-rank isolation) every
+    rank's GPU is ordinal 0 -- and not the bus number alone: two GPUs in different PCI
+    domains can share a bus number.  Ranks whose identities are equal share one GPU."""
+    uuid = str(getattr(props, "uuid", "") or "")
+    if uuid.strip("0-") == "":
+        uuid = ""  # an all-zero UUID identifies nothing
+    return (f"{uuid}|{getattr(props, 'pci_domain_id', 0):04x}:{getattr(props, 'pci_bus_id', 0):02x}:"
+            f"{getattr(props, 'pci_device_id', 0):02x}|{props.name}")
+
+
 class DeviceGroup:
     """GPU side of a communicator (one per host communicator per process)."""
 
@@ -272,7 +284,7 @@ class DeviceGroup:
         # HBM roofline on 64-256 MiB collectives, 96 in total only 0.3, 1024 less
         # than 512.  One rank per GPU gets the same 512 (2 CTAs per CU).
         props = torch.cuda.get_device_properties(self.device)
-        key = f"{getattr(props, 'pci_bus_id', 0)}:{getattr(props, 'pci_device_id', 0)}:{props.name}:{self.device.index}"
+        key = device_identity(props)
         keys = host_comm.allgather(key)
         self.ranks_per_device = keys.count(key)
         self.shared_device = self.ranks_per_device > 1
@@ -712,8 +724,16 @@ class DeviceGroup:
             if not ok:
                 raise ValueError("collective: symmetric=True needs 16-B aligned symmetric-heap tensors")
             return True
-        if self.size == 1 or self.reg_min <= 0 or nbytes < self.reg_min:
+        if self.size == 1:
             return self._symm(*ts)
+        if self.reg_min <= 0 or nbytes < self.reg_min:
+            ok = self._symm(*ts)
+            if nbytes > self.scratch.numel() // 2:
+                # rank-local so far, and beyond half the scratch the ring / RHD launch sequence
+                # depends on the decision (symmetric: pieces bounded by the inbox alone; staged:
+                # half-scratch pieces): agree on it, or one rank issues 1 launch and another N
+                ok = all(self.host.allgather(ok))
+            return ok
         return self._register_call(ts)
 
     def _alloc_generation(self) -> int:

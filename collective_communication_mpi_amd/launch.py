@@ -22,6 +22,10 @@ Open MPI style flags that make no sense for a single-host shm runtime
   the IO die (8-rank library Allreduce of 4 KiB 8.1 us unbound, 3.3-3.9 us in one CCD; the
   reference's myAllreduce loop 26.3 -> 14.8-17.3 us; ``profiles/r5_host/``).  A set rather
   than one CPU per rank: a GPU rank's runtime threads (HIP, RCCL proxy) float within it;
+* ``gpu``: rank r on the CPUs local to the GPU it drives (local rank r -> visible GPU
+  r % ngpu), its own L3 domain within them, least busy first (``topology.gpu_plan``: KFD
+  topology + PCI ``local_cpulist`` read from sysfs before any GPU call).  ``bench.py`` uses
+  it for every GPU job; with no GPU in sysfs it falls back to ``l3``;
 * ``l3core``: rank r on one hardware thread of the r-th physical core of those domains;
 * ``core``: rank r on the r-th CPU the launcher may use;
 * ``none`` (or any other level): placement left to the OS.
@@ -37,6 +41,8 @@ import time
 import uuid
 from pathlib import Path
 from typing import List, Optional
+
+from collective_communication_mpi_amd.topology import format_cpu_list, gpu_plan
 
 REPO = Path(__file__).resolve().parent.parent
 
@@ -199,6 +205,13 @@ def launch(n: int, cmd: List[str], timeout: Optional[float] = None, env_extra=No
     base["PYTHONPATH"] = str(REPO) + (os.pathsep + pp if pp else "")
     bind = base.get("CCMPI_BIND", "l3")
     plan = None  # per rank: the CPU set it is bound to
+    if bind == "gpu":
+        try:
+            plan = gpu_plan(n, env=base, busy=_cpu_busy())
+        except (OSError, ValueError):
+            plan = None
+        if plan is None:
+            bind = "l3"
     if bind == "l3":
         dom = l3_set(n)
         plan = [dom] * n if dom is not None else None
@@ -219,8 +232,9 @@ def launch(n: int, cmd: List[str], timeout: Optional[float] = None, env_extra=No
         for k in ("PMI_RANK", "PMI_SIZE", "OMPI_COMM_WORLD_RANK", "OMPI_COMM_WORLD_SIZE", "RANK", "WORLD_SIZE"):
             env.pop(k, None)
         pin = plan[r] if plan is not None else None
+        env["CCMPI_BIND_EFFECTIVE"] = bind if pin is not None else "none"
         if pin is not None:
-            env["CCMPI_BOUND_CPUS"] = ",".join(map(str, pin))
+            env["CCMPI_BOUND_CPUS"] = format_cpu_list(pin)
         procs.append(subprocess.Popen(cmd, env=env, start_new_session=True,
                                       preexec_fn=(lambda c=pin: os.sched_setaffinity(0, set(c))) if pin is not None else None))
 

@@ -852,6 +852,7 @@ class MnistTPLayer:
                                           st, ws.data_ptr())
             self._dwo_done = True
         else:
+            self._dwo_done = False  # a stale flag from an earlier fused head must not skip dW_o
             _native.device().xent_head(zp.data_ptr(), zp.stride(0), 0, y.data_ptr(),  # zp already holds + o_b
                                        y.dtype == torch.int64, B,
                                        cfg.n_classes, cfg.out_pad, 1.0 / global_batch, loss.data_ptr(), dzp.data_ptr(),

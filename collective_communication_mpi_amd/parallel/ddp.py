@@ -22,6 +22,13 @@ gradient all-reduce on that DP communicator:
 * ``finish()`` (call after ``backward()``, before the optimizer) launches
   buckets whose parameters got no gradient, joins the side stream and applies
   the 1/dp average;
+* ``schedule``: ``"overlap"`` (the above), ``"deferred"`` (every bucket all-reduced
+  in ``finish``, back to back on the compute stream at the group's full CTA budget:
+  no collective CTAs beside the backward's GEMMs), or ``"auto"`` (default): the
+  first synchronising steps run each schedule in turn, the device time between
+  consecutive ``finish`` calls is compared (max over ranks) and the faster schedule
+  is kept -- overlap can then never make a step slower than not overlapping
+  (``schedule_choice`` records both times);
 * gradient sinks (``grad_sink=True``, CUDA): the framework's own layers
   (tensor_parallel: Column/RowParallelLinear, ParallelSwiGLUMLP) write their weight
   gradients straight into the bucket views from the dW GEMM and notify the bucket
@@ -97,8 +104,16 @@ class DistributedDataParallel(torch.nn.Module):
 
     def __init__(self, module: torch.nn.Module, comm, bucket_bytes: Optional[int] = None, algo: str = "auto",
                  average: bool = True, overlap: bool = True, broadcast_params: bool = True, grad_sink="auto",
-                 max_blocks: Optional[int] = None):
+                 max_blocks: Optional[int] = None, schedule: Optional[str] = None):
         super().__init__()
+        schedule = schedule or os.environ.get("CCMPI_DP_SCHEDULE", "auto")
+        if schedule not in ("overlap", "deferred", "auto"):
+            raise ValueError(f"DistributedDataParallel: schedule {schedule!r} not in overlap/deferred/auto")
+        # auto: trial steps (the first of each schedule is a warm-up), then the faster one
+        self._trial = (["overlap"] * 3 + ["deferred"] * 3) if schedule == "auto" else []
+        self.schedule = self._trial[0] if self._trial else schedule
+        self.schedule_choice: Optional[dict] = None
+        self._trial_events: List = []
         if bucket_bytes is None:
             # bucket sweep (profiles/r2_overlap/buckets.md): per-call cost makes buckets
             # below ~64 MiB expensive (16 MiB: 2.3x the comm time of 416 MiB buckets)
@@ -247,12 +262,18 @@ class DistributedDataParallel(torch.nn.Module):
         if b.launched or self.p == 1 or not self.require_backward_grad_sync:
             b.launched = True
             return
+        if self.schedule == "deferred" and not self._finishing:
+            return  # all-reduced by finish(), after the backward
         b.launched = True
         b.reduced = True
         if self.dev is None:  # host plane
             from .. import mpi as MPI
 
             self.hc.Allreduce(MPI.IN_PLACE, b.buf.numpy(), op=MPI.SUM)
+            return
+        if self.schedule == "deferred":
+            # nothing else runs: the compute stream and the full CTA budget
+            self.dev.allreduce(b.buf, b.buf, "SUM", self.algo, max_blocks=self.dev.max_blocks, symmetric=True)
             return
         if self.stream is None:
             self.dev.allreduce(b.buf, b.buf, "SUM", self.algo, symmetric=True)
@@ -269,15 +290,21 @@ class DistributedDataParallel(torch.nn.Module):
         ``overlap_blocks``), never above the group's ``overlap_cap``."""
         return min(self.max_blocks or self.dev.overlap_blocks, getattr(self.dev, "overlap_cap", 1 << 30))
 
+    _finishing = False
+
     def finish(self) -> None:
         """Complete the gradient synchronisation (after backward, before the step)."""
-        for b in self.buckets:  # parameters that received no gradient this step
-            if not b.launched:
-                for sk in b.sinks:
-                    if sk.fresh:  # no gradient since zero_grad: the view must read as zero
-                        sk.view.zero_()
-                        sk.fresh = False
-                self._launch(b)
+        self._finishing = True
+        try:
+            for b in self.buckets:  # parameters that received no gradient this step (deferred: all)
+                if not b.launched:
+                    for sk in b.sinks:
+                        if sk.fresh:  # no gradient since zero_grad: the view must read as zero
+                            sk.view.zero_()
+                            sk.fresh = False
+                    self._launch(b)
+        finally:
+            self._finishing = False
         if self.stream is not None:
             torch.cuda.current_stream(self.device).wait_stream(self.stream)
         if self._late:
@@ -315,6 +342,30 @@ class DistributedDataParallel(torch.nn.Module):
             for sk in b.sinks:
                 sk.reported = False
                 sk.param.grad = sk.view
+        if self._trial and self.require_backward_grad_sync and self.p > 1 and self.dev is not None:
+            self._trial_step()
+
+    def _trial_step(self) -> None:
+        """``schedule="auto"``: an event at the end of every synchronising step; step k ran
+        ``_trial[k]``.  After the last trial step: the median device time between
+        consecutive events of each schedule (its first step, the switch, excluded), max over
+        ranks (a host all-reduce: every rank takes the same decision), and the faster
+        schedule kept."""
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record(torch.cuda.current_stream(self.device))
+        self._trial_events.append(ev)
+        k = len(self._trial_events) - 1
+        if k + 1 < len(self._trial):
+            self.schedule = self._trial[k + 1]
+            return
+        from .. import mpi as MPI
+
+        ev.synchronize()
+        evs = self._trial_events
+        gaps = [evs[i - 1].elapsed_time(evs[i]) for i in range(1, len(evs))]
+        self.schedule_choice = pick_schedule(self._trial, gaps, lambda v: self.hc.allreduce(v, op=MPI.MAX))
+        self.schedule = self.schedule_choice["chosen"]
+        self._trial, self._trial_events = [], []
 
     def zero_grad(self, set_to_none: bool = False) -> None:
         """Zero the gradients and re-attach every ``.grad`` view (``set_to_none`` is ignored).
@@ -335,13 +386,14 @@ class DistributedDataParallel(torch.nn.Module):
             for q in b.params:
                 q.grad = None if id(q) in sunk else self._view_of[id(q)]
 
-    def allreduce_all(self) -> None:
+    def allreduce_all(self, max_blocks: Optional[int] = None) -> None:
         """All-reduce every bucket now, back to back on the current stream (the comm-only
-        time of the overlap measurement; no averaging)."""
+        time of the overlap measurement; no averaging).  ``max_blocks``: the CTA budget
+        (default: the overlap budget)."""
         if self.dev is None or self.p == 1:
             return
         for b in self.buckets:
-            self.dev.allreduce(b.buf, b.buf, "SUM", self.algo, max_blocks=self._blocks(),
+            self.dev.allreduce(b.buf, b.buf, "SUM", self.algo, max_blocks=max_blocks or self._blocks(),
                                symmetric=True)
 
     @property
@@ -349,8 +401,23 @@ class DistributedDataParallel(torch.nn.Module):
         return [b.buf.numel() * b.buf.element_size() for b in self.buckets]
 
 
+def pick_schedule(trial: List[str], gaps_ms: List[float], agree_max) -> dict:
+    """The ``schedule="auto"`` decision.  ``trial[k]``: the schedule step k ran;
+    ``gaps_ms[k - 1]``: device time from the end of step k - 1 to the end of step k.  A
+    step whose predecessor ran another schedule (the first of each, a warm-up or the
+    switch) is not counted; per schedule the median, max over ranks (``agree_max``, so
+    every rank decides the same), the smaller wins (ties: overlap)."""
+    times: Dict[str, List[float]] = {}
+    for k in range(1, len(trial)):
+        if trial[k] == trial[k - 1] and k - 1 < len(gaps_ms):
+            times.setdefault(trial[k], []).append(gaps_ms[k - 1])
+    med = {s: agree_max(sorted(v)[len(v) // 2]) for s, v in sorted(times.items(), key=lambda kv: kv[0] != "overlap")}
+    chosen = min(med, key=med.get) if med else "overlap"
+    return {"chosen": chosen, **{f"{s}_ms": round(v, 3) for s, v in med.items()}}
+
+
 def ddp_wrap(module: torch.nn.Module, comm, **kw) -> DistributedDataParallel:
     return DistributedDataParallel(module, comm, **kw)
 
 
-__all__ = ["DistributedDataParallel", "ddp_wrap"]
+__all__ = ["DistributedDataParallel", "ddp_wrap", "pick_schedule"]

@@ -135,10 +135,12 @@ def _self_comm(comm):
 def measure_ddp_overlap(comm, layers: int = 32, tokens: int = 4096, seq: int = 2048, vocab: bool = True,
                         iters: int = 2, cfg: LlamaConfig = LLAMA3_8B, bucket_mb: Optional[int] = None,
                         blocks_sweep: List[int] = (32, 64, 128, 256), verbose: bool = False) -> Dict:
-    """Compute-only, comm-only and overlapped step times (forward + backward + finish,
-    max over ranks) of the Llama-3-8B-shaped model under DDP over ``comm``, and the hidden
-    fraction ``(compute + comm - overlapped) / comm``; the bucket all-reduces' CTA budget
-    swept over ``blocks_sweep`` (the best is the record).  Collective: every rank calls."""
+    """Compute-only, comm-only, overlapped and deferred step times (forward + backward +
+    finish, max over ranks) of the Llama-3-8B-shaped model under DDP over ``comm``, and the
+    signed hidden fraction ``(compute + comm - overlapped) / comm``; the bucket all-reduces'
+    CTA budget swept over ``blocks_sweep`` (the best overlapped one is the record), then the
+    deferred schedule (all buckets after the backward at the full budget).  ``step_ms`` is
+    the faster schedule (``schedule``), both on record.  Collective: every rank calls."""
     from .. import mpi as MPI
 
     hc = comm.comm
@@ -160,8 +162,9 @@ def measure_ddp_overlap(comm, layers: int = 32, tokens: int = 4096, seq: int = 2
     model = LlamaModel(c, tp, device, vocab=vocab)
     nparams = sum(q.numel() for q in model.parameters())
     say(f"model: {nparams / 1e9:.2f} B params, {time.perf_counter() - t0:.1f}s")
+    # the schedules are timed explicitly below (overlapped per budget, then deferred)
     ddp = DistributedDataParallel(model, comm, bucket_bytes=(bucket_mb << 20) if bucket_mb else None,
-                                  broadcast_params=False)
+                                  broadcast_params=False, schedule="overlap")
     say(f"DDP: {len(ddp.buckets)} buckets, {time.perf_counter() - t0:.1f}s")
     g = torch.Generator(device=device).manual_seed(1234 + rank)  # each DP rank its own data shard
     ids = torch.randint(0, c.vocab, (batch, seq), generator=g, device=device)
@@ -191,7 +194,8 @@ def measure_ddp_overlap(comm, layers: int = 32, tokens: int = 4096, seq: int = 2
     ddp.require_backward_grad_sync = True
 
     def hidden_of(t_c: float, t_o: float):
-        return None if p == 1 or t_c == 0 else max(0.0, min(1.0, (t_compute + t_c - t_o) / t_c))
+        # signed: negative when the overlapped step is slower than compute + comm back to back
+        return None if p == 1 or t_c == 0 else (t_compute + t_c - t_o) / t_c
 
     # comm-only at the group's full CTA budget (max_blocks): the bound the links set, with no
     # compute beside it
@@ -218,12 +222,23 @@ def measure_ddp_overlap(comm, layers: int = 32, tokens: int = 4096, seq: int = 2
         say(f"{mb} CTAs per bucket all-reduce: comm-only {t_c * 1e3:.1f} ms, overlapped {sweep[mb] * 1e3:.1f} ms")
     best_mb = min(sweep, key=sweep.get)
     ddp.max_blocks = best_mb or None
-    t_both = sweep[best_mb]
+    t_over = sweep[best_mb]
     t_comm = per[best_mb]["comm_ms"] / 1e3
+    # deferred: every bucket all-reduced after the backward at the full budget (nothing
+    # beside the GEMMs); the step is the faster of the two schedules -- DDP's own
+    # schedule="auto" makes the same choice in a training loop
+    t_def = None
+    if p > 1:
+        ddp.schedule = "deferred"
+        t_def = timed(step)
+        say(f"deferred (post-backward, {dev.max_blocks} CTAs) {t_def * 1e3:.1f} ms")
+    chosen = "deferred" if (t_def is not None and t_def < t_over) else "overlap"
+    ddp.schedule = chosen
+    t_both = t_def if chosen == "deferred" else t_over
     loss = float(step().item())
     torch.cuda.synchronize()
     dev.check()
-    hidden = hidden_of(t_comm, t_both)
+    hidden = hidden_of(t_comm, t_over)
     gbytes = sum(b.buf.numel() * b.buf.element_size() for b in ddp.buckets)
     nonemb = nparams - (c.vocab * c.d if vocab else 0)
     flops = 6 * nonemb * batch * seq  # fwd + bwd GEMM work (attention scores not counted)
@@ -233,7 +248,10 @@ def measure_ddp_overlap(comm, layers: int = 32, tokens: int = 4096, seq: int = 2
            "ranks": p, "params": nparams, "grad_bytes_bf16": gbytes, "tokens_per_rank": batch * seq,
            "seq_len": seq, "backward": "autograd (real dX + dW GEMMs, attention, norms, embedding)",
            "compute_ms": round(t_compute * 1e3, 2), "comm_ms": round(t_comm * 1e3, 2),
-           "overlapped_ms": round(t_both * 1e3, 2), "comm_hidden_fraction": None if hidden is None else round(hidden, 3),
+           "step_ms": round(t_both * 1e3, 2), "schedule": chosen,
+           "overlapped_ms": round(t_over * 1e3, 2), "deferred_ms": None if t_def is None else round(t_def * 1e3, 2),
+           # signed: (compute + comm - overlapped) / comm of the overlapped schedule
+           "comm_hidden_fraction": None if hidden is None else round(hidden, 3),
            "comm_algbw_GBps": round(gbytes / t_comm / 1e9, 2) if t_comm else None,
            "comm_full_ms": round(t_full * 1e3, 2), "comm_full_blocks": dev.max_blocks if p > 1 else None,
            "comm_full_algbw_GBps": round(gbytes / t_full / 1e9, 2) if t_full else None,

@@ -20,13 +20,14 @@ from .tensor_parallel import ParallelSwiGLUMLP, all_reduce_
 
 
 def measure_tp_mlp(comm, tokens: int = 4096, d: int = 4096, ffn: int = 14336, iters: int = 10, warmup: int = 3,
-                   eager_gate: bool = False, variants: bool = False, mode: str = "") -> Dict:
+                   eager_gate: bool = False, variants: bool = False, mode: str = "", modes=None) -> Dict:
     """Median forward and forward + backward times (max over ranks), the whole group's
     model TFLOP/s, the T x d bf16 TP all-reduce alone, and the host calls the device
     plane made during one steady-state forward + backward (0 expected).  ``variants``
     (p > 1): the same block with each row-parallel mode (plain / chunked / fused / push)
     side by side FIRST; the fastest correct one is recorded as this shape's ``auto`` (the
     group's ``row_modes``, CCMPI_TUNE_FILE), and the headline then runs ``auto``.
+    ``modes``: the row modes of that side-by-side (default all of ``tp.ROW_MODES``).
     Collective: every rank calls."""
     from .. import mpi as MPI
 
@@ -100,7 +101,8 @@ def measure_tp_mlp(comm, tokens: int = 4096, d: int = 4096, ffn: int = 14336, it
         # correct forward becomes this (M, N)'s "auto" for groups of this identity -- written
         # to CCMPI_TUNE_FILE like the collectives' table, and used by the headline below
         var, ref = {}, None
-        for m in tp.ROW_MODES:
+        for m in (modes or tp.ROW_MODES):
+            rec, err, exact, close, ran_ok = None, None, 0, 0, 0
             try:
                 mlp = build(m)
                 vf, vfb, vh, vchk = run(mlp)
@@ -110,20 +112,30 @@ def measure_tp_mlp(comm, tokens: int = 4096, d: int = 4096, ffn: int = 14336, it
                 ran = [k for k, v in tp.CALLS.items() if v != calls0.get(k, 0) and k.startswith("row_")]
                 if ref is None:
                     ref = out_m
-                exact = bool(hc.allreduce(int(torch.equal(out_m, ref)), op=MPI.MIN))
-                close = bool(hc.allreduce(int(torch.allclose(out_m.float(), ref.float(), rtol=2e-2, atol=2e-3)),
-                                          op=MPI.MIN))
-                var[m] = {"fwd_ms": round(vf * 1e3, 3), "fwd_bwd_ms": round(vfb * 1e3, 3), "host_calls_per_step": vh,
-                          "out_abs_mean": round(vchk, 6), "bitwise_equal_plain": exact, "close_to_plain": close,
-                          "ran": ran}
+                exact = int(torch.equal(out_m, ref))
+                close = int(torch.allclose(out_m.float(), ref.float(), rtol=2e-2, atol=2e-3))
+                ran_ok = int(any(r == f"row_{m}" for r in ran))  # the mode ran (not a fallback)
+                rec = {"fwd_ms": round(vf * 1e3, 3), "fwd_bwd_ms": round(vfb * 1e3, 3), "host_calls_per_step": vh,
+                       "out_abs_mean": round(vchk, 6), "ran": ran}
                 del mlp, out_m
             except Exception as e:  # noqa: BLE001 - one variant must not cost the record
-                var[m] = {"error": f"{type(e).__name__}: {e}"[:200]}
+                err = f"{type(e).__name__}: {e}"[:200]
+            # every outcome agreed on every rank -- a rank that raised still makes these
+            # calls, so the group's collectives stay matched and every rank sees one verdict
+            ok_all = bool(hc.allreduce(int(err is None), op=MPI.MIN))
+            exact = bool(hc.allreduce(exact, op=MPI.MIN))
+            close = bool(hc.allreduce(close, op=MPI.MIN))
+            ran_ok = bool(hc.allreduce(ran_ok, op=MPI.MIN))
+            if not ok_all:
+                var[m] = {"error": err or "failed on another rank"}
+                continue
+            var[m] = {**rec, "bitwise_equal_plain": exact, "close_to_plain": close, "ran_as_named": ran_ok}
         ok = {m: v["fwd_ms"] for m, v in var.items()
               if "error" not in v and v["close_to_plain"] and (m != "push" or v["bitwise_equal_plain"])
-              and any(r == f"row_{m}" for r in v["ran"])}  # the mode actually ran (not a fallback)
-        if ok:
-            best = min(ok, key=ok.get)
+              and v["ran_as_named"]}
+        # fwd_ms is already the max over ranks; rank 0's choice is everyone's regardless
+        best = hc.bcast(min(ok, key=ok.get) if ok else None, root=0)
+        if best:
             dg = comm.dev
             dg.row_modes[(tokens, d)] = best
             path = getattr(dg, "tune_file", None)

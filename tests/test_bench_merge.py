@@ -238,3 +238,33 @@ def test_sweep_curve_from_tune_times():
     alg = (1 << 20) / 1e-4 / 1e9
     assert curve[0]["algbw_GBps"] == round(alg, 2) and curve[0]["busbw_GBps"] == round(alg * 1.5, 2)
     assert [c["best"] for c in DeviceGroup.sweep_curve(G(), "bfloat16")] == ["ring"]
+
+
+def test_phase_binding_paths(monkeypatch):
+    """both launch paths place GPU ranks the same way.  torchrun (nobody
+    bound the supervisor): rank 0 reads the GPU-local plan once and every rank takes its
+    local rank's set; launch.py (``CCMPI_BOUND_CPUS`` set): the children inherit that
+    binding; ``CCMPI_BIND=none``: the OS places them."""
+    from collective_communication_mpi_amd import topology
+
+    plan = [[0, 1], [2, 3], [64, 65], [66, 67]]
+    monkeypatch.setattr(topology, "gpu_plan", lambda n, **k: plan[:n])
+
+    class World:
+        def Get_size(self):
+            return 4
+
+        def bcast(self, obj, root=0):
+            return obj if obj is not None else plan
+
+    monkeypatch.delenv("CCMPI_BOUND_CPUS", raising=False)
+    monkeypatch.delenv("CCMPI_BIND", raising=False)
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "4")
+    assert bench.phase_binding(World(), 0, 0) == ([0, 1], "gpu")
+    assert bench.phase_binding(World(), 2, 2) == ([64, 65], "gpu")
+    monkeypatch.setenv("CCMPI_BIND", "none")
+    assert bench.phase_binding(World(), 1, 1) == (None, "none")
+    monkeypatch.setenv("CCMPI_BIND", "gpu")
+    monkeypatch.setenv("CCMPI_BOUND_CPUS", "8-15")
+    monkeypatch.setenv("CCMPI_BIND_EFFECTIVE", "gpu")
+    assert bench.phase_binding(World(), 1, 1) == (None, "gpu")

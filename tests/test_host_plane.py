@@ -158,6 +158,33 @@ def test_tensor_parallel_layers_and_ddp_cpu(n):
     assert "tp/ddp OK" in r.stdout
 
 
+@pytest.mark.parametrize("schedule", ["overlap", "deferred"])
+def test_ddp_schedules_cpu(schedule):
+    """the deferred schedule (every bucket all-reduced in finish(), after
+    the backward) gives the same gradients and SGD steps as the overlapped one."""
+    r = run_ranks(4, py("tests/workers/tp_ddp_worker.py", "--device", "cpu", "--schedule", schedule), timeout=300)
+    assert "tp/ddp OK" in r.stdout and f"schedule={schedule}" in r.stdout
+
+
+def test_ddp_auto_schedule_choice():
+    """``schedule="auto"``: the trial steps' device times (max over ranks) pick the faster
+    schedule; the first step of each schedule (warm-up / switch) is not counted."""
+    from collective_communication_mpi_amd.parallel.ddp import pick_schedule
+
+    trial = ["overlap"] * 3 + ["deferred"] * 3
+    # gaps: step1, step2 overlap; step3 = switch (excluded); step4, step5 deferred
+    slow_overlap = [34.7, 34.9, 99.0, 32.1, 32.3]
+    c = pick_schedule(trial, slow_overlap, lambda v: v)
+    assert c["chosen"] == "deferred" and c["overlap_ms"] == 34.9 and c["deferred_ms"] == 32.3
+    fast_overlap = [28.0, 28.2, 5.0, 32.1, 32.3]
+    assert pick_schedule(trial, fast_overlap, lambda v: v)["chosen"] == "overlap"
+    # another rank is slower with overlap: max over ranks decides for everyone
+    assert pick_schedule(trial, fast_overlap, lambda v: v + 10 if v < 30 else v)["chosen"] == "deferred"
+    # ties keep overlap; no usable sample keeps overlap
+    assert pick_schedule(trial, [30.0] * 5, lambda v: v)["chosen"] == "overlap"
+    assert pick_schedule(["overlap"], [], lambda v: v)["chosen"] == "overlap"
+
+
 def test_llama_ddp_cpu():
     """DistributedDataParallel over a tiny Llama-shaped model of the framework's TP layers
     (parallel/llama_dp.py) on the host plane: every rank's gradients equal the mean of the

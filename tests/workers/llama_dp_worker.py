@@ -114,7 +114,8 @@ if args.measure and device.type == "cuda":
                             blocks_sweep=[64, 128])
     if rank == 0:
         print("measure:", r, flush=True)
-    if not (r["compute_ms"] > 0 and r["overlapped_ms"] > 0 and r["comm_hidden_fraction"] is not None):
+    if not (r["compute_ms"] > 0 and r["overlapped_ms"] > 0 and r["comm_hidden_fraction"] is not None
+            and r["deferred_ms"] > 0 and r["step_ms"] == min(r["overlapped_ms"], r["deferred_ms"])):
         fails.append(f"measure_ddp_overlap record incomplete: {r}")
 bad = hc.allgather(fails)
 if rank == 0:

@@ -25,6 +25,7 @@ from collective_communication_mpi_amd.parallel.tensor_parallel import _init_full
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--device", default="cpu")
+ap.add_argument("--schedule", default=None, help="DDP schedule: overlap | deferred | auto (default)")
 args = ap.parse_args()
 comm = Communicator(MPI.COMM_WORLD)
 rank, world = comm.Get_rank(), comm.Get_size()
@@ -74,7 +75,7 @@ def rel(a, b):
     return ((a.float().cpu() - b.float().cpu()).norm() / b.float().cpu().norm().clamp_min(1e-12)).item()
 
 
-model = DistributedDataParallel(TPModel(), dp_comm, bucket_bytes=16 << 10)
+model = DistributedDataParallel(TPModel(), dp_comm, bucket_bytes=16 << 10, schedule=args.schedule)
 ref = RefModel()
 opt = torch.optim.SGD(model.parameters(), lr=0.05)
 ropt = torch.optim.SGD(ref.parameters(), lr=0.05)
@@ -119,4 +120,5 @@ if fails:
     print(f"[rank {rank}] FAIL: {fails}", flush=True)
     sys.exit(1)
 if rank == 0:
-    print(f"tp/ddp OK world={world} tp={tp} dp={dp} device={args.device} buckets={len(model.buckets)}", flush=True)
+    print(f"tp/ddp OK world={world} tp={tp} dp={dp} device={args.device} buckets={len(model.buckets)} "
+          f"schedule={model.schedule}", flush=True)

@@ -1,0 +1,15 @@
+#!/usr/bin/env bash
+# Round 5: TN GEMM with two K tiles in flight (numerics over prefetch depths, micro-timings,
+# the training step).
+set -o pipefail
+cd "$(dirname "$0")/../.."
+OUT=gpurun_out/${OUT_TAG:-r5_32}
+mkdir -p $OUT
+export TMPDIR=/tmp
+timeout -k 10 400 python3 -u -m pytest -x -v --timeout 120 --timeout-method thread -m gpu \
+  tests/test_gpu_kernels.py -k "gemm_tn" > $OUT/tests.log 2>&1
+rc=$?; tail -3 $OUT/tests.log; [ $rc -ne 0 ] && { grep -E "FAILED|^E |Error" $OUT/tests.log | head -30; exit $rc; }
+timeout -k 10 300 python3 benchmarks/train_kernels_micro.py gemm_tn_a > $OUT/micro.jsonl 2> $OUT/micro.err
+rc=$?; cat $OUT/micro.jsonl; [ $rc -ne 0 ] && { tail -20 $OUT/micro.err; exit $rc; }
+timeout -k 10 200 python3 benchmarks/train_graph_probe.py > $OUT/probe.txt 2> $OUT/probe.err
+rc=$?; cat $OUT/probe.txt; exit $rc
