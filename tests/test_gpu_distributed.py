@@ -355,6 +355,19 @@ def test_tensor_parallel_layers_and_ddp_gpu(n):
     assert "tp/ddp OK" in r.stdout
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("schedule,steps", [("deferred", 2), ("auto", 7)])
+def test_ddp_schedules_gpu(schedule, steps):
+    """the deferred schedule (buckets all-reduced after the backward at the
+    full CTA budget) matches the fp32 reference like the overlapped one; ``auto`` times both
+    over its trial steps and settles on one (every step still checked)."""
+    r = run_ranks(4, py("tests/workers/tp_ddp_worker.py", "--device", "cuda", "--schedule", schedule,
+                        "--steps", str(steps)), timeout=300, env=ENV)
+    assert "tp/ddp OK" in r.stdout
+    if schedule == "auto":
+        assert "choice={'chosen'" in r.stdout, r.stdout
+
+
 def test_bench_tuning_table_drives_auto(tmp_path):
     """the bench's tuning sweep writes CCMPI_TUNE_FILE; a device group
     created afterwards loads it and ``auto`` runs what the table says (ring, RHD), 4 ranks."""
