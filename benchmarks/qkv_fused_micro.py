@@ -27,6 +27,43 @@ def timed(fn, iters):
     return s.elapsed_time(e) * 1e3 / iters  # us
 
 
+def trace_phases(fused, mode, train, mean, cap, npairs):
+    """Launch once more with phase stamps; medians over waves of each phase (shader clocks).
+    Stamp k: 0 entry, 1 loop entry (prologue done), per iteration j < 4 at 2 + 5 j: start
+    (X in registers), +1 q|k|v projected, +2 z formed, +3 before the workgroup barrier (image
+    mode: after the DMA wait and the next X build), +4 epilogue stored; 31 kernel end."""
+    import numpy as np
+
+    waves = min(cap, (npairs + 3) // 4) * 4
+    ts = torch.zeros(waves * 32, dtype=torch.int64, device="cuda")
+    fused(mode, train, mean, ts.data_ptr())()
+    torch.cuda.synchronize()
+    t = ts.view(waves, 32).cpu().numpy().astype(np.int64)
+    t = t[t[:, 0] != 0]
+    out = {"waves": int(len(t)), "prologue": int(np.median(t[:, 1] - t[:, 0]))}
+    # inside the prologue: 24 W_h loads issued, 25 tail fragments + biases in, 26 (image mode)
+    # every load and both images' DMA in, 27 first X built
+    pro = {"w_issue": (0, 24), "w_arrive": (24, 25), "dma_wait": (25, 26), "build_x0": (26, 27), "to_loop": (27, 1)}
+    out["prologue_parts"] = {k: int(np.median(t[:, b] - t[:, a])) for k, (a, b) in pro.items()
+                             if (t[:, a] != 0).all() and (t[:, b] != 0).all()}
+    names = ["proj", "attn_z", "dma_wait_build", "barrier_epilogue", "to_next"]
+    for j in range(4):
+        b = 2 + 5 * j
+        ok = t[:, b] != 0
+        if not ok.any():
+            break
+        tj = t[ok]
+        ph = {"from_prev": int(np.median(tj[:, b] - (tj[:, 1] if j == 0 else tj[:, b - 1])))}
+        for k, nm in enumerate(names[:4]):
+            ph[nm] = int(np.median(tj[:, b + k + 1] - tj[:, b + k]))
+        out[f"it{j}"] = ph
+    out["tail"] = int(np.median(t[:, 31] - np.max(np.where(t[:, 2:22] != 0, t[:, 2:22], 0), axis=1)))
+    out["wave_span_median"] = int(np.median(t[:, 31] - t[:, 0]))
+    out["kernel_span"] = int(t[:, 31].max() - t[:, 0].min())
+    out["start_skew"] = int(np.percentile(t[:, 0], 95) - t[:, 0].min())
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=200)
@@ -35,6 +72,9 @@ def main():
     ap.add_argument("--only", default="")
     ap.add_argument("--grid", type=int, default=0, help="only this persistent grid size")
     ap.add_argument("--train", type=int, default=-1, help="0/1: only inference / training stores")
+    ap.add_argument("--nolse", action="store_true", help="inference without the lse store (lse = null)")
+    ap.add_argument("--trace", action="store_true",
+                    help="one extra launch with phase stamps (AttnArgs.tstamp): per-phase shader-clock medians")
     args = ap.parse_args()
     dev = _native.device()
     st = torch.cuda.current_stream().cuda_stream
@@ -58,8 +98,12 @@ def main():
                   zrows=0, zpush=[], stream=st, ld_xq=kp, kq=kp, wq=w.data_ptr(), ld_wq=w.stride(0), bq=bq.data_ptr(),
                   ld_qkv=qkv.stride(0))
 
-    def fused(mode, train, mean):
+    def fused(mode, train, mean, tstamp=0):
         kw = dict(common)
+        if args.nolse and not train:
+            kw["lse"] = 0
+        if tstamp:
+            kw["tstamp"] = tstamp
         kw.update(pool=pool.data_ptr() if train else 0,  # (the model passes pool only for a backward)
                   xq=0 if mode == "img" else xp.data_ptr(), img=img.data_ptr() if mode == "img" else 0,
                   xq_out=xp.data_ptr() if (mode == "img" and train) else 0, qkv_out=qkv.data_ptr() if train else 0,
@@ -83,7 +127,9 @@ def main():
                     if args.only and args.only != mode:
                         continue
                     rows.append(dict(kernel="fused", mode=mode, train=train, mean=mean, grid=cap,
-                                     us=timed(fused(mode, train, mean), args.iters)))
+                                     us=timed(fused(mode, train, mean), args.iters), nolse=args.nolse))
+                    if args.trace:
+                        rows[-1]["phases"] = trace_phases(fused, mode, train, mean, cap, B * H)
     dev.attn_set_qkv_grid(0)
     for r in rows:
         r.update(B=B, H=H)

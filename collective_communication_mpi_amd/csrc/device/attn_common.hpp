@@ -69,7 +69,11 @@ struct AttnArgs {
   uint16_t* fold_out;
   int ld_fold_out, fold_R, fold_d, fold_kp;
   int fold_at_start;  // 1: the fold runs before the attention work (its loads under W_h's), 0: after
+  // diagnostic (fused QKV forward): per wave kTStamps shader-clock stamps of the kernel's
+  // phases ([grid * 4 waves][32] u64; s_memtime, buffered in LDS, stored at the end), or null
+  unsigned long long* tstamp;
 };
+constexpr int kTStamps = 32;
 
 // MFMA path (attn_mfma.hip): S <= 16, D in {32, 64, 128}, 16-B aligned rows.
 bool mfma_supported(const AttnArgs& a, bool bwd);

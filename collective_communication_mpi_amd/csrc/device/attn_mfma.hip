@@ -118,6 +118,12 @@ __device__ __forceinline__ float pair32_max(float v) {
   return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
 }
 
+// DPP row rotation: lane l of each 16-lane row reads lane (l - N) mod 16 of the same row
+template <int N>
+__device__ __forceinline__ float row_ror(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x120 + N, 0xf, 0xf, false));
+}
+
 __device__ __forceinline__ s4 ld_s4(const uint16_t* p, bool ok) {
   const uint2 z = ok ? *reinterpret_cast<const uint2*>(p) : uint2{0, 0};
   return __builtin_bit_cast(s4, z);
@@ -230,6 +236,20 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
   const int S = a.S, HD = a.Hl * D, npairs = a.B * a.Hl;
   const float inv_s = 1.f / (float)S;  // (fused path: means as multiplies)
+  // diagnostic phase stamps (a.tstamp): shader clock per phase, lane 0 of each wave, into LDS
+  __shared__ unsigned long long tsb[QKV ? WPB : 1][QKV ? kTStamps : 1];
+  const bool tsr = QKV && a.tstamp != nullptr;
+  auto stamp = [&](int k) {
+    if constexpr (QKV) {
+      if (tsr) {
+        const unsigned long long t = __builtin_amdgcn_s_memtime();
+        if (lane == 0 && k < kTStamps) tsb[wave][k] = t;
+      }
+    }
+  };
+  if (tsr && lane < kTStamps) tsb[wave][lane] = 0ull;  // (slots a short wave never reaches read 0)
+  stamp(0);
+  int itn = 0;  // iteration count (stamps 2 + 5 j .. 6 + 5 j, j < 4)
   // fused QKV: Hl | 4, so pair -> (sequence, head) is a shift and a mask, not a division
   const int lhl = a.Hl == 4 ? 2 : a.Hl == 2 ? 1 : 0;
   auto div_hl = [&](int x) { return QKV ? x >> lhl : x / a.Hl; };
@@ -345,11 +365,18 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
       for (int id = threadIdx.x; id < nseq * 160; id += WPB * 64) {
         const int sq = id / 160, rem = id - sq * 160, t = rem / 10, ch = rem - t * 10;
         const float* im = imgs[buf] + sq * 784 + (t >> 2) * 196 + (t & 3) * 7;
+        // pixel (pr, pc) of column 8 ch, stepped along the chunk; every lane reads (a clamped
+        // address past the 49 pixels) and selects: no divergent branch per column
+        int pr = (8 * ch) / 7, pc = 8 * ch - 7 * pr;
         float v[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const int cc = 8 * ch + j;
-          v[j] = cc < 49 ? im[(cc / 7) * 28 + cc % 7] : ((cc == 49 || cc == 50 + t) ? 1.f : 0.f);
+          const float px = im[cc < 49 ? pr * 28 + pc : 0];
+          v[j] = cc < 49 ? px : ((cc == 49 || cc == 50 + t) ? 1.f : 0.f);
+          const bool wrap = pc == 6;
+          pc = wrap ? 0 : pc + 1;
+          pr += wrap ? 1 : 0;
         }
         const u32x4 w = {pk_bf16(v[0], v[1]), pk_bf16(v[2], v[3]), pk_bf16(v[4], v[5]), pk_bf16(v[6], v[7])};
         *reinterpret_cast<u32x4*>(xs[buf][sq] + t * LDX + 8 * ch) = w;
@@ -359,6 +386,11 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
   };
   if constexpr (QKV) {
     const int hw = mod_hl(wave);
+    // every load first (the bias by every lane, unconditionally), every use after: a bias load
+    // inside `g == gb` whose value was consumed at once (and the partial overwrite of a tail
+    // fragment still being loaded) made the prologue 12 serialised global round trips --
+    // 13-16 k of the kernel's ~30 k shader clocks per wave (profiles/r6_attn, phase stamps)
+    float bqv[3][NT];
 #pragma unroll
     for (int sel = 0; sel < 3; ++sel)
 #pragma unroll
@@ -368,13 +400,20 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
         wf[sel][nt][0] = ld_row16(w + 8 * g, 8 * g < a.kq);
         wf[sel][nt][1] = ld_row16(w + 32 + 8 * g, 32 + 8 * g < a.kq);
         wtl[sel][nt] = ld_s4(w + 64 + 4 * g, 64 + 4 * g < a.kq);
-        if (g == gb) {
-          const float bias = a.bq[f];
-          const uint32_t hi = f32_to_bf16_bits(bias);
-          wtl[sel][nt][0] = (short)hi;
-          wtl[sel][nt][1] = (short)f32_to_bf16_bits(bias - __uint_as_float(hi << 16));
-        }
+        bqv[sel][nt] = a.bq[f];
       }
+    stamp(24);  // every W_h load issued
+#pragma unroll
+    for (int sel = 0; sel < 3; ++sel)
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        const float bias = bqv[sel][nt];
+        const uint32_t hi = f32_to_bf16_bits(bias);
+        const short lo = (short)f32_to_bf16_bits(bias - __uint_as_float(hi << 16));
+        wtl[sel][nt][0] = g == gb ? (short)hi : wtl[sel][nt][0];
+        wtl[sel][nt][1] = g == gb ? lo : wtl[sel][nt][1];
+      }
+    stamp(25);  // W_h's tail fragments and biases arrived
     if constexpr (!IMG) load_x(blockIdx.x * WPB + wave);
     if constexpr (IMG) {
       // images two iterations deep: the first two now, X of the first one built
@@ -382,13 +421,17 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
       stage_imgs(0, p0);
       if (p0 + stride < npairs) stage_imgs(1, p0 + stride);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      stamp(26);  // every W_h load and both images' DMA landed
       __syncthreads();
       build_x(0, p0);
+      stamp(27);
       __syncthreads();
     }
   }
-  for (int base = blockIdx.x * WPB; base < npairs; base += stride, it ^= 1) {
+  stamp(1);
+  for (int base = blockIdx.x * WPB; base < npairs; base += stride, it ^= 1, ++itn) {
    const int pr = base + wave;
+   const int sj = itn < 4 ? 2 + 5 * itn : kTStamps;  // this iteration's stamp slots
    bf16x8 xr[2];
    s4 xt;
    if constexpr (QKV) {
@@ -406,6 +449,7 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
     xt = xtn;
     if constexpr (!IMG) load_x(pr + stride);
    }
+   stamp(sj);
    if (pr < npairs) {
     const int b = div_hl(pr), h = mod_hl(pr);
     bf16x8 qr[NK], kr[NK];
@@ -476,6 +520,7 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
       }
       __builtin_amdgcn_wave_barrier();
       if (qo) rows_out<D, LD>(O, qo + 2 * HD, a.ld_qkv, S, lane);
+      stamp(sj + 1);
     } else {
       const uint16_t* qb = a.qkv + (size_t)b * S * a.ld_qkv + h * D;
       bf16x8 vr[NK];
@@ -508,7 +553,7 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
     // (fused path: the hardware reciprocal -- the precise division is ~10 VALU ops, and the
     // probabilities are rounded to bf16 right after)
     const float inv = QKV ? __builtin_amdgcn_rcpf(s) : 1.f / s;
-    if (g == 0 && c < S) a.lse[(size_t)pr * S + c] = m + __logf(s);
+    if (a.lse && g == 0 && c < S) a.lse[(size_t)pr * S + c] = m + __logf(s);
     const s4 pa = pack4(e[0] * inv, e[1] * inv, e[2] * inv, e[3] * inv);  // A[i = c][j = 4g + jj]
     __builtin_amdgcn_wave_barrier();
     if constexpr (QKV) {
@@ -523,6 +568,7 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
       for (int nt = 0; nt < NT; ++nt) zt = mma16(pack4(ot[nt][0], ot[nt][1], ot[nt][2], ot[nt][3]), wo16[nt], zt);
 #pragma unroll
       for (int r = 0; r < 4; ++r) ztp[it][wave][(4 * g + r) * 16 + c] = zt[r];  // z[i = 4g + r][cls = c]
+      stamp(sj + 2);
       if (a.pool) {
         // pool[f] = mean over the S queries of O[i][f]: recompute O un-transposed (4 more
         // 16x16x16 MFMAs, one tile live at a time) so the column sum is 4 adds + 2 shuffles per
@@ -605,6 +651,7 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (base + stride < npairs) build_x(it ^ 1, base + stride);
     }
+    stamp(sj + 3);
     __syncthreads();  // (the next iteration writes the other buffer)
     const int i = lane >> 2, q = (lane & 3) * 4, w = wave * a.Hl;
     const int prw = base + w;
@@ -639,8 +686,10 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           m[r] = i < S ? v[r] : 0.f;
-          m[r] += __shfl_xor(m[r], 4);
-          m[r] += __shfl_xor(m[r], 8);
+          // the row's 4 tokens of this class group (lanes 4 apart in a 16-lane row) by DPP row
+          // rotations of 4, 8 and 12 (the other three, whichever way the rotation runs), not a
+          // ds_bpermute round trip per __shfl_xor
+          m[r] = ((m[r] + row_ror<4>(m[r])) + row_ror<12>(m[r])) + row_ror<8>(m[r]);
           m[r] = pair32_sum(pair16_sum(m[r]));
         }
         if (i == 0) {
@@ -649,6 +698,7 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
         }
       }
     }
+    stamp(sj + 4);
    }
    if (!QKV && a.zp) {  // sum the Hl heads of each sequence in rank order (deterministic) and add the bias
     __syncthreads();  // (the next iteration writes the other buffer: one barrier per iteration)
@@ -667,6 +717,13 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
     if (a.fold_out && !a.fold_at_start) {
       __syncthreads();
       fold_tail(a, &imgs[0][0]);
+    }
+  }
+  if constexpr (QKV) {
+    if (tsr) {
+      stamp(kTStamps - 1);
+      __builtin_amdgcn_wave_barrier();
+      if (lane < kTStamps) a.tstamp[((size_t)blockIdx.x * WPB + wave) * kTStamps + lane] = tsb[wave][lane];
     }
   }
 }

@@ -284,9 +284,9 @@ void attn_qkv_fwd(uint64_t xq, int ld_xq, int kq, uint64_t wq, int ld_wq, uint64
                   int ld_wo, int n_out, uint64_t bo, uint64_t ztok, int ld_zt, int zrows,
                   const std::vector<uint64_t>& zpush, uint64_t stream, uint64_t img, uint64_t xq_out, uint64_t zmean,
                   int ld_zmean, uint64_t fold_wq, int ld_fold_wq, uint64_t fold_we, int ld_fold_we, uint64_t fold_out,
-                  int ld_fold_out, int fold_R, int fold_d) {
+                  int ld_fold_out, int fold_R, int fold_d, uint64_t tstamp) {
   if (S < 1 || S > 16 || !(D == 32 || D == 64) || Hl < 1 || 4 % Hl || kq < 8 || kq > 72 || kq % 8 || ld_xq % 8 ||
-      ld_wq % 8 || ld_wo % 8 || (xq % 16) || (wq % 16) || (wo % 16) || !wo || !bq || (bq % 16) || !lse || n_out < 1 ||
+      ld_wq % 8 || ld_wo % 8 || (xq % 16) || (wq % 16) || (wo % 16) || !wo || !bq || (bq % 16) || n_out < 1 ||
       n_out > 16 ||
       ld_zt < 16 || ld_zt % 4 || (ztok % 16) || (!ztok && !zrows && !zmean) || (qkv_out && (ld_qkv % 8 || qkv_out % 16)) ||
       (zmean && (zmean % 16 || ld_zmean % 4 || ld_zmean < 16 || zrows)) ||
@@ -303,7 +303,8 @@ void attn_qkv_fwd(uint64_t xq, int ld_xq, int kq, uint64_t wq, int ld_wq, uint64
     throw std::invalid_argument("attention: the fold tail needs image mode, fp32 Wq [R][d] (16-B aligned, d % 4 == 0, "
                                 "d <= 1024) and We [d][kq], and an output other than the W_eff being read");
   AttnArgs a{};
-  a.lse = (float*)lse;
+  a.lse = (float*)lse;  // null: not stored (an inference forward: only a backward reads it)
+  a.tstamp = (unsigned long long*)tstamp;
   a.B = B; a.S = S; a.Hl = Hl; a.D = D; a.ld_qkv = ld_qkv; a.scale = scale;
   a.pool = (uint16_t*)pool; a.ld_pool = ld_pool;
   a.wo = (const uint16_t*)wo; a.ld_wo = ld_wo; a.n_out = n_out; a.bo = (const float*)bo;
@@ -641,7 +642,7 @@ void register_attn_ops(pybind11::module_& m) {
         py::arg("stream"), py::arg("img") = 0, py::arg("xq_out") = 0, py::arg("zmean") = 0, py::arg("ld_zmean") = 16,
         py::arg("fold_wq") = 0, py::arg("ld_fold_wq") = 0, py::arg("fold_we") = 0, py::arg("ld_fold_we") = 0,
         py::arg("fold_out") = 0, py::arg("ld_fold_out") = 0, py::arg("fold_R") = 0, py::arg("fold_d") = 0,
-        py::call_guard<py::gil_scoped_release>());
+        py::arg("tstamp") = 0, py::call_guard<py::gil_scoped_release>());
   m.def("attn_small_bwd", &attn_bwd, py::arg("qkv"), py::arg("o"), py::arg("lse"), py::arg("dout"), py::arg("dqkv"),
         py::arg("dbias"), py::arg("B"), py::arg("S"), py::arg("Hl"), py::arg("D"), py::arg("ld_qkv"), py::arg("ld_o"),
         py::arg("scale"), py::arg("dout_bstride"), py::arg("dout_rstride"), py::arg("stream"), py::arg("dz") = 0,

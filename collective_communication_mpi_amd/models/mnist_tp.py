@@ -699,7 +699,8 @@ class MnistTPLayer:
                                fold_R=fwq.shape[0], fold_d=fwq.shape[1])
                 D.attn_qkv_fwd(0 if img is not None else xp.data_ptr(), xp.stride(0), cfg.kp, weff.data_ptr(),
                                weff.stride(0), bq.data_ptr(), qkv.data_ptr() if keep else 0, qkv.stride(0),
-                               lse.data_ptr(), B, S, self.hl, cfg.head_dim, 1.0 / math.sqrt(cfg.head_dim),
+                               lse.data_ptr() if keep else 0,  # lse: only a backward reads it
+                               B, S, self.hl, cfg.head_dim, 1.0 / math.sqrt(cfg.head_dim),
                                pool.data_ptr() if keep else 0, pool.stride(0),  # pool: only the backward reads it
                                wo, ld_wo, n_out, bo, ztok, ld_zt, zrows, list(zpush),
                                stream, img=0 if img is None else img.data_ptr(),
