@@ -34,7 +34,8 @@ def trace_phases(fused, mode, train, mean, cap, npairs):
     mode: after the DMA wait and the next X build), +4 epilogue stored; 31 kernel end."""
     import numpy as np
 
-    waves = min(cap, (npairs + 3) // 4) * 4
+    nw = 8  # waves per workgroup of k_qkv_attn16_fwd (attn_mfma.hip kQkvWaves)
+    waves = min(cap, (npairs + nw - 1) // nw) * nw
     ts = torch.zeros(waves * 32, dtype=torch.int64, device="cuda")
     fused(mode, train, mean, ts.data_ptr())()
     torch.cuda.synchronize()
@@ -73,6 +74,8 @@ def main():
     ap.add_argument("--grid", type=int, default=0, help="only this persistent grid size")
     ap.add_argument("--train", type=int, default=-1, help="0/1: only inference / training stores")
     ap.add_argument("--nolse", action="store_true", help="inference without the lse store (lse = null)")
+    ap.add_argument("--fold", action="store_true",
+                    help="image mode also folds the next W_eff in-kernel (the pipelined plan's fold tail, d = 768)")
     ap.add_argument("--trace", action="store_true",
                     help="one extra launch with phase stamps (AttnArgs.tstamp): per-phase shader-clock medians")
     args = ap.parse_args()
@@ -98,8 +101,15 @@ def main():
                   zrows=0, zpush=[], stream=st, ld_xq=kp, kq=kp, wq=w.data_ptr(), ld_wq=w.stride(0), bq=bq.data_ptr(),
                   ld_qkv=qkv.stride(0))
 
+    wq32 = torch.randn(3 * HD, 768, device="cuda", generator=g) / 768 ** 0.5
+    we32 = torch.randn(768, kp, device="cuda", generator=g) / 8
+    wnext = torch.empty(3 * HD, kp, device="cuda", dtype=torch.bfloat16)
+
     def fused(mode, train, mean, tstamp=0):
         kw = dict(common)
+        if args.fold and mode == "img":
+            kw.update(fold_wq=wq32.data_ptr(), ld_fold_wq=768, fold_we=we32.data_ptr(), ld_fold_we=kp,
+                      fold_out=wnext.data_ptr(), ld_fold_out=kp, fold_R=3 * HD, fold_d=768)
         if args.nolse and not train:
             kw["lse"] = 0
         if tstamp:
@@ -127,7 +137,8 @@ def main():
                     if args.only and args.only != mode:
                         continue
                     rows.append(dict(kernel="fused", mode=mode, train=train, mean=mean, grid=cap,
-                                     us=timed(fused(mode, train, mean), args.iters), nolse=args.nolse))
+                                     us=timed(fused(mode, train, mean), args.iters), nolse=args.nolse,
+                                     fold=bool(args.fold and mode == "img")))
                     if args.trace:
                         rows[-1]["phases"] = trace_phases(fused, mode, train, mean, cap, B * H)
     dev.attn_set_qkv_grid(0)

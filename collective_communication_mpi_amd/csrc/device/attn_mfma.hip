@@ -159,7 +159,10 @@ __device__ __forceinline__ void rows_out(const uint16_t* T, uint16_t* dst, int l
 // partial tiles summed in slice order in LDS: bitwise that kernel's output, without its launch.
 constexpr int kFoldSlices = 16, kFoldMaxJ = 4;
 
+template <int NW>
 __device__ __forceinline__ void fold_tail(const AttnArgs& a, float* part /* >= 16 * 16 * 17 floats of LDS */) {
+  constexpr int SPW = kFoldSlices / NW;  // K slices per wave (4 waves: 4, 8 waves: 2)
+  static_assert(SPW % 2 == 0 && SPW * NW == kFoldSlices, "fold_tail: 4 or 8 waves");
   typedef float f4v __attribute__((ext_vector_type(4)));
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
   const int R = a.fold_R, d = a.fold_d, kp = a.fold_kp;
@@ -173,12 +176,12 @@ __device__ __forceinline__ void fold_tail(const AttnArgs& a, float* part /* >= 1
     const float* arow = a.fold_wq + (size_t)(rok ? r0 + c : 0) * a.ld_fold_wq;
     // two slices' operands at a time (all four at once would take 128 VGPRs and spill)
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
+    for (int h = 0; h < SPW / 2; ++h) {
       float4 a4[2][kFoldMaxJ];
       float b[2][kFoldMaxJ][4];
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
-        const int j0 = (4 * wave + 2 * h + s) * per;
+        const int j0 = (SPW * wave + 2 * h + s) * per;
 #pragma unroll
         for (int u = 0; u < kFoldMaxJ; ++u) {
           const int k = 16 * (j0 + u) + 4 * g;
@@ -199,13 +202,13 @@ __device__ __forceinline__ void fold_tail(const AttnArgs& a, float* part /* >= 1
           acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[s][u].w, b[s][u][3], acc, 0, 0, 0);
         }
 #pragma unroll
-        for (int r = 0; r < 4; ++r) part[((4 * wave + 2 * h + s) * 16 + 4 * g + r) * 17 + c] = acc[r];
+        for (int r = 0; r < 4; ++r) part[((SPW * wave + 2 * h + s) * 16 + 4 * g + r) * 17 + c] = acc[r];
       }
     }
     __syncthreads();
     {
-      const int r = threadIdx.x >> 4, cc = threadIdx.x & 15;  // 256 threads: one output each
-      if (r0 + r < R && c0 + cc < kp) {
+      const int r = threadIdx.x >> 4, cc = threadIdx.x & 15;  // the first 256 threads: one output each
+      if (threadIdx.x < 256 && r0 + r < R && c0 + cc < kp) {
         float sum = 0.f;
 #pragma unroll
         for (int w = 0; w < kFoldSlices; ++w) sum += part[(w * 16 + r) * 17 + cc];
@@ -216,28 +219,40 @@ __device__ __forceinline__ void fold_tail(const AttnArgs& a, float* part /* >= 1
   }
 }
 
-template <int D, bool QKV, bool IMG = false>
+template <int D, bool QKV, bool IMG = false, int NW = WPB>
 __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
   constexpr int LD = D + 8, NK = D / 32, NT = D / 16;
-  __shared__ __attribute__((aligned(16))) uint16_t vt[WPB][16 * LD];
-  __shared__ __attribute__((aligned(16))) uint16_t ot[WPB][16 * LD];
-  __shared__ float zpart[2][WPB][16];  // fused fc_o: per-wave (= per-head) partial logits, double-buffered
-  // per-token fused fc_o: per-wave (= per-head) z tiles [16 tokens][16 classes], double-buffered
-  __shared__ float ztp[2][WPB][16 * 16];
-  // fused patchify: the WPB / Hl images of an iteration (consecutive in memory), double-buffered
-  // and padded to whole 1-KiB LDS-DMA pieces
-  constexpr int kImgPieces = (WPB * 784 * 4 + 1023) / 1024;
-  __shared__ __attribute__((aligned(16))) float imgs[IMG ? 2 : 1][IMG ? kImgPieces * 256 : 1];
-  static_assert(!IMG || 2 * kImgPieces * 256 >= 16 * 16 * 17, "fold_tail reuses the image buffers");
-  // ... and their patch rows X (bf16, 80 columns + pad), built ONCE per sequence by the whole
-  // workgroup (not once per head), double-buffered
+  // One LDS block carved into the kernel's buffers; the per-wave V / O tiles and the X tiles come
+  // first and back to back, so the prologue can stage W_h through all three at once.
+  //   vt, ot  [NW][16 * LD] bf16: per-wave V^T / O tiles
+  //   xs      [2][NW][16 * LDX] bf16 (fused QKV): the iteration's patch rows X, double-buffered
+  //   zpart   [2][NW][16] fp32: fused pooled fc_o partial logits, double-buffered
+  //   ztp     [2][NW][16 * 16] fp32: per-token fused fc_o z tiles per head, double-buffered
+  //   imgs    [2][kImgPieces * 256] fp32 (image mode): the NW / Hl images of an iteration,
+  //           double-buffered, padded to whole 1-KiB LDS-DMA pieces
+  //   tsb     [NW][kTStamps] u64: diagnostic phase stamps
   constexpr int LDX = 88;
-  __shared__ __attribute__((aligned(16))) uint16_t xs[IMG ? 2 : 1][IMG ? WPB : 1][IMG ? 16 * LDX : 1];
+  constexpr int kImgPieces = (NW * 784 * 4 + 1023) / 1024;
+  constexpr int kVt = NW * 16 * LD * 2, kXs = QKV ? 2 * NW * 16 * LDX * 2 : 0;
+  constexpr int kZpart = 2 * NW * 16 * 4, kZtp = 2 * NW * 256 * 4;
+  constexpr int kImgs = IMG ? 2 * kImgPieces * 1024 : 0, kTsb = QKV ? NW * kTStamps * 8 : 0;
+  constexpr int oVt = 0, oOt = oVt + kVt, oXs = oOt + kVt, oZpart = oXs + kXs, oZtp = oZpart + kZpart,
+                oImgs = oZtp + kZtp, oTsb = oImgs + kImgs, kSmem = oTsb + kTsb;
+  constexpr int kStageBytes = oZpart;  // vt | ot | xs: W_h's staging room in the prologue
+  static_assert(oXs % 16 == 0 && oImgs % 16 == 0 && oTsb % 16 == 0, "16-B aligned LDS carve");
+  __shared__ __attribute__((aligned(16))) char smem[kSmem];
+  auto vt = reinterpret_cast<uint16_t(*)[16 * LD]>(smem + oVt);
+  auto ot = reinterpret_cast<uint16_t(*)[16 * LD]>(smem + oOt);
+  auto xs = reinterpret_cast<uint16_t(*)[NW][16 * LDX]>(smem + oXs);
+  auto zpart = reinterpret_cast<float(*)[NW][16]>(smem + oZpart);
+  auto ztp = reinterpret_cast<float(*)[NW][16 * 16]>(smem + oZtp);
+  auto imgs = reinterpret_cast<float(*)[kImgPieces * 256]>(smem + oImgs);
+  static_assert(!IMG || 2 * kImgPieces * 256 >= 16 * 16 * 17, "fold_tail reuses the image buffers");
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
   const int S = a.S, HD = a.Hl * D, npairs = a.B * a.Hl;
   const float inv_s = 1.f / (float)S;  // (fused path: means as multiplies)
   // diagnostic phase stamps (a.tstamp): shader clock per phase, lane 0 of each wave, into LDS
-  __shared__ unsigned long long tsb[QKV ? WPB : 1][QKV ? kTStamps : 1];
+  auto tsb = reinterpret_cast<unsigned long long(*)[kTStamps]>(smem + oTsb);
   const bool tsr = QKV && a.tstamp != nullptr;
   auto stamp = [&](int k) {
     if constexpr (QKV) {
@@ -260,8 +275,8 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
   uint16_t* V = vt[wave];
   uint16_t* O = ot[wave];
   // workgroup-uniform trip count (the fused fc_o reduces across the waves of an iteration);
-  // with Hl | WPB the Hl heads of a sequence are consecutive waves of one workgroup
-  // fused fc_o: with Hl | WPB this wave always serves head h = wave % Hl, so its W_o
+  // with Hl | NW the Hl heads of a sequence are consecutive waves of one workgroup
+  // fused fc_o: with Hl | NW this wave always serves head h = wave % Hl, so its W_o
   // entries (classes 4g..4g+3, features 16nt + c) are loaded once, packed as bf16 pairs
   uint32_t wpk[NT][2];
   if (!QKV && a.zp) {
@@ -295,11 +310,11 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
         wb[kk] = ld_row16(a.wo + (size_t)c * a.ld_wo + hw * D + 32 * kk + 8 * g, c < a.n_out);
     }
   }
-  const int stride = gridDim.x * WPB;
+  const int stride = gridDim.x * NW;
   if constexpr (QKV && IMG) {
     // the next forward's weight fold before any image is staged (imgs is free), its operand
     // loads in flight with W_h's fragment loads below
-    if (a.fold_out && a.fold_at_start) fold_tail(a, &imgs[0][0]);
+    if (a.fold_out && a.fold_at_start) fold_tail<NW>(a, &imgs[0][0]);
   }
   // the fc_o bias of this lane's epilogue classes (4 (lane & 3) .. +3), loaded once (the
   // compiler cannot hoist it past the loop's global stores)
@@ -344,12 +359,12 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
   // global memory into LDS, no VGPRs held; bytes past the batch read as zero (buffer bounds)
   auto stage_imgs = [&](int buf, int p0) {
     if constexpr (IMG) {
-      const int nseq = div_hl(WPB), pieces = (nseq * 784 * 4 + 1023) / 1024;
+      const int nseq = div_hl(NW), pieces = (nseq * 784 * 4 + 1023) / 1024;
       // (the descriptor starts at the iteration's first image: the bounds check covers
       // voffset, so the batch end clips exactly)
       const int b0 = div_hl(p0);
       const Rsrc rs = make_rsrc(uniform_ptr(reinterpret_cast<char*>(const_cast<float*>(a.img + (size_t)b0 * 784))), (uint32_t)((size_t)(a.B - b0) * 784 * 4));
-      for (int pc = wave; pc < pieces; pc += WPB)
+      for (int pc = wave; pc < pieces; pc += NW)
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rs.r, (__attribute__((address_space(3))) void*)(imgs[buf] + pc * 256),
                                                  16, (pc * 64 + lane) * 16, 0, 0, 0);
     }
@@ -361,8 +376,8 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
   // position one-hot, the rest zero (the QKV bias columns are set in load_x)
   auto build_x = [&](int buf, int p0) {
     if constexpr (IMG) {
-      const int nseq = div_hl(WPB);
-      for (int id = threadIdx.x; id < nseq * 160; id += WPB * 64) {
+      const int nseq = div_hl(NW);
+      for (int id = threadIdx.x; id < nseq * 160; id += NW * 64) {
         const int sq = id / 160, rem = id - sq * 160, t = rem / 10, ch = rem - t * 10;
         const float* im = imgs[buf] + sq * 784 + (t >> 2) * 196 + (t & 3) * 7;
         // pixel (pr, pc) of column 8 ch, stepped along the chunk; every lane reads (a clamped
@@ -373,7 +388,9 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
         for (int j = 0; j < 8; ++j) {
           const int cc = 8 * ch + j;
           const float px = im[cc < 49 ? pr * 28 + pc : 0];
-          v[j] = cc < 49 ? px : ((cc == 49 || cc == 50 + t) ? 1.f : 0.f);
+          // px * 1 + 0 or px * 0 + (0 | 1): the load's value is always used, so the compiler
+          // keeps it unconditional (a select let it sink the read into a branch per column)
+          v[j] = fmaf(px, cc < 49 ? 1.f : 0.f, (cc == 49 || cc == 50 + t) ? 1.f : 0.f);
           const bool wrap = pc == 6;
           pc = wrap ? 0 : pc + 1;
           pr += wrap ? 1 : 0;
@@ -386,6 +403,11 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
   };
   if constexpr (QKV) {
     const int hw = mod_hl(wave);
+    if constexpr (IMG) {
+      const int p0 = blockIdx.x * NW;
+      stage_imgs(0, p0);
+      if (p0 + stride < npairs) stage_imgs(1, p0 + stride);
+    }
     // every load first (the bias by every lane, unconditionally), every use after: a bias load
     // inside `g == gb` whose value was consumed at once (and the partial overwrite of a tail
     // fragment still being loaded) made the prologue 12 serialised global round trips --
@@ -394,15 +416,57 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
 #pragma unroll
     for (int sel = 0; sel < 3; ++sel)
 #pragma unroll
-      for (int nt = 0; nt < NT; ++nt) {
-        const int f = sel * HD + hw * D + 16 * nt + c;
-        const uint16_t* w = a.wq + (size_t)f * a.ld_wq;
-        wf[sel][nt][0] = ld_row16(w + 8 * g, 8 * g < a.kq);
-        wf[sel][nt][1] = ld_row16(w + 32 + 8 * g, 32 + 8 * g < a.kq);
-        wtl[sel][nt] = ld_s4(w + 64 + 4 * g, 64 + 4 * g < a.kq);
-        bqv[sel][nt] = a.bq[f];
+      for (int nt = 0; nt < NT; ++nt) bqv[sel][nt] = a.bq[sel * HD + hw * D + 16 * nt + c];
+    // W_h staged ONCE per workgroup: the wave reading it from global memory itself made every
+    // wave of the grid pull its head's 27.6 KiB through L2 at the same moment (57 MiB at
+    // B = 2048: 9-12 k shader clocks of issue stalls per wave before any work, a third of the
+    // kernel, profiles/r6_attn).  Per projection (q, k, v) the Hl local heads' rows -- one
+    // contiguous HD x 144-B block when ld_wq = 72 -- go into the X tiles' LDS by LDS-DMA and every
+    // wave reads its fragments from there: the grid's L2 traffic for W falls by the waves per
+    // head of a workgroup (NW / Hl: 4 at TP = 2, 2 at TP = 1).
+    const int selb = HD * 144;  // one projection's rows of every local head (ld_wq = 72)
+    if (a.ld_wq == 72 && selb <= kStageBytes) {
+      char* stg = smem + oVt;
+      // as many projections per round as the V / O / X tiles hold: TP = 2 (HD = 128) all three at
+      // once, TP = 1 (HD = 256) q | k then v -- every round one LDS-DMA latency and two barriers
+      const int per_round = kStageBytes / selb;
+      int done = 0, r0 = 0;  // end of the staged projections, first projection of the round
+#pragma unroll
+      for (int sel = 0; sel < 3; ++sel) {
+        if (sel == done) {  // issue the round starting at this projection
+          const int nsel = min(per_round, 3 - sel), bytes = nsel * selb, pieces = (bytes + 1023) / 1024;
+          const Rsrc rs = make_rsrc(uniform_ptr(reinterpret_cast<char*>(const_cast<uint16_t*>(a.wq + (size_t)sel * HD * 72))),
+                                    (uint32_t)bytes);
+          for (int pc = wave; pc < pieces; pc += NW)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs.r, (__attribute__((address_space(3))) void*)(stg + pc * 1024), 16,
+                                                     (pc * 64 + lane) * 16, 0, 0, 0);
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          __syncthreads();
+          done = sel + nsel;
+          r0 = sel;
+        }
+        const int slot = sel - r0;  // this projection's block in the stage
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+          const uint16_t* row = reinterpret_cast<const uint16_t*>(stg + (size_t)slot * selb) + (size_t)(hw * D + 16 * nt + c) * 72;
+          wf[sel][nt][0] = 8 * g < a.kq ? *reinterpret_cast<const bf16x8*>(row + 8 * g) : bf16x8{};
+          wf[sel][nt][1] = 32 + 8 * g < a.kq ? *reinterpret_cast<const bf16x8*>(row + 32 + 8 * g) : bf16x8{};
+          wtl[sel][nt] = 64 + 4 * g < a.kq ? *reinterpret_cast<const s4*>(row + 64 + 4 * g) : s4{0, 0, 0, 0};
+        }
+        if (sel + 1 == done) __syncthreads();  // (the round's last projection read: the stage is free)
       }
-    stamp(24);  // every W_h load issued
+    } else {
+#pragma unroll
+      for (int sel = 0; sel < 3; ++sel)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+          const uint16_t* w = a.wq + (size_t)(sel * HD + hw * D + 16 * nt + c) * a.ld_wq;
+          wf[sel][nt][0] = ld_row16(w + 8 * g, 8 * g < a.kq);
+          wf[sel][nt][1] = ld_row16(w + 32 + 8 * g, 32 + 8 * g < a.kq);
+          wtl[sel][nt] = ld_s4(w + 64 + 4 * g, 64 + 4 * g < a.kq);
+        }
+    }
+    stamp(24);  // every W_h load issued (staged: and its fragments read back)
 #pragma unroll
     for (int sel = 0; sel < 3; ++sel)
 #pragma unroll
@@ -414,12 +478,11 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
         wtl[sel][nt][1] = g == gb ? lo : wtl[sel][nt][1];
       }
     stamp(25);  // W_h's tail fragments and biases arrived
-    if constexpr (!IMG) load_x(blockIdx.x * WPB + wave);
+    if constexpr (!IMG) load_x(blockIdx.x * NW + wave);
     if constexpr (IMG) {
-      // images two iterations deep: the first two now, X of the first one built
-      const int p0 = blockIdx.x * WPB;
-      stage_imgs(0, p0);
-      if (p0 + stride < npairs) stage_imgs(1, p0 + stride);
+      // images two iterations deep: the first two (their DMA issued before W_h's), X of the
+      // first one built
+      const int p0 = blockIdx.x * NW;
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       stamp(26);  // every W_h load and both images' DMA landed
       __syncthreads();
@@ -429,7 +492,7 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
     }
   }
   stamp(1);
-  for (int base = blockIdx.x * WPB; base < npairs; base += stride, it ^= 1, ++itn) {
+  for (int base = blockIdx.x * NW; base < npairs; base += stride, it ^= 1, ++itn) {
    const int pr = base + wave;
    const int sj = itn < 4 ? 2 + 5 * itn : kTStamps;  // this iteration's stamp slots
    bf16x8 xr[2];
@@ -640,8 +703,8 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
     }  // !QKV
    }
    if (tok) {
-    // the Hl heads of each sequence of this iteration (consecutive waves, Hl | WPB), summed in
-    // head order, + the bias.  Wave s writes sequence s (waves s >= WPB / Hl idle): lane l =
+    // the Hl heads of each sequence of this iteration (consecutive waves, Hl | NW), summed in
+    // head order, + the bias.  Wave s writes sequence s (waves s >= NW / Hl idle): lane l =
     // (token l >> 2, classes 4 (l & 3) .. +3), one 16-B store per lane, a sequence's S x 16
     // fp32 rows as whole lines
     if constexpr (IMG) {
@@ -655,7 +718,7 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
     __syncthreads();  // (the next iteration writes the other buffer)
     const int i = lane >> 2, q = (lane & 3) * 4, w = wave * a.Hl;
     const int prw = base + w;
-    if (w < WPB && prw < npairs) {
+    if (w < NW && prw < npairs) {
       const int b = div_hl(prw);
       float v[4];
 #pragma unroll
@@ -703,7 +766,7 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
    if (!QKV && a.zp) {  // sum the Hl heads of each sequence in rank order (deterministic) and add the bias
     __syncthreads();  // (the next iteration writes the other buffer: one barrier per iteration)
     const int t = threadIdx.x, w = t >> 4, cls = t & 15, prw = base + w;
-    if (t < WPB * 16 && prw < npairs && mod_hl(prw) == 0 && cls < a.n_out) {
+    if (t < NW * 16 && prw < npairs && mod_hl(prw) == 0 && cls < a.n_out) {
       float acc = 0.f;
       for (int k = 0; k < a.Hl; ++k) acc += zpart[it][w + k][cls];
       if (a.bo) acc += a.bo[cls];
@@ -716,14 +779,14 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
     // trip ends with vmcnt(0) and a barrier, and the trip count is workgroup-uniform)
     if (a.fold_out && !a.fold_at_start) {
       __syncthreads();
-      fold_tail(a, &imgs[0][0]);
+      fold_tail<NW>(a, &imgs[0][0]);
     }
   }
   if constexpr (QKV) {
     if (tsr) {
       stamp(kTStamps - 1);
       __builtin_amdgcn_wave_barrier();
-      if (lane < kTStamps) a.tstamp[((size_t)blockIdx.x * WPB + wave) * kTStamps + lane] = tsb[wave][lane];
+      if (lane < kTStamps) a.tstamp[((size_t)blockIdx.x * NW + wave) * kTStamps + lane] = tsb[wave][lane];
     }
   }
 }
@@ -735,9 +798,12 @@ __global__ void __launch_bounds__(256) k_attn16_fwd(AttnArgs a) {
 }
 
 // two workgroups (8 waves) per CU: <= 256 VGPRs, W_h's fragments included
+// One workgroup of kQkvWaves waves per CU (two per SIMD): <= 256 VGPRs a wave, W_h's fragments
+// included; the waves of a workgroup share its staged W_h (see attn16_fwd_body).
+constexpr int kQkvWaves = 8;
 template <int D, bool IMG>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) k_qkv_attn16_fwd(AttnArgs a) {
-  attn16_fwd_body<D, true, IMG>(a);
+__global__ void __launch_bounds__(64 * kQkvWaves) __attribute__((amdgpu_waves_per_eu(2))) k_qkv_attn16_fwd(AttnArgs a) {
+  attn16_fwd_body<D, true, IMG, kQkvWaves>(a);
 }
 
 template <int D>
@@ -900,7 +966,7 @@ constexpr size_t bwd_lds_bytes() {
   return (size_t)WPB * 4 * 16 * (D + 8) * sizeof(uint16_t);
 }
 
-int grid_for(int npairs, int cap) { return std::max(1, std::min((npairs + WPB - 1) / WPB, cap)); }
+int grid_for(int npairs, int cap, int nw = WPB) { return std::max(1, std::min((npairs + nw - 1) / nw, cap)); }
 
 }  // namespace
 
@@ -918,17 +984,19 @@ void launch_fwd_mfma(const AttnArgs& a, hipStream_t stream) {
   else hipLaunchKernelGGL(k_attn16_fwd<128>, dim3(grid), dim3(256), 0, stream, a);
 }
 
-// persistent: two workgroups per CU (W_h loaded once per wave); attn_set_qkv_grid / CCMPI_QKV_GRID
-int g_qkv_grid_cap = std::getenv("CCMPI_QKV_GRID") ? std::atoi(std::getenv("CCMPI_QKV_GRID")) : 512;
+// persistent: one 8-wave workgroup per CU (W_h staged once per workgroup, held in registers by
+// every wave); attn_set_qkv_grid / CCMPI_QKV_GRID
+int g_qkv_grid_cap = std::getenv("CCMPI_QKV_GRID") ? std::atoi(std::getenv("CCMPI_QKV_GRID")) : 256;
 
 void launch_qkv_fwd_mfma(const AttnArgs& a, hipStream_t stream) {
-  const int grid = grid_for(a.B * a.Hl, g_qkv_grid_cap);
+  const int grid = grid_for(a.B * a.Hl, g_qkv_grid_cap, kQkvWaves);
+  const dim3 block(64 * kQkvWaves);
   if (a.img) {
-    if (a.D == 32) hipLaunchKernelGGL((k_qkv_attn16_fwd<32, true>), dim3(grid), dim3(256), 0, stream, a);
-    else hipLaunchKernelGGL((k_qkv_attn16_fwd<64, true>), dim3(grid), dim3(256), 0, stream, a);
+    if (a.D == 32) hipLaunchKernelGGL((k_qkv_attn16_fwd<32, true>), dim3(grid), block, 0, stream, a);
+    else hipLaunchKernelGGL((k_qkv_attn16_fwd<64, true>), dim3(grid), block, 0, stream, a);
   } else {
-    if (a.D == 32) hipLaunchKernelGGL((k_qkv_attn16_fwd<32, false>), dim3(grid), dim3(256), 0, stream, a);
-    else hipLaunchKernelGGL((k_qkv_attn16_fwd<64, false>), dim3(grid), dim3(256), 0, stream, a);
+    if (a.D == 32) hipLaunchKernelGGL((k_qkv_attn16_fwd<32, false>), dim3(grid), block, 0, stream, a);
+    else hipLaunchKernelGGL((k_qkv_attn16_fwd<64, false>), dim3(grid), block, 0, stream, a);
   }
 }
 

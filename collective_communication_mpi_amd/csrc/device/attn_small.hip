@@ -625,7 +625,7 @@ void register_attn_ops(pybind11::module_& m) {
         pybind11::arg("ld_z"), pybind11::arg("out"), pybind11::arg("ld_out"), pybind11::arg("groups"),
         pybind11::arg("S"), pybind11::arg("ncol"), pybind11::arg("stream"),
         pybind11::call_guard<pybind11::gil_scoped_release>());
-  m.def("attn_set_qkv_grid", [](int cap) { attn::g_qkv_grid_cap = cap > 0 ? cap : 512; },
+  m.def("attn_set_qkv_grid", [](int cap) { attn::g_qkv_grid_cap = cap > 0 ? cap : 256; },
         "workgroups of the fused QKV forward (default 512: two per CU)", pybind11::arg("cap"));
   m.def("attn_set_bwd_grid", [](int cap) { attn::g_bwd_grid_cap = cap > 0 ? cap : 0; },
         "backward kernel grid cap (tuning)");
