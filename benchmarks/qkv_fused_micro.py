@@ -44,7 +44,8 @@ def trace_phases(fused, mode, train, mean, cap, npairs):
     out = {"waves": int(len(t)), "prologue": int(np.median(t[:, 1] - t[:, 0]))}
     # inside the prologue: 24 W_h loads issued, 25 tail fragments + biases in, 26 (image mode)
     # every load and both images' DMA in, 27 first X built
-    pro = {"w_issue": (0, 24), "w_arrive": (24, 25), "dma_wait": (25, 26), "build_x0": (26, 27), "to_loop": (27, 1)}
+    pro = {"w_issue": (0, 24), "w_arrive": (24, 25), "dma_wait": (25, 26), "build_x0": (26, 27), "to_loop": (27, 1),
+           "first_loads": (0, 28), "w_dma": (28, 29), "w_frags": (29, 24)}
     out["prologue_parts"] = {k: int(np.median(t[:, b] - t[:, a])) for k, (a, b) in pro.items()
                              if (t[:, a] != 0).all() and (t[:, b] != 0).all()}
     names = ["proj", "attn_z", "dma_wait_build", "barrier_epilogue", "to_next"]

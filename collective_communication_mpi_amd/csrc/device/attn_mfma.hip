@@ -239,6 +239,7 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
   constexpr int oVt = 0, oOt = oVt + kVt, oXs = oOt + kVt, oZpart = oXs + kXs, oZtp = oZpart + kZpart,
                 oImgs = oZtp + kZtp, oTsb = oImgs + kImgs, kSmem = oTsb + kTsb;
   constexpr int kStageBytes = oZpart;  // vt | ot | xs: W_h's staging room in the prologue
+  static_assert(!QKV || kStageBytes >= 16 * 16 * 17 * 4, "the fold tail's partial tiles fit the stage");
   static_assert(oXs % 16 == 0 && oImgs % 16 == 0 && oTsb % 16 == 0, "16-B aligned LDS carve");
   __shared__ __attribute__((aligned(16))) char smem[kSmem];
   auto vt = reinterpret_cast<uint16_t(*)[16 * LD]>(smem + oVt);
@@ -262,6 +263,17 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
       }
     }
   };
+  if constexpr (QKV) {
+    // Touch every 64-B line of the argument block at once.  The prologue's argument reads are
+    // spread over branches (fc_o bias, fold, image mode, ...), so the compiler waits on them in
+    // ~10 batches; when the block is not in the scalar cache each batch was a full round trip to
+    // the kernarg segment before any real work (profiles/r6_attn).  One round trip instead.
+    const uint32_t __attribute__((address_space(4)))* kp =
+        (const uint32_t __attribute__((address_space(4)))*)__builtin_amdgcn_kernarg_segment_ptr();
+    static_assert(sizeof(AttnArgs) <= 8 * 64, "kernarg touch: 8 lines");
+    asm volatile("" ::"s"(kp[0]), "s"(kp[16]), "s"(kp[32]), "s"(kp[48]), "s"(kp[64]), "s"(kp[80]), "s"(kp[96]),
+                 "s"(kp[112]));
+  }
   if (tsr && lane < kTStamps) tsb[wave][lane] = 0ull;  // (slots a short wave never reaches read 0)
   stamp(0);
   int itn = 0;  // iteration count (stamps 2 + 5 j .. 6 + 5 j, j < 4)
@@ -311,11 +323,6 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
     }
   }
   const int stride = gridDim.x * NW;
-  if constexpr (QKV && IMG) {
-    // the next forward's weight fold before any image is staged (imgs is free), its operand
-    // loads in flight with W_h's fragment loads below
-    if (a.fold_out && a.fold_at_start) fold_tail<NW>(a, &imgs[0][0]);
-  }
   // the fc_o bias of this lane's epilogue classes (4 (lane & 3) .. +3), loaded once (the
   // compiler cannot hoist it past the loop's global stores)
   float bov[4];
@@ -408,15 +415,17 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
       stage_imgs(0, p0);
       if (p0 + stride < npairs) stage_imgs(1, p0 + stride);
     }
-    // every load first (the bias by every lane, unconditionally), every use after: a bias load
-    // inside `g == gb` whose value was consumed at once (and the partial overwrite of a tail
-    // fragment still being loaded) made the prologue 12 serialised global round trips --
-    // 13-16 k of the kernel's ~30 k shader clocks per wave (profiles/r6_attn, phase stamps)
+    // every load first (the bias by every lane, unconditionally), every use after
     float bqv[3][NT];
 #pragma unroll
     for (int sel = 0; sel < 3; ++sel)
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) bqv[sel][nt] = a.bq[sel * HD + hw * D + 16 * nt + c];
+    if constexpr (IMG) {
+      // the next forward's weight fold, its latency under the images' DMA issued above, its
+      // partial tiles in the V / O / X tiles (free until W_h is staged into them below)
+      if (a.fold_out && a.fold_at_start) fold_tail<NW>(a, reinterpret_cast<float*>(smem + oVt));
+    }
     // W_h staged ONCE per workgroup: the wave reading it from global memory itself made every
     // wave of the grid pull its head's 27.6 KiB through L2 at the same moment (57 MiB at
     // B = 2048: 9-12 k shader clocks of issue stalls per wave before any work, a third of the
@@ -434,6 +443,10 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
 #pragma unroll
       for (int sel = 0; sel < 3; ++sel) {
         if (sel == done) {  // issue the round starting at this projection
+          if (tsr && sel == 0) {  // (diagnostic only: the argument / bias / image loads alone)
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            stamp(28);
+          }
           const int nsel = min(per_round, 3 - sel), bytes = nsel * selb, pieces = (bytes + 1023) / 1024;
           const Rsrc rs = make_rsrc(uniform_ptr(reinterpret_cast<char*>(const_cast<uint16_t*>(a.wq + (size_t)sel * HD * 72))),
                                     (uint32_t)bytes);
@@ -441,6 +454,7 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
             __builtin_amdgcn_raw_ptr_buffer_load_lds(rs.r, (__attribute__((address_space(3))) void*)(stg + pc * 1024), 16,
                                                      (pc * 64 + lane) * 16, 0, 0, 0);
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          if (sel == 0) stamp(29);  // this wave's W_h DMA landed
           __syncthreads();
           done = sel + nsel;
           r0 = sel;
