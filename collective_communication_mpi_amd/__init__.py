@@ -16,7 +16,7 @@ import os as _os
 
 # Kernel arguments in device memory: every kernel's first argument fetch then comes from HBM /
 # L2 instead of the host-side kernarg pool.  Measured on the fused attention kernel (one launch
-# per forward step): 1.1-1.2 us less per launch (profiles/r6_attn/kernarg.md).  Read by the HIP
+# per forward step): 1.1-1.2 us less per launch (profiles/r6_attn/README.md).  Read by the HIP
 # runtime at its initialisation, so it must be set before the first GPU call; an explicit
 # setting wins.
 _os.environ.setdefault("HIP_FORCE_DEV_KERNARG", "1")

@@ -210,10 +210,11 @@ def bench_forward(comm, tp: int = 2, batch: int = 2048, steps: int = 20, warmup:
     used_graph = False
     g = None
     hazard = multi_stream_graph_hazard(cfg, layer) if graph else None
-    if graph and not hazard and _device.SHARED_GPU_IN_PROCESS and os.environ.get("CCMPI_FORCE_GRAPH") != "1":
+    if (graph and not hazard and _device.SHARED_GPU_IN_PROCESS
+            and "1" not in (os.environ.get("CCMPI_FORCE_GRAPH"), os.environ.get("CCMPI_SHARED_GRAPH"))):
         # ranks sharing one GPU (the dry run): their graph replays serialise on the one hardware
         # queue each -- 0.8-15 ms against 0.22 ms for the launch plan (profiles/r6_bind)
-        hazard = "ranks share one GPU: HIP graph replays serialise, not captured (CCMPI_FORCE_GRAPH=1 to force)"
+        hazard = "ranks share one GPU: HIP graph replays serialise, not captured (CCMPI_SHARED_GRAPH=1 to capture)"
     if hazard:
         say(hazard)
     if graph and not hazard and os.environ.get("CCMPI_NO_GRAPH") != "1":

@@ -61,7 +61,8 @@ def test_harness_graph_replay_after_collectives_one_queue():
     pipeline's graph is what crashed the HIP runtime (profiles/r4_bisect); it is timed eagerly
     under few queues, every other forward replays its graph."""
     r = run_ranks(8, py("benchmarks/graph_replay_repro.py", "--prefix", "ar,bf16,a2a,free", "--size-mb", "256",
-                        "--variants", "token:1,row:1,token:4"), timeout=400, env=dict(ENV, GPU_MAX_HW_QUEUES="1"))
+                        "--variants", "token:1,row:1,token:4"), timeout=400,
+                  env=dict(ENV, GPU_MAX_HW_QUEUES="1", CCMPI_SHARED_GRAPH="1"))  # capture despite sharing
     assert "replay OK" in r.stdout
     import json
 
