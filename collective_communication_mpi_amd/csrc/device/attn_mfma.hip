@@ -152,69 +152,93 @@ __device__ __forceinline__ void rows_out(const uint16_t* T, uint16_t* dst, int l
 // launch, its 2 x B*S x 3 Hl D x 2 B of qkv write + read, and the old per-head W staging
 // (one wave per sequence, two workgroup barriers per head: 38.9 us vs 23.1 + 17.0 us
 // unfused) are gone.
-// The weight fold W_eff = bf16(Wq . We) as the tail of the fused forward (AttnArgs fold_*):
-// one 16 x 16 output tile per workgroup and trip, the K axis cut into 16 slices exactly as
-// wgrad.hip's k_fold_mfma cuts it over its 16 waves -- here each of the 4 waves runs the MFMA
-// chains of 4 slices, two slices' operands in flight at a time -- and the 16
-// partial tiles summed in slice order in LDS: bitwise that kernel's output, without its launch.
-constexpr int kFoldSlices = 16, kFoldMaxJ = 4;
+constexpr int kFoldSlices = 16, kFoldMaxJ = 4;  // the weight fold's K slices (see fold_tail)
+
+// One 16 x 16 fold tile in three steps, so the fused kernel can put the operand loads in flight
+// with its own prologue loads and share its barriers: fold_issue (operands into registers: each
+// wave's K slices), fold_mma (the slices' MFMA chains -> partial tiles in LDS), fold_reduce (the
+// first 256 threads sum the 16 partials in slice order and store).
+template <int NW>
+struct FoldOps {
+  static constexpr int SPW = kFoldSlices / NW;  // K slices per wave (4 waves: 4, 8 waves: 2)
+  float4 a4[SPW][kFoldMaxJ];
+  float b[SPW][kFoldMaxJ][4];
+};
+
+__device__ __forceinline__ int fold_tiles(const AttnArgs& a) {
+  return ((a.fold_R + 15) / 16) * ((a.fold_kp + 15) / 16);
+}
 
 template <int NW>
-__device__ __forceinline__ void fold_tail(const AttnArgs& a, float* part /* >= 16 * 16 * 17 floats of LDS */) {
-  constexpr int SPW = kFoldSlices / NW;  // K slices per wave (4 waves: 4, 8 waves: 2)
-  static_assert(SPW % 2 == 0 && SPW * NW == kFoldSlices, "fold_tail: 4 or 8 waves");
-  typedef float f4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void fold_issue(const AttnArgs& a, int tile, FoldOps<NW>& f) {
+  constexpr int SPW = FoldOps<NW>::SPW;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
-  const int R = a.fold_R, d = a.fold_d, kp = a.fold_kp;
-  const int tiles_c = (kp + 15) / 16, ntiles = ((R + 15) / 16) * tiles_c;
+  const int R = a.fold_R, d = a.fold_d, kp = a.fold_kp, tiles_c = (kp + 15) / 16;
   const int nj = (d + 15) / 16, per = (nj + kFoldSlices - 1) / kFoldSlices;
+  const int r0 = (tile / tiles_c) * 16, col = (tile % tiles_c) * 16 + c;
+  const bool rok = r0 + c < R, cok = col < kp;
+  const float* arow = a.fold_wq + (size_t)(rok ? r0 + c : 0) * a.ld_fold_wq;
+#pragma unroll
+  for (int s = 0; s < SPW; ++s) {
+    const int j0 = (SPW * wave + s) * per;
+#pragma unroll
+    for (int u = 0; u < kFoldMaxJ; ++u) {
+      const int k = 16 * (j0 + u) + 4 * g;
+      const bool kok = u < per && k < d;
+      f.a4[s][u] = (rok && kok) ? *reinterpret_cast<const float4*>(arow + k) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) f.b[s][u][i] = (cok && kok) ? a.fold_we[(size_t)(k + i) * a.ld_fold_we + col] : 0.f;
+    }
+  }
+}
+
+template <int NW>
+__device__ __forceinline__ void fold_mma(const FoldOps<NW>& f, float* part /* 16 * 16 * 17 floats */) {
+  typedef float f4v __attribute__((ext_vector_type(4)));
+  constexpr int SPW = FoldOps<NW>::SPW;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
+#pragma unroll
+  for (int s = 0; s < SPW; ++s) {
+    f4v acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int u = 0; u < kFoldMaxJ; ++u) {
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(f.a4[s][u].x, f.b[s][u][0], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(f.a4[s][u].y, f.b[s][u][1], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(f.a4[s][u].z, f.b[s][u][2], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(f.a4[s][u].w, f.b[s][u][3], acc, 0, 0, 0);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) part[((SPW * wave + s) * 16 + 4 * g + r) * 17 + c] = acc[r];
+  }
+}
+
+__device__ __forceinline__ void fold_reduce(const AttnArgs& a, int tile, const float* part) {
+  const int tiles_c = (a.fold_kp + 15) / 16;
+  const int r0 = (tile / tiles_c) * 16, c0 = (tile % tiles_c) * 16;
+  const int r = threadIdx.x >> 4, cc = threadIdx.x & 15;  // the first 256 threads: one output each
+  if (threadIdx.x < 256 && r0 + r < a.fold_R && c0 + cc < a.fold_kp) {
+    float sum = 0.f;
+#pragma unroll
+    for (int w = 0; w < kFoldSlices; ++w) sum += part[(w * 16 + r) * 17 + cc];
+    a.fold_out[(size_t)(r0 + r) * a.ld_fold_out + c0 + cc] = static_cast<uint16_t>(f32_to_bf16_bits(sum));
+  }
+}
+
+// The weight fold W_eff = bf16(Wq . We) as the tail of the fused forward (AttnArgs fold_*): one
+// 16 x 16 output tile per workgroup and trip, the K axis cut into 16 slices exactly as wgrad.hip's
+// k_fold_mfma cuts it over its 16 waves, the 16 partial tiles summed in slice order in LDS:
+// bitwise that kernel's output, without its launch.  Tiles from `first` in steps of the grid.
+template <int NW>
+__device__ __forceinline__ void fold_tail(const AttnArgs& a, float* part /* >= 16 * 16 * 17 floats of LDS */,
+                                          int first = -1) {
   // (tiles from the last workgroup down measured 0.0237-0.0239 vs 0.0232-0.0233 ms per forward:
   // the first-dispatched workgroups take them)
-  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    const int r0 = (tile / tiles_c) * 16, c0 = (tile % tiles_c) * 16, col = c0 + c;
-    const bool rok = r0 + c < R, cok = col < kp;
-    const float* arow = a.fold_wq + (size_t)(rok ? r0 + c : 0) * a.ld_fold_wq;
-    // two slices' operands at a time (all four at once would take 128 VGPRs and spill)
-#pragma unroll
-    for (int h = 0; h < SPW / 2; ++h) {
-      float4 a4[2][kFoldMaxJ];
-      float b[2][kFoldMaxJ][4];
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const int j0 = (SPW * wave + 2 * h + s) * per;
-#pragma unroll
-        for (int u = 0; u < kFoldMaxJ; ++u) {
-          const int k = 16 * (j0 + u) + 4 * g;
-          const bool kok = u < per && k < d;
-          a4[s][u] = (rok && kok) ? *reinterpret_cast<const float4*>(arow + k) : make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-          for (int i = 0; i < 4; ++i) b[s][u][i] = (cok && kok) ? a.fold_we[(size_t)(k + i) * a.ld_fold_we + col] : 0.f;
-        }
-      }
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        f4v acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int u = 0; u < kFoldMaxJ; ++u) {
-          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[s][u].x, b[s][u][0], acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[s][u].y, b[s][u][1], acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[s][u].z, b[s][u][2], acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[s][u].w, b[s][u][3], acc, 0, 0, 0);
-        }
-#pragma unroll
-        for (int r = 0; r < 4; ++r) part[((SPW * wave + 2 * h + s) * 16 + 4 * g + r) * 17 + c] = acc[r];
-      }
-    }
+  for (int tile = first < 0 ? (int)blockIdx.x : first; tile < fold_tiles(a); tile += gridDim.x) {
+    FoldOps<NW> f;
+    fold_issue<NW>(a, tile, f);
+    fold_mma<NW>(f, part);
     __syncthreads();
-    {
-      const int r = threadIdx.x >> 4, cc = threadIdx.x & 15;  // the first 256 threads: one output each
-      if (threadIdx.x < 256 && r0 + r < R && c0 + cc < kp) {
-        float sum = 0.f;
-#pragma unroll
-        for (int w = 0; w < kFoldSlices; ++w) sum += part[(w * 16 + r) * 17 + cc];
-        a.fold_out[(size_t)(r0 + r) * a.ld_fold_out + c0 + cc] = static_cast<uint16_t>(f32_to_bf16_bits(sum));
-      }
-    }
+    fold_reduce(a, tile, part);
     __syncthreads();
   }
 }
@@ -240,6 +264,7 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
                 oImgs = oZtp + kZtp, oTsb = oImgs + kImgs, kSmem = oTsb + kTsb;
   constexpr int kStageBytes = oZpart;  // vt | ot | xs: W_h's staging room in the prologue
   static_assert(!QKV || kStageBytes >= 16 * 16 * 17 * 4, "the fold tail's partial tiles fit the stage");
+  static_assert(!QKV || kZpart + kZtp >= 16 * 16 * 17 * 4, "... and the z-tile region");
   static_assert(oXs % 16 == 0 && oImgs % 16 == 0 && oTsb % 16 == 0, "16-B aligned LDS carve");
   __shared__ __attribute__((aligned(16))) char smem[kSmem];
   auto vt = reinterpret_cast<uint16_t(*)[16 * LD]>(smem + oVt);
@@ -421,11 +446,19 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
     for (int sel = 0; sel < 3; ++sel)
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) bqv[sel][nt] = a.bq[sel * HD + hw * D + 16 * nt + c];
+    // the next forward's weight fold (image mode, at the start): this workgroup's tile's operand
+    // loads go out with the prologue's own; with W_h staged below, its MFMAs run after the same
+    // wait, its partial tiles go to the z-tile region (free until the first iteration) and the
+    // staging barrier doubles as the fold's -- one round trip for both
+    const bool staged = a.ld_wq == 72 && HD * 144 <= kStageBytes;
+    const bool fold_first = IMG && a.fold_out && a.fold_at_start;
+    const bool fold_here = fold_first && staged && (int)blockIdx.x < fold_tiles(a);
+    FoldOps<NW> fo;
     if constexpr (IMG) {
-      // the next forward's weight fold, its latency under the images' DMA issued above, its
-      // partial tiles in the V / O / X tiles (free until W_h is staged into them below)
-      if (a.fold_out && a.fold_at_start) fold_tail<NW>(a, reinterpret_cast<float*>(smem + oVt));
+      if (fold_here) fold_issue<NW>(a, blockIdx.x, fo);
+      else if (fold_first && !staged) fold_tail<NW>(a, reinterpret_cast<float*>(smem + oVt));
     }
+    float* fold_part = reinterpret_cast<float*>(smem + oZpart);  // zpart | ztp: 16 * 16 * 17 floats
     // W_h staged ONCE per workgroup: the wave reading it from global memory itself made every
     // wave of the grid pull its head's 27.6 KiB through L2 at the same moment (57 MiB at
     // B = 2048: 9-12 k shader clocks of issue stalls per wave before any work, a third of the
@@ -434,7 +467,7 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
     // wave reads its fragments from there: the grid's L2 traffic for W falls by the waves per
     // head of a workgroup (NW / Hl: 4 at TP = 2, 2 at TP = 1).
     const int selb = HD * 144;  // one projection's rows of every local head (ld_wq = 72)
-    if (a.ld_wq == 72 && selb <= kStageBytes) {
+    if (staged) {
       char* stg = smem + oVt;
       // as many projections per round as the V / O / X tiles hold: TP = 2 (HD = 128) all three at
       // once, TP = 1 (HD = 256) q | k then v -- every round one LDS-DMA latency and two barriers
@@ -455,7 +488,9 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
                                                      (pc * 64 + lane) * 16, 0, 0, 0);
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
           if (sel == 0) stamp(29);  // this wave's W_h DMA landed
+          if (IMG && sel == 0 && fold_here) fold_mma<NW>(fo, fold_part);
           __syncthreads();
+          if (IMG && sel == 0 && fold_here) fold_reduce(a, blockIdx.x, fold_part);
           done = sel + nsel;
           r0 = sel;
         }
@@ -469,6 +504,7 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
         }
         if (sel + 1 == done) __syncthreads();  // (the round's last projection read: the stage is free)
       }
+
     } else {
 #pragma unroll
       for (int sel = 0; sel < 3; ++sel)
@@ -794,6 +830,11 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
     if (a.fold_out && !a.fold_at_start) {
       __syncthreads();
       fold_tail<NW>(a, &imgs[0][0]);
+    } else if (a.fold_out && a.ld_wq == 72 && HD * 144 <= kStageBytes) {
+      // the prologue folded this workgroup's first tile; a grid smaller than the fold's tiles
+      // does the rest here, where W_h's registers are free
+      __syncthreads();
+      fold_tail<NW>(a, &imgs[0][0], blockIdx.x + gridDim.x);
     }
   }
   if constexpr (QKV) {
