@@ -758,11 +758,11 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
     // (token l >> 2, classes 4 (l & 3) .. +3), one 16-B store per lane, a sequence's S x 16
     // fp32 rows as whole lines
     if constexpr (IMG) {
-      // this wave's DMA of the images two iterations ahead has landed (visible to every wave
-      // after the barrier below); the next iteration's X, from images that landed one
-      // barrier ago, goes to the other X buffer
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      // the next iteration's X, from images that landed one barrier ago, into the other X buffer
+      // -- built while this wave's DMA of the images two iterations ahead is still in flight;
+      // then that DMA has landed (visible to every wave after the barrier below)
       if (base + stride < npairs) build_x(it ^ 1, base + stride);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     stamp(sj + 3);
     __syncthreads();  // (the next iteration writes the other buffer)
