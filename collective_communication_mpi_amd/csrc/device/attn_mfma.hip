@@ -249,7 +249,8 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
   // One LDS block carved into the kernel's buffers; the per-wave V / O tiles and the X tiles come
   // first and back to back, so the prologue can stage W_h through all three at once.
   //   vt, ot  [NW][16 * LD] bf16: per-wave V^T / O tiles
-  //   xs      [2][NW][16 * LDX] bf16 (fused QKV): the iteration's patch rows X, double-buffered
+  //   xs      [2][NW][16 * LDX] bf16 (fused QKV): room for W_h's staging in the prologue (once the
+  //           X tiles of the image mode's workgroup-wide build, which read_x replaced)
   //   zpart   [2][NW][16] fp32: fused pooled fc_o partial logits, double-buffered
   //   ztp     [2][NW][16 * 16] fp32: per-token fused fc_o z tiles per head, double-buffered
   //   imgs    [2][kImgPieces * 256] fp32 (image mode): the NW / Hl images of an iteration,
@@ -269,7 +270,6 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
   __shared__ __attribute__((aligned(16))) char smem[kSmem];
   auto vt = reinterpret_cast<uint16_t(*)[16 * LD]>(smem + oVt);
   auto ot = reinterpret_cast<uint16_t(*)[16 * LD]>(smem + oOt);
-  auto xs = reinterpret_cast<uint16_t(*)[NW][16 * LDX]>(smem + oXs);
   auto zpart = reinterpret_cast<float(*)[NW][16]>(smem + oZpart);
   auto ztp = reinterpret_cast<float(*)[NW][16 * 16]>(smem + oZtp);
   auto imgs = reinterpret_cast<float(*)[kImgPieces * 256]>(smem + oImgs);
@@ -368,20 +368,12 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
   // bias split into bf16 hi + lo parts, so the bias rides in the MFMA's fp32 accumulation (to
   // ~2^-17 relative -- far below the bf16 rounding of q | k | v) instead of 12 per-tile loads
   const int kb = a.kq > 64 ? a.kq : 64, gb = (kb - 64) >> 2;
-  auto load_x = [&](int p) {
+  auto load_x = [&](int p) {  // patch-row mode: the pair's X rows from global memory
     const bool ok = p < npairs && c < S;
-    if constexpr (IMG) {
-      // this iteration's X tile of the wave's sequence (built at the end of the previous one)
-      const uint16_t* X = xs[it][div_hl(wave)] + c * LDX;
-      xn[0] = *reinterpret_cast<const bf16x8*>(X + 8 * g);
-      xn[1] = *reinterpret_cast<const bf16x8*>(X + 32 + 8 * g);
-      xtn = *reinterpret_cast<const s4*>(X + 64 + 4 * g);
-    } else {
-      const uint16_t* row = a.xq + (size_t)(ok ? div_hl(p) * S + c : 0) * a.ld_xq;
-      xn[0] = ld_row16(row + 8 * g, ok && 8 * g < a.kq);
-      xn[1] = ld_row16(row + 32 + 8 * g, ok && 32 + 8 * g < a.kq);
-      xtn = ld_s4(row + 64 + 4 * g, ok && 64 + 4 * g < a.kq);
-    }
+    const uint16_t* row = a.xq + (size_t)(ok ? div_hl(p) * S + c : 0) * a.ld_xq;
+    xn[0] = ld_row16(row + 8 * g, ok && 8 * g < a.kq);
+    xn[1] = ld_row16(row + 32 + 8 * g, ok && 32 + 8 * g < a.kq);
+    xtn = ld_s4(row + 64 + 4 * g, ok && 64 + 4 * g < a.kq);
     if (g == gb) {  // the bias columns kb, kb + 1 of X are ones
       xtn[0] = (short)0x3F80;
       xtn[1] = (short)0x3F80;
@@ -401,36 +393,41 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
                                                  16, (pc * 64 + lane) * 16, 0, 0, 0);
     }
   };
-  // the X tiles of the iteration starting at pair p0 from its LDS images, by the whole
-  // workgroup: one 8-column chunk (4 packed conversions, one 16-B LDS store) per thread and
-  // step.  MNIST 28 x 28 with 7 x 7 patches (S = 16): token t = patch (t / 4, t % 4); column
-  // cc < 49 is pixel (cc / 7, cc % 7) of the patch, 49 the embedding bias 1, 50 + t the
-  // position one-hot, the rest zero (the QKV bias columns are set in load_x)
-  auto build_x = [&](int buf, int p0) {
+  // image mode: the wave's own X fragments (lane (c, g): token c; columns 8 g .., 32 + 8 g ..,
+  // 64 + 4 g ..) straight from its sequence's image in LDS buffer buf.  MNIST 28 x 28 with 7 x 7
+  // patches (S = 16): token t = patch (t / 4, t % 4); column cc < 49 is pixel (cc / 7, cc % 7) of
+  // the patch, 49 the embedding bias 1, 50 + t the position one-hot, the rest zero, plus the QKV
+  // bias columns kb, kb + 1 -- k_patchify's rows, bitwise.  (Round 6 until now: the workgroup
+  // built the iteration's X tiles in LDS and every wave read its rows back -- one build round
+  // and its stores cost ~1 k shader clocks per iteration, profiles/r6_attn.)  The
+  // reads go out under the current pair's work; the next iteration consumes them.
+  auto read_x = [&](int buf) {
     if constexpr (IMG) {
-      const int nseq = div_hl(NW);
-      for (int id = threadIdx.x; id < nseq * 160; id += NW * 64) {
-        const int sq = id / 160, rem = id - sq * 160, t = rem / 10, ch = rem - t * 10;
-        const float* im = imgs[buf] + sq * 784 + (t >> 2) * 196 + (t & 3) * 7;
-        // pixel (pr, pc) of column 8 ch, stepped along the chunk; every lane reads (a clamped
-        // address past the 49 pixels) and selects: no divergent branch per column
-        int pr = (8 * ch) / 7, pc = 8 * ch - 7 * pr;
+      const float* im = imgs[buf] + div_hl(wave) * 784 + (c >> 2) * 196 + (c & 3) * 7;
+      auto chunk = [&](int c0) {  // columns c0 .. c0 + 7 (c0 < 49 or past the pixels)
+        int pr = c0 / 7, pc = c0 - 7 * pr;
         float v[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          const int cc = 8 * ch + j;
+          const int cc = c0 + j;
           const float px = im[cc < 49 ? pr * 28 + pc : 0];
-          // px * 1 + 0 or px * 0 + (0 | 1): the load's value is always used, so the compiler
-          // keeps it unconditional (a select let it sink the read into a branch per column)
-          v[j] = fmaf(px, cc < 49 ? 1.f : 0.f, (cc == 49 || cc == 50 + t) ? 1.f : 0.f);
+          v[j] = fmaf(px, cc < 49 ? 1.f : 0.f, (cc == 49 || cc == 50 + c) ? 1.f : 0.f);
           const bool wrap = pc == 6;
           pc = wrap ? 0 : pc + 1;
           pr += wrap ? 1 : 0;
         }
         const u32x4 w = {pk_bf16(v[0], v[1]), pk_bf16(v[2], v[3]), pk_bf16(v[4], v[5]), pk_bf16(v[6], v[7])};
-        *reinterpret_cast<u32x4*>(xs[buf][sq] + t * LDX + 8 * ch) = w;
+        return __builtin_bit_cast(bf16x8, w);
+      };
+      xn[0] = chunk(8 * g);
+      xn[1] = chunk(32 + 8 * g);
+      // the tail (columns 64 + 4 g .. +3): the position one-hot of tokens 14 and 15, the bias columns
+#pragma unroll
+      for (int j = 0; j < 4; ++j) xtn[j] = (64 + 4 * g + j == 50 + c) ? (short)0x3F80 : (short)0;
+      if (g == gb) {
+        xtn[0] = (short)0x3F80;
+        xtn[1] = (short)0x3F80;
       }
-      (void)p0;
     }
   };
   if constexpr (QKV) {
@@ -530,15 +527,13 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
     stamp(25);  // W_h's tail fragments and biases arrived
     if constexpr (!IMG) load_x(blockIdx.x * NW + wave);
     if constexpr (IMG) {
-      // images two iterations deep: the first two (their DMA issued before W_h's), X of the
-      // first one built
-      const int p0 = blockIdx.x * NW;
+      // images two iterations deep: the first two (their DMA issued before W_h's), the first
+      // one's X fragments read once they are visible
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       stamp(26);  // every W_h load and both images' DMA landed
       __syncthreads();
-      build_x(0, p0);
+      read_x(0);
       stamp(27);
-      __syncthreads();
     }
   }
   stamp(1);
@@ -548,19 +543,23 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
    bf16x8 xr[2];
    s4 xt;
    if constexpr (QKV) {
-    // (image mode builds this iteration's rows now, from LDS: the prefetch is the images' DMA)
+    // (image mode: xn holds this iteration's fragments, read during the previous one)
     if constexpr (IMG) {
-      load_x(pr);
-      // the images of the iteration after next, into the buffer whose images this iteration's
-      // X was built from (the body issues no further global loads, so nothing waits on this
-      // DMA before the epilogue's vmcnt(0); the trip count is workgroup-uniform, so every
-      // piece is issued)
+      // the images of the iteration after next, into the buffer this iteration's X was read
+      // from -- by every wave before the last barrier (the body issues no further global
+      // loads, so nothing waits on this DMA before the epilogue's vmcnt(0); the trip count is
+      // workgroup-uniform, so every piece is issued)
       if (base + 2 * stride < npairs) stage_imgs(it, base + 2 * stride);
     }
     xr[0] = xn[0];
     xr[1] = xn[1];
     xt = xtn;
-    if constexpr (!IMG) load_x(pr + stride);
+    if constexpr (IMG) {
+      // the next iteration's X, from images visible since the last barrier
+      if (base + stride < npairs) read_x(it ^ 1);
+    } else {
+      load_x(pr + stride);
+    }
    }
    stamp(sj);
    if (pr < npairs) {
@@ -758,10 +757,8 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
     // (token l >> 2, classes 4 (l & 3) .. +3), one 16-B store per lane, a sequence's S x 16
     // fp32 rows as whole lines
     if constexpr (IMG) {
-      // the next iteration's X, from images that landed one barrier ago, into the other X buffer
-      // -- built while this wave's DMA of the images two iterations ahead is still in flight;
-      // then that DMA has landed (visible to every wave after the barrier below)
-      if (base + stride < npairs) build_x(it ^ 1, base + stride);
+      // this wave's DMA of the images two iterations ahead has landed (visible to every wave
+      // after the barrier below)
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     stamp(sj + 3);
