@@ -399,8 +399,7 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
   // the patch, 49 the embedding bias 1, 50 + t the position one-hot, the rest zero, plus the QKV
   // bias columns kb, kb + 1 -- k_patchify's rows, bitwise.  (Round 6 until now: the workgroup
   // built the iteration's X tiles in LDS and every wave read its rows back -- one build round
-  // and its stores cost ~1 k shader clocks per iteration, profiles/r6_attn.)  The
-  // reads go out under the current pair's work; the next iteration consumes them.
+  // and its stores cost ~1 k shader clocks per iteration, profiles/r6_attn.)
   auto read_x = [&](int buf) {
     if constexpr (IMG) {
       const float* im = imgs[buf] + div_hl(wave) * 784 + (c >> 2) * 196 + (c & 3) * 7;
@@ -543,7 +542,7 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
    bf16x8 xr[2];
    s4 xt;
    if constexpr (QKV) {
-    // (image mode: xn holds this iteration's fragments, read during the previous one)
+    // (image mode: xn holds this iteration's fragments, read at the end of the previous one)
     if constexpr (IMG) {
       // the images of the iteration after next, into the buffer this iteration's X was read
       // from -- by every wave before the last barrier (the body issues no further global
@@ -554,12 +553,7 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
     xr[0] = xn[0];
     xr[1] = xn[1];
     xt = xtn;
-    if constexpr (IMG) {
-      // the next iteration's X, from images visible since the last barrier
-      if (base + stride < npairs) read_x(it ^ 1);
-    } else {
-      load_x(pr + stride);
-    }
+    if constexpr (!IMG) load_x(pr + stride);
    }
    stamp(sj);
    if (pr < npairs) {
@@ -757,8 +751,10 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
     // (token l >> 2, classes 4 (l & 3) .. +3), one 16-B store per lane, a sequence's S x 16
     // fp32 rows as whole lines
     if constexpr (IMG) {
-      // this wave's DMA of the images two iterations ahead has landed (visible to every wave
-      // after the barrier below)
+      // the next iteration's X, from images visible since the last barrier (read before the
+      // barrier below: the next iteration's DMA overwrites this buffer); then this wave's DMA
+      // of the images two iterations ahead has landed (visible to every wave after the barrier)
+      if (base + stride < npairs) read_x(it ^ 1);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     stamp(sj + 3);
