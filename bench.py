@@ -155,8 +155,13 @@ def _run_child(cmd, env, budget: float, abort_flag: str = "", cpus=None):
     import signal
 
     t0 = time.monotonic()
-    pre = (lambda c=frozenset(cpus): os.sched_setaffinity(0, c)) if cpus else None
-    p = subprocess.Popen(cmd, env=env, cwd=REPO, start_new_session=True, preexec_fn=pre)
+    def pre(c=frozenset(cpus or ())):
+        try:
+            os.sched_setaffinity(0, c)
+        except OSError:  # (a set outside this container's cpuset: the OS places the child)
+            pass
+
+    p = subprocess.Popen(cmd, env=env, cwd=REPO, start_new_session=True, preexec_fn=pre if cpus else None)
     rc = None
     while True:
         try:
@@ -203,7 +208,8 @@ def phase_binding(world, rank: int, local: int):
         nloc = int(os.environ.get("LOCAL_WORLD_SIZE", os.environ.get("CCMPI_LOCAL_SIZE", world.Get_size())))
         try:
             plan = gpu_plan(nloc, busy=_cpu_busy())
-        except (OSError, ValueError):
+        except Exception as e:  # (any failure: every rank still reaches the bcast below)
+            print(f"[bench] GPU-local placement unavailable ({type(e).__name__}: {e}); OS placement", file=sys.stderr)
             plan = None
     plan = world.bcast(plan, root=0) if mode == "gpu" else None
     if not plan or local >= len(plan):
