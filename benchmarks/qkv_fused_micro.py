@@ -137,11 +137,16 @@ def main():
                 for mean in (False, True):
                     if args.only and args.only != mode:
                         continue
-                    rows.append(dict(kernel="fused", mode=mode, train=train, mean=mean, grid=cap,
-                                     us=timed(fused(mode, train, mean), args.iters), nolse=args.nolse,
-                                     fold=bool(args.fold and mode == "img")))
-                    if args.trace:
-                        rows[-1]["phases"] = trace_phases(fused, mode, train, mean, cap, B * H)
+                    fold = bool(args.fold and mode == "img")
+                    # with the fold: the fold-aware block schedule on (1) and off (0), interleaved
+                    for sched in ((1, 0) if fold else (-1,)):
+                        dev.attn_set_qkv_fold_sched(sched)
+                        rows.append(dict(kernel="fused", mode=mode, train=train, mean=mean, grid=cap,
+                                         us=timed(fused(mode, train, mean), args.iters), nolse=args.nolse,
+                                         fold=fold, **({"fold_sched": sched} if fold else {})))
+                        if args.trace:
+                            rows[-1]["phases"] = trace_phases(fused, mode, train, mean, cap, B * H)
+                    dev.attn_set_qkv_fold_sched(-1)
     dev.attn_set_qkv_grid(0)
     for r in rows:
         r.update(B=B, H=H)

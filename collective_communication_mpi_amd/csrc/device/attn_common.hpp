@@ -69,6 +69,9 @@ struct AttnArgs {
   uint16_t* fold_out;
   int ld_fold_out, fold_R, fold_d, fold_kp;
   int fold_at_start;  // 1: the fold runs before the attention work (its loads under W_h's), 0: after
+  // set by launch_qkv_fwd_mfma: 0 = every workgroup takes its pair blocks grid-stride; k + 1 = the
+  // fold-owning workgroups stop after k rounds and the others share the remaining blocks
+  int fold_sched;
   // diagnostic (fused QKV forward): per wave kTStamps shader-clock stamps of the kernel's
   // phases ([grid * 4 waves][32] u64; s_memtime, buffered in LDS, stored at the end), or null
   unsigned long long* tstamp;
@@ -81,6 +84,7 @@ void launch_fwd_mfma(const AttnArgs& a, hipStream_t stream);
 void launch_bwd_mfma(const AttnArgs& a, hipStream_t stream);
 void launch_qkv_fwd_mfma(const AttnArgs& a, hipStream_t stream);  // fused QKV + attention + token fc_o
 extern int g_qkv_grid_cap;  // workgroups of the fused QKV forward (persistent grid)
+extern int g_qkv_fold_sched;  // fold-aware block schedule of the fused forward: -1 env, 0 off, 1 on
 extern int g_bwd_grid_cap;  // workgroups of the backward kernel when it also reduces the bias gradient
 
 }  // namespace attn

@@ -30,6 +30,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "attn_common.hpp"
 #include "common.hpp"
@@ -347,7 +348,21 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
         wb[kk] = ld_row16(a.wo + (size_t)c * a.ld_wo + hw * D + 32 * kk + 8 * g, c < a.n_out);
     }
   }
-  const int stride = gridDim.x * NW;
+  // the workgroup's pair blocks (NW consecutive pairs each): grid-stride, except with the weight
+  // fold at the start (pipelined plan) where a fold-owning workgroup (the first F) stops after kf
+  // rounds and the others share the rest -- the fold costs ~1.5 iterations (profiles/r6_attn), so
+  // at H = 2 (2 rounds) the fold owners' extra work no longer sets the kernel's length
+  const int nblk = (npairs + NW - 1) / NW, G = gridDim.x, wg = blockIdx.x;
+  int kf = 0x7fffffff, F = 0;
+  if constexpr (QKV && IMG) {
+    if (a.fold_sched > 0 && a.fold_out && a.fold_at_start && a.ld_wq == 72 && HD * 144 <= kStageBytes) {
+      F = min(fold_tiles(a), G);
+      if (F < G) kf = a.fold_sched - 1;
+    }
+  }
+  auto blk = [&](int i) {  // this workgroup's i-th block; >= nblk: none (monotone in i)
+    return i < kf ? wg + i * G : (wg < F ? nblk : kf * G + (wg - F) + (i - kf) * (G - F));
+  };
   // the fc_o bias of this lane's epilogue classes (4 (lane & 3) .. +3), loaded once (the
   // compiler cannot hoist it past the loop's global stores)
   float bov[4];
@@ -432,9 +447,9 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
   if constexpr (QKV) {
     const int hw = mod_hl(wave);
     if constexpr (IMG) {
-      const int p0 = blockIdx.x * NW;
-      stage_imgs(0, p0);
-      if (p0 + stride < npairs) stage_imgs(1, p0 + stride);
+      // (a fold owner may have no block at all: kf = 0)
+      if (blk(0) < nblk) stage_imgs(0, blk(0) * NW);
+      if (blk(1) < nblk) stage_imgs(1, blk(1) * NW);
     }
     // every load first (the bias by every lane, unconditionally), every use after
     float bqv[3][NT];
@@ -524,7 +539,7 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
         wtl[sel][nt][1] = g == gb ? lo : wtl[sel][nt][1];
       }
     stamp(25);  // W_h's tail fragments and biases arrived
-    if constexpr (!IMG) load_x(blockIdx.x * NW + wave);
+    if constexpr (!IMG) load_x(blk(0) * NW + wave);
     if constexpr (IMG) {
       // images two iterations deep: the first two (their DMA issued before W_h's), the first
       // one's X fragments read once they are visible
@@ -536,7 +551,8 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
     }
   }
   stamp(1);
-  for (int base = blockIdx.x * NW; base < npairs; base += stride, it ^= 1, ++itn) {
+  for (int bi = blk(0); bi < nblk; bi = blk(itn + 1), it ^= 1, ++itn) {
+   const int base = bi * NW;
    const int pr = base + wave;
    const int sj = itn < 4 ? 2 + 5 * itn : kTStamps;  // this iteration's stamp slots
    bf16x8 xr[2];
@@ -548,12 +564,12 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
       // from -- by every wave before the last barrier (the body issues no further global
       // loads, so nothing waits on this DMA before the epilogue's vmcnt(0); the trip count is
       // workgroup-uniform, so every piece is issued)
-      if (base + 2 * stride < npairs) stage_imgs(it, base + 2 * stride);
+      if (blk(itn + 2) < nblk) stage_imgs(it, blk(itn + 2) * NW);
     }
     xr[0] = xn[0];
     xr[1] = xn[1];
     xt = xtn;
-    if constexpr (!IMG) load_x(pr + stride);
+    if constexpr (!IMG) load_x(blk(itn + 1) * NW + wave);
    }
    stamp(sj);
    if (pr < npairs) {
@@ -754,7 +770,7 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
       // the next iteration's X, from images visible since the last barrier (read before the
       // barrier below: the next iteration's DMA overwrites this buffer); then this wave's DMA
       // of the images two iterations ahead has landed (visible to every wave after the barrier)
-      if (base + stride < npairs) read_x(it ^ 1);
+      if (blk(itn + 1) < nblk) read_x(it ^ 1);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     stamp(sj + 3);
@@ -1036,9 +1052,42 @@ void launch_fwd_mfma(const AttnArgs& a, hipStream_t stream) {
 // every wave); attn_set_qkv_grid / CCMPI_QKV_GRID
 int g_qkv_grid_cap = std::getenv("CCMPI_QKV_GRID") ? std::atoi(std::getenv("CCMPI_QKV_GRID")) : 256;
 
-void launch_qkv_fwd_mfma(const AttnArgs& a, hipStream_t stream) {
-  const int grid = grid_for(a.B * a.Hl, g_qkv_grid_cap, kQkvWaves);
+// The in-kernel weight fold's cost in pair rounds of the fused forward (H = 2: ~3 us against
+// ~2.1 us per round; H = 4: ~3.2 against ~2.7; profiles/r6_attn trace_v9_fold / trace_v12).
+constexpr double kFoldRounds = 1.5;
+int g_qkv_fold_sched = -1;  // -1: CCMPI_QKV_FOLD_SCHED (default on), 0: grid-stride always, 1: on
+
+// AttnArgs::fold_sched for a launch of `grid` workgroups: the rounds kf of the fold-owning
+// workgroups that minimise max(kf + fold, the others' rounds); 0 when grid-stride is as good
+int fold_sched_for(const AttnArgs& a, int grid) {
+  if (g_qkv_fold_sched < 0) {
+    const char* e = std::getenv("CCMPI_QKV_FOLD_SCHED");
+    g_qkv_fold_sched = (e && std::atoi(e) == 0) ? 0 : 1;
+  }
+  if (!g_qkv_fold_sched || !a.img || !a.fold_out || !a.fold_at_start) return 0;
+  const int nblk = (a.B * a.Hl + kQkvWaves - 1) / kQkvWaves;
+  const int F = std::min(((a.fold_R + 15) / 16) * ((a.fold_kp + 15) / 16), grid);
+  if (F <= 0 || F >= grid) return 0;
+  const int kstd = (nblk + grid - 1) / grid;
+  double best = kstd + kFoldRounds;
+  int bk = kstd;
+  for (int kf = kstd - 1; kf >= 0; --kf) {
+    const int rest = nblk - kf * grid;
+    const int others = kf + (rest > 0 ? (rest + grid - F - 1) / (grid - F) : 0);
+    const double cost = std::max(kf + kFoldRounds, (double)others);
+    if (cost < best) {
+      best = cost;
+      bk = kf;
+    }
+  }
+  return bk == kstd ? 0 : bk + 1;
+}
+
+void launch_qkv_fwd_mfma(const AttnArgs& args, hipStream_t stream) {
+  const int grid = grid_for(args.B * args.Hl, g_qkv_grid_cap, kQkvWaves);
   const dim3 block(64 * kQkvWaves);
+  AttnArgs a = args;
+  a.fold_sched = fold_sched_for(args, grid);
   if (a.img) {
     if (a.D == 32) hipLaunchKernelGGL((k_qkv_attn16_fwd<32, true>), dim3(grid), block, 0, stream, a);
     else hipLaunchKernelGGL((k_qkv_attn16_fwd<64, true>), dim3(grid), block, 0, stream, a);

@@ -626,7 +626,10 @@ void register_attn_ops(pybind11::module_& m) {
         pybind11::arg("S"), pybind11::arg("ncol"), pybind11::arg("stream"),
         pybind11::call_guard<pybind11::gil_scoped_release>());
   m.def("attn_set_qkv_grid", [](int cap) { attn::g_qkv_grid_cap = cap > 0 ? cap : 256; },
-        "workgroups of the fused QKV forward (default 512: two per CU)", pybind11::arg("cap"));
+        "workgroups of the fused QKV forward (default 256: one 8-wave workgroup per CU)", pybind11::arg("cap"));
+  m.def("attn_set_qkv_fold_sched", [](int v) { attn::g_qkv_fold_sched = v < 0 ? -1 : (v ? 1 : 0); },
+        "fused QKV forward with the in-kernel fold: 1 = fold owners take fewer pair blocks, 0 = grid-stride, "
+        "-1 = CCMPI_QKV_FOLD_SCHED (default 1)", pybind11::arg("v"));
   m.def("attn_set_bwd_grid", [](int cap) { attn::g_bwd_grid_cap = cap > 0 ? cap : 0; },
         "backward kernel grid cap (tuning)");
   namespace py = pybind11;

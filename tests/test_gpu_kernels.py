@@ -581,6 +581,56 @@ def test_attn_qkv_fused_patchify(B, H, D):
                          zrows=0, zpush=[], stream=st, img=img.data_ptr())
 
 
+@pytest.mark.parametrize("B,H", [(2048, 2), (2048, 4), (1000, 2), (37, 1)])
+def test_attn_qkv_fold_schedule(B, H):
+    """The fused forward's in-kernel weight fold (the pipelined plan's) with the fold-aware block
+    schedule -- fold-owning workgroups take fewer pair blocks, at B = 1000 / H = 2 none at all --
+    against plain grid-stride and against the forward without the fold: token-mean logits bitwise
+    equal, and the folded W_eff bitwise the standalone fp32-MFMA fold kernel's."""
+    from collective_communication_mpi_amd import _native
+
+    dev = _native.device()
+    st = torch.cuda.current_stream().cuda_stream
+    g = torch.Generator(device="cuda").manual_seed(B * 7 + H)
+    S, kp, D = 16, 72, 64
+    HD = H * D
+    img = torch.rand(B, 784, device="cuda", generator=g)
+    w = (torch.randn(3 * HD, kp, device="cuda", generator=g) / kp ** 0.5).bfloat16()
+    bq = torch.randn(3 * HD, device="cuda", generator=g) * 0.1
+    wo = (torch.randn(16, HD, device="cuda", generator=g) * 0.1).bfloat16()
+    bo = torch.randn(16, device="cuda", generator=g)
+    wq32 = torch.randn(3 * HD, 768, device="cuda", generator=g) / 768 ** 0.5
+    we32 = torch.randn(768, kp, device="cuda", generator=g) / 8
+    outs = {}
+    try:
+        for sched in (0, 1, None):
+            zm = torch.full((B, 16), float("nan"), device="cuda")
+            wn = torch.full((3 * HD, kp), float("nan"), device="cuda").bfloat16()
+            kw = dict(xq=0, ld_xq=kp, kq=kp, wq=w.data_ptr(), ld_wq=w.stride(0), bq=bq.data_ptr(), qkv_out=0,
+                      ld_qkv=3 * HD, lse=0, B=B, S=S, Hl=H, D=D, scale=D ** -0.5, pool=0, ld_pool=HD,
+                      wo=wo.data_ptr(), ld_wo=wo.stride(0), n_out=16, bo=bo.data_ptr(), ztok=0, ld_zt=16, zrows=0,
+                      zpush=[], zmean=zm.data_ptr(), ld_zmean=16, stream=st, img=img.data_ptr())
+            if sched is not None:
+                kw.update(fold_wq=wq32.data_ptr(), ld_fold_wq=768, fold_we=we32.data_ptr(), ld_fold_we=kp,
+                          fold_out=wn.data_ptr(), ld_fold_out=kp, fold_R=3 * HD, fold_d=768)
+            dev.attn_set_qkv_fold_sched(-1 if sched is None else sched)
+            dev.attn_qkv_fwd(**kw)
+            outs[sched] = (zm, wn)
+    finally:
+        dev.attn_set_qkv_fold_sched(-1)
+    ref = torch.full((3 * HD, kp), float("nan"), device="cuda").bfloat16()
+    dev.fold_set_variant(1)
+    try:
+        dev.fold_emb_qkv(wq32.data_ptr(), 768, we32.data_ptr(), kp, ref.data_ptr(), kp, 3 * HD, 768, kp, st)
+    finally:
+        dev.fold_set_variant(-1)
+    torch.cuda.synchronize()
+    (z0, w0), (z1, w1), (zn, _) = outs[0], outs[1], outs[None]
+    assert not torch.isnan(z1).any()
+    assert torch.equal(z0, z1) and torch.equal(z0, zn)
+    assert torch.equal(w0, w1) and torch.equal(w1, ref)
+
+
 @pytest.mark.parametrize("img,patch,misalign", [(28, 7, 0), (28, 7, 1), (24, 6, 0)])  # LDS / plain / runtime sizes
 def test_patchify_columns(img, patch, misalign):
     from collective_communication_mpi_amd.models.mnist_tp import LayerConfig, patchify
