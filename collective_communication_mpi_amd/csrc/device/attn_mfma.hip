@@ -542,10 +542,15 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
     if constexpr (!IMG) load_x(blk(0) * NW + wave);
     if constexpr (IMG) {
       // images two iterations deep: the first two (their DMA issued before W_h's), the first
-      // one's X fragments read once they are visible
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      stamp(26);  // every W_h load and both images' DMA landed
-      __syncthreads();
+      // one's X fragments read once they are visible -- with W_h staged, every wave waited for
+      // all its loads (images included) before the staging barrier, so they are already
+      if (!staged) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        stamp(26);  // every W_h load and both images' DMA landed
+        __syncthreads();
+      } else {
+        stamp(26);
+      }
       read_x(0);
       stamp(27);
     }
