@@ -244,7 +244,7 @@ __device__ __forceinline__ void fold_tail(const AttnArgs& a, float* part /* >= 1
   }
 }
 
-template <int D, bool QKV, bool IMG = false, int NW = WPB>
+template <int D, bool QKV, bool IMG = false, int NW = WPB, bool TS = false>
 __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
   constexpr int LD = D + 8, NK = D / 32, NT = D / 16;
   // One LDS block carved into the kernel's buffers; the per-wave V / O tiles and the X tiles come
@@ -280,7 +280,8 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
   const float inv_s = 1.f / (float)S;  // (fused path: means as multiplies)
   // diagnostic phase stamps (a.tstamp): shader clock per phase, lane 0 of each wave, into LDS
   auto tsb = reinterpret_cast<unsigned long long(*)[kTStamps]>(smem + oTsb);
-  const bool tsr = QKV && a.tstamp != nullptr;
+  // (TS: the diagnostic instantiation; the production kernel carries no stamp code at all)
+  const bool tsr = TS && QKV && a.tstamp != nullptr;
   auto stamp = [&](int k) {
     if constexpr (QKV) {
       if (tsr) {
@@ -552,6 +553,9 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
         stamp(26);
       }
       read_x(0);
+      // every wave's reads of buffer 0 done before any wave's first loop DMA refills it (the
+      // images of the third block; an L2-resident image lands within a few hundred clocks)
+      if (blk(2) < nblk) __syncthreads();
       stamp(27);
     }
   }
@@ -866,13 +870,12 @@ __global__ void __launch_bounds__(256) k_attn16_fwd(AttnArgs a) {
   attn16_fwd_body<D, false>(a);
 }
 
-// two workgroups (8 waves) per CU: <= 256 VGPRs, W_h's fragments included
 // One workgroup of kQkvWaves waves per CU (two per SIMD): <= 256 VGPRs a wave, W_h's fragments
 // included; the waves of a workgroup share its staged W_h (see attn16_fwd_body).
 constexpr int kQkvWaves = 8;
-template <int D, bool IMG>
+template <int D, bool IMG, bool TS = false>
 __global__ void __launch_bounds__(64 * kQkvWaves) __attribute__((amdgpu_waves_per_eu(2))) k_qkv_attn16_fwd(AttnArgs a) {
-  attn16_fwd_body<D, true, IMG, kQkvWaves>(a);
+  attn16_fwd_body<D, true, IMG, kQkvWaves, TS>(a);
 }
 
 template <int D>
@@ -1093,7 +1096,15 @@ void launch_qkv_fwd_mfma(const AttnArgs& args, hipStream_t stream) {
   const dim3 block(64 * kQkvWaves);
   AttnArgs a = args;
   a.fold_sched = fold_sched_for(args, grid);
-  if (a.img) {
+  if (a.tstamp) {  // the phase-stamp diagnostic: its own instantiation
+    if (a.img) {
+      if (a.D == 32) hipLaunchKernelGGL((k_qkv_attn16_fwd<32, true, true>), dim3(grid), block, 0, stream, a);
+      else hipLaunchKernelGGL((k_qkv_attn16_fwd<64, true, true>), dim3(grid), block, 0, stream, a);
+    } else {
+      if (a.D == 32) hipLaunchKernelGGL((k_qkv_attn16_fwd<32, false, true>), dim3(grid), block, 0, stream, a);
+      else hipLaunchKernelGGL((k_qkv_attn16_fwd<64, false, true>), dim3(grid), block, 0, stream, a);
+    }
+  } else if (a.img) {
     if (a.D == 32) hipLaunchKernelGGL((k_qkv_attn16_fwd<32, true>), dim3(grid), block, 0, stream, a);
     else hipLaunchKernelGGL((k_qkv_attn16_fwd<64, true>), dim3(grid), block, 0, stream, a);
   } else {
