@@ -244,7 +244,7 @@ __device__ __forceinline__ void fold_tail(const AttnArgs& a, float* part /* >= 1
   }
 }
 
-template <int D, bool QKV, bool IMG = false, int NW = WPB, bool TS = false>
+template <int D, bool QKV, bool IMG = false, int NW = WPB, bool TS = false, bool TR = true>
 __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
   constexpr int LD = D + 8, NK = D / 32, NT = D / 16;
   // One LDS block carved into the kernel's buffers; the per-wave V / O tiles and the X tiles come
@@ -280,7 +280,8 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
   const float inv_s = 1.f / (float)S;  // (fused path: means as multiplies)
   // diagnostic phase stamps (a.tstamp): shader clock per phase, lane 0 of each wave, into LDS
   auto tsb = reinterpret_cast<unsigned long long(*)[kTStamps]>(smem + oTsb);
-  // (TS: the diagnostic instantiation; the production kernel carries no stamp code at all)
+  // (TS: the diagnostic instantiation; the production kernel carries no stamp code at all.
+  // TR = false: the inference instantiation -- no lse / qkv / X-row / pool stores in its code)
   const bool tsr = TS && QKV && a.tstamp != nullptr;
   auto stamp = [&](int k) {
     if constexpr (QKV) {
@@ -611,7 +612,7 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
           }
         }
       };
-      if (IMG && a.xq_out && h == 0 && c < S) {  // the patch rows, for the backward (one head's wave)
+      if (TR && IMG && a.xq_out && h == 0 && c < S) {  // the patch rows, for the backward (one head's wave)
         uint16_t* xo = a.xq_out + (size_t)(b * S + c) * a.ld_xq;
         if (8 * g < a.kq) *reinterpret_cast<bf16x8*>(xo + 8 * g) = xr[0];
         if (32 + 8 * g < a.kq) *reinterpret_cast<bf16x8*>(xo + 32 + 8 * g) = xr[1];
@@ -625,7 +626,7 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
         qr[kk] = *reinterpret_cast<const bf16x8*>(O + c * LD + 32 * kk + 8 * g);
         kr[kk] = *reinterpret_cast<const bf16x8*>(V + c * LD + 32 * kk + 8 * g);
       }
-      uint16_t* qo = a.qkv_out ? a.qkv_out + (size_t)b * S * a.ld_qkv + h * D : nullptr;
+      uint16_t* qo = TR && a.qkv_out ? a.qkv_out + (size_t)b * S * a.ld_qkv + h * D : nullptr;
       if (qo) {
         rows_out<D, LD>(O, qo, a.ld_qkv, S, lane);
         rows_out<D, LD>(V, qo + HD, a.ld_qkv, S, lane);
@@ -684,7 +685,7 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
     // (fused path: the hardware reciprocal -- the precise division is ~10 VALU ops, and the
     // probabilities are rounded to bf16 right after)
     const float inv = QKV ? __builtin_amdgcn_rcpf(s) : 1.f / s;
-    if (a.lse && g == 0 && c < S) a.lse[(size_t)pr * S + c] = m + __logf(s);
+    if (TR && a.lse && g == 0 && c < S) a.lse[(size_t)pr * S + c] = m + __logf(s);
     const s4 pa = pack4(e[0] * inv, e[1] * inv, e[2] * inv, e[3] * inv);  // A[i = c][j = 4g + jj]
     __builtin_amdgcn_wave_barrier();
     if constexpr (QKV) {
@@ -700,7 +701,7 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) ztp[it][wave][(4 * g + r) * 16 + c] = zt[r];  // z[i = 4g + r][cls = c]
       stamp(sj + 2);
-      if (a.pool) {
+      if (TR && a.pool) {
         // pool[f] = mean over the S queries of O[i][f]: recompute O un-transposed (4 more
         // 16x16x16 MFMAs, one tile live at a time) so the column sum is 4 adds + 2 shuffles per
         // tile -- and bitwise the unfused kernel's pool.  (A 15-shuffle butterfly over the
@@ -873,9 +874,9 @@ __global__ void __launch_bounds__(256) k_attn16_fwd(AttnArgs a) {
 // One workgroup of kQkvWaves waves per CU (two per SIMD): <= 256 VGPRs a wave, W_h's fragments
 // included; the waves of a workgroup share its staged W_h (see attn16_fwd_body).
 constexpr int kQkvWaves = 8;
-template <int D, bool IMG, bool TS = false>
+template <int D, bool IMG, bool TS = false, bool TR = true>
 __global__ void __launch_bounds__(64 * kQkvWaves) __attribute__((amdgpu_waves_per_eu(2))) k_qkv_attn16_fwd(AttnArgs a) {
-  attn16_fwd_body<D, true, IMG, kQkvWaves, TS>(a);
+  attn16_fwd_body<D, true, IMG, kQkvWaves, TS, TR>(a);
 }
 
 template <int D>
@@ -1103,6 +1104,14 @@ void launch_qkv_fwd_mfma(const AttnArgs& args, hipStream_t stream) {
     } else {
       if (a.D == 32) hipLaunchKernelGGL((k_qkv_attn16_fwd<32, false, true>), dim3(grid), block, 0, stream, a);
       else hipLaunchKernelGGL((k_qkv_attn16_fwd<64, false, true>), dim3(grid), block, 0, stream, a);
+    }
+  } else if (!(a.lse || a.qkv_out || a.xq_out || a.pool)) {  // inference: no training stores
+    if (a.img) {
+      if (a.D == 32) hipLaunchKernelGGL((k_qkv_attn16_fwd<32, true, false, false>), dim3(grid), block, 0, stream, a);
+      else hipLaunchKernelGGL((k_qkv_attn16_fwd<64, true, false, false>), dim3(grid), block, 0, stream, a);
+    } else {
+      if (a.D == 32) hipLaunchKernelGGL((k_qkv_attn16_fwd<32, false, false, false>), dim3(grid), block, 0, stream, a);
+      else hipLaunchKernelGGL((k_qkv_attn16_fwd<64, false, false, false>), dim3(grid), block, 0, stream, a);
     }
   } else if (a.img) {
     if (a.D == 32) hipLaunchKernelGGL((k_qkv_attn16_fwd<32, true>), dim3(grid), block, 0, stream, a);
