@@ -463,7 +463,9 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
     // loads go out with the prologue's own; with W_h staged below, its MFMAs run after the same
     // wait, its partial tiles go to the z-tile region (free until the first iteration) and the
     // staging barrier doubles as the fold's -- one round trip for both
-    const bool staged = a.ld_wq == 72 && HD * 144 <= kStageBytes;
+    // (the inference instantiation is launched only for the staged layout: no other W_h path in
+    // its code)
+    const bool staged = !TR || (a.ld_wq == 72 && HD * 144 <= kStageBytes);
     const bool fold_first = IMG && a.fold_out && a.fold_at_start;
     const bool fold_here = fold_first && staged && (int)blockIdx.x < fold_tiles(a);
     FoldOps<NW> fo;
@@ -846,10 +848,10 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
   if constexpr (QKV && IMG) {
     // the next forward's weight fold in the images' LDS (every DMA into it has landed: each
     // trip ends with vmcnt(0) and a barrier, and the trip count is workgroup-uniform)
-    if (a.fold_out && !a.fold_at_start) {
+    if (TR && a.fold_out && !a.fold_at_start) {  // (inference: launched only with the fold at the start)
       __syncthreads();
       fold_tail<NW>(a, &imgs[0][0]);
-    } else if (a.fold_out && a.ld_wq == 72 && HD * 144 <= kStageBytes) {
+    } else if (a.fold_out && (!TR || (a.ld_wq == 72 && HD * 144 <= kStageBytes))) {
       // the prologue folded this workgroup's first tile; a grid smaller than the fold's tiles
       // does the rest here, where W_h's registers are free
       __syncthreads();
@@ -1105,7 +1107,8 @@ void launch_qkv_fwd_mfma(const AttnArgs& args, hipStream_t stream) {
       if (a.D == 32) hipLaunchKernelGGL((k_qkv_attn16_fwd<32, false, true>), dim3(grid), block, 0, stream, a);
       else hipLaunchKernelGGL((k_qkv_attn16_fwd<64, false, true>), dim3(grid), block, 0, stream, a);
     }
-  } else if (!(a.lse || a.qkv_out || a.xq_out || a.pool)) {  // inference: no training stores
+  } else if (!(a.lse || a.qkv_out || a.xq_out || a.pool) && a.ld_wq == 72 && (!a.fold_out || a.fold_at_start)) {
+    // inference (no training stores), W_h staged, any fold at the start: the lean instantiation
     if (a.img) {
       if (a.D == 32) hipLaunchKernelGGL((k_qkv_attn16_fwd<32, true, false, false>), dim3(grid), block, 0, stream, a);
       else hipLaunchKernelGGL((k_qkv_attn16_fwd<64, true, false, false>), dim3(grid), block, 0, stream, a);
