@@ -37,6 +37,9 @@
 
 namespace ccmpi {
 namespace dev {
+// wgrad.hip: the standalone fp32-MFMA weight fold (a fold too large for the fused kernel's grid)
+void fold_emb_qkv_mfma(const float* Wq, int ld_wq, const float* We, int ld_we, uint16_t* Weff, int ld_eff, int R, int d,
+                       int kp, hipStream_t stream);
 namespace attn {
 namespace {
 
@@ -851,12 +854,8 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
     if (TR && a.fold_out && !a.fold_at_start) {  // (inference: launched only with the fold at the start)
       __syncthreads();
       fold_tail<NW>(a, &imgs[0][0]);
-    } else if (a.fold_out && (!TR || (a.ld_wq == 72 && HD * 144 <= kStageBytes))) {
-      // the prologue folded this workgroup's first tile; a grid smaller than the fold's tiles
-      // does the rest here, where W_h's registers are free
-      __syncthreads();
-      fold_tail<NW>(a, &imgs[0][0], blockIdx.x + gridDim.x);
-    }
+    }  // (fold at the start: one tile per workgroup at most -- launch_qkv_fwd_mfma moves a
+       // larger fold to the standalone kernel)
   }
   if constexpr (QKV) {
     if (tsr) {
@@ -1098,7 +1097,12 @@ void launch_qkv_fwd_mfma(const AttnArgs& args, hipStream_t stream) {
   const int grid = grid_for(args.B * args.Hl, g_qkv_grid_cap, kQkvWaves);
   const dim3 block(64 * kQkvWaves);
   AttnArgs a = args;
-  a.fold_sched = fold_sched_for(args, grid);
+  // more fold tiles than workgroups (small batches): the whole fold goes to the standalone
+  // fp32-MFMA kernel after this one (bitwise the same; it writes the NEXT forward's W_eff, which
+  // this kernel does not read), so the fused kernel carries one copy of the fold code, not two
+  const bool fold_apart = a.fold_out && ((a.fold_R + 15) / 16) * ((a.fold_kp + 15) / 16) > grid;
+  if (fold_apart) a.fold_out = nullptr;
+  a.fold_sched = fold_sched_for(a, grid);
   if (a.tstamp) {  // the phase-stamp diagnostic: its own instantiation
     if (a.img) {
       if (a.D == 32) hipLaunchKernelGGL((k_qkv_attn16_fwd<32, true, true>), dim3(grid), block, 0, stream, a);
@@ -1123,6 +1127,9 @@ void launch_qkv_fwd_mfma(const AttnArgs& args, hipStream_t stream) {
     if (a.D == 32) hipLaunchKernelGGL((k_qkv_attn16_fwd<32, false>), dim3(grid), block, 0, stream, a);
     else hipLaunchKernelGGL((k_qkv_attn16_fwd<64, false>), dim3(grid), block, 0, stream, a);
   }
+  if (fold_apart)
+    fold_emb_qkv_mfma(args.fold_wq, args.ld_fold_wq, args.fold_we, args.ld_fold_we, args.fold_out, args.ld_fold_out,
+                      args.fold_R, args.fold_d, args.fold_kp, stream);
 }
 
 int g_bwd_grid_cap = 0;  // tuning knob (attn_set_bwd_grid); 0 = 256 workgroups per head (measured best)

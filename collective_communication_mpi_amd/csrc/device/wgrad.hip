@@ -487,6 +487,16 @@ void fold_emb_qkv(uint64_t Wq, int ld_wq, uint64_t We, int ld_we, uint64_t Weff,
 
 }  // namespace
 
+// The fused forward's weight fold when it has more tiles than that kernel has workgroups
+// (attn_mfma.hip launch_qkv_fwd_mfma): the fp32-MFMA kernel -- bitwise the in-kernel fold,
+// whatever CCMPI_FOLD selects for the standalone fold
+void fold_emb_qkv_mfma(const float* Wq, int ld_wq, const float* We, int ld_we, uint16_t* Weff, int ld_eff, int R, int d,
+                       int kp, hipStream_t stream) {
+  hipLaunchKernelGGL(k_fold_mfma, dim3((R + 15) / 16, (kp + 15) / 16), dim3(kFmWaves * 64), 0, stream, Wq, ld_wq, We,
+                     ld_we, Weff, ld_eff, R, d, kp, nullptr, -1);
+  CCMPI_HIP_CHECK(hipGetLastError());
+}
+
 void register_wgrad_ops(pybind11::module_& m) {
   m.def("fold_emb_qkv", &fold_emb_qkv,
         "Weff (bf16) = Wq . We (+ bias in column bias_col), fp32 accumulate, fixed summation order",
