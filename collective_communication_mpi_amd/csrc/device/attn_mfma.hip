@@ -247,7 +247,7 @@ __device__ __forceinline__ void fold_tail(const AttnArgs& a, float* part /* >= 1
   }
 }
 
-template <int D, bool QKV, bool IMG = false, int NW = WPB, bool TS = false, bool TR = true>
+template <int D, bool QKV, bool IMG = false, int NW = WPB, bool TS = false, bool TR = true, bool LEAN = false>
 __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
   constexpr int LD = D + 8, NK = D / 32, NT = D / 16;
   // One LDS block carved into the kernel's buffers; the per-wave V / O tiles and the X tiles come
@@ -466,9 +466,9 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
     // loads go out with the prologue's own; with W_h staged below, its MFMAs run after the same
     // wait, its partial tiles go to the z-tile region (free until the first iteration) and the
     // staging barrier doubles as the fold's -- one round trip for both
-    // (the inference instantiation is launched only for the staged layout: no other W_h path in
-    // its code)
-    const bool staged = !TR || (a.ld_wq == 72 && HD * 144 <= kStageBytes);
+    // (LEAN instantiations are launched only for the staged layout: no other W_h path in their
+    // code)
+    const bool staged = LEAN || (a.ld_wq == 72 && HD * 144 <= kStageBytes);
     const bool fold_first = IMG && a.fold_out && a.fold_at_start;
     const bool fold_here = fold_first && staged && (int)blockIdx.x < fold_tiles(a);
     FoldOps<NW> fo;
@@ -851,7 +851,7 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
   if constexpr (QKV && IMG) {
     // the next forward's weight fold in the images' LDS (every DMA into it has landed: each
     // trip ends with vmcnt(0) and a barrier, and the trip count is workgroup-uniform)
-    if (TR && a.fold_out && !a.fold_at_start) {  // (inference: launched only with the fold at the start)
+    if (!LEAN && a.fold_out && !a.fold_at_start) {  // (LEAN: launched only with the fold at the start)
       __syncthreads();
       fold_tail<NW>(a, &imgs[0][0]);
     }  // (fold at the start: one tile per workgroup at most -- launch_qkv_fwd_mfma moves a
@@ -875,9 +875,9 @@ __global__ void __launch_bounds__(256) k_attn16_fwd(AttnArgs a) {
 // One workgroup of kQkvWaves waves per CU (two per SIMD): <= 256 VGPRs a wave, W_h's fragments
 // included; the waves of a workgroup share its staged W_h (see attn16_fwd_body).
 constexpr int kQkvWaves = 8;
-template <int D, bool IMG, bool TS = false, bool TR = true>
+template <int D, bool IMG, bool TS, bool TR, bool LEAN>
 __global__ void __launch_bounds__(64 * kQkvWaves) __attribute__((amdgpu_waves_per_eu(2))) k_qkv_attn16_fwd(AttnArgs a) {
-  attn16_fwd_body<D, true, IMG, kQkvWaves, TS, TR>(a);
+  attn16_fwd_body<D, true, IMG, kQkvWaves, TS, TR, LEAN>(a);
 }
 
 template <int D>
@@ -1093,6 +1093,17 @@ int fold_sched_for(const AttnArgs& a, int grid) {
   return bk == kstd ? 0 : bk + 1;
 }
 
+template <bool TS, bool TR, bool LEAN>
+void launch_qkv_variant(const AttnArgs& a, int grid, dim3 block, hipStream_t stream) {
+  if (a.img) {
+    if (a.D == 32) hipLaunchKernelGGL((k_qkv_attn16_fwd<32, true, TS, TR, LEAN>), dim3(grid), block, 0, stream, a);
+    else hipLaunchKernelGGL((k_qkv_attn16_fwd<64, true, TS, TR, LEAN>), dim3(grid), block, 0, stream, a);
+  } else {
+    if (a.D == 32) hipLaunchKernelGGL((k_qkv_attn16_fwd<32, false, TS, TR, LEAN>), dim3(grid), block, 0, stream, a);
+    else hipLaunchKernelGGL((k_qkv_attn16_fwd<64, false, TS, TR, LEAN>), dim3(grid), block, 0, stream, a);
+  }
+}
+
 void launch_qkv_fwd_mfma(const AttnArgs& args, hipStream_t stream) {
   const int grid = grid_for(args.B * args.Hl, g_qkv_grid_cap, kQkvWaves);
   const dim3 block(64 * kQkvWaves);
@@ -1103,30 +1114,14 @@ void launch_qkv_fwd_mfma(const AttnArgs& args, hipStream_t stream) {
   const bool fold_apart = a.fold_out && ((a.fold_R + 15) / 16) * ((a.fold_kp + 15) / 16) > grid;
   if (fold_apart) a.fold_out = nullptr;
   a.fold_sched = fold_sched_for(a, grid);
-  if (a.tstamp) {  // the phase-stamp diagnostic: its own instantiation
-    if (a.img) {
-      if (a.D == 32) hipLaunchKernelGGL((k_qkv_attn16_fwd<32, true, true>), dim3(grid), block, 0, stream, a);
-      else hipLaunchKernelGGL((k_qkv_attn16_fwd<64, true, true>), dim3(grid), block, 0, stream, a);
-    } else {
-      if (a.D == 32) hipLaunchKernelGGL((k_qkv_attn16_fwd<32, false, true>), dim3(grid), block, 0, stream, a);
-      else hipLaunchKernelGGL((k_qkv_attn16_fwd<64, false, true>), dim3(grid), block, 0, stream, a);
-    }
-  } else if (!(a.lse || a.qkv_out || a.xq_out || a.pool) && a.ld_wq == 72 && (!a.fold_out || a.fold_at_start)) {
-    // inference (no training stores), W_h staged, any fold at the start: the lean instantiation
-    if (a.img) {
-      if (a.D == 32) hipLaunchKernelGGL((k_qkv_attn16_fwd<32, true, false, false>), dim3(grid), block, 0, stream, a);
-      else hipLaunchKernelGGL((k_qkv_attn16_fwd<64, true, false, false>), dim3(grid), block, 0, stream, a);
-    } else {
-      if (a.D == 32) hipLaunchKernelGGL((k_qkv_attn16_fwd<32, false, false, false>), dim3(grid), block, 0, stream, a);
-      else hipLaunchKernelGGL((k_qkv_attn16_fwd<64, false, false, false>), dim3(grid), block, 0, stream, a);
-    }
-  } else if (a.img) {
-    if (a.D == 32) hipLaunchKernelGGL((k_qkv_attn16_fwd<32, true>), dim3(grid), block, 0, stream, a);
-    else hipLaunchKernelGGL((k_qkv_attn16_fwd<64, true>), dim3(grid), block, 0, stream, a);
-  } else {
-    if (a.D == 32) hipLaunchKernelGGL((k_qkv_attn16_fwd<32, false>), dim3(grid), block, 0, stream, a);
-    else hipLaunchKernelGGL((k_qkv_attn16_fwd<64, false>), dim3(grid), block, 0, stream, a);
-  }
+  // instantiations: TS = the phase-stamp diagnostic; TR = the training stores (lse, qkv, X rows,
+  // pool) in the code; LEAN = W_h staged and any fold at the start, the only paths in the code
+  // (the instruction cache: every byte of a path the kernel never takes still costs fetch time)
+  const bool train = a.lse || a.qkv_out || a.xq_out || a.pool;
+  const bool lean = a.ld_wq == 72 && (!a.fold_out || a.fold_at_start);
+  if (a.tstamp) launch_qkv_variant<true, true, false>(a, grid, block, stream);
+  else if (lean) (train ? launch_qkv_variant<false, true, true> : launch_qkv_variant<false, false, true>)(a, grid, block, stream);
+  else (train ? launch_qkv_variant<false, true, false> : launch_qkv_variant<false, false, false>)(a, grid, block, stream);
   if (fold_apart)
     fold_emb_qkv_mfma(args.fold_wq, args.ld_fold_wq, args.fold_we, args.ld_fold_we, args.fold_out, args.ld_fold_out,
                       args.fold_R, args.fold_d, args.fold_kp, stream);
