@@ -1069,12 +1069,16 @@ int g_qkv_fold_sched = -1;  // -1: CCMPI_QKV_FOLD_SCHED (default on), 0: grid-st
 
 // AttnArgs::fold_sched for a launch of `grid` workgroups: the rounds kf of the fold-owning
 // workgroups that minimise max(kf + fold, the others' rounds); 0 when grid-stride is as good
-int fold_sched_for(const AttnArgs& a, int grid) {
+bool fold_sched_on() {
   if (g_qkv_fold_sched < 0) {
     const char* e = std::getenv("CCMPI_QKV_FOLD_SCHED");
     g_qkv_fold_sched = (e && std::atoi(e) == 0) ? 0 : 1;
   }
-  if (!g_qkv_fold_sched || !a.img || !a.fold_out || !a.fold_at_start) return 0;
+  return g_qkv_fold_sched != 0;
+}
+
+int fold_sched_for(const AttnArgs& a, int grid) {
+  if (!fold_sched_on() || !a.img || !a.fold_out || !a.fold_at_start) return 0;
   const int nblk = (a.B * a.Hl + kQkvWaves - 1) / kQkvWaves;
   const int F = std::min(((a.fold_R + 15) / 16) * ((a.fold_kp + 15) / 16), grid);
   if (F <= 0 || F >= grid) return 0;
@@ -1105,13 +1109,21 @@ void launch_qkv_variant(const AttnArgs& a, int grid, dim3 block, hipStream_t str
 }
 
 void launch_qkv_fwd_mfma(const AttnArgs& args, hipStream_t stream) {
-  const int grid = grid_for(args.B * args.Hl, g_qkv_grid_cap, kQkvWaves);
+  int grid = grid_for(args.B * args.Hl, g_qkv_grid_cap, kQkvWaves);
+  const int fold_tiles_n = args.fold_out ? ((args.fold_R + 15) / 16) * ((args.fold_kp + 15) / 16) : 0;
+  // a fold at the start on a grid with CUs to spare (a small per-rank batch -- DP4 x TP2 at 512
+  // sequences is 128 blocks): the fold's tiles get workgroups of their own beside the attention
+  // workgroups (fold_sched_for then gives them no pair block), instead of running before those
+  // workgroups' only block
+  if (args.img && fold_tiles_n && args.fold_at_start && args.ld_wq == 72 && fold_sched_on() &&
+      grid < g_qkv_grid_cap)
+    grid = std::min(g_qkv_grid_cap, grid + fold_tiles_n);
   const dim3 block(64 * kQkvWaves);
   AttnArgs a = args;
   // more fold tiles than workgroups (small batches): the whole fold goes to the standalone
   // fp32-MFMA kernel after this one (bitwise the same; it writes the NEXT forward's W_eff, which
   // this kernel does not read), so the fused kernel carries one copy of the fold code, not two
-  const bool fold_apart = a.fold_out && ((a.fold_R + 15) / 16) * ((a.fold_kp + 15) / 16) > grid;
+  const bool fold_apart = a.fold_out && fold_tiles_n > grid;
   if (fold_apart) a.fold_out = nullptr;
   a.fold_sched = fold_sched_for(a, grid);
   // instantiations: TS = the phase-stamp diagnostic; TR = the training stores (lse, qkv, X rows,

@@ -581,10 +581,11 @@ def test_attn_qkv_fused_patchify(B, H, D):
                          zrows=0, zpush=[], stream=st, img=img.data_ptr())
 
 
-@pytest.mark.parametrize("B,H", [(2048, 2), (2048, 4), (1000, 2), (37, 1)])
+@pytest.mark.parametrize("B,H", [(2048, 2), (2048, 4), (1000, 2), (512, 2), (37, 1)])
 def test_attn_qkv_fold_schedule(B, H):
     """The fused forward's in-kernel weight fold (the pipelined plan's) with the fold-aware block
-    schedule -- fold-owning workgroups take fewer pair blocks, at B = 1000 / H = 2 none at all --
+    schedule -- fold-owning workgroups take fewer pair blocks; at B = 1000 and 512 (the DP4 x TP2
+    per-rank shape) / H = 2 the grid grows by the fold's tiles and their workgroups take none --
     against plain grid-stride and against the forward without the fold: token-mean logits bitwise
     equal, and the folded W_eff bitwise the standalone fp32-MFMA fold kernel's."""
     from collective_communication_mpi_amd import _native
