@@ -85,6 +85,7 @@ void launch_bwd_mfma(const AttnArgs& a, hipStream_t stream);
 void launch_qkv_fwd_mfma(const AttnArgs& a, hipStream_t stream);  // fused QKV + attention + token fc_o
 extern int g_qkv_grid_cap;  // workgroups of the fused QKV forward (persistent grid)
 extern int g_qkv_fold_sched;  // fold-aware block schedule of the fused forward: -1 env, 0 off, 1 on
+extern int g_qkv_fold_grid;   // ... and its grid widened by the fold's tiles at small batches (1) or not (0)
 extern int g_bwd_grid_cap;  // workgroups of the backward kernel when it also reduces the bias gradient
 
 }  // namespace attn

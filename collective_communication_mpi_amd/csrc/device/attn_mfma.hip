@@ -368,6 +368,21 @@ __device__ __forceinline__ void attn16_fwd_body(const AttnArgs& a) {
   auto blk = [&](int i) {  // this workgroup's i-th block; >= nblk: none (monotone in i)
     return i < kf ? wg + i * G : (wg < F ? nblk : kf * G + (wg - F) + (i - kf) * (G - F));
   };
+  if constexpr (QKV && IMG) {
+    // a fold-only workgroup (the grid widened by the fold's tiles, kf = 0): its tile and out --
+    // no W_h staging, no images, nothing the attention workgroups beside it need
+    if (F > 0 && blk(0) >= nblk) {
+      if ((int)blockIdx.x < fold_tiles(a)) {
+        float* part = reinterpret_cast<float*>(smem + oZpart);
+        FoldOps<NW> fo;
+        fold_issue<NW>(a, blockIdx.x, fo);
+        fold_mma<NW>(fo, part);
+        __syncthreads();
+        fold_reduce(a, blockIdx.x, part);
+      }
+      return;
+    }
+  }
   // the fc_o bias of this lane's epilogue classes (4 (lane & 3) .. +3), loaded once (the
   // compiler cannot hoist it past the loop's global stores)
   float bov[4];
@@ -1066,6 +1081,7 @@ int g_qkv_grid_cap = std::getenv("CCMPI_QKV_GRID") ? std::atoi(std::getenv("CCMP
 // ~2.1 us per round; H = 4: ~3.2 against ~2.7; profiles/r6_attn trace_v9_fold / trace_v12).
 constexpr double kFoldRounds = 1.5;
 int g_qkv_fold_sched = -1;  // -1: CCMPI_QKV_FOLD_SCHED (default on), 0: grid-stride always, 1: on
+int g_qkv_fold_grid = 1;    // fold workgroups of their own on a grid with CUs to spare (0 when ranks share the GPU)
 
 // AttnArgs::fold_sched for a launch of `grid` workgroups: the rounds kf of the fold-owning
 // workgroups that minimise max(kf + fold, the others' rounds); 0 when grid-stride is as good
@@ -1115,7 +1131,8 @@ void launch_qkv_fwd_mfma(const AttnArgs& args, hipStream_t stream) {
   // sequences is 128 blocks): the fold's tiles get workgroups of their own beside the attention
   // workgroups (fold_sched_for then gives them no pair block), instead of running before those
   // workgroups' only block
-  if (args.img && fold_tiles_n && args.fold_at_start && args.ld_wq == 72 && fold_sched_on() &&
+  // (not when ranks share the GPU, g_qkv_fold_grid = 0: their kernels already fill every CU)
+  if (args.img && fold_tiles_n && args.fold_at_start && args.ld_wq == 72 && fold_sched_on() && g_qkv_fold_grid &&
       grid < g_qkv_grid_cap)
     grid = std::min(g_qkv_grid_cap, grid + fold_tiles_n);
   const dim3 block(64 * kQkvWaves);

@@ -630,6 +630,9 @@ void register_attn_ops(pybind11::module_& m) {
   m.def("attn_set_qkv_fold_sched", [](int v) { attn::g_qkv_fold_sched = v < 0 ? -1 : (v ? 1 : 0); },
         "fused QKV forward with the in-kernel fold: 1 = fold owners take fewer pair blocks, 0 = grid-stride, "
         "-1 = CCMPI_QKV_FOLD_SCHED (default 1)", pybind11::arg("v"));
+  m.def("attn_set_qkv_fold_grid", [](int v) { attn::g_qkv_fold_grid = v ? 1 : 0; },
+        "fused QKV forward with the in-kernel fold: 1 = at small batches the grid grows by the fold's tiles "
+        "(fold-only workgroups beside the attention ones), 0 = not (ranks sharing one GPU)", pybind11::arg("v"));
   m.def("attn_set_bwd_grid", [](int cap) { attn::g_bwd_grid_cap = cap > 0 ? cap : 0; },
         "backward kernel grid cap (tuning)");
   namespace py = pybind11;

@@ -302,6 +302,9 @@ class DeviceGroup:
             # uses, exercised beside another rank's collectives on one GPU)
             if not self.shared_ring:
                 self.D.gemm_set_ring_min(0)
+            # the fused attention forward's fold-only workgroups help only on a GPU with CUs
+            # to spare; several ranks' kernels already fill it (profiles/r6_attn)
+            self.D.attn_set_qkv_fold_grid(0)
         self._async_done = None  # (stream, event) of the last start()ed collective, until ordered
         self._inflight: List = []  # (done event, tensors) of start()ed collectives not yet known complete
         default_blocks = max(1, 512 // self.ranks_per_device)

@@ -1,6 +1,7 @@
 #!/usr/bin/env bash
 # Round 6: fold workgroups of their own at small per-rank batches (grid widened by the fold's
-# tiles) -- kernel tests, micro at B = 512 / 2048 (fold schedule on / off), the N = 1 harness.
+# tiles; fold-only workgroups skip the attention prologue) -- kernel tests, micro at B = 512 / 2048
+# (fold schedule on / off), the N = 1 harness.
 set -o pipefail
 cd "$(dirname "$0")/../.."
 export TMPDIR=/tmp
