@@ -27,6 +27,15 @@
 //     per column per wave (and whenever a wave's head changes).
 // The kernel is memory bound (a few KiB moved per ~10 MFMAs): its cost is the
 // QKV read and the O / dQKV write.
+//
+// The harness forward runs the fused form instead (k_qkv_attn16_fwd, attn16_fwd_body with
+// QKV = true): patchify + QKV projection + attention + per-token fc_o (+ token mean, or the TP
+// push into the peers' inboxes) + optionally the next step's weight fold, one kernel.  Persistent
+// 8-wave workgroups, one per CU; W_h staged once per workgroup by LDS-DMA and held in registers;
+// each wave reads its X fragments straight from the images in LDS (LDS-DMA two blocks ahead); a
+// fold-aware block schedule (fold owners take fewer pair blocks, or at small batches the fold gets
+// workgroups of its own); and lean instantiations carrying only the paths they take -- the
+// instruction cache, not the arithmetic, set the last 10 % (profiles/r6_attn/README.md).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -148,9 +157,10 @@ __device__ __forceinline__ void rows_out(const uint16_t* T, uint16_t* dst, int l
 // its (sequence, head)'s q | k | v = X W_h^T + b itself on the MFMA from the sequence's patch
 // rows X (B*S x kq bf16, kq <= 80: two 16x16x32 k-steps + one 16x16x16 tail).  With Hl | WPB
 // a wave always serves head h = wave % Hl, so W_h's 3 D x kq operand fragments (120 VGPRs at
-// D = 64) are loaded ONCE and stay in registers for the whole grid-stride loop
-// (workgroups are persistent: two per CU); each iteration loads only X (prefetched one
-// iteration ahead).  q and k are rounded to bf16 (the values the unfused QKV GEMM would store)
+// D = 64) are loaded ONCE and stay in registers for the whole block loop (workgroups are
+// persistent: one 8-wave workgroup per CU); each iteration reads only X (patch-row mode:
+// prefetched one iteration ahead; image mode: from the images LDS-DMA'd two blocks ahead).
+// q and k are rounded to bf16 (the values the unfused QKV GEMM would store)
 // and turned into row fragments through the wave's O / V tiles, v lands in the V tile the PV
 // product reads; qkv is written only when a backward needs it (qkv_out).  The QKV GEMM's
 // launch, its 2 x B*S x 3 Hl D x 2 B of qkv write + read, and the old per-head W staging
