@@ -15,7 +15,9 @@ from collective_communication_mpi_amd.ops.kernels import gemm_nt  # noqa: E402
 
 
 def timed(fn, iters):
-    for _ in range(5):
+    # (50 untimed launches: with 5, whichever configuration ran first after a switch read
+    # 0.3-1 us slower than the same launch timed later -- profiles/r6_attn micro_v1x)
+    for _ in range(50):
         fn()
     torch.cuda.synchronize()
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
