@@ -6,6 +6,9 @@
 * RCCL is the library comparison: even when it is faster it never replaces ``value``
   (``config.rccl`` + ``handwritten_vs_rccl``);
 * the phase plan: the harness always runs in a phase of its own."""
+import os
+import sys
+
 import bench
 
 
@@ -268,3 +271,32 @@ def test_phase_binding_paths(monkeypatch):
     monkeypatch.setenv("CCMPI_BOUND_CPUS", "8-15")
     monkeypatch.setenv("CCMPI_BIND_EFFECTIVE", "gpu")
     assert bench.phase_binding(World(), 1, 1) == (None, "gpu")
+
+
+def test_phase_binding_plan_failure_reaches_every_rank(monkeypatch):
+    """A placement plan that fails on rank 0 (any exception, not only OSError) must still reach
+    the broadcast every other rank waits in -- with None, so every rank falls back to the OS's
+    placement -- and a child binding outside the cpuset must not stop the phase child."""
+    from collective_communication_mpi_amd import topology
+
+    def boom(n, **k):
+        raise KeyError("no such sysfs attribute")
+
+    monkeypatch.setattr(topology, "gpu_plan", boom)
+    calls = []
+
+    class World:
+        def Get_size(self):
+            return 2
+
+        def bcast(self, obj, root=0):
+            calls.append(obj)
+            return obj
+
+    monkeypatch.delenv("CCMPI_BOUND_CPUS", raising=False)
+    monkeypatch.setenv("CCMPI_BIND", "gpu")
+    assert bench.phase_binding(World(), 0, 0) == (None, "none")
+    assert calls == [None]
+    # a CPU set the process may not use: the child starts anyway, placed by the OS
+    rc, _ = bench._run_child([sys.executable, "-c", "pass"], dict(os.environ), 60, cpus=[1 << 20])
+    assert rc == 0
